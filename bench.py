@@ -1,0 +1,215 @@
+#!/usr/bin/env python3
+"""bench.py — k-mer scan throughput on MI355X (BASELINE.json metric).
+
+Workload (BASELINE.json configs[1]): k=6 over a 1 GB synthetic ACGT stream per
+GPU, input resident in HBM before the timed region.  One step = one pass of
+the hot path over the batch: zero the table, k_count + k_scan + k_redo (the
+engine's fk_engine_feed), and the result scalars (fk_engine_finish).  With
+--gpus N (one process per GPU, torch.distributed over RCCL) each rank owns the
+next 1 GB shard of one N GB stream: the shard entry state is stitched by
+all-gathering the 96-byte shard transfer functions, and the count tables are
+summed with an all-reduce — the path's two real exchange steps.
+
+Prints ONE JSON line on rank 0 (contract in the task statement): value =
+bases/s over all ranks, plus "roofline" for the dominant kernel (k_count, HIP
+events on the engine's stream) and "cpu_baseline" (the reference binary, or
+the oracle port if it is absent, on a bounded sample, rank 0 at N=1 only).
+"""
+import argparse
+import ctypes
+import json
+import os
+import subprocess
+import sys
+import tempfile
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+HBM_PEAK_GBS = 8000.0    # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+METRIC = "bases/sec scanned at fixed k; achieved HBM GB/s vs roofline, 1/2/4/8 GPUs"
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--k", type=int, default=6)
+    ap.add_argument("--bases", type=int, default=1_000_000_000, help="bases per GPU")
+    ap.add_argument("--fasta-line", type=int, default=0, help="0 = pure ACGT stream (configs[1]); 80 = FASTA")
+    ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--cpu-sample-bytes", type=int, default=0, help="0 = auto (~10-20 s of reference CPU work)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    return ap.parse_args()
+
+
+def cpu_baseline(args, n_sample):
+    """The reference CPU loop on a bounded prefix of the same stream."""
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    import oracle   # checker / baseline only
+    data = oracle.synth(n_sample, args.seed, args.fasta_line if args.fasta_line > 0 else 0)
+    bases = n_sample
+    ref = oracle.REF_BIN
+    if os.path.exists(ref) and os.access(ref, os.X_OK):
+        with tempfile.TemporaryDirectory() as td:
+            p = os.path.join(td, "sample.fa")
+            data.tofile(p)
+            t0 = time.perf_counter()
+            subprocess.run([ref, "-q", "1", "-k", str(args.k), "-p", "sample.fa"], cwd=td,
+                           stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+            dt = time.perf_counter() - t0
+        kind = "reference"
+        what = (f"oracle/_ref/findKmer_ref (reference findKmer.cpp, g++ -O3, single thread) "
+                f"end-to-end on the first {bases} bases of the same stream, k={args.k}")
+    else:
+        t0 = time.perf_counter()
+        oracle.count_dense(data.tobytes(), args.k)
+        dt = time.perf_counter() - t0
+        kind = "port"
+        what = f"oracle port (fk_oracle.c, 1 thread) on the first {bases} bases, k={args.k}"
+    return {"value": bases / dt, "unit": "bases/s", "cores": 1, "kind": kind,
+            "sample": what, "seconds": round(dt, 3)}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    import findkmer_amd as fk
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    k = args.k
+    n = args.bases
+    L = args.fasta_line
+    assert n % 1280 == 0, "--bases must be a multiple of 1280 (32-base generator words, 80-col lines)"
+
+    # this rank's shard of one stream: bases [rank*n, (rank+1)*n), plus the
+    # bytes just before it (halo) so the engine can guess the entry state
+    halo_bases = 0 if rank == 0 else (1280 if L > 0 else 256)
+    first = rank * n - halo_bases
+    if L > 0:
+        halo = halo_bases + halo_bases // L
+        frame = L if rank == 0 else -L
+        size = fk.synth_size(n + halo_bases, frame)
+    else:
+        halo = halo_bases
+        frame = 0
+        size = n + halo_bases
+    buf = torch.empty(size + 64, dtype=torch.uint8, device="cuda")
+    w = fk.synth_device(buf.data_ptr(), size, n + halo_bases, args.seed + first // 32, frame)
+    assert w == size
+    nbytes = size - halo
+    torch.cuda.synchronize()
+
+    eng = fk.Engine(k, device=local)
+    table_t = torch.empty(1 << (2 * k), dtype=torch.int32, device="cuda") if world > 1 else None
+
+    def step():
+        eng.reset()
+        if world == 1:
+            eng.feed_device(buf.data_ptr(), nbytes)
+        else:
+            eng.feed_shard_device(buf.data_ptr() + halo, nbytes, halo)
+            s = eng.summary()
+            mine = torch.tensor(list(s.w), dtype=torch.int64, device="cuda")
+            allv = [torch.empty_like(mine) for _ in range(world)]
+            dist.all_gather(allv, mine)
+            st = fk.FkState()
+            for r in range(rank):
+                sm = fk.FkSummary()
+                for i, v in enumerate(allv[r].tolist()):
+                    sm.w[i] = v & 0xFFFFFFFFFFFFFFFF
+                st = fk.summary_apply(sm, st)
+            eng.resolve(st)
+            eng.table_to_device(table_t.data_ptr())
+            dist.all_reduce(table_t)          # u32 sums, bitwise identical in int32
+            eng.table_from_device(table_t.data_ptr())
+        rc, r = eng.finish()
+        return r
+
+    for _ in range(args.warmup):
+        step()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    main_ms = 0.0
+    dev_ms = 0.0
+    last = None
+    for _ in range(args.steps):
+        last = step()
+        main_ms += last.main_kernel_ms
+        dev_ms += last.device_ms
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if dist:
+        tt = torch.tensor([dt], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+
+    # correctness guard on the measured pass (pure ACGT: every window counts)
+    if L == 0 and world == 1:
+        assert last.windows == n - k + 1, (last.windows, n - k + 1)
+
+    ms_step = dt / args.steps * 1e3
+    value = world * n / (dt / args.steps)
+    kern_ms = main_ms / args.steps
+    algo_bytes = nbytes + 4 * (1 << (2 * k))       # input read once + u32 table written once
+    achieved = algo_bytes / (kern_ms * 1e-3) / 1e9
+    traffic = None
+    tf = os.path.join(REPO, "profiles", f"traffic_k{k}_L{L}.json")
+    if os.path.exists(tf):
+        try:
+            traffic = json.load(open(tf)).get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+    out = {
+        "metric": METRIC,
+        "value": value,
+        "unit": "bases/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_step,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic (splitmix64 uniform ACGT, generated in HBM)",
+        "config": {
+            "workload": (f"k={k} over a {n / 1e9:g} G-base synthetic "
+                         + ("ACGT stream" if L == 0 else f"FASTA ({L}-col lines)")
+                         + " per GPU (BASELINE.json configs[1])" if k == 6 and L == 0 else
+                         f"k={k} over a {n / 1e9:g} G-base synthetic " + ("ACGT stream" if L == 0 else f"FASTA ({L}-col lines)") + " per GPU"),
+            "k": k, "bases_per_gpu": n, "input_bytes_per_gpu": nbytes,
+            "parallelism": f"shard{world}",
+        },
+        "roofline": {
+            "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+            "kernel": "k_count", "kernel_ms": kern_ms, "algorithmic_bytes": algo_bytes,
+        },
+        "device_ms_per_step": dev_ms / args.steps,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        sample = args.cpu_sample_bytes or (512 << 20 if k <= 7 else 48 << 20)
+        sample = min(sample, n)
+        out["cpu_baseline"] = cpu_baseline(args, sample)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    eng.close()
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,299 @@
+"""findkmer_amd — Python binding of the MI355X k-mer engine C-ABI (include/findkmer.h).
+
+The product is the native library ``findkmer_amd/lib/libfindkmer_hip.so`` (HIP
+kernels for gfx950 + the byte-identical writer) and the drop-in ``./findKmer``
+program.  This module is a thin ctypes layer over that library for tests and
+``bench.py``; it never falls back to a CPU implementation: if the library is
+missing or no GPU is visible, calls raise.
+
+Reference interface mirrored: the scan ``findKmer()`` of
+findKmer/src/findKmer.cpp:962-1069 (counts + base statistics), ``statistics()``
+(:491-565) and ``histo_recursive()`` (:699-942).
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libfindkmer_hip.so")
+
+FK_OK = 0
+FK_E_INVALID = -1
+FK_E_K_UNSUPPORTED = -2
+FK_E_NO_DEVICE = -3
+FK_E_HIP = -4
+FK_E_OOM = -5
+FK_E_EMPTY = -6
+FK_E_UNTERMINATED_HEADER = -7
+FK_E_ROLLOVER = -8
+FK_E_STATE = -9
+FK_K_MAX_DENSE = 16
+
+
+class FkState(ctypes.Structure):
+    _fields_ = [("run", ctypes.c_uint64), ("code", ctypes.c_uint64),
+                ("hdr", ctypes.c_uint32), ("pad", ctypes.c_uint32)]
+
+
+class FkResult(ctypes.Structure):
+    _fields_ = [("base_count", ctypes.c_uint64 * 4),
+                ("valid_bases", ctypes.c_uint64),
+                ("windows", ctypes.c_uint64),
+                ("distinct", ctypes.c_uint64),
+                ("depth1", ctypes.c_uint64 * 4),
+                ("nodes", ctypes.c_uint64),
+                ("unknown_chars", ctypes.c_uint64),
+                ("scanned_bytes", ctypes.c_uint64),
+                ("hit_eof_byte", ctypes.c_int32),
+                ("unterminated_header", ctypes.c_int32),
+                ("rollover", ctypes.c_int32),
+                ("nodes_valid", ctypes.c_int32),
+                ("chunks", ctypes.c_uint64),
+                ("redo_chunks", ctypes.c_uint64),
+                ("device_ms", ctypes.c_double),
+                ("main_kernel_ms", ctypes.c_double)]
+
+    def as_dict(self):
+        d = {}
+        for name, _ in self._fields_:
+            v = getattr(self, name)
+            d[name] = list(v) if isinstance(v, ctypes.Array) else v
+        return d
+
+
+class FkOpts(ctypes.Structure):
+    _fields_ = [("device", ctypes.c_int32), ("want_nodes", ctypes.c_int32),
+                ("stream", ctypes.c_void_p), ("collect_unknown", ctypes.c_int32),
+                ("reserved", ctypes.c_int32 * 7)]
+
+
+class FkSummary(ctypes.Structure):
+    _fields_ = [("w", ctypes.c_uint64 * 12)]
+
+
+# (name, restype, argtypes) for every symbol declared in include/findkmer.h
+_P = ctypes.c_void_p
+_U8P = ctypes.POINTER(ctypes.c_uint8)
+_U32P = ctypes.POINTER(ctypes.c_uint32)
+_U64P = ctypes.POINTER(ctypes.c_uint64)
+SIGNATURES = [
+    ("fk_abi_version", ctypes.c_int, []),
+    ("fk_strerror", ctypes.c_char_p, [ctypes.c_int]),
+    ("fk_device_count", ctypes.c_int, []),
+    ("fk_engine_create", ctypes.c_int, [ctypes.c_int, ctypes.POINTER(FkOpts), ctypes.POINTER(_P)]),
+    ("fk_engine_destroy", None, [_P]),
+    ("fk_engine_reset", ctypes.c_int, [_P]),
+    ("fk_engine_feed", ctypes.c_int, [_P, _P, ctypes.c_uint64, ctypes.c_int]),
+    ("fk_engine_feed_shard", ctypes.c_int, [_P, _P, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int]),
+    ("fk_engine_summary", ctypes.c_int, [_P, ctypes.POINTER(FkSummary)]),
+    ("fk_summary_apply", ctypes.c_int, [ctypes.POINTER(FkSummary), ctypes.POINTER(FkState), ctypes.POINTER(FkState)]),
+    ("fk_engine_resolve", ctypes.c_int, [_P, ctypes.POINTER(FkState)]),
+    ("fk_engine_finish", ctypes.c_int, [_P, ctypes.POINTER(FkResult)]),
+    ("fk_engine_table", ctypes.c_int, [_P, _U32P]),
+    ("fk_engine_table_device", ctypes.c_int, [_P, ctypes.POINTER(_P)]),
+    ("fk_engine_table_to_device", ctypes.c_int, [_P, _P]),
+    ("fk_engine_table_from_device", ctypes.c_int, [_P, _P]),
+    ("fk_engine_state", ctypes.c_int, [_P, ctypes.POINTER(FkState)]),
+    ("fk_engine_progress", ctypes.c_int, [_P, _U64P, _U64P]),
+    ("fk_engine_merge_from", ctypes.c_int, [_P, _P]),
+    ("fk_engine_unknown", ctypes.c_int, [_P, _U8P, ctypes.c_uint64, _U64P]),
+    ("fk_count", ctypes.c_int, [_P, ctypes.c_uint64, ctypes.c_int, ctypes.POINTER(FkOpts), _U32P, ctypes.POINTER(FkResult)]),
+    ("fk_count_multi", ctypes.c_int, [_P, ctypes.c_uint64, ctypes.c_int, ctypes.c_int, ctypes.POINTER(FkOpts), _U32P, ctypes.POINTER(FkResult)]),
+    ("fk_synth_device", ctypes.c_int, [_P, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int, _P, _U64P]),
+    ("fk_write_stats", ctypes.c_int, [ctypes.c_char_p, ctypes.c_int, ctypes.POINTER(FkResult), _P, ctypes.POINTER(ctypes.c_double)]),
+    ("fk_write_rows", ctypes.c_int, [_P, ctypes.c_int, _U32P, ctypes.POINTER(ctypes.c_double), ctypes.c_uint64, ctypes.c_int, ctypes.c_double, ctypes.c_int]),
+    ("fk_write_csv", ctypes.c_int, [ctypes.c_char_p, ctypes.c_int, _U32P, ctypes.POINTER(ctypes.c_double), ctypes.c_uint64, ctypes.c_int, ctypes.c_double, ctypes.c_int]),
+]
+
+_lib = None
+
+
+class FindKmerError(RuntimeError):
+    def __init__(self, code, what=""):
+        self.code = code
+        msg = lib().fk_strerror(code).decode() if _lib is not None else str(code)
+        super().__init__(f"{what}: {msg} ({code})" if what else f"{msg} ({code})")
+
+
+def lib():
+    """Load the native library (raises if it was not built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"{LIB_PATH} missing: run `make` (or __graft_entry__.build())")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, res, args in SIGNATURES:
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+def _check(rc, what, ok=(FK_OK,)):
+    if rc not in ok:
+        raise FindKmerError(rc, what)
+    return rc
+
+
+def device_count():
+    return lib().fk_device_count()
+
+
+def _ptr(obj):
+    """Address of a bytes-like host buffer, numpy array or torch tensor."""
+    if hasattr(obj, "data_ptr"):
+        return obj.data_ptr()
+    if hasattr(obj, "ctypes"):
+        return obj.ctypes.data
+    if isinstance(obj, (bytes, bytearray, memoryview)):
+        mv = memoryview(obj)
+        if mv.readonly:
+            buf = (ctypes.c_char * len(mv)).from_buffer_copy(mv)
+            _ptr.keep = buf
+            return ctypes.addressof(buf)
+        return ctypes.addressof((ctypes.c_char * len(mv)).from_buffer(mv))
+    raise TypeError(type(obj))
+
+
+class Engine:
+    """One k-mer engine on one GPU (mirrors the findKmer() scan, :962-1069)."""
+
+    def __init__(self, k, device=-1, want_nodes=False, collect_unknown=False, stream=None):
+        L = lib()
+        self.k = k
+        o = FkOpts()
+        o.device = device
+        o.want_nodes = 1 if want_nodes else 0
+        o.collect_unknown = 1 if collect_unknown else 0
+        o.stream = stream
+        h = ctypes.c_void_p()
+        _check(L.fk_engine_create(k, ctypes.byref(o), ctypes.byref(h)), "fk_engine_create")
+        self.h = h
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().fk_engine_destroy(self.h)
+            self.h = None
+
+    __del__ = close
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def reset(self):
+        _check(lib().fk_engine_reset(self.h), "reset")
+
+    def feed(self, buf, nbytes=None, on_device=False):
+        n = len(buf) if nbytes is None else nbytes
+        _check(lib().fk_engine_feed(self.h, _ptr(buf), n, 1 if on_device else 0), "feed")
+
+    def feed_device(self, ptr, nbytes):
+        _check(lib().fk_engine_feed(self.h, ptr, nbytes, 1), "feed")
+
+    def feed_shard_device(self, ptr, nbytes, halo):
+        _check(lib().fk_engine_feed_shard(self.h, ptr, nbytes, halo, 1), "feed_shard")
+
+    def summary(self):
+        s = FkSummary()
+        _check(lib().fk_engine_summary(self.h, ctypes.byref(s)), "summary")
+        return s
+
+    def resolve(self, state):
+        _check(lib().fk_engine_resolve(self.h, ctypes.byref(state)), "resolve")
+
+    def state(self):
+        s = FkState()
+        _check(lib().fk_engine_state(self.h, ctypes.byref(s)), "state")
+        return s
+
+    def finish(self, allow=(FK_OK,)):
+        r = FkResult()
+        rc = lib().fk_engine_finish(self.h, ctypes.byref(r))
+        _check(rc, "finish", ok=tuple(allow))
+        return rc, r
+
+    def table(self):
+        import numpy as np
+        t = np.zeros(1 << (2 * self.k), dtype=np.uint32)
+        _check(lib().fk_engine_table(self.h, t.ctypes.data_as(_U32P)), "table")
+        return t
+
+    def table_device_ptr(self):
+        p = ctypes.c_void_p()
+        _check(lib().fk_engine_table_device(self.h, ctypes.byref(p)), "table_device")
+        return p.value
+
+    def table_to_device(self, ptr):
+        _check(lib().fk_engine_table_to_device(self.h, ptr), "table_to_device")
+
+    def table_from_device(self, ptr):
+        _check(lib().fk_engine_table_from_device(self.h, ptr), "table_from_device")
+
+    def unknown_bytes(self):
+        n = ctypes.c_uint64()
+        _check(lib().fk_engine_unknown(self.h, None, 0, ctypes.byref(n)), "unknown")
+        out = (ctypes.c_uint8 * max(1, n.value))()
+        _check(lib().fk_engine_unknown(self.h, out, n.value, ctypes.byref(n)), "unknown")
+        return bytes(out[: n.value])
+
+
+def summary_apply(summary, state):
+    out = FkState()
+    _check(lib().fk_summary_apply(ctypes.byref(summary), ctypes.byref(state), ctypes.byref(out)), "summary_apply")
+    return out
+
+
+def count(data, k, ngpu=1, want_nodes=False):
+    """Count k-mers of a host byte buffer on the GPU(s).  Returns (rc, table, result)."""
+    import numpy as np
+    L = lib()
+    t = np.zeros(1 << (2 * k), dtype=np.uint32)
+    r = FkResult()
+    o = FkOpts()
+    o.device = -1
+    o.want_nodes = 1 if want_nodes else 0
+    buf = np.frombuffer(bytes(data), dtype=np.uint8) if not hasattr(data, "ctypes") else data
+    if len(buf) == 0:
+        buf = np.zeros(1, dtype=np.uint8)
+        n = 0
+    else:
+        n = len(buf)
+    if ngpu > 1:
+        rc = L.fk_count_multi(buf.ctypes.data, n, k, ngpu, ctypes.byref(o), t.ctypes.data_as(_U32P), ctypes.byref(r))
+    else:
+        rc = L.fk_count(buf.ctypes.data, n, k, ctypes.byref(o), t.ctypes.data_as(_U32P), ctypes.byref(r))
+    if rc not in (FK_OK, FK_E_EMPTY, FK_E_UNTERMINATED_HEADER, FK_E_ROLLOVER):
+        raise FindKmerError(rc, "fk_count")
+    return rc, t, r
+
+
+def synth_device(ptr, cap, n_bases, seed, fasta_line=0, stream=None):
+    w = ctypes.c_uint64()
+    _check(lib().fk_synth_device(ptr, cap, n_bases, seed, fasta_line, stream, ctypes.byref(w)), "synth")
+    return w.value
+
+
+def synth_size(n_bases, fasta_line=0):
+    if fasta_line > 0:
+        return 11 + n_bases + n_bases // fasta_line
+    if fasta_line < 0:
+        return n_bases + n_bases // (-fasta_line)
+    return n_bases
+
+
+def write_stats(path, k, result, prob_out=True):
+    import numpy as np
+    p = (ctypes.c_double * 4)()
+    rc = lib().fk_write_stats(path.encode(), k, ctypes.byref(result), None, p)
+    return rc, [p[i] for i in range(4)]
+
+
+def write_csv(path, k, counts, prob, windows, z_enable=0, z_threshold=0.0, threads=0):
+    import numpy as np
+    c = np.ascontiguousarray(counts, dtype=np.uint32)
+    p = (ctypes.c_double * 4)(*prob)
+    _check(lib().fk_write_csv(path.encode(), k, c.ctypes.data_as(_U32P), p, windows, z_enable,
+                              float(z_threshold), threads), "write_csv")

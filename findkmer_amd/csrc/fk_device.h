@@ -1,0 +1,181 @@
+/*
+ * fk_device.h — device-side building blocks shared by the engine kernels.
+ *
+ * Scan semantics restated from findKmer/src/findKmer.cpp:962-1069 (see
+ * DESIGN.md §2).  A stream position's scan state is (hdr, R, code):
+ *   hdr  — inside a '>' comment line (:991-1008)
+ *   R    — valid bases since the last run break, modulo 2^32: the reference's
+ *          `int seqSize` (:977) is seq = (int32)R, so its wrap after 2^31-1 is
+ *          reproduced exactly
+ *   code — the last bases, 2 bits each, first base most significant
+ *          (base2int :567-589; the window :947-958)
+ */
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define FK_TILE_BYTES 1024u            /* one wave x 16 B */
+#define FK_CHUNK_TILES 64u
+#define FK_CHUNK_BYTES (FK_TILE_BYTES * FK_CHUNK_TILES)   /* 64 KiB per chunk */
+#define FK_HALO_BYTES 256u             /* bytes before a chunk used to guess state */
+#define FK_BLOCK 512u
+#define FK_WAVES_PER_BLOCK (FK_BLOCK / 64u)
+#define FK_LDS_MAX_K 7                 /* 4^7 u32 = 64 KiB of LDS bins */
+
+/* accumulator slots (u64, device) */
+enum {
+    ACC_BASE = 0,        /* 4: baseStatistics counts */
+    ACC_VALID = 4,       /* baseCounter */
+    ACC_WIN = 5,         /* TotalNumSequencesN */
+    ACC_D1W = 6,         /* 4: depth-1 trie freq from windows */
+    ACC_D1S = 10,        /* 4: depth-1 trie freq from short (<k) walks */
+    ACC_N = 16
+};
+
+/* per-chunk record written by the count pass (64 B) */
+struct ChunkRec {
+    uint64_t a_code;     /* assumed entering state */
+    uint32_t a_R, a_hdr;
+    uint64_t x_code;     /* exit state of the counted trajectory */
+    uint32_t x_R, x_hdr;
+    uint32_t flags;      /* CR_* */
+    uint32_t R_at_p1;    /* R just before the chunk's first '\n'/'>' byte */
+    uint32_t nv_total;   /* bases processed (meaningful when no reset) */
+    uint32_t eof_off;    /* first 0xFF outside a header, chunk-relative */
+    uint32_t unknown;    /* unknown-character bytes in the chunk */
+    uint32_t pad[3];
+};
+enum {
+    CR_FOUND_P1 = 1u,       /* chunk contains '\n' or '>' */
+    CR_P1_GT = 2u,          /* ... and the first one is '>' */
+    CR_ANY_RESET = 4u,      /* the counted trajectory broke the run */
+    CR_RESET_AFTER_P1 = 8u  /* ... after the first special byte */
+};
+#define FK_NO_EOF 0xFFFFFFFFu
+
+struct DState {
+    uint64_t code;
+    uint32_t R;
+    uint32_t hdr;
+};
+
+/* Exact (64-bit run) state and chunk transfer function for the state scan. */
+struct XState {
+    uint64_t R;
+    uint64_t code;
+    uint32_t hdr;
+    uint32_t pad;
+};
+struct TF {
+    XState c1;           /* result when entering inside a header (R = 0) */
+    XState c0;           /* result when entering outside a header, if f0_const */
+    uint64_t nv;         /* else: shift by nv bases ... */
+    uint64_t cs;         /* ... whose last bases are cs */
+    uint32_t f0_const;
+    uint32_t pad;
+};
+
+__host__ __device__ inline uint64_t fk_join(uint64_t x, uint64_t y, uint64_t n) {
+    /* append n bases y (low 2n bits) after x; keep the last 32 bases */
+    if (n >= 32) return y;
+    uint64_t m = (1ull << (2 * n)) - 1;
+    return (x << (2 * n)) | (y & m);
+}
+
+__host__ __device__ inline XState fk_apply(const TF &f, const XState &s) {
+    if (s.hdr) return f.c1;
+    if (f.f0_const) return f.c0;
+    XState o;
+    o.hdr = 0;
+    o.pad = 0;
+    o.R = s.R + f.nv;
+    o.code = fk_join(s.code, f.cs, f.nv);
+    return o;
+}
+
+/* h = f then g */
+__host__ __device__ inline TF fk_compose(const TF &f, const TF &g) {
+    TF h;
+    h.c1 = fk_apply(g, f.c1);
+    h.pad = 0;
+    if (f.f0_const) {
+        h.f0_const = 1;
+        h.c0 = fk_apply(g, f.c0);
+        h.nv = 0;
+        h.cs = 0;
+    } else if (g.f0_const) {
+        h.f0_const = 1;
+        h.c0 = g.c0;
+        h.nv = 0;
+        h.cs = 0;
+    } else {
+        h.f0_const = 0;
+        h.c0 = XState{0, 0, 0, 0};
+        h.nv = f.nv + g.nv;
+        h.cs = fk_join(f.cs, g.cs, g.nv);
+    }
+    return h;
+}
+
+__host__ __device__ inline TF fk_identity() {
+    TF t;
+    t.c1 = XState{0, 0, 1, 0};
+    t.c0 = XState{0, 0, 0, 0};
+    t.nv = 0;
+    t.cs = 0;
+    t.f0_const = 0;
+    t.pad = 0;
+    return t;
+}
+
+/* Transfer function of one chunk from what its count pass recorded. */
+__host__ __device__ inline TF fk_tf_of(const ChunkRec &r) {
+    TF t;
+    t.pad = 0;
+    XState x{r.x_R, r.x_code, r.x_hdr, 0};
+    if (r.a_hdr == 0) {
+        if (r.flags & CR_ANY_RESET) {
+            t.f0_const = 1;
+            t.c0 = x;
+            t.nv = 0;
+            t.cs = 0;
+        } else {
+            t.f0_const = 0;
+            t.c0 = XState{0, 0, 0, 0};
+            t.nv = r.nv_total;
+            t.cs = r.x_code;
+        }
+        if (!(r.flags & CR_FOUND_P1)) {
+            t.c1 = XState{0, 0, 1, 0};
+        } else if (r.flags & CR_P1_GT) {
+            t.c1 = x;
+        } else {
+            uint32_t rr = (r.flags & CR_RESET_AFTER_P1) ? r.x_R : (uint32_t)(r.x_R - r.R_at_p1);
+            t.c1 = XState{rr, r.x_code, r.x_hdr, 0};
+        }
+    } else {
+        /* entering inside a header was certain: f0 never applies */
+        t.c1 = x;
+        t.f0_const = 1;
+        t.c0 = x;
+        t.nv = 0;
+        t.cs = 0;
+    }
+    return t;
+}
+
+/* Would counting a chunk from state a and from state t give identical
+ * contributions?  nvb bounds the bases in the chunk. */
+__host__ __device__ inline bool fk_equiv(const DState &a, const XState &t, int k, uint64_t nvb) {
+    if (a.hdr != t.hdr) return false;
+    if (t.hdr) return true;
+    uint32_t ra = a.R, rt = (uint32_t)t.R;
+    bool deep_a = (int32_t)ra >= k && (uint64_t)ra + nvb <= 0x7FFFFFFFull;
+    bool deep_t = (int32_t)rt >= k && (uint64_t)rt + nvb <= 0x7FFFFFFFull;
+    if (!(ra == rt || (deep_a && deep_t))) return false;
+    int32_t s = (int32_t)rt;
+    int d = s <= 0 ? 0 : (s > k - 1 ? k - 1 : s);
+    if (deep_a && deep_t) d = k - 1;
+    uint64_t m = d ? ((d >= 32) ? ~0ull : ((1ull << (2 * d)) - 1)) : 0ull;
+    return ((a.code ^ t.code) & m) == 0;
+}

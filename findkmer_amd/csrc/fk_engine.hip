@@ -1,0 +1,1489 @@
+/*
+ * fk_engine.hip — MI355X (gfx950) k-mer counting engine behind include/findkmer.h.
+ *
+ * Replaces the reference hot path findKmer() (findKmer/src/findKmer.cpp:962-1069)
+ * and its trie (:107-111, :612-690) with three HIP kernels per input segment:
+ *
+ *   k_count  one wave per 64 KiB chunk (grid-stride, 8 waves per 512-thread
+ *            block).  16 B per lane per 1 KiB tile, coalesced.  The chunk's
+ *            entering scan state is guessed from the 256 bytes before it; the
+ *            wave derives each lane's state with a 64-lane scan of per-lane
+ *            run summaries, then every lane walks its 16 bytes and adds each
+ *            counted window to the table: LDS-privatised u32 bins for k <= 7
+ *            (flushed once per block), global u32 atomics otherwise.  It
+ *            records the chunk's transfer function and the guessed state.
+ *   k_scan   one workgroup composes the chunk transfer functions (parallel
+ *            prefix) into the exact entering state of every chunk (64-bit run
+ *            length, so the reference's int32 seqSize wrap is exact) and lists
+ *            the chunks whose guess would count differently.
+ *   k_redo   re-counts only the listed chunks: once with weight -1 from the
+ *            guessed state (cancels k_count's contribution exactly), once with
+ *            weight +1 from the true state.  Normally the list is empty.
+ *
+ * Counting rules per valid base (seq = (int32)R after the increment):
+ *   seq >  k : window, baseCounter++, base[new]++            (:1035-1042)
+ *   seq == k : window, base[all k]++, baseCounter += k        (:1044-1057)
+ *   0<seq<k  : depth-1 trie touch only (prefix walk)          (:1059-1062)
+ * Runs break at '>' (then skip to '\n'), 'N' and any other non-ACGT byte;
+ * '\n' is transparent; 0xFF outside a header ends the input (:988).
+ */
+#include <hip/hip_runtime.h>
+
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <chrono>
+#include <vector>
+
+#include "findkmer.h"
+#include "fk_device.h"
+
+/* ------------------------------------------------------------------------- */
+/* device helpers                                                             */
+/* ------------------------------------------------------------------------- */
+
+__device__ __forceinline__ uint32_t fk_byte(const uint32_t w[4], int j) {
+    return (w[j >> 2] >> (8 * (j & 3))) & 0xFFu;
+}
+
+/* A=0 C=1 G=2 T=3 (base2int :567-589), -1 otherwise */
+__device__ __forceinline__ int fk_sym(uint32_t c) {
+    return c == 'A' ? 0 : c == 'C' ? 1 : c == 'G' ? 2 : c == 'T' ? 3 : -1;
+}
+
+__device__ __forceinline__ uint32_t shup(uint32_t v, int d) { return __shfl_up(v, (unsigned)d, 64); }
+
+__device__ __forceinline__ uint32_t rdlane(uint32_t v, int l) {
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, l);
+}
+__device__ __forceinline__ uint64_t rdlane64(uint64_t v, int l) {
+    return ((uint64_t)rdlane((uint32_t)(v >> 32), l) << 32) | rdlane((uint32_t)v, l);
+}
+
+__device__ __forceinline__ uint64_t comp_packed(uint64_t x, int k, uint64_t maskk) {
+    /* counts of A,C,G,T among the k digits of x, packed 16 bits each */
+    const uint64_t m5 = 0x5555555555555555ull & maskk;
+    uint64_t lo = x & m5, hi = (x >> 1) & m5;
+    uint32_t nT = __popcll(lo & hi);
+    uint32_t nG = __popcll(hi) - nT;
+    uint32_t nC = __popcll(lo) - nT;
+    uint32_t nA = (uint32_t)k - nT - nG - nC;
+    return (uint64_t)nA | ((uint64_t)nC << 16) | ((uint64_t)nG << 32) | ((uint64_t)nT << 48);
+}
+
+struct Counters {       /* per lane; flushed per chunk */
+    uint64_t base;      /* 4 x 16-bit */
+    uint64_t d1w;
+    uint64_t d1s;
+    uint32_t valid;
+    uint32_t win;
+    uint32_t unknown;
+    uint32_t eof;       /* chunk-relative offset of first 0xFF, or FK_NO_EOF */
+};
+
+struct Facts {          /* wave-uniform per chunk */
+    uint32_t found_p1, p1_gt, any_reset, reset_after_p1, R_at_p1, nv_total;
+};
+
+struct Ctx {            /* kernel-wide constants */
+    const uint8_t *buf;
+    uint64_t len;
+    int64_t lo;         /* lowest readable offset (negative: halo before buf) */
+    uint32_t *table;    /* global 4^k */
+    uint32_t *lds;      /* LDS bins (k <= FK_LDS_MAX_K) or nullptr */
+    uint32_t *shortcnt; /* sum_{d<k} 4^d */
+    unsigned long long *acc;
+    uint64_t maskk;
+    int k;
+};
+
+template <bool USE_LDS>
+__device__ __forceinline__ void hist_add(const Ctx &cx, uint64_t idx, uint32_t w) {
+    if (USE_LDS) {
+        atomicAdd(&cx.lds[(uint32_t)idx], w);
+    } else {
+        atomicAdd(&cx.table[idx], w);
+    }
+}
+
+__device__ __forceinline__ void short_run(const Ctx &cx, int seq, uint64_t code, uint32_t w) {
+    /* a run ended with 1 <= seqSize < k: its prefix-only trie walk left nodes
+       for nodeCounter (:1059-1062).  Offset of depth d: (4^d - 4) / 3. */
+    uint64_t off = ((1ull << (2 * seq)) - 4) / 3;
+    uint64_t m = (1ull << (2 * seq)) - 1;
+    atomicAdd(&cx.shortcnt[off + (code & m)], w);
+}
+
+/* Load the 16 bytes of lane `l` of a tile starting at byte offset `off`
+ * (relative to cx.buf; may be negative down to cx.lo).  Fully-inside lanes use
+ * one 16-B load; the stream's last partial lane loads bytewise. */
+__device__ __forceinline__ int load16(const Ctx &cx, int64_t off, uint32_t w[4]) {
+    w[0] = w[1] = w[2] = w[3] = 0;
+    if (off < cx.lo || off >= (int64_t)cx.len) return 0;
+    if (off + 16 <= (int64_t)cx.len) {
+        uint4 v = *reinterpret_cast<const uint4 *>(cx.buf + off);
+        w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
+        return 16;
+    }
+    int nb = (int)((int64_t)cx.len - off);
+    for (int j = 0; j < nb; j++) w[j >> 2] |= (uint32_t)cx.buf[off + j] << (8 * (j & 3));
+    return nb;
+}
+
+/*
+ * Process one tile (one wave, 16 bytes per lane, `nb` valid).
+ * COUNT=false: only advance the wave state (halo guess).
+ * `tile_off` is the tile's byte offset inside its chunk.
+ */
+template <bool COUNT, bool USE_LDS>
+__device__ __forceinline__ void tile_general(const Ctx &cx, const uint32_t w[4], int nb,
+                                             uint32_t tile_off, DState &st, Facts &f,
+                                             Counters &cnt, uint32_t weight) {
+    const int lane = threadIdx.x & 63;
+    const int k = cx.k;
+
+    /* -- 1. header flag at each lane start: last '>' vs last '\n' before it */
+    uint32_t lastGT = 0, lastNL = 0, firstSp = 0xFFFFu, firstGT = 0;
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+        uint32_t c = fk_byte(w, j);
+        bool in = j < nb;
+        uint32_t pos = (uint32_t)lane * 16u + (uint32_t)j + 1u;
+        bool gt = in && c == '>';
+        bool nl = in && c == '\n';
+        if (gt) lastGT = pos;
+        if (nl) lastNL = pos;
+        if ((gt || nl) && firstSp == 0xFFFFu) { firstSp = pos - 1; firstGT = gt; }
+    }
+    uint32_t g = lastGT, n = lastNL;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        uint32_t tg = shup(g, d), tn = shup(n, d);
+        if (lane >= d) { g = max(g, tg); n = max(n, tn); }
+    }
+    uint32_t gx = shup(g, 1), nx = shup(n, 1);
+    if (lane == 0) { gx = 0; nx = 0; }
+    const uint32_t hdr0 = (gx | nx) ? (gx > nx ? 1u : 0u) : st.hdr;
+
+    /* -- 2. per-lane run summary under hdr0: (reset?, bases since, code) */
+    uint32_t hdr = hdr0, rs = 0, nv = 0, hdr_end;
+    uint64_t code = 0;
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+        if (j < nb) {
+            uint32_t c = fk_byte(w, j);
+            if (hdr) {
+                if (c == '\n') hdr = 0;
+            } else if (c == '>') {
+                rs = 1; nv = 0; hdr = 1;
+            } else if (c != '\n') {
+                int s = fk_sym(c);
+                if (s < 0) { rs = 1; nv = 0; }
+                else { code = (code << 2) | (uint32_t)s; nv++; }
+            }
+        }
+    }
+    hdr_end = hdr;
+
+    /* -- 3. inclusive scan of run summaries across the wave */
+    uint32_t p = (rs << 31) | nv;
+    uint64_t cd = code;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        uint32_t tp = shup(p, d);
+        uint32_t tlo = shup((uint32_t)cd, d), thi = shup((uint32_t)(cd >> 32), d);
+        if (lane >= d && !(p >> 31)) {
+            uint32_t mynv = p & 0x7FFFFFFFu;
+            uint64_t tc = ((uint64_t)thi << 32) | tlo;
+            cd = fk_join(tc, cd, mynv);
+            p = (tp & 0x80000000u) | ((tp & 0x7FFFFFFFu) + mynv);
+        }
+    }
+    /* wave exit state from lane 63's inclusive summary */
+    const uint32_t p63 = rdlane(p, 63);
+    const uint64_t cd63 = rdlane64(cd, 63);
+    const uint32_t hdr63 = rdlane(hdr_end, 63);
+    DState nst;
+    nst.hdr = hdr63;
+    nst.R = (p63 >> 31) ? (p63 & 0x7FFFFFFFu) : st.R + (p63 & 0x7FFFFFFFu);
+    nst.code = (p63 >> 31) ? cd63 : fk_join(st.code, cd63, p63 & 0x7FFFFFFFu);
+
+    if (COUNT) {
+        /* exclusive summary -> this lane's entering state */
+        uint32_t ep = shup(p, 1);
+        uint32_t elo = shup((uint32_t)cd, 1), ehi = shup((uint32_t)(cd >> 32), 1);
+        if (lane == 0) { ep = 0; elo = 0; ehi = 0; }
+        uint64_t ecd = ((uint64_t)ehi << 32) | elo;
+        uint32_t R = (ep >> 31) ? (ep & 0x7FFFFFFFu) : st.R + (ep & 0x7FFFFFFFu);
+        uint64_t lc = (ep >> 31) ? ecd : fk_join(st.code, ecd, ep & 0x7FFFFFFFu);
+        hdr = hdr0;
+
+        /* first special byte of the chunk ('\n' or '>') */
+        uint64_t spm = __ballot(firstSp != 0xFFFFu);
+        uint32_t p1 = 0xFFFFFFFFu;    /* resets after position p1 count as after p1 */
+        int p1_lane = -1;
+        if (f.found_p1) {
+            p1 = 0;                   /* found in an earlier tile: everything is after */
+        } else if (spm) {
+            p1_lane = __ffsll((long long)spm) - 1;
+            p1 = rdlane(firstSp, p1_lane);
+        }
+        const bool p1_here = !f.found_p1 && spm;
+        uint32_t r_at = 0, lane_reset = 0, lane_reset_after = 0;
+
+#pragma unroll
+        for (int j = 0; j < 16; j++) {
+            if (j < nb) {
+                uint32_t c = fk_byte(w, j);
+                uint32_t pos = (uint32_t)lane * 16u + (uint32_t)j;
+                if (p1_here && pos == p1) r_at = R;
+                if (hdr) {
+                    if (c == '\n') hdr = 0;
+                    continue;
+                }
+                if (c == '\n') continue;
+                int s = fk_sym(c);
+                if (s < 0) {                      /* run break: '>', N, other */
+                    int seq = (int)R;
+                    if (seq >= 1 && seq < k) short_run(cx, seq, lc, weight);
+                    R = 0;
+                    lane_reset = 1;
+                    if (f.found_p1 || (p1_here && pos > p1)) lane_reset_after = 1;
+                    if (c == '>') {
+                        hdr = 1;
+                    } else if (c == 0xFFu) {
+                        uint32_t o = tile_off + pos;
+                        cnt.eof = min(cnt.eof, o);
+                    } else if (c != 'N') {
+                        cnt.unknown++;
+                    }
+                    continue;
+                }
+                lc = (lc << 2) | (uint32_t)s;
+                R += 1;
+                int seq = (int)R;
+                if (seq > k) {
+                    uint64_t idx = lc & cx.maskk;
+                    hist_add<USE_LDS>(cx, idx, weight);
+                    cnt.base += 1ull << (16 * s);
+                    cnt.valid += 1;
+                    cnt.win += 1;
+                    cnt.d1w += 1ull << (16 * (uint32_t)((idx >> (2 * k - 2)) & 3));
+                } else if (seq == k) {
+                    uint64_t idx = lc & cx.maskk;
+                    hist_add<USE_LDS>(cx, idx, weight);
+                    cnt.base += comp_packed(idx, k, cx.maskk);
+                    cnt.valid += (uint32_t)k;
+                    cnt.win += 1;
+                    cnt.d1w += 1ull << (16 * (uint32_t)((idx >> (2 * k - 2)) & 3));
+                } else if (seq >= 1) {
+                    cnt.d1s += 1ull << (16 * (uint32_t)((lc >> (2 * seq - 2)) & 3));
+                }
+            }
+        }
+
+        /* chunk facts */
+        if (__ballot(lane_reset)) f.any_reset = 1;
+        if (__ballot(lane_reset_after)) f.reset_after_p1 = 1;
+        if (!(p63 >> 31)) f.nv_total += p63 & 0x7FFFFFFFu;
+        if (p1_here) {
+            f.found_p1 = 1;
+            f.p1_gt = rdlane(firstGT, p1_lane);
+            f.R_at_p1 = rdlane(r_at, p1_lane);
+        }
+    }
+    st = nst;
+}
+
+/* wave-wide sum via butterfly */
+__device__ __forceinline__ uint32_t wsum32(uint32_t v) {
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+    return v;
+}
+__device__ __forceinline__ uint32_t wmin32(uint32_t v) {
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v = min(v, (uint32_t)__shfl_xor(v, d, 64));
+    return v;
+}
+
+__device__ __forceinline__ void acc_add(unsigned long long *a, uint64_t v, uint32_t weight) {
+    if (v) atomicAdd(a, (unsigned long long)(weight == 1u ? v : (0ull - v)));
+}
+
+__device__ void flush_counters(const Ctx &cx, Counters &cnt, uint32_t weight) {
+    const int lane = threadIdx.x & 63;
+    uint32_t vals[14];
+    for (int b = 0; b < 4; b++) {
+        vals[b] = (uint32_t)((cnt.base >> (16 * b)) & 0xFFFF);
+        vals[6 + b] = (uint32_t)((cnt.d1w >> (16 * b)) & 0xFFFF);
+        vals[10 + b] = (uint32_t)((cnt.d1s >> (16 * b)) & 0xFFFF);
+    }
+    vals[4] = cnt.valid;
+    vals[5] = cnt.win;
+#pragma unroll
+    for (int i = 0; i < 14; i++) vals[i] = wsum32(vals[i]);
+    if (lane == 0) {
+#pragma unroll
+        for (int i = 0; i < 14; i++) acc_add(&cx.acc[i], vals[i], weight);
+    }
+    cnt.base = cnt.d1w = cnt.d1s = 0;
+    cnt.valid = cnt.win = 0;
+}
+
+/* Count one chunk from entering state st.  Returns the exit state. */
+template <bool USE_LDS>
+__device__ void count_chunk(const Ctx &cx, uint64_t chunk, DState st, uint32_t weight,
+                            ChunkRec *rec, bool write_facts, bool write_obs) {
+    const int lane = threadIdx.x & 63;
+    const int64_t start = (int64_t)(chunk * FK_CHUNK_BYTES);
+    const uint64_t clen = min((uint64_t)FK_CHUNK_BYTES, cx.len - (uint64_t)start);
+    const uint32_t ntiles = (uint32_t)((clen + FK_TILE_BYTES - 1) / FK_TILE_BYTES);
+    Facts f{0, 0, 0, 0, 0, 0};
+    Counters cnt{0, 0, 0, 0, 0, 0, FK_NO_EOF};
+    const DState a = st;
+    for (uint32_t t = 0; t < ntiles; t++) {
+        uint32_t w[4];
+        int nb = load16(cx, start + (int64_t)t * FK_TILE_BYTES + lane * 16, w);
+        tile_general<true, USE_LDS>(cx, w, nb, t * FK_TILE_BYTES, st, f, cnt, weight);
+    }
+    flush_counters(cx, cnt, weight);
+    uint32_t unk = wsum32(cnt.unknown);
+    uint32_t eof = wmin32(cnt.eof);
+    if (lane == 0) {
+        ChunkRec &r = rec[chunk];
+        if (write_facts) {
+            r.a_code = a.code; r.a_R = a.R; r.a_hdr = a.hdr;
+            r.x_code = st.code; r.x_R = st.R; r.x_hdr = st.hdr;
+            r.flags = (f.found_p1 ? CR_FOUND_P1 : 0u) | (f.p1_gt ? CR_P1_GT : 0u) |
+                      (f.any_reset ? CR_ANY_RESET : 0u) |
+                      (f.reset_after_p1 ? CR_RESET_AFTER_P1 : 0u);
+            r.R_at_p1 = f.R_at_p1;
+            r.nv_total = f.nv_total;
+        }
+        if (write_obs) {
+            r.unknown = unk;
+            r.eof_off = eof;
+        }
+    }
+}
+
+/* Guess the state entering `chunk` from the FK_HALO_BYTES before it. */
+template <bool USE_LDS>
+__device__ DState halo_state(const Ctx &cx, uint64_t chunk) {
+    const int lane = threadIdx.x & 63;
+    const int64_t start = (int64_t)(chunk * FK_CHUNK_BYTES);
+    const int64_t hs = start - (int64_t)FK_HALO_BYTES;
+    uint32_t w[4];
+    int nb = 0;
+    if (lane < (int)(FK_HALO_BYTES / 16)) nb = load16(cx, hs + lane * 16, w);
+    else { w[0] = w[1] = w[2] = w[3] = 0; }
+    DState st{0, 0, 0};
+    Facts f{0, 0, 0, 0, 0, 0};
+    Counters cnt{0, 0, 0, 0, 0, 0, FK_NO_EOF};
+    tile_general<false, USE_LDS>(cx, w, nb, 0, st, f, cnt, 1u);
+    return st;
+}
+
+__device__ void lds_zero(uint32_t *lds, uint32_t nbins) {
+    for (uint32_t i = threadIdx.x; i < nbins; i += blockDim.x) lds[i] = 0;
+    __syncthreads();
+}
+__device__ void lds_flush(uint32_t *lds, uint32_t nbins, uint32_t *table) {
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < nbins; i += blockDim.x) {
+        uint32_t v = lds[i];
+        if (v) atomicAdd(&table[i], v);
+    }
+}
+
+/*
+ * k_count: main pass.  Chunk 0 takes the known entering state *d_init when
+ * has_init != 0 (stream continuation); every other chunk guesses from its halo.
+ */
+template <bool USE_LDS>
+__global__ void __launch_bounds__(FK_BLOCK)
+k_count(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint32_t *table,
+        uint32_t *shortcnt, unsigned long long *acc, ChunkRec *rec, uint64_t nchunks,
+        const XState *d_init, int has_init) {
+    extern __shared__ uint32_t lds_bins[];
+    const uint32_t nbins = USE_LDS ? (1u << (2 * k)) : 0u;
+    if (USE_LDS) lds_zero(lds_bins, nbins);
+    Ctx cx{buf, len, lo, table, USE_LDS ? lds_bins : nullptr, shortcnt, acc, maskk, k};
+    const uint64_t wave = blockIdx.x * FK_WAVES_PER_BLOCK + (threadIdx.x >> 6);
+    const uint64_t nwaves = (uint64_t)gridDim.x * FK_WAVES_PER_BLOCK;
+    for (uint64_t c = wave; c < nchunks; c += nwaves) {
+        DState st;
+        if (c == 0 && has_init) {
+            st.hdr = d_init->hdr;
+            st.R = (uint32_t)d_init->R;
+            st.code = d_init->code;
+        } else {
+            st = halo_state<USE_LDS>(cx, c);
+        }
+        count_chunk<USE_LDS>(cx, c, st, 1u, rec, true, true);
+    }
+    if (USE_LDS) lds_flush(lds_bins, nbins, table);
+}
+
+/*
+ * k_redo: for each listed chunk, cancel the main pass's contribution (weight
+ * -1 from the guessed state recorded in rec) and count it again from the
+ * exact state.  mode 1 = "cancel all from s_true" (used when a 0xFF byte
+ * truncates the segment and everything must be undone).
+ */
+template <bool USE_LDS>
+__global__ void __launch_bounds__(FK_BLOCK)
+k_redo(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint32_t *table,
+       uint32_t *shortcnt, unsigned long long *acc, ChunkRec *rec, const XState *s_true,
+       const uint32_t *list, const uint32_t *list_n, uint64_t nchunks, int mode) {
+    extern __shared__ uint32_t lds_bins[];
+    const uint32_t nbins = USE_LDS ? (1u << (2 * k)) : 0u;
+    const uint64_t n = mode == 1 ? nchunks : (uint64_t)*list_n;
+    if (n == 0) return;   /* uniform across the grid */
+    if (USE_LDS) lds_zero(lds_bins, nbins);
+    Ctx cx{buf, len, lo, table, USE_LDS ? lds_bins : nullptr, shortcnt, acc, maskk, k};
+    const uint64_t wave = blockIdx.x * FK_WAVES_PER_BLOCK + (threadIdx.x >> 6);
+    const uint64_t nwaves = (uint64_t)gridDim.x * FK_WAVES_PER_BLOCK;
+    for (uint64_t i = wave; i < n; i += nwaves) {
+        uint64_t c = mode == 1 ? i : list[i];
+        const XState t = s_true[c];
+        DState ts{t.code, (uint32_t)t.R, t.hdr};
+        if (mode == 1) {
+            count_chunk<USE_LDS>(cx, c, ts, 0xFFFFFFFFu, rec, false, false);
+        } else {
+            const ChunkRec r = rec[c];
+            DState as{r.a_code, r.a_R, r.a_hdr};
+            count_chunk<USE_LDS>(cx, c, as, 0xFFFFFFFFu, rec, false, false);
+            count_chunk<USE_LDS>(cx, c, ts, 1u, rec, false, true);
+        }
+    }
+    if (USE_LDS) lds_flush(lds_bins, nbins, table);
+}
+
+/*
+ * k_scan: exact entering state of every chunk.  One 1024-thread workgroup:
+ * each thread composes a contiguous run of chunk transfer functions, a
+ * Hillis-Steele scan over the 1024 aggregates in LDS, then each thread
+ * replays its run from its exact entering state.  mode 0 = resolve from
+ * *d_state (and write the exit back there); mode 1 = only reduce the total
+ * transfer function into *tf_total (shard summary).
+ */
+#define SCAN_THREADS 1024
+__global__ void __launch_bounds__(SCAN_THREADS)
+k_scan(const ChunkRec *rec, uint64_t n, XState *d_state, XState *s_true, uint32_t *redo_list,
+       uint32_t *redo_n, int k, int mode, TF *tf_total) {
+    __shared__ TF agg[SCAN_THREADS];
+    const uint32_t t = threadIdx.x;
+    const uint64_t per = (n + SCAN_THREADS - 1) / SCAN_THREADS;
+    const uint64_t lo = min((uint64_t)t * per, n), hi = min(lo + per, n);
+    TF a = fk_identity();
+    for (uint64_t c = lo; c < hi; c++) a = fk_compose(a, fk_tf_of(rec[c]));
+    agg[t] = a;
+    __syncthreads();
+    for (uint32_t d = 1; d < SCAN_THREADS; d <<= 1) {
+        TF mine = agg[t];
+        TF other = t >= d ? agg[t - d] : fk_identity();
+        __syncthreads();
+        if (t >= d) agg[t] = fk_compose(other, mine);
+        __syncthreads();
+    }
+    if (mode == 1) {
+        if (t == 0) *tf_total = agg[SCAN_THREADS - 1];
+        return;
+    }
+    const XState init = *d_state;
+    __syncthreads();
+    XState s = t == 0 ? init : fk_apply(agg[t - 1], init);
+    for (uint64_t c = lo; c < hi; c++) {
+        const ChunkRec r = rec[c];
+        s_true[c] = s;
+        DState as{r.a_code, r.a_R, r.a_hdr};
+        if (!fk_equiv(as, s, k, FK_CHUNK_BYTES)) {
+            uint32_t slot = atomicAdd(redo_n, 1u);
+            redo_list[slot] = (uint32_t)c;
+        }
+        s = fk_apply(fk_tf_of(r), s);
+    }
+    if (t == SCAN_THREADS - 1) {
+        XState fin = fk_apply(agg[SCAN_THREADS - 1], init);
+        s_true[n] = fin;
+        *d_state = fin;
+    }
+}
+
+/* Reduce per-chunk observations: first 0xFF byte (absolute) and unknown count. */
+__global__ void k_obs(const ChunkRec *rec, uint64_t n, unsigned long long *out /*[2]*/) {
+    unsigned long long unk = 0, eof = ~0ull;
+    for (uint64_t c = blockIdx.x * blockDim.x + threadIdx.x; c < n; c += (uint64_t)gridDim.x * blockDim.x) {
+        unk += rec[c].unknown;
+        if (rec[c].eof_off != FK_NO_EOF) eof = min(eof, (unsigned long long)(c * FK_CHUNK_BYTES + rec[c].eof_off));
+    }
+    if (unk) atomicAdd(&out[0], unk);
+    if (eof != ~0ull) atomicMin(&out[1], eof);
+}
+
+/* distinct k-mers: number of non-zero counters */
+__global__ void k_distinct(const uint32_t *table, uint64_t n, unsigned long long *out) {
+    unsigned long long c = 0;
+    const uint64_t n4 = n / 4;
+    const uint4 *t4 = reinterpret_cast<const uint4 *>(table);
+    for (uint64_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (uint64_t)gridDim.x * blockDim.x) {
+        uint4 v = t4[i];
+        c += (v.x != 0) + (v.y != 0) + (v.z != 0) + (v.w != 0);
+    }
+    for (uint64_t i = n4 * 4 + blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+        c += table[i] != 0;
+    c = wsum32((uint32_t)c);   /* <= 256 per lane-visit sum fits easily per wave */
+    if ((threadIdx.x & 63) == 0 && c) atomicAdd(out, c);
+}
+
+/* trie prefix presence, level d from level d+1 (or from the table at d = k-1) */
+__global__ void k_fold_from_table(const uint32_t *table, const uint32_t *shortd, uint8_t *pres,
+                                  uint64_t nd, unsigned long long *count) {
+    unsigned long long c = 0;
+    for (uint64_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nd; i += (uint64_t)gridDim.x * blockDim.x) {
+        uint4 v = reinterpret_cast<const uint4 *>(table)[i];
+        uint8_t p = (v.x | v.y | v.z | v.w) != 0 || shortd[i] != 0;
+        pres[i] = p;
+        c += p;
+    }
+    c = wsum32((uint32_t)c);
+    if ((threadIdx.x & 63) == 0 && c) atomicAdd(count, c);
+}
+__global__ void k_fold_level(const uint8_t *child, const uint32_t *shortd, uint8_t *pres,
+                             uint64_t nd, unsigned long long *count) {
+    unsigned long long c = 0;
+    for (uint64_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nd; i += (uint64_t)gridDim.x * blockDim.x) {
+        uint32_t ch = reinterpret_cast<const uint32_t *>(child)[i];
+        uint8_t p = ch != 0 || shortd[i] != 0;
+        pres[i] = p;
+        c += p;
+    }
+    c = wsum32((uint32_t)c);
+    if ((threadIdx.x & 63) == 0 && c) atomicAdd(count, c);
+}
+
+
+/* Header flag at each lane's start (last '>' vs last '\n' before it). */
+__device__ __forceinline__ uint32_t lane_hdr_entry(const uint32_t w[4], int nb, uint32_t hdr_in) {
+    const int lane = threadIdx.x & 63;
+    uint32_t g = 0, n = 0;
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+        uint32_t c = fk_byte(w, j);
+        uint32_t pos = (uint32_t)lane * 16u + (uint32_t)j + 1u;
+        if (j < nb && c == '>') g = pos;
+        if (j < nb && c == '\n') n = pos;
+    }
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        uint32_t tg = shup(g, d), tn = shup(n, d);
+        if (lane >= d) { g = max(g, tg); n = max(n, tn); }
+    }
+    uint32_t gx = shup(g, 1), nx = shup(n, 1);
+    if (lane == 0) { gx = 0; nx = 0; }
+    return (gx | nx) ? (gx > nx ? 1u : 0u) : hdr_in;
+}
+
+/*
+ * k_extract: copy the bytes that make the reference print "Unknown character
+ * %c processed!" (:581-584) to out[], in stream order.  One wave per listed
+ * chunk, entering header flag from the exact state scan.
+ */
+__global__ void __launch_bounds__(FK_BLOCK)
+k_extract(const uint8_t *buf, uint64_t len, int64_t lo, const XState *s_true, const uint32_t *list,
+          const uint64_t *offs, uint32_t nlist, uint8_t *out) {
+    const int lane = threadIdx.x & 63;
+    Ctx cx{buf, len, lo, nullptr, nullptr, nullptr, nullptr, 0, 0};
+    const uint64_t wave = blockIdx.x * FK_WAVES_PER_BLOCK + (threadIdx.x >> 6);
+    const uint64_t nwaves = (uint64_t)gridDim.x * FK_WAVES_PER_BLOCK;
+    for (uint64_t i = wave; i < nlist; i += nwaves) {
+        const uint64_t c = list[i];
+        uint32_t hdr = s_true[c].hdr;
+        uint64_t base = offs[i];
+        const int64_t start = (int64_t)(c * FK_CHUNK_BYTES);
+        const uint64_t clen = min((uint64_t)FK_CHUNK_BYTES, len - (uint64_t)start);
+        const uint32_t ntiles = (uint32_t)((clen + FK_TILE_BYTES - 1) / FK_TILE_BYTES);
+        for (uint32_t t = 0; t < ntiles; t++) {
+            uint32_t w[4];
+            int nb = load16(cx, start + (int64_t)t * FK_TILE_BYTES + lane * 16, w);
+            uint32_t h = lane_hdr_entry(w, nb, hdr);
+            uint32_t cntu = 0;
+#pragma unroll
+            for (int j = 0; j < 16; j++) {
+                if (j < nb) {
+                    uint32_t ch = fk_byte(w, j);
+                    if (h) { if (ch == '\n') h = 0; }
+                    else if (ch == '>') h = 1;
+                    else if (ch != '\n' && ch != 'N' && ch != 0xFFu && fk_sym(ch) < 0) cntu++;
+                }
+            }
+            uint32_t incl = cntu;
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {
+                uint32_t tv = shup(incl, d);
+                if (lane >= d) incl += tv;
+            }
+            uint64_t o = base + incl - cntu;
+            h = lane_hdr_entry(w, nb, hdr);
+#pragma unroll
+            for (int j = 0; j < 16; j++) {
+                if (j < nb) {
+                    uint32_t ch = fk_byte(w, j);
+                    if (h) { if (ch == '\n') h = 0; }
+                    else if (ch == '>') h = 1;
+                    else if (ch != '\n' && ch != 'N' && ch != 0xFFu && fk_sym(ch) < 0) out[o++] = (uint8_t)ch;
+                }
+            }
+            base += rdlane(incl, 63);
+            hdr = rdlane(h, 63);
+        }
+    }
+}
+
+__global__ void k_add_short(uint32_t *shortcnt, uint64_t idx) { atomicAdd(&shortcnt[idx], 1u); }
+
+/* synthetic input: byte[i] = "ACGT"[(splitmix64(seed + (i>>5)) >> 2(i&31)) & 3] */
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+    x += 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+__global__ void k_synth(uint8_t *out, uint64_t total, uint64_t seed, int fasta_line, uint64_t hlen) {
+    const uint64_t i16 = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) * 16;
+    if (i16 >= total) return;
+    uint8_t b[16];
+    const char *hdr = ">synthetic\n";
+    for (int j = 0; j < 16; j++) {
+        uint64_t o = i16 + j;
+        uint8_t v = 0;
+        if (o < total) {
+            if (o < hlen) {
+                v = (uint8_t)hdr[o];
+            } else {
+                uint64_t q = o - hlen, i;
+                if (fasta_line > 0) {
+                    uint64_t L = (uint64_t)fasta_line;
+                    uint64_t line = q / (L + 1), r = q % (L + 1);
+                    if (r == L) { b[j] = '\n'; continue; }
+                    i = line * L + r;
+                } else {
+                    i = q;
+                }
+                uint64_t wv = splitmix64(seed + (i >> 5));
+                v = (uint8_t)"ACGT"[(wv >> (2 * (i & 31))) & 3];
+            }
+        }
+        b[j] = v;
+    }
+    if (i16 + 16 <= total) {
+        uint4 v;
+        memcpy(&v, b, 16);
+        *reinterpret_cast<uint4 *>(out + i16) = v;
+    } else {
+        for (int j = 0; j < 16 && i16 + j < total; j++) out[i16 + j] = b[j];
+    }
+}
+
+/* ------------------------------------------------------------------------- */
+/* host engine                                                                */
+/* ------------------------------------------------------------------------- */
+
+#define HIPCHK(x)                                                               \
+    do {                                                                        \
+        hipError_t _e = (x);                                                    \
+        if (_e != hipSuccess) {                                                 \
+            fprintf(stderr, "findkmer: %s failed: %s (%s:%d)\n", #x,             \
+                    hipGetErrorString(_e), __FILE__, __LINE__);                 \
+            return FK_E_HIP;                                                    \
+        }                                                                       \
+    } while (0)
+
+static const uint64_t SEG_MAX_BYTES = 1ull << 34;                 /* 16 GiB per segment */
+static const uint64_t STAGE_BYTES = 256ull << 20;                 /* host feed staging */
+
+struct fk_engine {
+    int dev = 0, k = 0;
+    hipStream_t stream = nullptr;
+    bool own_stream = false;
+    fk_opts opts{};
+    uint64_t nbins = 0, nshort = 0, maskk = 0;
+    uint32_t *d_table = nullptr, *d_short = nullptr;
+    unsigned long long *d_acc = nullptr;   /* ACC_N slots */
+    unsigned long long *d_obs = nullptr;   /* [0] unknown, [1] eof, [2] distinct, [3] level count */
+    ChunkRec *d_rec = nullptr;
+    XState *d_strue = nullptr, *d_state = nullptr;
+    uint32_t *d_redo = nullptr, *d_redo_n = nullptr;
+    TF *d_tf = nullptr;
+    uint8_t *d_stage[2] = {nullptr, nullptr};
+    uint8_t *h_stage[2] = {nullptr, nullptr};
+    hipEvent_t ev[4] = {};
+    int cus = 256;
+    /* host-side bookkeeping */
+    XState state{0, 0, 0, 0};
+    uint64_t fed = 0, scanned = 0, unknown = 0, chunks = 0, redo = 0;
+    int ended = 0;         /* a 0xFF byte ended the input */
+    int shard_pending = 0; /* feed_shard done, resolve pending */
+    uint64_t shard_len = 0;
+    const uint8_t *shard_buf = nullptr;
+    int64_t shard_lo = 0;
+    double dev_ms = 0, main_ms = 0;
+    std::vector<uint8_t> unknown_bytes;
+    uint64_t chunk_cap = 0;
+};
+
+static int set_dev(fk_engine *e) {
+    HIPCHK(hipSetDevice(e->dev));
+    return FK_OK;
+}
+
+extern "C" int fk_abi_version(void) { return FK_ABI_VERSION; }
+
+extern "C" const char *fk_strerror(int s) {
+    switch (s) {
+    case FK_OK: return "ok";
+    case FK_E_INVALID: return "invalid argument";
+    case FK_E_K_UNSUPPORTED: return "k outside the dense-table range of this engine (1..16)";
+    case FK_E_NO_DEVICE: return "no HIP device available";
+    case FK_E_HIP: return "HIP runtime error";
+    case FK_E_OOM: return "out of memory";
+    case FK_E_EMPTY: return "Sequence File Is Empty, Ending Program";
+    case FK_E_UNTERMINATED_HEADER: return "input ends inside a '>' header line";
+    case FK_E_ROLLOVER: return "COUNTER ROLLOVER DETECTED";
+    case FK_E_STATE: return "engine API called out of order";
+    case FK_E_IO: return "I/O error";
+    case FK_E_RCCL: return "collective failed";
+    default: return "unknown error";
+    }
+}
+
+extern "C" int fk_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+static int zero_all(fk_engine *e) {
+    HIPCHK(hipMemsetAsync(e->d_table, 0, e->nbins * sizeof(uint32_t), e->stream));
+    if (e->nshort) HIPCHK(hipMemsetAsync(e->d_short, 0, e->nshort * sizeof(uint32_t), e->stream));
+    HIPCHK(hipMemsetAsync(e->d_acc, 0, ACC_N * sizeof(unsigned long long), e->stream));
+    XState z{0, 0, 0, 0};
+    HIPCHK(hipMemcpyAsync(e->d_state, &z, sizeof z, hipMemcpyHostToDevice, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    e->state = z;
+    e->fed = e->scanned = e->unknown = e->chunks = e->redo = 0;
+    e->ended = 0;
+    e->shard_pending = 0;
+    e->dev_ms = e->main_ms = 0;
+    e->unknown_bytes.clear();
+    return FK_OK;
+}
+
+extern "C" void fk_engine_destroy(fk_engine *e) {
+    if (!e) return;
+    hipSetDevice(e->dev);
+    if (e->stream) hipStreamSynchronize(e->stream);
+    hipFree(e->d_table); hipFree(e->d_short); hipFree(e->d_acc); hipFree(e->d_obs);
+    hipFree(e->d_rec); hipFree(e->d_strue); hipFree(e->d_state); hipFree(e->d_redo);
+    hipFree(e->d_redo_n); hipFree(e->d_tf);
+    for (int i = 0; i < 2; i++) { hipFree(e->d_stage[i]); hipHostFree(e->h_stage[i]); }
+    for (int i = 0; i < 4; i++) if (e->ev[i]) hipEventDestroy(e->ev[i]);
+    if (e->own_stream && e->stream) hipStreamDestroy(e->stream);
+    delete e;
+}
+
+extern "C" int fk_engine_create(int k, const fk_opts *opts, fk_engine **out) {
+    if (!out) return FK_E_INVALID;
+    *out = nullptr;
+    if (k < FK_K_MIN || k > FK_K_MAX_REF) return FK_E_INVALID;
+    if (k > FK_K_MAX_DENSE) return FK_E_K_UNSUPPORTED;
+    int ndev = fk_device_count();
+    if (ndev <= 0) return FK_E_NO_DEVICE;
+    fk_engine *e = new fk_engine();
+    if (opts) e->opts = *opts;
+    e->k = k;
+    if (e->opts.device >= 0) e->dev = e->opts.device;
+    else if (hipGetDevice(&e->dev) != hipSuccess) e->dev = 0;
+    if (e->dev >= ndev) { delete e; return FK_E_NO_DEVICE; }
+    int rc = set_dev(e);
+    if (rc) { delete e; return rc; }
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, e->dev) == hipSuccess && prop.multiProcessorCount > 0)
+        e->cus = prop.multiProcessorCount;
+    e->nbins = 1ull << (2 * k);
+    e->maskk = (k >= 32) ? ~0ull : (e->nbins - 1);
+    e->nshort = k > 1 ? ((1ull << (2 * k)) - 4) / 3 : 0;
+    if (e->opts.stream) { e->stream = (hipStream_t)e->opts.stream; }
+    else {
+        if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) { delete e; return FK_E_HIP; }
+        e->own_stream = true;
+    }
+#define ALLOC(p, bytes)                                                         \
+    if (hipMalloc((void **)&(p), (bytes)) != hipSuccess) { fk_engine_destroy(e); return FK_E_OOM; }
+    ALLOC(e->d_table, e->nbins * sizeof(uint32_t));
+    if (e->nshort) { ALLOC(e->d_short, e->nshort * sizeof(uint32_t)); }
+    ALLOC(e->d_acc, ACC_N * sizeof(unsigned long long));
+    ALLOC(e->d_obs, 8 * sizeof(unsigned long long));
+    ALLOC(e->d_state, sizeof(XState));
+    ALLOC(e->d_redo_n, sizeof(uint32_t));
+    ALLOC(e->d_tf, sizeof(TF));
+#undef ALLOC
+    for (int i = 0; i < 4; i++)
+        if (hipEventCreate(&e->ev[i]) != hipSuccess) { fk_engine_destroy(e); return FK_E_HIP; }
+    rc = zero_all(e);
+    if (rc) { fk_engine_destroy(e); return rc; }
+    *out = e;
+    return FK_OK;
+}
+
+extern "C" int fk_engine_reset(fk_engine *e) {
+    if (!e) return FK_E_INVALID;
+    int rc = set_dev(e);
+    if (rc) return rc;
+    return zero_all(e);
+}
+
+static int grow_chunk_arrays(fk_engine *e, uint64_t nchunks, uint64_t &cap) {
+    if (nchunks <= cap && e->d_rec) return FK_OK;
+    uint64_t nc = std::max<uint64_t>(nchunks, 1024);
+    hipFree(e->d_rec); hipFree(e->d_strue); hipFree(e->d_redo);
+    e->d_rec = nullptr; e->d_strue = nullptr; e->d_redo = nullptr;
+    if (hipMalloc((void **)&e->d_rec, nc * sizeof(ChunkRec)) != hipSuccess) return FK_E_OOM;
+    if (hipMalloc((void **)&e->d_strue, (nc + 1) * sizeof(XState)) != hipSuccess) return FK_E_OOM;
+    if (hipMalloc((void **)&e->d_redo, nc * sizeof(uint32_t)) != hipSuccess) return FK_E_OOM;
+    cap = nc;
+    return FK_OK;
+}
+
+static bool use_lds(const fk_engine *e) { return e->k <= FK_LDS_MAX_K; }
+
+static unsigned grid_for(const fk_engine *e, uint64_t nwork_waves) {
+    /* persistent: up to 2 blocks (16 waves) per CU for LDS bins, 4 otherwise */
+    uint64_t per_cu = use_lds(e) ? 2 : 4;
+    uint64_t maxb = (uint64_t)e->cus * per_cu;
+    uint64_t need = (nwork_waves + FK_WAVES_PER_BLOCK - 1) / FK_WAVES_PER_BLOCK;
+    return (unsigned)std::max<uint64_t>(1, std::min(maxb, need));
+}
+
+static size_t lds_bytes(const fk_engine *e) { return use_lds(e) ? (size_t)e->nbins * sizeof(uint32_t) : 0; }
+
+static int launch_count(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t lo, uint64_t nchunks,
+                        int has_init) {
+    unsigned g = grid_for(e, nchunks);
+    size_t sh = lds_bytes(e);
+    if (use_lds(e))
+        hipLaunchKernelGGL((k_count<true>), dim3(g), dim3(FK_BLOCK), sh, e->stream, buf, len, lo, e->k,
+                           e->maskk, e->d_table, e->d_short, e->d_acc, e->d_rec, nchunks, e->d_state,
+                           has_init);
+    else
+        hipLaunchKernelGGL((k_count<false>), dim3(g), dim3(FK_BLOCK), 0, e->stream, buf, len, lo, e->k,
+                           e->maskk, e->d_table, e->d_short, e->d_acc, e->d_rec, nchunks, e->d_state,
+                           has_init);
+    HIPCHK(hipGetLastError());
+    return FK_OK;
+}
+
+static int launch_redo(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t lo, uint64_t nchunks,
+                       int mode) {
+    unsigned g = mode == 1 ? grid_for(e, nchunks) : grid_for(e, std::min<uint64_t>(nchunks, 4096));
+    size_t sh = lds_bytes(e);
+    if (use_lds(e))
+        hipLaunchKernelGGL((k_redo<true>), dim3(g), dim3(FK_BLOCK), sh, e->stream, buf, len, lo, e->k,
+                           e->maskk, e->d_table, e->d_short, e->d_acc, e->d_rec, e->d_strue, e->d_redo,
+                           e->d_redo_n, nchunks, mode);
+    else
+        hipLaunchKernelGGL((k_redo<false>), dim3(g), dim3(FK_BLOCK), 0, e->stream, buf, len, lo, e->k,
+                           e->maskk, e->d_table, e->d_short, e->d_acc, e->d_rec, e->d_strue, e->d_redo,
+                           e->d_redo_n, nchunks, mode);
+    HIPCHK(hipGetLastError());
+    return FK_OK;
+}
+
+static int launch_scan(fk_engine *e, uint64_t nchunks, int mode) {
+    HIPCHK(hipMemsetAsync(e->d_redo_n, 0, sizeof(uint32_t), e->stream));
+    hipLaunchKernelGGL(k_scan, dim3(1), dim3(SCAN_THREADS), 0, e->stream, e->d_rec, nchunks, e->d_state,
+                       e->d_strue, e->d_redo, e->d_redo_n, e->k, mode, e->d_tf);
+    HIPCHK(hipGetLastError());
+    return FK_OK;
+}
+
+struct SegOut {
+    XState exit;
+    unsigned long long unknown, eof;
+    uint32_t redo_n;
+};
+
+static int read_segment(fk_engine *e, uint64_t nchunks, SegOut &o) {
+    HIPCHK(hipMemsetAsync(e->d_obs, 0, 2 * sizeof(unsigned long long), e->stream));
+    unsigned long long init_eof = ~0ull;
+    HIPCHK(hipMemcpyAsync(e->d_obs + 1, &init_eof, sizeof init_eof, hipMemcpyHostToDevice, e->stream));
+    unsigned g = (unsigned)std::min<uint64_t>(1024, (nchunks + 255) / 256 + 1);
+    hipLaunchKernelGGL(k_obs, dim3(g), dim3(256), 0, e->stream, e->d_rec, nchunks, e->d_obs);
+    HIPCHK(hipGetLastError());
+    unsigned long long obs[2];
+    HIPCHK(hipMemcpyAsync(obs, e->d_obs, sizeof obs, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipMemcpyAsync(&o.exit, e->d_state, sizeof(XState), hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipMemcpyAsync(&o.redo_n, e->d_redo_n, sizeof(uint32_t), hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    o.unknown = obs[0];
+    o.eof = obs[1];
+    return FK_OK;
+}
+
+/* Collect the unknown bytes of the just-counted segment (stream order). */
+static int collect_unknown(fk_engine *e, const uint8_t *dbuf, uint64_t len, int64_t lo, uint64_t nchunks,
+                           uint64_t total) {
+    if (!total || !e->opts.collect_unknown) return FK_OK;
+    std::vector<ChunkRec> rec((size_t)nchunks);
+    HIPCHK(hipMemcpyAsync(rec.data(), e->d_rec, nchunks * sizeof(ChunkRec), hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    std::vector<uint32_t> list;
+    std::vector<uint64_t> offs;
+    uint64_t acc = 0;
+    for (uint64_t c = 0; c < nchunks; c++)
+        if (rec[(size_t)c].unknown) { list.push_back((uint32_t)c); offs.push_back(acc); acc += rec[(size_t)c].unknown; }
+    uint32_t *d_list = nullptr;
+    uint64_t *d_offs = nullptr;
+    uint8_t *d_out = nullptr;
+    if (hipMalloc((void **)&d_list, list.size() * 4) != hipSuccess ||
+        hipMalloc((void **)&d_offs, offs.size() * 8) != hipSuccess ||
+        hipMalloc((void **)&d_out, acc) != hipSuccess) {
+        hipFree(d_list); hipFree(d_offs); hipFree(d_out);
+        return FK_E_OOM;
+    }
+    HIPCHK(hipMemcpyAsync(d_list, list.data(), list.size() * 4, hipMemcpyHostToDevice, e->stream));
+    HIPCHK(hipMemcpyAsync(d_offs, offs.data(), offs.size() * 8, hipMemcpyHostToDevice, e->stream));
+    unsigned g = grid_for(e, list.size());
+    hipLaunchKernelGGL(k_extract, dim3(g), dim3(FK_BLOCK), 0, e->stream, dbuf, len, lo, e->d_strue, d_list, d_offs,
+                       (uint32_t)list.size(), d_out);
+    HIPCHK(hipGetLastError());
+    size_t old = e->unknown_bytes.size();
+    e->unknown_bytes.resize(old + acc);
+    HIPCHK(hipMemcpyAsync(e->unknown_bytes.data() + old, d_out, acc, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    hipFree(d_list); hipFree(d_offs); hipFree(d_out);
+    return FK_OK;
+}
+
+/* Count one device-resident segment continuing from e->state (exact). */
+static int process_segment(fk_engine *e, const uint8_t *dbuf, uint64_t len, uint64_t &cap) {
+    if (len == 0 || e->ended) return FK_OK;
+    uint64_t nchunks = (len + FK_CHUNK_BYTES - 1) / FK_CHUNK_BYTES;
+    int rc = grow_chunk_arrays(e, nchunks, cap);
+    if (rc) return rc;
+    HIPCHK(hipEventRecord(e->ev[0], e->stream));
+    rc = launch_count(e, dbuf, len, 0, nchunks, 1);
+    if (rc) return rc;
+    HIPCHK(hipEventRecord(e->ev[1], e->stream));
+    rc = launch_scan(e, nchunks, 0);
+    if (rc) return rc;
+    rc = launch_redo(e, dbuf, len, 0, nchunks, 0);
+    if (rc) return rc;
+    HIPCHK(hipEventRecord(e->ev[2], e->stream));
+    SegOut o;
+    rc = read_segment(e, nchunks, o);
+    if (rc) return rc;
+    float ms_main = 0, ms_all = 0;
+    hipEventElapsedTime(&ms_main, e->ev[0], e->ev[1]);
+    hipEventElapsedTime(&ms_all, e->ev[0], e->ev[2]);
+    e->main_ms += ms_main;
+    e->dev_ms += ms_all;
+    e->chunks += nchunks;
+    e->redo += o.redo_n;
+    if (o.eof != ~0ull) {
+        /* A 0xFF byte outside a header ends the reference's scan (:988):
+           undo this segment and count only the bytes before it. */
+        rc = launch_redo(e, dbuf, len, 0, nchunks, 1);
+        if (rc) return rc;
+        XState entering = e->state;
+        HIPCHK(hipMemcpyAsync(e->d_state, &entering, sizeof entering, hipMemcpyHostToDevice, e->stream));
+        uint64_t tl = o.eof;
+        e->ended = 1;
+        e->scanned += tl;
+        if (tl == 0) {
+            HIPCHK(hipStreamSynchronize(e->stream));
+            return FK_OK;
+        }
+        uint64_t nc2 = (tl + FK_CHUNK_BYTES - 1) / FK_CHUNK_BYTES;
+        rc = launch_count(e, dbuf, tl, 0, nc2, 1);
+        if (rc) return rc;
+        rc = launch_scan(e, nc2, 0);
+        if (rc) return rc;
+        rc = launch_redo(e, dbuf, tl, 0, nc2, 0);
+        if (rc) return rc;
+        SegOut o2;
+        rc = read_segment(e, nc2, o2);
+        if (rc) return rc;
+        e->state = o2.exit;
+        e->unknown += o2.unknown;
+        e->redo += o2.redo_n;
+        return collect_unknown(e, dbuf, tl, 0, nc2, o2.unknown);
+    }
+    e->state = o.exit;
+    e->unknown += o.unknown;
+    e->scanned += len;
+    return collect_unknown(e, dbuf, len, 0, nchunks, o.unknown);
+}
+
+extern "C" int fk_engine_feed(fk_engine *e, const uint8_t *buf, uint64_t len, int on_device) {
+    if (!e || (!buf && len)) return FK_E_INVALID;
+    if (e->shard_pending) return FK_E_STATE;
+    int rc = set_dev(e);
+    if (rc) return rc;
+    e->fed += len;
+    if (e->ended || len == 0) return FK_OK;
+    uint64_t &cap = e->chunk_cap;
+    if (on_device && ((uintptr_t)buf & 15) == 0) {
+        for (uint64_t off = 0; off < len && !e->ended; off += SEG_MAX_BYTES) {
+            uint64_t n = std::min(SEG_MAX_BYTES, len - off);
+            rc = process_segment(e, buf + off, n, cap);
+            if (rc) return rc;
+        }
+        return FK_OK;
+    }
+    /* stage through pinned host memory (or realign device input) */
+    if (!e->d_stage[0] && hipMalloc((void **)&e->d_stage[0], STAGE_BYTES) != hipSuccess) return FK_E_OOM;
+    if (!on_device && !e->h_stage[0] &&
+        hipHostMalloc((void **)&e->h_stage[0], STAGE_BYTES, hipHostMallocDefault) != hipSuccess)
+        return FK_E_OOM;
+    for (uint64_t off = 0; off < len && !e->ended; off += STAGE_BYTES) {
+        uint64_t n = std::min(STAGE_BYTES, len - off);
+        if (on_device) {
+            HIPCHK(hipMemcpyAsync(e->d_stage[0], buf + off, n, hipMemcpyDeviceToDevice, e->stream));
+        } else {
+            memcpy(e->h_stage[0], buf + off, n);
+            HIPCHK(hipMemcpyAsync(e->d_stage[0], e->h_stage[0], n, hipMemcpyHostToDevice, e->stream));
+        }
+        rc = process_segment(e, e->d_stage[0], n, cap);
+        if (rc) return rc;
+    }
+    return FK_OK;
+}
+
+extern "C" int fk_engine_state(fk_engine *e, fk_state *out) {
+    if (!e || !out) return FK_E_INVALID;
+    out->run = e->state.R;
+    out->code = e->state.code;
+    out->hdr = e->state.hdr;
+    out->pad = 0;
+    return FK_OK;
+}
+
+/* ---- shards ---- */
+
+extern "C" int fk_engine_feed_shard(fk_engine *e, const uint8_t *buf, uint64_t len, uint64_t halo,
+                                    int on_device) {
+    if (!e || !buf || !on_device) return FK_E_INVALID;   /* shards are device-resident */
+    if (e->fed || e->shard_pending) return FK_E_STATE;
+    if (len > SEG_MAX_BYTES || ((uintptr_t)buf & 15) || (halo & 15)) return FK_E_INVALID;
+    int rc = set_dev(e);
+    if (rc) return rc;
+    uint64_t &cap = e->chunk_cap;
+    e->fed = len;
+    e->shard_buf = buf;
+    e->shard_len = len;
+    e->shard_lo = -(int64_t)std::min<uint64_t>(halo, FK_HALO_BYTES);
+    e->shard_pending = 1;
+    if (len == 0) return FK_OK;
+    uint64_t nchunks = (len + FK_CHUNK_BYTES - 1) / FK_CHUNK_BYTES;
+    rc = grow_chunk_arrays(e, nchunks, cap);
+    if (rc) return rc;
+    HIPCHK(hipEventRecord(e->ev[0], e->stream));
+    rc = launch_count(e, buf, len, e->shard_lo, nchunks, 0);
+    if (rc) return rc;
+    HIPCHK(hipEventRecord(e->ev[1], e->stream));
+    rc = launch_scan(e, nchunks, 1);
+    if (rc) return rc;
+    HIPCHK(hipStreamSynchronize(e->stream));
+    float ms = 0;
+    hipEventElapsedTime(&ms, e->ev[0], e->ev[1]);
+    e->main_ms += ms;
+    e->dev_ms += ms;
+    e->chunks += nchunks;
+    return FK_OK;
+}
+
+extern "C" int fk_engine_summary(fk_engine *e, fk_summary *out) {
+    if (!e || !out) return FK_E_INVALID;
+    static_assert(sizeof(TF) <= sizeof(fk_summary), "summary too small");
+    memset(out, 0, sizeof *out);
+    TF t = fk_identity();
+    if (e->shard_pending && e->shard_len) {
+        int rc = set_dev(e);
+        if (rc) return rc;
+        HIPCHK(hipMemcpy(&t, e->d_tf, sizeof t, hipMemcpyDeviceToHost));
+    }
+    memcpy(out, &t, sizeof t);
+    return FK_OK;
+}
+
+extern "C" int fk_summary_apply(const fk_summary *s, const fk_state *in, fk_state *out) {
+    if (!s || !in || !out) return FK_E_INVALID;
+    TF t;
+    memcpy(&t, s, sizeof t);
+    XState x{in->run, in->code, in->hdr, 0};
+    XState y = fk_apply(t, x);
+    out->run = y.R;
+    out->code = y.code;
+    out->hdr = y.hdr;
+    out->pad = 0;
+    return FK_OK;
+}
+
+extern "C" int fk_engine_resolve(fk_engine *e, const fk_state *entering) {
+    if (!e || !entering) return FK_E_INVALID;
+    if (!e->shard_pending) return FK_E_STATE;
+    int rc = set_dev(e);
+    if (rc) return rc;
+    XState in{entering->run, entering->code, entering->hdr, 0};
+    e->shard_pending = 0;
+    e->state = in;
+    HIPCHK(hipMemcpyAsync(e->d_state, &in, sizeof in, hipMemcpyHostToDevice, e->stream));
+    if (e->shard_len == 0) return FK_OK;
+    uint64_t nchunks = (e->shard_len + FK_CHUNK_BYTES - 1) / FK_CHUNK_BYTES;
+    HIPCHK(hipEventRecord(e->ev[0], e->stream));
+    rc = launch_scan(e, nchunks, 0);
+    if (rc) return rc;
+    rc = launch_redo(e, e->shard_buf, e->shard_len, e->shard_lo, nchunks, 0);
+    if (rc) return rc;
+    HIPCHK(hipEventRecord(e->ev[2], e->stream));
+    SegOut o;
+    rc = read_segment(e, nchunks, o);
+    if (rc) return rc;
+    float ms = 0;
+    hipEventElapsedTime(&ms, e->ev[0], e->ev[2]);
+    e->dev_ms += ms;
+    e->redo += o.redo_n;
+    if (o.eof != ~0ull) {
+        /* cancel everything and recount the prefix before the 0xFF byte */
+        rc = launch_redo(e, e->shard_buf, e->shard_len, e->shard_lo, nchunks, 1);
+        if (rc) return rc;
+        HIPCHK(hipMemcpyAsync(e->d_state, &in, sizeof in, hipMemcpyHostToDevice, e->stream));
+        e->ended = 1;
+        e->scanned += o.eof;
+        uint64_t tl = o.eof;
+        if (tl) {
+            uint64_t nc2 = (tl + FK_CHUNK_BYTES - 1) / FK_CHUNK_BYTES;
+            rc = launch_count(e, e->shard_buf, tl, e->shard_lo, nc2, 1);
+            if (rc) return rc;
+            rc = launch_scan(e, nc2, 0);
+            if (rc) return rc;
+            rc = launch_redo(e, e->shard_buf, tl, e->shard_lo, nc2, 0);
+            if (rc) return rc;
+            SegOut o2;
+            rc = read_segment(e, nc2, o2);
+            if (rc) return rc;
+            e->state = o2.exit;
+            e->unknown += o2.unknown;
+            return collect_unknown(e, e->shard_buf, tl, e->shard_lo, nc2, o2.unknown);
+        }
+        HIPCHK(hipStreamSynchronize(e->stream));
+        return FK_OK;
+    }
+    e->state = o.exit;
+    e->unknown += o.unknown;
+    e->scanned += e->shard_len;
+    return collect_unknown(e, e->shard_buf, e->shard_len, e->shard_lo, nchunks, o.unknown);
+}
+
+/* ---- finish ---- */
+
+extern "C" int fk_engine_finish(fk_engine *e, fk_result *res) {
+    if (!e || !res) return FK_E_INVALID;
+    if (e->shard_pending) return FK_E_STATE;
+    int rc = set_dev(e);
+    if (rc) return rc;
+    memset(res, 0, sizeof *res);
+    const int k = e->k;
+    /* an input ending with a run of 1..k-1 bases leaves its prefix walk */
+    int32_t seq = (int32_t)(uint32_t)e->state.R;
+    if (!e->state.hdr && seq >= 1 && seq < k) {
+        uint64_t off = ((1ull << (2 * seq)) - 4) / 3;
+        uint64_t idx = off + (e->state.code & ((1ull << (2 * seq)) - 1));
+        hipLaunchKernelGGL(k_add_short, dim3(1), dim3(1), 0, e->stream, e->d_short, idx);
+        HIPCHK(hipGetLastError());
+    }
+    unsigned long long acc[ACC_N];
+    HIPCHK(hipMemcpyAsync(acc, e->d_acc, sizeof acc, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipMemsetAsync(e->d_obs + 2, 0, sizeof(unsigned long long), e->stream));
+    unsigned gd = (unsigned)std::min<uint64_t>((uint64_t)e->cus * 4, (e->nbins / 4 + 255) / 256 + 1);
+    hipLaunchKernelGGL(k_distinct, dim3(gd), dim3(256), 0, e->stream, e->d_table, e->nbins, e->d_obs + 2);
+    HIPCHK(hipGetLastError());
+    unsigned long long distinct = 0;
+    HIPCHK(hipMemcpyAsync(&distinct, e->d_obs + 2, sizeof distinct, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    for (int b = 0; b < 4; b++) {
+        res->base_count[b] = acc[ACC_BASE + b];
+        res->depth1[b] = acc[ACC_D1W + b] + acc[ACC_D1S + b];
+        if (res->depth1[b] >= (1ull << 32)) res->rollover = 1;
+    }
+    res->valid_bases = acc[ACC_VALID];
+    res->windows = acc[ACC_WIN];
+    res->distinct = distinct;
+    res->unknown_chars = e->unknown;
+    res->scanned_bytes = e->ended ? e->scanned : e->fed;
+    res->hit_eof_byte = e->ended;
+    res->unterminated_header = e->state.hdr ? 1 : 0;
+    res->chunks = e->chunks;
+    res->redo_chunks = e->redo;
+    res->device_ms = e->dev_ms;
+    res->main_kernel_ms = e->main_ms;
+    uint64_t any_walk = res->depth1[0] | res->depth1[1] | res->depth1[2] | res->depth1[3];
+    if (e->opts.want_nodes) {
+        /* nodeCounter = head + distinct prefixes of every walk (:620) */
+        uint64_t nodes = 0;
+        if (any_walk) {
+            nodes = 1 + distinct;
+            if (k >= 2) {
+                uint8_t *pa = nullptr, *pb = nullptr;
+                uint64_t n1 = 1ull << (2 * (k - 1));
+                if (hipMalloc((void **)&pa, n1) != hipSuccess) return FK_E_OOM;
+                if (hipMalloc((void **)&pb, std::max<uint64_t>(n1 / 4, 4)) != hipSuccess) { hipFree(pa); return FK_E_OOM; }
+                uint8_t *cur = pa, *nxt = pb;
+                for (int d = k - 1; d >= 1; d--) {
+                    uint64_t nd = 1ull << (2 * d);
+                    uint64_t off = ((1ull << (2 * d)) - 4) / 3;
+                    HIPCHK(hipMemsetAsync(e->d_obs + 3, 0, sizeof(unsigned long long), e->stream));
+                    unsigned g = (unsigned)std::min<uint64_t>((uint64_t)e->cus * 4, nd / 256 + 1);
+                    if (d == k - 1)
+                        hipLaunchKernelGGL(k_fold_from_table, dim3(g), dim3(256), 0, e->stream, e->d_table,
+                                           e->d_short + off, cur, nd, e->d_obs + 3);
+                    else
+                        hipLaunchKernelGGL(k_fold_level, dim3(g), dim3(256), 0, e->stream, nxt,
+                                           e->d_short + off, cur, nd, e->d_obs + 3);
+                    HIPCHK(hipGetLastError());
+                    unsigned long long c = 0;
+                    HIPCHK(hipMemcpyAsync(&c, e->d_obs + 3, sizeof c, hipMemcpyDeviceToHost, e->stream));
+                    HIPCHK(hipStreamSynchronize(e->stream));
+                    nodes += c;
+                    std::swap(cur, nxt);   /* this level becomes the child level */
+                }
+                hipFree(pa);
+                hipFree(pb);
+            }
+        }
+        res->nodes = nodes;
+        res->nodes_valid = 1;
+    }
+    if (e->fed == 0) return FK_E_EMPTY;
+    if (res->rollover) return FK_E_ROLLOVER;
+    if (res->unterminated_header) return FK_E_UNTERMINATED_HEADER;
+    return FK_OK;
+}
+
+extern "C" int fk_engine_progress(fk_engine *e, uint64_t *valid_bases, uint64_t *windows) {
+    if (!e) return FK_E_INVALID;
+    int rc = set_dev(e);
+    if (rc) return rc;
+    unsigned long long acc[ACC_N];
+    HIPCHK(hipMemcpyAsync(acc, e->d_acc, sizeof acc, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    if (valid_bases) *valid_bases = acc[ACC_VALID];
+    if (windows) *windows = acc[ACC_WIN];
+    return FK_OK;
+}
+
+extern "C" int fk_engine_table(fk_engine *e, uint32_t *counts) {
+    if (!e || !counts) return FK_E_INVALID;
+    int rc = set_dev(e);
+    if (rc) return rc;
+    HIPCHK(hipMemcpyAsync(counts, e->d_table, e->nbins * sizeof(uint32_t), hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    return FK_OK;
+}
+
+extern "C" int fk_engine_table_device(fk_engine *e, uint32_t **dev_counts) {
+    if (!e || !dev_counts) return FK_E_INVALID;
+    *dev_counts = e->d_table;
+    return FK_OK;
+}
+
+extern "C" int fk_engine_table_to_device(fk_engine *e, void *dst) {
+    if (!e || !dst) return FK_E_INVALID;
+    int rc = set_dev(e);
+    if (rc) return rc;
+    HIPCHK(hipMemcpyAsync(dst, e->d_table, e->nbins * sizeof(uint32_t), hipMemcpyDeviceToDevice, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    return FK_OK;
+}
+
+extern "C" int fk_engine_table_from_device(fk_engine *e, const void *src) {
+    if (!e || !src) return FK_E_INVALID;
+    int rc = set_dev(e);
+    if (rc) return rc;
+    HIPCHK(hipMemcpyAsync(e->d_table, src, e->nbins * sizeof(uint32_t), hipMemcpyDeviceToDevice, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    return FK_OK;
+}
+
+extern "C" int fk_engine_unknown(fk_engine *e, uint8_t *out, uint64_t cap, uint64_t *n) {
+    if (!e || !n) return FK_E_INVALID;
+    *n = e->unknown_bytes.size();
+    if (out) memcpy(out, e->unknown_bytes.data(), std::min<uint64_t>(cap, *n));
+    return FK_OK;
+}
+
+__global__ void k_add_tables(uint32_t *dst, const uint32_t *src, uint64_t n) {
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+        dst[i] += src[i];
+}
+__global__ void k_add_acc(unsigned long long *dst, const unsigned long long *src, int n) {
+    int i = threadIdx.x;
+    if (i < n) dst[i] += src[i];
+}
+
+extern "C" int fk_engine_merge_from(fk_engine *dst, fk_engine *src) {
+    if (!dst || !src || dst->k != src->k) return FK_E_INVALID;
+    int rc = set_dev(src);
+    if (rc) return rc;
+    HIPCHK(hipStreamSynchronize(src->stream));
+    rc = set_dev(dst);
+    if (rc) return rc;
+    uint32_t *tmp = nullptr;
+    uint32_t *tmps = nullptr;
+    unsigned long long *tmpa = nullptr;
+    if (hipMalloc((void **)&tmp, dst->nbins * sizeof(uint32_t)) != hipSuccess) return FK_E_OOM;
+    if (dst->nshort && hipMalloc((void **)&tmps, dst->nshort * sizeof(uint32_t)) != hipSuccess) { hipFree(tmp); return FK_E_OOM; }
+    if (hipMalloc((void **)&tmpa, ACC_N * sizeof(unsigned long long)) != hipSuccess) { hipFree(tmp); hipFree(tmps); return FK_E_OOM; }
+    HIPCHK(hipMemcpyPeerAsync(tmp, dst->dev, src->d_table, src->dev, dst->nbins * sizeof(uint32_t), dst->stream));
+    if (dst->nshort) HIPCHK(hipMemcpyPeerAsync(tmps, dst->dev, src->d_short, src->dev, dst->nshort * sizeof(uint32_t), dst->stream));
+    HIPCHK(hipMemcpyPeerAsync(tmpa, dst->dev, src->d_acc, src->dev, ACC_N * sizeof(unsigned long long), dst->stream));
+    unsigned g = (unsigned)std::min<uint64_t>((uint64_t)dst->cus * 8, dst->nbins / 256 + 1);
+    hipLaunchKernelGGL(k_add_tables, dim3(g), dim3(256), 0, dst->stream, dst->d_table, tmp, dst->nbins);
+    if (dst->nshort) {
+        unsigned gs = (unsigned)std::min<uint64_t>((uint64_t)dst->cus * 8, dst->nshort / 256 + 1);
+        hipLaunchKernelGGL(k_add_tables, dim3(gs), dim3(256), 0, dst->stream, dst->d_short, tmps, dst->nshort);
+    }
+    hipLaunchKernelGGL(k_add_acc, dim3(1), dim3(64), 0, dst->stream, dst->d_acc, tmpa, (int)ACC_N);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(dst->stream));
+    hipFree(tmp); hipFree(tmps); hipFree(tmpa);
+    dst->unknown += src->unknown;
+    dst->unknown_bytes.insert(dst->unknown_bytes.end(), src->unknown_bytes.begin(), src->unknown_bytes.end());
+    dst->chunks += src->chunks;
+    dst->redo += src->redo;
+    dst->dev_ms += src->dev_ms;
+    dst->main_ms += src->main_ms;
+    return FK_OK;
+}
+
+/* ---- one-shot helpers ---- */
+
+extern "C" int fk_count(const uint8_t *buf, uint64_t len, int k, const fk_opts *opts, uint32_t *counts,
+                        fk_result *res) {
+    fk_engine *e = nullptr;
+    int rc = fk_engine_create(k, opts, &e);
+    if (rc) return rc;
+    fk_result tmp;
+    if (!res) res = &tmp;
+    rc = fk_engine_feed(e, buf, len, 0);
+    if (rc == FK_OK) {
+        rc = fk_engine_finish(e, res);
+        if (counts && (rc == FK_OK || rc == FK_E_UNTERMINATED_HEADER)) {
+            int r2 = fk_engine_table(e, counts);
+            if (r2) rc = r2;
+        }
+    }
+    fk_engine_destroy(e);
+    return rc;
+}
+
+extern "C" int fk_count_multi(const uint8_t *buf, uint64_t len, int k, int ngpu, const fk_opts *opts,
+                              uint32_t *counts, fk_result *res) {
+    int ndev = fk_device_count();
+    if (ngpu <= 0 || ngpu > ndev) ngpu = ndev;
+    if (ngpu <= 1 || len < (uint64_t)ngpu * FK_CHUNK_BYTES) return fk_count(buf, len, k, opts, counts, res);
+    std::vector<fk_engine *> eng((size_t)ngpu, nullptr);
+    std::vector<uint8_t *> dbuf((size_t)ngpu, nullptr);
+    int rc = FK_OK;
+    /* contiguous shards aligned to chunk multiples; each carries a halo */
+    uint64_t per = ((len / (uint64_t)ngpu) / FK_CHUNK_BYTES) * FK_CHUNK_BYTES;
+    std::vector<uint64_t> off((size_t)ngpu + 1);
+    for (int g = 0; g < ngpu; g++) off[(size_t)g] = (uint64_t)g * per;
+    off[(size_t)ngpu] = len;
+    for (int g = 0; g < ngpu && rc == FK_OK; g++) {
+        fk_opts o = opts ? *opts : fk_opts{};
+        o.device = g;
+        o.stream = nullptr;
+        rc = fk_engine_create(k, &o, &eng[(size_t)g]);
+        if (rc) break;
+        uint64_t halo = g ? FK_HALO_BYTES : 0;
+        uint64_t n = off[(size_t)g + 1] - off[(size_t)g];
+        hipSetDevice(g);
+        if (hipMalloc((void **)&dbuf[(size_t)g], n + halo + 16) != hipSuccess) { rc = FK_E_OOM; break; }
+        if (hipMemcpy(dbuf[(size_t)g], buf + off[(size_t)g] - halo, n + halo, hipMemcpyHostToDevice) != hipSuccess) { rc = FK_E_HIP; break; }
+        rc = fk_engine_feed_shard(eng[(size_t)g], dbuf[(size_t)g] + halo, n, halo, 1);
+    }
+    if (rc == FK_OK) {
+        fk_state s{0, 0, 0, 0};
+        for (int g = 0; g < ngpu && rc == FK_OK; g++) {
+            fk_summary sm;
+            rc = fk_engine_summary(eng[(size_t)g], &sm);
+            if (rc) break;
+            rc = fk_engine_resolve(eng[(size_t)g], &s);
+            if (rc) break;
+            if (eng[(size_t)g]->ended) {   /* a 0xFF byte: later shards are not scanned */
+                for (int h = g + 1; h < ngpu; h++) { eng[(size_t)h]->shard_pending = 0; }
+                fk_engine_state(eng[(size_t)g], &s);
+                for (int h = g + 1; h < ngpu; h++) {
+                    fk_engine_reset(eng[(size_t)h]);
+                }
+                break;
+            }
+            fk_engine_state(eng[(size_t)g], &s);
+        }
+    }
+    if (rc == FK_OK) {
+        for (int g = 1; g < ngpu && rc == FK_OK; g++) rc = fk_engine_merge_from(eng[0], eng[(size_t)g]);
+        /* the stream's end state lives in the last shard that scanned */
+        if (rc == FK_OK) {
+            fk_state s;
+            int last = ngpu - 1;
+            for (int g = 0; g < ngpu; g++) if (eng[(size_t)g]->ended) { last = g; break; }
+            fk_engine_state(eng[(size_t)last], &s);
+            eng[0]->state = XState{s.run, s.code, s.hdr, 0};
+            uint64_t fed = 0, sc = 0;
+            int ended = 0;
+            for (int g = 0; g < ngpu; g++) {
+                fed += eng[(size_t)g]->fed;
+                if (!ended) sc += eng[(size_t)g]->ended ? eng[(size_t)g]->scanned : eng[(size_t)g]->fed;
+                if (eng[(size_t)g]->ended) ended = 1;
+            }
+            eng[0]->fed = fed;
+            eng[0]->scanned = sc;
+            eng[0]->ended = ended;
+            fk_result tmp;
+            if (!res) res = &tmp;
+            rc = fk_engine_finish(eng[0], res);
+            if (counts && (rc == FK_OK || rc == FK_E_UNTERMINATED_HEADER)) {
+                int r2 = fk_engine_table(eng[0], counts);
+                if (r2) rc = r2;
+            }
+        }
+    }
+    for (int g = 0; g < ngpu; g++) {
+        if (dbuf[(size_t)g]) { hipSetDevice(g); hipFree(dbuf[(size_t)g]); }
+        fk_engine_destroy(eng[(size_t)g]);
+    }
+    return rc;
+}
+
+extern "C" int fk_synth_device(uint8_t *dev_out, uint64_t cap, uint64_t n_bases, uint64_t seed,
+                               int fasta_line, void *stream, uint64_t *written) {
+    uint64_t hlen = fasta_line > 0 ? 11 : 0;
+    int L = fasta_line < 0 ? -fasta_line : fasta_line;
+    uint64_t total = hlen + n_bases + (L > 0 ? n_bases / (uint64_t)L : 0);
+    if (total > cap) total = cap;
+    uint64_t threads = (total + 15) / 16;
+    unsigned blocks = (unsigned)((threads + 255) / 256);
+    if (blocks)
+        hipLaunchKernelGGL(k_synth, dim3(blocks), dim3(256), 0, (hipStream_t)stream, dev_out, total, seed,
+                           L, hlen);
+    HIPCHK(hipGetLastError());
+    if (written) *written = total;
+    return FK_OK;
+}

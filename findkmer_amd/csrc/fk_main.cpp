@@ -1,0 +1,415 @@
+/*
+ * fk_main.cpp — ./findKmer, the drop-in host program.
+ *
+ * Mirrors the reference main() (findKmer/src/findKmer.cpp:1292-1379): the same
+ * argv grammar (parse_arguments :394-490), defaults (:74-82, set_default_conf
+ * :257-305), output file names, stdout/stderr text and exit codes, so that
+ * k6thru11fullANDupstream.sh and users can call it unchanged.  The scan
+ * (findKmer() :962-1069) runs on the GPU through the C-ABI in
+ * include/findkmer.h; the CSV and stats files are written by fk_writer.cpp.
+ *
+ * Deliberate differences:
+ *  - the reference always crashes in free() after writing its outputs
+ *    (:1370, exit 134/139); this program exits 0 there;
+ *  - a missing option value makes the reference re-print the usage forever
+ *    (`while (!parse_arguments(...)) usage();`, :1302); this program prints it
+ *    once more and exits 1;
+ *  - an input ending inside a '>' line makes the reference spin forever
+ *    (:1005); this program reports it and exits 1.
+ * Extension: FINDKMER_GPUS=N splits the scan over N GPUs of this node.
+ */
+#include "findkmer.h"
+
+#include <math.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <iostream>
+#include <string>
+#include <vector>
+
+#define DEFAULT_SEQUENCE_FILE_NAME "test.txt"
+#define DEFAULT_K_VALUE 7
+#define OUT_FILE_COLUMN_HEADERS "Sequence, Shannon Entropy h, Shannon Entropy H, Frequency, Z score"
+#define DEFAULT_SUPPRESS_OUTPUT_VALUE 0
+#define DEFAULT_Z_THRESHOLD_ENABLE 0
+#define DEFAULT_Z_THRESHOLD 1000
+
+static struct conf {
+    const char *sequence_file;
+    FILE *sequence_file_pointer;
+    std::string out_file;
+    bool out_set;
+    FILE *out_file_pointer;
+    int k;
+    int suppressOutputEnable;
+    long double zThreshold;
+    int zThresholdEnable;
+} config;
+
+static void check_file(const char *filename, const char *mode) {   /* :233-242 */
+    FILE *file = fopen(filename, mode);
+    if (file == NULL) {
+        fprintf(stderr, "Unable to open file %s in %s mode\nFile MUST be in current directory.\n",
+                filename, mode);
+        exit(EXIT_FAILURE);
+    } else
+        fclose(file);
+}
+
+static void init_conf() {                                           /* :246-255 */
+    config.sequence_file = NULL;
+    config.sequence_file_pointer = NULL;
+    config.out_set = false;
+    config.out_file_pointer = NULL;
+    config.k = 0;
+    config.suppressOutputEnable = -1;
+    config.zThresholdEnable = -1;
+    config.zThreshold = -1;
+}
+
+static void set_default_conf() {                                    /* :257-305 */
+    if (!config.sequence_file) config.sequence_file = DEFAULT_SEQUENCE_FILE_NAME;
+    if (!config.k) config.k = DEFAULT_K_VALUE;
+    if (config.suppressOutputEnable < 0) config.suppressOutputEnable = DEFAULT_SUPPRESS_OUTPUT_VALUE;
+    if (config.zThresholdEnable < 0) {
+        config.zThresholdEnable = DEFAULT_Z_THRESHOLD_ENABLE;
+        config.zThreshold = DEFAULT_Z_THRESHOLD;
+    }
+    if (!config.out_set) {
+        char buf[64];
+        snprintf(buf, sizeof buf, "%d", config.k);
+        config.out_file = std::string(buf) + "mer_Historam_Of_" + config.sequence_file +
+                          (config.zThresholdEnable == 0 ? "" : "zScoreFiltered") + ".csv";
+        config.out_set = true;
+    }
+}
+
+static void print_conf(int argc) {                                  /* :307-364 */
+    fprintf(stdout, "\nATTEMPTING CONFIGURATION: \n");
+    set_default_conf();
+    if (config.sequence_file) fprintf(stdout, "- sequence_file file: %s\n", config.sequence_file);
+    fprintf(stdout, "- export file: %s\n", config.out_file.c_str());
+    if (config.k) fprintf(stdout, "- k size: %d\n", config.k);
+    fprintf(stdout, "- %s\n",
+            config.suppressOutputEnable > 0 ? "Suppressing file read output and breaks."
+                                            : "Showing DNA Sequence identifier and allowing breaks.");
+    fprintf(stdout, "- Z score filtering is %s", config.zThresholdEnable ? "enabled" : "disabled");
+    if (config.zThresholdEnable > 0) fprintf(stdout, "\n    with threshold of %LG", config.zThreshold);
+    fprintf(stdout, ".\n");
+    if (config.suppressOutputEnable == 0 && argc < 2) {
+        fprintf(stdout, "Press enter to proceed with this configuration.");
+        getchar();
+    }
+    if (config.k < 0 || config.k > 20) {
+        fprintf(stderr, "%d is not a valid value for k. Please select a number greater than zero\n", config.k);
+        exit(EXIT_FAILURE);
+    }
+    if ((config.sequence_file_pointer = fopen(config.sequence_file, "r")) == NULL) {
+        fprintf(stderr, "Sequence file failed to open\n\n");
+        exit(EXIT_FAILURE);
+    }
+    if ((config.out_file_pointer = fopen(config.out_file.c_str(), "w")) != NULL) {
+        fprintf(config.out_file_pointer, OUT_FILE_COLUMN_HEADERS);
+    } else {
+        fprintf(stderr, "Out file failed to open\nFile MUST be in current directory.\n");
+        exit(EXIT_FAILURE);
+    }
+    fprintf(stdout, "Sequence file and out file opened properly\n");
+    fprintf(stdout, "\n");
+}
+
+static void usage() {                                               /* :366-393 */
+    fprintf(stdout, "\n");
+    fprintf(stdout, "Usage: findKmer [options]\n");
+    fprintf(stdout,
+            "             [--parse|-p <sequence_file.txt>] \n"
+            "               File with DNA sequence data.\n"
+            "               File must be in current directory.\n"
+            "               Parser follows .fas and .fa formats\n"
+            "                Default is %s.\n\n",
+            DEFAULT_SEQUENCE_FILE_NAME);
+    fprintf(stdout,
+            "             [--export|-e  <out_file.csv>] \n"
+            "               File to output histogram data to.\n"
+            "                Default output file name is dynamic.\n\n");
+    fprintf(stdout,
+            "             [--ksize|-k  <k>] \n"
+            "               Size of sequence for histogram.\n"
+            "                Default is %d.\n\n",
+            DEFAULT_K_VALUE);
+    fprintf(stdout,
+            "             [--quiet|-q  < 0 for FALSE | 1 for TRUE >] \n"
+            "               Suppress file read output and breaks.\n"
+            "                Default is %s.\n\n",
+            DEFAULT_SUPPRESS_OUTPUT_VALUE ? "true" : "false");
+    long double tempzThreshold = DEFAULT_Z_THRESHOLD;
+    fprintf(stdout,
+            "             [--zthreshold|-z  < Threshold_for_Z >] \n"
+            "               Suppress sequences with Z scores < threshold.\n"
+            "                Default is %s with a value of %LG.\n\n",
+            DEFAULT_Z_THRESHOLD_ENABLE ? "enabled" : "disabled", tempzThreshold);
+    fprintf(stdout, "\n");
+}
+
+static int parse_arguments(int argc, char **argv) {                 /* :394-490 */
+    int i = 1;
+    if (argc < 2) return 1;
+    while (i < argc) {
+        if (strcmp(argv[i], "-h") == 0 || strcmp(argv[i], "--help") == 0) {
+            exit(1);
+        } else if (strcmp(argv[i], "-e") == 0 || strcmp(argv[i], "--export") == 0) {
+            i++;
+            if (i == argc) {
+                fprintf(stderr, "Export file name missing.\n");
+                return 0;
+            }
+            check_file(argv[i], "w");
+            config.out_file = argv[i];
+            config.out_set = true;
+        } else if (strcmp(argv[i], "-p") == 0 || strcmp(argv[i], "--parse") == 0) {
+            i++;
+            if (i == argc) {
+                fprintf(stderr, "Sequence data file name missing.\n");
+                return 0;
+            }
+            check_file(argv[i], "r");
+            config.sequence_file = argv[i];
+        } else if (strcmp(argv[i], "-k") == 0 || strcmp(argv[i], "--ksize") == 0) {
+            i++;
+            if (i == argc) {
+                fprintf(stderr, "Number for size of k is missing.\n");
+                return 0;
+            } else {
+                int k = atoi(argv[i]);
+                if (k < 0 || k > 20) {
+                    fprintf(stderr,
+                            "%d is not a valid value for k.\nPlease select a number greater than zero and less than 21\n",
+                            k);
+                    exit(EXIT_FAILURE);
+                }
+                config.k = k;
+            }
+        } else if (strcmp(argv[i], "-q") == 0 || strcmp(argv[i], "--quiet") == 0) {
+            i++;
+            if (i == argc) {
+                fprintf(stderr,
+                        "True/false value for quiet option is missing.\nUsage is \"-q 1\" for suppression OR \"-q 0\" for expansion\n");
+                exit(EXIT_FAILURE);
+            } else {
+                int opt = atoi(argv[i]);
+                if (opt == 1 || opt == 0) {
+                    config.suppressOutputEnable = opt;
+                } else {
+                    fprintf(stderr,
+                            "%d is not a valid value for suppress Output Enable Option.\nPlease select either 0 for FALSE or a 1 for TRUE",
+                            opt);
+                    exit(EXIT_FAILURE);
+                }
+            }
+        } else if (strcmp(argv[i], "-z") == 0 || strcmp(argv[i], "--zthreshold") == 0) {
+            i++;
+            if (i == argc) {
+                fprintf(stderr, "Z threshold number is missing\nUsage is \"-z 1000\".\n");
+                exit(EXIT_FAILURE);
+            } else {
+                config.zThresholdEnable = 1;
+                config.zThreshold = atoi(argv[i]);
+            }
+        } else {
+            fprintf(stderr, "Ignoring invalid option %s\n", argv[i]);
+            if (config.suppressOutputEnable == 0) {
+                fprintf(stderr, "Press enter to continue.\n");
+                getchar();
+            }
+        }
+        i++;
+    }
+    return 1;
+}
+
+static unsigned long estimate_RAM_usage() {                         /* :1226-1291 */
+    const unsigned long node_t_size = 48;   /* sizeof(node_t) on x86-64 (:107-111) */
+    unsigned long maxNumberOfNodes = 1;
+    double n = 1;
+    while (n <= config.k) maxNumberOfNodes += pow(4.0, n++);
+    if (((sizeof(char) * (config.k + 10)) * maxNumberOfNodes) >= (1024 * 1024 * 1024)) {
+        std::cout << ((sizeof(char) * (config.k + 10)) * maxNumberOfNodes) / (double)(1024 * 1024 * 1024)
+                  << " gibibytes";
+    } else {
+        std::cout << ((sizeof(char) * (config.k + 10)) * maxNumberOfNodes) / (double)(1024 * 1024)
+                  << " mibibytes";
+    }
+    std::cout << " of disk usage and ";
+    if (maxNumberOfNodes * node_t_size >= (1024 * 1024 * 1024)) {
+        std::cout << (maxNumberOfNodes * node_t_size / (double)(1024 * 1024 * 1024))
+                  << " gibibytes of RAM usage likely" << std::endl;
+        std::cout << "We are stopping here to make sure that is ok with you!" << std::endl;
+        std::cout << "Hit enter to proceed or else abort the program." << std::endl;
+        if (config.suppressOutputEnable == 0) getchar();
+    } else {
+        std::cout << (maxNumberOfNodes * node_t_size / (double)(1024 * 1024))
+                  << " mibibytes of RAM usage likely" << std::endl;
+    }
+    return maxNumberOfNodes;
+}
+
+static void die_engine(int rc) {
+    fprintf(stderr, "findKmer: GPU engine error: %s\n", fk_strerror(rc));
+    exit(EXIT_FAILURE);
+}
+
+/*
+ * Drive the engine over the whole file.  With quiet == 0 the reference prints
+ * "Read %llu bases\n>" + the header line at every '>' that starts a comment
+ * (:996-1002), with baseCounter as of that point; we feed the engine up to
+ * each such '>' and read its running counter (host only splits the stream).
+ */
+static int scan_file(fk_engine *e, FILE *f, fk_result *res) {
+    const size_t PIECE = 256u << 20;
+    std::vector<uint8_t> buf(PIECE);
+    int in_hdr = 0, ended = 0;
+    for (;;) {
+        size_t n = fread(buf.data(), 1, buf.size(), f);
+        if (n == 0) break;
+        if (config.suppressOutputEnable != 0 || ended) {
+            int rc = fk_engine_feed(e, buf.data(), n, 0);
+            if (rc) return rc;
+            continue;
+        }
+        size_t pos = 0;
+        while (pos < n) {
+            int rc;
+            if (ended) {
+                rc = fk_engine_feed(e, buf.data() + pos, n - pos, 0);
+                if (rc) return rc;
+                break;
+            }
+            if (in_hdr) {                        /* echo the header line (:999-1002) */
+                size_t r = pos;
+                while (r < n && buf[r] != '\n') fputc(buf[r++], stdout);
+                rc = fk_engine_feed(e, buf.data() + pos, r - pos, 0);
+                if (rc) return rc;
+                if (r == n) break;               /* continues in the next piece */
+                fprintf(stdout, "\n");
+                rc = fk_engine_feed(e, buf.data() + r, 1, 0);
+                if (rc) return rc;
+                in_hdr = 0;
+                pos = r + 1;
+                continue;
+            }
+            size_t q = pos;
+            while (q < n && buf[q] != '>' && buf[q] != 0xFF) q++;
+            if (q > pos) {
+                rc = fk_engine_feed(e, buf.data() + pos, q - pos, 0);
+                if (rc) return rc;
+            }
+            if (q == n) break;
+            if (buf[q] == 0xFF) {                /* (char)0xFF == EOF ends the scan (:988) */
+                ended = 1;
+                pos = q;
+                continue;
+            }
+            uint64_t vb = 0;
+            rc = fk_engine_progress(e, &vb, nullptr);
+            if (rc) return rc;
+            fprintf(stdout, "Read %llu bases\n%c", (unsigned long long)vb, '>');   /* :997 */
+            rc = fk_engine_feed(e, buf.data() + q, 1, 0);
+            if (rc) return rc;
+            in_hdr = 1;
+            pos = q + 1;
+        }
+    }
+    return fk_engine_finish(e, res);
+}
+
+int main(int argc, char *argv[]) {                                  /* :1292-1379 */
+    init_conf();
+    usage();
+    if (!parse_arguments(argc, argv)) {
+        usage();
+        return EXIT_FAILURE;
+    }
+    print_conf(argc);
+    unsigned long maxNumberOfNodes = estimate_RAM_usage();
+    (void)maxNumberOfNodes;
+
+    fprintf(stdout, "!!!Find The KMER!!!\n");
+    fprintf(stdout, "Reading sequence from file\n");
+    fprintf(stdout, "     2858658142 bases in the reference genome FYI.\nThat is 2,858,658,142 by the way.\n");
+    fflush(stdout);
+
+    /* empty-file check (:982-985) */
+    int c0 = fgetc(config.sequence_file_pointer);
+    if (c0 == EOF) {
+        fprintf(stderr, "Sequence File Is Empty, Ending Program");
+        exit(EXIT_FAILURE);
+    }
+    rewind(config.sequence_file_pointer);
+
+    if (config.k > FK_K_MAX_DENSE) {
+        fprintf(stderr, "findKmer: k=%d needs the sparse table, which this build does not have yet (k <= %d)\n",
+                config.k, FK_K_MAX_DENSE);
+        exit(EXIT_FAILURE);
+    }
+    fk_opts opts;
+    memset(&opts, 0, sizeof opts);
+    opts.device = -1;
+    opts.want_nodes = 1;
+    opts.collect_unknown = 1;
+    fk_engine *eng = nullptr;
+    int rc = fk_engine_create(config.k, &opts, &eng);
+    if (rc) die_engine(rc);
+    fk_result res;
+    rc = scan_file(eng, config.sequence_file_pointer, &res);
+    if (rc == FK_E_ROLLOVER) {                                       /* :642-648 */
+        const char *m = "\n\n!!! COUNTER ROLLOVER DETECTED! \nIncrease the number of bits used for the counter variable if you have the source code, else use a smaller sequence file.\n\n";
+        fprintf(stderr, "%s", m);
+        fprintf(stdout, "%s", m);
+        exit(EXIT_FAILURE);
+    }
+    if (rc == FK_E_UNTERMINATED_HEADER) {
+        fprintf(stderr, "findKmer: the sequence file ends inside a '>' header line (the reference program hangs here)\n");
+        exit(EXIT_FAILURE);
+    }
+    if (rc != FK_OK && rc != FK_E_EMPTY) die_engine(rc);
+    /* "Unknown character" warnings (:582-584), in stream order */
+    if (res.unknown_chars) {
+        uint64_t n = 0;
+        fk_engine_unknown(eng, nullptr, 0, &n);
+        std::vector<uint8_t> u((size_t)n);
+        if (n) fk_engine_unknown(eng, u.data(), n, &n);
+        for (uint64_t i = 0; i < n; i++)
+            fprintf(stderr, "Unknown character %c processed! File may be corrupted.\n", (char)u[(size_t)i]);
+    }
+
+    std::string stats_name = std::to_string(config.k) + "mer_Base_Stats_Of_" + config.sequence_file + ".txt";
+    double prob[4];
+    int st = fk_write_stats(stats_name.c_str(), config.k, &res, stdout, prob);
+    if (st == 1 || st == FK_E_IO) {
+        fflush(config.out_file_pointer);
+        exit(EXIT_FAILURE);
+    }
+
+    fprintf(stdout, "Now creating histogram.\n");
+    fflush(stdout);
+    std::vector<uint32_t> counts((size_t)1 << (2 * config.k));
+    rc = fk_engine_table(eng, counts.data());
+    if (rc) die_engine(rc);
+    fk_engine_destroy(eng);
+    rc = fk_write_rows(config.out_file_pointer, config.k, counts.data(), prob, res.windows,
+                       config.zThresholdEnable, (double)config.zThreshold, 0);
+    if (rc) die_engine(rc);
+
+    fprintf(stdout, "histogram creation finished.\n");
+    if (fclose(config.out_file_pointer) == EOF) {
+        fprintf(stderr,
+                "Out file close error! This is not expected and might mean the data was not written to the file properly before the close.\n");
+    }
+    fprintf(stdout, "Your file can be found in the current directory as: \n    %s\n", config.out_file.c_str());
+    if (fclose(config.sequence_file_pointer) == EOF) {
+        fprintf(stderr, "Sequence file close error! This is likely ok though.\n");
+    }
+    return 0;
+}

@@ -1,0 +1,203 @@
+/*
+ * findkmer.h — C-ABI of the MI355X k-mer counting engine (libfindkmer_hip.so).
+ *
+ * Drop-in boundary.  The reference (soundude462/findKmer) has no plugin or FFI
+ * API: its hot path is the in-process call
+ *
+ *     node_t* findKmer(node_t* headNode, unsigned long long* baseCounter,
+ *                      statistics_t* baseStatistics,
+ *                      unsigned long long* TotalNumSequencesN);
+ *                                             (findKmer/src/findKmer.cpp:962-964)
+ *
+ * which scans config.sequence_file_pointer byte by byte and grows a 4-ary
+ * trie (:107-111, :612-690) whose depth-k leaves hold the k-mer counts, read
+ * back by statistics() (:491-565) and histo_recursive() (:699-942).  This
+ * header replaces that call with plain pointers and sizes: the trie becomes a
+ * dense table of 4^k uint32 counters (the reference's `unsigned int
+ * frequency`, :110) indexed by the 2-bit packing A=0 C=1 G=2 T=3, first base
+ * most significant (base2int, :567-589), i.e. the trie's DFS order
+ * (:719-724).  Errors are returned, never exit()ed; the host main
+ * (./findKmer) maps them onto the reference's messages and exit codes.
+ *
+ * Threading: an engine is bound to one HIP device and is driven from one host
+ * thread.  Multi-GPU runs use one engine per device (one process per GPU in
+ * bench.py; fk_count_multi below fans out inside one process).
+ */
+#ifndef FINDKMER_H
+#define FINDKMER_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FK_ABI_VERSION 1
+#define FK_K_MIN 1
+#define FK_K_MAX_DENSE 16   /* 4^16 uint32 = 16 GiB table on one 288 GB GPU */
+#define FK_K_MAX_REF 20     /* the reference accepts k <= 20 (:438) */
+
+/* status codes (all < 0 are errors) */
+enum {
+    FK_OK = 0,
+    FK_E_INVALID = -1,          /* bad argument */
+    FK_E_K_UNSUPPORTED = -2,    /* 17 <= k <= 20: sparse table not built yet */
+    FK_E_NO_DEVICE = -3,        /* no HIP device / extension cannot run */
+    FK_E_HIP = -4,              /* a HIP runtime call failed */
+    FK_E_OOM = -5,              /* device or host allocation failed */
+    FK_E_EMPTY = -6,            /* empty input: ref prints "Sequence File Is
+                                   Empty, Ending Program" and exits (:982-985) */
+    FK_E_UNTERMINATED_HEADER = -7, /* input ends inside a '>' line: the ref
+                                      spins forever in the loop at :1005 */
+    FK_E_ROLLOVER = -8,         /* a trie counter would wrap: ref prints
+                                   COUNTER ROLLOVER and exits (:642-648) */
+    FK_E_STATE = -9,            /* API called out of order */
+    FK_E_IO = -10,              /* host file I/O failed */
+    FK_E_RCCL = -11             /* a collective failed */
+};
+
+/* Scan state carried between byte ranges (exact; used for streaming feeds and
+ * for stitching GPU shards).  `run` is the number of valid bases since the
+ * last run break (the ref's seqSize, an int that wraps: we keep it exact and
+ * apply the 32-bit wrap where the ref would); `code` holds the last bases,
+ * first base most significant; `hdr` = inside a '>' comment line. */
+typedef struct {
+    uint64_t run;
+    uint64_t code;
+    uint32_t hdr;
+    uint32_t pad;
+} fk_state;
+
+typedef struct {
+    uint64_t base_count[4];   /* baseStatistics[b].Count, exact (the ref keeps
+                                 it in a u32 that wraps silently, :94) */
+    uint64_t valid_bases;     /* baseCounter */
+    uint64_t windows;         /* TotalNumSequencesN */
+    uint64_t distinct;        /* k-mers with count >= 1 */
+    uint64_t depth1[4];       /* depth-1 trie node frequencies (rollover) */
+    uint64_t nodes;           /* nodeCounter incl. head (0 if not computed) */
+    uint64_t unknown_chars;   /* bytes that print "Unknown character" */
+    uint64_t scanned_bytes;   /* bytes consumed (stops at a 0xFF byte) */
+    int32_t  hit_eof_byte;    /* a 0xFF byte outside a header ended the scan */
+    int32_t  unterminated_header;
+    int32_t  rollover;
+    int32_t  nodes_valid;     /* `nodes` was computed */
+    /* instrumentation (not part of parity) */
+    uint64_t chunks;          /* 64 KiB scan chunks processed */
+    uint64_t redo_chunks;     /* chunks re-counted after the state scan */
+    double   device_ms;       /* HIP-event time of all scan kernels */
+    double   main_kernel_ms;  /* HIP-event time of the main count kernel */
+} fk_result;
+
+typedef struct {
+    int32_t device;           /* HIP device ordinal; -1 = current device */
+    int32_t want_nodes;       /* compute nodeCounter (stdout "tree density") */
+    void   *stream;           /* hipStream_t to use, NULL = engine-owned */
+    int32_t collect_unknown;  /* keep the unknown bytes for stderr replay */
+    int32_t reserved[7];
+} fk_opts;
+
+typedef struct fk_engine fk_engine;
+
+/* Library identity. */
+int         fk_abi_version(void);
+const char *fk_strerror(int status);
+int         fk_device_count(void);   /* 0 when no GPU is visible */
+
+/* Engine lifecycle: one engine per (device, k).  The device table lives in
+ * HBM for the engine's lifetime. */
+int  fk_engine_create(int k, const fk_opts *opts, fk_engine **out);
+void fk_engine_destroy(fk_engine *e);
+int  fk_engine_reset(fk_engine *e);     /* zero table, counters and state */
+
+/* Feed a byte range of the stream.  `buf` is a device pointer when
+ * on_device != 0, else host memory (staged through pinned buffers).  Feeds
+ * continue the scan state of the previous feed exactly. */
+int  fk_engine_feed(fk_engine *e, const uint8_t *buf, uint64_t len,
+                    int on_device);
+
+/* Shard entry (multi-GPU): feed bytes whose entering state is not known yet.
+ * `halo` bytes immediately preceding buf (may be 0) are used to guess it;
+ * fk_engine_resolve() later supplies the true entering state and re-counts
+ * the chunks the guess got wrong.  fk_engine_summary() returns the
+ * transfer function of everything fed so far as an opaque blob (fk_summary)
+ * that the caller exchanges between shards. */
+typedef struct { uint64_t w[12]; } fk_summary;
+int  fk_engine_feed_shard(fk_engine *e, const uint8_t *buf, uint64_t len,
+                          uint64_t halo, int on_device);
+int  fk_engine_summary(fk_engine *e, fk_summary *out);
+int  fk_summary_apply(const fk_summary *s, const fk_state *in, fk_state *out);
+int  fk_engine_resolve(fk_engine *e, const fk_state *entering);
+
+/* Finish the stream (end-of-input rules) and fill *res.  Returns FK_OK or one
+ * of FK_E_EMPTY / FK_E_UNTERMINATED_HEADER / FK_E_ROLLOVER (res is filled in
+ * every case). */
+int  fk_engine_finish(fk_engine *e, fk_result *res);
+
+/* Copy the 4^k table to host memory (counts[4^k]) / borrow the device
+ * pointer (valid until reset/destroy). */
+int  fk_engine_table(fk_engine *e, uint32_t *counts);
+int  fk_engine_table_device(fk_engine *e, uint32_t **dev_counts);
+/* Copy the table into a caller-owned device buffer (4^k uint32), e.g. a
+ * torch tensor handed to an RCCL collective; and load it back. */
+int  fk_engine_table_to_device(fk_engine *e, void *dst);
+int  fk_engine_table_from_device(fk_engine *e, const void *src);
+int  fk_engine_state(fk_engine *e, fk_state *out);
+
+/* Running counters without finishing the stream (the -q 0 "Read %llu bases"
+ * lines print baseCounter at every header, :996-997). */
+int  fk_engine_progress(fk_engine *e, uint64_t *valid_bases, uint64_t *windows);
+
+/* Add another engine's table and counters into this one (same k) — the
+ * single-process multi-GPU merge when RCCL is not used. */
+int  fk_engine_merge_from(fk_engine *dst, fk_engine *src);
+
+/* Unknown bytes in stream order (collect_unknown=1): *n receives the number
+ * available; copies min(cap, n). */
+int  fk_engine_unknown(fk_engine *e, uint8_t *out, uint64_t cap, uint64_t *n);
+
+/* One-shot convenience: count a whole buffer on one device. */
+int  fk_count(const uint8_t *buf, uint64_t len, int k, const fk_opts *opts,
+              uint32_t *counts /* host, 4^k */, fk_result *res);
+
+/* One-shot multi-GPU: split buf (host) into ngpu contiguous shards, count
+ * each on its own device, stitch the states, merge the tables. */
+int  fk_count_multi(const uint8_t *buf, uint64_t len, int k, int ngpu,
+                    const fk_opts *opts, uint32_t *counts, fk_result *res);
+
+/* Deterministic on-device synthetic input (same bytes as the oracle's
+ * fko_synth): n_bases uniform ACGT from `seed`, optional FASTA framing
+ * (">synthetic\n" + '\n' every fasta_line bases; fasta_line < 0: '\n' every
+ * -fasta_line bases and no header — a later shard of the same file).  Bytes
+ * are those of base index >= 0 of the stream seeded `seed`; a shard starting
+ * at base b (b a multiple of 32) uses seed + b/32.  Returns bytes written. */
+int  fk_synth_device(uint8_t *dev_out, uint64_t cap, uint64_t n_bases,
+                     uint64_t seed, int fasta_line, void *stream,
+                     uint64_t *written);
+
+/* ---- host side of the boundary: byte-identical output writers ---------- */
+
+/* statistics() (:491-565): writes "<k>mer_Base_Stats_Of_<file>.txt" content to
+ * stats_path and the stdout lines to `log` (may be NULL).  Returns FK_OK, or 1
+ * when a base probability is 0 ("Division overflow", ref exits 1 after
+ * writing the earlier lines, :522-525). */
+int  fk_write_stats(const char *stats_path, int k, const fk_result *res,
+                    void *log /* FILE* */, double prob_out[4]);
+
+/* histo_recursive() rows (:699-942) for all k-mers with count >= 1, in
+ * ascending index order, appended to `out` (FILE*, header already written).
+ * z filtering as -z (:852-854).  threads <= 0: use all host cores. */
+int  fk_write_rows(void *out, int k, const uint32_t *counts,
+                   const double prob[4], uint64_t windows, int z_enable,
+                   double z_threshold, int threads);
+
+/* Path-based variant for bindings: writes header + rows to csv_path. */
+int  fk_write_csv(const char *csv_path, int k, const uint32_t *counts,
+                  const double prob[4], uint64_t windows, int z_enable,
+                  double z_threshold, int threads);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FINDKMER_H */

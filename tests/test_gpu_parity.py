@@ -1,0 +1,300 @@
+"""GPU parity: the HIP engine (through the C-ABI) vs the CPU oracle, bit-exact.
+
+Every comparison covers the full count table and every scalar the reference's
+outputs depend on (base counts, baseCounter, windows, distinct, depth-1 trie
+frequencies, nodeCounter, unknown bytes in order, bytes scanned).
+"""
+import os
+import random
+import shutil
+import subprocess
+
+import numpy as np
+import pytest
+
+import findkmer_amd as fk
+import oracle
+from conftest import REPO, case_k, case_z, golden_file, golden_input
+
+pytestmark = pytest.mark.gpu
+
+
+def assert_same(data, k, want_nodes=True, feeds=None, ngpu_shards=None):
+    t_o, r_o, ub_o = oracle.count_dense(data, k, unknown_cap=1 << 20)
+    if ngpu_shards:
+        t_g, r_g, ub_g, rc = shard_count(data, k, ngpu_shards)
+    else:
+        with fk.Engine(k, want_nodes=want_nodes, collect_unknown=True) as e:
+            arr = np.frombuffer(bytes(data), dtype=np.uint8)
+            if feeds is None:
+                feeds = [len(arr)]
+            pos = 0
+            for n in feeds:
+                if n:
+                    e.feed(np.ascontiguousarray(arr[pos:pos + n]))
+                pos += n
+            assert pos == len(arr)
+            rc, r_g = e.finish(allow=(fk.FK_OK, fk.FK_E_EMPTY, fk.FK_E_UNTERMINATED_HEADER, fk.FK_E_ROLLOVER))
+            t_g = e.table()
+            ub_g = e.unknown_bytes()
+    bad = np.nonzero(t_o != t_g)[0]
+    assert len(bad) == 0, f"k={k}: {len(bad)} bins differ, first {bad[:8]} oracle={t_o[bad[:8]]} gpu={t_g[bad[:8]]}"
+    assert list(r_g.base_count) == list(r_o.base_count)
+    assert r_g.valid_bases == r_o.valid_bases
+    assert r_g.windows == r_o.windows
+    assert r_g.distinct == r_o.distinct
+    assert list(r_g.depth1) == list(r_o.depth1)
+    assert r_g.unknown_chars == r_o.unknown_chars
+    assert ub_g == ub_o
+    assert r_g.hit_eof_byte == r_o.hit_eof_byte
+    assert r_g.unterminated_header == r_o.unterminated_header
+    assert r_g.scanned_bytes == r_o.scanned_bytes
+    if want_nodes and not ngpu_shards:
+        assert r_g.nodes == r_o.nodes
+    return r_g
+
+
+def shard_count(data, k, nshards):
+    """Exercise the multi-GPU shard protocol with several engines (on the one
+    GPU of the test box): guess-from-halo, summaries, resolve, merge."""
+    import torch
+    arr = np.frombuffer(bytes(data), dtype=np.uint8)
+    n = len(arr)
+    chunk = 65536
+    per = max(chunk, (n // nshards) // chunk * chunk)
+    bounds = [min(i * per, n) for i in range(nshards)] + [n]
+    dev = torch.from_numpy(arr.copy()).cuda() if n else torch.zeros(16, dtype=torch.uint8).cuda()
+    engines = []
+    for i in range(nshards):
+        e = fk.Engine(k, collect_unknown=True)
+        lo, hi = bounds[i], bounds[i + 1]
+        halo = min(256, lo) // 16 * 16
+        e.feed_shard_device(dev.data_ptr() + lo, hi - lo, halo)
+        engines.append(e)
+    st = fk.FkState()
+    for e in engines:
+        e.resolve(st)
+        st = e.state()
+    base = engines[0]
+    for e in engines[1:]:
+        assert fk.lib().fk_engine_merge_from(base.h, e.h) == 0
+    # table and counters are complete after the merge; end-of-stream fields
+    # (short-run nodes, unterminated header) belong to the last shard
+    rc, r = base.finish(allow=(fk.FK_OK, fk.FK_E_EMPTY, fk.FK_E_UNTERMINATED_HEADER, fk.FK_E_ROLLOVER))
+    t = base.table()
+    ub = base.unknown_bytes()
+    for e in engines:
+        e.close()
+    return t, r, ub, rc
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if fk.device_count() < 1:
+        pytest.fail("no GPU visible: the gpu tests must run on the MI355X box")
+
+
+GOLDEN_INPUTS = ["test.txt", "edge.txt", "rand120k.fa", "missing.txt", "ffbyte.bin", "shortruns.txt"]
+
+
+@pytest.mark.parametrize("name", GOLDEN_INPUTS)
+@pytest.mark.parametrize("k", [1, 2, 3, 4, 5, 6, 7, 8, 11, 12])
+def test_golden_inputs(name, k):
+    assert_same(golden_input(name), k)
+
+
+def random_text(rng, n, alphabet, weights):
+    return bytes(rng.choices(alphabet, weights=weights, k=n))
+
+
+def mixed_input(seed, n):
+    """Random bytes with every class the scan distinguishes, long runs, lines
+    of varying width and headers that cross chunk (64 KiB) boundaries."""
+    rng = random.Random(seed)
+    parts = []
+    size = 0
+    while size < n:
+        r = rng.random()
+        if r < 0.45:
+            L = rng.randint(1, 5000)
+            seq = random_text(rng, L, b"ACGT", [1, 1, 1, 1])
+            w = rng.choice([0, 60, 80, 7, 1000])
+            if w:
+                seq = b"\n".join(seq[i:i + w] for i in range(0, len(seq), w))
+            parts.append(seq)
+        elif r < 0.55:
+            parts.append(b">" + random_text(rng, rng.randint(0, 300), b"ACGTN >xyz\xff\r", [5, 5, 5, 5, 1, 2, 1, 1, 1, 1, 1, 1]) + b"\n")
+        elif r < 0.60:
+            parts.append(b">" + b"A" * rng.randint(60000, 140000) + b"\n")   # long header over a chunk edge
+        elif r < 0.75:
+            parts.append(random_text(rng, rng.randint(1, 40), b"ACGTNn\r\n\x00acgt1>", [3, 3, 3, 3, 2, 1, 1, 3, 1, 1, 1, 1, 1, 1, 1]))
+        elif r < 0.80:
+            parts.append(b"\n" * rng.randint(1, 3000))
+        else:
+            parts.append(random_text(rng, rng.randint(10000, 200000), b"ACGT", [4, 1, 1, 4]))
+        size += len(parts[-1])
+    return b"".join(parts)
+
+
+@pytest.mark.parametrize("seed", range(6))
+@pytest.mark.parametrize("k", [2, 5, 6, 7, 9, 11, 13])
+def test_mixed_random(seed, k):
+    data = mixed_input(1000 + seed, 1_500_000 + 300_000 * seed)
+    assert_same(data, k)
+
+
+@pytest.mark.parametrize("k", [3, 6, 11])
+def test_streaming_feeds_equal_one_shot(k):
+    data = mixed_input(77, 2_000_000)
+    rng = random.Random(5)
+    feeds = []
+    left = len(data)
+    while left:
+        n = min(left, rng.choice([1, 2, 15, 16, 17, 1000, 65536, 65537, 300000]))
+        feeds.append(n)
+        left -= n
+    assert_same(data, k, feeds=feeds)
+
+
+@pytest.mark.parametrize("k", [4, 6, 11])
+@pytest.mark.parametrize("nshards", [2, 3, 5])
+def test_shards_match_single(k, nshards):
+    data = mixed_input(4242 + nshards, 1_200_000)
+    # drop 0xFF and make sure it ends outside a header for the shard check
+    data = data.replace(b"\xff", b"Z") + b"\nACGT"
+    t_o, r_o, _ = oracle.count_dense(data, k)
+    t_g, r_g, ub, rc = shard_count(data, k, nshards)
+    assert np.array_equal(t_o, t_g)
+    assert r_g.windows == r_o.windows and r_g.valid_bases == r_o.valid_bases
+    assert list(r_g.base_count) == list(r_o.base_count)
+
+
+@pytest.mark.parametrize("k", [1, 6, 11, 16])
+def test_edge_sizes(k):
+    for data in [b"", b"A", b"ACGT" * 3, b">", b">abc", b"ACGT>x\n", b"\xff", b"AC\xffGT",
+                 b"A" * 65535, b"A" * 65536, b"A" * 65537, b"C" * (3 * 65536 + 17)]:
+        if k > 12:
+            continue
+        assert_same(data, k)
+
+
+def _read_u32(dev_ptr, idx):
+    import ctypes
+    hip = ctypes.CDLL("libamdhip64.so")
+    out = ctypes.c_uint32()
+    assert hip.hipMemcpy(ctypes.byref(out), ctypes.c_void_p(dev_ptr + 4 * int(idx)), ctypes.c_size_t(4), 2) == 0
+    return out.value
+
+
+def test_k16_dense_table():
+    """k=16: 4^16 u32 bins (16 GiB) in HBM; sampled bins vs the sparse oracle."""
+    data = mixed_input(9, 800_000)
+    codes, cnts, r = oracle.count_sparse(data, 16)
+    with fk.Engine(16) as e:
+        e.feed(np.frombuffer(data, dtype=np.uint8).copy())
+        rc, rg = e.finish(allow=(fk.FK_OK, fk.FK_E_UNTERMINATED_HEADER))
+        ptr = e.table_device_ptr()
+        rng = np.random.default_rng(0)
+        for i in rng.choice(len(codes), size=min(300, len(codes)), replace=False):
+            assert _read_u32(ptr, codes[i]) == cnts[i]
+        for c in rng.integers(0, 1 << 32, size=50):
+            if c not in set(codes[:0]):
+                j = np.searchsorted(codes, c)
+                want = cnts[j] if j < len(codes) and codes[j] == c else 0
+                assert _read_u32(ptr, c) == want
+    assert rg.windows == r.windows and rg.distinct == r.distinct
+    assert list(rg.base_count) == list(r.base_count)
+
+
+def test_int32_seqsize_wrap():
+    """A run longer than 2^31-1 bases: the reference stops counting windows
+    when its int seqSize wraps (verified on the real binary: 'ACGTN' + A*(2^31+100)
+    at k=2 gives AA=2147483646, AC=CG=GT=1, baseCounter 2147483651)."""
+    import torch
+    L = 2 ** 31 + 100
+    buf = torch.full((5 + L,), ord("A"), dtype=torch.uint8, device="cuda")
+    buf[:5] = torch.tensor(list(b"ACGTN"), dtype=torch.uint8)
+    with fk.Engine(2) as e:
+        e.feed_device(buf.data_ptr(), 5 + L)
+        rc, r = e.finish()
+        t = e.table()
+    assert t[0] == 2147483646
+    assert t[1] == 1 and t[6] == 1 and t[11] == 1
+    assert int(t.sum()) == 2147483646 + 3
+    assert r.valid_bases == 2147483651
+    assert list(r.base_count) == [2147483648, 1, 1, 1]
+
+
+def test_int32_seqsize_two_zones():
+    """Run of 2^32 + 2^31 + 50 'A' at k=3: windows count for R in [3, 2^31-1]
+    and again for R in [2^32+3, 2^32+2^31-1] (int32 seqSize climbs back to k)."""
+    import torch
+    L = 2 ** 32 + 2 ** 31 + 50
+    k = 3
+    buf = torch.full((L,), ord("A"), dtype=torch.uint8, device="cuda")
+    with fk.Engine(k) as e:
+        e.feed_device(buf.data_ptr(), L)
+        rc, r = e.finish(allow=(fk.FK_OK, fk.FK_E_ROLLOVER))
+        t = e.table()
+    z1 = (2 ** 31 - 1) - k + 1
+    z2 = (2 ** 32 + 2 ** 31 - 1) - (2 ** 32 + k) + 1
+    assert int(t[0]) == z1 + z2
+    assert r.windows == z1 + z2
+    # first windows of both zones add k bases each
+    assert r.valid_bases == (z1 - 1 + k) + (z2 - 1 + k)
+    del buf
+
+
+@pytest.mark.parametrize("k", [6, 11])
+def test_full_size_properties(k):
+    """BASELINE config sizes (1 GB stream, 1 GB of 80-col FASTA): exact
+    totals, the oracle on a 64 MiB prefix, and a checksum of checksums."""
+    import torch
+    n = 1_000_000_000
+    fasta = 80 if k == 11 else 0
+    tot = fk.synth_size(n, fasta)
+    buf = torch.empty(tot + 16, dtype=torch.uint8, device="cuda")
+    w = fk.synth_device(buf.data_ptr(), tot, n, 1 if k == 6 else 2, fasta)
+    assert w == tot
+    with fk.Engine(k) as e:
+        e.feed_device(buf.data_ptr(), tot)
+        rc, r = e.finish()
+        t = e.table()
+    assert r.windows == n - k + 1
+    assert int(t.sum(dtype=np.uint64)) == r.windows
+    assert r.valid_bases == n
+    assert sum(r.base_count) == n
+    # prefix parity with the oracle (synthetic bytes are identical on CPU)
+    m = 64 << 20
+    host = oracle.synth(m, 1 if k == 6 else 2, fasta)
+    dev_prefix = buf[: len(host)].cpu().numpy()
+    assert np.array_equal(host, dev_prefix)
+    assert_same(host.tobytes(), k)
+
+
+GOLD_CLI = ["test_k6", "test_k1", "test_k11", "test_k6_q0", "test_k0_default7", "test_k6_export",
+            "test_k6_badopt", "edge_k3", "rand_k5", "rand_k6_z3", "rand_k8", "rand_k4_z2",
+            "rand_k11", "missing_k3", "ffbyte_k3", "shortruns_k5", "empty_k3"]
+
+
+@pytest.mark.parametrize("case", GOLD_CLI)
+def test_cli_matches_reference(case, manifest, tmp_path):
+    """./findKmer (GPU) vs the golden outputs of the reference binary."""
+    entry = manifest[case]
+    shutil.copy(os.path.join(REPO, "tests", "golden", "inputs", entry["input"]), tmp_path / entry["input"])
+    p = subprocess.run([os.path.join(REPO, "findKmer")] + entry["args"], cwd=tmp_path,
+                       capture_output=True, timeout=300)
+    ref_exit = entry["exit"]
+    if ref_exit in (-11, -6, 134, 139):
+        assert p.returncode == 0, p.stderr.decode()
+    else:
+        assert p.returncode == ref_exit
+    import hashlib
+    for kind, rec in entry["files"].items():
+        got = open(tmp_path / rec["name"], "rb").read()
+        assert hashlib.sha256(got).hexdigest() == rec["sha256"], (kind, got[:300])
+    # stdout identical (the reference's own stdout ends where it crashes)
+    assert p.stdout == golden_file(case, "stdout")
+    gerr = golden_file(case, "stderr")
+    gerr = gerr.replace(b"free(): invalid pointer\n", b"")
+    assert p.stderr == gerr
