@@ -90,6 +90,7 @@ SIGNATURES = [
     ("fk_engine_finish", ctypes.c_int, [_P, ctypes.POINTER(FkResult)]),
     ("fk_engine_table", ctypes.c_int, [_P, _U32P]),
     ("fk_engine_table_device", ctypes.c_int, [_P, ctypes.POINTER(_P)]),
+    ("fk_engine_table_range", ctypes.c_int, [_P, ctypes.c_uint64, ctypes.c_uint64, _U32P]),
     ("fk_engine_table_to_device", ctypes.c_int, [_P, _P]),
     ("fk_engine_table_from_device", ctypes.c_int, [_P, _P]),
     ("fk_engine_state", ctypes.c_int, [_P, ctypes.POINTER(FkState)]),
@@ -120,6 +121,15 @@ def lib():
     if _lib is None:
         if not os.path.exists(LIB_PATH):
             raise ImportError(f"{LIB_PATH} missing: run `make` (or __graft_entry__.build())")
+        # PyTorch-ROCm bundles its own HIP runtime.  Two runtimes share the
+        # process's GPU address space only if torch initialises first, so when
+        # torch is in use, bring it up before this library touches HIP.
+        import sys
+        if "torch" in sys.modules:
+            try:
+                sys.modules["torch"].cuda.is_available()
+            except Exception:
+                pass
         L = ctypes.CDLL(LIB_PATH)
         for name, res, args in SIGNATURES:
             f = getattr(L, name)
@@ -219,6 +229,12 @@ class Engine:
         import numpy as np
         t = np.zeros(1 << (2 * self.k), dtype=np.uint32)
         _check(lib().fk_engine_table(self.h, t.ctypes.data_as(_U32P)), "table")
+        return t
+
+    def table_range(self, first, n):
+        import numpy as np
+        t = np.zeros(n, dtype=np.uint32)
+        _check(lib().fk_engine_table_range(self.h, first, n, t.ctypes.data_as(_U32P)), "table_range")
         return t
 
     def table_device_ptr(self):

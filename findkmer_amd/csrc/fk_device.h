@@ -20,15 +20,16 @@
 #define FK_HALO_BYTES 256u             /* bytes before a chunk used to guess state */
 #define FK_BLOCK 512u
 #define FK_WAVES_PER_BLOCK (FK_BLOCK / 64u)
-#define FK_LDS_MAX_K 7                 /* 4^7 u32 = 64 KiB of LDS bins */
 
 /* accumulator slots (u64, device) */
 enum {
-    ACC_BASE = 0,        /* 4: baseStatistics counts */
-    ACC_VALID = 4,       /* baseCounter */
+    ACC_BASE = 0,        /* 4: bases a run's first window adds beyond its last
+                            base (the rest of baseStatistics comes from the
+                            table's last-base marginal) */
+    ACC_VALID = 4,       /* baseCounter beyond one per window */
     ACC_WIN = 5,         /* TotalNumSequencesN */
-    ACC_D1W = 6,         /* 4: depth-1 trie freq from windows */
-    ACC_D1S = 10,        /* 4: depth-1 trie freq from short (<k) walks */
+    ACC_D1S = 10,        /* 4: depth-1 trie freq from short (<k) walks (the
+                            window part is the table's first-base marginal) */
     ACC_N = 16
 };
 

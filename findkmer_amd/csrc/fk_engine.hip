@@ -73,12 +73,13 @@ __device__ __forceinline__ uint64_t comp_packed(uint64_t x, int k, uint64_t mask
     return (uint64_t)nA | ((uint64_t)nC << 16) | ((uint64_t)nG << 32) | ((uint64_t)nT << 48);
 }
 
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
 struct Counters {       /* per lane; flushed per chunk */
-    uint64_t base;      /* 4 x 16-bit */
-    uint64_t d1w;
-    uint64_t d1s;
-    uint32_t valid;
-    uint32_t win;
+    uint64_t base;      /* 4 x 16-bit: first-window extra bases (first k-1 digits) */
+    uint64_t d1s;       /* 4 x 16-bit: depth-1 trie touches of short walks */
+    uint32_t valid;     /* baseCounter beyond one per window ((k-1) per first window) */
+    uint32_t win;       /* windows counted */
     uint32_t unknown;
     uint32_t eof;       /* chunk-relative offset of first 0xFF, or FK_NO_EOF */
 };
@@ -87,24 +88,34 @@ struct Facts {          /* wave-uniform per chunk */
     uint32_t found_p1, p1_gt, any_reset, reset_after_p1, R_at_p1, nv_total;
 };
 
+/* Where windows are accumulated. */
+enum HistMode {
+    H_PAIRS = 0,    /* k <= 6: LDS bins of (k+1)-mers at every other base + LDS k-mer singles */
+    H_LDS = 1,      /* k == 7: LDS k-mer bins */
+    H_GLOBAL = 2    /* k >= 8: global u32 atomics */
+};
+
 struct Ctx {            /* kernel-wide constants */
     const uint8_t *buf;
     uint64_t len;
     int64_t lo;         /* lowest readable offset (negative: halo before buf) */
     uint32_t *table;    /* global 4^k */
-    uint32_t *lds;      /* LDS bins (k <= FK_LDS_MAX_K) or nullptr */
+    uint32_t *lds;      /* LDS bins or nullptr */
     uint32_t *shortcnt; /* sum_{d<k} 4^d */
     unsigned long long *acc;
     uint64_t maskk;
+    uint32_t single_off;/* H_PAIRS: offset of the k-mer singles in LDS (4^(k+1)) */
     int k;
 };
 
-template <bool USE_LDS>
+template <int HM>
 __device__ __forceinline__ void hist_add(const Ctx &cx, uint64_t idx, uint32_t w) {
-    if (USE_LDS) {
+    if (HM == H_GLOBAL) {
+        atomicAdd(&cx.table[idx], w);
+    } else if (HM == H_LDS) {
         atomicAdd(&cx.lds[(uint32_t)idx], w);
     } else {
-        atomicAdd(&cx.table[idx], w);
+        atomicAdd(&cx.lds[cx.single_off + (uint32_t)idx], w);
     }
 }
 
@@ -123,7 +134,7 @@ __device__ __forceinline__ int load16(const Ctx &cx, int64_t off, uint32_t w[4])
     w[0] = w[1] = w[2] = w[3] = 0;
     if (off < cx.lo || off >= (int64_t)cx.len) return 0;
     if (off + 16 <= (int64_t)cx.len) {
-        uint4 v = *reinterpret_cast<const uint4 *>(cx.buf + off);
+        u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(cx.buf + off));
         w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
         return 16;
     }
@@ -133,12 +144,12 @@ __device__ __forceinline__ int load16(const Ctx &cx, int64_t off, uint32_t w[4])
 }
 
 /*
- * Process one tile (one wave, 16 bytes per lane, `nb` valid).
+ * Slow, fully general tile (one wave, 16 bytes per lane, `nb` valid).
  * COUNT=false: only advance the wave state (halo guess).
  * `tile_off` is the tile's byte offset inside its chunk.
  */
-template <bool COUNT, bool USE_LDS>
-__device__ __forceinline__ void tile_general(const Ctx &cx, const uint32_t w[4], int nb,
+template <bool COUNT, int HM>
+__device__ __attribute__((noinline)) void tile_general(const Ctx &cx, const uint32_t w[4], int nb,
                                              uint32_t tile_off, DState &st, Facts &f,
                                              Counters &cnt, uint32_t weight) {
     const int lane = threadIdx.x & 63;
@@ -222,16 +233,17 @@ __device__ __forceinline__ void tile_general(const Ctx &cx, const uint32_t w[4],
 
         /* first special byte of the chunk ('\n' or '>') */
         uint64_t spm = __ballot(firstSp != 0xFFFFu);
-        uint32_t p1 = 0xFFFFFFFFu;    /* resets after position p1 count as after p1 */
+        uint32_t p1 = 0xFFFFFFFFu;
         int p1_lane = -1;
         if (f.found_p1) {
-            p1 = 0;                   /* found in an earlier tile: everything is after */
+            p1 = 0;
         } else if (spm) {
             p1_lane = __ffsll((long long)spm) - 1;
             p1 = rdlane(firstSp, p1_lane);
         }
         const bool p1_here = !f.found_p1 && spm;
         uint32_t r_at = 0, lane_reset = 0, lane_reset_after = 0;
+        const uint64_t maskk1 = cx.maskk >> 2;
 
 #pragma unroll
         for (int j = 0; j < 16; j++) {
@@ -264,20 +276,14 @@ __device__ __forceinline__ void tile_general(const Ctx &cx, const uint32_t w[4],
                 lc = (lc << 2) | (uint32_t)s;
                 R += 1;
                 int seq = (int)R;
-                if (seq > k) {
+                if (seq >= k) {
                     uint64_t idx = lc & cx.maskk;
-                    hist_add<USE_LDS>(cx, idx, weight);
-                    cnt.base += 1ull << (16 * s);
-                    cnt.valid += 1;
+                    hist_add<HM>(cx, idx, weight);
                     cnt.win += 1;
-                    cnt.d1w += 1ull << (16 * (uint32_t)((idx >> (2 * k - 2)) & 3));
-                } else if (seq == k) {
-                    uint64_t idx = lc & cx.maskk;
-                    hist_add<USE_LDS>(cx, idx, weight);
-                    cnt.base += comp_packed(idx, k, cx.maskk);
-                    cnt.valid += (uint32_t)k;
-                    cnt.win += 1;
-                    cnt.d1w += 1ull << (16 * (uint32_t)((idx >> (2 * k - 2)) & 3));
+                    if (seq == k) {               /* first window: its first k-1 bases */
+                        cnt.base += comp_packed(idx >> 2, k - 1, maskk1);
+                        cnt.valid += (uint32_t)(k - 1);
+                    }
                 } else if (seq >= 1) {
                     cnt.d1s += 1ull << (16 * (uint32_t)((lc >> (2 * seq - 2)) & 3));
                 }
@@ -295,6 +301,123 @@ __device__ __forceinline__ void tile_general(const Ctx &cx, const uint32_t w[4],
         }
     }
     st = nst;
+}
+
+/* byte-wise "is non-zero" mask (bit 7 of each byte), exact per byte */
+__device__ __forceinline__ uint32_t nz_bytes(uint32_t d) {
+    return (((d & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | d) & 0x80808080u;
+}
+
+/*
+ * Fast tile: every byte is A/C/G/T except at most one '\n' per lane, the wave
+ * is outside a header and deep inside a run (every window counts as
+ * seqSize > k).  Returns false (without side effects) when the tile does not
+ * qualify; the caller then runs tile_general.
+ *
+ * Per lane: 16 bytes -> 2-bit codes (A0 C1 G2 T3) in one 32-bit word, first
+ * base in the top digit (v_dot4_u32_u8 packs 4 bases per instruction); the
+ * previous lane's word (one __shfl_up) supplies the k-1 bases of context;
+ * each window is one v_alignbit of the 64-bit {prev, mine} pair.
+ */
+template <bool COUNT, int HM>
+__device__ __forceinline__ bool tile_fast(const Ctx &cx, const uint32_t w[4], uint32_t tile_off,
+                                          DState &st, Facts &f, Counters &cnt, uint32_t weight) {
+    const int lane = threadIdx.x & 63;
+    const int k = cx.k;
+    uint32_t cw[4];
+    uint32_t bad = 0, nlm = 0;
+#pragma unroll
+    for (int d = 0; d < 4; d++) {
+        uint32_t x = (w[d] >> 1) & 0x03030303u;
+        uint32_t c = x ^ ((x >> 1) & 0x01010101u);         /* A0 C1 G2 T3 per byte */
+        cw[d] = c;
+        uint32_t e = __builtin_amdgcn_perm(0u, 0x54474341u, c);   /* "ACGT"[c] */
+        if (e != w[d]) {
+            uint32_t mis = nz_bytes(e ^ w[d]);
+            uint32_t isnl = ~nz_bytes(w[d] ^ 0x0A0A0A0Au) & 0x80808080u;
+            bad |= mis & ~isnl;
+            /* newline byte positions -> bits 4d..4d+3 */
+            nlm |= ((isnl >> 7) & 1u) << (4 * d) | ((isnl >> 15) & 1u) << (4 * d + 1) |
+                   ((isnl >> 23) & 1u) << (4 * d + 2) | ((isnl >> 31) & 1u) << (4 * d + 3);
+        }
+    }
+    const bool lane_ok = bad == 0 && __popc(nlm) <= 1;
+    if (__ballot(!lane_ok)) return false;
+    if (COUNT && !((int32_t)st.R >= k && st.R <= 0x7FFFFFFFu - FK_TILE_BYTES)) return false;
+
+    /* pack: P = 16 digits, byte 0 in bits 31:30 */
+    uint32_t P = __builtin_amdgcn_udot4(cw[0], 0x01041040u, 0u, false);
+    P = __builtin_amdgcn_udot4(cw[1], 0x01041040u, P << 8, false);
+    P = __builtin_amdgcn_udot4(cw[2], 0x01041040u, P << 8, false);
+    P = __builtin_amdgcn_udot4(cw[3], 0x01041040u, P << 8, false);
+    /* squeeze out the newline digit: S = 15 digits right-aligned */
+    const bool has_nl = nlm != 0;
+    uint32_t S = P;
+    if (has_nl) {
+        int j = __ffs(nlm) - 1;                                /* byte index 0..15 */
+        uint32_t lo_bits = 30u - 2u * (uint32_t)j;             /* digits after the '\n' */
+        uint32_t hi = j ? (P >> (32u - 2u * (uint32_t)j)) : 0u;
+        uint32_t lo = lo_bits ? (P & ((1u << lo_bits) - 1u)) : 0u;
+        S = (lo_bits < 32u ? (hi << lo_bits) : 0u) | lo;
+    }
+    uint32_t prev = shup(S, 1);
+    if (lane == 0) prev = (uint32_t)st.code;
+    /* make {C, S2} one contiguous base stream with S2 holding 16 digits */
+    const uint32_t S2 = has_nl ? (S | ((prev & 3u) << 30)) : S;
+    const uint32_t C = has_nl ? (prev >> 2) : prev;
+
+    const uint64_t nlb = __ballot(has_nl);
+    const uint32_t nsym = FK_TILE_BYTES - (uint32_t)__popcll(nlb);
+
+    if (COUNT) {
+        const uint32_t m2 = (uint32_t)cx.maskk << 2;
+        if (HM == H_PAIRS) {
+            /* (k+1)-mers ending at odd slots 1,3,..,15 cover the k-mers at
+               slots (0,1),(2,3),... ; a lane with a '\n' has no real slot 0,
+               so its first pair becomes the single k-mer at slot 1 */
+            const uint32_t m3 = (uint32_t)((cx.maskk << 2) | 3u) << 2;
+            char *L = reinterpret_cast<char *>(cx.lds);
+            {
+                uint32_t a7 = __builtin_amdgcn_alignbit(C, S2, 26u) & m3;
+                uint32_t a6 = __builtin_amdgcn_alignbit(C, S2, 26u) & m2;
+                uint32_t addr = has_nl ? (cx.single_off * 4u + a6) : a7;
+                atomicAdd(reinterpret_cast<uint32_t *>(L + addr), weight);
+            }
+#pragma unroll
+            for (int j = 1; j < 7; j++) {
+                uint32_t a = __builtin_amdgcn_alignbit(C, S2, (uint32_t)(26 - 4 * j)) & m3;
+                atomicAdd(reinterpret_cast<uint32_t *>(L + a), weight);
+            }
+            {
+                uint32_t a = (S2 << 2) & m3;
+                atomicAdd(reinterpret_cast<uint32_t *>(L + a), weight);
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < 16; i++) {
+                uint32_t sh = 2u * (15u - (uint32_t)i);
+                uint32_t v = i < 15 ? __builtin_amdgcn_alignbit(C, S2, sh) : S2;
+                uint32_t idx = v & (uint32_t)cx.maskk;
+                if (i > 0 || !has_nl) {
+                    if (HM == H_LDS) atomicAdd(&cx.lds[idx], weight);
+                    else atomicAdd(&cx.table[idx], weight);
+                }
+            }
+        }
+        if (lane == 0) cnt.win += nsym;
+        /* chunk facts: the first '\n' of the chunk */
+        if (!f.found_p1 && nlb) {
+            int L0 = __ffsll((long long)nlb) - 1;
+            uint32_t j0 = (uint32_t)(__ffs(rdlane(nlm, L0)) - 1);
+            f.found_p1 = 1;
+            f.p1_gt = 0;
+            f.R_at_p1 = st.R + (uint32_t)L0 * 16u + j0;
+        }
+        f.nv_total += nsym;
+    }
+    st.R += nsym;
+    st.code = ((uint64_t)rdlane(C, 63) << 32) | rdlane(S2, 63);
+    return true;
 }
 
 /* wave-wide sum via butterfly */
@@ -315,40 +438,82 @@ __device__ __forceinline__ void acc_add(unsigned long long *a, uint64_t v, uint3
 
 __device__ void flush_counters(const Ctx &cx, Counters &cnt, uint32_t weight) {
     const int lane = threadIdx.x & 63;
-    uint32_t vals[14];
+    uint32_t vals[10];
     for (int b = 0; b < 4; b++) {
         vals[b] = (uint32_t)((cnt.base >> (16 * b)) & 0xFFFF);
-        vals[6 + b] = (uint32_t)((cnt.d1w >> (16 * b)) & 0xFFFF);
-        vals[10 + b] = (uint32_t)((cnt.d1s >> (16 * b)) & 0xFFFF);
+        vals[6 + b] = (uint32_t)((cnt.d1s >> (16 * b)) & 0xFFFF);
     }
     vals[4] = cnt.valid;
     vals[5] = cnt.win;
 #pragma unroll
-    for (int i = 0; i < 14; i++) vals[i] = wsum32(vals[i]);
+    for (int i = 0; i < 10; i++) vals[i] = wsum32(vals[i]);
     if (lane == 0) {
 #pragma unroll
-        for (int i = 0; i < 14; i++) acc_add(&cx.acc[i], vals[i], weight);
+        for (int i = 0; i < 4; i++) acc_add(&cx.acc[ACC_BASE + i], vals[i], weight);
+        acc_add(&cx.acc[ACC_VALID], vals[4], weight);
+        acc_add(&cx.acc[ACC_WIN], vals[5], weight);
+#pragma unroll
+        for (int i = 0; i < 4; i++) acc_add(&cx.acc[ACC_D1S + i], vals[6 + i], weight);
     }
-    cnt.base = cnt.d1w = cnt.d1s = 0;
+    cnt.base = cnt.d1s = 0;
     cnt.valid = cnt.win = 0;
 }
 
-/* Count one chunk from entering state st.  Returns the exit state. */
-template <bool USE_LDS>
-__device__ void count_chunk(const Ctx &cx, uint64_t chunk, DState st, uint32_t weight,
-                            ChunkRec *rec, bool write_facts, bool write_obs) {
+template <bool COUNT, int HM>
+__device__ __forceinline__ void do_tile(const Ctx &cx, const uint32_t w[4], int64_t toff, uint32_t tile_off,
+                                        bool full, DState &st, Facts &f, Counters &cnt, uint32_t weight) {
+    if (full && st.hdr == 0 && cx.k <= 16 && tile_fast<COUNT, HM>(cx, w, tile_off, st, f, cnt, weight))
+        return;
+    const int lane = threadIdx.x & 63;
+    uint32_t v[4] = {w[0], w[1], w[2], w[3]};
+    int nb = 16;
+    if (!full) nb = load16(cx, toff + lane * 16, v);
+    tile_general<COUNT, HM>(cx, v, nb, tile_off, st, f, cnt, weight);
+}
+
+/* Count one chunk from entering state st; returns the exit state. */
+template <int HM>
+__device__ DState count_chunk(const Ctx &cx, uint64_t chunk, DState st, uint32_t weight,
+                              ChunkRec *rec, bool write_facts, bool write_obs) {
     const int lane = threadIdx.x & 63;
     const int64_t start = (int64_t)(chunk * FK_CHUNK_BYTES);
     const uint64_t clen = min((uint64_t)FK_CHUNK_BYTES, cx.len - (uint64_t)start);
     const uint32_t ntiles = (uint32_t)((clen + FK_TILE_BYTES - 1) / FK_TILE_BYTES);
     Facts f{0, 0, 0, 0, 0, 0};
-    Counters cnt{0, 0, 0, 0, 0, 0, FK_NO_EOF};
+    Counters cnt{0, 0, 0, 0, 0, FK_NO_EOF};
     const DState a = st;
-    for (uint32_t t = 0; t < ntiles; t++) {
-        uint32_t w[4];
-        int nb = load16(cx, start + (int64_t)t * FK_TILE_BYTES + lane * 16, w);
-        tile_general<true, USE_LDS>(cx, w, nb, t * FK_TILE_BYTES, st, f, cnt, weight);
+    /* 4-tile groups, next group's loads in flight while this one is counted */
+    uint32_t g[4][4], nx[4][4];
+#define FK_LOADG(dst, grp)                                                           \
+    _Pragma("unroll") for (int q = 0; q < 4; q++) {                                  \
+        uint32_t t_ = (grp) * 4u + (uint32_t)q;                                      \
+        int64_t o_ = start + (int64_t)t_ * FK_TILE_BYTES + lane * 16;                \
+        if (t_ < ntiles && o_ + 16 <= (int64_t)cx.len) {                             \
+            u32x4 v_ = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(cx.buf + o_)); \
+            dst[q][0] = v_.x; dst[q][1] = v_.y; dst[q][2] = v_.z; dst[q][3] = v_.w;   \
+        } else {                                                                     \
+            dst[q][0] = dst[q][1] = dst[q][2] = dst[q][3] = 0;                       \
+        }                                                                            \
     }
+    const uint32_t ngroups = (ntiles + 3) / 4;
+    FK_LOADG(g, 0u);
+    for (uint32_t grp = 0; grp < ngroups; grp++) {
+        if (grp + 1 < ngroups) { FK_LOADG(nx, grp + 1); }
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            uint32_t t = grp * 4u + (uint32_t)q;
+            if (t < ntiles) {
+                int64_t toff = start + (int64_t)t * FK_TILE_BYTES;
+                bool full = toff + (int64_t)FK_TILE_BYTES <= (int64_t)cx.len;
+                do_tile<true, HM>(cx, g[q], toff, t * FK_TILE_BYTES, full, st, f, cnt, weight);
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < 4; q++)
+#pragma unroll
+            for (int d = 0; d < 4; d++) g[q][d] = nx[q][d];
+    }
+#undef FK_LOADG
     flush_counters(cx, cnt, weight);
     uint32_t unk = wsum32(cnt.unknown);
     uint32_t eof = wmin32(cnt.eof);
@@ -368,10 +533,11 @@ __device__ void count_chunk(const Ctx &cx, uint64_t chunk, DState st, uint32_t w
             r.eof_off = eof;
         }
     }
+    return st;
 }
 
 /* Guess the state entering `chunk` from the FK_HALO_BYTES before it. */
-template <bool USE_LDS>
+template <int HM>
 __device__ DState halo_state(const Ctx &cx, uint64_t chunk) {
     const int lane = threadIdx.x & 63;
     const int64_t start = (int64_t)(chunk * FK_CHUNK_BYTES);
@@ -382,50 +548,72 @@ __device__ DState halo_state(const Ctx &cx, uint64_t chunk) {
     else { w[0] = w[1] = w[2] = w[3] = 0; }
     DState st{0, 0, 0};
     Facts f{0, 0, 0, 0, 0, 0};
-    Counters cnt{0, 0, 0, 0, 0, 0, FK_NO_EOF};
-    tile_general<false, USE_LDS>(cx, w, nb, 0, st, f, cnt, 1u);
+    Counters cnt{0, 0, 0, 0, 0, FK_NO_EOF};
+    tile_general<false, HM>(cx, w, nb, 0, st, f, cnt, 1u);
     return st;
 }
 
-__device__ void lds_zero(uint32_t *lds, uint32_t nbins) {
-    for (uint32_t i = threadIdx.x; i < nbins; i += blockDim.x) lds[i] = 0;
+__device__ uint32_t lds_words(int HM, int k) {
+    return HM == H_PAIRS ? (1u << (2 * k + 2)) + (1u << (2 * k)) : HM == H_LDS ? (1u << (2 * k)) : 0u;
+}
+
+__device__ void lds_zero(uint32_t *lds, uint32_t nw) {
+    for (uint32_t i = threadIdx.x; i < nw; i += blockDim.x) lds[i] = 0;
     __syncthreads();
 }
-__device__ void lds_flush(uint32_t *lds, uint32_t nbins, uint32_t *table) {
+
+/* fold the block's LDS bins into the global table */
+template <int HM>
+__device__ void lds_flush(const Ctx &cx) {
     __syncthreads();
-    for (uint32_t i = threadIdx.x; i < nbins; i += blockDim.x) {
-        uint32_t v = lds[i];
-        if (v) atomicAdd(&table[i], v);
+    const uint32_t nk = 1u << (2 * cx.k);
+    for (uint32_t i = threadIdx.x; i < nk; i += blockDim.x) {
+        uint32_t v;
+        if (HM == H_PAIRS) {
+            const uint32_t *pr = cx.lds;
+            v = cx.lds[cx.single_off + i];
+            /* k-mer i is the prefix of (k+1)-mers 4i+a and the suffix of a*4^k+i */
+            v += pr[4 * i] + pr[4 * i + 1] + pr[4 * i + 2] + pr[4 * i + 3];
+            v += pr[i] + pr[nk + i] + pr[2 * nk + i] + pr[3 * nk + i];
+        } else {
+            v = cx.lds[i];
+        }
+        if (v) atomicAdd(&cx.table[i], v);
     }
 }
 
 /*
- * k_count: main pass.  Chunk 0 takes the known entering state *d_init when
- * has_init != 0 (stream continuation); every other chunk guesses from its halo.
+ * k_count: main pass.  Wave w counts the contiguous chunk range
+ * [w*cpw, (w+1)*cpw): the first chunk of the range guesses its entering state
+ * from its halo (or takes the known stream state *d_init for chunk 0), the
+ * next ones continue from the previous chunk's exit.
  */
-template <bool USE_LDS>
-__global__ void __launch_bounds__(FK_BLOCK)
+template <int HM>
+__global__ void __launch_bounds__(FK_BLOCK, 4)
 k_count(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint32_t *table,
         uint32_t *shortcnt, unsigned long long *acc, ChunkRec *rec, uint64_t nchunks,
-        const XState *d_init, int has_init) {
+        const XState *d_init, int has_init, uint64_t cpw) {
     extern __shared__ uint32_t lds_bins[];
-    const uint32_t nbins = USE_LDS ? (1u << (2 * k)) : 0u;
-    if (USE_LDS) lds_zero(lds_bins, nbins);
-    Ctx cx{buf, len, lo, table, USE_LDS ? lds_bins : nullptr, shortcnt, acc, maskk, k};
+    const uint32_t nw = lds_words(HM, k);
+    if (HM != H_GLOBAL) lds_zero(lds_bins, nw);
+    Ctx cx{buf, len, lo, table, HM != H_GLOBAL ? lds_bins : nullptr, shortcnt, acc, maskk,
+           1u << (2 * k + 2), k};
     const uint64_t wave = blockIdx.x * FK_WAVES_PER_BLOCK + (threadIdx.x >> 6);
-    const uint64_t nwaves = (uint64_t)gridDim.x * FK_WAVES_PER_BLOCK;
-    for (uint64_t c = wave; c < nchunks; c += nwaves) {
-        DState st;
-        if (c == 0 && has_init) {
-            st.hdr = d_init->hdr;
-            st.R = (uint32_t)d_init->R;
-            st.code = d_init->code;
-        } else {
-            st = halo_state<USE_LDS>(cx, c);
+    const uint64_t c0 = wave * cpw, c1 = min(c0 + cpw, nchunks);
+    DState st{0, 0, 0};
+    for (uint64_t c = c0; c < c1; c++) {
+        if (c == c0) {
+            if (c == 0 && has_init) {
+                st.hdr = d_init->hdr;
+                st.R = (uint32_t)d_init->R;
+                st.code = d_init->code;
+            } else {
+                st = halo_state<HM>(cx, c);
+            }
         }
-        count_chunk<USE_LDS>(cx, c, st, 1u, rec, true, true);
+        st = count_chunk<HM>(cx, c, st, 1u, rec, true, true);
     }
-    if (USE_LDS) lds_flush(lds_bins, nbins, table);
+    if (HM != H_GLOBAL) lds_flush<HM>(cx);
 }
 
 /*
@@ -434,17 +622,18 @@ k_count(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uin
  * exact state.  mode 1 = "cancel all from s_true" (used when a 0xFF byte
  * truncates the segment and everything must be undone).
  */
-template <bool USE_LDS>
+template <int HM>
 __global__ void __launch_bounds__(FK_BLOCK)
 k_redo(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint32_t *table,
        uint32_t *shortcnt, unsigned long long *acc, ChunkRec *rec, const XState *s_true,
        const uint32_t *list, const uint32_t *list_n, uint64_t nchunks, int mode) {
     extern __shared__ uint32_t lds_bins[];
-    const uint32_t nbins = USE_LDS ? (1u << (2 * k)) : 0u;
     const uint64_t n = mode == 1 ? nchunks : (uint64_t)*list_n;
     if (n == 0) return;   /* uniform across the grid */
-    if (USE_LDS) lds_zero(lds_bins, nbins);
-    Ctx cx{buf, len, lo, table, USE_LDS ? lds_bins : nullptr, shortcnt, acc, maskk, k};
+    const uint32_t nw = lds_words(HM, k);
+    if (HM != H_GLOBAL) lds_zero(lds_bins, nw);
+    Ctx cx{buf, len, lo, table, HM != H_GLOBAL ? lds_bins : nullptr, shortcnt, acc, maskk,
+           1u << (2 * k + 2), k};
     const uint64_t wave = blockIdx.x * FK_WAVES_PER_BLOCK + (threadIdx.x >> 6);
     const uint64_t nwaves = (uint64_t)gridDim.x * FK_WAVES_PER_BLOCK;
     for (uint64_t i = wave; i < n; i += nwaves) {
@@ -452,15 +641,15 @@ k_redo(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint
         const XState t = s_true[c];
         DState ts{t.code, (uint32_t)t.R, t.hdr};
         if (mode == 1) {
-            count_chunk<USE_LDS>(cx, c, ts, 0xFFFFFFFFu, rec, false, false);
+            count_chunk<HM>(cx, c, ts, 0xFFFFFFFFu, rec, false, false);
         } else {
             const ChunkRec r = rec[c];
             DState as{r.a_code, r.a_R, r.a_hdr};
-            count_chunk<USE_LDS>(cx, c, as, 0xFFFFFFFFu, rec, false, false);
-            count_chunk<USE_LDS>(cx, c, ts, 1u, rec, false, true);
+            count_chunk<HM>(cx, c, as, 0xFFFFFFFFu, rec, false, false);
+            count_chunk<HM>(cx, c, ts, 1u, rec, false, true);
         }
     }
-    if (USE_LDS) lds_flush(lds_bins, nbins, table);
+    if (HM != H_GLOBAL) lds_flush<HM>(cx);
 }
 
 /*
@@ -525,19 +714,45 @@ __global__ void k_obs(const ChunkRec *rec, uint64_t n, unsigned long long *out /
     if (eof != ~0ull) atomicMin(&out[1], eof);
 }
 
-/* distinct k-mers: number of non-zero counters */
-__global__ void k_distinct(const uint32_t *table, uint64_t n, unsigned long long *out) {
-    unsigned long long c = 0;
+/* One pass over the final table: distinct k-mers, total, and the first- and
+ * last-base marginals (-> depth-1 trie frequencies and base composition). */
+__device__ __forceinline__ unsigned long long wsum64(unsigned long long v) {
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+    return v;
+}
+__global__ void k_table_stats(const uint32_t *table, uint64_t n, int k, unsigned long long *out) {
+    unsigned long long dist = 0, sum = 0, last[4] = {0, 0, 0, 0}, first[4] = {0, 0, 0, 0};
     const uint64_t n4 = n / 4;
     const uint4 *t4 = reinterpret_cast<const uint4 *>(table);
-    for (uint64_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (uint64_t)gridDim.x * blockDim.x) {
+    const int fs = 2 * (k - 1);
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n4; i += (uint64_t)gridDim.x * blockDim.x) {
         uint4 v = t4[i];
-        c += (v.x != 0) + (v.y != 0) + (v.z != 0) + (v.w != 0);
+        dist += (v.x != 0) + (v.y != 0) + (v.z != 0) + (v.w != 0);
+        unsigned long long s4 = (unsigned long long)v.x + v.y + v.z + v.w;
+        sum += s4;
+        last[0] += v.x; last[1] += v.y; last[2] += v.z; last[3] += v.w;
+        if (k == 1) {
+            first[0] += v.x; first[1] += v.y; first[2] += v.z; first[3] += v.w;
+        } else {
+            uint32_t fd = (uint32_t)(((i * 4) >> fs) & 3);
+            first[0] += fd == 0 ? s4 : 0; first[1] += fd == 1 ? s4 : 0;
+            first[2] += fd == 2 ? s4 : 0; first[3] += fd == 3 ? s4 : 0;
+        }
     }
-    for (uint64_t i = n4 * 4 + blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
-        c += table[i] != 0;
-    c = wsum32((uint32_t)c);   /* <= 256 per lane-visit sum fits easily per wave */
-    if ((threadIdx.x & 63) == 0 && c) atomicAdd(out, c);
+    dist = wsum64(dist);
+    sum = wsum64(sum);
+#pragma unroll
+    for (int b = 0; b < 4; b++) { last[b] = wsum64(last[b]); first[b] = wsum64(first[b]); }
+    if ((threadIdx.x & 63) == 0) {
+        if (dist) atomicAdd(&out[0], dist);
+        if (sum) atomicAdd(&out[1], sum);
+#pragma unroll
+        for (int b = 0; b < 4; b++) {
+            if (last[b]) atomicAdd(&out[2 + b], last[b]);
+            if (first[b]) atomicAdd(&out[6 + b], first[b]);
+        }
+    }
 }
 
 /* trie prefix presence, level d from level d+1 (or from the table at d = k-1) */
@@ -714,7 +929,8 @@ struct fk_engine {
     uint64_t nbins = 0, nshort = 0, maskk = 0;
     uint32_t *d_table = nullptr, *d_short = nullptr;
     unsigned long long *d_acc = nullptr;   /* ACC_N slots */
-    unsigned long long *d_obs = nullptr;   /* [0] unknown, [1] eof, [2] distinct, [3] level count */
+    unsigned long long *d_obs = nullptr;   /* [0] unknown, [1] eof, [2] spare, [3] level count */
+    unsigned long long *d_tstat = nullptr; /* k_table_stats output */
     ChunkRec *d_rec = nullptr;
     XState *d_strue = nullptr, *d_state = nullptr;
     uint32_t *d_redo = nullptr, *d_redo_n = nullptr;
@@ -787,7 +1003,7 @@ extern "C" void fk_engine_destroy(fk_engine *e) {
     if (!e) return;
     hipSetDevice(e->dev);
     if (e->stream) hipStreamSynchronize(e->stream);
-    hipFree(e->d_table); hipFree(e->d_short); hipFree(e->d_acc); hipFree(e->d_obs);
+    hipFree(e->d_table); hipFree(e->d_short); hipFree(e->d_acc); hipFree(e->d_obs); hipFree(e->d_tstat);
     hipFree(e->d_rec); hipFree(e->d_strue); hipFree(e->d_state); hipFree(e->d_redo);
     hipFree(e->d_redo_n); hipFree(e->d_tf);
     for (int i = 0; i < 2; i++) { hipFree(e->d_stage[i]); hipHostFree(e->h_stage[i]); }
@@ -828,6 +1044,7 @@ extern "C" int fk_engine_create(int k, const fk_opts *opts, fk_engine **out) {
     if (e->nshort) { ALLOC(e->d_short, e->nshort * sizeof(uint32_t)); }
     ALLOC(e->d_acc, ACC_N * sizeof(unsigned long long));
     ALLOC(e->d_obs, 8 * sizeof(unsigned long long));
+    ALLOC(e->d_tstat, 10 * sizeof(unsigned long long));
     ALLOC(e->d_state, sizeof(XState));
     ALLOC(e->d_redo_n, sizeof(uint32_t));
     ALLOC(e->d_tf, sizeof(TF));
@@ -859,30 +1076,43 @@ static int grow_chunk_arrays(fk_engine *e, uint64_t nchunks, uint64_t &cap) {
     return FK_OK;
 }
 
-static bool use_lds(const fk_engine *e) { return e->k <= FK_LDS_MAX_K; }
+static int hist_mode(const fk_engine *e) { return e->k <= 6 ? H_PAIRS : e->k == 7 ? H_LDS : H_GLOBAL; }
+
+static uint64_t blocks_per_cu(const fk_engine *e) { return hist_mode(e) == H_GLOBAL ? 4 : 2; }
 
 static unsigned grid_for(const fk_engine *e, uint64_t nwork_waves) {
-    /* persistent: up to 2 blocks (16 waves) per CU for LDS bins, 4 otherwise */
-    uint64_t per_cu = use_lds(e) ? 2 : 4;
-    uint64_t maxb = (uint64_t)e->cus * per_cu;
+    uint64_t maxb = (uint64_t)e->cus * blocks_per_cu(e);
     uint64_t need = (nwork_waves + FK_WAVES_PER_BLOCK - 1) / FK_WAVES_PER_BLOCK;
     return (unsigned)std::max<uint64_t>(1, std::min(maxb, need));
 }
 
-static size_t lds_bytes(const fk_engine *e) { return use_lds(e) ? (size_t)e->nbins * sizeof(uint32_t) : 0; }
+static size_t lds_bytes(const fk_engine *e) {
+    int m = hist_mode(e);
+    if (m == H_PAIRS) return ((size_t)e->nbins * 4 + e->nbins) * sizeof(uint32_t);
+    if (m == H_LDS) return (size_t)e->nbins * sizeof(uint32_t);
+    return 0;
+}
+
+#define FK_DISPATCH(HMV, ...)                                                   \
+    switch (HMV) {                                                              \
+    case H_PAIRS: { constexpr int HM = H_PAIRS; __VA_ARGS__; } break;          \
+    case H_LDS: { constexpr int HM = H_LDS; __VA_ARGS__; } break;              \
+    default: { constexpr int HM = H_GLOBAL; __VA_ARGS__; } break;              \
+    }
 
 static int launch_count(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t lo, uint64_t nchunks,
                         int has_init) {
-    unsigned g = grid_for(e, nchunks);
+    /* contiguous chunk ranges: enough waves to fill the chip, each taking
+       cpw consecutive chunks (only a range's first chunk needs a halo) */
+    uint64_t max_waves = (uint64_t)e->cus * blocks_per_cu(e) * FK_WAVES_PER_BLOCK;
+    uint64_t cpw = (nchunks + max_waves - 1) / max_waves;
+    uint64_t nwaves = (nchunks + cpw - 1) / cpw;
+    unsigned g = (unsigned)std::max<uint64_t>(1, (nwaves + FK_WAVES_PER_BLOCK - 1) / FK_WAVES_PER_BLOCK);
     size_t sh = lds_bytes(e);
-    if (use_lds(e))
-        hipLaunchKernelGGL((k_count<true>), dim3(g), dim3(FK_BLOCK), sh, e->stream, buf, len, lo, e->k,
-                           e->maskk, e->d_table, e->d_short, e->d_acc, e->d_rec, nchunks, e->d_state,
-                           has_init);
-    else
-        hipLaunchKernelGGL((k_count<false>), dim3(g), dim3(FK_BLOCK), 0, e->stream, buf, len, lo, e->k,
-                           e->maskk, e->d_table, e->d_short, e->d_acc, e->d_rec, nchunks, e->d_state,
-                           has_init);
+    FK_DISPATCH(hist_mode(e),
+                hipLaunchKernelGGL((k_count<HM>), dim3(g), dim3(FK_BLOCK), sh, e->stream, buf, len, lo, e->k,
+                                   e->maskk, e->d_table, e->d_short, e->d_acc, e->d_rec, nchunks, e->d_state,
+                                   has_init, cpw));
     HIPCHK(hipGetLastError());
     return FK_OK;
 }
@@ -891,14 +1121,10 @@ static int launch_redo(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t l
                        int mode) {
     unsigned g = mode == 1 ? grid_for(e, nchunks) : grid_for(e, std::min<uint64_t>(nchunks, 4096));
     size_t sh = lds_bytes(e);
-    if (use_lds(e))
-        hipLaunchKernelGGL((k_redo<true>), dim3(g), dim3(FK_BLOCK), sh, e->stream, buf, len, lo, e->k,
-                           e->maskk, e->d_table, e->d_short, e->d_acc, e->d_rec, e->d_strue, e->d_redo,
-                           e->d_redo_n, nchunks, mode);
-    else
-        hipLaunchKernelGGL((k_redo<false>), dim3(g), dim3(FK_BLOCK), 0, e->stream, buf, len, lo, e->k,
-                           e->maskk, e->d_table, e->d_short, e->d_acc, e->d_rec, e->d_strue, e->d_redo,
-                           e->d_redo_n, nchunks, mode);
+    FK_DISPATCH(hist_mode(e),
+                hipLaunchKernelGGL((k_redo<HM>), dim3(g), dim3(FK_BLOCK), sh, e->stream, buf, len, lo, e->k,
+                                   e->maskk, e->d_table, e->d_short, e->d_acc, e->d_rec, e->d_strue, e->d_redo,
+                                   e->d_redo_n, nchunks, mode));
     HIPCHK(hipGetLastError());
     return FK_OK;
 }
@@ -1209,20 +1435,26 @@ extern "C" int fk_engine_finish(fk_engine *e, fk_result *res) {
     }
     unsigned long long acc[ACC_N];
     HIPCHK(hipMemcpyAsync(acc, e->d_acc, sizeof acc, hipMemcpyDeviceToHost, e->stream));
-    HIPCHK(hipMemsetAsync(e->d_obs + 2, 0, sizeof(unsigned long long), e->stream));
+    HIPCHK(hipMemsetAsync(e->d_tstat, 0, 10 * sizeof(unsigned long long), e->stream));
     unsigned gd = (unsigned)std::min<uint64_t>((uint64_t)e->cus * 4, (e->nbins / 4 + 255) / 256 + 1);
-    hipLaunchKernelGGL(k_distinct, dim3(gd), dim3(256), 0, e->stream, e->d_table, e->nbins, e->d_obs + 2);
+    hipLaunchKernelGGL(k_table_stats, dim3(gd), dim3(256), 0, e->stream, e->d_table, e->nbins, k, e->d_tstat);
     HIPCHK(hipGetLastError());
-    unsigned long long distinct = 0;
-    HIPCHK(hipMemcpyAsync(&distinct, e->d_obs + 2, sizeof distinct, hipMemcpyDeviceToHost, e->stream));
+    unsigned long long ts[10];
+    HIPCHK(hipMemcpyAsync(ts, e->d_tstat, sizeof ts, hipMemcpyDeviceToHost, e->stream));
     HIPCHK(hipStreamSynchronize(e->stream));
+    const unsigned long long distinct = ts[0];
+    res->windows = acc[ACC_WIN];
+    /* every window's last base is a base counted by the reference; a run's
+       first window also counts its first k-1 bases (:1035-1057) */
     for (int b = 0; b < 4; b++) {
-        res->base_count[b] = acc[ACC_BASE + b];
-        res->depth1[b] = acc[ACC_D1W + b] + acc[ACC_D1S + b];
+        res->base_count[b] = ts[2 + b] + acc[ACC_BASE + b];
+        res->depth1[b] = ts[6 + b] + acc[ACC_D1S + b];
         if (res->depth1[b] >= (1ull << 32)) res->rollover = 1;
     }
-    res->valid_bases = acc[ACC_VALID];
-    res->windows = acc[ACC_WIN];
+    /* a bin that wrapped past 2^32 loses 2^32 from the table total: some
+       trie counter reached 2^32 -> the reference's rollover exit (:642) */
+    if (ts[1] != res->windows) res->rollover = 1;
+    res->valid_bases = res->windows + acc[ACC_VALID];
     res->distinct = distinct;
     res->unknown_chars = e->unknown;
     res->scanned_bytes = e->ended ? e->scanned : e->fed;
@@ -1292,6 +1524,15 @@ extern "C" int fk_engine_table(fk_engine *e, uint32_t *counts) {
     int rc = set_dev(e);
     if (rc) return rc;
     HIPCHK(hipMemcpyAsync(counts, e->d_table, e->nbins * sizeof(uint32_t), hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    return FK_OK;
+}
+
+extern "C" int fk_engine_table_range(fk_engine *e, uint64_t first, uint64_t n, uint32_t *counts) {
+    if (!e || (!counts && n) || first > e->nbins || n > e->nbins - first) return FK_E_INVALID;
+    int rc = set_dev(e);
+    if (rc) return rc;
+    if (n) HIPCHK(hipMemcpyAsync(counts, e->d_table + first, n * sizeof(uint32_t), hipMemcpyDeviceToHost, e->stream));
     HIPCHK(hipStreamSynchronize(e->stream));
     return FK_OK;
 }

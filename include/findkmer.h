@@ -139,6 +139,8 @@ int  fk_engine_finish(fk_engine *e, fk_result *res);
  * pointer (valid until reset/destroy). */
 int  fk_engine_table(fk_engine *e, uint32_t *counts);
 int  fk_engine_table_device(fk_engine *e, uint32_t **dev_counts);
+/* Copy bins [first, first+n) to host (stream a large-k table in pieces). */
+int  fk_engine_table_range(fk_engine *e, uint64_t first, uint64_t n, uint32_t *counts);
 /* Copy the table into a caller-owned device buffer (4^k uint32), e.g. a
  * torch tensor handed to an RCCL collective; and load it back. */
 int  fk_engine_table_to_device(fk_engine *e, void *dst);

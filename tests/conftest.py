@@ -12,6 +12,15 @@ sys.path.insert(0, os.path.join(REPO, "tests"))
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (run via gpurun)")
+    # torch bundles its own HIP runtime: it must initialise before
+    # libfindkmer_hip.so does (see findkmer_amd.lib()).  Only when a GPU run
+    # is requested: the CPU suite never touches HIP.
+    if "not gpu" not in (config.getoption("-m") or ""):
+        try:
+            import torch
+            torch.cuda.is_available()
+        except Exception:
+            pass
 
 
 @pytest.fixture(scope="session")

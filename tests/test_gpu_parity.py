@@ -178,14 +178,6 @@ def test_edge_sizes(k):
         assert_same(data, k)
 
 
-def _read_u32(dev_ptr, idx):
-    import ctypes
-    hip = ctypes.CDLL("libamdhip64.so")
-    out = ctypes.c_uint32()
-    assert hip.hipMemcpy(ctypes.byref(out), ctypes.c_void_p(dev_ptr + 4 * int(idx)), ctypes.c_size_t(4), 2) == 0
-    return out.value
-
-
 def test_k16_dense_table():
     """k=16: 4^16 u32 bins (16 GiB) in HBM; sampled bins vs the sparse oracle."""
     data = mixed_input(9, 800_000)
@@ -193,15 +185,17 @@ def test_k16_dense_table():
     with fk.Engine(16) as e:
         e.feed(np.frombuffer(data, dtype=np.uint8).copy())
         rc, rg = e.finish(allow=(fk.FK_OK, fk.FK_E_UNTERMINATED_HEADER))
-        ptr = e.table_device_ptr()
-        rng = np.random.default_rng(0)
-        for i in rng.choice(len(codes), size=min(300, len(codes)), replace=False):
-            assert _read_u32(ptr, codes[i]) == cnts[i]
-        for c in rng.integers(0, 1 << 32, size=50):
-            if c not in set(codes[:0]):
-                j = np.searchsorted(codes, c)
-                want = cnts[j] if j < len(codes) and codes[j] == c else 0
-                assert _read_u32(ptr, c) == want
+        # stream the 16 GiB table through host in 256 Mi-bin pieces
+        step = 1 << 28
+        seen = 0
+        for first in range(0, 1 << 32, step):
+            part = e.table_range(first, step)
+            nz = np.nonzero(part)[0]
+            sel = (codes >= first) & (codes < first + step)
+            assert np.array_equal(nz.astype(np.uint64) + first, codes[sel])
+            assert np.array_equal(part[nz], cnts[sel])
+            seen += len(nz)
+        assert seen == len(codes)
     assert rg.windows == r.windows and rg.distinct == r.distinct
     assert list(rg.base_count) == list(r.base_count)
 
@@ -295,6 +289,7 @@ def test_cli_matches_reference(case, manifest, tmp_path):
         assert hashlib.sha256(got).hexdigest() == rec["sha256"], (kind, got[:300])
     # stdout identical (the reference's own stdout ends where it crashes)
     assert p.stdout == golden_file(case, "stdout")
-    gerr = golden_file(case, "stderr")
-    gerr = gerr.replace(b"free(): invalid pointer\n", b"")
+    # the reference dies in free() (findKmer.cpp:1370): drop glibc's abort line
+    import re
+    gerr = re.sub(rb"(?m)^[a-z_]+\(\): invalid pointer\n", b"", golden_file(case, "stderr"))
     assert p.stderr == gerr
