@@ -30,6 +30,7 @@ enum {
     ACC_WIN = 5,         /* TotalNumSequencesN */
     ACC_D1S = 10,        /* 4: depth-1 trie freq from short (<k) walks (the
                             window part is the table's first-base marginal) */
+    ACC_UNK = 14,        /* "Unknown character" bytes */
     ACC_N = 16
 };
 
@@ -164,6 +165,25 @@ __host__ __device__ inline TF fk_tf_of(const ChunkRec &r) {
     }
     return t;
 }
+
+/* A wave's contiguous run of chunks [c0, c1): the composed transfer function
+ * and the state guessed for its first chunk (the others continue from the
+ * previous chunk's exit). */
+struct RangeRec {
+    TF tf;
+    uint64_t a_code;
+    uint32_t a_R, a_hdr;
+    uint64_t c0, c1;
+};
+
+/* Per-feed results, fetched with one device-to-host copy. */
+struct DevRes {
+    unsigned long long tstat[10];   /* k_table_stats: distinct, sum, last[4], first[4] */
+    XState exit;                    /* stream state after the feed */
+    unsigned long long eof_cand;    /* smallest 0xFF offset seen (a candidate) */
+    uint32_t redo_n;                /* ranges re-counted */
+    uint32_t pad;
+};
 
 /* Would counting a chunk from state a and from state t give identical
  * contributions?  nvb bounds the bases in the chunk. */

@@ -4,21 +4,27 @@
  * Replaces the reference hot path findKmer() (findKmer/src/findKmer.cpp:962-1069)
  * and its trie (:107-111, :612-690) with three HIP kernels per input segment:
  *
- *   k_count  one wave per 64 KiB chunk (grid-stride, 8 waves per 512-thread
- *            block).  16 B per lane per 1 KiB tile, coalesced.  The chunk's
- *            entering scan state is guessed from the 256 bytes before it; the
- *            wave derives each lane's state with a 64-lane scan of per-lane
- *            run summaries, then every lane walks its 16 bytes and adds each
- *            counted window to the table: LDS-privatised u32 bins for k <= 7
- *            (flushed once per block), global u32 atomics otherwise.  It
- *            records the chunk's transfer function and the guessed state.
- *   k_scan   one workgroup composes the chunk transfer functions (parallel
- *            prefix) into the exact entering state of every chunk (64-bit run
- *            length, so the reference's int32 seqSize wrap is exact) and lists
- *            the chunks whose guess would count differently.
- *   k_redo   re-counts only the listed chunks: once with weight -1 from the
- *            guessed state (cancels k_count's contribution exactly), once with
- *            weight +1 from the true state.  Normally the list is empty.
+ *   k_count  each wave owns a contiguous range of 64 KiB chunks (8 waves per
+ *            512-thread block, ~one range per wave slot of the chip).  16 B
+ *            per lane per 1 KiB tile, coalesced, 4 tiles prefetched.  The
+ *            range's entering scan state is guessed from the 256 bytes before
+ *            it.  Fast tiles (only A/C/G/T and at most one '\n' per lane, deep
+ *            in a run) pack each lane's bases into one 32-bit word with
+ *            v_dot4_u32_u8 and cut windows out of {previous lane, own} with
+ *            v_alignbit; other tiles take a general path (64-lane scan of
+ *            per-lane run summaries, then a byte walk).  Windows go to LDS
+ *            bins for k <= 7 ((k+1)-mers at every other base for k <= 6,
+ *            marginalised at the flush) and to global u32 atomics otherwise.
+ *            Each chunk records its transfer function; each range the
+ *            composition.
+ *   k_scan   one workgroup scans the range transfer functions into the exact
+ *            entering state of every range (64-bit run length, so the
+ *            reference's int32 seqSize wrap is exact) and lists the ranges
+ *            whose guess would count differently.
+ *   k_redo   walks only the listed ranges chunk by chunk: a chunk whose guess
+ *            is not equivalent is counted again with weight -1 from the guess
+ *            (cancelling k_count's contribution exactly) and +1 from the true
+ *            state.  Normally the list is empty.
  *
  * Counting rules per valid base (seq = (int32)R after the increment):
  *   seq >  k : window, baseCounter++, base[new]++            (:1035-1042)
@@ -46,6 +52,13 @@
 
 __device__ __forceinline__ uint32_t fk_byte(const uint32_t w[4], int j) {
     return (w[j >> 2] >> (8 * (j & 3))) & 0xFFu;
+}
+
+/* byte j (runtime) of a 16-byte lane without indexing the register array */
+__device__ __forceinline__ uint32_t fk_byte_rt(const uint32_t w[4], uint32_t j) {
+    uint32_t d = j >> 2;
+    uint32_t v = d == 0 ? w[0] : d == 1 ? w[1] : d == 2 ? w[2] : w[3];
+    return (v >> (8 * (j & 3))) & 0xFFu;
 }
 
 /* A=0 C=1 G=2 T=3 (base2int :567-589), -1 otherwise */
@@ -103,6 +116,7 @@ struct Ctx {            /* kernel-wide constants */
     uint32_t *lds;      /* LDS bins or nullptr */
     uint32_t *shortcnt; /* sum_{d<k} 4^d */
     unsigned long long *acc;
+    DevRes *res;
     uint64_t maskk;
     uint32_t single_off;/* H_PAIRS: offset of the k-mer singles in LDS (4^(k+1)) */
     int k;
@@ -149,7 +163,7 @@ __device__ __forceinline__ int load16(const Ctx &cx, int64_t off, uint32_t w[4])
  * `tile_off` is the tile's byte offset inside its chunk.
  */
 template <bool COUNT, int HM>
-__device__ __attribute__((noinline)) void tile_general(const Ctx &cx, const uint32_t w[4], int nb,
+__device__ __forceinline__ void tile_general(const Ctx &cx, const uint32_t w[4], int nb,
                                              uint32_t tile_off, DState &st, Facts &f,
                                              Counters &cnt, uint32_t weight) {
     const int lane = threadIdx.x & 63;
@@ -157,9 +171,9 @@ __device__ __attribute__((noinline)) void tile_general(const Ctx &cx, const uint
 
     /* -- 1. header flag at each lane start: last '>' vs last '\n' before it */
     uint32_t lastGT = 0, lastNL = 0, firstSp = 0xFFFFu, firstGT = 0;
-#pragma unroll
+#pragma unroll 1
     for (int j = 0; j < 16; j++) {
-        uint32_t c = fk_byte(w, j);
+        uint32_t c = fk_byte_rt(w, (uint32_t)j);
         bool in = j < nb;
         uint32_t pos = (uint32_t)lane * 16u + (uint32_t)j + 1u;
         bool gt = in && c == '>';
@@ -181,10 +195,10 @@ __device__ __attribute__((noinline)) void tile_general(const Ctx &cx, const uint
     /* -- 2. per-lane run summary under hdr0: (reset?, bases since, code) */
     uint32_t hdr = hdr0, rs = 0, nv = 0, hdr_end;
     uint64_t code = 0;
-#pragma unroll
-    for (int j = 0; j < 16; j++) {
-        if (j < nb) {
-            uint32_t c = fk_byte(w, j);
+#pragma unroll 1
+    for (int j = 0; j < nb; j++) {
+        {
+            uint32_t c = fk_byte_rt(w, (uint32_t)j);
             if (hdr) {
                 if (c == '\n') hdr = 0;
             } else if (c == '>') {
@@ -245,10 +259,10 @@ __device__ __attribute__((noinline)) void tile_general(const Ctx &cx, const uint
         uint32_t r_at = 0, lane_reset = 0, lane_reset_after = 0;
         const uint64_t maskk1 = cx.maskk >> 2;
 
-#pragma unroll
-        for (int j = 0; j < 16; j++) {
-            if (j < nb) {
-                uint32_t c = fk_byte(w, j);
+#pragma unroll 1
+        for (int j = 0; j < nb; j++) {
+            {
+                uint32_t c = fk_byte_rt(w, (uint32_t)j);
                 uint32_t pos = (uint32_t)lane * 16u + (uint32_t)j;
                 if (p1_here && pos == p1) r_at = R;
                 if (hdr) {
@@ -438,15 +452,17 @@ __device__ __forceinline__ void acc_add(unsigned long long *a, uint64_t v, uint3
 
 __device__ void flush_counters(const Ctx &cx, Counters &cnt, uint32_t weight) {
     const int lane = threadIdx.x & 63;
-    uint32_t vals[10];
+    uint32_t vals[11];
+#pragma unroll
     for (int b = 0; b < 4; b++) {
         vals[b] = (uint32_t)((cnt.base >> (16 * b)) & 0xFFFF);
         vals[6 + b] = (uint32_t)((cnt.d1s >> (16 * b)) & 0xFFFF);
     }
     vals[4] = cnt.valid;
     vals[5] = cnt.win;
+    vals[10] = cnt.unknown;
 #pragma unroll
-    for (int i = 0; i < 10; i++) vals[i] = wsum32(vals[i]);
+    for (int i = 0; i < 11; i++) vals[i] = wsum32(vals[i]);
     if (lane == 0) {
 #pragma unroll
         for (int i = 0; i < 4; i++) acc_add(&cx.acc[ACC_BASE + i], vals[i], weight);
@@ -454,6 +470,7 @@ __device__ void flush_counters(const Ctx &cx, Counters &cnt, uint32_t weight) {
         acc_add(&cx.acc[ACC_WIN], vals[5], weight);
 #pragma unroll
         for (int i = 0; i < 4; i++) acc_add(&cx.acc[ACC_D1S + i], vals[6 + i], weight);
+        acc_add(&cx.acc[ACC_UNK], vals[10], weight);
     }
     cnt.base = cnt.d1s = 0;
     cnt.valid = cnt.win = 0;
@@ -517,6 +534,8 @@ __device__ DState count_chunk(const Ctx &cx, uint64_t chunk, DState st, uint32_t
     flush_counters(cx, cnt, weight);
     uint32_t unk = wsum32(cnt.unknown);
     uint32_t eof = wmin32(cnt.eof);
+    if (lane == 0 && eof != FK_NO_EOF && weight == 1u)
+        atomicMin(&cx.res->eof_cand, (unsigned long long)(chunk * FK_CHUNK_BYTES + eof));
     if (lane == 0) {
         ChunkRec &r = rec[chunk];
         if (write_facts) {
@@ -586,21 +605,23 @@ __device__ void lds_flush(const Ctx &cx) {
  * k_count: main pass.  Wave w counts the contiguous chunk range
  * [w*cpw, (w+1)*cpw): the first chunk of the range guesses its entering state
  * from its halo (or takes the known stream state *d_init for chunk 0), the
- * next ones continue from the previous chunk's exit.
+ * next ones continue from the previous chunk's exit.  At the end lane 0
+ * composes the range's chunk transfer functions into rr[w].
  */
 template <int HM>
 __global__ void __launch_bounds__(FK_BLOCK, 4)
 k_count(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint32_t *table,
-        uint32_t *shortcnt, unsigned long long *acc, ChunkRec *rec, uint64_t nchunks,
-        const XState *d_init, int has_init, uint64_t cpw) {
+        uint32_t *shortcnt, unsigned long long *acc, DevRes *res, ChunkRec *rec, RangeRec *rr,
+        uint64_t nchunks, const XState *d_init, int has_init, uint64_t cpw) {
     extern __shared__ uint32_t lds_bins[];
     const uint32_t nw = lds_words(HM, k);
     if (HM != H_GLOBAL) lds_zero(lds_bins, nw);
-    Ctx cx{buf, len, lo, table, HM != H_GLOBAL ? lds_bins : nullptr, shortcnt, acc, maskk,
+    Ctx cx{buf, len, lo, table, HM != H_GLOBAL ? lds_bins : nullptr, shortcnt, acc, res, maskk,
            1u << (2 * k + 2), k};
     const uint64_t wave = blockIdx.x * FK_WAVES_PER_BLOCK + (threadIdx.x >> 6);
     const uint64_t c0 = wave * cpw, c1 = min(c0 + cpw, nchunks);
     DState st{0, 0, 0};
+    DState first{0, 0, 0};
     for (uint64_t c = c0; c < c1; c++) {
         if (c == c0) {
             if (c == 0 && has_init) {
@@ -610,66 +631,82 @@ k_count(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uin
             } else {
                 st = halo_state<HM>(cx, c);
             }
+            first = st;
         }
         st = count_chunk<HM>(cx, c, st, 1u, rec, true, true);
     }
     if (HM != H_GLOBAL) lds_flush<HM>(cx);
+    if (c0 < c1 && (threadIdx.x & 63) == 0) {
+        TF t = fk_identity();
+        for (uint64_t c = c0; c < c1; c++) t = fk_compose(t, fk_tf_of(rec[c]));
+        RangeRec &r = rr[wave];
+        r.tf = t;
+        r.a_code = first.code; r.a_R = first.R; r.a_hdr = first.hdr;
+        r.c0 = c0; r.c1 = c1;
+    }
 }
 
 /*
- * k_redo: for each listed chunk, cancel the main pass's contribution (weight
- * -1 from the guessed state recorded in rec) and count it again from the
- * exact state.  mode 1 = "cancel all from s_true" (used when a 0xFF byte
- * truncates the segment and everything must be undone).
+ * k_redo, mode 0: for each listed range, walk its chunks from the exact
+ * entering state; a chunk whose guessed entering state (rec[c].a) would count
+ * differently is cancelled (weight -1 from the guess) and recounted (weight
+ * +1 from the exact state).  mode 1: cancel every chunk of every range (a
+ * 0xFF byte truncates the input and the segment is recounted).
  */
 template <int HM>
-__global__ void __launch_bounds__(FK_BLOCK)
+__global__ void __launch_bounds__(FK_BLOCK, 4)
 k_redo(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint32_t *table,
-       uint32_t *shortcnt, unsigned long long *acc, ChunkRec *rec, const XState *s_true,
-       const uint32_t *list, const uint32_t *list_n, uint64_t nchunks, int mode) {
+       uint32_t *shortcnt, unsigned long long *acc, DevRes *res, ChunkRec *rec, const RangeRec *rr,
+       const XState *rtrue, const uint32_t *list, uint64_t nranges, int mode) {
     extern __shared__ uint32_t lds_bins[];
-    const uint64_t n = mode == 1 ? nchunks : (uint64_t)*list_n;
+    const uint64_t n = mode == 1 ? nranges : (uint64_t)res->redo_n;
     if (n == 0) return;   /* uniform across the grid */
     const uint32_t nw = lds_words(HM, k);
     if (HM != H_GLOBAL) lds_zero(lds_bins, nw);
-    Ctx cx{buf, len, lo, table, HM != H_GLOBAL ? lds_bins : nullptr, shortcnt, acc, maskk,
+    Ctx cx{buf, len, lo, table, HM != H_GLOBAL ? lds_bins : nullptr, shortcnt, acc, res, maskk,
            1u << (2 * k + 2), k};
     const uint64_t wave = blockIdx.x * FK_WAVES_PER_BLOCK + (threadIdx.x >> 6);
     const uint64_t nwaves = (uint64_t)gridDim.x * FK_WAVES_PER_BLOCK;
     for (uint64_t i = wave; i < n; i += nwaves) {
-        uint64_t c = mode == 1 ? i : list[i];
-        const XState t = s_true[c];
-        DState ts{t.code, (uint32_t)t.R, t.hdr};
-        if (mode == 1) {
-            count_chunk<HM>(cx, c, ts, 0xFFFFFFFFu, rec, false, false);
-        } else {
-            const ChunkRec r = rec[c];
-            DState as{r.a_code, r.a_R, r.a_hdr};
-            count_chunk<HM>(cx, c, as, 0xFFFFFFFFu, rec, false, false);
-            count_chunk<HM>(cx, c, ts, 1u, rec, false, true);
+        const uint64_t r = mode == 1 ? i : list[i];
+        XState t = rtrue[r];
+        const uint64_t c0 = rr[r].c0, c1 = rr[r].c1;
+        for (uint64_t c = c0; c < c1; c++) {
+            const ChunkRec cr = rec[c];
+            DState ts{t.code, (uint32_t)t.R, t.hdr};
+            if (mode == 1) {
+                count_chunk<HM>(cx, c, ts, 0xFFFFFFFFu, rec, false, false);
+            } else {
+                DState as{cr.a_code, cr.a_R, cr.a_hdr};
+                if (!fk_equiv(as, t, k, FK_CHUNK_BYTES)) {
+                    count_chunk<HM>(cx, c, as, 0xFFFFFFFFu, rec, false, false);
+                    count_chunk<HM>(cx, c, ts, 1u, rec, false, true);
+                }
+            }
+            t = fk_apply(fk_tf_of(cr), t);
         }
     }
     if (HM != H_GLOBAL) lds_flush<HM>(cx);
 }
 
 /*
- * k_scan: exact entering state of every chunk.  One 1024-thread workgroup:
- * each thread composes a contiguous run of chunk transfer functions, a
- * Hillis-Steele scan over the 1024 aggregates in LDS, then each thread
- * replays its run from its exact entering state.  mode 0 = resolve from
- * *d_state (and write the exit back there); mode 1 = only reduce the total
- * transfer function into *tf_total (shard summary).
+ * k_scan: exact entering state of every range.  One 1024-thread workgroup
+ * scans the range transfer functions (a few per thread, then a Hillis-Steele
+ * scan of the 1024 aggregates in LDS).  mode 0: resolve from *d_state, list
+ * the ranges whose guess is not equivalent, write the exit state back to
+ * *d_state and res->exit.  mode 1: only the total transfer function (shard
+ * summary) into *tf_total.
  */
 #define SCAN_THREADS 1024
 __global__ void __launch_bounds__(SCAN_THREADS)
-k_scan(const ChunkRec *rec, uint64_t n, XState *d_state, XState *s_true, uint32_t *redo_list,
-       uint32_t *redo_n, int k, int mode, TF *tf_total) {
+k_scan(const RangeRec *rr, uint64_t n, XState *d_state, XState *rtrue, uint32_t *redo_list,
+       DevRes *res, int k, int mode, TF *tf_total) {
     __shared__ TF agg[SCAN_THREADS];
     const uint32_t t = threadIdx.x;
     const uint64_t per = (n + SCAN_THREADS - 1) / SCAN_THREADS;
     const uint64_t lo = min((uint64_t)t * per, n), hi = min(lo + per, n);
     TF a = fk_identity();
-    for (uint64_t c = lo; c < hi; c++) a = fk_compose(a, fk_tf_of(rec[c]));
+    for (uint64_t r = lo; r < hi; r++) a = fk_compose(a, rr[r].tf);
     agg[t] = a;
     __syncthreads();
     for (uint32_t d = 1; d < SCAN_THREADS; d <<= 1) {
@@ -686,32 +723,33 @@ k_scan(const ChunkRec *rec, uint64_t n, XState *d_state, XState *s_true, uint32_
     const XState init = *d_state;
     __syncthreads();
     XState s = t == 0 ? init : fk_apply(agg[t - 1], init);
-    for (uint64_t c = lo; c < hi; c++) {
-        const ChunkRec r = rec[c];
-        s_true[c] = s;
-        DState as{r.a_code, r.a_R, r.a_hdr};
-        if (!fk_equiv(as, s, k, FK_CHUNK_BYTES)) {
-            uint32_t slot = atomicAdd(redo_n, 1u);
-            redo_list[slot] = (uint32_t)c;
+    for (uint64_t r = lo; r < hi; r++) {
+        const RangeRec q = rr[r];
+        rtrue[r] = s;
+        DState as{q.a_code, q.a_R, q.a_hdr};
+        if (!fk_equiv(as, s, k, (q.c1 - q.c0) * FK_CHUNK_BYTES)) {
+            uint32_t slot = atomicAdd(&res->redo_n, 1u);
+            redo_list[slot] = (uint32_t)r;
         }
-        s = fk_apply(fk_tf_of(r), s);
+        s = fk_apply(q.tf, s);
     }
     if (t == SCAN_THREADS - 1) {
         XState fin = fk_apply(agg[SCAN_THREADS - 1], init);
-        s_true[n] = fin;
         *d_state = fin;
+        res->exit = fin;
     }
 }
 
-/* Reduce per-chunk observations: first 0xFF byte (absolute) and unknown count. */
-__global__ void k_obs(const ChunkRec *rec, uint64_t n, unsigned long long *out /*[2]*/) {
-    unsigned long long unk = 0, eof = ~0ull;
-    for (uint64_t c = blockIdx.x * blockDim.x + threadIdx.x; c < n; c += (uint64_t)gridDim.x * blockDim.x) {
-        unk += rec[c].unknown;
-        if (rec[c].eof_off != FK_NO_EOF) eof = min(eof, (unsigned long long)(c * FK_CHUNK_BYTES + rec[c].eof_off));
+/* exact entering state of every chunk (for the unknown-byte extraction) */
+__global__ void k_expand(const ChunkRec *rec, const RangeRec *rr, const XState *rtrue, uint64_t nranges,
+                         XState *strue) {
+    uint64_t r = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (r >= nranges) return;
+    XState t = rtrue[r];
+    for (uint64_t c = rr[r].c0; c < rr[r].c1; c++) {
+        strue[c] = t;
+        t = fk_apply(fk_tf_of(rec[c]), t);
     }
-    if (unk) atomicAdd(&out[0], unk);
-    if (eof != ~0ull) atomicMin(&out[1], eof);
 }
 
 /* One pass over the final table: distinct k-mers, total, and the first- and
@@ -812,7 +850,7 @@ __global__ void __launch_bounds__(FK_BLOCK)
 k_extract(const uint8_t *buf, uint64_t len, int64_t lo, const XState *s_true, const uint32_t *list,
           const uint64_t *offs, uint32_t nlist, uint8_t *out) {
     const int lane = threadIdx.x & 63;
-    Ctx cx{buf, len, lo, nullptr, nullptr, nullptr, nullptr, 0, 0};
+    Ctx cx{buf, len, lo, nullptr, nullptr, nullptr, nullptr, nullptr, 0, 0, 0};
     const uint64_t wave = blockIdx.x * FK_WAVES_PER_BLOCK + (threadIdx.x >> 6);
     const uint64_t nwaves = (uint64_t)gridDim.x * FK_WAVES_PER_BLOCK;
     for (uint64_t i = wave; i < nlist; i += nwaves) {
@@ -920,6 +958,7 @@ __global__ void k_synth(uint8_t *out, uint64_t total, uint64_t seed, int fasta_l
 
 static const uint64_t SEG_MAX_BYTES = 1ull << 34;                 /* 16 GiB per segment */
 static const uint64_t STAGE_BYTES = 256ull << 20;                 /* host feed staging */
+static const unsigned long long NO_EOF64 = ~0ull;
 
 struct fk_engine {
     int dev = 0, k = 0;
@@ -927,29 +966,34 @@ struct fk_engine {
     bool own_stream = false;
     fk_opts opts{};
     uint64_t nbins = 0, nshort = 0, maskk = 0;
-    uint32_t *d_table = nullptr, *d_short = nullptr;
-    unsigned long long *d_acc = nullptr;   /* ACC_N slots */
-    unsigned long long *d_obs = nullptr;   /* [0] unknown, [1] eof, [2] spare, [3] level count */
-    unsigned long long *d_tstat = nullptr; /* k_table_stats output */
-    ChunkRec *d_rec = nullptr;
-    XState *d_strue = nullptr, *d_state = nullptr;
-    uint32_t *d_redo = nullptr, *d_redo_n = nullptr;
-    TF *d_tf = nullptr;
-    uint8_t *d_stage[2] = {nullptr, nullptr};
-    uint8_t *h_stage[2] = {nullptr, nullptr};
-    hipEvent_t ev[4] = {};
     int cus = 256;
-    /* host-side bookkeeping */
+    /* device state */
+    uint32_t *d_table = nullptr, *d_short = nullptr;
+    unsigned long long *d_acc = nullptr;      /* ACC_N, engine lifetime */
+    DevRes *d_res = nullptr;                  /* per feed */
+    unsigned long long *d_tmp = nullptr;      /* scratch counters */
+    XState *d_state = nullptr;                /* entering state of the next feed */
+    ChunkRec *d_rec = nullptr;
+    RangeRec *d_rr = nullptr;
+    XState *d_rtrue = nullptr, *d_strue = nullptr;
+    uint32_t *d_redo = nullptr;
+    TF *d_tf = nullptr;
+    uint64_t chunk_cap = 0, range_cap = 0;
+    uint8_t *d_stage = nullptr, *h_stage = nullptr;
+    hipEvent_t ev[3] = {};
+    /* host bookkeeping */
     XState state{0, 0, 0, 0};
-    uint64_t fed = 0, scanned = 0, unknown = 0, chunks = 0, redo = 0;
-    int ended = 0;         /* a 0xFF byte ended the input */
-    int shard_pending = 0; /* feed_shard done, resolve pending */
-    uint64_t shard_len = 0;
+    DevRes last{};                            /* last feed's results */
+    bool stats_valid = false;                 /* last.tstat describes the table */
+    bool tail_added = false;                  /* end-of-input short run recorded */
+    uint64_t fed = 0, scanned = 0, chunks = 0, redo = 0;
+    int ended = 0;                            /* a 0xFF byte ended the input */
+    int shard_pending = 0;
     const uint8_t *shard_buf = nullptr;
+    uint64_t shard_len = 0;
     int64_t shard_lo = 0;
     double dev_ms = 0, main_ms = 0;
     std::vector<uint8_t> unknown_bytes;
-    uint64_t chunk_cap = 0;
 };
 
 static int set_dev(fk_engine *e) {
@@ -983,15 +1027,29 @@ extern "C" int fk_device_count(void) {
     return n;
 }
 
+static int hist_mode(const fk_engine *e) { return e->k <= 6 ? H_PAIRS : e->k == 7 ? H_LDS : H_GLOBAL; }
+
+/* 128 VGPRs -> 4 waves/SIMD = two 512-thread blocks per CU */
+static uint64_t blocks_per_cu(const fk_engine *) { return 2; }
+
+static size_t lds_bytes(const fk_engine *e) {
+    int m = hist_mode(e);
+    if (m == H_PAIRS) return ((size_t)e->nbins * 4 + e->nbins) * sizeof(uint32_t);
+    if (m == H_LDS) return (size_t)e->nbins * sizeof(uint32_t);
+    return 0;
+}
+
+/* Zero table, counters and the stream state (asynchronous, stream-ordered). */
 static int zero_all(fk_engine *e) {
     HIPCHK(hipMemsetAsync(e->d_table, 0, e->nbins * sizeof(uint32_t), e->stream));
     if (e->nshort) HIPCHK(hipMemsetAsync(e->d_short, 0, e->nshort * sizeof(uint32_t), e->stream));
     HIPCHK(hipMemsetAsync(e->d_acc, 0, ACC_N * sizeof(unsigned long long), e->stream));
-    XState z{0, 0, 0, 0};
-    HIPCHK(hipMemcpyAsync(e->d_state, &z, sizeof z, hipMemcpyHostToDevice, e->stream));
-    HIPCHK(hipStreamSynchronize(e->stream));
-    e->state = z;
-    e->fed = e->scanned = e->unknown = e->chunks = e->redo = 0;
+    HIPCHK(hipMemsetAsync(e->d_state, 0, sizeof(XState), e->stream));
+    e->state = XState{0, 0, 0, 0};
+    memset(&e->last, 0, sizeof e->last);
+    e->stats_valid = false;
+    e->tail_added = false;
+    e->fed = e->scanned = e->chunks = e->redo = 0;
     e->ended = 0;
     e->shard_pending = 0;
     e->dev_ms = e->main_ms = 0;
@@ -1003,11 +1061,11 @@ extern "C" void fk_engine_destroy(fk_engine *e) {
     if (!e) return;
     hipSetDevice(e->dev);
     if (e->stream) hipStreamSynchronize(e->stream);
-    hipFree(e->d_table); hipFree(e->d_short); hipFree(e->d_acc); hipFree(e->d_obs); hipFree(e->d_tstat);
-    hipFree(e->d_rec); hipFree(e->d_strue); hipFree(e->d_state); hipFree(e->d_redo);
-    hipFree(e->d_redo_n); hipFree(e->d_tf);
-    for (int i = 0; i < 2; i++) { hipFree(e->d_stage[i]); hipHostFree(e->h_stage[i]); }
-    for (int i = 0; i < 4; i++) if (e->ev[i]) hipEventDestroy(e->ev[i]);
+    hipFree(e->d_table); hipFree(e->d_short); hipFree(e->d_acc); hipFree(e->d_res); hipFree(e->d_tmp);
+    hipFree(e->d_state); hipFree(e->d_rec); hipFree(e->d_rr); hipFree(e->d_rtrue); hipFree(e->d_strue);
+    hipFree(e->d_redo); hipFree(e->d_tf); hipFree(e->d_stage);
+    if (e->h_stage) hipHostFree(e->h_stage);
+    for (int i = 0; i < 3; i++) if (e->ev[i]) hipEventDestroy(e->ev[i]);
     if (e->own_stream && e->stream) hipStreamDestroy(e->stream);
     delete e;
 }
@@ -1031,10 +1089,11 @@ extern "C" int fk_engine_create(int k, const fk_opts *opts, fk_engine **out) {
     if (hipGetDeviceProperties(&prop, e->dev) == hipSuccess && prop.multiProcessorCount > 0)
         e->cus = prop.multiProcessorCount;
     e->nbins = 1ull << (2 * k);
-    e->maskk = (k >= 32) ? ~0ull : (e->nbins - 1);
+    e->maskk = e->nbins - 1;
     e->nshort = k > 1 ? ((1ull << (2 * k)) - 4) / 3 : 0;
-    if (e->opts.stream) { e->stream = (hipStream_t)e->opts.stream; }
-    else {
+    if (e->opts.stream) {
+        e->stream = (hipStream_t)e->opts.stream;
+    } else {
         if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) { delete e; return FK_E_HIP; }
         e->own_stream = true;
     }
@@ -1043,15 +1102,21 @@ extern "C" int fk_engine_create(int k, const fk_opts *opts, fk_engine **out) {
     ALLOC(e->d_table, e->nbins * sizeof(uint32_t));
     if (e->nshort) { ALLOC(e->d_short, e->nshort * sizeof(uint32_t)); }
     ALLOC(e->d_acc, ACC_N * sizeof(unsigned long long));
-    ALLOC(e->d_obs, 8 * sizeof(unsigned long long));
-    ALLOC(e->d_tstat, 10 * sizeof(unsigned long long));
+    ALLOC(e->d_res, sizeof(DevRes));
+    ALLOC(e->d_tmp, 8 * sizeof(unsigned long long));
     ALLOC(e->d_state, sizeof(XState));
-    ALLOC(e->d_redo_n, sizeof(uint32_t));
     ALLOC(e->d_tf, sizeof(TF));
 #undef ALLOC
-    for (int i = 0; i < 4; i++)
+    /* the LDS bins need more than the default dynamic-LDS limit */
+    size_t sh = lds_bytes(e);
+    if (sh > 65536) {
+        hipFuncSetAttribute((const void *)k_count<H_PAIRS>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh);
+        hipFuncSetAttribute((const void *)k_redo<H_PAIRS>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh);
+    }
+    for (int i = 0; i < 3; i++)
         if (hipEventCreate(&e->ev[i]) != hipSuccess) { fk_engine_destroy(e); return FK_E_HIP; }
     rc = zero_all(e);
+    if (rc == FK_OK && hipStreamSynchronize(e->stream) != hipSuccess) rc = FK_E_HIP;
     if (rc) { fk_engine_destroy(e); return rc; }
     *out = e;
     return FK_OK;
@@ -1064,33 +1129,40 @@ extern "C" int fk_engine_reset(fk_engine *e) {
     return zero_all(e);
 }
 
-static int grow_chunk_arrays(fk_engine *e, uint64_t nchunks, uint64_t &cap) {
-    if (nchunks <= cap && e->d_rec) return FK_OK;
-    uint64_t nc = std::max<uint64_t>(nchunks, 1024);
-    hipFree(e->d_rec); hipFree(e->d_strue); hipFree(e->d_redo);
-    e->d_rec = nullptr; e->d_strue = nullptr; e->d_redo = nullptr;
-    if (hipMalloc((void **)&e->d_rec, nc * sizeof(ChunkRec)) != hipSuccess) return FK_E_OOM;
-    if (hipMalloc((void **)&e->d_strue, (nc + 1) * sizeof(XState)) != hipSuccess) return FK_E_OOM;
-    if (hipMalloc((void **)&e->d_redo, nc * sizeof(uint32_t)) != hipSuccess) return FK_E_OOM;
-    cap = nc;
+/* per-chunk and per-range arrays */
+static int grow_arrays(fk_engine *e, uint64_t nchunks, uint64_t nranges) {
+    if (nchunks > e->chunk_cap || !e->d_rec) {
+        uint64_t nc = std::max<uint64_t>(nchunks, 1024);
+        hipFree(e->d_rec); hipFree(e->d_strue);
+        e->d_rec = nullptr; e->d_strue = nullptr;
+        if (hipMalloc((void **)&e->d_rec, nc * sizeof(ChunkRec)) != hipSuccess) return FK_E_OOM;
+        e->chunk_cap = nc;
+    }
+    if (nranges > e->range_cap || !e->d_rr) {
+        uint64_t nr = std::max<uint64_t>(nranges, 1024);
+        hipFree(e->d_rr); hipFree(e->d_rtrue); hipFree(e->d_redo);
+        e->d_rr = nullptr; e->d_rtrue = nullptr; e->d_redo = nullptr;
+        if (hipMalloc((void **)&e->d_rr, nr * sizeof(RangeRec)) != hipSuccess) return FK_E_OOM;
+        if (hipMalloc((void **)&e->d_rtrue, nr * sizeof(XState)) != hipSuccess) return FK_E_OOM;
+        if (hipMalloc((void **)&e->d_redo, nr * sizeof(uint32_t)) != hipSuccess) return FK_E_OOM;
+        e->range_cap = nr;
+    }
     return FK_OK;
 }
 
-static int hist_mode(const fk_engine *e) { return e->k <= 6 ? H_PAIRS : e->k == 7 ? H_LDS : H_GLOBAL; }
-
-static uint64_t blocks_per_cu(const fk_engine *e) { return hist_mode(e) == H_GLOBAL ? 4 : 2; }
-
-static unsigned grid_for(const fk_engine *e, uint64_t nwork_waves) {
-    uint64_t maxb = (uint64_t)e->cus * blocks_per_cu(e);
-    uint64_t need = (nwork_waves + FK_WAVES_PER_BLOCK - 1) / FK_WAVES_PER_BLOCK;
-    return (unsigned)std::max<uint64_t>(1, std::min(maxb, need));
-}
-
-static size_t lds_bytes(const fk_engine *e) {
-    int m = hist_mode(e);
-    if (m == H_PAIRS) return ((size_t)e->nbins * 4 + e->nbins) * sizeof(uint32_t);
-    if (m == H_LDS) return (size_t)e->nbins * sizeof(uint32_t);
-    return 0;
+/* A segment's decomposition into per-wave chunk ranges. */
+struct Geo {
+    uint64_t nchunks, cpw, nranges;
+    unsigned grid;
+};
+static Geo geometry(const fk_engine *e, uint64_t len) {
+    Geo g;
+    g.nchunks = (len + FK_CHUNK_BYTES - 1) / FK_CHUNK_BYTES;
+    uint64_t max_waves = (uint64_t)e->cus * blocks_per_cu(e) * FK_WAVES_PER_BLOCK;
+    g.cpw = std::max<uint64_t>(1, (g.nchunks + max_waves - 1) / max_waves);
+    g.nranges = (g.nchunks + g.cpw - 1) / g.cpw;
+    g.grid = (unsigned)std::max<uint64_t>(1, (g.nranges + FK_WAVES_PER_BLOCK - 1) / FK_WAVES_PER_BLOCK);
+    return g;
 }
 
 #define FK_DISPATCH(HMV, ...)                                                   \
@@ -1100,78 +1172,101 @@ static size_t lds_bytes(const fk_engine *e) {
     default: { constexpr int HM = H_GLOBAL; __VA_ARGS__; } break;              \
     }
 
-static int launch_count(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t lo, uint64_t nchunks,
+static int launch_count(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t lo, const Geo &g,
                         int has_init) {
-    /* contiguous chunk ranges: enough waves to fill the chip, each taking
-       cpw consecutive chunks (only a range's first chunk needs a halo) */
-    uint64_t max_waves = (uint64_t)e->cus * blocks_per_cu(e) * FK_WAVES_PER_BLOCK;
-    uint64_t cpw = (nchunks + max_waves - 1) / max_waves;
-    uint64_t nwaves = (nchunks + cpw - 1) / cpw;
-    unsigned g = (unsigned)std::max<uint64_t>(1, (nwaves + FK_WAVES_PER_BLOCK - 1) / FK_WAVES_PER_BLOCK);
     size_t sh = lds_bytes(e);
     FK_DISPATCH(hist_mode(e),
-                hipLaunchKernelGGL((k_count<HM>), dim3(g), dim3(FK_BLOCK), sh, e->stream, buf, len, lo, e->k,
-                                   e->maskk, e->d_table, e->d_short, e->d_acc, e->d_rec, nchunks, e->d_state,
-                                   has_init, cpw));
+                hipLaunchKernelGGL((k_count<HM>), dim3(g.grid), dim3(FK_BLOCK), sh, e->stream, buf, len, lo, e->k,
+                                   e->maskk, e->d_table, e->d_short, e->d_acc, e->d_res, e->d_rec, e->d_rr,
+                                   g.nchunks, e->d_state, has_init, g.cpw));
     HIPCHK(hipGetLastError());
     return FK_OK;
 }
 
-static int launch_redo(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t lo, uint64_t nchunks,
-                       int mode) {
-    unsigned g = mode == 1 ? grid_for(e, nchunks) : grid_for(e, std::min<uint64_t>(nchunks, 4096));
+static int launch_redo(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t lo, const Geo &g, int mode) {
     size_t sh = lds_bytes(e);
+    unsigned grid = mode == 1 ? g.grid : (unsigned)std::min<uint64_t>(g.grid, (uint64_t)e->cus);
     FK_DISPATCH(hist_mode(e),
-                hipLaunchKernelGGL((k_redo<HM>), dim3(g), dim3(FK_BLOCK), sh, e->stream, buf, len, lo, e->k,
-                                   e->maskk, e->d_table, e->d_short, e->d_acc, e->d_rec, e->d_strue, e->d_redo,
-                                   e->d_redo_n, nchunks, mode));
+                hipLaunchKernelGGL((k_redo<HM>), dim3(grid), dim3(FK_BLOCK), sh, e->stream, buf, len, lo, e->k,
+                                   e->maskk, e->d_table, e->d_short, e->d_acc, e->d_res, e->d_rec, e->d_rr,
+                                   e->d_rtrue, e->d_redo, g.nranges, mode));
     HIPCHK(hipGetLastError());
     return FK_OK;
 }
 
-static int launch_scan(fk_engine *e, uint64_t nchunks, int mode) {
-    HIPCHK(hipMemsetAsync(e->d_redo_n, 0, sizeof(uint32_t), e->stream));
-    hipLaunchKernelGGL(k_scan, dim3(1), dim3(SCAN_THREADS), 0, e->stream, e->d_rec, nchunks, e->d_state,
-                       e->d_strue, e->d_redo, e->d_redo_n, e->k, mode, e->d_tf);
+static int launch_scan(fk_engine *e, const Geo &g, int mode) {
+    hipLaunchKernelGGL(k_scan, dim3(1), dim3(SCAN_THREADS), 0, e->stream, e->d_rr, g.nranges, e->d_state,
+                       e->d_rtrue, e->d_redo, e->d_res, e->k, mode, e->d_tf);
     HIPCHK(hipGetLastError());
     return FK_OK;
 }
 
-struct SegOut {
-    XState exit;
-    unsigned long long unknown, eof;
-    uint32_t redo_n;
-};
-
-static int read_segment(fk_engine *e, uint64_t nchunks, SegOut &o) {
-    HIPCHK(hipMemsetAsync(e->d_obs, 0, 2 * sizeof(unsigned long long), e->stream));
-    unsigned long long init_eof = ~0ull;
-    HIPCHK(hipMemcpyAsync(e->d_obs + 1, &init_eof, sizeof init_eof, hipMemcpyHostToDevice, e->stream));
-    unsigned g = (unsigned)std::min<uint64_t>(1024, (nchunks + 255) / 256 + 1);
-    hipLaunchKernelGGL(k_obs, dim3(g), dim3(256), 0, e->stream, e->d_rec, nchunks, e->d_obs);
+static int launch_table_stats(fk_engine *e) {
+    HIPCHK(hipMemsetAsync(e->d_res->tstat, 0, sizeof(e->d_res->tstat), e->stream));
+    unsigned gd = (unsigned)std::min<uint64_t>((uint64_t)e->cus * 4, (e->nbins / 4 + 255) / 256 + 1);
+    hipLaunchKernelGGL(k_table_stats, dim3(gd), dim3(256), 0, e->stream, e->d_table, e->nbins, e->k,
+                       e->d_res->tstat);
     HIPCHK(hipGetLastError());
-    unsigned long long obs[2];
-    HIPCHK(hipMemcpyAsync(obs, e->d_obs, sizeof obs, hipMemcpyDeviceToHost, e->stream));
-    HIPCHK(hipMemcpyAsync(&o.exit, e->d_state, sizeof(XState), hipMemcpyDeviceToHost, e->stream));
-    HIPCHK(hipMemcpyAsync(&o.redo_n, e->d_redo_n, sizeof(uint32_t), hipMemcpyDeviceToHost, e->stream));
+    return FK_OK;
+}
+
+/* Reset the per-feed result block (redo count, eof candidate). */
+static int res_begin(fk_engine *e) {
+    HIPCHK(hipMemsetAsync(&e->d_res->redo_n, 0, sizeof(uint32_t), e->stream));
+    HIPCHK(hipMemsetAsync(&e->d_res->eof_cand, 0xFF, sizeof(unsigned long long), e->stream));
+    return FK_OK;
+}
+
+/* scan + redo + table stats, then one device->host copy of the results */
+static int resolve_and_fetch(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t lo, const Geo &g) {
+    int rc = launch_scan(e, g, 0);
+    if (rc) return rc;
+    rc = launch_redo(e, buf, len, lo, g, 0);
+    if (rc) return rc;
+    rc = launch_table_stats(e);
+    if (rc) return rc;
+    HIPCHK(hipEventRecord(e->ev[2], e->stream));
+    HIPCHK(hipMemcpyAsync(&e->last, e->d_res, sizeof(DevRes), hipMemcpyDeviceToHost, e->stream));
     HIPCHK(hipStreamSynchronize(e->stream));
-    o.unknown = obs[0];
-    o.eof = obs[1];
+    e->stats_valid = true;
+    e->redo += e->last.redo_n;
+    return FK_OK;
+}
+
+/* exact first 0xFF outside a header (per-chunk records are exact after redo) */
+__global__ void k_obs_eof(const ChunkRec *rec, uint64_t n, unsigned long long *out) {
+    unsigned long long eof = ~0ull;
+    for (uint64_t c = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; c < n; c += (uint64_t)gridDim.x * blockDim.x)
+        if (rec[c].eof_off != FK_NO_EOF) eof = min(eof, (unsigned long long)(c * FK_CHUNK_BYTES + rec[c].eof_off));
+    if (eof != ~0ull) atomicMin(out, eof);
+}
+
+static int exact_eof(fk_engine *e, const Geo &g, unsigned long long &eof) {
+    HIPCHK(hipMemsetAsync(e->d_tmp, 0xFF, sizeof(unsigned long long), e->stream));
+    unsigned gr = (unsigned)std::min<uint64_t>(1024, g.nchunks / 256 + 1);
+    hipLaunchKernelGGL(k_obs_eof, dim3(gr), dim3(256), 0, e->stream, e->d_rec, g.nchunks, e->d_tmp);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(&eof, e->d_tmp, sizeof eof, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
     return FK_OK;
 }
 
 /* Collect the unknown bytes of the just-counted segment (stream order). */
-static int collect_unknown(fk_engine *e, const uint8_t *dbuf, uint64_t len, int64_t lo, uint64_t nchunks,
-                           uint64_t total) {
-    if (!total || !e->opts.collect_unknown) return FK_OK;
-    std::vector<ChunkRec> rec((size_t)nchunks);
-    HIPCHK(hipMemcpyAsync(rec.data(), e->d_rec, nchunks * sizeof(ChunkRec), hipMemcpyDeviceToHost, e->stream));
+static int collect_unknown(fk_engine *e, const uint8_t *dbuf, uint64_t len, int64_t lo, const Geo &g) {
+    if (!e->opts.collect_unknown) return FK_OK;
+    std::vector<ChunkRec> rec((size_t)g.nchunks);
+    HIPCHK(hipMemcpyAsync(rec.data(), e->d_rec, g.nchunks * sizeof(ChunkRec), hipMemcpyDeviceToHost, e->stream));
     HIPCHK(hipStreamSynchronize(e->stream));
     std::vector<uint32_t> list;
     std::vector<uint64_t> offs;
     uint64_t acc = 0;
-    for (uint64_t c = 0; c < nchunks; c++)
+    for (uint64_t c = 0; c < g.nchunks; c++)
         if (rec[(size_t)c].unknown) { list.push_back((uint32_t)c); offs.push_back(acc); acc += rec[(size_t)c].unknown; }
+    if (!acc) return FK_OK;
+    if (!e->d_strue && hipMalloc((void **)&e->d_strue, e->chunk_cap * sizeof(XState)) != hipSuccess) return FK_E_OOM;
+    hipLaunchKernelGGL(k_expand, dim3((unsigned)((g.nranges + 255) / 256)), dim3(256), 0, e->stream, e->d_rec, e->d_rr,
+                       e->d_rtrue, g.nranges, e->d_strue);
+    HIPCHK(hipGetLastError());
     uint32_t *d_list = nullptr;
     uint64_t *d_offs = nullptr;
     uint8_t *d_out = nullptr;
@@ -1183,8 +1278,8 @@ static int collect_unknown(fk_engine *e, const uint8_t *dbuf, uint64_t len, int6
     }
     HIPCHK(hipMemcpyAsync(d_list, list.data(), list.size() * 4, hipMemcpyHostToDevice, e->stream));
     HIPCHK(hipMemcpyAsync(d_offs, offs.data(), offs.size() * 8, hipMemcpyHostToDevice, e->stream));
-    unsigned g = grid_for(e, list.size());
-    hipLaunchKernelGGL(k_extract, dim3(g), dim3(FK_BLOCK), 0, e->stream, dbuf, len, lo, e->d_strue, d_list, d_offs,
+    unsigned gx = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((list.size() + 7) / 8, (uint64_t)e->cus * 2));
+    hipLaunchKernelGGL(k_extract, dim3(gx), dim3(FK_BLOCK), 0, e->stream, dbuf, len, lo, e->d_strue, d_list, d_offs,
                        (uint32_t)list.size(), d_out);
     HIPCHK(hipGetLastError());
     size_t old = e->unknown_bytes.size();
@@ -1195,64 +1290,78 @@ static int collect_unknown(fk_engine *e, const uint8_t *dbuf, uint64_t len, int6
     return FK_OK;
 }
 
-/* Count one device-resident segment continuing from e->state (exact). */
-static int process_segment(fk_engine *e, const uint8_t *dbuf, uint64_t len, uint64_t &cap) {
-    if (len == 0 || e->ended) return FK_OK;
-    uint64_t nchunks = (len + FK_CHUNK_BYTES - 1) / FK_CHUNK_BYTES;
-    int rc = grow_chunk_arrays(e, nchunks, cap);
+/*
+ * Count one device-resident segment whose entering state is *d_state (exact).
+ * has_init = 0 is the shard case (entering state unknown; resolved later).
+ */
+static int count_segment(fk_engine *e, const uint8_t *dbuf, uint64_t len, int64_t lo, int has_init, Geo &g) {
+    g = geometry(e, len);
+    int rc = grow_arrays(e, g.nchunks, g.nranges);
+    if (rc) return rc;
+    rc = res_begin(e);
     if (rc) return rc;
     HIPCHK(hipEventRecord(e->ev[0], e->stream));
-    rc = launch_count(e, dbuf, len, 0, nchunks, 1);
+    rc = launch_count(e, dbuf, len, lo, g, has_init);
     if (rc) return rc;
     HIPCHK(hipEventRecord(e->ev[1], e->stream));
-    rc = launch_scan(e, nchunks, 0);
-    if (rc) return rc;
-    rc = launch_redo(e, dbuf, len, 0, nchunks, 0);
-    if (rc) return rc;
-    HIPCHK(hipEventRecord(e->ev[2], e->stream));
-    SegOut o;
-    rc = read_segment(e, nchunks, o);
-    if (rc) return rc;
-    float ms_main = 0, ms_all = 0;
-    hipEventElapsedTime(&ms_main, e->ev[0], e->ev[1]);
-    hipEventElapsedTime(&ms_all, e->ev[0], e->ev[2]);
-    e->main_ms += ms_main;
-    e->dev_ms += ms_all;
-    e->chunks += nchunks;
-    e->redo += o.redo_n;
-    if (o.eof != ~0ull) {
-        /* A 0xFF byte outside a header ends the reference's scan (:988):
-           undo this segment and count only the bytes before it. */
-        rc = launch_redo(e, dbuf, len, 0, nchunks, 1);
+    e->chunks += g.nchunks;
+    return FK_OK;
+}
+
+static void add_times(fk_engine *e) {
+    float a = 0, b = 0;
+    if (hipEventElapsedTime(&a, e->ev[0], e->ev[1]) == hipSuccess) e->main_ms += a;
+    if (hipEventElapsedTime(&b, e->ev[0], e->ev[2]) == hipSuccess) e->dev_ms += b;
+}
+
+/* After resolve: handle a 0xFF byte (recount the prefix) and unknown bytes. */
+static int finish_segment(fk_engine *e, const uint8_t *dbuf, uint64_t len, int64_t lo, const Geo &g,
+                          const XState &entering) {
+    add_times(e);
+    if (e->last.eof_cand != NO_EOF64) {
+        unsigned long long eof = NO_EOF64;
+        int rc = exact_eof(e, g, eof);
         if (rc) return rc;
-        XState entering = e->state;
-        HIPCHK(hipMemcpyAsync(e->d_state, &entering, sizeof entering, hipMemcpyHostToDevice, e->stream));
-        uint64_t tl = o.eof;
-        e->ended = 1;
-        e->scanned += tl;
-        if (tl == 0) {
-            HIPCHK(hipStreamSynchronize(e->stream));
-            return FK_OK;
+        if (eof != NO_EOF64) {
+            /* A 0xFF byte outside a header ends the reference's scan (:988):
+               undo this segment and count only the bytes before it. */
+            rc = launch_redo(e, dbuf, len, lo, g, 1);
+            if (rc) return rc;
+            HIPCHK(hipMemcpyAsync(e->d_state, &entering, sizeof entering, hipMemcpyHostToDevice, e->stream));
+            e->ended = 1;
+            e->scanned += eof;
+            if (eof == 0) {
+                rc = launch_table_stats(e);
+                if (rc) return rc;
+                HIPCHK(hipMemcpyAsync(&e->last, e->d_res, sizeof(DevRes), hipMemcpyDeviceToHost, e->stream));
+                HIPCHK(hipStreamSynchronize(e->stream));
+                e->state = entering;
+                return FK_OK;
+            }
+            Geo g2;
+            rc = count_segment(e, dbuf, eof, lo, 1, g2);
+            if (rc) return rc;
+            rc = resolve_and_fetch(e, dbuf, eof, lo, g2);
+            if (rc) return rc;
+            add_times(e);
+            e->state = e->last.exit;
+            return collect_unknown(e, dbuf, eof, lo, g2);
         }
-        uint64_t nc2 = (tl + FK_CHUNK_BYTES - 1) / FK_CHUNK_BYTES;
-        rc = launch_count(e, dbuf, tl, 0, nc2, 1);
-        if (rc) return rc;
-        rc = launch_scan(e, nc2, 0);
-        if (rc) return rc;
-        rc = launch_redo(e, dbuf, tl, 0, nc2, 0);
-        if (rc) return rc;
-        SegOut o2;
-        rc = read_segment(e, nc2, o2);
-        if (rc) return rc;
-        e->state = o2.exit;
-        e->unknown += o2.unknown;
-        e->redo += o2.redo_n;
-        return collect_unknown(e, dbuf, tl, 0, nc2, o2.unknown);
     }
-    e->state = o.exit;
-    e->unknown += o.unknown;
+    e->state = e->last.exit;
     e->scanned += len;
-    return collect_unknown(e, dbuf, len, 0, nchunks, o.unknown);
+    return collect_unknown(e, dbuf, len, lo, g);
+}
+
+static int process_segment(fk_engine *e, const uint8_t *dbuf, uint64_t len) {
+    if (len == 0 || e->ended) return FK_OK;
+    XState entering = e->state;
+    Geo g;
+    int rc = count_segment(e, dbuf, len, 0, 1, g);
+    if (rc) return rc;
+    rc = resolve_and_fetch(e, dbuf, len, 0, g);
+    if (rc) return rc;
+    return finish_segment(e, dbuf, len, 0, g, entering);
 }
 
 extern "C" int fk_engine_feed(fk_engine *e, const uint8_t *buf, uint64_t len, int on_device) {
@@ -1262,29 +1371,28 @@ extern "C" int fk_engine_feed(fk_engine *e, const uint8_t *buf, uint64_t len, in
     if (rc) return rc;
     e->fed += len;
     if (e->ended || len == 0) return FK_OK;
-    uint64_t &cap = e->chunk_cap;
+    if (e->tail_added) return FK_E_STATE;     /* finish() already closed the stream */
     if (on_device && ((uintptr_t)buf & 15) == 0) {
         for (uint64_t off = 0; off < len && !e->ended; off += SEG_MAX_BYTES) {
-            uint64_t n = std::min(SEG_MAX_BYTES, len - off);
-            rc = process_segment(e, buf + off, n, cap);
+            rc = process_segment(e, buf + off, std::min(SEG_MAX_BYTES, len - off));
             if (rc) return rc;
         }
         return FK_OK;
     }
     /* stage through pinned host memory (or realign device input) */
-    if (!e->d_stage[0] && hipMalloc((void **)&e->d_stage[0], STAGE_BYTES) != hipSuccess) return FK_E_OOM;
-    if (!on_device && !e->h_stage[0] &&
-        hipHostMalloc((void **)&e->h_stage[0], STAGE_BYTES, hipHostMallocDefault) != hipSuccess)
+    if (!e->d_stage && hipMalloc((void **)&e->d_stage, STAGE_BYTES) != hipSuccess) return FK_E_OOM;
+    if (!on_device && !e->h_stage &&
+        hipHostMalloc((void **)&e->h_stage, STAGE_BYTES, hipHostMallocDefault) != hipSuccess)
         return FK_E_OOM;
     for (uint64_t off = 0; off < len && !e->ended; off += STAGE_BYTES) {
         uint64_t n = std::min(STAGE_BYTES, len - off);
         if (on_device) {
-            HIPCHK(hipMemcpyAsync(e->d_stage[0], buf + off, n, hipMemcpyDeviceToDevice, e->stream));
+            HIPCHK(hipMemcpyAsync(e->d_stage, buf + off, n, hipMemcpyDeviceToDevice, e->stream));
         } else {
-            memcpy(e->h_stage[0], buf + off, n);
-            HIPCHK(hipMemcpyAsync(e->d_stage[0], e->h_stage[0], n, hipMemcpyHostToDevice, e->stream));
+            memcpy(e->h_stage, buf + off, n);
+            HIPCHK(hipMemcpyAsync(e->d_stage, e->h_stage, n, hipMemcpyHostToDevice, e->stream));
         }
-        rc = process_segment(e, e->d_stage[0], n, cap);
+        rc = process_segment(e, e->d_stage, n);
         if (rc) return rc;
     }
     return FK_OK;
@@ -1308,28 +1416,17 @@ extern "C" int fk_engine_feed_shard(fk_engine *e, const uint8_t *buf, uint64_t l
     if (len > SEG_MAX_BYTES || ((uintptr_t)buf & 15) || (halo & 15)) return FK_E_INVALID;
     int rc = set_dev(e);
     if (rc) return rc;
-    uint64_t &cap = e->chunk_cap;
     e->fed = len;
     e->shard_buf = buf;
     e->shard_len = len;
     e->shard_lo = -(int64_t)std::min<uint64_t>(halo, FK_HALO_BYTES);
     e->shard_pending = 1;
     if (len == 0) return FK_OK;
-    uint64_t nchunks = (len + FK_CHUNK_BYTES - 1) / FK_CHUNK_BYTES;
-    rc = grow_chunk_arrays(e, nchunks, cap);
+    Geo g;
+    rc = count_segment(e, buf, len, e->shard_lo, 0, g);
     if (rc) return rc;
-    HIPCHK(hipEventRecord(e->ev[0], e->stream));
-    rc = launch_count(e, buf, len, e->shard_lo, nchunks, 0);
+    rc = launch_scan(e, g, 1);
     if (rc) return rc;
-    HIPCHK(hipEventRecord(e->ev[1], e->stream));
-    rc = launch_scan(e, nchunks, 1);
-    if (rc) return rc;
-    HIPCHK(hipStreamSynchronize(e->stream));
-    float ms = 0;
-    hipEventElapsedTime(&ms, e->ev[0], e->ev[1]);
-    e->main_ms += ms;
-    e->dev_ms += ms;
-    e->chunks += nchunks;
     return FK_OK;
 }
 
@@ -1341,7 +1438,8 @@ extern "C" int fk_engine_summary(fk_engine *e, fk_summary *out) {
     if (e->shard_pending && e->shard_len) {
         int rc = set_dev(e);
         if (rc) return rc;
-        HIPCHK(hipMemcpy(&t, e->d_tf, sizeof t, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpyAsync(&t, e->d_tf, sizeof t, hipMemcpyDeviceToHost, e->stream));
+        HIPCHK(hipStreamSynchronize(e->stream));
     }
     memcpy(out, &t, sizeof t);
     return FK_OK;
@@ -1369,51 +1467,14 @@ extern "C" int fk_engine_resolve(fk_engine *e, const fk_state *entering) {
     e->shard_pending = 0;
     e->state = in;
     HIPCHK(hipMemcpyAsync(e->d_state, &in, sizeof in, hipMemcpyHostToDevice, e->stream));
-    if (e->shard_len == 0) return FK_OK;
-    uint64_t nchunks = (e->shard_len + FK_CHUNK_BYTES - 1) / FK_CHUNK_BYTES;
-    HIPCHK(hipEventRecord(e->ev[0], e->stream));
-    rc = launch_scan(e, nchunks, 0);
-    if (rc) return rc;
-    rc = launch_redo(e, e->shard_buf, e->shard_len, e->shard_lo, nchunks, 0);
-    if (rc) return rc;
-    HIPCHK(hipEventRecord(e->ev[2], e->stream));
-    SegOut o;
-    rc = read_segment(e, nchunks, o);
-    if (rc) return rc;
-    float ms = 0;
-    hipEventElapsedTime(&ms, e->ev[0], e->ev[2]);
-    e->dev_ms += ms;
-    e->redo += o.redo_n;
-    if (o.eof != ~0ull) {
-        /* cancel everything and recount the prefix before the 0xFF byte */
-        rc = launch_redo(e, e->shard_buf, e->shard_len, e->shard_lo, nchunks, 1);
-        if (rc) return rc;
-        HIPCHK(hipMemcpyAsync(e->d_state, &in, sizeof in, hipMemcpyHostToDevice, e->stream));
-        e->ended = 1;
-        e->scanned += o.eof;
-        uint64_t tl = o.eof;
-        if (tl) {
-            uint64_t nc2 = (tl + FK_CHUNK_BYTES - 1) / FK_CHUNK_BYTES;
-            rc = launch_count(e, e->shard_buf, tl, e->shard_lo, nc2, 1);
-            if (rc) return rc;
-            rc = launch_scan(e, nc2, 0);
-            if (rc) return rc;
-            rc = launch_redo(e, e->shard_buf, tl, e->shard_lo, nc2, 0);
-            if (rc) return rc;
-            SegOut o2;
-            rc = read_segment(e, nc2, o2);
-            if (rc) return rc;
-            e->state = o2.exit;
-            e->unknown += o2.unknown;
-            return collect_unknown(e, e->shard_buf, tl, e->shard_lo, nc2, o2.unknown);
-        }
+    if (e->shard_len == 0) {
         HIPCHK(hipStreamSynchronize(e->stream));
         return FK_OK;
     }
-    e->state = o.exit;
-    e->unknown += o.unknown;
-    e->scanned += e->shard_len;
-    return collect_unknown(e, e->shard_buf, e->shard_len, e->shard_lo, nchunks, o.unknown);
+    Geo g = geometry(e, e->shard_len);
+    rc = resolve_and_fetch(e, e->shard_buf, e->shard_len, e->shard_lo, g);
+    if (rc) return rc;
+    return finish_segment(e, e->shard_buf, e->shard_len, e->shard_lo, g, in);
 }
 
 /* ---- finish ---- */
@@ -1427,36 +1488,37 @@ extern "C" int fk_engine_finish(fk_engine *e, fk_result *res) {
     const int k = e->k;
     /* an input ending with a run of 1..k-1 bases leaves its prefix walk */
     int32_t seq = (int32_t)(uint32_t)e->state.R;
-    if (!e->state.hdr && seq >= 1 && seq < k) {
+    if (!e->state.hdr && seq >= 1 && seq < k && e->opts.want_nodes && !e->tail_added) {
         uint64_t off = ((1ull << (2 * seq)) - 4) / 3;
         uint64_t idx = off + (e->state.code & ((1ull << (2 * seq)) - 1));
         hipLaunchKernelGGL(k_add_short, dim3(1), dim3(1), 0, e->stream, e->d_short, idx);
         HIPCHK(hipGetLastError());
     }
+    e->tail_added = true;
+    if (!e->stats_valid) {
+        rc = launch_table_stats(e);
+        if (rc) return rc;
+        HIPCHK(hipMemcpyAsync(e->last.tstat, e->d_res->tstat, sizeof e->last.tstat, hipMemcpyDeviceToHost, e->stream));
+    }
     unsigned long long acc[ACC_N];
     HIPCHK(hipMemcpyAsync(acc, e->d_acc, sizeof acc, hipMemcpyDeviceToHost, e->stream));
-    HIPCHK(hipMemsetAsync(e->d_tstat, 0, 10 * sizeof(unsigned long long), e->stream));
-    unsigned gd = (unsigned)std::min<uint64_t>((uint64_t)e->cus * 4, (e->nbins / 4 + 255) / 256 + 1);
-    hipLaunchKernelGGL(k_table_stats, dim3(gd), dim3(256), 0, e->stream, e->d_table, e->nbins, k, e->d_tstat);
-    HIPCHK(hipGetLastError());
-    unsigned long long ts[10];
-    HIPCHK(hipMemcpyAsync(ts, e->d_tstat, sizeof ts, hipMemcpyDeviceToHost, e->stream));
     HIPCHK(hipStreamSynchronize(e->stream));
-    const unsigned long long distinct = ts[0];
+    e->stats_valid = true;
+    const unsigned long long *ts = e->last.tstat;
     res->windows = acc[ACC_WIN];
-    /* every window's last base is a base counted by the reference; a run's
-       first window also counts its first k-1 bases (:1035-1057) */
+    /* every window's last base is a base the reference counts; a run's first
+       window also counts its first k-1 bases (:1035-1057) */
     for (int b = 0; b < 4; b++) {
         res->base_count[b] = ts[2 + b] + acc[ACC_BASE + b];
         res->depth1[b] = ts[6 + b] + acc[ACC_D1S + b];
         if (res->depth1[b] >= (1ull << 32)) res->rollover = 1;
     }
-    /* a bin that wrapped past 2^32 loses 2^32 from the table total: some
-       trie counter reached 2^32 -> the reference's rollover exit (:642) */
+    /* a bin that wrapped past 2^32 loses 2^32 from the table total: some trie
+       counter reached 2^32 -> the reference's rollover exit (:642) */
     if (ts[1] != res->windows) res->rollover = 1;
     res->valid_bases = res->windows + acc[ACC_VALID];
-    res->distinct = distinct;
-    res->unknown_chars = e->unknown;
+    res->distinct = ts[0];
+    res->unknown_chars = acc[ACC_UNK];
     res->scanned_bytes = e->ended ? e->scanned : e->fed;
     res->hit_eof_byte = e->ended;
     res->unterminated_header = e->state.hdr ? 1 : 0;
@@ -1469,7 +1531,7 @@ extern "C" int fk_engine_finish(fk_engine *e, fk_result *res) {
         /* nodeCounter = head + distinct prefixes of every walk (:620) */
         uint64_t nodes = 0;
         if (any_walk) {
-            nodes = 1 + distinct;
+            nodes = 1 + res->distinct;
             if (k >= 2) {
                 uint8_t *pa = nullptr, *pb = nullptr;
                 uint64_t n1 = 1ull << (2 * (k - 1));
@@ -1479,17 +1541,17 @@ extern "C" int fk_engine_finish(fk_engine *e, fk_result *res) {
                 for (int d = k - 1; d >= 1; d--) {
                     uint64_t nd = 1ull << (2 * d);
                     uint64_t off = ((1ull << (2 * d)) - 4) / 3;
-                    HIPCHK(hipMemsetAsync(e->d_obs + 3, 0, sizeof(unsigned long long), e->stream));
+                    HIPCHK(hipMemsetAsync(e->d_tmp, 0, sizeof(unsigned long long), e->stream));
                     unsigned g = (unsigned)std::min<uint64_t>((uint64_t)e->cus * 4, nd / 256 + 1);
                     if (d == k - 1)
                         hipLaunchKernelGGL(k_fold_from_table, dim3(g), dim3(256), 0, e->stream, e->d_table,
-                                           e->d_short + off, cur, nd, e->d_obs + 3);
+                                           e->d_short + off, cur, nd, e->d_tmp);
                     else
                         hipLaunchKernelGGL(k_fold_level, dim3(g), dim3(256), 0, e->stream, nxt,
-                                           e->d_short + off, cur, nd, e->d_obs + 3);
+                                           e->d_short + off, cur, nd, e->d_tmp);
                     HIPCHK(hipGetLastError());
                     unsigned long long c = 0;
-                    HIPCHK(hipMemcpyAsync(&c, e->d_obs + 3, sizeof c, hipMemcpyDeviceToHost, e->stream));
+                    HIPCHK(hipMemcpyAsync(&c, e->d_tmp, sizeof c, hipMemcpyDeviceToHost, e->stream));
                     HIPCHK(hipStreamSynchronize(e->stream));
                     nodes += c;
                     std::swap(cur, nxt);   /* this level becomes the child level */
@@ -1514,7 +1576,7 @@ extern "C" int fk_engine_progress(fk_engine *e, uint64_t *valid_bases, uint64_t 
     unsigned long long acc[ACC_N];
     HIPCHK(hipMemcpyAsync(acc, e->d_acc, sizeof acc, hipMemcpyDeviceToHost, e->stream));
     HIPCHK(hipStreamSynchronize(e->stream));
-    if (valid_bases) *valid_bases = acc[ACC_VALID];
+    if (valid_bases) *valid_bases = acc[ACC_WIN] + acc[ACC_VALID];
     if (windows) *windows = acc[ACC_WIN];
     return FK_OK;
 }
@@ -1558,6 +1620,7 @@ extern "C" int fk_engine_table_from_device(fk_engine *e, const void *src) {
     if (rc) return rc;
     HIPCHK(hipMemcpyAsync(e->d_table, src, e->nbins * sizeof(uint32_t), hipMemcpyDeviceToDevice, e->stream));
     HIPCHK(hipStreamSynchronize(e->stream));
+    e->stats_valid = false;
     return FK_OK;
 }
 
@@ -1603,7 +1666,7 @@ extern "C" int fk_engine_merge_from(fk_engine *dst, fk_engine *src) {
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(dst->stream));
     hipFree(tmp); hipFree(tmps); hipFree(tmpa);
-    dst->unknown += src->unknown;
+    dst->stats_valid = false;
     dst->unknown_bytes.insert(dst->unknown_bytes.end(), src->unknown_bytes.begin(), src->unknown_bytes.end());
     dst->chunks += src->chunks;
     dst->redo += src->redo;
@@ -1633,6 +1696,12 @@ extern "C" int fk_count(const uint8_t *buf, uint64_t len, int k, const fk_opts *
     return rc;
 }
 
+/*
+ * One process, ngpu devices: contiguous shards (chunk-aligned), each counted
+ * on its own GPU from a guessed entry state, stitched in order with the shard
+ * transfer functions, re-counted where the guess was wrong, then the tables
+ * are merged into device 0 (peer copies over xGMI).
+ */
 extern "C" int fk_count_multi(const uint8_t *buf, uint64_t len, int k, int ngpu, const fk_opts *opts,
                               uint32_t *counts, fk_result *res) {
     int ndev = fk_device_count();
@@ -1641,7 +1710,6 @@ extern "C" int fk_count_multi(const uint8_t *buf, uint64_t len, int k, int ngpu,
     std::vector<fk_engine *> eng((size_t)ngpu, nullptr);
     std::vector<uint8_t *> dbuf((size_t)ngpu, nullptr);
     int rc = FK_OK;
-    /* contiguous shards aligned to chunk multiples; each carries a halo */
     uint64_t per = ((len / (uint64_t)ngpu) / FK_CHUNK_BYTES) * FK_CHUNK_BYTES;
     std::vector<uint64_t> off((size_t)ngpu + 1);
     for (int g = 0; g < ngpu; g++) off[(size_t)g] = (uint64_t)g * per;
@@ -1654,54 +1722,43 @@ extern "C" int fk_count_multi(const uint8_t *buf, uint64_t len, int k, int ngpu,
         if (rc) break;
         uint64_t halo = g ? FK_HALO_BYTES : 0;
         uint64_t n = off[(size_t)g + 1] - off[(size_t)g];
-        hipSetDevice(g);
+        if (hipSetDevice(g) != hipSuccess) { rc = FK_E_HIP; break; }
         if (hipMalloc((void **)&dbuf[(size_t)g], n + halo + 16) != hipSuccess) { rc = FK_E_OOM; break; }
-        if (hipMemcpy(dbuf[(size_t)g], buf + off[(size_t)g] - halo, n + halo, hipMemcpyHostToDevice) != hipSuccess) { rc = FK_E_HIP; break; }
+        if (hipMemcpy(dbuf[(size_t)g], buf + off[(size_t)g] - halo, n + halo, hipMemcpyHostToDevice) != hipSuccess) {
+            rc = FK_E_HIP;
+            break;
+        }
         rc = fk_engine_feed_shard(eng[(size_t)g], dbuf[(size_t)g] + halo, n, halo, 1);
     }
+    int last = ngpu - 1;
     if (rc == FK_OK) {
         fk_state s{0, 0, 0, 0};
         for (int g = 0; g < ngpu && rc == FK_OK; g++) {
-            fk_summary sm;
-            rc = fk_engine_summary(eng[(size_t)g], &sm);
-            if (rc) break;
             rc = fk_engine_resolve(eng[(size_t)g], &s);
             if (rc) break;
-            if (eng[(size_t)g]->ended) {   /* a 0xFF byte: later shards are not scanned */
-                for (int h = g + 1; h < ngpu; h++) { eng[(size_t)h]->shard_pending = 0; }
-                fk_engine_state(eng[(size_t)g], &s);
-                for (int h = g + 1; h < ngpu; h++) {
-                    fk_engine_reset(eng[(size_t)h]);
-                }
+            fk_engine_state(eng[(size_t)g], &s);
+            if (eng[(size_t)g]->ended) {          /* a 0xFF byte: later shards do not count */
+                for (int h = g + 1; h < ngpu; h++) fk_engine_reset(eng[(size_t)h]);
+                last = g;
                 break;
             }
-            fk_engine_state(eng[(size_t)g], &s);
         }
     }
     if (rc == FK_OK) {
         for (int g = 1; g < ngpu && rc == FK_OK; g++) rc = fk_engine_merge_from(eng[0], eng[(size_t)g]);
-        /* the stream's end state lives in the last shard that scanned */
         if (rc == FK_OK) {
-            fk_state s;
-            int last = ngpu - 1;
-            for (int g = 0; g < ngpu; g++) if (eng[(size_t)g]->ended) { last = g; break; }
-            fk_engine_state(eng[(size_t)last], &s);
-            eng[0]->state = XState{s.run, s.code, s.hdr, 0};
-            uint64_t fed = 0, sc = 0;
-            int ended = 0;
-            for (int g = 0; g < ngpu; g++) {
-                fed += eng[(size_t)g]->fed;
-                if (!ended) sc += eng[(size_t)g]->ended ? eng[(size_t)g]->scanned : eng[(size_t)g]->fed;
-                if (eng[(size_t)g]->ended) ended = 1;
-            }
-            eng[0]->fed = fed;
-            eng[0]->scanned = sc;
-            eng[0]->ended = ended;
+            fk_engine *e0 = eng[0];
+            e0->state = eng[(size_t)last]->state;
+            uint64_t sc = 0;
+            for (int g = 0; g <= last; g++) sc += eng[(size_t)g]->ended ? eng[(size_t)g]->scanned : eng[(size_t)g]->fed;
+            e0->fed = len;
+            e0->scanned = sc;
+            e0->ended = eng[(size_t)last]->ended;
             fk_result tmp;
             if (!res) res = &tmp;
-            rc = fk_engine_finish(eng[0], res);
+            rc = fk_engine_finish(e0, res);
             if (counts && (rc == FK_OK || rc == FK_E_UNTERMINATED_HEADER)) {
-                int r2 = fk_engine_table(eng[0], counts);
+                int r2 = fk_engine_table(e0, counts);
                 if (r2) rc = r2;
             }
         }
