@@ -14,9 +14,10 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#define FK_TILE_BYTES 1024u            /* one wave x 16 B */
-#define FK_CHUNK_TILES 64u
-#define FK_CHUNK_BYTES (FK_TILE_BYTES * FK_CHUNK_TILES)   /* 64 KiB per chunk */
+#define FK_LANE_BYTES 32u              /* bytes per lane per tile */
+#define FK_TILE_BYTES (64u * FK_LANE_BYTES)   /* one wave: 2 KiB */
+#define FK_CHUNK_TILES 8u
+#define FK_CHUNK_BYTES (FK_TILE_BYTES * FK_CHUNK_TILES)   /* 16 KiB per chunk */
 #define FK_HALO_BYTES 256u             /* bytes before a chunk used to guess state */
 #define FK_BLOCK 512u
 #define FK_WAVES_PER_BLOCK (FK_BLOCK / 64u)
@@ -34,26 +35,20 @@ enum {
     ACC_N = 16
 };
 
-/* per-chunk record written by the count pass (64 B) */
-struct ChunkRec {
-    uint64_t a_code;     /* assumed entering state */
-    uint32_t a_R, a_hdr;
-    uint64_t x_code;     /* exit state of the counted trajectory */
-    uint32_t x_R, x_hdr;
-    uint32_t flags;      /* CR_* */
-    uint32_t R_at_p1;    /* R just before the chunk's first '\n'/'>' byte */
-    uint32_t nv_total;   /* bases processed (meaningful when no reset) */
-    uint32_t eof_off;    /* first 0xFF outside a header, chunk-relative */
-    uint32_t unknown;    /* unknown-character bytes in the chunk */
-    uint32_t pad[3];
-};
-enum {
-    CR_FOUND_P1 = 1u,       /* chunk contains '\n' or '>' */
-    CR_P1_GT = 2u,          /* ... and the first one is '>' */
-    CR_ANY_RESET = 4u,      /* the counted trajectory broke the run */
-    CR_RESET_AFTER_P1 = 8u  /* ... after the first special byte */
-};
 #define FK_NO_EOF 0xFFFFFFFFu
+#define FK_NO_EOF64 0xFFFFFFFFFFFFFFFFull
+
+/* What a counted trajectory over a span of bytes (a wave's range) observed,
+ * wave-uniform; with the entering and exit states it determines the span's
+ * transfer function (fk_tf_span). */
+struct Facts {
+    uint32_t found_p1;        /* the span contains '\n' or '>' */
+    uint32_t p1_gt;           /* ... and the first one is '>' */
+    uint32_t any_reset;       /* the trajectory broke the run */
+    uint32_t reset_after_p1;  /* ... after the first special byte */
+    uint32_t R_at_p1;         /* R just before the first special byte */
+    uint32_t nv_total;        /* bases processed (meaningful without a reset) */
+};
 
 struct DState {
     uint64_t code;
@@ -76,6 +71,12 @@ struct TF {
     uint32_t f0_const;
     uint32_t pad;
 };
+
+/* Digit-wise map between the internal base encoding (A0 C1 T2 G3) and the
+ * reference's (A0 C1 G2 T3): swaps digit values 2 and 3; an involution. */
+__host__ __device__ inline uint64_t fk_sigma(uint64_t x) {
+    return x ^ ((x >> 1) & 0x5555555555555555ull);
+}
 
 __host__ __device__ inline uint64_t fk_join(uint64_t x, uint64_t y, uint64_t n) {
     /* append n bases y (low 2n bits) after x; keep the last 32 bases */
@@ -130,50 +131,65 @@ __host__ __device__ inline TF fk_identity() {
     return t;
 }
 
-/* Transfer function of one chunk from what its count pass recorded. */
-__host__ __device__ inline TF fk_tf_of(const ChunkRec &r) {
+/* Transfer function of a span counted from entering state a (exit x, facts f). */
+__host__ __device__ inline TF fk_tf_span(const DState &a, const DState &x, const Facts &f) {
     TF t;
     t.pad = 0;
-    XState x{r.x_R, r.x_code, r.x_hdr, 0};
-    if (r.a_hdr == 0) {
-        if (r.flags & CR_ANY_RESET) {
+    XState xs{x.R, x.code, x.hdr, 0};
+    if (a.hdr == 0) {
+        if (f.any_reset) {
             t.f0_const = 1;
-            t.c0 = x;
+            t.c0 = xs;
             t.nv = 0;
             t.cs = 0;
         } else {
             t.f0_const = 0;
             t.c0 = XState{0, 0, 0, 0};
-            t.nv = r.nv_total;
-            t.cs = r.x_code;
+            t.nv = f.nv_total;
+            t.cs = x.code;
         }
-        if (!(r.flags & CR_FOUND_P1)) {
+        if (!f.found_p1) {
             t.c1 = XState{0, 0, 1, 0};
-        } else if (r.flags & CR_P1_GT) {
-            t.c1 = x;
+        } else if (f.p1_gt) {
+            t.c1 = xs;
         } else {
-            uint32_t rr = (r.flags & CR_RESET_AFTER_P1) ? r.x_R : (uint32_t)(r.x_R - r.R_at_p1);
-            t.c1 = XState{rr, r.x_code, r.x_hdr, 0};
+            uint32_t rr = f.reset_after_p1 ? x.R : (uint32_t)(x.R - f.R_at_p1);
+            t.c1 = XState{rr, x.code, x.hdr, 0};
         }
     } else {
         /* entering inside a header was certain: f0 never applies */
-        t.c1 = x;
+        t.c1 = xs;
         t.f0_const = 1;
-        t.c0 = x;
+        t.c0 = xs;
         t.nv = 0;
         t.cs = 0;
     }
     return t;
 }
 
-/* A wave's contiguous run of chunks [c0, c1): the composed transfer function
- * and the state guessed for its first chunk (the others continue from the
- * previous chunk's exit). */
+/* A wave's contiguous run of chunks [c0, c1): its transfer function, the
+ * state guessed for its start, and what its counted trajectory observed
+ * (exact once the range is resolved). */
 struct RangeRec {
     TF tf;
     uint64_t a_code;
     uint32_t a_R, a_hdr;
     uint64_t c0, c1;
+    uint64_t eof;        /* first 0xFF outside a header, range-relative, or FK_NO_EOF64 */
+    uint32_t unknown;    /* "Unknown character" bytes in the range */
+    uint32_t pad;
+};
+
+/* A range k_count stopped in (first tile the fast path cannot take):
+ * k_resume continues it from here. */
+struct ResumeRec {
+    uint64_t tile;       /* range-relative tile index */
+    uint64_t code;       /* state entering that tile */
+    uint32_t R, hdr;
+    uint64_t a_code;     /* the range's guessed entering state */
+    uint32_t a_R, a_hdr;
+    uint32_t range, pad;
+    Facts f;             /* facts of the range so far */
 };
 
 /* Per-feed results, fetched with one device-to-host copy. */
@@ -182,11 +198,11 @@ struct DevRes {
     XState exit;                    /* stream state after the feed */
     unsigned long long eof_cand;    /* smallest 0xFF offset seen (a candidate) */
     uint32_t redo_n;                /* ranges re-counted */
-    uint32_t pad;
+    uint32_t resume_n;              /* ranges handed from k_count to k_resume */
 };
 
-/* Would counting a chunk from state a and from state t give identical
- * contributions?  nvb bounds the bases in the chunk. */
+/* Would counting a span from state a and from state t give identical
+ * contributions?  nvb bounds the bases in the span. */
 __host__ __device__ inline bool fk_equiv(const DState &a, const XState &t, int k, uint64_t nvb) {
     if (a.hdr != t.hdr) return false;
     if (t.hdr) return true;

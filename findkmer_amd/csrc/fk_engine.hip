@@ -61,9 +61,24 @@ __device__ __forceinline__ uint32_t fk_byte_rt(const uint32_t w[4], uint32_t j) 
     return (v >> (8 * (j & 3))) & 0xFFu;
 }
 
-/* A=0 C=1 G=2 T=3 (base2int :567-589), -1 otherwise */
+/* Internal base encoding A=0 C=1 T=2 G=3, i.e. (byte >> 1) & 3, so the fast
+ * path needs no arithmetic beyond a shift and a mask; fk_sigma() maps indices
+ * to the reference's A=0 C=1 G=2 T=3 (base2int :567-589).  -1: not a base. */
 __device__ __forceinline__ int fk_sym(uint32_t c) {
-    return c == 'A' ? 0 : c == 'C' ? 1 : c == 'G' ? 2 : c == 'T' ? 3 : -1;
+    return c == 'A' ? 0 : c == 'C' ? 1 : c == 'T' ? 2 : c == 'G' ? 3 : -1;
+}
+
+/* A use of a tile buffer on every path (even where its tile is not
+   counted): the waitcnt bookkeeping then sees one consistent pending-load
+   state at each merge and waits for exactly the tile being used. */
+__device__ __forceinline__ void consume(const uint32_t w[8]) {
+    asm volatile("" ::"v"(w[0]), "v"(w[1]), "v"(w[2]), "v"(w[3]), "v"(w[4]), "v"(w[5]), "v"(w[6]), "v"(w[7]));
+}
+
+/* wave index inside the block, provably wave-uniform (lives in an SGPR, so
+   the loops it bounds stay scalar) */
+__device__ __forceinline__ uint32_t wave_in_block() {
+    return (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
 }
 
 __device__ __forceinline__ uint32_t shup(uint32_t v, int d) { return __shfl_up(v, (unsigned)d, 64); }
@@ -88,17 +103,13 @@ __device__ __forceinline__ uint64_t comp_packed(uint64_t x, int k, uint64_t mask
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
-struct Counters {       /* per lane; flushed per chunk */
+struct Counters {       /* per lane; flushed per range */
     uint64_t base;      /* 4 x 16-bit: first-window extra bases (first k-1 digits) */
     uint64_t d1s;       /* 4 x 16-bit: depth-1 trie touches of short walks */
     uint32_t valid;     /* baseCounter beyond one per window ((k-1) per first window) */
     uint32_t win;       /* windows counted */
     uint32_t unknown;
-    uint32_t eof;       /* chunk-relative offset of first 0xFF, or FK_NO_EOF */
-};
-
-struct Facts {          /* wave-uniform per chunk */
-    uint32_t found_p1, p1_gt, any_reset, reset_after_p1, R_at_p1, nv_total;
+    uint32_t eof;       /* range-relative offset of first 0xFF, or FK_NO_EOF */
 };
 
 /* Where windows are accumulated. */
@@ -122,10 +133,11 @@ struct Ctx {            /* kernel-wide constants */
     int k;
 };
 
+/* idx in the internal encoding (A0 C1 T2 G3) */
 template <int HM>
 __device__ __forceinline__ void hist_add(const Ctx &cx, uint64_t idx, uint32_t w) {
     if (HM == H_GLOBAL) {
-        atomicAdd(&cx.table[idx], w);
+        atomicAdd(&cx.table[fk_sigma(idx)], w);
     } else if (HM == H_LDS) {
         atomicAdd(&cx.lds[(uint32_t)idx], w);
     } else {
@@ -138,46 +150,64 @@ __device__ __forceinline__ void short_run(const Ctx &cx, int seq, uint64_t code,
        for nodeCounter (:1059-1062).  Offset of depth d: (4^d - 4) / 3. */
     uint64_t off = ((1ull << (2 * seq)) - 4) / 3;
     uint64_t m = (1ull << (2 * seq)) - 1;
-    atomicAdd(&cx.shortcnt[off + (code & m)], w);
+    atomicAdd(&cx.shortcnt[off + fk_sigma(code & m)], w);
 }
 
-/* Load the 16 bytes of lane `l` of a tile starting at byte offset `off`
- * (relative to cx.buf; may be negative down to cx.lo).  Fully-inside lanes use
- * one 16-B load; the stream's last partial lane loads bytewise. */
-__device__ __forceinline__ int load16(const Ctx &cx, int64_t off, uint32_t w[4]) {
-    w[0] = w[1] = w[2] = w[3] = 0;
+/* Load lane bytes [off, off+nbytes) (nbytes = 16 or 32, relative to cx.buf;
+ * may start below 0 down to cx.lo).  Fully-inside lanes use 16-B loads; the
+ * stream's last partial lane loads bytewise.  Returns the valid byte count. */
+template <int NB>
+__device__ __forceinline__ int load_lane(const Ctx &cx, int64_t off, uint32_t w[NB / 4]) {
+#pragma unroll
+    for (int d = 0; d < NB / 4; d++) w[d] = 0;
     if (off < cx.lo || off >= (int64_t)cx.len) return 0;
-    if (off + 16 <= (int64_t)cx.len) {
-        u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(cx.buf + off));
-        w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
-        return 16;
+    if (off + NB <= (int64_t)cx.len) {
+#pragma unroll
+        for (int q = 0; q < NB / 16; q++) {
+            u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(cx.buf + off) + q);
+            w[4 * q] = v.x; w[4 * q + 1] = v.y; w[4 * q + 2] = v.z; w[4 * q + 3] = v.w;
+        }
+        return NB;
     }
     int nb = (int)((int64_t)cx.len - off);
-    for (int j = 0; j < nb; j++) w[j >> 2] |= (uint32_t)cx.buf[off + j] << (8 * (j & 3));
+    for (int j = 0; j < nb; j++) {
+        uint32_t b = (uint32_t)cx.buf[off + j] << (8 * (j & 3));
+        /* select-chain store: no dynamic register indexing */
+#pragma unroll
+        for (int d = 0; d < NB / 4; d++) if ((j >> 2) == d) w[d] |= b;
+    }
     return nb;
 }
 
+/* byte j (runtime) of a lane's 32 bytes without indexing the register array */
+__device__ __forceinline__ uint32_t lane_byte(const uint32_t w[8], uint32_t j) {
+    uint32_t d = j >> 2;
+    uint32_t lo = d == 0 ? w[0] : d == 1 ? w[1] : d == 2 ? w[2] : w[3];
+    uint32_t hi = d == 4 ? w[4] : d == 5 ? w[5] : d == 6 ? w[6] : w[7];
+    return ((d < 4 ? lo : hi) >> (8 * (j & 3))) & 0xFFu;
+}
+
 /*
- * Slow, fully general tile (one wave, 16 bytes per lane, `nb` valid).
- * COUNT=false: only advance the wave state (halo guess).
- * `tile_off` is the tile's byte offset inside its chunk.
+ * General tile (one wave, FK_LANE_BYTES per lane, `nb` valid): any bytes,
+ * any state.  COUNT=false only advances the wave state (halo guess).
+ * `tile_off` is the tile's byte offset inside its range.
  */
 template <bool COUNT, int HM>
-__device__ __forceinline__ void tile_general(const Ctx &cx, const uint32_t w[4], int nb,
+__device__ __forceinline__ void tile_general(const Ctx &cx, const uint32_t w[8], int nb,
                                              uint32_t tile_off, DState &st, Facts &f,
                                              Counters &cnt, uint32_t weight) {
     const int lane = threadIdx.x & 63;
     const int k = cx.k;
+    const uint32_t LB = FK_LANE_BYTES;
 
     /* -- 1. header flag at each lane start: last '>' vs last '\n' before it */
     uint32_t lastGT = 0, lastNL = 0, firstSp = 0xFFFFu, firstGT = 0;
 #pragma unroll 1
-    for (int j = 0; j < 16; j++) {
-        uint32_t c = fk_byte_rt(w, (uint32_t)j);
-        bool in = j < nb;
-        uint32_t pos = (uint32_t)lane * 16u + (uint32_t)j + 1u;
-        bool gt = in && c == '>';
-        bool nl = in && c == '\n';
+    for (int j = 0; j < nb; j++) {
+        uint32_t c = lane_byte(w, (uint32_t)j);
+        uint32_t pos = (uint32_t)lane * LB + (uint32_t)j + 1u;
+        bool gt = c == '>';
+        bool nl = c == '\n';
         if (gt) lastGT = pos;
         if (nl) lastNL = pos;
         if ((gt || nl) && firstSp == 0xFFFFu) { firstSp = pos - 1; firstGT = gt; }
@@ -197,17 +227,15 @@ __device__ __forceinline__ void tile_general(const Ctx &cx, const uint32_t w[4],
     uint64_t code = 0;
 #pragma unroll 1
     for (int j = 0; j < nb; j++) {
-        {
-            uint32_t c = fk_byte_rt(w, (uint32_t)j);
-            if (hdr) {
-                if (c == '\n') hdr = 0;
-            } else if (c == '>') {
-                rs = 1; nv = 0; hdr = 1;
-            } else if (c != '\n') {
-                int s = fk_sym(c);
-                if (s < 0) { rs = 1; nv = 0; }
-                else { code = (code << 2) | (uint32_t)s; nv++; }
-            }
+        uint32_t c = lane_byte(w, (uint32_t)j);
+        if (hdr) {
+            if (c == '\n') hdr = 0;
+        } else if (c == '>') {
+            rs = 1; nv = 0; hdr = 1;
+        } else if (c != '\n') {
+            int s = fk_sym(c);
+            if (s < 0) { rs = 1; nv = 0; }
+            else { code = (code << 2) | (uint32_t)s; nv++; }
         }
     }
     hdr_end = hdr;
@@ -261,46 +289,45 @@ __device__ __forceinline__ void tile_general(const Ctx &cx, const uint32_t w[4],
 
 #pragma unroll 1
         for (int j = 0; j < nb; j++) {
-            {
-                uint32_t c = fk_byte_rt(w, (uint32_t)j);
-                uint32_t pos = (uint32_t)lane * 16u + (uint32_t)j;
-                if (p1_here && pos == p1) r_at = R;
-                if (hdr) {
-                    if (c == '\n') hdr = 0;
-                    continue;
-                }
-                if (c == '\n') continue;
-                int s = fk_sym(c);
-                if (s < 0) {                      /* run break: '>', N, other */
-                    int seq = (int)R;
-                    if (seq >= 1 && seq < k) short_run(cx, seq, lc, weight);
-                    R = 0;
-                    lane_reset = 1;
-                    if (f.found_p1 || (p1_here && pos > p1)) lane_reset_after = 1;
-                    if (c == '>') {
-                        hdr = 1;
-                    } else if (c == 0xFFu) {
-                        uint32_t o = tile_off + pos;
-                        cnt.eof = min(cnt.eof, o);
-                    } else if (c != 'N') {
-                        cnt.unknown++;
-                    }
-                    continue;
-                }
-                lc = (lc << 2) | (uint32_t)s;
-                R += 1;
+            uint32_t c = lane_byte(w, (uint32_t)j);
+            uint32_t pos = (uint32_t)lane * LB + (uint32_t)j;
+            if (p1_here && pos == p1) r_at = R;
+            if (hdr) {
+                if (c == '\n') hdr = 0;
+                continue;
+            }
+            if (c == '\n') continue;
+            int s = fk_sym(c);
+            if (s < 0) {                      /* run break: '>', N, other */
                 int seq = (int)R;
-                if (seq >= k) {
-                    uint64_t idx = lc & cx.maskk;
-                    hist_add<HM>(cx, idx, weight);
-                    cnt.win += 1;
-                    if (seq == k) {               /* first window: its first k-1 bases */
-                        cnt.base += comp_packed(idx >> 2, k - 1, maskk1);
-                        cnt.valid += (uint32_t)(k - 1);
-                    }
-                } else if (seq >= 1) {
-                    cnt.d1s += 1ull << (16 * (uint32_t)((lc >> (2 * seq - 2)) & 3));
+                if (seq >= 1 && seq < k) short_run(cx, seq, lc, weight);
+                R = 0;
+                lane_reset = 1;
+                if (f.found_p1 || (p1_here && pos > p1)) lane_reset_after = 1;
+                if (c == '>') {
+                    hdr = 1;
+                } else if (c == 0xFFu) {
+                    uint32_t o = tile_off + pos;
+                    cnt.eof = min(cnt.eof, o);
+                } else if (c != 'N') {
+                    cnt.unknown++;
                 }
+                continue;
+            }
+            lc = (lc << 2) | (uint32_t)s;
+            R += 1;
+            int seq = (int)R;
+            if (seq >= k) {
+                uint64_t idx = lc & cx.maskk;
+                hist_add<HM>(cx, idx, weight);
+                cnt.win += 1;
+                if (seq == k) {               /* first window: its first k-1 bases */
+                    cnt.base += comp_packed(fk_sigma(idx) >> 2, k - 1, maskk1);
+                    cnt.valid += (uint32_t)(k - 1);
+                }
+            } else if (seq >= 1) {
+                uint32_t d0 = (uint32_t)((lc >> (2 * seq - 2)) & 3);
+                cnt.d1s += 1ull << (16 * (d0 ^ (d0 >> 1)));
             }
         }
 
@@ -317,120 +344,152 @@ __device__ __forceinline__ void tile_general(const Ctx &cx, const uint32_t w[4],
     st = nst;
 }
 
+
 /* byte-wise "is non-zero" mask (bit 7 of each byte), exact per byte */
 __device__ __forceinline__ uint32_t nz_bytes(uint32_t d) {
     return (((d & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | d) & 0x80808080u;
 }
 
-/*
- * Fast tile: every byte is A/C/G/T except at most one '\n' per lane, the wave
- * is outside a header and deep inside a run (every window counts as
- * seqSize > k).  Returns false (without side effects) when the tile does not
- * qualify; the caller then runs tile_general.
- *
- * Per lane: 16 bytes -> 2-bit codes (A0 C1 G2 T3) in one 32-bit word, first
- * base in the top digit (v_dot4_u32_u8 packs 4 bases per instruction); the
- * previous lane's word (one __shfl_up) supplies the k-1 bases of context;
- * each window is one v_alignbit of the 64-bit {prev, mine} pair.
- */
-template <bool COUNT, int HM>
-__device__ __forceinline__ bool tile_fast(const Ctx &cx, const uint32_t w[4], uint32_t tile_off,
-                                          DState &st, Facts &f, Counters &cnt, uint32_t weight) {
-    const int lane = threadIdx.x & 63;
-    const int k = cx.k;
-    uint32_t cw[4];
-    uint32_t bad = 0, nlm = 0;
+/* previous lane's value (DPP wave_shr:1); lane 0 receives `carry` */
+__device__ __forceinline__ uint32_t from_prev_lane(uint32_t v, uint32_t carry) {
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)carry, (int)v, 0x138, 0xF, 0xF, false);
+}
+
+/* Classify one 16-byte half: bad (non-ACGT, non-'\n') bytes and '\n' mask. */
+__device__ __forceinline__ void half_check(const uint32_t *w, const uint32_t *x, uint32_t &bad,
+                                           uint32_t &nlm) {
+    nlm = 0;
+    bad = 0;
 #pragma unroll
     for (int d = 0; d < 4; d++) {
-        uint32_t x = (w[d] >> 1) & 0x03030303u;
-        uint32_t c = x ^ ((x >> 1) & 0x01010101u);         /* A0 C1 G2 T3 per byte */
-        cw[d] = c;
-        uint32_t e = __builtin_amdgcn_perm(0u, 0x54474341u, c);   /* "ACGT"[c] */
-        if (e != w[d]) {
-            uint32_t mis = nz_bytes(e ^ w[d]);
-            uint32_t isnl = ~nz_bytes(w[d] ^ 0x0A0A0A0Au) & 0x80808080u;
-            bad |= mis & ~isnl;
-            /* newline byte positions -> bits 4d..4d+3 */
-            nlm |= ((isnl >> 7) & 1u) << (4 * d) | ((isnl >> 15) & 1u) << (4 * d + 1) |
-                   ((isnl >> 23) & 1u) << (4 * d + 2) | ((isnl >> 31) & 1u) << (4 * d + 3);
+        uint32_t e = __builtin_amdgcn_perm(0u, 0x47544341u, x[d]);   /* "ACTG"[x] */
+        uint32_t mis = nz_bytes(e ^ w[d]);
+        uint32_t isnl = ~nz_bytes(w[d] ^ 0x0A0A0A0Au) & 0x80808080u;
+        bad |= mis & ~isnl;
+        nlm |= ((isnl >> 7) & 1u) << (4 * d) | ((isnl >> 15) & 1u) << (4 * d + 1) |
+               ((isnl >> 23) & 1u) << (4 * d + 2) | ((isnl >> 31) & 1u) << (4 * d + 3);
+    }
+}
+
+/* 16 bases -> 32-bit word, first base in bits 31:30 (v_dot4_u32_u8 x4) */
+__device__ __forceinline__ uint32_t pack16(const uint32_t *x) {
+    uint32_t P = __builtin_amdgcn_udot4(x[0], 0x01041040u, 0u, false);
+    P = __builtin_amdgcn_udot4(x[1], 0x01041040u, P << 8, false);
+    P = __builtin_amdgcn_udot4(x[2], 0x01041040u, P << 8, false);
+    return __builtin_amdgcn_udot4(x[3], 0x01041040u, P << 8, false);
+}
+
+/* drop the '\n' digit (byte j) -> 15 bases right-aligned */
+__device__ __forceinline__ uint32_t squeeze(uint32_t P, uint32_t nlm) {
+    int j = __ffs(nlm) - 1;
+    uint32_t lo_bits = 30u - 2u * (uint32_t)j;
+    uint32_t hi = j ? (P >> (32u - 2u * (uint32_t)j)) : 0u;
+    uint32_t lo = lo_bits ? (P & ((1u << lo_bits) - 1u)) : 0u;
+    return (lo_bits < 32u ? (hi << lo_bits) : 0u) | lo;
+}
+
+/* Count the 16 windows ending in one half: {C, S2} is a contiguous base
+ * stream with S2 holding this half's 16 slots (slot 0 belongs to the previous
+ * half when `skip0`). */
+template <int HM>
+__device__ __forceinline__ void half_windows(const Ctx &cx, uint32_t C, uint32_t S2, bool skip0,
+                                             uint32_t weight) {
+    const uint32_t m2 = (uint32_t)cx.maskk << 2;
+    if (HM == H_PAIRS) {
+        /* (k+1)-mers ending at odd slots 1,3,..,15 cover the k-mers at slots
+           (0,1),(2,3),...; without a real slot 0 the first pair becomes the
+           single k-mer at slot 1 */
+        const uint32_t m3 = (uint32_t)((cx.maskk << 2) | 3u) << 2;
+        char *L = reinterpret_cast<char *>(cx.lds);
+        {
+            uint32_t v = __builtin_amdgcn_alignbit(C, S2, 26u);
+            uint32_t addr = skip0 ? (cx.single_off * 4u + (v & m2)) : (v & m3);
+            atomicAdd(reinterpret_cast<uint32_t *>(L + addr), weight);
+        }
+#pragma unroll
+        for (int j = 1; j < 7; j++) {
+            uint32_t a = __builtin_amdgcn_alignbit(C, S2, (uint32_t)(26 - 4 * j)) & m3;
+            atomicAdd(reinterpret_cast<uint32_t *>(L + a), weight);
+        }
+        atomicAdd(reinterpret_cast<uint32_t *>(L + ((S2 << 2) & m3)), weight);
+    } else {
+#pragma unroll
+        for (int i = 0; i < 16; i++) {
+            uint32_t sh = 2u * (15u - (uint32_t)i);
+            uint32_t v = i < 15 ? __builtin_amdgcn_alignbit(C, S2, sh) : S2;
+            uint32_t idx = v & (uint32_t)cx.maskk;
+            if (i > 0 || !skip0) {
+                if (HM == H_LDS) atomicAdd(&cx.lds[idx], weight);
+                else atomicAdd(&cx.table[fk_sigma(idx)], weight);
+            }
         }
     }
-    const bool lane_ok = bad == 0 && __popc(nlm) <= 1;
+}
+
+/*
+ * Fast tile: every byte is A/C/G/T except at most one '\n' per 16-byte half
+ * lane, the wave is outside a header and deep inside a run (every window
+ * counts as seqSize > k).  Returns false (without side effects) when the
+ * tile does not qualify; the caller then runs tile_general.
+ *
+ * Per lane (32 bytes): bases -> 2-bit codes (A0 C1 T2 G3 = (byte>>1)&3, a
+ * v_perm checks them against the bytes), two 32-bit words via
+ * v_dot4_u32_u8; the previous lane's last word arrives by DPP wave_shr:1;
+ * each window is one v_alignbit of a 64-bit {context, word} pair.
+ */
+template <bool COUNT, int HM>
+__device__ __forceinline__ bool tile_fast(const Ctx &cx, const uint32_t w[8], DState &st, Facts &f,
+                                          Counters &cnt, uint32_t weight) {
+    const int lane = threadIdx.x & 63;
+    const int k = cx.k;
+    uint32_t x[8];
+    uint32_t mis = 0;
+#pragma unroll
+    for (int d = 0; d < 8; d++) {
+        x[d] = (w[d] >> 1) & 0x03030303u;
+        mis |= __builtin_amdgcn_perm(0u, 0x47544341u, x[d]) ^ w[d];
+    }
+    uint32_t nl0 = 0, nl1 = 0;
+    bool lane_ok = true;
+    if (mis) {                                   /* some byte is not a base */
+        uint32_t b0, b1;
+        half_check(w, x, b0, nl0);
+        half_check(w + 4, x + 4, b1, nl1);
+        lane_ok = (b0 | b1) == 0 && __popc(nl0) <= 1 && __popc(nl1) <= 1;
+    }
     if (__ballot(!lane_ok)) return false;
     if (COUNT && !((int32_t)st.R >= k && st.R <= 0x7FFFFFFFu - FK_TILE_BYTES)) return false;
 
-    /* pack: P = 16 digits, byte 0 in bits 31:30 */
-    uint32_t P = __builtin_amdgcn_udot4(cw[0], 0x01041040u, 0u, false);
-    P = __builtin_amdgcn_udot4(cw[1], 0x01041040u, P << 8, false);
-    P = __builtin_amdgcn_udot4(cw[2], 0x01041040u, P << 8, false);
-    P = __builtin_amdgcn_udot4(cw[3], 0x01041040u, P << 8, false);
-    /* squeeze out the newline digit: S = 15 digits right-aligned */
-    const bool has_nl = nlm != 0;
-    uint32_t S = P;
-    if (has_nl) {
-        int j = __ffs(nlm) - 1;                                /* byte index 0..15 */
-        uint32_t lo_bits = 30u - 2u * (uint32_t)j;             /* digits after the '\n' */
-        uint32_t hi = j ? (P >> (32u - 2u * (uint32_t)j)) : 0u;
-        uint32_t lo = lo_bits ? (P & ((1u << lo_bits) - 1u)) : 0u;
-        S = (lo_bits < 32u ? (hi << lo_bits) : 0u) | lo;
-    }
-    uint32_t prev = shup(S, 1);
-    if (lane == 0) prev = (uint32_t)st.code;
-    /* make {C, S2} one contiguous base stream with S2 holding 16 digits */
-    const uint32_t S2 = has_nl ? (S | ((prev & 3u) << 30)) : S;
-    const uint32_t C = has_nl ? (prev >> 2) : prev;
+    uint32_t S0 = pack16(x), S1 = pack16(x + 4);
+    const bool h0 = nl0 != 0, h1 = nl1 != 0;
+    if (h0) S0 = squeeze(S0, nl0);
+    if (h1) S1 = squeeze(S1, nl1);
+    const uint32_t prev = from_prev_lane(S1, (uint32_t)st.code);
+    /* make each {C, S2} one contiguous base stream with S2 holding 16 digits */
+    const uint32_t A2 = h0 ? (S0 | ((prev & 3u) << 30)) : S0;
+    const uint32_t AC = h0 ? (prev >> 2) : prev;
+    const uint32_t B2 = h1 ? (S1 | ((S0 & 3u) << 30)) : S1;
+    const uint32_t BC = h1 ? (S0 >> 2) : S0;
 
-    const uint64_t nlb = __ballot(has_nl);
-    const uint32_t nsym = FK_TILE_BYTES - (uint32_t)__popcll(nlb);
-
+    const uint64_t nb0 = __ballot(h0), nb1 = __ballot(h1);
+    const uint32_t nsym = FK_TILE_BYTES - (uint32_t)__popcll(nb0) - (uint32_t)__popcll(nb1);
     if (COUNT) {
-        const uint32_t m2 = (uint32_t)cx.maskk << 2;
-        if (HM == H_PAIRS) {
-            /* (k+1)-mers ending at odd slots 1,3,..,15 cover the k-mers at
-               slots (0,1),(2,3),... ; a lane with a '\n' has no real slot 0,
-               so its first pair becomes the single k-mer at slot 1 */
-            const uint32_t m3 = (uint32_t)((cx.maskk << 2) | 3u) << 2;
-            char *L = reinterpret_cast<char *>(cx.lds);
-            {
-                uint32_t a7 = __builtin_amdgcn_alignbit(C, S2, 26u) & m3;
-                uint32_t a6 = __builtin_amdgcn_alignbit(C, S2, 26u) & m2;
-                uint32_t addr = has_nl ? (cx.single_off * 4u + a6) : a7;
-                atomicAdd(reinterpret_cast<uint32_t *>(L + addr), weight);
-            }
-#pragma unroll
-            for (int j = 1; j < 7; j++) {
-                uint32_t a = __builtin_amdgcn_alignbit(C, S2, (uint32_t)(26 - 4 * j)) & m3;
-                atomicAdd(reinterpret_cast<uint32_t *>(L + a), weight);
-            }
-            {
-                uint32_t a = (S2 << 2) & m3;
-                atomicAdd(reinterpret_cast<uint32_t *>(L + a), weight);
-            }
-        } else {
-#pragma unroll
-            for (int i = 0; i < 16; i++) {
-                uint32_t sh = 2u * (15u - (uint32_t)i);
-                uint32_t v = i < 15 ? __builtin_amdgcn_alignbit(C, S2, sh) : S2;
-                uint32_t idx = v & (uint32_t)cx.maskk;
-                if (i > 0 || !has_nl) {
-                    if (HM == H_LDS) atomicAdd(&cx.lds[idx], weight);
-                    else atomicAdd(&cx.table[idx], weight);
-                }
-            }
-        }
+        half_windows<HM>(cx, AC, A2, h0, weight);
+        half_windows<HM>(cx, BC, B2, h1, weight);
         if (lane == 0) cnt.win += nsym;
         /* chunk facts: the first '\n' of the chunk */
-        if (!f.found_p1 && nlb) {
-            int L0 = __ffsll((long long)nlb) - 1;
-            uint32_t j0 = (uint32_t)(__ffs(rdlane(nlm, L0)) - 1);
+        if (!f.found_p1 && (nb0 | nb1)) {
+            int L0 = __ffsll((long long)(nb0 | nb1)) - 1;
+            uint32_t a = rdlane(nl0, L0), b = rdlane(nl1, L0);
+            uint32_t j0 = a ? (uint32_t)(__ffs(a) - 1) : 16u + (uint32_t)(__ffs(b) - 1);
             f.found_p1 = 1;
             f.p1_gt = 0;
-            f.R_at_p1 = st.R + (uint32_t)L0 * 16u + j0;
+            f.R_at_p1 = st.R + (uint32_t)L0 * FK_LANE_BYTES + j0;
         }
         f.nv_total += nsym;
     }
     st.R += nsym;
-    st.code = ((uint64_t)rdlane(C, 63) << 32) | rdlane(S2, 63);
+    st.code = ((uint64_t)rdlane(BC, 63) << 32) | rdlane(B2, 63);
     return true;
 }
 
@@ -476,95 +535,101 @@ __device__ void flush_counters(const Ctx &cx, Counters &cnt, uint32_t weight) {
     cnt.valid = cnt.win = 0;
 }
 
-template <bool COUNT, int HM>
-__device__ __forceinline__ void do_tile(const Ctx &cx, const uint32_t w[4], int64_t toff, uint32_t tile_off,
+/* One tile of count_range: the fast path when it qualifies, else the general
+ * path (which also takes a tile only partly inside the input). */
+template <int HM>
+__device__ __forceinline__ void do_tile(const Ctx &cx, const uint32_t w[8], int64_t toff, uint32_t tile_off,
                                         bool full, DState &st, Facts &f, Counters &cnt, uint32_t weight) {
-    if (full && st.hdr == 0 && cx.k <= 16 && tile_fast<COUNT, HM>(cx, w, tile_off, st, f, cnt, weight))
-        return;
+    if (full && st.hdr == 0 && tile_fast<true, HM>(cx, w, st, f, cnt, weight)) return;
     const int lane = threadIdx.x & 63;
-    uint32_t v[4] = {w[0], w[1], w[2], w[3]};
-    int nb = 16;
-    if (!full) nb = load16(cx, toff + lane * 16, v);
-    tile_general<COUNT, HM>(cx, v, nb, tile_off, st, f, cnt, weight);
+    uint32_t v[8];
+    int nb = FK_LANE_BYTES;
+    if (full) {
+#pragma unroll
+        for (int d = 0; d < 8; d++) v[d] = w[d];
+    } else {
+        nb = load_lane<FK_LANE_BYTES>(cx, toff + lane * (int64_t)FK_LANE_BYTES, v);
+    }
+    tile_general<true, HM>(cx, v, nb, tile_off, st, f, cnt, weight);
 }
 
-/* Count one chunk from entering state st; returns the exit state. */
+/* Bytes [rbase, rend) of a range and its tile count. */
+struct Span {
+    uint64_t rbase, rend, ntiles, nfull;
+};
+__device__ __forceinline__ Span range_span(const RangeRec &r, uint64_t len) {
+    Span s;
+    s.rbase = r.c0 * FK_CHUNK_BYTES;
+    s.rend = min(r.c1 * FK_CHUNK_BYTES, len);
+    s.ntiles = (s.rend - s.rbase + FK_TILE_BYTES - 1) / FK_TILE_BYTES;
+    s.nfull = (s.rend - s.rbase) / FK_TILE_BYTES;
+    return s;
+}
+
+/* Count tiles [t0, sp.ntiles) of a range from state st (weight 1, or
+ * 0xFFFFFFFF to cancel), any bytes.  Tile t+1's loads stay in flight while
+ * tile t is counted (A/B ping-pong). */
 template <int HM>
-__device__ DState count_chunk(const Ctx &cx, uint64_t chunk, DState st, uint32_t weight,
-                              ChunkRec *rec, bool write_facts, bool write_obs) {
+__device__ void count_range(const Ctx &cx, const Span &sp, uint64_t t0, DState &st, Facts &f,
+                            Counters &cnt, uint32_t weight) {
     const int lane = threadIdx.x & 63;
-    const int64_t start = (int64_t)(chunk * FK_CHUNK_BYTES);
-    const uint64_t clen = min((uint64_t)FK_CHUNK_BYTES, cx.len - (uint64_t)start);
-    const uint32_t ntiles = (uint32_t)((clen + FK_TILE_BYTES - 1) / FK_TILE_BYTES);
-    Facts f{0, 0, 0, 0, 0, 0};
-    Counters cnt{0, 0, 0, 0, 0, FK_NO_EOF};
-    const DState a = st;
-    /* 4-tile groups, next group's loads in flight while this one is counted */
-    uint32_t g[4][4], nx[4][4];
-#define FK_LOADG(dst, grp)                                                           \
-    _Pragma("unroll") for (int q = 0; q < 4; q++) {                                  \
-        uint32_t t_ = (grp) * 4u + (uint32_t)q;                                      \
-        int64_t o_ = start + (int64_t)t_ * FK_TILE_BYTES + lane * 16;                \
-        if (t_ < ntiles && o_ + 16 <= (int64_t)cx.len) {                             \
-            u32x4 v_ = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(cx.buf + o_)); \
-            dst[q][0] = v_.x; dst[q][1] = v_.y; dst[q][2] = v_.z; dst[q][3] = v_.w;   \
-        } else {                                                                     \
-            dst[q][0] = dst[q][1] = dst[q][2] = dst[q][3] = 0;                       \
-        }                                                                            \
+    uint32_t A[8], B[8];
+    /* unconditional loads clamped into the range keep the vmcnt accounting
+       static; a tile only partly inside the input is reloaded by do_tile */
+#define FK_LOADT(dst, t_)                                                            \
+    {                                                                                \
+        uint64_t o_ = sp.rbase + (uint64_t)(t_) * FK_TILE_BYTES + (uint64_t)lane * FK_LANE_BYTES; \
+        o_ = min(o_, sp.rend - FK_LANE_BYTES);                                       \
+        const u32x4 *p_ = reinterpret_cast<const u32x4 *>(cx.buf + o_);              \
+        u32x4 v0_ = __builtin_nontemporal_load(p_);                                  \
+        u32x4 v1_ = __builtin_nontemporal_load(p_ + 1);                              \
+        dst[0] = v0_.x; dst[1] = v0_.y; dst[2] = v0_.z; dst[3] = v0_.w;               \
+        dst[4] = v1_.x; dst[5] = v1_.y; dst[6] = v1_.z; dst[7] = v1_.w;               \
     }
-    const uint32_t ngroups = (ntiles + 3) / 4;
-    FK_LOADG(g, 0u);
-    for (uint32_t grp = 0; grp < ngroups; grp++) {
-        if (grp + 1 < ngroups) { FK_LOADG(nx, grp + 1); }
-#pragma unroll
-        for (int q = 0; q < 4; q++) {
-            uint32_t t = grp * 4u + (uint32_t)q;
-            if (t < ntiles) {
-                int64_t toff = start + (int64_t)t * FK_TILE_BYTES;
-                bool full = toff + (int64_t)FK_TILE_BYTES <= (int64_t)cx.len;
-                do_tile<true, HM>(cx, g[q], toff, t * FK_TILE_BYTES, full, st, f, cnt, weight);
-            }
-        }
-#pragma unroll
-        for (int q = 0; q < 4; q++)
-#pragma unroll
-            for (int d = 0; d < 4; d++) g[q][d] = nx[q][d];
+#define FK_DOT(buf_, t_)                                                             \
+    {                                                                                \
+        do_tile<HM>(cx, buf_, (int64_t)(sp.rbase + (uint64_t)(t_) * FK_TILE_BYTES),  \
+                    (uint32_t)((t_) * FK_TILE_BYTES), (t_) < sp.nfull, st, f, cnt, weight); \
     }
-#undef FK_LOADG
+    FK_LOADT(A, t0);
+    for (uint64_t t = t0; t < sp.ntiles; t += 2) {
+        FK_LOADT(B, t + 1);
+        FK_DOT(A, t);
+        if (t + 1 >= sp.ntiles) break;
+        FK_LOADT(A, t + 2);
+        FK_DOT(B, t + 1);
+    }
+#undef FK_DOT
+    (void)lane;
+}
+
+/* Flush a range's counters; lane 0 records its observations in rr. */
+__device__ void range_obs(const Ctx &cx, Counters &cnt, uint32_t weight, const Span &sp, RangeRec *r,
+                          bool write) {
     flush_counters(cx, cnt, weight);
-    uint32_t unk = wsum32(cnt.unknown);
-    uint32_t eof = wmin32(cnt.eof);
-    if (lane == 0 && eof != FK_NO_EOF && weight == 1u)
-        atomicMin(&cx.res->eof_cand, (unsigned long long)(chunk * FK_CHUNK_BYTES + eof));
-    if (lane == 0) {
-        ChunkRec &r = rec[chunk];
-        if (write_facts) {
-            r.a_code = a.code; r.a_R = a.R; r.a_hdr = a.hdr;
-            r.x_code = st.code; r.x_R = st.R; r.x_hdr = st.hdr;
-            r.flags = (f.found_p1 ? CR_FOUND_P1 : 0u) | (f.p1_gt ? CR_P1_GT : 0u) |
-                      (f.any_reset ? CR_ANY_RESET : 0u) |
-                      (f.reset_after_p1 ? CR_RESET_AFTER_P1 : 0u);
-            r.R_at_p1 = f.R_at_p1;
-            r.nv_total = f.nv_total;
-        }
-        if (write_obs) {
-            r.unknown = unk;
-            r.eof_off = eof;
+    const uint32_t unk = wsum32(cnt.unknown);
+    const uint32_t eof = wmin32(cnt.eof);
+    if ((threadIdx.x & 63) == 0 && weight == 1u) {
+        if (eof != FK_NO_EOF) atomicMin(&cx.res->eof_cand, (unsigned long long)(sp.rbase + eof));
+        if (write) {
+            r->eof = eof == FK_NO_EOF ? FK_NO_EOF64 : (uint64_t)eof;
+            r->unknown = unk;
         }
     }
-    return st;
 }
 
-/* Guess the state entering `chunk` from the FK_HALO_BYTES before it. */
+/* Guess the state entering byte `start` from the FK_HALO_BYTES before it. */
 template <int HM>
-__device__ DState halo_state(const Ctx &cx, uint64_t chunk) {
+__device__ DState halo_state(const Ctx &cx, uint64_t start) {
     const int lane = threadIdx.x & 63;
-    const int64_t start = (int64_t)(chunk * FK_CHUNK_BYTES);
-    const int64_t hs = start - (int64_t)FK_HALO_BYTES;
-    uint32_t w[4];
+    const int64_t hs = (int64_t)start - (int64_t)FK_HALO_BYTES;
+    uint32_t w[8];
     int nb = 0;
-    if (lane < (int)(FK_HALO_BYTES / 16)) nb = load16(cx, hs + lane * 16, w);
-    else { w[0] = w[1] = w[2] = w[3] = 0; }
+    if (lane < (int)(FK_HALO_BYTES / FK_LANE_BYTES)) nb = load_lane<FK_LANE_BYTES>(cx, hs + lane * (int64_t)FK_LANE_BYTES, w);
+    else {
+#pragma unroll
+        for (int d = 0; d < 8; d++) w[d] = 0;
+    }
     DState st{0, 0, 0};
     Facts f{0, 0, 0, 0, 0, 0};
     Counters cnt{0, 0, 0, 0, 0, FK_NO_EOF};
@@ -597,93 +662,187 @@ __device__ void lds_flush(const Ctx &cx) {
         } else {
             v = cx.lds[i];
         }
-        if (v) atomicAdd(&cx.table[i], v);
+        if (v) atomicAdd(&cx.table[fk_sigma(i)], v);
     }
 }
 
 /*
- * k_count: main pass.  Wave w counts the contiguous chunk range
- * [w*cpw, (w+1)*cpw): the first chunk of the range guesses its entering state
- * from its halo (or takes the known stream state *d_init for chunk 0), the
- * next ones continue from the previous chunk's exit.  At the end lane 0
- * composes the range's chunk transfer functions into rr[w].
+ * k_count: main pass, fast path only.  Wave w owns the chunk range
+ * [w*cpw, (w+1)*cpw); its entering state is guessed from the halo before it
+ * (or is the known stream state *d_init for chunk 0).  The wave streams the
+ * range's tiles with three tiles in flight and counts them with tile_fast;
+ * nothing else is in the loop (no byte walk, no stores), so the loads stay
+ * in flight across chunk boundaries.  The first tile the fast path cannot
+ * take (header, run break, several newlines per half, the input's ragged
+ * end) ends the wave's work: it appends a ResumeRec and k_resume continues
+ * the range from there.  A range counted to its end gets its RangeRec here.
  */
 template <int HM>
-__global__ void __launch_bounds__(FK_BLOCK, 4)
+__global__ void __launch_bounds__(FK_BLOCK, 2)
 k_count(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint32_t *table,
-        uint32_t *shortcnt, unsigned long long *acc, DevRes *res, ChunkRec *rec, RangeRec *rr,
-        uint64_t nchunks, const XState *d_init, int has_init, uint64_t cpw) {
+        uint32_t *shortcnt, unsigned long long *acc, DevRes *res, RangeRec *rr,
+        uint64_t nchunks, const XState *d_init, int has_init, uint64_t cpw, ResumeRec *resume) {
     extern __shared__ uint32_t lds_bins[];
     const uint32_t nw = lds_words(HM, k);
     if (HM != H_GLOBAL) lds_zero(lds_bins, nw);
     Ctx cx{buf, len, lo, table, HM != H_GLOBAL ? lds_bins : nullptr, shortcnt, acc, res, maskk,
            1u << (2 * k + 2), k};
-    const uint64_t wave = blockIdx.x * FK_WAVES_PER_BLOCK + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const uint64_t wave = blockIdx.x * FK_WAVES_PER_BLOCK + wave_in_block();
     const uint64_t c0 = wave * cpw, c1 = min(c0 + cpw, nchunks);
-    DState st{0, 0, 0};
-    DState first{0, 0, 0};
-    for (uint64_t c = c0; c < c1; c++) {
-        if (c == c0) {
-            if (c == 0 && has_init) {
-                st.hdr = d_init->hdr;
-                st.R = (uint32_t)d_init->R;
-                st.code = d_init->code;
-            } else {
-                st = halo_state<HM>(cx, c);
-            }
-            first = st;
+    if (c0 < c1) {
+        RangeRec hdr_r;
+        hdr_r.c0 = c0;
+        hdr_r.c1 = c1;
+        const Span sp = range_span(hdr_r, len);
+        DState st;
+        if (c0 == 0 && has_init) {
+            st.hdr = d_init->hdr;
+            st.R = (uint32_t)d_init->R;
+            st.code = d_init->code;
+        } else {
+            st = halo_state<HM>(cx, sp.rbase);
         }
-        st = count_chunk<HM>(cx, c, st, 1u, rec, true, true);
+        const DState first = st;
+        Facts f{0, 0, 0, 0, 0, 0};
+        Counters cnt{0, 0, 0, 0, 0, FK_NO_EOF};
+        uint32_t A[8], B[8], C[8];
+        uint64_t t = 0;
+        /* issue order A, B, C as in the loop (the barriers keep the compiler
+           from reordering them, which would merge two different pending-load
+           orders at the loop header) */
+        FK_LOADT(A, 0);
+        asm volatile("" ::: "memory");
+        FK_LOADT(B, 1);
+        asm volatile("" ::: "memory");
+        FK_LOADT(C, 2);
+        /* one exit per group of three tiles and unconditional loads: every
+           path into the latch has the same loads in flight, so each tile waits
+           only for its own data */
+        bool live = st.hdr == 0;
+        for (uint64_t g = 0; live; g += 3) {
+            live = t < sp.nfull && tile_fast<true, HM>(cx, A, st, f, cnt, 1u);
+            t += live;
+            consume(A);
+            FK_LOADT(A, g + 3);
+            live = live && t < sp.nfull && tile_fast<true, HM>(cx, B, st, f, cnt, 1u);
+            t += live;
+            consume(B);
+            FK_LOADT(B, g + 4);
+            live = live && t < sp.nfull && tile_fast<true, HM>(cx, C, st, f, cnt, 1u);
+            t += live;
+            consume(C);
+            FK_LOADT(C, g + 5);
+        }
+        if (lane == 0) {
+            if (f.nv_total) atomicAdd(&acc[ACC_WIN], (unsigned long long)f.nv_total);
+            if (t < sp.ntiles) {
+                const uint32_t slot = atomicAdd(&res->resume_n, 1u);
+                ResumeRec q;
+                q.tile = t;
+                q.code = st.code; q.R = st.R; q.hdr = st.hdr;
+                q.a_code = first.code; q.a_R = first.R; q.a_hdr = first.hdr;
+                q.range = (uint32_t)wave;
+                q.pad = 0;
+                q.f = f;
+                resume[slot] = q;
+            } else {
+                RangeRec r;
+                r.tf = fk_tf_span(first, st, f);
+                r.a_code = first.code; r.a_R = first.R; r.a_hdr = first.hdr;
+                r.c0 = c0; r.c1 = c1;
+                r.eof = FK_NO_EOF64;
+                r.unknown = 0;
+                r.pad = 0;
+                rr[wave] = r;
+            }
+        }
     }
     if (HM != H_GLOBAL) lds_flush<HM>(cx);
-    if (c0 < c1 && (threadIdx.x & 63) == 0) {
-        TF t = fk_identity();
-        for (uint64_t c = c0; c < c1; c++) t = fk_compose(t, fk_tf_of(rec[c]));
-        RangeRec &r = rr[wave];
-        r.tf = t;
-        r.a_code = first.code; r.a_R = first.R; r.a_hdr = first.hdr;
-        r.c0 = c0; r.c1 = c1;
+}
+#undef FK_LOADT
+
+/*
+ * k_resume: finish the ranges k_count stopped in, one wave per range, with
+ * the general path wherever the fast path does not apply, and write their
+ * RangeRecs.
+ */
+template <int HM>
+__global__ void __launch_bounds__(FK_BLOCK)
+k_resume(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint32_t *table,
+         uint32_t *shortcnt, unsigned long long *acc, DevRes *res, RangeRec *rr, uint64_t nchunks,
+         uint64_t cpw, const ResumeRec *resume) {
+    extern __shared__ uint32_t lds_bins[];
+    const uint64_t n = res->resume_n;
+    if ((uint64_t)blockIdx.x * FK_WAVES_PER_BLOCK >= n) return;   /* uniform per block */
+    const uint32_t nw = lds_words(HM, k);
+    if (HM != H_GLOBAL) lds_zero(lds_bins, nw);
+    Ctx cx{buf, len, lo, table, HM != H_GLOBAL ? lds_bins : nullptr, shortcnt, acc, res, maskk,
+           1u << (2 * k + 2), k};
+    const uint64_t wave = blockIdx.x * FK_WAVES_PER_BLOCK + wave_in_block();
+    const uint64_t nwaves = (uint64_t)gridDim.x * FK_WAVES_PER_BLOCK;
+    for (uint64_t i = wave; i < n; i += nwaves) {
+        const ResumeRec q = resume[i];
+        RangeRec r;
+        r.c0 = (uint64_t)q.range * cpw;
+        r.c1 = min(r.c0 + cpw, nchunks);
+        const Span sp = range_span(r, len);
+        DState st{q.code, q.R, q.hdr};
+        const DState a{q.a_code, q.a_R, q.a_hdr};
+        Facts f = q.f;
+        Counters cnt{0, 0, 0, 0, 0, FK_NO_EOF};
+        count_range<HM>(cx, sp, q.tile, st, f, cnt, 1u);
+        r.tf = fk_tf_span(a, st, f);
+        r.a_code = a.code; r.a_R = a.R; r.a_hdr = a.hdr;
+        r.pad = 0;
+        range_obs(cx, cnt, 1u, sp, &r, true);
+        if ((threadIdx.x & 63) == 0) rr[q.range] = r;
     }
+    if (HM != H_GLOBAL) lds_flush<HM>(cx);
 }
 
 /*
- * k_redo, mode 0: for each listed range, walk its chunks from the exact
- * entering state; a chunk whose guessed entering state (rec[c].a) would count
- * differently is cancelled (weight -1 from the guess) and recounted (weight
- * +1 from the exact state).  mode 1: cancel every chunk of every range (a
- * 0xFF byte truncates the input and the segment is recounted).
+ * k_redo, mode 0: each listed range (its guessed entering state would count
+ * differently from the exact one) is counted again with weight -1 from the
+ * guess, cancelling k_count + k_resume exactly, and with weight +1 from the
+ * exact state, which also replaces its observations.  mode 1: cancel every
+ * range from its exact state (a 0xFF byte truncates the input and the
+ * segment is recounted).
  */
 template <int HM>
-__global__ void __launch_bounds__(FK_BLOCK, 4)
+__global__ void __launch_bounds__(FK_BLOCK)
 k_redo(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint32_t *table,
-       uint32_t *shortcnt, unsigned long long *acc, DevRes *res, ChunkRec *rec, const RangeRec *rr,
+       uint32_t *shortcnt, unsigned long long *acc, DevRes *res, RangeRec *rr,
        const XState *rtrue, const uint32_t *list, uint64_t nranges, int mode) {
     extern __shared__ uint32_t lds_bins[];
     const uint64_t n = mode == 1 ? nranges : (uint64_t)res->redo_n;
-    if (n == 0) return;   /* uniform across the grid */
+    if ((uint64_t)blockIdx.x * FK_WAVES_PER_BLOCK >= n) return;   /* uniform per block */
     const uint32_t nw = lds_words(HM, k);
     if (HM != H_GLOBAL) lds_zero(lds_bins, nw);
     Ctx cx{buf, len, lo, table, HM != H_GLOBAL ? lds_bins : nullptr, shortcnt, acc, res, maskk,
            1u << (2 * k + 2), k};
-    const uint64_t wave = blockIdx.x * FK_WAVES_PER_BLOCK + (threadIdx.x >> 6);
+    const uint64_t wave = blockIdx.x * FK_WAVES_PER_BLOCK + wave_in_block();
     const uint64_t nwaves = (uint64_t)gridDim.x * FK_WAVES_PER_BLOCK;
     for (uint64_t i = wave; i < n; i += nwaves) {
         const uint64_t r = mode == 1 ? i : list[i];
-        XState t = rtrue[r];
-        const uint64_t c0 = rr[r].c0, c1 = rr[r].c1;
-        for (uint64_t c = c0; c < c1; c++) {
-            const ChunkRec cr = rec[c];
-            DState ts{t.code, (uint32_t)t.R, t.hdr};
-            if (mode == 1) {
-                count_chunk<HM>(cx, c, ts, 0xFFFFFFFFu, rec, false, false);
-            } else {
-                DState as{cr.a_code, cr.a_R, cr.a_hdr};
-                if (!fk_equiv(as, t, k, FK_CHUNK_BYTES)) {
-                    count_chunk<HM>(cx, c, as, 0xFFFFFFFFu, rec, false, false);
-                    count_chunk<HM>(cx, c, ts, 1u, rec, false, true);
-                }
-            }
-            t = fk_apply(fk_tf_of(cr), t);
+        RangeRec q = rr[r];
+        const Span sp = range_span(q, len);
+        const XState t = rtrue[r];
+        DState ts{t.code, (uint32_t)t.R, t.hdr};
+        Facts f{0, 0, 0, 0, 0, 0};
+        Counters cnt{0, 0, 0, 0, 0, FK_NO_EOF};
+        if (mode == 1) {
+            count_range<HM>(cx, sp, 0, ts, f, cnt, 0xFFFFFFFFu);
+            flush_counters(cx, cnt, 0xFFFFFFFFu);
+        } else {
+            DState as{q.a_code, q.a_R, q.a_hdr};
+            count_range<HM>(cx, sp, 0, as, f, cnt, 0xFFFFFFFFu);
+            flush_counters(cx, cnt, 0xFFFFFFFFu);
+            cnt = Counters{0, 0, 0, 0, 0, FK_NO_EOF};
+            f = Facts{0, 0, 0, 0, 0, 0};
+            count_range<HM>(cx, sp, 0, ts, f, cnt, 1u);
+            range_obs(cx, cnt, 1u, sp, &q, true);
+            if ((threadIdx.x & 63) == 0) { rr[r].eof = q.eof; rr[r].unknown = q.unknown; }
         }
     }
     if (HM != H_GLOBAL) lds_flush<HM>(cx);
@@ -737,18 +896,6 @@ k_scan(const RangeRec *rr, uint64_t n, XState *d_state, XState *rtrue, uint32_t 
         XState fin = fk_apply(agg[SCAN_THREADS - 1], init);
         *d_state = fin;
         res->exit = fin;
-    }
-}
-
-/* exact entering state of every chunk (for the unknown-byte extraction) */
-__global__ void k_expand(const ChunkRec *rec, const RangeRec *rr, const XState *rtrue, uint64_t nranges,
-                         XState *strue) {
-    uint64_t r = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
-    if (r >= nranges) return;
-    XState t = rtrue[r];
-    for (uint64_t c = rr[r].c0; c < rr[r].c1; c++) {
-        strue[c] = t;
-        t = fk_apply(fk_tf_of(rec[c]), t);
     }
 }
 
@@ -844,25 +991,26 @@ __device__ __forceinline__ uint32_t lane_hdr_entry(const uint32_t w[4], int nb, 
 /*
  * k_extract: copy the bytes that make the reference print "Unknown character
  * %c processed!" (:581-584) to out[], in stream order.  One wave per listed
- * chunk, entering header flag from the exact state scan.
+ * range, entering header flag from the exact state scan.
  */
 __global__ void __launch_bounds__(FK_BLOCK)
-k_extract(const uint8_t *buf, uint64_t len, int64_t lo, const XState *s_true, const uint32_t *list,
-          const uint64_t *offs, uint32_t nlist, uint8_t *out) {
+k_extract(const uint8_t *buf, uint64_t len, int64_t lo, const RangeRec *rr, const XState *rtrue,
+          const uint32_t *list, const uint64_t *offs, uint32_t nlist, uint8_t *out) {
     const int lane = threadIdx.x & 63;
     Ctx cx{buf, len, lo, nullptr, nullptr, nullptr, nullptr, nullptr, 0, 0, 0};
-    const uint64_t wave = blockIdx.x * FK_WAVES_PER_BLOCK + (threadIdx.x >> 6);
+    const uint64_t wave = blockIdx.x * FK_WAVES_PER_BLOCK + wave_in_block();
     const uint64_t nwaves = (uint64_t)gridDim.x * FK_WAVES_PER_BLOCK;
     for (uint64_t i = wave; i < nlist; i += nwaves) {
-        const uint64_t c = list[i];
-        uint32_t hdr = s_true[c].hdr;
+        const uint32_t r = list[i];
+        const Span sp = range_span(rr[r], len);
+        uint32_t hdr = rtrue[r].hdr;
         uint64_t base = offs[i];
-        const int64_t start = (int64_t)(c * FK_CHUNK_BYTES);
-        const uint64_t clen = min((uint64_t)FK_CHUNK_BYTES, len - (uint64_t)start);
-        const uint32_t ntiles = (uint32_t)((clen + FK_TILE_BYTES - 1) / FK_TILE_BYTES);
-        for (uint32_t t = 0; t < ntiles; t++) {
+        const uint64_t ntiles = (sp.rend - sp.rbase + 1023) / 1024;
+        for (uint64_t t = 0; t < ntiles; t++) {
             uint32_t w[4];
-            int nb = load16(cx, start + (int64_t)t * FK_TILE_BYTES + lane * 16, w);
+            const int64_t toff = (int64_t)(sp.rbase + t * 1024);
+            int nb = load_lane<16>(cx, toff + lane * 16, w);
+            nb = (int)min((int64_t)nb, max((int64_t)0, (int64_t)sp.rend - (toff + lane * 16)));
             uint32_t h = lane_hdr_entry(w, nb, hdr);
             uint32_t cntu = 0;
 #pragma unroll
@@ -973,12 +1121,12 @@ struct fk_engine {
     DevRes *d_res = nullptr;                  /* per feed */
     unsigned long long *d_tmp = nullptr;      /* scratch counters */
     XState *d_state = nullptr;                /* entering state of the next feed */
-    ChunkRec *d_rec = nullptr;
     RangeRec *d_rr = nullptr;
-    XState *d_rtrue = nullptr, *d_strue = nullptr;
+    XState *d_rtrue = nullptr;
     uint32_t *d_redo = nullptr;
+    ResumeRec *d_resume = nullptr;            /* ranges k_count hands to k_resume */
     TF *d_tf = nullptr;
-    uint64_t chunk_cap = 0, range_cap = 0;
+    uint64_t range_cap = 0;
     uint8_t *d_stage = nullptr, *h_stage = nullptr;
     hipEvent_t ev[3] = {};
     /* host bookkeeping */
@@ -1062,8 +1210,8 @@ extern "C" void fk_engine_destroy(fk_engine *e) {
     hipSetDevice(e->dev);
     if (e->stream) hipStreamSynchronize(e->stream);
     hipFree(e->d_table); hipFree(e->d_short); hipFree(e->d_acc); hipFree(e->d_res); hipFree(e->d_tmp);
-    hipFree(e->d_state); hipFree(e->d_rec); hipFree(e->d_rr); hipFree(e->d_rtrue); hipFree(e->d_strue);
-    hipFree(e->d_redo); hipFree(e->d_tf); hipFree(e->d_stage);
+    hipFree(e->d_state); hipFree(e->d_rr); hipFree(e->d_rtrue);
+    hipFree(e->d_redo); hipFree(e->d_tf); hipFree(e->d_stage); hipFree(e->d_resume);
     if (e->h_stage) hipHostFree(e->h_stage);
     for (int i = 0; i < 3; i++) if (e->ev[i]) hipEventDestroy(e->ev[i]);
     if (e->own_stream && e->stream) hipStreamDestroy(e->stream);
@@ -1112,6 +1260,7 @@ extern "C" int fk_engine_create(int k, const fk_opts *opts, fk_engine **out) {
     if (sh > 65536) {
         hipFuncSetAttribute((const void *)k_count<H_PAIRS>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh);
         hipFuncSetAttribute((const void *)k_redo<H_PAIRS>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh);
+        hipFuncSetAttribute((const void *)k_resume<H_PAIRS>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh);
     }
     for (int i = 0; i < 3; i++)
         if (hipEventCreate(&e->ev[i]) != hipSuccess) { fk_engine_destroy(e); return FK_E_HIP; }
@@ -1129,22 +1278,16 @@ extern "C" int fk_engine_reset(fk_engine *e) {
     return zero_all(e);
 }
 
-/* per-chunk and per-range arrays */
-static int grow_arrays(fk_engine *e, uint64_t nchunks, uint64_t nranges) {
-    if (nchunks > e->chunk_cap || !e->d_rec) {
-        uint64_t nc = std::max<uint64_t>(nchunks, 1024);
-        hipFree(e->d_rec); hipFree(e->d_strue);
-        e->d_rec = nullptr; e->d_strue = nullptr;
-        if (hipMalloc((void **)&e->d_rec, nc * sizeof(ChunkRec)) != hipSuccess) return FK_E_OOM;
-        e->chunk_cap = nc;
-    }
+/* per-range arrays */
+static int grow_arrays(fk_engine *e, uint64_t nranges) {
     if (nranges > e->range_cap || !e->d_rr) {
         uint64_t nr = std::max<uint64_t>(nranges, 1024);
-        hipFree(e->d_rr); hipFree(e->d_rtrue); hipFree(e->d_redo);
-        e->d_rr = nullptr; e->d_rtrue = nullptr; e->d_redo = nullptr;
+        hipFree(e->d_rr); hipFree(e->d_rtrue); hipFree(e->d_redo); hipFree(e->d_resume);
+        e->d_rr = nullptr; e->d_rtrue = nullptr; e->d_redo = nullptr; e->d_resume = nullptr;
         if (hipMalloc((void **)&e->d_rr, nr * sizeof(RangeRec)) != hipSuccess) return FK_E_OOM;
         if (hipMalloc((void **)&e->d_rtrue, nr * sizeof(XState)) != hipSuccess) return FK_E_OOM;
         if (hipMalloc((void **)&e->d_redo, nr * sizeof(uint32_t)) != hipSuccess) return FK_E_OOM;
+        if (hipMalloc((void **)&e->d_resume, nr * sizeof(ResumeRec)) != hipSuccess) return FK_E_OOM;
         e->range_cap = nr;
     }
     return FK_OK;
@@ -1177,18 +1320,27 @@ static int launch_count(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t 
     size_t sh = lds_bytes(e);
     FK_DISPATCH(hist_mode(e),
                 hipLaunchKernelGGL((k_count<HM>), dim3(g.grid), dim3(FK_BLOCK), sh, e->stream, buf, len, lo, e->k,
-                                   e->maskk, e->d_table, e->d_short, e->d_acc, e->d_res, e->d_rec, e->d_rr,
-                                   g.nchunks, e->d_state, has_init, g.cpw));
+                                   e->maskk, e->d_table, e->d_short, e->d_acc, e->d_res, e->d_rr,
+                                   g.nchunks, e->d_state, has_init, g.cpw, e->d_resume));
+    HIPCHK(hipGetLastError());
+    return FK_OK;
+}
+
+static int launch_resume(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t lo, const Geo &g) {
+    size_t sh = lds_bytes(e);
+    FK_DISPATCH(hist_mode(e),
+                hipLaunchKernelGGL((k_resume<HM>), dim3(g.grid), dim3(FK_BLOCK), sh, e->stream, buf, len, lo, e->k,
+                                   e->maskk, e->d_table, e->d_short, e->d_acc, e->d_res, e->d_rr, g.nchunks,
+                                   g.cpw, e->d_resume));
     HIPCHK(hipGetLastError());
     return FK_OK;
 }
 
 static int launch_redo(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t lo, const Geo &g, int mode) {
     size_t sh = lds_bytes(e);
-    unsigned grid = mode == 1 ? g.grid : (unsigned)std::min<uint64_t>(g.grid, (uint64_t)e->cus);
     FK_DISPATCH(hist_mode(e),
-                hipLaunchKernelGGL((k_redo<HM>), dim3(grid), dim3(FK_BLOCK), sh, e->stream, buf, len, lo, e->k,
-                                   e->maskk, e->d_table, e->d_short, e->d_acc, e->d_res, e->d_rec, e->d_rr,
+                hipLaunchKernelGGL((k_redo<HM>), dim3(g.grid), dim3(FK_BLOCK), sh, e->stream, buf, len, lo, e->k,
+                                   e->maskk, e->d_table, e->d_short, e->d_acc, e->d_res, e->d_rr,
                                    e->d_rtrue, e->d_redo, g.nranges, mode));
     HIPCHK(hipGetLastError());
     return FK_OK;
@@ -1212,7 +1364,7 @@ static int launch_table_stats(fk_engine *e) {
 
 /* Reset the per-feed result block (redo count, eof candidate). */
 static int res_begin(fk_engine *e) {
-    HIPCHK(hipMemsetAsync(&e->d_res->redo_n, 0, sizeof(uint32_t), e->stream));
+    HIPCHK(hipMemsetAsync(&e->d_res->redo_n, 0, 2 * sizeof(uint32_t), e->stream));   /* redo_n, resume_n */
     HIPCHK(hipMemsetAsync(&e->d_res->eof_cand, 0xFF, sizeof(unsigned long long), e->stream));
     return FK_OK;
 }
@@ -1233,18 +1385,18 @@ static int resolve_and_fetch(fk_engine *e, const uint8_t *buf, uint64_t len, int
     return FK_OK;
 }
 
-/* exact first 0xFF outside a header (per-chunk records are exact after redo) */
-__global__ void k_obs_eof(const ChunkRec *rec, uint64_t n, unsigned long long *out) {
+/* exact first 0xFF outside a header (range observations are exact after redo) */
+__global__ void k_obs_eof(const RangeRec *rr, uint64_t n, unsigned long long *out) {
     unsigned long long eof = ~0ull;
-    for (uint64_t c = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; c < n; c += (uint64_t)gridDim.x * blockDim.x)
-        if (rec[c].eof_off != FK_NO_EOF) eof = min(eof, (unsigned long long)(c * FK_CHUNK_BYTES + rec[c].eof_off));
+    for (uint64_t r = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; r < n; r += (uint64_t)gridDim.x * blockDim.x)
+        if (rr[r].eof != FK_NO_EOF64) eof = min(eof, (unsigned long long)(rr[r].c0 * FK_CHUNK_BYTES + rr[r].eof));
     if (eof != ~0ull) atomicMin(out, eof);
 }
 
 static int exact_eof(fk_engine *e, const Geo &g, unsigned long long &eof) {
     HIPCHK(hipMemsetAsync(e->d_tmp, 0xFF, sizeof(unsigned long long), e->stream));
-    unsigned gr = (unsigned)std::min<uint64_t>(1024, g.nchunks / 256 + 1);
-    hipLaunchKernelGGL(k_obs_eof, dim3(gr), dim3(256), 0, e->stream, e->d_rec, g.nchunks, e->d_tmp);
+    unsigned gr = (unsigned)std::min<uint64_t>(1024, g.nranges / 256 + 1);
+    hipLaunchKernelGGL(k_obs_eof, dim3(gr), dim3(256), 0, e->stream, e->d_rr, g.nranges, e->d_tmp);
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpyAsync(&eof, e->d_tmp, sizeof eof, hipMemcpyDeviceToHost, e->stream));
     HIPCHK(hipStreamSynchronize(e->stream));
@@ -1254,19 +1406,15 @@ static int exact_eof(fk_engine *e, const Geo &g, unsigned long long &eof) {
 /* Collect the unknown bytes of the just-counted segment (stream order). */
 static int collect_unknown(fk_engine *e, const uint8_t *dbuf, uint64_t len, int64_t lo, const Geo &g) {
     if (!e->opts.collect_unknown) return FK_OK;
-    std::vector<ChunkRec> rec((size_t)g.nchunks);
-    HIPCHK(hipMemcpyAsync(rec.data(), e->d_rec, g.nchunks * sizeof(ChunkRec), hipMemcpyDeviceToHost, e->stream));
+    std::vector<RangeRec> rr((size_t)g.nranges);
+    HIPCHK(hipMemcpyAsync(rr.data(), e->d_rr, g.nranges * sizeof(RangeRec), hipMemcpyDeviceToHost, e->stream));
     HIPCHK(hipStreamSynchronize(e->stream));
     std::vector<uint32_t> list;
     std::vector<uint64_t> offs;
     uint64_t acc = 0;
-    for (uint64_t c = 0; c < g.nchunks; c++)
-        if (rec[(size_t)c].unknown) { list.push_back((uint32_t)c); offs.push_back(acc); acc += rec[(size_t)c].unknown; }
+    for (uint64_t r = 0; r < g.nranges; r++)
+        if (rr[(size_t)r].unknown) { list.push_back((uint32_t)r); offs.push_back(acc); acc += rr[(size_t)r].unknown; }
     if (!acc) return FK_OK;
-    if (!e->d_strue && hipMalloc((void **)&e->d_strue, e->chunk_cap * sizeof(XState)) != hipSuccess) return FK_E_OOM;
-    hipLaunchKernelGGL(k_expand, dim3((unsigned)((g.nranges + 255) / 256)), dim3(256), 0, e->stream, e->d_rec, e->d_rr,
-                       e->d_rtrue, g.nranges, e->d_strue);
-    HIPCHK(hipGetLastError());
     uint32_t *d_list = nullptr;
     uint64_t *d_offs = nullptr;
     uint8_t *d_out = nullptr;
@@ -1279,8 +1427,8 @@ static int collect_unknown(fk_engine *e, const uint8_t *dbuf, uint64_t len, int6
     HIPCHK(hipMemcpyAsync(d_list, list.data(), list.size() * 4, hipMemcpyHostToDevice, e->stream));
     HIPCHK(hipMemcpyAsync(d_offs, offs.data(), offs.size() * 8, hipMemcpyHostToDevice, e->stream));
     unsigned gx = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((list.size() + 7) / 8, (uint64_t)e->cus * 2));
-    hipLaunchKernelGGL(k_extract, dim3(gx), dim3(FK_BLOCK), 0, e->stream, dbuf, len, lo, e->d_strue, d_list, d_offs,
-                       (uint32_t)list.size(), d_out);
+    hipLaunchKernelGGL(k_extract, dim3(gx), dim3(FK_BLOCK), 0, e->stream, dbuf, len, lo, e->d_rr, e->d_rtrue, d_list,
+                       d_offs, (uint32_t)list.size(), d_out);
     HIPCHK(hipGetLastError());
     size_t old = e->unknown_bytes.size();
     e->unknown_bytes.resize(old + acc);
@@ -1296,7 +1444,7 @@ static int collect_unknown(fk_engine *e, const uint8_t *dbuf, uint64_t len, int6
  */
 static int count_segment(fk_engine *e, const uint8_t *dbuf, uint64_t len, int64_t lo, int has_init, Geo &g) {
     g = geometry(e, len);
-    int rc = grow_arrays(e, g.nchunks, g.nranges);
+    int rc = grow_arrays(e, g.nranges);
     if (rc) return rc;
     rc = res_begin(e);
     if (rc) return rc;
@@ -1304,6 +1452,8 @@ static int count_segment(fk_engine *e, const uint8_t *dbuf, uint64_t len, int64_
     rc = launch_count(e, dbuf, len, lo, g, has_init);
     if (rc) return rc;
     HIPCHK(hipEventRecord(e->ev[1], e->stream));
+    rc = launch_resume(e, dbuf, len, lo, g);
+    if (rc) return rc;
     e->chunks += g.nchunks;
     return FK_OK;
 }
@@ -1355,6 +1505,12 @@ static int finish_segment(fk_engine *e, const uint8_t *dbuf, uint64_t len, int64
 
 static int process_segment(fk_engine *e, const uint8_t *dbuf, uint64_t len) {
     if (len == 0 || e->ended) return FK_OK;
+    if (len < FK_LANE_BYTES && dbuf != e->d_stage) {
+        /* too short for the clamped prefetch: copy into the staging buffer */
+        if (!e->d_stage && hipMalloc((void **)&e->d_stage, STAGE_BYTES) != hipSuccess) return FK_E_OOM;
+        HIPCHK(hipMemcpyAsync(e->d_stage, dbuf, len, hipMemcpyDeviceToDevice, e->stream));
+        dbuf = e->d_stage;
+    }
     XState entering = e->state;
     Geo g;
     int rc = count_segment(e, dbuf, len, 0, 1, g);
@@ -1372,7 +1528,9 @@ extern "C" int fk_engine_feed(fk_engine *e, const uint8_t *buf, uint64_t len, in
     e->fed += len;
     if (e->ended || len == 0) return FK_OK;
     if (e->tail_added) return FK_E_STATE;     /* finish() already closed the stream */
-    if (on_device && ((uintptr_t)buf & 15) == 0) {
+    /* k_count's prefetch loads are clamped to [0, len-32]: inputs shorter
+       than one lane go through the (larger) staging buffer */
+    if (on_device && ((uintptr_t)buf & 15) == 0 && len >= FK_LANE_BYTES) {
         for (uint64_t off = 0; off < len && !e->ended; off += SEG_MAX_BYTES) {
             rc = process_segment(e, buf + off, std::min(SEG_MAX_BYTES, len - off));
             if (rc) return rc;
@@ -1401,7 +1559,7 @@ extern "C" int fk_engine_feed(fk_engine *e, const uint8_t *buf, uint64_t len, in
 extern "C" int fk_engine_state(fk_engine *e, fk_state *out) {
     if (!e || !out) return FK_E_INVALID;
     out->run = e->state.R;
-    out->code = e->state.code;
+    out->code = fk_sigma(e->state.code);     /* API codes use A0 C1 G2 T3 */
     out->hdr = e->state.hdr;
     out->pad = 0;
     return FK_OK;
@@ -1414,6 +1572,7 @@ extern "C" int fk_engine_feed_shard(fk_engine *e, const uint8_t *buf, uint64_t l
     if (!e || !buf || !on_device) return FK_E_INVALID;   /* shards are device-resident */
     if (e->fed || e->shard_pending) return FK_E_STATE;
     if (len > SEG_MAX_BYTES || ((uintptr_t)buf & 15) || (halo & 15)) return FK_E_INVALID;
+    if (len && len < FK_LANE_BYTES) return FK_E_INVALID;   /* shards are at least one lane */
     int rc = set_dev(e);
     if (rc) return rc;
     e->fed = len;
@@ -1449,10 +1608,10 @@ extern "C" int fk_summary_apply(const fk_summary *s, const fk_state *in, fk_stat
     if (!s || !in || !out) return FK_E_INVALID;
     TF t;
     memcpy(&t, s, sizeof t);
-    XState x{in->run, in->code, in->hdr, 0};
+    XState x{in->run, fk_sigma(in->code), in->hdr, 0};
     XState y = fk_apply(t, x);
     out->run = y.R;
-    out->code = y.code;
+    out->code = fk_sigma(y.code);
     out->hdr = y.hdr;
     out->pad = 0;
     return FK_OK;
@@ -1463,7 +1622,7 @@ extern "C" int fk_engine_resolve(fk_engine *e, const fk_state *entering) {
     if (!e->shard_pending) return FK_E_STATE;
     int rc = set_dev(e);
     if (rc) return rc;
-    XState in{entering->run, entering->code, entering->hdr, 0};
+    XState in{entering->run, fk_sigma(entering->code), entering->hdr, 0};
     e->shard_pending = 0;
     e->state = in;
     HIPCHK(hipMemcpyAsync(e->d_state, &in, sizeof in, hipMemcpyHostToDevice, e->stream));
@@ -1490,7 +1649,7 @@ extern "C" int fk_engine_finish(fk_engine *e, fk_result *res) {
     int32_t seq = (int32_t)(uint32_t)e->state.R;
     if (!e->state.hdr && seq >= 1 && seq < k && e->opts.want_nodes && !e->tail_added) {
         uint64_t off = ((1ull << (2 * seq)) - 4) / 3;
-        uint64_t idx = off + (e->state.code & ((1ull << (2 * seq)) - 1));
+        uint64_t idx = off + fk_sigma(e->state.code & ((1ull << (2 * seq)) - 1));
         hipLaunchKernelGGL(k_add_short, dim3(1), dim3(1), 0, e->stream, e->d_short, idx);
         HIPCHK(hipGetLastError());
     }
