@@ -20,6 +20,7 @@
 #define FK_CHUNK_BYTES (FK_TILE_BYTES * FK_CHUNK_TILES)   /* 16 KiB per chunk */
 #define FK_HALO_BYTES 256u             /* bytes before a chunk used to guess state */
 #define FK_BLOCK 512u
+#define FK_COUNT_GENERAL_TILES 8u      /* general-path tiles k_count takes per range */
 #define FK_WAVES_PER_BLOCK (FK_BLOCK / 64u)
 
 /* accumulator slots (u64, device) */
@@ -177,28 +178,32 @@ struct RangeRec {
     uint64_t c0, c1;
     uint64_t eof;        /* first 0xFF outside a header, range-relative, or FK_NO_EOF64 */
     uint32_t unknown;    /* "Unknown character" bytes in the range */
-    uint32_t pad;
+    uint32_t resume;     /* k_count stopped early: resume[range] holds where */
 };
 
 /* A range k_count stopped in (first tile the fast path cannot take):
- * k_resume continues it from here. */
+ * k_resume continues it from here.  Indexed by range. */
 struct ResumeRec {
     uint64_t tile;       /* range-relative tile index */
     uint64_t code;       /* state entering that tile */
     uint32_t R, hdr;
     uint64_t a_code;     /* the range's guessed entering state */
     uint32_t a_R, a_hdr;
-    uint32_t range, pad;
+    uint32_t range;
+    uint32_t unknown;    /* observations of the tiles before it */
+    uint32_t eof;        /* range-relative, or FK_NO_EOF */
+    uint32_t pad;
     Facts f;             /* facts of the range so far */
 };
 
 /* Per-feed results, fetched with one device-to-host copy. */
 struct DevRes {
     unsigned long long tstat[10];   /* k_table_stats: distinct, sum, last[4], first[4] */
+    unsigned long long acc[16];     /* k_table_stats: snapshot of the accumulators */
     XState exit;                    /* stream state after the feed */
     unsigned long long eof_cand;    /* smallest 0xFF offset seen (a candidate) */
     uint32_t redo_n;                /* ranges re-counted */
-    uint32_t resume_n;              /* ranges handed from k_count to k_resume */
+    uint32_t pad;
 };
 
 /* Would counting a span from state a and from state t give identical

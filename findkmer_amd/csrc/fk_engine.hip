@@ -37,6 +37,7 @@
 
 #include <stdio.h>
 #include <stdlib.h>
+#include <stddef.h>
 #include <string.h>
 
 #include <algorithm>
@@ -169,12 +170,13 @@ __device__ __forceinline__ int load_lane(const Ctx &cx, int64_t off, uint32_t w[
         }
         return NB;
     }
+    /* the stream's last partial lane: independent (clamped) byte loads, all
+       in flight together */
     int nb = (int)((int64_t)cx.len - off);
-    for (int j = 0; j < nb; j++) {
-        uint32_t b = (uint32_t)cx.buf[off + j] << (8 * (j & 3));
-        /* select-chain store: no dynamic register indexing */
 #pragma unroll
-        for (int d = 0; d < NB / 4; d++) if ((j >> 2) == d) w[d] |= b;
+    for (int j = 0; j < NB; j++) {
+        uint32_t b = cx.buf[min(off + j, (int64_t)cx.len - 1)];
+        w[j >> 2] |= (j < nb ? b : 0u) << (8 * (j & 3));
     }
     return nb;
 }
@@ -681,7 +683,8 @@ template <int HM>
 __global__ void __launch_bounds__(FK_BLOCK, 2)
 k_count(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint32_t *table,
         uint32_t *shortcnt, unsigned long long *acc, DevRes *res, RangeRec *rr,
-        uint64_t nchunks, const XState *d_init, int has_init, uint64_t cpw, ResumeRec *resume) {
+        uint64_t nchunks, const XState *d_init, int has_init, uint64_t cpw, ResumeRec *resume,
+        uint32_t general_tiles) {
     extern __shared__ uint32_t lds_bins[];
     const uint32_t nw = lds_words(HM, k);
     if (HM != H_GLOBAL) lds_zero(lds_bins, nw);
@@ -708,52 +711,70 @@ k_count(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uin
         Counters cnt{0, 0, 0, 0, 0, FK_NO_EOF};
         uint32_t A[8], B[8], C[8];
         uint64_t t = 0;
-        /* issue order A, B, C as in the loop (the barriers keep the compiler
-           from reordering them, which would merge two different pending-load
-           orders at the loop header) */
-        FK_LOADT(A, 0);
-        asm volatile("" ::: "memory");
-        FK_LOADT(B, 1);
-        asm volatile("" ::: "memory");
-        FK_LOADT(C, 2);
-        /* one exit per group of three tiles and unconditional loads: every
-           path into the latch has the same loads in flight, so each tile waits
-           only for its own data */
-        bool live = st.hdr == 0;
-        for (uint64_t g = 0; live; g += 3) {
-            live = t < sp.nfull && tile_fast<true, HM>(cx, A, st, f, cnt, 1u);
-            t += live;
-            consume(A);
-            FK_LOADT(A, g + 3);
-            live = live && t < sp.nfull && tile_fast<true, HM>(cx, B, st, f, cnt, 1u);
-            t += live;
-            consume(B);
-            FK_LOADT(B, g + 4);
-            live = live && t < sp.nfull && tile_fast<true, HM>(cx, C, st, f, cnt, 1u);
-            t += live;
-            consume(C);
-            FK_LOADT(C, g + 5);
+        uint32_t general_left = general_tiles;
+        for (;;) {
+            /* issue order A, B, C as in the loop (the barriers keep the
+               compiler from reordering them, which would merge two different
+               pending-load orders at the loop header) */
+            FK_LOADT(A, t);
+            asm volatile("" ::: "memory");
+            FK_LOADT(B, t + 1);
+            asm volatile("" ::: "memory");
+            FK_LOADT(C, t + 2);
+            /* one exit per group of three tiles and unconditional loads:
+               every path into the latch has the same loads in flight, so each
+               tile waits only for its own data */
+            bool live = st.hdr == 0;
+            for (uint64_t g = t; live; g += 3) {
+                live = t < sp.nfull && tile_fast<true, HM>(cx, A, st, f, cnt, 1u);
+                t += live;
+                consume(A);
+                FK_LOADT(A, g + 3);
+                live = live && t < sp.nfull && tile_fast<true, HM>(cx, B, st, f, cnt, 1u);
+                t += live;
+                consume(B);
+                FK_LOADT(B, g + 4);
+                live = live && t < sp.nfull && tile_fast<true, HM>(cx, C, st, f, cnt, 1u);
+                t += live;
+                consume(C);
+                FK_LOADT(C, g + 5);
+            }
+            if (t >= sp.ntiles || general_left == 0) break;
+            /* a tile the fast path cannot take (stream start, header, run
+               break, the ragged end): general path, then back to streaming */
+            general_left--;
+            uint32_t v[8];
+            const int64_t toff = (int64_t)(sp.rbase + t * FK_TILE_BYTES);
+            const int nb = load_lane<FK_LANE_BYTES>(cx, toff + lane * (int64_t)FK_LANE_BYTES, v);
+            tile_general<true, HM>(cx, v, nb, (uint32_t)(t * FK_TILE_BYTES), st, f, cnt, 1u);
+            t++;
         }
+        flush_counters(cx, cnt, 1u);
+        const uint32_t unk = wsum32(cnt.unknown);
+        const uint32_t eof = wmin32(cnt.eof);
         if (lane == 0) {
-            if (f.nv_total) atomicAdd(&acc[ACC_WIN], (unsigned long long)f.nv_total);
             if (t < sp.ntiles) {
-                const uint32_t slot = atomicAdd(&res->resume_n, 1u);
                 ResumeRec q;
                 q.tile = t;
                 q.code = st.code; q.R = st.R; q.hdr = st.hdr;
                 q.a_code = first.code; q.a_R = first.R; q.a_hdr = first.hdr;
                 q.range = (uint32_t)wave;
+                q.unknown = unk;
+                q.eof = eof;
                 q.pad = 0;
                 q.f = f;
-                resume[slot] = q;
+                resume[wave] = q;
+                RangeRec &r = rr[wave];
+                r.c0 = c0; r.c1 = c1;
+                r.resume = 1;
             } else {
                 RangeRec r;
                 r.tf = fk_tf_span(first, st, f);
                 r.a_code = first.code; r.a_R = first.R; r.a_hdr = first.hdr;
                 r.c0 = c0; r.c1 = c1;
-                r.eof = FK_NO_EOF64;
-                r.unknown = 0;
-                r.pad = 0;
+                r.eof = eof == FK_NO_EOF ? FK_NO_EOF64 : (uint64_t)eof;
+                r.unknown = unk;
+                r.resume = 0;
                 rr[wave] = r;
             }
         }
@@ -763,29 +784,26 @@ k_count(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uin
 #undef FK_LOADT
 
 /*
- * k_resume: finish the ranges k_count stopped in, one wave per range, with
- * the general path wherever the fast path does not apply, and write their
- * RangeRecs.
+ * k_resume: finish the ranges k_count stopped in (one wave per range, as in
+ * k_count), with the general path wherever the fast path does not apply, and
+ * write their RangeRecs.  Blocks without such a range exit at once.
  */
 template <int HM>
 __global__ void __launch_bounds__(FK_BLOCK)
 k_resume(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint32_t *table,
-         uint32_t *shortcnt, unsigned long long *acc, DevRes *res, RangeRec *rr, uint64_t nchunks,
-         uint64_t cpw, const ResumeRec *resume) {
+         uint32_t *shortcnt, unsigned long long *acc, DevRes *res, RangeRec *rr, uint64_t nranges,
+         const ResumeRec *resume) {
     extern __shared__ uint32_t lds_bins[];
-    const uint64_t n = res->resume_n;
-    if ((uint64_t)blockIdx.x * FK_WAVES_PER_BLOCK >= n) return;   /* uniform per block */
+    const uint64_t wave = blockIdx.x * FK_WAVES_PER_BLOCK + wave_in_block();
+    const bool mine = wave < nranges && rr[wave].resume;
+    if (!__syncthreads_or(mine)) return;   /* uniform per block */
     const uint32_t nw = lds_words(HM, k);
     if (HM != H_GLOBAL) lds_zero(lds_bins, nw);
     Ctx cx{buf, len, lo, table, HM != H_GLOBAL ? lds_bins : nullptr, shortcnt, acc, res, maskk,
            1u << (2 * k + 2), k};
-    const uint64_t wave = blockIdx.x * FK_WAVES_PER_BLOCK + wave_in_block();
-    const uint64_t nwaves = (uint64_t)gridDim.x * FK_WAVES_PER_BLOCK;
-    for (uint64_t i = wave; i < n; i += nwaves) {
-        const ResumeRec q = resume[i];
-        RangeRec r;
-        r.c0 = (uint64_t)q.range * cpw;
-        r.c1 = min(r.c0 + cpw, nchunks);
+    if (mine) {
+        const ResumeRec q = resume[wave];
+        RangeRec r = rr[wave];
         const Span sp = range_span(r, len);
         DState st{q.code, q.R, q.hdr};
         const DState a{q.a_code, q.a_R, q.a_hdr};
@@ -794,9 +812,13 @@ k_resume(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, ui
         count_range<HM>(cx, sp, q.tile, st, f, cnt, 1u);
         r.tf = fk_tf_span(a, st, f);
         r.a_code = a.code; r.a_R = a.R; r.a_hdr = a.hdr;
-        r.pad = 0;
         range_obs(cx, cnt, 1u, sp, &r, true);
-        if ((threadIdx.x & 63) == 0) rr[q.range] = r;
+        if ((threadIdx.x & 63) == 0) {
+            /* plus what k_count observed before the resume point */
+            r.unknown += q.unknown;
+            if (q.eof != FK_NO_EOF) r.eof = min(r.eof, (uint64_t)q.eof);
+            rr[wave] = r;
+        }
     }
     if (HM != H_GLOBAL) lds_flush<HM>(cx);
 }
@@ -849,41 +871,85 @@ k_redo(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint
 }
 
 /*
- * k_scan: exact entering state of every range.  One 1024-thread workgroup
- * scans the range transfer functions (a few per thread, then a Hillis-Steele
- * scan of the 1024 aggregates in LDS).  mode 0: resolve from *d_state, list
- * the ranges whose guess is not equivalent, write the exit state back to
- * *d_state and res->exit.  mode 1: only the total transfer function (shard
- * summary) into *tf_total.
+ * k_scan: exact entering state of every range.  One 1024-thread workgroup:
+ * each thread composes the transfer functions of a few consecutive ranges,
+ * the 64 lanes of a wave scan theirs with shuffles, the 16 wave aggregates
+ * are composed in LDS.  mode 0: resolve from *d_state, list the ranges whose
+ * guess is not equivalent, write the exit state back to *d_state and
+ * res->exit, and open the feed's result block (redo count, eof candidate
+ * from the range observations, table-stat sums).  mode 1: only the total
+ * transfer function (shard summary) into *tf_total.
  */
 #define SCAN_THREADS 1024
+#define SCAN_WAVES (SCAN_THREADS / 64)
+
+__device__ __forceinline__ uint64_t shup64(uint64_t v, int d) {
+    return ((uint64_t)shup((uint32_t)(v >> 32), d) << 32) | shup((uint32_t)v, d);
+}
+__device__ __forceinline__ XState xs_shup(const XState &x, int d) {
+    return XState{shup64(x.R, d), shup64(x.code, d), shup(x.hdr, d), 0};
+}
+__device__ __forceinline__ TF tf_shup(const TF &a, int d) {
+    TF b;
+    b.c1 = xs_shup(a.c1, d);
+    b.c0 = xs_shup(a.c0, d);
+    b.nv = shup64(a.nv, d);
+    b.cs = shup64(a.cs, d);
+    b.f0_const = shup(a.f0_const, d);
+    b.pad = 0;
+    return b;
+}
+
 __global__ void __launch_bounds__(SCAN_THREADS)
 k_scan(const RangeRec *rr, uint64_t n, XState *d_state, XState *rtrue, uint32_t *redo_list,
        DevRes *res, int k, int mode, TF *tf_total) {
-    __shared__ TF agg[SCAN_THREADS];
-    const uint32_t t = threadIdx.x;
+    __shared__ TF wagg[SCAN_WAVES];
+    __shared__ unsigned long long eof_min;
+    const uint32_t t = threadIdx.x, lane = t & 63, w = t >> 6;
+    if (mode == 0 && t == 0) {
+        eof_min = ~0ull;
+        atomicExch(&res->redo_n, 0u);
+    }
+    if (mode == 0 && t < 10) atomicExch(&res->tstat[t], 0ull);
     const uint64_t per = (n + SCAN_THREADS - 1) / SCAN_THREADS;
     const uint64_t lo = min((uint64_t)t * per, n), hi = min(lo + per, n);
     TF a = fk_identity();
-    for (uint64_t r = lo; r < hi; r++) a = fk_compose(a, rr[r].tf);
-    agg[t] = a;
-    __syncthreads();
-    for (uint32_t d = 1; d < SCAN_THREADS; d <<= 1) {
-        TF mine = agg[t];
-        TF other = t >= d ? agg[t - d] : fk_identity();
-        __syncthreads();
-        if (t >= d) agg[t] = fk_compose(other, mine);
-        __syncthreads();
+    unsigned long long em = ~0ull;
+    for (uint64_t r = lo; r < hi; r++) {
+        a = fk_compose(a, rr[r].tf);
+        const uint64_t e = rr[r].eof;
+        if (e != FK_NO_EOF64) em = min(em, (unsigned long long)(rr[r].c0 * FK_CHUNK_BYTES + e));
     }
+    /* inclusive scan across the wave */
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        TF b = tf_shup(a, d);
+        if (lane >= (uint32_t)d) a = fk_compose(b, a);
+    }
+    if (lane == 63) wagg[w] = a;
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+        unsigned long long o = ((unsigned long long)__shfl_xor((unsigned)(em >> 32), d, 64) << 32) |
+                               (unsigned)__shfl_xor((unsigned)em, d, 64);
+        em = min(em, o);
+    }
+    __syncthreads();
+    if (mode == 0 && lane == 0 && em != ~0ull) atomicMin(&eof_min, em);
+    if (t == 0)
+        for (int i = 1; i < SCAN_WAVES; i++) wagg[i] = fk_compose(wagg[i - 1], wagg[i]);
+    __syncthreads();
     if (mode == 1) {
-        if (t == 0) *tf_total = agg[SCAN_THREADS - 1];
+        if (t == 0) *tf_total = wagg[SCAN_WAVES - 1];
         return;
     }
+    /* exclusive prefix of this thread's ranges */
+    TF ex = tf_shup(a, 1);
+    if (lane == 0) ex = fk_identity();
+    if (w > 0) ex = fk_compose(wagg[w - 1], ex);
     const XState init = *d_state;
-    __syncthreads();
-    XState s = t == 0 ? init : fk_apply(agg[t - 1], init);
+    XState s = fk_apply(ex, init);
     for (uint64_t r = lo; r < hi; r++) {
-        const RangeRec q = rr[r];
+        const RangeRec &q = rr[r];
         rtrue[r] = s;
         DState as{q.a_code, q.a_R, q.a_hdr};
         if (!fk_equiv(as, s, k, (q.c1 - q.c0) * FK_CHUNK_BYTES)) {
@@ -892,11 +958,13 @@ k_scan(const RangeRec *rr, uint64_t n, XState *d_state, XState *rtrue, uint32_t 
         }
         s = fk_apply(q.tf, s);
     }
+    __syncthreads();   /* every thread has read *d_state */
     if (t == SCAN_THREADS - 1) {
-        XState fin = fk_apply(agg[SCAN_THREADS - 1], init);
+        XState fin = fk_apply(wagg[SCAN_WAVES - 1], init);
         *d_state = fin;
         res->exit = fin;
     }
+    if (t == 0) res->eof_cand = eof_min;
 }
 
 /* One pass over the final table: distinct k-mers, total, and the first- and
@@ -906,7 +974,9 @@ __device__ __forceinline__ unsigned long long wsum64(unsigned long long v) {
     for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
     return v;
 }
-__global__ void k_table_stats(const uint32_t *table, uint64_t n, int k, unsigned long long *out) {
+__global__ void k_table_stats(const uint32_t *table, uint64_t n, int k, unsigned long long *out,
+                              const unsigned long long *acc, unsigned long long *acc_out) {
+    if (blockIdx.x == 0 && threadIdx.x < ACC_N) acc_out[threadIdx.x] = acc[threadIdx.x];
     unsigned long long dist = 0, sum = 0, last[4] = {0, 0, 0, 0}, first[4] = {0, 0, 0, 0};
     const uint64_t n4 = n / 4;
     const uint4 *t4 = reinterpret_cast<const uint4 *>(table);
@@ -1047,6 +1117,20 @@ k_extract(const uint8_t *buf, uint64_t len, int64_t lo, const RangeRec *rr, cons
 
 __global__ void k_add_short(uint32_t *shortcnt, uint64_t idx) { atomicAdd(&shortcnt[idx], 1u); }
 
+/* engine reset: table, short-walk counts, accumulators and stream state in
+   one launch */
+__global__ void k_zero(uint32_t *table, uint64_t nbins, uint32_t *shortcnt, uint64_t nshort,
+                       unsigned long long *acc, XState *state) {
+    const uint64_t i0 = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    const uint64_t step = (uint64_t)gridDim.x * blockDim.x;
+    uint4 *t4 = reinterpret_cast<uint4 *>(table);
+    for (uint64_t i = i0; i < nbins / 4; i += step) t4[i] = make_uint4(0, 0, 0, 0);
+    for (uint64_t i = (nbins / 4) * 4 + i0; i < nbins; i += step) table[i] = 0;
+    for (uint64_t i = i0; i < nshort; i += step) shortcnt[i] = 0;
+    if (i0 < ACC_N) acc[i0] = 0;
+    if (i0 == 0) *state = XState{0, 0, 0, 0};
+}
+
 /* synthetic input: byte[i] = "ACGT"[(splitmix64(seed + (i>>5)) >> 2(i&31)) & 3] */
 __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
     x += 0x9E3779B97F4A7C15ull;
@@ -1115,6 +1199,7 @@ struct fk_engine {
     fk_opts opts{};
     uint64_t nbins = 0, nshort = 0, maskk = 0;
     int cus = 256;
+    uint32_t general_tiles = FK_COUNT_GENERAL_TILES;   /* per range in k_count (env FK_GENERAL_TILES) */
     /* device state */
     uint32_t *d_table = nullptr, *d_short = nullptr;
     unsigned long long *d_acc = nullptr;      /* ACC_N, engine lifetime */
@@ -1189,10 +1274,11 @@ static size_t lds_bytes(const fk_engine *e) {
 
 /* Zero table, counters and the stream state (asynchronous, stream-ordered). */
 static int zero_all(fk_engine *e) {
-    HIPCHK(hipMemsetAsync(e->d_table, 0, e->nbins * sizeof(uint32_t), e->stream));
-    if (e->nshort) HIPCHK(hipMemsetAsync(e->d_short, 0, e->nshort * sizeof(uint32_t), e->stream));
-    HIPCHK(hipMemsetAsync(e->d_acc, 0, ACC_N * sizeof(unsigned long long), e->stream));
-    HIPCHK(hipMemsetAsync(e->d_state, 0, sizeof(XState), e->stream));
+    const uint64_t work = std::max<uint64_t>(e->nbins / 4, std::max<uint64_t>(e->nshort, ACC_N));
+    const unsigned grid = (unsigned)std::min<uint64_t>((uint64_t)e->cus * 8, (work + 255) / 256);
+    hipLaunchKernelGGL(k_zero, dim3(grid), dim3(256), 0, e->stream, e->d_table, e->nbins, e->d_short, e->nshort,
+                       e->d_acc, e->d_state);
+    HIPCHK(hipGetLastError());
     e->state = XState{0, 0, 0, 0};
     memset(&e->last, 0, sizeof e->last);
     e->stats_valid = false;
@@ -1236,13 +1322,17 @@ extern "C" int fk_engine_create(int k, const fk_opts *opts, fk_engine **out) {
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, e->dev) == hipSuccess && prop.multiProcessorCount > 0)
         e->cus = prop.multiProcessorCount;
+    if (const char *gt = getenv("FK_GENERAL_TILES")) e->general_tiles = (uint32_t)strtoul(gt, nullptr, 10);
     e->nbins = 1ull << (2 * k);
     e->maskk = e->nbins - 1;
     e->nshort = k > 1 ? ((1ull << (2 * k)) - 4) / 3 : 0;
     if (e->opts.stream) {
         e->stream = (hipStream_t)e->opts.stream;
     } else {
-        if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) { delete e; return FK_E_HIP; }
+        /* a blocking stream: feeds of device buffers order after work on the
+           device's legacy default stream (where PyTorch's default stream
+           runs), so a buffer just filled there is complete when read */
+        if (hipStreamCreateWithFlags(&e->stream, hipStreamDefault) != hipSuccess) { delete e; return FK_E_HIP; }
         e->own_stream = true;
     }
 #define ALLOC(p, bytes)                                                         \
@@ -1321,7 +1411,7 @@ static int launch_count(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t 
     FK_DISPATCH(hist_mode(e),
                 hipLaunchKernelGGL((k_count<HM>), dim3(g.grid), dim3(FK_BLOCK), sh, e->stream, buf, len, lo, e->k,
                                    e->maskk, e->d_table, e->d_short, e->d_acc, e->d_res, e->d_rr,
-                                   g.nchunks, e->d_state, has_init, g.cpw, e->d_resume));
+                                   g.nchunks, e->d_state, has_init, g.cpw, e->d_resume, e->general_tiles));
     HIPCHK(hipGetLastError());
     return FK_OK;
 }
@@ -1330,8 +1420,8 @@ static int launch_resume(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t
     size_t sh = lds_bytes(e);
     FK_DISPATCH(hist_mode(e),
                 hipLaunchKernelGGL((k_resume<HM>), dim3(g.grid), dim3(FK_BLOCK), sh, e->stream, buf, len, lo, e->k,
-                                   e->maskk, e->d_table, e->d_short, e->d_acc, e->d_res, e->d_rr, g.nchunks,
-                                   g.cpw, e->d_resume));
+                                   e->maskk, e->d_table, e->d_short, e->d_acc, e->d_res, e->d_rr, g.nranges,
+                                   e->d_resume));
     HIPCHK(hipGetLastError());
     return FK_OK;
 }
@@ -1353,19 +1443,14 @@ static int launch_scan(fk_engine *e, const Geo &g, int mode) {
     return FK_OK;
 }
 
-static int launch_table_stats(fk_engine *e) {
-    HIPCHK(hipMemsetAsync(e->d_res->tstat, 0, sizeof(e->d_res->tstat), e->stream));
+/* Table statistics and an accumulator snapshot into d_res.  The feed path's
+   k_scan has zeroed the sums already; other callers ask for a memset. */
+static int launch_table_stats(fk_engine *e, bool zero_first) {
+    if (zero_first) HIPCHK(hipMemsetAsync(e->d_res->tstat, 0, sizeof(e->d_res->tstat), e->stream));
     unsigned gd = (unsigned)std::min<uint64_t>((uint64_t)e->cus * 4, (e->nbins / 4 + 255) / 256 + 1);
     hipLaunchKernelGGL(k_table_stats, dim3(gd), dim3(256), 0, e->stream, e->d_table, e->nbins, e->k,
-                       e->d_res->tstat);
+                       e->d_res->tstat, e->d_acc, e->d_res->acc);
     HIPCHK(hipGetLastError());
-    return FK_OK;
-}
-
-/* Reset the per-feed result block (redo count, eof candidate). */
-static int res_begin(fk_engine *e) {
-    HIPCHK(hipMemsetAsync(&e->d_res->redo_n, 0, 2 * sizeof(uint32_t), e->stream));   /* redo_n, resume_n */
-    HIPCHK(hipMemsetAsync(&e->d_res->eof_cand, 0xFF, sizeof(unsigned long long), e->stream));
     return FK_OK;
 }
 
@@ -1375,7 +1460,7 @@ static int resolve_and_fetch(fk_engine *e, const uint8_t *buf, uint64_t len, int
     if (rc) return rc;
     rc = launch_redo(e, buf, len, lo, g, 0);
     if (rc) return rc;
-    rc = launch_table_stats(e);
+    rc = launch_table_stats(e, false);
     if (rc) return rc;
     HIPCHK(hipEventRecord(e->ev[2], e->stream));
     HIPCHK(hipMemcpyAsync(&e->last, e->d_res, sizeof(DevRes), hipMemcpyDeviceToHost, e->stream));
@@ -1446,8 +1531,6 @@ static int count_segment(fk_engine *e, const uint8_t *dbuf, uint64_t len, int64_
     g = geometry(e, len);
     int rc = grow_arrays(e, g.nranges);
     if (rc) return rc;
-    rc = res_begin(e);
-    if (rc) return rc;
     HIPCHK(hipEventRecord(e->ev[0], e->stream));
     rc = launch_count(e, dbuf, len, lo, g, has_init);
     if (rc) return rc;
@@ -1481,7 +1564,7 @@ static int finish_segment(fk_engine *e, const uint8_t *dbuf, uint64_t len, int64
             e->ended = 1;
             e->scanned += eof;
             if (eof == 0) {
-                rc = launch_table_stats(e);
+                rc = launch_table_stats(e, true);
                 if (rc) return rc;
                 HIPCHK(hipMemcpyAsync(&e->last, e->d_res, sizeof(DevRes), hipMemcpyDeviceToHost, e->stream));
                 HIPCHK(hipStreamSynchronize(e->stream));
@@ -1655,14 +1738,18 @@ extern "C" int fk_engine_finish(fk_engine *e, fk_result *res) {
     }
     e->tail_added = true;
     if (!e->stats_valid) {
-        rc = launch_table_stats(e);
+        rc = launch_table_stats(e, true);
         if (rc) return rc;
-        HIPCHK(hipMemcpyAsync(e->last.tstat, e->d_res->tstat, sizeof e->last.tstat, hipMemcpyDeviceToHost, e->stream));
+        HIPCHK(hipMemcpyAsync(e->last.tstat, e->d_res->tstat, sizeof e->last.tstat + sizeof e->last.acc,
+                              hipMemcpyDeviceToHost, e->stream));
+        HIPCHK(hipStreamSynchronize(e->stream));
+        e->stats_valid = true;
     }
-    unsigned long long acc[ACC_N];
-    HIPCHK(hipMemcpyAsync(acc, e->d_acc, sizeof acc, hipMemcpyDeviceToHost, e->stream));
-    HIPCHK(hipStreamSynchronize(e->stream));
-    e->stats_valid = true;
+    static_assert(offsetof(DevRes, acc) == offsetof(DevRes, tstat) + sizeof(((DevRes *)0)->tstat),
+                  "tstat and acc are fetched with one copy");
+    /* the table stats and the accumulator snapshot of the last feed (or of
+       the call above) describe the engine: no device round trip here */
+    const unsigned long long *acc = e->last.acc;
     const unsigned long long *ts = e->last.tstat;
     res->windows = acc[ACC_WIN];
     /* every window's last base is a base the reference counts; a run's first

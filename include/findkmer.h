@@ -93,7 +93,9 @@ typedef struct {
 typedef struct {
     int32_t device;           /* HIP device ordinal; -1 = current device */
     int32_t want_nodes;       /* compute nodeCounter (stdout "tree density") */
-    void   *stream;           /* hipStream_t to use, NULL = engine-owned */
+    void   *stream;           /* hipStream_t to use; NULL = an engine-owned
+                                 blocking stream (orders after the device's
+                                 legacy default stream) */
     int32_t collect_unknown;  /* keep the unknown bytes for stderr replay */
     int32_t reserved[7];
 } fk_opts;
@@ -113,7 +115,8 @@ int  fk_engine_reset(fk_engine *e);     /* zero table, counters and state */
 
 /* Feed a byte range of the stream.  `buf` is a device pointer when
  * on_device != 0, else host memory (staged through pinned buffers).  Feeds
- * continue the scan state of the previous feed exactly. */
+ * continue the scan state of the previous feed exactly.  A device buffer
+ * must be complete in the engine's stream order (see fk_opts.stream). */
 int  fk_engine_feed(fk_engine *e, const uint8_t *buf, uint64_t len,
                     int on_device);
 

@@ -64,6 +64,7 @@ def shard_count(data, k, nshards):
     per = max(chunk, (n // nshards) // chunk * chunk)
     bounds = [min(i * per, n) for i in range(nshards)] + [n]
     dev = torch.from_numpy(arr.copy()).cuda() if n else torch.zeros(16, dtype=torch.uint8).cuda()
+    torch.cuda.synchronize()
     engines = []
     for i in range(nshards):
         e = fk.Engine(k, collect_unknown=True)
@@ -208,6 +209,7 @@ def test_int32_seqsize_wrap():
     L = 2 ** 31 + 100
     buf = torch.full((5 + L,), ord("A"), dtype=torch.uint8, device="cuda")
     buf[:5] = torch.tensor(list(b"ACGTN"), dtype=torch.uint8)
+    torch.cuda.synchronize()
     with fk.Engine(2) as e:
         e.feed_device(buf.data_ptr(), 5 + L)
         rc, r = e.finish()
@@ -226,6 +228,7 @@ def test_int32_seqsize_two_zones():
     L = 2 ** 32 + 2 ** 31 + 50
     k = 3
     buf = torch.full((L,), ord("A"), dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
     with fk.Engine(k) as e:
         e.feed_device(buf.data_ptr(), L)
         rc, r = e.finish(allow=(fk.FK_OK, fk.FK_E_ROLLOVER))

@@ -1,0 +1,14 @@
+import os, sys, torch
+sys.path.insert(0, os.environ.get("GRAFT_REPO_ROOT", "."))
+torch.cuda.init()
+import findkmer_amd as fk
+L = 2 ** 32 + 2 ** 31 + 50
+k = 3
+buf = torch.full((L,), ord("A"), dtype=torch.uint8, device="cuda")
+with fk.Engine(k) as e:
+    e.feed_device(buf.data_ptr(), L)
+    rc, r = e.finish(allow=(fk.FK_OK, fk.FK_E_ROLLOVER))
+    t = e.table()
+z = 2 ** 31 - 3
+print("GT", os.environ.get("FK_GENERAL_TILES"), "t0", int(t[0]), "exp", 2 * z, "diff", 2 * z - int(t[0]),
+      "windows", r.windows, "valid", r.valid_bases, "redo", r.redo_chunks, "rollover", r.rollover, flush=True)
