@@ -203,7 +203,7 @@ struct DevRes {
     XState exit;                    /* stream state after the feed */
     unsigned long long eof_cand;    /* smallest 0xFF offset seen (a candidate) */
     uint32_t redo_n;                /* ranges re-counted */
-    uint32_t pad;
+    uint32_t seq;                   /* host copy: written last (feed sequence number) */
 };
 
 /* Would counting a span from state a and from state t give identical

@@ -33,6 +33,7 @@
  * Runs break at '>' (then skip to '\n'), 'N' and any other non-ACGT byte;
  * '\n' is transparent; 0xFF outside a header ends the input (:988).
  */
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <stdio.h>
@@ -686,6 +687,13 @@ k_count(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uin
         uint64_t nchunks, const XState *d_init, int has_init, uint64_t cpw, ResumeRec *resume,
         uint32_t general_tiles) {
     extern __shared__ uint32_t lds_bins[];
+    /* open the feed's result block (the kernels after this one in the
+       stream accumulate into it) */
+    if (blockIdx.x == 0) {
+        if (threadIdx.x < 10) res->tstat[threadIdx.x] = 0;
+        if (threadIdx.x == 10) res->eof_cand = ~0ull;
+        if (threadIdx.x == 11) res->redo_n = 0;
+    }
     const uint32_t nw = lds_words(HM, k);
     if (HM != H_GLOBAL) lds_zero(lds_bins, nw);
     Ctx cx{buf, len, lo, table, HM != H_GLOBAL ? lds_bins : nullptr, shortcnt, acc, res, maskk,
@@ -871,16 +879,20 @@ k_redo(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint
 }
 
 /*
- * k_scan: exact entering state of every range.  One 1024-thread workgroup:
- * each thread composes the transfer functions of a few consecutive ranges,
- * the 64 lanes of a wave scan theirs with shuffles, the 16 wave aggregates
- * are composed in LDS.  mode 0: resolve from *d_state, list the ranges whose
- * guess is not equivalent, write the exit state back to *d_state and
- * res->exit, and open the feed's result block (redo count, eof candidate
- * from the range observations, table-stat sums).  mode 1: only the total
- * transfer function (shard summary) into *tf_total.
+ * k_scan: exact entering state of every range, one thread per range.  Each
+ * 256-thread block scans its ranges' transfer functions (wave shuffles, then
+ * the four wave aggregates), publishes the block aggregate with an
+ * epoch-tagged flag, waits for the flags of all blocks before it and
+ * composes their aggregates with one wave scan (all predecessors publish at
+ * about the same time, so this is one round trip, not a chain).
+ * mode 0: resolve from *d_state, list the ranges whose guess is not
+ * equivalent, write the exit state back to *d_state and res->exit.
+ * mode 1: only the total transfer function (shard summary) into *tf_total.
+ * Every block reads *d_state before publishing its flag; the last block
+ * writes it only after seeing every flag.  All blocks are co-resident (a
+ * handful), and a block only waits on blocks dispatched before it.
  */
-#define SCAN_THREADS 1024
+#define SCAN_THREADS 256
 #define SCAN_WAVES (SCAN_THREADS / 64)
 
 __device__ __forceinline__ uint64_t shup64(uint64_t v, int d) {
@@ -899,34 +911,46 @@ __device__ __forceinline__ TF tf_shup(const TF &a, int d) {
     b.pad = 0;
     return b;
 }
-
-__global__ void __launch_bounds__(SCAN_THREADS)
-k_scan(const RangeRec *rr, uint64_t n, XState *d_state, XState *rtrue, uint32_t *redo_list,
-       DevRes *res, int k, int mode, TF *tf_total) {
-    __shared__ TF wagg[SCAN_WAVES];
-    __shared__ unsigned long long eof_min;
-    const uint32_t t = threadIdx.x, lane = t & 63, w = t >> 6;
-    if (mode == 0 && t == 0) {
-        eof_min = ~0ull;
-        atomicExch(&res->redo_n, 0u);
-    }
-    if (mode == 0 && t < 10) atomicExch(&res->tstat[t], 0ull);
-    const uint64_t per = (n + SCAN_THREADS - 1) / SCAN_THREADS;
-    const uint64_t lo = min((uint64_t)t * per, n), hi = min(lo + per, n);
-    TF a = fk_identity();
-    unsigned long long em = ~0ull;
-    for (uint64_t r = lo; r < hi; r++) {
-        a = fk_compose(a, rr[r].tf);
-        const uint64_t e = rr[r].eof;
-        if (e != FK_NO_EOF64) em = min(em, (unsigned long long)(rr[r].c0 * FK_CHUNK_BYTES + e));
-    }
-    /* inclusive scan across the wave */
+__device__ __forceinline__ TF tf_rdlane(const TF &x, int l) {
+    TF o;
+    o.c1 = XState{rdlane64(x.c1.R, l), rdlane64(x.c1.code, l), rdlane(x.c1.hdr, l), 0};
+    o.c0 = XState{rdlane64(x.c0.R, l), rdlane64(x.c0.code, l), rdlane(x.c0.hdr, l), 0};
+    o.nv = rdlane64(x.nv, l);
+    o.cs = rdlane64(x.cs, l);
+    o.f0_const = rdlane(x.f0_const, l);
+    o.pad = 0;
+    return o;
+}
+/* inclusive scan of one TF per lane across the wave */
+__device__ __forceinline__ TF tf_wave_scan(TF a) {
+    const uint32_t lane = threadIdx.x & 63;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
         TF b = tf_shup(a, d);
         if (lane >= (uint32_t)d) a = fk_compose(b, a);
     }
-    if (lane == 63) wagg[w] = a;
+    return a;
+}
+
+__global__ void __launch_bounds__(SCAN_THREADS)
+k_scan(const RangeRec *rr, uint64_t n, XState *d_state, XState *rtrue, uint32_t *redo_list,
+       DevRes *res, int k, int mode, TF *tf_total, TF *aggs, uint32_t *flags, uint32_t epoch) {
+    __shared__ TF wincl[SCAN_WAVES];   /* inclusive wave aggregates */
+    __shared__ TF bprefix;
+    __shared__ unsigned long long eof_min;
+    const uint32_t t = threadIdx.x, lane = t & 63, w = t >> 6, b = blockIdx.x;
+    const uint64_t r = (uint64_t)b * SCAN_THREADS + t;
+    const XState init = *d_state;
+    if (t == 0) eof_min = ~0ull;
+    TF a = fk_identity();
+    unsigned long long em = ~0ull;
+    if (r < n) {
+        a = rr[r].tf;
+        const uint64_t e = rr[r].eof;
+        if (e != FK_NO_EOF64) em = rr[r].c0 * FK_CHUNK_BYTES + e;
+    }
+    a = tf_wave_scan(a);
+    if (lane == 63) wincl[w] = a;
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) {
         unsigned long long o = ((unsigned long long)__shfl_xor((unsigned)(em >> 32), d, 64) << 32) |
@@ -934,37 +958,57 @@ k_scan(const RangeRec *rr, uint64_t n, XState *d_state, XState *rtrue, uint32_t 
         em = min(em, o);
     }
     __syncthreads();
-    if (mode == 0 && lane == 0 && em != ~0ull) atomicMin(&eof_min, em);
-    if (t == 0)
-        for (int i = 1; i < SCAN_WAVES; i++) wagg[i] = fk_compose(wagg[i - 1], wagg[i]);
+    if (lane == 0 && em != ~0ull) atomicMin(&eof_min, em);
+    if (t == 0) {
+        for (int i = 1; i < SCAN_WAVES; i++) wincl[i] = fk_compose(wincl[i - 1], wincl[i]);
+        aggs[b] = wincl[SCAN_WAVES - 1];
+        __threadfence();
+        __hip_atomic_store(&flags[b], epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    /* prefix of all blocks before this one (wave 0) */
+    if (w == 0) {
+        TF carry = fk_identity();
+        for (uint32_t base = 0; base < b; base += 64) {
+            const uint32_t i = base + lane;
+            TF x = fk_identity();
+            if (i < b) {
+                while (__hip_atomic_load(&flags[i], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != epoch)
+                    __builtin_amdgcn_s_sleep(1);
+                x = aggs[i];
+            }
+            x = tf_wave_scan(x);
+            /* lane 63 holds the chunk's aggregate (identity padding is neutral) */
+            const TF chunk = tf_rdlane(x, 63);
+            carry = fk_compose(carry, chunk);
+        }
+        if (lane == 0) bprefix = carry;
+    }
     __syncthreads();
     if (mode == 1) {
-        if (t == 0) *tf_total = wagg[SCAN_WAVES - 1];
+        if (b == gridDim.x - 1 && t == 0) *tf_total = fk_compose(bprefix, wincl[SCAN_WAVES - 1]);
         return;
     }
-    /* exclusive prefix of this thread's ranges */
+    /* exclusive prefix of this thread's range */
     TF ex = tf_shup(a, 1);
     if (lane == 0) ex = fk_identity();
-    if (w > 0) ex = fk_compose(wagg[w - 1], ex);
-    const XState init = *d_state;
-    XState s = fk_apply(ex, init);
-    for (uint64_t r = lo; r < hi; r++) {
+    if (w > 0) ex = fk_compose(wincl[w - 1], ex);
+    ex = fk_compose(bprefix, ex);
+    if (r < n) {
         const RangeRec &q = rr[r];
+        const XState s = fk_apply(ex, init);
         rtrue[r] = s;
         DState as{q.a_code, q.a_R, q.a_hdr};
         if (!fk_equiv(as, s, k, (q.c1 - q.c0) * FK_CHUNK_BYTES)) {
             uint32_t slot = atomicAdd(&res->redo_n, 1u);
             redo_list[slot] = (uint32_t)r;
         }
-        s = fk_apply(q.tf, s);
+        if (r == n - 1) {
+            const XState fin = fk_apply(q.tf, s);
+            *d_state = fin;
+            res->exit = fin;
+        }
     }
-    __syncthreads();   /* every thread has read *d_state */
-    if (t == SCAN_THREADS - 1) {
-        XState fin = fk_apply(wagg[SCAN_WAVES - 1], init);
-        *d_state = fin;
-        res->exit = fin;
-    }
-    if (t == 0) res->eof_cand = eof_min;
+    if (t == 0 && eof_min != ~0ull) atomicMin(&res->eof_cand, eof_min);
 }
 
 /* One pass over the final table: distinct k-mers, total, and the first- and
@@ -974,9 +1018,10 @@ __device__ __forceinline__ unsigned long long wsum64(unsigned long long v) {
     for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
     return v;
 }
-__global__ void k_table_stats(const uint32_t *table, uint64_t n, int k, unsigned long long *out,
-                              const unsigned long long *acc, unsigned long long *acc_out) {
-    if (blockIdx.x == 0 && threadIdx.x < ACC_N) acc_out[threadIdx.x] = acc[threadIdx.x];
+__global__ void k_table_stats(const uint32_t *table, uint64_t n, int k, DevRes *res,
+                              const unsigned long long *acc, DevRes *host_res, uint32_t *done, uint32_t seq) {
+    unsigned long long *out = res->tstat;
+    if (blockIdx.x == 0 && threadIdx.x < ACC_N) res->acc[threadIdx.x] = acc[threadIdx.x];
     unsigned long long dist = 0, sum = 0, last[4] = {0, 0, 0, 0}, first[4] = {0, 0, 0, 0};
     const uint64_t n4 = n / 4;
     const uint4 *t4 = reinterpret_cast<const uint4 *>(table);
@@ -1007,6 +1052,26 @@ __global__ void k_table_stats(const uint32_t *table, uint64_t n, int k, unsigned
             if (last[b]) atomicAdd(&out[2 + b], last[b]);
             if (first[b]) atomicAdd(&out[6 + b], first[b]);
         }
+    }
+    if (!host_res) return;
+    /* the last block to finish publishes the whole result block to pinned
+       host memory, sequence number last: the host spins on it instead of a
+       copy plus a stream synchronisation */
+    __shared__ uint32_t is_last;
+    __threadfence();
+    __syncthreads();
+    if (threadIdx.x == 0) is_last = atomicAdd(done, 1u) == gridDim.x - 1;
+    __syncthreads();
+    if (!is_last) return;
+    __threadfence();
+    const uint32_t *src = reinterpret_cast<const uint32_t *>(res);
+    uint32_t *dst = reinterpret_cast<uint32_t *>(host_res);
+    for (uint32_t i = threadIdx.x; i < offsetof(DevRes, seq) / 4; i += blockDim.x) dst[i] = src[i];
+    __threadfence_system();
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        *done = 0;
+        __hip_atomic_store(&host_res->seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
 
@@ -1210,10 +1275,18 @@ struct fk_engine {
     XState *d_rtrue = nullptr;
     uint32_t *d_redo = nullptr;
     ResumeRec *d_resume = nullptr;            /* ranges k_count hands to k_resume */
+    TF *d_aggs = nullptr;                     /* k_scan block aggregates */
+    uint32_t *d_flags = nullptr;              /* ... and their epoch flags */
+    uint32_t scan_epoch = 0;
     TF *d_tf = nullptr;
     uint64_t range_cap = 0;
     uint8_t *d_stage = nullptr, *h_stage = nullptr;
     hipEvent_t ev[3] = {};
+    bool times_pending = false;               /* ev[] of the last feed not yet read */
+    bool zero_pending = false;                /* reset() not yet issued to the device */
+    DevRes *h_res = nullptr, *h_res_dev = nullptr;   /* pinned, mapped result block */
+    uint32_t *d_done = nullptr;               /* k_table_stats finished-block count */
+    uint32_t res_seq = 0;
     /* host bookkeeping */
     XState state{0, 0, 0, 0};
     DevRes last{};                            /* last feed's results */
@@ -1229,9 +1302,26 @@ struct fk_engine {
     std::vector<uint8_t> unknown_bytes;
 };
 
+__global__ void k_zero(uint32_t *table, uint64_t nbins, uint32_t *shortcnt, uint64_t nshort,
+                       unsigned long long *acc, XState *state);
+
+/* A reset is issued lazily, with the next device work (every API entry that
+   touches the device goes through set_dev), so that it reaches the GPU
+   back to back with that work. */
+static int flush_zero(fk_engine *e) {
+    if (!e->zero_pending) return FK_OK;
+    e->zero_pending = false;
+    const uint64_t work = std::max<uint64_t>(e->nbins / 4, std::max<uint64_t>(e->nshort, ACC_N));
+    const unsigned grid = (unsigned)std::min<uint64_t>((uint64_t)e->cus * 8, (work + 255) / 256);
+    hipLaunchKernelGGL(k_zero, dim3(grid), dim3(256), 0, e->stream, e->d_table, e->nbins, e->d_short, e->nshort,
+                       e->d_acc, e->d_state);
+    HIPCHK(hipGetLastError());
+    return FK_OK;
+}
+
 static int set_dev(fk_engine *e) {
     HIPCHK(hipSetDevice(e->dev));
-    return FK_OK;
+    return flush_zero(e);
 }
 
 extern "C" int fk_abi_version(void) { return FK_ABI_VERSION; }
@@ -1274,11 +1364,7 @@ static size_t lds_bytes(const fk_engine *e) {
 
 /* Zero table, counters and the stream state (asynchronous, stream-ordered). */
 static int zero_all(fk_engine *e) {
-    const uint64_t work = std::max<uint64_t>(e->nbins / 4, std::max<uint64_t>(e->nshort, ACC_N));
-    const unsigned grid = (unsigned)std::min<uint64_t>((uint64_t)e->cus * 8, (work + 255) / 256);
-    hipLaunchKernelGGL(k_zero, dim3(grid), dim3(256), 0, e->stream, e->d_table, e->nbins, e->d_short, e->nshort,
-                       e->d_acc, e->d_state);
-    HIPCHK(hipGetLastError());
+    e->zero_pending = true;
     e->state = XState{0, 0, 0, 0};
     memset(&e->last, 0, sizeof e->last);
     e->stats_valid = false;
@@ -1298,8 +1384,11 @@ extern "C" void fk_engine_destroy(fk_engine *e) {
     hipFree(e->d_table); hipFree(e->d_short); hipFree(e->d_acc); hipFree(e->d_res); hipFree(e->d_tmp);
     hipFree(e->d_state); hipFree(e->d_rr); hipFree(e->d_rtrue);
     hipFree(e->d_redo); hipFree(e->d_tf); hipFree(e->d_stage); hipFree(e->d_resume);
+    hipFree(e->d_aggs); hipFree(e->d_flags);
     if (e->h_stage) hipHostFree(e->h_stage);
     for (int i = 0; i < 3; i++) if (e->ev[i]) hipEventDestroy(e->ev[i]);
+    if (e->h_res) hipHostFree(e->h_res);
+    hipFree(e->d_done);
     if (e->own_stream && e->stream) hipStreamDestroy(e->stream);
     delete e;
 }
@@ -1354,6 +1443,14 @@ extern "C" int fk_engine_create(int k, const fk_opts *opts, fk_engine **out) {
     }
     for (int i = 0; i < 3; i++)
         if (hipEventCreate(&e->ev[i]) != hipSuccess) { fk_engine_destroy(e); return FK_E_HIP; }
+    if (hipHostMalloc((void **)&e->h_res, sizeof(DevRes), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+        hipHostGetDevicePointer((void **)&e->h_res_dev, e->h_res, 0) != hipSuccess ||
+        hipMalloc((void **)&e->d_done, sizeof(uint32_t)) != hipSuccess ||
+        hipMemsetAsync(e->d_done, 0, sizeof(uint32_t), e->stream) != hipSuccess) {
+        fk_engine_destroy(e);
+        return FK_E_OOM;
+    }
+    memset(e->h_res, 0, sizeof(DevRes));
     rc = zero_all(e);
     if (rc == FK_OK && hipStreamSynchronize(e->stream) != hipSuccess) rc = FK_E_HIP;
     if (rc) { fk_engine_destroy(e); return rc; }
@@ -1373,11 +1470,18 @@ static int grow_arrays(fk_engine *e, uint64_t nranges) {
     if (nranges > e->range_cap || !e->d_rr) {
         uint64_t nr = std::max<uint64_t>(nranges, 1024);
         hipFree(e->d_rr); hipFree(e->d_rtrue); hipFree(e->d_redo); hipFree(e->d_resume);
+        hipFree(e->d_aggs); hipFree(e->d_flags);
         e->d_rr = nullptr; e->d_rtrue = nullptr; e->d_redo = nullptr; e->d_resume = nullptr;
+        e->d_aggs = nullptr; e->d_flags = nullptr;
         if (hipMalloc((void **)&e->d_rr, nr * sizeof(RangeRec)) != hipSuccess) return FK_E_OOM;
         if (hipMalloc((void **)&e->d_rtrue, nr * sizeof(XState)) != hipSuccess) return FK_E_OOM;
         if (hipMalloc((void **)&e->d_redo, nr * sizeof(uint32_t)) != hipSuccess) return FK_E_OOM;
         if (hipMalloc((void **)&e->d_resume, nr * sizeof(ResumeRec)) != hipSuccess) return FK_E_OOM;
+        const size_t nb = nr / SCAN_THREADS + 1;
+        if (hipMalloc((void **)&e->d_aggs, nb * sizeof(TF)) != hipSuccess) return FK_E_OOM;
+        if (hipMalloc((void **)&e->d_flags, nb * sizeof(uint32_t) + 64) != hipSuccess) return FK_E_OOM;
+        HIPCHK(hipMemsetAsync(e->d_flags, 0, nb * sizeof(uint32_t) + 64, e->stream));
+        e->scan_epoch = 0;
         e->range_cap = nr;
     }
     return FK_OK;
@@ -1409,7 +1513,8 @@ static int launch_count(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t 
                         int has_init) {
     size_t sh = lds_bytes(e);
     FK_DISPATCH(hist_mode(e),
-                hipLaunchKernelGGL((k_count<HM>), dim3(g.grid), dim3(FK_BLOCK), sh, e->stream, buf, len, lo, e->k,
+                hipExtLaunchKernelGGL((k_count<HM>), dim3(g.grid), dim3(FK_BLOCK), sh, e->stream, e->ev[0], e->ev[1],
+                                      0, buf, len, lo, e->k,
                                    e->maskk, e->d_table, e->d_short, e->d_acc, e->d_res, e->d_rr,
                                    g.nchunks, e->d_state, has_init, g.cpw, e->d_resume, e->general_tiles));
     HIPCHK(hipGetLastError());
@@ -1437,20 +1542,49 @@ static int launch_redo(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t l
 }
 
 static int launch_scan(fk_engine *e, const Geo &g, int mode) {
-    hipLaunchKernelGGL(k_scan, dim3(1), dim3(SCAN_THREADS), 0, e->stream, e->d_rr, g.nranges, e->d_state,
-                       e->d_rtrue, e->d_redo, e->d_res, e->k, mode, e->d_tf);
+    const unsigned blocks = (unsigned)((g.nranges + SCAN_THREADS - 1) / SCAN_THREADS);
+    if (++e->scan_epoch == 0) {   /* flags hold epochs; never reuse 0 */
+        HIPCHK(hipMemsetAsync(e->d_flags, 0, e->range_cap / SCAN_THREADS * sizeof(uint32_t) + 64, e->stream));
+        e->scan_epoch = 1;
+    }
+    hipLaunchKernelGGL(k_scan, dim3(blocks), dim3(SCAN_THREADS), 0, e->stream, e->d_rr, g.nranges, e->d_state,
+                       e->d_rtrue, e->d_redo, e->d_res, e->k, mode, e->d_tf, e->d_aggs, e->d_flags, e->scan_epoch);
     HIPCHK(hipGetLastError());
     return FK_OK;
 }
 
-/* Table statistics and an accumulator snapshot into d_res.  The feed path's
-   k_scan has zeroed the sums already; other callers ask for a memset. */
-static int launch_table_stats(fk_engine *e, bool zero_first) {
+/* Table statistics and an accumulator snapshot into d_res, published to the
+   pinned host copy (e->h_res) with a new sequence number.  The feed path's
+   k_count has zeroed the sums already; other callers ask for a memset.
+   `stop` (optional) is recorded when the kernel completes. */
+static int launch_table_stats(fk_engine *e, bool zero_first, hipEvent_t stop = nullptr) {
     if (zero_first) HIPCHK(hipMemsetAsync(e->d_res->tstat, 0, sizeof(e->d_res->tstat), e->stream));
     unsigned gd = (unsigned)std::min<uint64_t>((uint64_t)e->cus * 4, (e->nbins / 4 + 255) / 256 + 1);
-    hipLaunchKernelGGL(k_table_stats, dim3(gd), dim3(256), 0, e->stream, e->d_table, e->nbins, e->k,
-                       e->d_res->tstat, e->d_acc, e->d_res->acc);
+    if (++e->res_seq == 0) e->res_seq = 1;
+    hipExtLaunchKernelGGL(k_table_stats, dim3(gd), dim3(256), 0, e->stream, nullptr, stop, 0, e->d_table,
+                          e->nbins, e->k, e->d_res, e->d_acc, e->h_res_dev, e->d_done, e->res_seq);
     HIPCHK(hipGetLastError());
+    return FK_OK;
+}
+
+/* Wait for the result block published by the last launch_table_stats() and
+   copy it to e->last: spin on its sequence number in pinned memory, checking
+   the stream for errors now and then. */
+static int wait_results(fk_engine *e) {
+    const uint32_t want = e->res_seq;
+    for (uint32_t spin = 1;; spin++) {
+        if (__atomic_load_n(&e->h_res->seq, __ATOMIC_ACQUIRE) == want) break;
+        if ((spin & 4095) == 0) {
+            hipError_t q = hipStreamQuery(e->stream);
+            if (q == hipSuccess) {
+                if (__atomic_load_n(&e->h_res->seq, __ATOMIC_ACQUIRE) == want) break;
+                return FK_E_HIP;   /* stream drained without publishing */
+            }
+            if (q != hipErrorNotReady) return FK_E_HIP;
+        }
+        __builtin_ia32_pause();
+    }
+    memcpy(&e->last, e->h_res, sizeof(DevRes));
     return FK_OK;
 }
 
@@ -1460,11 +1594,10 @@ static int resolve_and_fetch(fk_engine *e, const uint8_t *buf, uint64_t len, int
     if (rc) return rc;
     rc = launch_redo(e, buf, len, lo, g, 0);
     if (rc) return rc;
-    rc = launch_table_stats(e, false);
+    rc = launch_table_stats(e, false, e->ev[2]);
     if (rc) return rc;
-    HIPCHK(hipEventRecord(e->ev[2], e->stream));
-    HIPCHK(hipMemcpyAsync(&e->last, e->d_res, sizeof(DevRes), hipMemcpyDeviceToHost, e->stream));
-    HIPCHK(hipStreamSynchronize(e->stream));
+    rc = wait_results(e);
+    if (rc) return rc;
     e->stats_valid = true;
     e->redo += e->last.redo_n;
     return FK_OK;
@@ -1523,6 +1656,28 @@ static int collect_unknown(fk_engine *e, const uint8_t *dbuf, uint64_t len, int6
     return FK_OK;
 }
 
+/* Feed timings: k_count (ev0 -> ev1, recorded in its dispatch) and the whole
+   device path (ev0 -> ev2, at the end of k_table_stats).  The host continues
+   as soon as the result block is published, so ev2 may still be pending: it
+   is read when the events are about to be reused, or at finish. */
+static void add_times(fk_engine *e) { e->times_pending = true; }
+static void settle_times(fk_engine *e, bool wait) {
+    if (!e->times_pending) return;
+    if (!wait && hipEventQuery(e->ev[2]) != hipSuccess) {
+        /* k_count's events completed long ago; the whole-path time is
+           best effort here (finish() does not wait for it) */
+        float a = 0;
+        if (hipEventElapsedTime(&a, e->ev[0], e->ev[1]) == hipSuccess) e->main_ms += a;
+        e->times_pending = false;
+        return;
+    }
+    e->times_pending = false;
+    float a = 0, b = 0;
+    if (hipEventQuery(e->ev[2]) != hipSuccess) hipEventSynchronize(e->ev[2]);
+    if (hipEventElapsedTime(&a, e->ev[0], e->ev[1]) == hipSuccess) e->main_ms += a;
+    if (hipEventElapsedTime(&b, e->ev[0], e->ev[2]) == hipSuccess) e->dev_ms += b;
+}
+
 /*
  * Count one device-resident segment whose entering state is *d_state (exact).
  * has_init = 0 is the shard case (entering state unknown; resolved later).
@@ -1531,21 +1686,15 @@ static int count_segment(fk_engine *e, const uint8_t *dbuf, uint64_t len, int64_
     g = geometry(e, len);
     int rc = grow_arrays(e, g.nranges);
     if (rc) return rc;
-    HIPCHK(hipEventRecord(e->ev[0], e->stream));
+    settle_times(e, true);   /* before ev[] are reused */
     rc = launch_count(e, dbuf, len, lo, g, has_init);
     if (rc) return rc;
-    HIPCHK(hipEventRecord(e->ev[1], e->stream));
     rc = launch_resume(e, dbuf, len, lo, g);
     if (rc) return rc;
     e->chunks += g.nchunks;
     return FK_OK;
 }
 
-static void add_times(fk_engine *e) {
-    float a = 0, b = 0;
-    if (hipEventElapsedTime(&a, e->ev[0], e->ev[1]) == hipSuccess) e->main_ms += a;
-    if (hipEventElapsedTime(&b, e->ev[0], e->ev[2]) == hipSuccess) e->dev_ms += b;
-}
 
 /* After resolve: handle a 0xFF byte (recount the prefix) and unknown bytes. */
 static int finish_segment(fk_engine *e, const uint8_t *dbuf, uint64_t len, int64_t lo, const Geo &g,
@@ -1566,8 +1715,8 @@ static int finish_segment(fk_engine *e, const uint8_t *dbuf, uint64_t len, int64
             if (eof == 0) {
                 rc = launch_table_stats(e, true);
                 if (rc) return rc;
-                HIPCHK(hipMemcpyAsync(&e->last, e->d_res, sizeof(DevRes), hipMemcpyDeviceToHost, e->stream));
-                HIPCHK(hipStreamSynchronize(e->stream));
+                rc = wait_results(e);
+                if (rc) return rc;
                 e->state = entering;
                 return FK_OK;
             }
@@ -1740,15 +1889,15 @@ extern "C" int fk_engine_finish(fk_engine *e, fk_result *res) {
     if (!e->stats_valid) {
         rc = launch_table_stats(e, true);
         if (rc) return rc;
-        HIPCHK(hipMemcpyAsync(e->last.tstat, e->d_res->tstat, sizeof e->last.tstat + sizeof e->last.acc,
-                              hipMemcpyDeviceToHost, e->stream));
-        HIPCHK(hipStreamSynchronize(e->stream));
+        rc = wait_results(e);
+        if (rc) return rc;
         e->stats_valid = true;
     }
     static_assert(offsetof(DevRes, acc) == offsetof(DevRes, tstat) + sizeof(((DevRes *)0)->tstat),
                   "tstat and acc are fetched with one copy");
     /* the table stats and the accumulator snapshot of the last feed (or of
        the call above) describe the engine: no device round trip here */
+    settle_times(e, false);
     const unsigned long long *acc = e->last.acc;
     const unsigned long long *ts = e->last.tstat;
     res->windows = acc[ACC_WIN];
@@ -1847,6 +1996,8 @@ extern "C" int fk_engine_table_range(fk_engine *e, uint64_t first, uint64_t n, u
 
 extern "C" int fk_engine_table_device(fk_engine *e, uint32_t **dev_counts) {
     if (!e || !dev_counts) return FK_E_INVALID;
+    int rc = set_dev(e);
+    if (rc) return rc;
     *dev_counts = e->d_table;
     return FK_OK;
 }
