@@ -131,7 +131,8 @@ def main():
             eng.table_to_device(table_t.data_ptr())
             dist.all_reduce(table_t)          # u32 sums, bitwise identical in int32
             eng.table_from_device(table_t.data_ptr())
-        rc, r = eng.finish()
+        # an ablation build (FINDKMER_LIB) may leave the table incomplete
+        rc, r = eng.finish(allow=(fk.FK_OK, fk.FK_E_ROLLOVER) if os.environ.get("FINDKMER_LIB") else (fk.FK_OK,))
         return r
 
     for _ in range(args.warmup):
@@ -157,7 +158,7 @@ def main():
         dt = float(tt.item())
 
     # correctness guard on the measured pass (pure ACGT: every window counts)
-    if L == 0 and world == 1:
+    if L == 0 and world == 1 and not os.environ.get("FINDKMER_LIB"):
         assert last.windows == n - k + 1, (last.windows, n - k + 1)
 
     ms_step = dt / args.steps * 1e3

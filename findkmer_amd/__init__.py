@@ -14,7 +14,9 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libfindkmer_hip.so")
+# FINDKMER_LIB selects another build of the same library (e.g. a variant
+# compiled for an experiment); the default is the in-tree build.
+LIB_PATH = os.environ.get("FINDKMER_LIB") or os.path.join(_HERE, "lib", "libfindkmer_hip.so")
 
 FK_OK = 0
 FK_E_INVALID = -1

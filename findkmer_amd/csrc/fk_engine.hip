@@ -48,6 +48,10 @@
 #include "findkmer.h"
 #include "fk_device.h"
 
+#ifndef FK_EXP
+#define FK_EXP 0   /* ablation builds only (tools/exp.sh); 0 = product */
+#endif
+
 /* ------------------------------------------------------------------------- */
 /* device helpers                                                             */
 /* ------------------------------------------------------------------------- */
@@ -404,17 +408,23 @@ __device__ __forceinline__ void half_windows(const Ctx &cx, uint32_t C, uint32_t
            single k-mer at slot 1 */
         const uint32_t m3 = (uint32_t)((cx.maskk << 2) | 3u) << 2;
         char *L = reinterpret_cast<char *>(cx.lds);
+#if FK_EXP == 1   /* ablation: addresses computed, no LDS atomics */
+#define FK_LDS_ADD(a_) asm volatile("" ::"v"(a_))
+#else
+#define FK_LDS_ADD(a_) atomicAdd(reinterpret_cast<uint32_t *>(L + (a_)), weight)
+#endif
         {
             uint32_t v = __builtin_amdgcn_alignbit(C, S2, 26u);
             uint32_t addr = skip0 ? (cx.single_off * 4u + (v & m2)) : (v & m3);
-            atomicAdd(reinterpret_cast<uint32_t *>(L + addr), weight);
+            FK_LDS_ADD(addr);
         }
 #pragma unroll
         for (int j = 1; j < 7; j++) {
             uint32_t a = __builtin_amdgcn_alignbit(C, S2, (uint32_t)(26 - 4 * j)) & m3;
-            atomicAdd(reinterpret_cast<uint32_t *>(L + a), weight);
+            FK_LDS_ADD(a);
         }
-        atomicAdd(reinterpret_cast<uint32_t *>(L + ((S2 << 2) & m3)), weight);
+        FK_LDS_ADD((S2 << 2) & m3);
+#undef FK_LDS_ADD
     } else {
 #pragma unroll
         for (int i = 0; i < 16; i++) {
@@ -440,9 +450,20 @@ __device__ __forceinline__ void half_windows(const Ctx &cx, uint32_t C, uint32_t
  * v_dot4_u32_u8; the previous lane's last word arrives by DPP wave_shr:1;
  * each window is one v_alignbit of a 64-bit {context, word} pair.
  */
-template <bool COUNT, int HM>
+template <bool COUNT, int HM, bool INTER>
 __device__ __forceinline__ bool tile_fast(const Ctx &cx, const uint32_t w[8], DState &st, Facts &f,
                                           Counters &cnt, uint32_t weight) {
+#if FK_EXP == 4   /* ablation: loop framework only */
+    {
+        uint32_t x = 0;
+#pragma unroll
+        for (int d = 0; d < 8; d++) x ^= w[d];
+        asm volatile("" ::"v"(x));
+        st.R += FK_TILE_BYTES;
+        if (threadIdx.x % 64 == 0) cnt.win += FK_TILE_BYTES;
+        return true;
+    }
+#endif
     const int lane = threadIdx.x & 63;
     const int k = cx.k;
     uint32_t x[8];
@@ -467,31 +488,50 @@ __device__ __forceinline__ bool tile_fast(const Ctx &cx, const uint32_t w[8], DS
     const bool h0 = nl0 != 0, h1 = nl1 != 0;
     if (h0) S0 = squeeze(S0, nl0);
     if (h1) S1 = squeeze(S1, nl1);
-    const uint32_t prev = from_prev_lane(S1, (uint32_t)st.code);
+    /* the 16-byte piece before each half: contiguous layout (lane = 32
+       bytes) -> half 0 follows the previous lane's half 1 and half 1 its own
+       half 0; interleaved layout (half h of lane L at h*1024 + 16L) -> each
+       half follows the previous lane's same half, lane 0's half 1 follows
+       lane 63's half 0 */
+    const uint32_t P0 = INTER ? from_prev_lane(S0, (uint32_t)st.code) : from_prev_lane(S1, (uint32_t)st.code);
+    const uint32_t P1 = INTER ? from_prev_lane(S1, rdlane(S0, 63)) : S0;
     /* make each {C, S2} one contiguous base stream with S2 holding 16 digits */
-    const uint32_t A2 = h0 ? (S0 | ((prev & 3u) << 30)) : S0;
-    const uint32_t AC = h0 ? (prev >> 2) : prev;
-    const uint32_t B2 = h1 ? (S1 | ((S0 & 3u) << 30)) : S1;
-    const uint32_t BC = h1 ? (S0 >> 2) : S0;
+    const uint32_t A2 = h0 ? (S0 | ((P0 & 3u) << 30)) : S0;
+    const uint32_t AC = h0 ? (P0 >> 2) : P0;
+    const uint32_t B2 = h1 ? (S1 | ((P1 & 3u) << 30)) : S1;
+    const uint32_t BC = h1 ? (P1 >> 2) : P1;
 
     const uint64_t nb0 = __ballot(h0), nb1 = __ballot(h1);
     const uint32_t nsym = FK_TILE_BYTES - (uint32_t)__popcll(nb0) - (uint32_t)__popcll(nb1);
     if (COUNT) {
+#if FK_EXP == 2   /* ablation: no window work at all */
+        asm volatile("" ::"v"(AC), "v"(A2), "v"(BC), "v"(B2));
+#else
         half_windows<HM>(cx, AC, A2, h0, weight);
         half_windows<HM>(cx, BC, B2, h1, weight);
+#endif
         if (lane == 0) cnt.win += nsym;
-        /* chunk facts: the first '\n' of the chunk */
+        /* facts: the first '\n' of the span (all bytes before it are bases) */
         if (!f.found_p1 && (nb0 | nb1)) {
-            int L0 = __ffsll((long long)(nb0 | nb1)) - 1;
-            uint32_t a = rdlane(nl0, L0), b = rdlane(nl1, L0);
-            uint32_t j0 = a ? (uint32_t)(__ffs(a) - 1) : 16u + (uint32_t)(__ffs(b) - 1);
+            uint32_t before;
+            if (INTER) {
+                const bool in0 = nb0 != 0;
+                const int L = __ffsll((long long)(in0 ? nb0 : nb1)) - 1;
+                const uint32_t m = in0 ? rdlane(nl0, L) : rdlane(nl1, L);
+                before = (in0 ? 0u : 1024u) + 16u * (uint32_t)L + (uint32_t)(__ffs(m) - 1);
+            } else {
+                const int L0 = __ffsll((long long)(nb0 | nb1)) - 1;
+                const uint32_t a = rdlane(nl0, L0), b = rdlane(nl1, L0);
+                before = (uint32_t)L0 * FK_LANE_BYTES + (a ? (uint32_t)(__ffs(a) - 1) : 16u + (uint32_t)(__ffs(b) - 1));
+            }
             f.found_p1 = 1;
             f.p1_gt = 0;
-            f.R_at_p1 = st.R + (uint32_t)L0 * FK_LANE_BYTES + j0;
+            f.R_at_p1 = st.R + before;
         }
         f.nv_total += nsym;
     }
     st.R += nsym;
+    /* the last 32 bases: lane 63's second half and its context (both layouts) */
     st.code = ((uint64_t)rdlane(BC, 63) << 32) | rdlane(B2, 63);
     return true;
 }
@@ -543,7 +583,7 @@ __device__ void flush_counters(const Ctx &cx, Counters &cnt, uint32_t weight) {
 template <int HM>
 __device__ __forceinline__ void do_tile(const Ctx &cx, const uint32_t w[8], int64_t toff, uint32_t tile_off,
                                         bool full, DState &st, Facts &f, Counters &cnt, uint32_t weight) {
-    if (full && st.hdr == 0 && tile_fast<true, HM>(cx, w, st, f, cnt, weight)) return;
+    if (full && st.hdr == 0 && tile_fast<true, HM, false>(cx, w, st, f, cnt, weight)) return;
     const int lane = threadIdx.x & 63;
     uint32_t v[8];
     int nb = FK_LANE_BYTES;
@@ -701,6 +741,19 @@ k_count(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uin
     const int lane = threadIdx.x & 63;
     const uint64_t wave = blockIdx.x * FK_WAVES_PER_BLOCK + wave_in_block();
     const uint64_t c0 = wave * cpw, c1 = min(c0 + cpw, nchunks);
+    /* interleaved tile loads: lane L takes bytes [16L, 16L+16) and
+       [1024+16L, ...) of a 2 KiB tile, so each instruction reads one
+       contiguous KiB; the tile base is clamped into the range (a scalar), so
+       prefetches past its end re-read its last tile */
+#define FK_LOADI(dst, t_)                                                            \
+    {                                                                                \
+        const uint64_t tb_ = min(sp.rbase + (uint64_t)(t_) * FK_TILE_BYTES, last_tile); \
+        const u32x4 *p_ = reinterpret_cast<const u32x4 *>(cx.buf + tb_) + lane;      \
+        u32x4 v0_ = __builtin_nontemporal_load(p_);                                  \
+        u32x4 v1_ = __builtin_nontemporal_load(p_ + 64);                             \
+        dst[0] = v0_.x; dst[1] = v0_.y; dst[2] = v0_.z; dst[3] = v0_.w;               \
+        dst[4] = v1_.x; dst[5] = v1_.y; dst[6] = v1_.z; dst[7] = v1_.w;               \
+    }
     if (c0 < c1) {
         RangeRec hdr_r;
         hdr_r.c0 = c0;
@@ -712,7 +765,11 @@ k_count(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uin
             st.R = (uint32_t)d_init->R;
             st.code = d_init->code;
         } else {
+#if FK_EXP >= 3   /* ablation: no halo guess */
+            st = DState{0, 100000u, 0};
+#else
             st = halo_state<HM>(cx, sp.rbase);
+#endif
         }
         const DState first = st;
         Facts f{0, 0, 0, 0, 0, 0};
@@ -720,32 +777,33 @@ k_count(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uin
         uint32_t A[8], B[8], C[8];
         uint64_t t = 0;
         uint32_t general_left = general_tiles;
+        const uint64_t last_tile = sp.nfull ? sp.rend - FK_TILE_BYTES : sp.rbase;
         for (;;) {
             /* issue order A, B, C as in the loop (the barriers keep the
                compiler from reordering them, which would merge two different
                pending-load orders at the loop header) */
-            FK_LOADT(A, t);
+            FK_LOADI(A, t);
             asm volatile("" ::: "memory");
-            FK_LOADT(B, t + 1);
+            FK_LOADI(B, t + 1);
             asm volatile("" ::: "memory");
-            FK_LOADT(C, t + 2);
+            FK_LOADI(C, t + 2);
             /* one exit per group of three tiles and unconditional loads:
                every path into the latch has the same loads in flight, so each
                tile waits only for its own data */
             bool live = st.hdr == 0;
             for (uint64_t g = t; live; g += 3) {
-                live = t < sp.nfull && tile_fast<true, HM>(cx, A, st, f, cnt, 1u);
+                live = t < sp.nfull && tile_fast<true, HM, true>(cx, A, st, f, cnt, 1u);
                 t += live;
                 consume(A);
-                FK_LOADT(A, g + 3);
-                live = live && t < sp.nfull && tile_fast<true, HM>(cx, B, st, f, cnt, 1u);
+                FK_LOADI(A, g + 3);
+                live = live && t < sp.nfull && tile_fast<true, HM, true>(cx, B, st, f, cnt, 1u);
                 t += live;
                 consume(B);
-                FK_LOADT(B, g + 4);
-                live = live && t < sp.nfull && tile_fast<true, HM>(cx, C, st, f, cnt, 1u);
+                FK_LOADI(B, g + 4);
+                live = live && t < sp.nfull && tile_fast<true, HM, true>(cx, C, st, f, cnt, 1u);
                 t += live;
                 consume(C);
-                FK_LOADT(C, g + 5);
+                FK_LOADI(C, g + 5);
             }
             if (t >= sp.ntiles || general_left == 0) break;
             /* a tile the fast path cannot take (stream start, header, run
@@ -789,6 +847,7 @@ k_count(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uin
     }
     if (HM != H_GLOBAL) lds_flush<HM>(cx);
 }
+#undef FK_LOADI
 #undef FK_LOADT
 
 /*

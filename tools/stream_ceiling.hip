@@ -49,6 +49,40 @@ __global__ void k_range(const u32x4 *p, size_t n16, size_t tiles_per_wave, unsig
     if (acc == 0x12345678u) out[0] = acc;
 }
 
+/* 2 KiB tiles, two 16-B loads per lane; INTER: +1024 (contiguous per
+   instruction) instead of +16 (lane stride 32) */
+template <int DEPTH, bool INTER>
+__global__ void k_tile2(const u32x4 *p, size_t n16, size_t tiles_per_wave, unsigned *out) {
+    const size_t wave = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const size_t t0 = wave * tiles_per_wave;
+    unsigned acc = 0;
+    u32x4 a[DEPTH], b[DEPTH];
+    auto idx = [&](size_t t, int h) -> size_t {
+        return INTER ? t * 128 + h * 64 + lane : t * 128 + lane * 2 + h;
+    };
+#pragma unroll
+    for (int d = 0; d < DEPTH; d++) {
+        size_t i0 = idx(t0 + d, 0), i1 = idx(t0 + d, 1);
+        a[d] = i0 < n16 ? __builtin_nontemporal_load(p + i0) : u32x4{0, 0, 0, 0};
+        b[d] = i1 < n16 ? __builtin_nontemporal_load(p + i1) : u32x4{0, 0, 0, 0};
+    }
+    for (size_t t = 0; t < tiles_per_wave; t += DEPTH) {
+#pragma unroll
+        for (int d = 0; d < DEPTH; d++) {
+            u32x4 va = a[d], vb = b[d];
+            size_t tn = t0 + t + DEPTH + d;
+            size_t i0 = idx(tn, 0), i1 = idx(tn, 1);
+            if (t + DEPTH + d < tiles_per_wave && i1 < n16) {
+                a[d] = __builtin_nontemporal_load(p + i0);
+                b[d] = __builtin_nontemporal_load(p + i1);
+            }
+            acc ^= va.x + va.y + va.z + va.w + vb.x + vb.y + vb.z + vb.w;
+        }
+    }
+    if (acc == 0x12345678u) out[0] = acc;
+}
+
 template <typename F>
 static double time_ms(F f, int reps) {
     hipEvent_t a, b;
@@ -81,9 +115,15 @@ int main(int argc, char **argv) {
         double b4 = time_ms([&] { hipLaunchKernelGGL((k_range<4, true>), dim3(blocks), dim3(512), 0, 0, p, n16, tpw, out); }, 20);
         double b8 = time_ms([&] { hipLaunchKernelGGL((k_range<8, true>), dim3(blocks), dim3(512), 0, 0, p, n16, tpw, out); }, 20);
         double d4 = time_ms([&] { hipLaunchKernelGGL((k_range<4, false>), dim3(blocks), dim3(512), 0, 0, p, n16, tpw, out); }, 20);
+        size_t tpw2 = (tiles / 2 + waves - 1) / waves;
+        double e3 = time_ms([&] { hipLaunchKernelGGL((k_tile2<3, false>), dim3(blocks), dim3(512), 0, 0, p, n16, tpw2, out); }, 20);
+        double f3 = time_ms([&] { hipLaunchKernelGGL((k_tile2<3, true>), dim3(blocks), dim3(512), 0, 0, p, n16, tpw2, out); }, 20);
+        double f4 = time_ms([&] { hipLaunchKernelGGL((k_tile2<4, true>), dim3(blocks), dim3(512), 0, 0, p, n16, tpw2, out); }, 20);
         printf("{\"waves_per_cu\": %d, \"bytes\": %zu, \"grid_stride_GBps\": %.1f, \"range_depth4_nt_GBps\": %.1f, "
-               "\"range_depth8_nt_GBps\": %.1f, \"range_depth4_GBps\": %.1f}\n",
-               wpc, bytes, bytes / a / 1e6, bytes / b4 / 1e6, bytes / b8 / 1e6, bytes / d4 / 1e6);
+               "\"range_depth8_nt_GBps\": %.1f, \"range_depth4_GBps\": %.1f, \"tile2k_stride32_d3_GBps\": %.1f, "
+               "\"tile2k_inter_d3_GBps\": %.1f, \"tile2k_inter_d4_GBps\": %.1f}\n",
+               wpc, bytes, bytes / a / 1e6, bytes / b4 / 1e6, bytes / b8 / 1e6, bytes / d4 / 1e6, bytes / e3 / 1e6,
+               bytes / f3 / 1e6, bytes / f4 / 1e6);
     }
     return 0;
 }
