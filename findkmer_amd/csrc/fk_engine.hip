@@ -661,22 +661,32 @@ __device__ void range_obs(const Ctx &cx, Counters &cnt, uint32_t weight, const S
     }
 }
 
-/* Guess the state entering byte `start` from the FK_HALO_BYTES before it. */
+/* Guess the state entering a range from the FK_HALO_BYTES before it (lanes
+ * 0..7 hold them, 32 contiguous bytes each; `valid` = this lane's bytes are
+ * readable input).  All bases (the common case): R = 256 and the last 32
+ * bases, packed as the fast path packs them; otherwise the general walk. */
 template <int HM>
-__device__ DState halo_state(const Ctx &cx, uint64_t start) {
-    const int lane = threadIdx.x & 63;
-    const int64_t hs = (int64_t)start - (int64_t)FK_HALO_BYTES;
-    uint32_t w[8];
-    int nb = 0;
-    if (lane < (int)(FK_HALO_BYTES / FK_LANE_BYTES)) nb = load_lane<FK_LANE_BYTES>(cx, hs + lane * (int64_t)FK_LANE_BYTES, w);
-    else {
+__device__ DState halo_guess(const Ctx &cx, const uint32_t w[8], bool valid) {
+    const uint32_t hl = FK_HALO_BYTES / FK_LANE_BYTES;
+    uint32_t x[8];
+    uint32_t mis = 0;
 #pragma unroll
-        for (int d = 0; d < 8; d++) w[d] = 0;
+    for (int d = 0; d < 8; d++) {
+        x[d] = (w[d] >> 1) & 0x03030303u;
+        mis |= __builtin_amdgcn_perm(0u, 0x47544341u, x[d]) ^ w[d];
     }
+    const uint64_t vm = __ballot(valid), bad = __ballot(valid && mis);
+    if (vm == (1ull << hl) - 1 && bad == 0) {
+        const uint32_t hi = rdlane(pack16(x), hl - 1), lo32 = rdlane(pack16(x + 4), hl - 1);
+        return DState{((uint64_t)hi << 32) | lo32, FK_HALO_BYTES, 0};
+    }
+    uint32_t v[8];
+#pragma unroll
+    for (int d = 0; d < 8; d++) v[d] = valid ? w[d] : 0u;
     DState st{0, 0, 0};
     Facts f{0, 0, 0, 0, 0, 0};
     Counters cnt{0, 0, 0, 0, 0, FK_NO_EOF};
-    tile_general<false, HM>(cx, w, nb, 0, st, f, cnt, 1u);
+    tile_general<false, HM>(cx, v, valid ? (int)FK_LANE_BYTES : 0, 0, st, f, cnt, 1u);
     return st;
 }
 
@@ -735,7 +745,6 @@ k_count(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uin
         if (threadIdx.x == 11) res->redo_n = 0;
     }
     const uint32_t nw = lds_words(HM, k);
-    if (HM != H_GLOBAL) lds_zero(lds_bins, nw);
     Ctx cx{buf, len, lo, table, HM != H_GLOBAL ? lds_bins : nullptr, shortcnt, acc, res, maskk,
            1u << (2 * k + 2), k};
     const int lane = threadIdx.x & 63;
@@ -744,7 +753,7 @@ k_count(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uin
     /* interleaved tile loads: lane L takes bytes [16L, 16L+16) and
        [1024+16L, ...) of a 2 KiB tile, so each instruction reads one
        contiguous KiB; the tile base is clamped into the range (a scalar), so
-       prefetches past its end re-read its last tile */
+       prefetches past its end re-read its last full tile */
 #define FK_LOADI(dst, t_)                                                            \
     {                                                                                \
         const uint64_t tb_ = min(sp.rbase + (uint64_t)(t_) * FK_TILE_BYTES, last_tile); \
@@ -754,11 +763,41 @@ k_count(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uin
         dst[0] = v0_.x; dst[1] = v0_.y; dst[2] = v0_.z; dst[3] = v0_.w;               \
         dst[4] = v1_.x; dst[5] = v1_.y; dst[6] = v1_.z; dst[7] = v1_.w;               \
     }
-    if (c0 < c1) {
-        RangeRec hdr_r;
-        hdr_r.c0 = c0;
-        hdr_r.c1 = c1;
-        const Span sp = range_span(hdr_r, len);
+    const bool has = c0 < c1;
+    RangeRec hdr_r;
+    hdr_r.c0 = has ? c0 : 0;
+    hdr_r.c1 = has ? c1 : 0;
+    const Span sp = range_span(hdr_r, len);
+    const uint64_t last_tile = sp.nfull ? sp.rend - FK_TILE_BYTES : 0;
+    /* prologue, all loads first: the halo before the range (lanes 0..7, 32
+       contiguous bytes each, clamped to valid memory), then the first three
+       tiles; LDS is zeroed and the halo state computed while they fly */
+    uint32_t hw[8];
+    const int64_t ho = (int64_t)sp.rbase - (int64_t)FK_HALO_BYTES + (int64_t)lane * FK_LANE_BYTES;
+    const bool hv = has && lane < (int)(FK_HALO_BYTES / FK_LANE_BYTES) && ho >= lo;
+    {
+        /* inputs shorter than a lane are staged in a large buffer, so
+           [lo, lo+32) is always readable */
+        const int64_t hc = max(min(ho, (int64_t)len - (int64_t)FK_LANE_BYTES), lo);
+        const u32x4 *hp = reinterpret_cast<const u32x4 *>(buf + hc);
+        u32x4 h0 = __builtin_nontemporal_load(hp), h1 = __builtin_nontemporal_load(hp + 1);
+        hw[0] = h0.x; hw[1] = h0.y; hw[2] = h0.z; hw[3] = h0.w;
+        hw[4] = h1.x; hw[5] = h1.y; hw[6] = h1.z; hw[7] = h1.w;
+    }
+    uint32_t A[8], B[8], C[8];
+    if (sp.nfull) {
+        /* issue order A, B, C as in the loop (the barriers keep the compiler
+           from reordering them, which would merge two different pending-load
+           orders at the loop header) */
+        asm volatile("" ::: "memory");
+        FK_LOADI(A, 0);
+        asm volatile("" ::: "memory");
+        FK_LOADI(B, 1);
+        asm volatile("" ::: "memory");
+        FK_LOADI(C, 2);
+    }
+    if (HM != H_GLOBAL) lds_zero(lds_bins, nw);
+    if (has) {
         DState st;
         if (c0 == 0 && has_init) {
             st.hdr = d_init->hdr;
@@ -768,42 +807,35 @@ k_count(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uin
 #if FK_EXP >= 3   /* ablation: no halo guess */
             st = DState{0, 100000u, 0};
 #else
-            st = halo_state<HM>(cx, sp.rbase);
+            st = halo_guess<HM>(cx, hw, hv);
 #endif
         }
         const DState first = st;
         Facts f{0, 0, 0, 0, 0, 0};
         Counters cnt{0, 0, 0, 0, 0, FK_NO_EOF};
-        uint32_t A[8], B[8], C[8];
         uint64_t t = 0;
         uint32_t general_left = general_tiles;
-        const uint64_t last_tile = sp.nfull ? sp.rend - FK_TILE_BYTES : sp.rbase;
+        bool primed = sp.nfull > 0;
         for (;;) {
-            /* issue order A, B, C as in the loop (the barriers keep the
-               compiler from reordering them, which would merge two different
-               pending-load orders at the loop header) */
-            FK_LOADI(A, t);
-            asm volatile("" ::: "memory");
-            FK_LOADI(B, t + 1);
-            asm volatile("" ::: "memory");
-            FK_LOADI(C, t + 2);
-            /* one exit per group of three tiles and unconditional loads:
-               every path into the latch has the same loads in flight, so each
-               tile waits only for its own data */
-            bool live = st.hdr == 0;
-            for (uint64_t g = t; live; g += 3) {
-                live = t < sp.nfull && tile_fast<true, HM, true>(cx, A, st, f, cnt, 1u);
-                t += live;
-                consume(A);
-                FK_LOADI(A, g + 3);
-                live = live && t < sp.nfull && tile_fast<true, HM, true>(cx, B, st, f, cnt, 1u);
-                t += live;
-                consume(B);
-                FK_LOADI(B, g + 4);
-                live = live && t < sp.nfull && tile_fast<true, HM, true>(cx, C, st, f, cnt, 1u);
-                t += live;
-                consume(C);
-                FK_LOADI(C, g + 5);
+            if (primed) {
+                /* one exit per group of three tiles and unconditional loads:
+                   every path into the latch has the same loads in flight, so each
+                   tile waits only for its own data */
+                bool live = st.hdr == 0;
+                for (uint64_t g = t; live; g += 3) {
+                    live = t < sp.nfull && tile_fast<true, HM, true>(cx, A, st, f, cnt, 1u);
+                    t += live;
+                    consume(A);
+                    FK_LOADI(A, g + 3);
+                    live = live && t < sp.nfull && tile_fast<true, HM, true>(cx, B, st, f, cnt, 1u);
+                    t += live;
+                    consume(B);
+                    FK_LOADI(B, g + 4);
+                    live = live && t < sp.nfull && tile_fast<true, HM, true>(cx, C, st, f, cnt, 1u);
+                    t += live;
+                    consume(C);
+                    FK_LOADI(C, g + 5);
+                }
             }
             if (t >= sp.ntiles || general_left == 0) break;
             /* a tile the fast path cannot take (stream start, header, run
@@ -814,6 +846,15 @@ k_count(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uin
             const int nb = load_lane<FK_LANE_BYTES>(cx, toff + lane * (int64_t)FK_LANE_BYTES, v);
             tile_general<true, HM>(cx, v, nb, (uint32_t)(t * FK_TILE_BYTES), st, f, cnt, 1u);
             t++;
+            primed = t < sp.nfull;
+            if (primed) {
+                asm volatile("" ::: "memory");
+                FK_LOADI(A, t);
+                asm volatile("" ::: "memory");
+                FK_LOADI(B, t + 1);
+                asm volatile("" ::: "memory");
+                FK_LOADI(C, t + 2);
+            }
         }
         flush_counters(cx, cnt, 1u);
         const uint32_t unk = wsum32(cnt.unknown);
