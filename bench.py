@@ -42,6 +42,8 @@ def parse():
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--cpu-sample-bytes", type=int, default=0, help="0 = auto (~10-20 s of reference CPU work)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="nccl = RCCL over xGMI (one GPU per rank); gloo = host-side rehearsal")
     return ap.parse_args()
 
 
@@ -80,11 +82,17 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
     import findkmer_amd as fk
+    import findkmer_amd.dist as fkdist
+    # a gloo rehearsal may put several ranks on one GPU
+    local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
     k = args.k
     n = args.bases
     L = args.fasta_line
@@ -109,28 +117,17 @@ def main():
     torch.cuda.synchronize()
 
     eng = fk.Engine(k, device=local)
-    table_t = torch.empty(1 << (2 * k), dtype=torch.int32, device="cuda") if world > 1 else None
+    coll_dev = "cuda" if args.dist_backend == "nccl" else "cpu"
+    table_t = torch.empty(1 << (2 * k), dtype=torch.int32, device=coll_dev) if world > 1 else None
 
     def step():
         eng.reset()
         if world == 1:
             eng.feed_device(buf.data_ptr(), nbytes)
         else:
-            eng.feed_shard_device(buf.data_ptr() + halo, nbytes, halo)
-            s = eng.summary()
-            mine = torch.tensor(list(s.w), dtype=torch.int64, device="cuda")
-            allv = [torch.empty_like(mine) for _ in range(world)]
-            dist.all_gather(allv, mine)
-            st = fk.FkState()
-            for r in range(rank):
-                sm = fk.FkSummary()
-                for i, v in enumerate(allv[r].tolist()):
-                    sm.w[i] = v & 0xFFFFFFFFFFFFFFFF
-                st = fk.summary_apply(sm, st)
-            eng.resolve(st)
-            eng.table_to_device(table_t.data_ptr())
-            dist.all_reduce(table_t)          # u32 sums, bitwise identical in int32
-            eng.table_from_device(table_t.data_ptr())
+            # shard, stitch entry states (all-gather of 96-B summaries), merge
+            # tables (all-reduce): findkmer_amd/dist.py
+            fkdist.count_sharded(eng, buf.data_ptr() + halo, nbytes, halo, table_t)
         # an ablation build (FINDKMER_LIB) may leave the table incomplete
         rc, r = eng.finish(allow=(fk.FK_OK, fk.FK_E_ROLLOVER) if os.environ.get("FINDKMER_LIB") else (fk.FK_OK,))
         return r
@@ -142,24 +139,30 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     main_ms = 0.0
-    dev_ms = 0.0
     last = None
     for _ in range(args.steps):
         last = step()
         main_ms += last.main_kernel_ms
-        dev_ms += last.device_ms
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     dt = time.perf_counter() - t0
     if dist:
-        tt = torch.tensor([dt], dtype=torch.float64, device="cuda")
+        tt = torch.tensor([dt], dtype=torch.float64, device=coll_dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
 
-    # correctness guard on the measured pass (pure ACGT: every window counts)
-    if L == 0 and world == 1 and not os.environ.get("FINDKMER_LIB"):
-        assert last.windows == n - k + 1, (last.windows, n - k + 1)
+    # correctness guard on the measured pass: the synthetic stream (pure ACGT,
+    # or FASTA whose '\n' are transparent) is one run, every window counts
+    if not os.environ.get("FINDKMER_LIB"):
+        total = last.windows
+        if dist:
+            w_t = torch.tensor([last.windows], dtype=torch.int64, device=coll_dev)
+            dist.all_reduce(w_t)
+            total = int(w_t.item())
+            merged = int(table_t.to(torch.int64).remainder(1 << 32).sum().item())
+            assert merged == total, (merged, total)
+        assert total == world * n - k + 1, (total, world * n - k + 1)
 
     ms_step = dt / args.steps * 1e3
     value = world * n / (dt / args.steps)
@@ -199,10 +202,10 @@ def main():
             "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
             "kernel": "k_count", "kernel_ms": kern_ms, "algorithmic_bytes": algo_bytes,
         },
-        "device_ms_per_step": dev_ms / args.steps,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        sample = args.cpu_sample_bytes or (512 << 20 if k <= 7 else 48 << 20)
+        # ~15 s of reference CPU work: ~76 Mbases/s at k=6, ~3 Mbases/s at k=11
+        sample = args.cpu_sample_bytes or (1 << 30 if k <= 7 else 48 << 20)
         sample = min(sample, n)
         out["cpu_baseline"] = cpu_baseline(args, sample)
     if rank == 0:

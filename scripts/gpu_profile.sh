@@ -2,7 +2,7 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-OUT=gpurun_out/prof
+OUT=${OUT:-gpurun_out/prof}
 mkdir -p $OUT
 K=${K:-6}; L=${L:-0}
 B="bench.py --k $K --fasta-line $L --steps ${STEPS:-10} --warmup 3 --no-cpu-baseline"
