@@ -75,6 +75,16 @@ def cpu_baseline(args, n_sample):
             "sample": what, "seconds": round(dt, 3)}
 
 
+def run_windows(n, k):
+    """Windows the reference counts in one run of n bases: those where its
+    `int seqSize` (findKmer.cpp:977) is >= k, i.e. R mod 2^32 in
+    [k, 2^31 - 1] for R = 1..n (a run longer than 2^31 - 1 bases stops
+    counting until the int32 wraps back to positive values)."""
+    period, hi = 1 << 32, (1 << 31) - 1
+    full, rem = divmod(n, period)
+    return full * (hi - k + 1) + max(0, min(rem, hi) - k + 1)
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -162,7 +172,7 @@ def main():
             total = int(w_t.item())
             merged = int(table_t.to(torch.int64).remainder(1 << 32).sum().item())
             assert merged == total, (merged, total)
-        assert total == world * n - k + 1, (total, world * n - k + 1)
+        assert total == run_windows(world * n, k), (total, run_windows(world * n, k))
 
     ms_step = dt / args.steps * 1e3
     value = world * n / (dt / args.steps)
@@ -173,7 +183,10 @@ def main():
     tf = os.path.join(REPO, "profiles", f"traffic_k{k}_L{L}.json")
     if os.path.exists(tf):
         try:
-            traffic = json.load(open(tf)).get("hbm_bytes_per_launch")
+            prof = json.load(open(tf))
+            # only a profile of this exact workload size describes this launch
+            if prof.get("input_bytes") == nbytes:
+                traffic = prof.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
     out = {

@@ -482,7 +482,12 @@ __device__ __forceinline__ bool tile_fast(const Ctx &cx, const uint32_t w[8], DS
         lane_ok = (b0 | b1) == 0 && __popc(nl0) <= 1 && __popc(nl1) <= 1;
     }
     if (__ballot(!lane_ok)) return false;
-    if (COUNT && !((int32_t)st.R >= k && st.R <= 0x7FFFFFFFu - FK_TILE_BYTES)) return false;
+    /* deep: every window of the tile counts (seq > k throughout); neg: the
+       reference's int32 seqSize stays negative for the whole tile (a run
+       past 2^31-1 bases, :977), so the tile only advances the state */
+    const bool deep = (int32_t)st.R >= k && st.R <= 0x7FFFFFFFu - FK_TILE_BYTES;
+    const bool neg = (int32_t)st.R < 0 && st.R <= 0xFFFFFFFFu - FK_TILE_BYTES;
+    if (COUNT && !deep && !neg) return false;
 
     uint32_t S0 = pack16(x), S1 = pack16(x + 4);
     const bool h0 = nl0 != 0, h1 = nl1 != 0;
@@ -504,13 +509,15 @@ __device__ __forceinline__ bool tile_fast(const Ctx &cx, const uint32_t w[8], DS
     const uint64_t nb0 = __ballot(h0), nb1 = __ballot(h1);
     const uint32_t nsym = FK_TILE_BYTES - (uint32_t)__popcll(nb0) - (uint32_t)__popcll(nb1);
     if (COUNT) {
+        if (deep) {
 #if FK_EXP == 2   /* ablation: no window work at all */
-        asm volatile("" ::"v"(AC), "v"(A2), "v"(BC), "v"(B2));
+            asm volatile("" ::"v"(AC), "v"(A2), "v"(BC), "v"(B2));
 #else
-        half_windows<HM>(cx, AC, A2, h0, weight);
-        half_windows<HM>(cx, BC, B2, h1, weight);
+            half_windows<HM>(cx, AC, A2, h0, weight);
+            half_windows<HM>(cx, BC, B2, h1, weight);
 #endif
-        if (lane == 0) cnt.win += nsym;
+            if (lane == 0) cnt.win += nsym;
+        }
         /* facts: the first '\n' of the span (all bytes before it are bases) */
         if (!f.found_p1 && (nb0 | nb1)) {
             uint32_t before;

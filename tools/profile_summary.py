@@ -52,7 +52,9 @@ if fetch and write:
     hbm = f_kib * 1024 * 2 + w_kib * 1024
     summary["k_count_pmc"] = {"launches": len(fetch), "fetch_size_kib": f_kib, "write_size_kib": w_kib,
                               "hbm_bytes_per_launch": hbm}
-    json.dump({"kernel": "k_count", "k": k, "fasta_line": L, "hbm_bytes_per_launch": hbm,
+    input_bytes = int(sys.argv[5]) if len(sys.argv) > 5 else None
+    json.dump({"kernel": "k_count", "k": k, "fasta_line": L, "input_bytes": input_bytes,
+               "hbm_bytes_per_launch": hbm,
                "fetch_size_kib": f_kib, "write_size_kib": w_kib,
                "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes over "
                          f"`bench.py --k {k} --fasta-line {L}`; bytes = 2*FETCH_SIZE*1024 (gfx950 "
