@@ -21,6 +21,7 @@
 #define FK_HALO_BYTES 256u             /* bytes before a chunk used to guess state */
 #define FK_BLOCK 512u
 #define FK_COUNT_GENERAL_TILES 8u      /* general-path tiles k_count takes per range */
+#define FK_SUBTABLES 16                /* table copies k_count's blocks flush into (LDS modes) */
 #define FK_WAVES_PER_BLOCK (FK_BLOCK / 64u)
 
 /* accumulator slots (u64, device) */

@@ -137,6 +137,7 @@ struct Ctx {            /* kernel-wide constants */
     uint64_t maskk;
     uint32_t single_off;/* H_PAIRS: offset of the k-mer singles in LDS (4^(k+1)) */
     int k;
+    uint32_t *flush;    /* where lds_flush adds the bins (nullptr: table) */
 };
 
 /* idx in the internal encoding (A0 C1 T2 G3) */
@@ -722,7 +723,11 @@ __device__ void lds_flush(const Ctx &cx) {
         } else {
             v = cx.lds[i];
         }
-        if (v) atomicAdd(&cx.table[fk_sigma(i)], v);
+#if FK_EXP == 5   /* ablation: no bin flush to the global table */
+        asm volatile("" ::"v"(v));
+#else
+        if (v) atomicAdd(&(cx.flush ? cx.flush : cx.table)[fk_sigma(i)], v);
+#endif
     }
 }
 
@@ -742,7 +747,7 @@ __global__ void __launch_bounds__(FK_BLOCK, 2)
 k_count(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint32_t *table,
         uint32_t *shortcnt, unsigned long long *acc, DevRes *res, RangeRec *rr,
         uint64_t nchunks, const XState *d_init, int has_init, uint64_t cpw, ResumeRec *resume,
-        uint32_t general_tiles) {
+        uint32_t general_tiles, uint32_t *subs) {
     extern __shared__ uint32_t lds_bins[];
     /* open the feed's result block (the kernels after this one in the
        stream accumulate into it) */
@@ -752,8 +757,12 @@ k_count(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uin
         if (threadIdx.x == 11) res->redo_n = 0;
     }
     const uint32_t nw = lds_words(HM, k);
+    /* the 509-odd blocks flush their bins into FK_SUBTABLES copies of the
+       table (fewer same-address atomics at the end of the kernel);
+       k_table_stats folds them into the table */
     Ctx cx{buf, len, lo, table, HM != H_GLOBAL ? lds_bins : nullptr, shortcnt, acc, res, maskk,
-           1u << (2 * k + 2), k};
+           1u << (2 * k + 2), k,
+           subs ? subs + (size_t)(blockIdx.x % FK_SUBTABLES) * ((size_t)1 << (2 * k)) : nullptr};
     const int lane = threadIdx.x & 63;
     const uint64_t wave = blockIdx.x * FK_WAVES_PER_BLOCK + wave_in_block();
     const uint64_t c0 = wave * cpw, c1 = min(c0 + cpw, nchunks);
@@ -1125,16 +1134,27 @@ __device__ __forceinline__ unsigned long long wsum64(unsigned long long v) {
     for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
     return v;
 }
-__global__ void k_table_stats(const uint32_t *table, uint64_t n, int k, DevRes *res,
-                              const unsigned long long *acc, DevRes *host_res, uint32_t *done, uint32_t seq) {
+__global__ void k_table_stats(uint32_t *table, uint64_t n, int k, DevRes *res,
+                              const unsigned long long *acc, DevRes *host_res, uint32_t *done, uint32_t seq,
+                              uint32_t *subs, int nsub) {
     unsigned long long *out = res->tstat;
     if (blockIdx.x == 0 && threadIdx.x < ACC_N) res->acc[threadIdx.x] = acc[threadIdx.x];
     unsigned long long dist = 0, sum = 0, last[4] = {0, 0, 0, 0}, first[4] = {0, 0, 0, 0};
     const uint64_t n4 = n / 4;
-    const uint4 *t4 = reinterpret_cast<const uint4 *>(table);
+    uint4 *t4 = reinterpret_cast<uint4 *>(table);
     const int fs = 2 * (k - 1);
     for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n4; i += (uint64_t)gridDim.x * blockDim.x) {
         uint4 v = t4[i];
+        if (nsub) {
+            /* fold k_count's sub-tables into the table (and clear them) */
+            for (int s = 0; s < nsub; s++) {
+                uint4 *p = reinterpret_cast<uint4 *>(subs + (size_t)s * n) + i;
+                const uint4 a = *p;
+                v.x += a.x; v.y += a.y; v.z += a.z; v.w += a.w;
+                *p = make_uint4(0, 0, 0, 0);
+            }
+            t4[i] = v;
+        }
         dist += (v.x != 0) + (v.y != 0) + (v.z != 0) + (v.w != 0);
         unsigned long long s4 = (unsigned long long)v.x + v.y + v.z + v.w;
         sum += s4;
@@ -1292,11 +1312,13 @@ __global__ void k_add_short(uint32_t *shortcnt, uint64_t idx) { atomicAdd(&short
 /* engine reset: table, short-walk counts, accumulators and stream state in
    one launch */
 __global__ void k_zero(uint32_t *table, uint64_t nbins, uint32_t *shortcnt, uint64_t nshort,
-                       unsigned long long *acc, XState *state) {
+                       unsigned long long *acc, XState *state, uint32_t *subs, int nsub) {
     const uint64_t i0 = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
     const uint64_t step = (uint64_t)gridDim.x * blockDim.x;
     uint4 *t4 = reinterpret_cast<uint4 *>(table);
     for (uint64_t i = i0; i < nbins / 4; i += step) t4[i] = make_uint4(0, 0, 0, 0);
+    uint4 *s4 = reinterpret_cast<uint4 *>(subs);
+    for (uint64_t i = i0; i < (uint64_t)nsub * nbins / 4; i += step) s4[i] = make_uint4(0, 0, 0, 0);
     for (uint64_t i = (nbins / 4) * 4 + i0; i < nbins; i += step) table[i] = 0;
     for (uint64_t i = i0; i < nshort; i += step) shortcnt[i] = 0;
     if (i0 < ACC_N) acc[i0] = 0;
@@ -1374,6 +1396,7 @@ struct fk_engine {
     uint32_t general_tiles = FK_COUNT_GENERAL_TILES;   /* per range in k_count (env FK_GENERAL_TILES) */
     /* device state */
     uint32_t *d_table = nullptr, *d_short = nullptr;
+    uint32_t *d_sub = nullptr;                /* FK_SUBTABLES table copies k_count flushes into (LDS modes) */
     unsigned long long *d_acc = nullptr;      /* ACC_N, engine lifetime */
     DevRes *d_res = nullptr;                  /* per feed */
     unsigned long long *d_tmp = nullptr;      /* scratch counters */
@@ -1410,7 +1433,7 @@ struct fk_engine {
 };
 
 __global__ void k_zero(uint32_t *table, uint64_t nbins, uint32_t *shortcnt, uint64_t nshort,
-                       unsigned long long *acc, XState *state);
+                       unsigned long long *acc, XState *state, uint32_t *subs, int nsub);
 
 /* A reset is issued lazily, with the next device work (every API entry that
    touches the device goes through set_dev), so that it reaches the GPU
@@ -1421,7 +1444,7 @@ static int flush_zero(fk_engine *e) {
     const uint64_t work = std::max<uint64_t>(e->nbins / 4, std::max<uint64_t>(e->nshort, ACC_N));
     const unsigned grid = (unsigned)std::min<uint64_t>((uint64_t)e->cus * 8, (work + 255) / 256);
     hipLaunchKernelGGL(k_zero, dim3(grid), dim3(256), 0, e->stream, e->d_table, e->nbins, e->d_short, e->nshort,
-                       e->d_acc, e->d_state);
+                       e->d_acc, e->d_state, e->d_sub, e->d_sub ? FK_SUBTABLES : 0);
     HIPCHK(hipGetLastError());
     return FK_OK;
 }
@@ -1488,7 +1511,7 @@ extern "C" void fk_engine_destroy(fk_engine *e) {
     if (!e) return;
     hipSetDevice(e->dev);
     if (e->stream) hipStreamSynchronize(e->stream);
-    hipFree(e->d_table); hipFree(e->d_short); hipFree(e->d_acc); hipFree(e->d_res); hipFree(e->d_tmp);
+    hipFree(e->d_table); hipFree(e->d_short); hipFree(e->d_sub); hipFree(e->d_acc); hipFree(e->d_res); hipFree(e->d_tmp);
     hipFree(e->d_state); hipFree(e->d_rr); hipFree(e->d_rtrue);
     hipFree(e->d_redo); hipFree(e->d_tf); hipFree(e->d_stage); hipFree(e->d_resume);
     hipFree(e->d_aggs); hipFree(e->d_flags);
@@ -1534,6 +1557,13 @@ extern "C" int fk_engine_create(int k, const fk_opts *opts, fk_engine **out) {
 #define ALLOC(p, bytes)                                                         \
     if (hipMalloc((void **)&(p), (bytes)) != hipSuccess) { fk_engine_destroy(e); return FK_E_OOM; }
     ALLOC(e->d_table, e->nbins * sizeof(uint32_t));
+    if (hist_mode(e) != H_GLOBAL) {
+        ALLOC(e->d_sub, FK_SUBTABLES * e->nbins * sizeof(uint32_t));
+        if (hipMemsetAsync(e->d_sub, 0, FK_SUBTABLES * e->nbins * sizeof(uint32_t), e->stream) != hipSuccess) {
+            fk_engine_destroy(e);
+            return FK_E_HIP;
+        }
+    }
     if (e->nshort) { ALLOC(e->d_short, e->nshort * sizeof(uint32_t)); }
     ALLOC(e->d_acc, ACC_N * sizeof(unsigned long long));
     ALLOC(e->d_res, sizeof(DevRes));
@@ -1623,7 +1653,8 @@ static int launch_count(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t 
                 hipExtLaunchKernelGGL((k_count<HM>), dim3(g.grid), dim3(FK_BLOCK), sh, e->stream, e->ev[0], e->ev[1],
                                       0, buf, len, lo, e->k,
                                    e->maskk, e->d_table, e->d_short, e->d_acc, e->d_res, e->d_rr,
-                                   g.nchunks, e->d_state, has_init, g.cpw, e->d_resume, e->general_tiles));
+                                   g.nchunks, e->d_state, has_init, g.cpw, e->d_resume, e->general_tiles,
+                                   e->d_sub));
     HIPCHK(hipGetLastError());
     return FK_OK;
 }
@@ -1669,7 +1700,8 @@ static int launch_table_stats(fk_engine *e, bool zero_first, hipEvent_t stop = n
     unsigned gd = (unsigned)std::min<uint64_t>((uint64_t)e->cus * 4, (e->nbins / 4 + 255) / 256 + 1);
     if (++e->res_seq == 0) e->res_seq = 1;
     hipExtLaunchKernelGGL(k_table_stats, dim3(gd), dim3(256), 0, e->stream, nullptr, stop, 0, e->d_table,
-                          e->nbins, e->k, e->d_res, e->d_acc, e->h_res_dev, e->d_done, e->res_seq);
+                          e->nbins, e->k, e->d_res, e->d_acc, e->h_res_dev, e->d_done, e->res_seq, e->d_sub,
+                          e->d_sub ? FK_SUBTABLES : 0);
     HIPCHK(hipGetLastError());
     return FK_OK;
 }
