@@ -122,7 +122,20 @@ struct Counters {       /* per lane; flushed per range */
 enum HistMode {
     H_PAIRS = 0,    /* k <= 6: LDS bins of (k+1)-mers at every other base + LDS k-mer singles */
     H_LDS = 1,      /* k == 7: LDS k-mer bins */
-    H_GLOBAL = 2    /* k >= 8: global u32 atomics */
+    H_GLOBAL = 2,   /* k >= 13, and cancellations: global u32 atomics */
+    H_NONE = 3,     /* 8 <= k <= 12, state pass: count nothing, only the scan state */
+    H_EMIT = 4      /* 8 <= k <= 12, k_part: fast tiles hand their windows to the
+                       partition, general tiles use global atomics */
+};
+
+/* a fast tile's windows for the partition (k_part): per half, the context
+   word, the 16-slot word and whether slot 0 is not a window */
+/* the modes that keep bins in LDS (zeroed at start, flushed at the end) */
+#define LDS_MODE(hm) ((hm) == H_PAIRS || (hm) == H_LDS)
+
+struct Emit {
+    uint32_t AC, A2, BC, B2;
+    bool h0, h1, deep;
 };
 
 struct Ctx {            /* kernel-wide constants */
@@ -143,7 +156,8 @@ struct Ctx {            /* kernel-wide constants */
 /* idx in the internal encoding (A0 C1 T2 G3) */
 template <int HM>
 __device__ __forceinline__ void hist_add(const Ctx &cx, uint64_t idx, uint32_t w) {
-    if (HM == H_GLOBAL) {
+    if (HM == H_NONE) return;
+    if (HM == H_GLOBAL || HM == H_EMIT) {
         atomicAdd(&cx.table[fk_sigma(idx)], w);
     } else if (HM == H_LDS) {
         atomicAdd(&cx.lds[(uint32_t)idx], w);
@@ -308,7 +322,7 @@ __device__ __forceinline__ void tile_general(const Ctx &cx, const uint32_t w[8],
             int s = fk_sym(c);
             if (s < 0) {                      /* run break: '>', N, other */
                 int seq = (int)R;
-                if (seq >= 1 && seq < k) short_run(cx, seq, lc, weight);
+                if (HM != H_NONE && seq >= 1 && seq < k) short_run(cx, seq, lc, weight);
                 R = 0;
                 lane_reset = 1;
                 if (f.found_p1 || (p1_here && pos > p1)) lane_reset_after = 1;
@@ -453,7 +467,7 @@ __device__ __forceinline__ void half_windows(const Ctx &cx, uint32_t C, uint32_t
  */
 template <bool COUNT, int HM, bool INTER>
 __device__ __forceinline__ bool tile_fast(const Ctx &cx, const uint32_t w[8], DState &st, Facts &f,
-                                          Counters &cnt, uint32_t weight) {
+                                          Counters &cnt, uint32_t weight, Emit *em = nullptr) {
 #if FK_EXP == 4   /* ablation: loop framework only */
     {
         uint32_t x = 0;
@@ -510,7 +524,12 @@ __device__ __forceinline__ bool tile_fast(const Ctx &cx, const uint32_t w[8], DS
     const uint64_t nb0 = __ballot(h0), nb1 = __ballot(h1);
     const uint32_t nsym = FK_TILE_BYTES - (uint32_t)__popcll(nb0) - (uint32_t)__popcll(nb1);
     if (COUNT) {
-        if (deep) {
+        if (HM == H_EMIT) {
+            em->AC = AC; em->A2 = A2; em->BC = BC; em->B2 = B2;
+            em->h0 = h0; em->h1 = h1; em->deep = deep;
+            if (deep && lane == 0) cnt.win += nsym;
+        } else if (HM == H_NONE) {
+        } else if (deep) {
 #if FK_EXP == 2   /* ablation: no window work at all */
             asm volatile("" ::"v"(AC), "v"(A2), "v"(BC), "v"(B2));
 #else
@@ -560,7 +579,7 @@ __device__ __forceinline__ void acc_add(unsigned long long *a, uint64_t v, uint3
     if (v) atomicAdd(a, (unsigned long long)(weight == 1u ? v : (0ull - v)));
 }
 
-__device__ void flush_counters(const Ctx &cx, Counters &cnt, uint32_t weight) {
+__device__ void flush_counters(const Ctx &cx, Counters &cnt, uint32_t weight, bool to_acc = true) {
     const int lane = threadIdx.x & 63;
     uint32_t vals[11];
 #pragma unroll
@@ -573,7 +592,7 @@ __device__ void flush_counters(const Ctx &cx, Counters &cnt, uint32_t weight) {
     vals[10] = cnt.unknown;
 #pragma unroll
     for (int i = 0; i < 11; i++) vals[i] = wsum32(vals[i]);
-    if (lane == 0) {
+    if (lane == 0 && to_acc) {
 #pragma unroll
         for (int i = 0; i < 4; i++) acc_add(&cx.acc[ACC_BASE + i], vals[i], weight);
         acc_add(&cx.acc[ACC_VALID], vals[4], weight);
@@ -656,8 +675,8 @@ __device__ void count_range(const Ctx &cx, const Span &sp, uint64_t t0, DState &
 
 /* Flush a range's counters; lane 0 records its observations in rr. */
 __device__ void range_obs(const Ctx &cx, Counters &cnt, uint32_t weight, const Span &sp, RangeRec *r,
-                          bool write) {
-    flush_counters(cx, cnt, weight);
+                          bool write, bool to_acc = true) {
+    flush_counters(cx, cnt, weight, to_acc);
     const uint32_t unk = wsum32(cnt.unknown);
     const uint32_t eof = wmin32(cnt.eof);
     if ((threadIdx.x & 63) == 0 && weight == 1u) {
@@ -760,7 +779,7 @@ k_count(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uin
     /* the 509-odd blocks flush their bins into FK_SUBTABLES copies of the
        table (fewer same-address atomics at the end of the kernel);
        k_table_stats folds them into the table */
-    Ctx cx{buf, len, lo, table, HM != H_GLOBAL ? lds_bins : nullptr, shortcnt, acc, res, maskk,
+    Ctx cx{buf, len, lo, table, LDS_MODE(HM) ? lds_bins : nullptr, shortcnt, acc, res, maskk,
            1u << (2 * k + 2), k,
            subs ? subs + (size_t)(blockIdx.x % FK_SUBTABLES) * ((size_t)1 << (2 * k)) : nullptr};
     const int lane = threadIdx.x & 63;
@@ -812,7 +831,7 @@ k_count(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uin
         asm volatile("" ::: "memory");
         FK_LOADI(C, 2);
     }
-    if (HM != H_GLOBAL) lds_zero(lds_bins, nw);
+    if (LDS_MODE(HM)) lds_zero(lds_bins, nw);
     if (has) {
         DState st;
         if (c0 == 0 && has_init) {
@@ -872,7 +891,7 @@ k_count(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uin
                 FK_LOADI(C, t + 2);
             }
         }
-        flush_counters(cx, cnt, 1u);
+        flush_counters(cx, cnt, 1u, HM != H_NONE);
         const uint32_t unk = wsum32(cnt.unknown);
         const uint32_t eof = wmin32(cnt.eof);
         if (lane == 0) {
@@ -902,7 +921,7 @@ k_count(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uin
             }
         }
     }
-    if (HM != H_GLOBAL) lds_flush<HM>(cx);
+    if (LDS_MODE(HM)) lds_flush<HM>(cx);
 }
 #undef FK_LOADI
 #undef FK_LOADT
@@ -922,8 +941,8 @@ k_resume(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, ui
     const bool mine = wave < nranges && rr[wave].resume;
     if (!__syncthreads_or(mine)) return;   /* uniform per block */
     const uint32_t nw = lds_words(HM, k);
-    if (HM != H_GLOBAL) lds_zero(lds_bins, nw);
-    Ctx cx{buf, len, lo, table, HM != H_GLOBAL ? lds_bins : nullptr, shortcnt, acc, res, maskk,
+    if (LDS_MODE(HM)) lds_zero(lds_bins, nw);
+    Ctx cx{buf, len, lo, table, LDS_MODE(HM) ? lds_bins : nullptr, shortcnt, acc, res, maskk,
            1u << (2 * k + 2), k};
     if (mine) {
         const ResumeRec q = resume[wave];
@@ -936,7 +955,7 @@ k_resume(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, ui
         count_range<HM>(cx, sp, q.tile, st, f, cnt, 1u);
         r.tf = fk_tf_span(a, st, f);
         r.a_code = a.code; r.a_R = a.R; r.a_hdr = a.hdr;
-        range_obs(cx, cnt, 1u, sp, &r, true);
+        range_obs(cx, cnt, 1u, sp, &r, true, HM != H_NONE);
         if ((threadIdx.x & 63) == 0) {
             /* plus what k_count observed before the resume point */
             r.unknown += q.unknown;
@@ -944,7 +963,7 @@ k_resume(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, ui
             rr[wave] = r;
         }
     }
-    if (HM != H_GLOBAL) lds_flush<HM>(cx);
+    if (LDS_MODE(HM)) lds_flush<HM>(cx);
 }
 
 /*
@@ -964,8 +983,8 @@ k_redo(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint
     const uint64_t n = mode == 1 ? nranges : (uint64_t)res->redo_n;
     if ((uint64_t)blockIdx.x * FK_WAVES_PER_BLOCK >= n) return;   /* uniform per block */
     const uint32_t nw = lds_words(HM, k);
-    if (HM != H_GLOBAL) lds_zero(lds_bins, nw);
-    Ctx cx{buf, len, lo, table, HM != H_GLOBAL ? lds_bins : nullptr, shortcnt, acc, res, maskk,
+    if (LDS_MODE(HM)) lds_zero(lds_bins, nw);
+    Ctx cx{buf, len, lo, table, LDS_MODE(HM) ? lds_bins : nullptr, shortcnt, acc, res, maskk,
            1u << (2 * k + 2), k};
     const uint64_t wave = blockIdx.x * FK_WAVES_PER_BLOCK + wave_in_block();
     const uint64_t nwaves = (uint64_t)gridDim.x * FK_WAVES_PER_BLOCK;
@@ -991,7 +1010,245 @@ k_redo(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint
             if ((threadIdx.x & 63) == 0) { rr[r].eof = q.eof; rr[r].unknown = q.unknown; }
         }
     }
-    if (HM != H_GLOBAL) lds_flush<HM>(cx);
+    if (LDS_MODE(HM)) lds_flush<HM>(cx);
+}
+
+/*
+ * Partitioned counting for 8 <= k <= 12 (the 4^k table does not fit in LDS,
+ * and global atomics top out near 27 G/s on this chip).  The state pass
+ * (k_count / k_resume in H_NONE mode, then k_scan) gives every range its
+ * exact entering state; then:
+ *
+ * k_part: one wave per range, three interleaved tiles in flight as in
+ *   k_count.  Each round, every wave counts one tile: a fast tile hands its
+ *   windows to the block's batch, any other tile is counted by the general
+ *   path with global atomics.  The block counting-sorts the round's windows
+ *   (up to 8 x 2048) by table slice (the top index bits) in LDS, writes the
+ *   sorted batch contiguously to its code region (the low `sh` index bits,
+ *   u16 each) and records each slice's run (start, count) in a slice-major
+ *   index.
+ * k_bucket_count: one block per slice (and group of rows) counts its runs in
+ *   an LDS slice of 2^sh bins and adds the slice into the table.
+ */
+#define PART_BLOCK 512u
+#define PART_MAX_BATCH (FK_WAVES_PER_BLOCK * FK_TILE_BYTES)   /* windows per round */
+#define PART_MAX_SLICES 1024u
+
+struct PartGeo {
+    uint16_t *codes;       /* per block: region_stride entries */
+    uint32_t *idx;         /* [slice][row]: (start << 16) | count */
+    uint32_t *row_base;    /* [row]: entries the block wrote before this row */
+    uint64_t region_stride;
+    uint32_t rounds;       /* rows per block */
+    uint32_t rows;         /* rows in all: grid * rounds */
+    uint32_t nslices;
+    uint32_t sh;           /* slice index = code >> sh; stored code = code & (2^sh - 1) */
+};
+
+/* The block-wide batch of one round: windows of the waves whose tile was
+ * fast (have), counting-sorted by slice.  Every thread of the block calls
+ * this the same number of times (it contains barriers). */
+__device__ __forceinline__ void part_batch(const Ctx &cx, const PartGeo &pg, const Emit &em, bool have,
+                                           uint32_t row, uint32_t &blk_cursor, uint32_t *hist, uint32_t *cur,
+                                           uint32_t *total, uint16_t *ent) {
+    const uint32_t t = threadIdx.x, lane = t & 63;
+    const uint32_t mk = (uint32_t)cx.maskk, sh = pg.sh, lowm = (1u << sh) - 1u;
+    /* 1: slice histogram */
+    if (have) {
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+            const uint32_t C = h ? em.BC : em.AC, S2 = h ? em.B2 : em.A2;
+            const bool skip0 = h ? em.h1 : em.h0;
+#pragma unroll
+            for (int i = 0; i < 16; i++) {
+                const uint32_t v = (i < 15 ? __builtin_amdgcn_alignbit(C, S2, 2u * (15u - (uint32_t)i)) : S2) & mk;
+                if (i > 0 || !skip0) atomicAdd(&hist[v >> sh], 1u);
+            }
+        }
+    }
+    __syncthreads();
+    /* 2: exclusive scan of the slice counts (wave 0), index row */
+    if (t < 64) {
+        const uint32_t per = (pg.nslices + 63) / 64;
+        uint32_t sum = 0;
+        for (uint32_t j = 0; j < per; j++) {
+            const uint32_t b = lane * per + j;
+            if (b < pg.nslices) sum += hist[b];
+        }
+        uint32_t inc = sum;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t v = shup(inc, d);
+            if (lane >= (uint32_t)d) inc += v;
+        }
+        uint32_t run = inc - sum;
+        for (uint32_t j = 0; j < per; j++) {
+            const uint32_t b = lane * per + j;
+            if (b < pg.nslices) {
+                const uint32_t c = hist[b];
+                cur[b] = run;
+                pg.idx[(size_t)b * pg.rows + row] = (run << 16) | c;
+                hist[b] = 0;
+                run += c;
+            }
+        }
+        if (lane == 63) *total = inc;
+        if (lane == 0) pg.row_base[row] = blk_cursor;
+    }
+    __syncthreads();
+    /* 3: place each window at its slot */
+    if (have) {
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+            const uint32_t C = h ? em.BC : em.AC, S2 = h ? em.B2 : em.A2;
+            const bool skip0 = h ? em.h1 : em.h0;
+#pragma unroll
+            for (int i = 0; i < 16; i++) {
+                const uint32_t v = (i < 15 ? __builtin_amdgcn_alignbit(C, S2, 2u * (15u - (uint32_t)i)) : S2) & mk;
+                if (i > 0 || !skip0) {
+                    const uint32_t p = atomicAdd(&cur[v >> sh], 1u);
+                    ent[p] = (uint16_t)(v & lowm);
+                }
+            }
+        }
+    }
+    __syncthreads();
+    /* 4: the sorted batch, contiguous, into the block's code region */
+    const uint32_t n = *total;
+    uint16_t *dst = pg.codes + (size_t)blockIdx.x * pg.region_stride + blk_cursor;
+    for (uint32_t i = t; i < n; i += PART_BLOCK) dst[i] = ent[i];
+    blk_cursor += n;
+}
+
+__global__ void __launch_bounds__(PART_BLOCK, 2)
+k_part(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint32_t *table,
+       uint32_t *shortcnt, unsigned long long *acc, DevRes *res, RangeRec *rr, uint64_t nchunks, uint64_t cpw,
+       const XState *rtrue, PartGeo pg) {
+    __shared__ uint32_t hist[PART_MAX_SLICES], cur[PART_MAX_SLICES], total;
+    __shared__ uint16_t ent[PART_MAX_BATCH];
+    for (uint32_t i = threadIdx.x; i < pg.nslices; i += PART_BLOCK) hist[i] = 0;
+    Ctx cx{buf, len, lo, table, nullptr, shortcnt, acc, res, maskk, 0, k, nullptr};
+    const int lane = threadIdx.x & 63;
+    const uint64_t wave = blockIdx.x * FK_WAVES_PER_BLOCK + wave_in_block();
+    const uint64_t c0 = wave * cpw, c1 = min(c0 + cpw, nchunks);
+    const bool has = c0 < c1;
+    RangeRec hdr_r;
+    hdr_r.c0 = has ? c0 : 0;
+    hdr_r.c1 = has ? c1 : 0;
+    const Span sp = range_span(hdr_r, len);
+    const uint64_t last_tile = sp.nfull ? sp.rend - FK_TILE_BYTES : 0;
+    const bool ld = sp.nfull > 0;
+#define FK_LOADP(dst, t_)                                                            \
+    if (ld) {                                                                        \
+        const uint64_t tb_ = min(sp.rbase + (uint64_t)(t_) * FK_TILE_BYTES, last_tile); \
+        const u32x4 *p_ = reinterpret_cast<const u32x4 *>(cx.buf + tb_) + lane;      \
+        u32x4 v0_ = __builtin_nontemporal_load(p_);                                  \
+        u32x4 v1_ = __builtin_nontemporal_load(p_ + 64);                             \
+        dst[0] = v0_.x; dst[1] = v0_.y; dst[2] = v0_.z; dst[3] = v0_.w;               \
+        dst[4] = v1_.x; dst[5] = v1_.y; dst[6] = v1_.z; dst[7] = v1_.w;               \
+    }
+    uint32_t A[8] = {}, B[8] = {}, C[8] = {};
+    FK_LOADP(A, 0);
+    asm volatile("" ::: "memory");
+    FK_LOADP(B, 1);
+    asm volatile("" ::: "memory");
+    FK_LOADP(C, 2);
+    DState st{0, 0, 0};
+    if (has) {
+        const XState x = rtrue[wave];
+        st = DState{x.code, (uint32_t)x.R, x.hdr};
+    }
+    Facts f{0, 0, 0, 0, 0, 0};
+    Counters cnt{0, 0, 0, 0, 0, FK_NO_EOF};
+    uint64_t t = 0;
+    bool done = !has || sp.ntiles == 0;
+    uint32_t blk_cursor = 0, round = 0;
+    __syncthreads();
+#define FK_ROUND(X)                                                                  \
+    {                                                                                \
+        Emit em{0, 0, 0, 0, false, false, false};                                    \
+        bool have = false;                                                           \
+        if (!done) {                                                                 \
+            if (t < sp.nfull && st.hdr == 0 && tile_fast<true, H_EMIT, true>(cx, X, st, f, cnt, 1u, &em)) { \
+                have = em.deep;                                                      \
+            } else {                                                                 \
+                uint32_t v_[8];                                                      \
+                const int64_t toff_ = (int64_t)(sp.rbase + t * FK_TILE_BYTES);       \
+                const int nb_ = load_lane<FK_LANE_BYTES>(cx, toff_ + lane * (int64_t)FK_LANE_BYTES, v_); \
+                tile_general<true, H_EMIT>(cx, v_, nb_, (uint32_t)(t * FK_TILE_BYTES), st, f, cnt, 1u); \
+            }                                                                        \
+            t++;                                                                     \
+            done = t >= sp.ntiles;                                                   \
+        }                                                                            \
+        consume(X);                                                                  \
+        FK_LOADP(X, t + 2);                                                          \
+        part_batch(cx, pg, em, have, blockIdx.x * pg.rounds + round, blk_cursor, hist, cur, &total, ent); \
+        round++;                                                                     \
+        if (!__syncthreads_or(!done) || round >= pg.rounds) break;                  \
+    }
+    for (;;) {
+        FK_ROUND(A);
+        FK_ROUND(B);
+        FK_ROUND(C);
+    }
+#undef FK_ROUND
+#undef FK_LOADP
+    /* rows the block did not reach are empty */
+    for (uint32_t r = round; r < pg.rounds; r++) {
+        const uint32_t row = blockIdx.x * pg.rounds + r;
+        for (uint32_t b = threadIdx.x; b < pg.nslices; b += PART_BLOCK) pg.idx[(size_t)b * pg.rows + row] = 0;
+        if (threadIdx.x == 0) pg.row_base[row] = blk_cursor;
+    }
+    /* exact observations of the range (its entering state was exact) */
+    if (has) {
+        RangeRec r = rr[wave];
+        range_obs(cx, cnt, 1u, sp, &r, true);
+        if (lane == 0) { rr[wave].eof = r.eof; rr[wave].unknown = r.unknown; }
+    } else {
+        flush_counters(cx, cnt, 1u);
+    }
+}
+
+__global__ void __launch_bounds__(1024)
+k_bucket_count(PartGeo pg, uint32_t groups, uint32_t *table) {
+    extern __shared__ uint32_t slice[];
+    const uint32_t nb = 1u << pg.sh;
+    const uint32_t b = blockIdx.x % pg.nslices, g = blockIdx.x / pg.nslices;
+    for (uint32_t i = threadIdx.x; i < nb; i += blockDim.x) slice[i] = 0;
+    __syncthreads();
+    const uint32_t *ix = pg.idx + (size_t)b * pg.rows;
+    for (uint32_t r = g * blockDim.x + threadIdx.x; r < pg.rows; r += groups * blockDim.x) {
+        const uint32_t e = ix[r];
+        const uint32_t cnt = e & 0xFFFFu;
+        if (!cnt) continue;
+        const uint32_t blk = r / pg.rounds;
+        /* the run [s0, s1) of u16 codes, read as aligned 8-code groups, four
+           groups in flight */
+        const uint64_t s0 = (uint64_t)blk * pg.region_stride + pg.row_base[r] + (e >> 16), s1 = s0 + cnt;
+        const uint4 *g4 = reinterpret_cast<const uint4 *>(pg.codes);
+        for (uint64_t q = s0 >> 3; q < (s1 + 7) >> 3; q += 4) {
+            uint4 v[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) v[u] = q + u < (s1 + 7) >> 3 ? g4[q + u] : make_uint4(0, 0, 0, 0);
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const uint32_t w4[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+                for (int h = 0; h < 8; h++) {
+                    const uint64_t at = (q + u) * 8 + h;
+                    if (at >= s0 && at < s1) atomicAdd(&slice[(w4[h >> 1] >> (16 * (h & 1))) & 0xFFFFu], 1u);
+                }
+            }
+        }
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < nb; i += blockDim.x) {
+        const uint32_t v = slice[i];
+        if (!v) continue;
+        uint32_t *dst = &table[fk_sigma(((uint64_t)b << pg.sh) | i)];
+        if (groups == 1) *dst += v;   /* this block owns the slice */
+        else atomicAdd(dst, v);
+    }
 }
 
 /*
@@ -1134,9 +1391,10 @@ __device__ __forceinline__ unsigned long long wsum64(unsigned long long v) {
     for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
     return v;
 }
-__global__ void k_table_stats(uint32_t *table, uint64_t n, int k, DevRes *res,
-                              const unsigned long long *acc, DevRes *host_res, uint32_t *done, uint32_t seq,
-                              uint32_t *subs, int nsub) {
+__global__ void __launch_bounds__(256)
+k_table_stats(uint32_t *table, uint64_t n, int k, DevRes *res,
+              const unsigned long long *acc, DevRes *host_res, uint32_t *done, uint32_t seq,
+              uint32_t *subs, int nsub, unsigned long long *part) {
     unsigned long long *out = res->tstat;
     if (blockIdx.x == 0 && threadIdx.x < ACC_N) res->acc[threadIdx.x] = acc[threadIdx.x];
     unsigned long long dist = 0, sum = 0, last[4] = {0, 0, 0, 0}, first[4] = {0, 0, 0, 0};
@@ -1167,23 +1425,25 @@ __global__ void k_table_stats(uint32_t *table, uint64_t n, int k, DevRes *res,
             first[2] += fd == 2 ? s4 : 0; first[3] += fd == 3 ? s4 : 0;
         }
     }
-    dist = wsum64(dist);
-    sum = wsum64(sum);
+    /* block partials (no same-address atomics across hundreds of blocks:
+       the last block adds them up) */
+    __shared__ unsigned long long wp[4][10];
+    unsigned long long v10[10] = {dist, sum, last[0], last[1], last[2], last[3], first[0], first[1], first[2], first[3]};
 #pragma unroll
-    for (int b = 0; b < 4; b++) { last[b] = wsum64(last[b]); first[b] = wsum64(first[b]); }
-    if ((threadIdx.x & 63) == 0) {
-        if (dist) atomicAdd(&out[0], dist);
-        if (sum) atomicAdd(&out[1], sum);
+    for (int q = 0; q < 10; q++) v10[q] = wsum64(v10[q]);
+    const uint32_t wv = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0)
 #pragma unroll
-        for (int b = 0; b < 4; b++) {
-            if (last[b]) atomicAdd(&out[2 + b], last[b]);
-            if (first[b]) atomicAdd(&out[6 + b], first[b]);
-        }
+        for (int q = 0; q < 10; q++) wp[wv][q] = v10[q];
+    __syncthreads();
+    if (threadIdx.x < 10) {
+        unsigned long long s = 0;
+        for (uint32_t w = 0; w < blockDim.x / 64; w++) s += wp[w][threadIdx.x];
+        part[(size_t)blockIdx.x * 10 + threadIdx.x] = s;
     }
-    if (!host_res) return;
-    /* the last block to finish publishes the whole result block to pinned
-       host memory, sequence number last: the host spins on it instead of a
-       copy plus a stream synchronisation */
+    /* the last block to finish sums the partials, then publishes the whole
+       result block to pinned host memory, sequence number last: the host
+       spins on it instead of a copy plus a stream synchronisation */
     __shared__ uint32_t is_last;
     __threadfence();
     __syncthreads();
@@ -1191,6 +1451,26 @@ __global__ void k_table_stats(uint32_t *table, uint64_t n, int k, DevRes *res,
     __syncthreads();
     if (!is_last) return;
     __threadfence();
+    {
+        /* every thread sums a strided share of the blocks, then the block */
+        unsigned long long acc10[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+        for (uint32_t b = threadIdx.x; b < gridDim.x; b += blockDim.x)
+#pragma unroll
+            for (int q = 0; q < 10; q++) acc10[q] += part[(size_t)b * 10 + q];
+#pragma unroll
+        for (int q = 0; q < 10; q++) acc10[q] = wsum64(acc10[q]);
+        __syncthreads();
+        if ((threadIdx.x & 63) == 0)
+#pragma unroll
+            for (int q = 0; q < 10; q++) wp[wv][q] = acc10[q];
+        __syncthreads();
+        if (threadIdx.x < 10) {
+            unsigned long long s = 0;
+            for (uint32_t w = 0; w < blockDim.x / 64; w++) s += wp[w][threadIdx.x];
+            out[threadIdx.x] = s;
+        }
+        __syncthreads();
+    }
     const uint32_t *src = reinterpret_cast<const uint32_t *>(res);
     uint32_t *dst = reinterpret_cast<uint32_t *>(host_res);
     for (uint32_t i = threadIdx.x; i < offsetof(DevRes, seq) / 4; i += blockDim.x) dst[i] = src[i];
@@ -1393,6 +1673,10 @@ struct fk_engine {
     fk_opts opts{};
     uint64_t nbins = 0, nshort = 0, maskk = 0;
     int cus = 256;
+    bool part = false;                        /* 8 <= k <= 12: partitioned counting (k_part) */
+    uint16_t *d_codes = nullptr;              /* k_part: block code regions */
+    uint32_t *d_pidx = nullptr, *d_prow = nullptr;   /* k_part: slice-major run index, row bases */
+    uint64_t codes_cap = 0, pidx_cap = 0, prow_cap = 0;
     uint32_t general_tiles = FK_COUNT_GENERAL_TILES;   /* per range in k_count (env FK_GENERAL_TILES) */
     /* device state */
     uint32_t *d_table = nullptr, *d_short = nullptr;
@@ -1416,6 +1700,7 @@ struct fk_engine {
     bool zero_pending = false;                /* reset() not yet issued to the device */
     DevRes *h_res = nullptr, *h_res_dev = nullptr;   /* pinned, mapped result block */
     uint32_t *d_done = nullptr;               /* k_table_stats finished-block count */
+    unsigned long long *d_tpart = nullptr;    /* k_table_stats per-block partial sums */
     uint32_t res_seq = 0;
     /* host bookkeeping */
     XState state{0, 0, 0, 0};
@@ -1511,7 +1796,8 @@ extern "C" void fk_engine_destroy(fk_engine *e) {
     if (!e) return;
     hipSetDevice(e->dev);
     if (e->stream) hipStreamSynchronize(e->stream);
-    hipFree(e->d_table); hipFree(e->d_short); hipFree(e->d_sub); hipFree(e->d_acc); hipFree(e->d_res); hipFree(e->d_tmp);
+    hipFree(e->d_table); hipFree(e->d_short); hipFree(e->d_sub);
+    hipFree(e->d_codes); hipFree(e->d_pidx); hipFree(e->d_prow); hipFree(e->d_acc); hipFree(e->d_res); hipFree(e->d_tmp);
     hipFree(e->d_state); hipFree(e->d_rr); hipFree(e->d_rtrue);
     hipFree(e->d_redo); hipFree(e->d_tf); hipFree(e->d_stage); hipFree(e->d_resume);
     hipFree(e->d_aggs); hipFree(e->d_flags);
@@ -1519,6 +1805,7 @@ extern "C" void fk_engine_destroy(fk_engine *e) {
     for (int i = 0; i < 3; i++) if (e->ev[i]) hipEventDestroy(e->ev[i]);
     if (e->h_res) hipHostFree(e->h_res);
     hipFree(e->d_done);
+    hipFree(e->d_tpart);
     if (e->own_stream && e->stream) hipStreamDestroy(e->stream);
     delete e;
 }
@@ -1543,6 +1830,11 @@ extern "C" int fk_engine_create(int k, const fk_opts *opts, fk_engine **out) {
         e->cus = prop.multiProcessorCount;
     if (const char *gt = getenv("FK_GENERAL_TILES")) e->general_tiles = (uint32_t)strtoul(gt, nullptr, 10);
     e->nbins = 1ull << (2 * k);
+#if FK_EXP == 6   /* ablation: the partitioned path for k >= 6 */
+    e->part = k >= 6 && k <= 12;
+#else
+    e->part = k >= 8 && k <= 12;
+#endif
     e->maskk = e->nbins - 1;
     e->nshort = k > 1 ? ((1ull << (2 * k)) - 4) / 3 : 0;
     if (e->opts.stream) {
@@ -1583,6 +1875,7 @@ extern "C" int fk_engine_create(int k, const fk_opts *opts, fk_engine **out) {
     if (hipHostMalloc((void **)&e->h_res, sizeof(DevRes), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
         hipHostGetDevicePointer((void **)&e->h_res_dev, e->h_res, 0) != hipSuccess ||
         hipMalloc((void **)&e->d_done, sizeof(uint32_t)) != hipSuccess ||
+        hipMalloc((void **)&e->d_tpart, (size_t)e->cus * 4 * 10 * sizeof(unsigned long long)) != hipSuccess ||
         hipMemsetAsync(e->d_done, 0, sizeof(uint32_t), e->stream) != hipSuccess) {
         fk_engine_destroy(e);
         return FK_E_OOM;
@@ -1645,11 +1938,16 @@ static Geo geometry(const fk_engine *e, uint64_t len) {
     case H_LDS: { constexpr int HM = H_LDS; __VA_ARGS__; } break;              \
     default: { constexpr int HM = H_GLOBAL; __VA_ARGS__; } break;              \
     }
+/* the counting passes of k_count / k_resume: state only (H_NONE) when the
+   partitioned path (k_part) does the counting */
+#define FK_DISPATCH_COUNT(e, ...)                                               \
+    if ((e)->part) { constexpr int HM = H_NONE; __VA_ARGS__; }                  \
+    else FK_DISPATCH(hist_mode(e), __VA_ARGS__)
 
 static int launch_count(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t lo, const Geo &g,
                         int has_init) {
     size_t sh = lds_bytes(e);
-    FK_DISPATCH(hist_mode(e),
+    FK_DISPATCH_COUNT(e,
                 hipExtLaunchKernelGGL((k_count<HM>), dim3(g.grid), dim3(FK_BLOCK), sh, e->stream, e->ev[0], e->ev[1],
                                       0, buf, len, lo, e->k,
                                    e->maskk, e->d_table, e->d_short, e->d_acc, e->d_res, e->d_rr,
@@ -1661,7 +1959,7 @@ static int launch_count(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t 
 
 static int launch_resume(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t lo, const Geo &g) {
     size_t sh = lds_bytes(e);
-    FK_DISPATCH(hist_mode(e),
+    FK_DISPATCH_COUNT(e,
                 hipLaunchKernelGGL((k_resume<HM>), dim3(g.grid), dim3(FK_BLOCK), sh, e->stream, buf, len, lo, e->k,
                                    e->maskk, e->d_table, e->d_short, e->d_acc, e->d_res, e->d_rr, g.nranges,
                                    e->d_resume));
@@ -1701,7 +1999,7 @@ static int launch_table_stats(fk_engine *e, bool zero_first, hipEvent_t stop = n
     if (++e->res_seq == 0) e->res_seq = 1;
     hipExtLaunchKernelGGL(k_table_stats, dim3(gd), dim3(256), 0, e->stream, nullptr, stop, 0, e->d_table,
                           e->nbins, e->k, e->d_res, e->d_acc, e->h_res_dev, e->d_done, e->res_seq, e->d_sub,
-                          e->d_sub ? FK_SUBTABLES : 0);
+                          e->d_sub ? FK_SUBTABLES : 0, e->d_tpart);
     HIPCHK(hipGetLastError());
     return FK_OK;
 }
@@ -1727,11 +2025,53 @@ static int wait_results(fk_engine *e) {
     return FK_OK;
 }
 
-/* scan + redo + table stats, then one device->host copy of the results */
+/* k_part + k_bucket_count over a resolved segment (exact range states in
+   d_rtrue): the counting of the partitioned path */
+static int launch_part(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t lo, const Geo &g) {
+    PartGeo pg;
+    const int k = e->k;
+    pg.sh = std::min(14, 2 * k - 6);                       /* >= 64 slices, <= 2^14 bins each */
+    pg.nslices = 1u << (2 * k - pg.sh);
+    pg.region_stride = (uint64_t)FK_WAVES_PER_BLOCK * g.cpw * FK_CHUNK_BYTES;   /* >= windows per block */
+    pg.rounds = (uint32_t)(g.cpw * FK_CHUNK_TILES + 2);
+    pg.rows = g.grid * pg.rounds;
+    const uint64_t ncodes = (uint64_t)g.grid * pg.region_stride, nidx = (uint64_t)pg.nslices * pg.rows;
+    if (ncodes > e->codes_cap) {
+        hipFree(e->d_codes);
+        e->d_codes = nullptr;
+        if (hipMalloc((void **)&e->d_codes, ncodes * sizeof(uint16_t)) != hipSuccess) return FK_E_OOM;
+        e->codes_cap = ncodes;
+    }
+    if (nidx > e->pidx_cap) {
+        hipFree(e->d_pidx);
+        e->d_pidx = nullptr;
+        if (hipMalloc((void **)&e->d_pidx, nidx * sizeof(uint32_t)) != hipSuccess) return FK_E_OOM;
+        e->pidx_cap = nidx;
+    }
+    if (pg.rows > e->prow_cap) {
+        hipFree(e->d_prow);
+        e->d_prow = nullptr;
+        if (hipMalloc((void **)&e->d_prow, (size_t)pg.rows * sizeof(uint32_t)) != hipSuccess) return FK_E_OOM;
+        e->prow_cap = pg.rows;
+    }
+    pg.codes = e->d_codes;
+    pg.idx = e->d_pidx;
+    pg.row_base = e->d_prow;
+    hipLaunchKernelGGL(k_part, dim3(g.grid), dim3(PART_BLOCK), 0, e->stream, buf, len, lo, e->k, e->maskk,
+                       e->d_table, e->d_short, e->d_acc, e->d_res, e->d_rr, g.nchunks, g.cpw, e->d_rtrue, pg);
+    HIPCHK(hipGetLastError());
+    const uint32_t groups = std::max<uint32_t>(1, 2 * (uint32_t)e->cus / pg.nslices);
+    hipLaunchKernelGGL(k_bucket_count, dim3(pg.nslices * groups), dim3(1024), (size_t)sizeof(uint32_t) << pg.sh,
+                       e->stream, pg, groups, e->d_table);
+    HIPCHK(hipGetLastError());
+    return FK_OK;
+}
+
+/* scan + redo (or the partitioned count) + table stats, then the results */
 static int resolve_and_fetch(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t lo, const Geo &g) {
     int rc = launch_scan(e, g, 0);
     if (rc) return rc;
-    rc = launch_redo(e, buf, len, lo, g, 0);
+    rc = e->part ? launch_part(e, buf, len, lo, g) : launch_redo(e, buf, len, lo, g, 0);
     if (rc) return rc;
     rc = launch_table_stats(e, false, e->ev[2]);
     if (rc) return rc;
