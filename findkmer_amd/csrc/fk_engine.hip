@@ -1048,9 +1048,9 @@ struct PartGeo {
 /* The block-wide batch of one round: windows of the waves whose tile was
  * fast (have), counting-sorted by slice.  Every thread of the block calls
  * this the same number of times (it contains barriers). */
-__device__ __forceinline__ void part_batch(const Ctx &cx, const PartGeo &pg, const Emit &em, bool have,
-                                           uint32_t row, uint32_t &blk_cursor, uint32_t *hist, uint32_t *cur,
-                                           uint32_t *total, uint16_t *ent) {
+__device__ __forceinline__ bool part_batch(const Ctx &cx, const PartGeo &pg, const Emit &em, bool have,
+                                           bool more, uint32_t row, uint32_t &blk_cursor, uint32_t *hist,
+                                           uint32_t *cur, uint32_t *total, uint16_t *ent) {
     const uint32_t t = threadIdx.x, lane = t & 63;
     const uint32_t mk = (uint32_t)cx.maskk, sh = pg.sh, lowm = (1u << sh) - 1u;
     /* 1: slice histogram */
@@ -1066,7 +1066,8 @@ __device__ __forceinline__ void part_batch(const Ctx &cx, const PartGeo &pg, con
             }
         }
     }
-    __syncthreads();
+    /* (the barrier also tells whether any wave has tiles left) */
+    const bool any_more = __syncthreads_or(more);
     /* 2: exclusive scan of the slice counts (wave 0), index row */
     if (t < 64) {
         const uint32_t per = (pg.nslices + 63) / 64;
@@ -1118,6 +1119,7 @@ __device__ __forceinline__ void part_batch(const Ctx &cx, const PartGeo &pg, con
     uint16_t *dst = pg.codes + (size_t)blockIdx.x * pg.region_stride + blk_cursor;
     for (uint32_t i = t; i < n; i += PART_BLOCK) dst[i] = ent[i];
     blk_cursor += n;
+    return any_more;
 }
 
 __global__ void __launch_bounds__(PART_BLOCK, 2)
@@ -1182,9 +1184,10 @@ k_part(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint
         }                                                                            \
         consume(X);                                                                  \
         FK_LOADP(X, t + 2);                                                          \
-        part_batch(cx, pg, em, have, blockIdx.x * pg.rounds + round, blk_cursor, hist, cur, &total, ent); \
+        const bool more_ = part_batch(cx, pg, em, have, !done, blockIdx.x * pg.rounds + round, blk_cursor, \
+                                      hist, cur, &total, ent);                       \
         round++;                                                                     \
-        if (!__syncthreads_or(!done) || round >= pg.rounds) break;                  \
+        if (!more_ || round >= pg.rounds) break;                                     \
     }
     for (;;) {
         FK_ROUND(A);
@@ -1217,25 +1220,27 @@ k_bucket_count(PartGeo pg, uint32_t groups, uint32_t *table) {
     for (uint32_t i = threadIdx.x; i < nb; i += blockDim.x) slice[i] = 0;
     __syncthreads();
     const uint32_t *ix = pg.idx + (size_t)b * pg.rows;
-    for (uint32_t r = g * blockDim.x + threadIdx.x; r < pg.rows; r += groups * blockDim.x) {
+    const uint4 *g4 = reinterpret_cast<const uint4 *>(pg.codes);
+    /* four lanes share a run and read it as contiguous 64-byte pieces (one
+       request per quad instead of one per lane) */
+    const uint32_t sub = threadIdx.x & 3u;
+    const uint32_t quads = blockDim.x / 4, step = groups * quads;
+    for (uint32_t r = g * quads + threadIdx.x / 4; r < pg.rows; r += step) {
         const uint32_t e = ix[r];
         const uint32_t cnt = e & 0xFFFFu;
         if (!cnt) continue;
-        const uint32_t blk = r / pg.rounds;
-        /* the run [s0, s1) of u16 codes, read as aligned 8-code groups, four
-           groups in flight */
-        const uint64_t s0 = (uint64_t)blk * pg.region_stride + pg.row_base[r] + (e >> 16), s1 = s0 + cnt;
-        const uint4 *g4 = reinterpret_cast<const uint4 *>(pg.codes);
-        for (uint64_t q = s0 >> 3; q < (s1 + 7) >> 3; q += 4) {
+        const uint64_t s0 = (uint64_t)(r / pg.rounds) * pg.region_stride + pg.row_base[r] + (e >> 16), s1 = s0 + cnt;
+        const uint64_t q1 = (s1 + 7) >> 3;
+        for (uint64_t q = (s0 >> 3) + sub; q < q1; q += 16) {
             uint4 v[4];
 #pragma unroll
-            for (int u = 0; u < 4; u++) v[u] = q + u < (s1 + 7) >> 3 ? g4[q + u] : make_uint4(0, 0, 0, 0);
+            for (int u = 0; u < 4; u++) v[u] = q + 4 * u < q1 ? g4[q + 4 * u] : make_uint4(0, 0, 0, 0);
 #pragma unroll
             for (int u = 0; u < 4; u++) {
                 const uint32_t w4[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
 #pragma unroll
                 for (int h = 0; h < 8; h++) {
-                    const uint64_t at = (q + u) * 8 + h;
+                    const uint64_t at = (q + 4 * u) * 8 + h;
                     if (at >= s0 && at < s1) atomicAdd(&slice[(w4[h >> 1] >> (16 * (h & 1))) & 0xFFFFu], 1u);
                 }
             }
@@ -1870,6 +1875,8 @@ extern "C" int fk_engine_create(int k, const fk_opts *opts, fk_engine **out) {
         hipFuncSetAttribute((const void *)k_redo<H_PAIRS>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh);
         hipFuncSetAttribute((const void *)k_resume<H_PAIRS>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh);
     }
+    if (e->part)   /* k_bucket_count: one 2^15-bin slice (128 KiB) in LDS */
+        hipFuncSetAttribute((const void *)k_bucket_count, hipFuncAttributeMaxDynamicSharedMemorySize, 4 << 15);
     for (int i = 0; i < 3; i++)
         if (hipEventCreate(&e->ev[i]) != hipSuccess) { fk_engine_destroy(e); return FK_E_HIP; }
     if (hipHostMalloc((void **)&e->h_res, sizeof(DevRes), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
@@ -2030,7 +2037,7 @@ static int wait_results(fk_engine *e) {
 static int launch_part(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t lo, const Geo &g) {
     PartGeo pg;
     const int k = e->k;
-    pg.sh = std::min(14, 2 * k - 6);                       /* >= 64 slices, <= 2^14 bins each */
+    pg.sh = std::min(15, 2 * k - 6);                       /* >= 64 slices, <= 2^15 bins (128 KiB) each */
     pg.nslices = 1u << (2 * k - pg.sh);
     pg.region_stride = (uint64_t)FK_WAVES_PER_BLOCK * g.cpw * FK_CHUNK_BYTES;   /* >= windows per block */
     pg.rounds = (uint32_t)(g.cpw * FK_CHUNK_TILES + 2);
@@ -2060,7 +2067,7 @@ static int launch_part(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t l
     hipLaunchKernelGGL(k_part, dim3(g.grid), dim3(PART_BLOCK), 0, e->stream, buf, len, lo, e->k, e->maskk,
                        e->d_table, e->d_short, e->d_acc, e->d_res, e->d_rr, g.nchunks, g.cpw, e->d_rtrue, pg);
     HIPCHK(hipGetLastError());
-    const uint32_t groups = std::max<uint32_t>(1, 2 * (uint32_t)e->cus / pg.nslices);
+    const uint32_t groups = std::max<uint32_t>(1, (uint32_t)e->cus / pg.nslices);
     hipLaunchKernelGGL(k_bucket_count, dim3(pg.nslices * groups), dim3(1024), (size_t)sizeof(uint32_t) << pg.sh,
                        e->stream, pg, groups, e->d_table);
     HIPCHK(hipGetLastError());

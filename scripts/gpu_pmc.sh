@@ -9,11 +9,11 @@ timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_IN
 timeout -k 10 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VMEM_RD SQ_INSTS_SALU SQ_INSTS_SMEM GRBM_GUI_ACTIVE --output-format csv -d $OUT/p2 -o run -- python3 $B > $OUT/p2.log 2>&1 || { tail -5 $OUT/p2.log; exit 1; }
 timeout -k 10 300 rocprofv3 --pmc SQ_INSTS_VMEM_WR SQ_INSTS_FLAT SQ_WAIT_INST_LDS SQ_INST_CYCLES_VMEM_RD SQ_INSTS_BRANCH --output-format csv -d $OUT/p3 -o run -- python3 $B > $OUT/p3.log 2>&1 || { tail -5 $OUT/p3.log; exit 1; }
 python3 - <<'PY'
-import csv, collections, glob
+import csv, collections, glob, os
 for f in sorted(glob.glob('gpurun_out/pmc/p*/run_counter_collection.csv')):
     agg=collections.defaultdict(list)
     for r in csv.DictReader(open(f)):
-        if 'k_count' in r['Kernel_Name']:
+        if os.environ.get('KERNEL', 'k_count') in r['Kernel_Name']:
             agg[r['Counter_Name']].append(float(r['Counter_Value']))
     for k,v in sorted(agg.items()):
         print(k, '%.4g' % (sum(v)/len(v)))
