@@ -1031,7 +1031,8 @@ k_redo(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint
  *   an LDS slice of 2^sh bins and adds the slice into the table.
  */
 #define PART_BLOCK 512u
-#define PART_MAX_BATCH (FK_WAVES_PER_BLOCK * FK_TILE_BYTES)   /* windows per round */
+#define PART_TILES_PER_BATCH 2u                                /* tiles per wave per batch */
+#define PART_MAX_BATCH (PART_TILES_PER_BATCH * FK_WAVES_PER_BLOCK * FK_TILE_BYTES)   /* windows per batch */
 #define PART_MAX_SLICES 1024u
 
 struct PartGeo {
@@ -1048,21 +1049,26 @@ struct PartGeo {
 /* The block-wide batch of one round: windows of the waves whose tile was
  * fast (have), counting-sorted by slice.  Every thread of the block calls
  * this the same number of times (it contains barriers). */
-__device__ __forceinline__ bool part_batch(const Ctx &cx, const PartGeo &pg, const Emit &em, bool have,
+__device__ __forceinline__ bool part_batch(const Ctx &cx, const PartGeo &pg, const Emit &e0, bool have0,
+                                           const Emit &e1, bool have1,
                                            bool more, uint32_t row, uint32_t &blk_cursor, uint32_t *hist,
                                            uint32_t *cur, uint32_t *total, uint16_t *ent) {
     const uint32_t t = threadIdx.x, lane = t & 63;
     const uint32_t mk = (uint32_t)cx.maskk, sh = pg.sh, lowm = (1u << sh) - 1u;
     /* 1: slice histogram */
-    if (have) {
 #pragma unroll
-        for (int h = 0; h < 2; h++) {
-            const uint32_t C = h ? em.BC : em.AC, S2 = h ? em.B2 : em.A2;
-            const bool skip0 = h ? em.h1 : em.h0;
+    for (int tt = 0; tt < 2; tt++) {
+        const Emit &em = tt ? e1 : e0;
+        if (tt ? have1 : have0) {
 #pragma unroll
-            for (int i = 0; i < 16; i++) {
-                const uint32_t v = (i < 15 ? __builtin_amdgcn_alignbit(C, S2, 2u * (15u - (uint32_t)i)) : S2) & mk;
-                if (i > 0 || !skip0) atomicAdd(&hist[v >> sh], 1u);
+            for (int h = 0; h < 2; h++) {
+                const uint32_t C = h ? em.BC : em.AC, S2 = h ? em.B2 : em.A2;
+                const bool skip0 = h ? em.h1 : em.h0;
+#pragma unroll
+                for (int i = 0; i < 16; i++) {
+                    const uint32_t v = (i < 15 ? __builtin_amdgcn_alignbit(C, S2, 2u * (15u - (uint32_t)i)) : S2) & mk;
+                    if (i > 0 || !skip0) atomicAdd(&hist[v >> sh], 1u);
+                }
             }
         }
     }
@@ -1098,17 +1104,21 @@ __device__ __forceinline__ bool part_batch(const Ctx &cx, const PartGeo &pg, con
     }
     __syncthreads();
     /* 3: place each window at its slot */
-    if (have) {
 #pragma unroll
-        for (int h = 0; h < 2; h++) {
-            const uint32_t C = h ? em.BC : em.AC, S2 = h ? em.B2 : em.A2;
-            const bool skip0 = h ? em.h1 : em.h0;
+    for (int tt = 0; tt < 2; tt++) {
+        const Emit &em = tt ? e1 : e0;
+        if (tt ? have1 : have0) {
 #pragma unroll
-            for (int i = 0; i < 16; i++) {
-                const uint32_t v = (i < 15 ? __builtin_amdgcn_alignbit(C, S2, 2u * (15u - (uint32_t)i)) : S2) & mk;
-                if (i > 0 || !skip0) {
-                    const uint32_t p = atomicAdd(&cur[v >> sh], 1u);
-                    ent[p] = (uint16_t)(v & lowm);
+            for (int h = 0; h < 2; h++) {
+                const uint32_t C = h ? em.BC : em.AC, S2 = h ? em.B2 : em.A2;
+                const bool skip0 = h ? em.h1 : em.h0;
+#pragma unroll
+                for (int i = 0; i < 16; i++) {
+                    const uint32_t v = (i < 15 ? __builtin_amdgcn_alignbit(C, S2, 2u * (15u - (uint32_t)i)) : S2) & mk;
+                    if (i > 0 || !skip0) {
+                        const uint32_t p = atomicAdd(&cur[v >> sh], 1u);
+                        ent[p] = (uint16_t)(v & lowm);
+                    }
                 }
             }
         }
@@ -1165,6 +1175,8 @@ k_part(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint
     uint64_t t = 0;
     bool done = !has || sp.ntiles == 0;
     uint32_t blk_cursor = 0, round = 0;
+    Emit stash{0, 0, 0, 0, false, false, false};
+    bool have_stash = false;
     __syncthreads();
 #define FK_ROUND(X)                                                                  \
     {                                                                                \
@@ -1184,10 +1196,16 @@ k_part(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint
         }                                                                            \
         consume(X);                                                                  \
         FK_LOADP(X, t + 2);                                                          \
-        const bool more_ = part_batch(cx, pg, em, have, !done, blockIdx.x * pg.rounds + round, blk_cursor, \
-                                      hist, cur, &total, ent);                       \
+        if (!(round & 1)) {                                                          \
+            stash = em;                                                              \
+            have_stash = have;                                                       \
+        } else {                                                                     \
+            const bool more_ = part_batch(cx, pg, stash, have_stash, em, have, !done, \
+                                          blockIdx.x * pg.rounds + (round >> 1), blk_cursor, hist, cur, \
+                                          &total, ent);                              \
+            if (!more_ || (round >> 1) + 1 >= pg.rounds) { round++; break; }         \
+        }                                                                            \
         round++;                                                                     \
-        if (!more_ || round >= pg.rounds) break;                                     \
     }
     for (;;) {
         FK_ROUND(A);
@@ -1197,7 +1215,7 @@ k_part(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint
 #undef FK_ROUND
 #undef FK_LOADP
     /* rows the block did not reach are empty */
-    for (uint32_t r = round; r < pg.rounds; r++) {
+    for (uint32_t r = (round + 1) >> 1; r < pg.rounds; r++) {
         const uint32_t row = blockIdx.x * pg.rounds + r;
         for (uint32_t b = threadIdx.x; b < pg.nslices; b += PART_BLOCK) pg.idx[(size_t)b * pg.rows + row] = 0;
         if (threadIdx.x == 0) pg.row_base[row] = blk_cursor;
@@ -2040,7 +2058,7 @@ static int launch_part(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t l
     pg.sh = std::min(15, 2 * k - 6);                       /* >= 64 slices, <= 2^15 bins (128 KiB) each */
     pg.nslices = 1u << (2 * k - pg.sh);
     pg.region_stride = (uint64_t)FK_WAVES_PER_BLOCK * g.cpw * FK_CHUNK_BYTES;   /* >= windows per block */
-    pg.rounds = (uint32_t)(g.cpw * FK_CHUNK_TILES + 2);
+    pg.rounds = (uint32_t)((g.cpw * FK_CHUNK_TILES + 2) / PART_TILES_PER_BATCH + 2);   /* rows (batches) per block */
     pg.rows = g.grid * pg.rounds;
     const uint64_t ncodes = (uint64_t)g.grid * pg.region_stride, nidx = (uint64_t)pg.nslices * pg.rows;
     if (ncodes > e->codes_cap) {
