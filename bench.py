@@ -213,7 +213,8 @@ def main():
         "roofline": {
             "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-            "kernel": "k_count", "kernel_ms": kern_ms, "algorithmic_bytes": algo_bytes,
+            "kernel": "k_part" if 8 <= k <= 12 else "k_count", "kernel_ms": kern_ms,
+            "algorithmic_bytes": algo_bytes,
         },
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

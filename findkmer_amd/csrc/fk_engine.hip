@@ -1135,9 +1135,16 @@ __device__ __forceinline__ bool part_batch(const Ctx &cx, const PartGeo &pg, con
 __global__ void __launch_bounds__(PART_BLOCK, 2)
 k_part(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint32_t *table,
        uint32_t *shortcnt, unsigned long long *acc, DevRes *res, RangeRec *rr, uint64_t nchunks, uint64_t cpw,
-       const XState *rtrue, PartGeo pg) {
+       const XState *d_init, int has_init, PartGeo pg) {
     __shared__ uint32_t hist[PART_MAX_SLICES], cur[PART_MAX_SLICES], total;
     __shared__ uint16_t ent[PART_MAX_BATCH];
+    /* open the feed's result block (the kernels after this one accumulate
+       into it) */
+    if (blockIdx.x == 0) {
+        if (threadIdx.x < 10) res->tstat[threadIdx.x] = 0;
+        if (threadIdx.x == 10) res->eof_cand = ~0ull;
+        if (threadIdx.x == 11) res->redo_n = 0;
+    }
     for (uint32_t i = threadIdx.x; i < pg.nslices; i += PART_BLOCK) hist[i] = 0;
     Ctx cx{buf, len, lo, table, nullptr, shortcnt, acc, res, maskk, 0, k, nullptr};
     const int lane = threadIdx.x & 63;
@@ -1159,17 +1166,33 @@ k_part(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint
         dst[0] = v0_.x; dst[1] = v0_.y; dst[2] = v0_.z; dst[3] = v0_.w;               \
         dst[4] = v1_.x; dst[5] = v1_.y; dst[6] = v1_.z; dst[7] = v1_.w;               \
     }
+    /* halo (lanes 0..7) and the first three tiles in flight before anything
+       waits (as in k_count) */
+    uint32_t hw[8];
+    const int64_t ho = (int64_t)sp.rbase - (int64_t)FK_HALO_BYTES + (int64_t)lane * FK_LANE_BYTES;
+    const bool hv = has && lane < (int)(FK_HALO_BYTES / FK_LANE_BYTES) && ho >= lo;
+    {
+        const int64_t hc = max(min(ho, (int64_t)len - (int64_t)FK_LANE_BYTES), lo);
+        const u32x4 *hp = reinterpret_cast<const u32x4 *>(buf + hc);
+        u32x4 h0 = __builtin_nontemporal_load(hp), h1 = __builtin_nontemporal_load(hp + 1);
+        hw[0] = h0.x; hw[1] = h0.y; hw[2] = h0.z; hw[3] = h0.w;
+        hw[4] = h1.x; hw[5] = h1.y; hw[6] = h1.z; hw[7] = h1.w;
+    }
     uint32_t A[8] = {}, B[8] = {}, C[8] = {};
+    asm volatile("" ::: "memory");
     FK_LOADP(A, 0);
     asm volatile("" ::: "memory");
     FK_LOADP(B, 1);
     asm volatile("" ::: "memory");
     FK_LOADP(C, 2);
+    /* entering state: the known stream state for chunk 0, else a guess from
+       the halo (k_scan checks it, k_redo recounts a range it got wrong) */
     DState st{0, 0, 0};
     if (has) {
-        const XState x = rtrue[wave];
-        st = DState{x.code, (uint32_t)x.R, x.hdr};
+        if (c0 == 0 && has_init) st = DState{d_init->code, (uint32_t)d_init->R, d_init->hdr};
+        else st = halo_guess<H_EMIT>(cx, hw, hv);
     }
+    const DState first = st;
     Facts f{0, 0, 0, 0, 0, 0};
     Counters cnt{0, 0, 0, 0, 0, FK_NO_EOF};
     uint64_t t = 0;
@@ -1220,11 +1243,15 @@ k_part(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint
         for (uint32_t b = threadIdx.x; b < pg.nslices; b += PART_BLOCK) pg.idx[(size_t)b * pg.rows + row] = 0;
         if (threadIdx.x == 0) pg.row_base[row] = blk_cursor;
     }
-    /* exact observations of the range (its entering state was exact) */
+    /* the range's record: transfer function, guess, observations */
     if (has) {
-        RangeRec r = rr[wave];
+        RangeRec r;
+        r.tf = fk_tf_span(first, st, f);
+        r.a_code = first.code; r.a_R = first.R; r.a_hdr = first.hdr;
+        r.c0 = c0; r.c1 = c1;
+        r.resume = 0;
         range_obs(cx, cnt, 1u, sp, &r, true);
-        if (lane == 0) { rr[wave].eof = r.eof; rr[wave].unknown = r.unknown; }
+        if (lane == 0) rr[wave] = r;
     } else {
         flush_counters(cx, cnt, 1u);
     }
@@ -2052,7 +2079,7 @@ static int wait_results(fk_engine *e) {
 
 /* k_part + k_bucket_count over a resolved segment (exact range states in
    d_rtrue): the counting of the partitioned path */
-static int launch_part(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t lo, const Geo &g) {
+static int launch_part(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t lo, const Geo &g, int has_init) {
     PartGeo pg;
     const int k = e->k;
     pg.sh = std::min(15, 2 * k - 6);                       /* >= 64 slices, <= 2^15 bins (128 KiB) each */
@@ -2082,8 +2109,9 @@ static int launch_part(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t l
     pg.codes = e->d_codes;
     pg.idx = e->d_pidx;
     pg.row_base = e->d_prow;
-    hipLaunchKernelGGL(k_part, dim3(g.grid), dim3(PART_BLOCK), 0, e->stream, buf, len, lo, e->k, e->maskk,
-                       e->d_table, e->d_short, e->d_acc, e->d_res, e->d_rr, g.nchunks, g.cpw, e->d_rtrue, pg);
+    hipExtLaunchKernelGGL(k_part, dim3(g.grid), dim3(PART_BLOCK), 0, e->stream, e->ev[0], e->ev[1], 0, buf, len,
+                          lo, e->k, e->maskk, e->d_table, e->d_short, e->d_acc, e->d_res, e->d_rr, g.nchunks,
+                          g.cpw, e->d_state, has_init, pg);
     HIPCHK(hipGetLastError());
     const uint32_t groups = std::max<uint32_t>(1, (uint32_t)e->cus / pg.nslices);
     hipLaunchKernelGGL(k_bucket_count, dim3(pg.nslices * groups), dim3(1024), (size_t)sizeof(uint32_t) << pg.sh,
@@ -2096,7 +2124,7 @@ static int launch_part(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t l
 static int resolve_and_fetch(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t lo, const Geo &g) {
     int rc = launch_scan(e, g, 0);
     if (rc) return rc;
-    rc = e->part ? launch_part(e, buf, len, lo, g) : launch_redo(e, buf, len, lo, g, 0);
+    rc = launch_redo(e, buf, len, lo, g, 0);
     if (rc) return rc;
     rc = launch_table_stats(e, false, e->ev[2]);
     if (rc) return rc;
@@ -2191,10 +2219,16 @@ static int count_segment(fk_engine *e, const uint8_t *dbuf, uint64_t len, int64_
     int rc = grow_arrays(e, g.nranges);
     if (rc) return rc;
     settle_times(e, true);   /* before ev[] are reused */
-    rc = launch_count(e, dbuf, len, lo, g, has_init);
-    if (rc) return rc;
-    rc = launch_resume(e, dbuf, len, lo, g);
-    if (rc) return rc;
+    if (e->part) {
+        /* 8 <= k <= 12: partitioned counting (k_part + k_bucket_count) */
+        rc = launch_part(e, dbuf, len, lo, g, has_init);
+        if (rc) return rc;
+    } else {
+        rc = launch_count(e, dbuf, len, lo, g, has_init);
+        if (rc) return rc;
+        rc = launch_resume(e, dbuf, len, lo, g);
+        if (rc) return rc;
+    }
     e->chunks += g.nchunks;
     return FK_OK;
 }

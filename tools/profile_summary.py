@@ -27,7 +27,12 @@ out = os.path.join(repo, "profiles")
 os.makedirs(out, exist_ok=True)
 
 
-def counter(pass_dir, name, kernel="k_count"):
+# the dominant kernel: k_count (k <= 7 or >= 13), k_part (8 <= k <= 12)
+main = "k_part" if 8 <= k <= 12 else "k_count"
+
+
+def counter(pass_dir, name, kernel=None):
+    kernel = kernel or main
     vals = []
     for f in glob.glob(os.path.join(src, pass_dir, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
@@ -50,10 +55,10 @@ if fetch and write:
     f_kib = statistics.mean(fetch)
     w_kib = statistics.mean(write)
     hbm = f_kib * 1024 * 2 + w_kib * 1024
-    summary["k_count_pmc"] = {"launches": len(fetch), "fetch_size_kib": f_kib, "write_size_kib": w_kib,
+    summary[main + "_pmc"] = {"launches": len(fetch), "fetch_size_kib": f_kib, "write_size_kib": w_kib,
                               "hbm_bytes_per_launch": hbm}
     input_bytes = int(sys.argv[5]) if len(sys.argv) > 5 else None
-    json.dump({"kernel": "k_count", "k": k, "fasta_line": L, "input_bytes": input_bytes,
+    json.dump({"kernel": main, "k": k, "fasta_line": L, "input_bytes": input_bytes,
                "hbm_bytes_per_launch": hbm,
                "fetch_size_kib": f_kib, "write_size_kib": w_kib,
                "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes over "
@@ -65,8 +70,8 @@ for p in ("pmc3", "pmc4"):
     for f in glob.glob(os.path.join(src, p, "**", "*counter_collection.csv"), recursive=True):
         agg = {}
         for r in csv.DictReader(open(f)):
-            if "k_count" in r["Kernel_Name"]:
+            if main in r["Kernel_Name"]:
                 agg.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
-        summary.setdefault("k_count_sq", {}).update({n: statistics.mean(v) for n, v in agg.items()})
+        summary.setdefault(main + "_sq", {}).update({n: statistics.mean(v) for n, v in agg.items()})
 json.dump(summary, open(os.path.join(out, f"{tag}_summary.json"), "w"), indent=1)
 print(json.dumps(summary, indent=1)[:3000])
