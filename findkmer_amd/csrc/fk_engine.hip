@@ -377,22 +377,6 @@ __device__ __forceinline__ uint32_t from_prev_lane(uint32_t v, uint32_t carry) {
     return (uint32_t)__builtin_amdgcn_update_dpp((int)carry, (int)v, 0x138, 0xF, 0xF, false);
 }
 
-/* Classify one 16-byte half: bad (non-ACGT, non-'\n') bytes and '\n' mask. */
-__device__ __forceinline__ void half_check(const uint32_t *w, const uint32_t *x, uint32_t &bad,
-                                           uint32_t &nlm) {
-    nlm = 0;
-    bad = 0;
-#pragma unroll
-    for (int d = 0; d < 4; d++) {
-        uint32_t e = __builtin_amdgcn_perm(0u, 0x47544341u, x[d]);   /* "ACTG"[x] */
-        uint32_t mis = nz_bytes(e ^ w[d]);
-        uint32_t isnl = ~nz_bytes(w[d] ^ 0x0A0A0A0Au) & 0x80808080u;
-        bad |= mis & ~isnl;
-        nlm |= ((isnl >> 7) & 1u) << (4 * d) | ((isnl >> 15) & 1u) << (4 * d + 1) |
-               ((isnl >> 23) & 1u) << (4 * d + 2) | ((isnl >> 31) & 1u) << (4 * d + 3);
-    }
-}
-
 /* 16 bases -> 32-bit word, first base in bits 31:30 (v_dot4_u32_u8 x4) */
 __device__ __forceinline__ uint32_t pack16(const uint32_t *x) {
     uint32_t P = __builtin_amdgcn_udot4(x[0], 0x01041040u, 0u, false);
@@ -401,13 +385,11 @@ __device__ __forceinline__ uint32_t pack16(const uint32_t *x) {
     return __builtin_amdgcn_udot4(x[3], 0x01041040u, P << 8, false);
 }
 
-/* drop the '\n' digit (byte j) -> 15 bases right-aligned */
-__device__ __forceinline__ uint32_t squeeze(uint32_t P, uint32_t nlm) {
-    int j = __ffs(nlm) - 1;
-    uint32_t lo_bits = 30u - 2u * (uint32_t)j;
-    uint32_t hi = j ? (P >> (32u - 2u * (uint32_t)j)) : 0u;
-    uint32_t lo = lo_bits ? (P & ((1u << lo_bits) - 1u)) : 0u;
-    return (lo_bits < 32u ? (hi << lo_bits) : 0u) | lo;
+/* drop digit j (the '\n' byte; first digit in bits 31:30) -> 15 bases
+   right-aligned: the digits after j stay, those before it move down one */
+__device__ __forceinline__ uint32_t squeeze(uint32_t P, uint32_t j) {
+    const uint32_t keep = __builtin_amdgcn_ubfe(0xFFFFFFFFu, 0u, 30u - 2u * j);   /* (1 << (30-2j)) - 1 */
+    return (P & keep) | ((P >> 2) & ~keep);
 }
 
 /* Count the 16 windows ending in one half: {C, S2} is a contiguous base
@@ -481,21 +463,38 @@ __device__ __forceinline__ bool tile_fast(const Ctx &cx, const uint32_t w[8], DS
 #endif
     const int lane = threadIdx.x & 63;
     const int k = cx.k;
-    uint32_t x[8];
+    uint32_t x[8], m[8];
     uint32_t mis = 0;
 #pragma unroll
     for (int d = 0; d < 8; d++) {
         x[d] = (w[d] >> 1) & 0x03030303u;
-        mis |= __builtin_amdgcn_perm(0u, 0x47544341u, x[d]) ^ w[d];
+        m[d] = __builtin_amdgcn_perm(0u, 0x47544341u, x[d]) ^ w[d];   /* byte != "ACTG"[x] */
+        mis |= m[d];
     }
+    /* per half: 0 = no '\n', 16 + j = one '\n' at byte j (more than one
+       gives >= 33) */
     uint32_t nl0 = 0, nl1 = 0;
     bool lane_ok = true;
+#if FK_EXP == 9   /* ablation: newline classification skipped (timing only) */
+    if (mis) { nl0 = 16u; nl1 = 0u; }
+#else
     if (mis) {                                   /* some byte is not a base */
-        uint32_t b0, b1;
-        half_check(w, x, b0, nl0);
-        half_check(w + 4, x + 4, b1, nl1);
-        lane_ok = (b0 | b1) == 0 && __popc(nl0) <= 1 && __popc(nl1) <= 1;
+        /* a byte is a base (m = 0) or '\n' (w ^ 0x0A = 0) iff the product
+           of the two is 0: one dot4 checks four bytes exactly */
+        uint32_t bad = 0;
+#pragma unroll
+        for (int d = 0; d < 8; d++) bad = __builtin_amdgcn_udot4(m[d], w[d] ^ 0x0A0A0A0Au, bad, false);
+        /* then m = 0x49 exactly at the '\n' bytes: bit 0 marks them, and a
+           dot4 with weights 16 + j gives the count-and-position code */
+#pragma unroll
+        for (int d = 0; d < 4; d++) {
+            const uint32_t wt = 0x13121110u + 0x04040404u * (uint32_t)d;
+            nl0 = __builtin_amdgcn_udot4(m[d] & 0x01010101u, wt, nl0, false);
+            nl1 = __builtin_amdgcn_udot4(m[d + 4] & 0x01010101u, wt, nl1, false);
+        }
+        lane_ok = bad == 0 && nl0 < 32u && nl1 < 32u;
     }
+#endif
     if (__ballot(!lane_ok)) return false;
     /* deep: every window of the tile counts (seq > k throughout); neg: the
        reference's int32 seqSize stays negative for the whole tile (a run
@@ -506,8 +505,8 @@ __device__ __forceinline__ bool tile_fast(const Ctx &cx, const uint32_t w[8], DS
 
     uint32_t S0 = pack16(x), S1 = pack16(x + 4);
     const bool h0 = nl0 != 0, h1 = nl1 != 0;
-    if (h0) S0 = squeeze(S0, nl0);
-    if (h1) S1 = squeeze(S1, nl1);
+    if (h0) S0 = squeeze(S0, nl0 - 16u);
+    if (h1) S1 = squeeze(S1, nl1 - 16u);
     /* the 16-byte piece before each half: contiguous layout (lane = 32
        bytes) -> half 0 follows the previous lane's half 1 and half 1 its own
        half 0; interleaved layout (half h of lane L at h*1024 + 16L) -> each
@@ -544,12 +543,12 @@ __device__ __forceinline__ bool tile_fast(const Ctx &cx, const uint32_t w[8], DS
             if (INTER) {
                 const bool in0 = nb0 != 0;
                 const int L = __ffsll((long long)(in0 ? nb0 : nb1)) - 1;
-                const uint32_t m = in0 ? rdlane(nl0, L) : rdlane(nl1, L);
-                before = (in0 ? 0u : 1024u) + 16u * (uint32_t)L + (uint32_t)(__ffs(m) - 1);
+                const uint32_t c = in0 ? rdlane(nl0, L) : rdlane(nl1, L);
+                before = (in0 ? 0u : 1024u) + 16u * (uint32_t)L + (c - 16u);
             } else {
                 const int L0 = __ffsll((long long)(nb0 | nb1)) - 1;
                 const uint32_t a = rdlane(nl0, L0), b = rdlane(nl1, L0);
-                before = (uint32_t)L0 * FK_LANE_BYTES + (a ? (uint32_t)(__ffs(a) - 1) : 16u + (uint32_t)(__ffs(b) - 1));
+                before = (uint32_t)L0 * FK_LANE_BYTES + (a ? a - 16u : b);
             }
             f.found_p1 = 1;
             f.p1_gt = 0;
@@ -845,6 +844,10 @@ k_count(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uin
             st = halo_guess<HM>(cx, hw, hv);
 #endif
         }
+        /* the halo words are waited for on every path (the d_init one too):
+           a load left pending into the loop makes its first tile wait for
+           vmcnt(0), i.e. for all three tiles in flight */
+        consume(hw);
         const DState first = st;
         Facts f{0, 0, 0, 0, 0, 0};
         Counters cnt{0, 0, 0, 0, 0, FK_NO_EOF};
@@ -880,6 +883,7 @@ k_count(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uin
             const int64_t toff = (int64_t)(sp.rbase + t * FK_TILE_BYTES);
             const int nb = load_lane<FK_LANE_BYTES>(cx, toff + lane * (int64_t)FK_LANE_BYTES, v);
             tile_general<true, HM>(cx, v, nb, (uint32_t)(t * FK_TILE_BYTES), st, f, cnt, 1u);
+            consume(v);
             t++;
             primed = t < sp.nfull;
             if (primed) {
@@ -1192,6 +1196,7 @@ k_part(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint
         if (c0 == 0 && has_init) st = DState{d_init->code, (uint32_t)d_init->R, d_init->hdr};
         else st = halo_guess<H_EMIT>(cx, hw, hv);
     }
+    consume(hw);   /* waited on every path (see k_count) */
     const DState first = st;
     Facts f{0, 0, 0, 0, 0, 0};
     Counters cnt{0, 0, 0, 0, 0, FK_NO_EOF};
@@ -1213,6 +1218,7 @@ k_part(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint
                 const int64_t toff_ = (int64_t)(sp.rbase + t * FK_TILE_BYTES);       \
                 const int nb_ = load_lane<FK_LANE_BYTES>(cx, toff_ + lane * (int64_t)FK_LANE_BYTES, v_); \
                 tile_general<true, H_EMIT>(cx, v_, nb_, (uint32_t)(t * FK_TILE_BYTES), st, f, cnt, 1u); \
+                consume(v_);                                                         \
             }                                                                        \
             t++;                                                                     \
             done = t >= sp.ntiles;                                                   \
@@ -1454,12 +1460,15 @@ k_table_stats(uint32_t *table, uint64_t n, int k, DevRes *res,
     for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n4; i += (uint64_t)gridDim.x * blockDim.x) {
         uint4 v = t4[i];
         if (nsub) {
-            /* fold k_count's sub-tables into the table (and clear them) */
-            for (int s = 0; s < nsub; s++) {
-                uint4 *p = reinterpret_cast<uint4 *>(subs + (size_t)s * n) + i;
-                const uint4 a = *p;
-                v.x += a.x; v.y += a.y; v.z += a.z; v.w += a.w;
-                *p = make_uint4(0, 0, 0, 0);
+            /* fold k_count's sub-tables into the table (and clear them); all
+               FK_SUBTABLES loads in flight at once */
+            uint4 a[FK_SUBTABLES];
+#pragma unroll
+            for (int s = 0; s < FK_SUBTABLES; s++) a[s] = reinterpret_cast<uint4 *>(subs + (size_t)s * n)[i];
+#pragma unroll
+            for (int s = 0; s < FK_SUBTABLES; s++) {
+                v.x += a[s].x; v.y += a[s].y; v.z += a[s].z; v.w += a[s].w;
+                reinterpret_cast<uint4 *>(subs + (size_t)s * n)[i] = make_uint4(0, 0, 0, 0);
             }
             t4[i] = v;
         }
