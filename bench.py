@@ -178,7 +178,7 @@ def main():
     value = world * n / (dt / args.steps)
     kern_ms = main_ms / args.steps
     algo_bytes = nbytes + 4 * (1 << (2 * k))       # input read once + u32 table written once
-    achieved = algo_bytes / (kern_ms * 1e-3) / 1e9
+    achieved = algo_bytes / (kern_ms * 1e-3) / 1e9 if kern_ms > 0 else 0.0   # 0: events off (FK_NO_EVENTS)
     traffic = None
     tf = os.path.join(REPO, "profiles", f"traffic_k{k}_L{L}.json")
     if os.path.exists(tf):

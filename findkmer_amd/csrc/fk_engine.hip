@@ -116,6 +116,7 @@ struct Counters {       /* per lane; flushed per range */
     uint32_t win;       /* windows counted */
     uint32_t unknown;
     uint32_t eof;       /* range-relative offset of first 0xFF, or FK_NO_EOF */
+    uint32_t win_u;     /* windows counted, wave-uniform (an SGPR; lane 0 flushes it) */
 };
 
 /* Where windows are accumulated. */
@@ -153,6 +154,17 @@ struct Ctx {            /* kernel-wide constants */
     uint32_t *flush;    /* where lds_flush adds the bins (nullptr: table) */
 };
 
+/* LDS atomic add at a byte offset into the bins.  The kernels that count
+   in LDS (k_count, k_resume, k_redo) have no static LDS, so their dynamic
+   bins start at LDS address 0 (checked on the host, lds_layout_ok): the
+   address is the offset itself, with no base add per atomic (a generic
+   pointer costs one v_add each, 16 per tile). */
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+__device__ __forceinline__ void lds_add(const Ctx &, uint32_t byte_off, uint32_t v) {
+    lds_u32 *p = (lds_u32 *)(uintptr_t)byte_off;
+    __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
 /* idx in the internal encoding (A0 C1 T2 G3) */
 template <int HM>
 __device__ __forceinline__ void hist_add(const Ctx &cx, uint64_t idx, uint32_t w) {
@@ -160,9 +172,9 @@ __device__ __forceinline__ void hist_add(const Ctx &cx, uint64_t idx, uint32_t w
     if (HM == H_GLOBAL || HM == H_EMIT) {
         atomicAdd(&cx.table[fk_sigma(idx)], w);
     } else if (HM == H_LDS) {
-        atomicAdd(&cx.lds[(uint32_t)idx], w);
+        lds_add(cx, (uint32_t)idx * 4u, w);
     } else {
-        atomicAdd(&cx.lds[cx.single_off + (uint32_t)idx], w);
+        lds_add(cx, (cx.single_off + (uint32_t)idx) * 4u, w);
     }
 }
 
@@ -385,10 +397,17 @@ __device__ __forceinline__ uint32_t pack16(const uint32_t *x) {
     return __builtin_amdgcn_udot4(x[3], 0x01041040u, P << 8, false);
 }
 
+/* The newline code of a half (tile_fast): 0 = no '\n'; 73 * (16 + j) = one
+   '\n' at byte j; anything >= NL_TWO = more than one.  nl_byte decodes j + 16
+   (exact for 16..31: 73 t * 899 >> 16 = t). */
+#define NL_TWO (73u * 33u)
+__device__ __forceinline__ uint32_t nl_byte(uint32_t c) { return __umul24(c, 899u) >> 16; }
+
 /* drop digit j (the '\n' byte; first digit in bits 31:30) -> 15 bases
-   right-aligned: the digits after j stay, those before it move down one */
-__device__ __forceinline__ uint32_t squeeze(uint32_t P, uint32_t j) {
-    const uint32_t keep = __builtin_amdgcn_ubfe(0xFFFFFFFFu, 0u, 30u - 2u * j);   /* (1 << (30-2j)) - 1 */
+   right-aligned: the digits after j stay, those before it move down one.
+   t = 16 + j. */
+__device__ __forceinline__ uint32_t squeeze(uint32_t P, uint32_t t) {
+    const uint32_t keep = __builtin_amdgcn_ubfe(0xFFFFFFFFu, 0u, 62u - 2u * t);   /* (1 << (30-2j)) - 1 */
     return (P & keep) | ((P >> 2) & ~keep);
 }
 
@@ -404,11 +423,10 @@ __device__ __forceinline__ void half_windows(const Ctx &cx, uint32_t C, uint32_t
            (0,1),(2,3),...; without a real slot 0 the first pair becomes the
            single k-mer at slot 1 */
         const uint32_t m3 = (uint32_t)((cx.maskk << 2) | 3u) << 2;
-        char *L = reinterpret_cast<char *>(cx.lds);
 #if FK_EXP == 1   /* ablation: addresses computed, no LDS atomics */
 #define FK_LDS_ADD(a_) asm volatile("" ::"v"(a_))
 #else
-#define FK_LDS_ADD(a_) atomicAdd(reinterpret_cast<uint32_t *>(L + (a_)), weight)
+#define FK_LDS_ADD(a_) lds_add(cx, (a_), weight)
 #endif
         {
             uint32_t v = __builtin_amdgcn_alignbit(C, S2, 26u);
@@ -429,7 +447,7 @@ __device__ __forceinline__ void half_windows(const Ctx &cx, uint32_t C, uint32_t
             uint32_t v = i < 15 ? __builtin_amdgcn_alignbit(C, S2, sh) : S2;
             uint32_t idx = v & (uint32_t)cx.maskk;
             if (i > 0 || !skip0) {
-                if (HM == H_LDS) atomicAdd(&cx.lds[idx], weight);
+                if (HM == H_LDS) lds_add(cx, idx * 4u, weight);
                 else atomicAdd(&cx.table[fk_sigma(idx)], weight);
             }
         }
@@ -447,55 +465,14 @@ __device__ __forceinline__ void half_windows(const Ctx &cx, uint32_t C, uint32_t
  * v_dot4_u32_u8; the previous lane's last word arrives by DPP wave_shr:1;
  * each window is one v_alignbit of a 64-bit {context, word} pair.
  */
-template <bool COUNT, int HM, bool INTER>
-__device__ __forceinline__ bool tile_fast(const Ctx &cx, const uint32_t w[8], DState &st, Facts &f,
-                                          Counters &cnt, uint32_t weight, Emit *em = nullptr) {
-#if FK_EXP == 4   /* ablation: loop framework only */
-    {
-        uint32_t x = 0;
-#pragma unroll
-        for (int d = 0; d < 8; d++) x ^= w[d];
-        asm volatile("" ::"v"(x));
-        st.R += FK_TILE_BYTES;
-        if (threadIdx.x % 64 == 0) cnt.win += FK_TILE_BYTES;
-        return true;
-    }
-#endif
+/* The part of a fast tile after classification.  NL: some lane has a '\n'
+ * (nl0/nl1 per half: 0, or 16 + its byte); without one every half holds 16
+ * bases and all of the newline handling folds away. */
+template <bool COUNT, int HM, bool INTER, bool NL>
+__device__ __forceinline__ bool tile_finish(const Ctx &cx, const uint32_t x[8], uint32_t nl0, uint32_t nl1,
+                                            DState &st, Facts &f, Counters &cnt, uint32_t weight, Emit *em) {
     const int lane = threadIdx.x & 63;
     const int k = cx.k;
-    uint32_t x[8], m[8];
-    uint32_t mis = 0;
-#pragma unroll
-    for (int d = 0; d < 8; d++) {
-        x[d] = (w[d] >> 1) & 0x03030303u;
-        m[d] = __builtin_amdgcn_perm(0u, 0x47544341u, x[d]) ^ w[d];   /* byte != "ACTG"[x] */
-        mis |= m[d];
-    }
-    /* per half: 0 = no '\n', 16 + j = one '\n' at byte j (more than one
-       gives >= 33) */
-    uint32_t nl0 = 0, nl1 = 0;
-    bool lane_ok = true;
-#if FK_EXP == 9   /* ablation: newline classification skipped (timing only) */
-    if (mis) { nl0 = 16u; nl1 = 0u; }
-#else
-    if (mis) {                                   /* some byte is not a base */
-        /* a byte is a base (m = 0) or '\n' (w ^ 0x0A = 0) iff the product
-           of the two is 0: one dot4 checks four bytes exactly */
-        uint32_t bad = 0;
-#pragma unroll
-        for (int d = 0; d < 8; d++) bad = __builtin_amdgcn_udot4(m[d], w[d] ^ 0x0A0A0A0Au, bad, false);
-        /* then m = 0x49 exactly at the '\n' bytes: bit 0 marks them, and a
-           dot4 with weights 16 + j gives the count-and-position code */
-#pragma unroll
-        for (int d = 0; d < 4; d++) {
-            const uint32_t wt = 0x13121110u + 0x04040404u * (uint32_t)d;
-            nl0 = __builtin_amdgcn_udot4(m[d] & 0x01010101u, wt, nl0, false);
-            nl1 = __builtin_amdgcn_udot4(m[d + 4] & 0x01010101u, wt, nl1, false);
-        }
-        lane_ok = bad == 0 && nl0 < 32u && nl1 < 32u;
-    }
-#endif
-    if (__ballot(!lane_ok)) return false;
     /* deep: every window of the tile counts (seq > k throughout); neg: the
        reference's int32 seqSize stays negative for the whole tile (a run
        past 2^31-1 bases, :977), so the tile only advances the state */
@@ -504,9 +481,13 @@ __device__ __forceinline__ bool tile_fast(const Ctx &cx, const uint32_t w[8], DS
     if (COUNT && !deep && !neg) return false;
 
     uint32_t S0 = pack16(x), S1 = pack16(x + 4);
-    const bool h0 = nl0 != 0, h1 = nl1 != 0;
-    if (h0) S0 = squeeze(S0, nl0 - 16u);
-    if (h1) S1 = squeeze(S1, nl1 - 16u);
+    const bool h0 = NL && nl0 != 0, h1 = NL && nl1 != 0;
+    /* a half with a '\n' holds 15 bases, right-aligned (the next lane's
+       context and the carried state read it as the stream's last digits) */
+    if (NL) {
+        S0 = h0 ? squeeze(S0, nl_byte(nl0)) : S0;
+        S1 = h1 ? squeeze(S1, nl_byte(nl1)) : S1;
+    }
     /* the 16-byte piece before each half: contiguous layout (lane = 32
        bytes) -> half 0 follows the previous lane's half 1 and half 1 its own
        half 0; interleaved layout (half h of lane L at h*1024 + 16L) -> each
@@ -515,18 +496,18 @@ __device__ __forceinline__ bool tile_fast(const Ctx &cx, const uint32_t w[8], DS
     const uint32_t P0 = INTER ? from_prev_lane(S0, (uint32_t)st.code) : from_prev_lane(S1, (uint32_t)st.code);
     const uint32_t P1 = INTER ? from_prev_lane(S1, rdlane(S0, 63)) : S0;
     /* make each {C, S2} one contiguous base stream with S2 holding 16 digits */
-    const uint32_t A2 = h0 ? (S0 | ((P0 & 3u) << 30)) : S0;
+    const uint32_t A2 = h0 ? (S0 | (P0 << 30)) : S0;
     const uint32_t AC = h0 ? (P0 >> 2) : P0;
-    const uint32_t B2 = h1 ? (S1 | ((P1 & 3u) << 30)) : S1;
+    const uint32_t B2 = h1 ? (S1 | (P1 << 30)) : S1;
     const uint32_t BC = h1 ? (P1 >> 2) : P1;
 
-    const uint64_t nb0 = __ballot(h0), nb1 = __ballot(h1);
-    const uint32_t nsym = FK_TILE_BYTES - (uint32_t)__popcll(nb0) - (uint32_t)__popcll(nb1);
+    const uint64_t nb0 = NL ? __ballot(h0) : 0ull, nb1 = NL ? __ballot(h1) : 0ull;
+    const uint32_t nsym = NL ? FK_TILE_BYTES - (uint32_t)__popcll(nb0) - (uint32_t)__popcll(nb1) : FK_TILE_BYTES;
     if (COUNT) {
         if (HM == H_EMIT) {
             em->AC = AC; em->A2 = A2; em->BC = BC; em->B2 = B2;
             em->h0 = h0; em->h1 = h1; em->deep = deep;
-            if (deep && lane == 0) cnt.win += nsym;
+            if (deep) cnt.win_u += nsym;
         } else if (HM == H_NONE) {
         } else if (deep) {
 #if FK_EXP == 2   /* ablation: no window work at all */
@@ -535,19 +516,19 @@ __device__ __forceinline__ bool tile_fast(const Ctx &cx, const uint32_t w[8], DS
             half_windows<HM>(cx, AC, A2, h0, weight);
             half_windows<HM>(cx, BC, B2, h1, weight);
 #endif
-            if (lane == 0) cnt.win += nsym;
+            cnt.win_u += nsym;
         }
         /* facts: the first '\n' of the span (all bytes before it are bases) */
-        if (!f.found_p1 && (nb0 | nb1)) {
+        if (NL && !f.found_p1 && (nb0 | nb1)) {
             uint32_t before;
             if (INTER) {
                 const bool in0 = nb0 != 0;
                 const int L = __ffsll((long long)(in0 ? nb0 : nb1)) - 1;
-                const uint32_t c = in0 ? rdlane(nl0, L) : rdlane(nl1, L);
+                const uint32_t c = nl_byte(in0 ? rdlane(nl0, L) : rdlane(nl1, L));
                 before = (in0 ? 0u : 1024u) + 16u * (uint32_t)L + (c - 16u);
             } else {
                 const int L0 = __ffsll((long long)(nb0 | nb1)) - 1;
-                const uint32_t a = rdlane(nl0, L0), b = rdlane(nl1, L0);
+                const uint32_t a = nl_byte(rdlane(nl0, L0)), b = nl_byte(rdlane(nl1, L0));
                 before = (uint32_t)L0 * FK_LANE_BYTES + (a ? a - 16u : b);
             }
             f.found_p1 = 1;
@@ -560,6 +541,76 @@ __device__ __forceinline__ bool tile_fast(const Ctx &cx, const uint32_t w[8], DS
     /* the last 32 bases: lane 63's second half and its context (both layouts) */
     st.code = ((uint64_t)rdlane(BC, 63) << 32) | rdlane(B2, 63);
     return true;
+}
+
+/*
+ * Fast tile: every byte is A/C/G/T except at most one '\n' per 16-byte half
+ * lane, the wave is outside a header and deep inside a run (every window
+ * counts as seqSize > k).  Returns false (without side effects) when the
+ * tile does not qualify; the caller then runs tile_general.
+ *
+ * Per lane (32 bytes): bases -> 2-bit codes (A0 C1 T2 G3 = (byte>>1)&3, a
+ * v_perm checks them against the bytes), two 32-bit words via
+ * v_dot4_u32_u8; the previous lane's last word arrives by DPP wave_shr:1;
+ * each window is one v_alignbit of a 64-bit {context, word} pair.  A tile
+ * of bases only (wave-uniform test) takes tile_finish<NL = false>.
+ */
+template <bool COUNT, int HM, bool INTER>
+__device__ __forceinline__ bool tile_fast(const Ctx &cx, const uint32_t w[8], DState &st, Facts &f,
+                                          Counters &cnt, uint32_t weight, Emit *em = nullptr) {
+#if FK_EXP == 4   /* ablation: loop framework only */
+    {
+        uint32_t x = 0;
+#pragma unroll
+        for (int d = 0; d < 8; d++) x ^= w[d];
+        asm volatile("" ::"v"(x));
+        st.R += FK_TILE_BYTES;
+        cnt.win_u += FK_TILE_BYTES;
+        return true;
+    }
+#endif
+    uint32_t x[8], m[8];
+    uint32_t mis = 0;
+#pragma unroll
+    for (int d = 0; d < 8; d++) {
+        x[d] = (w[d] >> 1) & 0x03030303u;
+        m[d] = __builtin_amdgcn_perm(0u, 0x47544341u, x[d]) ^ w[d];   /* byte != "ACTG"[x] */
+        mis |= m[d];
+    }
+    if (!__ballot(mis != 0)) return tile_finish<COUNT, HM, INTER, false>(cx, x, 0u, 0u, st, f, cnt, weight, em);
+    /* some lane has a non-base byte: every lane classifies (the wave runs
+       this once for all of them).  A byte is a base (m = 0) or '\n'
+       (w ^ 0x0A = 0) iff the product of the two is 0, so dot4(m, w ^ 0x0A)
+       checks four bytes exactly (short chains: the dot4 latency is long).
+       On a lane without other bytes m = 0x49 exactly at the '\n's, and a
+       dot4 with weights 16 + j gives the half's newline code (NL_TWO). */
+    uint32_t bad4[4], nl0, nl1;
+#if FK_EXP == 9   /* ablation: newline classification skipped (timing only) */
+    nl0 = mis ? 73u * 16u : 0u;
+    nl1 = 0u;
+    const bool lane_ok = true;
+#else
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+        bad4[c] = __builtin_amdgcn_udot4(m[2 * c], w[2 * c] ^ 0x0A0A0A0Au, 0u, false);
+        bad4[c] = __builtin_amdgcn_udot4(m[2 * c + 1], w[2 * c + 1] ^ 0x0A0A0A0Au, bad4[c], false);
+    }
+    {
+        uint32_t a0 = __builtin_amdgcn_udot4(m[0], 0x13121110u, 0u, false);
+        uint32_t a1 = __builtin_amdgcn_udot4(m[2], 0x1B1A1918u, 0u, false);
+        uint32_t b0 = __builtin_amdgcn_udot4(m[4], 0x13121110u, 0u, false);
+        uint32_t b1 = __builtin_amdgcn_udot4(m[6], 0x1B1A1918u, 0u, false);
+        a0 = __builtin_amdgcn_udot4(m[1], 0x17161514u, a0, false);
+        a1 = __builtin_amdgcn_udot4(m[3], 0x1F1E1D1Cu, a1, false);
+        b0 = __builtin_amdgcn_udot4(m[5], 0x17161514u, b0, false);
+        b1 = __builtin_amdgcn_udot4(m[7], 0x1F1E1D1Cu, b1, false);
+        nl0 = a0 + a1;
+        nl1 = b0 + b1;
+    }
+    const bool lane_ok = (bad4[0] | bad4[1] | bad4[2] | bad4[3]) == 0 && nl0 < NL_TWO && nl1 < NL_TWO;
+#endif
+    if (__ballot(!lane_ok)) return false;
+    return tile_finish<COUNT, HM, INTER, true>(cx, x, nl0, nl1, st, f, cnt, weight, em);
 }
 
 /* wave-wide sum via butterfly */
@@ -587,7 +638,7 @@ __device__ void flush_counters(const Ctx &cx, Counters &cnt, uint32_t weight, bo
         vals[6 + b] = (uint32_t)((cnt.d1s >> (16 * b)) & 0xFFFF);
     }
     vals[4] = cnt.valid;
-    vals[5] = cnt.win;
+    vals[5] = cnt.win + (lane == 0 ? cnt.win_u : 0u);
     vals[10] = cnt.unknown;
 #pragma unroll
     for (int i = 0; i < 11; i++) vals[i] = wsum32(vals[i]);
@@ -601,7 +652,7 @@ __device__ void flush_counters(const Ctx &cx, Counters &cnt, uint32_t weight, bo
         acc_add(&cx.acc[ACC_UNK], vals[10], weight);
     }
     cnt.base = cnt.d1s = 0;
-    cnt.valid = cnt.win = 0;
+    cnt.valid = cnt.win = cnt.win_u = 0;
 }
 
 /* One tile of count_range: the fast path when it qualifies, else the general
@@ -943,7 +994,21 @@ k_resume(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, ui
     extern __shared__ uint32_t lds_bins[];
     const uint64_t wave = blockIdx.x * FK_WAVES_PER_BLOCK + wave_in_block();
     const bool mine = wave < nranges && rr[wave].resume;
-    if (!__syncthreads_or(mine)) return;   /* uniform per block */
+    /* uniform per block; in the LDS modes through the first bin (before the
+       bins are zeroed): __syncthreads_or keeps its reduction in static LDS,
+       which would move the bins off address 0 (lds_add) */
+    bool any;
+    if (LDS_MODE(HM)) {
+        if (threadIdx.x == 0) lds_bins[0] = 0;
+        __syncthreads();
+        if (mine) lds_bins[0] = 1;
+        __syncthreads();
+        any = lds_bins[0] != 0;
+        __syncthreads();
+    } else {
+        any = __syncthreads_or(mine);
+    }
+    if (!any) return;
     const uint32_t nw = lds_words(HM, k);
     if (LDS_MODE(HM)) lds_zero(lds_bins, nw);
     Ctx cx{buf, len, lo, table, LDS_MODE(HM) ? lds_bins : nullptr, shortcnt, acc, res, maskk,
@@ -1756,6 +1821,7 @@ struct fk_engine {
     uint8_t *d_stage = nullptr, *h_stage = nullptr;
     hipEvent_t ev[3] = {};
     bool times_pending = false;               /* ev[] of the last feed not yet read */
+    bool timing = true;                       /* record ev[] (env FK_NO_EVENTS=1: off) */
     bool zero_pending = false;                /* reset() not yet issued to the device */
     DevRes *h_res = nullptr, *h_res_dev = nullptr;   /* pinned, mapped result block */
     uint32_t *d_done = nullptr;               /* k_table_stats finished-block count */
@@ -1869,6 +1935,23 @@ extern "C" void fk_engine_destroy(fk_engine *e) {
     delete e;
 }
 
+/* the LDS-counting kernels keep their bins at LDS address 0 (lds_add) */
+static bool lds_layout_ok() {
+    static int ok = -1;
+    if (ok < 0) {
+        const void *fns[] = {(const void *)k_count<H_PAIRS>, (const void *)k_count<H_LDS>,
+                             (const void *)k_resume<H_PAIRS>, (const void *)k_resume<H_LDS>,
+                             (const void *)k_redo<H_PAIRS>, (const void *)k_redo<H_LDS>};
+        int good = 1;
+        for (const void *f : fns) {
+            hipFuncAttributes a;
+            if (hipFuncGetAttributes(&a, f) != hipSuccess || a.sharedSizeBytes != 0) good = 0;
+        }
+        ok = good;
+    }
+    return ok == 1;
+}
+
 extern "C" int fk_engine_create(int k, const fk_opts *opts, fk_engine **out) {
     if (!out) return FK_E_INVALID;
     *out = nullptr;
@@ -1888,6 +1971,7 @@ extern "C" int fk_engine_create(int k, const fk_opts *opts, fk_engine **out) {
     if (hipGetDeviceProperties(&prop, e->dev) == hipSuccess && prop.multiProcessorCount > 0)
         e->cus = prop.multiProcessorCount;
     if (const char *gt = getenv("FK_GENERAL_TILES")) e->general_tiles = (uint32_t)strtoul(gt, nullptr, 10);
+    if (const char *ne = getenv("FK_NO_EVENTS")) e->timing = ne[0] != '1';
     e->nbins = 1ull << (2 * k);
 #if FK_EXP == 6   /* ablation: the partitioned path for k >= 6 */
     e->part = k >= 6 && k <= 12;
@@ -1922,6 +2006,9 @@ extern "C" int fk_engine_create(int k, const fk_opts *opts, fk_engine **out) {
     ALLOC(e->d_state, sizeof(XState));
     ALLOC(e->d_tf, sizeof(TF));
 #undef ALLOC
+    /* lds_add addresses the bins from LDS address 0: the kernels that count
+       in LDS must not have static LDS (a build invariant, checked once) */
+    if (!lds_layout_ok()) { fk_engine_destroy(e); return FK_E_HIP; }
     /* the LDS bins need more than the default dynamic-LDS limit */
     size_t sh = lds_bytes(e);
     if (sh > 65536) {
@@ -1932,7 +2019,13 @@ extern "C" int fk_engine_create(int k, const fk_opts *opts, fk_engine **out) {
     if (e->part)   /* k_bucket_count: one 2^15-bin slice (128 KiB) in LDS */
         hipFuncSetAttribute((const void *)k_bucket_count, hipFuncAttributeMaxDynamicSharedMemorySize, 4 << 15);
     for (int i = 0; i < 3; i++)
-        if (hipEventCreate(&e->ev[i]) != hipSuccess) { fk_engine_destroy(e); return FK_E_HIP; }
+        /* timing only (results travel through mapped memory): no system-scope
+           fence, which costs a cache writeback + invalidate and a gap of
+           several us around each recorded launch */
+        if (hipEventCreateWithFlags(&e->ev[i], hipEventDisableSystemFence) != hipSuccess) {
+            fk_engine_destroy(e);
+            return FK_E_HIP;
+        }
     if (hipHostMalloc((void **)&e->h_res, sizeof(DevRes), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
         hipHostGetDevicePointer((void **)&e->h_res_dev, e->h_res, 0) != hipSuccess ||
         hipMalloc((void **)&e->d_done, sizeof(uint32_t)) != hipSuccess ||
@@ -2005,11 +2098,14 @@ static Geo geometry(const fk_engine *e, uint64_t len) {
     if ((e)->part) { constexpr int HM = H_NONE; __VA_ARGS__; }                  \
     else FK_DISPATCH(hist_mode(e), __VA_ARGS__)
 
+/* the timing events of a launch (none when timing is off) */
+static hipEvent_t tev(const fk_engine *e, int i) { return e->timing ? e->ev[i] : nullptr; }
+
 static int launch_count(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t lo, const Geo &g,
                         int has_init) {
     size_t sh = lds_bytes(e);
     FK_DISPATCH_COUNT(e,
-                hipExtLaunchKernelGGL((k_count<HM>), dim3(g.grid), dim3(FK_BLOCK), sh, e->stream, e->ev[0], e->ev[1],
+                hipExtLaunchKernelGGL((k_count<HM>), dim3(g.grid), dim3(FK_BLOCK), sh, e->stream, tev(e, 0), tev(e, 1),
                                       0, buf, len, lo, e->k,
                                    e->maskk, e->d_table, e->d_short, e->d_acc, e->d_res, e->d_rr,
                                    g.nchunks, e->d_state, has_init, g.cpw, e->d_resume, e->general_tiles,
@@ -2118,7 +2214,7 @@ static int launch_part(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t l
     pg.codes = e->d_codes;
     pg.idx = e->d_pidx;
     pg.row_base = e->d_prow;
-    hipExtLaunchKernelGGL(k_part, dim3(g.grid), dim3(PART_BLOCK), 0, e->stream, e->ev[0], e->ev[1], 0, buf, len,
+    hipExtLaunchKernelGGL(k_part, dim3(g.grid), dim3(PART_BLOCK), 0, e->stream, tev(e, 0), tev(e, 1), 0, buf, len,
                           lo, e->k, e->maskk, e->d_table, e->d_short, e->d_acc, e->d_res, e->d_rr, g.nchunks,
                           g.cpw, e->d_state, has_init, pg);
     HIPCHK(hipGetLastError());
@@ -2135,7 +2231,7 @@ static int resolve_and_fetch(fk_engine *e, const uint8_t *buf, uint64_t len, int
     if (rc) return rc;
     rc = launch_redo(e, buf, len, lo, g, 0);
     if (rc) return rc;
-    rc = launch_table_stats(e, false, e->ev[2]);
+    rc = launch_table_stats(e, false, tev(e, 2));
     if (rc) return rc;
     rc = wait_results(e);
     if (rc) return rc;
@@ -2201,7 +2297,7 @@ static int collect_unknown(fk_engine *e, const uint8_t *dbuf, uint64_t len, int6
    device path (ev0 -> ev2, at the end of k_table_stats).  The host continues
    as soon as the result block is published, so ev2 may still be pending: it
    is read when the events are about to be reused, or at finish. */
-static void add_times(fk_engine *e) { e->times_pending = true; }
+static void add_times(fk_engine *e) { e->times_pending = e->timing; }
 static void settle_times(fk_engine *e, bool wait) {
     if (!e->times_pending) return;
     if (!wait && hipEventQuery(e->ev[2]) != hipSuccess) {
