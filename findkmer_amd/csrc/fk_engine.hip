@@ -1859,9 +1859,12 @@ static int flush_zero(fk_engine *e) {
     return FK_OK;
 }
 
-static int set_dev(fk_engine *e) {
+/* make e's device current; flush a pending reset unless the caller launches
+   it itself right before its first kernel (count_segment: no host work
+   between the two launches, so the GPU does not idle after k_zero) */
+static int set_dev(fk_engine *e, bool flush = true) {
     HIPCHK(hipSetDevice(e->dev));
-    return flush_zero(e);
+    return flush ? flush_zero(e) : FK_OK;
 }
 
 extern "C" int fk_abi_version(void) { return FK_ABI_VERSION; }
@@ -2324,6 +2327,8 @@ static int count_segment(fk_engine *e, const uint8_t *dbuf, uint64_t len, int64_
     int rc = grow_arrays(e, g.nranges);
     if (rc) return rc;
     settle_times(e, true);   /* before ev[] are reused */
+    rc = flush_zero(e);      /* a pending reset, just before the first launch */
+    if (rc) return rc;
     if (e->part) {
         /* 8 <= k <= 12: partitioned counting (k_part + k_bucket_count) */
         rc = launch_part(e, dbuf, len, lo, g, has_init);
@@ -2398,7 +2403,7 @@ static int process_segment(fk_engine *e, const uint8_t *dbuf, uint64_t len) {
 extern "C" int fk_engine_feed(fk_engine *e, const uint8_t *buf, uint64_t len, int on_device) {
     if (!e || (!buf && len)) return FK_E_INVALID;
     if (e->shard_pending) return FK_E_STATE;
-    int rc = set_dev(e);
+    int rc = set_dev(e, false);   /* count_segment flushes a pending reset */
     if (rc) return rc;
     e->fed += len;
     if (e->ended || len == 0) return FK_OK;
