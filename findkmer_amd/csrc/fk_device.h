@@ -204,7 +204,27 @@ struct DevRes {
     XState exit;                    /* stream state after the feed */
     unsigned long long eof_cand;    /* smallest 0xFF offset seen (a candidate) */
     uint32_t redo_n;                /* ranges re-counted */
+    uint32_t need;                  /* one-pass k_count: 0 = complete, else ONE_* bits
+                                       (the host runs the rest of the path) */
+    uint32_t pad;
     uint32_t seq;                   /* host copy: written last (feed sequence number) */
+};
+
+/* what a one-pass k_count left for the host-launched kernels */
+enum { ONE_SCAN = 1u,     /* a guess check failed (or could not be made): k_scan, k_redo, k_table_stats */
+       ONE_RESUME = 2u }; /* some range ran out of general tiles: k_resume first */
+
+/* Device state of one-pass feeds (k_count's block_summary, k_tail), in
+ * device memory: k_count takes a pointer to it plus one flag word, so its
+ * counting loop carries no extra kernel arguments. */
+enum { OP_ON = 1u,        /* one pass: k_count summarises its blocks, k_tail finishes */
+       OP_FRESH = 2u };   /* a reset is pending: zero table, state and accumulators */
+struct OnePassCfg {
+    void *bsum;                      /* per k_count block: a BlockSum (fk_engine.hip) */
+    XState *rtrue;                   /* entering state per range */
+    unsigned long long *acc_total;   /* the engine's accumulators (the feed counts into the feed accumulators) */
+    DevRes *host_res;                /* pinned, mapped */
+    XState *state;                   /* the engine's stream state (in: entering, out: exit) */
 };
 
 /* Would counting a span from state a and from state t give identical

@@ -800,6 +800,175 @@ __device__ void lds_flush(const Ctx &cx) {
     }
 }
 
+/* transfer-function wave scans (k_count's one-pass tail, k_scan) */
+__device__ __forceinline__ uint64_t shup64(uint64_t v, int d) {
+    return ((uint64_t)shup((uint32_t)(v >> 32), d) << 32) | shup((uint32_t)v, d);
+}
+__device__ __forceinline__ XState xs_shup(const XState &x, int d) {
+    return XState{shup64(x.R, d), shup64(x.code, d), shup(x.hdr, d), 0};
+}
+__device__ __forceinline__ TF tf_shup(const TF &a, int d) {
+    TF b;
+    b.c1 = xs_shup(a.c1, d);
+    b.c0 = xs_shup(a.c0, d);
+    b.nv = shup64(a.nv, d);
+    b.cs = shup64(a.cs, d);
+    b.f0_const = shup(a.f0_const, d);
+    b.pad = 0;
+    return b;
+}
+__device__ __forceinline__ TF tf_rdlane(const TF &x, int l) {
+    TF o;
+    o.c1 = XState{rdlane64(x.c1.R, l), rdlane64(x.c1.code, l), rdlane(x.c1.hdr, l), 0};
+    o.c0 = XState{rdlane64(x.c0.R, l), rdlane64(x.c0.code, l), rdlane(x.c0.hdr, l), 0};
+    o.nv = rdlane64(x.nv, l);
+    o.cs = rdlane64(x.cs, l);
+    o.f0_const = rdlane(x.f0_const, l);
+    o.pad = 0;
+    return o;
+}
+/* inclusive scan of one TF per lane across the wave */
+__device__ __forceinline__ TF tf_wave_scan(TF a) {
+    const uint32_t lane = threadIdx.x & 63;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        TF b = tf_shup(a, d);
+        if (lane >= (uint32_t)d) a = fk_compose(b, a);
+    }
+    return a;
+}
+
+__device__ __forceinline__ unsigned long long wsum64(unsigned long long v) {
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+    return v;
+}
+
+/* Copy the result block to pinned host memory, sequence number last (the
+ * host spins on it instead of a copy plus a stream synchronisation).  The
+ * whole block calls. */
+__device__ void publish_res(const DevRes *res, DevRes *host_res, uint32_t seq) {
+    __syncthreads();
+    const uint32_t *src = reinterpret_cast<const uint32_t *>(res);
+    uint32_t *dst = reinterpret_cast<uint32_t *>(host_res);
+    for (uint32_t i = threadIdx.x; i < offsetof(DevRes, seq) / 4; i += blockDim.x) dst[i] = src[i];
+    __threadfence_system();
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store(&host_res->seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+/* k_tail timeline probe (FK_EXP == 20 builds only): s_memrealtime (100 MHz)
+   at points of k_tail, max over blocks; slot 0: min at entry */
+#if FK_EXP == 20
+__device__ unsigned long long g_tp[16];
+#define TP(i) do { if (threadIdx.x == 0) atomicMax(&g_tp[i], (unsigned long long)__builtin_amdgcn_s_memrealtime()); } while (0)
+#else
+#define TP(i) do { } while (0)
+#endif
+
+/* LDS layout of k_tail's last block */
+#define TAIL_BLOCKS 16u
+#define TAIL_THREADS 512u
+
+/*
+ * One-pass feeds (LDS modes, entering state of the segment known): k_count
+ * plus k_tail do what k_resume, k_scan, k_redo and k_table_stats did in four
+ * launches, in two, and without a segment-wide scan of range states.
+ *
+ * In k_count, after its flush, wave 0 of every block (lane l = range 8b+l)
+ *  - composes its ranges' transfer functions (the block aggregate);
+ *  - checks each range's guessed entering state against the exit state of
+ *    the range before it, counted from that range's own guess.  If the
+ *    previous guess counts like the exact state, so does the exit state it
+ *    reaches (same header flag and last bases; the same run length, or both
+ *    deep in a run), so a guess equivalent to it is equivalent to the exact
+ *    state -- provided no run length in the segment reaches the reference's
+ *    int32 wrap, which k_tail checks.  By induction from range 0 (whose
+ *    guess is the exact entering state), every guess is then exact enough;
+ *  - writes a BlockSum: aggregate, first guess, last exit, flags.
+ * k_tail (16 blocks) folds the sub-tables into the table with its
+ * statistics, then its last block checks the block boundaries the same way,
+ * reduces the aggregates to the exit state, merges the accumulators and
+ * publishes the result block.  A failed check, a range that ran out of
+ * general tiles, or a segment long enough for the int32 wrap: the result
+ * block says so and the host runs k_resume / k_scan / k_redo /
+ * k_table_stats as before.
+ */
+struct BlockSum {
+    uint64_t e_R, e_code;    /* exit state of its last range, counted from that range's guess */
+    uint64_t g_code;         /* guessed entering state of its first range */
+    uint64_t nvb;            /* bytes of its first range */
+    uint64_t eof;            /* smallest 0xFF candidate (segment offset) of its ranges */
+    uint64_t nv;             /* bases of its ranges (the exit R shift, when not absorbing) */
+    uint32_t e_hdr, g_R, g_hdr;
+    uint32_t flags;          /* ONE_RESUME: a range has no transfer function yet; ONE_SCAN: a
+                                local check failed; BS_ABSORB: the exit does not depend on the
+                                block's entering state (a run break, or it enters a header) */
+};
+static_assert(sizeof(BlockSum) == 64, "BlockSums are 64 bytes");
+#define BS_ABSORB 8u
+
+/* k_count, one-pass mode: wave 0 of the block summarises its ranges (after
+ * the flush, when their RangeRecs are written). */
+__device__ __forceinline__ void block_summary(const Ctx &cx, const OnePassCfg *opc, RangeRec *rr, uint64_t nranges) {
+    const uint32_t lane = threadIdx.x & 63, b = blockIdx.x;
+    const uint64_t r = (uint64_t)b * FK_WAVES_PER_BLOCK + lane;
+    const bool mine = lane < FK_WAVES_PER_BLOCK && r < nranges;
+    TF x = fk_identity();
+    uint64_t g_code = 0, nvb = 0, eof = ~0ull;
+    uint32_t g_R = 0, g_hdr = 0;
+    bool res_here = false;
+    if (mine) {
+        const RangeRec &q = rr[r];
+        res_here = q.resume != 0;
+        if (!res_here) {
+            x = q.tf;
+            g_code = q.a_code; g_R = q.a_R; g_hdr = q.a_hdr;
+            nvb = (q.c1 - q.c0) * FK_CHUNK_BYTES;
+            if (q.eof != FK_NO_EOF64) eof = q.c0 * FK_CHUNK_BYTES + q.eof;
+        }
+    }
+    const XState g{g_R, g_code, g_hdr, 0};
+    /* the exit state each range reached from its own guess; range l's guess
+       is checked against range l-1's */
+    const XState e = fk_apply(x, g);
+    const XState e_prev = xs_shup(e, 1);
+    const bool bad = mine && lane > 0 && !fk_equiv(DState{g_code, g_R, g_hdr}, e_prev, cx.k, nvb);
+    /* a range whose transfer function is constant (a run break, or entering
+       inside a header) decides the exit state's run length */
+    const bool absorb = __ballot(mine && !res_here && x.f0_const) != 0;
+    uint64_t nv = mine ? x.nv : 0;
+#pragma unroll
+    for (int d = 4; d >= 1; d >>= 1) {
+        const uint64_t o = ((uint64_t)__shfl_xor((uint32_t)(nv >> 32), d, 64) << 32) |
+                           (uint32_t)__shfl_xor((uint32_t)nv, d, 64);
+        nv += o;
+    }
+    const uint32_t flags = (__ballot(mine && res_here) ? (uint32_t)ONE_RESUME : 0u) |
+                           (__ballot(bad) ? (uint32_t)ONE_SCAN : 0u) | (absorb ? BS_ABSORB : 0u);
+    if (mine && !res_here) opc->rtrue[r] = g;   /* equivalent to the exact state when the feed completes here */
+#pragma unroll
+    for (int d = 4; d >= 1; d >>= 1) {
+        const uint64_t o = ((uint64_t)__shfl_xor((uint32_t)(eof >> 32), d, 64) << 32) |
+                           (uint32_t)__shfl_xor((uint32_t)eof, d, 64);
+        eof = min(eof, o);
+    }
+    const uint32_t lastl = (uint32_t)min((uint64_t)FK_WAVES_PER_BLOCK, nranges - (uint64_t)b * FK_WAVES_PER_BLOCK) - 1;
+    const uint64_t el_R = rdlane64(e.R, lastl), el_code = rdlane64(e.code, lastl);
+    const uint32_t el_hdr = rdlane(e.hdr, lastl);
+    const uint64_t f_code = rdlane64(g_code, 0), f_nvb = rdlane64(nvb, 0);
+    const uint32_t f_R = rdlane(g_R, 0), f_hdr = rdlane(g_hdr, 0);
+    if (lane == 0) {
+        BlockSum *bs = reinterpret_cast<BlockSum *>(opc->bsum) + b;
+        bs->e_R = el_R; bs->e_code = el_code; bs->e_hdr = el_hdr;
+        bs->g_code = f_code; bs->g_R = f_R; bs->g_hdr = f_hdr;
+        bs->nvb = f_nvb;
+        bs->eof = eof;
+        bs->nv = nv;
+        bs->flags = flags;
+    }
+}
+
 /*
  * k_count: main pass, fast path only.  Wave w owns the chunk range
  * [w*cpw, (w+1)*cpw); its entering state is guessed from the halo before it
@@ -816,14 +985,18 @@ __global__ void __launch_bounds__(FK_BLOCK, 2)
 k_count(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint32_t *table,
         uint32_t *shortcnt, unsigned long long *acc, DevRes *res, RangeRec *rr,
         uint64_t nchunks, const XState *d_init, int has_init, uint64_t cpw, ResumeRec *resume,
-        uint32_t general_tiles, uint32_t *subs) {
+        uint32_t general_tiles, uint32_t *subs, const OnePassCfg *opc, uint32_t op_flags) {
     extern __shared__ uint32_t lds_bins[];
     /* open the feed's result block (the kernels after this one in the
        stream accumulate into it) */
     if (blockIdx.x == 0) {
-        if (threadIdx.x < 10) res->tstat[threadIdx.x] = 0;
-        if (threadIdx.x == 10) res->eof_cand = ~0ull;
-        if (threadIdx.x == 11) res->redo_n = 0;
+        if (!(op_flags & OP_ON)) {
+            if (threadIdx.x < 10) res->tstat[threadIdx.x] = 0;
+            if (threadIdx.x == 10) res->eof_cand = ~0ull;
+            if (threadIdx.x == 11) res->redo_n = 0;
+        }
+        /* one pass: k_tail writes the whole result block, and does a
+           pending reset (table = 0 + the sub-tables) */
     }
     const uint32_t nw = lds_words(HM, k);
     /* the 509-odd blocks flush their bins into FK_SUBTABLES copies of the
@@ -885,9 +1058,10 @@ k_count(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uin
     if (has) {
         DState st;
         if (c0 == 0 && has_init) {
-            st.hdr = d_init->hdr;
-            st.R = (uint32_t)d_init->R;
-            st.code = d_init->code;
+            const XState in = (op_flags & OP_FRESH) ? XState{0, 0, 0, 0} : *d_init;
+            st.hdr = in.hdr;
+            st.R = (uint32_t)in.R;
+            st.code = in.code;
         } else {
 #if FK_EXP >= 3   /* ablation: no halo guess */
             st = DState{0, 100000u, 0};
@@ -976,7 +1150,10 @@ k_count(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uin
             }
         }
     }
-    if (LDS_MODE(HM)) lds_flush<HM>(cx);
+    if (LDS_MODE(HM)) {
+        lds_flush<HM>(cx);
+        if ((op_flags & OP_ON) && threadIdx.x < 64) block_summary(cx, opc, rr, (nchunks + cpw - 1) / cpw);
+    }
 }
 #undef FK_LOADI
 #undef FK_LOADT
@@ -992,6 +1169,9 @@ k_resume(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, ui
          uint32_t *shortcnt, unsigned long long *acc, DevRes *res, RangeRec *rr, uint64_t nranges,
          const ResumeRec *resume) {
     extern __shared__ uint32_t lds_bins[];
+    /* k_scan lists the ranges to redo after this kernel (a one-pass k_count
+       that gave up may have listed some already) */
+    if (blockIdx.x == 0 && threadIdx.x == 0) res->redo_n = 0;
     const uint64_t wave = blockIdx.x * FK_WAVES_PER_BLOCK + wave_in_block();
     const bool mine = wave < nranges && rr[wave].resume;
     /* uniform per block; in the LDS modes through the first bin (before the
@@ -1389,43 +1569,6 @@ k_bucket_count(PartGeo pg, uint32_t groups, uint32_t *table) {
 #define SCAN_THREADS 256
 #define SCAN_WAVES (SCAN_THREADS / 64)
 
-__device__ __forceinline__ uint64_t shup64(uint64_t v, int d) {
-    return ((uint64_t)shup((uint32_t)(v >> 32), d) << 32) | shup((uint32_t)v, d);
-}
-__device__ __forceinline__ XState xs_shup(const XState &x, int d) {
-    return XState{shup64(x.R, d), shup64(x.code, d), shup(x.hdr, d), 0};
-}
-__device__ __forceinline__ TF tf_shup(const TF &a, int d) {
-    TF b;
-    b.c1 = xs_shup(a.c1, d);
-    b.c0 = xs_shup(a.c0, d);
-    b.nv = shup64(a.nv, d);
-    b.cs = shup64(a.cs, d);
-    b.f0_const = shup(a.f0_const, d);
-    b.pad = 0;
-    return b;
-}
-__device__ __forceinline__ TF tf_rdlane(const TF &x, int l) {
-    TF o;
-    o.c1 = XState{rdlane64(x.c1.R, l), rdlane64(x.c1.code, l), rdlane(x.c1.hdr, l), 0};
-    o.c0 = XState{rdlane64(x.c0.R, l), rdlane64(x.c0.code, l), rdlane(x.c0.hdr, l), 0};
-    o.nv = rdlane64(x.nv, l);
-    o.cs = rdlane64(x.cs, l);
-    o.f0_const = rdlane(x.f0_const, l);
-    o.pad = 0;
-    return o;
-}
-/* inclusive scan of one TF per lane across the wave */
-__device__ __forceinline__ TF tf_wave_scan(TF a) {
-    const uint32_t lane = threadIdx.x & 63;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        TF b = tf_shup(a, d);
-        if (lane >= (uint32_t)d) a = fk_compose(b, a);
-    }
-    return a;
-}
-
 __global__ void __launch_bounds__(SCAN_THREADS)
 k_scan(const RangeRec *rr, uint64_t n, XState *d_state, XState *rtrue, uint32_t *redo_list,
        DevRes *res, int k, int mode, TF *tf_total, TF *aggs, uint32_t *flags, uint32_t epoch) {
@@ -1505,19 +1648,241 @@ k_scan(const RangeRec *rr, uint64_t n, XState *d_state, XState *rtrue, uint32_t 
     if (t == 0 && eof_min != ~0ull) atomicMin(&res->eof_cand, eof_min);
 }
 
+/*
+ * k_tail (one-pass feeds, after k_count; TAIL_BLOCKS x TAIL_THREADS).  Block
+ * j takes 1/B of the table and 1/B of k_count's BlockSums:
+ *  - table bins: table = (fresh ? 0 : table) + the FK_SUBTABLES sub-tables
+ *    (zeroed), and their statistics;
+ *  - BlockSums: each block's first guess against the previous block's last
+ *    exit (the local check of block_summary, across blocks), flags, 0xFF
+ *    candidates, and for the exit state's run length the last absorbing
+ *    block (its exit R is exact) plus the bases of the blocks after it.
+ * The last block to finish combines the B partial results (a segmented
+ * reduction for the run length), merges the feed's accumulators and
+ * publishes the result block.
+ */
+struct TailPart {
+    unsigned long long st[10];   /* table statistics of the bin slice */
+    uint64_t eof;                /* smallest 0xFF candidate */
+    uint64_t Rj;                 /* exit R of the slice's last absorbing block */
+    uint64_t nv_after;           /* bases of the slice's blocks after it (all, if none) */
+    uint32_t need;               /* ONE_* bits */
+    int32_t j;                   /* the slice's last absorbing block, or -1 */
+};
+
+__device__ __forceinline__ unsigned long long wmax64s(long long v) {
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+        const long long o = (long long)(((uint64_t)__shfl_xor((uint32_t)((uint64_t)v >> 32), d, 64) << 32) |
+                                        (uint32_t)__shfl_xor((uint32_t)v, d, 64));
+        v = max(v, o);
+    }
+    return (unsigned long long)v;
+}
+
+__global__ void __launch_bounds__(TAIL_THREADS)
+k_tail(const OnePassCfg *opc, uint32_t flags, uint32_t seq, uint32_t *table, int k, uint32_t *subs,
+       unsigned long long *facc, DevRes *res, const XState *d_init, uint32_t G, uint64_t seg_len,
+       TailPart *part, uint32_t *done) {
+    __shared__ unsigned long long sh[TAIL_THREADS / 64][16];
+    __shared__ uint32_t bc[4];
+    const uint32_t t = threadIdx.x, lane = t & 63, w = t >> 6, B = gridDim.x, jb = blockIdx.x;
+    const uint32_t nbins = 1u << (2 * k);
+    const bool fresh = (flags & OP_FRESH) != 0;
+    const BlockSum *bsum = reinterpret_cast<const BlockSum *>(opc->bsum);
+#if FK_EXP == 20
+    if (t == 0) atomicMin(&g_tp[0], (unsigned long long)__builtin_amdgcn_s_memrealtime());
+#endif
+    /* every load of the slice phase first (one round trip): this block's
+       BlockSums [b0, b1) and their predecessors' exits, one per thread, and
+       its table bins with the sub-tables (bins strided over the threads) */
+    const uint32_t b0 = (uint32_t)((uint64_t)G * jb / B), b1 = (uint32_t)((uint64_t)G * (jb + 1) / B);
+    const uint32_t lo = (uint32_t)((uint64_t)nbins * jb / B), hi = (uint32_t)((uint64_t)nbins * (jb + 1) / B);
+    const uint32_t bi = b0 + t;
+    const bool hb = bi < b1;   /* G <= 2 x CUs <= B x TAIL_THREADS: one BlockSum per thread at most */
+    BlockSum bs;
+    uint64_t pe_R = 0, pe_code = 0;
+    uint32_t pe_hdr = 0;
+    if (hb) {
+        bs = bsum[bi];
+        if (bi > 0) { pe_R = bsum[bi - 1].e_R; pe_code = bsum[bi - 1].e_code; pe_hdr = bsum[bi - 1].e_hdr; }
+    }
+    const int fs = 2 * (k - 1);
+    unsigned long long v10[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    for (uint32_t i = lo + t; i < hi; i += blockDim.x) {
+        uint32_t a[FK_SUBTABLES];
+#pragma unroll
+        for (int j = 0; j < FK_SUBTABLES; j++) a[j] = subs[(size_t)j * nbins + i];
+        uint32_t v = fresh ? 0u : table[i];
+#pragma unroll
+        for (int j = 0; j < FK_SUBTABLES; j++) {
+            v += a[j];
+            if (a[j]) subs[(size_t)j * nbins + i] = 0;
+        }
+        table[i] = v;
+        v10[0] += v != 0;
+        v10[1] += v;
+        const uint32_t ld = i & 3u, fd = k == 1 ? ld : (i >> fs) & 3u;
+        v10[2] += ld == 0 ? v : 0; v10[3] += ld == 1 ? v : 0; v10[4] += ld == 2 ? v : 0; v10[5] += ld == 3 ? v : 0;
+        v10[6] += fd == 0 ? v : 0; v10[7] += fd == 1 ? v : 0; v10[8] += fd == 2 ? v : 0; v10[9] += fd == 3 ? v : 0;
+    }
+    /* BlockSum i: its first guess against block i-1's last exit (the local
+       check of block_summary, across blocks), flags, 0xFF candidate */
+    uint32_t need = 0;
+    uint64_t eof = ~0ull;
+    long long jmax = -1;
+    if (hb) {
+        need = bs.flags & (ONE_RESUME | ONE_SCAN);
+        if (bi > 0 && !fk_equiv(DState{bs.g_code, bs.g_R, bs.g_hdr}, XState{pe_R, pe_code, pe_hdr, 0}, k, bs.nvb))
+            need |= ONE_SCAN;
+        eof = bs.eof;
+        if (bs.flags & BS_ABSORB) jmax = bi;
+    }
+    /* the slice's last absorbing block, then the bases after it */
+    const long long jw = (long long)wmax64s(jmax);
+    if (lane == 0) sh[w][10] = (unsigned long long)jw;
+    __syncthreads();
+    long long js = -1;
+    for (uint32_t q = 0; q < blockDim.x / 64; q++) js = max(js, (long long)sh[q][10]);
+    uint64_t nv_after = hb && (long long)bi > js ? bs.nv : 0;
+    if (hb && (long long)bi == js) sh[0][11] = bs.e_R;   /* the owner publishes its R */
+#pragma unroll
+    for (int q = 0; q < 10; q++) v10[q] = wsum64(v10[q]);
+    nv_after = wsum64(nv_after);
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+        need |= __shfl_xor(need, d, 64);
+        const uint64_t o = ((uint64_t)__shfl_xor((uint32_t)(eof >> 32), d, 64) << 32) |
+                           (uint32_t)__shfl_xor((uint32_t)eof, d, 64);
+        eof = min(eof, o);
+    }
+    __syncthreads();
+    if (lane == 0) {
+#pragma unroll
+        for (int q = 0; q < 10; q++) sh[w][q] = v10[q];
+        sh[w][12] = nv_after;
+        sh[w][13] = need;
+        sh[w][14] = eof;
+    }
+    __syncthreads();
+    if (t < 16) {
+        unsigned long long a = t == 14 ? ~0ull : 0ull;
+        for (uint32_t q = 0; q < blockDim.x / 64; q++) {
+            const unsigned long long v = sh[q][t];
+            if (t < 10 || t == 12) a += v;
+            else if (t == 13) a |= v;
+            else if (t == 14) a = min(a, v);
+        }
+        TailPart &P = part[jb];
+        if (t < 10) P.st[t] = a;
+        if (t == 12) P.nv_after = a;
+        if (t == 13) P.need = (uint32_t)a;
+        if (t == 14) P.eof = a;
+        if (t == 15) { P.j = (int32_t)js; P.Rj = js >= 0 ? sh[0][11] : 0; }
+    }
+    TP(1);
+    /* 2. the last block to finish combines (the partials were stored by
+       wave 0, which fences them) */
+    if (w == 0) __threadfence();
+    __syncthreads();
+    if (t == 0) bc[0] = atomicAdd(done, 1u) == B - 1;
+    __syncthreads();
+    if (!bc[0]) return;
+    TP(2);
+    if (t < 64) {
+        if (t == 0) {
+            __threadfence();
+            *done = 0;
+        }
+        /* every load of the combine first: partial `lane`, the last
+           BlockSum, the entering state, the accumulators */
+        const bool have = lane < B;
+        uint32_t nd = 0;
+        uint64_t ef = ~0ull, pR = 0, pn = 0;
+        int32_t pj = -1;
+        unsigned long long st[10];
+        if (have) {
+            const TailPart P = part[lane];
+            nd = P.need; ef = P.eof; pj = P.j; pR = P.Rj; pn = P.nv_after;
+#pragma unroll
+            for (int q = 0; q < 10; q++) st[q] = P.st[q];
+        } else {
+#pragma unroll
+            for (int q = 0; q < 10; q++) st[q] = 0;
+        }
+        const BlockSum lb = bsum[G - 1];
+        const XState init = fresh ? XState{0, 0, 0, 0} : *d_init;
+        const unsigned long long fa = lane < ACC_N ? facc[lane] : 0ull;
+        const unsigned long long ta = lane < ACC_N && !fresh ? opc->acc_total[lane] : 0ull;
+#pragma unroll
+        for (int q = 0; q < 10; q++) st[q] = wsum64(st[q]);
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) {
+            nd |= __shfl_xor(nd, d, 64);
+            const uint64_t o = ((uint64_t)__shfl_xor((uint32_t)(ef >> 32), d, 64) << 32) |
+                               (uint32_t)__shfl_xor((uint32_t)ef, d, 64);
+            ef = min(ef, o);
+        }
+        /* exit run length: the last slice with an absorbing block, its R,
+           plus the bases after it */
+        const uint64_t hasj = __ballot(have && pj >= 0);
+        const int sstar = hasj ? 63 - __builtin_clzll(hasj) : -1;
+        const uint64_t add = wsum64((have && (int)lane > sstar) ? pn : 0);
+        const uint64_t base = sstar >= 0 ? rdlane64(pR, sstar) + rdlane64(pn, sstar) : init.R;
+        uint32_t need_all = nd;
+        /* no run length in the segment reaches the int32 wrap (the local
+           checks rely on it) */
+        if ((uint64_t)(uint32_t)init.R + seg_len + FK_CHUNK_BYTES > 0x7FFFFFFFull) need_all |= ONE_SCAN;
+        /* the exit state: header flag and last bases of the last block's
+           exit (identical trajectories), exact when it absorbs or holds at
+           least 32 bases; else the host path */
+        if (!(lb.flags & BS_ABSORB) && lb.nv < 32) need_all |= ONE_SCAN;
+#pragma unroll
+        for (int q = 0; q < 10; q++)
+            if (lane == (uint32_t)q) res->tstat[q] = st[q];
+        if (need_all == 0 && lane < ACC_N) {
+            const unsigned long long v = ta + fa;
+            opc->acc_total[lane] = v;
+            facc[lane] = 0;
+            res->acc[lane] = v;
+        }
+        if (lane == 0) {
+            if (need_all == 0) {
+                const uint64_t fR = base + add;
+                XState *ps = opc->state;
+                ps->R = fR; ps->code = lb.e_code; ps->hdr = lb.e_hdr; ps->pad = 0;
+                res->exit.R = fR; res->exit.code = lb.e_code; res->exit.hdr = lb.e_hdr; res->exit.pad = 0;
+            } else if (fresh) {
+                XState *ps = opc->state;   /* k_scan starts from it */
+                ps->R = 0; ps->code = 0; ps->hdr = 0; ps->pad = 0;
+            }
+            res->eof_cand = need_all ? ~0ull : ef;
+            res->redo_n = 0;
+            res->need = need_all;
+        }
+    }
+    TP(3);
+    publish_res(res, opc->host_res, seq);
+    TP(4);
+}
+
 /* One pass over the final table: distinct k-mers, total, and the first- and
  * last-base marginals (-> depth-1 trie frequencies and base composition). */
-__device__ __forceinline__ unsigned long long wsum64(unsigned long long v) {
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
-    return v;
-}
 __global__ void __launch_bounds__(256)
 k_table_stats(uint32_t *table, uint64_t n, int k, DevRes *res,
-              const unsigned long long *acc, DevRes *host_res, uint32_t *done, uint32_t seq,
-              uint32_t *subs, int nsub, unsigned long long *part) {
+              unsigned long long *acc, unsigned long long *facc, int fresh, DevRes *host_res, uint32_t *done,
+              uint32_t seq, uint32_t *subs, int nsub, unsigned long long *part) {
     unsigned long long *out = res->tstat;
-    if (blockIdx.x == 0 && threadIdx.x < ACC_N) res->acc[threadIdx.x] = acc[threadIdx.x];
+    if (blockIdx.x == 0) {
+        /* the feed's counters (facc, zero between feeds) join the engine's */
+        if (threadIdx.x < ACC_N) {
+            const unsigned long long v = (fresh ? 0ull : acc[threadIdx.x]) + facc[threadIdx.x];
+            acc[threadIdx.x] = v;
+            facc[threadIdx.x] = 0;
+            res->acc[threadIdx.x] = v;
+        }
+        if (threadIdx.x == 0) res->need = 0;
+    }
     unsigned long long dist = 0, sum = 0, last[4] = {0, 0, 0, 0}, first[4] = {0, 0, 0, 0};
     const uint64_t n4 = n / 4;
     uint4 *t4 = reinterpret_cast<uint4 *>(table);
@@ -1725,7 +2090,7 @@ __global__ void k_zero(uint32_t *table, uint64_t nbins, uint32_t *shortcnt, uint
     for (uint64_t i = i0; i < (uint64_t)nsub * nbins / 4; i += step) s4[i] = make_uint4(0, 0, 0, 0);
     for (uint64_t i = (nbins / 4) * 4 + i0; i < nbins; i += step) table[i] = 0;
     for (uint64_t i = i0; i < nshort; i += step) shortcnt[i] = 0;
-    if (i0 < ACC_N) acc[i0] = 0;
+    if (i0 < 2 * ACC_N) acc[i0] = 0;   /* engine + feed accumulators */
     if (i0 == 0) *state = XState{0, 0, 0, 0};
 }
 
@@ -1805,7 +2170,17 @@ struct fk_engine {
     /* device state */
     uint32_t *d_table = nullptr, *d_short = nullptr;
     uint32_t *d_sub = nullptr;                /* FK_SUBTABLES table copies k_count flushes into (LDS modes) */
-    unsigned long long *d_acc = nullptr;      /* ACC_N, engine lifetime */
+    unsigned long long *d_acc = nullptr;      /* ACC_N, engine lifetime (+ ACC_N: d_facc) */
+    unsigned long long *d_facc = nullptr;     /* ACC_N the counting kernels of a feed add into;
+                                                 merged into d_acc by the feed's publisher, zero between feeds */
+    /* one-pass k_count (k <= 7, entering state known) */
+    bool onepass = true;                      /* env FK_NO_ONEPASS=1: off */
+    BlockSum *d_bsum = nullptr;               /* per block of k_count */
+    uint32_t *d_ctl = nullptr;                /* k_tail's finished-block count */
+    OnePassCfg *d_opc = nullptr;
+    bool op_pending = false;                  /* the last count_segment launched a one-pass k_count */
+    bool op_fresh = false;                    /* ... which did a pending reset itself */
+    int dev_ev = 2;                           /* event that ends the last feed's device path */
     DevRes *d_res = nullptr;                  /* per feed */
     unsigned long long *d_tmp = nullptr;      /* scratch counters */
     XState *d_state = nullptr;                /* entering state of the next feed */
@@ -1869,6 +2244,17 @@ static int set_dev(fk_engine *e, bool flush = true) {
 
 extern "C" int fk_abi_version(void) { return FK_ABI_VERSION; }
 
+#if FK_EXP == 20
+/* experiment builds: read and reset the k_tail timeline probe */
+extern "C" int fk_debug_tailprof(unsigned long long *out16) {
+    if (out16 && hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_tp), sizeof(g_tp)) != hipSuccess) return FK_E_HIP;
+    unsigned long long z[16] = {};
+    z[0] = ~0ull;
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_tp), z, sizeof(z)) == hipSuccess ? FK_OK : FK_E_HIP;
+}
+#endif
+
+
 extern "C" const char *fk_strerror(int s) {
     switch (s) {
     case FK_OK: return "ok";
@@ -1929,6 +2315,7 @@ extern "C" void fk_engine_destroy(fk_engine *e) {
     hipFree(e->d_state); hipFree(e->d_rr); hipFree(e->d_rtrue);
     hipFree(e->d_redo); hipFree(e->d_tf); hipFree(e->d_stage); hipFree(e->d_resume);
     hipFree(e->d_aggs); hipFree(e->d_flags);
+    hipFree(e->d_bsum); hipFree(e->d_ctl); hipFree(e->d_opc);
     if (e->h_stage) hipHostFree(e->h_stage);
     for (int i = 0; i < 3; i++) if (e->ev[i]) hipEventDestroy(e->ev[i]);
     if (e->h_res) hipHostFree(e->h_res);
@@ -1975,6 +2362,7 @@ extern "C" int fk_engine_create(int k, const fk_opts *opts, fk_engine **out) {
         e->cus = prop.multiProcessorCount;
     if (const char *gt = getenv("FK_GENERAL_TILES")) e->general_tiles = (uint32_t)strtoul(gt, nullptr, 10);
     if (const char *ne = getenv("FK_NO_EVENTS")) e->timing = ne[0] != '1';
+    if (const char *no = getenv("FK_NO_ONEPASS")) e->onepass = no[0] != '1';
     e->nbins = 1ull << (2 * k);
 #if FK_EXP == 6   /* ablation: the partitioned path for k >= 6 */
     e->part = k >= 6 && k <= 12;
@@ -2003,7 +2391,17 @@ extern "C" int fk_engine_create(int k, const fk_opts *opts, fk_engine **out) {
         }
     }
     if (e->nshort) { ALLOC(e->d_short, e->nshort * sizeof(uint32_t)); }
-    ALLOC(e->d_acc, ACC_N * sizeof(unsigned long long));
+    ALLOC(e->d_acc, 2 * ACC_N * sizeof(unsigned long long));
+    e->d_facc = e->d_acc + ACC_N;
+    ALLOC(e->d_opc, sizeof(OnePassCfg));
+    ALLOC(e->d_ctl, 4 * sizeof(uint32_t));
+    /* the feed accumulators are zero between feeds (a fresh one-pass feed
+       does not launch k_zero) */
+    if (hipMemsetAsync(e->d_acc, 0, 2 * ACC_N * sizeof(unsigned long long), e->stream) != hipSuccess ||
+        hipMemsetAsync(e->d_ctl, 0, 4 * sizeof(uint32_t), e->stream) != hipSuccess) {
+        fk_engine_destroy(e);
+        return FK_E_HIP;
+    }
     ALLOC(e->d_res, sizeof(DevRes));
     ALLOC(e->d_tmp, 8 * sizeof(unsigned long long));
     ALLOC(e->d_state, sizeof(XState));
@@ -2057,9 +2455,9 @@ static int grow_arrays(fk_engine *e, uint64_t nranges) {
     if (nranges > e->range_cap || !e->d_rr) {
         uint64_t nr = std::max<uint64_t>(nranges, 1024);
         hipFree(e->d_rr); hipFree(e->d_rtrue); hipFree(e->d_redo); hipFree(e->d_resume);
-        hipFree(e->d_aggs); hipFree(e->d_flags);
+        hipFree(e->d_aggs); hipFree(e->d_flags); hipFree(e->d_bsum);
         e->d_rr = nullptr; e->d_rtrue = nullptr; e->d_redo = nullptr; e->d_resume = nullptr;
-        e->d_aggs = nullptr; e->d_flags = nullptr;
+        e->d_aggs = nullptr; e->d_flags = nullptr; e->d_bsum = nullptr;
         if (hipMalloc((void **)&e->d_rr, nr * sizeof(RangeRec)) != hipSuccess) return FK_E_OOM;
         if (hipMalloc((void **)&e->d_rtrue, nr * sizeof(XState)) != hipSuccess) return FK_E_OOM;
         if (hipMalloc((void **)&e->d_redo, nr * sizeof(uint32_t)) != hipSuccess) return FK_E_OOM;
@@ -2069,6 +2467,12 @@ static int grow_arrays(fk_engine *e, uint64_t nranges) {
         if (hipMalloc((void **)&e->d_flags, nb * sizeof(uint32_t) + 64) != hipSuccess) return FK_E_OOM;
         HIPCHK(hipMemsetAsync(e->d_flags, 0, nb * sizeof(uint32_t) + 64, e->stream));
         e->scan_epoch = 0;
+        const size_t nblk = nr / FK_WAVES_PER_BLOCK + 1;
+        if (hipMalloc((void **)&e->d_bsum, nblk * sizeof(BlockSum)) != hipSuccess) return FK_E_OOM;
+        OnePassCfg c;
+        c.bsum = e->d_bsum; c.rtrue = e->d_rtrue; c.acc_total = e->d_acc; c.host_res = e->h_res_dev;
+        c.state = e->d_state;
+        HIPCHK(hipMemcpy(e->d_opc, &c, sizeof c, hipMemcpyHostToDevice));
         e->range_cap = nr;
     }
     return FK_OK;
@@ -2105,15 +2509,23 @@ static Geo geometry(const fk_engine *e, uint64_t len) {
 static hipEvent_t tev(const fk_engine *e, int i) { return e->timing ? e->ev[i] : nullptr; }
 
 static int launch_count(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t lo, const Geo &g,
-                        int has_init) {
+                        int has_init, bool onepass = false, bool fresh = false) {
     size_t sh = lds_bytes(e);
+    const uint32_t flags = onepass ? (OP_ON | (fresh ? OP_FRESH : 0u)) : 0u;
     FK_DISPATCH_COUNT(e,
                 hipExtLaunchKernelGGL((k_count<HM>), dim3(g.grid), dim3(FK_BLOCK), sh, e->stream, tev(e, 0), tev(e, 1),
                                       0, buf, len, lo, e->k,
-                                   e->maskk, e->d_table, e->d_short, e->d_acc, e->d_res, e->d_rr,
+                                   e->maskk, e->d_table, e->d_short, e->d_facc, e->d_res, e->d_rr,
                                    g.nchunks, e->d_state, has_init, g.cpw, e->d_resume, e->general_tiles,
-                                   e->d_sub));
+                                   e->d_sub, e->d_opc, flags));
     HIPCHK(hipGetLastError());
+    if (onepass) {
+        if (++e->res_seq == 0) e->res_seq = 1;
+        hipExtLaunchKernelGGL(k_tail, dim3(TAIL_BLOCKS), dim3(TAIL_THREADS), 0, e->stream, nullptr, tev(e, 2), 0,
+                              e->d_opc, flags, e->res_seq, e->d_table, e->k, e->d_sub, e->d_facc, e->d_res,
+                              e->d_state, g.grid, len, reinterpret_cast<TailPart *>(e->d_tpart), e->d_ctl);
+        HIPCHK(hipGetLastError());
+    }
     return FK_OK;
 }
 
@@ -2121,7 +2533,7 @@ static int launch_resume(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t
     size_t sh = lds_bytes(e);
     FK_DISPATCH_COUNT(e,
                 hipLaunchKernelGGL((k_resume<HM>), dim3(g.grid), dim3(FK_BLOCK), sh, e->stream, buf, len, lo, e->k,
-                                   e->maskk, e->d_table, e->d_short, e->d_acc, e->d_res, e->d_rr, g.nranges,
+                                   e->maskk, e->d_table, e->d_short, e->d_facc, e->d_res, e->d_rr, g.nranges,
                                    e->d_resume));
     HIPCHK(hipGetLastError());
     return FK_OK;
@@ -2131,7 +2543,7 @@ static int launch_redo(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t l
     size_t sh = lds_bytes(e);
     FK_DISPATCH(hist_mode(e),
                 hipLaunchKernelGGL((k_redo<HM>), dim3(g.grid), dim3(FK_BLOCK), sh, e->stream, buf, len, lo, e->k,
-                                   e->maskk, e->d_table, e->d_short, e->d_acc, e->d_res, e->d_rr,
+                                   e->maskk, e->d_table, e->d_short, e->d_facc, e->d_res, e->d_rr,
                                    e->d_rtrue, e->d_redo, g.nranges, mode));
     HIPCHK(hipGetLastError());
     return FK_OK;
@@ -2153,13 +2565,14 @@ static int launch_scan(fk_engine *e, const Geo &g, int mode) {
    pinned host copy (e->h_res) with a new sequence number.  The feed path's
    k_count has zeroed the sums already; other callers ask for a memset.
    `stop` (optional) is recorded when the kernel completes. */
-static int launch_table_stats(fk_engine *e, bool zero_first, hipEvent_t stop = nullptr) {
+static int launch_table_stats(fk_engine *e, bool zero_first, hipEvent_t stop = nullptr, bool subs = true,
+                              bool fresh = false) {
     if (zero_first) HIPCHK(hipMemsetAsync(e->d_res->tstat, 0, sizeof(e->d_res->tstat), e->stream));
     unsigned gd = (unsigned)std::min<uint64_t>((uint64_t)e->cus * 4, (e->nbins / 4 + 255) / 256 + 1);
     if (++e->res_seq == 0) e->res_seq = 1;
     hipExtLaunchKernelGGL(k_table_stats, dim3(gd), dim3(256), 0, e->stream, nullptr, stop, 0, e->d_table,
-                          e->nbins, e->k, e->d_res, e->d_acc, e->h_res_dev, e->d_done, e->res_seq, e->d_sub,
-                          e->d_sub ? FK_SUBTABLES : 0, e->d_tpart);
+                          e->nbins, e->k, e->d_res, e->d_acc, e->d_facc, fresh ? 1 : 0, e->h_res_dev, e->d_done,
+                          e->res_seq, e->d_sub, (subs && e->d_sub) ? FK_SUBTABLES : 0, e->d_tpart);
     HIPCHK(hipGetLastError());
     return FK_OK;
 }
@@ -2218,7 +2631,7 @@ static int launch_part(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t l
     pg.idx = e->d_pidx;
     pg.row_base = e->d_prow;
     hipExtLaunchKernelGGL(k_part, dim3(g.grid), dim3(PART_BLOCK), 0, e->stream, tev(e, 0), tev(e, 1), 0, buf, len,
-                          lo, e->k, e->maskk, e->d_table, e->d_short, e->d_acc, e->d_res, e->d_rr, g.nchunks,
+                          lo, e->k, e->maskk, e->d_table, e->d_short, e->d_facc, e->d_res, e->d_rr, g.nchunks,
                           g.cpw, e->d_state, has_init, pg);
     HIPCHK(hipGetLastError());
     const uint32_t groups = std::max<uint32_t>(1, (uint32_t)e->cus / pg.nslices);
@@ -2230,7 +2643,38 @@ static int launch_part(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t l
 
 /* scan + redo (or the partitioned count) + table stats, then the results */
 static int resolve_and_fetch(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t lo, const Geo &g) {
-    int rc = launch_scan(e, g, 0);
+    int rc;
+    if (e->op_pending) {
+        /* a one-pass k_count published the results itself, or says what is
+           left to do */
+        e->op_pending = false;
+        rc = wait_results(e);
+        if (rc) return rc;
+        const uint32_t need = e->last.need;
+        if (need == 0) {
+            e->stats_valid = true;
+            return FK_OK;
+        }
+        if (need & ONE_RESUME) {
+            rc = launch_resume(e, buf, len, lo, g);
+            if (rc) return rc;
+        }
+        rc = launch_scan(e, g, 0);
+        if (rc) return rc;
+        rc = launch_redo(e, buf, len, lo, g, 0);
+        if (rc) return rc;
+        /* the tail folded the sub-tables already */
+        rc = launch_table_stats(e, false, tev(e, 2), false, e->op_fresh);
+        if (rc) return rc;
+        rc = wait_results(e);
+        if (rc) return rc;
+        e->stats_valid = true;
+        e->dev_ev = 2;
+        e->redo += e->last.redo_n;
+        return FK_OK;
+    }
+    e->dev_ev = 2;
+    rc = launch_scan(e, g, 0);
     if (rc) return rc;
     rc = launch_redo(e, buf, len, lo, g, 0);
     if (rc) return rc;
@@ -2303,7 +2747,8 @@ static int collect_unknown(fk_engine *e, const uint8_t *dbuf, uint64_t len, int6
 static void add_times(fk_engine *e) { e->times_pending = e->timing; }
 static void settle_times(fk_engine *e, bool wait) {
     if (!e->times_pending) return;
-    if (!wait && hipEventQuery(e->ev[2]) != hipSuccess) {
+    hipEvent_t end = e->ev[e->dev_ev];
+    if (!wait && hipEventQuery(end) != hipSuccess) {
         /* k_count's events completed long ago; the whole-path time is
            best effort here (finish() does not wait for it) */
         float a = 0;
@@ -2313,9 +2758,9 @@ static void settle_times(fk_engine *e, bool wait) {
     }
     e->times_pending = false;
     float a = 0, b = 0;
-    if (hipEventQuery(e->ev[2]) != hipSuccess) hipEventSynchronize(e->ev[2]);
+    if (hipEventQuery(end) != hipSuccess) hipEventSynchronize(end);
     if (hipEventElapsedTime(&a, e->ev[0], e->ev[1]) == hipSuccess) e->main_ms += a;
-    if (hipEventElapsedTime(&b, e->ev[0], e->ev[2]) == hipSuccess) e->dev_ms += b;
+    if (hipEventElapsedTime(&b, e->ev[0], end) == hipSuccess) e->dev_ms += b;
 }
 
 /*
@@ -2327,17 +2772,31 @@ static int count_segment(fk_engine *e, const uint8_t *dbuf, uint64_t len, int64_
     int rc = grow_arrays(e, g.nranges);
     if (rc) return rc;
     settle_times(e, true);   /* before ev[] are reused */
-    rc = flush_zero(e);      /* a pending reset, just before the first launch */
-    if (rc) return rc;
+    /* one pass (k_count resolves, folds and publishes by itself) where the
+       bins live in LDS and the entering state is known; it also does a
+       pending reset (without nodeCounter, whose short-walk counts k_count
+       adds to from every block) */
+    bool op = e->onepass && !e->part && LDS_MODE(hist_mode(e)) && has_init;
+    const bool fresh = op && e->zero_pending && !e->opts.want_nodes;
+    if (fresh) {
+        e->zero_pending = false;
+    } else {
+        rc = flush_zero(e);      /* a pending reset, just before the first launch */
+        if (rc) return rc;
+    }
+    e->op_pending = op;
+    e->op_fresh = fresh;
     if (e->part) {
         /* 8 <= k <= 12: partitioned counting (k_part + k_bucket_count) */
         rc = launch_part(e, dbuf, len, lo, g, has_init);
         if (rc) return rc;
     } else {
-        rc = launch_count(e, dbuf, len, lo, g, has_init);
+        rc = launch_count(e, dbuf, len, lo, g, has_init, op, fresh);
         if (rc) return rc;
-        rc = launch_resume(e, dbuf, len, lo, g);
-        if (rc) return rc;
+        if (!op) {
+            rc = launch_resume(e, dbuf, len, lo, g);
+            if (rc) return rc;
+        }
     }
     e->chunks += g.nchunks;
     return FK_OK;

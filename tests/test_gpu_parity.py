@@ -296,3 +296,63 @@ def test_cli_matches_reference(case, manifest, tmp_path):
     import re
     gerr = re.sub(rb"(?m)^[a-z_]+\(\): invalid pointer\n", b"", golden_file(case, "stderr"))
     assert p.stderr == gerr
+
+
+def _long_header_input(seed, n):
+    """ACGT runs with '>' lines longer than the 256-byte halo, so ranges
+    start inside a header their halo cannot see the start of (the one-pass
+    k_count's redo path), plus short lines and N runs"""
+    rng = random.Random(seed)
+    out = bytearray()
+    while len(out) < n:
+        r = rng.random()
+        if r < 0.5:
+            seq = bytes(rng.choices(b"ACGT", k=rng.randint(1000, 30000)))
+            w = rng.choice([0, 60, 80])
+            if w:
+                seq = b"\n".join(seq[i:i + w] for i in range(0, len(seq), w))
+            out += seq
+        elif r < 0.7:
+            out += b">" + bytes(rng.choices(b"ACGTN x", k=rng.randint(300, 40000))) + b"\n"
+        else:
+            out += b"N" * rng.randint(1, 600)
+    return bytes(out[:n]) + b"\n"
+
+
+@pytest.mark.parametrize("k", [2, 5, 6, 7])
+@pytest.mark.parametrize("want_nodes", [False, True])
+def test_onepass_long_headers(k, want_nodes):
+    data = _long_header_input(1000 + k, 600_000)
+    assert_same(data, k, want_nodes=want_nodes)
+
+
+@pytest.mark.parametrize("k", [3, 6, 7])
+def test_onepass_reset_reuse(k):
+    """the bench's cycle on one engine: reset, feed, finish, several times over
+    different inputs (the one-pass k_count does the pending reset itself)"""
+    inputs = [_long_header_input(7 + i, 150_000 + 40_000 * i) for i in range(3)]
+    inputs.append(bytes(random.Random(5).choices(b"ACGT", k=300_000)))
+    with fk.Engine(k) as e:
+        for rep in range(2):
+            for data in inputs:
+                e.reset()
+                e.feed(np.frombuffer(data, dtype=np.uint8).copy())
+                rc, r_g = e.finish(allow=(fk.FK_OK,))
+                t_g = e.table()
+                t_o, r_o, _ = oracle.count_dense(data, k)
+                assert np.array_equal(t_g, t_o)
+                assert r_g.windows == r_o.windows and r_g.valid_bases == r_o.valid_bases
+                assert list(r_g.base_count) == list(r_o.base_count)
+                assert r_g.distinct == r_o.distinct
+
+
+@pytest.mark.parametrize("k", [4, 6, 7])
+def test_onepass_many_headers_no_nodes(k):
+    """headers every few hundred bytes: ranges run out of general tiles (the
+    one-pass k_count's resume fallback), without nodeCounter (fresh reset)"""
+    rng = random.Random(77 + k)
+    out = bytearray()
+    while len(out) < 400_000:
+        out += b">" + bytes(rng.choices(b"ACGT xyz", k=rng.randint(5, 60))) + b"\n"
+        out += bytes(rng.choices(b"ACGT", k=rng.randint(20, 300))) + b"\n"
+    assert_same(bytes(out), k, want_nodes=False)
