@@ -52,7 +52,7 @@ class FkResult(ctypes.Structure):
                 ("chunks", ctypes.c_uint64),
                 ("redo_chunks", ctypes.c_uint64),
                 ("device_ms", ctypes.c_double),
-                ("main_kernel_ms", ctypes.c_double)]
+                ("main_kernel_ms", ctypes.c_double), ("timed_kernels", ctypes.c_uint64)]
 
     def as_dict(self):
         d = {}
@@ -65,7 +65,7 @@ class FkResult(ctypes.Structure):
 class FkOpts(ctypes.Structure):
     _fields_ = [("device", ctypes.c_int32), ("want_nodes", ctypes.c_int32),
                 ("stream", ctypes.c_void_p), ("collect_unknown", ctypes.c_int32),
-                ("reserved", ctypes.c_int32 * 7)]
+                ("timing_every", ctypes.c_int32), ("reserved", ctypes.c_int32 * 6)]
 
 
 class FkSummary(ctypes.Structure):
@@ -170,7 +170,7 @@ def _ptr(obj):
 class Engine:
     """One k-mer engine on one GPU (mirrors the findKmer() scan, :962-1069)."""
 
-    def __init__(self, k, device=-1, want_nodes=False, collect_unknown=False, stream=None):
+    def __init__(self, k, device=-1, want_nodes=False, collect_unknown=False, stream=None, timing_every=1):
         L = lib()
         self.k = k
         o = FkOpts()
@@ -178,6 +178,7 @@ class Engine:
         o.want_nodes = 1 if want_nodes else 0
         o.collect_unknown = 1 if collect_unknown else 0
         o.stream = stream
+        o.timing_every = int(timing_every)
         h = ctypes.c_void_p()
         _check(L.fk_engine_create(k, ctypes.byref(o), ctypes.byref(h)), "fk_engine_create")
         self.h = h

@@ -847,14 +847,25 @@ __device__ __forceinline__ unsigned long long wsum64(unsigned long long v) {
 /* Copy the result block to pinned host memory, sequence number last (the
  * host spins on it instead of a copy plus a stream synchronisation).  The
  * whole block calls. */
-__device__ void publish_res(const DevRes *res, DevRes *host_res, uint32_t seq) {
-    __syncthreads();
+__device__ void publish_res_wave(const DevRes *res, DevRes *host_res, uint32_t seq) {
+    /* one wave (which wrote *res itself); one system fence */
+    const uint32_t lane = threadIdx.x & 63;
     const uint32_t *src = reinterpret_cast<const uint32_t *>(res);
     uint32_t *dst = reinterpret_cast<uint32_t *>(host_res);
-    for (uint32_t i = threadIdx.x; i < offsetof(DevRes, seq) / 4; i += blockDim.x) dst[i] = src[i];
+    for (uint32_t i = lane; i < offsetof(DevRes, seq) / 4; i += 64) dst[i] = src[i];
     __threadfence_system();
-    __syncthreads();
-    if (threadIdx.x == 0) __hip_atomic_store(&host_res->seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (lane == 0) __hip_atomic_store(&host_res->seq, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__device__ __forceinline__ void keep(uint32_t v) { asm volatile("" ::"v"(v)); }
+template <typename T>
+__device__ __forceinline__ uint32_t xput(T *p, T v) {
+    /* returning exchange: the caller waits for it by keeping the result */
+    return (uint32_t)__hip_atomic_exchange(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <typename T>
+__device__ __forceinline__ T xget(const T *p) {
+    return __hip_atomic_load(const_cast<T *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 /* k_tail timeline probe (FK_EXP == 20 builds only): s_memrealtime (100 MHz)
@@ -1717,9 +1728,11 @@ k_tail(const OnePassCfg *opc, uint32_t flags, uint32_t seq, uint32_t *table, int
 #pragma unroll
         for (int j = 0; j < FK_SUBTABLES; j++) {
             v += a[j];
-            if (a[j]) subs[(size_t)j * nbins + i] = 0;
+            /* streaming stores: no dirty L2 lines for the publish's system
+               fence to write back */
+            if (a[j]) __builtin_nontemporal_store(0u, &subs[(size_t)j * nbins + i]);
         }
-        table[i] = v;
+        __builtin_nontemporal_store(v, &table[i]);
         v10[0] += v != 0;
         v10[1] += v;
         const uint32_t ld = i & 3u, fd = k == 1 ? ld : (i >> fs) & 3u;
@@ -1765,35 +1778,35 @@ k_tail(const OnePassCfg *opc, uint32_t flags, uint32_t seq, uint32_t *table, int
         sh[w][14] = eof;
     }
     __syncthreads();
-    if (t < 16) {
-        unsigned long long a = t == 14 ? ~0ull : 0ull;
-        for (uint32_t q = 0; q < blockDim.x / 64; q++) {
-            const unsigned long long v = sh[q][t];
-            if (t < 10 || t == 12) a += v;
-            else if (t == 13) a |= v;
-            else if (t == 14) a = min(a, v);
+    if (w == 0) {
+        /* the partial record, with returning exchanges (waited for before
+           the count below: no release fence) */
+        uint32_t sink = 0;
+        if (t < 16) {
+            unsigned long long a = t == 14 ? ~0ull : 0ull;
+            for (uint32_t q = 0; q < blockDim.x / 64; q++) {
+                const unsigned long long v = sh[q][t];
+                if (t < 10 || t == 12) a += v;
+                else if (t == 13) a |= v;
+                else if (t == 14) a = min(a, v);
+            }
+            TailPart &P = part[jb];
+            if (t < 10) sink = xput(&P.st[t], a);
+            if (t == 12) sink = xput(&P.nv_after, (uint64_t)a);
+            if (t == 13) sink = xput(&P.need, (uint32_t)a);
+            if (t == 14) sink = xput(&P.eof, (uint64_t)a);
+            if (t == 15) sink = xput(&P.j, (int32_t)js) | xput(&P.Rj, (uint64_t)(js >= 0 ? sh[0][11] : 0));
         }
-        TailPart &P = part[jb];
-        if (t < 10) P.st[t] = a;
-        if (t == 12) P.nv_after = a;
-        if (t == 13) P.need = (uint32_t)a;
-        if (t == 14) P.eof = a;
-        if (t == 15) { P.j = (int32_t)js; P.Rj = js >= 0 ? sh[0][11] : 0; }
+        keep(sink);
+        TP(1);
+        /* 2. the last block to finish combines */
+        if (t == 0) bc[0] = atomicAdd(done, 1u) == B - 1;
     }
-    TP(1);
-    /* 2. the last block to finish combines (the partials were stored by
-       wave 0, which fences them) */
-    if (w == 0) __threadfence();
-    __syncthreads();
-    if (t == 0) bc[0] = atomicAdd(done, 1u) == B - 1;
     __syncthreads();
     if (!bc[0]) return;
     TP(2);
     if (t < 64) {
-        if (t == 0) {
-            __threadfence();
-            *done = 0;
-        }
+        if (t == 0) *done = 0;
         /* every load of the combine first: partial `lane`, the last
            BlockSum, the entering state, the accumulators */
         const bool have = lane < B;
@@ -1802,10 +1815,10 @@ k_tail(const OnePassCfg *opc, uint32_t flags, uint32_t seq, uint32_t *table, int
         int32_t pj = -1;
         unsigned long long st[10];
         if (have) {
-            const TailPart P = part[lane];
-            nd = P.need; ef = P.eof; pj = P.j; pR = P.Rj; pn = P.nv_after;
+            const TailPart &P = part[lane];   /* device-coherent loads (other XCDs wrote them) */
+            nd = xget(&P.need); ef = xget(&P.eof); pj = xget(&P.j); pR = xget(&P.Rj); pn = xget(&P.nv_after);
 #pragma unroll
-            for (int q = 0; q < 10; q++) st[q] = P.st[q];
+            for (int q = 0; q < 10; q++) st[q] = xget(&P.st[q]);
         } else {
 #pragma unroll
             for (int q = 0; q < 10; q++) st[q] = 0;
@@ -1860,9 +1873,9 @@ k_tail(const OnePassCfg *opc, uint32_t flags, uint32_t seq, uint32_t *table, int
             res->redo_n = 0;
             res->need = need_all;
         }
+        TP(3);
+        publish_res_wave(res, opc->host_res, seq);
     }
-    TP(3);
-    publish_res(res, opc->host_res, seq);
     TP(4);
 }
 
@@ -2214,6 +2227,10 @@ struct fk_engine {
     uint64_t shard_len = 0;
     int64_t shard_lo = 0;
     double dev_ms = 0, main_ms = 0;
+    uint64_t timed_n = 0;                     /* launches main_ms covers */
+    uint64_t launch_no = 0;                   /* counting launches, for timing_every */
+    uint32_t timing_every = 1;
+    bool cur_timed = true;                    /* the current feed's launches record events */
     std::vector<uint8_t> unknown_bytes;
 };
 
@@ -2302,6 +2319,7 @@ static int zero_all(fk_engine *e) {
     e->ended = 0;
     e->shard_pending = 0;
     e->dev_ms = e->main_ms = 0;
+    e->timed_n = 0;
     e->unknown_bytes.clear();
     return FK_OK;
 }
@@ -2363,6 +2381,7 @@ extern "C" int fk_engine_create(int k, const fk_opts *opts, fk_engine **out) {
     if (const char *gt = getenv("FK_GENERAL_TILES")) e->general_tiles = (uint32_t)strtoul(gt, nullptr, 10);
     if (const char *ne = getenv("FK_NO_EVENTS")) e->timing = ne[0] != '1';
     if (const char *no = getenv("FK_NO_ONEPASS")) e->onepass = no[0] != '1';
+    if (e->opts.timing_every > 1) e->timing_every = (uint32_t)e->opts.timing_every;
     e->nbins = 1ull << (2 * k);
 #if FK_EXP == 6   /* ablation: the partitioned path for k >= 6 */
     e->part = k >= 6 && k <= 12;
@@ -2506,7 +2525,7 @@ static Geo geometry(const fk_engine *e, uint64_t len) {
     else FK_DISPATCH(hist_mode(e), __VA_ARGS__)
 
 /* the timing events of a launch (none when timing is off) */
-static hipEvent_t tev(const fk_engine *e, int i) { return e->timing ? e->ev[i] : nullptr; }
+static hipEvent_t tev(const fk_engine *e, int i) { return e->timing && e->cur_timed ? e->ev[i] : nullptr; }
 
 static int launch_count(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t lo, const Geo &g,
                         int has_init, bool onepass = false, bool fresh = false) {
@@ -2744,7 +2763,7 @@ static int collect_unknown(fk_engine *e, const uint8_t *dbuf, uint64_t len, int6
    device path (ev0 -> ev2, at the end of k_table_stats).  The host continues
    as soon as the result block is published, so ev2 may still be pending: it
    is read when the events are about to be reused, or at finish. */
-static void add_times(fk_engine *e) { e->times_pending = e->timing; }
+static void add_times(fk_engine *e) { e->times_pending = e->timing && e->cur_timed; }
 static void settle_times(fk_engine *e, bool wait) {
     if (!e->times_pending) return;
     hipEvent_t end = e->ev[e->dev_ev];
@@ -2752,14 +2771,14 @@ static void settle_times(fk_engine *e, bool wait) {
         /* k_count's events completed long ago; the whole-path time is
            best effort here (finish() does not wait for it) */
         float a = 0;
-        if (hipEventElapsedTime(&a, e->ev[0], e->ev[1]) == hipSuccess) e->main_ms += a;
+        if (hipEventElapsedTime(&a, e->ev[0], e->ev[1]) == hipSuccess) { e->main_ms += a; e->timed_n++; }
         e->times_pending = false;
         return;
     }
     e->times_pending = false;
     float a = 0, b = 0;
     if (hipEventQuery(end) != hipSuccess) hipEventSynchronize(end);
-    if (hipEventElapsedTime(&a, e->ev[0], e->ev[1]) == hipSuccess) e->main_ms += a;
+    if (hipEventElapsedTime(&a, e->ev[0], e->ev[1]) == hipSuccess) { e->main_ms += a; e->timed_n++; }
     if (hipEventElapsedTime(&b, e->ev[0], end) == hipSuccess) e->dev_ms += b;
 }
 
@@ -2772,6 +2791,7 @@ static int count_segment(fk_engine *e, const uint8_t *dbuf, uint64_t len, int64_
     int rc = grow_arrays(e, g.nranges);
     if (rc) return rc;
     settle_times(e, true);   /* before ev[] are reused */
+    e->cur_timed = (e->launch_no++ % e->timing_every) == 0;
     /* one pass (k_count resolves, folds and publishes by itself) where the
        bins live in LDS and the entering state is known; it also does a
        pending reset (without nodeCounter, whose short-walk counts k_count
@@ -3028,6 +3048,7 @@ extern "C" int fk_engine_finish(fk_engine *e, fk_result *res) {
     res->redo_chunks = e->redo;
     res->device_ms = e->dev_ms;
     res->main_kernel_ms = e->main_ms;
+    res->timed_kernels = e->timed_n;
     uint64_t any_walk = res->depth1[0] | res->depth1[1] | res->depth1[2] | res->depth1[3];
     if (e->opts.want_nodes) {
         /* nodeCounter = head + distinct prefixes of every walk (:620) */
@@ -3176,6 +3197,7 @@ extern "C" int fk_engine_merge_from(fk_engine *dst, fk_engine *src) {
     dst->redo += src->redo;
     dst->dev_ms += src->dev_ms;
     dst->main_ms += src->main_ms;
+    dst->timed_n += src->timed_n;
     return FK_OK;
 }
 

@@ -87,7 +87,8 @@ typedef struct {
     uint64_t chunks;          /* 64 KiB scan chunks processed */
     uint64_t redo_chunks;     /* chunks re-counted after the state scan */
     double   device_ms;       /* HIP-event time of all scan kernels */
-    double   main_kernel_ms;  /* HIP-event time of the main count kernel */
+    double   main_kernel_ms;  /* HIP-event time of the main count kernel ... */
+    uint64_t timed_kernels;   /* ... over this many launches (see fk_opts.timing_every) */
 } fk_result;
 
 typedef struct {
@@ -97,7 +98,9 @@ typedef struct {
                                  blocking stream (orders after the device's
                                  legacy default stream) */
     int32_t collect_unknown;  /* keep the unknown bytes for stderr replay */
-    int32_t reserved[7];
+    int32_t timing_every;     /* time the count kernel with HIP events on every
+                                 Nth launch (0 or 1: every launch) */
+    int32_t reserved[6];
 } fk_opts;
 
 typedef struct fk_engine fk_engine;
