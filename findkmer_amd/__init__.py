@@ -28,6 +28,7 @@ FK_E_EMPTY = -6
 FK_E_UNTERMINATED_HEADER = -7
 FK_E_ROLLOVER = -8
 FK_E_STATE = -9
+FK_E_SUMMARY = -12
 FK_K_MAX_DENSE = 16
 
 
@@ -87,6 +88,7 @@ SIGNATURES = [
     ("fk_engine_feed", ctypes.c_int, [_P, _P, ctypes.c_uint64, ctypes.c_int]),
     ("fk_engine_feed_shard", ctypes.c_int, [_P, _P, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int]),
     ("fk_engine_summary", ctypes.c_int, [_P, ctypes.POINTER(FkSummary)]),
+    ("fk_engine_summary_full", ctypes.c_int, [_P, ctypes.POINTER(FkSummary)]),
     ("fk_summary_apply", ctypes.c_int, [ctypes.POINTER(FkSummary), ctypes.POINTER(FkState), ctypes.POINTER(FkState)]),
     ("fk_engine_resolve", ctypes.c_int, [_P, ctypes.POINTER(FkState)]),
     ("fk_engine_finish", ctypes.c_int, [_P, ctypes.POINTER(FkResult)]),
@@ -212,6 +214,11 @@ class Engine:
     def summary(self):
         s = FkSummary()
         _check(lib().fk_engine_summary(self.h, ctypes.byref(s)), "summary")
+        return s
+
+    def summary_full(self):
+        s = FkSummary()
+        _check(lib().fk_engine_summary_full(self.h, ctypes.byref(s)), "summary_full")
         return s
 
     def resolve(self, state):

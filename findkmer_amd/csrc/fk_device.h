@@ -197,6 +197,18 @@ struct ResumeRec {
     Facts f;             /* facts of the range so far */
 };
 
+/* A shard counted in one pass (k_tail): its effect on the scan state, valid
+ * for an entering state equivalent to its first range's guess (fk_equiv) and
+ * far enough from the int32 wrap (the host checks both at resolve). */
+struct ShardSum {
+    uint64_t g_code;                /* the first range's guessed entering state */
+    uint32_t g_R, g_hdr;
+    uint64_t nvb0;                  /* bytes of the first range */
+    uint64_t c_R, c_code;           /* absorb: the exit state; else a shift by nv bases ending in c_code */
+    uint32_t c_hdr, absorb;
+    uint64_t nv;
+};
+
 /* Per-feed results, fetched with one device-to-host copy. */
 struct DevRes {
     unsigned long long tstat[10];   /* k_table_stats: distinct, sum, last[4], first[4] */
@@ -207,6 +219,8 @@ struct DevRes {
     uint32_t need;                  /* one-pass k_count: 0 = complete, else ONE_* bits
                                        (the host runs the rest of the path) */
     uint32_t pad;
+    ShardSum shard;                 /* one-pass shard feeds */
+    uint32_t pad2;
     uint32_t seq;                   /* host copy: written last (feed sequence number) */
 };
 
@@ -218,7 +232,8 @@ enum { ONE_SCAN = 1u,     /* a guess check failed (or could not be made): k_scan
  * device memory: k_count takes a pointer to it plus one flag word, so its
  * counting loop carries no extra kernel arguments. */
 enum { OP_ON = 1u,        /* one pass: k_count summarises its blocks, k_tail finishes */
-       OP_FRESH = 2u };   /* a reset is pending: zero table, state and accumulators */
+       OP_FRESH = 2u,     /* a reset is pending: zero table, state and accumulators */
+       OP_SHARD = 4u };   /* a shard: the entering state is the first guess until resolved */
 struct OnePassCfg {
     void *bsum;                      /* per k_count block: a BlockSum (fk_engine.hip) */
     XState *rtrue;                   /* entering state per range */

@@ -1824,7 +1824,12 @@ k_tail(const OnePassCfg *opc, uint32_t flags, uint32_t seq, uint32_t *table, int
             for (int q = 0; q < 10; q++) st[q] = 0;
         }
         const BlockSum lb = bsum[G - 1];
-        const XState init = fresh ? XState{0, 0, 0, 0} : *d_init;
+        /* a shard's entering state is unknown: count from its first guess
+           (the host checks it against the stitched state at resolve) */
+        const bool shard = (flags & OP_SHARD) != 0;
+        const BlockSum b0s = bsum[0];
+        const XState init = shard ? XState{b0s.g_R, b0s.g_code, b0s.g_hdr, 0}
+                                  : fresh ? XState{0, 0, 0, 0} : *d_init;
         const unsigned long long fa = lane < ACC_N ? facc[lane] : 0ull;
         const unsigned long long ta = lane < ACC_N && !fresh ? opc->acc_total[lane] : 0ull;
 #pragma unroll
@@ -1845,7 +1850,7 @@ k_tail(const OnePassCfg *opc, uint32_t flags, uint32_t seq, uint32_t *table, int
         uint32_t need_all = nd;
         /* no run length in the segment reaches the int32 wrap (the local
            checks rely on it) */
-        if ((uint64_t)(uint32_t)init.R + seg_len + FK_CHUNK_BYTES > 0x7FFFFFFFull) need_all |= ONE_SCAN;
+        if (!shard && (uint64_t)(uint32_t)init.R + seg_len + FK_CHUNK_BYTES > 0x7FFFFFFFull) need_all |= ONE_SCAN;
         /* the exit state: header flag and last bases of the last block's
            exit (identical trajectories), exact when it absorbs or holds at
            least 32 bases; else the host path */
@@ -1872,6 +1877,15 @@ k_tail(const OnePassCfg *opc, uint32_t flags, uint32_t seq, uint32_t *table, int
             res->eof_cand = need_all ? ~0ull : ef;
             res->redo_n = 0;
             res->need = need_all;
+            if (shard) {
+                ShardSum &ss = res->shard;
+                ss.g_code = b0s.g_code; ss.g_R = b0s.g_R; ss.g_hdr = b0s.g_hdr;
+                ss.nvb0 = b0s.nvb;
+                ss.absorb = sstar >= 0;
+                ss.c_R = sstar >= 0 ? base + add : 0;
+                ss.nv = add;
+                ss.c_code = lb.e_code; ss.c_hdr = lb.e_hdr;
+            }
         }
         TP(3);
         publish_res_wave(res, opc->host_res, seq);
@@ -2193,6 +2207,8 @@ struct fk_engine {
     OnePassCfg *d_opc = nullptr;
     bool op_pending = false;                  /* the last count_segment launched a one-pass k_count */
     bool op_fresh = false;                    /* ... which did a pending reset itself */
+    /* a shard counted in one pass: its k_tail result (compact summary) */
+    bool shard_op = false, shard_waited = false, shard_full = false, shard_resumed = false;
     int dev_ev = 2;                           /* event that ends the last feed's device path */
     DevRes *d_res = nullptr;                  /* per feed */
     unsigned long long *d_tmp = nullptr;      /* scratch counters */
@@ -2286,6 +2302,7 @@ extern "C" const char *fk_strerror(int s) {
     case FK_E_STATE: return "engine API called out of order";
     case FK_E_IO: return "I/O error";
     case FK_E_RCCL: return "collective failed";
+    case FK_E_SUMMARY: return "shard summary does not apply to this state (exchange the full summaries)";
     default: return "unknown error";
     }
 }
@@ -2528,9 +2545,9 @@ static Geo geometry(const fk_engine *e, uint64_t len) {
 static hipEvent_t tev(const fk_engine *e, int i) { return e->timing && e->cur_timed ? e->ev[i] : nullptr; }
 
 static int launch_count(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t lo, const Geo &g,
-                        int has_init, bool onepass = false, bool fresh = false) {
+                        int has_init, bool onepass = false, bool fresh = false, bool shard = false) {
     size_t sh = lds_bytes(e);
-    const uint32_t flags = onepass ? (OP_ON | (fresh ? OP_FRESH : 0u)) : 0u;
+    const uint32_t flags = onepass ? (OP_ON | (fresh ? OP_FRESH : 0u) | (shard ? OP_SHARD : 0u)) : 0u;
     FK_DISPATCH_COUNT(e,
                 hipExtLaunchKernelGGL((k_count<HM>), dim3(g.grid), dim3(FK_BLOCK), sh, e->stream, tev(e, 0), tev(e, 1),
                                       0, buf, len, lo, e->k,
@@ -2786,7 +2803,8 @@ static void settle_times(fk_engine *e, bool wait) {
  * Count one device-resident segment whose entering state is *d_state (exact).
  * has_init = 0 is the shard case (entering state unknown; resolved later).
  */
-static int count_segment(fk_engine *e, const uint8_t *dbuf, uint64_t len, int64_t lo, int has_init, Geo &g) {
+static int count_segment(fk_engine *e, const uint8_t *dbuf, uint64_t len, int64_t lo, int has_init, Geo &g,
+                         bool shard = false) {
     g = geometry(e, len);
     int rc = grow_arrays(e, g.nranges);
     if (rc) return rc;
@@ -2796,7 +2814,7 @@ static int count_segment(fk_engine *e, const uint8_t *dbuf, uint64_t len, int64_
        bins live in LDS and the entering state is known; it also does a
        pending reset (without nodeCounter, whose short-walk counts k_count
        adds to from every block) */
-    bool op = e->onepass && !e->part && LDS_MODE(hist_mode(e)) && has_init;
+    bool op = e->onepass && !e->part && LDS_MODE(hist_mode(e)) && (has_init || shard);
     const bool fresh = op && e->zero_pending && !e->opts.want_nodes;
     if (fresh) {
         e->zero_pending = false;
@@ -2811,7 +2829,7 @@ static int count_segment(fk_engine *e, const uint8_t *dbuf, uint64_t len, int64_
         rc = launch_part(e, dbuf, len, lo, g, has_init);
         if (rc) return rc;
     } else {
-        rc = launch_count(e, dbuf, len, lo, g, has_init, op, fresh);
+        rc = launch_count(e, dbuf, len, lo, g, has_init, op, fresh, shard);
         if (rc) return rc;
         if (!op) {
             rc = launch_resume(e, dbuf, len, lo, g);
@@ -2932,29 +2950,91 @@ extern "C" int fk_engine_feed_shard(fk_engine *e, const uint8_t *buf, uint64_t l
     if (e->fed || e->shard_pending) return FK_E_STATE;
     if (len > SEG_MAX_BYTES || ((uintptr_t)buf & 15) || (halo & 15)) return FK_E_INVALID;
     if (len && len < FK_LANE_BYTES) return FK_E_INVALID;   /* shards are at least one lane */
-    int rc = set_dev(e);
+    int rc = set_dev(e, false);
     if (rc) return rc;
     e->fed = len;
     e->shard_buf = buf;
     e->shard_len = len;
     e->shard_lo = -(int64_t)std::min<uint64_t>(halo, FK_HALO_BYTES);
     e->shard_pending = 1;
-    if (len == 0) return FK_OK;
+    e->shard_op = e->shard_waited = e->shard_full = e->shard_resumed = false;
+    if (len == 0) return flush_zero(e);
     Geo g;
-    rc = count_segment(e, buf, len, e->shard_lo, 0, g);
+    rc = count_segment(e, buf, len, e->shard_lo, 0, g, true);
     if (rc) return rc;
-    rc = launch_scan(e, g, 1);
+    if (e->op_pending) {
+        /* one pass: k_tail publishes a compact summary (fetched lazily) */
+        e->op_pending = false;
+        e->shard_op = true;
+        return FK_OK;
+    }
+    return launch_scan(e, g, 1);
+}
+
+/* the one-pass shard's result block (once) */
+static int shard_wait(fk_engine *e) {
+    if (!e->shard_op || e->shard_waited) return FK_OK;
+    int rc = wait_results(e);
     if (rc) return rc;
+    e->shard_waited = true;
     return FK_OK;
 }
 
+/* the full transfer function of a one-pass shard (k_resume if a range ran
+   out of general tiles, then k_scan mode 1) into d_tf */
+static int shard_full_tf(fk_engine *e) {
+    if (!e->shard_op || e->shard_full) return FK_OK;
+    int rc = shard_wait(e);
+    if (rc) return rc;
+    const Geo g = geometry(e, e->shard_len);
+    if ((e->last.need & ONE_RESUME) && !e->shard_resumed) {
+        rc = launch_resume(e, e->shard_buf, e->shard_len, e->shard_lo, g);
+        if (rc) return rc;
+        e->shard_resumed = true;
+    }
+    rc = launch_scan(e, g, 1);
+    if (rc) return rc;
+    e->shard_full = true;
+    return FK_OK;
+}
+
+#define FK_SUMMARY_COMPACT 0x434F4D50414354ull   /* "COMPACT": tag in w[11] */
+
 extern "C" int fk_engine_summary(fk_engine *e, fk_summary *out) {
     if (!e || !out) return FK_E_INVALID;
-    static_assert(sizeof(TF) <= sizeof(fk_summary), "summary too small");
+    static_assert(sizeof(TF) <= sizeof(fk_summary) - 8, "summary too small");
+    memset(out, 0, sizeof *out);
+    if (e->shard_pending && e->shard_len && e->shard_op && !e->shard_full) {
+        int rc = set_dev(e);
+        if (rc) return rc;
+        rc = shard_wait(e);
+        if (rc) return rc;
+        if (e->last.need == 0) {
+            const ShardSum &ss = e->last.shard;
+            out->w[0] = ss.g_code;
+            out->w[1] = (uint64_t)ss.g_R | ((uint64_t)ss.g_hdr << 32);
+            out->w[2] = ss.nvb0;
+            out->w[3] = ss.c_R;
+            out->w[4] = ss.c_code;
+            out->w[5] = (uint64_t)ss.c_hdr | ((uint64_t)ss.absorb << 32);
+            out->w[6] = ss.nv;
+            out->w[7] = e->shard_len;
+            out->w[8] = (uint64_t)e->k;
+            out->w[11] = FK_SUMMARY_COMPACT;
+            return FK_OK;
+        }
+    }
+    return fk_engine_summary_full(e, out);
+}
+
+extern "C" int fk_engine_summary_full(fk_engine *e, fk_summary *out) {
+    if (!e || !out) return FK_E_INVALID;
     memset(out, 0, sizeof *out);
     TF t = fk_identity();
     if (e->shard_pending && e->shard_len) {
         int rc = set_dev(e);
+        if (rc) return rc;
+        rc = shard_full_tf(e);
         if (rc) return rc;
         HIPCHK(hipMemcpyAsync(&t, e->d_tf, sizeof t, hipMemcpyDeviceToHost, e->stream));
         HIPCHK(hipStreamSynchronize(e->stream));
@@ -2963,12 +3043,35 @@ extern "C" int fk_engine_summary(fk_engine *e, fk_summary *out) {
     return FK_OK;
 }
 
+/* A compact summary applied to an entering state (false: it does not apply:
+   the state would count the shard's first range differently from its guess,
+   or a run could reach the int32 wrap, which its local checks exclude). */
+static bool compact_apply(const fk_summary *s, const XState &in, XState &out) {
+    const DState g{s->w[0], (uint32_t)s->w[1], (uint32_t)(s->w[1] >> 32)};
+    const int k = (int)s->w[8];
+    if (!fk_equiv(g, in, k, s->w[2])) return false;
+    if (!in.hdr && (uint64_t)(uint32_t)in.R + s->w[7] + FK_CHUNK_BYTES > 0x7FFFFFFFull) return false;
+    const uint32_t c_hdr = (uint32_t)s->w[5], absorb = (uint32_t)(s->w[5] >> 32);
+    if (absorb) {
+        out = XState{s->w[3], s->w[4], c_hdr, 0};
+    } else {
+        /* no run break and no header in the shard: a shift */
+        out = XState{in.R + s->w[6], fk_join(in.code, s->w[4], s->w[6]), c_hdr, 0};
+    }
+    return true;
+}
+
 extern "C" int fk_summary_apply(const fk_summary *s, const fk_state *in, fk_state *out) {
     if (!s || !in || !out) return FK_E_INVALID;
-    TF t;
-    memcpy(&t, s, sizeof t);
     XState x{in->run, fk_sigma(in->code), in->hdr, 0};
-    XState y = fk_apply(t, x);
+    XState y;
+    if (s->w[11] == FK_SUMMARY_COMPACT) {
+        if (!compact_apply(s, x, y)) return FK_E_SUMMARY;
+    } else {
+        TF t;
+        memcpy(&t, s, sizeof t);
+        y = fk_apply(t, x);
+    }
     out->run = y.R;
     out->code = fk_sigma(y.code);
     out->hdr = y.hdr;
@@ -2984,12 +3087,53 @@ extern "C" int fk_engine_resolve(fk_engine *e, const fk_state *entering) {
     XState in{entering->run, fk_sigma(entering->code), entering->hdr, 0};
     e->shard_pending = 0;
     e->state = in;
-    HIPCHK(hipMemcpyAsync(e->d_state, &in, sizeof in, hipMemcpyHostToDevice, e->stream));
     if (e->shard_len == 0) {
+        HIPCHK(hipMemcpyAsync(e->d_state, &in, sizeof in, hipMemcpyHostToDevice, e->stream));
         HIPCHK(hipStreamSynchronize(e->stream));
         return FK_OK;
     }
     Geo g = geometry(e, e->shard_len);
+    if (e->shard_op) {
+        rc = shard_wait(e);
+        if (rc) return rc;
+        if (e->last.need == 0 && !e->shard_full) {
+            fk_summary s;
+            rc = fk_engine_summary(e, &s);
+            if (rc) return rc;
+            XState ex;
+            if (compact_apply(&s, in, ex)) {
+                /* the guessed states count exactly: nothing to recount */
+                e->last.exit = ex;
+                HIPCHK(hipMemcpyAsync(e->d_state, &ex, sizeof ex, hipMemcpyHostToDevice, e->stream));
+                e->stats_valid = true;
+                return finish_segment(e, e->shard_buf, e->shard_len, e->shard_lo, g, in);
+            }
+        }
+        /* the multi-launch path from the exact entering state: k_scan lists
+           the ranges whose guess counts differently, k_redo recounts them */
+        if ((e->last.need & ONE_RESUME) && !e->shard_resumed) {
+            rc = launch_resume(e, e->shard_buf, e->shard_len, e->shard_lo, g);
+            if (rc) return rc;
+            e->shard_resumed = true;
+        }
+        HIPCHK(hipMemcpyAsync(e->d_state, &in, sizeof in, hipMemcpyHostToDevice, e->stream));
+        HIPCHK(hipMemsetAsync(&e->d_res->redo_n, 0, sizeof(uint32_t), e->stream));
+        HIPCHK(hipMemsetAsync(&e->d_res->eof_cand, 0xFF, sizeof(unsigned long long), e->stream));
+        rc = launch_scan(e, g, 0);
+        if (rc) return rc;
+        rc = launch_redo(e, e->shard_buf, e->shard_len, e->shard_lo, g, 0);
+        if (rc) return rc;
+        /* k_tail folded the sub-tables, and merged the feed's counters if
+           it published a complete result */
+        rc = launch_table_stats(e, false, tev(e, 2), false, e->op_fresh && e->last.need != 0);
+        if (rc) return rc;
+        rc = wait_results(e);
+        if (rc) return rc;
+        e->stats_valid = true;
+        e->redo += e->last.redo_n;
+        return finish_segment(e, e->shard_buf, e->shard_len, e->shard_lo, g, in);
+    }
+    HIPCHK(hipMemcpyAsync(e->d_state, &in, sizeof in, hipMemcpyHostToDevice, e->stream));
     rc = resolve_and_fetch(e, e->shard_buf, e->shard_len, e->shard_lo, g);
     if (rc) return rc;
     return finish_segment(e, e->shard_buf, e->shard_len, e->shard_lo, g, in);

@@ -4,10 +4,13 @@ One process per GPU.  Each rank owns a contiguous byte range of the stream
 (plus up to 256 bytes of halo before it) and counts it with guessed entry
 states (fk_engine_feed_shard).  The path has exactly two exchange steps:
 
-1. state stitch: all-gather the 96-byte shard summaries (the shard's scan
-   transfer function, fk_engine_summary) and compose those of the ranks
-   before this one (fk_summary_apply) -> the exact entering state, handed to
-   fk_engine_resolve, which recounts only what the guess got wrong;
+1. state stitch: all-gather the 96-byte shard summaries (fk_engine_summary:
+   for a shard counted in one pass, a compact summary valid for entering
+   states equivalent to the shard's guessed entry; else the full transfer
+   function) and compose them in rank order (fk_summary_apply) -> the exact
+   entering state, handed to fk_engine_resolve, which recounts only what the
+   guess got wrong (nothing, when the compact summaries applied).  If one
+   does not apply, all ranks exchange the full summaries in a second round;
 2. table merge: one all-reduce of the 4^k count tables.  Counts are u32 in
    the reference (findKmer.cpp:110); int32 sums are bitwise identical.
 
@@ -17,7 +20,7 @@ and over gloo on the CPU (tests/test_dist_cpu.py).
 import torch
 import torch.distributed as dist
 
-from . import FkState, FkSummary, summary_apply
+from . import FK_E_SUMMARY, FindKmerError, FkState, FkSummary, summary_apply
 
 SUMMARY_WORDS = 12
 _U64 = 1 << 64
@@ -28,22 +31,32 @@ def _to_i64(v):
 
 
 def stitch_entry_state(summary_words, group=None, device=None):
-    """All-gather every rank's shard summary (12 u64 words) and compose the
-    summaries of the ranks before this one, starting from the stream's
-    initial state.  Returns the exact entering state (FkState) of this rank's
-    shard."""
+    """All-gather every rank's shard summary (12 u64 words) and compose them
+    in rank order from the stream's initial state.  Returns the exact
+    entering state (FkState) of this rank's shard, or None when some rank's
+    compact summary does not apply to the state entering it (its shard's
+    guessed entry would count differently): then every rank sees the same
+    failure and the caller exchanges the full summaries instead."""
     rank = dist.get_rank(group)
     world = dist.get_world_size(group)
     mine = torch.tensor([_to_i64(int(w)) for w in summary_words], dtype=torch.int64, device=device)
     everyone = [torch.empty_like(mine) for _ in range(world)]
     dist.all_gather(everyone, mine, group=group)
     state = FkState()
-    for r in range(rank):
+    entering = None
+    for r in range(world):
+        if r == rank:
+            entering = state
         s = FkSummary()
         for i, v in enumerate(everyone[r].tolist()):
             s.w[i] = v % _U64
-        state = summary_apply(s, state)
-    return state
+        try:
+            state = summary_apply(s, state)
+        except FindKmerError as err:
+            if err.code != FK_E_SUMMARY:
+                raise
+            return None
+    return entering
 
 
 def sum_tables(table, group=None):
@@ -62,6 +75,10 @@ def count_sharded(engine, ptr, nbytes, halo, table, group=None):
     the CSV come from the merged table."""
     engine.feed_shard_device(ptr, nbytes, halo)
     state = stitch_entry_state(list(engine.summary().w), group, table.device)
+    if state is None:
+        # a compact summary did not apply somewhere: the full transfer
+        # functions (every rank takes this branch together)
+        state = stitch_entry_state(list(engine.summary_full().w), group, table.device)
     engine.resolve(state)
     if table.is_cuda:
         engine.table_to_device(table.data_ptr())

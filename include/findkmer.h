@@ -54,7 +54,10 @@ enum {
                                    COUNTER ROLLOVER and exits (:642-648) */
     FK_E_STATE = -9,            /* API called out of order */
     FK_E_IO = -10,              /* host file I/O failed */
-    FK_E_RCCL = -11             /* a collective failed */
+    FK_E_RCCL = -11,            /* a collective failed */
+    FK_E_SUMMARY = -12          /* a compact shard summary does not apply to
+                                   this entering state: exchange the full ones
+                                   (fk_engine_summary_full) */
 };
 
 /* Scan state carried between byte ranges (exact; used for streaming feeds and
@@ -126,13 +129,18 @@ int  fk_engine_feed(fk_engine *e, const uint8_t *buf, uint64_t len,
 /* Shard entry (multi-GPU): feed bytes whose entering state is not known yet.
  * `halo` bytes immediately preceding buf (may be 0) are used to guess it;
  * fk_engine_resolve() later supplies the true entering state and re-counts
- * the chunks the guess got wrong.  fk_engine_summary() returns the
- * transfer function of everything fed so far as an opaque blob (fk_summary)
- * that the caller exchanges between shards. */
+ * what the guess got wrong.  fk_engine_summary() returns the shard's effect
+ * on the scan state as an opaque blob (fk_summary) that the caller exchanges
+ * between shards: for a shard counted in one pass, a compact summary valid
+ * for entering states equivalent to the shard's guess (fk_summary_apply then
+ * returns FK_E_SUMMARY for any other state); otherwise, or from
+ * fk_engine_summary_full(), the full transfer function, which applies to
+ * every state. */
 typedef struct { uint64_t w[12]; } fk_summary;
 int  fk_engine_feed_shard(fk_engine *e, const uint8_t *buf, uint64_t len,
                           uint64_t halo, int on_device);
 int  fk_engine_summary(fk_engine *e, fk_summary *out);
+int  fk_engine_summary_full(fk_engine *e, fk_summary *out);
 int  fk_summary_apply(const fk_summary *s, const fk_state *in, fk_state *out);
 int  fk_engine_resolve(fk_engine *e, const fk_state *entering);
 

@@ -89,3 +89,53 @@ def test_cli_k_out_of_range_message():
     p = subprocess.run([os.path.join(REPO, "findKmer"), "-k", "21"], capture_output=True, text=True)
     assert p.returncode == 1
     assert "21 is not a valid value for k.\nPlease select a number greater than zero and less than 21\n" in p.stderr
+
+
+COMPACT = 0x434F4D50414354   # "COMPACT" tag of a one-pass shard summary (fk_engine.hip)
+
+
+def _compact(g_run, g_code, g_hdr, nvb0, c_run, c_code, c_hdr, absorb, nv, shard_len, k):
+    """a compact shard summary in the C-ABI's 12 words; codes in the engine's
+    internal order (the C-ABI converts fk_state codes with sigma)"""
+    s = fk.FkSummary()
+    w = [g_code, g_run | (g_hdr << 32), nvb0, c_run, c_code, c_hdr | (absorb << 32), nv, shard_len, k, 0, 0, COMPACT]
+    for i, v in enumerate(w):
+        s.w[i] = v
+    return s
+
+
+def _sigma(x):
+    return x ^ ((x >> 1) & 0x5555555555555555)
+
+
+def test_compact_summary_apply():
+    """fk_summary_apply on compact summaries (host-only arithmetic): a shift
+    for a state equivalent to the shard's guess, the constant exit for an
+    absorbing shard, FK_E_SUMMARY for a state that would count the shard's
+    first range differently or could reach the int32 wrap"""
+    k = 6
+    mask = (1 << (2 * (k - 1))) - 1
+    # shard guessed deep in a run (R=256, last bases 0x0ABC), 1000 bases, no break
+    s = _compact(256, 0x0ABC, 0, 16384, 0, 0x3F3F, 0, 0, 1000, 16384, k)
+    st = fk.FkState(run=5000, code=_sigma(0x1230ABC & ((1 << 64) - 1)), hdr=0)
+    out = fk.summary_apply(s, st)
+    assert out.run == 6000 and out.hdr == 0
+    assert _sigma(out.code) & ((1 << 64) - 1) == 0x3F3F   # 1000 >= 32 new bases
+    # a state whose last k-1 bases differ from the guess: not equivalent
+    bad = fk.FkState(run=5000, code=_sigma(0x0ABD), hdr=0)
+    with pytest.raises(fk.FindKmerError) as e:
+        fk.summary_apply(s, bad)
+    assert e.value.code == fk.FK_E_SUMMARY
+    # a short run (R < k) is not equivalent to a deep guess
+    with pytest.raises(fk.FindKmerError):
+        fk.summary_apply(s, fk.FkState(run=3, code=_sigma(0x0ABC & mask), hdr=0))
+    # near the int32 wrap: the shard's local checks do not cover it
+    with pytest.raises(fk.FindKmerError):
+        fk.summary_apply(s, fk.FkState(run=(1 << 31) - 20000, code=_sigma(0x0ABC), hdr=0))
+    # an absorbing shard (run break inside): constant exit
+    a = _compact(256, 0x0ABC, 0, 16384, 77, 0x155, 0, 1, 0, 16384, k)
+    out = fk.summary_apply(a, fk.FkState(run=9999, code=_sigma(0x0ABC), hdr=0))
+    assert out.run == 77 and _sigma(out.code) == 0x155 and out.hdr == 0
+    # header status must match the guess
+    with pytest.raises(fk.FindKmerError):
+        fk.summary_apply(a, fk.FkState(run=0, code=0, hdr=1))

@@ -54,9 +54,11 @@ def assert_same(data, k, want_nodes=True, feeds=None, ngpu_shards=None):
     return r_g
 
 
-def shard_count(data, k, nshards):
+def shard_count(data, k, nshards, summaries=False):
     """Exercise the multi-GPU shard protocol with several engines (on the one
-    GPU of the test box): guess-from-halo, summaries, resolve, merge."""
+    GPU of the test box): guess-from-halo, summaries, resolve, merge.
+    summaries=True stitches as findkmer_amd/dist.py does: compose every
+    shard's (compact) summary in order, and on FK_E_SUMMARY the full ones."""
     import torch
     arr = np.frombuffer(bytes(data), dtype=np.uint8)
     n = len(arr)
@@ -72,10 +74,27 @@ def shard_count(data, k, nshards):
         halo = min(256, lo) // 16 * 16
         e.feed_shard_device(dev.data_ptr() + lo, hi - lo, halo)
         engines.append(e)
-    st = fk.FkState()
-    for e in engines:
-        e.resolve(st)
-        st = e.state()
+    if summaries:
+        def chain(sums):
+            st, ent = fk.FkState(), []
+            for sm in sums:
+                ent.append(st)
+                st = fk.summary_apply(sm, st)
+            return ent
+        try:
+            entering = chain([e.summary() for e in engines])
+            shard_count.compact_ok += 1
+        except fk.FindKmerError as err:
+            assert err.code == fk.FK_E_SUMMARY
+            entering = chain([e.summary_full() for e in engines])
+            shard_count.compact_failed += 1
+        for e, st in zip(engines, entering):
+            e.resolve(st)
+    else:
+        st = fk.FkState()
+        for e in engines:
+            e.resolve(st)
+            st = e.state()
     base = engines[0]
     for e in engines[1:]:
         assert fk.lib().fk_engine_merge_from(base.h, e.h) == 0
@@ -87,6 +106,9 @@ def shard_count(data, k, nshards):
     for e in engines:
         e.close()
     return t, r, ub, rc
+
+
+shard_count.compact_ok = shard_count.compact_failed = 0
 
 
 @pytest.fixture(scope="module", autouse=True)
@@ -356,3 +378,30 @@ def test_onepass_many_headers_no_nodes(k):
         out += b">" + bytes(rng.choices(b"ACGT xyz", k=rng.randint(5, 60))) + b"\n"
         out += bytes(rng.choices(b"ACGT", k=rng.randint(20, 300))) + b"\n"
     assert_same(bytes(out), k, want_nodes=False)
+
+
+@pytest.mark.parametrize("k", [4, 6, 7, 11])
+@pytest.mark.parametrize("nshards", [2, 3])
+@pytest.mark.parametrize("kind", ["mixed", "long_headers", "acgt"])
+def test_shards_summaries(k, nshards, kind):
+    """dist.py's stitch on one GPU: compact summaries of one-pass shards,
+    composed in order; the full transfer functions where one does not apply
+    (a shard starting inside a header longer than the halo)"""
+    if kind == "mixed":
+        data = mixed_input(77 + nshards, 900_000).replace(b"\xff", b"Z") + b"\nACGT"
+    elif kind == "long_headers":
+        data = _long_header_input(500 + nshards, 900_000)
+    else:
+        data = bytes(random.Random(k).choices(b"ACGT", k=800_000))
+    t_o, r_o, _ = oracle.count_dense(data, k)
+    t_g, r_g, ub, rc = shard_count(data, k, nshards, summaries=True)
+    assert np.array_equal(t_o, t_g)
+    assert r_g.windows == r_o.windows and r_g.valid_bases == r_o.valid_bases
+    assert list(r_g.base_count) == list(r_o.base_count)
+
+
+def test_shards_summaries_took_both_paths():
+    """the compact stitch and its fallback were both exercised above"""
+    if shard_count.compact_ok == 0 or shard_count.compact_failed == 0:
+        pytest.skip("run with test_shards_summaries")
+    assert shard_count.compact_ok > 0 and shard_count.compact_failed > 0
