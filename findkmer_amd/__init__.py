@@ -101,11 +101,14 @@ SIGNATURES = [
     ("fk_engine_progress", ctypes.c_int, [_P, _U64P, _U64P]),
     ("fk_engine_merge_from", ctypes.c_int, [_P, _P]),
     ("fk_engine_unknown", ctypes.c_int, [_P, _U8P, ctypes.c_uint64, _U64P]),
+    ("fk_engine_sparse", ctypes.c_int, [_P, _U64P, _U32P, ctypes.c_uint64, _U64P]),
     ("fk_count", ctypes.c_int, [_P, ctypes.c_uint64, ctypes.c_int, ctypes.POINTER(FkOpts), _U32P, ctypes.POINTER(FkResult)]),
     ("fk_count_multi", ctypes.c_int, [_P, ctypes.c_uint64, ctypes.c_int, ctypes.c_int, ctypes.POINTER(FkOpts), _U32P, ctypes.POINTER(FkResult)]),
     ("fk_synth_device", ctypes.c_int, [_P, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int, _P, _U64P]),
     ("fk_write_stats", ctypes.c_int, [ctypes.c_char_p, ctypes.c_int, ctypes.POINTER(FkResult), _P, ctypes.POINTER(ctypes.c_double)]),
     ("fk_write_rows", ctypes.c_int, [_P, ctypes.c_int, _U32P, ctypes.POINTER(ctypes.c_double), ctypes.c_uint64, ctypes.c_int, ctypes.c_double, ctypes.c_int]),
+    ("fk_write_rows_sparse", ctypes.c_int, [_P, ctypes.c_int, _U64P, _U32P, ctypes.c_uint64, ctypes.POINTER(ctypes.c_double), ctypes.c_uint64, ctypes.c_int, ctypes.c_double, ctypes.c_int]),
+    ("fk_write_csv_sparse", ctypes.c_int, [ctypes.c_char_p, ctypes.c_int, _U64P, _U32P, ctypes.c_uint64, ctypes.POINTER(ctypes.c_double), ctypes.c_uint64, ctypes.c_int, ctypes.c_double, ctypes.c_int]),
     ("fk_write_csv", ctypes.c_int, [ctypes.c_char_p, ctypes.c_int, _U32P, ctypes.POINTER(ctypes.c_double), ctypes.c_uint64, ctypes.c_int, ctypes.c_double, ctypes.c_int]),
 ]
 
@@ -258,6 +261,18 @@ class Engine:
     def table_from_device(self, ptr):
         _check(lib().fk_engine_table_from_device(self.h, ptr), "table_from_device")
 
+    def sparse(self):
+        """17 <= k <= 20, after finish(): (distinct k-mer indices uint64
+        ascending, their uint32 counts)"""
+        import numpy as np
+        n = ctypes.c_uint64()
+        _check(lib().fk_engine_sparse(self.h, None, None, 0, ctypes.byref(n)), "sparse")
+        keys = np.zeros(max(1, n.value), dtype=np.uint64)
+        cnts = np.zeros(max(1, n.value), dtype=np.uint32)
+        _check(lib().fk_engine_sparse(self.h, keys.ctypes.data_as(_U64P), cnts.ctypes.data_as(_U32P), n.value,
+                                      ctypes.byref(n)), "sparse")
+        return keys[: n.value], cnts[: n.value]
+
     def unknown_bytes(self):
         n = ctypes.c_uint64()
         _check(lib().fk_engine_unknown(self.h, None, 0, ctypes.byref(n)), "unknown")
@@ -323,3 +338,19 @@ def write_csv(path, k, counts, prob, windows, z_enable=0, z_threshold=0.0, threa
     p = (ctypes.c_double * 4)(*prob)
     _check(lib().fk_write_csv(path.encode(), k, c.ctypes.data_as(_U32P), p, windows, z_enable,
                               float(z_threshold), threads), "write_csv")
+
+
+def write_csv_sparse(path, k, keys, counts, prob, windows, z_enable=0, z_threshold=0.0, threads=0):
+    """CSV of a sparse table (17 <= k <= 20): distinct k-mer indices ascending + counts"""
+    import numpy as np
+    kk = np.ascontiguousarray(keys, dtype=np.uint64)
+    c = np.ascontiguousarray(counts, dtype=np.uint32)
+    if len(kk) == 0:
+        kk = np.zeros(1, dtype=np.uint64)
+        c = np.zeros(1, dtype=np.uint32)
+        n = 0
+    else:
+        n = len(kk)
+    p = (ctypes.c_double * 4)(*prob)
+    _check(lib().fk_write_csv_sparse(path.encode(), k, kk.ctypes.data_as(_U64P), c.ctypes.data_as(_U32P), n, p,
+                                     windows, z_enable, float(z_threshold), threads), "write_csv_sparse")

@@ -47,6 +47,7 @@
 
 #include "findkmer.h"
 #include "fk_device.h"
+#include "fk_sparse.h"
 
 #ifndef FK_EXP
 #define FK_EXP 0   /* ablation builds only (tools/exp.sh); 0 = product */
@@ -125,9 +126,16 @@ enum HistMode {
     H_LDS = 1,      /* k == 7: LDS k-mer bins */
     H_GLOBAL = 2,   /* k >= 13, and cancellations: global u32 atomics */
     H_NONE = 3,     /* 8 <= k <= 12, state pass: count nothing, only the scan state */
-    H_EMIT = 4      /* 8 <= k <= 12, k_part: fast tiles hand their windows to the
+    H_EMIT = 4,     /* 8 <= k <= 12, k_part: fast tiles hand their windows to the
                        partition, general tiles use global atomics */
+    H_SPARSE = 5    /* 17 <= k <= 20: general tiles from exact states write every
+                       window's index (and every short walk) at its byte's slot */
 };
+
+/* sparse slots (H_SPARSE, one u64 per input byte): a window's reference-order
+   index (< 2^40), a short walk (tag | depth << 40 | its code), or empty */
+#define SP_SHORT (1ull << 62)
+#define SP_EMPTY (~0ull)
 
 /* a fast tile's windows for the partition (k_part): per half, the context
    word, the 16-slot word and whether slot 0 is not a window */
@@ -152,6 +160,7 @@ struct Ctx {            /* kernel-wide constants */
     uint32_t single_off;/* H_PAIRS: offset of the k-mer singles in LDS (4^(k+1)) */
     int k;
     uint32_t *flush;    /* where lds_flush adds the bins (nullptr: table) */
+    uint64_t *slots;    /* H_SPARSE: the current range's slots (range-relative byte offset) */
 };
 
 /* LDS atomic add at a byte offset into the bins.  The kernels that count
@@ -334,7 +343,13 @@ __device__ __forceinline__ void tile_general(const Ctx &cx, const uint32_t w[8],
             int s = fk_sym(c);
             if (s < 0) {                      /* run break: '>', N, other */
                 int seq = (int)R;
-                if (HM != H_NONE && seq >= 1 && seq < k) short_run(cx, seq, lc, weight);
+                if (HM == H_SPARSE) {
+                    if (seq >= 1 && seq < k)
+                        cx.slots[tile_off + pos] =
+                            SP_SHORT | ((uint64_t)seq << 40) | fk_sigma(lc & ((1ull << (2 * seq)) - 1));
+                } else if (HM != H_NONE && seq >= 1 && seq < k) {
+                    short_run(cx, seq, lc, weight);
+                }
                 R = 0;
                 lane_reset = 1;
                 if (f.found_p1 || (p1_here && pos > p1)) lane_reset_after = 1;
@@ -353,7 +368,8 @@ __device__ __forceinline__ void tile_general(const Ctx &cx, const uint32_t w[8],
             int seq = (int)R;
             if (seq >= k) {
                 uint64_t idx = lc & cx.maskk;
-                hist_add<HM>(cx, idx, weight);
+                if (HM == H_SPARSE) cx.slots[tile_off + pos] = fk_sigma(idx);
+                else hist_add<HM>(cx, idx, weight);
                 cnt.win += 1;
                 if (seq == k) {               /* first window: its first k-1 bases */
                     cnt.base += comp_packed(fk_sigma(idx) >> 2, k - 1, maskk1);
@@ -660,7 +676,7 @@ __device__ void flush_counters(const Ctx &cx, Counters &cnt, uint32_t weight, bo
 template <int HM>
 __device__ __forceinline__ void do_tile(const Ctx &cx, const uint32_t w[8], int64_t toff, uint32_t tile_off,
                                         bool full, DState &st, Facts &f, Counters &cnt, uint32_t weight) {
-    if (full && st.hdr == 0 && tile_fast<true, HM, false>(cx, w, st, f, cnt, weight)) return;
+    if (HM != H_SPARSE && full && st.hdr == 0 && tile_fast<true, HM, false>(cx, w, st, f, cnt, weight)) return;
     const int lane = threadIdx.x & 63;
     uint32_t v[8];
     int nb = FK_LANE_BYTES;
@@ -1238,9 +1254,9 @@ template <int HM>
 __global__ void __launch_bounds__(FK_BLOCK)
 k_redo(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint32_t *table,
        uint32_t *shortcnt, unsigned long long *acc, DevRes *res, RangeRec *rr,
-       const XState *rtrue, const uint32_t *list, uint64_t nranges, int mode) {
+       const XState *rtrue, const uint32_t *list, uint64_t nranges, int mode, uint64_t *slots) {
     extern __shared__ uint32_t lds_bins[];
-    const uint64_t n = mode == 1 ? nranges : (uint64_t)res->redo_n;
+    const uint64_t n = mode != 0 ? nranges : (uint64_t)res->redo_n;
     if ((uint64_t)blockIdx.x * FK_WAVES_PER_BLOCK >= n) return;   /* uniform per block */
     const uint32_t nw = lds_words(HM, k);
     if (LDS_MODE(HM)) lds_zero(lds_bins, nw);
@@ -1249,16 +1265,23 @@ k_redo(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint
     const uint64_t wave = blockIdx.x * FK_WAVES_PER_BLOCK + wave_in_block();
     const uint64_t nwaves = (uint64_t)gridDim.x * FK_WAVES_PER_BLOCK;
     for (uint64_t i = wave; i < n; i += nwaves) {
-        const uint64_t r = mode == 1 ? i : list[i];
+        const uint64_t r = mode != 0 ? i : list[i];
         RangeRec q = rr[r];
         const Span sp = range_span(q, len);
         const XState t = rtrue[r];
+        if (HM == H_SPARSE) cx.slots = slots + sp.rbase;
         DState ts{t.code, (uint32_t)t.R, t.hdr};
         Facts f{0, 0, 0, 0, 0, 0};
         Counters cnt{0, 0, 0, 0, 0, FK_NO_EOF};
         if (mode == 1) {
             count_range<HM>(cx, sp, 0, ts, f, cnt, 0xFFFFFFFFu);
             flush_counters(cx, cnt, 0xFFFFFFFFu);
+        } else if (mode == 2) {
+            /* H_SPARSE: the range's slots from its exact state; exact
+               observations replace the state pass's */
+            count_range<HM>(cx, sp, 0, ts, f, cnt, 1u);
+            range_obs(cx, cnt, 1u, sp, &q, true);
+            if ((threadIdx.x & 63) == 0) { rr[r].eof = q.eof; rr[r].unknown = q.unknown; }
         } else {
             DState as{q.a_code, q.a_R, q.a_hdr};
             count_range<HM>(cx, sp, 0, as, f, cnt, 0xFFFFFFFFu);
@@ -2190,6 +2213,12 @@ struct fk_engine {
     uint64_t nbins = 0, nshort = 0, maskk = 0;
     int cus = 256;
     bool part = false;                        /* 8 <= k <= 12: partitioned counting (k_part) */
+    bool sparse = false;                      /* 17 <= k <= 20: slots, sorted at finish (fk_sparse.hip) */
+    uint64_t *d_slots = nullptr;              /* sparse: one u64 per byte fed (+1: the final short walk) */
+    uint64_t slots_cap = 0, slots_len = 0;
+    FksState fks;
+    bool sp_done = false;                     /* fks holds the finished table */
+    unsigned long long sp_nodes = 0, sp_roll = 0, sp_tstat[10] = {};
     uint16_t *d_codes = nullptr;              /* k_part: block code regions */
     uint32_t *d_pidx = nullptr, *d_prow = nullptr;   /* k_part: slice-major run index, row bases */
     uint64_t codes_cap = 0, pidx_cap = 0, prow_cap = 0;
@@ -2313,7 +2342,9 @@ extern "C" int fk_device_count(void) {
     return n;
 }
 
-static int hist_mode(const fk_engine *e) { return e->k <= 6 ? H_PAIRS : e->k == 7 ? H_LDS : H_GLOBAL; }
+static int hist_mode(const fk_engine *e) {
+    return e->sparse ? H_SPARSE : e->k <= 6 ? H_PAIRS : e->k == 7 ? H_LDS : H_GLOBAL;
+}
 
 /* 128 VGPRs -> 4 waves/SIMD = two 512-thread blocks per CU */
 static uint64_t blocks_per_cu(const fk_engine *) { return 2; }
@@ -2337,6 +2368,8 @@ static int zero_all(fk_engine *e) {
     e->shard_pending = 0;
     e->dev_ms = e->main_ms = 0;
     e->timed_n = 0;
+    e->slots_len = 0;
+    e->sp_done = false;
     e->unknown_bytes.clear();
     return FK_OK;
 }
@@ -2351,6 +2384,8 @@ extern "C" void fk_engine_destroy(fk_engine *e) {
     hipFree(e->d_redo); hipFree(e->d_tf); hipFree(e->d_stage); hipFree(e->d_resume);
     hipFree(e->d_aggs); hipFree(e->d_flags);
     hipFree(e->d_bsum); hipFree(e->d_ctl); hipFree(e->d_opc);
+    hipFree(e->d_slots);
+    fks_free(&e->fks);
     if (e->h_stage) hipHostFree(e->h_stage);
     for (int i = 0; i < 3; i++) if (e->ev[i]) hipEventDestroy(e->ev[i]);
     if (e->h_res) hipHostFree(e->h_res);
@@ -2381,7 +2416,6 @@ extern "C" int fk_engine_create(int k, const fk_opts *opts, fk_engine **out) {
     if (!out) return FK_E_INVALID;
     *out = nullptr;
     if (k < FK_K_MIN || k > FK_K_MAX_REF) return FK_E_INVALID;
-    if (k > FK_K_MAX_DENSE) return FK_E_K_UNSUPPORTED;
     int ndev = fk_device_count();
     if (ndev <= 0) return FK_E_NO_DEVICE;
     fk_engine *e = new fk_engine();
@@ -2399,14 +2433,15 @@ extern "C" int fk_engine_create(int k, const fk_opts *opts, fk_engine **out) {
     if (const char *ne = getenv("FK_NO_EVENTS")) e->timing = ne[0] != '1';
     if (const char *no = getenv("FK_NO_ONEPASS")) e->onepass = no[0] != '1';
     if (e->opts.timing_every > 1) e->timing_every = (uint32_t)e->opts.timing_every;
-    e->nbins = 1ull << (2 * k);
+    e->sparse = k > FK_K_MAX_DENSE;
+    e->nbins = e->sparse ? 0 : 1ull << (2 * k);
 #if FK_EXP == 6   /* ablation: the partitioned path for k >= 6 */
     e->part = k >= 6 && k <= 12;
 #else
     e->part = k >= 8 && k <= 12;
 #endif
-    e->maskk = e->nbins - 1;
-    e->nshort = k > 1 ? ((1ull << (2 * k)) - 4) / 3 : 0;
+    e->maskk = (1ull << (2 * k)) - 1;
+    e->nshort = k > 1 && !e->sparse ? ((1ull << (2 * k)) - 4) / 3 : 0;
     if (e->opts.stream) {
         e->stream = (hipStream_t)e->opts.stream;
     } else {
@@ -2418,7 +2453,7 @@ extern "C" int fk_engine_create(int k, const fk_opts *opts, fk_engine **out) {
     }
 #define ALLOC(p, bytes)                                                         \
     if (hipMalloc((void **)&(p), (bytes)) != hipSuccess) { fk_engine_destroy(e); return FK_E_OOM; }
-    ALLOC(e->d_table, e->nbins * sizeof(uint32_t));
+    ALLOC(e->d_table, std::max<uint64_t>(e->nbins, 4) * sizeof(uint32_t));
     if (hist_mode(e) != H_GLOBAL) {
         ALLOC(e->d_sub, FK_SUBTABLES * e->nbins * sizeof(uint32_t));
         if (hipMemsetAsync(e->d_sub, 0, FK_SUBTABLES * e->nbins * sizeof(uint32_t), e->stream) != hipSuccess) {
@@ -2533,12 +2568,13 @@ static Geo geometry(const fk_engine *e, uint64_t len) {
     switch (HMV) {                                                              \
     case H_PAIRS: { constexpr int HM = H_PAIRS; __VA_ARGS__; } break;          \
     case H_LDS: { constexpr int HM = H_LDS; __VA_ARGS__; } break;              \
+    case H_SPARSE: { constexpr int HM = H_SPARSE; __VA_ARGS__; } break;        \
     default: { constexpr int HM = H_GLOBAL; __VA_ARGS__; } break;              \
     }
 /* the counting passes of k_count / k_resume: state only (H_NONE) when the
    partitioned path (k_part) does the counting */
 #define FK_DISPATCH_COUNT(e, ...)                                               \
-    if ((e)->part) { constexpr int HM = H_NONE; __VA_ARGS__; }                  \
+    if ((e)->part || (e)->sparse) { constexpr int HM = H_NONE; __VA_ARGS__; }   \
     else FK_DISPATCH(hist_mode(e), __VA_ARGS__)
 
 /* the timing events of a launch (none when timing is off) */
@@ -2575,12 +2611,13 @@ static int launch_resume(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t
     return FK_OK;
 }
 
-static int launch_redo(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t lo, const Geo &g, int mode) {
+static int launch_redo(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t lo, const Geo &g, int mode,
+                       uint64_t *slots = nullptr) {
     size_t sh = lds_bytes(e);
     FK_DISPATCH(hist_mode(e),
                 hipLaunchKernelGGL((k_redo<HM>), dim3(g.grid), dim3(FK_BLOCK), sh, e->stream, buf, len, lo, e->k,
                                    e->maskk, e->d_table, e->d_short, e->d_facc, e->d_res, e->d_rr,
-                                   e->d_rtrue, e->d_redo, g.nranges, mode));
+                                   e->d_rtrue, e->d_redo, g.nranges, mode, slots));
     HIPCHK(hipGetLastError());
     return FK_OK;
 }
@@ -2880,6 +2917,72 @@ static int finish_segment(fk_engine *e, const uint8_t *dbuf, uint64_t len, int64
     return collect_unknown(e, dbuf, len, lo, g);
 }
 
+/* sparse slots for `need` bytes (grown geometrically, contents kept) */
+static int ensure_slots(fk_engine *e, uint64_t need) {
+    if (need <= e->slots_cap && e->d_slots) return FK_OK;
+    uint64_t cap = std::max<uint64_t>(need, std::max<uint64_t>(2 * e->slots_cap, 1u << 20));
+    uint64_t *p = nullptr;
+    if (hipMalloc((void **)&p, cap * sizeof(uint64_t)) != hipSuccess) return FK_E_OOM;
+    if (e->slots_len)
+        HIPCHK(hipMemcpyAsync(p, e->d_slots, e->slots_len * sizeof(uint64_t), hipMemcpyDeviceToDevice, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    hipFree(e->d_slots);
+    e->d_slots = p;
+    e->slots_cap = cap;
+    return FK_OK;
+}
+
+/*
+ * A segment for 17 <= k <= 20: the state pass (k_count / k_resume in H_NONE
+ * mode, k_scan) gives every range its exact entering state; k_redo mode 2
+ * then writes the segment's slots (and its counters and exact observations)
+ * from those states.  A 0xFF byte outside a header: cancel the counters,
+ * clear the slots and count the prefix again.
+ */
+static int sparse_segment(fk_engine *e, const uint8_t *dbuf, uint64_t len, bool prefix = false) {
+    const XState entering = e->state;
+    int rc = ensure_slots(e, e->slots_len + len + 1);   /* (+1: finish's final short walk) */
+    if (rc) return rc;
+    Geo g;
+    rc = count_segment(e, dbuf, len, 0, 1, g);
+    if (rc) return rc;
+    uint64_t *sl = e->d_slots + e->slots_len;
+    HIPCHK(hipMemsetAsync(sl, 0xFF, len * sizeof(uint64_t), e->stream));
+    rc = launch_scan(e, g, 0);
+    if (rc) return rc;
+    rc = launch_redo(e, dbuf, len, 0, g, 2, sl);
+    if (rc) return rc;
+    rc = launch_table_stats(e, false, tev(e, 2));   /* no dense table: publishes counters and state */
+    if (rc) return rc;
+    rc = wait_results(e);
+    if (rc) return rc;
+    add_times(e);
+    if (!prefix && e->last.eof_cand != NO_EOF64) {
+        unsigned long long eof = NO_EOF64;
+        rc = exact_eof(e, g, eof);
+        if (rc) return rc;
+        if (eof != NO_EOF64) {
+            rc = launch_redo(e, dbuf, len, 0, g, 1, sl);
+            if (rc) return rc;
+            HIPCHK(hipMemsetAsync(sl, 0xFF, len * sizeof(uint64_t), e->stream));
+            HIPCHK(hipMemcpyAsync(e->d_state, &entering, sizeof entering, hipMemcpyHostToDevice, e->stream));
+            e->state = entering;
+            e->ended = 1;
+            e->scanned += eof;
+            if (eof == 0) {
+                rc = launch_table_stats(e, true);
+                if (rc) return rc;
+                return wait_results(e);
+            }
+            return sparse_segment(e, dbuf, eof, true);
+        }
+    }
+    e->state = e->last.exit;
+    if (!prefix) e->scanned += len;
+    e->slots_len += len;
+    return collect_unknown(e, dbuf, len, 0, g);
+}
+
 static int process_segment(fk_engine *e, const uint8_t *dbuf, uint64_t len) {
     if (len == 0 || e->ended) return FK_OK;
     if (len < FK_LANE_BYTES && dbuf != e->d_stage) {
@@ -2888,6 +2991,7 @@ static int process_segment(fk_engine *e, const uint8_t *dbuf, uint64_t len) {
         HIPCHK(hipMemcpyAsync(e->d_stage, dbuf, len, hipMemcpyDeviceToDevice, e->stream));
         dbuf = e->d_stage;
     }
+    if (e->sparse) return sparse_segment(e, dbuf, len);
     XState entering = e->state;
     Geo g;
     int rc = count_segment(e, dbuf, len, 0, 1, g);
@@ -3150,7 +3254,24 @@ extern "C" int fk_engine_finish(fk_engine *e, fk_result *res) {
     const int k = e->k;
     /* an input ending with a run of 1..k-1 bases leaves its prefix walk */
     int32_t seq = (int32_t)(uint32_t)e->state.R;
-    if (!e->state.hdr && seq >= 1 && seq < k && e->opts.want_nodes && !e->tail_added) {
+    if (e->sparse) {
+        if (!e->sp_done) {
+            /* sort the slots (+ the final short walk): table, statistics, nodes */
+            uint64_t n = e->slots_len;
+            if (!e->state.hdr && seq >= 1 && seq < k && e->opts.want_nodes) {
+                rc = ensure_slots(e, n + 1);
+                if (rc) return rc;
+                const uint64_t v = SP_SHORT | ((uint64_t)seq << 40) | fk_sigma(e->state.code & ((1ull << (2 * seq)) - 1));
+                HIPCHK(hipMemcpyAsync(e->d_slots + n, &v, sizeof v, hipMemcpyHostToDevice, e->stream));
+                HIPCHK(hipStreamSynchronize(e->stream));
+                n++;
+            }
+            if (fks_finalize(&e->fks, e->d_slots, n, k, e->opts.want_nodes, e->stream, e->sp_tstat, &e->sp_roll,
+                             &e->sp_nodes))
+                return FK_E_HIP;
+            e->sp_done = true;
+        }
+    } else if (!e->state.hdr && seq >= 1 && seq < k && e->opts.want_nodes && !e->tail_added) {
         uint64_t off = ((1ull << (2 * seq)) - 4) / 3;
         uint64_t idx = off + fk_sigma(e->state.code & ((1ull << (2 * seq)) - 1));
         hipLaunchKernelGGL(k_add_short, dim3(1), dim3(1), 0, e->stream, e->d_short, idx);
@@ -3169,6 +3290,7 @@ extern "C" int fk_engine_finish(fk_engine *e, fk_result *res) {
     /* the table stats and the accumulator snapshot of the last feed (or of
        the call above) describe the engine: no device round trip here */
     settle_times(e, false);
+    if (e->sparse) memcpy(e->last.tstat, e->sp_tstat, sizeof e->sp_tstat);
     const unsigned long long *acc = e->last.acc;
     const unsigned long long *ts = e->last.tstat;
     res->windows = acc[ACC_WIN];
@@ -3182,6 +3304,7 @@ extern "C" int fk_engine_finish(fk_engine *e, fk_result *res) {
     /* a bin that wrapped past 2^32 loses 2^32 from the table total: some trie
        counter reached 2^32 -> the reference's rollover exit (:642) */
     if (ts[1] != res->windows) res->rollover = 1;
+    if (e->sparse && e->sp_roll) res->rollover = 1;
     res->valid_bases = res->windows + acc[ACC_VALID];
     res->distinct = ts[0];
     res->unknown_chars = acc[ACC_UNK];
@@ -3194,7 +3317,10 @@ extern "C" int fk_engine_finish(fk_engine *e, fk_result *res) {
     res->main_kernel_ms = e->main_ms;
     res->timed_kernels = e->timed_n;
     uint64_t any_walk = res->depth1[0] | res->depth1[1] | res->depth1[2] | res->depth1[3];
-    if (e->opts.want_nodes) {
+    if (e->opts.want_nodes && e->sparse) {
+        res->nodes = e->sp_nodes;
+        res->nodes_valid = 1;
+    } else if (e->opts.want_nodes) {
         /* nodeCounter = head + distinct prefixes of every walk (:620) */
         uint64_t nodes = 0;
         if (any_walk) {
@@ -3250,6 +3376,7 @@ extern "C" int fk_engine_progress(fk_engine *e, uint64_t *valid_bases, uint64_t 
 
 extern "C" int fk_engine_table(fk_engine *e, uint32_t *counts) {
     if (!e || !counts) return FK_E_INVALID;
+    if (e->sparse) return FK_E_INVALID;   /* 17 <= k <= 20: fk_engine_sparse */
     int rc = set_dev(e);
     if (rc) return rc;
     HIPCHK(hipMemcpyAsync(counts, e->d_table, e->nbins * sizeof(uint32_t), hipMemcpyDeviceToHost, e->stream));
@@ -3259,6 +3386,7 @@ extern "C" int fk_engine_table(fk_engine *e, uint32_t *counts) {
 
 extern "C" int fk_engine_table_range(fk_engine *e, uint64_t first, uint64_t n, uint32_t *counts) {
     if (!e || (!counts && n) || first > e->nbins || n > e->nbins - first) return FK_E_INVALID;
+    if (e->sparse) return FK_E_INVALID;   /* 17 <= k <= 20: fk_engine_sparse */
     int rc = set_dev(e);
     if (rc) return rc;
     if (n) HIPCHK(hipMemcpyAsync(counts, e->d_table + first, n * sizeof(uint32_t), hipMemcpyDeviceToHost, e->stream));
@@ -3268,6 +3396,7 @@ extern "C" int fk_engine_table_range(fk_engine *e, uint64_t first, uint64_t n, u
 
 extern "C" int fk_engine_table_device(fk_engine *e, uint32_t **dev_counts) {
     if (!e || !dev_counts) return FK_E_INVALID;
+    if (e->sparse) return FK_E_INVALID;   /* 17 <= k <= 20: fk_engine_sparse */
     int rc = set_dev(e);
     if (rc) return rc;
     *dev_counts = e->d_table;
@@ -3276,6 +3405,7 @@ extern "C" int fk_engine_table_device(fk_engine *e, uint32_t **dev_counts) {
 
 extern "C" int fk_engine_table_to_device(fk_engine *e, void *dst) {
     if (!e || !dst) return FK_E_INVALID;
+    if (e->sparse) return FK_E_INVALID;   /* 17 <= k <= 20: fk_engine_sparse */
     int rc = set_dev(e);
     if (rc) return rc;
     HIPCHK(hipMemcpyAsync(dst, e->d_table, e->nbins * sizeof(uint32_t), hipMemcpyDeviceToDevice, e->stream));
@@ -3285,11 +3415,31 @@ extern "C" int fk_engine_table_to_device(fk_engine *e, void *dst) {
 
 extern "C" int fk_engine_table_from_device(fk_engine *e, const void *src) {
     if (!e || !src) return FK_E_INVALID;
+    if (e->sparse) return FK_E_INVALID;   /* 17 <= k <= 20: fk_engine_sparse */
     int rc = set_dev(e);
     if (rc) return rc;
     HIPCHK(hipMemcpyAsync(e->d_table, src, e->nbins * sizeof(uint32_t), hipMemcpyDeviceToDevice, e->stream));
     HIPCHK(hipStreamSynchronize(e->stream));
     e->stats_valid = false;
+    return FK_OK;
+}
+
+/* The sparse table (17 <= k <= 20) after fk_engine_finish: the distinct
+   k-mer indices (reference order, ascending = CSV row order) and their u32
+   frequencies.  keys/counts may be NULL to ask for *n only. */
+extern "C" int fk_engine_sparse(fk_engine *e, uint64_t *keys, uint32_t *counts, uint64_t cap, uint64_t *n) {
+    if (!e || !n) return FK_E_INVALID;
+    if (!e->sparse || !e->sp_done) return FK_E_STATE;
+    *n = e->fks.nw;
+    if (!keys && !counts) return FK_OK;
+    if (cap < e->fks.nw) return FK_E_INVALID;
+    int rc = set_dev(e);
+    if (rc) return rc;
+    if (keys && e->fks.nw)
+        HIPCHK(hipMemcpyAsync(keys, e->fks.keys, e->fks.nw * sizeof(uint64_t), hipMemcpyDeviceToHost, e->stream));
+    if (counts && e->fks.nw)
+        HIPCHK(hipMemcpyAsync(counts, e->fks.lo, e->fks.nw * sizeof(uint32_t), hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
     return FK_OK;
 }
 
@@ -3311,6 +3461,7 @@ __global__ void k_add_acc(unsigned long long *dst, const unsigned long long *src
 
 extern "C" int fk_engine_merge_from(fk_engine *dst, fk_engine *src) {
     if (!dst || !src || dst->k != src->k) return FK_E_INVALID;
+    if (dst->sparse || src->sparse) return FK_E_INVALID;
     int rc = set_dev(src);
     if (rc) return rc;
     HIPCHK(hipStreamSynchronize(src->stream));
@@ -3349,6 +3500,7 @@ extern "C" int fk_engine_merge_from(fk_engine *dst, fk_engine *src) {
 
 extern "C" int fk_count(const uint8_t *buf, uint64_t len, int k, const fk_opts *opts, uint32_t *counts,
                         fk_result *res) {
+    if (k > FK_K_MAX_DENSE) return FK_E_K_UNSUPPORTED;   /* a dense table out: engine + fk_engine_sparse */
     fk_engine *e = nullptr;
     int rc = fk_engine_create(k, opts, &e);
     if (rc) return rc;
@@ -3374,6 +3526,7 @@ extern "C" int fk_count(const uint8_t *buf, uint64_t len, int k, const fk_opts *
  */
 extern "C" int fk_count_multi(const uint8_t *buf, uint64_t len, int k, int ngpu, const fk_opts *opts,
                               uint32_t *counts, fk_result *res) {
+    if (k > FK_K_MAX_DENSE) return FK_E_K_UNSUPPORTED;
     int ndev = fk_device_count();
     if (ngpu <= 0 || ngpu > ndev) ngpu = ndev;
     if (ngpu <= 1 || len < (uint64_t)ngpu * FK_CHUNK_BYTES) return fk_count(buf, len, k, opts, counts, res);

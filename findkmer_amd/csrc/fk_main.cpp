@@ -348,11 +348,6 @@ int main(int argc, char *argv[]) {                                  /* :1292-137
     }
     rewind(config.sequence_file_pointer);
 
-    if (config.k > FK_K_MAX_DENSE) {
-        fprintf(stderr, "findKmer: k=%d needs the sparse table, which this build does not have yet (k <= %d)\n",
-                config.k, FK_K_MAX_DENSE);
-        exit(EXIT_FAILURE);
-    }
     fk_opts opts;
     memset(&opts, 0, sizeof opts);
     opts.device = -1;
@@ -394,12 +389,26 @@ int main(int argc, char *argv[]) {                                  /* :1292-137
 
     fprintf(stdout, "Now creating histogram.\n");
     fflush(stdout);
-    std::vector<uint32_t> counts((size_t)1 << (2 * config.k));
-    rc = fk_engine_table(eng, counts.data());
-    if (rc) die_engine(rc);
-    fk_engine_destroy(eng);
-    rc = fk_write_rows(config.out_file_pointer, config.k, counts.data(), prob, res.windows,
-                       config.zThresholdEnable, (double)config.zThreshold, 0);
+    if (config.k > FK_K_MAX_DENSE) {
+        /* 17 <= k <= 20: the engine's sparse table (distinct k-mers, sorted) */
+        uint64_t n = 0;
+        rc = fk_engine_sparse(eng, nullptr, nullptr, 0, &n);
+        if (rc) die_engine(rc);
+        std::vector<uint64_t> keys((size_t)n + 1);
+        std::vector<uint32_t> cnts((size_t)n + 1);
+        rc = fk_engine_sparse(eng, keys.data(), cnts.data(), n, &n);
+        if (rc) die_engine(rc);
+        fk_engine_destroy(eng);
+        rc = fk_write_rows_sparse(config.out_file_pointer, config.k, keys.data(), cnts.data(), n, prob, res.windows,
+                                  config.zThresholdEnable, (double)config.zThreshold, 0);
+    } else {
+        std::vector<uint32_t> counts((size_t)1 << (2 * config.k));
+        rc = fk_engine_table(eng, counts.data());
+        if (rc) die_engine(rc);
+        fk_engine_destroy(eng);
+        rc = fk_write_rows(config.out_file_pointer, config.k, counts.data(), prob, res.windows,
+                           config.zThresholdEnable, (double)config.zThreshold, 0);
+    }
     if (rc) die_engine(rc);
 
     fprintf(stdout, "histogram creation finished.\n");

@@ -89,6 +89,7 @@ inline void digits_of(uint64_t idx, int k, int cnt[4], char *kmer) {
 struct RowCtx {
     int k;
     const uint32_t *counts;
+    const uint64_t *keys;   /* sparse: row i is k-mer keys[i] with count counts[i] */
     unsigned long long n;   /* TotalNumSequencesN */
     int z_enable;
     long double z_thr;
@@ -100,8 +101,9 @@ void format_range(const RowCtx &c, uint64_t lo, uint64_t hi, std::string &out) {
     char kmer[32];
     char num[64];
     int cnt[4];
-    for (uint64_t idx = lo; idx < hi; idx++) {
-        uint32_t f = c.counts[idx];
+    for (uint64_t i = lo; i < hi; i++) {
+        const uint64_t idx = c.keys ? c.keys[i] : i;
+        uint32_t f = c.counts[i];
         if (!f) continue;
         digits_of(idx, c.k, cnt, kmer);
         const Comp &cp = (*c.comps)[comp_key(cnt[0], cnt[1], cnt[2])];
@@ -166,11 +168,8 @@ extern "C" int fk_write_stats(const char *stats_path, int k, const fk_result *re
     return FK_OK;
 }
 
-extern "C" int fk_write_rows(void *out_v, int k, const uint32_t *counts,
-                             const double prob[4], uint64_t windows, int z_enable,
-                             double z_threshold, int threads) {
-    FILE *out = (FILE *)out_v;
-    if (!out || !counts || k < 1 || k > FK_K_MAX_DENSE) return FK_E_INVALID;
+static int write_rows(FILE *out, int k, const uint64_t *keys, uint64_t n_rows, const uint32_t *counts,
+                      const double prob[4], uint64_t windows, int z_enable, double z_threshold, int threads) {
     std::vector<Comp> comps(21 * 21 * 21);
     unsigned long long n = windows;
     /* memoise every composition that can occur */
@@ -180,8 +179,8 @@ extern "C" int fk_write_rows(void *out_v, int k, const uint32_t *counts,
                 int cnt[4] = { a, c, g, k - a - c - g };
                 build_comp(comps[comp_key(a, c, g)], cnt, k, prob, n);
             }
-    RowCtx ctx { k, counts, n, z_enable, (long double)z_threshold, &comps };
-    uint64_t total = 1ull << (2 * k);
+    RowCtx ctx { k, counts, keys, n, z_enable, (long double)z_threshold, &comps };
+    uint64_t total = keys ? n_rows : 1ull << (2 * k);
     if (threads <= 0) {
         unsigned hc = std::thread::hardware_concurrency();
         threads = hc ? (int)std::min(hc, 64u) : 1;
@@ -212,6 +211,37 @@ extern "C" int fk_write_rows(void *out_v, int k, const uint32_t *counts,
         }
     }
     return FK_OK;
+}
+
+extern "C" int fk_write_rows(void *out_v, int k, const uint32_t *counts,
+                             const double prob[4], uint64_t windows, int z_enable,
+                             double z_threshold, int threads) {
+    FILE *out = (FILE *)out_v;
+    if (!out || !counts || k < 1 || k > FK_K_MAX_DENSE) return FK_E_INVALID;
+    return write_rows(out, k, nullptr, 0, counts, prob, windows, z_enable, z_threshold, threads);
+}
+
+/* The rows of a sparse table (17 <= k <= 20, fk_engine_sparse): the same
+ * bytes fk_write_rows writes for the dense table with those counts. */
+extern "C" int fk_write_rows_sparse(void *out_v, int k, const uint64_t *keys, const uint32_t *counts, uint64_t n,
+                                    const double prob[4], uint64_t windows, int z_enable, double z_threshold,
+                                    int threads) {
+    FILE *out = (FILE *)out_v;
+    if (!out || (n && (!keys || !counts)) || k < 1 || k > FK_K_MAX_REF) return FK_E_INVALID;
+    static const uint32_t zero = 0;
+    return write_rows(out, k, keys ? keys : (const uint64_t *)&zero, n, counts ? counts : &zero, prob, windows,
+                      z_enable, z_threshold, threads);
+}
+
+extern "C" int fk_write_csv_sparse(const char *csv_path, int k, const uint64_t *keys, const uint32_t *counts,
+                                   uint64_t n, const double prob[4], uint64_t windows, int z_enable,
+                                   double z_threshold, int threads) {
+    FILE *f = fopen(csv_path, "w");
+    if (!f) return FK_E_IO;
+    fputs("Sequence, Shannon Entropy h, Shannon Entropy H, Frequency, Z score", f);
+    int rc = fk_write_rows_sparse(f, k, keys, counts, n, prob, windows, z_enable, z_threshold, threads);
+    if (fclose(f) != 0 && rc == FK_OK) rc = FK_E_IO;
+    return rc;
 }
 
 extern "C" int fk_write_csv(const char *csv_path, int k, const uint32_t *counts,

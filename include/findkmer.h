@@ -42,7 +42,9 @@ extern "C" {
 enum {
     FK_OK = 0,
     FK_E_INVALID = -1,          /* bad argument */
-    FK_E_K_UNSUPPORTED = -2,    /* 17 <= k <= 20: sparse table not built yet */
+    FK_E_K_UNSUPPORTED = -2,    /* a dense-table entry point (fk_count*) with
+                                   17 <= k <= 20: use an engine and
+                                   fk_engine_sparse */
     FK_E_NO_DEVICE = -3,        /* no HIP device / extension cannot run */
     FK_E_HIP = -4,              /* a HIP runtime call failed */
     FK_E_OOM = -5,              /* device or host allocation failed */
@@ -173,6 +175,14 @@ int  fk_engine_merge_from(fk_engine *dst, fk_engine *src);
  * available; copies min(cap, n). */
 int  fk_engine_unknown(fk_engine *e, uint8_t *out, uint64_t cap, uint64_t *n);
 
+/* 17 <= k <= 20 (the reference's k limit, :438): the table is sparse.  After
+ * fk_engine_finish, the distinct k-mer indices in ascending order (= the
+ * CSV's row order) and their u32 frequencies; keys and counts may be NULL to
+ * ask for *n.  The dense table calls (fk_engine_table...) return
+ * FK_E_INVALID for these k.  Device memory: 8 bytes per input byte fed
+ * (slots), plus ~24 per byte while fk_engine_finish sorts them. */
+int  fk_engine_sparse(fk_engine *e, uint64_t *keys, uint32_t *counts, uint64_t cap, uint64_t *n);
+
 /* One-shot convenience: count a whole buffer on one device. */
 int  fk_count(const uint8_t *buf, uint64_t len, int k, const fk_opts *opts,
               uint32_t *counts /* host, 4^k */, fk_result *res);
@@ -207,6 +217,13 @@ int  fk_write_stats(const char *stats_path, int k, const fk_result *res,
 int  fk_write_rows(void *out, int k, const uint32_t *counts,
                    const double prob[4], uint64_t windows, int z_enable,
                    double z_threshold, int threads);
+/* the same rows for a sparse table (fk_engine_sparse's keys and counts) */
+int  fk_write_rows_sparse(void *out, int k, const uint64_t *keys, const uint32_t *counts, uint64_t n,
+                          const double prob[4], uint64_t windows, int z_enable,
+                          double z_threshold, int threads);
+int  fk_write_csv_sparse(const char *csv_path, int k, const uint64_t *keys, const uint32_t *counts,
+                         uint64_t n, const double prob[4], uint64_t windows, int z_enable,
+                         double z_threshold, int threads);
 
 /* Path-based variant for bindings: writes header + rows to csv_path. */
 int  fk_write_csv(const char *csv_path, int k, const uint32_t *counts,

@@ -35,6 +35,12 @@ def cases():
     c.append(("ffbyte_k3", "ffbyte.bin", ["-q", "1", "-k", "3", "-p", "ffbyte.bin"]))
     c.append(("shortruns_k5", "shortruns.txt", ["-q", "1", "-k", "5", "-p", "shortruns.txt"]))
     c.append(("empty_k3", "empty.txt", ["-q", "1", "-k", "3", "-p", "empty.txt"]))
+    # 17 <= k <= 20: the sparse table
+    c.append(("rand_k17", "rand120k.fa", ["-q", "1", "-k", "17", "-p", "rand120k.fa"]))
+    c.append(("rand_k19_z4", "rand120k.fa", ["-q", "1", "-k", "19", "-z", "4", "-p", "rand120k.fa"]))
+    c.append(("shortruns_k18", "shortruns.txt", ["-q", "1", "-k", "18", "-p", "shortruns.txt"]))
+    c.append(("edge_k20", "edge.txt", ["-q", "1", "-k", "20", "-p", "edge.txt"]))
+    c.append(("ffbyte_k17", "ffbyte.bin", ["-q", "1", "-k", "17", "-p", "ffbyte.bin"]))
     return c
 
 def main():

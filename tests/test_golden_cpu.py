@@ -23,6 +23,7 @@ CPU_CASES = [c for c in [
     "test_k6_q0", "test_k0_default7", "edge_k2", "edge_k3", "edge_k4",
     "rand_k5", "rand_k6_z3", "rand_k8", "rand_k4_z2", "rand_k11",
     "missing_k3", "ffbyte_k3", "shortruns_k5",
+    "rand_k17", "rand_k19_z4", "shortruns_k18", "edge_k20", "ffbyte_k17",
 ]]
 
 
@@ -54,15 +55,18 @@ def write_outputs(tmp_path, entry, k):
     csv_path = str(tmp_path / "out.csv")
     zen, zthr = case_z(entry)
     if rc == 0:
-        if isinstance(tbl, tuple):
-            # sparse oracle (k > 13): rows are only written for present k-mers,
-            # so a dense table is not needed; build one through a small map
+        if isinstance(tbl, tuple) and k > 16:
+            # 17 <= k <= 20: the product's sparse writer
             codes, cnts = tbl
-            assert k <= 16
-            dense = np.zeros(1 << (2 * k), dtype=np.uint32)
-            dense[codes.astype(np.int64)] = cnts
-            tbl = dense
-        fk.write_csv(csv_path, k, tbl, prob, r.windows, zen, zthr, threads=4)
+            fk.write_csv_sparse(csv_path, k, codes, cnts, prob, r.windows, zen, zthr, threads=4)
+        else:
+            if isinstance(tbl, tuple):
+                # sparse oracle (k > 13) into a dense table
+                codes, cnts = tbl
+                dense = np.zeros(1 << (2 * k), dtype=np.uint32)
+                dense[codes.astype(np.int64)] = cnts
+                tbl = dense
+            fk.write_csv(csv_path, k, tbl, prob, r.windows, zen, zthr, threads=4)
     else:
         open(csv_path, "w").write("Sequence, Shannon Entropy h, Shannon Entropy H, Frequency, Z score")
     return stats_path, csv_path, r
@@ -72,8 +76,6 @@ def write_outputs(tmp_path, entry, k):
 def test_writer_matches_reference(case, manifest, tmp_path):
     entry = manifest[case]
     k = case_k(entry)
-    if k > 16:
-        pytest.skip("k > 16 needs the sparse table (not built yet)")
     stats_path, csv_path, r = write_outputs(tmp_path, entry, k)
     gs = entry["files"]["stats"]
     got = open(stats_path, "rb").read()

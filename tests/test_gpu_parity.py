@@ -293,7 +293,8 @@ def test_full_size_properties(k):
 
 GOLD_CLI = ["test_k6", "test_k1", "test_k11", "test_k6_q0", "test_k0_default7", "test_k6_export",
             "test_k6_badopt", "edge_k3", "rand_k5", "rand_k6_z3", "rand_k8", "rand_k4_z2",
-            "rand_k11", "missing_k3", "ffbyte_k3", "shortruns_k5", "empty_k3"]
+            "rand_k11", "missing_k3", "ffbyte_k3", "shortruns_k5", "empty_k3",
+            "test_k15", "test_k20", "rand_k17", "rand_k19_z4", "shortruns_k18", "edge_k20", "ffbyte_k17"]
 
 
 @pytest.mark.parametrize("case", GOLD_CLI)
@@ -405,3 +406,68 @@ def test_shards_summaries_took_both_paths():
     if shard_count.compact_ok == 0 or shard_count.compact_failed == 0:
         pytest.skip("run with test_shards_summaries")
     assert shard_count.compact_ok > 0 and shard_count.compact_failed > 0
+
+
+def assert_same_sparse(data, k, feeds=None):
+    """17 <= k <= 20: the engine's sparse table and scalars vs the oracle's"""
+    keys_o, cnt_o, r_o = oracle.count_sparse(data, k, cap=max(16, len(data) + 16))
+    with fk.Engine(k, want_nodes=True, collect_unknown=True) as e:
+        arr = np.frombuffer(bytes(data), dtype=np.uint8)
+        if feeds is None:
+            feeds = [len(arr)]
+        pos = 0
+        for n in feeds:
+            if n:
+                e.feed(np.ascontiguousarray(arr[pos:pos + n]))
+            pos += n
+        assert pos == len(arr)
+        rc, r_g = e.finish(allow=(fk.FK_OK, fk.FK_E_EMPTY, fk.FK_E_UNTERMINATED_HEADER, fk.FK_E_ROLLOVER))
+        keys_g, cnt_g = e.sparse()
+        ub_g = e.unknown_bytes()
+    _, _, ub_o = oracle.count_dense(data, 3, unknown_cap=1 << 20)   # unknown bytes do not depend on k
+    assert np.array_equal(keys_g, keys_o), (len(keys_g), len(keys_o))
+    assert np.array_equal(cnt_g, cnt_o)
+    assert list(r_g.base_count) == list(r_o.base_count)
+    assert r_g.valid_bases == r_o.valid_bases and r_g.windows == r_o.windows
+    assert r_g.distinct == r_o.distinct == len(keys_o)
+    assert list(r_g.depth1) == list(r_o.depth1)
+    assert r_g.nodes == r_o.nodes
+    assert r_g.unknown_chars == r_o.unknown_chars and ub_g == ub_o
+    assert r_g.hit_eof_byte == r_o.hit_eof_byte and r_g.scanned_bytes == r_o.scanned_bytes
+    assert r_g.unterminated_header == r_o.unterminated_header
+
+
+@pytest.mark.parametrize("name", GOLDEN_INPUTS)
+@pytest.mark.parametrize("k", [17, 18, 20])
+def test_sparse_golden_inputs(name, k):
+    assert_same_sparse(golden_input(name), k)
+
+
+@pytest.mark.parametrize("k", [17, 19, 20])
+def test_sparse_mixed_and_streaming(k):
+    data = mixed_input(900 + k, 400_000)
+    assert_same_sparse(data, k)
+    rng = random.Random(k)
+    feeds, left = [], len(data)
+    while left:
+        n = min(left, rng.choice([1, 31, 4096, 70001, 150000]))
+        feeds.append(n)
+        left -= n
+    assert_same_sparse(data, k, feeds=feeds)
+
+
+@pytest.mark.parametrize("k", [17, 20])
+def test_sparse_long_headers_and_acgt(k):
+    assert_same_sparse(_long_header_input(33 + k, 500_000), k)
+    assert_same_sparse(bytes(random.Random(k).choices(b"ACGT", k=700_000)), k)
+
+
+def test_sparse_dense_entry_points_refuse():
+    """the dense-table calls answer FK_E_INVALID / FK_E_K_UNSUPPORTED for k > 16"""
+    with fk.Engine(17) as e:
+        e.feed(np.frombuffer(b"ACGT" * 100, dtype=np.uint8).copy())
+        e.finish()
+        with pytest.raises(fk.FindKmerError):
+            e.table_range(0, 16)
+    rc, _, _ = (None, None, None)
+    assert fk.lib().fk_count(None, 0, 17, None, None, None) == fk.FK_E_K_UNSUPPORTED
