@@ -1271,26 +1271,33 @@ k_redo(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint
         const XState t = rtrue[r];
         if (HM == H_SPARSE) cx.slots = slots + sp.rbase;
         DState ts{t.code, (uint32_t)t.R, t.hdr};
-        Facts f{0, 0, 0, 0, 0, 0};
-        Counters cnt{0, 0, 0, 0, 0, FK_NO_EOF};
-        if (mode == 1) {
-            count_range<HM>(cx, sp, 0, ts, f, cnt, 0xFFFFFFFFu);
-            flush_counters(cx, cnt, 0xFFFFFFFFu);
-        } else if (mode == 2) {
-            /* H_SPARSE: the range's slots from its exact state; exact
-               observations replace the state pass's */
-            count_range<HM>(cx, sp, 0, ts, f, cnt, 1u);
-            range_obs(cx, cnt, 1u, sp, &q, true);
-            if ((threadIdx.x & 63) == 0) { rr[r].eof = q.eof; rr[r].unknown = q.unknown; }
-        } else {
-            DState as{q.a_code, q.a_R, q.a_hdr};
-            count_range<HM>(cx, sp, 0, as, f, cnt, 0xFFFFFFFFu);
-            flush_counters(cx, cnt, 0xFFFFFFFFu);
-            cnt = Counters{0, 0, 0, 0, 0, FK_NO_EOF};
-            f = Facts{0, 0, 0, 0, 0, 0};
-            count_range<HM>(cx, sp, 0, ts, f, cnt, 1u);
-            range_obs(cx, cnt, 1u, sp, &q, true);
-            if ((threadIdx.x & 63) == 0) { rr[r].eof = q.eof; rr[r].unknown = q.unknown; }
+        /* passes over the range (one inlined count_range: its register
+           footprint decides this kernel's occupancy):
+           mode 0: -1 from the guess, then +1 from the exact state -- except
+                   when the whole range lies in the reference's negative
+                   int32 zone (seqSize < 0 from its first base to its last,
+                   no run break: a run longer than 2^31 bases, :977), where
+                   the exact state counts nothing: one read instead of two;
+           mode 1: -1 from the exact state;
+           mode 2: +1 from the exact state (H_SPARSE: the slots). */
+        const bool neg_zone = mode == 0 && !t.hdr && !q.tf.f0_const && (int32_t)(uint32_t)t.R < 0 &&
+                              (uint64_t)(uint32_t)t.R + (sp.rend - sp.rbase) <= 0xFFFFFFFFull;
+        const int npass = mode == 0 && !neg_zone ? 2 : 1;
+#pragma unroll 1
+        for (int pass = 0; pass < npass; pass++) {
+            const bool cancel = mode == 1 || (mode == 0 && pass == 0);
+            const uint32_t wt = cancel ? 0xFFFFFFFFu : 1u;
+            DState st = (mode == 0 && pass == 0) ? DState{q.a_code, q.a_R, q.a_hdr} : ts;
+            Facts f{0, 0, 0, 0, 0, 0};
+            Counters cnt{0, 0, 0, 0, 0, FK_NO_EOF};
+            count_range<HM>(cx, sp, 0, st, f, cnt, wt);
+            if (cancel) {
+                flush_counters(cx, cnt, wt);
+            } else {
+                /* exact observations replace the guessed trajectory's */
+                range_obs(cx, cnt, 1u, sp, &q, true);
+                if ((threadIdx.x & 63) == 0) { rr[r].eof = q.eof; rr[r].unknown = q.unknown; }
+            }
         }
     }
     if (LDS_MODE(HM)) lds_flush<HM>(cx);
