@@ -7,7 +7,9 @@ the hot path over the batch: reset, k_count + k_tail (the engine's
 fk_engine_feed: count, fold, check the guessed range states, publish), and the
 result scalars (fk_engine_finish).  With
 --gpus N (one process per GPU, torch.distributed over RCCL) each rank owns the
-next 1 GB shard of one N GB stream: the shard entry state is stitched by
+next 1 GB shard of one N GB stream (a synthetic genome with an 'N' run break
+every 1.5 Gbases, so no run reaches the reference's int32 wrap; the N=1 stream
+has none): the shard entry state is stitched by
 all-gathering the 96-byte shard transfer functions, and the count tables are
 summed with an all-reduce — the path's two real exchange steps.
 
@@ -30,6 +32,7 @@ sys.path.insert(0, REPO)
 
 HBM_PEAK_GBS = 8000.0    # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 METRIC = "bases/sec scanned at fixed k; achieved HBM GB/s vs roofline, 1/2/4/8 GPUs"
+CHROM = 1_500_000_000   # multi-GPU stream: an 'N' run break every CHROM bases (synthetic chromosomes)
 
 
 def parse():
@@ -43,6 +46,8 @@ def parse():
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--cpu-sample-bytes", type=int, default=0, help="0 = auto (~10-20 s of reference CPU work)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--chrom", type=int, default=CHROM,
+                    help="multi-GPU stream: an 'N' run break every this many bases")
     ap.add_argument("--timing-every", type=int, default=4,
                     help="time the count kernel with HIP events on every Nth step")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
@@ -88,6 +93,19 @@ def run_windows(n, k):
     return full * (hi - k + 1) + max(0, min(rem, hi) - k + 1)
 
 
+
+
+def expected_windows(total, k, chrom):
+    """Windows in a pure-ACGT stream of `total` positions whose positions
+    j*chrom (j >= 1) hold 'N' run breaks: each run is shorter than 2^31, so
+    the reference's int32 seqSize (findKmer.cpp:977) never wraps."""
+    w, start = 0, 0
+    for b in range(chrom, total, chrom):
+        w += run_windows(b - start, k)
+        start = b + 1
+    return w + run_windows(total - start, k)
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -127,6 +145,12 @@ def main():
     w = fk.synth_device(buf.data_ptr(), size, n + halo_bases, args.seed + first // 32, frame)
     assert w == size
     nbytes = size - halo
+    if world > 1 and L == 0:
+        # one N-GB stream as a genome of CHROM-base chromosomes: an 'N' at
+        # every multiple of CHROM (as in real genomes, no run reaches the
+        # reference's int32 seqSize wrap at 2^31 bases)
+        for b in range((first // args.chrom + 1) * args.chrom, first + size, args.chrom):
+            buf[b - first] = ord("N")
     torch.cuda.synchronize()
 
     # the count kernel's HIP events on every 4th step of the timed region
@@ -178,7 +202,8 @@ def main():
             total = int(w_t.item())
             merged = int(table_t.to(torch.int64).remainder(1 << 32).sum().item())
             assert merged == total, (merged, total)
-        assert total == run_windows(world * n, k), (total, run_windows(world * n, k))
+        want = expected_windows(world * n, k, args.chrom) if world > 1 and L == 0 else run_windows(world * n, k)
+        assert total == want, (total, want)
 
     ms_step = dt / args.steps * 1e3
     value = world * n / (dt / args.steps)

@@ -15,12 +15,15 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("k,fasta", [(6, 0), (11, 80)])
-def test_two_rank_shards_gloo(k, fasta):
+@pytest.mark.parametrize("k,fasta,chrom", [(6, 0, 1_500_000_000), (11, 80, 1_500_000_000), (6, 0, 20_000_000),
+                                           (7, 0, 12_799_900)])
+def test_two_rank_shards_gloo(k, fasta, chrom):
+    """chrom < 25.6M puts an 'N' run break inside rank 1's shard (20M), or in
+    its 256-byte halo (12_799_900: 100 bases before the shard)"""
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-           "--master-addr", "127.0.0.1", "--master-port", str(29600 + k), os.path.join(REPO, "bench.py"),
+           "--master-addr", "127.0.0.1", "--master-port", str(29600 + k + chrom % 97), os.path.join(REPO, "bench.py"),
            "--gpus", "2", "--steps", "2", "--warmup", "1", "--no-cpu-baseline", "--dist-backend", "gloo",
-           "--k", str(k), "--fasta-line", str(fasta), "--bases", "12800000"]
+           "--k", str(k), "--fasta-line", str(fasta), "--bases", "12800000", "--chrom", str(chrom)]
     p = subprocess.run(cmd, cwd=REPO, capture_output=True, text=True, timeout=600)
     assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-4000:]
     line = [l for l in p.stdout.splitlines() if l.startswith("{")][-1]
