@@ -487,7 +487,6 @@ __device__ __forceinline__ void half_windows(const Ctx &cx, uint32_t C, uint32_t
 template <bool COUNT, int HM, bool INTER, bool NL>
 __device__ __forceinline__ bool tile_finish(const Ctx &cx, const uint32_t x[8], uint32_t nl0, uint32_t nl1,
                                             DState &st, Facts &f, Counters &cnt, uint32_t weight, Emit *em) {
-    const int lane = threadIdx.x & 63;
     const int k = cx.k;
     /* deep: every window of the tile counts (seq > k throughout); neg: the
        reference's int32 seqSize stays negative for the whole tile (a run
@@ -1414,11 +1413,14 @@ __device__ __forceinline__ bool part_batch(const Ctx &cx, const PartGeo &pg, con
         }
     }
     __syncthreads();
-    /* 4: the sorted batch, contiguous, into the block's code region */
-    const uint32_t n = *total;
-    uint16_t *dst = pg.codes + (size_t)blockIdx.x * pg.region_stride + blk_cursor;
-    for (uint32_t i = t; i < n; i += PART_BLOCK) dst[i] = ent[i];
-    blk_cursor += n;
+    /* 4: the sorted batch, contiguous, into the block's code region: 16-B
+       pieces (rows start at multiples of 8 codes; the up to 7 codes past
+       the batch's end are padding no run covers) */
+    const uint32_t n8 = (*total + 7u) >> 3;
+    uint4 *dst = reinterpret_cast<uint4 *>(pg.codes + (size_t)blockIdx.x * pg.region_stride + blk_cursor);
+    const uint4 *src = reinterpret_cast<const uint4 *>(ent);
+    for (uint32_t i = t; i < n8; i += PART_BLOCK) dst[i] = src[i];
+    blk_cursor += n8 << 3;
     return any_more;
 }
 
@@ -1427,7 +1429,7 @@ k_part(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint
        uint32_t *shortcnt, unsigned long long *acc, DevRes *res, RangeRec *rr, uint64_t nchunks, uint64_t cpw,
        const XState *d_init, int has_init, PartGeo pg) {
     __shared__ uint32_t hist[PART_MAX_SLICES], cur[PART_MAX_SLICES], total;
-    __shared__ uint16_t ent[PART_MAX_BATCH];
+    __shared__ __attribute__((aligned(16))) uint16_t ent[PART_MAX_BATCH];
     /* open the feed's result block (the kernels after this one accumulate
        into it) */
     if (blockIdx.x == 0) {
@@ -1923,13 +1925,42 @@ k_tail(const OnePassCfg *opc, uint32_t flags, uint32_t seq, uint32_t *table, int
     TP(4);
 }
 
+/* Sum the per-block partials of k_table_stats into res->tstat and publish
+   the result block (one block of 256 threads). */
+__device__ void stats_publish(DevRes *res, DevRes *host_res, const unsigned long long *part, uint32_t nparts,
+                              uint32_t seq) {
+    __shared__ unsigned long long wq[4][10];
+    const uint32_t wv = threadIdx.x >> 6;
+    unsigned long long acc10[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    for (uint32_t b = threadIdx.x; b < nparts; b += blockDim.x)
+#pragma unroll
+        for (int q = 0; q < 10; q++) acc10[q] += part[(size_t)b * 10 + q];
+#pragma unroll
+    for (int q = 0; q < 10; q++) acc10[q] = wsum64(acc10[q]);
+    if ((threadIdx.x & 63) == 0)
+#pragma unroll
+        for (int q = 0; q < 10; q++) wq[wv][q] = acc10[q];
+    __syncthreads();
+    if (threadIdx.x < 10) {
+        unsigned long long s = 0;
+        for (uint32_t w = 0; w < blockDim.x / 64; w++) s += wq[w][threadIdx.x];
+        res->tstat[threadIdx.x] = s;
+    }
+    __syncthreads();
+    const uint32_t *src = reinterpret_cast<const uint32_t *>(res);
+    uint32_t *dst = reinterpret_cast<uint32_t *>(host_res);
+    for (uint32_t i = threadIdx.x; i < offsetof(DevRes, seq) / 4; i += blockDim.x) dst[i] = src[i];
+    __threadfence_system();
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store(&host_res->seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 /* One pass over the final table: distinct k-mers, total, and the first- and
  * last-base marginals (-> depth-1 trie frequencies and base composition). */
 __global__ void __launch_bounds__(256)
 k_table_stats(uint32_t *table, uint64_t n, int k, DevRes *res,
               unsigned long long *acc, unsigned long long *facc, int fresh, DevRes *host_res, uint32_t *done,
-              uint32_t seq, uint32_t *subs, int nsub, unsigned long long *part) {
-    unsigned long long *out = res->tstat;
+              uint32_t seq, uint32_t *subs, int nsub, unsigned long long *part, int split) {
     if (blockIdx.x == 0) {
         /* the feed's counters (facc, zero between feeds) join the engine's */
         if (threadIdx.x < ACC_N) {
@@ -1989,7 +2020,11 @@ k_table_stats(uint32_t *table, uint64_t n, int k, DevRes *res,
     }
     /* the last block to finish sums the partials, then publishes the whole
        result block to pinned host memory, sequence number last: the host
-       spins on it instead of a copy plus a stream synchronisation */
+       spins on it instead of a copy plus a stream synchronisation.  With
+       `split` (large tables: hundreds of blocks, whose release fences would
+       each write back the L2 the table was just written into) the blocks
+       stop here and k_table_final does that in a second launch. */
+    if (split) return;
     __shared__ uint32_t is_last;
     __threadfence();
     __syncthreads();
@@ -1997,35 +2032,13 @@ k_table_stats(uint32_t *table, uint64_t n, int k, DevRes *res,
     __syncthreads();
     if (!is_last) return;
     __threadfence();
-    {
-        /* every thread sums a strided share of the blocks, then the block */
-        unsigned long long acc10[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-        for (uint32_t b = threadIdx.x; b < gridDim.x; b += blockDim.x)
-#pragma unroll
-            for (int q = 0; q < 10; q++) acc10[q] += part[(size_t)b * 10 + q];
-#pragma unroll
-        for (int q = 0; q < 10; q++) acc10[q] = wsum64(acc10[q]);
-        __syncthreads();
-        if ((threadIdx.x & 63) == 0)
-#pragma unroll
-            for (int q = 0; q < 10; q++) wp[wv][q] = acc10[q];
-        __syncthreads();
-        if (threadIdx.x < 10) {
-            unsigned long long s = 0;
-            for (uint32_t w = 0; w < blockDim.x / 64; w++) s += wp[w][threadIdx.x];
-            out[threadIdx.x] = s;
-        }
-        __syncthreads();
-    }
-    const uint32_t *src = reinterpret_cast<const uint32_t *>(res);
-    uint32_t *dst = reinterpret_cast<uint32_t *>(host_res);
-    for (uint32_t i = threadIdx.x; i < offsetof(DevRes, seq) / 4; i += blockDim.x) dst[i] = src[i];
-    __threadfence_system();
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        *done = 0;
-        __hip_atomic_store(&host_res->seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
+    stats_publish(res, host_res, part, gridDim.x, seq);
+    if (threadIdx.x == 0) *done = 0;
+}
+
+__global__ void __launch_bounds__(256)
+k_table_final(DevRes *res, DevRes *host_res, const unsigned long long *part, uint32_t nparts, uint32_t seq) {
+    stats_publish(res, host_res, part, nparts, seq);
 }
 
 /* trie prefix presence, level d from level d+1 (or from the table at d = k-1) */
@@ -2219,6 +2232,7 @@ struct fk_engine {
     fk_opts opts{};
     uint64_t nbins = 0, nshort = 0, maskk = 0;
     int cus = 256;
+    uint32_t ts_blocks = 0;                   /* k_table_stats grid override (0 = default) */
     bool part = false;                        /* 8 <= k <= 12: partitioned counting (k_part) */
     bool sparse = false;                      /* 17 <= k <= 20: slots, sorted at finish (fk_sparse.hip) */
     uint64_t *d_slots = nullptr;              /* sparse: one u64 per byte fed (+1: the final short walk) */
@@ -2439,6 +2453,7 @@ extern "C" int fk_engine_create(int k, const fk_opts *opts, fk_engine **out) {
     if (const char *gt = getenv("FK_GENERAL_TILES")) e->general_tiles = (uint32_t)strtoul(gt, nullptr, 10);
     if (const char *ne = getenv("FK_NO_EVENTS")) e->timing = ne[0] != '1';
     if (const char *no = getenv("FK_NO_ONEPASS")) e->onepass = no[0] != '1';
+    if (const char *tb = getenv("FK_TS_BLOCKS")) e->ts_blocks = (uint32_t)strtoul(tb, nullptr, 10);
     if (e->opts.timing_every > 1) e->timing_every = (uint32_t)e->opts.timing_every;
     e->sparse = k > FK_K_MAX_DENSE;
     e->nbins = e->sparse ? 0 : 1ull << (2 * k);
@@ -2649,11 +2664,18 @@ static int launch_table_stats(fk_engine *e, bool zero_first, hipEvent_t stop = n
                               bool fresh = false) {
     if (zero_first) HIPCHK(hipMemsetAsync(e->d_res->tstat, 0, sizeof(e->d_res->tstat), e->stream));
     unsigned gd = (unsigned)std::min<uint64_t>((uint64_t)e->cus * 4, (e->nbins / 4 + 255) / 256 + 1);
+    if (e->ts_blocks) gd = std::min<unsigned>(e->ts_blocks, (unsigned)e->cus * 4);
+    const int split = gd > 16;   /* large tables: partials, then k_table_final */
     if (++e->res_seq == 0) e->res_seq = 1;
-    hipExtLaunchKernelGGL(k_table_stats, dim3(gd), dim3(256), 0, e->stream, nullptr, stop, 0, e->d_table,
-                          e->nbins, e->k, e->d_res, e->d_acc, e->d_facc, fresh ? 1 : 0, e->h_res_dev, e->d_done,
-                          e->res_seq, e->d_sub, (subs && e->d_sub) ? FK_SUBTABLES : 0, e->d_tpart);
+    hipExtLaunchKernelGGL(k_table_stats, dim3(gd), dim3(256), 0, e->stream, nullptr, split ? nullptr : stop, 0,
+                          e->d_table, e->nbins, e->k, e->d_res, e->d_acc, e->d_facc, fresh ? 1 : 0, e->h_res_dev,
+                          e->d_done, e->res_seq, e->d_sub, (subs && e->d_sub) ? FK_SUBTABLES : 0, e->d_tpart, split);
     HIPCHK(hipGetLastError());
+    if (split) {
+        hipExtLaunchKernelGGL(k_table_final, dim3(1), dim3(256), 0, e->stream, nullptr, stop, 0, e->d_res,
+                              e->h_res_dev, e->d_tpart, gd, e->res_seq);
+        HIPCHK(hipGetLastError());
+    }
     return FK_OK;
 }
 
@@ -2685,8 +2707,9 @@ static int launch_part(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t l
     const int k = e->k;
     pg.sh = std::min(15, 2 * k - 6);                       /* >= 64 slices, <= 2^15 bins (128 KiB) each */
     pg.nslices = 1u << (2 * k - pg.sh);
-    pg.region_stride = (uint64_t)FK_WAVES_PER_BLOCK * g.cpw * FK_CHUNK_BYTES;   /* >= windows per block */
     pg.rounds = (uint32_t)((g.cpw * FK_CHUNK_TILES + 2) / PART_TILES_PER_BATCH + 2);   /* rows (batches) per block */
+    /* >= windows per block, plus each row's padding to a multiple of 8 codes */
+    pg.region_stride = (uint64_t)FK_WAVES_PER_BLOCK * g.cpw * FK_CHUNK_BYTES + 8ull * pg.rounds;
     pg.rows = g.grid * pg.rounds;
     const uint64_t ncodes = (uint64_t)g.grid * pg.region_stride, nidx = (uint64_t)pg.nslices * pg.rows;
     if (ncodes > e->codes_cap) {
