@@ -31,7 +31,11 @@ $(BUILD)/fk_sparse.o: $(CSRC)/fk_sparse.hip $(CSRC)/fk_sparse.h
 	@mkdir -p $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -c -x hip $< -o $@
 
-$(LIB): $(BUILD)/fk_engine.o $(BUILD)/fk_sparse.o $(BUILD)/fk_writer.o
+$(BUILD)/fk_ingest.o: $(CSRC)/fk_ingest.hip $(ROOT)include/findkmer.h
+	@mkdir -p $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -c -x hip $< -o $@
+
+$(LIB): $(BUILD)/fk_engine.o $(BUILD)/fk_sparse.o $(BUILD)/fk_ingest.o $(BUILD)/fk_writer.o
 	@mkdir -p $(LIBDIR)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -lpthread
 

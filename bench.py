@@ -47,7 +47,7 @@ def parse():
     ap.add_argument("--cpu-sample-bytes", type=int, default=0, help="0 = auto (~10-20 s of reference CPU work)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--chrom", type=int, default=CHROM,
-                    help="multi-GPU stream: an 'N' run break every this many bases")
+                    help="streams longer than this (pure ACGT): an 'N' run break every this many bases, a genome of chromosomes (0 = one run)")
     ap.add_argument("--timing-every", type=int, default=4,
                     help="time the count kernel with HIP events on every Nth step")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
@@ -145,7 +145,8 @@ def main():
     w = fk.synth_device(buf.data_ptr(), size, n + halo_bases, args.seed + first // 32, frame)
     assert w == size
     nbytes = size - halo
-    if world > 1 and L == 0:
+    chrom_breaks = L == 0 and args.chrom > 0 and world * n > args.chrom
+    if chrom_breaks:
         # one N-GB stream as a genome of CHROM-base chromosomes: an 'N' at
         # every multiple of CHROM (as in real genomes, no run reaches the
         # reference's int32 seqSize wrap at 2^31 bases)
@@ -202,7 +203,7 @@ def main():
             total = int(w_t.item())
             merged = int(table_t.to(torch.int64).remainder(1 << 32).sum().item())
             assert merged == total, (merged, total)
-        want = expected_windows(world * n, k, args.chrom) if world > 1 and L == 0 else run_windows(world * n, k)
+        want = expected_windows(world * n, k, args.chrom) if chrom_breaks else run_windows(world * n, k)
         assert total == want, (total, want)
 
     ms_step = dt / args.steps * 1e3
@@ -235,9 +236,10 @@ def main():
         "data": "synthetic (splitmix64 uniform ACGT, generated in HBM)",
         "config": {
             "workload": (f"k={k} over a {n / 1e9:g} G-base synthetic "
-                         + ("ACGT stream" if L == 0 else f"FASTA ({L}-col lines)")
-                         + " per GPU (BASELINE.json configs[1])" if k == 6 and L == 0 else
-                         f"k={k} over a {n / 1e9:g} G-base synthetic " + ("ACGT stream" if L == 0 else f"FASTA ({L}-col lines)") + " per GPU"),
+                         + ("ACGT stream" if L == 0 else f"FASTA ({L}-col lines)") + " per GPU"
+                         + (f", one {world * n / 1e9:g} G-base genome of {args.chrom / 1e9:g} G-base chromosomes"
+                            if chrom_breaks else "")
+                         + (" (BASELINE.json configs[1])" if (k, L, n) == (6, 0, 1_000_000_000) else "")),
             "k": k, "bases_per_gpu": n, "input_bytes_per_gpu": nbytes,
             "parallelism": f"shard{world}",
         },

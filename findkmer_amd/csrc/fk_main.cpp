@@ -16,7 +16,14 @@
  *    once more and exits 1;
  *  - an input ending inside a '>' line makes the reference spin forever
  *    (:1005); this program reports it and exits 1.
- * Extension: FINDKMER_GPUS=N splits the scan over N GPUs of this node.
+ * Extensions:
+ *  - with -q 1 the file is first made device-resident by parallel pread into
+ *    pinned buffers + async H2D (fk_input_load), then scanned in one feed;
+ *    -q 0 (per-record progress lines) and non-regular files stream it in
+ *    256 MiB pieces (FINDKMER_INGEST=stream forces that path);
+ *  - --sweep KMAX: run k, k+1, ..., KMAX over one read of the file, writing
+ *    each k's files exactly as separate invocations would (what
+ *    k6thru11fullANDupstream.sh does with six processes per file).
  */
 #include "findkmer.h"
 
@@ -47,6 +54,10 @@ static struct conf {
     long double zThreshold;
     int zThresholdEnable;
 } config;
+
+static int sweep_kmax = -1;          /* --sweep KMAX (extension) */
+static fk_input *g_input = nullptr;  /* device-resident copy of the sequence file */
+static bool g_input_tried = false;
 
 static void check_file(const char *filename, const char *mode) {   /* :233-242 */
     FILE *file = fopen(filename, mode);
@@ -217,6 +228,13 @@ static int parse_arguments(int argc, char **argv) {                 /* :394-490 
                 config.zThresholdEnable = 1;
                 config.zThreshold = atoi(argv[i]);
             }
+        } else if (strcmp(argv[i], "--sweep") == 0) {
+            i++;
+            if (i == argc) {
+                fprintf(stderr, "Largest k for --sweep is missing.\nUsage is \"-k 6 --sweep 11\".\n");
+                exit(EXIT_FAILURE);
+            }
+            sweep_kmax = atoi(argv[i]);
         } else {
             fprintf(stderr, "Ignoring invalid option %s\n", argv[i]);
             if (config.suppressOutputEnable == 0) {
@@ -324,13 +342,19 @@ static int scan_file(fk_engine *e, FILE *f, fk_result *res) {
     return fk_engine_finish(e, res);
 }
 
-int main(int argc, char *argv[]) {                                  /* :1292-1379 */
-    init_conf();
-    usage();
-    if (!parse_arguments(argc, argv)) {
-        usage();
-        return EXIT_FAILURE;
-    }
+/* The whole file, device-resident (fk_input_load), in one feed. */
+static int scan_device(fk_engine *e, fk_result *res) {
+    const uint8_t *d = nullptr;
+    uint64_t len = 0;
+    int rc = fk_input_info(g_input, &d, &len, nullptr, nullptr);
+    if (rc) return rc;
+    rc = fk_engine_feed(e, d, len, 1);
+    if (rc) return rc;
+    return fk_engine_finish(e, res);
+}
+
+/* One k: the reference's main() from print_conf() on (:1303-1379). */
+static int run_k(int argc) {
     print_conf(argc);
     unsigned long maxNumberOfNodes = estimate_RAM_usage();
     (void)maxNumberOfNodes;
@@ -348,16 +372,30 @@ int main(int argc, char *argv[]) {                                  /* :1292-137
     }
     rewind(config.sequence_file_pointer);
 
+    /* quiet runs print nothing per record: load the file to HBM once (and
+       reuse it for every k of a sweep) */
+    if (config.suppressOutputEnable != 0 && !g_input_tried) {
+        g_input_tried = true;
+        const char *ing = getenv("FINDKMER_INGEST");
+        if (!ing || strcmp(ing, "stream") != 0) {
+            int lrc = fk_input_load(config.sequence_file, -1, 0, &g_input);
+            if (lrc == FK_E_OOM || lrc == FK_E_HIP || lrc == FK_E_NO_DEVICE) die_engine(lrc);
+            if (lrc) g_input = nullptr;   /* not a regular file: stream it */
+        }
+    }
+    const bool on_device = g_input != nullptr && config.suppressOutputEnable != 0;
+
     fk_opts opts;
     memset(&opts, 0, sizeof opts);
     opts.device = -1;
+    if (on_device) fk_input_info(g_input, nullptr, nullptr, &opts.device, nullptr);
     opts.want_nodes = 1;
     opts.collect_unknown = 1;
     fk_engine *eng = nullptr;
     int rc = fk_engine_create(config.k, &opts, &eng);
     if (rc) die_engine(rc);
     fk_result res;
-    rc = scan_file(eng, config.sequence_file_pointer, &res);
+    rc = on_device ? scan_device(eng, &res) : scan_file(eng, config.sequence_file_pointer, &res);
     if (rc == FK_E_ROLLOVER) {                                       /* :642-648 */
         const char *m = "\n\n!!! COUNTER ROLLOVER DETECTED! \nIncrease the number of bits used for the counter variable if you have the source code, else use a smaller sequence file.\n\n";
         fprintf(stderr, "%s", m);
@@ -421,4 +459,33 @@ int main(int argc, char *argv[]) {                                  /* :1292-137
         fprintf(stderr, "Sequence file close error! This is likely ok though.\n");
     }
     return 0;
+}
+
+int main(int argc, char *argv[]) {                                  /* :1292-1379 */
+    init_conf();
+    usage();
+    if (!parse_arguments(argc, argv)) {
+        usage();
+        return EXIT_FAILURE;
+    }
+    const bool explicit_out = config.out_set;
+    const int kfirst = config.k ? config.k : DEFAULT_K_VALUE;
+    int klast = kfirst;
+    if (sweep_kmax >= 0) {
+        if (explicit_out || sweep_kmax < kfirst || sweep_kmax > 20) {
+            fprintf(stderr, "--sweep %d: needs %d <= KMAX <= 20 and no -e (one output file per k)\n", sweep_kmax,
+                    kfirst);
+            return EXIT_FAILURE;
+        }
+        klast = sweep_kmax;
+    }
+    int rc = 0;
+    for (int k = kfirst; k <= klast && rc == 0; k++) {
+        config.k = k;
+        if (!explicit_out) config.out_set = false;
+        if (k > kfirst) usage();   /* stdout == the separate runs' stdout, concatenated */
+        rc = run_k(argc);
+    }
+    if (g_input) fk_input_destroy(g_input);
+    return rc;
 }

@@ -202,6 +202,22 @@ int  fk_synth_device(uint8_t *dev_out, uint64_t cap, uint64_t n_bases,
                      uint64_t seed, int fasta_line, void *stream,
                      uint64_t *written);
 
+/* ---- file ingest (replaces the reference's per-byte fgetc reads of
+ * config.sequence_file_pointer, findKmer.cpp:988, with a device-resident
+ * copy of the whole file) --------------------------------------------------
+ * fk_input_load: `threads` host threads (<= 0: up to 8) pread() the regular
+ * file at `path` in 32 MiB chunks into pinned buffers and copy them
+ * asynchronously into one device buffer on `device` (-1: current device),
+ * overlapping reads with copies.  The buffer is 16-B aligned and can be fed
+ * to any number of engines on that device (fk_engine_feed(..., 1)).
+ * Returns FK_E_IO for unreadable or non-regular files (pipes: stream with
+ * fk_engine_feed instead). */
+typedef struct fk_input fk_input;
+int  fk_input_load(const char *path, int device, int threads, fk_input **out);
+int  fk_input_info(const fk_input *in, const uint8_t **dev_ptr, uint64_t *len,
+                   int *device, double *seconds /* load wall time */);
+void fk_input_destroy(fk_input *in);
+
 /* ---- host side of the boundary: byte-identical output writers ---------- */
 
 /* statistics() (:491-565): writes "<k>mer_Base_Stats_Of_<file>.txt" content to
