@@ -145,13 +145,16 @@ def main():
     w = fk.synth_device(buf.data_ptr(), size, n + halo_bases, args.seed + first // 32, frame)
     assert w == size
     nbytes = size - halo
-    chrom_breaks = L == 0 and args.chrom > 0 and world * n > args.chrom
+    # one N-GB stream as a genome of CHROM-base chromosomes: an 'N' at every
+    # base index that is a multiple of CHROM (as in real genomes, no run
+    # reaches the reference's int32 seqSize wrap at 2^31 bases).  FASTA
+    # framing: single-GPU streams only (base b sits at byte 11 + b + b // L).
+    chrom_breaks = args.chrom > 0 and world * n > args.chrom and (L == 0 or world == 1)
     if chrom_breaks:
-        # one N-GB stream as a genome of CHROM-base chromosomes: an 'N' at
-        # every multiple of CHROM (as in real genomes, no run reaches the
-        # reference's int32 seqSize wrap at 2^31 bases)
-        for b in range((first // args.chrom + 1) * args.chrom, first + size, args.chrom):
-            buf[b - first] = ord("N")
+        for b in range((max(first, 0) // args.chrom + 1) * args.chrom, first + n + halo_bases, args.chrom):
+            off = b - first if L == 0 else 11 + b + b // L
+            assert chr(buf[off].item()) in "ACGT", (b, off)
+            buf[off] = ord("N")
     torch.cuda.synchronize()
 
     # the count kernel's HIP events on every 4th step of the timed region

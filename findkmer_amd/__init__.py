@@ -105,6 +105,9 @@ SIGNATURES = [
     ("fk_count", ctypes.c_int, [_P, ctypes.c_uint64, ctypes.c_int, ctypes.POINTER(FkOpts), _U32P, ctypes.POINTER(FkResult)]),
     ("fk_count_multi", ctypes.c_int, [_P, ctypes.c_uint64, ctypes.c_int, ctypes.c_int, ctypes.POINTER(FkOpts), _U32P, ctypes.POINTER(FkResult)]),
     ("fk_synth_device", ctypes.c_int, [_P, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int, _P, _U64P]),
+    ("fk_input_load", ctypes.c_int, [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.POINTER(_P)]),
+    ("fk_input_info", ctypes.c_int, [_P, ctypes.POINTER(_P), _U64P, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_double)]),
+    ("fk_input_destroy", None, [_P]),
     ("fk_write_stats", ctypes.c_int, [ctypes.c_char_p, ctypes.c_int, ctypes.POINTER(FkResult), _P, ctypes.POINTER(ctypes.c_double)]),
     ("fk_write_rows", ctypes.c_int, [_P, ctypes.c_int, _U32P, ctypes.POINTER(ctypes.c_double), ctypes.c_uint64, ctypes.c_int, ctypes.c_double, ctypes.c_int]),
     ("fk_write_rows_sparse", ctypes.c_int, [_P, ctypes.c_int, _U64P, _U32P, ctypes.c_uint64, ctypes.POINTER(ctypes.c_double), ctypes.c_uint64, ctypes.c_int, ctypes.c_double, ctypes.c_int]),
@@ -315,6 +318,36 @@ def synth_device(ptr, cap, n_bases, seed, fasta_line=0, stream=None):
     w = ctypes.c_uint64()
     _check(lib().fk_synth_device(ptr, cap, n_bases, seed, fasta_line, stream, ctypes.byref(w)), "synth")
     return w.value
+
+
+class DeviceInput:
+    """A file made device-resident by fk_input_load (parallel pread into
+    pinned buffers, async H2D); feed it with Engine.feed_device(ptr, len)."""
+
+    def __init__(self, path, device=-1, threads=0):
+        self.h = _P()
+        _check(lib().fk_input_load(os.fsencode(path), device, threads, ctypes.byref(self.h)), "input_load")
+        ptr, n, dev, sec = _P(), ctypes.c_uint64(), ctypes.c_int(), ctypes.c_double()
+        _check(lib().fk_input_info(self.h, ctypes.byref(ptr), ctypes.byref(n), ctypes.byref(dev),
+                                   ctypes.byref(sec)), "input_info")
+        self.ptr, self.len, self.device, self.seconds = ptr.value or 0, n.value, dev.value, sec.value
+
+    def close(self):
+        if self.h:
+            lib().fk_input_destroy(self.h)
+            self.h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def synth_size(n_bases, fasta_line=0):

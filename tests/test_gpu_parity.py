@@ -343,6 +343,25 @@ def test_cli_stream_ingest_matches_reference(case, manifest, tmp_path):
     assert p.stdout == golden_file(case, "stdout")
 
 
+@pytest.mark.parametrize("k", [3, 7, 11])
+def test_device_input_matches_oracle(k, tmp_path):
+    """fk_input_load (Python DeviceInput) -> one device feed == the oracle"""
+    data = _long_header_input(21 + k, (40 << 20) + 12345)   # > one 32 MiB ingest chunk, ragged
+    path = tmp_path / "in.fa"
+    path.write_bytes(data)
+    t_o, r_o, ub_o = oracle.count_dense(data, k, unknown_cap=1 << 24)
+    with fk.DeviceInput(str(path)) as inp, fk.Engine(k, collect_unknown=True) as e:
+        assert inp.len == len(data)
+        e.feed_device(inp.ptr, inp.len)
+        rc, r = e.finish()
+        t = e.table()
+        ub = e.unknown_bytes()
+    assert rc == fk.FK_OK
+    assert np.array_equal(t, t_o)
+    assert r.windows == r_o.windows and list(r.base_count) == list(r_o.base_count)
+    assert ub == ub_o
+
+
 def test_cli_sweep_matches_separate_runs(tmp_path):
     """--sweep 5..9 over one device-resident read == five separate runs
     (stdout concatenated, the same CSV and stats files per k)"""
