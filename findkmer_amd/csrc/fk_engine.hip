@@ -1319,10 +1319,18 @@ k_redo(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint
  * k_bucket_count: one block per slice (and group of rows) counts its runs in
  *   an LDS slice of 2^sh bins and adds the slice into the table.
  */
-#define PART_BLOCK 512u
+/* waves per k_part block.  4-wave blocks (four per CU) make k_part itself
+   ~4% faster, but halve the batch, so k_bucket_count reads twice as many,
+   shorter runs: the k=11 step is 5% slower and k=12 30% slower (measured,
+   tools/exp_part.sh) */
+#ifndef PART_WAVES
+#define PART_WAVES 8u
+#endif
+#define PART_BLOCK (PART_WAVES * 64u)
+#define PART_BLOCKS_PER_CU (16u / PART_WAVES)
 #define PART_TILES_PER_BATCH 2u                                /* tiles per wave per batch */
-#define PART_MAX_BATCH (PART_TILES_PER_BATCH * FK_WAVES_PER_BLOCK * FK_TILE_BYTES)   /* windows per batch */
-#define PART_MAX_SLICES 1024u
+#define PART_MAX_BATCH (PART_TILES_PER_BATCH * PART_WAVES * FK_TILE_BYTES)   /* windows per batch */
+#define PART_MAX_SLICES 512u                                   /* k = 12: 2^24 bins / 2^15 per slice */
 
 struct PartGeo {
     uint16_t *codes;       /* per block: region_stride entries */
@@ -1424,7 +1432,7 @@ __device__ __forceinline__ bool part_batch(const Ctx &cx, const PartGeo &pg, con
     return any_more;
 }
 
-__global__ void __launch_bounds__(PART_BLOCK, 2)
+__global__ void __launch_bounds__(PART_BLOCK, PART_BLOCKS_PER_CU)
 k_part(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint32_t *table,
        uint32_t *shortcnt, unsigned long long *acc, DevRes *res, RangeRec *rr, uint64_t nchunks, uint64_t cpw,
        const XState *d_init, int has_init, PartGeo pg) {
@@ -1440,7 +1448,7 @@ k_part(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint
     for (uint32_t i = threadIdx.x; i < pg.nslices; i += PART_BLOCK) hist[i] = 0;
     Ctx cx{buf, len, lo, table, nullptr, shortcnt, acc, res, maskk, 0, k, nullptr};
     const int lane = threadIdx.x & 63;
-    const uint64_t wave = blockIdx.x * FK_WAVES_PER_BLOCK + wave_in_block();
+    const uint64_t wave = blockIdx.x * PART_WAVES + wave_in_block();
     const uint64_t c0 = wave * cpw, c1 = min(c0 + cpw, nchunks);
     const bool has = c0 < c1;
     RangeRec hdr_r;
@@ -2709,9 +2717,10 @@ static int launch_part(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t l
     pg.nslices = 1u << (2 * k - pg.sh);
     pg.rounds = (uint32_t)((g.cpw * FK_CHUNK_TILES + 2) / PART_TILES_PER_BATCH + 2);   /* rows (batches) per block */
     /* >= windows per block, plus each row's padding to a multiple of 8 codes */
-    pg.region_stride = (uint64_t)FK_WAVES_PER_BLOCK * g.cpw * FK_CHUNK_BYTES + 8ull * pg.rounds;
-    pg.rows = g.grid * pg.rounds;
-    const uint64_t ncodes = (uint64_t)g.grid * pg.region_stride, nidx = (uint64_t)pg.nslices * pg.rows;
+    pg.region_stride = (uint64_t)PART_WAVES * g.cpw * FK_CHUNK_BYTES + 8ull * pg.rounds;
+    const unsigned pgrid = (unsigned)((g.nranges + PART_WAVES - 1) / PART_WAVES);   /* same ranges, smaller blocks */
+    pg.rows = pgrid * pg.rounds;
+    const uint64_t ncodes = (uint64_t)pgrid * pg.region_stride, nidx = (uint64_t)pg.nslices * pg.rows;
     if (ncodes > e->codes_cap) {
         hipFree(e->d_codes);
         e->d_codes = nullptr;
@@ -2733,7 +2742,7 @@ static int launch_part(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t l
     pg.codes = e->d_codes;
     pg.idx = e->d_pidx;
     pg.row_base = e->d_prow;
-    hipExtLaunchKernelGGL(k_part, dim3(g.grid), dim3(PART_BLOCK), 0, e->stream, tev(e, 0), tev(e, 1), 0, buf, len,
+    hipExtLaunchKernelGGL(k_part, dim3(pgrid), dim3(PART_BLOCK), 0, e->stream, tev(e, 0), tev(e, 1), 0, buf, len,
                           lo, e->k, e->maskk, e->d_table, e->d_short, e->d_facc, e->d_res, e->d_rr, g.nchunks,
                           g.cpw, e->d_state, has_init, pg);
     HIPCHK(hipGetLastError());
