@@ -1327,10 +1327,11 @@ k_redo(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint
 #define PART_WAVES 8u
 #endif
 #define PART_BLOCK (PART_WAVES * 64u)
-#define PART_BLOCKS_PER_CU (16u / PART_WAVES)
-#define PART_TILES_PER_BATCH 2u                                /* tiles per wave per batch */
-#define PART_MAX_BATCH (PART_TILES_PER_BATCH * PART_WAVES * FK_TILE_BYTES)   /* windows per batch */
-#define PART_MAX_SLICES 512u                                   /* k = 12: 2^24 bins / 2^15 per slice */
+/* tiles per wave per batch: 2 single-window tiles or 4 pair tiles fill the
+   same LDS batch (a pair tile hands over half as many entries) */
+#define PART_TILES(PAIRS) ((PAIRS) ? 4u : 2u)
+#define PART_MAX_BATCH (2u * PART_WAVES * FK_TILE_BYTES)   /* entries per batch */
+#define PART_MAX_SLICES 1024u   /* k = 11 pairs: 2^24 / 2^15 pair slices + 2^22 / 2^15 single slices */
 
 struct PartGeo {
     uint16_t *codes;       /* per block: region_stride entries */
@@ -1341,34 +1342,58 @@ struct PartGeo {
     uint32_t rows;         /* rows in all: grid * rounds */
     uint32_t nslices;
     uint32_t sh;           /* slice index = code >> sh; stored code = code & (2^sh - 1) */
+    uint32_t npair;        /* pairs mode: slices [0, npair) hold (k+1)-mer pairs, the rest single k-mers */
+    uint32_t *pairs;       /* pairs mode: 4^(k+1) pair bins (k_bucket_count -> k_pair_fold) */
+    uint32_t *singles;     /* pairs mode: 4^k single k-mer bins */
 };
+
+/* Every entry a fast tile's Emit hands to the partition, as f(slice, low).
+ * Single windows: the 16 windows ending in each half (15 when slot 0 is not
+ * a window).  PAIRS (as half_windows<H_PAIRS> does in LDS): the (k+1)-mers
+ * ending at the odd slots 1, 3, .., 15 of each half, each standing for the
+ * two k-mers ending at slots (2j, 2j+1); without a real slot 0 the first one
+ * is the single k-mer at slot 1, in slices npair and up. */
+template <bool PAIRS, typename F>
+__device__ __forceinline__ void part_entries(const Emit &em, uint32_t mk, uint32_t m1, uint32_t sh, uint32_t lowm,
+                                             uint32_t npair, F &&f) {
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+        const uint32_t C = h ? em.BC : em.AC, S2 = h ? em.B2 : em.A2;
+        const bool skip0 = h ? em.h1 : em.h0;
+        if (PAIRS) {
+            const uint32_t v0 = __builtin_amdgcn_alignbit(C, S2, 28u);
+            const uint32_t c0 = skip0 ? (v0 & mk) : (v0 & m1);
+            f(skip0 ? npair + (c0 >> sh) : (c0 >> sh), c0 & lowm);
+#pragma unroll
+            for (int j = 1; j < 8; j++) {
+                const uint32_t v = (j < 7 ? __builtin_amdgcn_alignbit(C, S2, 28u - 4u * (uint32_t)j) : S2) & m1;
+                f(v >> sh, v & lowm);
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < 16; i++) {
+                const uint32_t v = (i < 15 ? __builtin_amdgcn_alignbit(C, S2, 2u * (15u - (uint32_t)i)) : S2) & mk;
+                if (i > 0 || !skip0) f(v >> sh, v & lowm);
+            }
+        }
+    }
+}
 
 /* The block-wide batch of one round: windows of the waves whose tile was
  * fast (have), counting-sorted by slice.  Every thread of the block calls
  * this the same number of times (it contains barriers). */
-__device__ __forceinline__ bool part_batch(const Ctx &cx, const PartGeo &pg, const Emit &e0, bool have0,
-                                           const Emit &e1, bool have1,
+template <bool PAIRS>
+__device__ __forceinline__ bool part_batch(const Ctx &cx, const PartGeo &pg, const Emit *es, const bool *haves,
                                            bool more, uint32_t row, uint32_t &blk_cursor, uint32_t *hist,
                                            uint32_t *cur, uint32_t *total, uint16_t *ent) {
+    constexpr int NT = PART_TILES(PAIRS);
     const uint32_t t = threadIdx.x, lane = t & 63;
     const uint32_t mk = (uint32_t)cx.maskk, sh = pg.sh, lowm = (1u << sh) - 1u;
+    const uint32_t m1 = (mk << 2) | 3u;
     /* 1: slice histogram */
 #pragma unroll
-    for (int tt = 0; tt < 2; tt++) {
-        const Emit &em = tt ? e1 : e0;
-        if (tt ? have1 : have0) {
-#pragma unroll
-            for (int h = 0; h < 2; h++) {
-                const uint32_t C = h ? em.BC : em.AC, S2 = h ? em.B2 : em.A2;
-                const bool skip0 = h ? em.h1 : em.h0;
-#pragma unroll
-                for (int i = 0; i < 16; i++) {
-                    const uint32_t v = (i < 15 ? __builtin_amdgcn_alignbit(C, S2, 2u * (15u - (uint32_t)i)) : S2) & mk;
-                    if (i > 0 || !skip0) atomicAdd(&hist[v >> sh], 1u);
-                }
-            }
-        }
-    }
+    for (int i = 0; i < NT; i++)
+        if (haves[i]) part_entries<PAIRS>(es[i], mk, m1, sh, lowm, pg.npair, [&](uint32_t b, uint32_t) { atomicAdd(&hist[b], 1u); });
     /* (the barrier also tells whether any wave has tiles left) */
     const bool any_more = __syncthreads_or(more);
     /* 2: exclusive scan of the slice counts (wave 0), index row */
@@ -1400,25 +1425,18 @@ __device__ __forceinline__ bool part_batch(const Ctx &cx, const PartGeo &pg, con
         if (lane == 0) pg.row_base[row] = blk_cursor;
     }
     __syncthreads();
-    /* 3: place each window at its slot */
+    /* 3: place each entry at its slot.  The codes are recomputed from the
+       Emit words (laundered, so the compiler cannot keep phase 1's codes
+       live across the barriers: that costs more VGPRs than it saves VALU) */
+    auto place = [&](uint32_t b, uint32_t low) {
+        const uint32_t p = atomicAdd(&cur[b], 1u);
+        ent[p] = (uint16_t)low;
+    };
 #pragma unroll
-    for (int tt = 0; tt < 2; tt++) {
-        const Emit &em = tt ? e1 : e0;
-        if (tt ? have1 : have0) {
-#pragma unroll
-            for (int h = 0; h < 2; h++) {
-                const uint32_t C = h ? em.BC : em.AC, S2 = h ? em.B2 : em.A2;
-                const bool skip0 = h ? em.h1 : em.h0;
-#pragma unroll
-                for (int i = 0; i < 16; i++) {
-                    const uint32_t v = (i < 15 ? __builtin_amdgcn_alignbit(C, S2, 2u * (15u - (uint32_t)i)) : S2) & mk;
-                    if (i > 0 || !skip0) {
-                        const uint32_t p = atomicAdd(&cur[v >> sh], 1u);
-                        ent[p] = (uint16_t)(v & lowm);
-                    }
-                }
-            }
-        }
+    for (int i = 0; i < NT; i++) {
+        Emit f = es[i];
+        asm volatile("" : "+v"(f.AC), "+v"(f.A2), "+v"(f.BC), "+v"(f.B2));
+        if (haves[i]) part_entries<PAIRS>(f, mk, m1, sh, lowm, pg.npair, place);
     }
     __syncthreads();
     /* 4: the sorted batch, contiguous, into the block's code region: 16-B
@@ -1432,7 +1450,8 @@ __device__ __forceinline__ bool part_batch(const Ctx &cx, const PartGeo &pg, con
     return any_more;
 }
 
-__global__ void __launch_bounds__(PART_BLOCK, PART_BLOCKS_PER_CU)
+template <bool PAIRS>
+__global__ void __launch_bounds__(PART_BLOCK, 4) /* 4 waves per SIMD (<= 128 VGPRs): two blocks per CU */
 k_part(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint32_t *table,
        uint32_t *shortcnt, unsigned long long *acc, DevRes *res, RangeRec *rr, uint64_t nchunks, uint64_t cpw,
        const XState *d_init, int has_init, PartGeo pg) {
@@ -1499,8 +1518,14 @@ k_part(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint
     uint64_t t = 0;
     bool done = !has || sp.ntiles == 0;
     uint32_t blk_cursor = 0, round = 0;
-    Emit stash{0, 0, 0, 0, false, false, false};
-    bool have_stash = false;
+    constexpr uint32_t NT = PART_TILES(PAIRS);
+    Emit stash[NT];
+    bool have_stash[NT];
+#pragma unroll
+    for (uint32_t i = 0; i < NT; i++) {
+        stash[i] = Emit{0, 0, 0, 0, false, false, false};
+        have_stash[i] = false;
+    }
     __syncthreads();
 #define FK_ROUND(X)                                                                  \
     {                                                                                \
@@ -1521,14 +1546,18 @@ k_part(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint
         }                                                                            \
         consume(X);                                                                  \
         FK_LOADP(X, t + 2);                                                          \
-        if (!(round & 1)) {                                                          \
-            stash = em;                                                              \
-            have_stash = have;                                                       \
-        } else {                                                                     \
-            const bool more_ = part_batch(cx, pg, stash, have_stash, em, have, !done, \
-                                          blockIdx.x * pg.rounds + (round >> 1), blk_cursor, hist, cur, \
-                                          &total, ent);                              \
-            if (!more_ || (round >> 1) + 1 >= pg.rounds) { round++; break; }         \
+        {   /* static stash slots (no dynamic register indexing) */                 \
+            const uint32_t ph_ = round % NT;                                         \
+            _Pragma("unroll") for (uint32_t i_ = 0; i_ < NT; i_++) if (ph_ == i_) {  \
+                stash[i_] = em;                                                      \
+                have_stash[i_] = have;                                               \
+            }                                                                        \
+            if (ph_ == NT - 1) {                                                     \
+                const bool more_ = part_batch<PAIRS>(cx, pg, stash, have_stash, !done, \
+                                                     blockIdx.x * pg.rounds + round / NT, blk_cursor, \
+                                                     hist, cur, &total, ent);        \
+                if (!more_ || round / NT + 1 >= pg.rounds) { round++; break; }       \
+            }                                                                        \
         }                                                                            \
         round++;                                                                     \
     }
@@ -1540,7 +1569,7 @@ k_part(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint
 #undef FK_ROUND
 #undef FK_LOADP
     /* rows the block did not reach are empty */
-    for (uint32_t r = (round + 1) >> 1; r < pg.rounds; r++) {
+    for (uint32_t r = (round + NT - 1) / NT; r < pg.rounds; r++) {
         const uint32_t row = blockIdx.x * pg.rounds + r;
         for (uint32_t b = threadIdx.x; b < pg.nslices; b += PART_BLOCK) pg.idx[(size_t)b * pg.rows + row] = 0;
         if (threadIdx.x == 0) pg.row_base[row] = blk_cursor;
@@ -1594,12 +1623,37 @@ k_bucket_count(PartGeo pg, uint32_t groups, uint32_t *table) {
         }
     }
     __syncthreads();
+    if (pg.pairs) {
+        /* pairs mode: the slice's bins, in kernel index order, into the pair
+           or single bins (k_pair_fold reduces them into the table) */
+        uint32_t *dst = b < pg.npair ? pg.pairs + ((size_t)b << pg.sh) : pg.singles + ((size_t)(b - pg.npair) << pg.sh);
+        for (uint32_t i = threadIdx.x; i < nb; i += blockDim.x) {
+            const uint32_t v = slice[i];
+            if (groups == 1) dst[i] = v;   /* this block owns the slice: every bin written */
+            else if (v) atomicAdd(&dst[i], v);
+        }
+        return;
+    }
     for (uint32_t i = threadIdx.x; i < nb; i += blockDim.x) {
         const uint32_t v = slice[i];
         if (!v) continue;
         uint32_t *dst = &table[fk_sigma(((uint64_t)b << pg.sh) | i)];
         if (groups == 1) *dst += v;   /* this block owns the slice */
         else atomicAdd(dst, v);
+    }
+}
+
+/* pairs mode: every k-mer x (kernel order) is the prefix of the pairs
+ * 4x + b and the suffix of the pairs b*4^k + x (a pair stands for both of
+ * its k-mers), plus the single windows counted at x */
+__global__ void __launch_bounds__(256)
+k_pair_fold(const uint32_t *pairs, const uint32_t *singles, uint64_t nbins, uint32_t *table) {
+    for (uint64_t x = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; x < nbins; x += (uint64_t)gridDim.x * blockDim.x) {
+        const uint4 pre = reinterpret_cast<const uint4 *>(pairs)[x];
+        uint32_t v = pre.x + pre.y + pre.z + pre.w + singles[x];
+#pragma unroll
+        for (int b = 0; b < 4; b++) v += pairs[(uint64_t)b * nbins + x];
+        if (v) table[fk_sigma(x)] += v;
     }
 }
 
@@ -2251,6 +2305,9 @@ struct fk_engine {
     uint16_t *d_codes = nullptr;              /* k_part: block code regions */
     uint32_t *d_pidx = nullptr, *d_prow = nullptr;   /* k_part: slice-major run index, row bases */
     uint64_t codes_cap = 0, pidx_cap = 0, prow_cap = 0;
+    uint32_t *d_pairs = nullptr;              /* k_part pairs mode: 4^(k+1) pair bins + 4^k single bins */
+    uint64_t pair_cap = 0;
+    int part_pairs_kmax = 11;                 /* pairs mode for k <= this (FK_PART_PAIRS_KMAX; 0 = off) */
     uint32_t general_tiles = FK_COUNT_GENERAL_TILES;   /* per range in k_count (env FK_GENERAL_TILES) */
     /* device state */
     uint32_t *d_table = nullptr, *d_short = nullptr;
@@ -2408,6 +2465,7 @@ extern "C" void fk_engine_destroy(fk_engine *e) {
     hipSetDevice(e->dev);
     if (e->stream) hipStreamSynchronize(e->stream);
     hipFree(e->d_table); hipFree(e->d_short); hipFree(e->d_sub);
+    hipFree(e->d_pairs);
     hipFree(e->d_codes); hipFree(e->d_pidx); hipFree(e->d_prow); hipFree(e->d_acc); hipFree(e->d_res); hipFree(e->d_tmp);
     hipFree(e->d_state); hipFree(e->d_rr); hipFree(e->d_rtrue);
     hipFree(e->d_redo); hipFree(e->d_tf); hipFree(e->d_stage); hipFree(e->d_resume);
@@ -2461,6 +2519,7 @@ extern "C" int fk_engine_create(int k, const fk_opts *opts, fk_engine **out) {
     if (const char *gt = getenv("FK_GENERAL_TILES")) e->general_tiles = (uint32_t)strtoul(gt, nullptr, 10);
     if (const char *ne = getenv("FK_NO_EVENTS")) e->timing = ne[0] != '1';
     if (const char *no = getenv("FK_NO_ONEPASS")) e->onepass = no[0] != '1';
+    if (const char *pp = getenv("FK_PART_PAIRS_KMAX")) e->part_pairs_kmax = atoi(pp);
     if (const char *tb = getenv("FK_TS_BLOCKS")) e->ts_blocks = (uint32_t)strtoul(tb, nullptr, 10);
     if (e->opts.timing_every > 1) e->timing_every = (uint32_t)e->opts.timing_every;
     e->sparse = k > FK_K_MAX_DENSE;
@@ -2713,9 +2772,26 @@ static int wait_results(fk_engine *e) {
 static int launch_part(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t lo, const Geo &g, int has_init) {
     PartGeo pg;
     const int k = e->k;
-    pg.sh = std::min(15, 2 * k - 6);                       /* >= 64 slices, <= 2^15 bins (128 KiB) each */
-    pg.nslices = 1u << (2 * k - pg.sh);
-    pg.rounds = (uint32_t)((g.cpw * FK_CHUNK_TILES + 2) / PART_TILES_PER_BATCH + 2);   /* rows (batches) per block */
+    /* k <= 11: (k+1)-mer pairs at every other base (half the entries), plus
+       the single k-mers at the first slot of halves with a '\n' */
+    const bool pairs = k <= e->part_pairs_kmax;
+    const int kb = pairs ? k + 1 : k;                      /* bits of a pair (or window) code: 2 kb */
+    pg.sh = std::min(15, 2 * kb - 6);                      /* >= 64 slices, <= 2^15 bins (128 KiB) each */
+    pg.npair = pairs ? 1u << (2 * kb - pg.sh) : 0u;
+    pg.nslices = pairs ? pg.npair + (1u << (2 * k - pg.sh)) : 1u << (2 * k - pg.sh);
+    pg.pairs = pg.singles = nullptr;
+    if (pairs) {
+        const uint64_t need = e->nbins * 5;                 /* 4^(k+1) pair bins + 4^k single bins */
+        if (need > e->pair_cap) {
+            hipFree(e->d_pairs);
+            e->d_pairs = nullptr;
+            if (hipMalloc((void **)&e->d_pairs, need * sizeof(uint32_t)) != hipSuccess) return FK_E_OOM;
+            e->pair_cap = need;
+        }
+        pg.pairs = e->d_pairs;
+        pg.singles = e->d_pairs + e->nbins * 4;
+    }
+    pg.rounds = (uint32_t)((g.cpw * FK_CHUNK_TILES + 2) / PART_TILES(pairs) + 2);   /* rows (batches) per block */
     /* >= windows per block, plus each row's padding to a multiple of 8 codes */
     pg.region_stride = (uint64_t)PART_WAVES * g.cpw * FK_CHUNK_BYTES + 8ull * pg.rounds;
     const unsigned pgrid = (unsigned)((g.nranges + PART_WAVES - 1) / PART_WAVES);   /* same ranges, smaller blocks */
@@ -2742,14 +2818,21 @@ static int launch_part(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t l
     pg.codes = e->d_codes;
     pg.idx = e->d_pidx;
     pg.row_base = e->d_prow;
-    hipExtLaunchKernelGGL(k_part, dim3(pgrid), dim3(PART_BLOCK), 0, e->stream, tev(e, 0), tev(e, 1), 0, buf, len,
-                          lo, e->k, e->maskk, e->d_table, e->d_short, e->d_facc, e->d_res, e->d_rr, g.nchunks,
-                          g.cpw, e->d_state, has_init, pg);
+    hipExtLaunchKernelGGL(pairs ? k_part<true> : k_part<false>, dim3(pgrid), dim3(PART_BLOCK), 0, e->stream,
+                          tev(e, 0), tev(e, 1), 0, buf, len, lo, e->k, e->maskk, e->d_table, e->d_short, e->d_facc,
+                          e->d_res, e->d_rr, g.nchunks, g.cpw, e->d_state, has_init, pg);
     HIPCHK(hipGetLastError());
     const uint32_t groups = std::max<uint32_t>(1, (uint32_t)e->cus / pg.nslices);
+    if (pairs && groups > 1) HIPCHK(hipMemsetAsync(e->d_pairs, 0, e->nbins * 5 * sizeof(uint32_t), e->stream));
     hipLaunchKernelGGL(k_bucket_count, dim3(pg.nslices * groups), dim3(1024), (size_t)sizeof(uint32_t) << pg.sh,
                        e->stream, pg, groups, e->d_table);
     HIPCHK(hipGetLastError());
+    if (pairs) {
+        const unsigned fg = (unsigned)std::min<uint64_t>((uint64_t)e->cus * 4, (e->nbins + 255) / 256);
+        hipLaunchKernelGGL(k_pair_fold, dim3(fg), dim3(256), 0, e->stream, e->d_pairs, e->d_pairs + e->nbins * 4,
+                           e->nbins, e->d_table);
+        HIPCHK(hipGetLastError());
+    }
     return FK_OK;
 }
 
