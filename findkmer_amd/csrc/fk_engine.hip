@@ -1598,27 +1598,50 @@ k_bucket_count(PartGeo pg, uint32_t groups, uint32_t *table) {
     const uint32_t *ix = pg.idx + (size_t)b * pg.rows;
     const uint4 *g4 = reinterpret_cast<const uint4 *>(pg.codes);
     /* four lanes share a run and read it as contiguous 64-byte pieces (one
-       request per quad instead of one per lane) */
+       request per quad instead of one per lane).  A quad takes four rows at
+       once: their index words, row bases and first 128 bytes of codes are
+       all in flight before any is used (a run is ~50-250 codes, so one
+       dependent chain per run would leave the CU waiting on latency) */
     const uint32_t sub = threadIdx.x & 3u;
     const uint32_t quads = blockDim.x / 4, step = groups * quads;
-    for (uint32_t r = g * quads + threadIdx.x / 4; r < pg.rows; r += step) {
-        const uint32_t e = ix[r];
-        const uint32_t cnt = e & 0xFFFFu;
-        if (!cnt) continue;
-        const uint64_t s0 = (uint64_t)(r / pg.rounds) * pg.region_stride + pg.row_base[r] + (e >> 16), s1 = s0 + cnt;
-        const uint64_t q1 = (s1 + 7) >> 3;
-        for (uint64_t q = (s0 >> 3) + sub; q < q1; q += 16) {
-            uint4 v[4];
+    auto add16 = [&](const uint4 &v, uint64_t q, uint64_t s0, uint64_t s1) {
+        const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-            for (int u = 0; u < 4; u++) v[u] = q + 4 * u < q1 ? g4[q + 4 * u] : make_uint4(0, 0, 0, 0);
+        for (int h = 0; h < 8; h++) {
+            const uint64_t at = q * 8 + h;
+            if (at >= s0 && at < s1) atomicAdd(&slice[(w4[h >> 1] >> (16 * (h & 1))) & 0xFFFFu], 1u);
+        }
+    };
+    for (uint32_t r = g * quads + threadIdx.x / 4; r < pg.rows; r += 4 * step) {
+        uint32_t e[4], rb[4];
 #pragma unroll
-            for (int u = 0; u < 4; u++) {
-                const uint32_t w4[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+        for (int j = 0; j < 4; j++) e[j] = r + j * step < pg.rows ? ix[r + j * step] : 0u;
 #pragma unroll
-                for (int h = 0; h < 8; h++) {
-                    const uint64_t at = (q + 4 * u) * 8 + h;
-                    if (at >= s0 && at < s1) atomicAdd(&slice[(w4[h >> 1] >> (16 * (h & 1))) & 0xFFFFu], 1u);
-                }
+        for (int j = 0; j < 4; j++) rb[j] = (e[j] & 0xFFFFu) ? pg.row_base[r + j * step] : 0u;
+        uint64_t s0[4], s1[4];
+        uint4 v[4][2];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            s0[j] = (uint64_t)((r + j * step) / pg.rounds) * pg.region_stride + rb[j] + (e[j] >> 16);
+            s1[j] = s0[j] + (e[j] & 0xFFFFu);
+            const uint64_t q0 = (s0[j] >> 3) + sub, q1 = (s1[j] + 7) >> 3;
+#pragma unroll
+            for (int u = 0; u < 2; u++) v[j][u] = q0 + 4 * u < q1 ? g4[q0 + 4 * u] : make_uint4(0, 0, 0, 0);
+        }
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const uint64_t q0 = (s0[j] >> 3) + sub, q1 = (s1[j] + 7) >> 3;
+#pragma unroll
+            for (int u = 0; u < 2; u++)
+                if (q0 + 4 * u < q1) add16(v[j][u], q0 + 4 * u, s0[j], s1[j]);
+            /* the rest of a long run */
+            for (uint64_t q = q0 + 8; q < q1; q += 16) {
+                uint4 w[4];
+#pragma unroll
+                for (int u = 0; u < 4; u++) w[u] = q + 4 * u < q1 ? g4[q + 4 * u] : make_uint4(0, 0, 0, 0);
+#pragma unroll
+                for (int u = 0; u < 4; u++)
+                    if (q + 4 * u < q1) add16(w[u], q + 4 * u, s0[j], s1[j]);
             }
         }
     }
