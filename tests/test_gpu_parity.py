@@ -406,6 +406,23 @@ def test_cli_device_ingest_large(tmp_path):
         assert (a / f).read_bytes() == (b / f).read_bytes(), f
 
 
+@pytest.mark.parametrize("k", [8, 10, 11, 12])
+@pytest.mark.parametrize("kind", ["polyA", "period7", "fasta_polyA"])
+def test_partition_skewed(k, kind):
+    """8 <= k <= 12 on inputs whose windows all fall in one or a few table
+    slices: k_part batches of one 16 K-32 K-entry run, k_bucket_count's
+    long-run loop, pair and single slices (FASTA halves with a newline)"""
+    n = 24 << 20
+    if kind == "polyA":
+        data = b"A" * n
+    elif kind == "period7":
+        data = (b"ACGTTGC" * (n // 7 + 1))[:n]
+    else:
+        line = b"A" * 60 + b"\n"
+        data = b">x\n" + line * (n // len(line))
+    assert_same(data, k, want_nodes=False)
+
+
 def _long_header_input(seed, n):
     """ACGT runs with '>' lines longer than the 256-byte halo, so ranges
     start inside a header their halo cannot see the start of (the one-pass
