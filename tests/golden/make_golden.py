@@ -35,6 +35,11 @@ def cases():
     c.append(("ffbyte_k3", "ffbyte.bin", ["-q", "1", "-k", "3", "-p", "ffbyte.bin"]))
     c.append(("shortruns_k5", "shortruns.txt", ["-q", "1", "-k", "5", "-p", "shortruns.txt"]))
     c.append(("empty_k3", "empty.txt", ["-q", "1", "-k", "3", "-p", "empty.txt"]))
+    # config 5 (k6thru11fullANDupstream.sh): an upstream-like FASTA
+    # (tools/make_upstream.py upstream1m.fas 1e6 3), k = 6..11 with a z filter
+    c.append(("up_k6", "upstream1m.fas", ["-q", "1", "-k", "6", "-p", "upstream1m.fas"]))
+    for k in range(6, 12):
+        c.append((f"up_k{k}_z3", "upstream1m.fas", ["-q", "1", "-k", str(k), "-z", "3", "-p", "upstream1m.fas"]))
     # 17 <= k <= 20: the sparse table
     c.append(("rand_k17", "rand120k.fa", ["-q", "1", "-k", "17", "-p", "rand120k.fa"]))
     c.append(("rand_k19_z4", "rand120k.fa", ["-q", "1", "-k", "19", "-z", "4", "-p", "rand120k.fa"]))

@@ -294,7 +294,8 @@ def test_full_size_properties(k):
 GOLD_CLI = ["test_k6", "test_k1", "test_k11", "test_k6_q0", "test_k0_default7", "test_k6_export",
             "test_k6_badopt", "edge_k3", "rand_k5", "rand_k6_z3", "rand_k8", "rand_k4_z2",
             "rand_k11", "missing_k3", "ffbyte_k3", "shortruns_k5", "empty_k3",
-            "test_k15", "test_k20", "rand_k17", "rand_k19_z4", "shortruns_k18", "edge_k20", "ffbyte_k17"]
+            "test_k15", "test_k20", "rand_k17", "rand_k19_z4", "shortruns_k18", "edge_k20", "ffbyte_k17",
+            "up_k6", "up_k11_z3"]
 
 
 @pytest.mark.parametrize("case", GOLD_CLI)
@@ -341,6 +342,24 @@ def test_cli_stream_ingest_matches_reference(case, manifest, tmp_path):
         got = open(tmp_path / rec["name"], "rb").read()
         assert hashlib.sha256(got).hexdigest() == rec["sha256"], (kind, got[:300])
     assert p.stdout == golden_file(case, "stdout")
+
+
+def test_cli_sweep_matches_reference_goldens(manifest, tmp_path):
+    """config 5: `-k 6 -z 3 --sweep 11` over the upstream-like FASTA writes,
+    for every k, the CSV and stats files the reference wrote in six runs"""
+    import hashlib
+    name = "upstream1m.fas"
+    shutil.copy(os.path.join(REPO, "tests", "golden", "inputs", name), tmp_path / name)
+    p = _run_cli(["-q", "1", "-k", "6", "-z", "3", "--sweep", "11", "-p", name], tmp_path)
+    assert p.returncode == 0, p.stderr.decode()
+    want_stdout = b""
+    for k in range(6, 12):
+        entry = manifest[f"up_k{k}_z3"]
+        for kind, rec in entry["files"].items():
+            got = open(tmp_path / rec["name"], "rb").read()
+            assert hashlib.sha256(got).hexdigest() == rec["sha256"], (k, kind)
+        want_stdout += golden_file(f"up_k{k}_z3", "stdout")
+    assert p.stdout == want_stdout
 
 
 @pytest.mark.parametrize("k", [3, 7, 11])
