@@ -170,13 +170,15 @@ def main():
         else:
             # shard, stitch entry states (all-gather of 96-B summaries), merge
             # tables (all-reduce): findkmer_amd/dist.py
-            fkdist.count_sharded(eng, buf.data_ptr() + halo, nbytes, halo, table_t)
+            fkdist.count_sharded(eng, buf.data_ptr() + halo, nbytes, halo, table_t, times=phase_s)
         # an ablation build (FINDKMER_LIB) may leave the table incomplete
         rc, r = eng.finish(allow=(fk.FK_OK, fk.FK_E_ROLLOVER) if os.environ.get("FINDKMER_LIB") else (fk.FK_OK,))
         return r
 
+    phase_s = {}
     for _ in range(args.warmup):
         step()
+    phase_s.clear()
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
@@ -253,6 +255,9 @@ def main():
             "algorithmic_bytes": algo_bytes,
         },
     }
+    if phase_s:
+        # rank 0's host time per step in each phase of the sharded pass
+        out["phase_ms_per_step"] = {k_: v / args.steps * 1e3 for k_, v in phase_s.items()}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         # ~15 s of reference CPU work: ~76 Mbases/s at k=6, ~3 Mbases/s at k=11
         sample = args.cpu_sample_bytes or (1 << 30 if k <= 7 else 48 << 20)
