@@ -108,6 +108,7 @@ SIGNATURES = [
     ("fk_input_load", ctypes.c_int, [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.POINTER(_P)]),
     ("fk_input_info", ctypes.c_int, [_P, ctypes.POINTER(_P), _U64P, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_double)]),
     ("fk_input_destroy", None, [_P]),
+    ("fk_input_headers", ctypes.c_int, [_P, ctypes.c_int, _U64P, _U64P, ctypes.c_uint64, _U64P]),
     ("fk_write_stats", ctypes.c_int, [ctypes.c_char_p, ctypes.c_int, ctypes.POINTER(FkResult), _P, ctypes.POINTER(ctypes.c_double)]),
     ("fk_write_rows", ctypes.c_int, [_P, ctypes.c_int, _U32P, ctypes.POINTER(ctypes.c_double), ctypes.c_uint64, ctypes.c_int, ctypes.c_double, ctypes.c_int]),
     ("fk_write_rows_sparse", ctypes.c_int, [_P, ctypes.c_int, _U64P, _U32P, ctypes.c_uint64, ctypes.POINTER(ctypes.c_double), ctypes.c_uint64, ctypes.c_int, ctypes.c_double, ctypes.c_int]),
@@ -331,6 +332,19 @@ class DeviceInput:
         _check(lib().fk_input_info(self.h, ctypes.byref(ptr), ctypes.byref(n), ctypes.byref(dev),
                                    ctypes.byref(sec)), "input_info")
         self.ptr, self.len, self.device, self.seconds = ptr.value or 0, n.value, dev.value, sec.value
+
+    def headers(self, k):
+        """(offsets of the '>' that start comment lines, baseCounter at each)
+        as numpy uint64 arrays; raises FindKmerError(FK_E_STATE) when the
+        file needs the streamed path"""
+        import numpy as np
+        n = ctypes.c_uint64()
+        _check(lib().fk_input_headers(self.h, k, None, None, 0, ctypes.byref(n)), "input_headers")
+        pos = np.zeros(max(1, n.value), dtype=np.uint64)
+        bases = np.zeros(max(1, n.value), dtype=np.uint64)
+        _check(lib().fk_input_headers(self.h, k, pos.ctypes.data_as(_U64P), bases.ctypes.data_as(_U64P), n.value,
+                                      ctypes.byref(n)), "input_headers")
+        return pos[:n.value], bases[:n.value]
 
     def close(self):
         if self.h:

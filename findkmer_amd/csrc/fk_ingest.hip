@@ -146,3 +146,176 @@ extern "C" void fk_input_destroy(fk_input *in) {
     }
     delete in;
 }
+
+/*
+ * Record progress for `-q 0` runs.  The reference prints, at every '>' that
+ * starts a comment line, "Read %llu bases\n>" + the line (findKmer.cpp:
+ * 996-1002), with baseCounter as of that byte.  baseCounter grows by k when a
+ * run reaches k bases and by 1 per base after that (:1040-1057), so at a
+ * header start it is the sum of g(L) = (L >= k ? L : 0) over the runs closed
+ * so far (a header start closes the current run) -- exact while every run is
+ * shorter than 2^31 bases (the reference's int32 seqSize, :977) and no 0xFF
+ * byte ends the scan early (:988); otherwise the caller uses the engine's
+ * streamed path.
+ *
+ * k_hdr_traj: one thread per 4 KiB chunk computes the chunk's two possible
+ * trajectories of the (in_header, run) state: entering outside a header
+ * (mode 0, with an unknown run length carried in) or inside one (mode 1: the
+ * chunk is skipped up to its first '\n').  The host composes the chunks in
+ * order (a few ns each), then k_hdr_list writes each chunk's header starts
+ * from the trajectory it actually takes.
+ */
+#define HDR_CHUNK 4096u
+
+struct HdrTraj {
+    uint64_t inner;      /* sum of g(L) over runs closed after the first break */
+    uint32_t head;       /* bases before the first break (joins the run carried in) */
+    uint32_t tail;       /* bases after the last break */
+    uint32_t nhdr;       /* header starts */
+    uint8_t broke, exit_hdr, ff, pad;
+};
+
+template <bool WRITE>
+__device__ void hdr_walk(const uint8_t *buf, uint64_t beg, uint64_t end, int mode, int k, HdrTraj &t,
+                         uint64_t *pos_out, uint64_t *inner_out) {
+    t = HdrTraj{0, 0, 0, 0, 0, 0, 0, 0};
+    int in_hdr = mode;
+    uint32_t L = 0;
+    uint32_t n = 0;
+    for (uint64_t p = beg; p < end; p++) {
+        const uint8_t c = buf[p];
+        if (in_hdr) {
+            if (c == '\n') in_hdr = 0;
+            continue;
+        }
+        if (c == 'A' || c == 'C' || c == 'G' || c == 'T') {
+            L++;
+        } else if (c == '\n') {
+        } else if (c == 0xFF) {
+            t.ff = 1;
+            break;
+        } else {
+            if (!t.broke) {
+                t.head = L;
+                t.broke = 1;
+            } else if (L >= (uint32_t)k) {
+                t.inner += L;
+            }
+            L = 0;
+            if (c == '>') {
+                if (WRITE) {
+                    pos_out[n] = p;
+                    inner_out[n] = t.inner;
+                }
+                n++;
+                in_hdr = 1;
+            }
+        }
+    }
+    if (!t.broke) t.head = L;
+    t.tail = L;
+    t.nhdr = n;
+    t.exit_hdr = (uint8_t)in_hdr;
+}
+
+__global__ void k_hdr_traj(const uint8_t *buf, uint64_t len, uint64_t nchunks, int k, HdrTraj *traj) {
+    const uint64_t c = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (c >= nchunks) return;
+    const uint64_t beg = c * HDR_CHUNK, end = std::min(len, beg + HDR_CHUNK);
+    hdr_walk<false>(buf, beg, end, 0, k, traj[2 * c], nullptr, nullptr);
+    hdr_walk<false>(buf, beg, end, 1, k, traj[2 * c + 1], nullptr, nullptr);
+}
+
+__global__ void k_hdr_list(const uint8_t *buf, uint64_t len, uint64_t nchunks, int k, const uint8_t *mode,
+                           const uint64_t *off, uint64_t *pos, uint64_t *inner) {
+    const uint64_t c = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (c >= nchunks) return;
+    const uint64_t beg = c * HDR_CHUNK, end = std::min(len, beg + HDR_CHUNK);
+    HdrTraj t;
+    hdr_walk<true>(buf, beg, end, mode[c], k, t, pos + off[c], inner + off[c]);
+}
+
+extern "C" int fk_input_headers(fk_input *in, int k, uint64_t *pos, uint64_t *bases, uint64_t cap, uint64_t *n) {
+    if (!in || !n || k < 1 || k > 20 || (cap && (!pos || !bases))) return FK_E_INVALID;
+    if (hipSetDevice(in->device) != hipSuccess) return FK_E_HIP;
+    const uint64_t nchunks = (in->len + HDR_CHUNK - 1) / HDR_CHUNK;
+    *n = 0;
+    if (!nchunks) return FK_OK;
+    HdrTraj *d_traj = nullptr;
+    uint8_t *d_mode = nullptr;
+    uint64_t *d_off = nullptr, *d_pos = nullptr, *d_inner = nullptr;
+    int rc = FK_OK;
+    std::vector<HdrTraj> traj(2 * nchunks);
+    std::vector<uint8_t> mode(nchunks);
+    std::vector<uint64_t> off(nchunks), cbase(nchunks);
+    uint64_t total = 0;
+    const unsigned grid = (unsigned)((nchunks + 255) / 256);
+    do {
+        if (hipMalloc((void **)&d_traj, 2 * nchunks * sizeof(HdrTraj)) != hipSuccess) { rc = FK_E_OOM; break; }
+        hipLaunchKernelGGL(k_hdr_traj, dim3(grid), dim3(256), 0, nullptr, in->d, in->len, nchunks, k, d_traj);
+        if (hipGetLastError() != hipSuccess ||
+            hipMemcpy(traj.data(), d_traj, 2 * nchunks * sizeof(HdrTraj), hipMemcpyDeviceToHost) != hipSuccess) {
+            rc = FK_E_HIP;
+            break;
+        }
+        /* compose the chunks in stream order */
+        int in_hdr = 0;
+        uint64_t L = 0, base = 0;
+        auto g = [k](uint64_t x) { return x >= (uint64_t)k ? x : 0ull; };
+        for (uint64_t c = 0; c < nchunks && rc == FK_OK; c++) {
+            const int m = in_hdr;
+            const HdrTraj &t = traj[2 * c + (size_t)m];
+            mode[c] = (uint8_t)m;
+            off[c] = total;
+            if (t.ff) { rc = FK_E_STATE; break; }   /* 0xFF ends the scan: streamed path */
+            const uint64_t L0 = m == 1 ? 0 : L;
+            if (t.broke) {
+                cbase[c] = base + g(L0 + t.head);
+                base = cbase[c] + t.inner;   /* every run closed in the chunk; the tail run stays open */
+                L = t.tail;
+            } else {
+                cbase[c] = base;
+                L = L0 + t.head;
+            }
+            total += t.nhdr;
+            in_hdr = t.exit_hdr;
+            if (L >= 0x7FFFFFFFull) { rc = FK_E_STATE; break; }   /* int32 seqSize zone: streamed path */
+        }
+        if (rc) break;
+        if (total > 0) {
+            if (hipMalloc((void **)&d_mode, nchunks) != hipSuccess ||
+                hipMalloc((void **)&d_off, nchunks * sizeof(uint64_t)) != hipSuccess ||
+                hipMalloc((void **)&d_pos, total * sizeof(uint64_t)) != hipSuccess ||
+                hipMalloc((void **)&d_inner, total * sizeof(uint64_t)) != hipSuccess) {
+                rc = FK_E_OOM;
+                break;
+            }
+            if (hipMemcpy(d_mode, mode.data(), nchunks, hipMemcpyHostToDevice) != hipSuccess ||
+                hipMemcpy(d_off, off.data(), nchunks * sizeof(uint64_t), hipMemcpyHostToDevice) != hipSuccess) {
+                rc = FK_E_HIP;
+                break;
+            }
+            hipLaunchKernelGGL(k_hdr_list, dim3(grid), dim3(256), 0, nullptr, in->d, in->len, nchunks, k, d_mode,
+                               d_off, d_pos, d_inner);
+            if (hipGetLastError() != hipSuccess) { rc = FK_E_HIP; break; }
+        }
+        *n = total;
+        if (cap) {
+            std::vector<uint64_t> inner((size_t)std::min(cap, total));
+            const uint64_t m = std::min(cap, total);
+            if (m && (hipMemcpy(pos, d_pos, m * sizeof(uint64_t), hipMemcpyDeviceToHost) != hipSuccess ||
+                      hipMemcpy(inner.data(), d_inner, m * sizeof(uint64_t), hipMemcpyDeviceToHost) != hipSuccess)) {
+                rc = FK_E_HIP;
+                break;
+            }
+            /* chunk of each header start -> its baseCounter */
+            for (uint64_t i = 0; i < m; i++) bases[i] = cbase[pos[i] / HDR_CHUNK] + inner[i];
+        }
+    } while (0);
+    hipFree(d_traj);
+    hipFree(d_mode);
+    hipFree(d_off);
+    hipFree(d_pos);
+    hipFree(d_inner);
+    return rc;
+}

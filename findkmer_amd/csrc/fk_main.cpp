@@ -31,6 +31,8 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
 
 #include <iostream>
 #include <string>
@@ -342,6 +344,40 @@ static int scan_file(fk_engine *e, FILE *f, fk_result *res) {
     return fk_engine_finish(e, res);
 }
 
+/* -q 0 on a device-resident file: the progress lines of every comment line
+   (:996-1002) come from fk_input_headers, the header text from the file.
+   Returns FK_E_STATE when the file needs the streamed path. */
+static int print_progress(int k) {
+    uint64_t n = 0;
+    int rc = fk_input_headers(g_input, k, nullptr, nullptr, 0, &n);
+    if (rc) return rc;
+    std::vector<uint64_t> pos((size_t)n + 1), bases((size_t)n + 1);
+    rc = fk_input_headers(g_input, k, pos.data(), bases.data(), n, &n);
+    if (rc) return rc;
+    /* the header text from a read-only mapping of the file */
+    const int fd = fileno(config.sequence_file_pointer);
+    struct stat sb;
+    if (fstat(fd, &sb) != 0) return FK_E_IO;
+    const size_t size = (size_t)sb.st_size;
+    const uint8_t *m = nullptr;
+    if (size) {
+        void *p = mmap(nullptr, size, PROT_READ, MAP_PRIVATE, fd, 0);
+        if (p == MAP_FAILED) return FK_E_IO;
+        madvise(p, size, MADV_SEQUENTIAL);
+        m = static_cast<const uint8_t *>(p);
+    }
+    for (uint64_t i = 0; i < n; i++) {
+        fprintf(stdout, "Read %llu bases\n%c", (unsigned long long)bases[(size_t)i], '>');   /* :997 */
+        const size_t b = (size_t)pos[(size_t)i] + 1;
+        const uint8_t *e = b < size ? static_cast<const uint8_t *>(memchr(m + b, '\n', size - b)) : nullptr;
+        const size_t end = e ? (size_t)(e - m) : size;
+        if (end > b) fwrite(m + b, 1, end - b, stdout);       /* echo the line (:999-1002) */
+        if (e) fputc('\n', stdout);
+    }
+    if (m) munmap(const_cast<uint8_t *>(m), size);
+    return FK_OK;
+}
+
 /* The whole file, device-resident (fk_input_load), in one feed. */
 static int scan_device(fk_engine *e, fk_result *res) {
     const uint8_t *d = nullptr;
@@ -372,9 +408,8 @@ static int run_k(int argc) {
     }
     rewind(config.sequence_file_pointer);
 
-    /* quiet runs print nothing per record: load the file to HBM once (and
-       reuse it for every k of a sweep) */
-    if (config.suppressOutputEnable != 0 && !g_input_tried) {
+    /* load the file to HBM once (and reuse it for every k of a sweep) */
+    if (!g_input_tried) {
         g_input_tried = true;
         const char *ing = getenv("FINDKMER_INGEST");
         if (!ing || strcmp(ing, "stream") != 0) {
@@ -383,7 +418,13 @@ static int run_k(int argc) {
             if (lrc) g_input = nullptr;   /* not a regular file: stream it */
         }
     }
-    const bool on_device = g_input != nullptr && config.suppressOutputEnable != 0;
+    bool on_device = g_input != nullptr;
+    if (on_device && config.suppressOutputEnable == 0) {
+        /* -q 0: the per-record progress lines, from the device copy */
+        int prc = print_progress(config.k);
+        if (prc == FK_E_STATE) on_device = false;   /* 0xFF / int32 zone: the streamed path prints them */
+        else if (prc) die_engine(prc);
+    }
 
     fk_opts opts;
     memset(&opts, 0, sizeof opts);

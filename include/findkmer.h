@@ -217,6 +217,14 @@ int  fk_input_load(const char *path, int device, int threads, fk_input **out);
 int  fk_input_info(const fk_input *in, const uint8_t **dev_ptr, uint64_t *len,
                    int *device, double *seconds /* load wall time */);
 void fk_input_destroy(fk_input *in);
+/* The comment lines of the loaded file, for the reference's -q 0 progress
+ * output (findKmer.cpp:996-1002): the offset of every '>' that starts one, and
+ * baseCounter (valid bases counted so far, at k) as of that byte.  Computed
+ * on the device (k_hdr_traj / k_hdr_list).  *n = how many; at most cap are
+ * written.  FK_E_STATE when the counts are not expressible this way (a 0xFF
+ * byte ends the scan, or a run reaches the reference's int32 seqSize wrap):
+ * feed the file in pieces and use fk_engine_progress instead. */
+int  fk_input_headers(fk_input *in, int k, uint64_t *pos, uint64_t *bases, uint64_t cap, uint64_t *n);
 
 /* ---- host side of the boundary: byte-identical output writers ---------- */
 

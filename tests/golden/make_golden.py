@@ -38,6 +38,7 @@ def cases():
     # config 5 (k6thru11fullANDupstream.sh): an upstream-like FASTA
     # (tools/make_upstream.py upstream1m.fas 1e6 3), k = 6..11 with a z filter
     c.append(("up_k6", "upstream1m.fas", ["-q", "1", "-k", "6", "-p", "upstream1m.fas"]))
+    c.append(("up_k7_q0", "upstream1m.fas", ["-q", "0", "-k", "7", "-p", "upstream1m.fas"]))
     for k in range(6, 12):
         c.append((f"up_k{k}_z3", "upstream1m.fas", ["-q", "1", "-k", str(k), "-z", "3", "-p", "upstream1m.fas"]))
     # 17 <= k <= 20: the sparse table

@@ -24,7 +24,7 @@ CPU_CASES = [c for c in [
     "rand_k5", "rand_k6_z3", "rand_k8", "rand_k4_z2", "rand_k11",
     "missing_k3", "ffbyte_k3", "shortruns_k5",
     "rand_k17", "rand_k19_z4", "shortruns_k18", "edge_k20", "ffbyte_k17",
-    "up_k6", *(f"up_k{k}_z3" for k in range(6, 12)),
+    "up_k6", "up_k7_q0", *(f"up_k{k}_z3" for k in range(6, 12)),
 ]]
 
 

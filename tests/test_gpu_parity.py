@@ -295,7 +295,7 @@ GOLD_CLI = ["test_k6", "test_k1", "test_k11", "test_k6_q0", "test_k0_default7", 
             "test_k6_badopt", "edge_k3", "rand_k5", "rand_k6_z3", "rand_k8", "rand_k4_z2",
             "rand_k11", "missing_k3", "ffbyte_k3", "shortruns_k5", "empty_k3",
             "test_k15", "test_k20", "rand_k17", "rand_k19_z4", "shortruns_k18", "edge_k20", "ffbyte_k17",
-            "up_k6", "up_k11_z3"]
+            "up_k6", "up_k11_z3", "up_k7_q0"]
 
 
 @pytest.mark.parametrize("case", GOLD_CLI)
@@ -379,6 +379,42 @@ def test_device_input_matches_oracle(k, tmp_path):
     assert np.array_equal(t, t_o)
     assert r.windows == r_o.windows and list(r.base_count) == list(r_o.base_count)
     assert ub == ub_o
+
+
+def _header_mix(seed, n):
+    """many short records, '>' inside header lines, N runs, runs shorter
+    than k, lines of several widths, headers across 4 KiB chunk edges"""
+    rng = random.Random(seed)
+    out = bytearray()
+    while len(out) < n:
+        out += b">" + bytes(rng.choices(b"ACGTN> x", k=rng.randint(0, 5000 if rng.random() < 0.05 else 60))) + b"\n"
+        for _ in range(rng.randint(0, 4)):
+            seq = bytes(rng.choices(b"ACGT", k=rng.choice([1, 3, 6, 7, 50, 900, 6000])))
+            w = rng.choice([0, 60, 13])
+            if w:
+                seq = b"\n".join(seq[i:i + w] for i in range(0, len(seq), w))
+            out += seq + rng.choice([b"", b"N", b"NNN", b"\n", b"q"])
+    return bytes(out)
+
+
+@pytest.mark.parametrize("k", [1, 6, 7, 11])
+def test_cli_q0_progress_device_vs_stream(k, tmp_path):
+    """-q 0 progress lines: device path (fk_input_headers) == streamed path
+    (feeds split at every header, fk_engine_progress)"""
+    data = _header_mix(100 + k, 2_000_000)
+    a, b = tmp_path / "a", tmp_path / "b"
+    a.mkdir()
+    b.mkdir()
+    (a / "h.fa").write_bytes(data)
+    (b / "h.fa").write_bytes(data)
+    pa = _run_cli(["-q", "0", "-k", str(k), "-p", "h.fa"], a)
+    pb = _run_cli(["-q", "0", "-k", str(k), "-p", "h.fa"], b, {"FINDKMER_INGEST": "stream"})
+    assert pa.returncode == 0 and pb.returncode == 0, (pa.stderr[-500:], pb.stderr[-500:])
+    assert pa.stdout.count(b"Read ") > 500
+    assert pa.stdout == pb.stdout
+    assert pa.stderr == pb.stderr
+    for f in sorted(x.name for x in a.iterdir()):
+        assert (a / f).read_bytes() == (b / f).read_bytes(), f
 
 
 def test_cli_sweep_matches_separate_runs(tmp_path):
