@@ -1006,6 +1006,13 @@ __device__ __forceinline__ void block_summary(const Ctx &cx, const OnePassCfg *o
  * end) ends the wave's work: it appends a ResumeRec and k_resume continues
  * the range from there.  A range counted to its end gets its RangeRec here.
  */
+#ifdef FK_WAVE_TIMES   /* experiment build (tools/wave_times.sh): per-wave start / loop end / end */
+__device__ unsigned long long fk_dbg_wt[32768 * 4];
+extern "C" int fk_debug_wave_times(unsigned long long *out, int n) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(fk_dbg_wt), (size_t)n * 4 * sizeof(unsigned long long)) == hipSuccess ? 0 : -1;
+}
+#endif
+
 template <int HM>
 __global__ void __launch_bounds__(FK_BLOCK, 2)
 k_count(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint32_t *table,
@@ -1013,6 +1020,9 @@ k_count(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uin
         uint64_t nchunks, const XState *d_init, int has_init, uint64_t cpw, ResumeRec *resume,
         uint32_t general_tiles, uint32_t *subs, const OnePassCfg *opc, uint32_t op_flags) {
     extern __shared__ uint32_t lds_bins[];
+#ifdef FK_WAVE_TIMES
+    const unsigned long long wt0 = __builtin_amdgcn_s_memrealtime();
+#endif
     /* open the feed's result block (the kernels after this one in the
        stream accumulate into it) */
     if (blockIdx.x == 0) {
@@ -1176,10 +1186,21 @@ k_count(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uin
             }
         }
     }
+#ifdef FK_WAVE_TIMES
+    const unsigned long long wt1 = __builtin_amdgcn_s_memrealtime();
+#endif
     if (LDS_MODE(HM)) {
         lds_flush<HM>(cx);
         if ((op_flags & OP_ON) && threadIdx.x < 64) block_summary(cx, opc, rr, (nchunks + cpw - 1) / cpw);
     }
+#ifdef FK_WAVE_TIMES
+    if ((threadIdx.x & 63) == 0 && wave < 32768) {
+        fk_dbg_wt[wave * 4 + 0] = wt0;
+        fk_dbg_wt[wave * 4 + 1] = wt1;
+        fk_dbg_wt[wave * 4 + 2] = __builtin_amdgcn_s_memrealtime();
+        fk_dbg_wt[wave * 4 + 3] = __builtin_amdgcn_s_getreg((20) | (0 << 6) | ((4 - 1) << 11)) & 0xF;
+    }
+#endif
 }
 #undef FK_LOADI
 #undef FK_LOADT
@@ -2342,6 +2363,7 @@ struct fk_engine {
     bool onepass = true;                      /* env FK_NO_ONEPASS=1: off */
     BlockSum *d_bsum = nullptr;               /* per block of k_count */
     uint32_t *d_ctl = nullptr;                /* k_tail's finished-block count */
+    uint32_t ranges_per_wave = 1;             /* k <= 7: ranges per k_count wave slot (FK_RANGES_PER_WAVE) */
     OnePassCfg *d_opc = nullptr;
     bool op_pending = false;                  /* the last count_segment launched a one-pass k_count */
     bool op_fresh = false;                    /* ... which did a pending reset itself */
@@ -2542,6 +2564,7 @@ extern "C" int fk_engine_create(int k, const fk_opts *opts, fk_engine **out) {
     if (const char *gt = getenv("FK_GENERAL_TILES")) e->general_tiles = (uint32_t)strtoul(gt, nullptr, 10);
     if (const char *ne = getenv("FK_NO_EVENTS")) e->timing = ne[0] != '1';
     if (const char *no = getenv("FK_NO_ONEPASS")) e->onepass = no[0] != '1';
+    if (const char *rw = getenv("FK_RANGES_PER_WAVE")) e->ranges_per_wave = std::max(1u, (uint32_t)strtoul(rw, nullptr, 10));
     if (const char *pp = getenv("FK_PART_PAIRS_KMAX")) e->part_pairs_kmax = atoi(pp);
     if (const char *tb = getenv("FK_TS_BLOCKS")) e->ts_blocks = (uint32_t)strtoul(tb, nullptr, 10);
     if (e->opts.timing_every > 1) e->timing_every = (uint32_t)e->opts.timing_every;
@@ -2670,6 +2693,13 @@ static Geo geometry(const fk_engine *e, uint64_t len) {
     Geo g;
     g.nchunks = (len + FK_CHUNK_BYTES - 1) / FK_CHUNK_BYTES;
     uint64_t max_waves = (uint64_t)e->cus * blocks_per_cu(e) * FK_WAVES_PER_BLOCK;
+    /* k <= 7 (k_count counts in LDS): ranges_per_wave ranges per wave slot
+       of the chip, i.e. that many rounds of blocks (experiment knob, default
+       1).  Equal static ranges finish up to 35 % apart (tools/wave_times.py:
+       per-XCD means differ by ~18 %), but more rounds of smaller blocks do
+       not fix it -- the dispatcher deals blocks to the XCDs round-robin --
+       and cost LDS zero/flush per block: 4 rounds 0.29 ms vs 0.18 ms. */
+    if (!e->part && !e->sparse && LDS_MODE(hist_mode(e))) max_waves *= e->ranges_per_wave;
     g.cpw = std::max<uint64_t>(1, (g.nchunks + max_waves - 1) / max_waves);
     g.nranges = (g.nchunks + g.cpw - 1) / g.cpw;
     g.grid = (unsigned)std::max<uint64_t>(1, (g.nranges + FK_WAVES_PER_BLOCK - 1) / FK_WAVES_PER_BLOCK);
