@@ -11,8 +11,9 @@ states (fk_engine_feed_shard).  The path has exactly two exchange steps:
    entering state, handed to fk_engine_resolve, which recounts only what the
    guess got wrong (nothing, when the compact summaries applied).  If one
    does not apply, all ranks exchange the full summaries in a second round;
-2. table merge: one all-reduce of the 4^k count tables.  Counts are u32 in
-   the reference (findKmer.cpp:110); int32 sums are bitwise identical.
+2. table merge: one reduce of the 4^k count tables to rank 0 (the rank that
+   writes the outputs).  Counts are u32 in the reference (findKmer.cpp:110);
+   int32 sums are bitwise identical.
 
 The same functions run over RCCL (backend "nccl", device tensors, bench.py)
 and over gloo on the CPU (tests/test_dist_cpu.py).
@@ -62,16 +63,22 @@ def stitch_entry_state(summary_words, group=None, device=None):
     return entering
 
 
-def sum_tables(table, group=None):
-    """Sum the ranks' count tables in place (int32 tensor = u32 counts)."""
-    dist.all_reduce(table, op=dist.ReduceOp.SUM, group=group)
+def sum_tables(table, group=None, everywhere=False):
+    """Sum the ranks' count tables (int32 tensor = u32 counts) into rank 0's
+    `table` (the rank that writes the CSV): one reduce, half the bytes of an
+    all-reduce over the xGMI ring (16 MiB per GPU at k=11).  everywhere=True:
+    all-reduce, every rank gets the sum."""
+    if everywhere:
+        dist.all_reduce(table, op=dist.ReduceOp.SUM, group=group)
+    else:
+        dist.reduce(table, dst=0, op=dist.ReduceOp.SUM, group=group)
     return table
 
 
 def count_sharded(engine, ptr, nbytes, halo, table, group=None, times=None):
     """One sharded pass on this rank's GPU: count the shard, stitch the entry
     state, recount what the guess got wrong, and merge the tables into
-    `table` (int32 tensor of 4^k entries = u32 counts, identical on every rank
+    `table` (int32 tensor of 4^k entries = u32 counts, the sum on rank 0
     afterwards; on the GPU for RCCL, on the host for a gloo rehearsal).  The
     engine keeps its own shard's table and counters: finish() reports this
     shard's windows and bases (additive across ranks); distinct k-mers and
