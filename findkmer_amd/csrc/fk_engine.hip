@@ -1355,10 +1355,8 @@ k_redo(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint
 #define PART_MAX_SLICES 1024u   /* k = 11 pairs: 2^24 / 2^15 pair slices + 2^22 / 2^15 single slices */
 
 struct PartGeo {
-    uint16_t *codes;       /* per block: region_stride entries */
+    uint16_t *codes;       /* per row (batch): PART_MAX_BATCH entries at row * PART_MAX_BATCH */
     uint32_t *idx;         /* [slice][row]: (start << 16) | count */
-    uint32_t *row_base;    /* [row]: entries the block wrote before this row */
-    uint64_t region_stride;
     uint32_t rounds;       /* rows per block */
     uint32_t rows;         /* rows in all: grid * rounds */
     uint32_t nslices;
@@ -1405,7 +1403,7 @@ __device__ __forceinline__ void part_entries(const Emit &em, uint32_t mk, uint32
  * this the same number of times (it contains barriers). */
 template <bool PAIRS>
 __device__ __forceinline__ bool part_batch(const Ctx &cx, const PartGeo &pg, const Emit *es, const bool *haves,
-                                           bool more, uint32_t row, uint32_t &blk_cursor, uint32_t *hist,
+                                           bool more, uint32_t row, uint32_t *hist,
                                            uint32_t *cur, uint32_t *total, uint16_t *ent) {
     constexpr int NT = PART_TILES(PAIRS);
     const uint32_t t = threadIdx.x, lane = t & 63;
@@ -1443,7 +1441,6 @@ __device__ __forceinline__ bool part_batch(const Ctx &cx, const PartGeo &pg, con
             }
         }
         if (lane == 63) *total = inc;
-        if (lane == 0) pg.row_base[row] = blk_cursor;
     }
     __syncthreads();
     /* 3: place each entry at its slot.  The codes are recomputed from the
@@ -1460,14 +1457,14 @@ __device__ __forceinline__ bool part_batch(const Ctx &cx, const PartGeo &pg, con
         if (haves[i]) part_entries<PAIRS>(f, mk, m1, sh, lowm, pg.npair, place);
     }
     __syncthreads();
-    /* 4: the sorted batch, contiguous, into the block's code region: 16-B
-       pieces (rows start at multiples of 8 codes; the up to 7 codes past
-       the batch's end are padding no run covers) */
+    /* 4: the sorted batch into its row's fixed slot (a batch holds at most
+       PART_MAX_BATCH entries: a run's position needs no per-row base), as
+       16-B pieces; the up to 7 codes past the batch's end are padding no
+       run covers */
     const uint32_t n8 = (*total + 7u) >> 3;
-    uint4 *dst = reinterpret_cast<uint4 *>(pg.codes + (size_t)blockIdx.x * pg.region_stride + blk_cursor);
+    uint4 *dst = reinterpret_cast<uint4 *>(pg.codes + (size_t)row * PART_MAX_BATCH);
     const uint4 *src = reinterpret_cast<const uint4 *>(ent);
     for (uint32_t i = t; i < n8; i += PART_BLOCK) dst[i] = src[i];
-    blk_cursor += n8 << 3;
     return any_more;
 }
 
@@ -1538,7 +1535,7 @@ k_part(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint
     Counters cnt{0, 0, 0, 0, 0, FK_NO_EOF};
     uint64_t t = 0;
     bool done = !has || sp.ntiles == 0;
-    uint32_t blk_cursor = 0, round = 0;
+    uint32_t round = 0;
     constexpr uint32_t NT = PART_TILES(PAIRS);
     Emit stash[NT];
     bool have_stash[NT];
@@ -1575,7 +1572,7 @@ k_part(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint
             }                                                                        \
             if (ph_ == NT - 1) {                                                     \
                 const bool more_ = part_batch<PAIRS>(cx, pg, stash, have_stash, !done, \
-                                                     blockIdx.x * pg.rounds + round / NT, blk_cursor, \
+                                                     blockIdx.x * pg.rounds + round / NT, \
                                                      hist, cur, &total, ent);        \
                 if (!more_ || round / NT + 1 >= pg.rounds) { round++; break; }       \
             }                                                                        \
@@ -1593,7 +1590,6 @@ k_part(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint
     for (uint32_t r = (round + NT - 1) / NT; r < pg.rounds; r++) {
         const uint32_t row = blockIdx.x * pg.rounds + r;
         for (uint32_t b = threadIdx.x; b < pg.nslices; b += PART_BLOCK) pg.idx[(size_t)b * pg.rows + row] = 0;
-        if (threadIdx.x == 0) pg.row_base[row] = blk_cursor;
     }
     /* the range's record: transfer function, guess, observations */
     if (has) {
@@ -1620,9 +1616,10 @@ k_bucket_count(PartGeo pg, uint32_t groups, uint32_t *table) {
     const uint4 *g4 = reinterpret_cast<const uint4 *>(pg.codes);
     /* four lanes share a run and read it as contiguous 64-byte pieces (one
        request per quad instead of one per lane).  A quad takes four rows at
-       once: their index words, row bases and first 128 bytes of codes are
-       all in flight before any is used (a run is ~50-250 codes, so one
-       dependent chain per run would leave the CU waiting on latency) */
+       once: their first 128 bytes of codes and the next four rows' index
+       words are all in flight together (a run is ~50-250 codes, so one
+       dependent chain per run would leave the CU waiting on latency; rows
+       sit at fixed offsets, so a run's position needs no further load) */
     const uint32_t sub = threadIdx.x & 3u;
     const uint32_t quads = blockDim.x / 4, step = groups * quads;
     auto add16 = [&](const uint4 &v, uint64_t q, uint64_t s0, uint64_t s1) {
@@ -1633,17 +1630,22 @@ k_bucket_count(PartGeo pg, uint32_t groups, uint32_t *table) {
             if (at >= s0 && at < s1) atomicAdd(&slice[(w4[h >> 1] >> (16 * (h & 1))) & 0xFFFFu], 1u);
         }
     };
-    for (uint32_t r = g * quads + threadIdx.x / 4; r < pg.rows; r += 4 * step) {
-        uint32_t e[4], rb[4];
+    uint32_t en[4];   /* the next iteration's index words, loaded with this one's codes */
+    const uint32_t r00 = g * quads + threadIdx.x / 4;
 #pragma unroll
-        for (int j = 0; j < 4; j++) e[j] = r + j * step < pg.rows ? ix[r + j * step] : 0u;
+    for (int j = 0; j < 4; j++) en[j] = r00 + j * step < pg.rows ? ix[r00 + j * step] : 0u;
+    for (uint32_t r = r00; r < pg.rows; r += 4 * step) {
+        uint32_t e[4];
 #pragma unroll
-        for (int j = 0; j < 4; j++) rb[j] = (e[j] & 0xFFFFu) ? pg.row_base[r + j * step] : 0u;
+        for (int j = 0; j < 4; j++) e[j] = en[j];
+        const uint32_t rn = r + 4 * step;
+#pragma unroll
+        for (int j = 0; j < 4; j++) en[j] = rn + j * step < pg.rows ? ix[rn + j * step] : 0u;
         uint64_t s0[4], s1[4];
         uint4 v[4][2];
 #pragma unroll
         for (int j = 0; j < 4; j++) {
-            s0[j] = (uint64_t)((r + j * step) / pg.rounds) * pg.region_stride + rb[j] + (e[j] >> 16);
+            s0[j] = (uint64_t)(r + j * step) * PART_MAX_BATCH + (e[j] >> 16);
             s1[j] = s0[j] + (e[j] & 0xFFFFu);
             const uint64_t q0 = (s0[j] >> 3) + sub, q1 = (s1[j] + 7) >> 3;
 #pragma unroll
@@ -2347,8 +2349,8 @@ struct fk_engine {
     bool sp_done = false;                     /* fks holds the finished table */
     unsigned long long sp_nodes = 0, sp_roll = 0, sp_tstat[10] = {};
     uint16_t *d_codes = nullptr;              /* k_part: block code regions */
-    uint32_t *d_pidx = nullptr, *d_prow = nullptr;   /* k_part: slice-major run index, row bases */
-    uint64_t codes_cap = 0, pidx_cap = 0, prow_cap = 0;
+    uint32_t *d_pidx = nullptr;               /* k_part: slice-major run index */
+    uint64_t codes_cap = 0, pidx_cap = 0;
     uint32_t *d_pairs = nullptr;              /* k_part pairs mode: 4^(k+1) pair bins + 4^k single bins */
     uint64_t pair_cap = 0;
     int part_pairs_kmax = 11;                 /* pairs mode for k <= this (FK_PART_PAIRS_KMAX; 0 = off) */
@@ -2511,7 +2513,7 @@ extern "C" void fk_engine_destroy(fk_engine *e) {
     if (e->stream) hipStreamSynchronize(e->stream);
     hipFree(e->d_table); hipFree(e->d_short); hipFree(e->d_sub);
     hipFree(e->d_pairs);
-    hipFree(e->d_codes); hipFree(e->d_pidx); hipFree(e->d_prow); hipFree(e->d_acc); hipFree(e->d_res); hipFree(e->d_tmp);
+    hipFree(e->d_codes); hipFree(e->d_pidx); hipFree(e->d_acc); hipFree(e->d_res); hipFree(e->d_tmp);
     hipFree(e->d_state); hipFree(e->d_rr); hipFree(e->d_rtrue);
     hipFree(e->d_redo); hipFree(e->d_tf); hipFree(e->d_stage); hipFree(e->d_resume);
     hipFree(e->d_aggs); hipFree(e->d_flags);
@@ -2845,11 +2847,9 @@ static int launch_part(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t l
         pg.singles = e->d_pairs + e->nbins * 4;
     }
     pg.rounds = (uint32_t)((g.cpw * FK_CHUNK_TILES + 2) / PART_TILES(pairs) + 2);   /* rows (batches) per block */
-    /* >= windows per block, plus each row's padding to a multiple of 8 codes */
-    pg.region_stride = (uint64_t)PART_WAVES * g.cpw * FK_CHUNK_BYTES + 8ull * pg.rounds;
     const unsigned pgrid = (unsigned)((g.nranges + PART_WAVES - 1) / PART_WAVES);   /* same ranges, smaller blocks */
     pg.rows = pgrid * pg.rounds;
-    const uint64_t ncodes = (uint64_t)pgrid * pg.region_stride, nidx = (uint64_t)pg.nslices * pg.rows;
+    const uint64_t ncodes = (uint64_t)pg.rows * PART_MAX_BATCH, nidx = (uint64_t)pg.nslices * pg.rows;
     if (ncodes > e->codes_cap) {
         hipFree(e->d_codes);
         e->d_codes = nullptr;
@@ -2862,15 +2862,8 @@ static int launch_part(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t l
         if (hipMalloc((void **)&e->d_pidx, nidx * sizeof(uint32_t)) != hipSuccess) return FK_E_OOM;
         e->pidx_cap = nidx;
     }
-    if (pg.rows > e->prow_cap) {
-        hipFree(e->d_prow);
-        e->d_prow = nullptr;
-        if (hipMalloc((void **)&e->d_prow, (size_t)pg.rows * sizeof(uint32_t)) != hipSuccess) return FK_E_OOM;
-        e->prow_cap = pg.rows;
-    }
     pg.codes = e->d_codes;
     pg.idx = e->d_pidx;
-    pg.row_base = e->d_prow;
     hipExtLaunchKernelGGL(pairs ? k_part<true> : k_part<false>, dim3(pgrid), dim3(PART_BLOCK), 0, e->stream,
                           tev(e, 0), tev(e, 1), 0, buf, len, lo, e->k, e->maskk, e->d_table, e->d_short, e->d_facc,
                           e->d_res, e->d_rr, g.nchunks, g.cpw, e->d_state, has_init, pg);
