@@ -417,9 +417,11 @@ def test_cli_q0_progress_device_vs_stream(k, tmp_path):
         assert (a / f).read_bytes() == (b / f).read_bytes(), f
 
 
-def test_cli_sweep_matches_separate_runs(tmp_path):
-    """--sweep 5..9 over one device-resident read == five separate runs
-    (stdout concatenated, the same CSV and stats files per k)"""
+@pytest.mark.parametrize("k0,k1", [(5, 9), (15, 17)])
+def test_cli_sweep_matches_separate_runs(k0, k1, tmp_path):
+    """--sweep k0..k1 over one device-resident read == separate runs
+    (stdout concatenated, the same CSV and stats files per k); 15..17
+    crosses from the dense table to the sparse one"""
     name = "mix.fa"
     data = _long_header_input(11, 3 << 20)
     a, b = tmp_path / "a", tmp_path / "b"
@@ -428,16 +430,16 @@ def test_cli_sweep_matches_separate_runs(tmp_path):
     (a / name).write_bytes(data)
     (b / name).write_bytes(data)
     outs = []
-    for k in range(5, 10):
+    for k in range(k0, k1 + 1):
         p = _run_cli(["-q", "1", "-k", str(k), "-z", "2", "-p", name], a)
         assert p.returncode == 0, p.stderr.decode()
         outs.append(p)
-    p = _run_cli(["-q", "1", "-k", "5", "-z", "2", "--sweep", "9", "-p", name], b)
+    p = _run_cli(["-q", "1", "-k", str(k0), "-z", "2", "--sweep", str(k1), "-p", name], b)
     assert p.returncode == 0, p.stderr.decode()
     assert p.stdout == b"".join(o.stdout for o in outs)
     assert p.stderr == b"".join(o.stderr for o in outs)
     files = sorted(f.name for f in a.iterdir())
-    assert files == sorted(f.name for f in b.iterdir()) and len(files) == 1 + 2 * 5
+    assert files == sorted(f.name for f in b.iterdir()) and len(files) == 1 + 2 * (k1 - k0 + 1)
     for f in files:
         assert (a / f).read_bytes() == (b / f).read_bytes(), f
 
