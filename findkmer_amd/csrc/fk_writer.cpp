@@ -22,8 +22,12 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
+#include <condition_variable>
+#include <mutex>
 #include <string>
 #include <thread>
+#include <unordered_map>
 #include <vector>
 
 namespace {
@@ -96,30 +100,53 @@ struct RowCtx {
     std::vector<Comp> *comps;
 };
 
+/* The tail of a row after h and H: the frequency and z (or nothing when
+ * the z filter drops the row).  z depends only on the composition and the
+ * count, so each (composition, count) pair is formatted once per thread:
+ * ~70 K pairs instead of 4 M snprintf("%LE") calls at k = 11. */
+struct Tail {
+    bool keep;
+    std::string s;
+};
+using TailCache = std::unordered_map<uint64_t, Tail>;
+
+const Tail &row_tail(const RowCtx &c, const Comp &cp, int key, uint32_t f, TailCache &cache) {
+    const uint64_t ck = ((uint64_t)key << 32) | f;
+    auto it = cache.find(ck);
+    if (it != cache.end()) return it->second;
+    Tail t;
+    unsigned long long x = f;
+    long double z = (x - cp.mean) / cp.sd;                          /* :839 */
+    t.keep = c.z_enable == 0 || (c.z_enable > 0 && fabsl(z) >= c.z_thr);   /* :852-854 */
+    if (t.keep) {
+        char num[64];
+        int m = snprintf(num, sizeof num, ", %d", (int)f);          /* :872 */
+        t.s.assign(num, (size_t)m);
+        if (cp.approx) {                                            /* :876-886 */
+            m = snprintf(num, sizeof num, ", %LE", z);
+            t.s.append(num, (size_t)m);
+        }
+    }
+    return cache.emplace(ck, std::move(t)).first->second;
+}
+
 /* format rows [lo, hi) into out */
-void format_range(const RowCtx &c, uint64_t lo, uint64_t hi, std::string &out) {
+void format_range(const RowCtx &c, uint64_t lo, uint64_t hi, std::string &out, TailCache &cache) {
     char kmer[32];
-    char num[64];
     int cnt[4];
     for (uint64_t i = lo; i < hi; i++) {
         const uint64_t idx = c.keys ? c.keys[i] : i;
         uint32_t f = c.counts[i];
         if (!f) continue;
         digits_of(idx, c.k, cnt, kmer);
-        const Comp &cp = (*c.comps)[comp_key(cnt[0], cnt[1], cnt[2])];
-        unsigned long long x = f;
-        long double z = (x - cp.mean) / cp.sd;                      /* :839 */
-        if (!(c.z_enable == 0 || (c.z_enable > 0 && fabsl(z) >= c.z_thr)))
-            continue;                                               /* :852-854 */
+        const int key = comp_key(cnt[0], cnt[1], cnt[2]);
+        const Comp &cp = (*c.comps)[key];
+        const Tail &t = row_tail(c, cp, key, f, cache);
+        if (!t.keep) continue;
         out.push_back('\n');                                        /* :858 */
         out.append(kmer, (size_t)c.k);                              /* :861-863 */
         out.append(cp.hH);                                          /* :866-869 */
-        int m = snprintf(num, sizeof num, ", %d", (int)f);          /* :872 */
-        out.append(num, (size_t)m);
-        if (cp.approx) {                                            /* :876-886 */
-            m = snprintf(num, sizeof num, ", %LE", z);
-            out.append(num, (size_t)m);
-        }
+        out.append(t.s);                                            /* :872-886 */
     }
 }
 
@@ -188,29 +215,46 @@ static int write_rows(FILE *out, int k, const uint64_t *keys, uint64_t n_rows, c
     if (total < (1u << 16)) threads = 1;
     if (threads == 1) {
         std::string s;
-        format_range(ctx, 0, total, s);
+        TailCache cache;
+        format_range(ctx, 0, total, s, cache);
         if (fwrite(s.data(), 1, s.size(), out) != s.size()) return FK_E_IO;
         return FK_OK;
     }
-    /* super-blocks of `threads` slices, written in order */
-    const uint64_t slice = 1ull << 18;
-    std::vector<std::string> bufs((size_t)threads);
-    for (uint64_t base = 0; base < total; base += slice * (uint64_t)threads) {
-        std::vector<std::thread> ts;
-        for (int t = 0; t < threads; t++) {
-            uint64_t lo = base + (uint64_t)t * slice;
-            uint64_t hi = std::min(lo + slice, total);
-            bufs[(size_t)t].clear();
-            if (lo >= total) continue;
-            ts.emplace_back([&, lo, hi, t] { format_range(ctx, lo, hi, bufs[(size_t)t]); });
-        }
-        for (auto &th : ts) th.join();
-        for (int t = 0; t < threads; t++) {
-            const std::string &s = bufs[(size_t)t];
-            if (!s.empty() && fwrite(s.data(), 1, s.size(), out) != s.size()) return FK_E_IO;
-        }
+    /* workers format slices in any order; this thread writes them in index
+       order as they complete, so the writes overlap the formatting */
+    const uint64_t slice = 1ull << 16;
+    const uint64_t nsl = (total + slice - 1) / slice;
+    std::vector<std::string> bufs((size_t)nsl);
+    std::vector<uint8_t> done((size_t)nsl, 0);
+    std::mutex mu;
+    std::condition_variable cv;
+    std::atomic<uint64_t> next{0};
+    std::vector<std::thread> ts;
+    for (int t = 0; t < threads; t++) {
+        ts.emplace_back([&] {
+            TailCache cache;
+            for (uint64_t sl; (sl = next.fetch_add(1)) < nsl;) {
+                std::string s;
+                format_range(ctx, sl * slice, std::min((sl + 1) * slice, total), s, cache);
+                std::lock_guard<std::mutex> g(mu);
+                bufs[(size_t)sl] = std::move(s);
+                done[(size_t)sl] = 1;
+                cv.notify_all();
+            }
+        });
     }
-    return FK_OK;
+    int rc = FK_OK;
+    for (uint64_t sl = 0; sl < nsl; sl++) {
+        std::string s;
+        {
+            std::unique_lock<std::mutex> g(mu);
+            cv.wait(g, [&] { return done[(size_t)sl] != 0; });
+            s = std::move(bufs[(size_t)sl]);
+        }
+        if (rc == FK_OK && !s.empty() && fwrite(s.data(), 1, s.size(), out) != s.size()) rc = FK_E_IO;
+    }
+    for (auto &th : ts) th.join();
+    return rc;
 }
 
 extern "C" int fk_write_rows(void *out_v, int k, const uint32_t *counts,
