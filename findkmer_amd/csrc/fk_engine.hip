@@ -223,6 +223,12 @@ __device__ __forceinline__ int load_lane(const Ctx &cx, int64_t off, uint32_t w[
 }
 
 /* byte j (runtime) of a lane's 32 bytes without indexing the register array */
+__device__ __forceinline__ uint32_t lane_word(const uint32_t w[8], uint32_t d) {
+    uint32_t lo = d == 0 ? w[0] : d == 1 ? w[1] : d == 2 ? w[2] : w[3];
+    uint32_t hi = d == 4 ? w[4] : d == 5 ? w[5] : d == 6 ? w[6] : w[7];
+    return d < 4 ? lo : hi;
+}
+
 __device__ __forceinline__ uint32_t lane_byte(const uint32_t w[8], uint32_t j) {
     uint32_t d = j >> 2;
     uint32_t lo = d == 0 ? w[0] : d == 1 ? w[1] : d == 2 ? w[2] : w[3];
@@ -246,14 +252,20 @@ __device__ __forceinline__ void tile_general(const Ctx &cx, const uint32_t w[8],
     /* -- 1. header flag at each lane start: last '>' vs last '\n' before it */
     uint32_t lastGT = 0, lastNL = 0, firstSp = 0xFFFFu, firstGT = 0;
 #pragma unroll 1
-    for (int j = 0; j < nb; j++) {
-        uint32_t c = lane_byte(w, (uint32_t)j);
+    for (int d_ = 0; d_ < 8 && 4 * d_ < nb; d_++) {
+        const uint32_t wd_ = lane_word(w, (uint32_t)d_);   /* one word select per 4 bytes */
+    #pragma unroll
+        for (int b_ = 0; b_ < 4; b_++) {
+        const int j = 4 * d_ + b_;
+        if (j >= nb) break;
+        uint32_t c = (wd_ >> (8 * b_)) & 0xFFu;
         uint32_t pos = (uint32_t)lane * LB + (uint32_t)j + 1u;
         bool gt = c == '>';
         bool nl = c == '\n';
         if (gt) lastGT = pos;
         if (nl) lastNL = pos;
         if ((gt || nl) && firstSp == 0xFFFFu) { firstSp = pos - 1; firstGT = gt; }
+    }
     }
     uint32_t g = lastGT, n = lastNL;
 #pragma unroll
@@ -269,8 +281,13 @@ __device__ __forceinline__ void tile_general(const Ctx &cx, const uint32_t w[8],
     uint32_t hdr = hdr0, rs = 0, nv = 0, hdr_end;
     uint64_t code = 0;
 #pragma unroll 1
-    for (int j = 0; j < nb; j++) {
-        uint32_t c = lane_byte(w, (uint32_t)j);
+    for (int d_ = 0; d_ < 8 && 4 * d_ < nb; d_++) {
+        const uint32_t wd_ = lane_word(w, (uint32_t)d_);   /* one word select per 4 bytes */
+    #pragma unroll
+        for (int b_ = 0; b_ < 4; b_++) {
+        const int j = 4 * d_ + b_;
+        if (j >= nb) break;
+        uint32_t c = (wd_ >> (8 * b_)) & 0xFFu;
         if (hdr) {
             if (c == '\n') hdr = 0;
         } else if (c == '>') {
@@ -280,6 +297,7 @@ __device__ __forceinline__ void tile_general(const Ctx &cx, const uint32_t w[8],
             if (s < 0) { rs = 1; nv = 0; }
             else { code = (code << 2) | (uint32_t)s; nv++; }
         }
+    }
     }
     hdr_end = hdr;
 
@@ -331,8 +349,13 @@ __device__ __forceinline__ void tile_general(const Ctx &cx, const uint32_t w[8],
         const uint64_t maskk1 = cx.maskk >> 2;
 
 #pragma unroll 1
-        for (int j = 0; j < nb; j++) {
-            uint32_t c = lane_byte(w, (uint32_t)j);
+        for (int d_ = 0; d_ < 8 && 4 * d_ < nb; d_++) {
+            const uint32_t wd_ = lane_word(w, (uint32_t)d_);   /* one word select per 4 bytes */
+        #pragma unroll
+            for (int b_ = 0; b_ < 4; b_++) {
+            const int j = 4 * d_ + b_;
+            if (j >= nb) break;
+            uint32_t c = (wd_ >> (8 * b_)) & 0xFFu;
             uint32_t pos = (uint32_t)lane * LB + (uint32_t)j;
             if (p1_here && pos == p1) r_at = R;
             if (hdr) {
@@ -379,6 +402,7 @@ __device__ __forceinline__ void tile_general(const Ctx &cx, const uint32_t w[8],
                 uint32_t d0 = (uint32_t)((lc >> (2 * seq - 2)) & 3);
                 cnt.d1s += 1ull << (16 * (d0 ^ (d0 >> 1)));
             }
+        }
         }
 
         /* chunk facts */
