@@ -397,6 +397,52 @@ def _header_mix(seed, n):
     return bytes(out)
 
 
+def _progress_model(data, k):
+    """test-only model of the reference's -q 0 progress numbers
+    (findKmer.cpp:996-1002, :1040-1057): baseCounter at every '>' that
+    starts a comment line"""
+    out, bc, run, hdr = [], 0, 0, False
+    for i, c in enumerate(data):
+        if hdr:
+            if c == 10:
+                hdr = False
+            continue
+        if c in b"ACGT":
+            run += 1
+            bc += k if run == k else (1 if run > k else 0)
+        elif c == 10:
+            continue
+        else:
+            run = 0
+            if c == 62:
+                out.append((i, bc))
+                hdr = True
+    return out
+
+
+@pytest.mark.parametrize("k", [2, 6, 11])
+def test_input_headers_match_model(k, tmp_path):
+    """fk_input_headers (k_hdr_traj / k_hdr_list) == a byte loop, on records
+    with '>' inside header lines, N runs and runs shorter than k, with
+    headers across 4 KiB chunk edges; a 0xFF byte outside a header is
+    refused (FK_E_STATE: the streamed path prints those files)"""
+    data = _header_mix(200 + k, 300_000)
+    path = tmp_path / "h.fa"
+    path.write_bytes(data)
+    want = _progress_model(data, k)
+    with fk.DeviceInput(str(path)) as inp:
+        pos, bases = inp.headers(k)
+    assert len(want) > 50
+    assert [int(p) for p in pos] == [p for p, _ in want]
+    assert [int(b) for b in bases] == [b for _, b in want]
+    path2 = tmp_path / "ff.fa"
+    path2.write_bytes(data[:100_000] + b"ACGT\xffACGT" + data[100_000:])
+    with fk.DeviceInput(str(path2)) as inp:
+        with pytest.raises(fk.FindKmerError) as ei:
+            inp.headers(k)
+        assert ei.value.code == fk.FK_E_STATE
+
+
 @pytest.mark.parametrize("k", [1, 6, 7, 11])
 def test_cli_q0_progress_device_vs_stream(k, tmp_path):
     """-q 0 progress lines: device path (fk_input_headers) == streamed path
