@@ -288,15 +288,15 @@ __device__ __forceinline__ void tile_general(const Ctx &cx, const uint32_t w[8],
         const int j = 4 * d_ + b_;
         if (j >= nb) break;
         uint32_t c = (wd_ >> (8 * b_)) & 0xFFu;
-        if (hdr) {
-            if (c == '\n') hdr = 0;
-        } else if (c == '>') {
-            rs = 1; nv = 0; hdr = 1;
-        } else if (c != '\n') {
-            int s = fk_sym(c);
-            if (s < 0) { rs = 1; nv = 0; }
-            else { code = (code << 2) | (uint32_t)s; nv++; }
-        }
+        /* branch-free: every lane takes the same instructions (selects) */
+        const int s = fk_sym(c);
+        const bool in = hdr != 0, nl = c == '\n', base = s >= 0;
+        const bool brk = !in && !nl && !base;          /* '>', N, any other byte */
+        const bool take = !in && base;
+        rs |= brk ? 1u : 0u;
+        nv = brk ? 0u : nv + (take ? 1u : 0u);
+        code = take ? (code << 2) | (uint32_t)s : code;
+        hdr = in ? (nl ? 0u : 1u) : (c == '>' ? 1u : 0u);
     }
     }
     hdr_end = hdr;
