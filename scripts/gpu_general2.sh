@@ -7,3 +7,8 @@ python tools/make_upstream.py /tmp/up1g.fas 1e9 3
 echo "upstream $(timeout -k 10 300 python tools/upstream_bench.py /tmp/up1g.fas 6 2>/dev/null | tail -1)"
 timeout -k 10 300 python bench.py --steps 20 --warmup 3 --no-cpu-baseline > gpurun_out/ab.log 2>&1 || { tail -5 gpurun_out/ab.log; exit 1; }
 echo "k6 $(tail -1 gpurun_out/ab.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['ms_per_step'], d['roofline']['kernel_ms'])")"
+echo "head upstream $(FINDKMER_LIB=build/exp/libfk_head.so timeout -k 10 300 python tools/upstream_bench.py /tmp/up1g.fas 6 2>/dev/null | tail -1)"
+for lib in "" build/exp/libfk_head.so; do
+FINDKMER_LIB=$lib timeout -k 10 300 python bench.py --steps 20 --warmup 3 --no-cpu-baseline > gpurun_out/ab.log 2>&1 || { tail -5 gpurun_out/ab.log; exit 1; }
+echo "lib=${lib:-product} k6 $(tail -1 gpurun_out/ab.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['ms_per_step'], d['roofline']['kernel_ms'])")"
+done
