@@ -93,8 +93,6 @@ def run_windows(n, k):
     return full * (hi - k + 1) + max(0, min(rem, hi) - k + 1)
 
 
-
-
 def expected_windows(total, k, chrom):
     """Windows in a pure-ACGT stream of `total` positions whose positions
     j*chrom (j >= 1) hold 'N' run breaks: each run is shorter than 2^31, so
@@ -104,6 +102,18 @@ def expected_windows(total, k, chrom):
         w += run_windows(b - start, k)
         start = b + 1
     return w + run_windows(total - start, k)
+
+
+def want_valid(total, k, chrom):
+    """baseCounter of the same stream: every base of a run of >= k bases
+    (findKmer.cpp:1040, :1056; runs are shorter than 2^31 here)"""
+    if not chrom:
+        return total if total >= k else 0
+    v, start = 0, 0
+    for b in range(chrom, total, chrom):
+        v += (b - start) if b - start >= k else 0
+        start = b + 1
+    return v + ((total - start) if total - start >= k else 0)
 
 
 def main():
@@ -161,19 +171,21 @@ def main():
     # (recording them on every launch costs ~2% of the step)
     eng = fk.Engine(k, device=local, timing_every=args.timing_every)
     coll_dev = "cuda" if args.dist_backend == "nccl" else "cpu"
-    table_t = torch.empty(1 << (2 * k), dtype=torch.int32, device=coll_dev) if world > 1 else None
+    merge_t = fkdist.merge_buffer(k, coll_dev) if world > 1 else None
+    pinned = torch.empty(fkdist.COUNTER_SLOTS, dtype=torch.int32, pin_memory=True) if coll_dev == "cuda" else None
 
     def step():
         eng.reset()
-        if world == 1:
-            eng.feed_device(buf.data_ptr(), nbytes)
-        else:
+        if world > 1:
             # shard, stitch entry states (all-gather of 96-B summaries), merge
-            # tables (reduce to rank 0): findkmer_amd/dist.py
-            fkdist.count_sharded(eng, buf.data_ptr() + halo, nbytes, halo, table_t, times=phase_s)
+            # tables + counters (reduce to rank 0): findkmer_amd/dist.py
+            res = fkdist.count_sharded(eng, buf.data_ptr() + halo, nbytes, halo, merge_t, times=phase_s,
+                                       pinned=pinned)
+            return res.local, res
+        eng.feed_device(buf.data_ptr(), nbytes)
         # an ablation build (FINDKMER_LIB) may leave the table incomplete
         rc, r = eng.finish(allow=(fk.FK_OK, fk.FK_E_ROLLOVER) if os.environ.get("FINDKMER_LIB") else (fk.FK_OK,))
-        return r
+        return r, None
 
     phase_s = {}
     for _ in range(args.warmup):
@@ -183,10 +195,10 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    last = None
+    last = merged = None
     main_ms, timed = 0.0, 0
     for _ in range(args.steps):
-        last = step()
+        last, merged = step()
         main_ms += last.main_kernel_ms
         timed += last.timed_kernels
     torch.cuda.synchronize()
@@ -200,15 +212,13 @@ def main():
 
     # correctness guard on the measured pass: the synthetic stream (pure ACGT,
     # or FASTA whose '\n' are transparent) is one run, every window counts
-    if not os.environ.get("FINDKMER_LIB"):
-        total = last.windows
-        if dist:
-            w_t = torch.tensor([last.windows], dtype=torch.int64, device=coll_dev)
-            dist.all_reduce(w_t)
-            total = int(w_t.item())
-            if rank == 0:   # the merged table lives on rank 0 (dist.reduce)
-                merged = int(table_t.to(torch.int64).remainder(1 << 32).sum().item())
-                assert merged == total, (merged, total)
+    if not os.environ.get("FINDKMER_LIB") and rank == 0:
+        # the merged counters and table live on rank 0 (dist.reduce)
+        total = merged.windows if merged is not None else last.windows
+        if merged is not None:
+            assert merged.status() == fk.FK_OK, "merged table: rollover or unterminated header"
+            if chrom_breaks or world * n < (1 << 31):   # no run reaches the int32 seqSize wrap
+                assert merged.valid_bases == want_valid(world * n, k, args.chrom if chrom_breaks else 0)
         want = expected_windows(world * n, k, args.chrom) if chrom_breaks else run_windows(world * n, k)
         assert total == want, (total, want)
 

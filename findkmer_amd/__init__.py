@@ -34,7 +34,7 @@ FK_K_MAX_DENSE = 16
 
 class FkState(ctypes.Structure):
     _fields_ = [("run", ctypes.c_uint64), ("code", ctypes.c_uint64),
-                ("hdr", ctypes.c_uint32), ("pad", ctypes.c_uint32)]
+                ("hdr", ctypes.c_uint32), ("ended", ctypes.c_uint32)]
 
 
 class FkResult(ctypes.Structure):
@@ -90,6 +90,7 @@ SIGNATURES = [
     ("fk_engine_summary", ctypes.c_int, [_P, ctypes.POINTER(FkSummary)]),
     ("fk_engine_summary_full", ctypes.c_int, [_P, ctypes.POINTER(FkSummary)]),
     ("fk_summary_apply", ctypes.c_int, [ctypes.POINTER(FkSummary), ctypes.POINTER(FkState), ctypes.POINTER(FkState)]),
+    ("fk_summary_is_full", ctypes.c_int, [ctypes.POINTER(FkSummary)]),
     ("fk_engine_resolve", ctypes.c_int, [_P, ctypes.POINTER(FkState)]),
     ("fk_engine_finish", ctypes.c_int, [_P, ctypes.POINTER(FkResult)]),
     ("fk_engine_table", ctypes.c_int, [_P, _U32P]),
@@ -289,6 +290,14 @@ def summary_apply(summary, state):
     out = FkState()
     _check(lib().fk_summary_apply(ctypes.byref(summary), ctypes.byref(state), ctypes.byref(out)), "summary_apply")
     return out
+
+
+def summary_is_full(summary):
+    """1 for a full transfer function, 0 for a compact summary"""
+    rc = lib().fk_summary_is_full(ctypes.byref(summary))
+    if rc < 0:
+        raise FindKmerError(rc, "summary_is_full")
+    return rc == 1
 
 
 def count(data, k, ngpu=1, want_nodes=False):

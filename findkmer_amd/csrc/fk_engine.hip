@@ -2353,6 +2353,18 @@ __global__ void k_synth(uint8_t *out, uint64_t total, uint64_t seed, int fasta_l
         }                                                                       \
     } while (0)
 
+/* A scratch device allocation, freed on every return path (hipFree waits for
+   the work queued on it). */
+struct DevScratch {
+    void *p = nullptr;
+    DevScratch() = default;
+    DevScratch(const DevScratch &) = delete;
+    DevScratch &operator=(const DevScratch &) = delete;
+    ~DevScratch() { if (p) hipFree(p); }
+    bool alloc(size_t n) { return hipMalloc(&p, n) == hipSuccess; }
+    template <class T> T *as() const { return (T *)p; }
+};
+
 static const uint64_t SEG_MAX_BYTES = 1ull << 34;                 /* 16 GiB per segment */
 static const uint64_t STAGE_BYTES = 256ull << 20;                 /* host feed staging */
 static const unsigned long long NO_EOF64 = ~0ull;
@@ -2982,15 +2994,11 @@ static int collect_unknown(fk_engine *e, const uint8_t *dbuf, uint64_t len, int6
     for (uint64_t r = 0; r < g.nranges; r++)
         if (rr[(size_t)r].unknown) { list.push_back((uint32_t)r); offs.push_back(acc); acc += rr[(size_t)r].unknown; }
     if (!acc) return FK_OK;
-    uint32_t *d_list = nullptr;
-    uint64_t *d_offs = nullptr;
-    uint8_t *d_out = nullptr;
-    if (hipMalloc((void **)&d_list, list.size() * 4) != hipSuccess ||
-        hipMalloc((void **)&d_offs, offs.size() * 8) != hipSuccess ||
-        hipMalloc((void **)&d_out, acc) != hipSuccess) {
-        hipFree(d_list); hipFree(d_offs); hipFree(d_out);
-        return FK_E_OOM;
-    }
+    DevScratch s_list, s_offs, s_out;
+    if (!s_list.alloc(list.size() * 4) || !s_offs.alloc(offs.size() * 8) || !s_out.alloc(acc)) return FK_E_OOM;
+    uint32_t *d_list = s_list.as<uint32_t>();
+    uint64_t *d_offs = s_offs.as<uint64_t>();
+    uint8_t *d_out = s_out.as<uint8_t>();
     HIPCHK(hipMemcpyAsync(d_list, list.data(), list.size() * 4, hipMemcpyHostToDevice, e->stream));
     HIPCHK(hipMemcpyAsync(d_offs, offs.data(), offs.size() * 8, hipMemcpyHostToDevice, e->stream));
     unsigned gx = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((list.size() + 7) / 8, (uint64_t)e->cus * 2));
@@ -3001,7 +3009,6 @@ static int collect_unknown(fk_engine *e, const uint8_t *dbuf, uint64_t len, int6
     e->unknown_bytes.resize(old + acc);
     HIPCHK(hipMemcpyAsync(e->unknown_bytes.data() + old, d_out, acc, hipMemcpyDeviceToHost, e->stream));
     HIPCHK(hipStreamSynchronize(e->stream));
-    hipFree(d_list); hipFree(d_offs); hipFree(d_out);
     return FK_OK;
 }
 
@@ -3234,7 +3241,7 @@ extern "C" int fk_engine_state(fk_engine *e, fk_state *out) {
     out->run = e->state.R;
     out->code = fk_sigma(e->state.code);     /* API codes use A0 C1 G2 T3 */
     out->hdr = e->state.hdr;
-    out->pad = 0;
+    out->ended = e->ended ? 1u : 0u;
     return FK_OK;
 }
 
@@ -3316,6 +3323,9 @@ extern "C" int fk_engine_summary(fk_engine *e, fk_summary *out) {
             out->w[6] = ss.nv;
             out->w[7] = e->shard_len;
             out->w[8] = (uint64_t)e->k;
+            /* the guesses hold for every equivalent entering state, so a 0xFF
+               byte they saw outside a header ends the stream in this shard */
+            out->w[9] = e->last.eof_cand != NO_EOF64 ? 1u : 0u;
             out->w[11] = FK_SUMMARY_COMPACT;
             return FK_OK;
         }
@@ -3357,12 +3367,23 @@ static bool compact_apply(const fk_summary *s, const XState &in, XState &out) {
     return true;
 }
 
+extern "C" int fk_summary_is_full(const fk_summary *s) {
+    if (!s) return FK_E_INVALID;
+    return s->w[11] == FK_SUMMARY_COMPACT ? 0 : 1;
+}
+
 extern "C" int fk_summary_apply(const fk_summary *s, const fk_state *in, fk_state *out) {
     if (!s || !in || !out) return FK_E_INVALID;
+    if (in->ended) {           /* absorbing: the stream ended before this span */
+        *out = *in;
+        return FK_OK;
+    }
     XState x{in->run, fk_sigma(in->code), in->hdr, 0};
     XState y;
+    uint32_t ended = 0;
     if (s->w[11] == FK_SUMMARY_COMPACT) {
         if (!compact_apply(s, x, y)) return FK_E_SUMMARY;
+        ended = s->w[9] ? 1u : 0u;
     } else {
         TF t;
         memcpy(&t, s, sizeof t);
@@ -3371,7 +3392,7 @@ extern "C" int fk_summary_apply(const fk_summary *s, const fk_state *in, fk_stat
     out->run = y.R;
     out->code = fk_sigma(y.code);
     out->hdr = y.hdr;
-    out->pad = 0;
+    out->ended = ended;
     return FK_OK;
 }
 
@@ -3381,6 +3402,16 @@ extern "C" int fk_engine_resolve(fk_engine *e, const fk_state *entering) {
     int rc = set_dev(e);
     if (rc) return rc;
     XState in{entering->run, fk_sigma(entering->code), entering->hdr, 0};
+    if (entering->ended) {
+        /* the stream ended before this shard (a 0xFF byte in an earlier one,
+           :988): it counts nothing; the pending count is zeroed lazily */
+        const uint64_t len = e->shard_len;
+        zero_all(e);
+        e->fed = len;
+        e->ended = 1;
+        e->state = in;
+        return FK_OK;
+    }
     e->shard_pending = 0;
     e->state = in;
     if (e->shard_len == 0) {
@@ -3518,11 +3549,10 @@ extern "C" int fk_engine_finish(fk_engine *e, fk_result *res) {
         if (any_walk) {
             nodes = 1 + res->distinct;
             if (k >= 2) {
-                uint8_t *pa = nullptr, *pb = nullptr;
+                DevScratch sa, sb;
                 uint64_t n1 = 1ull << (2 * (k - 1));
-                if (hipMalloc((void **)&pa, n1) != hipSuccess) return FK_E_OOM;
-                if (hipMalloc((void **)&pb, std::max<uint64_t>(n1 / 4, 4)) != hipSuccess) { hipFree(pa); return FK_E_OOM; }
-                uint8_t *cur = pa, *nxt = pb;
+                if (!sa.alloc(n1) || !sb.alloc(std::max<uint64_t>(n1 / 4, 4))) return FK_E_OOM;
+                uint8_t *cur = sa.as<uint8_t>(), *nxt = sb.as<uint8_t>();
                 for (int d = k - 1; d >= 1; d--) {
                     uint64_t nd = 1ull << (2 * d);
                     uint64_t off = ((1ull << (2 * d)) - 4) / 3;
@@ -3541,8 +3571,6 @@ extern "C" int fk_engine_finish(fk_engine *e, fk_result *res) {
                     nodes += c;
                     std::swap(cur, nxt);   /* this level becomes the child level */
                 }
-                hipFree(pa);
-                hipFree(pb);
             }
         }
         res->nodes = nodes;
@@ -3659,12 +3687,12 @@ extern "C" int fk_engine_merge_from(fk_engine *dst, fk_engine *src) {
     HIPCHK(hipStreamSynchronize(src->stream));
     rc = set_dev(dst);
     if (rc) return rc;
-    uint32_t *tmp = nullptr;
-    uint32_t *tmps = nullptr;
-    unsigned long long *tmpa = nullptr;
-    if (hipMalloc((void **)&tmp, dst->nbins * sizeof(uint32_t)) != hipSuccess) return FK_E_OOM;
-    if (dst->nshort && hipMalloc((void **)&tmps, dst->nshort * sizeof(uint32_t)) != hipSuccess) { hipFree(tmp); return FK_E_OOM; }
-    if (hipMalloc((void **)&tmpa, ACC_N * sizeof(unsigned long long)) != hipSuccess) { hipFree(tmp); hipFree(tmps); return FK_E_OOM; }
+    DevScratch s_tab, s_short, s_acc;
+    if (!s_tab.alloc(dst->nbins * sizeof(uint32_t))) return FK_E_OOM;
+    if (dst->nshort && !s_short.alloc(dst->nshort * sizeof(uint32_t))) return FK_E_OOM;
+    if (!s_acc.alloc(ACC_N * sizeof(unsigned long long))) return FK_E_OOM;
+    uint32_t *tmp = s_tab.as<uint32_t>(), *tmps = s_short.as<uint32_t>();
+    unsigned long long *tmpa = s_acc.as<unsigned long long>();
     HIPCHK(hipMemcpyPeerAsync(tmp, dst->dev, src->d_table, src->dev, dst->nbins * sizeof(uint32_t), dst->stream));
     if (dst->nshort) HIPCHK(hipMemcpyPeerAsync(tmps, dst->dev, src->d_short, src->dev, dst->nshort * sizeof(uint32_t), dst->stream));
     HIPCHK(hipMemcpyPeerAsync(tmpa, dst->dev, src->d_acc, src->dev, ACC_N * sizeof(unsigned long long), dst->stream));
@@ -3677,7 +3705,6 @@ extern "C" int fk_engine_merge_from(fk_engine *dst, fk_engine *src) {
     hipLaunchKernelGGL(k_add_acc, dim3(1), dim3(64), 0, dst->stream, dst->d_acc, tmpa, (int)ACC_N);
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(dst->stream));
-    hipFree(tmp); hipFree(tmps); hipFree(tmpa);
     dst->stats_valid = false;
     dst->unknown_bytes.insert(dst->unknown_bytes.end(), src->unknown_bytes.begin(), src->unknown_bytes.end());
     dst->chunks += src->chunks;
@@ -3751,7 +3778,8 @@ extern "C" int fk_count_multi(const uint8_t *buf, uint64_t len, int k, int ngpu,
         for (int g = 0; g < ngpu && rc == FK_OK; g++) {
             rc = fk_engine_resolve(eng[(size_t)g], &s);
             if (rc) break;
-            fk_engine_state(eng[(size_t)g], &s);
+            rc = fk_engine_state(eng[(size_t)g], &s);
+            if (rc) break;
             if (eng[(size_t)g]->ended) {          /* a 0xFF byte: later shards do not count */
                 for (int h = g + 1; h < ngpu; h++) fk_engine_reset(eng[(size_t)h]);
                 last = g;

@@ -270,6 +270,9 @@ extern "C" int fk_input_headers(fk_input *in, int k, uint64_t *pos, uint64_t *ba
             if (t.ff) { rc = FK_E_STATE; break; }   /* 0xFF ends the scan: streamed path */
             const uint64_t L0 = m == 1 ? 0 : L;
             if (t.broke) {
+                /* a run that crosses 2^31-1 bases and closes in this chunk:
+                   the int32 seqSize zone as well */
+                if (L0 + t.head >= 0x7FFFFFFFull) { rc = FK_E_STATE; break; }
                 cbase[c] = base + g(L0 + t.head);
                 base = cbase[c] + t.inner;   /* every run closed in the chunk; the tail run stays open */
                 L = t.tail;

@@ -286,14 +286,14 @@ static void die_engine(int rc) {
  * (:996-1002), with baseCounter as of that point; we feed the engine up to
  * each such '>' and read its running counter (host only splits the stream).
  */
-static int scan_file(fk_engine *e, FILE *f, fk_result *res) {
+static int scan_file(fk_engine *e, FILE *f, fk_result *res, bool echo = true) {
     const size_t PIECE = 256u << 20;
     std::vector<uint8_t> buf(PIECE);
     int in_hdr = 0, ended = 0;
     for (;;) {
         size_t n = fread(buf.data(), 1, buf.size(), f);
         if (n == 0) break;
-        if (config.suppressOutputEnable != 0 || ended) {
+        if (config.suppressOutputEnable != 0 || !echo || ended) {
             int rc = fk_engine_feed(e, buf.data(), n, 0);
             if (rc) return rc;
             continue;
@@ -414,16 +414,19 @@ static int run_k(int argc) {
         const char *ing = getenv("FINDKMER_INGEST");
         if (!ing || strcmp(ing, "stream") != 0) {
             int lrc = fk_input_load(config.sequence_file, -1, 0, &g_input);
-            if (lrc == FK_E_OOM || lrc == FK_E_HIP || lrc == FK_E_NO_DEVICE) die_engine(lrc);
-            if (lrc) g_input = nullptr;   /* not a regular file: stream it */
+            if (lrc == FK_E_HIP || lrc == FK_E_NO_DEVICE) die_engine(lrc);
+            /* not a regular file, or larger than free HBM: stream it */
+            if (lrc) g_input = nullptr;
         }
     }
     bool on_device = g_input != nullptr;
+    bool echoed = false;   /* the -q 0 progress lines are already printed */
     if (on_device && config.suppressOutputEnable == 0) {
         /* -q 0: the per-record progress lines, from the device copy */
         int prc = print_progress(config.k);
         if (prc == FK_E_STATE) on_device = false;   /* 0xFF / int32 zone: the streamed path prints them */
         else if (prc) die_engine(prc);
+        else echoed = true;
     }
 
     fk_opts opts;
@@ -437,6 +440,17 @@ static int run_k(int argc) {
     if (rc) die_engine(rc);
     fk_result res;
     rc = on_device ? scan_device(eng, &res) : scan_file(eng, config.sequence_file_pointer, &res);
+    if (rc == FK_E_OOM && on_device) {
+        /* the resident file copy and the engine's buffers (k >= 17: 8 bytes
+           of slots per input byte) do not fit together: drop the copy and
+           stream the file through the engine's pinned staging instead */
+        fk_input_destroy(g_input);
+        g_input = nullptr;
+        rc = fk_engine_reset(eng);
+        if (rc) die_engine(rc);
+        rewind(config.sequence_file_pointer);
+        rc = scan_file(eng, config.sequence_file_pointer, &res, !echoed);
+    }
     if (rc == FK_E_ROLLOVER) {                                       /* :642-648 */
         const char *m = "\n\n!!! COUNTER ROLLOVER DETECTED! \nIncrease the number of bits used for the counter variable if you have the source code, else use a smaller sequence file.\n\n";
         fprintf(stderr, "%s", m);

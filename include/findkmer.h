@@ -66,12 +66,15 @@ enum {
  * for stitching GPU shards).  `run` is the number of valid bases since the
  * last run break (the ref's seqSize, an int that wraps: we keep it exact and
  * apply the 32-bit wrap where the ref would); `code` holds the last bases,
- * first base most significant; `hdr` = inside a '>' comment line. */
+ * first base most significant; `hdr` = inside a '>' comment line; `ended` = a
+ * 0xFF byte outside a header already ended the stream (the reference's
+ * signed-char EOF test, findKmer.cpp:988): an absorbing state, nothing after
+ * it counts. */
 typedef struct {
     uint64_t run;
     uint64_t code;
     uint32_t hdr;
-    uint32_t pad;
+    uint32_t ended;
 } fk_state;
 
 typedef struct {
@@ -137,13 +140,20 @@ int  fk_engine_feed(fk_engine *e, const uint8_t *buf, uint64_t len,
  * for entering states equivalent to the shard's guess (fk_summary_apply then
  * returns FK_E_SUMMARY for any other state); otherwise, or from
  * fk_engine_summary_full(), the full transfer function, which applies to
- * every state. */
+ * every state.  A compact summary also records whether the shard ends the
+ * stream (a 0xFF byte outside a header): fk_summary_apply sets out->ended.
+ * A full summary does not know it (fk_summary_is_full): the caller learns
+ * each shard's end from fk_engine_state(...).ended after fk_engine_resolve.
+ * Applied to an ended state, any summary returns that state unchanged, and
+ * fk_engine_resolve with an ended entering state drops the shard (its table
+ * and counters stay zero). */
 typedef struct { uint64_t w[12]; } fk_summary;
 int  fk_engine_feed_shard(fk_engine *e, const uint8_t *buf, uint64_t len,
                           uint64_t halo, int on_device);
 int  fk_engine_summary(fk_engine *e, fk_summary *out);
 int  fk_engine_summary_full(fk_engine *e, fk_summary *out);
 int  fk_summary_apply(const fk_summary *s, const fk_state *in, fk_state *out);
+int  fk_summary_is_full(const fk_summary *s);   /* 1: full transfer function, 0: compact */
 int  fk_engine_resolve(fk_engine *e, const fk_state *entering);
 
 /* Finish the stream (end-of-input rules) and fill *res.  Returns FK_OK or one

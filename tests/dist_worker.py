@@ -1,0 +1,76 @@
+"""TEST INFRASTRUCTURE: one rank of a sharded count on the GPU with the real
+engine (findkmer_amd.Engine) and findkmer_amd/dist.py, launched by
+tests/test_gpu_dist.py under torch.distributed.run (gloo; every rank on
+cuda:0).  The input is a mixed FASTA-like stream (tests/test_dist_cpu._input)
+of --bytes bytes; --eof-in R puts a 0xFF byte outside a header in the middle
+of rank R's shard (the reference's signed-char EOF, findKmer.cpp:988).
+Rank 0 checks the merged table and counters against the CPU oracle and
+prints one JSON line."""
+import argparse
+import json
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(HERE))
+sys.path.insert(0, HERE)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--k", type=int, default=6)
+    ap.add_argument("--bytes", type=int, default=3_000_000)
+    ap.add_argument("--seed", type=int, default=5)
+    ap.add_argument("--eof-in", type=int, default=-1)
+    args = ap.parse_args()
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    import findkmer_amd as fk
+    import findkmer_amd.dist as fkdist
+    import oracle
+    from test_dist_cpu import _input
+
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo")
+    rank, world = dist.get_rank(), dist.get_world_size()
+    data = bytearray(_input(args.seed, args.bytes))
+    n = len(data)
+    bounds = [0] + [n * i // world // 16 * 16 for i in range(1, world)] + [n]
+    if args.eof_in >= 0:
+        at = (bounds[args.eof_in] + bounds[args.eof_in + 1]) // 2
+        data[at - 2:at + 1] = b"\nA\xff"
+    data = bytes(data)
+    lo, hi = bounds[rank], bounds[rank + 1]
+    halo = min(256, lo)
+    dev = torch.empty(hi - lo + halo + 64, dtype=torch.uint8, device="cuda")
+    dev[: hi - lo + halo].copy_(torch.frombuffer(bytearray(data[lo - halo:hi]), dtype=torch.uint8))
+    torch.cuda.synchronize()
+    eng = fk.Engine(args.k, device=0)
+    buf = fkdist.merge_buffer(args.k, "cpu")
+    res = fkdist.count_sharded(eng, dev.data_ptr() + halo, hi - lo, halo, buf)
+    out = {"rank": rank}
+    if rank == 0:
+        want, r, _ = oracle.count_dense(data, args.k)
+        got = res.table.numpy().view(np.uint32)
+        out.update({
+            "table_equal": bool(np.array_equal(got, want)),
+            "windows": [res.windows, r.windows],
+            "valid_bases": [res.valid_bases, r.valid_bases],
+            "base_count": [res.base_count, list(r.base_count)],
+            "depth1": [res.depth1, list(r.depth1)],
+            "unknown_chars": [res.unknown_chars, r.unknown_chars],
+            "scanned_bytes": [res.scanned_bytes, r.scanned_bytes],
+            "hit_eof_byte": [res.hit_eof_byte, r.hit_eof_byte],
+            "unterminated_header": [res.unterminated_header, r.unterminated_header],
+            "distinct": [res.distinct, r.distinct],
+            "rollover": res.rollover,
+            "first_end": res.first_end,
+        })
+        print(json.dumps(out), flush=True)
+    eng.close()
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

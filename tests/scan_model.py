@@ -86,3 +86,138 @@ def count_from(data, k, hdr, R, code, table):
         if seq >= k:
             table[sigma(code & mask)] += 1
     return hdr, R, code
+
+
+FK_SUMMARY_COMPACT = 0x434F4D50414354   # fk_engine.hip: tag of a compact summary (w[11])
+
+
+class _Res:
+    """the fk_result fields count_sharded reads"""
+
+    def __init__(self):
+        self.windows = self.valid_bases = self.unknown_chars = self.scanned_bytes = 0
+        self.base_count = [0, 0, 0, 0]
+        self.depth1 = [0, 0, 0, 0]
+        self.hit_eof_byte = self.unterminated_header = 0
+
+
+class ModelEngine:
+    """Stands in for findkmer_amd.Engine in the CPU multi-process tests of
+    findkmer_amd/dist.py: the same shard calls, computed with the reference
+    rules (findKmer.cpp:962-1069, 0xFF = EOF at :988) on a host shard.
+    guess = None: full transfer-function summaries (as for 8 <= k <= 12);
+    else the (hdr, R, internal code) the shard's count is guessed from, and
+    summary() returns a compact summary valid for equivalent states."""
+
+    REF = {ord("A"): 0, ord("C"): 1, ord("G"): 2, ord("T"): 3}
+
+    def __init__(self, k, shard, guess=None):
+        self.k = k
+        self.data = bytes(shard)
+        self.guess = guess
+        self.entering = None
+        self.tab = np.zeros(1 << (2 * k), dtype=np.uint32)
+
+    def feed_shard_device(self, ptr, nbytes, halo):
+        assert nbytes == len(self.data)
+
+    def summary_full(self):
+        from findkmer_amd import FkSummary
+        s = FkSummary()
+        for i, v in enumerate(summary_words(self.data)):
+            s.w[i] = v % (1 << 64)
+        return s
+
+    def summary(self):
+        if self.guess is None:
+            return self.summary_full()
+        from findkmer_amd import FkSummary
+        hdr, R, code = self.guess
+        h, r, c, ended = hdr, R, code, 0
+        absorb, nv = 0, 0
+        for ch in self.data:
+            if h:
+                if ch == 10:
+                    h = 0
+                continue
+            if ch == ord(">"):
+                h, r, absorb = 1, 0, 1
+                continue
+            if ch == 10:
+                continue
+            s = SYM.get(ch)
+            if s is None:
+                if ch == 0xFF:
+                    ended = 1
+                r, absorb = 0, 1
+                continue
+            c = ((c << 2) | s) & M64
+            r += 1
+            nv += 1
+        if hdr and not absorb:
+            absorb = 1   # a guessed header span: the state after it is fixed
+        s = FkSummary()
+        w = [code, R | (hdr << 32), len(self.data), r, c, h | (absorb << 32), nv, len(self.data), self.k,
+             ended, 0, FK_SUMMARY_COMPACT]
+        for i, v in enumerate(w):
+            s.w[i] = v % (1 << 64)
+        return s
+
+    def resolve(self, state):
+        self.entering = (state.hdr, state.run, sigma(state.code), state.ended)
+
+    def finish(self, allow=None):
+        hdr, R, code, ended = self.entering
+        k = self.k
+        res = _Res()
+        self.tab[:] = 0
+        if ended:
+            res.hit_eof_byte = 1
+            return 0, res
+        mask = (1 << (2 * k)) - 1
+        # the reference's kmer[] window in reference codes, rebuilt from the
+        # entering code (internal A0 C1 T2 G3 -> reference A0 C1 G2 T3)
+        rcode = sigma(code)
+        for pos, ch in enumerate(self.data):
+            if hdr:
+                if ch == 10:
+                    hdr = 0
+                continue
+            if ch == ord(">"):
+                hdr, R = 1, 0
+                continue
+            if ch == 10:
+                continue
+            b = self.REF.get(ch)
+            if b is None:
+                if ch == 0xFF:
+                    res.hit_eof_byte = 1
+                    res.scanned_bytes = pos
+                    return 0, res
+                if ch != ord("N"):
+                    res.unknown_chars += 1
+                R = 0
+                continue
+            rcode = ((rcode << 2) | b) & M64
+            R += 1
+            seq = int(np.int64(R & 0xFFFFFFFF).astype(np.int32))
+            if seq >= k:
+                idx = rcode & mask
+                self.tab[idx] += 1
+                res.windows += 1
+                res.depth1[idx >> (2 * k - 2)] += 1
+                if seq > k:
+                    res.valid_bases += 1
+                    res.base_count[b] += 1
+                else:
+                    res.valid_bases += k
+                    for j in range(k):
+                        res.base_count[(idx >> (2 * (k - 1 - j))) & 3] += 1
+            elif seq >= 1:
+                res.depth1[(rcode >> (2 * seq - 2)) & 3] += 1
+        res.scanned_bytes = len(self.data)
+        res.unterminated_header = hdr
+        return 0, res
+
+    def table(self):
+        return self.tab.copy()

@@ -1,10 +1,13 @@
 """Multi-process shard stitching on the CPU (world_size 2 and 3, gloo).
 
 Runs the real orchestration of findkmer_amd/dist.py (all-gather of shard
-summaries, composition with the C-ABI fk_summary_apply, all-reduce of the
-tables) with tests/scan_model.py standing in for the GPU engine.  Checks the
+summaries, composition with the C-ABI fk_summary_apply, the end-flag
+exchange, the reduce of tables + counter limbs) with
+tests/scan_model.ModelEngine standing in for the GPU engine.  Checks the
 stitched entering state of every shard against a direct scan of the prefix,
-and the merged table against the oracle on the whole input.
+and the merged table and counters against the oracle on the whole input --
+including inputs whose stream ends at a 0xFF byte in a middle shard (the
+reference's signed-char EOF, findKmer.cpp:988).
 """
 import os
 import random
@@ -48,7 +51,7 @@ def _input(seed, n):
     return bytes(out[:n])
 
 
-def _worker(rank, world, port, data, bounds, results):
+def _worker(rank, world, port, data, bounds, mode, results):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     import torch
@@ -58,35 +61,124 @@ def _worker(rank, world, port, data, bounds, results):
     try:
         lo, hi = bounds[rank], bounds[rank + 1]
         shard = data[lo:hi]
-        state = fkdist.stitch_entry_state(scan_model.summary_words(shard))
-        # the stitched state is the state a direct scan of the prefix reaches
         hdr, R, code, _, _ = scan_model.advance(data[:lo], 0, 0, 0)
-        assert state.hdr == hdr and state.run == R, (rank, state.hdr, hdr, state.run, R)
-        if not hdr:
-            nb = min(R, 32)
-            m = (1 << (2 * nb)) - 1
-            assert (state.code & m) == (scan_model.sigma(code) & m)
-        table = torch.zeros(1 << (2 * K), dtype=torch.int32)
-        t = table.numpy()
-        scan_model.count_from(shard, K, state.hdr, state.run, scan_model.sigma(state.code), t)
-        fkdist.sum_tables(table)
+        if mode == "state":
+            # the stitched state is the state a direct scan of the prefix reaches
+            state, _, _ = fkdist.stitch_entry_state(scan_model.summary_words(shard), full=True)
+            assert state.hdr == hdr and state.run == R, (rank, state.hdr, hdr, state.run, R)
+            if not hdr:
+                nb = min(R, 32)
+                m = (1 << (2 * nb)) - 1
+                assert (state.code & m) == (scan_model.sigma(code) & m)
+            return
+        guess = None
+        if mode == "compact":
+            guess = (hdr, R, code)                 # every guess right: no full round
+        elif mode == "compact_miss" and rank == 1:
+            guess = (1 - hdr, 0, 0)                # rank 1 guessed wrong: full summaries
+        elif mode == "compact_miss":
+            guess = (hdr, R, code)
+        eng = scan_model.ModelEngine(K, shard, guess)
+        buf = fkdist.merge_buffer(K, "cpu")
+        res = fkdist.count_sharded(eng, 0, len(shard), 0, buf)
         if rank == 0:
-            results.put(table.numpy().astype(np.uint32).tobytes())
+            out = {n: getattr(res, n) for n in ("windows", "valid_bases", "base_count", "depth1",
+                                                 "unknown_chars", "scanned_bytes", "hit_eof_byte",
+                                                 "unterminated_header", "distinct", "rollover")}
+            out["first_end"] = res.first_end
+            results.put((res.table.numpy().astype(np.uint32).tobytes(), out))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_stitch_and_merge_gloo(world):
+def _run(world, data, bounds, mode):
     import torch.multiprocessing as mp
-    data = _input(world, 24000)
-    n = len(data)
-    bounds = [0] + [n * i // world // 16 * 16 for i in range(1, world)] + [n]
     ctx = mp.get_context("spawn")
     results = ctx.SimpleQueue()
-    mp.start_processes(_worker, args=(world, _free_port(), data, bounds, results), nprocs=world,
+    mp.start_processes(_worker, args=(world, _free_port(), data, bounds, mode, results), nprocs=world,
                        join=True, start_method="spawn")
-    merged = np.frombuffer(results.get(), dtype=np.uint32)
-    want, res, _ = oracle.count_dense(data, K)
-    assert np.array_equal(merged, want)
-    assert int(merged.sum()) == res.windows
+    return None if mode == "state" else results.get()
+
+
+def _bounds(n, world):
+    return [0] + [n * i // world // 16 * 16 for i in range(1, world)] + [n]
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_stitched_states_gloo(world):
+    data = _input(world, 24000)
+    _run(world, data, _bounds(len(data), world), "state")
+
+
+def _check(data, world, mode, bounds=None):
+    bounds = bounds or _bounds(len(data), world)
+    table, got = _run(world, data, bounds, mode)
+    want, r, _ = oracle.count_dense(data, K)
+    assert np.array_equal(np.frombuffer(table, dtype=np.uint32), want)
+    assert got["windows"] == r.windows
+    assert got["valid_bases"] == r.valid_bases
+    assert got["base_count"] == list(r.base_count)
+    assert got["depth1"] == list(r.depth1)
+    assert got["unknown_chars"] == r.unknown_chars
+    assert got["scanned_bytes"] == r.scanned_bytes
+    assert got["hit_eof_byte"] == r.hit_eof_byte
+    assert got["unterminated_header"] == r.unterminated_header
+    assert got["distinct"] == r.distinct
+    assert not got["rollover"]
+    return got
+
+
+@pytest.mark.parametrize("world,mode", [(2, "full"), (3, "full"), (3, "compact"), (3, "compact_miss")])
+def test_merge_gloo(world, mode):
+    got = _check(_input(world + 7, 24000), world, mode)
+    assert got["first_end"] is None
+
+
+@pytest.mark.parametrize("mode", ["full", "compact", "compact_miss"])
+def test_eof_byte_in_middle_shard_gloo(mode):
+    """A 0xFF outside a header in rank 1's shard ends the stream there:
+    rank 2 (and rank 1's bytes after it) must count nothing."""
+    data = bytearray(_input(11, 24000))
+    n = len(data)
+    b = _bounds(n, 3)
+    # a 0xFF in the middle of rank 1's shard, outside any header
+    at = (b[1] + b[2]) // 2
+    data[at - 2:at + 1] = b"\nA\xff"
+    data = bytes(data)
+    _, r, _ = oracle.count_dense(data, K)
+    assert r.hit_eof_byte and r.scanned_bytes == at
+    got = _check(data, 3, mode, b)
+    assert got["first_end"] == 1
+
+
+def test_eof_byte_in_header_is_not_the_end_gloo():
+    """A 0xFF inside a '>' line is skipped with the header (:999-1005)."""
+    data = bytearray(_input(12, 24000))
+    b = _bounds(len(data), 3)
+    at = (b[1] + b[2]) // 2
+    data[at - 3:at + 3] = b"\n>\xff\xffx\n"
+    got = _check(bytes(data), 3, "full", b)
+    assert got["first_end"] is None and not got["hit_eof_byte"]
+
+
+def test_merged_rollover_detection():
+    """Rank 0's checks on the reduced buffer: a merged bin that wrapped past
+    2^32 (table total short of the window count), or a depth-1 counter
+    reaching 2^32, is the reference's COUNTER ROLLOVER exit (:642-648)."""
+    import torch
+    import findkmer_amd as fk
+    import findkmer_amd.dist as fkdist
+
+    def result(table_vals, windows, depth1=(0, 0, 0, 0)):
+        buf = fkdist.merge_buffer(2, "cpu")
+        buf[:16] = torch.tensor(np.array(table_vals, dtype=np.uint32).view(np.int32))
+        vals = [windows, 0, 0, 0, 0, 0, *depth1, 0, 0, 0, 0]
+        fkdist._put_counters(buf, vals, None)
+        return fkdist.ShardedResult(buf, 2, 0, None)
+
+    ok = result([3] * 15 + [0xFFFFFFFF], 45 + 0xFFFFFFFF)
+    assert not ok.rollover and ok.status() == fk.FK_OK and ok.distinct == 16
+    wrapped = result([3] * 15 + [4], 45 + (1 << 32) + 4)          # bin 15 reached 2^32 + 4
+    assert wrapped.rollover and wrapped.status() == fk.FK_E_ROLLOVER
+    deep = result([1] * 16, 16, depth1=(1 << 32, 0, 0, 0))
+    assert deep.rollover

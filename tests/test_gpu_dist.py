@@ -1,9 +1,8 @@
-"""Sharded multi-process path on the GPU box: bench.py under torchrun with
-two ranks sharing cuda:0 and host-side (gloo) collectives.  Exercises the
-real engine's feed_shard / summary / resolve / table exchange through
-findkmer_amd/dist.py; bench.py asserts the merged table and the summed
-window counts against the exact totals of the one stream.  (RCCL itself
-needs one GPU per rank: the driver's multi-GPU bench covers it.)"""
+"""Sharded multi-process path on the GPU box, two or three ranks sharing
+cuda:0 with host-side (gloo) collectives: the real engine's feed_shard /
+summary / resolve and findkmer_amd/dist.py's stitch, end-flag exchange and
+table + counter merge.  (RCCL itself needs one GPU per rank: the driver's
+multi-GPU bench covers it.)"""
 import json
 import os
 import subprocess
@@ -14,18 +13,39 @@ import pytest
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
+def _torchrun(nproc, port, script, args):
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(nproc),
+           "--master-addr", "127.0.0.1", "--master-port", str(port), script] + args
+    p = subprocess.run(cmd, cwd=REPO, capture_output=True, text=True, timeout=600)
+    assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-4000:]
+    line = [l for l in p.stdout.splitlines() if l.startswith("{")][-1]
+    return json.loads(line)
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("k,fasta,chrom", [(6, 0, 1_500_000_000), (11, 80, 1_500_000_000), (6, 0, 20_000_000),
                                            (7, 0, 12_799_900)])
 def test_two_rank_shards_gloo(k, fasta, chrom):
-    """chrom < 25.6M puts an 'N' run break inside rank 1's shard (20M), or in
-    its 256-byte halo (12_799_900: 100 bases before the shard)"""
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-           "--master-addr", "127.0.0.1", "--master-port", str(29600 + k + chrom % 97), os.path.join(REPO, "bench.py"),
-           "--gpus", "2", "--steps", "2", "--warmup", "1", "--no-cpu-baseline", "--dist-backend", "gloo",
-           "--k", str(k), "--fasta-line", str(fasta), "--bases", "12800000", "--chrom", str(chrom)]
-    p = subprocess.run(cmd, cwd=REPO, capture_output=True, text=True, timeout=600)
-    assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-4000:]
-    line = [l for l in p.stdout.splitlines() if l.startswith("{")][-1]
-    out = json.loads(line)
+    """bench.py under torchrun: chrom < 25.6M puts an 'N' run break inside
+    rank 1's shard (20M), or in its 256-byte halo (12_799_900: 100 bases
+    before the shard); bench.py asserts the merged windows and bases"""
+    out = _torchrun(2, 29600 + k + chrom % 97, os.path.join(REPO, "bench.py"),
+                    ["--gpus", "2", "--steps", "2", "--warmup", "1", "--no-cpu-baseline", "--dist-backend", "gloo",
+                     "--k", str(k), "--fasta-line", str(fasta), "--bases", "12800000", "--chrom", str(chrom)])
     assert out["n_gpus"] == 2 and out["value"] > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k,world,eof_in", [(6, 3, 1), (6, 3, -1), (11, 3, 1), (11, 2, 0), (5, 2, -1), (13, 3, 1)])
+def test_sharded_mixed_input_against_oracle(k, world, eof_in):
+    """headers, N runs, unknown bytes, ragged lines; eof_in >= 0: a 0xFF
+    byte ends the stream inside that rank's shard, and the later ranks'
+    counts must not reach the merged table"""
+    out = _torchrun(world, 29700 + 7 * k + world + eof_in, os.path.join(REPO, "tests", "dist_worker.py"),
+                    ["--k", str(k), "--eof-in", str(eof_in)])
+    assert out["table_equal"]
+    for key in ("windows", "valid_bases", "base_count", "depth1", "unknown_chars", "scanned_bytes",
+                "hit_eof_byte", "unterminated_header", "distinct"):
+        assert out[key][0] == out[key][1], (key, out[key])
+    assert not out["rollover"]
+    assert out["first_end"] == (eof_in if eof_in >= 0 else None)
