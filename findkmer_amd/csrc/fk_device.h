@@ -36,6 +36,11 @@ enum {
     ACC_UNK = 14,        /* "Unknown character" bytes */
     ACC_N = 16
 };
+/* The feed accumulators are FK_ACC_COPIES copies of ACC_N counters: a
+ * wave flushes into copy (global wave index % FK_ACC_COPIES), so the
+ * same-address atomics of thousands of waves finishing together spread over
+ * 16 lines; k_tail / k_table_stats sum and clear the copies. */
+#define FK_ACC_COPIES 16
 
 #define FK_NO_EOF 0xFFFFFFFFu
 #define FK_NO_EOF64 0xFFFFFFFFFFFFFFFFull
@@ -223,6 +228,54 @@ struct DevRes {
     uint32_t pad2;
     uint32_t seq;                   /* host copy: written last (feed sequence number) */
 };
+
+/* k_count's dynamic ranges (k <= 7, LDS bins; large segments).  Static
+ * ranges [0, nstatic) are one per wave, chunks [r*cpw, (r+1)*cpw); the rest
+ * of the segment, from chunk `base` on, is cut into ndyn smaller ranges
+ * (range ids nstatic + d, in stream order) in three tiers of shrinking size
+ * (sz[0] > sz[1] > sz[2] chunks).  A wave that is done with its static
+ * range claims dynamic ones from its block's pool (d % npools, in order of
+ * d: largest first) until it is empty: the fast waves of a CU take the work
+ * its slow ones would otherwise end with. */
+struct DynGeo {
+    uint64_t base;       /* first dynamic chunk */
+    uint64_t nchunks;    /* chunks of the segment */
+    uint32_t n[3];       /* ranges per tier */
+    uint32_t sz[3];      /* chunks per range of each tier */
+    uint32_t ndyn;       /* n[0] + n[1] + n[2] (0: static ranges only) */
+    uint32_t npools;     /* claim pools (d % npools), one per CU's pair of blocks */
+    /* static ranges by wave class: the first npools blocks (one per CU,
+       dispatched first) and the rest, waves 0-3 and 4-7 of each block: a
+       SIMD's four waves issue oldest first, so they stream at different
+       speeds, and each class gets a share of the work to match */
+    uint32_t cls[4];     /* chunks per static range: first-round waves 0-3, 4-7; second-round 0-3, 4-7 */
+};
+/* static range of wave w (dynamic-range mode) */
+__host__ __device__ inline void static_span(const DynGeo &g, uint64_t w, uint64_t &c0, uint64_t &c1) {
+    const uint64_t b = w / 8, wi = w % 8;
+    const bool first = b < g.npools;
+    const uint64_t a = first ? g.cls[0] : g.cls[2], bb = first ? g.cls[1] : g.cls[3];
+    const uint64_t blk0 = 4ull * g.cls[0] + 4ull * g.cls[1], blk1 = 4ull * g.cls[2] + 4ull * g.cls[3];
+    const uint64_t base = first ? b * blk0 : (uint64_t)g.npools * blk0 + (b - g.npools) * blk1;
+    c0 = base + (wi < 4 ? wi * a : 4 * a + (wi - 4) * bb);
+    c1 = c0 + (wi < 4 ? a : bb);
+}
+__host__ __device__ inline void dyn_span(const DynGeo &g, uint32_t d, uint64_t &c0, uint64_t &c1) {
+    uint64_t off = g.base;
+    uint32_t sz;
+    if (d < g.n[0]) {
+        off += (uint64_t)d * g.sz[0];
+        sz = g.sz[0];
+    } else if (d < g.n[0] + g.n[1]) {
+        off += (uint64_t)g.n[0] * g.sz[0] + (uint64_t)(d - g.n[0]) * g.sz[1];
+        sz = g.sz[1];
+    } else {
+        off += (uint64_t)g.n[0] * g.sz[0] + (uint64_t)g.n[1] * g.sz[1] + (uint64_t)(d - g.n[0] - g.n[1]) * g.sz[2];
+        sz = g.sz[2];
+    }
+    c0 = off;
+    c1 = off + sz < g.nchunks ? off + sz : g.nchunks;
+}
 
 /* what a one-pass k_count left for the host-launched kernels */
 enum { ONE_SCAN = 1u,     /* a guess check failed (or could not be made): k_scan, k_redo, k_table_stats */

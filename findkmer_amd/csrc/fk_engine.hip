@@ -682,13 +682,15 @@ __device__ void flush_counters(const Ctx &cx, Counters &cnt, uint32_t weight, bo
 #pragma unroll
     for (int i = 0; i < 11; i++) vals[i] = wsum32(vals[i]);
     if (lane == 0 && to_acc) {
+        unsigned long long *a =
+            cx.acc + ((blockIdx.x * FK_WAVES_PER_BLOCK + (threadIdx.x >> 6)) % FK_ACC_COPIES) * ACC_N;
 #pragma unroll
-        for (int i = 0; i < 4; i++) acc_add(&cx.acc[ACC_BASE + i], vals[i], weight);
-        acc_add(&cx.acc[ACC_VALID], vals[4], weight);
-        acc_add(&cx.acc[ACC_WIN], vals[5], weight);
+        for (int i = 0; i < 4; i++) acc_add(&a[ACC_BASE + i], vals[i], weight);
+        acc_add(&a[ACC_VALID], vals[4], weight);
+        acc_add(&a[ACC_WIN], vals[5], weight);
 #pragma unroll
-        for (int i = 0; i < 4; i++) acc_add(&cx.acc[ACC_D1S + i], vals[6 + i], weight);
-        acc_add(&cx.acc[ACC_UNK], vals[10], weight);
+        for (int i = 0; i < 4; i++) acc_add(&a[ACC_D1S + i], vals[6 + i], weight);
+        acc_add(&a[ACC_UNK], vals[10], weight);
     }
     cnt.base = cnt.d1s = 0;
     cnt.valid = cnt.win = cnt.win_u = 0;
@@ -918,6 +920,13 @@ __device__ unsigned long long g_tp[16];
 
 /* LDS layout of k_tail's last block */
 #define TAIL_BLOCKS 16u
+#define FK_DYN_TARGET 16384u   /* k_count: at most ~this many dynamic ranges per segment */
+#define FK_FLUSH_BYTES (1u << 20)   /* k_count: a wave flushes its counters after this many bytes */
+/* k_count's dynamic-range pool heads (one per CU's pair of blocks), 64 B apart */
+#define FK_HEAD_STRIDE 16u
+#define FK_HEADS_OFF 64u
+#define FK_MAX_POOLS 1024u
+#define FK_CTL_WORDS (FK_HEADS_OFF + FK_MAX_POOLS * FK_HEAD_STRIDE)
 #define TAIL_THREADS 512u
 
 /*
@@ -1031,18 +1040,193 @@ __device__ __forceinline__ void block_summary(const Ctx &cx, const OnePassCfg *o
  * the range from there.  A range counted to its end gets its RangeRec here.
  */
 #ifdef FK_WAVE_TIMES   /* experiment build (tools/wave_times.sh): per-wave start / loop end / end */
-__device__ unsigned long long fk_dbg_wt[32768 * 4];
+__device__ unsigned long long fk_dbg_wt[32768 * 8];
 extern "C" int fk_debug_wave_times(unsigned long long *out, int n) {
-    return hipMemcpyFromSymbol(out, HIP_SYMBOL(fk_dbg_wt), (size_t)n * 4 * sizeof(unsigned long long)) == hipSuccess ? 0 : -1;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(fk_dbg_wt), (size_t)n * 8 * sizeof(unsigned long long)) == hipSuccess ? 0 : -1;
 }
 #endif
+
+#if FK_EXP == 40
+__device__ uint32_t fk_exp_heads[32768 * 16];
+#endif
+
+/* A wave's next dynamic range (wave-uniform), from its block's pool: pool
+ * blockIdx % npools, whose ranges are d = p, p + npools, ... (largest first).
+ * The pools are sized for the two blocks one CU holds (blocks b and
+ * b + npools under the dispatcher's round-robin placement -- for speed only:
+ * any placement drains every pool, since each pool's blocks exist).  The
+ * waves of a CU run at different speeds (oldest-first issue: a SIMD's four
+ * waves finish a static range at 113 / 126 / 138 / 160 us at 1 GB), and the
+ * pool evens that out with a claim that only 16 waves contend for.
+ * Returns dg.ndyn when the pool is empty. */
+__device__ __forceinline__ uint32_t claim_dyn(uint32_t *heads, const DynGeo &dg) {
+    const uint32_t p = blockIdx.x % dg.npools;
+    const uint32_t np = dg.ndyn > p ? (dg.ndyn - 1 - p) / dg.npools + 1 : 0;
+    uint32_t j = np;
+    if ((threadIdx.x & 63) == 0) j = atomicAdd(&heads[p * FK_HEAD_STRIDE], 1u);
+    j = (uint32_t)__builtin_amdgcn_readfirstlane((int)j);
+    return j < np ? j * dg.npools + p : dg.ndyn;
+}
+
+/* interleaved tile loads: lane L takes bytes [16L, 16L+16) and [1024+16L, ...)
+   of a 2 KiB tile, so each instruction reads one contiguous KiB; the tile
+   base is clamped into the range (a scalar), so prefetches past its end
+   re-read its last full tile */
+#define FK_LOADI(dst, t_)                                                            \
+    {                                                                                \
+        const uint64_t tb_ = min(sp.rbase + (uint64_t)(t_) * FK_TILE_BYTES, last_tile); \
+        const u32x4 *p_ = reinterpret_cast<const u32x4 *>(cx.buf + tb_) + lane;      \
+        u32x4 v0_ = __builtin_nontemporal_load(p_);                                  \
+        u32x4 v1_ = __builtin_nontemporal_load(p_ + 64);                             \
+        dst[0] = v0_.x; dst[1] = v0_.y; dst[2] = v0_.z; dst[3] = v0_.w;               \
+        dst[4] = v1_.x; dst[5] = v1_.y; dst[6] = v1_.z; dst[7] = v1_.w;               \
+    }
+
+/* A range's prologue loads: the halo before it (lanes 0..7, 32 contiguous
+   bytes each, clamped to valid memory), then its first three tiles. */
+__device__ __forceinline__ void range_prologue(const Ctx &cx, const Span &sp, uint64_t last_tile, bool has,
+                                               uint32_t (&hw)[8], bool &hv, uint32_t (&A)[8], uint32_t (&B)[8],
+                                               uint32_t (&C)[8]) {
+    const int lane = threadIdx.x & 63;
+    const int64_t ho = (int64_t)sp.rbase - (int64_t)FK_HALO_BYTES + (int64_t)lane * FK_LANE_BYTES;
+    hv = has && lane < (int)(FK_HALO_BYTES / FK_LANE_BYTES) && ho >= cx.lo;
+    {
+        /* inputs shorter than a lane are staged in a large buffer, so
+           [lo, lo+32) is always readable */
+        const int64_t hc = max(min(ho, (int64_t)cx.len - (int64_t)FK_LANE_BYTES), cx.lo);
+        const u32x4 *hp = reinterpret_cast<const u32x4 *>(cx.buf + hc);
+        u32x4 h0 = __builtin_nontemporal_load(hp), h1 = __builtin_nontemporal_load(hp + 1);
+        hw[0] = h0.x; hw[1] = h0.y; hw[2] = h0.z; hw[3] = h0.w;
+        hw[4] = h1.x; hw[5] = h1.y; hw[6] = h1.z; hw[7] = h1.w;
+    }
+    if (sp.nfull) {
+        /* issue order A, B, C as in the loop (the barriers keep the compiler
+           from reordering them, which would merge two different pending-load
+           orders at the loop header) */
+        asm volatile("" ::: "memory");
+        FK_LOADI(A, 0);
+        asm volatile("" ::: "memory");
+        FK_LOADI(B, 1);
+        asm volatile("" ::: "memory");
+        FK_LOADI(C, 2);
+    }
+}
+
+/* Count range `rid` (chunks [c0, c1)) whose prologue loads are in flight,
+   and write its RangeRec (or, if it ran out of general tiles, a ResumeRec).
+   The wave's counters accumulate across its ranges (`cnt`, flushed by the
+   caller); `unk_seen` = the wave's unknown bytes counted before this range. */
+template <int HM>
+__device__ __forceinline__ void count_wave_range(const Ctx &cx, const Span &sp, uint64_t last_tile, uint64_t rid,
+                                                 uint64_t c0, uint64_t c1, uint32_t (&hw)[8], bool hv,
+                                                 uint32_t (&A)[8], uint32_t (&B)[8], uint32_t (&C)[8],
+                                                 const XState *d_init, int has_init, uint32_t op_flags,
+                                                 ResumeRec *resume, RangeRec *rr, uint32_t general_tiles,
+                                                 Counters &cnt, uint32_t &unk_seen) {
+    const int lane = threadIdx.x & 63;
+    DState st;
+    if (c0 == 0 && has_init) {
+        const XState in = (op_flags & OP_FRESH) ? XState{0, 0, 0, 0} : *d_init;
+        st.hdr = in.hdr;
+        st.R = (uint32_t)in.R;
+        st.code = in.code;
+    } else {
+#if FK_EXP >= 3   /* ablation: no halo guess */
+        st = DState{0, 100000u, 0};
+#else
+        st = halo_guess<HM>(cx, hw, hv);
+#endif
+    }
+    /* the halo words are waited for on every path (the d_init one too):
+       a load left pending into the loop makes its first tile wait for
+       vmcnt(0), i.e. for all three tiles in flight */
+    consume(hw);
+    const DState first = st;
+    Facts f{0, 0, 0, 0, 0, 0};
+    cnt.eof = FK_NO_EOF;
+    uint64_t t = 0;
+    uint32_t general_left = general_tiles;
+    bool primed = sp.nfull > 0;
+    for (;;) {
+        if (primed) {
+            /* one exit per group of three tiles and unconditional loads:
+               every path into the latch has the same loads in flight, so each
+               tile waits only for its own data */
+            bool live = st.hdr == 0;
+            for (uint64_t g = t; live; g += 3) {
+                live = t < sp.nfull && tile_fast<true, HM, true>(cx, A, st, f, cnt, 1u);
+                t += live;
+                consume(A);
+                FK_LOADI(A, g + 3);
+                live = live && t < sp.nfull && tile_fast<true, HM, true>(cx, B, st, f, cnt, 1u);
+                t += live;
+                consume(B);
+                FK_LOADI(B, g + 4);
+                live = live && t < sp.nfull && tile_fast<true, HM, true>(cx, C, st, f, cnt, 1u);
+                t += live;
+                consume(C);
+                FK_LOADI(C, g + 5);
+            }
+        }
+        if (t >= sp.ntiles || general_left == 0) break;
+        /* a tile the fast path cannot take (stream start, header, run
+           break, the ragged end): general path, then back to streaming */
+        general_left--;
+        uint32_t v[8];
+        const int64_t toff = (int64_t)(sp.rbase + t * FK_TILE_BYTES);
+        const int nb = load_lane<FK_LANE_BYTES>(cx, toff + lane * (int64_t)FK_LANE_BYTES, v);
+        tile_general<true, HM>(cx, v, nb, (uint32_t)(t * FK_TILE_BYTES), st, f, cnt, 1u);
+        consume(v);
+        t++;
+        primed = t < sp.nfull;
+        if (primed) {
+            asm volatile("" ::: "memory");
+            FK_LOADI(A, t);
+            asm volatile("" ::: "memory");
+            FK_LOADI(B, t + 1);
+            asm volatile("" ::: "memory");
+            FK_LOADI(C, t + 2);
+        }
+    }
+    const uint32_t unk_all = wsum32(cnt.unknown);
+    const uint32_t unk = unk_all - unk_seen;
+    unk_seen = unk_all;
+    const uint32_t eof = wmin32(cnt.eof);
+    if (lane == 0) {
+        if (t < sp.ntiles) {
+            ResumeRec q;
+            q.tile = t;
+            q.code = st.code; q.R = st.R; q.hdr = st.hdr;
+            q.a_code = first.code; q.a_R = first.R; q.a_hdr = first.hdr;
+            q.range = (uint32_t)rid;
+            q.unknown = unk;
+            q.eof = eof;
+            q.pad = 0;
+            q.f = f;
+            resume[rid] = q;
+            RangeRec &r = rr[rid];
+            r.c0 = c0; r.c1 = c1;
+            r.resume = 1;
+        } else {
+            RangeRec r;
+            r.tf = fk_tf_span(first, st, f);
+            r.a_code = first.code; r.a_R = first.R; r.a_hdr = first.hdr;
+            r.c0 = c0; r.c1 = c1;
+            r.eof = eof == FK_NO_EOF ? FK_NO_EOF64 : (uint64_t)eof;
+            r.unknown = unk;
+            r.resume = 0;
+            rr[rid] = r;
+        }
+    }
+}
 
 template <int HM>
 __global__ void __launch_bounds__(FK_BLOCK, 2)
 k_count(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint32_t *table,
         uint32_t *shortcnt, unsigned long long *acc, DevRes *res, RangeRec *rr,
         uint64_t nchunks, const XState *d_init, int has_init, uint64_t cpw, ResumeRec *resume,
-        uint32_t general_tiles, uint32_t *subs, const OnePassCfg *opc, uint32_t op_flags) {
+        uint32_t general_tiles, uint32_t *subs, const OnePassCfg *opc, uint32_t op_flags,
+        uint64_t nstatic, DynGeo dg, uint32_t *heads) {
     extern __shared__ uint32_t lds_bins[];
 #ifdef FK_WAVE_TIMES
     const unsigned long long wt0 = __builtin_amdgcn_s_memrealtime();
@@ -1065,164 +1249,114 @@ k_count(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uin
     Ctx cx{buf, len, lo, table, LDS_MODE(HM) ? lds_bins : nullptr, shortcnt, acc, res, maskk,
            1u << (2 * k + 2), k,
            subs ? subs + (size_t)(blockIdx.x % FK_SUBTABLES) * ((size_t)1 << (2 * k)) : nullptr};
-    const int lane = threadIdx.x & 63;
     const uint64_t wave = blockIdx.x * FK_WAVES_PER_BLOCK + wave_in_block();
-    const uint64_t c0 = wave * cpw, c1 = min(c0 + cpw, nchunks);
-    /* interleaved tile loads: lane L takes bytes [16L, 16L+16) and
-       [1024+16L, ...) of a 2 KiB tile, so each instruction reads one
-       contiguous KiB; the tile base is clamped into the range (a scalar), so
-       prefetches past its end re-read its last full tile */
-#define FK_LOADI(dst, t_)                                                            \
-    {                                                                                \
-        const uint64_t tb_ = min(sp.rbase + (uint64_t)(t_) * FK_TILE_BYTES, last_tile); \
-        const u32x4 *p_ = reinterpret_cast<const u32x4 *>(cx.buf + tb_) + lane;      \
-        u32x4 v0_ = __builtin_nontemporal_load(p_);                                  \
-        u32x4 v1_ = __builtin_nontemporal_load(p_ + 64);                             \
-        dst[0] = v0_.x; dst[1] = v0_.y; dst[2] = v0_.z; dst[3] = v0_.w;               \
-        dst[4] = v1_.x; dst[5] = v1_.y; dst[6] = v1_.z; dst[7] = v1_.w;               \
-    }
-    const bool has = c0 < c1;
+    /* the wave's static range; the static ranges end where the dynamic ones
+       begin */
+    const uint64_t send = dg.ndyn ? dg.base : nchunks;
+    uint64_t rid = wave;
+    uint64_t c0 = wave * cpw, c1 = min(c0 + cpw, send);
+    if (dg.ndyn) static_span(dg, wave, c0, c1);
+    bool has = wave < nstatic && c0 < c1;
     RangeRec hdr_r;
     hdr_r.c0 = has ? c0 : 0;
     hdr_r.c1 = has ? c1 : 0;
-    const Span sp = range_span(hdr_r, len);
-    const uint64_t last_tile = sp.nfull ? sp.rend - FK_TILE_BYTES : 0;
-    /* prologue, all loads first: the halo before the range (lanes 0..7, 32
-       contiguous bytes each, clamped to valid memory), then the first three
-       tiles; LDS is zeroed and the halo state computed while they fly */
-    uint32_t hw[8];
-    const int64_t ho = (int64_t)sp.rbase - (int64_t)FK_HALO_BYTES + (int64_t)lane * FK_LANE_BYTES;
-    const bool hv = has && lane < (int)(FK_HALO_BYTES / FK_LANE_BYTES) && ho >= lo;
-    {
-        /* inputs shorter than a lane are staged in a large buffer, so
-           [lo, lo+32) is always readable */
-        const int64_t hc = max(min(ho, (int64_t)len - (int64_t)FK_LANE_BYTES), lo);
-        const u32x4 *hp = reinterpret_cast<const u32x4 *>(buf + hc);
-        u32x4 h0 = __builtin_nontemporal_load(hp), h1 = __builtin_nontemporal_load(hp + 1);
-        hw[0] = h0.x; hw[1] = h0.y; hw[2] = h0.z; hw[3] = h0.w;
-        hw[4] = h1.x; hw[5] = h1.y; hw[6] = h1.z; hw[7] = h1.w;
-    }
-    uint32_t A[8], B[8], C[8];
-    if (sp.nfull) {
-        /* issue order A, B, C as in the loop (the barriers keep the compiler
-           from reordering them, which would merge two different pending-load
-           orders at the loop header) */
-        asm volatile("" ::: "memory");
-        FK_LOADI(A, 0);
-        asm volatile("" ::: "memory");
-        FK_LOADI(B, 1);
-        asm volatile("" ::: "memory");
-        FK_LOADI(C, 2);
-    }
+    Span sp = range_span(hdr_r, len);
+    uint64_t last_tile = sp.nfull ? sp.rend - FK_TILE_BYTES : 0;
+    /* prologue, all loads first; LDS is zeroed and the halo state computed
+       while they fly */
+    uint32_t hw[8], A[8], B[8], C[8];
+    bool hv;
+    range_prologue(cx, sp, last_tile, has, hw, hv, A, B, C);
     if (LDS_MODE(HM)) lds_zero(lds_bins, nw);
-    if (has) {
-        DState st;
-        if (c0 == 0 && has_init) {
-            const XState in = (op_flags & OP_FRESH) ? XState{0, 0, 0, 0} : *d_init;
-            st.hdr = in.hdr;
-            st.R = (uint32_t)in.R;
-            st.code = in.code;
-        } else {
-#if FK_EXP >= 3   /* ablation: no halo guess */
-            st = DState{0, 100000u, 0};
+#if FK_EXP == 41
+    uint32_t empty = 0;
+#endif
+    /* the wave's counters, flushed once per FK_FLUSH_BYTES of its ranges
+       (packed 16-bit fields per lane) and at the end: one set of
+       accumulator atomics per wave, not per range */
+    Counters cnt{0, 0, 0, 0, 0, FK_NO_EOF};
+    uint32_t unk_seen = 0;
+    uint64_t since = 0;
+#ifdef FK_WAVE_TIMES
+    unsigned long long wt_static = 0, wt_claim = 0, wt_ndyn = 0, wt_dbytes = 0;
+#endif
+    for (;;) {
+        if (has) {
+            count_wave_range<HM>(cx, sp, last_tile, rid, c0, c1, hw, hv, A, B, C, d_init, has_init, op_flags,
+                                 resume, rr, general_tiles, cnt, unk_seen);
+            since += sp.rend - sp.rbase;
+            if (since >= FK_FLUSH_BYTES) {
+                flush_counters(cx, cnt, 1u, HM != H_NONE);
+                cnt.unknown = 0;
+                unk_seen = 0;
+                since = 0;
+            }
+        }
+        if (dg.ndyn == 0) break;
+#ifdef FK_WAVE_TIMES
+        const unsigned long long wc0 = __builtin_amdgcn_s_memrealtime();
+        if (!wt_static) wt_static = wc0;
+#endif
+#if FK_EXP == 40 || FK_EXP == 41
+        /* experiments: wave-private interleaved pools (40: an uncontended
+           atomic per claim; 41: no atomic) */
+        uint32_t d;
+        {
+            const uint64_t W = (uint64_t)gridDim.x * FK_WAVES_PER_BLOCK;
+#if FK_EXP == 40
+            uint32_t j = 0;
+            if ((threadIdx.x & 63) == 0) j = atomicAdd(&fk_exp_heads[wave * 16], 1u);
+            j = (uint32_t)__builtin_amdgcn_readfirstlane((int)j);
 #else
-            st = halo_guess<HM>(cx, hw, hv);
+            const uint32_t j = empty++;
+#endif
+            const uint64_t dd = wave + (uint64_t)j * W;
+            d = dd < dg.ndyn ? (uint32_t)dd : dg.ndyn;
+#if FK_EXP == 40
+            if (d >= dg.ndyn && (threadIdx.x & 63) == 0) fk_exp_heads[wave * 16] = 0;
 #endif
         }
-        /* the halo words are waited for on every path (the d_init one too):
-           a load left pending into the loop makes its first tile wait for
-           vmcnt(0), i.e. for all three tiles in flight */
-        consume(hw);
-        const DState first = st;
-        Facts f{0, 0, 0, 0, 0, 0};
-        Counters cnt{0, 0, 0, 0, 0, FK_NO_EOF};
-        uint64_t t = 0;
-        uint32_t general_left = general_tiles;
-        bool primed = sp.nfull > 0;
-        for (;;) {
-            if (primed) {
-                /* one exit per group of three tiles and unconditional loads:
-                   every path into the latch has the same loads in flight, so each
-                   tile waits only for its own data */
-                bool live = st.hdr == 0;
-                for (uint64_t g = t; live; g += 3) {
-                    live = t < sp.nfull && tile_fast<true, HM, true>(cx, A, st, f, cnt, 1u);
-                    t += live;
-                    consume(A);
-                    FK_LOADI(A, g + 3);
-                    live = live && t < sp.nfull && tile_fast<true, HM, true>(cx, B, st, f, cnt, 1u);
-                    t += live;
-                    consume(B);
-                    FK_LOADI(B, g + 4);
-                    live = live && t < sp.nfull && tile_fast<true, HM, true>(cx, C, st, f, cnt, 1u);
-                    t += live;
-                    consume(C);
-                    FK_LOADI(C, g + 5);
-                }
-            }
-            if (t >= sp.ntiles || general_left == 0) break;
-            /* a tile the fast path cannot take (stream start, header, run
-               break, the ragged end): general path, then back to streaming */
-            general_left--;
-            uint32_t v[8];
-            const int64_t toff = (int64_t)(sp.rbase + t * FK_TILE_BYTES);
-            const int nb = load_lane<FK_LANE_BYTES>(cx, toff + lane * (int64_t)FK_LANE_BYTES, v);
-            tile_general<true, HM>(cx, v, nb, (uint32_t)(t * FK_TILE_BYTES), st, f, cnt, 1u);
-            consume(v);
-            t++;
-            primed = t < sp.nfull;
-            if (primed) {
-                asm volatile("" ::: "memory");
-                FK_LOADI(A, t);
-                asm volatile("" ::: "memory");
-                FK_LOADI(B, t + 1);
-                asm volatile("" ::: "memory");
-                FK_LOADI(C, t + 2);
-            }
-        }
-        flush_counters(cx, cnt, 1u, HM != H_NONE);
-        const uint32_t unk = wsum32(cnt.unknown);
-        const uint32_t eof = wmin32(cnt.eof);
-        if (lane == 0) {
-            if (t < sp.ntiles) {
-                ResumeRec q;
-                q.tile = t;
-                q.code = st.code; q.R = st.R; q.hdr = st.hdr;
-                q.a_code = first.code; q.a_R = first.R; q.a_hdr = first.hdr;
-                q.range = (uint32_t)wave;
-                q.unknown = unk;
-                q.eof = eof;
-                q.pad = 0;
-                q.f = f;
-                resume[wave] = q;
-                RangeRec &r = rr[wave];
-                r.c0 = c0; r.c1 = c1;
-                r.resume = 1;
-            } else {
-                RangeRec r;
-                r.tf = fk_tf_span(first, st, f);
-                r.a_code = first.code; r.a_R = first.R; r.a_hdr = first.hdr;
-                r.c0 = c0; r.c1 = c1;
-                r.eof = eof == FK_NO_EOF ? FK_NO_EOF64 : (uint64_t)eof;
-                r.unknown = unk;
-                r.resume = 0;
-                rr[wave] = r;
-            }
-        }
+#else
+        const uint32_t d = claim_dyn(heads, dg);
+#endif
+#ifdef FK_WAVE_TIMES
+        wt_claim += __builtin_amdgcn_s_memrealtime() - wc0;
+#endif
+        if (d >= dg.ndyn) break;
+#ifdef FK_WAVE_TIMES
+        wt_ndyn++;
+#endif
+        rid = nstatic + d;
+        dyn_span(dg, d, c0, c1);
+        hdr_r.c0 = c0;
+        hdr_r.c1 = c1;
+        sp = range_span(hdr_r, len);
+        last_tile = sp.nfull ? sp.rend - FK_TILE_BYTES : 0;
+        has = true;
+#ifdef FK_WAVE_TIMES
+        wt_dbytes += sp.rend - sp.rbase;
+#endif
+        range_prologue(cx, sp, last_tile, has, hw, hv, A, B, C);
     }
+    flush_counters(cx, cnt, 1u, HM != H_NONE);
 #ifdef FK_WAVE_TIMES
     const unsigned long long wt1 = __builtin_amdgcn_s_memrealtime();
 #endif
     if (LDS_MODE(HM)) {
         lds_flush<HM>(cx);
-        if ((op_flags & OP_ON) && threadIdx.x < 64) block_summary(cx, opc, rr, (nchunks + cpw - 1) / cpw);
+        if ((op_flags & OP_ON) && threadIdx.x < 64) block_summary(cx, opc, rr, nstatic);
     }
 #ifdef FK_WAVE_TIMES
     if ((threadIdx.x & 63) == 0 && wave < 32768) {
-        fk_dbg_wt[wave * 4 + 0] = wt0;
-        fk_dbg_wt[wave * 4 + 1] = wt1;
-        fk_dbg_wt[wave * 4 + 2] = __builtin_amdgcn_s_memrealtime();
-        fk_dbg_wt[wave * 4 + 3] = __builtin_amdgcn_s_getreg((20) | (0 << 6) | ((4 - 1) << 11)) & 0xF;
+        fk_dbg_wt[wave * 8 + 0] = wt0;
+        fk_dbg_wt[wave * 8 + 1] = wt1;
+        fk_dbg_wt[wave * 8 + 2] = __builtin_amdgcn_s_memrealtime();
+        fk_dbg_wt[wave * 8 + 3] = (__builtin_amdgcn_s_getreg((20) | (0 << 6) | ((4 - 1) << 11)) & 0xF) |
+                                  ((unsigned long long)__builtin_amdgcn_s_getreg((4) | (0 << 6) | ((32 - 1) << 11)) << 32);
+        fk_dbg_wt[wave * 8 + 4] = wt_static ? wt_static : wt1;
+        fk_dbg_wt[wave * 8 + 5] = wt_ndyn;
+        fk_dbg_wt[wave * 8 + 6] = wt_claim;
+        fk_dbg_wt[wave * 8 + 7] = wt_dbytes;
     }
 #endif
 }
@@ -1238,11 +1372,14 @@ template <int HM>
 __global__ void __launch_bounds__(FK_BLOCK)
 k_resume(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint32_t *table,
          uint32_t *shortcnt, unsigned long long *acc, DevRes *res, RangeRec *rr, uint64_t nranges,
-         const ResumeRec *resume) {
+         const ResumeRec *resume, uint32_t *heads) {
     extern __shared__ uint32_t lds_bins[];
     /* k_scan lists the ranges to redo after this kernel (a one-pass k_count
        that gave up may have listed some already) */
     if (blockIdx.x == 0 && threadIdx.x == 0) res->redo_n = 0;
+    /* k_count is done: reset its dynamic-range pools for the next launch */
+    if (blockIdx.x == 0)
+        for (uint32_t q = threadIdx.x; q < FK_MAX_POOLS; q += blockDim.x) heads[q * FK_HEAD_STRIDE] = 0;
     const uint64_t wave = blockIdx.x * FK_WAVES_PER_BLOCK + wave_in_block();
     const bool mine = wave < nranges && rr[wave].resume;
     /* uniform per block; in the LDS modes through the first bin (before the
@@ -1855,16 +1992,47 @@ __device__ __forceinline__ unsigned long long wmax64s(long long v) {
     return (unsigned long long)v;
 }
 
+/* Item i of k_tail's chain: a k_count block's BlockSum (i < G), else the
+ * dynamic range nstatic + (i - G), summarised here from its RangeRec as a
+ * block of one range would be (block_summary). */
+__device__ __forceinline__ BlockSum tail_item(const BlockSum *bsum, const RangeRec *rr, uint32_t G,
+                                              uint64_t nstatic, uint32_t i) {
+    if (i < G) return bsum[i];
+    const RangeRec q = rr[nstatic + (i - G)];
+    BlockSum b;
+    if (q.resume) {
+        b.e_R = 0; b.e_code = 0; b.e_hdr = 0;
+        b.g_code = 0; b.g_R = 0; b.g_hdr = 0;
+        b.nvb = 0; b.eof = ~0ull; b.nv = 0;
+        b.flags = ONE_RESUME;
+        return b;
+    }
+    const XState g{q.a_R, q.a_code, q.a_hdr, 0};
+    const XState e = fk_apply(q.tf, g);
+    b.e_R = e.R; b.e_code = e.code; b.e_hdr = e.hdr;
+    b.g_code = q.a_code; b.g_R = q.a_R; b.g_hdr = q.a_hdr;
+    b.nvb = (q.c1 - q.c0) * FK_CHUNK_BYTES;
+    b.eof = q.eof != FK_NO_EOF64 ? q.c0 * FK_CHUNK_BYTES + q.eof : ~0ull;
+    b.nv = q.tf.nv;
+    b.flags = q.tf.f0_const ? BS_ABSORB : 0u;
+    return b;
+}
+
 __global__ void __launch_bounds__(TAIL_THREADS)
 k_tail(const OnePassCfg *opc, uint32_t flags, uint32_t seq, uint32_t *table, int k, uint32_t *subs,
-       unsigned long long *facc, DevRes *res, const XState *d_init, uint32_t G, uint64_t seg_len,
-       TailPart *part, uint32_t *done) {
+       unsigned long long *facc, DevRes *res, const XState *d_init, uint32_t G0, uint64_t seg_len,
+       TailPart *part, uint32_t *done, const RangeRec *rr, uint64_t nstatic, uint32_t ndyn) {
     __shared__ unsigned long long sh[TAIL_THREADS / 64][16];
     __shared__ uint32_t bc[4];
     const uint32_t t = threadIdx.x, lane = t & 63, w = t >> 6, B = gridDim.x, jb = blockIdx.x;
     const uint32_t nbins = 1u << (2 * k);
     const bool fresh = (flags & OP_FRESH) != 0;
     const BlockSum *bsum = reinterpret_cast<const BlockSum *>(opc->bsum);
+    /* the chain: G0 block summaries, then the dynamic ranges */
+    const uint32_t G = G0 + ndyn;
+    /* k_count is done: reset its dynamic-range pools for the next launch */
+    if (jb == 0)
+        for (uint32_t q = t; q < FK_MAX_POOLS; q += blockDim.x) done[FK_HEADS_OFF + q * FK_HEAD_STRIDE] = 0;
 #if FK_EXP == 20
     if (t == 0) atomicMin(&g_tp[0], (unsigned long long)__builtin_amdgcn_s_memrealtime());
 #endif
@@ -1874,13 +2042,20 @@ k_tail(const OnePassCfg *opc, uint32_t flags, uint32_t seq, uint32_t *table, int
     const uint32_t b0 = (uint32_t)((uint64_t)G * jb / B), b1 = (uint32_t)((uint64_t)G * (jb + 1) / B);
     const uint32_t lo = (uint32_t)((uint64_t)nbins * jb / B), hi = (uint32_t)((uint64_t)nbins * (jb + 1) / B);
     const uint32_t bi = b0 + t;
-    const bool hb = bi < b1;   /* G <= 2 x CUs <= B x TAIL_THREADS: one BlockSum per thread at most */
+    const bool hb = bi < b1;   /* G <= B x TAIL_THREADS (host): one item per thread at most */
     BlockSum bs;
     uint64_t pe_R = 0, pe_code = 0;
     uint32_t pe_hdr = 0;
     if (hb) {
-        bs = bsum[bi];
-        if (bi > 0) { pe_R = bsum[bi - 1].e_R; pe_code = bsum[bi - 1].e_code; pe_hdr = bsum[bi - 1].e_hdr; }
+        bs = tail_item(bsum, rr, G0, nstatic, bi);
+        if (bi > 0) {
+            const BlockSum pb = tail_item(bsum, rr, G0, nstatic, bi - 1);
+            pe_R = pb.e_R; pe_code = pb.e_code; pe_hdr = pb.e_hdr;
+        }
+        /* a dynamic range's guess is its exact entering state when the feed
+           completes here (block_summary does this for the static ranges) */
+        if (bi >= G0 && !(bs.flags & ONE_RESUME))
+            opc->rtrue[nstatic + (bi - G0)] = XState{bs.g_R, bs.g_code, bs.g_hdr, 0};
     }
     const int fs = 2 * (k - 1);
     unsigned long long v10[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
@@ -1987,14 +2162,17 @@ k_tail(const OnePassCfg *opc, uint32_t flags, uint32_t seq, uint32_t *table, int
 #pragma unroll
             for (int q = 0; q < 10; q++) st[q] = 0;
         }
-        const BlockSum lb = bsum[G - 1];
+        const BlockSum lb = tail_item(bsum, rr, G0, nstatic, G - 1);
         /* a shard's entering state is unknown: count from its first guess
            (the host checks it against the stitched state at resolve) */
         const bool shard = (flags & OP_SHARD) != 0;
         const BlockSum b0s = bsum[0];
         const XState init = shard ? XState{b0s.g_R, b0s.g_code, b0s.g_hdr, 0}
                                   : fresh ? XState{0, 0, 0, 0} : *d_init;
-        const unsigned long long fa = lane < ACC_N ? facc[lane] : 0ull;
+        unsigned long long fa = 0;
+        if (lane < ACC_N)
+#pragma unroll
+            for (int c = 0; c < FK_ACC_COPIES; c++) fa += facc[c * ACC_N + lane];
         const unsigned long long ta = lane < ACC_N && !fresh ? opc->acc_total[lane] : 0ull;
 #pragma unroll
         for (int q = 0; q < 10; q++) st[q] = wsum64(st[q]);
@@ -2025,7 +2203,8 @@ k_tail(const OnePassCfg *opc, uint32_t flags, uint32_t seq, uint32_t *table, int
         if (need_all == 0 && lane < ACC_N) {
             const unsigned long long v = ta + fa;
             opc->acc_total[lane] = v;
-            facc[lane] = 0;
+#pragma unroll
+            for (int c = 0; c < FK_ACC_COPIES; c++) facc[c * ACC_N + lane] = 0;
             res->acc[lane] = v;
         }
         if (lane == 0) {
@@ -2096,9 +2275,12 @@ k_table_stats(uint32_t *table, uint64_t n, int k, DevRes *res,
     if (blockIdx.x == 0) {
         /* the feed's counters (facc, zero between feeds) join the engine's */
         if (threadIdx.x < ACC_N) {
-            const unsigned long long v = (fresh ? 0ull : acc[threadIdx.x]) + facc[threadIdx.x];
+            unsigned long long v = fresh ? 0ull : acc[threadIdx.x];
+#pragma unroll
+            for (int c = 0; c < FK_ACC_COPIES; c++) v += facc[c * ACC_N + threadIdx.x];
             acc[threadIdx.x] = v;
-            facc[threadIdx.x] = 0;
+#pragma unroll
+            for (int c = 0; c < FK_ACC_COPIES; c++) facc[c * ACC_N + threadIdx.x] = 0;
             res->acc[threadIdx.x] = v;
         }
         if (threadIdx.x == 0) res->need = 0;
@@ -2292,7 +2474,7 @@ __global__ void k_zero(uint32_t *table, uint64_t nbins, uint32_t *shortcnt, uint
     for (uint64_t i = i0; i < (uint64_t)nsub * nbins / 4; i += step) s4[i] = make_uint4(0, 0, 0, 0);
     for (uint64_t i = (nbins / 4) * 4 + i0; i < nbins; i += step) table[i] = 0;
     for (uint64_t i = i0; i < nshort; i += step) shortcnt[i] = 0;
-    if (i0 < 2 * ACC_N) acc[i0] = 0;   /* engine + feed accumulators */
+    if (i0 < (1 + FK_ACC_COPIES) * ACC_N) acc[i0] = 0;   /* engine + feed accumulators */
     if (i0 == 0) *state = XState{0, 0, 0, 0};
 }
 
@@ -2395,13 +2577,21 @@ struct fk_engine {
     uint32_t *d_table = nullptr, *d_short = nullptr;
     uint32_t *d_sub = nullptr;                /* FK_SUBTABLES table copies k_count flushes into (LDS modes) */
     unsigned long long *d_acc = nullptr;      /* ACC_N, engine lifetime (+ ACC_N: d_facc) */
-    unsigned long long *d_facc = nullptr;     /* ACC_N the counting kernels of a feed add into;
+    unsigned long long *d_facc = nullptr;     /* FK_ACC_COPIES x ACC_N the counting kernels of a feed add into;
                                                  merged into d_acc by the feed's publisher, zero between feeds */
     /* one-pass k_count (k <= 7, entering state known) */
     bool onepass = true;                      /* env FK_NO_ONEPASS=1: off */
     BlockSum *d_bsum = nullptr;               /* per block of k_count */
     uint32_t *d_ctl = nullptr;                /* k_tail's finished-block count */
     uint32_t ranges_per_wave = 1;             /* k <= 7: ranges per k_count wave slot (FK_RANGES_PER_WAVE) */
+    uint32_t static_pct = 100;                /* k <= 7: % of a large segment in static ranges (FK_STATIC_PCT;
+                                                 100 = no dynamic ranges: on a plain stream the waves that
+                                                 finish early hand their bandwidth to the others, so
+                                                 balancing gains nothing -- 1 GB k=6 0.174 ms either way --
+                                                 while header-dense input gains 9 % at 75) */
+    uint32_t cls_w[4] = {1000, 1000, 1000, 1000};   /* static share per wave class, per mille (FK_CLASS_W) */
+    uint64_t dyn_min_chunks = 0;              /* segments with dynamic ranges: >= this many chunks (0: 8 per
+                                                 wave slot; FK_DYN_MIN_CHUNKS, tests) */
     OnePassCfg *d_opc = nullptr;
     bool op_pending = false;                  /* the last count_segment launched a one-pass k_count */
     bool op_fresh = false;                    /* ... which did a pending reset itself */
@@ -2457,7 +2647,7 @@ __global__ void k_zero(uint32_t *table, uint64_t nbins, uint32_t *shortcnt, uint
 static int flush_zero(fk_engine *e) {
     if (!e->zero_pending) return FK_OK;
     e->zero_pending = false;
-    const uint64_t work = std::max<uint64_t>(e->nbins / 4, std::max<uint64_t>(e->nshort, ACC_N));
+    const uint64_t work = std::max<uint64_t>(e->nbins / 4, std::max<uint64_t>(e->nshort, (1 + FK_ACC_COPIES) * ACC_N));
     const unsigned grid = (unsigned)std::min<uint64_t>((uint64_t)e->cus * 8, (work + 255) / 256);
     hipLaunchKernelGGL(k_zero, dim3(grid), dim3(256), 0, e->stream, e->d_table, e->nbins, e->d_short, e->nshort,
                        e->d_acc, e->d_state, e->d_sub, e->d_sub ? FK_SUBTABLES : 0);
@@ -2603,6 +2793,14 @@ extern "C" int fk_engine_create(int k, const fk_opts *opts, fk_engine **out) {
     if (const char *ne = getenv("FK_NO_EVENTS")) e->timing = ne[0] != '1';
     if (const char *no = getenv("FK_NO_ONEPASS")) e->onepass = no[0] != '1';
     if (const char *rw = getenv("FK_RANGES_PER_WAVE")) e->ranges_per_wave = std::max(1u, (uint32_t)strtoul(rw, nullptr, 10));
+    if (const char *sp = getenv("FK_STATIC_PCT")) e->static_pct = std::min(100u, std::max(1u, (uint32_t)strtoul(sp, nullptr, 10)));
+    if (const char *dm = getenv("FK_DYN_MIN_CHUNKS")) e->dyn_min_chunks = strtoull(dm, nullptr, 10);
+    if (const char *cw = getenv("FK_CLASS_W")) {
+        unsigned a = 0, b = 0, c = 0, d = 0;
+        if (sscanf(cw, "%u,%u,%u,%u", &a, &b, &c, &d) == 4 && a && b && c && d) {
+            e->cls_w[0] = a; e->cls_w[1] = b; e->cls_w[2] = c; e->cls_w[3] = d;
+        }
+    }
     if (const char *pp = getenv("FK_PART_PAIRS_KMAX")) e->part_pairs_kmax = atoi(pp);
     if (const char *tb = getenv("FK_TS_BLOCKS")) e->ts_blocks = (uint32_t)strtoul(tb, nullptr, 10);
     if (e->opts.timing_every > 1) e->timing_every = (uint32_t)e->opts.timing_every;
@@ -2635,14 +2833,14 @@ extern "C" int fk_engine_create(int k, const fk_opts *opts, fk_engine **out) {
         }
     }
     if (e->nshort) { ALLOC(e->d_short, e->nshort * sizeof(uint32_t)); }
-    ALLOC(e->d_acc, 2 * ACC_N * sizeof(unsigned long long));
+    ALLOC(e->d_acc, (1 + FK_ACC_COPIES) * ACC_N * sizeof(unsigned long long));
     e->d_facc = e->d_acc + ACC_N;
     ALLOC(e->d_opc, sizeof(OnePassCfg));
-    ALLOC(e->d_ctl, 4 * sizeof(uint32_t));
+    ALLOC(e->d_ctl, FK_CTL_WORDS * sizeof(uint32_t));   /* [0] k_tail's block count; k_count's pool heads */
     /* the feed accumulators are zero between feeds (a fresh one-pass feed
        does not launch k_zero) */
-    if (hipMemsetAsync(e->d_acc, 0, 2 * ACC_N * sizeof(unsigned long long), e->stream) != hipSuccess ||
-        hipMemsetAsync(e->d_ctl, 0, 4 * sizeof(uint32_t), e->stream) != hipSuccess) {
+    if (hipMemsetAsync(e->d_acc, 0, (1 + FK_ACC_COPIES) * ACC_N * sizeof(unsigned long long), e->stream) != hipSuccess ||
+        hipMemsetAsync(e->d_ctl, 0, FK_CTL_WORDS * sizeof(uint32_t), e->stream) != hipSuccess) {
         fk_engine_destroy(e);
         return FK_E_HIP;
     }
@@ -2725,7 +2923,10 @@ static int grow_arrays(fk_engine *e, uint64_t nranges) {
 /* A segment's decomposition into per-wave chunk ranges. */
 struct Geo {
     uint64_t nchunks, cpw, nranges;
-    unsigned grid;
+    uint64_t nstatic;     /* static ranges (one per k_count wave) */
+    DynGeo dg;            /* the dynamic ranges after them (k <= 7) */
+    unsigned grid;        /* k_count's blocks */
+    unsigned rgrid;       /* blocks of the one-wave-per-range kernels (k_resume, k_redo) */
 };
 static Geo geometry(const fk_engine *e, uint64_t len) {
     Geo g;
@@ -2738,9 +2939,55 @@ static Geo geometry(const fk_engine *e, uint64_t len) {
        not fix it -- the dispatcher deals blocks to the XCDs round-robin --
        and cost LDS zero/flush per block: 4 rounds 0.29 ms vs 0.18 ms. */
     if (!e->part && !e->sparse && LDS_MODE(hist_mode(e))) max_waves *= e->ranges_per_wave;
-    g.cpw = std::max<uint64_t>(1, (g.nchunks + max_waves - 1) / max_waves);
-    g.nranges = (g.nchunks + g.cpw - 1) / g.cpw;
-    g.grid = (unsigned)std::max<uint64_t>(1, (g.nranges + FK_WAVES_PER_BLOCK - 1) / FK_WAVES_PER_BLOCK);
+    memset(&g.dg, 0, sizeof g.dg);
+    g.dg.nchunks = g.nchunks;
+    const uint64_t min_chunks = e->dyn_min_chunks ? e->dyn_min_chunks : 8 * max_waves;
+    const bool dyn = !e->part && !e->sparse && LDS_MODE(hist_mode(e)) && e->static_pct < 100 &&
+                     g.nchunks >= std::max<uint64_t>(min_chunks, 4);
+    if (dyn) {
+        /* static ranges cover static_pct % of the segment (one per wave, or
+           fewer for a short segment); the rest is cut into dynamic ranges of
+           4u, 2u and u chunks (half, a quarter and a quarter of it), u chosen
+           so that there are at most ~16 K of them */
+        const uint64_t sc = std::max<uint64_t>(1, g.nchunks * e->static_pct / 100);
+        g.cpw = std::max<uint64_t>(1, sc / max_waves);
+        g.nstatic = std::min<uint64_t>(max_waves, sc / g.cpw);
+        DynGeo &d = g.dg;
+        const uint64_t grid = (g.nstatic + FK_WAVES_PER_BLOCK - 1) / FK_WAVES_PER_BLOCK;
+        /* one pool per pair of k_count blocks (the blocks one CU holds) */
+        d.npools = (uint32_t)std::min<uint64_t>(FK_MAX_POOLS, std::max<uint64_t>(1, grid / blocks_per_cu(e)));
+        for (int c = 0; c < 4; c++) d.cls[c] = (uint32_t)g.cpw;
+        if (g.nstatic == max_waves && grid == 2ull * d.npools) {
+            /* weighted static ranges per wave class (cls_w, per mille) */
+            const uint64_t wsum = e->cls_w[0] + e->cls_w[1] + e->cls_w[2] + e->cls_w[3];
+            const uint64_t avg = sc / max_waves;
+            uint64_t tot = 0;
+            for (int c = 0; c < 4; c++) {
+                d.cls[c] = (uint32_t)std::max<uint64_t>(1, avg * e->cls_w[c] * 4 / wsum);
+                tot += d.cls[c];
+            }
+            if (tot * (max_waves / 4) >= g.nchunks)
+                for (int c = 0; c < 4; c++) d.cls[c] = (uint32_t)g.cpw;   /* keep a dynamic part */
+        }
+        const uint64_t stot = (uint64_t)d.npools * (4ull * d.cls[0] + 4ull * d.cls[1]) +
+                              (grid - std::min<uint64_t>(grid, d.npools)) * (4ull * d.cls[2] + 4ull * d.cls[3]);
+        const bool uniform = d.cls[0] == d.cls[1] && d.cls[1] == d.cls[2] && d.cls[2] == d.cls[3];
+        d.base = uniform ? g.nstatic * g.cpw : stot;
+        const uint64_t D = g.nchunks - d.base;
+        const uint64_t u = std::max<uint64_t>(1, (D + 2 * FK_DYN_TARGET - 1) / (2 * FK_DYN_TARGET));
+        d.sz[0] = (uint32_t)(4 * u); d.sz[1] = (uint32_t)(2 * u); d.sz[2] = (uint32_t)u;
+        d.n[0] = (uint32_t)(D / 2 / d.sz[0]);
+        d.n[1] = (uint32_t)(D / 4 / d.sz[1]);
+        const uint64_t rem = D - (uint64_t)d.n[0] * d.sz[0] - (uint64_t)d.n[1] * d.sz[1];
+        d.n[2] = (uint32_t)((rem + u - 1) / u);
+        d.ndyn = d.n[0] + d.n[1] + d.n[2];
+    } else {
+        g.cpw = std::max<uint64_t>(1, (g.nchunks + max_waves - 1) / max_waves);
+        g.nstatic = (g.nchunks + g.cpw - 1) / g.cpw;
+    }
+    g.nranges = g.nstatic + g.dg.ndyn;
+    g.grid = (unsigned)std::max<uint64_t>(1, (g.nstatic + FK_WAVES_PER_BLOCK - 1) / FK_WAVES_PER_BLOCK);
+    g.rgrid = (unsigned)std::max<uint64_t>(1, (g.nranges + FK_WAVES_PER_BLOCK - 1) / FK_WAVES_PER_BLOCK);
     return g;
 }
 
@@ -2769,13 +3016,17 @@ static int launch_count(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t 
                                       0, buf, len, lo, e->k,
                                    e->maskk, e->d_table, e->d_short, e->d_facc, e->d_res, e->d_rr,
                                    g.nchunks, e->d_state, has_init, g.cpw, e->d_resume, e->general_tiles,
-                                   e->d_sub, e->d_opc, flags));
+                                   e->d_sub, e->d_opc, flags, g.nstatic, g.dg, e->d_ctl + FK_HEADS_OFF));
     HIPCHK(hipGetLastError());
     if (onepass) {
         if (++e->res_seq == 0) e->res_seq = 1;
-        hipExtLaunchKernelGGL(k_tail, dim3(TAIL_BLOCKS), dim3(TAIL_THREADS), 0, e->stream, nullptr, tev(e, 2), 0,
+        /* one chain item per thread: the block summaries, then the dynamic ranges */
+        const uint64_t items = (uint64_t)g.grid + g.dg.ndyn;
+        const unsigned tb = (unsigned)std::max<uint64_t>(TAIL_BLOCKS, (items + TAIL_THREADS - 1) / TAIL_THREADS);
+        hipExtLaunchKernelGGL(k_tail, dim3(tb), dim3(TAIL_THREADS), 0, e->stream, nullptr, tev(e, 2), 0,
                               e->d_opc, flags, e->res_seq, e->d_table, e->k, e->d_sub, e->d_facc, e->d_res,
-                              e->d_state, g.grid, len, reinterpret_cast<TailPart *>(e->d_tpart), e->d_ctl);
+                              e->d_state, g.grid, len, reinterpret_cast<TailPart *>(e->d_tpart), e->d_ctl,
+                              e->d_rr, g.nstatic, g.dg.ndyn);
         HIPCHK(hipGetLastError());
     }
     return FK_OK;
@@ -2784,9 +3035,9 @@ static int launch_count(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t 
 static int launch_resume(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t lo, const Geo &g) {
     size_t sh = lds_bytes(e);
     FK_DISPATCH_COUNT(e,
-                hipLaunchKernelGGL((k_resume<HM>), dim3(g.grid), dim3(FK_BLOCK), sh, e->stream, buf, len, lo, e->k,
+                hipLaunchKernelGGL((k_resume<HM>), dim3(g.rgrid), dim3(FK_BLOCK), sh, e->stream, buf, len, lo, e->k,
                                    e->maskk, e->d_table, e->d_short, e->d_facc, e->d_res, e->d_rr, g.nranges,
-                                   e->d_resume));
+                                   e->d_resume, e->d_ctl + FK_HEADS_OFF));
     HIPCHK(hipGetLastError());
     return FK_OK;
 }
@@ -2795,7 +3046,7 @@ static int launch_redo(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t l
                        uint64_t *slots = nullptr) {
     size_t sh = lds_bytes(e);
     FK_DISPATCH(hist_mode(e),
-                hipLaunchKernelGGL((k_redo<HM>), dim3(g.grid), dim3(FK_BLOCK), sh, e->stream, buf, len, lo, e->k,
+                hipLaunchKernelGGL((k_redo<HM>), dim3(g.rgrid), dim3(FK_BLOCK), sh, e->stream, buf, len, lo, e->k,
                                    e->maskk, e->d_table, e->d_short, e->d_facc, e->d_res, e->d_rr,
                                    e->d_rtrue, e->d_redo, g.nranges, mode, slots));
     HIPCHK(hipGetLastError());
@@ -3412,6 +3663,19 @@ extern "C" int fk_engine_resolve(fk_engine *e, const fk_state *entering) {
         e->state = in;
         return FK_OK;
     }
+    /* the shard's compact summary, taken while the shard is still pending
+       (fk_engine_summary describes a pending shard only) */
+    fk_summary s;
+    bool compact = false;
+    if (e->shard_len && e->shard_op) {
+        rc = shard_wait(e);
+        if (rc) return rc;
+        if (e->last.need == 0 && !e->shard_full) {
+            rc = fk_engine_summary(e, &s);
+            if (rc) return rc;
+            compact = s.w[11] == FK_SUMMARY_COMPACT;
+        }
+    }
     e->shard_pending = 0;
     e->state = in;
     if (e->shard_len == 0) {
@@ -3421,12 +3685,7 @@ extern "C" int fk_engine_resolve(fk_engine *e, const fk_state *entering) {
     }
     Geo g = geometry(e, e->shard_len);
     if (e->shard_op) {
-        rc = shard_wait(e);
-        if (rc) return rc;
-        if (e->last.need == 0 && !e->shard_full) {
-            fk_summary s;
-            rc = fk_engine_summary(e, &s);
-            if (rc) return rc;
+        if (compact) {
             XState ex;
             if (compact_apply(&s, in, ex)) {
                 /* the guessed states count exactly: nothing to recount */

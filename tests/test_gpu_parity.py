@@ -90,6 +90,12 @@ def shard_count(data, k, nshards, summaries=False):
             shard_count.compact_failed += 1
         for e, st in zip(engines, entering):
             e.resolve(st)
+        # a full summary does not know where the stream ends: as dist.py
+        # does, the shards after the first one that ended contribute nothing
+        ends = [i for i, e in enumerate(engines) if e.state().ended]
+        if ends:
+            for e in engines[ends[0] + 1:]:
+                e.reset()
     else:
         st = fk.FkState()
         for e in engines:
@@ -676,3 +682,116 @@ def test_sparse_dense_entry_points_refuse():
             e.table_range(0, 16)
     rc, _, _ = (None, None, None)
     assert fk.lib().fk_count(None, 0, 17, None, None, None) == fk.FK_E_K_UNSUPPORTED
+
+
+# ---- k_count's dynamic ranges (k <= 7): static ranges, then claims --------
+# FK_STATIC_PCT < 100 turns them on (the product default is 100: static
+# ranges only, measured as fast on plain streams) and FK_DYN_MIN_CHUNKS=1 for
+# inputs of any size (else only segments of >= 8 chunks per wave slot), so
+# the claim path, k_tail's per-range chain items and the multi-launch
+# fallbacks over dynamic ranges all meet the oracle here.
+
+@pytest.fixture
+def dyn_env(monkeypatch):
+    monkeypatch.setenv("FK_DYN_MIN_CHUNKS", "1")
+    monkeypatch.setenv("FK_STATIC_PCT", "75")
+    yield
+
+
+@pytest.mark.parametrize("seed", range(3))
+@pytest.mark.parametrize("k", [2, 5, 6, 7])
+def test_dynamic_ranges_mixed(dyn_env, seed, k):
+    data = mixed_input(3000 + seed, 2_000_000 + 700_000 * seed)
+    assert_same(data, k)
+    assert_same(data, k, want_nodes=False)
+
+
+@pytest.mark.parametrize("k", [3, 6, 7])
+def test_dynamic_ranges_headers_and_resume(dyn_env, k):
+    assert_same(_long_header_input(900 + k, 3_000_000), k, want_nodes=False)
+    rng = random.Random(78 + k)
+    out = bytearray()
+    while len(out) < 2_000_000:
+        out += b">" + bytes(rng.choices(b"ACGT xyz", k=rng.randint(5, 60))) + b"\n"
+        out += bytes(rng.choices(b"ACGT", k=rng.randint(20, 300))) + b"\n"
+    assert_same(bytes(out), k, want_nodes=False)
+
+
+@pytest.mark.parametrize("k", [4, 6, 7])
+def test_dynamic_ranges_acgt_and_streaming(dyn_env, k):
+    data = bytes(random.Random(k).choices(b"ACGT", k=6_000_001))
+    assert_same(data, k, want_nodes=False)
+    mixed = mixed_input(99, 3_000_000)
+    assert_same(mixed, k, feeds=[1_000_000, 17, 65536, len(mixed) - 1_065_553])
+
+
+@pytest.mark.parametrize("k", [5, 6])
+@pytest.mark.parametrize("pct", ["1", "50", "99"])
+def test_dynamic_ranges_static_share(dyn_env, monkeypatch, k, pct):
+    """from almost all dynamic to almost all static"""
+    monkeypatch.setenv("FK_STATIC_PCT", pct)
+    data = mixed_input(4000 + int(pct), 2_500_000)
+    assert_same(data, k, want_nodes=False)
+
+
+@pytest.mark.parametrize("k", [6, 7])
+@pytest.mark.parametrize("nshards", [2, 3])
+def test_dynamic_ranges_shards(dyn_env, k, nshards):
+    data = mixed_input(55 + nshards, 3_000_000).replace(b"\xff", b"Z") + b"\nACGT"
+    t_o, r_o, _ = oracle.count_dense(data, k)
+    t_g, r_g, ub, rc = shard_count(data, k, nshards, summaries=True)
+    assert np.array_equal(t_o, t_g)
+    assert r_g.windows == r_o.windows and r_g.valid_bases == r_o.valid_bases
+    assert list(r_g.base_count) == list(r_o.base_count)
+
+
+@pytest.mark.parametrize("k", [6, 11])
+@pytest.mark.parametrize("summaries", [False, True])
+def test_shards_with_eof_byte(k, summaries):
+    """a 0xFF outside a header in the second of three shards ends the stream
+    there: the chained state is `ended` and the third shard counts nothing"""
+    base = mixed_input(808, 3 * 400_000).replace(b"\xff", b"Z")
+    data = bytearray(base)
+    at = len(data) // 2
+    data[at - 2:at + 1] = b"\nA\xff"
+    data = bytes(data)
+    t_o, r_o, _ = oracle.count_dense(data, k)
+    assert r_o.hit_eof_byte
+    t_g, r_g, ub, rc = shard_count(data, k, 3, summaries=summaries)
+    assert np.array_equal(t_o, t_g)
+    assert r_g.windows == r_o.windows and r_g.valid_bases == r_o.valid_bases
+    assert list(r_g.base_count) == list(r_o.base_count)
+
+
+@pytest.mark.parametrize("k", [4, 6, 7, 11])
+@pytest.mark.parametrize("kind", ["mixed", "acgt"])
+def test_shard_exit_states_match_stream(k, kind):
+    """after resolve, a shard engine's state is the stream's state at the
+    shard's end (one engine fed the prefix): the compact path of
+    fk_engine_resolve must apply the shard's own summary"""
+    if kind == "mixed":
+        data = mixed_input(31 + k, 1_500_000).replace(b"\xff", b"Z")
+    else:
+        data = bytes(random.Random(k).choices(b"ACGT", k=1_200_000))
+    import torch
+    arr = np.frombuffer(data, dtype=np.uint8)
+    n = len(arr)
+    per = (n // 3) // 65536 * 65536
+    bounds = [0, per, 2 * per, n]
+    dev = torch.from_numpy(arr.copy()).cuda()
+    torch.cuda.synchronize()
+    want = []
+    with fk.Engine(k) as e:
+        for i in range(3):
+            e.feed(np.ascontiguousarray(arr[bounds[i]:bounds[i + 1]]))
+            s = e.state()
+            want.append((s.hdr, s.run, s.code & ((1 << (2 * min(s.run, 31))) - 1) if not s.hdr else 0))
+    st = fk.FkState()
+    for i in range(3):
+        with fk.Engine(k) as e:
+            lo, hi = bounds[i], bounds[i + 1]
+            e.feed_shard_device(dev.data_ptr() + lo, hi - lo, min(256, lo))
+            e.resolve(st)
+            st = e.state()
+            got = (st.hdr, st.run, st.code & ((1 << (2 * min(st.run, 31))) - 1) if not st.hdr else 0)
+            assert got == want[i], (i, got, want[i])
