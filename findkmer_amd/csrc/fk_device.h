@@ -286,7 +286,8 @@ enum { ONE_SCAN = 1u,     /* a guess check failed (or could not be made): k_scan
  * counting loop carries no extra kernel arguments. */
 enum { OP_ON = 1u,        /* one pass: k_count summarises its blocks, k_tail finishes */
        OP_FRESH = 2u,     /* a reset is pending: zero table, state and accumulators */
-       OP_SHARD = 4u };   /* a shard: the entering state is the first guess until resolved */
+       OP_SHARD = 4u,     /* a shard: the entering state is the first guess until resolved */
+       OP_NOMIX = 8u };   /* no mixed tiles (FK_NO_MIXED=1: the general byte walk instead) */
 struct OnePassCfg {
     void *bsum;                      /* per k_count block: a BlockSum (fk_engine.hip) */
     XState *rtrue;                   /* entering state per range */

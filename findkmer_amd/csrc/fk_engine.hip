@@ -145,6 +145,8 @@ enum HistMode {
 struct Emit {
     uint32_t AC, A2, BC, B2;
     bool h0, h1, deep;
+    bool masked;        /* a mixed tile (tile_mixed): cm says which slots end a window */
+    uint32_t cm;        /* half 0 in bits 15:0, half 1 in 31:16; bit 15 - s = slot s */
 };
 
 struct Ctx {            /* kernel-wide constants */
@@ -652,6 +654,293 @@ __device__ __forceinline__ bool tile_fast(const Ctx &cx, const uint32_t w[8], DS
     return tile_finish<COUNT, HM, INTER, true>(cx, x, nl0, nl1, st, f, cnt, weight, em);
 }
 
+/*
+ * Mixed tile: any bytes (comment lines, run breaks, several newlines, N,
+ * unknown bytes, 0xFF), interleaved layout, counted without a byte walk.  The
+ * tile is two sub-tiles of 1 KiB (half h of every lane: the 16 bytes at
+ * h*1024 + 16L), counted in stream order by sub_mixed.  Per lane, over its 16
+ * bytes as bit masks (bit j = byte j):
+ *   - byte classes ('\n', '>', not a base) by SWAR byte compares;
+ *   - the comment flag entering each lane from two ballots (is the last '>'
+ *     or '\n' before it a '>'), then the comment bytes by one add: a '>'
+ *     starts a carry that runs through the bytes up to the next '\n'
+ *     (findKmer.cpp:991-1008; a '>' inside a comment changes nothing);
+ *   - takes (bases outside comments) and breaks (every other byte outside
+ *     comments but '\n', :1011-1024), and run starts (a take whose last take
+ *     or break before it is a break) by the same add;
+ *   - the takes' 2-bit codes compacted (blocks of other bytes squeezed out),
+ *     right-aligned: the lane's digit stream;
+ *   - the wave scan of (reset, bases since, code) that tile_general uses gives
+ *     each lane its entering run length R and last 32 bases;
+ *   - the slots that end a window (R >= k, :1035-1057) form a 16-bit mask W;
+ *     windows go to the bins as in half_windows (a (k+1)-mer pair where both
+ *     of a pair's slots count, else a single k-mer), or to the partition with
+ *     the mask (H_EMIT).
+ * The rare parts -- a run's first window (its first k-1 bases), the depth-1
+ * touches of a run's first k-1 bases, runs shorter than k (:1059-1062), N,
+ * unknown and 0xFF bytes -- loop over set bits, only in lanes that have them.
+ * Not for the sparse mode or near the reference's int32 seqSize wrap: the
+ * caller runs tile_general then.
+ */
+__device__ __forceinline__ uint32_t zero_bytes(uint32_t d) {   /* bit 7 of each byte: byte == 0 */
+    return ~(((d & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | d) & 0x80808080u;
+}
+__device__ __forceinline__ uint32_t bits4(uint32_t m) {   /* bit 7 of byte j -> bit j */
+    return __builtin_amdgcn_udot4((m >> 7) & 0x01010101u, 0x08040201u, 0u, false);
+}
+__device__ __forceinline__ uint32_t hibit(uint32_t v) { return 31u - (uint32_t)__clz((int)v); }   /* v != 0 */
+
+/* One sub-tile (16 bytes per lane at byte sub_off + 16L of the range).  Out:
+   the lane's window words {C, S2} (S2 = the 16 slots ending at its last
+   base, C the 16 before) and the slot mask W (bit 15 - s = slot s). */
+template <int HM>
+__device__ __forceinline__ void sub_mixed(const Ctx &cx, const uint32_t q[4], uint32_t sub_off, DState &st,
+                                          Facts &f, Counters &cnt, uint32_t weight, uint32_t &oC, uint32_t &oS2,
+                                          uint32_t &oW, bool &plain) {
+    const uint32_t lane = threadIdx.x & 63;
+    const int k = cx.k;
+    /* -- 1. classes */
+    uint32_t x[4], nbm = 0, nlm = 0, gtm = 0;
+#pragma unroll
+    for (int d = 0; d < 4; d++) {
+        x[d] = (q[d] >> 1) & 0x03030303u;
+        const uint32_t mb = __builtin_amdgcn_perm(0u, 0x47544341u, x[d]) ^ q[d];   /* 0: A/C/G/T */
+        nbm |= bits4(nz_bytes(mb)) << (4 * d);
+        nlm |= bits4(zero_bytes(q[d] ^ 0x0A0A0A0Au)) << (4 * d);
+        gtm |= bits4(zero_bytes(q[d] ^ 0x3E3E3E3Eu)) << (4 * d);
+    }
+    /* -- 2. comment flag entering each lane, and after the sub-tile */
+    const uint32_t ev = nlm | gtm;
+    const bool lgt = ev != 0 && ((gtm >> hibit(ev | 1u)) & 1u);
+    const uint64_t bev = __ballot(ev != 0), bgt = __ballot(lgt);
+    const uint64_t before = bev & ((1ull << lane) - 1ull);
+    const uint32_t hin = before ? (uint32_t)(bgt >> (63 - __clzll((long long)before))) & 1u : st.hdr;
+    const uint32_t hout = bev ? (uint32_t)(bgt >> (63 - __clzll((long long)bev))) & 1u : st.hdr;
+    /* -- 3. comment bytes (bit j: inside a comment before byte j), takes, breaks */
+    const uint32_t pm = ((~nlm & 0xFFFFu) << 1) | hin, am = (gtm << 1) | hin;
+    const uint32_t hb = (((pm + am) ^ pm) | am) & ~(nlm << 1) & 0xFFFFu;
+    const uint32_t T = ~nbm & ~hb & 0xFFFFu;
+    const uint32_t K = nbm & ~nlm & ~hb & 0xFFFFu;
+    const uint32_t oth = K & ~gtm;   /* N, 0xFF, unknown */
+    if (__ballot(oth != 0)) {
+        uint32_t nm = 0, fm = 0;
+#pragma unroll
+        for (int d = 0; d < 4; d++) {
+            nm |= bits4(zero_bytes(q[d] ^ 0x4E4E4E4Eu)) << (4 * d);
+            fm |= bits4(zero_bytes(~q[d])) << (4 * d);
+        }
+        cnt.unknown += __popc(oth & ~nm & ~fm);
+        const uint32_t ff = oth & fm;
+        if (ff) cnt.eof = min(cnt.eof, sub_off + 16u * lane + (uint32_t)(__ffs((int)ff) - 1));
+    }
+    /* -- 4. run starts; trailk: a break after the lane's last take */
+    const uint32_t pz = ~T & 0xFFFFu, zs = pz + K;
+    const uint32_t rbb = ((zs ^ pz) | K) & T;
+    const uint32_t trailk = zs >> 16;
+    /* -- 5. compaction: digit j at bit 15 - j, blocks of non-takes squeezed out
+       from the first one on (the digits before a block move down past it) */
+    const uint32_t nt = __popc(T);
+    uint32_t P = pack16(x);
+    uint32_t U = __builtin_bitreverse32(pz) >> 16;
+    uint32_t RB = __builtin_bitreverse32(rbb) >> 16;
+    while (__ballot(U != 0)) {
+        if (U) {
+            const uint32_t hi = hibit(U);
+            const uint32_t V = ~U & ((1u << hi) - 1u);
+            const uint32_t lo = V ? hibit(V) + 1u : 0u;
+            const uint32_t L = hi - lo + 1u;
+            const uint32_t k2 = (1u << (2u * lo)) - 1u, k1 = (1u << lo) - 1u;
+            P = (P & k2) | ((uint32_t)((uint64_t)P >> (2u * L)) & ~k2);
+            RB = (RB & k1) | ((RB >> L) & ~k1);
+            U &= k1;
+        }
+    }
+    /* -- 6. scan of (reset, bases since the last break, code) */
+    const uint32_t after_k = K ? ~((2u << hibit(K)) - 1u) : 0xFFFFFFFFu;
+    uint32_t p = (K ? 0x80000000u : 0u) | (uint32_t)__popc(T & after_k);
+    uint64_t cd = P;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t tp = shup(p, d);
+        const uint32_t tlo = shup((uint32_t)cd, d), thi = shup((uint32_t)(cd >> 32), d);
+        if (lane >= (uint32_t)d && !(p >> 31)) {
+            const uint32_t mynv = p & 0x7FFFFFFFu;
+            cd = fk_join(((uint64_t)thi << 32) | tlo, cd, mynv);
+            p = (tp & 0x80000000u) | ((tp & 0x7FFFFFFFu) + mynv);
+        }
+    }
+    const uint32_t p63 = rdlane(p, 63);
+    const uint64_t cd63 = rdlane64(cd, 63);
+    uint32_t ep = shup(p, 1);
+    uint32_t elo = shup((uint32_t)cd, 1), ehi = shup((uint32_t)(cd >> 32), 1);
+    if (lane == 0) { ep = 0; elo = 0; ehi = 0; }
+    const uint64_t ecd = ((uint64_t)ehi << 32) | elo;
+    const uint32_t Rin = (ep >> 31) ? (ep & 0x7FFFFFFFu) : st.R + (ep & 0x7FFFFFFFu);
+    const uint64_t cin = (ep >> 31) ? ecd : fk_join(st.code, ecd, ep & 0x7FFFFFFFu);
+    /* -- 7. facts (before the window work: what they need dies here): the span's first '\n' or '>' (any state), breaks, bases */
+    const bool anyk = __ballot(K != 0) != 0;
+    if (!f.found_p1 && bev) {
+        const int L1 = __ffsll((long long)bev) - 1;
+        const uint32_t jf = ev ? (uint32_t)(__ffs((int)ev) - 1) : 0u;
+        const uint32_t below = (1u << jf) - 1u, kb = K & below;
+        const uint32_t r = kb ? (uint32_t)__popc(T & below & ~((2u << hibit(kb)) - 1u)) : Rin + (uint32_t)__popc(T & below);
+        const bool after = lane > (uint32_t)L1 ? K != 0 : (lane == (uint32_t)L1 && (K >> (jf + 1u)) != 0);
+        if (__ballot(after)) f.reset_after_p1 = 1;
+        f.found_p1 = 1;
+        f.p1_gt = rdlane((gtm >> jf) & 1u, L1);
+        f.R_at_p1 = rdlane(r, L1);
+    } else if (f.found_p1 && anyk) {
+        f.reset_after_p1 = 1;
+    }
+    if (anyk) f.any_reset = 1;
+    else f.nv_total += p63 & 0x7FFFFFFFu;
+    /* bases only, at most one '\n' per lane, outside comments: the fast path's kind */
+    plain = !anyk && st.hdr == 0 && hout == 0 && !__ballot(gtm != 0 || __popc(nlm) > 1);
+    /* -- 8. digits with 1 <= R < k (F) and the window slots (W) */
+    const uint32_t vd = (1u << nt) - 1u;
+    uint32_t F = 0;
+    if (k > 1) {
+        uint32_t s = RB;   /* each run start covers its first k-1 digits */
+        for (int cov = 1; cov < k - 1;) {
+            const int sh = min(cov, k - 1 - cov);
+            s |= s >> sh;
+            cov += sh;
+        }
+        F = s;
+        if (Rin < (uint32_t)(k - 1)) {
+            const uint32_t m = min(nt, (uint32_t)(k - 1) - Rin);
+            F |= vd & ~((1u << (nt - m)) - 1u);
+        }
+        F &= vd;
+    }
+    const uint32_t W = vd & ~F;
+    const uint64_t full = (cin << (2u * nt)) | P;   /* the last 32 bases up to the lane's last take */
+    const uint32_t C = (uint32_t)(full >> 32), S2 = (uint32_t)full;
+    cnt.win += __popc(W);
+    if (HM == H_PAIRS) {
+        /* pair j: slots 2j, 2j + 1; {C, S2} << 2 puts slot 15's pair at 0 */
+        const uint32_t m2 = (uint32_t)cx.maskk << 2, m3 = (uint32_t)((cx.maskk << 2) | 3u) << 2;
+        const uint32_t S4 = S2 << 2;
+#pragma unroll 2
+        for (uint32_t j = 0; j < 8; j++) {
+            const uint32_t two = (W >> (14u - 2u * j)) & 3u;   /* bit 1: slot 2j, bit 0: slot 2j + 1 */
+            const uint32_t odd = j < 7u ? __builtin_amdgcn_alignbit(C, S2, 26u - 4u * j) : S4;
+            if (two == 3u) lds_add(cx, odd & m3, weight);
+            if (two == 1u || two == 2u) {
+                const uint32_t a = two == 1u ? odd : __builtin_amdgcn_alignbit(C, S2, 28u - 4u * j);
+                lds_add(cx, cx.single_off * 4u + (a & m2), weight);
+            }
+        }
+    } else if (HM == H_LDS || HM == H_GLOBAL) {
+#pragma unroll 2
+        for (uint32_t i = 0; i < 16; i++) {
+            if ((W >> (15u - i)) & 1u) {
+                const uint32_t v = i < 15u ? __builtin_amdgcn_alignbit(C, S2, 2u * (15u - i)) : S2;
+                hist_add<HM>(cx, v & (uint32_t)cx.maskk, weight);
+            }
+        }
+    }
+    if (k > 1) {
+        /* a run's first window adds its first k-1 bases (:1044-1057) */
+        uint32_t fw = RB >> (k - 1);
+        if (Rin < (uint32_t)k && (uint32_t)(k - 1) - Rin < nt) fw |= 1u << (nt - 1u - ((uint32_t)(k - 1) - Rin));
+        fw &= W;
+        const uint64_t maskk1 = cx.maskk >> 2;
+        while (__ballot(fw != 0)) {
+            if (fw) {
+                const uint32_t b = (uint32_t)(__ffs((int)fw) - 1);
+                fw &= fw - 1u;
+                const uint64_t idx = (full >> (2u * b)) & cx.maskk;
+                cnt.base += comp_packed(fk_sigma(idx) >> 2, k - 1, maskk1);
+                cnt.valid += (uint32_t)(k - 1);
+            }
+        }
+        /* depth-1 touches: every digit with R < k, for its run's first base */
+        if (__ballot(F != 0)) {
+            const uint32_t top = RB ? ~((2u << hibit(RB)) - 1u) : 0xFFFFFFFFu;   /* before the first start */
+            const uint32_t c0 = __popc(F & top);
+            if (c0) {
+                const uint32_t d0 = Rin ? (uint32_t)(cin >> (2u * (Rin - 1u))) & 3u : (P >> (2u * (nt - 1u))) & 3u;
+                cnt.d1s += (uint64_t)c0 << (16 * (d0 ^ (d0 >> 1)));
+            }
+            uint32_t rem = F ? RB : 0u;
+            while (__ballot(rem != 0)) {
+                if (rem) {
+                    const uint32_t b = hibit(rem);
+                    rem &= ~(1u << b);
+                    const uint32_t seg = ((2u << b) - 1u) & (rem ? ~((2u << hibit(rem)) - 1u) : 0xFFFFFFFFu);
+                    const uint32_t c = __popc(F & seg);
+                    if (c) {
+                        const uint32_t d0 = (P >> (2u * b)) & 3u;
+                        cnt.d1s += (uint64_t)c << (16 * (d0 ^ (d0 >> 1)));
+                    }
+                }
+            }
+        }
+        /* runs that a break ends before they reach k bases: their prefix walk */
+        if (HM != H_NONE && __ballot(K != 0)) {
+            const uint32_t top = RB ? ~((2u << hibit(RB)) - 1u) : 0xFFFFFFFFu;
+            if (K) {
+                const uint32_t n0 = __popc(vd & top);
+                const uint32_t L0 = Rin + n0;
+                if ((RB || trailk) && L0 >= 1u && L0 < (uint32_t)k)
+                    short_run(cx, (int)L0, n0 ? (full >> (2u * (nt - n0))) : cin, weight);
+            }
+            uint32_t rem = K ? RB : 0u;
+            while (__ballot(rem != 0)) {
+                if (rem) {
+                    const uint32_t b = hibit(rem);
+                    rem &= ~(1u << b);
+                    const uint32_t e = rem ? hibit(rem) + 1u : 0u;   /* the run's last digit */
+                    if ((rem || trailk) && b - e + 1u < (uint32_t)k) short_run(cx, (int)(b - e + 1u), full >> (2u * e), weight);
+                }
+            }
+        }
+    }
+    st.hdr = hout;
+    st.R = (p63 >> 31) ? (p63 & 0x7FFFFFFFu) : st.R + (p63 & 0x7FFFFFFFu);
+    st.code = (p63 >> 31) ? cd63 : fk_join(st.code, cd63, p63 & 0x7FFFFFFFu);
+    oC = C;
+    oS2 = S2;
+    oW = W;
+}
+
+/* A tile by sub_mixed.  plain: the tile was of the fast path's kind (bases
+   only, at most one '\n' per 16 bytes, outside comments) and ends deep in a
+   run, so the next tile most likely is too. */
+template <int HM>
+__device__ __forceinline__ bool tile_mixed(const Ctx &cx, const uint32_t w[8], uint32_t tile_off, DState &st,
+                                           Facts &f, Counters &cnt, uint32_t weight, bool &plain,
+                                           Emit *em = nullptr) {
+    plain = false;
+    if (HM == H_SPARSE || st.R > 0x7FFFFFFFu - FK_TILE_BYTES) return false;
+    uint32_t C0 = 0, S0 = 0, W0 = 0;
+    bool pl = true;
+#pragma unroll 1
+    for (uint32_t h = 0; h < 2; h++) {   /* one copy of sub_mixed: register pressure */
+        uint32_t q[4];
+#pragma unroll
+        for (int d = 0; d < 4; d++) q[d] = h ? w[4 + d] : w[d];
+        uint32_t C, S2, W;
+        bool p;
+        sub_mixed<HM>(cx, q, tile_off + h * (FK_TILE_BYTES / 2), st, f, cnt, weight, C, S2, W, p);
+        pl = pl && p;
+        if (HM == H_EMIT) {
+            if (h == 0) {
+                C0 = C; S0 = S2; W0 = W;
+            } else {
+                em->AC = C0; em->A2 = S0; em->BC = C; em->B2 = S2;
+                em->h0 = em->h1 = false;
+                em->deep = true;
+                em->masked = true;
+                em->cm = W0 | (W << 16);
+            }
+        }
+    }
+    plain = pl && st.R >= (uint32_t)cx.k;
+    return true;
+}
+
 /* wave-wide sum via butterfly */
 __device__ __forceinline__ uint32_t wsum32(uint32_t v) {
 #pragma unroll
@@ -696,21 +985,20 @@ __device__ void flush_counters(const Ctx &cx, Counters &cnt, uint32_t weight, bo
     cnt.valid = cnt.win = cnt.win_u = 0;
 }
 
-/* One tile of count_range: the fast path when it qualifies, else the general
- * path (which also takes a tile only partly inside the input). */
+/* One tile of count_range (interleaved layout): the fast path when it
+ * qualifies, else a mixed tile, else the general path on the tile reloaded
+ * in the contiguous layout (which also takes a tile only partly inside the
+ * input). */
 template <int HM>
 __device__ __forceinline__ void do_tile(const Ctx &cx, const uint32_t w[8], int64_t toff, uint32_t tile_off,
-                                        bool full, DState &st, Facts &f, Counters &cnt, uint32_t weight) {
-    if (HM != H_SPARSE && full && st.hdr == 0 && tile_fast<true, HM, false>(cx, w, st, f, cnt, weight)) return;
+                                        bool full, DState &st, Facts &f, Counters &cnt, uint32_t weight,
+                                        bool mixed) {
+    if (HM != H_SPARSE && full && st.hdr == 0 && tile_fast<true, HM, true>(cx, w, st, f, cnt, weight)) return;
+    bool plain;
+    if (HM != H_SPARSE && full && mixed && tile_mixed<HM>(cx, w, tile_off, st, f, cnt, weight, plain)) return;
     const int lane = threadIdx.x & 63;
     uint32_t v[8];
-    int nb = FK_LANE_BYTES;
-    if (full) {
-#pragma unroll
-        for (int d = 0; d < 8; d++) v[d] = w[d];
-    } else {
-        nb = load_lane<FK_LANE_BYTES>(cx, toff + lane * (int64_t)FK_LANE_BYTES, v);
-    }
+    const int nb = load_lane<FK_LANE_BYTES>(cx, toff + lane * (int64_t)FK_LANE_BYTES, v);
     tile_general<true, HM>(cx, v, nb, tile_off, st, f, cnt, weight);
 }
 
@@ -732,25 +1020,26 @@ __device__ __forceinline__ Span range_span(const RangeRec &r, uint64_t len) {
  * tile t is counted (A/B ping-pong). */
 template <int HM>
 __device__ void count_range(const Ctx &cx, const Span &sp, uint64_t t0, DState &st, Facts &f,
-                            Counters &cnt, uint32_t weight) {
+                            Counters &cnt, uint32_t weight, bool mixed) {
     const int lane = threadIdx.x & 63;
     uint32_t A[8], B[8];
-    /* unconditional loads clamped into the range keep the vmcnt accounting
-       static; a tile only partly inside the input is reloaded by do_tile */
+    /* interleaved tiles (lane L: bytes 16L.. and 1024 + 16L..); unconditional
+       loads clamped into the range keep the vmcnt accounting static (a full
+       tile is never clamped); a tile only partly inside the input is
+       reloaded by do_tile */
 #define FK_LOADT(dst, t_)                                                            \
     {                                                                                \
-        uint64_t o_ = sp.rbase + (uint64_t)(t_) * FK_TILE_BYTES + (uint64_t)lane * FK_LANE_BYTES; \
-        o_ = min(o_, sp.rend - FK_LANE_BYTES);                                       \
-        const u32x4 *p_ = reinterpret_cast<const u32x4 *>(cx.buf + o_);              \
-        u32x4 v0_ = __builtin_nontemporal_load(p_);                                  \
-        u32x4 v1_ = __builtin_nontemporal_load(p_ + 1);                              \
+        const uint64_t tb_ = sp.rbase + (uint64_t)(t_) * FK_TILE_BYTES + 16u * (uint64_t)lane; \
+        const uint64_t o0_ = min(tb_, sp.rend - 16u), o1_ = min(tb_ + 1024u, sp.rend - 16u); \
+        u32x4 v0_ = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(cx.buf + o0_)); \
+        u32x4 v1_ = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(cx.buf + o1_)); \
         dst[0] = v0_.x; dst[1] = v0_.y; dst[2] = v0_.z; dst[3] = v0_.w;               \
         dst[4] = v1_.x; dst[5] = v1_.y; dst[6] = v1_.z; dst[7] = v1_.w;               \
     }
 #define FK_DOT(buf_, t_)                                                             \
     {                                                                                \
         do_tile<HM>(cx, buf_, (int64_t)(sp.rbase + (uint64_t)(t_) * FK_TILE_BYTES),  \
-                    (uint32_t)((t_) * FK_TILE_BYTES), (t_) < sp.nfull, st, f, cnt, weight); \
+                    (uint32_t)((t_) * FK_TILE_BYTES), (t_) < sp.nfull, st, f, cnt, weight, mixed); \
     }
     FK_LOADT(A, t0);
     for (uint64_t t = t0; t < sp.ntiles; t += 2) {
@@ -1170,7 +1459,9 @@ __device__ __forceinline__ void count_wave_range(const Ctx &cx, const Span &sp, 
         }
         if (t >= sp.ntiles || general_left == 0) break;
         /* a tile the fast path cannot take (stream start, header, run
-           break, the ragged end): general path, then back to streaming */
+           break, the ragged end): general path, then back to streaming;
+           past the budget k_resume takes the rest of the range, with mixed
+           tiles */
         general_left--;
         uint32_t v[8];
         const int64_t toff = (int64_t)(sp.rbase + t * FK_TILE_BYTES);
@@ -1369,10 +1660,10 @@ k_count(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uin
  * write their RangeRecs.  Blocks without such a range exit at once.
  */
 template <int HM>
-__global__ void __launch_bounds__(FK_BLOCK)
+__global__ void __launch_bounds__(FK_BLOCK, 4)   /* 4 waves per SIMD (<= 128 VGPRs): two blocks per CU */
 k_resume(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint32_t *table,
          uint32_t *shortcnt, unsigned long long *acc, DevRes *res, RangeRec *rr, uint64_t nranges,
-         const ResumeRec *resume, uint32_t *heads) {
+         const ResumeRec *resume, uint32_t *heads, int mixed) {
     extern __shared__ uint32_t lds_bins[];
     /* k_scan lists the ranges to redo after this kernel (a one-pass k_count
        that gave up may have listed some already) */
@@ -1409,7 +1700,7 @@ k_resume(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, ui
         const DState a{q.a_code, q.a_R, q.a_hdr};
         Facts f = q.f;
         Counters cnt{0, 0, 0, 0, 0, FK_NO_EOF};
-        count_range<HM>(cx, sp, q.tile, st, f, cnt, 1u);
+        count_range<HM>(cx, sp, q.tile, st, f, cnt, 1u, mixed);
         r.tf = fk_tf_span(a, st, f);
         r.a_code = a.code; r.a_R = a.R; r.a_hdr = a.hdr;
         range_obs(cx, cnt, 1u, sp, &r, true, HM != H_NONE);
@@ -1432,10 +1723,10 @@ k_resume(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, ui
  * segment is recounted).
  */
 template <int HM>
-__global__ void __launch_bounds__(FK_BLOCK)
+__global__ void __launch_bounds__(FK_BLOCK, 4)
 k_redo(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint32_t *table,
        uint32_t *shortcnt, unsigned long long *acc, DevRes *res, RangeRec *rr,
-       const XState *rtrue, const uint32_t *list, uint64_t nranges, int mode, uint64_t *slots) {
+       const XState *rtrue, const uint32_t *list, uint64_t nranges, int mode, uint64_t *slots, int mixed) {
     extern __shared__ uint32_t lds_bins[];
     const uint64_t n = mode != 0 ? nranges : (uint64_t)res->redo_n;
     if ((uint64_t)blockIdx.x * FK_WAVES_PER_BLOCK >= n) return;   /* uniform per block */
@@ -1471,7 +1762,7 @@ k_redo(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint
             DState st = (mode == 0 && pass == 0) ? DState{q.a_code, q.a_R, q.a_hdr} : ts;
             Facts f{0, 0, 0, 0, 0, 0};
             Counters cnt{0, 0, 0, 0, 0, FK_NO_EOF};
-            count_range<HM>(cx, sp, 0, st, f, cnt, wt);
+            count_range<HM>(cx, sp, 0, st, f, cnt, wt, mixed);
             if (cancel) {
                 flush_counters(cx, cnt, wt);
             } else {
@@ -1505,6 +1796,9 @@ k_redo(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint
    ~4% faster, but halve the batch, so k_bucket_count reads twice as many,
    shorter runs: the k=11 step is 5% slower and k=12 30% slower (measured,
    tools/exp_part.sh) */
+#ifndef FK_PART_MIXED
+#define FK_PART_MIXED 0   /* mixed tiles in k_part (register pressure: off for now) */
+#endif
 #ifndef PART_WAVES
 #define PART_WAVES 8u
 #endif
@@ -1525,6 +1819,7 @@ struct PartGeo {
     uint32_t npair;        /* pairs mode: slices [0, npair) hold (k+1)-mer pairs, the rest single k-mers */
     uint32_t *pairs;       /* pairs mode: 4^(k+1) pair bins (k_bucket_count -> k_pair_fold) */
     uint32_t *singles;     /* pairs mode: 4^k single k-mer bins */
+    uint32_t nomix;        /* FK_NO_MIXED: tiles the fast path cannot take go to tile_general */
 };
 
 /* Every entry a fast tile's Emit hands to the partition, as f(slice, low).
@@ -1536,6 +1831,38 @@ struct PartGeo {
 template <bool PAIRS, typename F>
 __device__ __forceinline__ void part_entries(const Emit &em, uint32_t mk, uint32_t m1, uint32_t sh, uint32_t lowm,
                                              uint32_t npair, F &&f) {
+    if (FK_PART_MIXED && em.masked) {
+        /* a mixed tile: only the slots in the mask end windows; a pair where
+           both of its slots do, else the single k-mer of the one that does */
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+            const uint32_t C = h ? em.BC : em.AC, S2 = h ? em.B2 : em.A2;
+            const uint32_t cm = (em.cm >> (16 * h)) & 0xFFFFu;
+            if (PAIRS) {
+#pragma unroll
+                for (int j = 0; j < 8; j++) {
+                    const uint32_t two = (cm >> (14 - 2 * j)) & 3u;
+                    if (two == 3u) {
+                        const uint32_t v = (j < 7 ? __builtin_amdgcn_alignbit(C, S2, 28u - 4u * (uint32_t)j) : S2) & m1;
+                        f(v >> sh, v & lowm);
+                    } else if (two) {
+                        const uint32_t s = 2u * (uint32_t)j + (two == 1u ? 1u : 0u);
+                        const uint32_t v = (s < 15u ? __builtin_amdgcn_alignbit(C, S2, 2u * (15u - s)) : S2) & mk;
+                        f(npair + (v >> sh), v & lowm);
+                    }
+                }
+            } else {
+#pragma unroll
+                for (int i = 0; i < 16; i++) {
+                    if ((cm >> (15 - i)) & 1u) {
+                        const uint32_t v = (i < 15 ? __builtin_amdgcn_alignbit(C, S2, 2u * (15u - (uint32_t)i)) : S2) & mk;
+                        f(v >> sh, v & lowm);
+                    }
+                }
+            }
+        }
+        return;
+    }
 #pragma unroll
     for (int h = 0; h < 2; h++) {
         const uint32_t C = h ? em.BC : em.AC, S2 = h ? em.B2 : em.A2;
@@ -1709,10 +2036,13 @@ k_part(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint
 #define FK_ROUND(X)                                                                  \
     {                                                                                \
         Emit em{0, 0, 0, 0, false, false, false};                                    \
-        bool have = false;                                                           \
+        bool have = false, plain_ = false;                                           \
         if (!done) {                                                                 \
             if (t < sp.nfull && st.hdr == 0 && tile_fast<true, H_EMIT, true>(cx, X, st, f, cnt, 1u, &em)) { \
                 have = em.deep;                                                      \
+            } else if (FK_PART_MIXED && t < sp.nfull && !pg.nomix &&                 \
+                       tile_mixed<H_EMIT>(cx, X, (uint32_t)(t * FK_TILE_BYTES), st, f, cnt, 1u, plain_, &em)) { \
+                have = true;                                                         \
             } else {                                                                 \
                 uint32_t v_[8];                                                      \
                 const int64_t toff_ = (int64_t)(sp.rbase + t * FK_TILE_BYTES);       \
@@ -2584,6 +2914,7 @@ struct fk_engine {
     BlockSum *d_bsum = nullptr;               /* per block of k_count */
     uint32_t *d_ctl = nullptr;                /* k_tail's finished-block count */
     uint32_t ranges_per_wave = 1;             /* k <= 7: ranges per k_count wave slot (FK_RANGES_PER_WAVE) */
+    bool no_mixed = false;                    /* FK_NO_MIXED=1: no mixed tiles (general byte walk) */
     uint32_t static_pct = 100;                /* k <= 7: % of a large segment in static ranges (FK_STATIC_PCT;
                                                  100 = no dynamic ranges: on a plain stream the waves that
                                                  finish early hand their bandwidth to the others, so
@@ -2789,6 +3120,10 @@ extern "C" int fk_engine_create(int k, const fk_opts *opts, fk_engine **out) {
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, e->dev) == hipSuccess && prop.multiProcessorCount > 0)
         e->cus = prop.multiProcessorCount;
+    if (const char *nm = getenv("FK_NO_MIXED")) e->no_mixed = nm[0] == '1';
+    /* k_count takes a couple of general tiles per range (the stream start, an
+       isolated comment line) and leaves denser ones to k_resume's mixed tiles */
+    if (!e->no_mixed) e->general_tiles = 2;
     if (const char *gt = getenv("FK_GENERAL_TILES")) e->general_tiles = (uint32_t)strtoul(gt, nullptr, 10);
     if (const char *ne = getenv("FK_NO_EVENTS")) e->timing = ne[0] != '1';
     if (const char *no = getenv("FK_NO_ONEPASS")) e->onepass = no[0] != '1';
@@ -3010,7 +3345,8 @@ static hipEvent_t tev(const fk_engine *e, int i) { return e->timing && e->cur_ti
 static int launch_count(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t lo, const Geo &g,
                         int has_init, bool onepass = false, bool fresh = false, bool shard = false) {
     size_t sh = lds_bytes(e);
-    const uint32_t flags = onepass ? (OP_ON | (fresh ? OP_FRESH : 0u) | (shard ? OP_SHARD : 0u)) : 0u;
+    const uint32_t flags = (onepass ? (OP_ON | (fresh ? OP_FRESH : 0u) | (shard ? OP_SHARD : 0u)) : 0u) |
+                           (e->no_mixed ? (uint32_t)OP_NOMIX : 0u);
     FK_DISPATCH_COUNT(e,
                 hipExtLaunchKernelGGL((k_count<HM>), dim3(g.grid), dim3(FK_BLOCK), sh, e->stream, tev(e, 0), tev(e, 1),
                                       0, buf, len, lo, e->k,
@@ -3037,7 +3373,7 @@ static int launch_resume(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t
     FK_DISPATCH_COUNT(e,
                 hipLaunchKernelGGL((k_resume<HM>), dim3(g.rgrid), dim3(FK_BLOCK), sh, e->stream, buf, len, lo, e->k,
                                    e->maskk, e->d_table, e->d_short, e->d_facc, e->d_res, e->d_rr, g.nranges,
-                                   e->d_resume, e->d_ctl + FK_HEADS_OFF));
+                                   e->d_resume, e->d_ctl + FK_HEADS_OFF, e->no_mixed ? 0 : 1));
     HIPCHK(hipGetLastError());
     return FK_OK;
 }
@@ -3048,7 +3384,7 @@ static int launch_redo(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t l
     FK_DISPATCH(hist_mode(e),
                 hipLaunchKernelGGL((k_redo<HM>), dim3(g.rgrid), dim3(FK_BLOCK), sh, e->stream, buf, len, lo, e->k,
                                    e->maskk, e->d_table, e->d_short, e->d_facc, e->d_res, e->d_rr,
-                                   e->d_rtrue, e->d_redo, g.nranges, mode, slots));
+                                   e->d_rtrue, e->d_redo, g.nranges, mode, slots, e->no_mixed ? 0 : 1));
     HIPCHK(hipGetLastError());
     return FK_OK;
 }
@@ -3122,6 +3458,7 @@ static int launch_part(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t l
     pg.npair = pairs ? 1u << (2 * kb - pg.sh) : 0u;
     pg.nslices = pairs ? pg.npair + (1u << (2 * k - pg.sh)) : 1u << (2 * k - pg.sh);
     pg.pairs = pg.singles = nullptr;
+    pg.nomix = e->no_mixed ? 1u : 0u;
     if (pairs) {
         const uint64_t need = e->nbins * 5;                 /* 4^(k+1) pair bins + 4^k single bins */
         if (need > e->pair_cap) {

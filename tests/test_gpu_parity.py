@@ -795,3 +795,100 @@ def test_shard_exit_states_match_stream(k, kind):
             st = e.state()
             got = (st.hdr, st.run, st.code & ((1 << (2 * min(st.run, 31))) - 1) if not st.hdr else 0)
             assert got == want[i], (i, got, want[i])
+
+
+def _dense_records(seed, n, min_len=1, max_len=3000):
+    """Header-dense FASTA: every tile holds comment lines, run breaks and
+    newlines in every arrangement, so nearly every tile takes the mixed path
+    (tile_mixed): upstream-like records, records shorter than k, N blocks,
+    soft-masked bases, empty lines, '\\r', headers made of bases only, headers
+    back to back, unknown and 0xFF bytes inside comments."""
+    rng = random.Random(seed)
+    parts, size, rec = [], 0, 0
+    while size < n:
+        r = rng.random()
+        if r < 0.08:
+            head = b">" + random_text(rng, rng.randint(0, 40), b"ACGT", [1, 1, 1, 1]) + b"\n"
+        elif r < 0.12:
+            head = b">" + random_text(rng, rng.randint(0, 30), b"AC>x\xff\rN", [3, 3, 1, 1, 1, 1, 1]) + b"\n"
+        else:
+            head = b">ENST%011d\n" % rec
+        rec += 1
+        L = rng.randint(min_len, max_len) if rng.random() < 0.8 else rng.randint(0, 20)
+        seq = bytearray(random_text(rng, L, b"ACGT", [1, 1, 1, 1]))
+        for _ in range(rng.choice([0, 0, 0, 1, 3])):
+            if seq:
+                a = rng.randrange(len(seq))
+                b = min(len(seq), a + rng.randint(1, 60))
+                seq[a:b] = rng.choice([b"N", b"n", b"a", b"\r", b"x"]) * (b - a)
+        w = rng.choice([0, 0, 0, 60, 80, 13, 1, 16])
+        if w:
+            seq = b"\n".join(bytes(seq[i:i + w]) for i in range(0, len(seq), w))
+        tail = b"\n" * rng.choice([1, 1, 1, 0, 2, 5])
+        parts.append(head + bytes(seq) + tail)
+        size += len(parts[-1])
+    return b"".join(parts)
+
+
+@pytest.mark.parametrize("seed", range(3))
+@pytest.mark.parametrize("k", [1, 2, 3, 5, 6, 7, 13])
+def test_mixed_tiles_header_dense(seed, k):
+    data = _dense_records(4000 + seed, 700_000 + 200_000 * seed)
+    assert_same(data, k)
+
+
+@pytest.mark.parametrize("k", [14, 15, 16])
+def test_mixed_tiles_header_dense_large_k(k):
+    """k = 14..16 (global atomics, dense table): nonzero bins vs the sparse oracle."""
+    data = _dense_records(4050 + k, 500_000)
+    codes, cnts, r = oracle.count_sparse(data, k)
+    with fk.Engine(k, want_nodes=True) as e:
+        e.feed(np.frombuffer(data, dtype=np.uint8).copy())
+        rc, rg = e.finish(allow=(fk.FK_OK, fk.FK_E_UNTERMINATED_HEADER))
+        step = 1 << 28
+        got_c, got_n = [], []
+        for first in range(0, 1 << (2 * k), step):
+            part = e.table_range(first, min(step, (1 << (2 * k)) - first))
+            nz = np.nonzero(part)[0]
+            got_c.append(nz.astype(np.uint64) + first)
+            got_n.append(part[nz])
+    assert np.array_equal(np.concatenate(got_c), codes)
+    assert np.array_equal(np.concatenate(got_n), cnts)
+    assert (rg.windows, rg.distinct, rg.valid_bases) == (r.windows, r.distinct, r.valid_bases)
+    assert list(rg.base_count) == list(r.base_count)
+    assert list(rg.depth1) == list(r.depth1)
+    assert rg.nodes == r.nodes
+
+
+@pytest.mark.parametrize("k", [2, 6, 7, 13])
+def test_mixed_tiles_short_records(k):
+    # records around k long: short runs (nodeCounter), first windows and
+    # depth-1 touches in nearly every lane
+    data = _dense_records(4100 + k, 600_000, min_len=1, max_len=3 * k)
+    assert_same(data, k)
+
+
+@pytest.mark.parametrize("k", [3, 6, 13])
+def test_mixed_tiles_ff_outside_comment(k):
+    data = bytearray(_dense_records(4200 + k, 400_000))
+    cut = 300_001
+    while data[cut] in b">\n":
+        cut += 1
+    # the first 0xFF outside a comment ends the reference's scan (:988)
+    j = data.rfind(b">", 0, cut)
+    if j >= 0 and data.find(b"\n", j, cut) < 0:
+        cut = data.find(b"\n", j) + 1
+    data[cut] = 0xFF
+    r = assert_same(bytes(data), k)
+    assert r.hit_eof_byte
+
+
+@pytest.mark.parametrize("k", [4, 6, 7])
+def test_mixed_tiles_match_general_path(k, monkeypatch):
+    # the same header-dense input with mixed tiles switched off (FK_NO_MIXED:
+    # the byte walk of tile_general) counts identically
+    data = _dense_records(4300 + k, 500_000)
+    r1 = assert_same(data, k)
+    monkeypatch.setenv("FK_NO_MIXED", "1")
+    r2 = assert_same(data, k)
+    assert (r1.windows, r1.valid_bases, r1.nodes) == (r2.windows, r2.valid_bases, r2.nodes)
