@@ -918,9 +918,10 @@ __device__ __forceinline__ bool tile_mixed(const Ctx &cx, const uint32_t w[8], u
     bool pl = true;
 #pragma unroll 1
     for (uint32_t h = 0; h < 2; h++) {   /* one copy of sub_mixed: register pressure */
+        const uint32_t hm = 0u - h;   /* select without indexing the register array */
         uint32_t q[4];
 #pragma unroll
-        for (int d = 0; d < 4; d++) q[d] = h ? w[4 + d] : w[d];
+        for (int d = 0; d < 4; d++) q[d] = (w[4 + d] & hm) | (w[d] & ~hm);
         uint32_t C, S2, W;
         bool p;
         sub_mixed<HM>(cx, q, tile_off + h * (FK_TILE_BYTES / 2), st, f, cnt, weight, C, S2, W, p);
@@ -957,7 +958,7 @@ __device__ __forceinline__ void acc_add(unsigned long long *a, uint64_t v, uint3
     if (v) atomicAdd(a, (unsigned long long)(weight == 1u ? v : (0ull - v)));
 }
 
-__device__ void flush_counters(const Ctx &cx, Counters &cnt, uint32_t weight, bool to_acc = true) {
+__device__ __forceinline__ void flush_counters(const Ctx &cx, Counters &cnt, uint32_t weight, bool to_acc = true) {
     const int lane = threadIdx.x & 63;
     uint32_t vals[11];
 #pragma unroll
@@ -1054,7 +1055,7 @@ __device__ void count_range(const Ctx &cx, const Span &sp, uint64_t t0, DState &
 }
 
 /* Flush a range's counters; lane 0 records its observations in rr. */
-__device__ void range_obs(const Ctx &cx, Counters &cnt, uint32_t weight, const Span &sp, RangeRec *r,
+__device__ __forceinline__ void range_obs(const Ctx &cx, Counters &cnt, uint32_t weight, const Span &sp, RangeRec *r,
                           bool write, bool to_acc = true) {
     flush_counters(cx, cnt, weight, to_acc);
     const uint32_t unk = wsum32(cnt.unknown);
@@ -1796,9 +1797,6 @@ k_redo(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint
    ~4% faster, but halve the batch, so k_bucket_count reads twice as many,
    shorter runs: the k=11 step is 5% slower and k=12 30% slower (measured,
    tools/exp_part.sh) */
-#ifndef FK_PART_MIXED
-#define FK_PART_MIXED 0   /* mixed tiles in k_part (register pressure: off for now) */
-#endif
 #ifndef PART_WAVES
 #define PART_WAVES 8u
 #endif
@@ -1820,6 +1818,9 @@ struct PartGeo {
     uint32_t *pairs;       /* pairs mode: 4^(k+1) pair bins (k_bucket_count -> k_pair_fold) */
     uint32_t *singles;     /* pairs mode: 4^k single k-mer bins */
     uint32_t nomix;        /* FK_NO_MIXED: tiles the fast path cannot take go to tile_general */
+    uint32_t general;      /* general tiles k_part takes per range before k_part<RES> takes the rest */
+    uint32_t stride;       /* index row stride: rows of both regions (k_part, then k_part<RES>) */
+    uint32_t *flag;        /* [0] != 0: some range went to k_part<RES>, region 2 holds rows */
 };
 
 /* Every entry a fast tile's Emit hands to the partition, as f(slice, low).
@@ -1828,10 +1829,10 @@ struct PartGeo {
  * ending at the odd slots 1, 3, .., 15 of each half, each standing for the
  * two k-mers ending at slots (2j, 2j+1); without a real slot 0 the first one
  * is the single k-mer at slot 1, in slices npair and up. */
-template <bool PAIRS, typename F>
+template <bool PAIRS, bool MIX, typename F>
 __device__ __forceinline__ void part_entries(const Emit &em, uint32_t mk, uint32_t m1, uint32_t sh, uint32_t lowm,
                                              uint32_t npair, F &&f) {
-    if (FK_PART_MIXED && em.masked) {
+    if (MIX && em.masked) {
         /* a mixed tile: only the slots in the mask end windows; a pair where
            both of its slots do, else the single k-mer of the one that does */
 #pragma unroll
@@ -1889,7 +1890,7 @@ __device__ __forceinline__ void part_entries(const Emit &em, uint32_t mk, uint32
 /* The block-wide batch of one round: windows of the waves whose tile was
  * fast (have), counting-sorted by slice.  Every thread of the block calls
  * this the same number of times (it contains barriers). */
-template <bool PAIRS>
+template <bool PAIRS, bool MIX>
 __device__ __forceinline__ bool part_batch(const Ctx &cx, const PartGeo &pg, const Emit *es, const bool *haves,
                                            bool more, uint32_t row, uint32_t *hist,
                                            uint32_t *cur, uint32_t *total, uint16_t *ent) {
@@ -1900,7 +1901,7 @@ __device__ __forceinline__ bool part_batch(const Ctx &cx, const PartGeo &pg, con
     /* 1: slice histogram */
 #pragma unroll
     for (int i = 0; i < NT; i++)
-        if (haves[i]) part_entries<PAIRS>(es[i], mk, m1, sh, lowm, pg.npair, [&](uint32_t b, uint32_t) { atomicAdd(&hist[b], 1u); });
+        if (haves[i]) part_entries<PAIRS, MIX>(es[i], mk, m1, sh, lowm, pg.npair, [&](uint32_t b, uint32_t) { atomicAdd(&hist[b], 1u); });
     /* (the barrier also tells whether any wave has tiles left) */
     const bool any_more = __syncthreads_or(more);
     /* 2: exclusive scan of the slice counts (wave 0), index row */
@@ -1923,7 +1924,7 @@ __device__ __forceinline__ bool part_batch(const Ctx &cx, const PartGeo &pg, con
             if (b < pg.nslices) {
                 const uint32_t c = hist[b];
                 cur[b] = run;
-                pg.idx[(size_t)b * pg.rows + row] = (run << 16) | c;
+                pg.idx[(size_t)b * pg.stride + row] = (run << 16) | c;
                 hist[b] = 0;
                 run += c;
             }
@@ -1942,7 +1943,7 @@ __device__ __forceinline__ bool part_batch(const Ctx &cx, const PartGeo &pg, con
     for (int i = 0; i < NT; i++) {
         Emit f = es[i];
         asm volatile("" : "+v"(f.AC), "+v"(f.A2), "+v"(f.BC), "+v"(f.B2));
-        if (haves[i]) part_entries<PAIRS>(f, mk, m1, sh, lowm, pg.npair, place);
+        if (haves[i]) part_entries<PAIRS, MIX>(f, mk, m1, sh, lowm, pg.npair, place);
     }
     __syncthreads();
     /* 4: the sorted batch into its row's fixed slot (a batch holds at most
@@ -1956,16 +1957,23 @@ __device__ __forceinline__ bool part_batch(const Ctx &cx, const PartGeo &pg, con
     return any_more;
 }
 
-template <bool PAIRS>
+/* RES = false: the main pass.  With mixed tiles on, a range that needs more
+ * than pg.general general tiles stops there (ResumeRec) and
+ * RES = true -- the same blocks and ranges, their rows in region 2 -- counts
+ * the rest of it, each tile fast, mixed (the masked entries of tile_mixed)
+ * or general.  Two kernels: tile_mixed's registers stay out of the main
+ * pass.  k_part<RES> returns at once unless some range stopped. */
+template <bool PAIRS, bool RES>
 __global__ void __launch_bounds__(PART_BLOCK, 4) /* 4 waves per SIMD (<= 128 VGPRs): two blocks per CU */
 k_part(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint32_t *table,
        uint32_t *shortcnt, unsigned long long *acc, DevRes *res, RangeRec *rr, uint64_t nchunks, uint64_t cpw,
-       const XState *d_init, int has_init, PartGeo pg) {
+       const XState *d_init, int has_init, PartGeo pg, ResumeRec *resume) {
     __shared__ uint32_t hist[PART_MAX_SLICES], cur[PART_MAX_SLICES], total;
     __shared__ __attribute__((aligned(16))) uint16_t ent[PART_MAX_BATCH];
+    if (RES && *(volatile uint32_t *)pg.flag == 0) return;   /* uniform: no range stopped */
     /* open the feed's result block (the kernels after this one accumulate
        into it) */
-    if (blockIdx.x == 0) {
+    if (!RES && blockIdx.x == 0) {
         if (threadIdx.x < 10) res->tstat[threadIdx.x] = 0;
         if (threadIdx.x == 10) res->eof_cand = ~0ull;
         if (threadIdx.x == 11) res->redo_n = 0;
@@ -1975,13 +1983,15 @@ k_part(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint
     const int lane = threadIdx.x & 63;
     const uint64_t wave = blockIdx.x * PART_WAVES + wave_in_block();
     const uint64_t c0 = wave * cpw, c1 = min(c0 + cpw, nchunks);
-    const bool has = c0 < c1;
+    const bool has = c0 < c1 && (!RES || rr[wave].resume);
     RangeRec hdr_r;
     hdr_r.c0 = has ? c0 : 0;
     hdr_r.c1 = has ? c1 : 0;
     const Span sp = range_span(hdr_r, len);
     const uint64_t last_tile = sp.nfull ? sp.rend - FK_TILE_BYTES : 0;
     const bool ld = sp.nfull > 0;
+    const ResumeRec *qr = resume + wave;   /* k_part<RES>: where k_part stopped (fields read where used) */
+    uint64_t t = RES && has ? qr->tile : 0;
 #define FK_LOADP(dst, t_)                                                            \
     if (ld) {                                                                        \
         const uint64_t tb_ = min(sp.rbase + (uint64_t)(t_) * FK_TILE_BYTES, last_tile); \
@@ -1993,10 +2003,10 @@ k_part(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint
     }
     /* halo (lanes 0..7) and the first three tiles in flight before anything
        waits (as in k_count) */
-    uint32_t hw[8];
+    uint32_t hw[8] = {};
     const int64_t ho = (int64_t)sp.rbase - (int64_t)FK_HALO_BYTES + (int64_t)lane * FK_LANE_BYTES;
     const bool hv = has && lane < (int)(FK_HALO_BYTES / FK_LANE_BYTES) && ho >= lo;
-    {
+    if (!RES) {
         const int64_t hc = max(min(ho, (int64_t)len - (int64_t)FK_LANE_BYTES), lo);
         const u32x4 *hp = reinterpret_cast<const u32x4 *>(buf + hc);
         u32x4 h0 = __builtin_nontemporal_load(hp), h1 = __builtin_nontemporal_load(hp + 1);
@@ -2005,25 +2015,33 @@ k_part(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint
     }
     uint32_t A[8] = {}, B[8] = {}, C[8] = {};
     asm volatile("" ::: "memory");
-    FK_LOADP(A, 0);
+    FK_LOADP(A, t);
     asm volatile("" ::: "memory");
-    FK_LOADP(B, 1);
+    FK_LOADP(B, t + 1);
     asm volatile("" ::: "memory");
-    FK_LOADP(C, 2);
+    FK_LOADP(C, t + 2);
     /* entering state: the known stream state for chunk 0, else a guess from
-       the halo (k_scan checks it, k_redo recounts a range it got wrong) */
-    DState st{0, 0, 0};
-    if (has) {
+       the halo (k_scan checks it, k_redo recounts a range it got wrong);
+       k_part<RES>: where k_part stopped */
+    DState st{0, 0, 0}, first{0, 0, 0};
+    Facts f{0, 0, 0, 0, 0, 0};
+    if (RES) {
+        if (has) {
+            st = DState{qr->code, qr->R, qr->hdr};
+            first = DState{qr->a_code, qr->a_R, qr->a_hdr};
+            f = qr->f;
+        }
+    } else if (has) {
         if (c0 == 0 && has_init) st = DState{d_init->code, (uint32_t)d_init->R, d_init->hdr};
         else st = halo_guess<H_EMIT>(cx, hw, hv);
+        first = st;
     }
     consume(hw);   /* waited on every path (see k_count) */
-    const DState first = st;
-    Facts f{0, 0, 0, 0, 0, 0};
     Counters cnt{0, 0, 0, 0, 0, FK_NO_EOF};
-    uint64_t t = 0;
-    bool done = !has || sp.ntiles == 0;
+    bool done = !has || t >= sp.ntiles, stopped = false;
+    uint32_t general_left = pg.nomix ? 0xFFFFFFFFu : max(pg.general, 1u);
     uint32_t round = 0;
+    const uint32_t row0 = (RES ? pg.rows : 0u) + blockIdx.x * pg.rounds;
     constexpr uint32_t NT = PART_TILES(PAIRS);
     Emit stash[NT];
     bool have_stash[NT];
@@ -2040,18 +2058,23 @@ k_part(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint
         if (!done) {                                                                 \
             if (t < sp.nfull && st.hdr == 0 && tile_fast<true, H_EMIT, true>(cx, X, st, f, cnt, 1u, &em)) { \
                 have = em.deep;                                                      \
-            } else if (FK_PART_MIXED && t < sp.nfull && !pg.nomix &&                 \
+                t++;                                                                 \
+            } else if (RES && t < sp.nfull &&                                        \
                        tile_mixed<H_EMIT>(cx, X, (uint32_t)(t * FK_TILE_BYTES), st, f, cnt, 1u, plain_, &em)) { \
                 have = true;                                                         \
+                t++;                                                                 \
             } else {                                                                 \
+                /* k_part stops after its last general tile (the range's rest  \
+                   goes to k_part<RES>) */                                        \
+                stopped = !RES && --general_left == 0;                               \
                 uint32_t v_[8];                                                      \
                 const int64_t toff_ = (int64_t)(sp.rbase + t * FK_TILE_BYTES);       \
                 const int nb_ = load_lane<FK_LANE_BYTES>(cx, toff_ + lane * (int64_t)FK_LANE_BYTES, v_); \
                 tile_general<true, H_EMIT>(cx, v_, nb_, (uint32_t)(t * FK_TILE_BYTES), st, f, cnt, 1u); \
                 consume(v_);                                                         \
+                t++;                                                                 \
             }                                                                        \
-            t++;                                                                     \
-            done = t >= sp.ntiles;                                                   \
+            done = stopped || t >= sp.ntiles;                                        \
         }                                                                            \
         consume(X);                                                                  \
         FK_LOADP(X, t + 2);                                                          \
@@ -2062,9 +2085,8 @@ k_part(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint
                 have_stash[i_] = have;                                               \
             }                                                                        \
             if (ph_ == NT - 1) {                                                     \
-                const bool more_ = part_batch<PAIRS>(cx, pg, stash, have_stash, !done, \
-                                                     blockIdx.x * pg.rounds + round / NT, \
-                                                     hist, cur, &total, ent);        \
+                const bool more_ = part_batch<PAIRS, RES>(cx, pg, stash, have_stash, !done, \
+                                                          row0 + round / NT, hist, cur, &total, ent); \
                 if (!more_ || round / NT + 1 >= pg.rounds) { round++; break; }       \
             }                                                                        \
         }                                                                            \
@@ -2079,20 +2101,48 @@ k_part(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint
 #undef FK_LOADP
     /* rows the block did not reach are empty */
     for (uint32_t r = (round + NT - 1) / NT; r < pg.rounds; r++) {
-        const uint32_t row = blockIdx.x * pg.rounds + r;
-        for (uint32_t b = threadIdx.x; b < pg.nslices; b += PART_BLOCK) pg.idx[(size_t)b * pg.rows + row] = 0;
+        const uint32_t row = row0 + r;
+        for (uint32_t b = threadIdx.x; b < pg.nslices; b += PART_BLOCK) pg.idx[(size_t)b * pg.stride + row] = 0;
+    }
+    if (!has) {
+        flush_counters(cx, cnt, 1u);
+        return;
+    }
+    if (!RES && stopped) {
+        /* k_part<RES> counts the rest of the range */
+        flush_counters(cx, cnt, 1u);
+        const uint32_t unk = wsum32(cnt.unknown), eof = wmin32(cnt.eof);
+        if (lane == 0) {
+            ResumeRec w;
+            w.tile = t;
+            w.code = st.code; w.R = st.R; w.hdr = st.hdr;
+            w.a_code = first.code; w.a_R = first.R; w.a_hdr = first.hdr;
+            w.range = (uint32_t)wave;
+            w.unknown = unk;
+            w.eof = eof;
+            w.pad = 0;
+            w.f = f;
+            resume[wave] = w;
+            RangeRec &r = rr[wave];
+            r.c0 = c0; r.c1 = c1;
+            r.resume = 1;
+            atomicOr(pg.flag, 1u);
+        }
+        return;
     }
     /* the range's record: transfer function, guess, observations */
-    if (has) {
-        RangeRec r;
-        r.tf = fk_tf_span(first, st, f);
-        r.a_code = first.code; r.a_R = first.R; r.a_hdr = first.hdr;
-        r.c0 = c0; r.c1 = c1;
-        r.resume = 0;
-        range_obs(cx, cnt, 1u, sp, &r, true);
-        if (lane == 0) rr[wave] = r;
-    } else {
-        flush_counters(cx, cnt, 1u);
+    RangeRec r;
+    r.tf = fk_tf_span(first, st, f);
+    r.a_code = first.code; r.a_R = first.R; r.a_hdr = first.hdr;
+    r.c0 = c0; r.c1 = c1;
+    r.resume = 0;
+    range_obs(cx, cnt, 1u, sp, &r, true);
+    if (lane == 0) {
+        if (RES) {   /* plus what k_part observed before it stopped */
+            r.unknown += qr->unknown;
+            if (qr->eof != FK_NO_EOF) r.eof = min(r.eof, (uint64_t)qr->eof);
+        }
+        rr[wave] = r;
     }
 }
 
@@ -2103,7 +2153,9 @@ k_bucket_count(PartGeo pg, uint32_t groups, uint32_t *table) {
     const uint32_t b = blockIdx.x % pg.nslices, g = blockIdx.x / pg.nslices;
     for (uint32_t i = threadIdx.x; i < nb; i += blockDim.x) slice[i] = 0;
     __syncthreads();
-    const uint32_t *ix = pg.idx + (size_t)b * pg.rows;
+    const uint32_t *ix = pg.idx + (size_t)b * pg.stride;
+    /* region 2 (k_part<RES>) holds rows only if some range went there */
+    const uint32_t nrows = pg.flag && *pg.flag ? 2u * pg.rows : pg.rows;
     const uint4 *g4 = reinterpret_cast<const uint4 *>(pg.codes);
     /* four lanes share a run and read it as contiguous 64-byte pieces (one
        request per quad instead of one per lane).  A quad takes four rows at
@@ -2124,14 +2176,14 @@ k_bucket_count(PartGeo pg, uint32_t groups, uint32_t *table) {
     uint32_t en[4];   /* the next iteration's index words, loaded with this one's codes */
     const uint32_t r00 = g * quads + threadIdx.x / 4;
 #pragma unroll
-    for (int j = 0; j < 4; j++) en[j] = r00 + j * step < pg.rows ? ix[r00 + j * step] : 0u;
-    for (uint32_t r = r00; r < pg.rows; r += 4 * step) {
+    for (int j = 0; j < 4; j++) en[j] = r00 + j * step < nrows ? ix[r00 + j * step] : 0u;
+    for (uint32_t r = r00; r < nrows; r += 4 * step) {
         uint32_t e[4];
 #pragma unroll
         for (int j = 0; j < 4; j++) e[j] = en[j];
         const uint32_t rn = r + 4 * step;
 #pragma unroll
-        for (int j = 0; j < 4; j++) en[j] = rn + j * step < pg.rows ? ix[rn + j * step] : 0u;
+        for (int j = 0; j < 4; j++) en[j] = rn + j * step < nrows ? ix[rn + j * step] : 0u;
         uint64_t s0[4], s1[4];
         uint4 v[4][2];
 #pragma unroll
@@ -2897,6 +2949,7 @@ struct fk_engine {
     bool sp_done = false;                     /* fks holds the finished table */
     unsigned long long sp_nodes = 0, sp_roll = 0, sp_tstat[10] = {};
     uint16_t *d_codes = nullptr;              /* k_part: block code regions */
+    uint32_t *d_pflag = nullptr;              /* k_part: a range went to k_part<RES> */
     uint32_t *d_pidx = nullptr;               /* k_part: slice-major run index */
     uint64_t codes_cap = 0, pidx_cap = 0;
     uint32_t *d_pairs = nullptr;              /* k_part pairs mode: 4^(k+1) pair bins + 4^k single bins */
@@ -3070,7 +3123,7 @@ extern "C" void fk_engine_destroy(fk_engine *e) {
     if (e->stream) hipStreamSynchronize(e->stream);
     hipFree(e->d_table); hipFree(e->d_short); hipFree(e->d_sub);
     hipFree(e->d_pairs);
-    hipFree(e->d_codes); hipFree(e->d_pidx); hipFree(e->d_acc); hipFree(e->d_res); hipFree(e->d_tmp);
+    hipFree(e->d_codes); hipFree(e->d_pidx); hipFree(e->d_pflag); hipFree(e->d_acc); hipFree(e->d_res); hipFree(e->d_tmp);
     hipFree(e->d_state); hipFree(e->d_rr); hipFree(e->d_rtrue);
     hipFree(e->d_redo); hipFree(e->d_tf); hipFree(e->d_stage); hipFree(e->d_resume);
     hipFree(e->d_aggs); hipFree(e->d_flags);
@@ -3473,7 +3526,15 @@ static int launch_part(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t l
     pg.rounds = (uint32_t)((g.cpw * FK_CHUNK_TILES + 2) / PART_TILES(pairs) + 2);   /* rows (batches) per block */
     const unsigned pgrid = (unsigned)((g.nranges + PART_WAVES - 1) / PART_WAVES);   /* same ranges, smaller blocks */
     pg.rows = pgrid * pg.rounds;
-    const uint64_t ncodes = (uint64_t)pg.rows * PART_MAX_BATCH, nidx = (uint64_t)pg.nslices * pg.rows;
+    /* mixed tiles: ranges past their general tiles go to k_part<RES>, whose
+       rows (region 2, as many as k_part's) follow k_part's */
+    const bool mixed = !e->no_mixed;
+    pg.general = e->general_tiles;
+    pg.stride = mixed ? 2 * pg.rows : pg.rows;
+    if (!e->d_pflag && hipMalloc((void **)&e->d_pflag, 64) != hipSuccess) return FK_E_OOM;
+    pg.flag = e->d_pflag;
+    HIPCHK(hipMemsetAsync(e->d_pflag, 0, sizeof(uint32_t), e->stream));
+    const uint64_t ncodes = (uint64_t)pg.stride * PART_MAX_BATCH, nidx = (uint64_t)pg.nslices * pg.stride;
     if (ncodes > e->codes_cap) {
         hipFree(e->d_codes);
         e->d_codes = nullptr;
@@ -3488,10 +3549,18 @@ static int launch_part(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t l
     }
     pg.codes = e->d_codes;
     pg.idx = e->d_pidx;
-    hipExtLaunchKernelGGL(pairs ? k_part<true> : k_part<false>, dim3(pgrid), dim3(PART_BLOCK), 0, e->stream,
-                          tev(e, 0), tev(e, 1), 0, buf, len, lo, e->k, e->maskk, e->d_table, e->d_short, e->d_facc,
-                          e->d_res, e->d_rr, g.nchunks, g.cpw, e->d_state, has_init, pg);
+    hipExtLaunchKernelGGL(pairs ? k_part<true, false> : k_part<false, false>, dim3(pgrid), dim3(PART_BLOCK), 0,
+                          e->stream, tev(e, 0), tev(e, 1), 0, buf, len, lo, e->k, e->maskk, e->d_table, e->d_short,
+                          e->d_facc, e->d_res, e->d_rr, g.nchunks, g.cpw, e->d_state, has_init, pg, e->d_resume);
     HIPCHK(hipGetLastError());
+    if (mixed) {
+        hipLaunchKernelGGL((pairs ? k_part<true, true> : k_part<false, true>), dim3(pgrid), dim3(PART_BLOCK), 0,
+                           e->stream, buf, len, lo, e->k, e->maskk, e->d_table, e->d_short, e->d_facc, e->d_res,
+                           e->d_rr, g.nchunks, g.cpw, e->d_state, has_init, pg, e->d_resume);
+        HIPCHK(hipGetLastError());
+    } else {
+        pg.flag = nullptr;
+    }
     const uint32_t groups = std::max<uint32_t>(1, (uint32_t)e->cus / pg.nslices);
     if (pairs && groups > 1) HIPCHK(hipMemsetAsync(e->d_pairs, 0, e->nbins * 5 * sizeof(uint32_t), e->stream));
     hipLaunchKernelGGL(k_bucket_count, dim3(pg.nslices * groups), dim3(1024), (size_t)sizeof(uint32_t) << pg.sh,

@@ -831,7 +831,7 @@ def _dense_records(seed, n, min_len=1, max_len=3000):
 
 
 @pytest.mark.parametrize("seed", range(3))
-@pytest.mark.parametrize("k", [1, 2, 3, 5, 6, 7, 13])
+@pytest.mark.parametrize("k", [1, 2, 3, 5, 6, 7, 8, 9, 11, 12, 13])
 def test_mixed_tiles_header_dense(seed, k):
     data = _dense_records(4000 + seed, 700_000 + 200_000 * seed)
     assert_same(data, k)
@@ -860,7 +860,7 @@ def test_mixed_tiles_header_dense_large_k(k):
     assert rg.nodes == r.nodes
 
 
-@pytest.mark.parametrize("k", [2, 6, 7, 13])
+@pytest.mark.parametrize("k", [2, 6, 7, 10, 13])
 def test_mixed_tiles_short_records(k):
     # records around k long: short runs (nodeCounter), first windows and
     # depth-1 touches in nearly every lane
@@ -868,7 +868,7 @@ def test_mixed_tiles_short_records(k):
     assert_same(data, k)
 
 
-@pytest.mark.parametrize("k", [3, 6, 13])
+@pytest.mark.parametrize("k", [3, 6, 11, 13])
 def test_mixed_tiles_ff_outside_comment(k):
     data = bytearray(_dense_records(4200 + k, 400_000))
     cut = 300_001
@@ -883,7 +883,7 @@ def test_mixed_tiles_ff_outside_comment(k):
     assert r.hit_eof_byte
 
 
-@pytest.mark.parametrize("k", [4, 6, 7])
+@pytest.mark.parametrize("k", [4, 6, 7, 11, 12])
 def test_mixed_tiles_match_general_path(k, monkeypatch):
     # the same header-dense input with mixed tiles switched off (FK_NO_MIXED:
     # the byte walk of tile_general) counts identically
@@ -892,3 +892,16 @@ def test_mixed_tiles_match_general_path(k, monkeypatch):
     monkeypatch.setenv("FK_NO_MIXED", "1")
     r2 = assert_same(data, k)
     assert (r1.windows, r1.valid_bases, r1.nodes) == (r2.windows, r2.valid_bases, r2.nodes)
+
+
+@pytest.mark.parametrize("k", [8, 11, 12])
+@pytest.mark.parametrize("budget", ["1", "3"])
+def test_part_resume_budgets(k, budget, monkeypatch):
+    # k_part stops a range after `budget` general tiles and k_part<RES> counts
+    # the rest (mixed tiles into region 2 of the partition); ranges that stop
+    # and ranges that do not in one feed
+    monkeypatch.setenv("FK_GENERAL_TILES", budget)
+    rng = random.Random(77 + k)
+    data = _dense_records(4400 + k, 300_000) + random_text(rng, 900_000, b"ACGT", [1, 1, 1, 1]) + \
+        _dense_records(4500 + k, 200_000)
+    assert_same(data, k)
