@@ -512,8 +512,10 @@ __device__ __forceinline__ void half_windows(const Ctx &cx, uint32_t C, uint32_t
  * bases and all of the newline handling folds away. */
 template <bool COUNT, int HM, bool INTER, bool NL>
 __device__ __forceinline__ bool tile_finish(const Ctx &cx, const uint32_t x[8], uint32_t nl0, uint32_t nl1,
-                                            DState &st, Facts &f, Counters &cnt, uint32_t weight, Emit *em) {
+                                            DState &st, Facts &f, Counters &cnt, uint32_t weight, Emit *em,
+                                            bool *kind) {
     const int k = cx.k;
+    if (kind) *kind = true;   /* bases only (the state may still not be deep) */
     /* deep: every window of the tile counts (seq > k throughout); neg: the
        reference's int32 seqSize stays negative for the whole tile (a run
        past 2^31-1 bases, :977), so the tile only advances the state */
@@ -598,7 +600,7 @@ __device__ __forceinline__ bool tile_finish(const Ctx &cx, const uint32_t x[8], 
  */
 template <bool COUNT, int HM, bool INTER>
 __device__ __forceinline__ bool tile_fast(const Ctx &cx, const uint32_t w[8], DState &st, Facts &f,
-                                          Counters &cnt, uint32_t weight, Emit *em = nullptr) {
+                                          Counters &cnt, uint32_t weight, Emit *em = nullptr, bool *kind = nullptr) {
 #if FK_EXP == 4   /* ablation: loop framework only */
     {
         uint32_t x = 0;
@@ -618,7 +620,7 @@ __device__ __forceinline__ bool tile_fast(const Ctx &cx, const uint32_t w[8], DS
         m[d] = __builtin_amdgcn_perm(0u, 0x47544341u, x[d]) ^ w[d];   /* byte != "ACTG"[x] */
         mis |= m[d];
     }
-    if (!__ballot(mis != 0)) return tile_finish<COUNT, HM, INTER, false>(cx, x, 0u, 0u, st, f, cnt, weight, em);
+    if (!__ballot(mis != 0)) return tile_finish<COUNT, HM, INTER, false>(cx, x, 0u, 0u, st, f, cnt, weight, em, kind);
     /* some lane has a non-base byte: every lane classifies (the wave runs
        this once for all of them).  A byte is a base (m = 0) or '\n'
        (w ^ 0x0A = 0) iff the product of the two is 0, so dot4(m, w ^ 0x0A)
@@ -651,7 +653,7 @@ __device__ __forceinline__ bool tile_fast(const Ctx &cx, const uint32_t w[8], DS
     const bool lane_ok = (bad4[0] | bad4[1] | bad4[2] | bad4[3]) == 0 && nl0 < NL_TWO && nl1 < NL_TWO;
 #endif
     if (__ballot(!lane_ok)) return false;
-    return tile_finish<COUNT, HM, INTER, true>(cx, x, nl0, nl1, st, f, cnt, weight, em);
+    return tile_finish<COUNT, HM, INTER, true>(cx, x, nl0, nl1, st, f, cnt, weight, em, kind);
 }
 
 /*
@@ -1818,7 +1820,8 @@ struct PartGeo {
     uint32_t *pairs;       /* pairs mode: 4^(k+1) pair bins (k_bucket_count -> k_pair_fold) */
     uint32_t *singles;     /* pairs mode: 4^k single k-mer bins */
     uint32_t nomix;        /* FK_NO_MIXED: tiles the fast path cannot take go to tile_general */
-    uint32_t general;      /* general tiles k_part takes per range before k_part<RES> takes the rest */
+    uint32_t general;      /* general tiles (other than bases-only ones) k_part takes per range
+                              before k_part<RES> takes the rest */
     uint32_t stride;       /* index row stride: rows of both regions (k_part, then k_part<RES>) */
     uint32_t *flag;        /* [0] != 0: some range went to k_part<RES>, region 2 holds rows */
 };
@@ -2039,7 +2042,7 @@ k_part(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint
     consume(hw);   /* waited on every path (see k_count) */
     Counters cnt{0, 0, 0, 0, 0, FK_NO_EOF};
     bool done = !has || t >= sp.ntiles, stopped = false;
-    uint32_t general_left = pg.nomix ? 0xFFFFFFFFu : max(pg.general, 1u);
+    uint32_t general_left = pg.nomix ? 0xFFFFFFFFu : pg.general;
     uint32_t round = 0;
     const uint32_t row0 = (RES ? pg.rows : 0u) + blockIdx.x * pg.rounds;
     constexpr uint32_t NT = PART_TILES(PAIRS);
@@ -2054,19 +2057,22 @@ k_part(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint
 #define FK_ROUND(X)                                                                  \
     {                                                                                \
         Emit em{0, 0, 0, 0, false, false, false};                                    \
-        bool have = false, plain_ = false;                                           \
+        bool have = false, plain_ = false, kind_ = false;                            \
         if (!done) {                                                                 \
-            if (t < sp.nfull && st.hdr == 0 && tile_fast<true, H_EMIT, true>(cx, X, st, f, cnt, 1u, &em)) { \
+            if (t < sp.nfull && st.hdr == 0 && tile_fast<true, H_EMIT, true>(cx, X, st, f, cnt, 1u, &em, &kind_)) { \
                 have = em.deep;                                                      \
                 t++;                                                                 \
             } else if (RES && t < sp.nfull &&                                        \
                        tile_mixed<H_EMIT>(cx, X, (uint32_t)(t * FK_TILE_BYTES), st, f, cnt, 1u, plain_, &em)) { \
                 have = true;                                                         \
                 t++;                                                                 \
+            } else if (!RES && !kind_ && general_left == 0) {                        \
+                /* k_part<RES> counts this tile and the rest of the range (the  \
+                   tile is skipped here: t advances on every path) */           \
+                stopped = true;                                                      \
+                t++;                                                                 \
             } else {                                                                 \
-                /* k_part stops after its last general tile (the range's rest  \
-                   goes to k_part<RES>) */                                        \
-                stopped = !RES && --general_left == 0;                               \
+                general_left -= kind_ ? 0u : 1u;                                     \
                 uint32_t v_[8];                                                      \
                 const int64_t toff_ = (int64_t)(sp.rbase + t * FK_TILE_BYTES);       \
                 const int nb_ = load_lane<FK_LANE_BYTES>(cx, toff_ + lane * (int64_t)FK_LANE_BYTES, v_); \
@@ -2114,7 +2120,7 @@ k_part(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint
         const uint32_t unk = wsum32(cnt.unknown), eof = wmin32(cnt.eof);
         if (lane == 0) {
             ResumeRec w;
-            w.tile = t;
+            w.tile = t - 1;   /* the tile it stopped at */
             w.code = st.code; w.R = st.R; w.hdr = st.hdr;
             w.a_code = first.code; w.a_R = first.R; w.a_hdr = first.hdr;
             w.range = (uint32_t)wave;
@@ -2968,6 +2974,7 @@ struct fk_engine {
     uint32_t *d_ctl = nullptr;                /* k_tail's finished-block count */
     uint32_t ranges_per_wave = 1;             /* k <= 7: ranges per k_count wave slot (FK_RANGES_PER_WAVE) */
     bool no_mixed = false;                    /* FK_NO_MIXED=1: no mixed tiles (general byte walk) */
+    uint32_t part_general = 1;                /* k_part: general tiles per range (FK_PART_GENERAL) */
     uint32_t static_pct = 100;                /* k <= 7: % of a large segment in static ranges (FK_STATIC_PCT;
                                                  100 = no dynamic ranges: on a plain stream the waves that
                                                  finish early hand their bandwidth to the others, so
@@ -3178,6 +3185,7 @@ extern "C" int fk_engine_create(int k, const fk_opts *opts, fk_engine **out) {
        isolated comment line) and leaves denser ones to k_resume's mixed tiles */
     if (!e->no_mixed) e->general_tiles = 2;
     if (const char *gt = getenv("FK_GENERAL_TILES")) e->general_tiles = (uint32_t)strtoul(gt, nullptr, 10);
+    if (const char *pg = getenv("FK_PART_GENERAL")) e->part_general = (uint32_t)strtoul(pg, nullptr, 10);
     if (const char *ne = getenv("FK_NO_EVENTS")) e->timing = ne[0] != '1';
     if (const char *no = getenv("FK_NO_ONEPASS")) e->onepass = no[0] != '1';
     if (const char *rw = getenv("FK_RANGES_PER_WAVE")) e->ranges_per_wave = std::max(1u, (uint32_t)strtoul(rw, nullptr, 10));
@@ -3529,7 +3537,10 @@ static int launch_part(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t l
     /* mixed tiles: ranges past their general tiles go to k_part<RES>, whose
        rows (region 2, as many as k_part's) follow k_part's */
     const bool mixed = !e->no_mixed;
-    pg.general = e->general_tiles;
+    /* one comment line (or run break) per range stays here; a second one
+       sends the range to k_part<RES>, whose block-wide rounds only pay off
+       when many ranges go there */
+    pg.general = e->part_general;
     pg.stride = mixed ? 2 * pg.rows : pg.rows;
     if (!e->d_pflag && hipMalloc((void **)&e->d_pflag, 64) != hipSuccess) return FK_E_OOM;
     pg.flag = e->d_pflag;

@@ -895,12 +895,12 @@ def test_mixed_tiles_match_general_path(k, monkeypatch):
 
 
 @pytest.mark.parametrize("k", [8, 11, 12])
-@pytest.mark.parametrize("budget", ["1", "3"])
+@pytest.mark.parametrize("budget", ["0", "1", "3"])
 def test_part_resume_budgets(k, budget, monkeypatch):
     # k_part stops a range after `budget` general tiles and k_part<RES> counts
     # the rest (mixed tiles into region 2 of the partition); ranges that stop
     # and ranges that do not in one feed
-    monkeypatch.setenv("FK_GENERAL_TILES", budget)
+    monkeypatch.setenv("FK_PART_GENERAL", budget)
     rng = random.Random(77 + k)
     data = _dense_records(4400 + k, 300_000) + random_text(rng, 900_000, b"ACGT", [1, 1, 1, 1]) + \
         _dense_records(4500 + k, 200_000)
