@@ -269,6 +269,10 @@ def main():
     if phase_s:
         # rank 0's host time per step in each phase of the sharded pass
         out["phase_ms_per_step"] = {k_: v / args.steps * 1e3 for k_, v in phase_s.items()}
+    if merged is not None:
+        # "fast": one all-reduce of tables + counters + shard summaries;
+        # "stitched": summary all-gather, then a reduce (findkmer_amd/dist.py)
+        out["exchange"] = merged.path
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         # ~15 s of reference CPU work: ~76 Mbases/s at k=6, ~3 Mbases/s at k=11
         sample = args.cpu_sample_bytes or (1 << 30 if k <= 7 else 48 << 20)

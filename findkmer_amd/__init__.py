@@ -30,6 +30,8 @@ FK_E_ROLLOVER = -8
 FK_E_STATE = -9
 FK_E_SUMMARY = -12
 FK_K_MAX_DENSE = 16
+FK_PACK_COUNTERS = 14     # include/findkmer.h: fk_engine_shard_pack's counters
+FK_PACK_ROW_WORDS = 32    # ... and its rows (uint32 words)
 
 
 class FkState(ctypes.Structure):
@@ -92,6 +94,9 @@ SIGNATURES = [
     ("fk_summary_apply", ctypes.c_int, [ctypes.POINTER(FkSummary), ctypes.POINTER(FkState), ctypes.POINTER(FkState)]),
     ("fk_summary_is_full", ctypes.c_int, [ctypes.POINTER(FkSummary)]),
     ("fk_engine_resolve", ctypes.c_int, [_P, ctypes.POINTER(FkState)]),
+    ("fk_engine_shard_pack", ctypes.c_int, [_P, _P, _P, _P, ctypes.c_int, ctypes.c_int, ctypes.c_int]),
+    ("fk_engine_stream", ctypes.c_int, [_P, ctypes.POINTER(_P)]),
+    ("fk_shard_rows_compose", ctypes.c_int, [_P, ctypes.c_int, ctypes.c_int, ctypes.POINTER(FkState)]),
     ("fk_engine_finish", ctypes.c_int, [_P, ctypes.POINTER(FkResult)]),
     ("fk_engine_table", ctypes.c_int, [_P, _U32P]),
     ("fk_engine_table_device", ctypes.c_int, [_P, ctypes.POINTER(_P)]),
@@ -232,6 +237,18 @@ class Engine:
     def resolve(self, state):
         _check(lib().fk_engine_resolve(self.h, ctypes.byref(state)), "resolve")
 
+    def shard_pack(self, table_ptr, counters_ptr, rows_ptr, nrows=1, slot=0, is_last=False):
+        """Enqueue the pending shard's one-pass result (table, counter limbs,
+        pack rows) into device buffers on the engine's stream (no wait)."""
+        _check(lib().fk_engine_shard_pack(self.h, table_ptr, counters_ptr, rows_ptr, nrows, slot,
+                                          1 if is_last else 0), "shard_pack")
+
+    def stream(self):
+        """The engine's hipStream_t (as an int)."""
+        p = ctypes.c_void_p()
+        _check(lib().fk_engine_stream(self.h, ctypes.byref(p)), "stream")
+        return p.value or 0
+
     def state(self):
         s = FkState()
         _check(lib().fk_engine_state(self.h, ctypes.byref(s)), "state")
@@ -289,6 +306,19 @@ class Engine:
 def summary_apply(summary, state):
     out = FkState()
     _check(lib().fk_summary_apply(ctypes.byref(summary), ctypes.byref(state), ctypes.byref(out)), "summary_apply")
+    return out
+
+
+def shard_rows_compose(rows_ptr, world, rank):
+    """Compose `world` gathered pack rows (host memory, uint32) in rank
+    order: the FkState entering `rank`'s shard, or None if some row is not
+    a valid pack or a compact summary does not apply (every rank gets the
+    same answer)."""
+    out = FkState()
+    rc = lib().fk_shard_rows_compose(rows_ptr, world, rank, ctypes.byref(out))
+    if rc == FK_E_SUMMARY:
+        return None
+    _check(rc, "shard_rows_compose")
     return out
 
 

@@ -4142,6 +4142,119 @@ extern "C" int fk_engine_resolve(fk_engine *e, const fk_state *entering) {
     return finish_segment(e, e->shard_buf, e->shard_len, e->shard_lo, g, in);
 }
 
+/* ---- one-collective shard exchange ---- */
+
+/* The pending one-pass shard's result into a caller's merge buffer: the
+ * table (every block, 16-B pieces), the counters as 16-bit limbs and the
+ * pack rows (block 0).  `valid`: the host knows the shard went through
+ * k_count + k_tail; the device adds k_tail's verdict (no ONE_* bits, no
+ * 0xFF candidate).  The counter values are fk_engine_finish's formulas. */
+__global__ void __launch_bounds__(1024)
+k_shard_pack(const DevRes *res, const uint32_t *table, uint64_t nbins, uint32_t *dt, int32_t *dc, uint32_t *rows,
+             int nrows, int slot, int is_last, int valid, uint64_t len, int k) {
+    const bool ok = valid && res->need == 0 && res->eof_cand == ~0ull;
+    if (valid) {
+        /* nbins >= 4 (k >= 1); 16-B pieces while they fit, then words */
+        const uint64_t n4 = nbins / 4;
+        const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+        for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n4; i += stride)
+            reinterpret_cast<uint4 *>(dt)[i] = reinterpret_cast<const uint4 *>(table)[i];
+    }
+    if (blockIdx.x != 0) return;
+    const uint32_t t = threadIdx.x;
+    if (t < FK_PACK_COUNTERS * 4) {
+        const unsigned long long *acc = res->acc, *ts = res->tstat;
+        const uint32_t c = t >> 2, limb = t & 3;
+        unsigned long long v = 0;
+        if (ok) {
+            switch (c) {
+            case 0: v = acc[ACC_WIN]; break;
+            case 1: v = acc[ACC_WIN] + acc[ACC_VALID]; break;
+            case 2: case 3: case 4: case 5: v = ts[2 + (c - 2)] + acc[ACC_BASE + (c - 2)]; break;
+            case 6: case 7: case 8: case 9: v = ts[6 + (c - 6)] + acc[ACC_D1S + (c - 6)]; break;
+            case 10: v = acc[ACC_UNK]; break;
+            case 11: v = len; break;
+            case 12: v = 0; break;                           /* ended: a 0xFF shard is never packed */
+            default: v = is_last ? res->exit.hdr : 0u; break;   /* unterminated_header */
+            }
+        }
+        dc[t] = (int32_t)((v >> (16 * limb)) & 0xFFFFu);
+    }
+    for (uint32_t i = t; i < (uint32_t)nrows * FK_PACK_ROW_WORDS; i += blockDim.x) {
+        const uint32_t r = i / FK_PACK_ROW_WORDS, j = i % FK_PACK_ROW_WORDS;
+        uint32_t v = 0;
+        if ((int)r == slot && ok) {
+            if (j < 24) {
+                const ShardSum &ss = res->shard;
+                uint64_t w = 0;
+                switch (j >> 1) {
+                case 0: w = ss.g_code; break;
+                case 1: w = (uint64_t)ss.g_R | ((uint64_t)ss.g_hdr << 32); break;
+                case 2: w = ss.nvb0; break;
+                case 3: w = ss.c_R; break;
+                case 4: w = ss.c_code; break;
+                case 5: w = (uint64_t)ss.c_hdr | ((uint64_t)ss.absorb << 32); break;
+                case 6: w = ss.nv; break;
+                case 7: w = len; break;
+                case 8: w = (uint64_t)k; break;
+                case 11: w = FK_SUMMARY_COMPACT; break;
+                default: w = 0; break;                        /* 9: no 0xFF byte; 10: unused */
+                }
+                v = (j & 1) ? (uint32_t)(w >> 32) : (uint32_t)w;
+            } else if (j == 24) {
+                v = 1u;
+            }
+        }
+        rows[i] = v;
+    }
+}
+
+extern "C" int fk_engine_shard_pack(fk_engine *e, uint32_t *table, int32_t *counters, uint32_t *rows, int nrows,
+                                    int slot, int is_last) {
+    if (!e || !table || !counters || !rows || nrows < 1 || slot < 0 || slot >= nrows) return FK_E_INVALID;
+    if (e->sparse) return FK_E_INVALID;   /* 17 <= k <= 20: no dense table to merge */
+    if (!e->shard_pending) return FK_E_STATE;
+    int rc = set_dev(e);
+    if (rc) return rc;
+    /* packable: counted in one pass (k_count + k_tail, k <= 7), nothing of
+       the multi-launch path run since */
+    const int valid = e->shard_len && e->shard_op && !e->shard_full && !e->shard_resumed ? 1 : 0;
+    const uint64_t n4 = e->nbins / 4;
+    const unsigned grid = valid ? (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((n4 + 1023) / 1024, 1024)) : 1u;
+    hipLaunchKernelGGL(k_shard_pack, dim3(grid), dim3(1024), 0, e->stream, e->d_res, e->d_table, e->nbins, table,
+                       counters, rows, nrows, slot, is_last ? 1 : 0, valid, e->shard_len, e->k);
+    HIPCHK(hipGetLastError());
+    return FK_OK;
+}
+
+extern "C" int fk_engine_stream(fk_engine *e, void **stream) {
+    if (!e || !stream) return FK_E_INVALID;
+    *stream = (void *)e->stream;
+    return FK_OK;
+}
+
+extern "C" int fk_shard_rows_compose(const uint32_t *rows, int world, int rank, fk_state *entering) {
+    if (!rows || world < 1 || rank < 0 || rank >= world || !entering) return FK_E_INVALID;
+    XState s{0, 0, 0, 0};   /* the stream's initial state */
+    XState mine = s;
+    for (int r = 0; r < world; r++) {
+        const uint32_t *row = rows + (size_t)r * FK_PACK_ROW_WORDS;
+        if (row[24] != 1u) return FK_E_SUMMARY;
+        fk_summary sm;
+        for (int j = 0; j < 12; j++) sm.w[j] = (uint64_t)row[2 * j] | ((uint64_t)row[2 * j + 1] << 32);
+        if (sm.w[11] != FK_SUMMARY_COMPACT || sm.w[9] != 0) return FK_E_SUMMARY;
+        if (r == rank) mine = s;
+        XState y;
+        if (!compact_apply(&sm, s, y)) return FK_E_SUMMARY;
+        s = y;
+    }
+    entering->run = mine.R;
+    entering->code = fk_sigma(mine.code);
+    entering->hdr = mine.hdr;
+    entering->ended = 0;
+    return FK_OK;
+}
+
 /* ---- finish ---- */
 
 extern "C" int fk_engine_finish(fk_engine *e, fk_result *res) {

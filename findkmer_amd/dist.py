@@ -27,6 +27,17 @@ only when a shard may end the stream:
    rollover exit (a u32 trie counter reaching 2^32, :642-648): a merged bin
    that wrapped makes the table total fall short of the window count.
 
+One-collective fast path (k <= 7, shards counted in one pass): before any
+host round trip, every rank packs what its shard would report if its guessed
+entering state holds -- table, counter limbs, and its compact summary in its
+own row of a rows region (fk_engine_shard_pack, on the engine's stream) --
+and ONE all-reduce merges the tables and counters and, since the other
+ranks' rows are zero, all-gathers the summaries.  Each rank then composes
+the rows on the host (fk_shard_rows_compose); when every guess held (the
+normal case: a 256-byte halo fixes the state deep in a run) the merged
+buffer is already exact and the shard is resolved without further device
+work.  Otherwise every rank sees the same failure and runs steps 1-2 above.
+
 The same functions run over RCCL (backend "nccl", device tensors, bench.py)
 and over gloo on the CPU (tests/test_dist_cpu.py, with a model engine).
 """
@@ -34,7 +45,8 @@ import torch
 import torch.distributed as dist
 
 from . import FK_E_EMPTY, FK_E_ROLLOVER, FK_E_SUMMARY, FK_E_UNTERMINATED_HEADER, FK_OK
-from . import FindKmerError, FkState, FkSummary, summary_apply, summary_is_full
+from . import FK_PACK_COUNTERS, FK_PACK_ROW_WORDS
+from . import FindKmerError, FkState, FkSummary, shard_rows_compose, summary_apply, summary_is_full
 
 SUMMARY_WORDS = 12
 GATHER_WORDS = SUMMARY_WORDS + 1      # + "my summary is full" flag
@@ -46,16 +58,27 @@ COUNTERS = ("windows", "valid_bases", "base0", "base1", "base2", "base3",
             "scanned_bytes", "ended", "unterminated_header")
 LIMBS = 4
 COUNTER_SLOTS = len(COUNTERS) * LIMBS
+assert len(COUNTERS) == FK_PACK_COUNTERS   # the order fk_engine_shard_pack writes them in
+ROW_WORDS = FK_PACK_ROW_WORDS
+FAST_KMAX = 7                          # shards counted in one pass (k_count + k_tail)
 
 
 def _to_i64(v):
     return v - _U64 if v >= 1 << 63 else v
 
 
-def merge_buffer(k, device):
-    """The int32 buffer count_sharded reduces: the 4^k table, then the
-    counter limbs."""
-    return torch.zeros((1 << (2 * k)) + COUNTER_SLOTS, dtype=torch.int32, device=device)
+def merge_buffer(k, device, world=None):
+    """The int32 buffer count_sharded merges: the 4^k table, the counter
+    limbs, then one pack row per rank (the fast path's all-gather)."""
+    if world is None:
+        world = dist.get_world_size() if dist.is_initialized() else 1
+    return torch.zeros((1 << (2 * k)) + COUNTER_SLOTS + world * ROW_WORDS, dtype=torch.int32, device=device)
+
+
+def _regions(buf, k, world):
+    nb = 1 << (2 * k)
+    assert buf.numel() >= nb + COUNTER_SLOTS + world * ROW_WORDS, "merge_buffer(k, device, world)"
+    return nb, buf[:nb + COUNTER_SLOTS], buf[nb + COUNTER_SLOTS:nb + COUNTER_SLOTS + world * ROW_WORDS]
 
 
 def _compose(words, world, rank):
@@ -134,26 +157,32 @@ class ShardedResult:
     fields mirror fk_result (include/findkmer.h); they are decoded from the
     reduced buffer on first access (one device-to-host copy)."""
 
-    def __init__(self, buf, k, rank, first_end, local=None):
+    def __init__(self, buf, k, rank, first_end, local=None, path="stitched"):
         self.local = local          # this rank's own fk_result (timings)
+        self.path = path            # "fast": one all-reduce; "stitched": summary exchange + reduce
         self.buf = buf
         self.k = k
         self.rank = rank
         self.first_end = first_end
-        nb = 1 << (2 * k)
-        self.table = buf[:nb]
+        self.nb = 1 << (2 * k)
+        self.table = buf[:self.nb]
         self._vals = None
-        if rank == 0:
-            # on the device, enqueued behind the reduce (no host wait here):
-            # the merged table's u64 total (int32 sum + 2^32 per negative
-            # bin) and its distinct k-mers
+        self._tsum = self._distinct = None
+
+    def _table_stats(self):
+        """The merged table's u64 total (int32 sum + 2^32 per negative bin)
+        and its distinct k-mers, computed on first use (like `table`, valid
+        until the buffer is merged into again)."""
+        assert self.rank == 0, "the merged table lives on rank 0"
+        if self._tsum is None:
             t = self.table
-            self._tsum = t.sum(dtype=torch.int64) + (t < 0).sum(dtype=torch.int64) * (1 << 32)
-            self._distinct = (t != 0).sum(dtype=torch.int64)
+            self._tsum = int((t.sum(dtype=torch.int64) + (t < 0).sum(dtype=torch.int64) * (1 << 32)).item())
+            self._distinct = int((t != 0).sum(dtype=torch.int64).item())
+        return self._tsum, self._distinct
 
     def _decode(self):
         if self._vals is None:
-            limbs = self.buf[-COUNTER_SLOTS:].tolist()
+            limbs = self.buf[self.nb:self.nb + COUNTER_SLOTS].tolist()
             vals = {}
             for i, name in enumerate(COUNTERS):
                 v = 0
@@ -164,7 +193,7 @@ class ShardedResult:
         return self._vals
 
     def __getattr__(self, name):
-        if name.startswith("_") or name in ("buf", "k", "rank", "first_end", "table", "local"):
+        if name.startswith("_") or name in ("buf", "k", "rank", "first_end", "table", "local", "nb", "path"):
             raise AttributeError(name)
         v = self._decode()
         if name == "base_count":
@@ -179,16 +208,15 @@ class ShardedResult:
 
     @property
     def distinct(self):
-        assert self.rank == 0, "the merged table lives on rank 0"
-        return int(self._distinct.item())
+        return self._table_stats()[1]
 
     @property
     def rollover(self):
         """The reference's COUNTER ROLLOVER exit (:642-648): a merged bin or
         a depth-1 trie counter reached 2^32."""
-        assert self.rank == 0, "the merged table lives on rank 0"
+        tsum, _ = self._table_stats()
         v = self._decode()
-        if int(self._tsum.item()) != v["windows"]:
+        if tsum != v["windows"]:
             return True
         return any(v[f"depth1_{b}"] >= 1 << 32 for b in range(4))
 
@@ -201,36 +229,105 @@ class ShardedResult:
         return FK_OK
 
 
-def _put_counters(buf, values, pinned):
-    """Write the u64 counters into the buffer's limb slots (host -> buffer)."""
+def _put_counters(buf, values, pinned, nb=None):
+    """Write the u64 counters into the buffer's limb slots (host -> buffer),
+    after the nb table bins (default: the last COUNTER_SLOTS entries)."""
     limbs = []
     for v in values:
         v = int(v) % _U64
         limbs.extend((v >> (16 * j)) & 0xFFFF for j in range(LIMBS))
+    dst = buf[nb:nb + COUNTER_SLOTS] if nb is not None else buf[-COUNTER_SLOTS:]
     if pinned is not None:
         pinned.copy_(torch.tensor(limbs, dtype=torch.int32))
-        buf[-COUNTER_SLOTS:].copy_(pinned, non_blocking=True)
+        dst.copy_(pinned, non_blocking=True)
     else:
-        buf[-COUNTER_SLOTS:].copy_(torch.tensor(limbs, dtype=torch.int32))
+        dst.copy_(torch.tensor(limbs, dtype=torch.int32))
 
 
-def count_sharded(engine, ptr, nbytes, halo, buf, group=None, times=None, pinned=None):
+class _FastPath:
+    """Per-engine scratch of the one-collective path: the engine's stream as
+    a torch stream, a pinned host copy of the rows, and (gloo rehearsal of a
+    GPU engine) a device staging buffer for the pack."""
+
+    def __init__(self, engine, buf, world):
+        self.host_pack = getattr(engine, "host_pack", False)
+        self.world = world
+        self.rows_h = None
+        self.stage = None
+        self.ext = None
+        if not self.host_pack:
+            self.ext = torch.cuda.ExternalStream(engine.stream())
+            self.rows_h = torch.empty(world * ROW_WORDS, dtype=torch.int32, pin_memory=True)
+            if not buf.is_cuda:
+                self.stage = torch.empty(buf.numel(), dtype=torch.int32, device="cuda")
+
+
+def _fast_exchange(engine, buf, rank, world, group, times, t0):
+    """The one-collective path (see the module docstring).  Returns a
+    ShardedResult, or None when some rank's pack is not valid or its compact
+    summary does not apply (all ranks return None together; the shard is
+    still pending)."""
+    import time
+    fp = getattr(engine, "_fk_fast", None)
+    if fp is None or fp.world != world or (fp.stage is None) != (buf.is_cuda or fp.host_pack):
+        fp = _FastPath(engine, buf, world)
+        engine._fk_fast = fp
+    k = engine.k
+    nb, merged, rows = _regions(buf, k, world)
+    n = nb + COUNTER_SLOTS + world * ROW_WORDS
+    dst = fp.stage if fp.stage is not None else buf
+    engine.shard_pack(dst.data_ptr(), dst.data_ptr() + 4 * nb, dst.data_ptr() + 4 * (nb + COUNTER_SLOTS),
+                      world, rank, rank == world - 1)
+    if fp.stage is not None:
+        # gloo rehearsal of a GPU engine: the host buffer gets the pack
+        buf[:n].copy_(fp.stage[:n].cpu())
+    elif not fp.host_pack:
+        # the collective runs after the pack (engine stream -> torch's)
+        torch.cuda.current_stream().wait_stream(fp.ext)
+    t1 = time.perf_counter()
+    dist.all_reduce(buf[:n], op=dist.ReduceOp.SUM, group=group)
+    if buf.is_cuda:
+        fp.rows_h.copy_(rows, non_blocking=True)
+        torch.cuda.current_stream().synchronize()
+        rows_ptr = fp.rows_h.data_ptr()
+    else:
+        rows_ptr = rows.data_ptr()
+    state = shard_rows_compose(rows_ptr, world, rank)
+    t2 = time.perf_counter()
+    if state is None:
+        return None
+    engine.resolve(state)
+    _, r = engine.finish(allow=(FK_OK, FK_E_ROLLOVER, FK_E_UNTERMINATED_HEADER, FK_E_EMPTY))
+    if times is not None:
+        times["count"] = times.get("count", 0.0) + (t1 - t0)
+        times["exchange"] = times.get("exchange", 0.0) + (t2 - t1)
+        times["resolve"] = times.get("resolve", 0.0) + (time.perf_counter() - t2)
+    return ShardedResult(buf, k, rank, None, r, path="fast")
+
+
+def count_sharded(engine, ptr, nbytes, halo, buf, group=None, times=None, pinned=None, fast=True):
     """One sharded pass on this rank's GPU: count the shard, stitch the entry
     state, recount what the guess got wrong, and merge the tables and
-    counters into `buf` (merge_buffer(k, device): on the GPU for RCCL, on the
-    host for a gloo rehearsal; the sum lands on rank 0).  Returns a
-    ShardedResult.  `pinned` (optional): a pinned host int32 tensor of
-    COUNTER_SLOTS entries for an asynchronous counter upload.
+    counters into `buf` (merge_buffer(k, device, world): on the GPU for RCCL,
+    on the host for a gloo rehearsal; the sum lands on rank 0, and on every
+    rank when the one-collective path applies).  Returns a ShardedResult.
+    `pinned` (optional): a pinned host int32 tensor of COUNTER_SLOTS entries
+    for an asynchronous counter upload.  fast=False: always the stitched
+    exchange (steps 1-2).
 
     `engine` is a findkmer_amd.Engine (or, in the CPU tests, a model with the
     same feed_shard_device / summary / summary_full / resolve / finish /
-    table_to_device methods)."""
+    table_to_device / shard_pack methods)."""
     import time
     rank = dist.get_rank(group)
     world = dist.get_world_size(group)
     dev = buf.device
     t0 = time.perf_counter()
     engine.feed_shard_device(ptr, nbytes, halo)
+    if fast and engine.k <= FAST_KMAX and hasattr(engine, "shard_pack"):
+        got = _fast_exchange(engine, buf, rank, world, group, times, t0)
+        if got is not None:
+            return got
     t1 = time.perf_counter()
     got = stitch_entry_state(engine.summary(), group, dev)
     if got is None:
@@ -248,7 +345,7 @@ def count_sharded(engine, ptr, nbytes, halo, buf, group=None, times=None, pinned
     t2 = time.perf_counter()
     counting = first_end is None or rank <= first_end
     last = first_end if first_end is not None else world - 1
-    nb = 1 << (2 * engine.k)
+    nb, merged, _ = _regions(buf, engine.k, world)
     if counting:
         if buf.is_cuda:
             engine.table_to_device(buf.data_ptr())
@@ -260,8 +357,8 @@ def count_sharded(engine, ptr, nbytes, halo, buf, group=None, times=None, pinned
     else:
         buf[:nb].zero_()
         vals = [0] * len(COUNTERS)
-    _put_counters(buf, vals, pinned)
-    sum_tables(buf, group)
+    _put_counters(buf, vals, pinned, nb)
+    sum_tables(merged, group)
     if times is not None:
         # host wall time per phase: count (the feed returns when the shard's
         # kernels are done), stitch + resolve, table merge (enqueued)

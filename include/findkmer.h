@@ -156,6 +156,40 @@ int  fk_summary_apply(const fk_summary *s, const fk_state *in, fk_state *out);
 int  fk_summary_is_full(const fk_summary *s);   /* 1: full transfer function, 0: compact */
 int  fk_engine_resolve(fk_engine *e, const fk_state *entering);
 
+/* One-collective shard exchange (multi-GPU, findkmer_amd/dist.py).  After
+ * fk_engine_feed_shard, enqueue on the engine's stream (no host wait) what
+ * fk_engine_finish would report if the shard's guessed entering state holds,
+ * into caller-owned device buffers that one collective then merges:
+ *   table     4^k uint32: the shard's counts;
+ *   counters  FK_PACK_COUNTERS u64 values, each as 4 little-endian 16-bit
+ *             limbs in int32 slots (sums over ranks stay exact): windows,
+ *             valid_bases, base_count[4], depth1[4], unknown_chars,
+ *             scanned_bytes, ended (0), unterminated_header (only if
+ *             is_last, else 0);
+ *   rows      nrows x FK_PACK_ROW_WORDS uint32, zeroed except row `slot`:
+ *             the shard's compact summary (fk_summary, words 0..23) and
+ *             word 24 = 1 when the pack is valid (a one-pass shard whose
+ *             range guesses held and that saw no 0xFF byte), else 0.
+ * A sum of such row regions over ranks with distinct slots is an
+ * all-gather, so with nrows = world the whole exchange is one all-reduce.
+ * The shard stays pending: the caller composes the gathered rows
+ * (fk_shard_rows_compose) and either calls fk_engine_resolve with the
+ * entering state it returns (the merged buffer is then exact) or, if any
+ * row is invalid, falls back to the fk_engine_summary exchange.  Replaces
+ * no reference call (the reference is single-threaded, findKmer.cpp:962). */
+#define FK_PACK_COUNTERS 14
+#define FK_PACK_ROW_WORDS 32
+int  fk_engine_shard_pack(fk_engine *e, uint32_t *table, int32_t *counters, uint32_t *rows, int nrows,
+                          int slot, int is_last);
+/* The engine's HIP stream (hipStream_t), for ordering a caller's collective
+ * after fk_engine_shard_pack. */
+int  fk_engine_stream(fk_engine *e, void **stream);
+/* Compose gathered pack rows (host memory, `world` rows in rank order) from
+ * the stream's initial state: FK_OK and *entering = the state entering
+ * `rank`'s shard when every row is valid and every compact summary applies;
+ * FK_E_SUMMARY otherwise (every rank gets the same answer: fall back). */
+int  fk_shard_rows_compose(const uint32_t *rows, int world, int rank, fk_state *entering);
+
 /* Finish the stream (end-of-input rules) and fill *res.  Returns FK_OK or one
  * of FK_E_EMPTY / FK_E_UNTERMINATED_HEADER / FK_E_ROLLOVER (res is filled in
  * every case). */

@@ -22,6 +22,11 @@ def main():
     ap.add_argument("--bytes", type=int, default=3_000_000)
     ap.add_argument("--seed", type=int, default=5)
     ap.add_argument("--eof-in", type=int, default=-1)
+    ap.add_argument("--backend", default="gloo", choices=["gloo", "nccl"],
+                    help="nccl: RCCL with a device merge buffer (one rank per GPU: world 1 on a 1-GPU box)")
+    ap.add_argument("--fast", type=int, default=1, help="0: always the stitched exchange")
+    ap.add_argument("--input", default="mixed", choices=["mixed", "fasta"],
+                    help="fasta: one header + 80-column ACGT lines (every k <= 7 shard counts in one pass)")
     args = ap.parse_args()
     import numpy as np
     import torch
@@ -32,9 +37,19 @@ def main():
     from test_dist_cpu import _input
 
     torch.cuda.set_device(0)
-    dist.init_process_group("gloo")
+    if args.backend == "nccl":
+        dist.init_process_group("nccl", device_id=torch.device("cuda", 0))
+    else:
+        dist.init_process_group("gloo")
     rank, world = dist.get_rank(), dist.get_world_size()
-    data = bytearray(_input(args.seed, args.bytes))
+    if args.input == "fasta":
+        rng = np.random.default_rng(args.seed)
+        bases = np.frombuffer(b"ACGT", dtype=np.uint8)[rng.integers(0, 4, args.bytes)]
+        lines = bases[: len(bases) // 80 * 80].reshape(-1, 80)
+        body = np.concatenate([lines, np.full((len(lines), 1), 10, dtype=np.uint8)], axis=1).tobytes()
+        data = bytearray(b">synthetic\n" + body)
+    else:
+        data = bytearray(_input(args.seed, args.bytes))
     n = len(data)
     bounds = [0] + [n * i // world // 16 * 16 for i in range(1, world)] + [n]
     if args.eof_in >= 0:
@@ -47,12 +62,16 @@ def main():
     dev[: hi - lo + halo].copy_(torch.frombuffer(bytearray(data[lo - halo:hi]), dtype=torch.uint8))
     torch.cuda.synchronize()
     eng = fk.Engine(args.k, device=0)
-    buf = fkdist.merge_buffer(args.k, "cpu")
-    res = fkdist.count_sharded(eng, dev.data_ptr() + halo, hi - lo, halo, buf)
+    buf = fkdist.merge_buffer(args.k, "cuda" if args.backend == "nccl" else "cpu")
+    # twice: the second pass reuses the engine, the buffer and the fast
+    # path's scratch (stale rows from the first must not leak into it)
+    for _ in range(2):
+        eng.reset()
+        res = fkdist.count_sharded(eng, dev.data_ptr() + halo, hi - lo, halo, buf, fast=bool(args.fast))
     out = {"rank": rank}
     if rank == 0:
         want, r, _ = oracle.count_dense(data, args.k)
-        got = res.table.numpy().view(np.uint32)
+        got = res.table.cpu().numpy().view(np.uint32)
         out.update({
             "table_equal": bool(np.array_equal(got, want)),
             "windows": [res.windows, r.windows],
@@ -66,6 +85,7 @@ def main():
             "distinct": [res.distinct, r.distinct],
             "rollover": res.rollover,
             "first_end": res.first_end,
+            "path": res.path,
         })
         print(json.dumps(out), flush=True)
     eng.close()

@@ -166,6 +166,43 @@ class ModelEngine:
     def resolve(self, state):
         self.entering = (state.hdr, state.run, sigma(state.code), state.ended)
 
+    # fk_engine_shard_pack writes device buffers; this model writes host ones
+    host_pack = True
+
+    def shard_pack(self, table_ptr, counters_ptr, rows_ptr, nrows=1, slot=0, is_last=False):
+        """fk_engine_shard_pack on host memory: the shard counted from its
+        guess, its counters as 16-bit limbs, its compact summary in row
+        `slot` (word 24 = 1 when valid: a compact guess and no 0xFF)."""
+        import ctypes
+        from findkmer_amd import FK_PACK_ROW_WORDS
+        nb = 1 << (2 * self.k)
+        tab = np.ctypeslib.as_array((ctypes.c_uint32 * nb).from_address(table_ptr))
+        cnt = np.ctypeslib.as_array((ctypes.c_int32 * 56).from_address(counters_ptr))
+        rows = np.ctypeslib.as_array((ctypes.c_uint32 * (nrows * FK_PACK_ROW_WORDS)).from_address(rows_ptr))
+        rows[:] = 0
+        cnt[:] = 0
+        if self.guess is None:
+            return
+        hdr, R, code = self.guess
+        saved = self.entering
+        self.entering = (hdr, R, code, 0)
+        _, res = self.finish()
+        self.entering = saved
+        if res.hit_eof_byte:
+            return
+        tab[:] = self.tab
+        vals = [res.windows, res.valid_bases, *res.base_count, *res.depth1, res.unknown_chars,
+                res.scanned_bytes, 0, res.unterminated_header if is_last else 0]
+        for i, v in enumerate(vals):
+            for j in range(4):
+                cnt[4 * i + j] = (v >> (16 * j)) & 0xFFFF
+        w = [int(x) for x in self.summary().w]
+        row = rows[slot * FK_PACK_ROW_WORDS:(slot + 1) * FK_PACK_ROW_WORDS]
+        for j, v in enumerate(w):
+            row[2 * j] = v & 0xFFFFFFFF
+            row[2 * j + 1] = v >> 32
+        row[24] = 1
+
     def finish(self, allow=None):
         hdr, R, code, ended = self.entering
         k = self.k

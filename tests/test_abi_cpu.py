@@ -139,3 +139,45 @@ def test_compact_summary_apply():
     # header status must match the guess
     with pytest.raises(fk.FindKmerError):
         fk.summary_apply(a, fk.FkState(run=0, code=0, hdr=1))
+
+
+def _rows(summaries, valid=None):
+    """pack rows (fk_engine_shard_pack's layout) of compact summaries"""
+    import numpy as np
+    rows = np.zeros(len(summaries) * fk.FK_PACK_ROW_WORDS, dtype=np.uint32)
+    for r, s in enumerate(summaries):
+        base = r * fk.FK_PACK_ROW_WORDS
+        for j in range(12):
+            rows[base + 2 * j] = s.w[j] & 0xFFFFFFFF
+            rows[base + 2 * j + 1] = s.w[j] >> 32
+        rows[base + 24] = 1 if valid is None or valid[r] else 0
+    return rows
+
+
+def test_shard_rows_compose():
+    """fk_shard_rows_compose (host-only): the entering state of each rank
+    from the gathered pack rows, None when a row is invalid or a guess does
+    not hold (every rank then falls back to the stitched exchange)"""
+    k = 6
+    # rank 0 from the stream start (guess R=0), 1000 bases, ends deep in a
+    # run with last bases 0x0ABC; rank 1 guessed deep with those bases
+    s0 = _compact(0, 0, 0, 16384, 0, 0x0ABC, 0, 0, 1000, 16384, k)
+    s1 = _compact(256, 0x0ABC, 0, 16384, 77, 0x155, 0, 1, 0, 16384, k)
+    s2 = _compact(50, 0x155, 0, 16384, 0, 0x3F3F, 0, 0, 500, 16384, k)
+    rows = _rows([s0, s1, s2])
+    st0 = fk.shard_rows_compose(rows.ctypes.data, 3, 0)
+    assert (st0.run, st0.code, st0.hdr, st0.ended) == (0, 0, 0, 0)
+    st1 = fk.shard_rows_compose(rows.ctypes.data, 3, 1)
+    assert st1.run == 1000 and _sigma(st1.code) == 0x0ABC and st1.hdr == 0
+    st2 = fk.shard_rows_compose(rows.ctypes.data, 3, 2)
+    assert st2.run == 77 and _sigma(st2.code) == 0x155
+    # rank 2 guessed R=50 where the true run is 77 bases: both deep, same bases
+    # -> equivalent; a guess of a different header flag is not
+    bad = _compact(0, 0, 1, 16384, 0, 0, 0, 1, 0, 16384, k)
+    assert fk.shard_rows_compose(_rows([s0, s1, bad]).ctypes.data, 3, 0) is None
+    # an invalid pack anywhere: every rank falls back
+    assert fk.shard_rows_compose(_rows([s0, s1, s2], valid=[1, 0, 1]).ctypes.data, 3, 2) is None
+    # a shard that ends the stream (0xFF) is never packed as valid
+    eof = _compact(0, 0, 0, 16384, 0, 0x0ABC, 0, 0, 1000, 16384, k)
+    eof.w[9] = 1
+    assert fk.shard_rows_compose(_rows([eof, s1]).ctypes.data, 2, 1) is None

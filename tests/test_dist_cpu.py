@@ -86,6 +86,7 @@ def _worker(rank, world, port, data, bounds, mode, results):
                                                  "unknown_chars", "scanned_bytes", "hit_eof_byte",
                                                  "unterminated_header", "distinct", "rollover")}
             out["first_end"] = res.first_end
+            out["path"] = res.path
             results.put((res.table.numpy().astype(np.uint32).tobytes(), out))
     finally:
         dist.destroy_process_group()
@@ -132,6 +133,9 @@ def _check(data, world, mode, bounds=None):
 def test_merge_gloo(world, mode):
     got = _check(_input(world + 7, 24000), world, mode)
     assert got["first_end"] is None
+    # every guess right: one all-reduce; a wrong guess or full summaries:
+    # the stitched exchange
+    assert got["path"] == ("fast" if mode == "compact" else "stitched")
 
 
 @pytest.mark.parametrize("mode", ["full", "compact", "compact_miss"])
@@ -173,7 +177,7 @@ def test_merged_rollover_detection():
         buf = fkdist.merge_buffer(2, "cpu")
         buf[:16] = torch.tensor(np.array(table_vals, dtype=np.uint32).view(np.int32))
         vals = [windows, 0, 0, 0, 0, 0, *depth1, 0, 0, 0, 0]
-        fkdist._put_counters(buf, vals, None)
+        fkdist._put_counters(buf, vals, None, 16)
         return fkdist.ShardedResult(buf, 2, 0, None)
 
     ok = result([3] * 15 + [0xFFFFFFFF], 45 + 0xFFFFFFFF)

@@ -33,6 +33,8 @@ def test_two_rank_shards_gloo(k, fasta, chrom):
                     ["--gpus", "2", "--steps", "2", "--warmup", "1", "--no-cpu-baseline", "--dist-backend", "gloo",
                      "--k", str(k), "--fasta-line", str(fasta), "--bases", "12800000", "--chrom", str(chrom)])
     assert out["n_gpus"] == 2 and out["value"] > 0
+    # pure ACGT shards with a halo that fixes the state: one all-reduce
+    assert out["exchange"] == ("fast" if k <= 7 else "stitched")
 
 
 @pytest.mark.gpu
@@ -49,3 +51,22 @@ def test_sharded_mixed_input_against_oracle(k, world, eof_in):
         assert out[key][0] == out[key][1], (key, out[key])
     assert not out["rollover"]
     assert out["first_end"] == (eof_in if eof_in >= 0 else None)
+    if eof_in >= 0 or k > 7:
+        assert out["path"] == "stitched"   # a 0xFF shard / k_part shards are never packed
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k,fast,eof_in", [(6, 1, -1), (7, 1, -1), (5, 0, -1), (6, 1, 0), (11, 1, -1)])
+def test_rccl_single_rank_merge(k, fast, eof_in):
+    """The RCCL code path on a one-GPU box (world 1, backend nccl): the pack
+    into the device merge buffer, the engine-stream -> collective ordering,
+    the all-reduce and the pinned rows; a 0xFF (eof_in 0) or k >= 8 takes
+    the stitched exchange over RCCL instead"""
+    out = _torchrun(1, 29800 + 3 * k + fast + eof_in, os.path.join(REPO, "tests", "dist_worker.py"),
+                    ["--k", str(k), "--backend", "nccl", "--fast", str(fast), "--eof-in", str(eof_in),
+                     "--input", "fasta"])
+    assert out["table_equal"]
+    for key in ("windows", "valid_bases", "base_count", "depth1", "unknown_chars", "scanned_bytes",
+                "hit_eof_byte", "unterminated_header", "distinct"):
+        assert out[key][0] == out[key][1], (key, out[key])
+    assert out["path"] == ("fast" if fast and k <= 7 and eof_in < 0 else "stitched")
