@@ -19,7 +19,7 @@ WFLAGS   := -O2 -fPIC -std=c++17 -ffp-contract=off -fno-fast-math -I$(ROOT)inclu
 
 all: $(LIB) $(ROOT)findKmer $(ROOT)Debug/findKmer oracle
 
-$(BUILD)/fk_engine.o: $(CSRC)/fk_engine.hip $(CSRC)/fk_device.h $(CSRC)/fk_sparse.h $(ROOT)include/findkmer.h
+$(BUILD)/fk_engine.o: $(CSRC)/fk_engine.hip $(CSRC)/fk_device.h $(CSRC)/fk_sparse.h $(CSRC)/fk_comm.h $(ROOT)include/findkmer.h
 	@mkdir -p $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -c -x hip $< -o $@
 
@@ -31,13 +31,17 @@ $(BUILD)/fk_sparse.o: $(CSRC)/fk_sparse.hip $(CSRC)/fk_sparse.h
 	@mkdir -p $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -c -x hip $< -o $@
 
+$(BUILD)/fk_comm.o: $(CSRC)/fk_comm.hip $(CSRC)/fk_comm.h $(ROOT)include/findkmer.h
+	@mkdir -p $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -c -x hip $< -o $@
+
 $(BUILD)/fk_ingest.o: $(CSRC)/fk_ingest.hip $(ROOT)include/findkmer.h
 	@mkdir -p $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -c -x hip $< -o $@
 
-$(LIB): $(BUILD)/fk_engine.o $(BUILD)/fk_sparse.o $(BUILD)/fk_ingest.o $(BUILD)/fk_writer.o
+$(LIB): $(BUILD)/fk_engine.o $(BUILD)/fk_sparse.o $(BUILD)/fk_ingest.o $(BUILD)/fk_comm.o $(BUILD)/fk_writer.o
 	@mkdir -p $(LIBDIR)
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -lpthread
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -lpthread -ldl
 
 $(BUILD)/fk_main.o: $(CSRC)/fk_main.cpp $(ROOT)include/findkmer.h
 	@mkdir -p $(BUILD)

@@ -50,6 +50,10 @@ def parse():
                     help="streams longer than this (pure ACGT): an 'N' run break every this many bases, a genome of chromosomes (0 = one run)")
     ap.add_argument("--timing-every", type=int, default=4,
                     help="time the count kernel with HIP events on every Nth step")
+    ap.add_argument("--stitched", action="store_true",
+                    help="sharded pass: always the summary all-gather + reduce (no one-collective path)")
+    ap.add_argument("--torch-exchange", action="store_true",
+                    help="one-collective path through torch.distributed instead of the library's RCCL communicator")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl = RCCL over xGMI (one GPU per rank); gloo = host-side rehearsal")
     return ap.parse_args()
@@ -128,7 +132,10 @@ def main():
     local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dist = None
-    if world > 1:
+    # under torch.distributed.run (WORLD_SIZE set, even to 1) the sharded
+    # pass with its exchange runs; `python bench.py` at N=1 feeds directly
+    sharded = world > 1 or "WORLD_SIZE" in os.environ
+    if sharded:
         import torch.distributed as dist
         if args.dist_backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -171,16 +178,16 @@ def main():
     # (recording them on every launch costs ~2% of the step)
     eng = fk.Engine(k, device=local, timing_every=args.timing_every)
     coll_dev = "cuda" if args.dist_backend == "nccl" else "cpu"
-    merge_t = fkdist.merge_buffer(k, coll_dev) if world > 1 else None
+    merge_t = fkdist.merge_buffer(k, coll_dev) if sharded else None
     pinned = torch.empty(fkdist.COUNTER_SLOTS, dtype=torch.int32, pin_memory=True) if coll_dev == "cuda" else None
 
     def step():
         eng.reset()
-        if world > 1:
+        if sharded:
             # shard, stitch entry states (all-gather of 96-B summaries), merge
             # tables + counters (reduce to rank 0): findkmer_amd/dist.py
             res = fkdist.count_sharded(eng, buf.data_ptr() + halo, nbytes, halo, merge_t, times=phase_s,
-                                       pinned=pinned)
+                                       pinned=pinned, fast=not args.stitched, native=not args.torch_exchange)
             return res.local, res
         eng.feed_device(buf.data_ptr(), nbytes)
         # an ablation build (FINDKMER_LIB) may leave the table incomplete
@@ -273,6 +280,7 @@ def main():
         # "fast": one all-reduce of tables + counters + shard summaries;
         # "stitched": summary all-gather, then a reduce (findkmer_amd/dist.py)
         out["exchange"] = merged.path
+        out["transport"] = merged.transport
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         # ~15 s of reference CPU work: ~76 Mbases/s at k=6, ~3 Mbases/s at k=11
         sample = args.cpu_sample_bytes or (1 << 30 if k <= 7 else 48 << 20)
@@ -282,6 +290,7 @@ def main():
         print(json.dumps(out), flush=True)
     eng.close()
     if dist:
+        fkdist.close_native_comms()
         dist.destroy_process_group()
 
 

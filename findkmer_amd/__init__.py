@@ -32,6 +32,7 @@ FK_E_SUMMARY = -12
 FK_K_MAX_DENSE = 16
 FK_PACK_COUNTERS = 14     # include/findkmer.h: fk_engine_shard_pack's counters
 FK_PACK_ROW_WORDS = 32    # ... and its rows (uint32 words)
+FK_COMM_ID_BYTES = 128
 
 
 class FkState(ctypes.Structure):
@@ -96,6 +97,10 @@ SIGNATURES = [
     ("fk_engine_resolve", ctypes.c_int, [_P, ctypes.POINTER(FkState)]),
     ("fk_engine_shard_pack", ctypes.c_int, [_P, _P, _P, _P, ctypes.c_int, ctypes.c_int, ctypes.c_int]),
     ("fk_engine_stream", ctypes.c_int, [_P, ctypes.POINTER(_P)]),
+    ("fk_comm_id", ctypes.c_int, [_P]),
+    ("fk_comm_create", ctypes.c_int, [_P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.POINTER(_P)]),
+    ("fk_comm_destroy", None, [_P]),
+    ("fk_engine_shard_exchange", ctypes.c_int, [_P, _P, _P]),
     ("fk_shard_rows_compose", ctypes.c_int, [_P, ctypes.c_int, ctypes.c_int, ctypes.POINTER(FkState)]),
     ("fk_engine_finish", ctypes.c_int, [_P, ctypes.POINTER(FkResult)]),
     ("fk_engine_table", ctypes.c_int, [_P, _U32P]),
@@ -243,6 +248,17 @@ class Engine:
         _check(lib().fk_engine_shard_pack(self.h, table_ptr, counters_ptr, rows_ptr, nrows, slot,
                                           1 if is_last else 0), "shard_pack")
 
+    def shard_exchange(self, comm, merge_ptr):
+        """fk_engine_shard_exchange: pack, one RCCL all-reduce of the merge
+        buffer over `comm` (a Comm) on the engine's stream, compose, resolve.
+        True: merged and resolved; False: fall back to the summary exchange
+        (the shard is still pending)."""
+        rc = lib().fk_engine_shard_exchange(self.h, comm.h, merge_ptr)
+        if rc == FK_E_SUMMARY:
+            return False
+        _check(rc, "shard_exchange")
+        return True
+
     def stream(self):
         """The engine's hipStream_t (as an int)."""
         p = ctypes.c_void_p()
@@ -307,6 +323,31 @@ def summary_apply(summary, state):
     out = FkState()
     _check(lib().fk_summary_apply(ctypes.byref(summary), ctypes.byref(state), ctypes.byref(out)), "summary_apply")
     return out
+
+
+def comm_id():
+    """A fresh RCCL unique id (FK_COMM_ID_BYTES bytes) for Comm: made by one
+    rank, handed to the others by the caller."""
+    b = (ctypes.c_uint8 * FK_COMM_ID_BYTES)()
+    _check(lib().fk_comm_id(b), "comm_id")
+    return bytes(b)
+
+
+class Comm:
+    """The library's own RCCL communicator (fk_comm): every rank constructs
+    it with the same id (collective)."""
+
+    def __init__(self, uid, world, rank, device):
+        b = (ctypes.c_uint8 * FK_COMM_ID_BYTES).from_buffer_copy(uid)
+        h = ctypes.c_void_p()
+        _check(lib().fk_comm_create(b, world, rank, device, ctypes.byref(h)), "comm_create")
+        self.h = h
+        self.world, self.rank, self.device = world, rank, device
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().fk_comm_destroy(self.h)
+            self.h = None
 
 
 def shard_rows_compose(rows_ptr, world, rank):

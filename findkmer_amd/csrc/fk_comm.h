@@ -1,0 +1,15 @@
+/* Library-internal interface of fk_comm.hip: the RCCL communicator behind
+ * the C-ABI's fk_comm (include/findkmer.h), used by the engine's
+ * one-collective shard exchange (fk_engine_shard_exchange). */
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+struct fk_comm;
+
+int fkc_world(const fk_comm *c);
+int fkc_rank(const fk_comm *c);
+int fkc_device(const fk_comm *c);
+/* in-place sum of n int32 over the ranks, enqueued on `s` */
+int fkc_allreduce_i32(fk_comm *c, int32_t *buf, size_t n, hipStream_t s);

@@ -1,0 +1,110 @@
+/*
+ * fk_comm: an RCCL communicator owned by the library (one rank per GPU, over
+ * xGMI), so that a sharded pass's exchange runs on the engine's own HIP
+ * stream with no framework in between: pack kernel -> ncclAllReduce ->
+ * rows publish kernel, one host wait (fk_engine_shard_exchange).
+ *
+ * RCCL is resolved at run time (dlopen) rather than linked: the drop-in
+ * ./findKmer never needs it, and inside a PyTorch process the copy torch has
+ * already loaded (same SONAME librccl.so.1) is the one used.  The unique id
+ * is created by one rank (fk_comm_id) and handed to the others by the
+ * caller (findkmer_amd/dist.py broadcasts it over torch.distributed).
+ *
+ * The reference has no counterpart: it is single-threaded
+ * (findKmer/src/findKmer.cpp:962-1069); SURVEY.md §8(e).
+ */
+#include <dlfcn.h>
+#include <string.h>
+
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include "findkmer.h"
+#include "fk_comm.h"
+
+namespace {
+
+struct Rccl {
+    decltype(&ncclGetUniqueId) get_id = nullptr;
+    decltype(&ncclCommInitRank) init_rank = nullptr;
+    decltype(&ncclCommDestroy) destroy = nullptr;
+    decltype(&ncclAllReduce) all_reduce = nullptr;
+    bool ok = false;
+};
+
+/* the process's RCCL: an already loaded copy first (torch's), else the
+   system one */
+const Rccl &rccl() {
+    static Rccl r = [] {
+        Rccl x;
+        void *h = dlopen("librccl.so.1", RTLD_NOW | RTLD_NOLOAD);
+        if (!h) h = dlopen("librccl.so.1", RTLD_NOW);
+        if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW);
+        if (!h) return x;
+        x.get_id = (decltype(x.get_id))dlsym(h, "ncclGetUniqueId");
+        x.init_rank = (decltype(x.init_rank))dlsym(h, "ncclCommInitRank");
+        x.destroy = (decltype(x.destroy))dlsym(h, "ncclCommDestroy");
+        x.all_reduce = (decltype(x.all_reduce))dlsym(h, "ncclAllReduce");
+        x.ok = x.get_id && x.init_rank && x.destroy && x.all_reduce;
+        return x;
+    }();
+    return r;
+}
+
+}  // namespace
+
+struct fk_comm {
+    ncclComm_t nc = nullptr;
+    int world = 0, rank = 0, device = 0;
+};
+
+static_assert(FK_COMM_ID_BYTES == NCCL_UNIQUE_ID_BYTES, "fk_comm ids are RCCL unique ids");
+
+extern "C" int fk_comm_id(uint8_t *id) {
+    if (!id) return FK_E_INVALID;
+    const Rccl &r = rccl();
+    if (!r.ok) return FK_E_RCCL;
+    ncclUniqueId u;
+    if (r.get_id(&u) != ncclSuccess) return FK_E_RCCL;
+    memcpy(id, u.internal, NCCL_UNIQUE_ID_BYTES);
+    return FK_OK;
+}
+
+extern "C" int fk_comm_create(const uint8_t *id, int world, int rank, int device, fk_comm **out) {
+    if (!id || !out || world < 1 || rank < 0 || rank >= world) return FK_E_INVALID;
+    *out = nullptr;
+    const Rccl &r = rccl();
+    if (!r.ok) return FK_E_RCCL;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n < 1) return FK_E_NO_DEVICE;
+    if (device < 0 || device >= n) return FK_E_INVALID;
+    if (hipSetDevice(device) != hipSuccess) return FK_E_HIP;
+    ncclUniqueId u;
+    memcpy(u.internal, id, NCCL_UNIQUE_ID_BYTES);
+    fk_comm *c = new fk_comm;
+    c->world = world;
+    c->rank = rank;
+    c->device = device;
+    /* collective: returns when every rank has joined */
+    if (r.init_rank(&c->nc, world, u, rank) != ncclSuccess) {
+        delete c;
+        return FK_E_RCCL;
+    }
+    *out = c;
+    return FK_OK;
+}
+
+extern "C" void fk_comm_destroy(fk_comm *c) {
+    if (!c) return;
+    if (c->nc && rccl().ok) rccl().destroy(c->nc);
+    delete c;
+}
+
+int fkc_world(const fk_comm *c) { return c->world; }
+int fkc_rank(const fk_comm *c) { return c->rank; }
+int fkc_device(const fk_comm *c) { return c->device; }
+
+int fkc_allreduce_i32(fk_comm *c, int32_t *buf, size_t n, hipStream_t s) {
+    if (!c || !c->nc || !rccl().ok) return FK_E_RCCL;
+    return rccl().all_reduce(buf, buf, n, ncclInt32, ncclSum, c->nc, s) == ncclSuccess ? FK_OK : FK_E_RCCL;
+}

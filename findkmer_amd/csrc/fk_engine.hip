@@ -46,6 +46,7 @@
 #include <vector>
 
 #include "findkmer.h"
+#include "fk_comm.h"
 #include "fk_device.h"
 #include "fk_sparse.h"
 
@@ -3027,6 +3028,10 @@ struct fk_engine {
     uint32_t timing_every = 1;
     bool cur_timed = true;                    /* the current feed's launches record events */
     std::vector<uint8_t> unknown_bytes;
+    /* fk_engine_shard_exchange: gathered pack rows, pinned and mapped (word
+       0: sequence number, rows from word 32) */
+    uint32_t *h_rows = nullptr, *h_rows_dev = nullptr;
+    uint32_t rows_cap = 0, rows_seq = 0;
 };
 
 __global__ void k_zero(uint32_t *table, uint64_t nbins, uint32_t *shortcnt, uint64_t nshort,
@@ -3140,6 +3145,7 @@ extern "C" void fk_engine_destroy(fk_engine *e) {
     if (e->h_stage) hipHostFree(e->h_stage);
     for (int i = 0; i < 3; i++) if (e->ev[i]) hipEventDestroy(e->ev[i]);
     if (e->h_res) hipHostFree(e->h_res);
+    if (e->h_rows) hipHostFree(e->h_rows);
     hipFree(e->d_done);
     hipFree(e->d_tpart);
     if (e->own_stream && e->stream) hipStreamDestroy(e->stream);
@@ -4225,6 +4231,62 @@ extern "C" int fk_engine_shard_pack(fk_engine *e, uint32_t *table, int32_t *coun
                        counters, rows, nrows, slot, is_last ? 1 : 0, valid, e->shard_len, e->k);
     HIPCHK(hipGetLastError());
     return FK_OK;
+}
+
+/* The gathered rows to pinned host memory, sequence number last (one wave,
+   one system fence; the host spins on it, as on the result block). */
+__global__ void __launch_bounds__(64) k_rows_publish(const uint32_t *rows, uint32_t n, uint32_t *host, uint32_t seq) {
+    for (uint32_t i = threadIdx.x; i < n; i += 64) host[32 + i] = rows[i];
+    __threadfence_system();
+    if (threadIdx.x == 0) __hip_atomic_store(&host[0], seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+extern "C" int fk_engine_shard_exchange(fk_engine *e, fk_comm *comm, int32_t *merge) {
+    if (!e || !comm || !merge) return FK_E_INVALID;
+    if (e->sparse) return FK_E_INVALID;
+    if (!e->shard_pending) return FK_E_STATE;
+    const int world = fkc_world(comm), rank = fkc_rank(comm);
+    if (fkc_device(comm) != e->dev) return FK_E_INVALID;
+    int rc = set_dev(e);
+    if (rc) return rc;
+    const uint32_t nrow = (uint32_t)world * FK_PACK_ROW_WORDS;
+    if (e->rows_cap < nrow) {
+        if (e->h_rows) hipHostFree(e->h_rows);
+        e->h_rows = e->h_rows_dev = nullptr;
+        e->rows_cap = 0;
+        if (hipHostMalloc((void **)&e->h_rows, (32 + nrow) * sizeof(uint32_t), hipHostMallocMapped | hipHostMallocCoherent) !=
+                hipSuccess ||
+            hipHostGetDevicePointer((void **)&e->h_rows_dev, e->h_rows, 0) != hipSuccess)
+            return FK_E_OOM;
+        memset(e->h_rows, 0, (32 + nrow) * sizeof(uint32_t));
+        e->rows_cap = nrow;
+    }
+    uint32_t *rows = reinterpret_cast<uint32_t *>(merge + e->nbins + 4 * FK_PACK_COUNTERS);
+    rc = fk_engine_shard_pack(e, reinterpret_cast<uint32_t *>(merge), merge + e->nbins, rows, world, rank,
+                              rank == world - 1);
+    if (rc) return rc;
+    rc = fkc_allreduce_i32(comm, merge, e->nbins + 4 * FK_PACK_COUNTERS + nrow, e->stream);
+    if (rc) return rc;
+    if (++e->rows_seq == 0) e->rows_seq = 1;
+    const uint32_t want = e->rows_seq;
+    hipLaunchKernelGGL(k_rows_publish, dim3(1), dim3(64), 0, e->stream, rows, nrow, e->h_rows_dev, want);
+    HIPCHK(hipGetLastError());
+    for (uint32_t spin = 1;; spin++) {
+        if (__atomic_load_n(&e->h_rows[0], __ATOMIC_ACQUIRE) == want) break;
+        if ((spin & 4095) == 0) {
+            hipError_t q = hipStreamQuery(e->stream);
+            if (q == hipSuccess) {
+                if (__atomic_load_n(&e->h_rows[0], __ATOMIC_ACQUIRE) == want) break;
+                return FK_E_HIP;   /* stream drained without publishing */
+            }
+            if (q != hipErrorNotReady) return FK_E_HIP;
+        }
+        __builtin_ia32_pause();
+    }
+    fk_state st;
+    rc = fk_shard_rows_compose(e->h_rows + 32, world, rank, &st);
+    if (rc) return rc;   /* FK_E_SUMMARY: the shard stays pending */
+    return fk_engine_resolve(e, &st);
 }
 
 extern "C" int fk_engine_stream(fk_engine *e, void **stream) {

@@ -46,7 +46,7 @@ import torch.distributed as dist
 
 from . import FK_E_EMPTY, FK_E_ROLLOVER, FK_E_SUMMARY, FK_E_UNTERMINATED_HEADER, FK_OK
 from . import FK_PACK_COUNTERS, FK_PACK_ROW_WORDS
-from . import FindKmerError, FkState, FkSummary, shard_rows_compose, summary_apply, summary_is_full
+from . import Comm, FindKmerError, FkState, FkSummary, comm_id, shard_rows_compose, summary_apply, summary_is_full
 
 SUMMARY_WORDS = 12
 GATHER_WORDS = SUMMARY_WORDS + 1      # + "my summary is full" flag
@@ -157,9 +157,10 @@ class ShardedResult:
     fields mirror fk_result (include/findkmer.h); they are decoded from the
     reduced buffer on first access (one device-to-host copy)."""
 
-    def __init__(self, buf, k, rank, first_end, local=None, path="stitched"):
+    def __init__(self, buf, k, rank, first_end, local=None, path="stitched", transport="torch"):
         self.local = local          # this rank's own fk_result (timings)
         self.path = path            # "fast": one all-reduce; "stitched": summary exchange + reduce
+        self.transport = transport  # "rccl-native": the library's own communicator; "torch": torch.distributed
         self.buf = buf
         self.k = k
         self.rank = rank
@@ -193,7 +194,8 @@ class ShardedResult:
         return self._vals
 
     def __getattr__(self, name):
-        if name.startswith("_") or name in ("buf", "k", "rank", "first_end", "table", "local", "nb", "path"):
+        if name.startswith("_") or name in ("buf", "k", "rank", "first_end", "table", "local", "nb", "path",
+                                                     "transport"):
             raise AttributeError(name)
         v = self._decode()
         if name == "base_count":
@@ -242,6 +244,34 @@ def _put_counters(buf, values, pinned, nb=None):
         dst.copy_(pinned, non_blocking=True)
     else:
         dst.copy_(torch.tensor(limbs, dtype=torch.int32))
+
+
+_comms = {}
+
+
+def native_comm(group=None):
+    """The library's own RCCL communicator (findkmer_amd.Comm) over the
+    ranks of `group` (backend nccl), made on first use: group rank 0 creates
+    the id, one broadcast hands it over, every rank joins."""
+    key = id(group) if group is not None else 0
+    c = _comms.get(key)
+    if c is None:
+        rank = dist.get_rank(group)
+        world = dist.get_world_size(group)
+        t = torch.zeros(128, dtype=torch.uint8, device="cuda")
+        if rank == 0:
+            t.copy_(torch.frombuffer(bytearray(comm_id()), dtype=torch.uint8))
+        src = dist.get_global_rank(group, 0) if group is not None else 0
+        dist.broadcast(t, src=src, group=group)
+        c = Comm(bytes(t.cpu().tolist()), world, rank, torch.cuda.current_device())
+        _comms[key] = c
+    return c
+
+
+def close_native_comms():
+    for c in _comms.values():
+        c.close()
+    _comms.clear()
 
 
 class _FastPath:
@@ -305,7 +335,8 @@ def _fast_exchange(engine, buf, rank, world, group, times, t0):
     return ShardedResult(buf, k, rank, None, r, path="fast")
 
 
-def count_sharded(engine, ptr, nbytes, halo, buf, group=None, times=None, pinned=None, fast=True):
+def count_sharded(engine, ptr, nbytes, halo, buf, group=None, times=None, pinned=None, fast=True,
+                  native=True):
     """One sharded pass on this rank's GPU: count the shard, stitch the entry
     state, recount what the guess got wrong, and merge the tables and
     counters into `buf` (merge_buffer(k, device, world): on the GPU for RCCL,
@@ -325,9 +356,19 @@ def count_sharded(engine, ptr, nbytes, halo, buf, group=None, times=None, pinned
     t0 = time.perf_counter()
     engine.feed_shard_device(ptr, nbytes, halo)
     if fast and engine.k <= FAST_KMAX and hasattr(engine, "shard_pack"):
-        got = _fast_exchange(engine, buf, rank, world, group, times, t0)
-        if got is not None:
-            return got
+        if native and buf.is_cuda and hasattr(engine, "shard_exchange") and dist.get_backend(group) == "nccl":
+            ok = engine.shard_exchange(native_comm(group), buf.data_ptr())
+            if ok:
+                t1 = time.perf_counter()
+                _, r = engine.finish(allow=(FK_OK, FK_E_ROLLOVER, FK_E_UNTERMINATED_HEADER, FK_E_EMPTY))
+                if times is not None:
+                    times["exchange"] = times.get("exchange", 0.0) + (t1 - t0)
+                    times["finish"] = times.get("finish", 0.0) + (time.perf_counter() - t1)
+                return ShardedResult(buf, engine.k, rank, None, r, path="fast", transport="rccl-native")
+        else:
+            got = _fast_exchange(engine, buf, rank, world, group, times, t0)
+            if got is not None:
+                return got
     t1 = time.perf_counter()
     got = stitch_entry_state(engine.summary(), group, dev)
     if got is None:

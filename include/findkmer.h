@@ -190,6 +190,29 @@ int  fk_engine_stream(fk_engine *e, void **stream);
  * FK_E_SUMMARY otherwise (every rank gets the same answer: fall back). */
 int  fk_shard_rows_compose(const uint32_t *rows, int world, int rank, fk_state *entering);
 
+/* An RCCL communicator of the library (one rank per GPU; RCCL is loaded at
+ * run time).  One rank creates the id, the caller hands it to every rank
+ * (e.g. a torch.distributed broadcast), and every rank calls fk_comm_create
+ * (collective: it returns when all have joined).  FK_E_RCCL when RCCL is
+ * unavailable or fails. */
+#define FK_COMM_ID_BYTES 128
+typedef struct fk_comm fk_comm;
+int  fk_comm_id(uint8_t *id /* FK_COMM_ID_BYTES */);
+int  fk_comm_create(const uint8_t *id, int world, int rank, int device, fk_comm **out);
+void fk_comm_destroy(fk_comm *c);
+/* The whole one-collective exchange on the engine's stream, after
+ * fk_engine_feed_shard: fk_engine_shard_pack(merge, merge + 4^k,
+ * merge + 4^k + 4 * FK_PACK_COUNTERS, world rows, slot = rank), an in-place
+ * all-reduce of the merge buffer (4^k + 4 * FK_PACK_COUNTERS +
+ * world * FK_PACK_ROW_WORDS int32) over `comm`, the rows published to host
+ * memory, one host wait, fk_shard_rows_compose, fk_engine_resolve.  FK_OK:
+ * every rank's merge buffer holds the merged table and counter limbs, and
+ * the shard is resolved (fk_engine_finish gives its own result).
+ * FK_E_SUMMARY: some shard's guess did not hold (or it was not counted in
+ * one pass); the shard is still pending, the merge buffer is scratch, and
+ * every rank gets this answer: fall back to the fk_engine_summary exchange. */
+int  fk_engine_shard_exchange(fk_engine *e, fk_comm *comm, int32_t *merge);
+
 /* Finish the stream (end-of-input rules) and fill *res.  Returns FK_OK or one
  * of FK_E_EMPTY / FK_E_UNTERMINATED_HEADER / FK_E_ROLLOVER (res is filled in
  * every case). */

@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--backend", default="gloo", choices=["gloo", "nccl"],
                     help="nccl: RCCL with a device merge buffer (one rank per GPU: world 1 on a 1-GPU box)")
     ap.add_argument("--fast", type=int, default=1, help="0: always the stitched exchange")
+    ap.add_argument("--native", type=int, default=1, help="nccl: 0 = the one-collective path through torch.distributed")
     ap.add_argument("--input", default="mixed", choices=["mixed", "fasta"],
                     help="fasta: one header + 80-column ACGT lines (every k <= 7 shard counts in one pass)")
     args = ap.parse_args()
@@ -67,7 +68,8 @@ def main():
     # path's scratch (stale rows from the first must not leak into it)
     for _ in range(2):
         eng.reset()
-        res = fkdist.count_sharded(eng, dev.data_ptr() + halo, hi - lo, halo, buf, fast=bool(args.fast))
+        res = fkdist.count_sharded(eng, dev.data_ptr() + halo, hi - lo, halo, buf, fast=bool(args.fast),
+                                   native=bool(args.native))
     out = {"rank": rank}
     if rank == 0:
         want, r, _ = oracle.count_dense(data, args.k)
@@ -86,9 +88,11 @@ def main():
             "rollover": res.rollover,
             "first_end": res.first_end,
             "path": res.path,
+            "transport": res.transport,
         })
         print(json.dumps(out), flush=True)
     eng.close()
+    fkdist.close_native_comms()
     dist.destroy_process_group()
 
 

@@ -56,17 +56,21 @@ def test_sharded_mixed_input_against_oracle(k, world, eof_in):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("k,fast,eof_in", [(6, 1, -1), (7, 1, -1), (5, 0, -1), (6, 1, 0), (11, 1, -1)])
-def test_rccl_single_rank_merge(k, fast, eof_in):
+@pytest.mark.parametrize("k,fast,eof_in,native", [(6, 1, -1, 1), (7, 1, -1, 1), (6, 1, -1, 0), (5, 0, -1, 1),
+                                                  (6, 1, 0, 1), (11, 1, -1, 1)])
+def test_rccl_single_rank_merge(k, fast, eof_in, native):
     """The RCCL code path on a one-GPU box (world 1, backend nccl): the pack
     into the device merge buffer, the engine-stream -> collective ordering,
     the all-reduce and the pinned rows; a 0xFF (eof_in 0) or k >= 8 takes
     the stitched exchange over RCCL instead"""
-    out = _torchrun(1, 29800 + 3 * k + fast + eof_in, os.path.join(REPO, "tests", "dist_worker.py"),
+    out = _torchrun(1, 29800 + 3 * k + fast + eof_in + 5 * native, os.path.join(REPO, "tests", "dist_worker.py"),
                     ["--k", str(k), "--backend", "nccl", "--fast", str(fast), "--eof-in", str(eof_in),
-                     "--input", "fasta"])
+                     "--input", "fasta", "--native", str(native)])
     assert out["table_equal"]
     for key in ("windows", "valid_bases", "base_count", "depth1", "unknown_chars", "scanned_bytes",
                 "hit_eof_byte", "unterminated_header", "distinct"):
         assert out[key][0] == out[key][1], (key, out[key])
     assert out["path"] == ("fast" if fast and k <= 7 and eof_in < 0 else "stitched")
+    if out["path"] == "fast":
+        # the library's own RCCL communicator on the engine's stream
+        assert out["transport"] == ("rccl-native" if native else "torch")
