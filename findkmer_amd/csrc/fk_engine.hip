@@ -1172,10 +1172,37 @@ __device__ __forceinline__ TF tf_wave_scan(TF a) {
     return a;
 }
 
+/* Wave-wide reductions of 64-bit values through DPP moves (quad_perm
+ * [1,0,3,2], [2,3,0,1], row_ror:4, row_ror:8, row_bcast:15, row_bcast:31):
+ * lane 63 ends with the result, read back as a wave-uniform value.  A
+ * butterfly of __shfl_xor is 12 dependent ds_bpermute round trips per 64-bit
+ * value (k_tail reduced 11 of them in ~3.4 us).  Every lane must be active. */
+template <int CTRL>
+__device__ __forceinline__ uint64_t dpp_mov64(uint64_t v) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)v, CTRL, 0xf, 0xf, false);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)(v >> 32), CTRL, 0xf, 0xf, false);
+    return ((uint64_t)hi << 32) | lo;
+}
+template <class Op>
+__device__ __forceinline__ uint64_t wred64(uint64_t v, Op op) {
+    v = op(v, dpp_mov64<0xb1>(v));
+    v = op(v, dpp_mov64<0x4e>(v));
+    v = op(v, dpp_mov64<0x124>(v));
+    v = op(v, dpp_mov64<0x128>(v));
+    v = op(v, dpp_mov64<0x142>(v));
+    v = op(v, dpp_mov64<0x143>(v));
+    return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), 63) << 32) |
+           (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, 63);
+}
+struct OpAdd64 { __device__ uint64_t operator()(uint64_t a, uint64_t b) const { return a + b; } };
+struct OpMin64 { __device__ uint64_t operator()(uint64_t a, uint64_t b) const { return a < b ? a : b; } };
+struct OpOr64 { __device__ uint64_t operator()(uint64_t a, uint64_t b) const { return a | b; } };
+struct OpMaxS64 {
+    __device__ uint64_t operator()(uint64_t a, uint64_t b) const { return (int64_t)a > (int64_t)b ? a : b; }
+};
+
 __device__ __forceinline__ unsigned long long wsum64(unsigned long long v) {
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
-    return v;
+    return (unsigned long long)wred64((uint64_t)v, OpAdd64{});
 }
 
 /* Copy the result block to pinned host memory, sequence number last (the
@@ -2372,13 +2399,7 @@ struct TailPart {
 };
 
 __device__ __forceinline__ unsigned long long wmax64s(long long v) {
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) {
-        const long long o = (long long)(((uint64_t)__shfl_xor((uint32_t)((uint64_t)v >> 32), d, 64) << 32) |
-                                        (uint32_t)__shfl_xor((uint32_t)v, d, 64));
-        v = max(v, o);
-    }
-    return (unsigned long long)v;
+    return (unsigned long long)wred64((uint64_t)v, OpMaxS64{});
 }
 
 /* Item i of k_tail's chain: a k_count block's BlockSum (i < G), else the
@@ -2407,6 +2428,17 @@ __device__ __forceinline__ BlockSum tail_item(const BlockSum *bsum, const RangeR
     return b;
 }
 
+#define TAIL_KEEP 2
+/* k_tail: bin i of the table, and zeros where the sub-tables held counts
+   (streaming stores: no dirty L2 lines for a system fence to write back) */
+__device__ __forceinline__ void tail_store(uint32_t *table, uint32_t *subs, uint32_t nbins, uint32_t i, uint32_t v,
+                                           uint32_t m) {
+#pragma unroll
+    for (int j = 0; j < FK_SUBTABLES; j++)
+        if (m & (1u << j)) __builtin_nontemporal_store(0u, &subs[(size_t)j * nbins + i]);
+    __builtin_nontemporal_store(v, &table[i]);
+}
+
 __global__ void __launch_bounds__(TAIL_THREADS)
 k_tail(const OnePassCfg *opc, uint32_t flags, uint32_t seq, uint32_t *table, int k, uint32_t *subs,
        unsigned long long *facc, DevRes *res, const XState *d_init, uint32_t G0, uint64_t seg_len,
@@ -2419,11 +2451,9 @@ k_tail(const OnePassCfg *opc, uint32_t flags, uint32_t seq, uint32_t *table, int
     const BlockSum *bsum = reinterpret_cast<const BlockSum *>(opc->bsum);
     /* the chain: G0 block summaries, then the dynamic ranges */
     const uint32_t G = G0 + ndyn;
-    /* k_count is done: reset its dynamic-range pools for the next launch */
-    if (jb == 0)
-        for (uint32_t q = t; q < FK_MAX_POOLS; q += blockDim.x) done[FK_HEADS_OFF + q * FK_HEAD_STRIDE] = 0;
 #if FK_EXP == 20
     if (t == 0) atomicMin(&g_tp[0], (unsigned long long)__builtin_amdgcn_s_memrealtime());
+    TP(8);
 #endif
     /* every load of the slice phase first (one round trip): this block's
        BlockSums [b0, b1) and their predecessors' exits, one per thread, and
@@ -2448,25 +2478,37 @@ k_tail(const OnePassCfg *opc, uint32_t flags, uint32_t seq, uint32_t *table, int
     }
     const int fs = 2 * (k - 1);
     unsigned long long v10[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    /* The stores (the table bins, zeros into the sub-tables) wait until this
+       block has reported its partial record: a wave's returning atomics come
+       back in order behind its earlier stores, so storing first made every
+       block's report wait for its stores to complete (~5 us).  A thread
+       keeps up to TAIL_KEEP bins (k <= 7: at most 2 with 16 blocks). */
+    uint32_t keep_v[TAIL_KEEP], keep_m[TAIL_KEEP], nkeep = 0;
     for (uint32_t i = lo + t; i < hi; i += blockDim.x) {
         uint32_t a[FK_SUBTABLES];
 #pragma unroll
         for (int j = 0; j < FK_SUBTABLES; j++) a[j] = subs[(size_t)j * nbins + i];
         uint32_t v = fresh ? 0u : table[i];
+        uint32_t m = 0;
 #pragma unroll
         for (int j = 0; j < FK_SUBTABLES; j++) {
             v += a[j];
-            /* streaming stores: no dirty L2 lines for the publish's system
-               fence to write back */
-            if (a[j]) __builtin_nontemporal_store(0u, &subs[(size_t)j * nbins + i]);
+            m |= a[j] ? 1u << j : 0u;
         }
-        __builtin_nontemporal_store(v, &table[i]);
+        if (nkeep < TAIL_KEEP) {
+            keep_v[nkeep] = v;
+            keep_m[nkeep] = m;
+            nkeep++;
+        } else {
+            tail_store(table, subs, nbins, i, v, m);
+        }
         v10[0] += v != 0;
         v10[1] += v;
         const uint32_t ld = i & 3u, fd = k == 1 ? ld : (i >> fs) & 3u;
         v10[2] += ld == 0 ? v : 0; v10[3] += ld == 1 ? v : 0; v10[4] += ld == 2 ? v : 0; v10[5] += ld == 3 ? v : 0;
         v10[6] += fd == 0 ? v : 0; v10[7] += fd == 1 ? v : 0; v10[8] += fd == 2 ? v : 0; v10[9] += fd == 3 ? v : 0;
     }
+    TP(5);
     /* BlockSum i: its first guess against block i-1's last exit (the local
        check of block_summary, across blocks), flags, 0xFF candidate */
     uint32_t need = 0;
@@ -2483,6 +2525,7 @@ k_tail(const OnePassCfg *opc, uint32_t flags, uint32_t seq, uint32_t *table, int
     const long long jw = (long long)wmax64s(jmax);
     if (lane == 0) sh[w][10] = (unsigned long long)jw;
     __syncthreads();
+    TP(6);
     long long js = -1;
     for (uint32_t q = 0; q < blockDim.x / 64; q++) js = max(js, (long long)sh[q][10]);
     uint64_t nv_after = hb && (long long)bi > js ? bs.nv : 0;
@@ -2490,13 +2533,9 @@ k_tail(const OnePassCfg *opc, uint32_t flags, uint32_t seq, uint32_t *table, int
 #pragma unroll
     for (int q = 0; q < 10; q++) v10[q] = wsum64(v10[q]);
     nv_after = wsum64(nv_after);
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) {
-        need |= __shfl_xor(need, d, 64);
-        const uint64_t o = ((uint64_t)__shfl_xor((uint32_t)(eof >> 32), d, 64) << 32) |
-                           (uint32_t)__shfl_xor((uint32_t)eof, d, 64);
-        eof = min(eof, o);
-    }
+    need = (uint32_t)wred64(need, OpOr64{});
+    eof = wred64(eof, OpMin64{});
+    TP(9);
     __syncthreads();
     if (lane == 0) {
 #pragma unroll
@@ -2525,13 +2564,21 @@ k_tail(const OnePassCfg *opc, uint32_t flags, uint32_t seq, uint32_t *table, int
             if (t == 14) sink = xput(&P.eof, (uint64_t)a);
             if (t == 15) sink = xput(&P.j, (int32_t)js) | xput(&P.Rj, (uint64_t)(js >= 0 ? sh[0][11] : 0));
         }
+        TP(10);
         keep(sink);
         TP(1);
         /* 2. the last block to finish combines */
         if (t == 0) bc[0] = atomicAdd(done, 1u) == B - 1;
     }
     __syncthreads();
-    if (!bc[0]) return;
+    /* k_count is done: block 0 resets its dynamic-range pools for the next
+       launch (after its report, like the bin stores) */
+    if (jb == 0)
+        for (uint32_t q = t; q < FK_MAX_POOLS; q += blockDim.x) done[FK_HEADS_OFF + q * FK_HEAD_STRIDE] = 0;
+    if (!bc[0]) {
+        for (uint32_t q = 0; q < nkeep; q++) tail_store(table, subs, nbins, lo + t + q * blockDim.x, keep_v[q], keep_m[q]);
+        return;
+    }
     TP(2);
     if (t < 64) {
         if (t == 0) *done = 0;
@@ -2565,13 +2612,8 @@ k_tail(const OnePassCfg *opc, uint32_t flags, uint32_t seq, uint32_t *table, int
         const unsigned long long ta = lane < ACC_N && !fresh ? opc->acc_total[lane] : 0ull;
 #pragma unroll
         for (int q = 0; q < 10; q++) st[q] = wsum64(st[q]);
-#pragma unroll
-        for (int d = 32; d >= 1; d >>= 1) {
-            nd |= __shfl_xor(nd, d, 64);
-            const uint64_t o = ((uint64_t)__shfl_xor((uint32_t)(ef >> 32), d, 64) << 32) |
-                               (uint32_t)__shfl_xor((uint32_t)ef, d, 64);
-            ef = min(ef, o);
-        }
+        nd = (uint32_t)wred64(nd, OpOr64{});
+        ef = wred64(ef, OpMin64{});
         /* exit run length: the last slice with an absorbing block, its R,
            plus the bases after it */
         const uint64_t hasj = __ballot(have && pj >= 0);
@@ -2623,6 +2665,7 @@ k_tail(const OnePassCfg *opc, uint32_t flags, uint32_t seq, uint32_t *table, int
         publish_res_wave(res, opc->host_res, seq);
     }
     TP(4);
+    for (uint32_t q = 0; q < nkeep; q++) tail_store(table, subs, nbins, lo + t + q * blockDim.x, keep_v[q], keep_m[q]);
 }
 
 /* Sum the per-block partials of k_table_stats into res->tstat and publish

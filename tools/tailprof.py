@@ -18,7 +18,7 @@ buf = torch.empty(n + 64, dtype=torch.uint8, device="cuda")
 fk.synth_device(buf.data_ptr(), n, n, 1, 0)
 torch.cuda.synchronize()
 out = (ctypes.c_ulonglong * 16)()
-names = ["entry", "sliced", "last_go", "results", "published"]
+names = ["entry", "sliced", "last_go", "results", "published", "loaded", "synced", "", "entry_max", "shuffled", "xput_issued"]
 with fk.Engine(k) as e:
     for step in range(8):
         lib.fk_debug_tailprof(None)
@@ -27,4 +27,4 @@ with fk.Engine(k) as e:
         e.finish()
         lib.fk_debug_tailprof(out)
         t0 = out[0]
-        print(f"k={k} step {step}: " + " ".join(f"{names[i]}={(out[i] - t0) / 100.0:.1f}" for i in (1, 2, 3, 4)), flush=True)
+        print(f"k={k} step {step}: " + " ".join(f"{names[i]}={(out[i] - t0) / 100.0:.1f}" for i in (8, 5, 6, 9, 10, 1, 2, 3, 4)), flush=True)
