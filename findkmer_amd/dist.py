@@ -252,25 +252,42 @@ _comms = {}
 def native_comm(group=None):
     """The library's own RCCL communicator (findkmer_amd.Comm) over the
     ranks of `group` (backend nccl), made on first use: group rank 0 creates
-    the id, one broadcast hands it over, every rank joins."""
+    the id, one broadcast hands it over, every rank joins.  None when RCCL
+    could not be set up on some rank (every rank then learns it from one
+    more all-reduce and uses the torch.distributed path instead)."""
     key = id(group) if group is not None else 0
-    c = _comms.get(key)
-    if c is None:
-        rank = dist.get_rank(group)
-        world = dist.get_world_size(group)
-        t = torch.zeros(128, dtype=torch.uint8, device="cuda")
-        if rank == 0:
-            t.copy_(torch.frombuffer(bytearray(comm_id()), dtype=torch.uint8))
-        src = dist.get_global_rank(group, 0) if group is not None else 0
-        dist.broadcast(t, src=src, group=group)
-        c = Comm(bytes(t.cpu().tolist()), world, rank, torch.cuda.current_device())
-        _comms[key] = c
+    if key in _comms:
+        return _comms[key]
+    rank = dist.get_rank(group)
+    world = dist.get_world_size(group)
+    t = torch.zeros(129, dtype=torch.uint8, device="cuda")
+    if rank == 0:
+        try:
+            t[:128].copy_(torch.frombuffer(bytearray(comm_id()), dtype=torch.uint8))
+        except FindKmerError:
+            t[128] = 1
+    src = dist.get_global_rank(group, 0) if group is not None else 0
+    dist.broadcast(t, src=src, group=group)
+    c, failed = None, bool(t[128].item())
+    if not failed:
+        try:
+            c = Comm(bytes(t[:128].cpu().tolist()), world, rank, torch.cuda.current_device())
+        except FindKmerError:
+            failed = True
+    bad = torch.tensor([1 if failed else 0], dtype=torch.int32, device="cuda")
+    dist.all_reduce(bad, group=group)
+    if int(bad.item()):
+        if c is not None:
+            c.close()
+        c = None
+    _comms[key] = c
     return c
 
 
 def close_native_comms():
     for c in _comms.values():
-        c.close()
+        if c is not None:
+            c.close()
     _comms.clear()
 
 
@@ -344,7 +361,10 @@ def count_sharded(engine, ptr, nbytes, halo, buf, group=None, times=None, pinned
     rank when the one-collective path applies).  Returns a ShardedResult.
     `pinned` (optional): a pinned host int32 tensor of COUNTER_SLOTS entries
     for an asynchronous counter upload.  fast=False: always the stitched
-    exchange (steps 1-2).
+    exchange (steps 1-2).  native: over RCCL (backend nccl, device buffer)
+    the one-collective path runs inside the library on the engine's stream
+    (fk_engine_shard_exchange with its own communicator, native_comm)
+    instead of through torch.distributed.
 
     `engine` is a findkmer_amd.Engine (or, in the CPU tests, a model with the
     same feed_shard_device / summary / summary_full / resolve / finish /
@@ -356,8 +376,11 @@ def count_sharded(engine, ptr, nbytes, halo, buf, group=None, times=None, pinned
     t0 = time.perf_counter()
     engine.feed_shard_device(ptr, nbytes, halo)
     if fast and engine.k <= FAST_KMAX and hasattr(engine, "shard_pack"):
+        comm = None
         if native and buf.is_cuda and hasattr(engine, "shard_exchange") and dist.get_backend(group) == "nccl":
-            ok = engine.shard_exchange(native_comm(group), buf.data_ptr())
+            comm = native_comm(group)
+        if comm is not None:
+            ok = engine.shard_exchange(comm, buf.data_ptr())
             if ok:
                 t1 = time.perf_counter()
                 _, r = engine.finish(allow=(FK_OK, FK_E_ROLLOVER, FK_E_UNTERMINATED_HEADER, FK_E_EMPTY))
