@@ -945,17 +945,30 @@ __device__ __forceinline__ bool tile_mixed(const Ctx &cx, const uint32_t w[8], u
     return true;
 }
 
-/* wave-wide sum via butterfly */
-__device__ __forceinline__ uint32_t wsum32(uint32_t v) {
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
-    return v;
+/* Wave-wide reductions through DPP moves (quad_perm [1,0,3,2], [2,3,0,1],
+ * row_ror:4, row_ror:8, row_bcast:15, row_bcast:31): lane 63 ends with the
+ * result, read back as a wave-uniform value.  A butterfly of __shfl_xor is a
+ * chain of 6 dependent ds_bpermute round trips per 32-bit value; a wave's
+ * counter flush reduces 13 of them.  Every lane must be active (the callers
+ * are wave-uniform). */
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp_mov32(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xf, 0xf, false);
 }
-__device__ __forceinline__ uint32_t wmin32(uint32_t v) {
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) v = min(v, (uint32_t)__shfl_xor(v, d, 64));
-    return v;
+template <class Op>
+__device__ __forceinline__ uint32_t wred32(uint32_t v, Op op) {
+    v = op(v, dpp_mov32<0xb1>(v));
+    v = op(v, dpp_mov32<0x4e>(v));
+    v = op(v, dpp_mov32<0x124>(v));
+    v = op(v, dpp_mov32<0x128>(v));
+    v = op(v, dpp_mov32<0x142>(v));
+    v = op(v, dpp_mov32<0x143>(v));
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
 }
+struct OpAdd32 { __device__ uint32_t operator()(uint32_t a, uint32_t b) const { return a + b; } };
+struct OpMin32 { __device__ uint32_t operator()(uint32_t a, uint32_t b) const { return a < b ? a : b; } };
+__device__ __forceinline__ uint32_t wsum32(uint32_t v) { return wred32(v, OpAdd32{}); }
+__device__ __forceinline__ uint32_t wmin32(uint32_t v) { return wred32(v, OpMin32{}); }
 
 __device__ __forceinline__ void acc_add(unsigned long long *a, uint64_t v, uint32_t weight) {
     if (v) atomicAdd(a, (unsigned long long)(weight == 1u ? v : (0ull - v)));
