@@ -1836,23 +1836,34 @@ k_redo(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint
  * k_bucket_count: one block per slice (and group of rows) counts its runs in
  *   an LDS slice of 2^sh bins and adds the slice into the table.
  */
-/* waves per k_part block.  4-wave blocks (four per CU) make k_part itself
-   ~4% faster, but halve the batch, so k_bucket_count reads twice as many,
-   shorter runs: the k=11 step is 5% slower and k=12 30% slower (measured,
-   tools/exp_part.sh) */
-#ifndef PART_WAVES
-#define PART_WAVES 8u
-#endif
-#define PART_BLOCK (PART_WAVES * 64u)
+/* Waves per k_part block (template parameter W, 8 or 16; chosen per k by
+   part_waves()).  Larger blocks make k_part itself slower (more waves per
+   barrier) but its batches larger, so k_bucket_count reads longer runs:
+   16-wave blocks (one per CU, 136 KiB of LDS) take the k=11 FASTA step from
+   1.12 to 1.08 ms (k_part 616 -> 660 us) and k=12 from 1.85 to 1.73 ms, but
+   k=8 (80 slices: long runs already) from 0.98 to 1.02 ms; 4-wave blocks
+   made k=11 5 % slower and k=12 30 % slower. */
+#define PART_BLOCK_W(W) ((W) * 64u)
 /* tiles per wave per batch: 2 single-window tiles or 4 pair tiles fill the
    same LDS batch (a pair tile hands over half as many entries) */
 #define PART_TILES(PAIRS) ((PAIRS) ? 4u : 2u)
-#define PART_MAX_BATCH (2u * PART_WAVES * FK_TILE_BYTES)   /* entries per batch */
+#define PART_MAX_BATCH_W(W) (2u * (W) * FK_TILE_BYTES)   /* entries per batch */
+static_assert(PART_MAX_BATCH_W(16u) <= 65536u, "run index words hold 16-bit starts and counts - 1");
 #define PART_MAX_SLICES 1024u   /* k = 11 pairs: 2^24 / 2^15 pair slices + 2^22 / 2^15 single slices */
 
+/* A run index word: (start << 16) | (count - 1) for a run of count >= 1
+   codes (a batch holds up to 2^16 of them, all possibly in one slice), and
+   PART_NO_RUN for an empty one (start + count <= 2^16 never encodes to it) */
+#define PART_NO_RUN 0xFFFFFFFFu
+__device__ __forceinline__ uint32_t run_word(uint32_t start, uint32_t count) {
+    return count ? (start << 16) | (count - 1u) : PART_NO_RUN;
+}
+__device__ __forceinline__ uint32_t run_count(uint32_t e) { return e == PART_NO_RUN ? 0u : (e & 0xFFFFu) + 1u; }
+
 struct PartGeo {
-    uint16_t *codes;       /* per row (batch): PART_MAX_BATCH entries at row * PART_MAX_BATCH */
-    uint32_t *idx;         /* [slice][row]: (start << 16) | count */
+    uint16_t *codes;       /* per row (batch): `batch` entries at row * batch */
+    uint32_t batch;        /* PART_MAX_BATCH_W of k_part's block size */
+    uint32_t *idx;         /* [slice][row]: run_word(start, count) */
     uint32_t rounds;       /* rows per block */
     uint32_t rows;         /* rows in all: grid * rounds */
     uint32_t nslices;
@@ -1934,7 +1945,7 @@ __device__ __forceinline__ void part_entries(const Emit &em, uint32_t mk, uint32
 /* The block-wide batch of one round: windows of the waves whose tile was
  * fast (have), counting-sorted by slice.  Every thread of the block calls
  * this the same number of times (it contains barriers). */
-template <bool PAIRS, bool MIX>
+template <bool PAIRS, bool MIX, uint32_t W>
 __device__ __forceinline__ bool part_batch(const Ctx &cx, const PartGeo &pg, const Emit *es, const bool *haves,
                                            bool more, uint32_t row, uint32_t *hist,
                                            uint32_t *cur, uint32_t *total, uint16_t *ent) {
@@ -1968,7 +1979,7 @@ __device__ __forceinline__ bool part_batch(const Ctx &cx, const PartGeo &pg, con
             if (b < pg.nslices) {
                 const uint32_t c = hist[b];
                 cur[b] = run;
-                pg.idx[(size_t)b * pg.stride + row] = (run << 16) | c;
+                pg.idx[(size_t)b * pg.stride + row] = run_word(run, c);
                 hist[b] = 0;
                 run += c;
             }
@@ -1991,13 +2002,13 @@ __device__ __forceinline__ bool part_batch(const Ctx &cx, const PartGeo &pg, con
     }
     __syncthreads();
     /* 4: the sorted batch into its row's fixed slot (a batch holds at most
-       PART_MAX_BATCH entries: a run's position needs no per-row base), as
-       16-B pieces; the up to 7 codes past the batch's end are padding no
+       PART_MAX_BATCH_W(W) entries: a run's position needs no per-row base),
+       as 16-B pieces; the up to 7 codes past the batch's end are padding no
        run covers */
     const uint32_t n8 = (*total + 7u) >> 3;
-    uint4 *dst = reinterpret_cast<uint4 *>(pg.codes + (size_t)row * PART_MAX_BATCH);
+    uint4 *dst = reinterpret_cast<uint4 *>(pg.codes + (size_t)row * PART_MAX_BATCH_W(W));
     const uint4 *src = reinterpret_cast<const uint4 *>(ent);
-    for (uint32_t i = t; i < n8; i += PART_BLOCK) dst[i] = src[i];
+    for (uint32_t i = t; i < n8; i += PART_BLOCK_W(W)) dst[i] = src[i];
     return any_more;
 }
 
@@ -2007,13 +2018,13 @@ __device__ __forceinline__ bool part_batch(const Ctx &cx, const PartGeo &pg, con
  * the rest of it, each tile fast, mixed (the masked entries of tile_mixed)
  * or general.  Two kernels: tile_mixed's registers stay out of the main
  * pass.  k_part<RES> returns at once unless some range stopped. */
-template <bool PAIRS, bool RES>
-__global__ void __launch_bounds__(PART_BLOCK, 4) /* 4 waves per SIMD (<= 128 VGPRs): two blocks per CU */
+template <bool PAIRS, bool RES, uint32_t W>
+__global__ void __launch_bounds__(PART_BLOCK_W(W), 4) /* 4 waves per SIMD (<= 128 VGPRs): 16 waves per CU */
 k_part(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint32_t *table,
        uint32_t *shortcnt, unsigned long long *acc, DevRes *res, RangeRec *rr, uint64_t nchunks, uint64_t cpw,
        const XState *d_init, int has_init, PartGeo pg, ResumeRec *resume) {
     __shared__ uint32_t hist[PART_MAX_SLICES], cur[PART_MAX_SLICES], total;
-    __shared__ __attribute__((aligned(16))) uint16_t ent[PART_MAX_BATCH];
+    __shared__ __attribute__((aligned(16))) uint16_t ent[PART_MAX_BATCH_W(W)];
     if (RES && *(volatile uint32_t *)pg.flag == 0) return;   /* uniform: no range stopped */
     /* open the feed's result block (the kernels after this one accumulate
        into it) */
@@ -2022,10 +2033,10 @@ k_part(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint
         if (threadIdx.x == 10) res->eof_cand = ~0ull;
         if (threadIdx.x == 11) res->redo_n = 0;
     }
-    for (uint32_t i = threadIdx.x; i < pg.nslices; i += PART_BLOCK) hist[i] = 0;
+    for (uint32_t i = threadIdx.x; i < pg.nslices; i += PART_BLOCK_W(W)) hist[i] = 0;
     Ctx cx{buf, len, lo, table, nullptr, shortcnt, acc, res, maskk, 0, k, nullptr};
     const int lane = threadIdx.x & 63;
-    const uint64_t wave = blockIdx.x * PART_WAVES + wave_in_block();
+    const uint64_t wave = blockIdx.x * W + wave_in_block();
     const uint64_t c0 = wave * cpw, c1 = min(c0 + cpw, nchunks);
     const bool has = c0 < c1 && (!RES || rr[wave].resume);
     RangeRec hdr_r;
@@ -2132,7 +2143,7 @@ k_part(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint
                 have_stash[i_] = have;                                               \
             }                                                                        \
             if (ph_ == NT - 1) {                                                     \
-                const bool more_ = part_batch<PAIRS, RES>(cx, pg, stash, have_stash, !done, \
+                const bool more_ = part_batch<PAIRS, RES, W>(cx, pg, stash, have_stash, !done, \
                                                           row0 + round / NT, hist, cur, &total, ent); \
                 if (!more_ || round / NT + 1 >= pg.rounds) { round++; break; }       \
             }                                                                        \
@@ -2149,7 +2160,7 @@ k_part(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint
     /* rows the block did not reach are empty */
     for (uint32_t r = (round + NT - 1) / NT; r < pg.rounds; r++) {
         const uint32_t row = row0 + r;
-        for (uint32_t b = threadIdx.x; b < pg.nslices; b += PART_BLOCK) pg.idx[(size_t)b * pg.stride + row] = 0;
+        for (uint32_t b = threadIdx.x; b < pg.nslices; b += PART_BLOCK_W(W)) pg.idx[(size_t)b * pg.stride + row] = PART_NO_RUN;
     }
     if (!has) {
         flush_counters(cx, cnt, 1u);
@@ -2223,20 +2234,20 @@ k_bucket_count(PartGeo pg, uint32_t groups, uint32_t *table) {
     uint32_t en[4];   /* the next iteration's index words, loaded with this one's codes */
     const uint32_t r00 = g * quads + threadIdx.x / 4;
 #pragma unroll
-    for (int j = 0; j < 4; j++) en[j] = r00 + j * step < nrows ? ix[r00 + j * step] : 0u;
+    for (int j = 0; j < 4; j++) en[j] = r00 + j * step < nrows ? ix[r00 + j * step] : PART_NO_RUN;
     for (uint32_t r = r00; r < nrows; r += 4 * step) {
         uint32_t e[4];
 #pragma unroll
         for (int j = 0; j < 4; j++) e[j] = en[j];
         const uint32_t rn = r + 4 * step;
 #pragma unroll
-        for (int j = 0; j < 4; j++) en[j] = rn + j * step < nrows ? ix[rn + j * step] : 0u;
+        for (int j = 0; j < 4; j++) en[j] = rn + j * step < nrows ? ix[rn + j * step] : PART_NO_RUN;
         uint64_t s0[4], s1[4];
         uint4 v[4][2];
 #pragma unroll
         for (int j = 0; j < 4; j++) {
-            s0[j] = (uint64_t)(r + j * step) * PART_MAX_BATCH + (e[j] >> 16);
-            s1[j] = s0[j] + (e[j] & 0xFFFFu);
+            s0[j] = (uint64_t)(r + j * step) * pg.batch + (e[j] == PART_NO_RUN ? 0u : e[j] >> 16);
+            s1[j] = s0[j] + run_count(e[j]);
             const uint64_t q0 = (s0[j] >> 3) + sub, q1 = (s1[j] + 7) >> 3;
 #pragma unroll
             for (int u = 0; u < 2; u++) v[j][u] = q0 + 4 * u < q1 ? g4[q0 + 4 * u] : make_uint4(0, 0, 0, 0);
@@ -3032,6 +3043,7 @@ struct fk_engine {
     uint32_t ranges_per_wave = 1;             /* k <= 7: ranges per k_count wave slot (FK_RANGES_PER_WAVE) */
     bool no_mixed = false;                    /* FK_NO_MIXED=1: no mixed tiles (general byte walk) */
     uint32_t part_general = 1;                /* k_part: general tiles per range (FK_PART_GENERAL) */
+    uint32_t part_waves = 0;                  /* k_part: waves per block (FK_PART_WAVES; 0 = by k) */
     uint32_t static_pct = 100;                /* k <= 7: % of a large segment in static ranges (FK_STATIC_PCT;
                                                  100 = no dynamic ranges: on a plain stream the waves that
                                                  finish early hand their bandwidth to the others, so
@@ -3247,6 +3259,10 @@ extern "C" int fk_engine_create(int k, const fk_opts *opts, fk_engine **out) {
        isolated comment line) and leaves denser ones to k_resume's mixed tiles */
     if (!e->no_mixed) e->general_tiles = 2;
     if (const char *gt = getenv("FK_GENERAL_TILES")) e->general_tiles = (uint32_t)strtoul(gt, nullptr, 10);
+    if (const char *pw = getenv("FK_PART_WAVES")) {
+        const uint32_t v = (uint32_t)strtoul(pw, nullptr, 10);
+        e->part_waves = v == 8u || v == 16u ? v : 0u;
+    }
     if (const char *pg = getenv("FK_PART_GENERAL")) e->part_general = (uint32_t)strtoul(pg, nullptr, 10);
     if (const char *ne = getenv("FK_NO_EVENTS")) e->timing = ne[0] != '1';
     if (const char *no = getenv("FK_NO_ONEPASS")) e->onepass = no[0] != '1';
@@ -3594,7 +3610,11 @@ static int launch_part(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t l
         pg.singles = e->d_pairs + e->nbins * 4;
     }
     pg.rounds = (uint32_t)((g.cpw * FK_CHUNK_TILES + 2) / PART_TILES(pairs) + 2);   /* rows (batches) per block */
-    const unsigned pgrid = (unsigned)((g.nranges + PART_WAVES - 1) / PART_WAVES);   /* same ranges, smaller blocks */
+    /* block size: 16 waves (larger batches, longer runs for k_bucket_count)
+       for the many-slice tables, else 8 (FK_PART_WAVES=8|16 forces one) */
+    const uint32_t W = e->part_waves ? e->part_waves : (k >= 11 ? 16u : 8u);
+    pg.batch = PART_MAX_BATCH_W(W);
+    const unsigned pgrid = (unsigned)((g.nranges + W - 1) / W);   /* the same ranges as k_count's waves */
     pg.rows = pgrid * pg.rounds;
     /* mixed tiles: ranges past their general tiles go to k_part<RES>, whose
        rows (region 2, as many as k_part's) follow k_part's */
@@ -3607,7 +3627,7 @@ static int launch_part(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t l
     if (!e->d_pflag && hipMalloc((void **)&e->d_pflag, 64) != hipSuccess) return FK_E_OOM;
     pg.flag = e->d_pflag;
     HIPCHK(hipMemsetAsync(e->d_pflag, 0, sizeof(uint32_t), e->stream));
-    const uint64_t ncodes = (uint64_t)pg.stride * PART_MAX_BATCH, nidx = (uint64_t)pg.nslices * pg.stride;
+    const uint64_t ncodes = (uint64_t)pg.stride * pg.batch, nidx = (uint64_t)pg.nslices * pg.stride;
     if (ncodes > e->codes_cap) {
         hipFree(e->d_codes);
         e->d_codes = nullptr;
@@ -3622,14 +3642,18 @@ static int launch_part(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t l
     }
     pg.codes = e->d_codes;
     pg.idx = e->d_pidx;
-    hipExtLaunchKernelGGL(pairs ? k_part<true, false> : k_part<false, false>, dim3(pgrid), dim3(PART_BLOCK), 0,
-                          e->stream, tev(e, 0), tev(e, 1), 0, buf, len, lo, e->k, e->maskk, e->d_table, e->d_short,
-                          e->d_facc, e->d_res, e->d_rr, g.nchunks, g.cpw, e->d_state, has_init, pg, e->d_resume);
+    auto kmain = W == 16u ? (pairs ? k_part<true, false, 16u> : k_part<false, false, 16u>)
+                          : (pairs ? k_part<true, false, 8u> : k_part<false, false, 8u>);
+    hipExtLaunchKernelGGL(kmain, dim3(pgrid), dim3(PART_BLOCK_W(W)), 0, e->stream, tev(e, 0), tev(e, 1), 0, buf, len,
+                          lo, e->k, e->maskk, e->d_table, e->d_short, e->d_facc, e->d_res, e->d_rr, g.nchunks, g.cpw,
+                          e->d_state, has_init, pg, e->d_resume);
     HIPCHK(hipGetLastError());
     if (mixed) {
-        hipLaunchKernelGGL((pairs ? k_part<true, true> : k_part<false, true>), dim3(pgrid), dim3(PART_BLOCK), 0,
-                           e->stream, buf, len, lo, e->k, e->maskk, e->d_table, e->d_short, e->d_facc, e->d_res,
-                           e->d_rr, g.nchunks, g.cpw, e->d_state, has_init, pg, e->d_resume);
+        auto kres = W == 16u ? (pairs ? k_part<true, true, 16u> : k_part<false, true, 16u>)
+                             : (pairs ? k_part<true, true, 8u> : k_part<false, true, 8u>);
+        hipLaunchKernelGGL(kres, dim3(pgrid), dim3(PART_BLOCK_W(W)), 0, e->stream, buf, len, lo, e->k, e->maskk,
+                           e->d_table, e->d_short, e->d_facc, e->d_res, e->d_rr, g.nchunks, g.cpw, e->d_state,
+                           has_init, pg, e->d_resume);
         HIPCHK(hipGetLastError());
     } else {
         pg.flag = nullptr;

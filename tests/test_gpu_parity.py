@@ -519,7 +519,8 @@ def test_cli_device_ingest_large(tmp_path):
 @pytest.mark.parametrize("kind", ["polyA", "period7", "fasta_polyA"])
 def test_partition_skewed(k, kind):
     """8 <= k <= 12 on inputs whose windows all fall in one or a few table
-    slices: k_part batches of one 16 K-32 K-entry run, k_bucket_count's
+    slices: k_part batches of one run of up to 64 K entries (the 16-bit
+    count field holds count - 1), k_bucket_count's
     long-run loop, pair and single slices (FASTA halves with a newline)"""
     n = 24 << 20
     if kind == "polyA":
