@@ -2204,6 +2204,16 @@ k_part(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint
     }
 }
 
+/* k_bucket_count's first loads per quad: BUCKET_ROWS rows at once, each
+   with BUCKET_U 16-B pieces per lane (64 B per quad each).  2 x 4 (256 B
+   of a ~200-B run, k=11 with 16-wave k_part blocks) beat 4 x 2 by ~1 %
+   (k=11 step 1.082 -> 1.070 ms); 3 x 3, 3 x 4 and 1 x 8 fell in between. */
+#ifndef BUCKET_U
+#define BUCKET_U 4
+#endif
+#ifndef BUCKET_ROWS
+#define BUCKET_ROWS 2
+#endif
 __global__ void __launch_bounds__(1024)
 k_bucket_count(PartGeo pg, uint32_t groups, uint32_t *table) {
     extern __shared__ uint32_t slice[];
@@ -2216,9 +2226,9 @@ k_bucket_count(PartGeo pg, uint32_t groups, uint32_t *table) {
     const uint32_t nrows = pg.flag && *pg.flag ? 2u * pg.rows : pg.rows;
     const uint4 *g4 = reinterpret_cast<const uint4 *>(pg.codes);
     /* four lanes share a run and read it as contiguous 64-byte pieces (one
-       request per quad instead of one per lane).  A quad takes four rows at
-       once: their first 128 bytes of codes and the next four rows' index
-       words are all in flight together (a run is ~50-250 codes, so one
+       request per quad instead of one per lane).  A quad takes BUCKET_ROWS
+       rows at once: their first 64 * BUCKET_U bytes of codes and the next
+       rows' index words are all in flight together (a run is ~50-250 codes, so one
        dependent chain per run would leave the CU waiting on latency; rows
        sit at fixed offsets, so a run's position needs no further load) */
     const uint32_t sub = threadIdx.x & 3u;
@@ -2231,35 +2241,35 @@ k_bucket_count(PartGeo pg, uint32_t groups, uint32_t *table) {
             if (at >= s0 && at < s1) atomicAdd(&slice[(w4[h >> 1] >> (16 * (h & 1))) & 0xFFFFu], 1u);
         }
     };
-    uint32_t en[4];   /* the next iteration's index words, loaded with this one's codes */
+    uint32_t en[BUCKET_ROWS];   /* the next iteration's index words, loaded with this one's codes */
     const uint32_t r00 = g * quads + threadIdx.x / 4;
 #pragma unroll
-    for (int j = 0; j < 4; j++) en[j] = r00 + j * step < nrows ? ix[r00 + j * step] : PART_NO_RUN;
-    for (uint32_t r = r00; r < nrows; r += 4 * step) {
-        uint32_t e[4];
+    for (int j = 0; j < BUCKET_ROWS; j++) en[j] = r00 + j * step < nrows ? ix[r00 + j * step] : PART_NO_RUN;
+    for (uint32_t r = r00; r < nrows; r += BUCKET_ROWS * step) {
+        uint32_t e[BUCKET_ROWS];
 #pragma unroll
-        for (int j = 0; j < 4; j++) e[j] = en[j];
-        const uint32_t rn = r + 4 * step;
+        for (int j = 0; j < BUCKET_ROWS; j++) e[j] = en[j];
+        const uint32_t rn = r + BUCKET_ROWS * step;
 #pragma unroll
-        for (int j = 0; j < 4; j++) en[j] = rn + j * step < nrows ? ix[rn + j * step] : PART_NO_RUN;
-        uint64_t s0[4], s1[4];
-        uint4 v[4][2];
+        for (int j = 0; j < BUCKET_ROWS; j++) en[j] = rn + j * step < nrows ? ix[rn + j * step] : PART_NO_RUN;
+        uint64_t s0[BUCKET_ROWS], s1[BUCKET_ROWS];
+        uint4 v[BUCKET_ROWS][BUCKET_U];
 #pragma unroll
-        for (int j = 0; j < 4; j++) {
+        for (int j = 0; j < BUCKET_ROWS; j++) {
             s0[j] = (uint64_t)(r + j * step) * pg.batch + (e[j] == PART_NO_RUN ? 0u : e[j] >> 16);
             s1[j] = s0[j] + run_count(e[j]);
             const uint64_t q0 = (s0[j] >> 3) + sub, q1 = (s1[j] + 7) >> 3;
 #pragma unroll
-            for (int u = 0; u < 2; u++) v[j][u] = q0 + 4 * u < q1 ? g4[q0 + 4 * u] : make_uint4(0, 0, 0, 0);
+            for (int u = 0; u < BUCKET_U; u++) v[j][u] = q0 + 4 * u < q1 ? g4[q0 + 4 * u] : make_uint4(0, 0, 0, 0);
         }
 #pragma unroll
-        for (int j = 0; j < 4; j++) {
+        for (int j = 0; j < BUCKET_ROWS; j++) {
             const uint64_t q0 = (s0[j] >> 3) + sub, q1 = (s1[j] + 7) >> 3;
 #pragma unroll
-            for (int u = 0; u < 2; u++)
+            for (int u = 0; u < BUCKET_U; u++)
                 if (q0 + 4 * u < q1) add16(v[j][u], q0 + 4 * u, s0[j], s1[j]);
             /* the rest of a long run */
-            for (uint64_t q = q0 + 8; q < q1; q += 16) {
+            for (uint64_t q = q0 + 4 * BUCKET_U; q < q1; q += 16) {
                 uint4 w[4];
 #pragma unroll
                 for (int u = 0; u < 4; u++) w[u] = q + 4 * u < q1 ? g4[q + 4 * u] : make_uint4(0, 0, 0, 0);
