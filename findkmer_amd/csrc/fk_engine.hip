@@ -91,6 +91,45 @@ __device__ __forceinline__ uint32_t wave_in_block() {
 
 __device__ __forceinline__ uint32_t shup(uint32_t v, int d) { return __shfl_up(v, (unsigned)d, 64); }
 
+/* Wave-wide reductions through DPP moves (quad_perm [1,0,3,2], [2,3,0,1],
+ * row_ror:4, row_ror:8, row_bcast:15, row_bcast:31): lane 63 ends with the
+ * result, read back as a wave-uniform value.  A butterfly of __shfl_xor is a
+ * chain of 6 dependent ds_bpermute round trips per 32-bit value; a wave's
+ * counter flush reduces 13 of them.  Every lane must be active (the callers
+ * are wave-uniform). */
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp_mov32(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xf, 0xf, false);
+}
+template <class Op>
+__device__ __forceinline__ uint32_t wred32(uint32_t v, Op op) {
+    v = op(v, dpp_mov32<0xb1>(v));
+    v = op(v, dpp_mov32<0x4e>(v));
+    v = op(v, dpp_mov32<0x124>(v));
+    v = op(v, dpp_mov32<0x128>(v));
+    v = op(v, dpp_mov32<0x142>(v));
+    v = op(v, dpp_mov32<0x143>(v));
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+}
+/* inclusive wave scan (sum) through DPP: row_shr 1/2/4/8 within each row of
+   16 lanes, then row_bcast:15 and row_bcast:31 across rows (rocPRIM's
+   sequence); every lane must be active */
+__device__ __forceinline__ uint32_t wscan_incl32(uint32_t v) {
+    const uint32_t lane = threadIdx.x & 63, rl = lane & 15;
+    uint32_t t;
+    t = dpp_mov32<0x111>(v); if (rl >= 1) v += t;
+    t = dpp_mov32<0x112>(v); if (rl >= 2) v += t;
+    t = dpp_mov32<0x114>(v); if (rl >= 4) v += t;
+    t = dpp_mov32<0x118>(v); if (rl >= 8) v += t;
+    t = dpp_mov32<0x142>(v); if ((lane & 31) >= 16) v += t;
+    t = dpp_mov32<0x143>(v); if (lane >= 32) v += t;
+    return v;
+}
+struct OpAdd32 { __device__ uint32_t operator()(uint32_t a, uint32_t b) const { return a + b; } };
+struct OpMin32 { __device__ uint32_t operator()(uint32_t a, uint32_t b) const { return a < b ? a : b; } };
+__device__ __forceinline__ uint32_t wsum32(uint32_t v) { return wred32(v, OpAdd32{}); }
+__device__ __forceinline__ uint32_t wmin32(uint32_t v) { return wred32(v, OpMin32{}); }
+
 __device__ __forceinline__ uint32_t rdlane(uint32_t v, int l) {
     return (uint32_t)__builtin_amdgcn_readlane((int)v, l);
 }
@@ -945,30 +984,6 @@ __device__ __forceinline__ bool tile_mixed(const Ctx &cx, const uint32_t w[8], u
     return true;
 }
 
-/* Wave-wide reductions through DPP moves (quad_perm [1,0,3,2], [2,3,0,1],
- * row_ror:4, row_ror:8, row_bcast:15, row_bcast:31): lane 63 ends with the
- * result, read back as a wave-uniform value.  A butterfly of __shfl_xor is a
- * chain of 6 dependent ds_bpermute round trips per 32-bit value; a wave's
- * counter flush reduces 13 of them.  Every lane must be active (the callers
- * are wave-uniform). */
-template <int CTRL>
-__device__ __forceinline__ uint32_t dpp_mov32(uint32_t v) {
-    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xf, 0xf, false);
-}
-template <class Op>
-__device__ __forceinline__ uint32_t wred32(uint32_t v, Op op) {
-    v = op(v, dpp_mov32<0xb1>(v));
-    v = op(v, dpp_mov32<0x4e>(v));
-    v = op(v, dpp_mov32<0x124>(v));
-    v = op(v, dpp_mov32<0x128>(v));
-    v = op(v, dpp_mov32<0x142>(v));
-    v = op(v, dpp_mov32<0x143>(v));
-    return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
-}
-struct OpAdd32 { __device__ uint32_t operator()(uint32_t a, uint32_t b) const { return a + b; } };
-struct OpMin32 { __device__ uint32_t operator()(uint32_t a, uint32_t b) const { return a < b ? a : b; } };
-__device__ __forceinline__ uint32_t wsum32(uint32_t v) { return wred32(v, OpAdd32{}); }
-__device__ __forceinline__ uint32_t wmin32(uint32_t v) { return wred32(v, OpMin32{}); }
 
 __device__ __forceinline__ void acc_add(unsigned long long *a, uint64_t v, uint32_t weight) {
     if (v) atomicAdd(a, (unsigned long long)(weight == 1u ? v : (0ull - v)));
@@ -1967,12 +1982,7 @@ __device__ __forceinline__ bool part_batch(const Ctx &cx, const PartGeo &pg, con
             const uint32_t b = lane * per + j;
             if (b < pg.nslices) sum += hist[b];
         }
-        uint32_t inc = sum;
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const uint32_t v = shup(inc, d);
-            if (lane >= (uint32_t)d) inc += v;
-        }
+        const uint32_t inc = wscan_incl32(sum);
         uint32_t run = inc - sum;
         for (uint32_t j = 0; j < per; j++) {
             const uint32_t b = lane * per + j;
