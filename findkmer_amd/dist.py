@@ -325,12 +325,13 @@ def _fast_exchange(engine, buf, rank, world, group, times, t0):
     dst = fp.stage if fp.stage is not None else buf
     engine.shard_pack(dst.data_ptr(), dst.data_ptr() + 4 * nb, dst.data_ptr() + 4 * (nb + COUNTER_SLOTS),
                       world, rank, rank == world - 1)
+    if not fp.host_pack:
+        # the copy or the collective runs after the pack (engine stream ->
+        # torch's current stream)
+        torch.cuda.current_stream().wait_stream(fp.ext)
     if fp.stage is not None:
         # gloo rehearsal of a GPU engine: the host buffer gets the pack
         buf[:n].copy_(fp.stage[:n].cpu())
-    elif not fp.host_pack:
-        # the collective runs after the pack (engine stream -> torch's)
-        torch.cuda.current_stream().wait_stream(fp.ext)
     t1 = time.perf_counter()
     dist.all_reduce(buf[:n], op=dist.ReduceOp.SUM, group=group)
     if buf.is_cuda:
