@@ -2032,7 +2032,7 @@ template <bool PAIRS, bool RES, uint32_t W>
 __global__ void __launch_bounds__(PART_BLOCK_W(W), 4) /* 4 waves per SIMD (<= 128 VGPRs): 16 waves per CU */
 k_part(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint32_t *table,
        uint32_t *shortcnt, unsigned long long *acc, DevRes *res, RangeRec *rr, uint64_t nchunks, uint64_t cpw,
-       const XState *d_init, int has_init, PartGeo pg, ResumeRec *resume) {
+       const XState *d_init, int has_init, PartGeo pg, ResumeRec *resume, const XState *exact) {
     __shared__ uint32_t hist[PART_MAX_SLICES], cur[PART_MAX_SLICES], total;
     __shared__ __attribute__((aligned(16))) uint16_t ent[PART_MAX_BATCH_W(W)];
     if (RES && *(volatile uint32_t *)pg.flag == 0) return;   /* uniform: no range stopped */
@@ -2097,8 +2097,15 @@ k_part(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint
             f = qr->f;
         }
     } else if (has) {
-        if (c0 == 0 && has_init) st = DState{d_init->code, (uint32_t)d_init->R, d_init->hdr};
-        else st = halo_guess<H_EMIT>(cx, hw, hv);
+        if (exact) {
+            /* a recount from the exact range states (resolve_and_fetch) */
+            const XState x = exact[wave];
+            st = DState{x.code, (uint32_t)x.R, x.hdr};
+        } else if (c0 == 0 && has_init) {
+            st = DState{d_init->code, (uint32_t)d_init->R, d_init->hdr};
+        } else {
+            st = halo_guess<H_EMIT>(cx, hw, hv);
+        }
         first = st;
     }
     consume(hw);   /* waited on every path (see k_count) */
@@ -3116,6 +3123,14 @@ struct fk_engine {
     uint32_t timing_every = 1;
     bool cur_timed = true;                    /* the current feed's launches record events */
     std::vector<uint8_t> unknown_bytes;
+    /* partitioned path near the reference's int32 seqSize zone: a segment
+       whose guessed range states are mostly wrong is recounted from the exact
+       states instead of cancelled range by range (resolve_and_fetch) */
+    bool dirty = false;                       /* table / short walks changed since the last reset */
+    bool seg_clean = true;                    /* ... not before the current segment */
+    bool seg_snap = false;                    /* d_snap holds them as before the current segment */
+    uint32_t *d_snap = nullptr;
+    uint64_t snap_cap = 0;
     /* fk_engine_shard_exchange: gathered pack rows, pinned and mapped (word
        0: sequence number, rows from word 32) */
     uint32_t *h_rows = nullptr, *h_rows_dev = nullptr;
@@ -3202,6 +3217,7 @@ static size_t lds_bytes(const fk_engine *e) {
 /* Zero table, counters and the stream state (asynchronous, stream-ordered). */
 static int zero_all(fk_engine *e) {
     e->zero_pending = true;
+    e->dirty = false;
     e->state = XState{0, 0, 0, 0};
     memset(&e->last, 0, sizeof e->last);
     e->stats_valid = false;
@@ -3221,7 +3237,7 @@ extern "C" void fk_engine_destroy(fk_engine *e) {
     if (!e) return;
     hipSetDevice(e->dev);
     if (e->stream) hipStreamSynchronize(e->stream);
-    hipFree(e->d_table); hipFree(e->d_short); hipFree(e->d_sub);
+    hipFree(e->d_table); hipFree(e->d_short); hipFree(e->d_sub); hipFree(e->d_snap);
     hipFree(e->d_pairs);
     hipFree(e->d_codes); hipFree(e->d_pidx); hipFree(e->d_pflag); hipFree(e->d_acc); hipFree(e->d_res); hipFree(e->d_tmp);
     hipFree(e->d_state); hipFree(e->d_rr); hipFree(e->d_rtrue);
@@ -3606,7 +3622,8 @@ static int wait_results(fk_engine *e) {
 
 /* k_part + k_bucket_count over a resolved segment (exact range states in
    d_rtrue): the counting of the partitioned path */
-static int launch_part(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t lo, const Geo &g, int has_init) {
+static int launch_part(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t lo, const Geo &g, int has_init,
+                       const XState *exact = nullptr) {
     PartGeo pg;
     const int k = e->k;
     /* k <= 11: (k+1)-mer pairs at every other base (half the entries), plus
@@ -3666,14 +3683,14 @@ static int launch_part(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t l
                           : (pairs ? k_part<true, false, 8u> : k_part<false, false, 8u>);
     hipExtLaunchKernelGGL(kmain, dim3(pgrid), dim3(PART_BLOCK_W(W)), 0, e->stream, tev(e, 0), tev(e, 1), 0, buf, len,
                           lo, e->k, e->maskk, e->d_table, e->d_short, e->d_facc, e->d_res, e->d_rr, g.nchunks, g.cpw,
-                          e->d_state, has_init, pg, e->d_resume);
+                          e->d_state, has_init, pg, e->d_resume, exact);
     HIPCHK(hipGetLastError());
     if (mixed) {
         auto kres = W == 16u ? (pairs ? k_part<true, true, 16u> : k_part<false, true, 16u>)
                              : (pairs ? k_part<true, true, 8u> : k_part<false, true, 8u>);
         hipLaunchKernelGGL(kres, dim3(pgrid), dim3(PART_BLOCK_W(W)), 0, e->stream, buf, len, lo, e->k, e->maskk,
                            e->d_table, e->d_short, e->d_facc, e->d_res, e->d_rr, g.nchunks, g.cpw, e->d_state,
-                           has_init, pg, e->d_resume);
+                           has_init, pg, e->d_resume, exact);
         HIPCHK(hipGetLastError());
     } else {
         pg.flag = nullptr;
@@ -3693,6 +3710,13 @@ static int launch_part(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t l
 }
 
 /* scan + redo (or the partitioned count) + table stats, then the results */
+/* Can a run reach the reference's int32 seqSize zone (findKmer.cpp:977) in
+   a segment of len bytes entered in state e->state? */
+static bool int32_zone_possible(const fk_engine *e, uint64_t len) {
+    const uint64_t r0 = e->state.hdr ? 0 : (uint64_t)(uint32_t)e->state.R;
+    return r0 + len + FK_CHUNK_BYTES > 0x7FFFFFFFull;
+}
+
 static int resolve_and_fetch(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t lo, const Geo &g) {
     int rc;
     if (e->op_pending) {
@@ -3727,6 +3751,41 @@ static int resolve_and_fetch(fk_engine *e, const uint8_t *buf, uint64_t len, int
     e->dev_ev = 2;
     rc = launch_scan(e, g, 0);
     if (rc) return rc;
+    if (e->part && int32_zone_possible(e, len)) {
+        /* A run past 2^31-1 bases (the reference's seqSize turns negative,
+           :977): every range in the negative zone was counted from a guess
+           that says "deep in a run", and k_redo would cancel each one with
+           global atomics (a 3 Gbase single-record FASTA at k=11: 36 ms).  If
+           many guesses were wrong, undo the segment and count it again with
+           the exact range states k_scan just computed (~2x one pass). */
+        uint32_t n = 0;
+        HIPCHK(hipMemcpyAsync(&n, &e->d_res->redo_n, sizeof n, hipMemcpyDeviceToHost, e->stream));
+        HIPCHK(hipStreamSynchronize(e->stream));
+        if ((uint64_t)n * 16 > g.nranges) {
+            if (e->seg_snap) {
+                HIPCHK(hipMemcpyAsync(e->d_table, e->d_snap, e->nbins * sizeof(uint32_t), hipMemcpyDeviceToDevice,
+                                      e->stream));
+                if (e->nshort)
+                    HIPCHK(hipMemcpyAsync(e->d_short, e->d_snap + e->nbins, e->nshort * sizeof(uint32_t),
+                                          hipMemcpyDeviceToDevice, e->stream));
+            } else if (e->seg_clean) {
+                HIPCHK(hipMemsetAsync(e->d_table, 0, e->nbins * sizeof(uint32_t), e->stream));
+                if (e->nshort) HIPCHK(hipMemsetAsync(e->d_short, 0, e->nshort * sizeof(uint32_t), e->stream));
+            } else {
+                return FK_E_STATE;   /* cannot happen: a dirty table is snapshotted when the zone is possible */
+            }
+            HIPCHK(hipMemsetAsync(e->d_facc, 0, FK_ACC_COPIES * ACC_N * sizeof(unsigned long long), e->stream));
+            rc = launch_part(e, buf, len, lo, g, 1, e->d_rtrue);
+            if (rc) return rc;
+            rc = launch_table_stats(e, false, tev(e, 2));
+            if (rc) return rc;
+            rc = wait_results(e);
+            if (rc) return rc;
+            e->stats_valid = true;
+            e->redo += n;
+            return FK_OK;
+        }
+    }
     rc = launch_redo(e, buf, len, lo, g, 0);
     if (rc) return rc;
     rc = launch_table_stats(e, false, tev(e, 2));
@@ -3834,6 +3893,25 @@ static int count_segment(fk_engine *e, const uint8_t *dbuf, uint64_t len, int64_
     }
     e->op_pending = op;
     e->op_fresh = fresh;
+    e->seg_clean = !e->dirty;
+    e->dirty = true;
+    e->seg_snap = false;
+    if (e->part && !e->seg_clean && int32_zone_possible(e, len)) {
+        /* the guessed count may have to be undone (resolve_and_fetch) */
+        const uint64_t n = e->nbins + e->nshort;
+        if (n > e->snap_cap) {
+            hipFree(e->d_snap);
+            e->d_snap = nullptr;
+            e->snap_cap = 0;
+            if (hipMalloc((void **)&e->d_snap, n * sizeof(uint32_t)) != hipSuccess) return FK_E_OOM;
+            e->snap_cap = n;
+        }
+        HIPCHK(hipMemcpyAsync(e->d_snap, e->d_table, e->nbins * sizeof(uint32_t), hipMemcpyDeviceToDevice, e->stream));
+        if (e->nshort)
+            HIPCHK(hipMemcpyAsync(e->d_snap + e->nbins, e->d_short, e->nshort * sizeof(uint32_t),
+                                  hipMemcpyDeviceToDevice, e->stream));
+        e->seg_snap = true;
+    }
     if (e->part) {
         /* 8 <= k <= 12: partitioned counting (k_part + k_bucket_count) */
         rc = launch_part(e, dbuf, len, lo, g, has_init);

@@ -270,6 +270,41 @@ def test_int32_seqsize_two_zones():
     del buf
 
 
+@pytest.mark.parametrize("k,split,extra", [(11, 0, 1 << 22), (11, 0, 1 << 28), (11, 1 << 20, 1 << 28),
+                                           (12, 0, 1 << 28), (8, 1 << 20, 1 << 28)])
+def test_int32_zone_partitioned(k, split, extra):
+    """8 <= k <= 12 on one run of random bases past 2^31-1 (the reference's
+    int32 seqSize turns negative, findKmer.cpp:977): no windows in the zone,
+    so the table is the table of the run's first 2^31-1 bases.  Most range
+    guesses are wrong there, and the partitioned path recounts the segment
+    from the exact states (resolve_and_fetch); split > 0 feeds the first
+    `split` bytes separately, so that the table is not clean when the long
+    segment starts (its snapshot is restored before the recount).  extra:
+    bases past 2^31 (4 Mi: a few wrong ranges, cancelled by k_redo; 256 Mi:
+    over 1/16 of the ranges, recounted)."""
+    import torch
+    L = 2 ** 31 + extra
+    buf = torch.empty(L + 64, dtype=torch.uint8, device="cuda")
+    assert fk.synth_device(buf.data_ptr(), L, L, 7, 0) == L
+    torch.cuda.synchronize()
+    with fk.Engine(k) as e:
+        if split:
+            e.feed_device(buf.data_ptr(), split)
+        e.feed_device(buf.data_ptr() + split, L - split)
+        rc, r = e.finish()
+        t = e.table()
+    with fk.Engine(k) as e:
+        e.feed_device(buf.data_ptr(), 2 ** 31 - 1)
+        rc2, r2 = e.finish()
+        t2 = e.table()
+    del buf
+    assert rc == rc2 == fk.FK_OK
+    assert r.windows == r2.windows == 2 ** 31 - 1 - k + 1
+    assert np.array_equal(t, t2)
+    assert list(r.base_count) == list(r2.base_count) and r.valid_bases == r2.valid_bases
+    assert list(r.depth1) == list(r2.depth1)
+
+
 @pytest.mark.parametrize("k", [6, 11])
 def test_full_size_properties(k):
     """BASELINE config sizes (1 GB stream, 1 GB of 80-col FASTA): exact
