@@ -3126,6 +3126,8 @@ struct fk_engine {
     /* partitioned path near the reference's int32 seqSize zone: a segment
        whose guessed range states are mostly wrong is recounted from the exact
        states instead of cancelled range by range (resolve_and_fetch) */
+    XState dstate_val{0, 0, 0, 0};            /* d_state to write before the next kernel that reads it */
+    bool dstate_pending = false;
     bool dirty = false;                       /* table / short walks changed since the last reset */
     bool seg_clean = true;                    /* ... not before the current segment */
     bool seg_snap = false;                    /* d_snap holds them as before the current segment */
@@ -3143,6 +3145,23 @@ __global__ void k_zero(uint32_t *table, uint64_t nbins, uint32_t *shortcnt, uint
 /* A reset is issued lazily, with the next device work (every API entry that
    touches the device goes through set_dev), so that it reaches the GPU
    back to back with that work. */
+/* d_state written lazily, as a kernel argument (no pageable host copy on
+   the host's critical path after a compact resolve), before the next kernel
+   that reads it (count_segment's launches, k_scan); a direct write replaces
+   a pending one */
+__global__ void k_set_state(XState *d, XState v) { *d = v; }
+static int flush_state(fk_engine *e) {
+    if (!e->dstate_pending) return FK_OK;
+    e->dstate_pending = false;
+    hipLaunchKernelGGL(k_set_state, dim3(1), dim3(1), 0, e->stream, e->d_state, e->dstate_val);
+    HIPCHK(hipGetLastError());
+    return FK_OK;
+}
+static hipError_t write_dstate(fk_engine *e, const XState &x) {
+    e->dstate_pending = false;
+    return hipMemcpyAsync(e->d_state, &x, sizeof x, hipMemcpyHostToDevice, e->stream);
+}
+
 static int flush_zero(fk_engine *e) {
     if (!e->zero_pending) return FK_OK;
     e->zero_pending = false;
@@ -3218,6 +3237,7 @@ static size_t lds_bytes(const fk_engine *e) {
 static int zero_all(fk_engine *e) {
     e->zero_pending = true;
     e->dirty = false;
+    e->dstate_pending = false;   /* the reset zeroes d_state */
     e->state = XState{0, 0, 0, 0};
     memset(&e->last, 0, sizeof e->last);
     e->stats_valid = false;
@@ -3564,7 +3584,12 @@ static int launch_redo(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t l
     return FK_OK;
 }
 
+
 static int launch_scan(fk_engine *e, const Geo &g, int mode) {
+    {
+        const int rc = flush_state(e);
+        if (rc) return rc;
+    }
     const unsigned blocks = (unsigned)((g.nranges + SCAN_THREADS - 1) / SCAN_THREADS);
     if (++e->scan_epoch == 0) {   /* flags hold epochs; never reuse 0 */
         HIPCHK(hipMemsetAsync(e->d_flags, 0, e->range_cap / SCAN_THREADS * sizeof(uint32_t) + 64, e->stream));
@@ -3877,6 +3902,8 @@ static int count_segment(fk_engine *e, const uint8_t *dbuf, uint64_t len, int64_
     g = geometry(e, len);
     int rc = grow_arrays(e, g.nranges);
     if (rc) return rc;
+    rc = flush_state(e);
+    if (rc) return rc;
     settle_times(e, true);   /* before ev[] are reused */
     e->cur_timed = (e->launch_no++ % e->timing_every) == 0;
     /* one pass (k_count resolves, folds and publishes by itself) where the
@@ -3942,7 +3969,7 @@ static int finish_segment(fk_engine *e, const uint8_t *dbuf, uint64_t len, int64
                undo this segment and count only the bytes before it. */
             rc = launch_redo(e, dbuf, len, lo, g, 1);
             if (rc) return rc;
-            HIPCHK(hipMemcpyAsync(e->d_state, &entering, sizeof entering, hipMemcpyHostToDevice, e->stream));
+            HIPCHK(write_dstate(e, entering));
             e->ended = 1;
             e->scanned += eof;
             if (eof == 0) {
@@ -4016,7 +4043,7 @@ static int sparse_segment(fk_engine *e, const uint8_t *dbuf, uint64_t len, bool 
             rc = launch_redo(e, dbuf, len, 0, g, 1, sl);
             if (rc) return rc;
             HIPCHK(hipMemsetAsync(sl, 0xFF, len * sizeof(uint64_t), e->stream));
-            HIPCHK(hipMemcpyAsync(e->d_state, &entering, sizeof entering, hipMemcpyHostToDevice, e->stream));
+            HIPCHK(write_dstate(e, entering));
             e->state = entering;
             e->ended = 1;
             e->scanned += eof;
@@ -4280,7 +4307,7 @@ extern "C" int fk_engine_resolve(fk_engine *e, const fk_state *entering) {
     e->shard_pending = 0;
     e->state = in;
     if (e->shard_len == 0) {
-        HIPCHK(hipMemcpyAsync(e->d_state, &in, sizeof in, hipMemcpyHostToDevice, e->stream));
+        HIPCHK(write_dstate(e, in));
         HIPCHK(hipStreamSynchronize(e->stream));
         return FK_OK;
     }
@@ -4291,7 +4318,8 @@ extern "C" int fk_engine_resolve(fk_engine *e, const fk_state *entering) {
             if (compact_apply(&s, in, ex)) {
                 /* the guessed states count exactly: nothing to recount */
                 e->last.exit = ex;
-                HIPCHK(hipMemcpyAsync(e->d_state, &ex, sizeof ex, hipMemcpyHostToDevice, e->stream));
+                e->dstate_val = ex;
+                e->dstate_pending = true;
                 e->stats_valid = true;
                 return finish_segment(e, e->shard_buf, e->shard_len, e->shard_lo, g, in);
             }
@@ -4303,7 +4331,7 @@ extern "C" int fk_engine_resolve(fk_engine *e, const fk_state *entering) {
             if (rc) return rc;
             e->shard_resumed = true;
         }
-        HIPCHK(hipMemcpyAsync(e->d_state, &in, sizeof in, hipMemcpyHostToDevice, e->stream));
+        HIPCHK(write_dstate(e, in));
         HIPCHK(hipMemsetAsync(&e->d_res->redo_n, 0, sizeof(uint32_t), e->stream));
         HIPCHK(hipMemsetAsync(&e->d_res->eof_cand, 0xFF, sizeof(unsigned long long), e->stream));
         rc = launch_scan(e, g, 0);
@@ -4320,7 +4348,7 @@ extern "C" int fk_engine_resolve(fk_engine *e, const fk_state *entering) {
         e->redo += e->last.redo_n;
         return finish_segment(e, e->shard_buf, e->shard_len, e->shard_lo, g, in);
     }
-    HIPCHK(hipMemcpyAsync(e->d_state, &in, sizeof in, hipMemcpyHostToDevice, e->stream));
+    HIPCHK(write_dstate(e, in));
     rc = resolve_and_fetch(e, e->shard_buf, e->shard_len, e->shard_lo, g);
     if (rc) return rc;
     return finish_segment(e, e->shard_buf, e->shard_len, e->shard_lo, g, in);
