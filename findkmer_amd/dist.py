@@ -255,7 +255,7 @@ def native_comm(group=None):
     the id, one broadcast hands it over, every rank joins.  None when RCCL
     could not be set up on some rank (every rank then learns it from one
     more all-reduce and uses the torch.distributed path instead)."""
-    key = id(group) if group is not None else 0
+    key = group   # None: the default group (process groups hash by identity)
     if key in _comms:
         return _comms[key]
     rank = dist.get_rank(group)
