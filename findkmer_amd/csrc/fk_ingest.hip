@@ -4,8 +4,8 @@
  * The reference reads its sequence file one fgetc() at a time inside the
  * scan loop (findKmer/src/findKmer.cpp:988).  Here the whole file is made
  * device-resident before the scan: T host threads pread() disjoint chunks
- * straight into their own pinned buffers (two per thread, so a thread's
- * next read overlaps its previous chunk's H2D copy) and copy them with
+ * straight into their own small pinned buffers (two per thread, so a
+ * thread's next read overlaps its previous chunk's H2D copy) and copy them with
  * hipMemcpyAsync on their own streams into one device buffer.  Page-cache
  * reads, which one thread does at a few GB/s, run in parallel, and PCIe
  * copies overlap the reads.  The engine then scans the buffer in one feed
@@ -17,6 +17,8 @@
 #include <hip/hip_runtime.h>
 
 #include <fcntl.h>
+#include <stdio.h>
+#include <stdlib.h>
 #include <sys/stat.h>
 #include <unistd.h>
 
@@ -33,7 +35,13 @@ struct fk_input {
     double seconds = 0;
 };
 
-static const uint64_t INGEST_CHUNK = 32ull << 20;   /* bytes per pread + H2D */
+/* Bytes per pread + H2D, and threads.  Pinning host memory costs about
+   0.5 ms per MiB on the MI355X boxes, so the pinned buffers are kept small:
+   a 2 GB page-cache-resident file took 250-280 ms with 8 threads x 2 x 32 MiB
+   (7-8 GB/s) and ~105 ms with 4 threads x 2 x 2 MiB (19 GB/s); more threads
+   were slower at every chunk size (scripts/gpu_ingest_chunks.sh). */
+static const uint64_t INGEST_CHUNK_DEFAULT = 2ull << 20;
+static const unsigned INGEST_THREADS_DEFAULT = 4;
 static const uint64_t INGEST_PAD = 64;              /* device bytes past the end (zeroed) */
 
 extern "C" int fk_input_load(const char *path, int device, int threads, fk_input **out) {
@@ -70,8 +78,11 @@ extern "C" int fk_input_load(const char *path, int device, int threads, fk_input
         fk_input_destroy(in);
         return FK_E_HIP;
     }
+    uint64_t INGEST_CHUNK = INGEST_CHUNK_DEFAULT;
+    if (const char *cm = getenv("FINDKMER_INGEST_CHUNK_MB")) INGEST_CHUNK = std::max<uint64_t>(1, strtoull(cm, nullptr, 10)) << 20;
     const uint64_t nchunks = (in->len + INGEST_CHUNK - 1) / INGEST_CHUNK;
-    if (threads <= 0) threads = (int)std::min<unsigned>(8, std::max(1u, std::thread::hardware_concurrency()));
+    if (threads <= 0)
+        threads = (int)std::min<unsigned>(INGEST_THREADS_DEFAULT, std::max(1u, std::thread::hardware_concurrency()));
     threads = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)threads, nchunks));
     std::atomic<uint64_t> next{0};
     std::atomic<int> status{FK_OK};
@@ -114,10 +125,18 @@ extern "C" int fk_input_load(const char *path, int device, int threads, fk_input
         }
         if (s) hipStreamDestroy(s);
     };
+    const auto t1 = std::chrono::steady_clock::now();
     std::vector<std::thread> pool;
     for (int t = 0; t < threads; t++) pool.emplace_back(worker);
     for (auto &t : pool) t.join();
     close(fd);
+    if (const char *tm = getenv("FINDKMER_TIMES")) {
+        if (tm[0] == '1')
+            fprintf(stderr, "[fk_input_load] %d threads: device buffer %.3f ms, read + copy %.3f ms (%.2f GB/s)\n",
+                    threads, std::chrono::duration<double, std::milli>(t1 - t0).count(),
+                    std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t1).count(),
+                    in->len / 1e6 / std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t1).count());
+    }
     if (status != FK_OK) {
         const int rc = status;
         fk_input_destroy(in);

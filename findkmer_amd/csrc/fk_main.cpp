@@ -31,12 +31,28 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
 
 #include <iostream>
 #include <string>
 #include <vector>
+
+/* FINDKMER_TIMES=1: wall time of each phase of a run on stderr (off by
+   default: stderr stays byte-identical to the reference's) */
+static double now_s() {
+    timespec t;
+    clock_gettime(CLOCK_MONOTONIC, &t);
+    return t.tv_sec + 1e-9 * t.tv_nsec;
+}
+static bool g_times = false;
+static void phase(int k, const char *what, double &t0) {
+    if (!g_times) return;
+    const double t = now_s();
+    fprintf(stderr, "[findKmer k=%d] %-16s %9.3f ms\n", k, what, (t - t0) * 1e3);
+    t0 = t;
+}
 
 #define DEFAULT_SEQUENCE_FILE_NAME "test.txt"
 #define DEFAULT_K_VALUE 7
@@ -408,17 +424,24 @@ static int run_k(int argc) {
     }
     rewind(config.sequence_file_pointer);
 
+    double tp = now_s();
+    if (g_times && !g_input_tried) {
+        fk_device_count();   /* the HIP runtime's start-up, timed on its own */
+        phase(config.k, "hip_init", tp);
+    }
     /* load the file to HBM once (and reuse it for every k of a sweep) */
     if (!g_input_tried) {
         g_input_tried = true;
         const char *ing = getenv("FINDKMER_INGEST");
         if (!ing || strcmp(ing, "stream") != 0) {
-            int lrc = fk_input_load(config.sequence_file, -1, 0, &g_input);
+            const char *nt = getenv("FINDKMER_INGEST_THREADS");   /* default: the library's choice */
+            int lrc = fk_input_load(config.sequence_file, -1, nt ? atoi(nt) : 0, &g_input);
             if (lrc == FK_E_HIP || lrc == FK_E_NO_DEVICE) die_engine(lrc);
             /* not a regular file, or larger than free HBM: stream it */
             if (lrc) g_input = nullptr;
         }
     }
+    phase(config.k, "ingest", tp);
     bool on_device = g_input != nullptr;
     bool echoed = false;   /* the -q 0 progress lines are already printed */
     if (on_device && config.suppressOutputEnable == 0) {
@@ -438,8 +461,10 @@ static int run_k(int argc) {
     fk_engine *eng = nullptr;
     int rc = fk_engine_create(config.k, &opts, &eng);
     if (rc) die_engine(rc);
+    phase(config.k, "engine_create", tp);
     fk_result res;
     rc = on_device ? scan_device(eng, &res) : scan_file(eng, config.sequence_file_pointer, &res);
+    phase(config.k, "scan", tp);
     if (rc == FK_E_OOM && on_device) {
         /* the resident file copy and the engine's buffers (k >= 17: 8 bytes
            of slots per input byte) do not fit together: drop the copy and
@@ -480,6 +505,7 @@ static int run_k(int argc) {
         exit(EXIT_FAILURE);
     }
 
+    phase(config.k, "stats", tp);
     fprintf(stdout, "Now creating histogram.\n");
     fflush(stdout);
     if (config.k > FK_K_MAX_DENSE) {
@@ -499,10 +525,12 @@ static int run_k(int argc) {
         rc = fk_engine_table(eng, counts.data());
         if (rc) die_engine(rc);
         fk_engine_destroy(eng);
+        phase(config.k, "table_copy", tp);
         rc = fk_write_rows(config.out_file_pointer, config.k, counts.data(), prob, res.windows,
                            config.zThresholdEnable, (double)config.zThreshold, 0);
     }
     if (rc) die_engine(rc);
+    phase(config.k, "histogram", tp);
 
     fprintf(stdout, "histogram creation finished.\n");
     if (fclose(config.out_file_pointer) == EOF) {
@@ -517,6 +545,8 @@ static int run_k(int argc) {
 }
 
 int main(int argc, char *argv[]) {                                  /* :1292-1379 */
+    const char *tm = getenv("FINDKMER_TIMES");
+    g_times = tm && tm[0] == '1';
     init_conf();
     usage();
     if (!parse_arguments(argc, argv)) {
