@@ -32,6 +32,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <time.h>
+#include <unistd.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
 
@@ -547,6 +548,7 @@ static int run_k(int argc) {
 int main(int argc, char *argv[]) {                                  /* :1292-1379 */
     const char *tm = getenv("FINDKMER_TIMES");
     g_times = tm && tm[0] == '1';
+    double t_main = now_s();
     init_conf();
     usage();
     if (!parse_arguments(argc, argv)) {
@@ -572,5 +574,11 @@ int main(int argc, char *argv[]) {                                  /* :1292-137
         rc = run_k(argc);
     }
     if (g_input) fk_input_destroy(g_input);
-    return rc;
+    phase(config.k, "main_total", t_main);
+    /* every output is written and closed, and the device work is complete:
+       leave without the HIP runtime's teardown (tens of ms per run of the
+       sweep script's six) */
+    fflush(stdout);
+    fflush(stderr);
+    _exit(rc);
 }
