@@ -100,7 +100,7 @@ SIGNATURES = [
     ("fk_comm_id", ctypes.c_int, [_P]),
     ("fk_comm_create", ctypes.c_int, [_P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.POINTER(_P)]),
     ("fk_comm_destroy", None, [_P]),
-    ("fk_engine_shard_exchange", ctypes.c_int, [_P, _P, _P]),
+    ("fk_engine_shard_exchange", ctypes.c_int, [_P, _P, _P, ctypes.POINTER(ctypes.c_int32)]),
     ("fk_shard_rows_compose", ctypes.c_int, [_P, ctypes.c_int, ctypes.c_int, ctypes.POINTER(FkState)]),
     ("fk_engine_finish", ctypes.c_int, [_P, ctypes.POINTER(FkResult)]),
     ("fk_engine_table", ctypes.c_int, [_P, _U32P]),
@@ -248,16 +248,15 @@ class Engine:
         _check(lib().fk_engine_shard_pack(self.h, table_ptr, counters_ptr, rows_ptr, nrows, slot,
                                           1 if is_last else 0), "shard_pack")
 
-    def shard_exchange(self, comm, merge_ptr):
-        """fk_engine_shard_exchange: pack, one RCCL all-reduce of the merge
-        buffer over `comm` (a Comm) on the engine's stream, compose, resolve.
-        True: merged and resolved; False: fall back to the summary exchange
-        (the shard is still pending)."""
-        rc = lib().fk_engine_shard_exchange(self.h, comm.h, merge_ptr)
-        if rc == FK_E_SUMMARY:
-            return False
-        _check(rc, "shard_exchange")
-        return True
+    def shard_exchange(self, comm, merge_ptr, fast=True):
+        """fk_engine_shard_exchange: the whole exchange of a pending shard over
+        `comm` (a Comm) on the engine's stream, into the device merge buffer.
+        Returns (one_collective, first_end): one_collective = every rank's
+        buffer holds the merged table (else rank 0's does); first_end = the
+        rank whose shard ends the stream (a 0xFF byte) or None."""
+        info = (ctypes.c_int32 * 2)(1 if fast else 0, -1)
+        _check(lib().fk_engine_shard_exchange(self.h, comm.h, merge_ptr, info), "shard_exchange")
+        return bool(info[0]), (info[1] if info[1] >= 0 else None)
 
     def stream(self):
         """The engine's hipStream_t (as an int)."""

@@ -13,3 +13,5 @@ int fkc_rank(const fk_comm *c);
 int fkc_device(const fk_comm *c);
 /* in-place sum of n int32 over the ranks, enqueued on `s` */
 int fkc_allreduce_i32(fk_comm *c, int32_t *buf, size_t n, hipStream_t s);
+/* in-place sum of n int32 onto rank `root`, enqueued on `s` */
+int fkc_reduce_i32(fk_comm *c, int32_t *buf, size_t n, int root, hipStream_t s);

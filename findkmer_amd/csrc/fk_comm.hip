@@ -29,6 +29,7 @@ struct Rccl {
     decltype(&ncclCommInitRank) init_rank = nullptr;
     decltype(&ncclCommDestroy) destroy = nullptr;
     decltype(&ncclAllReduce) all_reduce = nullptr;
+    decltype(&ncclReduce) reduce = nullptr;
     bool ok = false;
 };
 
@@ -45,7 +46,8 @@ const Rccl &rccl() {
         x.init_rank = (decltype(x.init_rank))dlsym(h, "ncclCommInitRank");
         x.destroy = (decltype(x.destroy))dlsym(h, "ncclCommDestroy");
         x.all_reduce = (decltype(x.all_reduce))dlsym(h, "ncclAllReduce");
-        x.ok = x.get_id && x.init_rank && x.destroy && x.all_reduce;
+        x.reduce = (decltype(x.reduce))dlsym(h, "ncclReduce");
+        x.ok = x.get_id && x.init_rank && x.destroy && x.all_reduce && x.reduce;
         return x;
     }();
     return r;
@@ -107,4 +109,9 @@ int fkc_device(const fk_comm *c) { return c->device; }
 int fkc_allreduce_i32(fk_comm *c, int32_t *buf, size_t n, hipStream_t s) {
     if (!c || !c->nc || !rccl().ok) return FK_E_RCCL;
     return rccl().all_reduce(buf, buf, n, ncclInt32, ncclSum, c->nc, s) == ncclSuccess ? FK_OK : FK_E_RCCL;
+}
+
+int fkc_reduce_i32(fk_comm *c, int32_t *buf, size_t n, int root, hipStream_t s) {
+    if (!c || !c->nc || !rccl().ok) return FK_E_RCCL;
+    return rccl().reduce(buf, buf, n, ncclInt32, ncclSum, root, c->nc, s) == ncclSuccess ? FK_OK : FK_E_RCCL;
 }

@@ -3136,6 +3136,7 @@ struct fk_engine {
     /* fk_engine_shard_exchange: gathered pack rows, pinned and mapped (word
        0: sequence number, rows from word 32) */
     uint32_t *h_rows = nullptr, *h_rows_dev = nullptr;
+    uint32_t *d_rows = nullptr;               /* the stitched exchange's rows (device) */
     uint32_t rows_cap = 0, rows_seq = 0;
 };
 
@@ -3270,6 +3271,7 @@ extern "C" void fk_engine_destroy(fk_engine *e) {
     for (int i = 0; i < 3; i++) if (e->ev[i]) hipEventDestroy(e->ev[i]);
     if (e->h_res) hipHostFree(e->h_res);
     if (e->h_rows) hipHostFree(e->h_rows);
+    hipFree(e->d_rows);
     hipFree(e->d_done);
     hipFree(e->d_tpart);
     if (e->own_stream && e->stream) hipStreamDestroy(e->stream);
@@ -4447,32 +4449,41 @@ __global__ void __launch_bounds__(64) k_rows_publish(const uint32_t *rows, uint3
     if (threadIdx.x == 0) __hip_atomic_store(&host[0], seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-extern "C" int fk_engine_shard_exchange(fk_engine *e, fk_comm *comm, int32_t *merge) {
-    if (!e || !comm || !merge) return FK_E_INVALID;
-    if (e->sparse) return FK_E_INVALID;
-    if (!e->shard_pending) return FK_E_STATE;
-    const int world = fkc_world(comm), rank = fkc_rank(comm);
-    if (fkc_device(comm) != e->dev) return FK_E_INVALID;
-    int rc = set_dev(e);
-    if (rc) return rc;
-    const uint32_t nrow = (uint32_t)world * FK_PACK_ROW_WORDS;
-    if (e->rows_cap < nrow) {
-        if (e->h_rows) hipHostFree(e->h_rows);
-        e->h_rows = e->h_rows_dev = nullptr;
-        e->rows_cap = 0;
-        if (hipHostMalloc((void **)&e->h_rows, (32 + nrow) * sizeof(uint32_t), hipHostMallocMapped | hipHostMallocCoherent) !=
-                hipSuccess ||
-            hipHostGetDevicePointer((void **)&e->h_rows_dev, e->h_rows, 0) != hipSuccess)
-            return FK_E_OOM;
-        memset(e->h_rows, 0, (32 + nrow) * sizeof(uint32_t));
-        e->rows_cap = nrow;
+/* One row of a rows region (zeros elsewhere): words [0, nsrc) from src (a
+   device transfer function), or w0 in word 0; word 24 = 1 (a valid row). */
+__global__ void __launch_bounds__(64) k_fill_row(uint32_t *rows, int nrows, int slot, const uint32_t *src,
+                                                 uint32_t nsrc, uint32_t w0) {
+    for (uint32_t i = threadIdx.x; i < (uint32_t)nrows * FK_PACK_ROW_WORDS; i += 64) {
+        const uint32_t r = i / FK_PACK_ROW_WORDS, j = i % FK_PACK_ROW_WORDS;
+        uint32_t v = 0;
+        if ((int)r == slot) v = j == 24 ? 1u : (src ? (j < nsrc ? src[j] : 0u) : (j == 0 ? w0 : 0u));
+        rows[i] = v;
     }
-    uint32_t *rows = reinterpret_cast<uint32_t *>(merge + e->nbins + 4 * FK_PACK_COUNTERS);
-    rc = fk_engine_shard_pack(e, reinterpret_cast<uint32_t *>(merge), merge + e->nbins, rows, world, rank,
-                              rank == world - 1);
-    if (rc) return rc;
-    rc = fkc_allreduce_i32(comm, merge, e->nbins + 4 * FK_PACK_COUNTERS + nrow, e->stream);
-    if (rc) return rc;
+}
+
+/* pinned, mapped scratch of the exchange: [0] sequence number, rows from
+   word 32, counter limbs (staging) after the rows */
+static int ensure_rows(fk_engine *e, uint32_t nrow) {
+    if (e->rows_cap >= nrow) return FK_OK;
+    if (e->h_rows) hipHostFree(e->h_rows);
+    hipFree(e->d_rows);
+    e->h_rows = e->h_rows_dev = nullptr;
+    e->d_rows = nullptr;
+    e->rows_cap = 0;
+    const size_t words = 32 + nrow + 4 * FK_PACK_COUNTERS;
+    if (hipHostMalloc((void **)&e->h_rows, words * sizeof(uint32_t), hipHostMallocMapped | hipHostMallocCoherent) !=
+            hipSuccess ||
+        hipHostGetDevicePointer((void **)&e->h_rows_dev, e->h_rows, 0) != hipSuccess ||
+        hipMalloc((void **)&e->d_rows, nrow * sizeof(uint32_t)) != hipSuccess)
+        return FK_E_OOM;
+    memset(e->h_rows, 0, words * sizeof(uint32_t));
+    e->rows_cap = nrow;
+    return FK_OK;
+}
+
+/* The rows (device, already all-reduced on e->stream) into e->h_rows + 32;
+   one host wait. */
+static int rows_fetch(fk_engine *e, const uint32_t *rows, uint32_t nrow) {
     if (++e->rows_seq == 0) e->rows_seq = 1;
     const uint32_t want = e->rows_seq;
     hipLaunchKernelGGL(k_rows_publish, dim3(1), dim3(64), 0, e->stream, rows, nrow, e->h_rows_dev, want);
@@ -4489,10 +4500,119 @@ extern "C" int fk_engine_shard_exchange(fk_engine *e, fk_comm *comm, int32_t *me
         }
         __builtin_ia32_pause();
     }
-    fk_state st;
-    rc = fk_shard_rows_compose(e->h_rows + 32, world, rank, &st);
-    if (rc) return rc;   /* FK_E_SUMMARY: the shard stays pending */
-    return fk_engine_resolve(e, &st);
+    return FK_OK;
+}
+
+/* The stitched exchange with the library's communicator (the shard is
+   pending): the shards' full transfer functions all-gathered (an
+   all-reduce of rows), composed on the host, the shard resolved; the shards'
+   end flags all-gathered the same way (a 0xFF byte, :988, exact only after
+   the resolve); then the table and counter limbs, zero for ranks after the
+   first ending shard, reduced onto rank 0. */
+static int stitched_exchange(fk_engine *e, fk_comm *comm, int32_t *merge, int32_t *first_end_out) {
+    const int world = fkc_world(comm), rank = fkc_rank(comm);
+    const uint32_t nrow = (uint32_t)world * FK_PACK_ROW_WORDS;
+    int rc = shard_full_tf(e);
+    if (rc) return rc;
+    if (e->shard_len == 0) {
+        const TF id = fk_identity();
+        HIPCHK(hipMemcpyAsync(e->d_tf, &id, sizeof id, hipMemcpyHostToDevice, e->stream));
+    }
+    hipLaunchKernelGGL(k_fill_row, dim3(1), dim3(64), 0, e->stream, e->d_rows, world, rank,
+                       reinterpret_cast<const uint32_t *>(e->d_tf), (uint32_t)(sizeof(TF) / 4), 0u);
+    HIPCHK(hipGetLastError());
+    rc = fkc_allreduce_i32(comm, reinterpret_cast<int32_t *>(e->d_rows), nrow, e->stream);
+    if (rc) return rc;
+    rc = rows_fetch(e, e->d_rows, nrow);
+    if (rc) return rc;
+    XState s{0, 0, 0, 0}, in = s;   /* from the stream's initial state */
+    for (int r = 0; r < world; r++) {
+        TF t;
+        memcpy(&t, e->h_rows + 32 + (size_t)r * FK_PACK_ROW_WORDS, sizeof t);
+        if (r == rank) in = s;
+        s = fk_apply(t, s);
+    }
+    fk_state ent{in.R, fk_sigma(in.code), in.hdr, 0};
+    rc = fk_engine_resolve(e, &ent);
+    if (rc) return rc;
+    fk_result res;
+    rc = fk_engine_finish(e, &res);
+    if (rc != FK_OK && rc != FK_E_ROLLOVER && rc != FK_E_UNTERMINATED_HEADER && rc != FK_E_EMPTY) return rc;
+    /* where the stream ends */
+    hipLaunchKernelGGL(k_fill_row, dim3(1), dim3(64), 0, e->stream, e->d_rows, world, rank, (const uint32_t *)nullptr,
+                       0u, res.hit_eof_byte ? 1u : 0u);
+    HIPCHK(hipGetLastError());
+    rc = fkc_allreduce_i32(comm, reinterpret_cast<int32_t *>(e->d_rows), nrow, e->stream);
+    if (rc) return rc;
+    rc = rows_fetch(e, e->d_rows, nrow);
+    if (rc) return rc;
+    int first_end = -1;
+    for (int r = 0; r < world && first_end < 0; r++)
+        if (e->h_rows[32 + (size_t)r * FK_PACK_ROW_WORDS]) first_end = r;
+    const bool counting = first_end < 0 || rank <= first_end;
+    const int last = first_end >= 0 ? first_end : world - 1;
+    /* the table and the counters (fk_engine_finish's values, as 16-bit limbs) */
+    uint64_t v[FK_PACK_COUNTERS] = {};
+    if (counting) {
+        v[0] = res.windows; v[1] = res.valid_bases;
+        for (int b = 0; b < 4; b++) { v[2 + b] = res.base_count[b]; v[6 + b] = res.depth1[b]; }
+        v[10] = res.unknown_chars; v[11] = res.scanned_bytes;
+        v[12] = rank == first_end ? 1u : 0u;
+        v[13] = rank == last ? (uint64_t)res.unterminated_header : 0u;
+        HIPCHK(hipMemcpyAsync(merge, e->d_table, e->nbins * sizeof(uint32_t), hipMemcpyDeviceToDevice, e->stream));
+    } else {
+        HIPCHK(hipMemsetAsync(merge, 0, e->nbins * sizeof(uint32_t), e->stream));
+    }
+    uint32_t *limbs = e->h_rows + 32 + e->rows_cap;   /* pinned staging */
+    for (int i = 0; i < FK_PACK_COUNTERS; i++)
+        for (int j = 0; j < 4; j++) limbs[4 * i + j] = (uint32_t)((v[i] >> (16 * j)) & 0xFFFFu);
+    HIPCHK(hipMemcpyAsync(merge + e->nbins, limbs, 4 * FK_PACK_COUNTERS * sizeof(uint32_t), hipMemcpyHostToDevice,
+                          e->stream));
+    rc = fkc_reduce_i32(comm, merge, e->nbins + 4 * FK_PACK_COUNTERS, 0, e->stream);
+    if (rc) return rc;
+    HIPCHK(hipStreamSynchronize(e->stream));
+    if (first_end_out) *first_end_out = first_end;
+    return FK_OK;
+}
+
+extern "C" int fk_engine_shard_exchange(fk_engine *e, fk_comm *comm, int32_t *merge, int32_t *info) {
+    if (!e || !comm || !merge) return FK_E_INVALID;
+    if (e->sparse) return FK_E_INVALID;
+    if (!e->shard_pending) return FK_E_STATE;
+    const int world = fkc_world(comm), rank = fkc_rank(comm);
+    if (fkc_device(comm) != e->dev) return FK_E_INVALID;
+    const bool try_fast = !info || info[0] != 0;
+    int rc = set_dev(e);
+    if (rc) return rc;
+    const uint32_t nrow = (uint32_t)world * FK_PACK_ROW_WORDS;
+    rc = ensure_rows(e, nrow);
+    if (rc) return rc;
+    if (try_fast) {
+        /* one collective: pack, all-reduce table + counters + rows, compose */
+        uint32_t *rows = reinterpret_cast<uint32_t *>(merge + e->nbins + 4 * FK_PACK_COUNTERS);
+        rc = fk_engine_shard_pack(e, reinterpret_cast<uint32_t *>(merge), merge + e->nbins, rows, world, rank,
+                                  rank == world - 1);
+        if (rc) return rc;
+        rc = fkc_allreduce_i32(comm, merge, e->nbins + 4 * FK_PACK_COUNTERS + nrow, e->stream);
+        if (rc) return rc;
+        rc = rows_fetch(e, rows, nrow);
+        if (rc) return rc;
+        fk_state st;
+        rc = fk_shard_rows_compose(e->h_rows + 32, world, rank, &st);
+        if (rc == FK_OK) {
+            rc = fk_engine_resolve(e, &st);
+            if (rc) return rc;
+            if (info) { info[0] = 1; info[1] = -1; }
+            return FK_OK;
+        }
+        if (rc != FK_E_SUMMARY) return rc;
+        /* some guess did not hold (every rank sees it): stitched, below */
+    }
+    int32_t first_end = -1;
+    rc = stitched_exchange(e, comm, merge, &first_end);
+    if (rc) return rc;
+    if (info) { info[0] = 0; info[1] = first_end; }
+    return FK_OK;
 }
 
 extern "C" int fk_engine_stream(fk_engine *e, void **stream) {

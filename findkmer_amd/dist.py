@@ -27,6 +27,12 @@ only when a shard may end the stream:
    rollover exit (a u32 trie counter reaching 2^32, :642-648): a merged bin
    that wrapped makes the table total fall short of the window count.
 
+The library's own RCCL communicator (backend nccl, native_comm) runs the
+whole exchange inside fk_engine_shard_exchange on the engine's stream: the
+one-collective path below when it applies, else steps 1-2 with
+all-reduces of rows standing in for the all-gathers (one host wait each).
+torch.distributed carries the same protocol for gloo rehearsals.
+
 One-collective fast path (k <= 7, shards counted in one pass): before any
 host round trip, every rank packs what its shard would report if its guessed
 entering state holds -- table, counter limbs, and its compact summary in its
@@ -376,23 +382,25 @@ def count_sharded(engine, ptr, nbytes, halo, buf, group=None, times=None, pinned
     dev = buf.device
     t0 = time.perf_counter()
     engine.feed_shard_device(ptr, nbytes, halo)
+    comm = None
+    if native and buf.is_cuda and hasattr(engine, "shard_exchange") and dist.get_backend(group) == "nccl":
+        comm = native_comm(group)
+    if comm is not None:
+        # the whole exchange inside the library, on the engine's stream: one
+        # all-reduce when every guess held (k <= 7), else the stitched
+        # exchange (fk_engine_shard_exchange)
+        one, first_end = engine.shard_exchange(comm, buf.data_ptr(), fast=fast and engine.k <= FAST_KMAX)
+        t1 = time.perf_counter()
+        _, r = engine.finish(allow=(FK_OK, FK_E_ROLLOVER, FK_E_UNTERMINATED_HEADER, FK_E_EMPTY))
+        if times is not None:
+            times["exchange"] = times.get("exchange", 0.0) + (t1 - t0)
+            times["finish"] = times.get("finish", 0.0) + (time.perf_counter() - t1)
+        return ShardedResult(buf, engine.k, rank, first_end, r, path="fast" if one else "stitched",
+                             transport="rccl-native")
     if fast and engine.k <= FAST_KMAX and hasattr(engine, "shard_pack"):
-        comm = None
-        if native and buf.is_cuda and hasattr(engine, "shard_exchange") and dist.get_backend(group) == "nccl":
-            comm = native_comm(group)
-        if comm is not None:
-            ok = engine.shard_exchange(comm, buf.data_ptr())
-            if ok:
-                t1 = time.perf_counter()
-                _, r = engine.finish(allow=(FK_OK, FK_E_ROLLOVER, FK_E_UNTERMINATED_HEADER, FK_E_EMPTY))
-                if times is not None:
-                    times["exchange"] = times.get("exchange", 0.0) + (t1 - t0)
-                    times["finish"] = times.get("finish", 0.0) + (time.perf_counter() - t1)
-                return ShardedResult(buf, engine.k, rank, None, r, path="fast", transport="rccl-native")
-        else:
-            got = _fast_exchange(engine, buf, rank, world, group, times, t0)
-            if got is not None:
-                return got
+        got = _fast_exchange(engine, buf, rank, world, group, times, t0)
+        if got is not None:
+            return got
     t1 = time.perf_counter()
     got = stitch_entry_state(engine.summary(), group, dev)
     if got is None:

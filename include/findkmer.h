@@ -200,18 +200,25 @@ typedef struct fk_comm fk_comm;
 int  fk_comm_id(uint8_t *id /* FK_COMM_ID_BYTES */);
 int  fk_comm_create(const uint8_t *id, int world, int rank, int device, fk_comm **out);
 void fk_comm_destroy(fk_comm *c);
-/* The whole one-collective exchange on the engine's stream, after
- * fk_engine_feed_shard: fk_engine_shard_pack(merge, merge + 4^k,
- * merge + 4^k + 4 * FK_PACK_COUNTERS, world rows, slot = rank), an in-place
- * all-reduce of the merge buffer (4^k + 4 * FK_PACK_COUNTERS +
- * world * FK_PACK_ROW_WORDS int32) over `comm`, the rows published to host
- * memory, one host wait, fk_shard_rows_compose, fk_engine_resolve.  FK_OK:
- * every rank's merge buffer holds the merged table and counter limbs, and
- * the shard is resolved (fk_engine_finish gives its own result).
- * FK_E_SUMMARY: some shard's guess did not hold (or it was not counted in
- * one pass); the shard is still pending, the merge buffer is scratch, and
- * every rank gets this answer: fall back to the fk_engine_summary exchange. */
-int  fk_engine_shard_exchange(fk_engine *e, fk_comm *comm, int32_t *merge);
+/* A sharded pass's whole exchange on the engine's stream, after
+ * fk_engine_feed_shard, with the library's communicator; `merge` is a device
+ * buffer of 4^k + 4 * FK_PACK_COUNTERS + world * FK_PACK_ROW_WORDS int32.
+ *  - one collective (tried when info == NULL or info[0] != 0): pack
+ *    (fk_engine_shard_pack, slot = rank), an in-place all-reduce of the whole
+ *    buffer, the rows published to host memory, one host wait,
+ *    fk_shard_rows_compose, fk_engine_resolve.  Every rank's buffer then
+ *    holds the merged table and counter limbs (info[0] = 1).
+ *  - otherwise (the one-collective path is off, the shard was not counted in
+ *    one pass -- 8 <= k <= 12 always --, or some guess did not hold; every
+ *    rank takes this branch together): the shards' full transfer functions
+ *    all-gathered and composed, fk_engine_resolve, the shards' end flags
+ *    all-gathered (a 0xFF byte, findKmer.cpp:988), then the table and counter
+ *    limbs -- zero on ranks after the first ending shard -- reduced onto rank
+ *    0 (info[0] = 0, info[1] = that shard's rank or -1).
+ * The shard is resolved either way (fk_engine_finish gives its own result),
+ * and the call returns after the device work.  Replaces no reference call
+ * (the reference is single-threaded, findKmer.cpp:962). */
+int  fk_engine_shard_exchange(fk_engine *e, fk_comm *comm, int32_t *merge, int32_t *info /* [2], may be NULL */);
 
 /* Finish the stream (end-of-input rules) and fill *res.  Returns FK_OK or one
  * of FK_E_EMPTY / FK_E_UNTERMINATED_HEADER / FK_E_ROLLOVER (res is filled in

@@ -57,7 +57,8 @@ def test_sharded_mixed_input_against_oracle(k, world, eof_in):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("k,fast,eof_in,native", [(6, 1, -1, 1), (7, 1, -1, 1), (6, 1, -1, 0), (5, 0, -1, 1),
-                                                  (6, 1, 0, 1), (11, 1, -1, 1)])
+                                                  (6, 1, 0, 1), (11, 1, -1, 1), (11, 1, 0, 1), (11, 1, -1, 0),
+                                                  (13, 1, -1, 1)])
 def test_rccl_single_rank_merge(k, fast, eof_in, native):
     """The RCCL code path on a one-GPU box (world 1, backend nccl): the pack
     into the device merge buffer, the engine-stream -> collective ordering,
@@ -71,6 +72,7 @@ def test_rccl_single_rank_merge(k, fast, eof_in, native):
                 "hit_eof_byte", "unterminated_header", "distinct"):
         assert out[key][0] == out[key][1], (key, out[key])
     assert out["path"] == ("fast" if fast and k <= 7 and eof_in < 0 else "stitched")
-    if out["path"] == "fast":
-        # the library's own RCCL communicator on the engine's stream
-        assert out["transport"] == ("rccl-native" if native else "torch")
+    # the library's own RCCL communicator on the engine's stream (both paths)
+    assert out["transport"] == ("rccl-native" if native else "torch")
+    if eof_in >= 0:
+        assert out["first_end"] == eof_in
