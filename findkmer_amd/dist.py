@@ -369,9 +369,10 @@ def count_sharded(engine, ptr, nbytes, halo, buf, group=None, times=None, pinned
     `pinned` (optional): a pinned host int32 tensor of COUNTER_SLOTS entries
     for an asynchronous counter upload.  fast=False: always the stitched
     exchange (steps 1-2).  native: over RCCL (backend nccl, device buffer)
-    the one-collective path runs inside the library on the engine's stream
-    (fk_engine_shard_exchange with its own communicator, native_comm)
-    instead of through torch.distributed.
+    the whole exchange -- one collective or stitched -- runs inside the
+    library on the engine's stream (fk_engine_shard_exchange with its own
+    communicator, native_comm) instead of through torch.distributed; the
+    buffer is complete when this returns.
 
     `engine` is a findkmer_amd.Engine (or, in the CPU tests, a model with the
     same feed_shard_device / summary / summary_full / resolve / finish /
