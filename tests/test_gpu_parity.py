@@ -551,15 +551,19 @@ def test_cli_device_ingest_large(tmp_path):
 
 
 @pytest.mark.parametrize("k", [8, 10, 11, 12])
-@pytest.mark.parametrize("kind", ["polyA", "period7", "fasta_polyA"])
+@pytest.mark.parametrize("kind", ["polyA", "period7", "fasta_polyA", "polyA_C"])
 def test_partition_skewed(k, kind):
     """8 <= k <= 12 on inputs whose windows all fall in one or a few table
     slices: k_part batches of one run of up to 64 K entries (the 16-bit
     count field holds count - 1), k_bucket_count's
-    long-run loop, pair and single slices (FASTA halves with a newline)"""
+    long-run loop, pair and single slices (FASTA halves with a newline).
+    polyA_C (A^30 C) puts hundreds of thousands of counts into two adjacent
+    bins (kernel codes 0 and 1: ...A and ...C), each past 2^16"""
     n = 24 << 20
     if kind == "polyA":
         data = b"A" * n
+    elif kind == "polyA_C":
+        data = ((b"A" * 30 + b"C") * (n // 31 + 1))[:n]
     elif kind == "period7":
         data = (b"ACGTTGC" * (n // 7 + 1))[:n]
     else:
