@@ -1,4 +1,4 @@
-"""Multi-process shard stitching on the CPU (world_size 2 and 3, gloo).
+"""Multi-process shard stitching on the CPU (world_size 2, 3 and 8, gloo).
 
 Runs the real orchestration of findkmer_amd/dist.py (all-gather of shard
 summaries, composition with the C-ABI fk_summary_apply, the end-flag
@@ -129,7 +129,8 @@ def _check(data, world, mode, bounds=None):
     return got
 
 
-@pytest.mark.parametrize("world,mode", [(2, "full"), (3, "full"), (3, "compact"), (3, "compact_miss")])
+@pytest.mark.parametrize("world,mode", [(2, "full"), (3, "full"), (3, "compact"), (3, "compact_miss"),
+                                        (8, "full"), (8, "compact"), (8, "compact_miss")])
 def test_merge_gloo(world, mode):
     got = _check(_input(world + 7, 24000), world, mode)
     assert got["first_end"] is None
