@@ -1,4 +1,4 @@
-"""Sharded multi-process path on the GPU box, two or three ranks sharing
+"""Sharded multi-process path on the GPU box, two, three or eight ranks sharing
 cuda:0 with host-side (gloo) collectives: the real engine's feed_shard /
 summary / resolve and findkmer_amd/dist.py's stitch, end-flag exchange and
 table + counter merge.  (RCCL itself needs one GPU per rank: the driver's
@@ -38,7 +38,21 @@ def test_two_rank_shards_gloo(k, fasta, chrom):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("k,world,eof_in", [(6, 3, 1), (6, 3, -1), (11, 3, 1), (11, 2, 0), (5, 2, -1), (13, 3, 1)])
+@pytest.mark.parametrize("k,fasta", [(6, 0), (11, 80)])
+def test_eight_rank_shards_gloo(k, fasta):
+    """The world size of the driver's 8-GPU bench, rehearsed with eight
+    ranks on cuda:0 over gloo: bench.py's shard layout (halos; pure ACGT:
+    'N' chromosome breaks at 40M and 80M bases, inside ranks 3 and 6), the
+    merged counts bench.py asserts, and both exchanges"""
+    out = _torchrun(8, 29650 + k, os.path.join(REPO, "bench.py"),
+                    ["--gpus", "8", "--steps", "2", "--warmup", "1", "--no-cpu-baseline", "--dist-backend", "gloo",
+                     "--k", str(k), "--fasta-line", str(fasta), "--bases", "12800000", "--chrom", "40000000"])
+    assert out["n_gpus"] == 8 and out["value"] > 0
+    assert out["exchange"] in (("fast", "stitched") if k <= 7 else ("stitched",))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k,world,eof_in", [(6, 8, 5), (11, 8, -1), (6, 3, 1), (6, 3, -1), (11, 3, 1), (11, 2, 0), (5, 2, -1), (13, 3, 1)])
 def test_sharded_mixed_input_against_oracle(k, world, eof_in):
     """headers, N runs, unknown bytes, ragged lines; eof_in >= 0: a 0xFF
     byte ends the stream inside that rank's shard, and the later ranks'
