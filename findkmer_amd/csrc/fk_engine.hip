@@ -2224,9 +2224,15 @@ k_part(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint
 /* k_bucket_count's first loads per quad: BUCKET_ROWS rows at once, each
    with BUCKET_U 16-B pieces per lane (64 B per quad each).  2 x 4 (256 B
    of a ~200-B run, k=11 with 16-wave k_part blocks) beat 4 x 2 by ~1 %
-   (k=11 step 1.082 -> 1.070 ms); 3 x 3, 3 x 4 and 1 x 8 fell in between. */
+   (k=11 step 1.082 -> 1.070 ms); 3 x 3, 3 x 4 and 1 x 8 fell in between.
+   2 x 5 (95 VGPRs, still 4 waves per SIMD): a k=11 pair run is ~120 codes,
+   so 4 pieces per lane (128 codes from the aligned-down start) sent a third
+   of the runs -- and so nearly every wave of 16 runs -- through the
+   long-run loop for a few codes; k_bucket_count 334 -> 325 us, k=11 step
+   1.081 -> 1.074 ms, k=12 1.684 -> 1.669 ms, k=8 unchanged (2 x 6: the
+   same within noise). */
 #ifndef BUCKET_U
-#define BUCKET_U 4
+#define BUCKET_U 5
 #endif
 #ifndef BUCKET_ROWS
 #define BUCKET_ROWS 2
