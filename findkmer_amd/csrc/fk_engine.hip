@@ -2230,7 +2230,7 @@ k_part(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint
    of the runs -- and so nearly every wave of 16 runs -- through the
    long-run loop for a few codes; k_bucket_count 334 -> 325 us, k=11 step
    1.081 -> 1.074 ms, k=12 1.684 -> 1.669 ms, k=8 unchanged (2 x 6: the
-   same within noise). */
+   same within noise; 3 x 5 at 128 VGPRs 331 -> 351 us, 1 x 10 -> 341 us). */
 #ifndef BUCKET_U
 #define BUCKET_U 5
 #endif
