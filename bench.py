@@ -1,25 +1,31 @@
 #!/usr/bin/env python3
 """bench.py — k-mer scan throughput on MI355X (BASELINE.json metric).
 
-Workload (BASELINE.json configs[1]): k=6 over a 1 GB synthetic ACGT stream per
-GPU, input resident in HBM before the timed region.  One step = one pass of
-the hot path over the batch: reset, k_count + k_tail (the engine's
-fk_engine_feed: count, fold, check the guessed range states, publish), and the
-result scalars (fk_engine_finish).  With
---gpus N (one process per GPU, torch.distributed over RCCL) each rank owns the
-next 1 GB shard of one N GB stream (a synthetic genome with an 'N' run break
-every 1.5 Gbases, so no run reaches the reference's int32 wrap; the N=1 stream
-has none): the shard entry state is stitched by
-all-gathering the 96-byte shard transfer functions, and the count tables are
-summed with a reduce to rank 0 — the path's two real exchange steps.
+Headline workload (BASELINE.json configs[2], the largest single-GPU config):
+k=11 over a 10 G-base synthetic genome per GPU — 80-column FASTA (one
+">synthetic" header, ≈1.0125e10 bytes), an 'N' run break every 1.5 Gbases
+(chromosomes), generated in HBM before the timed region.  One step = one pass
+of the hot path over the batch: reset, the engine's feed (k_part +
+k_bucket_count + k_pair_fold + the statistics kernels for 8 <= k <= 12) and
+fk_engine_finish.
+
+The same line carries the north-star gate as a sub-record ("north_star"):
+k=6 over a 10 G-base pure-ACGT genome (1.5-Gbase chromosomes), with its own
+value, ms_per_step and roofline (k_count).
+
+With --gpus N (one process per GPU, torch.distributed over RCCL) each rank
+owns the next 10 G-base shard of one N x 10 G-base stream (weak scaling): the
+shard entry state is stitched and the count tables merged onto rank 0 inside
+the library (findkmer_amd/dist.py, fk_engine_shard_exchange) -- the path's
+real exchange steps.
 
 Prints ONE JSON line on rank 0 (contract in the task statement): value =
-bases/s over all ranks, plus "roofline" for the dominant kernel (k_count, HIP
-events on the engine's stream) and "cpu_baseline" (the reference binary, or
-the oracle port if it is absent, on a bounded sample, rank 0 at N=1 only).
+bases/s over all ranks, "roofline" for the dominant kernel (HIP events on the
+engine's stream, recorded inside the launch), "cpu_baseline" (the reference
+binary on a bounded sample, rank 0 at N=1 only) and "cpu_baseline_multicore"
+(the oracle's dense scan over 16 host threads, the "fast CPU" of BASELINE.md).
 """
 import argparse
-import ctypes
 import json
 import os
 import subprocess
@@ -32,59 +38,70 @@ sys.path.insert(0, REPO)
 
 HBM_PEAK_GBS = 8000.0    # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 METRIC = "bases/sec scanned at fixed k; achieved HBM GB/s vs roofline, 1/2/4/8 GPUs"
-CHROM = 1_500_000_000   # multi-GPU stream: an 'N' run break every CHROM bases (synthetic chromosomes)
+CHROM = 1_500_000_000    # an 'N' run break every CHROM bases (synthetic chromosomes)
+HEADER = 11              # len(">synthetic\n"), fk_synth_device with fasta_line > 0
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--k", type=int, default=6)
-    ap.add_argument("--bases", type=int, default=1_000_000_000, help="bases per GPU")
-    ap.add_argument("--fasta-line", type=int, default=0, help="0 = pure ACGT stream (configs[1]); 80 = FASTA")
-    ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--k", type=int, default=11)
+    ap.add_argument("--bases", type=int, default=10_000_000_000, help="bases per GPU")
+    ap.add_argument("--fasta-line", type=int, default=80, help="80 = FASTA (configs[2]); 0 = pure ACGT stream")
+    ap.add_argument("--seed", type=int, default=2)
+    ap.add_argument("--chrom", type=int, default=CHROM,
+                    help="an 'N' run break at every base index that is a multiple of this (0 = one run)")
+    ap.add_argument("--north-star-bases", type=int, default=10_000_000_000,
+                    help="sub-record: k=6 over this many pure-ACGT bases per GPU (0 = skip)")
     ap.add_argument("--cpu-sample-bytes", type=int, default=0, help="0 = auto (~10-20 s of reference CPU work)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--chrom", type=int, default=CHROM,
-                    help="streams longer than this (pure ACGT): an 'N' run break every this many bases, a genome of chromosomes (0 = one run)")
     ap.add_argument("--timing-every", type=int, default=4,
                     help="time the count kernel with HIP events on every Nth step")
     ap.add_argument("--stitched", action="store_true",
                     help="sharded pass: always the summary all-gather + reduce (no one-collective path)")
     ap.add_argument("--torch-exchange", action="store_true",
-                    help="one-collective path through torch.distributed instead of the library's RCCL communicator")
+                    help="exchange through torch.distributed instead of the library's RCCL communicator")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl = RCCL over xGMI (one GPU per rank); gloo = host-side rehearsal")
-    return ap.parse_args()
+    ap.add_argument("--verify-single", action="store_true",
+                    help="rank 0 also counts the whole stream with one engine and compares the merged "
+                         "table and counters with it (configs[3] parity)")
+    return ap.parse_args(argv)
 
 
-def cpu_baseline(args, n_sample):
-    """The reference CPU loop on a bounded prefix of the same stream."""
-    sys.path.insert(0, os.path.join(REPO, "tests"))
-    import oracle   # checker / baseline only
-    data = oracle.synth(n_sample, args.seed, args.fasta_line if args.fasta_line > 0 else 0)
-    bases = n_sample
-    ref = oracle.REF_BIN
-    if os.path.exists(ref) and os.access(ref, os.X_OK):
-        with tempfile.TemporaryDirectory() as td:
-            p = os.path.join(td, "sample.fa")
-            data.tofile(p)
-            t0 = time.perf_counter()
-            subprocess.run([ref, "-q", "1", "-k", str(args.k), "-p", "sample.fa"], cwd=td,
-                           stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
-            dt = time.perf_counter() - t0
-        kind = "reference"
-        what = (f"oracle/_ref/findKmer_ref (reference findKmer.cpp, g++ -O3, single thread) "
-                f"end-to-end on the first {bases} bases of the same stream, k={args.k}")
-    else:
-        t0 = time.perf_counter()
-        oracle.count_dense(data.tobytes(), args.k)
-        dt = time.perf_counter() - t0
-        kind = "port"
-        what = f"oracle port (fk_oracle.c, 1 thread) on the first {bases} bases, k={args.k}"
-    return {"value": bases / dt, "unit": "bases/s", "cores": 1, "kind": kind,
-            "sample": what, "seconds": round(dt, 3)}
+# ---------------------------------------------------------------- the stream
+
+def base_offset(b, first, fasta_line, rank0):
+    """Byte offset of stream base b in a buffer that starts at base `first`
+    (plus the header on rank 0 of a FASTA stream)."""
+    rel = b - first
+    if fasta_line <= 0:
+        return rel
+    return (HEADER if rank0 else 0) + rel + rel // fasta_line
+
+
+def make_genome(n, fasta_line, seed, chrom, first=0, rank0=True, device="cuda"):
+    """The synthetic genome's bases [first, first + n) in a fresh device
+    buffer (+64 bytes of slack): fk_synth_device's splitmix64 ACGT (the same
+    bytes as the oracle's fko_synth), FASTA framing when fasta_line > 0 (the
+    header only on the stream's first shard), and an 'N' at every base index
+    j*chrom (j >= 1).  Returns (buffer, size in bytes)."""
+    import torch
+    import findkmer_amd as fk
+    assert first % 32 == 0 and (fasta_line <= 0 or first % fasta_line == 0)
+    frame = (fasta_line if rank0 else -fasta_line) if fasta_line > 0 else 0
+    size = fk.synth_size(n, frame)
+    buf = torch.empty(size + 64, dtype=torch.uint8, device=device)
+    w = fk.synth_device(buf.data_ptr(), size, n, seed + first // 32, frame)
+    assert w == size
+    if chrom > 0:
+        for b in range((first // chrom + 1) * chrom, first + n, chrom):
+            off = base_offset(b, first, fasta_line, rank0)
+            assert chr(buf[off].item()) in "ACGT", (b, off)
+            buf[off] = ord("N")
+    return buf, size
 
 
 def run_windows(n, k):
@@ -97,95 +114,117 @@ def run_windows(n, k):
     return full * (hi - k + 1) + max(0, min(rem, hi) - k + 1)
 
 
-def expected_windows(total, k, chrom):
-    """Windows in a pure-ACGT stream of `total` positions whose positions
-    j*chrom (j >= 1) hold 'N' run breaks: each run is shorter than 2^31, so
-    the reference's int32 seqSize (findKmer.cpp:977) never wraps."""
-    w, start = 0, 0
+def _runs(total, chrom):
+    if not chrom:
+        return [total]
+    out, start = [], 0
     for b in range(chrom, total, chrom):
-        w += run_windows(b - start, k)
+        out.append(b - start)
         start = b + 1
-    return w + run_windows(total - start, k)
+    return out + [total - start]
+
+
+def expected_windows(total, k, chrom):
+    """Windows in a stream of `total` bases with 'N' at j*chrom (j >= 1)"""
+    return sum(run_windows(r, k) for r in _runs(total, chrom))
 
 
 def want_valid(total, k, chrom):
-    """baseCounter of the same stream: every base of a run of >= k bases
-    (findKmer.cpp:1040, :1056; runs are shorter than 2^31 here)"""
-    if not chrom:
-        return total if total >= k else 0
-    v, start = 0, 0
-    for b in range(chrom, total, chrom):
-        v += (b - start) if b - start >= k else 0
-        start = b + 1
-    return v + ((total - start) if total - start >= k else 0)
+    """baseCounter of the same stream when no run reaches 2^31 bases: every
+    base of a run of >= k bases (findKmer.cpp:1040, :1056)"""
+    return sum(r for r in _runs(total, chrom) if r >= k)
 
 
-def main():
-    args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+# ---------------------------------------------------------------- baselines
+
+def cpu_baseline(k, seed, fasta_line, n_sample):
+    """The reference CPU loop (oracle/_ref/findKmer_ref, the reference
+    program compiled from its source) on a bounded prefix of the same stream."""
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    import oracle   # checker / baseline only
+    data = oracle.synth(n_sample, seed, fasta_line)
+    ref = oracle.REF_BIN
+    if os.path.exists(ref) and os.access(ref, os.X_OK):
+        with tempfile.TemporaryDirectory() as td:
+            p = os.path.join(td, "sample.fa")
+            data.tofile(p)
+            t0 = time.perf_counter()
+            subprocess.run([ref, "-q", "1", "-k", str(k), "-p", "sample.fa"], cwd=td,
+                           stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+            dt = time.perf_counter() - t0
+        kind = "reference"
+        what = (f"oracle/_ref/findKmer_ref (reference findKmer.cpp, g++ -O3, single thread) "
+                f"end-to-end on the first {n_sample} bases of the same stream, k={k}")
+    else:
+        t0 = time.perf_counter()
+        oracle.count_dense(data, k)
+        dt = time.perf_counter() - t0
+        kind = "port"
+        what = f"oracle port (fk_oracle.c, 1 thread) on the first {n_sample} bases, k={k}"
+    return {"value": n_sample / dt, "unit": "bases/s", "cores": 1, "kind": kind,
+            "sample": what, "seconds": round(dt, 3)}
+
+
+def cpu_baseline_multicore(k, seed, fasta_line, n_sample):
+    """BASELINE.md's "fast CPU": the oracle's dense-table scan split over the
+    host threads this process may use (fko_count_dense_par, 16 on the GPU
+    box), on a bounded prefix of the same stream, input in host memory."""
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    import oracle
+    data = oracle.synth(n_sample, seed, fasta_line)
+    th = oracle.host_threads()
+    oracle.count_dense(data[: 1 << 20], k, threads=th)       # page in the library
+    t0 = time.perf_counter()
+    oracle.count_dense(data, k, threads=th)
+    dt = time.perf_counter() - t0
+    cpu = ""
+    try:
+        cpu = next(l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name"))
+    except Exception:
+        pass
+    return {"value": n_sample / dt, "unit": "bases/s", "cores": th, "kind": "port",
+            "sample": f"fko_count_dense_par (dense u32 table, {th} threads) on the first {n_sample} bases "
+                      f"of the same stream, k={k}; host CPU {cpu}, os.cpu_count()={os.cpu_count()}",
+            "seconds": round(dt, 3)}
+
+
+# ---------------------------------------------------------------- one workload
+
+class Ctx:
+    def __init__(self, args, world, rank, local, dist, coll_dev):
+        self.args, self.world, self.rank, self.local, self.dist, self.coll_dev = \
+            args, world, rank, local, dist, coll_dev
+
+
+def measure(ctx, k, n, L, seed, chrom, steps, warmup, verify=False):
+    """Time `steps` passes of the hot path over this rank's shard of the
+    stream (n bases per rank).  Returns the record (rank 0's view)."""
     import torch
     import findkmer_amd as fk
     import findkmer_amd.dist as fkdist
-    # a gloo rehearsal may put several ranks on one GPU
-    local = local % max(1, torch.cuda.device_count())
-    torch.cuda.set_device(local)
-    dist = None
-    # under torch.distributed.run (WORLD_SIZE set, even to 1) the sharded
-    # pass with its exchange runs; `python bench.py` at N=1 feeds directly
-    sharded = world > 1 or "WORLD_SIZE" in os.environ
-    if sharded:
-        import torch.distributed as dist
-        if args.dist_backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        else:
-            dist.init_process_group("gloo")
-    k = args.k
-    n = args.bases
-    L = args.fasta_line
-    assert n % 1280 == 0, "--bases must be a multiple of 1280 (32-base generator words, 80-col lines)"
-
-    # this rank's shard of one stream: bases [rank*n, (rank+1)*n), plus the
-    # bytes just before it (halo) so the engine can guess the entry state
+    args, world, rank, dist = ctx.args, ctx.world, ctx.rank, ctx.dist
+    sharded = dist is not None
+    assert n % 32 == 0 and (L <= 0 or n % L == 0), \
+        "--bases: a multiple of 32 (generator words) and of the FASTA line width"
+    # this rank's shard: bases [rank*n, (rank+1)*n) plus the bytes just before
+    # it (halo) so the engine can guess the entry state
     halo_bases = 0 if rank == 0 else (1280 if L > 0 else 256)
     first = rank * n - halo_bases
-    if L > 0:
-        halo = halo_bases + halo_bases // L
-        frame = L if rank == 0 else -L
-        size = fk.synth_size(n + halo_bases, frame)
-    else:
-        halo = halo_bases
-        frame = 0
-        size = n + halo_bases
-    buf = torch.empty(size + 64, dtype=torch.uint8, device="cuda")
-    w = fk.synth_device(buf.data_ptr(), size, n + halo_bases, args.seed + first // 32, frame)
-    assert w == size
+    chrom_on = chrom > 0 and world * n > chrom
+    buf, size = make_genome(n + halo_bases, L, seed, chrom if chrom_on else 0, first, rank == 0)
+    halo = base_offset(first + halo_bases, first, L, rank == 0) - (HEADER if (L > 0 and rank == 0) else 0)
     nbytes = size - halo
-    # one N-GB stream as a genome of CHROM-base chromosomes: an 'N' at every
-    # base index that is a multiple of CHROM (as in real genomes, no run
-    # reaches the reference's int32 seqSize wrap at 2^31 bases).  FASTA
-    # framing: single-GPU streams only (base b sits at byte 11 + b + b // L).
-    chrom_breaks = args.chrom > 0 and world * n > args.chrom and (L == 0 or world == 1)
-    if chrom_breaks:
-        for b in range((max(first, 0) // args.chrom + 1) * args.chrom, first + n + halo_bases, args.chrom):
-            off = b - first if L == 0 else 11 + b + b // L
-            assert chr(buf[off].item()) in "ACGT", (b, off)
-            buf[off] = ord("N")
     torch.cuda.synchronize()
 
-    # the count kernel's HIP events on every 4th step of the timed region
-    # (recording them on every launch costs ~2% of the step)
-    eng = fk.Engine(k, device=local, timing_every=args.timing_every)
-    coll_dev = "cuda" if args.dist_backend == "nccl" else "cpu"
-    merge_t = fkdist.merge_buffer(k, coll_dev) if sharded else None
-    pinned = torch.empty(fkdist.COUNTER_SLOTS, dtype=torch.int32, pin_memory=True) if coll_dev == "cuda" else None
+    eng = fk.Engine(k, device=ctx.local, timing_every=args.timing_every)
+    merge_t = fkdist.merge_buffer(k, ctx.coll_dev) if sharded else None
+    pinned = torch.empty(fkdist.COUNTER_SLOTS, dtype=torch.int32, pin_memory=True) \
+        if (sharded and ctx.coll_dev == "cuda") else None
+    phase_s = {}
 
     def step():
         eng.reset()
         if sharded:
-            # shard, stitch entry states (all-gather of 96-B summaries), merge
-            # tables + counters (reduce to rank 0): findkmer_amd/dist.py
             res = fkdist.count_sharded(eng, buf.data_ptr() + halo, nbytes, halo, merge_t, times=phase_s,
                                        pinned=pinned, fast=not args.stitched, native=not args.torch_exchange)
             return res.local, res
@@ -194,8 +233,7 @@ def main():
         rc, r = eng.finish(allow=(fk.FK_OK, fk.FK_E_ROLLOVER) if os.environ.get("FINDKMER_LIB") else (fk.FK_OK,))
         return r, None
 
-    phase_s = {}
-    for _ in range(args.warmup):
+    for _ in range(warmup):
         step()
     phase_s.clear()
     if dist:
@@ -204,7 +242,7 @@ def main():
     t0 = time.perf_counter()
     last = merged = None
     main_ms, timed = 0.0, 0
-    for _ in range(args.steps):
+    for _ in range(steps):
         last, merged = step()
         main_ms += last.main_kernel_ms
         timed += last.timed_kernels
@@ -212,83 +250,170 @@ def main():
     if dist:
         dist.barrier()
     dt = time.perf_counter() - t0
+    kern_ms = main_ms / timed if timed else 0.0   # mean over the timed launches of the timed region
     if dist:
-        tt = torch.tensor([dt], dtype=torch.float64, device=coll_dev)
+        tt = torch.tensor([dt, kern_ms], dtype=torch.float64, device=ctx.coll_dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        dt = float(tt.item())
+        dt, kern_ms = float(tt[0].item()), float(tt[1].item())
 
-    # correctness guard on the measured pass: the synthetic stream (pure ACGT,
-    # or FASTA whose '\n' are transparent) is one run, every window counts
+    # correctness guard on the measured pass (the merged result lives on rank 0)
     if not os.environ.get("FINDKMER_LIB") and rank == 0:
-        # the merged counters and table live on rank 0 (dist.reduce)
         total = merged.windows if merged is not None else last.windows
         if merged is not None:
             assert merged.status() == fk.FK_OK, "merged table: rollover or unterminated header"
-            if chrom_breaks or world * n < (1 << 31):   # no run reaches the int32 seqSize wrap
-                assert merged.valid_bases == want_valid(world * n, k, args.chrom if chrom_breaks else 0)
-        want = expected_windows(world * n, k, args.chrom) if chrom_breaks else run_windows(world * n, k)
+        valid = merged.valid_bases if merged is not None else last.valid_bases
+        if chrom_on and chrom < (1 << 31):
+            assert valid == want_valid(world * n, k, chrom), (valid, want_valid(world * n, k, chrom))
+        want = expected_windows(world * n, k, chrom if chrom_on else 0)
         assert total == want, (total, want)
 
-    ms_step = dt / args.steps * 1e3
-    value = world * n / (dt / args.steps)
-    kern_ms = main_ms / timed if timed else 0.0   # mean over the timed launches of the timed region
+    check = None
+    if verify:
+        check = verify_single(ctx, k, n, L, seed, chrom if chrom_on else 0, merged, last)
+
+    ms_step = dt / steps * 1e3
     algo_bytes = nbytes + 4 * (1 << (2 * k))       # input read once + u32 table written once
     achieved = algo_bytes / (kern_ms * 1e-3) / 1e9 if kern_ms > 0 else 0.0   # 0: events off (FK_NO_EVENTS)
-    traffic = None
-    tf = os.path.join(REPO, "profiles", f"traffic_k{k}_L{L}.json")
-    if os.path.exists(tf):
-        try:
-            prof = json.load(open(tf))
-            # only a profile of this exact workload size describes this launch
-            if prof.get("input_bytes") == nbytes:
-                traffic = prof.get("hbm_bytes_per_launch")
-        except Exception:
-            traffic = None
+    step_gbs = algo_bytes / (ms_step * 1e-3) / 1e9
+    main = "k_part" if 8 <= k <= 12 else "k_count"
+    rec = {
+        "value": world * n / (dt / steps),
+        "ms_per_step": ms_step,
+        "workload": (f"k={k} over a {n / 1e9:g} G-base synthetic "
+                     + ("ACGT stream" if L == 0 else f"FASTA genome ({L}-col lines)") + " per GPU"
+                     + (f", {args.chrom / 1e9:g} G-base chromosomes" if chrom_on else ", one run")),
+        "k": k, "bases_per_gpu": n, "input_bytes_per_gpu": nbytes,
+        "roofline": {
+            "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS, "traffic": traffic_for(k, L, nbytes, main),
+            "kernel": main, "kernel_ms": kern_ms, "timed_launches": timed,
+            "algorithmic_bytes": algo_bytes,
+            "step_achieved": step_gbs, "step_frac": step_gbs / HBM_PEAK_GBS,
+        },
+    }
+    if phase_s:
+        rec["phase_ms_per_step"] = {k_: v / steps * 1e3 for k_, v in phase_s.items()}
+    if merged is not None:
+        rec["exchange"] = merged.path
+        rec["transport"] = merged.transport
+    if check is not None:
+        rec["verify"] = check
+    eng.close()
+    del buf, merge_t
+    torch.cuda.empty_cache()
+    return rec
+
+
+def traffic_for(k, L, nbytes, main):
+    """HBM bytes per launch of the dominant kernel from the committed PMC
+    profile of this exact workload (profiles/traffic_k<K>_L<L>_n<bytes>.json,
+    written by tools/profile_summary.py), else None."""
+    tf = os.path.join(REPO, "profiles", f"traffic_k{k}_L{L}_n{nbytes}.json")
+    try:
+        prof = json.load(open(tf))
+    except Exception:
+        return None
+    if prof.get("input_bytes") == nbytes and prof.get("kernel") == main:
+        return prof.get("hbm_bytes_per_launch")
+    return None
+
+
+def verify_single(ctx, k, n, L, seed, chrom, merged, last):
+    """configs[3] parity: rank 0 counts the whole world x n stream with one
+    engine and compares it with the sharded pass's merged table and counters."""
+    import numpy as np
+    import torch
+    import findkmer_amd as fk
+    if ctx.rank != 0:
+        return None
+    buf, size = make_genome(ctx.world * n, L, seed, chrom)
+    torch.cuda.synchronize()
+    with fk.Engine(k, device=ctx.local) as e:
+        e.feed_device(buf.data_ptr(), size)
+        rc, r = e.finish()
+        t = e.table()
+    del buf
+    torch.cuda.empty_cache()
+    if merged is None:
+        raise SystemExit("--verify-single needs a sharded run (torchrun)")
+    got = merged.table.cpu().numpy().view(np.uint32)
+    out = {"table_equal": bool(np.array_equal(got, t)), "status": rc}
+    for key in ("windows", "valid_bases", "unknown_chars", "scanned_bytes", "hit_eof_byte",
+                "unterminated_header", "distinct"):
+        out[key] = [int(getattr(merged, key)), int(getattr(r, key))]
+    out["base_count"] = [list(merged.base_count), list(r.base_count)]
+    out["depth1"] = [list(merged.depth1), list(r.depth1)]
+    return out
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    import findkmer_amd.dist as fkdist
+    # a gloo rehearsal may put several ranks on one GPU
+    local = local % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(local)
+    dist = None
+    # under torch.distributed.run (WORLD_SIZE set, even to 1) the sharded
+    # pass with its exchange runs; `python bench.py` at N=1 feeds directly
+    if world > 1 or "WORLD_SIZE" in os.environ:
+        import torch.distributed as dist
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
+    coll_dev = "cuda" if args.dist_backend == "nccl" else "cpu"
+    ctx = Ctx(args, world, rank, local, dist, coll_dev)
+
+    head = measure(ctx, args.k, args.bases, args.fasta_line, args.seed, args.chrom, args.steps, args.warmup,
+                   verify=args.verify_single)
+    ns = None
+    if args.north_star_bases > 0:
+        ns = measure(ctx, 6, args.north_star_bases, 0, 1, CHROM, args.steps, args.warmup)
+        ns["gate"] = "k=6 over a 10 GB synthetic genome at >= 70% of single-GPU HBM-read roofline (BASELINE.json)"
+
+    cfg_tag = {(11, 80, 10_000_000_000): " (BASELINE.json configs[2])",
+               (6, 0, 1_000_000_000): " (BASELINE.json configs[1])"}.get((args.k, args.fasta_line, args.bases), "")
+    if world > 1 and (args.k, args.fasta_line) == (11, 80):
+        cfg_tag = f" (BASELINE.json configs[3] layout, weak scaling: {args.bases / 1e9:g} G bases per GPU)"
     out = {
         "metric": METRIC,
-        "value": value,
+        "value": head["value"],
         "unit": "bases/s",
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": ms_step,
+        "ms_per_step": head["ms_per_step"],
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "u8",
-        "data": "synthetic (splitmix64 uniform ACGT, generated in HBM)",
+        "data": "synthetic (splitmix64 uniform ACGT genome, generated in HBM)",
         "config": {
-            "workload": (f"k={k} over a {n / 1e9:g} G-base synthetic "
-                         + ("ACGT stream" if L == 0 else f"FASTA ({L}-col lines)") + " per GPU"
-                         + (f", one {world * n / 1e9:g} G-base genome of {args.chrom / 1e9:g} G-base chromosomes"
-                            if chrom_breaks else "")
-                         + (" (BASELINE.json configs[1])" if (k, L, n) == (6, 0, 1_000_000_000) else "")),
-            "k": k, "bases_per_gpu": n, "input_bytes_per_gpu": nbytes,
+            "workload": head["workload"] + cfg_tag,
+            "k": args.k, "bases_per_gpu": args.bases, "input_bytes_per_gpu": head["input_bytes_per_gpu"],
             "parallelism": f"shard{world}",
         },
-        "roofline": {
-            "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-            "kernel": "k_part" if 8 <= k <= 12 else "k_count", "kernel_ms": kern_ms, "timed_launches": timed,
-            "algorithmic_bytes": algo_bytes,
-        },
+        "roofline": head["roofline"],
     }
-    if phase_s:
-        # rank 0's host time per step in each phase of the sharded pass
-        out["phase_ms_per_step"] = {k_: v / args.steps * 1e3 for k_, v in phase_s.items()}
-    if merged is not None:
-        # "fast": one all-reduce of tables + counters + shard summaries;
-        # "stitched": summary all-gather, then a reduce (findkmer_amd/dist.py)
-        out["exchange"] = merged.path
-        out["transport"] = merged.transport
+    for key in ("phase_ms_per_step", "exchange", "transport", "verify"):
+        if key in head:
+            out[key] = head[key]
+    if ns is not None:
+        out["north_star"] = {key: ns[key] for key in ("workload", "gate", "value", "ms_per_step", "roofline",
+                                                       "exchange", "transport") if key in ns}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         # ~15 s of reference CPU work: ~76 Mbases/s at k=6, ~3 Mbases/s at k=11
-        sample = args.cpu_sample_bytes or (1 << 30 if k <= 7 else 48 << 20)
-        sample = min(sample, n)
-        out["cpu_baseline"] = cpu_baseline(args, sample)
+        sample = args.cpu_sample_bytes or (1 << 30 if args.k <= 7 else 48 << 20)
+        sample = min(sample, args.bases)
+        out["cpu_baseline"] = cpu_baseline(args.k, args.seed, args.fasta_line, sample)
+        out["cpu_baseline_multicore"] = cpu_baseline_multicore(args.k, args.seed, args.fasta_line,
+                                                               min(1 << 30, args.bases))
     if rank == 0:
         print(json.dumps(out), flush=True)
-    eng.close()
     if dist:
         fkdist.close_native_comms()
         dist.destroy_process_group()

@@ -4261,6 +4261,7 @@ extern "C" int fk_summary_is_full(const fk_summary *s) {
 
 extern "C" int fk_summary_apply(const fk_summary *s, const fk_state *in, fk_state *out) {
     if (!s || !in || !out) return FK_E_INVALID;
+    if (in->ended > 1) return FK_E_INVALID;   /* 0 or 1 only (the field was padding before ABI 1.1) */
     if (in->ended) {           /* absorbing: the stream ended before this span */
         *out = *in;
         return FK_OK;
@@ -4286,10 +4287,13 @@ extern "C" int fk_summary_apply(const fk_summary *s, const fk_state *in, fk_stat
 extern "C" int fk_engine_resolve(fk_engine *e, const fk_state *entering) {
     if (!e || !entering) return FK_E_INVALID;
     if (!e->shard_pending) return FK_E_STATE;
+    /* `ended` is 0 or 1: a caller that left the old padding word
+       uninitialised gets an error, not a silently dropped shard */
+    if (entering->ended > 1) return FK_E_INVALID;
     int rc = set_dev(e);
     if (rc) return rc;
     XState in{entering->run, fk_sigma(entering->code), entering->hdr, 0};
-    if (entering->ended) {
+    if (entering->ended == 1) {
         /* the stream ended before this shard (a 0xFF byte in an earlier one,
            :988): it counts nothing; the pending count is zeroed lazily */
         const uint64_t len = e->shard_len;
@@ -4447,12 +4451,15 @@ extern "C" int fk_engine_shard_pack(fk_engine *e, uint32_t *table, int32_t *coun
     return FK_OK;
 }
 
-/* The gathered rows to pinned host memory, sequence number last (one wave,
-   one system fence; the host spins on it, as on the result block). */
+/* The gathered rows to pinned host memory, sequence number last (one block,
+   one system fence per thread, then a block barrier before thread 0's
+   release store: every thread's row stores are ordered before the sequence
+   number the host spins on, whatever the block size). */
 __global__ void __launch_bounds__(64) k_rows_publish(const uint32_t *rows, uint32_t n, uint32_t *host, uint32_t seq) {
-    for (uint32_t i = threadIdx.x; i < n; i += 64) host[32 + i] = rows[i];
+    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) host[32 + i] = rows[i];
     __threadfence_system();
-    if (threadIdx.x == 0) __hip_atomic_store(&host[0], seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store(&host[0], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 /* One row of a rows region (zeros elsewhere): words [0, nsrc) from src (a

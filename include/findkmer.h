@@ -69,7 +69,9 @@ enum {
  * first base most significant; `hdr` = inside a '>' comment line; `ended` = a
  * 0xFF byte outside a header already ended the stream (the reference's
  * signed-char EOF test, findKmer.cpp:988): an absorbing state, nothing after
- * it counts. */
+ * it counts.  `ended` must be 0 or 1 (it was a padding word before): any
+ * other value makes fk_engine_resolve / fk_summary_apply return
+ * FK_E_INVALID. */
 typedef struct {
     uint64_t run;
     uint64_t code;

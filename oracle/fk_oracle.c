@@ -30,16 +30,18 @@
 #include <stdlib.h>
 #include <string.h>
 
-static inline int base2code(uint8_t c) {          /* :567-589 */
-    switch (c) {
-    case 'A': return 0;
-    case 'C': return 1;
-    case 'G': return 2;
-    case 'T': return 3;
-    case 'N': return -2;
-    default:  return -1;
-    }
-}
+/* base2int (:567-589) as a table: A0 C1 G2 T3, 'N' -2, any other byte -1 */
+#pragma GCC diagnostic push
+#pragma GCC diagnostic ignored "-Woverride-init"
+static const signed char B2C[256] = {
+    [0 ... 255] = -1, ['A'] = 0, ['C'] = 1, ['G'] = 2, ['T'] = 3, ['N'] = -2,
+};
+/* bytes that neither break a run nor start a comment: the bases and '\n' */
+static const unsigned char BASE_OR_NL[256] = {
+    [0 ... 255] = 0, ['A'] = 1, ['C'] = 1, ['G'] = 1, ['T'] = 1, ['\n'] = 1,
+};
+#pragma GCC diagnostic pop
+static inline int base2code(uint8_t c) { return B2C[c]; }
 
 /* Short trie walks that never reached depth k leave prefix nodes behind
  * (:1059-1062).  They matter only for nodeCounter; we record each maximal
@@ -65,14 +67,20 @@ static int short_push(short_list *s, uint64_t code, int len) {
 /* Core scan.  emit(code) is called once per counted window. */
 typedef void (*emit_fn)(void *ctx, uint64_t code);
 
-static int scan(const uint8_t *buf, uint64_t len, int k, emit_fn emit,
+/* The scan's state between bytes (the reference's locals of findKmer(),
+ * :966-977): inside a comment line, seqSize, the window, and whether a walk
+ * of 1..k-1 bases is open.  The stream starts from all zeros. */
+typedef struct { int in_hdr; int32_t seq; uint64_t code; int short_open; } scan_state;
+
+/* always inlined: each caller's emit() is inlined into its own copy */
+static inline __attribute__((always_inline)) int scan(const uint8_t *buf, uint64_t len, int k, emit_fn emit,
                 void *ctx, fko_result *res, short_list *shorts,
-                uint8_t *unknown_out, uint64_t unknown_cap) {
+                uint8_t *unknown_out, uint64_t unknown_cap, const scan_state *init) {
     const uint64_t mask = (k >= 32) ? ~0ull : ((1ull << (2 * k)) - 1);
-    int in_hdr = 0;
-    int32_t seq = 0;          /* seqSize, int at :977; wraps like the ref */
-    uint64_t code = 0;        /* last k bases, first base most significant */
-    int short_open = 0;       /* a walk of length 1..k-1 is in progress */
+    int in_hdr = init ? init->in_hdr : 0;
+    int32_t seq = init ? init->seq : 0;   /* seqSize, int at :977; wraps like the ref */
+    uint64_t code = init ? init->code : 0; /* last k bases, first base most significant */
+    int short_open = init ? init->short_open : 0;   /* a walk of length 1..k-1 is in progress */
     memset(res, 0, sizeof(*res));
     uint64_t i = 0;
     for (; i < len; i++) {
@@ -143,7 +151,7 @@ static int scan(const uint8_t *buf, uint64_t len, int k, emit_fn emit,
 
 typedef struct { uint32_t *counts; } dense_ctx;
 
-static void dense_emit(void *ctx, uint64_t code) {
+static inline void dense_emit(void *ctx, uint64_t code) {
     ((dense_ctx *)ctx)->counts[code]++;
 }
 
@@ -181,7 +189,7 @@ int fko_count_dense(const uint8_t *buf, uint64_t len, int k, uint32_t *counts,
     memset(counts, 0, n * sizeof(uint32_t));
     dense_ctx ctx = { counts };
     short_list s = { 0, 0, 0 };
-    if (scan(buf, len, k, dense_emit, &ctx, res, &s, unknown_out, unknown_cap)) {
+    if (scan(buf, len, k, dense_emit, &ctx, res, &s, unknown_out, unknown_cap, NULL)) {
         free(s.v);
         return -1;
     }
@@ -192,6 +200,222 @@ int fko_count_dense(const uint8_t *buf, uint64_t len, int k, uint32_t *counts,
     res->nodes = dense_nodes(counts, k, &s, any_walk);
     free(s.v);
     return 0;
+}
+
+/* ---------------- dense form, split over threads ----------------
+ *
+ * The same scan cut into contiguous pieces, each scanned from its exact
+ * entering state (scan_state), the results summed in stream order.  Exact
+ * for any input: the entering state at a cut q is derived from the bytes
+ * before q by the reference's own rules --
+ *   j = the last byte before q that is not A/C/G/T/'\n' (:1011, :1019);
+ *   j inside a comment line (a '>' earlier on its line, or j itself is '>',
+ *   :991-1008): the comment ends at the next '\n' (state hdr=0, seqSize=0
+ *   after it), or q is still inside it (hdr=1);
+ *   else j broke the run (:1019-1024): seqSize=0 after j;
+ *   no such j: the stream's initial state at byte 0;
+ * then seqSize = the bases from there to q (mod 2^32, :977/:1029), the
+ * window = the last of them, and a short walk is open iff 0 < seqSize < k
+ * (:1059-1062).  A piece whose predecessor hit a 0xFF byte (:988) is
+ * dropped.  Only the cost is parallel; the rules are scan()'s. */
+#include <pthread.h>
+#ifdef __SSE2__
+#include <emmintrin.h>
+#endif
+
+/* j <= q with buf[j..q) all bases or '\n', j as small as possible */
+static uint64_t back_over_bases(const uint8_t *buf, uint64_t q) {
+    uint64_t j = q;
+#ifdef __SSE2__
+    const __m128i A = _mm_set1_epi8('A'), C = _mm_set1_epi8('C'), G = _mm_set1_epi8('G'),
+                  T = _mm_set1_epi8('T'), NL = _mm_set1_epi8('\n');
+    while (j >= 16) {
+        __m128i v = _mm_loadu_si128((const __m128i *)(buf + j - 16));
+        __m128i m = _mm_or_si128(_mm_or_si128(_mm_cmpeq_epi8(v, A), _mm_cmpeq_epi8(v, C)),
+                                 _mm_or_si128(_mm_or_si128(_mm_cmpeq_epi8(v, G), _mm_cmpeq_epi8(v, T)),
+                                              _mm_cmpeq_epi8(v, NL)));
+        if (_mm_movemask_epi8(m) != 0xFFFF) break;
+        j -= 16;
+    }
+#endif
+    while (j > 0 && BASE_OR_NL[buf[j - 1]]) j--;
+    return j;
+}
+
+/* the '\n' bytes in [p, q) */
+static uint64_t count_nl(const uint8_t *buf, uint64_t p, uint64_t q) {
+    uint64_t n = 0, x = p;
+#ifdef __SSE2__
+    const __m128i NL = _mm_set1_epi8('\n');
+    for (; x + 16 <= q; x += 16)
+        n += (uint64_t)__builtin_popcount((unsigned)_mm_movemask_epi8(
+                 _mm_cmpeq_epi8(_mm_loadu_si128((const __m128i *)(buf + x)), NL)));
+#endif
+    for (; x < q; x++) n += buf[x] == '\n';
+    return n;
+}
+
+
+static void entry_state(const uint8_t *buf, uint64_t q, int k, scan_state *st) {
+    memset(st, 0, sizeof(*st));
+    uint64_t p = 0;                     /* state (hdr 0, seqSize 0) at p */
+    uint64_t j = back_over_bases(buf, q);
+    if (j > 0) {
+        uint64_t b = j - 1;             /* the last breaker before q */
+        int hdr = buf[b] == '>';
+        for (uint64_t x = b; !hdr && x > 0 && buf[x - 1] != '\n'; x--)
+            if (buf[x - 1] == '>') hdr = 1;
+        if (hdr) {
+            uint64_t e = b + 1;
+            while (e < q && buf[e] != '\n') e++;
+            if (e >= q) { st->in_hdr = 1; return; }
+            p = e + 1;
+        } else {
+            p = b + 1;
+        }
+    }
+    /* [p, q) holds only bases and '\n': seqSize = its bases, the window =
+     * the last k of them */
+    uint64_t R = q - p - count_nl(buf, p, q), code = 0;
+    int got = 0;
+    for (uint64_t x = q; x > p && got < k; x--) {
+        if (buf[x - 1] == '\n') continue;
+        code |= (uint64_t)base2code(buf[x - 1]) << (2 * got++);
+    }
+    st->seq = (int32_t)(uint32_t)R;
+    st->code = code;
+    st->short_open = st->seq > 0 && st->seq < k;
+}
+
+typedef struct {
+    const uint8_t *buf;
+    uint64_t lo, hi;
+    int k;
+    uint32_t *counts;
+    fko_result res;
+    short_list shorts;
+    uint8_t *unknown;
+    uint64_t unknown_cap;
+    int rc;
+} piece_t;
+
+static void *piece_run(void *arg) {
+    piece_t *p = (piece_t *)arg;
+    scan_state st;
+    entry_state(p->buf, p->lo, p->k, &st);
+    dense_ctx ctx = { p->counts };
+    /* counters on this thread's stack: the pieces' records share cache lines */
+    fko_result res;
+    short_list shorts = { 0, 0, 0 };
+    int rc = scan(p->buf + p->lo, p->hi - p->lo, p->k, dense_emit, &ctx, &res, &shorts,
+                  p->unknown, p->unknown_cap, p->lo ? &st : NULL);
+    p->res = res;
+    p->shorts = shorts;
+    p->rc = rc;
+    return NULL;
+}
+
+typedef struct { uint32_t *dst; uint32_t **src; int nsrc; uint64_t lo, hi; } sum_t;
+
+static void *sum_run(void *arg) {
+    sum_t *s = (sum_t *)arg;
+    for (int t = 0; t < s->nsrc; t++)
+        for (uint64_t i = s->lo; i < s->hi; i++) s->dst[i] += s->src[t][i];   /* u32, wraps like :110 */
+    return NULL;
+}
+
+int fko_count_dense_par(const uint8_t *buf, uint64_t len, int k, uint32_t *counts,
+                        fko_result *res, uint8_t *unknown_out, uint64_t unknown_cap, int threads) {
+    if (k < 1 || k > 13) return -1;
+    if (threads < 1) threads = 1;
+    if ((uint64_t)threads > len / 4096 + 1) threads = (int)(len / 4096 + 1);
+    if (threads == 1) return fko_count_dense(buf, len, k, counts, res, unknown_out, unknown_cap);
+    const uint64_t n = 1ull << (2 * k);
+    piece_t *pc = (piece_t *)calloc((size_t)threads, sizeof(piece_t));
+    pthread_t *th = (pthread_t *)calloc((size_t)threads, sizeof(pthread_t));
+    int rc = -1;
+    if (!pc || !th) goto out;
+    for (int t = 0; t < threads; t++) {
+        pc[t].buf = buf;
+        pc[t].lo = len * (uint64_t)t / (uint64_t)threads;
+        pc[t].hi = len * (uint64_t)(t + 1) / (uint64_t)threads;
+        pc[t].k = k;
+        pc[t].counts = t ? (uint32_t *)calloc(n, sizeof(uint32_t)) : counts;
+        if (!pc[t].counts) goto out;
+        if (unknown_out && unknown_cap) {
+            pc[t].unknown = (uint8_t *)malloc(unknown_cap);
+            if (!pc[t].unknown) goto out;
+            pc[t].unknown_cap = unknown_cap;
+        }
+    }
+    memset(counts, 0, n * sizeof(uint32_t));
+    for (int t = 0; t < threads; t++) pthread_create(&th[t], NULL, piece_run, &pc[t]);
+    for (int t = 0; t < threads; t++) pthread_join(th[t], NULL);
+    for (int t = 0; t < threads; t++) if (pc[t].rc) goto out;
+    /* pieces after the first that met a 0xFF byte outside a comment never
+     * happen in the reference (:988): drop them */
+    int used = threads;
+    for (int t = 0; t < threads; t++)
+        if (pc[t].res.hit_eof_byte) { used = t + 1; break; }
+    {
+        uint32_t **src = (uint32_t **)calloc((size_t)threads, sizeof(uint32_t *));
+        if (!src) goto out;
+        for (int t = 1; t < used; t++) src[t - 1] = pc[t].counts;
+        sum_t *sm = (sum_t *)calloc((size_t)threads, sizeof(sum_t));
+        if (!sm) { free(src); goto out; }
+        for (int t = 0; t < threads; t++) {
+            sm[t].dst = counts; sm[t].src = src; sm[t].nsrc = used - 1;
+            sm[t].lo = n * (uint64_t)t / (uint64_t)threads;
+            sm[t].hi = n * (uint64_t)(t + 1) / (uint64_t)threads;
+            pthread_create(&th[t], NULL, sum_run, &sm[t]);
+        }
+        for (int t = 0; t < threads; t++) pthread_join(th[t], NULL);
+        free(sm);
+        free(src);
+    }
+    memset(res, 0, sizeof(*res));
+    short_list all = { 0, 0, 0 };
+    uint64_t nunk = 0;
+    for (int t = 0; t < used; t++) {
+        const fko_result *r = &pc[t].res;
+        for (int b = 0; b < 4; b++) {
+            res->base_count[b] += r->base_count[b];
+            res->depth1[b] += r->depth1[b];
+        }
+        res->valid_bases += r->valid_bases;
+        res->windows += r->windows;
+        for (uint64_t u = 0; u < r->unknown_chars && unknown_out && nunk + u < unknown_cap && u < unknown_cap; u++)
+            unknown_out[nunk + u] = pc[t].unknown[u];
+        nunk += r->unknown_chars;
+        for (uint64_t s = 0; s < pc[t].shorts.n; s++)
+            if (short_push(&all, pc[t].shorts.v[s].code, pc[t].shorts.v[s].len)) { free(all.v); goto out; }
+        if (t == used - 1) {
+            res->scanned_bytes = pc[t].lo + r->scanned_bytes;
+            res->hit_eof_byte = r->hit_eof_byte;
+            res->unterminated_header = r->unterminated_header;
+        }
+    }
+    res->unknown_chars = nunk;
+    for (int b = 0; b < 4; b++)
+        if (res->depth1[b] >= (1ull << 32)) res->rollover = 1;
+    uint64_t distinct = 0;
+    for (uint64_t i = 0; i < n; i++) distinct += counts[i] != 0;
+    res->distinct = distinct;
+    uint64_t any_walk = res->depth1[0] | res->depth1[1] | res->depth1[2] | res->depth1[3];
+    res->nodes = dense_nodes(counts, k, &all, any_walk);
+    free(all.v);
+    rc = 0;
+out:
+    if (pc) {
+        for (int t = 0; t < threads; t++) {
+            if (t && pc[t].counts) free(pc[t].counts);
+            free(pc[t].unknown);
+            free(pc[t].shorts.v);
+        }
+    }
+    free(pc);
+    free(th);
+    return rc;
 }
 
 /* ---------------- sparse form ---------------- */
@@ -221,7 +445,7 @@ int fko_count_sparse(const uint8_t *buf, uint64_t len, int k, uint64_t *codes,
     if (k < 1 || k > 20) return -1;
     vec_ctx ctx = { 0, 0, 0, 0 };
     short_list s = { 0, 0, 0 };
-    int rc = scan(buf, len, k, vec_emit, &ctx, res, &s, NULL, 0);
+    int rc = scan(buf, len, k, vec_emit, &ctx, res, &s, NULL, 0, NULL);
     if (rc || ctx.fail) { free(ctx.v); free(s.v); return -1; }
     qsort(ctx.v, ctx.n, sizeof(uint64_t), cmp_u64);
     uint64_t u = 0;

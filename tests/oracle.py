@@ -42,6 +42,10 @@ def olib():
         L.fko_count_dense.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int,
                                       ctypes.c_void_p, ctypes.POINTER(FkoResult),
                                       ctypes.c_void_p, ctypes.c_uint64]
+        L.fko_count_dense_par.restype = ctypes.c_int
+        L.fko_count_dense_par.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int,
+                                          ctypes.c_void_p, ctypes.POINTER(FkoResult),
+                                          ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int]
         L.fko_count_sparse.restype = ctypes.c_int
         L.fko_count_sparse.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int,
                                        ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
@@ -61,14 +65,26 @@ def _buf(data):
     return a, len(a)
 
 
-def count_dense(data, k, unknown_cap=0):
-    """Oracle counts: (table uint32[4^k], result, unknown_bytes)."""
+def host_threads():
+    """Threads for the oracle on this host: the GPU box gives a process 16
+    CPUs although os.cpu_count() shows the whole machine's."""
+    return max(1, min(16, os.cpu_count() or 1))
+
+
+def count_dense(data, k, unknown_cap=0, threads=1):
+    """Oracle counts: (table uint32[4^k], result, unknown_bytes).  threads > 1:
+    fko_count_dense_par (the same scan over contiguous pieces, each from its
+    exact entering state)."""
     a, n = _buf(data)
     t = np.zeros(1 << (2 * k), dtype=np.uint32)
     r = FkoResult()
     ub = np.zeros(max(1, unknown_cap), dtype=np.uint8)
-    rc = olib().fko_count_dense(a.ctypes.data, n, k, t.ctypes.data, ctypes.byref(r),
-                                ub.ctypes.data if unknown_cap else None, unknown_cap)
+    if threads > 1:
+        rc = olib().fko_count_dense_par(a.ctypes.data, n, k, t.ctypes.data, ctypes.byref(r),
+                                        ub.ctypes.data if unknown_cap else None, unknown_cap, threads)
+    else:
+        rc = olib().fko_count_dense(a.ctypes.data, n, k, t.ctypes.data, ctypes.byref(r),
+                                    ub.ctypes.data if unknown_cap else None, unknown_cap)
     assert rc == 0
     return t, r, bytes(ub[: min(unknown_cap, r.unknown_chars)])
 

@@ -157,3 +157,46 @@ def test_synth_generator_deterministic():
     assert bytes(a) == bytes(b) and set(bytes(a)) <= set(b"ACGT")
     f = oracle.synth(200, 2, fasta_line=80)
     assert bytes(f[:11]) == b">synthetic\n" and f[11 + 80] == ord("\n")
+
+
+def _cut_inputs():
+    """inputs whose cuts land in every place the entering state depends on:
+    long comment lines (cuts inside one), '>' inside comments, runs shorter
+    than k, N runs, unknown bytes, a 0xFF byte outside a comment, one long run"""
+    import random
+    rng = random.Random(11)
+    out = []
+    for seed in range(3):
+        parts = bytearray()
+        while len(parts) < 400_000:
+            r = rng.random()
+            if r < 0.3:
+                parts += b">" + bytes(rng.choices(b"ACGT>xN\xff", k=rng.randint(0, 30000))) + b"\n"
+            elif r < 0.7:
+                seq = bytes(rng.choices(b"ACGT", k=rng.randint(1, 20000)))
+                w = rng.choice([0, 1, 7, 80])
+                parts += b"\n".join(seq[i:i + w] for i in range(0, len(seq), w)) if w else seq
+            else:
+                parts += bytes(rng.choices(b"ACGTNn\r1\n", k=rng.randint(1, 50)))
+        out.append(bytes(parts))
+    ff = bytearray(out[0])
+    j = ff.rfind(b"\n", 0, 250_000)
+    ff[j + 1] = 0xFF          # line start: outside a comment
+    out.append(bytes(ff))
+    out.append(b"ACGT" * 300_000)
+    out.append(b">" + b"A" * 1_500_000)
+    return out
+
+
+@pytest.mark.parametrize("k", [1, 4, 7, 11])
+def test_oracle_pieces_equal_sequential(k):
+    """fko_count_dense_par (the scan over contiguous pieces, each from the
+    entering state derived from the bytes before its cut) == the sequential
+    scan, for every table bin and every scalar"""
+    for data in _cut_inputs():
+        t1, r1, u1 = oracle.count_dense(data, k, unknown_cap=1 << 20)
+        for th in (2, 5, 16):
+            t2, r2, u2 = oracle.count_dense(data, k, unknown_cap=1 << 20, threads=th)
+            assert np.array_equal(t1, t2)
+            assert bytes(r1) == bytes(r2)
+            assert u1 == u2

@@ -31,6 +31,7 @@ def test_two_rank_shards_gloo(k, fasta, chrom):
     before the shard); bench.py asserts the merged windows and bases"""
     out = _torchrun(2, 29600 + k + chrom % 97, os.path.join(REPO, "bench.py"),
                     ["--gpus", "2", "--steps", "2", "--warmup", "1", "--no-cpu-baseline", "--dist-backend", "gloo",
+                     "--north-star-bases", "0",
                      "--k", str(k), "--fasta-line", str(fasta), "--bases", "12800000", "--chrom", str(chrom)])
     assert out["n_gpus"] == 2 and out["value"] > 0
     # pure ACGT shards with a halo that fixes the state: one all-reduce
@@ -46,9 +47,31 @@ def test_eight_rank_shards_gloo(k, fasta):
     merged counts bench.py asserts, and both exchanges"""
     out = _torchrun(8, 29650 + k, os.path.join(REPO, "bench.py"),
                     ["--gpus", "8", "--steps", "2", "--warmup", "1", "--no-cpu-baseline", "--dist-backend", "gloo",
+                     "--north-star-bases", "0",
                      "--k", str(k), "--fasta-line", str(fasta), "--bases", "12800000", "--chrom", "40000000"])
     assert out["n_gpus"] == 8 and out["value"] > 0
     assert out["exchange"] in (("fast", "stitched") if k <= 7 else ("stitched",))
+
+
+@pytest.mark.gpu
+def test_configs3_eight_ranks_full_size():
+    """BASELINE.json configs[3] at its size: k=11 over one 10 G-base genome
+    (80-column FASTA, 1.5-Gbase chromosomes) cut into 8 shards of 1.25 G
+    bases, eight ranks (gloo, all on cuda:0) through bench.py's sharded pass;
+    rank 0 then counts the whole stream with one engine (--verify-single) and
+    the merged table and every counter must equal it"""
+    out = _torchrun(8, 29690, os.path.join(REPO, "bench.py"),
+                    ["--gpus", "8", "--steps", "1", "--warmup", "0", "--no-cpu-baseline", "--dist-backend", "gloo",
+                     "--north-star-bases", "0", "--k", "11", "--fasta-line", "80", "--bases", "1250000000",
+                     "--verify-single"])
+    assert out["n_gpus"] == 8 and out["exchange"] == "stitched"
+    v = out["verify"]
+    assert v["table_equal"] and v["status"] == 0
+    for key in ("windows", "valid_bases", "base_count", "depth1", "unknown_chars", "scanned_bytes",
+                "hit_eof_byte", "unterminated_header", "distinct"):
+        assert v[key][0] == v[key][1], (key, v[key])
+    import bench
+    assert v["windows"][0] == bench.expected_windows(10_000_000_000, 11, bench.CHROM)
 
 
 @pytest.mark.gpu

@@ -305,6 +305,42 @@ def test_int32_zone_partitioned(k, split, extra):
     assert list(r.depth1) == list(r2.depth1)
 
 
+@pytest.mark.parametrize("k,fasta,seed", [(11, 80, 2), (6, 0, 1)])
+def test_baseline_genome_10g_vs_oracle(k, fasta, seed):
+    """BASELINE.json configs[2] at its size -- k=11 over a 10 G-base
+    synthetic genome (80-column FASTA, 1.5-Gbase chromosomes, ≈1.0125e10
+    bytes), the bench's headline -- and the north-star genome (k=6, 10 G
+    pure-ACGT bases): the engine's table and every scalar against the CPU
+    oracle over all 10 GB (fko_count_dense_par: the same scan in pieces, each
+    from its exact entering state, on the box's host threads)"""
+    import torch
+    import bench
+    n = 10_000_000_000
+    buf, size = bench.make_genome(n, fasta, seed, bench.CHROM)
+    torch.cuda.synchronize()
+    with fk.Engine(k, want_nodes=True, collect_unknown=True) as e:
+        e.feed_device(buf.data_ptr(), size)
+        rc, r_g = e.finish()
+        t_g = e.table()
+        ub_g = e.unknown_bytes()
+    host = buf[:size].cpu().numpy()
+    del buf
+    torch.cuda.empty_cache()
+    assert rc == fk.FK_OK
+    assert r_g.windows == bench.expected_windows(n, k, bench.CHROM)
+    t_o, r_o, ub_o = oracle.count_dense(host, k, unknown_cap=16, threads=oracle.host_threads())
+    del host
+    bad = np.nonzero(t_o != t_g)[0]
+    assert len(bad) == 0, f"{len(bad)} bins differ, first {bad[:8]}"
+    assert list(r_g.base_count) == list(r_o.base_count)
+    assert (r_g.valid_bases, r_g.windows, r_g.distinct, r_g.nodes) == \
+        (r_o.valid_bases, r_o.windows, r_o.distinct, r_o.nodes)
+    assert list(r_g.depth1) == list(r_o.depth1)
+    assert (r_g.unknown_chars, r_g.scanned_bytes, r_g.hit_eof_byte, r_g.unterminated_header) == \
+        (r_o.unknown_chars, r_o.scanned_bytes, r_o.hit_eof_byte, r_o.unterminated_header)
+    assert ub_g == ub_o == b""
+
+
 @pytest.mark.parametrize("k", [6, 11])
 def test_full_size_properties(k):
     """BASELINE config sizes (1 GB stream, 1 GB of 80-col FASTA): exact
@@ -652,11 +688,32 @@ def test_shards_summaries(k, nshards, kind):
     assert list(r_g.base_count) == list(r_o.base_count)
 
 
-def test_shards_summaries_took_both_paths():
-    """the compact stitch and its fallback were both exercised above"""
-    if shard_count.compact_ok == 0 or shard_count.compact_failed == 0:
-        pytest.skip("run with test_shards_summaries")
-    assert shard_count.compact_ok > 0 and shard_count.compact_failed > 0
+@pytest.mark.parametrize("k", [4, 6, 7])
+def test_shards_summaries_take_both_paths(k):
+    """dist.py's stitch takes both paths, on inputs built for each: pure ACGT
+    shards (every compact summary applies), and a shard that starts inside a
+    comment line longer than its 256-byte halo, made of bases only, so the
+    halo looks like a run: the guess is wrong, the compact summary refuses
+    the true entering state (FK_E_SUMMARY) and the full transfer functions
+    are exchanged instead"""
+    rng = random.Random(90 + k)
+    ok0, failed0 = shard_count.compact_ok, shard_count.compact_failed
+    acgt = random_text(rng, 600_000, b"ACGT", [1, 1, 1, 1])
+    t_o, r_o, _ = oracle.count_dense(acgt, k)
+    t_g, r_g, _, _ = shard_count(acgt, k, 2, summaries=True)
+    assert np.array_equal(t_o, t_g) and r_g.windows == r_o.windows
+    assert shard_count.compact_ok == ok0 + 1 and shard_count.compact_failed == failed0
+    # shard_count cuts 600000 bytes into two shards at 262144 (4 x 64 KiB)
+    cut = 262144
+    data = bytearray(acgt)
+    data[cut - 1000:cut + 2000] = b">" + random_text(rng, 2998, b"ACGT", [1, 1, 1, 1]) + b"\n"
+    data = bytes(data)
+    t_o, r_o, _ = oracle.count_dense(data, k)
+    t_g, r_g, _, _ = shard_count(data, k, 2, summaries=True)
+    assert np.array_equal(t_o, t_g)
+    assert r_g.windows == r_o.windows and r_g.valid_bases == r_o.valid_bases
+    assert list(r_g.base_count) == list(r_o.base_count)
+    assert shard_count.compact_failed == failed0 + 1, "the shard inside a long comment must refuse its compact summary"
 
 
 def assert_same_sparse(data, k, feeds=None):
