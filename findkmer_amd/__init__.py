@@ -32,6 +32,10 @@ FK_E_SUMMARY = -12
 FK_K_MAX_DENSE = 16
 FK_PACK_COUNTERS = 14     # include/findkmer.h: fk_engine_shard_pack's counters
 FK_PACK_ROW_WORDS = 32    # ... and its rows (uint32 words)
+FK_PACK_STATS = 8         # a sharded table's (total, distinct) as limbs
+FK_XCHG_FAST = 1          # fk_engine_shard_exchange flags (info[0])
+FK_XCHG_SHARD_TABLE = 2
+FK_XCHG_TEST_INVALID = 4
 FK_COMM_ID_BYTES = 128
 
 
@@ -101,6 +105,8 @@ SIGNATURES = [
     ("fk_comm_create", ctypes.c_int, [_P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.POINTER(_P)]),
     ("fk_comm_destroy", None, [_P]),
     ("fk_engine_shard_exchange", ctypes.c_int, [_P, _P, _P, ctypes.POINTER(ctypes.c_int32)]),
+    ("fk_merge_layout", ctypes.c_int, [ctypes.c_int, ctypes.c_int, _U64P, _U64P]),
+    ("fk_comm_available", ctypes.c_int, [ctypes.c_int]),
     ("fk_shard_rows_compose", ctypes.c_int, [_P, ctypes.c_int, ctypes.c_int, ctypes.POINTER(FkState)]),
     ("fk_engine_finish", ctypes.c_int, [_P, ctypes.POINTER(FkResult)]),
     ("fk_engine_table", ctypes.c_int, [_P, _U32P]),
@@ -120,6 +126,8 @@ SIGNATURES = [
     ("fk_input_info", ctypes.c_int, [_P, ctypes.POINTER(_P), _U64P, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_double)]),
     ("fk_input_destroy", None, [_P]),
     ("fk_input_headers", ctypes.c_int, [_P, ctypes.c_int, _U64P, _U64P, ctypes.c_uint64, _U64P]),
+    ("fk_device_select", ctypes.c_int, [ctypes.c_uint64, ctypes.POINTER(ctypes.c_int)]),
+    ("fk_device_policy", ctypes.c_int, [ctypes.c_int, _U64P, ctypes.c_uint64, ctypes.c_uint32]),
     ("fk_write_stats", ctypes.c_int, [ctypes.c_char_p, ctypes.c_int, ctypes.POINTER(FkResult), _P, ctypes.POINTER(ctypes.c_double)]),
     ("fk_write_rows", ctypes.c_int, [_P, ctypes.c_int, _U32P, ctypes.POINTER(ctypes.c_double), ctypes.c_uint64, ctypes.c_int, ctypes.c_double, ctypes.c_int]),
     ("fk_write_rows_sparse", ctypes.c_int, [_P, ctypes.c_int, _U64P, _U32P, ctypes.c_uint64, ctypes.POINTER(ctypes.c_double), ctypes.c_uint64, ctypes.c_int, ctypes.c_double, ctypes.c_int]),
@@ -248,13 +256,16 @@ class Engine:
         _check(lib().fk_engine_shard_pack(self.h, table_ptr, counters_ptr, rows_ptr, nrows, slot,
                                           1 if is_last else 0), "shard_pack")
 
-    def shard_exchange(self, comm, merge_ptr, fast=True):
+    def shard_exchange(self, comm, merge_ptr, fast=True, shard_table=False, test_invalid=False):
         """fk_engine_shard_exchange: the whole exchange of a pending shard over
         `comm` (a Comm) on the engine's stream, into the device merge buffer.
         Returns (one_collective, first_end): one_collective = every rank's
-        buffer holds the merged table (else rank 0's does); first_end = the
-        rank whose shard ends the stream (a 0xFF byte) or None."""
-        info = (ctypes.c_int32 * 2)(1 if fast else 0, -1)
+        buffer holds the merged table (else rank 0's does, or with
+        shard_table each rank its slice); first_end = the rank whose shard
+        ends the stream (a 0xFF byte) or None."""
+        flags = (FK_XCHG_FAST if fast else 0) | (FK_XCHG_SHARD_TABLE if shard_table else 0) | \
+            (FK_XCHG_TEST_INVALID if test_invalid else 0)
+        info = (ctypes.c_int32 * 2)(flags, -1)
         _check(lib().fk_engine_shard_exchange(self.h, comm.h, merge_ptr, info), "shard_exchange")
         return bool(info[0]), (info[1] if info[1] >= 0 else None)
 

@@ -30,6 +30,12 @@ struct Rccl {
     decltype(&ncclCommDestroy) destroy = nullptr;
     decltype(&ncclAllReduce) all_reduce = nullptr;
     decltype(&ncclReduce) reduce = nullptr;
+    decltype(&ncclReduceScatter) reduce_scatter = nullptr;
+    decltype(&ncclAllGather) all_gather = nullptr;
+    decltype(&ncclSend) send = nullptr;
+    decltype(&ncclRecv) recv = nullptr;
+    decltype(&ncclGroupStart) group_start = nullptr;
+    decltype(&ncclGroupEnd) group_end = nullptr;
     bool ok = false;
 };
 
@@ -47,7 +53,14 @@ const Rccl &rccl() {
         x.destroy = (decltype(x.destroy))dlsym(h, "ncclCommDestroy");
         x.all_reduce = (decltype(x.all_reduce))dlsym(h, "ncclAllReduce");
         x.reduce = (decltype(x.reduce))dlsym(h, "ncclReduce");
-        x.ok = x.get_id && x.init_rank && x.destroy && x.all_reduce && x.reduce;
+        x.reduce_scatter = (decltype(x.reduce_scatter))dlsym(h, "ncclReduceScatter");
+        x.all_gather = (decltype(x.all_gather))dlsym(h, "ncclAllGather");
+        x.send = (decltype(x.send))dlsym(h, "ncclSend");
+        x.recv = (decltype(x.recv))dlsym(h, "ncclRecv");
+        x.group_start = (decltype(x.group_start))dlsym(h, "ncclGroupStart");
+        x.group_end = (decltype(x.group_end))dlsym(h, "ncclGroupEnd");
+        x.ok = x.get_id && x.init_rank && x.destroy && x.all_reduce && x.reduce && x.reduce_scatter &&
+               x.all_gather && x.send && x.recv && x.group_start && x.group_end;
         return x;
     }();
     return r;
@@ -70,6 +83,17 @@ extern "C" int fk_comm_id(uint8_t *id) {
     if (r.get_id(&u) != ncclSuccess) return FK_E_RCCL;
     memcpy(id, u.internal, NCCL_UNIQUE_ID_BYTES);
     return FK_OK;
+}
+
+/* Everything fk_comm_create checks before its collective ncclCommInitRank,
+   without joining anything: callers agree on it first (one all-reduce), so
+   that no rank is left alone inside the collective init. */
+extern "C" int fk_comm_available(int device) {
+    if (!rccl().ok) return FK_E_RCCL;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n < 1) return FK_E_NO_DEVICE;
+    if (device < 0 || device >= n) return FK_E_INVALID;
+    return hipSetDevice(device) == hipSuccess ? FK_OK : FK_E_HIP;
 }
 
 extern "C" int fk_comm_create(const uint8_t *id, int world, int rank, int device, fk_comm **out) {
@@ -114,4 +138,27 @@ int fkc_allreduce_i32(fk_comm *c, int32_t *buf, size_t n, hipStream_t s) {
 int fkc_reduce_i32(fk_comm *c, int32_t *buf, size_t n, int root, hipStream_t s) {
     if (!c || !c->nc || !rccl().ok) return FK_E_RCCL;
     return rccl().reduce(buf, buf, n, ncclInt32, ncclSum, root, c->nc, s) == ncclSuccess ? FK_OK : FK_E_RCCL;
+}
+
+int fkc_reduce_scatter_i32(fk_comm *c, int32_t *buf, size_t per_rank, hipStream_t s) {
+    if (!c || !c->nc || !rccl().ok) return FK_E_RCCL;
+    /* in place: rank r's block of the sum lands at buf + r * per_rank */
+    return rccl().reduce_scatter(buf, buf + (size_t)c->rank * per_rank, per_rank, ncclInt32, ncclSum, c->nc, s) ==
+                   ncclSuccess
+               ? FK_OK
+               : FK_E_RCCL;
+}
+
+int fkc_alltoallv_u8(fk_comm *c, const uint8_t *send, const uint64_t *send_off, const uint64_t *send_len,
+                     uint8_t *recv, const uint64_t *recv_off, const uint64_t *recv_len, hipStream_t s) {
+    if (!c || !c->nc || !rccl().ok) return FK_E_RCCL;
+    const Rccl &r = rccl();
+    if (r.group_start() != ncclSuccess) return FK_E_RCCL;
+    bool ok = true;
+    for (int p = 0; p < c->world && ok; p++) {
+        if (send_len[p]) ok = r.send(send + send_off[p], send_len[p], ncclUint8, p, c->nc, s) == ncclSuccess;
+        if (ok && recv_len[p]) ok = r.recv(recv + recv_off[p], recv_len[p], ncclUint8, p, c->nc, s) == ncclSuccess;
+    }
+    const bool end_ok = r.group_end() == ncclSuccess;
+    return ok && end_ok ? FK_OK : FK_E_RCCL;
 }

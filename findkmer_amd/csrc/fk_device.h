@@ -287,7 +287,7 @@ enum { ONE_SCAN = 1u,     /* a guess check failed (or could not be made): k_scan
 enum { OP_ON = 1u,        /* one pass: k_count summarises its blocks, k_tail finishes */
        OP_FRESH = 2u,     /* a reset is pending: zero table, state and accumulators */
        OP_SHARD = 4u,     /* a shard: the entering state is the first guess until resolved */
-       OP_NOMIX = 8u };   /* no mixed tiles (FK_NO_MIXED=1: the general byte walk instead) */
+       OP_NOMIX = 8u };   /* no mixed tiles (FINDKMER_TUNE no_mixed=1: the general byte walk instead) */
 struct OnePassCfg {
     void *bsum;                      /* per k_count block: a BlockSum (fk_engine.hip) */
     XState *rtrue;                   /* entering state per range */

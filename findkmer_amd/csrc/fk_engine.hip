@@ -50,9 +50,6 @@
 #include "fk_device.h"
 #include "fk_sparse.h"
 
-#ifndef FK_EXP
-#define FK_EXP 0   /* ablation builds only (tools/exp.sh); 0 = product */
-#endif
 
 /* ------------------------------------------------------------------------- */
 /* device helpers                                                             */
@@ -505,11 +502,7 @@ __device__ __forceinline__ void half_windows(const Ctx &cx, uint32_t C, uint32_t
            (0,1),(2,3),...; without a real slot 0 the first pair becomes the
            single k-mer at slot 1 */
         const uint32_t m3 = (uint32_t)((cx.maskk << 2) | 3u) << 2;
-#if FK_EXP == 1   /* ablation: addresses computed, no LDS atomics */
-#define FK_LDS_ADD(a_) asm volatile("" ::"v"(a_))
-#else
 #define FK_LDS_ADD(a_) lds_add(cx, (a_), weight)
-#endif
         {
             uint32_t v = __builtin_amdgcn_alignbit(C, S2, 26u);
             uint32_t addr = skip0 ? (cx.single_off * 4u + (v & m2)) : (v & m3);
@@ -593,12 +586,8 @@ __device__ __forceinline__ bool tile_finish(const Ctx &cx, const uint32_t x[8], 
             if (deep) cnt.win_u += nsym;
         } else if (HM == H_NONE) {
         } else if (deep) {
-#if FK_EXP == 2   /* ablation: no window work at all */
-            asm volatile("" ::"v"(AC), "v"(A2), "v"(BC), "v"(B2));
-#else
             half_windows<HM>(cx, AC, A2, h0, weight);
             half_windows<HM>(cx, BC, B2, h1, weight);
-#endif
             cnt.win_u += nsym;
         }
         /* facts: the first '\n' of the span (all bytes before it are bases) */
@@ -641,17 +630,6 @@ __device__ __forceinline__ bool tile_finish(const Ctx &cx, const uint32_t x[8], 
 template <bool COUNT, int HM, bool INTER>
 __device__ __forceinline__ bool tile_fast(const Ctx &cx, const uint32_t w[8], DState &st, Facts &f,
                                           Counters &cnt, uint32_t weight, Emit *em = nullptr, bool *kind = nullptr) {
-#if FK_EXP == 4   /* ablation: loop framework only */
-    {
-        uint32_t x = 0;
-#pragma unroll
-        for (int d = 0; d < 8; d++) x ^= w[d];
-        asm volatile("" ::"v"(x));
-        st.R += FK_TILE_BYTES;
-        cnt.win_u += FK_TILE_BYTES;
-        return true;
-    }
-#endif
     uint32_t x[8], m[8];
     uint32_t mis = 0;
 #pragma unroll
@@ -668,11 +646,6 @@ __device__ __forceinline__ bool tile_fast(const Ctx &cx, const uint32_t w[8], DS
        On a lane without other bytes m = 0x49 exactly at the '\n's, and a
        dot4 with weights 16 + j gives the half's newline code (NL_TWO). */
     uint32_t bad4[4], nl0, nl1;
-#if FK_EXP == 9   /* ablation: newline classification skipped (timing only) */
-    nl0 = mis ? 73u * 16u : 0u;
-    nl1 = 0u;
-    const bool lane_ok = true;
-#else
 #pragma unroll
     for (int c = 0; c < 4; c++) {
         bad4[c] = __builtin_amdgcn_udot4(m[2 * c], w[2 * c] ^ 0x0A0A0A0Au, 0u, false);
@@ -691,7 +664,6 @@ __device__ __forceinline__ bool tile_fast(const Ctx &cx, const uint32_t w[8], DS
         nl1 = b0 + b1;
     }
     const bool lane_ok = (bad4[0] | bad4[1] | bad4[2] | bad4[3]) == 0 && nl0 < NL_TWO && nl1 < NL_TWO;
-#endif
     if (__ballot(!lane_ok)) return false;
     return tile_finish<COUNT, HM, INTER, true>(cx, x, nl0, nl1, st, f, cnt, weight, em, kind);
 }
@@ -1154,11 +1126,7 @@ __device__ void lds_flush(const Ctx &cx) {
         } else {
             v = cx.lds[i];
         }
-#if FK_EXP == 5   /* ablation: no bin flush to the global table */
-        asm volatile("" ::"v"(v));
-#else
         if (v) atomicAdd(&(cx.flush ? cx.flush : cx.table)[fk_sigma(i)], v);
-#endif
     }
 }
 
@@ -1256,15 +1224,6 @@ template <typename T>
 __device__ __forceinline__ T xget(const T *p) {
     return __hip_atomic_load(const_cast<T *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-
-/* k_tail timeline probe (FK_EXP == 20 builds only): s_memrealtime (100 MHz)
-   at points of k_tail, max over blocks; slot 0: min at entry */
-#if FK_EXP == 20
-__device__ unsigned long long g_tp[16];
-#define TP(i) do { if (threadIdx.x == 0) atomicMax(&g_tp[i], (unsigned long long)__builtin_amdgcn_s_memrealtime()); } while (0)
-#else
-#define TP(i) do { } while (0)
-#endif
 
 /* LDS layout of k_tail's last block */
 #define TAIL_BLOCKS 16u
@@ -1387,16 +1346,7 @@ __device__ __forceinline__ void block_summary(const Ctx &cx, const OnePassCfg *o
  * end) ends the wave's work: it appends a ResumeRec and k_resume continues
  * the range from there.  A range counted to its end gets its RangeRec here.
  */
-#ifdef FK_WAVE_TIMES   /* experiment build (tools/wave_times.sh): per-wave start / loop end / end */
-__device__ unsigned long long fk_dbg_wt[32768 * 8];
-extern "C" int fk_debug_wave_times(unsigned long long *out, int n) {
-    return hipMemcpyFromSymbol(out, HIP_SYMBOL(fk_dbg_wt), (size_t)n * 8 * sizeof(unsigned long long)) == hipSuccess ? 0 : -1;
-}
-#endif
 
-#if FK_EXP == 40
-__device__ uint32_t fk_exp_heads[32768 * 16];
-#endif
 
 /* A wave's next dynamic range (wave-uniform), from its block's pool: pool
  * blockIdx % npools, whose ranges are d = p, p + npools, ... (largest first).
@@ -1479,11 +1429,7 @@ __device__ __forceinline__ void count_wave_range(const Ctx &cx, const Span &sp, 
         st.R = (uint32_t)in.R;
         st.code = in.code;
     } else {
-#if FK_EXP >= 3   /* ablation: no halo guess */
-        st = DState{0, 100000u, 0};
-#else
         st = halo_guess<HM>(cx, hw, hv);
-#endif
     }
     /* the halo words are waited for on every path (the d_init one too):
        a load left pending into the loop makes its first tile wait for
@@ -1578,9 +1524,6 @@ k_count(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uin
         uint32_t general_tiles, uint32_t *subs, const OnePassCfg *opc, uint32_t op_flags,
         uint64_t nstatic, DynGeo dg, uint32_t *heads) {
     extern __shared__ uint32_t lds_bins[];
-#ifdef FK_WAVE_TIMES
-    const unsigned long long wt0 = __builtin_amdgcn_s_memrealtime();
-#endif
     /* open the feed's result block (the kernels after this one in the
        stream accumulate into it) */
     if (blockIdx.x == 0) {
@@ -1618,18 +1561,12 @@ k_count(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uin
     bool hv;
     range_prologue(cx, sp, last_tile, has, hw, hv, A, B, C);
     if (LDS_MODE(HM)) lds_zero(lds_bins, nw);
-#if FK_EXP == 41
-    uint32_t empty = 0;
-#endif
     /* the wave's counters, flushed once per FK_FLUSH_BYTES of its ranges
        (packed 16-bit fields per lane) and at the end: one set of
        accumulator atomics per wave, not per range */
     Counters cnt{0, 0, 0, 0, 0, FK_NO_EOF};
     uint32_t unk_seen = 0;
     uint64_t since = 0;
-#ifdef FK_WAVE_TIMES
-    unsigned long long wt_static = 0, wt_claim = 0, wt_ndyn = 0, wt_dbytes = 0;
-#endif
     for (;;) {
         if (has) {
             count_wave_range<HM>(cx, sp, last_tile, rid, c0, c1, hw, hv, A, B, C, d_init, has_init, op_flags,
@@ -1643,39 +1580,8 @@ k_count(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uin
             }
         }
         if (dg.ndyn == 0) break;
-#ifdef FK_WAVE_TIMES
-        const unsigned long long wc0 = __builtin_amdgcn_s_memrealtime();
-        if (!wt_static) wt_static = wc0;
-#endif
-#if FK_EXP == 40 || FK_EXP == 41
-        /* experiments: wave-private interleaved pools (40: an uncontended
-           atomic per claim; 41: no atomic) */
-        uint32_t d;
-        {
-            const uint64_t W = (uint64_t)gridDim.x * FK_WAVES_PER_BLOCK;
-#if FK_EXP == 40
-            uint32_t j = 0;
-            if ((threadIdx.x & 63) == 0) j = atomicAdd(&fk_exp_heads[wave * 16], 1u);
-            j = (uint32_t)__builtin_amdgcn_readfirstlane((int)j);
-#else
-            const uint32_t j = empty++;
-#endif
-            const uint64_t dd = wave + (uint64_t)j * W;
-            d = dd < dg.ndyn ? (uint32_t)dd : dg.ndyn;
-#if FK_EXP == 40
-            if (d >= dg.ndyn && (threadIdx.x & 63) == 0) fk_exp_heads[wave * 16] = 0;
-#endif
-        }
-#else
         const uint32_t d = claim_dyn(heads, dg);
-#endif
-#ifdef FK_WAVE_TIMES
-        wt_claim += __builtin_amdgcn_s_memrealtime() - wc0;
-#endif
         if (d >= dg.ndyn) break;
-#ifdef FK_WAVE_TIMES
-        wt_ndyn++;
-#endif
         rid = nstatic + d;
         dyn_span(dg, d, c0, c1);
         hdr_r.c0 = c0;
@@ -1683,32 +1589,13 @@ k_count(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uin
         sp = range_span(hdr_r, len);
         last_tile = sp.nfull ? sp.rend - FK_TILE_BYTES : 0;
         has = true;
-#ifdef FK_WAVE_TIMES
-        wt_dbytes += sp.rend - sp.rbase;
-#endif
         range_prologue(cx, sp, last_tile, has, hw, hv, A, B, C);
     }
     flush_counters(cx, cnt, 1u, HM != H_NONE);
-#ifdef FK_WAVE_TIMES
-    const unsigned long long wt1 = __builtin_amdgcn_s_memrealtime();
-#endif
     if (LDS_MODE(HM)) {
         lds_flush<HM>(cx);
         if ((op_flags & OP_ON) && threadIdx.x < 64) block_summary(cx, opc, rr, nstatic);
     }
-#ifdef FK_WAVE_TIMES
-    if ((threadIdx.x & 63) == 0 && wave < 32768) {
-        fk_dbg_wt[wave * 8 + 0] = wt0;
-        fk_dbg_wt[wave * 8 + 1] = wt1;
-        fk_dbg_wt[wave * 8 + 2] = __builtin_amdgcn_s_memrealtime();
-        fk_dbg_wt[wave * 8 + 3] = (__builtin_amdgcn_s_getreg((20) | (0 << 6) | ((4 - 1) << 11)) & 0xF) |
-                                  ((unsigned long long)__builtin_amdgcn_s_getreg((4) | (0 << 6) | ((32 - 1) << 11)) << 32);
-        fk_dbg_wt[wave * 8 + 4] = wt_static ? wt_static : wt1;
-        fk_dbg_wt[wave * 8 + 5] = wt_ndyn;
-        fk_dbg_wt[wave * 8 + 6] = wt_claim;
-        fk_dbg_wt[wave * 8 + 7] = wt_dbytes;
-    }
-#endif
 }
 #undef FK_LOADI
 #undef FK_LOADT
@@ -1886,7 +1773,7 @@ struct PartGeo {
     uint32_t npair;        /* pairs mode: slices [0, npair) hold (k+1)-mer pairs, the rest single k-mers */
     uint32_t *pairs;       /* pairs mode: 4^(k+1) pair bins (k_bucket_count -> k_pair_fold) */
     uint32_t *singles;     /* pairs mode: 4^k single k-mer bins */
-    uint32_t nomix;        /* FK_NO_MIXED: tiles the fast path cannot take go to tile_general */
+    uint32_t nomix;        /* no_mixed: tiles the fast path cannot take go to tile_general */
     uint32_t general;      /* general tiles (other than bases-only ones) k_part takes per range
                               before k_part<RES> takes the rest */
     uint32_t stride;       /* index row stride: rows of both regions (k_part, then k_part<RES>) */
@@ -2508,10 +2395,6 @@ k_tail(const OnePassCfg *opc, uint32_t flags, uint32_t seq, uint32_t *table, int
     const BlockSum *bsum = reinterpret_cast<const BlockSum *>(opc->bsum);
     /* the chain: G0 block summaries, then the dynamic ranges */
     const uint32_t G = G0 + ndyn;
-#if FK_EXP == 20
-    if (t == 0) atomicMin(&g_tp[0], (unsigned long long)__builtin_amdgcn_s_memrealtime());
-    TP(8);
-#endif
     /* every load of the slice phase first (one round trip): this block's
        BlockSums [b0, b1) and their predecessors' exits, one per thread, and
        its table bins with the sub-tables (bins strided over the threads) */
@@ -2565,7 +2448,6 @@ k_tail(const OnePassCfg *opc, uint32_t flags, uint32_t seq, uint32_t *table, int
         v10[2] += ld == 0 ? v : 0; v10[3] += ld == 1 ? v : 0; v10[4] += ld == 2 ? v : 0; v10[5] += ld == 3 ? v : 0;
         v10[6] += fd == 0 ? v : 0; v10[7] += fd == 1 ? v : 0; v10[8] += fd == 2 ? v : 0; v10[9] += fd == 3 ? v : 0;
     }
-    TP(5);
     /* BlockSum i: its first guess against block i-1's last exit (the local
        check of block_summary, across blocks), flags, 0xFF candidate */
     uint32_t need = 0;
@@ -2582,7 +2464,6 @@ k_tail(const OnePassCfg *opc, uint32_t flags, uint32_t seq, uint32_t *table, int
     const long long jw = (long long)wmax64s(jmax);
     if (lane == 0) sh[w][10] = (unsigned long long)jw;
     __syncthreads();
-    TP(6);
     long long js = -1;
     for (uint32_t q = 0; q < blockDim.x / 64; q++) js = max(js, (long long)sh[q][10]);
     uint64_t nv_after = hb && (long long)bi > js ? bs.nv : 0;
@@ -2592,7 +2473,6 @@ k_tail(const OnePassCfg *opc, uint32_t flags, uint32_t seq, uint32_t *table, int
     nv_after = wsum64(nv_after);
     need = (uint32_t)wred64(need, OpOr64{});
     eof = wred64(eof, OpMin64{});
-    TP(9);
     __syncthreads();
     if (lane == 0) {
 #pragma unroll
@@ -2621,9 +2501,7 @@ k_tail(const OnePassCfg *opc, uint32_t flags, uint32_t seq, uint32_t *table, int
             if (t == 14) sink = xput(&P.eof, (uint64_t)a);
             if (t == 15) sink = xput(&P.j, (int32_t)js) | xput(&P.Rj, (uint64_t)(js >= 0 ? sh[0][11] : 0));
         }
-        TP(10);
         keep(sink);
-        TP(1);
         /* 2. the last block to finish combines */
         if (t == 0) bc[0] = atomicAdd(done, 1u) == B - 1;
     }
@@ -2636,7 +2514,6 @@ k_tail(const OnePassCfg *opc, uint32_t flags, uint32_t seq, uint32_t *table, int
         for (uint32_t q = 0; q < nkeep; q++) tail_store(table, subs, nbins, lo + t + q * blockDim.x, keep_v[q], keep_m[q]);
         return;
     }
-    TP(2);
     if (t < 64) {
         if (t == 0) *done = 0;
         /* every load of the combine first: partial `lane`, the last
@@ -2718,10 +2595,8 @@ k_tail(const OnePassCfg *opc, uint32_t flags, uint32_t seq, uint32_t *table, int
                 ss.c_code = lb.e_code; ss.c_hdr = lb.e_hdr;
             }
         }
-        TP(3);
         publish_res_wave(res, opc->host_res, seq);
     }
-    TP(4);
     for (uint32_t q = 0; q < nkeep; q++) tail_store(table, subs, nbins, lo + t + q * blockDim.x, keep_v[q], keep_m[q]);
 }
 
@@ -3061,8 +2936,8 @@ struct fk_engine {
     uint64_t codes_cap = 0, pidx_cap = 0;
     uint32_t *d_pairs = nullptr;              /* k_part pairs mode: 4^(k+1) pair bins + 4^k single bins */
     uint64_t pair_cap = 0;
-    int part_pairs_kmax = 11;                 /* pairs mode for k <= this (FK_PART_PAIRS_KMAX; 0 = off) */
-    uint32_t general_tiles = FK_COUNT_GENERAL_TILES;   /* per range in k_count (env FK_GENERAL_TILES) */
+    int part_pairs_kmax = 11;                 /* pairs mode for k <= this */
+    uint32_t general_tiles = FK_COUNT_GENERAL_TILES;   /* per range in k_count */
     /* device state */
     uint32_t *d_table = nullptr, *d_short = nullptr;
     uint32_t *d_sub = nullptr;                /* FK_SUBTABLES table copies k_count flushes into (LDS modes) */
@@ -3070,21 +2945,21 @@ struct fk_engine {
     unsigned long long *d_facc = nullptr;     /* FK_ACC_COPIES x ACC_N the counting kernels of a feed add into;
                                                  merged into d_acc by the feed's publisher, zero between feeds */
     /* one-pass k_count (k <= 7, entering state known) */
-    bool onepass = true;                      /* env FK_NO_ONEPASS=1: off */
+    bool onepass = true;                      /* k <= 7: k_count + k_tail in one pass */
     BlockSum *d_bsum = nullptr;               /* per block of k_count */
     uint32_t *d_ctl = nullptr;                /* k_tail's finished-block count */
-    uint32_t ranges_per_wave = 1;             /* k <= 7: ranges per k_count wave slot (FK_RANGES_PER_WAVE) */
-    bool no_mixed = false;                    /* FK_NO_MIXED=1: no mixed tiles (general byte walk) */
-    uint32_t part_general = 1;                /* k_part: general tiles per range (FK_PART_GENERAL) */
-    uint32_t part_waves = 0;                  /* k_part: waves per block (FK_PART_WAVES; 0 = by k) */
-    uint32_t static_pct = 100;                /* k <= 7: % of a large segment in static ranges (FK_STATIC_PCT;
+    uint32_t ranges_per_wave = 1;             /* k <= 7: ranges per k_count wave slot */
+    bool no_mixed = false;                    /* FINDKMER_TUNE no_mixed=1: no mixed tiles (general byte walk) */
+    uint32_t part_general = 1;                /* k_part: general tiles per range (FINDKMER_TUNE part_general) */
+    uint32_t part_waves = 0;                  /* k_part: waves per block (FINDKMER_TUNE part_waves; 0 = by k) */
+    uint32_t static_pct = 100;                /* k <= 7: % of a large segment in static ranges (FINDKMER_TUNE static_pct;
                                                  100 = no dynamic ranges: on a plain stream the waves that
                                                  finish early hand their bandwidth to the others, so
                                                  balancing gains nothing -- 1 GB k=6 0.174 ms either way --
                                                  while header-dense input gains 9 % at 75) */
-    uint32_t cls_w[4] = {1000, 1000, 1000, 1000};   /* static share per wave class, per mille (FK_CLASS_W) */
+    uint32_t cls_w[4] = {1000, 1000, 1000, 1000};   /* static share per wave class, per mille */
     uint64_t dyn_min_chunks = 0;              /* segments with dynamic ranges: >= this many chunks (0: 8 per
-                                                 wave slot; FK_DYN_MIN_CHUNKS, tests) */
+                                                 wave slot; FINDKMER_TUNE dyn_min_chunks, tests) */
     OnePassCfg *d_opc = nullptr;
     bool op_pending = false;                  /* the last count_segment launched a one-pass k_count */
     bool op_fresh = false;                    /* ... which did a pending reset itself */
@@ -3106,7 +2981,7 @@ struct fk_engine {
     uint8_t *d_stage = nullptr, *h_stage = nullptr;
     hipEvent_t ev[3] = {};
     bool times_pending = false;               /* ev[] of the last feed not yet read */
-    bool timing = true;                       /* record ev[] (env FK_NO_EVENTS=1: off) */
+    bool timing = true;                       /* record ev[] (FINDKMER_TUNE events=0: off) */
     bool zero_pending = false;                /* reset() not yet issued to the device */
     DevRes *h_res = nullptr, *h_res_dev = nullptr;   /* pinned, mapped result block */
     uint32_t *d_done = nullptr;               /* k_table_stats finished-block count */
@@ -3190,15 +3065,6 @@ static int set_dev(fk_engine *e, bool flush = true) {
 
 extern "C" int fk_abi_version(void) { return FK_ABI_VERSION; }
 
-#if FK_EXP == 20
-/* experiment builds: read and reset the k_tail timeline probe */
-extern "C" int fk_debug_tailprof(unsigned long long *out16) {
-    if (out16 && hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_tp), sizeof(g_tp)) != hipSuccess) return FK_E_HIP;
-    unsigned long long z[16] = {};
-    z[0] = ~0ull;
-    return hipMemcpyToSymbol(HIP_SYMBOL(g_tp), z, sizeof(z)) == hipSuccess ? FK_OK : FK_E_HIP;
-}
-#endif
 
 
 extern "C" const char *fk_strerror(int s) {
@@ -3301,6 +3167,24 @@ static bool lds_layout_ok() {
     return ok == 1;
 }
 
+/* One knob of FINDKMER_TUNE ("name=value,name=value"): true and *v = value
+   when `name` is set. */
+static bool tune_knob(const char *name, uint64_t *v) {
+    const char *t = getenv("FINDKMER_TUNE");
+    if (!t) return false;
+    const size_t n = strlen(name);
+    for (const char *p = t; *p;) {
+        if (strncmp(p, name, n) == 0 && p[n] == '=') {
+            *v = strtoull(p + n + 1, nullptr, 10);
+            return true;
+        }
+        const char *c = strchr(p, ',');
+        if (!c) break;
+        p = c + 1;
+    }
+    return false;
+}
+
 extern "C" int fk_engine_create(int k, const fk_opts *opts, fk_engine **out) {
     if (!out) return FK_E_INVALID;
     *out = nullptr;
@@ -3318,37 +3202,26 @@ extern "C" int fk_engine_create(int k, const fk_opts *opts, fk_engine **out) {
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, e->dev) == hipSuccess && prop.multiProcessorCount > 0)
         e->cus = prop.multiProcessorCount;
-    if (const char *nm = getenv("FK_NO_MIXED")) e->no_mixed = nm[0] == '1';
+    /* test and tuning knobs, all in one variable FINDKMER_TUNE="name=value,..."
+       (tune_knob): no_mixed=1 (tile_general instead of mixed tiles),
+       part_general=N (general tiles k_part takes per range before
+       k_part<RES>), static_pct=P / dyn_min_chunks=N (k_count's dynamic
+       ranges), part_waves=8|16 (k_part block size), events=0 (no HIP events),
+       seg_kb=N (device feeds cut into N-KiB segments) */
+    uint64_t kv = 0;
+    if (tune_knob("no_mixed", &kv)) e->no_mixed = kv == 1;
     /* k_count takes a couple of general tiles per range (the stream start, an
        isolated comment line) and leaves denser ones to k_resume's mixed tiles */
     if (!e->no_mixed) e->general_tiles = 2;
-    if (const char *gt = getenv("FK_GENERAL_TILES")) e->general_tiles = (uint32_t)strtoul(gt, nullptr, 10);
-    if (const char *pw = getenv("FK_PART_WAVES")) {
-        const uint32_t v = (uint32_t)strtoul(pw, nullptr, 10);
-        e->part_waves = v == 8u || v == 16u ? v : 0u;
-    }
-    if (const char *pg = getenv("FK_PART_GENERAL")) e->part_general = (uint32_t)strtoul(pg, nullptr, 10);
-    if (const char *ne = getenv("FK_NO_EVENTS")) e->timing = ne[0] != '1';
-    if (const char *no = getenv("FK_NO_ONEPASS")) e->onepass = no[0] != '1';
-    if (const char *rw = getenv("FK_RANGES_PER_WAVE")) e->ranges_per_wave = std::max(1u, (uint32_t)strtoul(rw, nullptr, 10));
-    if (const char *sp = getenv("FK_STATIC_PCT")) e->static_pct = std::min(100u, std::max(1u, (uint32_t)strtoul(sp, nullptr, 10)));
-    if (const char *dm = getenv("FK_DYN_MIN_CHUNKS")) e->dyn_min_chunks = strtoull(dm, nullptr, 10);
-    if (const char *cw = getenv("FK_CLASS_W")) {
-        unsigned a = 0, b = 0, c = 0, d = 0;
-        if (sscanf(cw, "%u,%u,%u,%u", &a, &b, &c, &d) == 4 && a && b && c && d) {
-            e->cls_w[0] = a; e->cls_w[1] = b; e->cls_w[2] = c; e->cls_w[3] = d;
-        }
-    }
-    if (const char *pp = getenv("FK_PART_PAIRS_KMAX")) e->part_pairs_kmax = atoi(pp);
-    if (const char *tb = getenv("FK_TS_BLOCKS")) e->ts_blocks = (uint32_t)strtoul(tb, nullptr, 10);
+    if (tune_knob("part_waves", &kv)) e->part_waves = kv == 8u || kv == 16u ? (uint32_t)kv : 0u;
+    if (tune_knob("part_general", &kv)) e->part_general = (uint32_t)kv;
+    if (tune_knob("events", &kv)) e->timing = kv != 0;
+    if (tune_knob("static_pct", &kv)) e->static_pct = (uint32_t)std::min<uint64_t>(100u, std::max<uint64_t>(1u, kv));
+    if (tune_knob("dyn_min_chunks", &kv)) e->dyn_min_chunks = kv;
     if (e->opts.timing_every > 1) e->timing_every = (uint32_t)e->opts.timing_every;
     e->sparse = k > FK_K_MAX_DENSE;
     e->nbins = e->sparse ? 0 : 1ull << (2 * k);
-#if FK_EXP == 6   /* ablation: the partitioned path for k >= 6 */
-    e->part = k >= 6 && k <= 12;
-#else
     e->part = k >= 8 && k <= 12;
-#endif
     e->maskk = (1ull << (2 * k)) - 1;
     e->nshort = k > 1 && !e->sparse ? ((1ull << (2 * k)) - 4) / 3 : 0;
     if (e->opts.stream) {
@@ -3681,7 +3554,7 @@ static int launch_part(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t l
     }
     pg.rounds = (uint32_t)((g.cpw * FK_CHUNK_TILES + 2) / PART_TILES(pairs) + 2);   /* rows (batches) per block */
     /* block size: 16 waves (larger batches, longer runs for k_bucket_count)
-       for the many-slice tables, else 8 (FK_PART_WAVES=8|16 forces one) */
+       for the many-slice tables, else 8 (FINDKMER_TUNE part_waves=8|16 forces one) */
     const uint32_t W = e->part_waves ? e->part_waves : (k >= 11 ? 16u : 8u);
     pg.batch = PART_MAX_BATCH_W(W);
     const unsigned pgrid = (unsigned)((g.nranges + W - 1) / W);   /* the same ranges as k_count's waves */
@@ -4087,6 +3960,29 @@ static int process_segment(fk_engine *e, const uint8_t *dbuf, uint64_t len) {
     return finish_segment(e, dbuf, len, 0, g, entering);
 }
 
+/* Segment length of a device feed.  8 <= k <= 12 allocates ~2 bytes of
+   partition codes per input byte of a segment (k_part's rows, both
+   regions): when free HBM cannot hold that for the whole feed (other
+   processes on the GPU, k6thru11fullANDupstream.sh:16-24), the feed is cut
+   into segments that fit -- segments carry the exact scan state, so the
+   counts do not depend on the cut. */
+static uint64_t segment_budget(fk_engine *e, uint64_t len) {
+    uint64_t seg = SEG_MAX_BYTES, kv = 0;
+    if (tune_knob("seg_kb", &kv) && kv)   /* tests: segments of this many KiB */
+        return std::max<uint64_t>(FK_CHUNK_BYTES, (kv << 10) / FK_CHUNK_BYTES * FK_CHUNK_BYTES);
+    if (!e->part) return seg;
+    const uint64_t per = 2 * sizeof(uint16_t) + 1;     /* codes + run index, bytes per input byte */
+    if (std::min(len, seg) * per <= e->codes_cap * sizeof(uint16_t)) return seg;   /* already allocated */
+    size_t fr = 0, tot = 0;
+    if (hipMemGetInfo(&fr, &tot) != hipSuccess) return seg;
+    const uint64_t margin = 512ull << 20;
+    const uint64_t avail = (uint64_t)fr + e->codes_cap * sizeof(uint16_t) + e->pidx_cap * sizeof(uint32_t);
+    const uint64_t fit = avail > margin ? (avail - margin) / per : 0;
+    const uint64_t floor_seg = 64ull << 20;
+    if (fit < seg) seg = std::max(floor_seg, fit / FK_CHUNK_BYTES * FK_CHUNK_BYTES);
+    return seg;
+}
+
 extern "C" int fk_engine_feed(fk_engine *e, const uint8_t *buf, uint64_t len, int on_device) {
     if (!e || (!buf && len)) return FK_E_INVALID;
     if (e->shard_pending) return FK_E_STATE;
@@ -4098,8 +3994,9 @@ extern "C" int fk_engine_feed(fk_engine *e, const uint8_t *buf, uint64_t len, in
     /* k_count's prefetch loads are clamped to [0, len-32]: inputs shorter
        than one lane go through the (larger) staging buffer */
     if (on_device && ((uintptr_t)buf & 15) == 0 && len >= FK_LANE_BYTES) {
-        for (uint64_t off = 0; off < len && !e->ended; off += SEG_MAX_BYTES) {
-            rc = process_segment(e, buf + off, std::min(SEG_MAX_BYTES, len - off));
+        const uint64_t seg = segment_budget(e, len);
+        for (uint64_t off = 0; off < len && !e->ended; off += seg) {
+            rc = process_segment(e, buf + off, std::min(seg, len - off));
             if (rc) return rc;
         }
         return FK_OK;
@@ -4475,7 +4372,7 @@ __global__ void __launch_bounds__(64) k_fill_row(uint32_t *rows, int nrows, int 
 }
 
 /* pinned, mapped scratch of the exchange: [0] sequence number, rows from
-   word 32, counter limbs (staging) after the rows */
+   word 32, counter and slice-statistics limbs (staging) after the rows */
 static int ensure_rows(fk_engine *e, uint32_t nrow) {
     if (e->rows_cap >= nrow) return FK_OK;
     if (e->h_rows) hipHostFree(e->h_rows);
@@ -4483,7 +4380,7 @@ static int ensure_rows(fk_engine *e, uint32_t nrow) {
     e->h_rows = e->h_rows_dev = nullptr;
     e->d_rows = nullptr;
     e->rows_cap = 0;
-    const size_t words = 32 + nrow + 4 * FK_PACK_COUNTERS;
+    const size_t words = 32 + nrow + 4 * FK_PACK_COUNTERS + FK_PACK_STATS;
     if (hipHostMalloc((void **)&e->h_rows, words * sizeof(uint32_t), hipHostMallocMapped | hipHostMallocCoherent) !=
             hipSuccess ||
         hipHostGetDevicePointer((void **)&e->h_rows_dev, e->h_rows, 0) != hipSuccess ||
@@ -4522,8 +4419,39 @@ static int rows_fetch(fk_engine *e, const uint32_t *rows, uint32_t nrow) {
    end flags all-gathered the same way (a 0xFF byte, :988, exact only after
    the resolve); then the table and counter limbs, zero for ranks after the
    first ending shard, reduced onto rank 0. */
-static int stitched_exchange(fk_engine *e, fk_comm *comm, int32_t *merge, int32_t *first_end_out) {
+/* merge buffer layout (include/findkmer.h, fk_merge_layout): the table
+   padded to a multiple of the world size, the counter limbs, the slice
+   statistics, the rows */
+static uint64_t merge_table_words(uint64_t nbins, int world) {
+    const uint64_t w = (uint64_t)std::max(1, world);
+    return (nbins + w - 1) / w * w;
+}
+
+/* the u64 sum and the nonzero bins of one table slice (sharded table) */
+__global__ void __launch_bounds__(256) k_slice_sum(const uint32_t *t, uint64_t n, unsigned long long *out2) {
+    unsigned long long sum = 0, nz = 0;
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t v = t[i];
+        sum += v;
+        nz += v != 0;
+    }
+    sum = wsum64(sum);
+    nz = wsum64(nz);
+    if ((threadIdx.x & 63) == 0) {
+        if (sum) atomicAdd(&out2[0], sum);
+        if (nz) atomicAdd(&out2[1], nz);
+    }
+}
+
+/* ... as 16-bit limbs in int32 words (sums over ranks stay exact) */
+__global__ void k_slice_limbs(const unsigned long long *in2, int32_t *limbs8) {
+    const uint32_t i = threadIdx.x;
+    if (i < 8) limbs8[i] = (int32_t)((in2[i >> 2] >> (16 * (i & 3))) & 0xFFFFu);
+}
+
+static int stitched_exchange(fk_engine *e, fk_comm *comm, int32_t *merge, int32_t *first_end_out, bool scatter) {
     const int world = fkc_world(comm), rank = fkc_rank(comm);
+    const uint64_t tw = merge_table_words(e->nbins, world);
     const uint32_t nrow = (uint32_t)world * FK_PACK_ROW_WORDS;
     int rc = shard_full_tf(e);
     if (rc) return rc;
@@ -4576,12 +4504,34 @@ static int stitched_exchange(fk_engine *e, fk_comm *comm, int32_t *merge, int32_
     } else {
         HIPCHK(hipMemsetAsync(merge, 0, e->nbins * sizeof(uint32_t), e->stream));
     }
+    if (tw > e->nbins) HIPCHK(hipMemsetAsync(merge + e->nbins, 0, (tw - e->nbins) * sizeof(uint32_t), e->stream));
     uint32_t *limbs = e->h_rows + 32 + e->rows_cap;   /* pinned staging */
     for (int i = 0; i < FK_PACK_COUNTERS; i++)
         for (int j = 0; j < 4; j++) limbs[4 * i + j] = (uint32_t)((v[i] >> (16 * j)) & 0xFFFFu);
-    HIPCHK(hipMemcpyAsync(merge + e->nbins, limbs, 4 * FK_PACK_COUNTERS * sizeof(uint32_t), hipMemcpyHostToDevice,
-                          e->stream));
-    rc = fkc_reduce_i32(comm, merge, e->nbins + 4 * FK_PACK_COUNTERS, 0, e->stream);
+    for (int j = 0; j < FK_PACK_STATS; j++) limbs[4 * FK_PACK_COUNTERS + j] = 0;
+    HIPCHK(hipMemcpyAsync(merge + tw, limbs, (4 * FK_PACK_COUNTERS + FK_PACK_STATS) * sizeof(uint32_t),
+                          hipMemcpyHostToDevice, e->stream));
+    if (scatter) {
+        /* the table sharded by its top index bits (the first bases): rank r
+           keeps bins [r * S, (r + 1) * S) of the sum, S = tw / world; the
+           counters and every slice's (sum, distinct) are all-reduced */
+        const uint64_t S = tw / (uint64_t)world;
+        rc = fkc_reduce_scatter_i32(comm, merge, S, e->stream);
+        if (rc) return rc;
+        const uint64_t lo = (uint64_t)rank * S, n = lo < e->nbins ? std::min(S, e->nbins - lo) : 0;
+        HIPCHK(hipMemsetAsync(e->d_tmp, 0, 2 * sizeof(unsigned long long), e->stream));
+        if (n) {
+            const unsigned gr = (unsigned)std::min<uint64_t>((uint64_t)e->cus * 4, (n + 255) / 256);
+            hipLaunchKernelGGL(k_slice_sum, dim3(gr), dim3(256), 0, e->stream,
+                               reinterpret_cast<const uint32_t *>(merge) + lo, n, e->d_tmp);
+        }
+        hipLaunchKernelGGL(k_slice_limbs, dim3(1), dim3(64), 0, e->stream, e->d_tmp,
+                           merge + tw + 4 * FK_PACK_COUNTERS);
+        HIPCHK(hipGetLastError());
+        rc = fkc_allreduce_i32(comm, merge + tw, 4 * FK_PACK_COUNTERS + FK_PACK_STATS, e->stream);
+    } else {
+        rc = fkc_reduce_i32(comm, merge, tw + 4 * FK_PACK_COUNTERS + FK_PACK_STATS, 0, e->stream);
+    }
     if (rc) return rc;
     HIPCHK(hipStreamSynchronize(e->stream));
     if (first_end_out) *first_end_out = first_end;
@@ -4594,19 +4544,27 @@ extern "C" int fk_engine_shard_exchange(fk_engine *e, fk_comm *comm, int32_t *me
     if (!e->shard_pending) return FK_E_STATE;
     const int world = fkc_world(comm), rank = fkc_rank(comm);
     if (fkc_device(comm) != e->dev) return FK_E_INVALID;
-    const bool try_fast = !info || info[0] != 0;
+    const int32_t flags = info ? info[0] : FK_XCHG_FAST;
+    const bool try_fast = (flags & FK_XCHG_FAST) != 0;
+    const bool scatter = (flags & FK_XCHG_SHARD_TABLE) != 0;
     int rc = set_dev(e);
     if (rc) return rc;
     const uint32_t nrow = (uint32_t)world * FK_PACK_ROW_WORDS;
     rc = ensure_rows(e, nrow);
     if (rc) return rc;
+    const uint64_t tw = merge_table_words(e->nbins, world);
     if (try_fast) {
         /* one collective: pack, all-reduce table + counters + rows, compose */
-        uint32_t *rows = reinterpret_cast<uint32_t *>(merge + e->nbins + 4 * FK_PACK_COUNTERS);
-        rc = fk_engine_shard_pack(e, reinterpret_cast<uint32_t *>(merge), merge + e->nbins, rows, world, rank,
+        int32_t *stats = merge + tw + 4 * FK_PACK_COUNTERS;
+        uint32_t *rows = reinterpret_cast<uint32_t *>(stats + FK_PACK_STATS);
+        rc = fk_engine_shard_pack(e, reinterpret_cast<uint32_t *>(merge), merge + tw, rows, world, rank,
                                   rank == world - 1);
         if (rc) return rc;
-        rc = fkc_allreduce_i32(comm, merge, e->nbins + 4 * FK_PACK_COUNTERS + nrow, e->stream);
+        if (tw > e->nbins) HIPCHK(hipMemsetAsync(merge + e->nbins, 0, (tw - e->nbins) * sizeof(uint32_t), e->stream));
+        HIPCHK(hipMemsetAsync(stats, 0, FK_PACK_STATS * sizeof(int32_t), e->stream));
+        if (flags & FK_XCHG_TEST_INVALID)   /* tests: this rank's pack row reads as invalid */
+            HIPCHK(hipMemsetAsync(rows + (size_t)rank * FK_PACK_ROW_WORDS + 24, 0, sizeof(uint32_t), e->stream));
+        rc = fkc_allreduce_i32(comm, merge, tw + 4 * FK_PACK_COUNTERS + FK_PACK_STATS + nrow, e->stream);
         if (rc) return rc;
         rc = rows_fetch(e, rows, nrow);
         if (rc) return rc;
@@ -4622,9 +4580,18 @@ extern "C" int fk_engine_shard_exchange(fk_engine *e, fk_comm *comm, int32_t *me
         /* some guess did not hold (every rank sees it): stitched, below */
     }
     int32_t first_end = -1;
-    rc = stitched_exchange(e, comm, merge, &first_end);
+    rc = stitched_exchange(e, comm, merge, &first_end, scatter);
     if (rc) return rc;
     if (info) { info[0] = 0; info[1] = first_end; }
+    return FK_OK;
+}
+
+extern "C" int fk_merge_layout(int k, int world, uint64_t *table_words, uint64_t *total_words) {
+    if (k < FK_K_MIN || k > FK_K_MAX_DENSE || world < 1) return FK_E_INVALID;
+    const uint64_t tw = merge_table_words(1ull << (2 * k), world);
+    if (table_words) *table_words = tw;
+    if (total_words)
+        *total_words = tw + 4 * FK_PACK_COUNTERS + FK_PACK_STATS + (uint64_t)world * FK_PACK_ROW_WORDS;
     return FK_OK;
 }
 

@@ -16,6 +16,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <ctype.h>
 #include <fcntl.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -164,6 +165,80 @@ extern "C" void fk_input_destroy(fk_input *in) {
         hipFree(in->d);
     }
     delete in;
+}
+
+/*
+ * Device choice for one process among many on a node.  The reference's sweep
+ * driver starts 24 ./findKmer processes at once (k6thru11fullANDupstream.sh:
+ * 16-24); with "the current device" every one of them would land on GPU 0.
+ * FINDKMER_DEVICE=<ordinal> pins a process; otherwise the candidates are the
+ * devices whose free HBM covers the run's estimated need, and the process
+ * takes candidate (salt mod count) -- salt = its pid, so processes started
+ * together spread round-robin instead of all picking the same emptiest GPU;
+ * with no candidate, the device with the most free HBM.  Free HBM comes from
+ * the amdgpu sysfs counters (no HIP context on the other GPUs), else from
+ * hipMemGetInfo.
+ */
+extern "C" int fk_device_policy(int ndev, const uint64_t *free_bytes, uint64_t need, uint32_t salt) {
+    if (ndev < 1 || !free_bytes) return FK_E_INVALID;
+    std::vector<int> fits;
+    int best = 0;
+    for (int d = 0; d < ndev; d++) {
+        if (free_bytes[d] >= need) fits.push_back(d);
+        if (free_bytes[d] > free_bytes[best]) best = d;
+    }
+    return fits.empty() ? best : fits[salt % fits.size()];
+}
+
+static bool read_u64(const char *path, uint64_t *v) {
+    FILE *f = fopen(path, "r");
+    if (!f) return false;
+    unsigned long long x = 0;
+    const bool ok = fscanf(f, "%llu", &x) == 1;
+    fclose(f);
+    *v = (uint64_t)x;
+    return ok;
+}
+
+static bool sysfs_free_vram(int dev, uint64_t *free_b) {
+    char bus[64] = {};
+    if (hipDeviceGetPCIBusId(bus, (int)sizeof bus - 1, dev) != hipSuccess) return false;
+    for (char *c = bus; *c; c++) *c = (char)tolower((unsigned char)*c);
+    char path[256];
+    uint64_t total = 0, used = 0;
+    snprintf(path, sizeof path, "/sys/bus/pci/devices/%s/mem_info_vram_total", bus);
+    if (!read_u64(path, &total) || total == 0) return false;
+    snprintf(path, sizeof path, "/sys/bus/pci/devices/%s/mem_info_vram_used", bus);
+    if (!read_u64(path, &used)) return false;
+    *free_b = total > used ? total - used : 0;
+    return true;
+}
+
+extern "C" int fk_device_select(uint64_t need, int *device) {
+    if (!device) return FK_E_INVALID;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1) return FK_E_NO_DEVICE;
+    int dev = 0;
+    if (const char *pin = getenv("FINDKMER_DEVICE")) {
+        char *end = nullptr;
+        const long v = strtol(pin, &end, 10);
+        if (!*pin || *end || v < 0 || v >= ndev) return FK_E_INVALID;
+        dev = (int)v;
+    } else if (ndev > 1) {
+        std::vector<uint64_t> fr((size_t)ndev, 0);
+        bool sysfs = true;
+        for (int d = 0; d < ndev && sysfs; d++) sysfs = sysfs_free_vram(d, &fr[(size_t)d]);
+        if (!sysfs) {
+            for (int d = 0; d < ndev; d++) {
+                size_t f = 0, t = 0;
+                if (hipSetDevice(d) == hipSuccess && hipMemGetInfo(&f, &t) == hipSuccess) fr[(size_t)d] = f;
+            }
+        }
+        dev = fk_device_policy(ndev, fr.data(), need, (uint32_t)getpid());
+    }
+    if (hipSetDevice(dev) != hipSuccess) return FK_E_HIP;
+    *device = dev;
+    return FK_OK;
 }
 
 /*

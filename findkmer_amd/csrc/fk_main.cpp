@@ -77,6 +77,7 @@ static struct conf {
 static int sweep_kmax = -1;          /* --sweep KMAX (extension) */
 static fk_input *g_input = nullptr;  /* device-resident copy of the sequence file */
 static bool g_input_tried = false;
+static int g_device = -1;            /* fk_device_select's choice */
 
 static void check_file(const char *filename, const char *mode) {   /* :233-242 */
     FILE *file = fopen(filename, mode);
@@ -433,10 +434,24 @@ static int run_k(int argc) {
     /* load the file to HBM once (and reuse it for every k of a sweep) */
     if (!g_input_tried) {
         g_input_tried = true;
+        /* the GPU of this process (fk_device_select: FINDKMER_DEVICE, else
+           spread over the devices with room for the file and the engine's
+           buffers: ~2 bytes of partition codes per input byte for
+           8 <= k <= 12, 8 bytes of slots for k >= 17) */
+        struct stat sb;
+        const uint64_t fsize = stat(config.sequence_file, &sb) == 0 ? (uint64_t)sb.st_size : 0;
+        const int kk = sweep_kmax > config.k ? sweep_kmax : config.k;
+        const uint64_t per = kk > FK_K_MAX_DENSE ? 10 : (kk >= 8 ? 4 : 2);
+        int dsel = fk_device_select(fsize * per + (256ull << 20), &g_device);
+        if (dsel == FK_E_INVALID) {
+            fprintf(stderr, "findKmer: FINDKMER_DEVICE names no visible GPU\n");
+            exit(EXIT_FAILURE);
+        }
+        if (dsel) die_engine(dsel);
         const char *ing = getenv("FINDKMER_INGEST");
         if (!ing || strcmp(ing, "stream") != 0) {
             const char *nt = getenv("FINDKMER_INGEST_THREADS");   /* default: the library's choice */
-            int lrc = fk_input_load(config.sequence_file, -1, nt ? atoi(nt) : 0, &g_input);
+            int lrc = fk_input_load(config.sequence_file, g_device, nt ? atoi(nt) : 0, &g_input);
             if (lrc == FK_E_HIP || lrc == FK_E_NO_DEVICE) die_engine(lrc);
             /* not a regular file, or larger than free HBM: stream it */
             if (lrc) g_input = nullptr;
@@ -455,7 +470,7 @@ static int run_k(int argc) {
 
     fk_opts opts;
     memset(&opts, 0, sizeof opts);
-    opts.device = -1;
+    opts.device = g_device;
     if (on_device) fk_input_info(g_input, nullptr, nullptr, &opts.device, nullptr);
     opts.want_nodes = 1;
     opts.collect_unknown = 1;

@@ -26,6 +26,14 @@ only when a shard may end the stream:
    from the same collective and checks the merged table for the reference's
    rollover exit (a u32 trie counter reaching 2^32, :642-648): a merged bin
    that wrapped makes the table total fall short of the window count.
+   For k >= SHARD_KMIN (4^k >= 16 Mi bins: 64 MiB to 16 GiB) the table is
+   sharded instead: a reduce-scatter leaves rank r the bins
+   [r*S, (r+1)*S) of the sum -- the k-mers whose first bases fall in r's
+   range, a contiguous run of the CSV's rows (findKmer.cpp:719-724) -- and
+   one small all-reduce gives every rank the counters plus every slice's
+   total and distinct bins (the rollover check needs the whole table's sum).
+   ShardedResult.table_full() gathers the slices onto rank 0 when one
+   process writes the CSV.
 
 The library's own RCCL communicator (backend nccl, native_comm) runs the
 whole exchange inside fk_engine_shard_exchange on the engine's stream: the
@@ -51,8 +59,8 @@ import torch
 import torch.distributed as dist
 
 from . import FK_E_EMPTY, FK_E_ROLLOVER, FK_E_SUMMARY, FK_E_UNTERMINATED_HEADER, FK_OK
-from . import FK_PACK_COUNTERS, FK_PACK_ROW_WORDS
-from . import Comm, FindKmerError, FkState, FkSummary, comm_id, shard_rows_compose, summary_apply, summary_is_full
+from . import FK_PACK_COUNTERS, FK_PACK_ROW_WORDS, FK_PACK_STATS
+from . import Comm, FindKmerError, FkState, FkSummary, comm_id, lib, shard_rows_compose, summary_apply, summary_is_full
 
 SUMMARY_WORDS = 12
 GATHER_WORDS = SUMMARY_WORDS + 1      # + "my summary is full" flag
@@ -66,25 +74,38 @@ LIMBS = 4
 COUNTER_SLOTS = len(COUNTERS) * LIMBS
 assert len(COUNTERS) == FK_PACK_COUNTERS   # the order fk_engine_shard_pack writes them in
 ROW_WORDS = FK_PACK_ROW_WORDS
+STAT_SLOTS = FK_PACK_STATS              # a sharded table's (total, distinct) as 4 limbs each
 FAST_KMAX = 7                          # shards counted in one pass (k_count + k_tail)
+SHARD_KMIN = 12                        # from here on the merged table is sharded over the ranks
 
 
 def _to_i64(v):
     return v - _U64 if v >= 1 << 63 else v
 
 
+def table_words(k, world):
+    """4^k rounded up to a multiple of world (fk_merge_layout)"""
+    nb = 1 << (2 * k)
+    return (nb + world - 1) // world * world
+
+
 def merge_buffer(k, device, world=None):
-    """The int32 buffer count_sharded merges: the 4^k table, the counter
-    limbs, then one pack row per rank (the fast path's all-gather)."""
+    """The int32 buffer count_sharded merges (include/findkmer.h,
+    fk_merge_layout): the table padded to a multiple of the world size, the
+    counter limbs, the slice statistics, then one pack row per rank (the fast
+    path's all-gather)."""
     if world is None:
         world = dist.get_world_size() if dist.is_initialized() else 1
-    return torch.zeros((1 << (2 * k)) + COUNTER_SLOTS + world * ROW_WORDS, dtype=torch.int32, device=device)
+    return torch.zeros(table_words(k, world) + COUNTER_SLOTS + STAT_SLOTS + world * ROW_WORDS, dtype=torch.int32,
+                       device=device)
 
 
 def _regions(buf, k, world):
-    nb = 1 << (2 * k)
-    assert buf.numel() >= nb + COUNTER_SLOTS + world * ROW_WORDS, "merge_buffer(k, device, world)"
-    return nb, buf[:nb + COUNTER_SLOTS], buf[nb + COUNTER_SLOTS:nb + COUNTER_SLOTS + world * ROW_WORDS]
+    """(4^k, padded table words, table + counters + stats, rows)"""
+    nb, tw = 1 << (2 * k), table_words(k, world)
+    end = tw + COUNTER_SLOTS + STAT_SLOTS
+    assert buf.numel() >= end + world * ROW_WORDS, "merge_buffer(k, device, world)"
+    return nb, tw, buf[:end], buf[end:end + world * ROW_WORDS]
 
 
 def _compose(words, world, rank):
@@ -157,51 +178,82 @@ def sum_tables(table, group=None, everywhere=False):
     return table
 
 
+def _limbs_value(limbs):
+    v = 0
+    for j, x in enumerate(limbs):
+        v += int(x) << (16 * j)
+    return v % _U64
+
+
 class ShardedResult:
     """The merged result of one sharded pass.  Complete on rank 0 (the reduce
-    destination); other ranks hold only their own contribution.  Counter
-    fields mirror fk_result (include/findkmer.h); they are decoded from the
-    reduced buffer on first access (one device-to-host copy)."""
+    destination), on every rank after the one-collective path, and with a
+    sharded table (`sharded`) each rank holds the slice [lo, hi) of the
+    merged table (`table`) and every merged counter.  Counter fields mirror
+    fk_result (include/findkmer.h); they are decoded from the buffer on
+    first access (one device-to-host copy)."""
 
-    def __init__(self, buf, k, rank, first_end, local=None, path="stitched", transport="torch"):
+    def __init__(self, buf, k, rank, first_end, local=None, path="stitched", transport="torch", world=1,
+                 sharded=False, group=None):
         self.local = local          # this rank's own fk_result (timings)
         self.path = path            # "fast": one all-reduce; "stitched": summary exchange + reduce
         self.transport = transport  # "rccl-native": the library's own communicator; "torch": torch.distributed
         self.buf = buf
         self.k = k
         self.rank = rank
+        self.world = world
+        self.group = group
         self.first_end = first_end
+        self.sharded = sharded and path == "stitched"
         self.nb = 1 << (2 * k)
-        self.table = buf[:self.nb]
+        self.tw = table_words(k, world)
+        if self.sharded:
+            S = self.tw // world
+            self.lo, self.hi = min(rank * S, self.nb), min((rank + 1) * S, self.nb)
+        else:
+            self.lo, self.hi = 0, self.nb
+        self.table = buf[self.lo:self.hi]
         self._vals = None
         self._tsum = self._distinct = None
 
     def _table_stats(self):
         """The merged table's u64 total (int32 sum + 2^32 per negative bin)
         and its distinct k-mers, computed on first use (like `table`, valid
-        until the buffer is merged into again)."""
-        assert self.rank == 0, "the merged table lives on rank 0"
+        until the buffer is merged into again); a sharded table's come from
+        the all-reduced slice statistics."""
         if self._tsum is None:
-            t = self.table
-            self._tsum = int((t.sum(dtype=torch.int64) + (t < 0).sum(dtype=torch.int64) * (1 << 32)).item())
-            self._distinct = int((t != 0).sum(dtype=torch.int64).item())
+            if self.sharded:
+                st = self.buf[self.tw + COUNTER_SLOTS:self.tw + COUNTER_SLOTS + STAT_SLOTS].tolist()
+                self._tsum, self._distinct = _limbs_value(st[:4]), _limbs_value(st[4:])
+            else:
+                assert self.rank == 0 or self.path == "fast", "the merged table lives on rank 0"
+                t = self.table
+                self._tsum = int((t.sum(dtype=torch.int64) + (t < 0).sum(dtype=torch.int64) * (1 << 32)).item())
+                self._distinct = int((t != 0).sum(dtype=torch.int64).item())
         return self._tsum, self._distinct
+
+    def table_full(self, dst=0):
+        """The whole merged table (int32 view of the u32 counts) on rank
+        `dst`, None on the others; a collective for a sharded table (every
+        rank calls it), a view of the buffer otherwise."""
+        if not self.sharded:
+            return self.buf[:self.nb] if self.rank == dst or self.path == "fast" else None
+        S = self.tw // self.world
+        mine = self.buf[self.rank * S:(self.rank + 1) * S].contiguous()
+        parts = [torch.empty_like(mine) for _ in range(self.world)] if self.rank == dst else None
+        dist.gather(mine, parts, dst=dist.get_global_rank(self.group, dst) if self.group is not None else dst,
+                    group=self.group)
+        return torch.cat(parts)[:self.nb] if parts is not None else None
 
     def _decode(self):
         if self._vals is None:
-            limbs = self.buf[self.nb:self.nb + COUNTER_SLOTS].tolist()
-            vals = {}
-            for i, name in enumerate(COUNTERS):
-                v = 0
-                for j in range(LIMBS):
-                    v += int(limbs[i * LIMBS + j]) << (16 * j)
-                vals[name] = v % _U64
-            self._vals = vals
+            limbs = self.buf[self.tw:self.tw + COUNTER_SLOTS].tolist()
+            self._vals = {name: _limbs_value(limbs[i * LIMBS:(i + 1) * LIMBS]) for i, name in enumerate(COUNTERS)}
         return self._vals
 
     def __getattr__(self, name):
         if name.startswith("_") or name in ("buf", "k", "rank", "first_end", "table", "local", "nb", "path",
-                                                     "transport"):
+                                                     "transport", "world", "group", "sharded", "tw", "lo", "hi"):
             raise AttributeError(name)
         v = self._decode()
         if name == "base_count":
@@ -239,7 +291,7 @@ class ShardedResult:
 
 def _put_counters(buf, values, pinned, nb=None):
     """Write the u64 counters into the buffer's limb slots (host -> buffer),
-    after the nb table bins (default: the last COUNTER_SLOTS entries)."""
+    after the nb table words (default: the last COUNTER_SLOTS entries)."""
     limbs = []
     for v in values:
         v = int(v) % _U64
@@ -266,14 +318,23 @@ def native_comm(group=None):
         return _comms[key]
     rank = dist.get_rank(group)
     world = dist.get_world_size(group)
-    t = torch.zeros(129, dtype=torch.uint8, device="cuda")
+    # every rank checks what fk_comm_create needs before its collective init
+    # (RCCL loadable, the device usable), and all agree first: a rank that
+    # cannot join must not leave the others blocked inside the init
+    ok = lib().fk_comm_available(torch.cuda.current_device()) == FK_OK
+    t = torch.zeros(130, dtype=torch.uint8, device="cuda")
+    t[129] = 0 if ok else 1
+    dist.all_reduce(t[129:], group=group)
+    if int(t[129].item()):
+        _comms[key] = None
+        return None
     if rank == 0:
         try:
             t[:128].copy_(torch.frombuffer(bytearray(comm_id()), dtype=torch.uint8))
         except FindKmerError:
             t[128] = 1
     src = dist.get_global_rank(group, 0) if group is not None else 0
-    dist.broadcast(t, src=src, group=group)
+    dist.broadcast(t[:129], src=src, group=group)
     c, failed = None, bool(t[128].item())
     if not failed:
         try:
@@ -326,10 +387,19 @@ def _fast_exchange(engine, buf, rank, world, group, times, t0):
         fp = _FastPath(engine, buf, world)
         engine._fk_fast = fp
     k = engine.k
-    nb, merged, rows = _regions(buf, k, world)
-    n = nb + COUNTER_SLOTS + world * ROW_WORDS
+    nb, tw, merged, rows = _regions(buf, k, world)
+    n = tw + COUNTER_SLOTS + STAT_SLOTS + world * ROW_WORDS
     dst = fp.stage if fp.stage is not None else buf
-    engine.shard_pack(dst.data_ptr(), dst.data_ptr() + 4 * nb, dst.data_ptr() + 4 * (nb + COUNTER_SLOTS),
+    if not fp.host_pack:
+        # the pack writes into the buffer after whatever torch's stream still
+        # has pending on it (a previous pass's collective or copy)
+        fp.ext.wait_stream(torch.cuda.current_stream())
+    if tw > nb or STAT_SLOTS:
+        dst[nb:tw].zero_()
+        dst[tw + COUNTER_SLOTS:tw + COUNTER_SLOTS + STAT_SLOTS].zero_()
+        if not fp.host_pack:
+            fp.ext.wait_stream(torch.cuda.current_stream())
+    engine.shard_pack(dst.data_ptr(), dst.data_ptr() + 4 * tw, dst.data_ptr() + 4 * (tw + COUNTER_SLOTS + STAT_SLOTS),
                       world, rank, rank == world - 1)
     if not fp.host_pack:
         # the copy or the collective runs after the pack (engine stream ->
@@ -356,11 +426,11 @@ def _fast_exchange(engine, buf, rank, world, group, times, t0):
         times["count"] = times.get("count", 0.0) + (t1 - t0)
         times["exchange"] = times.get("exchange", 0.0) + (t2 - t1)
         times["resolve"] = times.get("resolve", 0.0) + (time.perf_counter() - t2)
-    return ShardedResult(buf, k, rank, None, r, path="fast")
+    return ShardedResult(buf, k, rank, None, r, path="fast", world=world, group=group)
 
 
 def count_sharded(engine, ptr, nbytes, halo, buf, group=None, times=None, pinned=None, fast=True,
-                  native=True):
+                  native=True, shard_table=None, test_invalid=False):
     """One sharded pass on this rank's GPU: count the shard, stitch the entry
     state, recount what the guess got wrong, and merge the tables and
     counters into `buf` (merge_buffer(k, device, world): on the GPU for RCCL,
@@ -376,11 +446,20 @@ def count_sharded(engine, ptr, nbytes, halo, buf, group=None, times=None, pinned
 
     `engine` is a findkmer_amd.Engine (or, in the CPU tests, a model with the
     same feed_shard_device / summary / summary_full / resolve / finish /
-    table_to_device / shard_pack methods)."""
+    table_to_device / shard_pack methods).
+
+    shard_table: the stitched path reduce-scatters the table (each rank
+    keeps its slice of the merged table) instead of reducing it onto rank 0;
+    None = for k >= SHARD_KMIN.  test_invalid (native path, tests): this
+    rank's pack row reads as invalid, forcing the fallback after the
+    one-collective all-reduce."""
     import time
     rank = dist.get_rank(group)
     world = dist.get_world_size(group)
     dev = buf.device
+    k = engine.k
+    if shard_table is None:
+        shard_table = k >= SHARD_KMIN
     t0 = time.perf_counter()
     engine.feed_shard_device(ptr, nbytes, halo)
     comm = None
@@ -390,14 +469,15 @@ def count_sharded(engine, ptr, nbytes, halo, buf, group=None, times=None, pinned
         # the whole exchange inside the library, on the engine's stream: one
         # all-reduce when every guess held (k <= 7), else the stitched
         # exchange (fk_engine_shard_exchange)
-        one, first_end = engine.shard_exchange(comm, buf.data_ptr(), fast=fast and engine.k <= FAST_KMAX)
+        one, first_end = engine.shard_exchange(comm, buf.data_ptr(), fast=fast and k <= FAST_KMAX,
+                                               shard_table=shard_table, test_invalid=test_invalid)
         t1 = time.perf_counter()
         _, r = engine.finish(allow=(FK_OK, FK_E_ROLLOVER, FK_E_UNTERMINATED_HEADER, FK_E_EMPTY))
         if times is not None:
             times["exchange"] = times.get("exchange", 0.0) + (t1 - t0)
             times["finish"] = times.get("finish", 0.0) + (time.perf_counter() - t1)
-        return ShardedResult(buf, engine.k, rank, first_end, r, path="fast" if one else "stitched",
-                             transport="rccl-native")
+        return ShardedResult(buf, k, rank, first_end, r, path="fast" if one else "stitched",
+                             transport="rccl-native", world=world, sharded=shard_table, group=group)
     if fast and engine.k <= FAST_KMAX and hasattr(engine, "shard_pack"):
         got = _fast_exchange(engine, buf, rank, world, group, times, t0)
         if got is not None:
@@ -419,7 +499,7 @@ def count_sharded(engine, ptr, nbytes, halo, buf, group=None, times=None, pinned
     t2 = time.perf_counter()
     counting = first_end is None or rank <= first_end
     last = first_end if first_end is not None else world - 1
-    nb, merged, _ = _regions(buf, engine.k, world)
+    nb, tw, merged, _ = _regions(buf, k, world)
     if counting:
         if buf.is_cuda:
             engine.table_to_device(buf.data_ptr())
@@ -431,12 +511,39 @@ def count_sharded(engine, ptr, nbytes, halo, buf, group=None, times=None, pinned
     else:
         buf[:nb].zero_()
         vals = [0] * len(COUNTERS)
-    _put_counters(buf, vals, pinned, nb)
-    sum_tables(merged, group)
+    buf[nb:tw].zero_()
+    buf[tw + COUNTER_SLOTS:tw + COUNTER_SLOTS + STAT_SLOTS].zero_()
+    _put_counters(buf, vals, pinned, tw)
+    if shard_table:
+        _scatter_tables(buf, k, rank, world, group)
+    else:
+        sum_tables(merged, group)
     if times is not None:
         # host wall time per phase: count (the feed returns when the shard's
         # kernels are done), stitch + resolve, table merge (enqueued)
         times["count"] = times.get("count", 0.0) + (t1 - t0)
         times["stitch"] = times.get("stitch", 0.0) + (t2 - t1)
         times["merge"] = times.get("merge", 0.0) + (time.perf_counter() - t2)
-    return ShardedResult(buf, engine.k, rank, first_end, r)
+    return ShardedResult(buf, k, rank, first_end, r, world=world, sharded=shard_table, group=group)
+
+
+def _scatter_tables(buf, k, rank, world, group):
+    """The sharded merge through torch.distributed: rank r gets bins
+    [r*S, (r+1)*S) of the summed table (a reduce-scatter over RCCL; gloo has
+    none, so an all-reduce whose other slices are then ignored), then the
+    counters and each slice's (total, distinct) limbs are all-reduced."""
+    nb, tw = 1 << (2 * k), table_words(k, world)
+    S = tw // world
+    table = buf[:tw]
+    if dist.get_backend(group) == "nccl":
+        mine = torch.empty(S, dtype=buf.dtype, device=buf.device)
+        dist.reduce_scatter_tensor(mine, table, op=dist.ReduceOp.SUM, group=group)
+        buf[rank * S:(rank + 1) * S].copy_(mine)
+    else:
+        dist.all_reduce(table, op=dist.ReduceOp.SUM, group=group)
+    sl = buf[min(rank * S, nb):min((rank + 1) * S, nb)]
+    tot = int((sl.sum(dtype=torch.int64) + (sl < 0).sum(dtype=torch.int64) * (1 << 32)).item())
+    nz = int((sl != 0).sum(dtype=torch.int64).item())
+    limbs = [(v >> (16 * j)) & 0xFFFF for v in (tot, nz) for j in range(LIMBS)]
+    buf[tw + COUNTER_SLOTS:tw + COUNTER_SLOTS + STAT_SLOTS].copy_(torch.tensor(limbs, dtype=torch.int32))
+    dist.all_reduce(buf[tw:tw + COUNTER_SLOTS + STAT_SLOTS], op=dist.ReduceOp.SUM, group=group)

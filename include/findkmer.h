@@ -202,10 +202,35 @@ typedef struct fk_comm fk_comm;
 int  fk_comm_id(uint8_t *id /* FK_COMM_ID_BYTES */);
 int  fk_comm_create(const uint8_t *id, int world, int rank, int device, fk_comm **out);
 void fk_comm_destroy(fk_comm *c);
+/* The merge buffer of a sharded pass (int32 words, device memory for
+ * fk_engine_shard_exchange):
+ *   [0, TW)           the count table, TW = 4^k rounded up to a multiple of
+ *                     `world` (zero padding after 4^k);
+ *   [TW, +4*14)       the counter limbs (fk_engine_shard_pack's order);
+ *   [.., +8)          FK_PACK_STATS: a sharded table's total u64 count and
+ *                     distinct bins, as 16-bit limbs;
+ *   [.., +world*32)   the pack rows.
+ * fk_merge_layout gives TW and the total size for (k, world). */
+#define FK_PACK_STATS 8
+int  fk_merge_layout(int k, int world, uint64_t *table_words, uint64_t *total_words);
+
+/* An RCCL communicator can be created on `device` in this process (RCCL
+ * loads with every entry point, the device is usable) -- everything
+ * fk_comm_create checks before its collective init, so ranks can agree on
+ * it first and never leave one rank alone inside ncclCommInitRank. */
+int  fk_comm_available(int device);
+
+/* Flags of fk_engine_shard_exchange (info[0]). */
+#define FK_XCHG_FAST 1          /* try the one-collective path */
+#define FK_XCHG_SHARD_TABLE 2   /* stitched path: reduce-scatter the table
+                                   instead of reducing it onto rank 0 */
+#define FK_XCHG_TEST_INVALID 4  /* tests: mark this rank's pack row invalid
+                                   (forces the fallback after the collective) */
+
 /* A sharded pass's whole exchange on the engine's stream, after
  * fk_engine_feed_shard, with the library's communicator; `merge` is a device
- * buffer of 4^k + 4 * FK_PACK_COUNTERS + world * FK_PACK_ROW_WORDS int32.
- *  - one collective (tried when info == NULL or info[0] != 0): pack
+ * buffer laid out as above (fk_merge_layout's total_words int32).
+ *  - one collective (info == NULL, or FK_XCHG_FAST in info[0]): pack
  *    (fk_engine_shard_pack, slot = rank), an in-place all-reduce of the whole
  *    buffer, the rows published to host memory, one host wait,
  *    fk_shard_rows_compose, fk_engine_resolve.  Every rank's buffer then
@@ -215,8 +240,13 @@ void fk_comm_destroy(fk_comm *c);
  *    rank takes this branch together): the shards' full transfer functions
  *    all-gathered and composed, fk_engine_resolve, the shards' end flags
  *    all-gathered (a 0xFF byte, findKmer.cpp:988), then the table and counter
- *    limbs -- zero on ranks after the first ending shard -- reduced onto rank
- *    0 (info[0] = 0, info[1] = that shard's rank or -1).
+ *    limbs -- zero on ranks after the first ending shard -- either reduced
+ *    onto rank 0, or with FK_XCHG_SHARD_TABLE reduce-scattered: rank r owns
+ *    bins [r*TW/world, (r+1)*TW/world) of the merged table (the table
+ *    sharded by its top index bits, i.e. the k-mers' first bases, which is
+ *    also the CSV's row order, findKmer.cpp:719-724), every rank gets the
+ *    merged counters and the table's total and distinct bins.  info[0] = 0,
+ *    info[1] = the first ending shard's rank or -1.
  * The shard is resolved either way (fk_engine_finish gives its own result),
  * and the call returns after the device work.  Replaces no reference call
  * (the reference is single-threaded, findKmer.cpp:962). */
@@ -301,6 +331,18 @@ void fk_input_destroy(fk_input *in);
  * byte ends the scan, or a run reaches the reference's int32 seqSize wrap):
  * feed the file in pieces and use fk_engine_progress instead. */
 int  fk_input_headers(fk_input *in, int k, uint64_t *pos, uint64_t *bases, uint64_t cap, uint64_t *n);
+
+/* ---- device choice (several ./findKmer processes on one node) -----------
+ * The reference's sweep driver starts 24 processes at once
+ * (k6thru11fullANDupstream.sh:16-24).  fk_device_select makes the chosen
+ * device current and returns it: FINDKMER_DEVICE=<ordinal> if set (else
+ * FK_E_INVALID for a bad value); otherwise, among the devices whose free HBM
+ * is >= need bytes, the one at (pid mod their count), so processes started
+ * together spread over the GPUs; if none has enough, the one with the most
+ * free HBM.  fk_device_policy is that rule alone (free_bytes[ndev] given):
+ * returns the ordinal. */
+int  fk_device_select(uint64_t need, int *device);
+int  fk_device_policy(int ndev, const uint64_t *free_bytes, uint64_t need, uint32_t salt);
 
 /* ---- host side of the boundary: byte-identical output writers ---------- */
 

@@ -1,9 +1,10 @@
-# the whole GPU suite + smoke (no profiles)
+# the whole -m gpu suite (as the driver runs it) plus smoke(), logs under gpurun_out/
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 1000 python -u -m pytest tests/ -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/tests.log 2>&1 || { tail -40 gpurun_out/tests.log; exit 1; }
-tail -2 gpurun_out/tests.log
-timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { tail -20 gpurun_out/smoke.log; exit 1; }
+mkdir -p gpurun_out
+timeout -k 10 ${TLIM:-1000} python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread ${SEL:-} \
+  > gpurun_out/suite.log 2>&1 || { tail -60 gpurun_out/suite.log; exit 1; }
+tail -3 gpurun_out/suite.log
+timeout -k 10 120 python3 -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { cat gpurun_out/smoke.log; exit 1; }
 tail -1 gpurun_out/smoke.log

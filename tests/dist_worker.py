@@ -28,6 +28,10 @@ def main():
     ap.add_argument("--native", type=int, default=1, help="nccl: 0 = the one-collective path through torch.distributed")
     ap.add_argument("--input", default="mixed", choices=["mixed", "fasta"],
                     help="fasta: one header + 80-column ACGT lines (every k <= 7 shard counts in one pass)")
+    ap.add_argument("--shard-table", default="auto", choices=["auto", "0", "1"],
+                    help="1: the merged table reduce-scattered over the ranks (auto: k >= 12)")
+    ap.add_argument("--test-invalid", type=int, default=0,
+                    help="native path: mark this rank's pack row invalid (the fallback after the all-reduce)")
     args = ap.parse_args()
     import numpy as np
     import torch
@@ -66,16 +70,25 @@ def main():
     buf = fkdist.merge_buffer(args.k, "cuda" if args.backend == "nccl" else "cpu")
     # twice: the second pass reuses the engine, the buffer and the fast
     # path's scratch (stale rows from the first must not leak into it)
+    shard = None if args.shard_table == "auto" else bool(int(args.shard_table))
     for _ in range(2):
         eng.reset()
         res = fkdist.count_sharded(eng, dev.data_ptr() + halo, hi - lo, halo, buf, fast=bool(args.fast),
-                                   native=bool(args.native))
+                                   native=bool(args.native), shard_table=shard, test_invalid=bool(args.test_invalid))
+    full = res.table_full()   # every rank (a gather when the table is sharded)
     out = {"rank": rank}
     if rank == 0:
-        want, r, _ = oracle.count_dense(data, args.k)
-        got = res.table.cpu().numpy().view(np.uint32)
+        got = full.cpu().numpy().view(np.uint32)
+        if args.k <= 13:
+            want, r, _ = oracle.count_dense(data, args.k)
+            equal = bool(np.array_equal(got, want))
+        else:
+            keys, cnts, r = oracle.count_sparse(data, args.k, cap=len(data) + 16)
+            nz = np.nonzero(got)[0]
+            equal = bool(np.array_equal(nz.astype(np.uint64), keys) and np.array_equal(got[nz], cnts))
         out.update({
-            "table_equal": bool(np.array_equal(got, want)),
+            "table_equal": equal,
+            "sharded": res.sharded,
             "windows": [res.windows, r.windows],
             "valid_bases": [res.valid_bases, r.valid_bases],
             "base_count": [res.base_count, list(r.base_count)],

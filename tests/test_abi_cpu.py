@@ -181,3 +181,21 @@ def test_shard_rows_compose():
     eof = _compact(0, 0, 0, 16384, 0, 0x0ABC, 0, 0, 1000, 16384, k)
     eof.w[9] = 1
     assert fk.shard_rows_compose(_rows([eof, s1]).ctypes.data, 2, 1) is None
+
+
+def test_device_policy_spreads_processes():
+    """fk_device_policy (host-only rule behind fk_device_select): devices
+    with room for the run take processes round-robin by salt (the pid), a
+    full device is skipped, and with no room anywhere the emptiest wins"""
+    import ctypes
+    L = fk.lib()
+    G = 1 << 30
+    free = (ctypes.c_uint64 * 8)(*[200 * G] * 8)
+    picks = [L.fk_device_policy(8, free, 20 * G, salt) for salt in range(1000, 1024)]
+    assert sorted(set(picks)) == list(range(8)) and all(picks.count(d) == 3 for d in range(8))
+    free[3] = 5 * G
+    picks = {L.fk_device_policy(8, free, 20 * G, salt) for salt in range(64)}
+    assert picks == set(range(8)) - {3}
+    small = (ctypes.c_uint64 * 3)(1 * G, 7 * G, 2 * G)
+    assert L.fk_device_policy(3, small, 20 * G, 5) == 1
+    assert L.fk_device_policy(0, small, 1, 0) == fk.FK_E_INVALID

@@ -51,7 +51,7 @@ def _input(seed, n):
     return bytes(out[:n])
 
 
-def _worker(rank, world, port, data, bounds, mode, results):
+def _worker(rank, world, port, data, bounds, mode, results, shard=False):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     import torch
@@ -60,6 +60,7 @@ def _worker(rank, world, port, data, bounds, mode, results):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         lo, hi = bounds[rank], bounds[rank + 1]
+        shard_table = shard
         shard = data[lo:hi]
         hdr, R, code, _, _ = scan_model.advance(data[:lo], 0, 0, 0)
         if mode == "state":
@@ -80,23 +81,30 @@ def _worker(rank, world, port, data, bounds, mode, results):
             guess = (hdr, R, code)
         eng = scan_model.ModelEngine(K, shard, guess)
         buf = fkdist.merge_buffer(K, "cpu")
-        res = fkdist.count_sharded(eng, 0, len(shard), 0, buf)
+        res = fkdist.count_sharded(eng, 0, len(shard), 0, buf, shard_table=bool(shard_table))
+        full = res.table_full()   # a collective when the table is sharded
+        if res.sharded:
+            # this rank's slice: the first bases' range [lo, hi) of the table
+            want_lo = min(rank * (fkdist.table_words(K, world) // world), 1 << (2 * K))
+            assert res.lo == want_lo and res.table.numel() == res.hi - res.lo
+            assert np.array_equal(res.table.numpy(), buf[res.lo:res.hi].numpy())
         if rank == 0:
             out = {n: getattr(res, n) for n in ("windows", "valid_bases", "base_count", "depth1",
                                                  "unknown_chars", "scanned_bytes", "hit_eof_byte",
                                                  "unterminated_header", "distinct", "rollover")}
             out["first_end"] = res.first_end
             out["path"] = res.path
-            results.put((res.table.numpy().astype(np.uint32).tobytes(), out))
+            out["sharded"] = res.sharded
+            results.put((full.numpy().astype(np.uint32).tobytes(), out))
     finally:
         dist.destroy_process_group()
 
 
-def _run(world, data, bounds, mode):
+def _run(world, data, bounds, mode, shard=False):
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     results = ctx.SimpleQueue()
-    mp.start_processes(_worker, args=(world, _free_port(), data, bounds, mode, results), nprocs=world,
+    mp.start_processes(_worker, args=(world, _free_port(), data, bounds, mode, results, shard), nprocs=world,
                        join=True, start_method="spawn")
     return None if mode == "state" else results.get()
 
@@ -111,9 +119,9 @@ def test_stitched_states_gloo(world):
     _run(world, data, _bounds(len(data), world), "state")
 
 
-def _check(data, world, mode, bounds=None):
+def _check(data, world, mode, bounds=None, shard=False):
     bounds = bounds or _bounds(len(data), world)
-    table, got = _run(world, data, bounds, mode)
+    table, got = _run(world, data, bounds, mode, shard)
     want, r, _ = oracle.count_dense(data, K)
     assert np.array_equal(np.frombuffer(table, dtype=np.uint32), want)
     assert got["windows"] == r.windows
@@ -187,3 +195,24 @@ def test_merged_rollover_detection():
     assert wrapped.rollover and wrapped.status() == fk.FK_E_ROLLOVER
     deep = result([1] * 16, 16, depth1=(1 << 32, 0, 0, 0))
     assert deep.rollover
+
+
+@pytest.mark.parametrize("world,mode", [(2, "full"), (3, "full"), (8, "compact_miss"), (3, "compact")])
+def test_sharded_table_gloo(world, mode):
+    """the table sharded over the ranks (reduce-scatter semantics: rank r
+    keeps bins [r*S, (r+1)*S), world 3 pads 4^5 to 1026 words): the slices
+    gathered in rank order are the oracle's table, and every rank's merged
+    counters, total and distinct bins are exact (the one-collective path,
+    "compact", leaves every rank the whole table instead)"""
+    got = _check(_input(world + 40, 24000), world, mode, shard=True)
+    assert got["sharded"] == (mode != "compact")
+    assert got["path"] == ("fast" if mode == "compact" else "stitched")
+
+
+def test_sharded_table_eof_in_middle_gloo():
+    data = bytearray(_input(41, 24000))
+    b = _bounds(len(data), 3)
+    at = (b[1] + b[2]) // 2
+    data[at - 2:at + 1] = b"\nA\xff"
+    got = _check(bytes(data), 3, "full", b, shard=True)
+    assert got["first_end"] == 1 and got["sharded"]

@@ -113,3 +113,41 @@ def test_rccl_single_rank_merge(k, fast, eof_in, native):
     assert out["transport"] == ("rccl-native" if native else "torch")
     if eof_in >= 0:
         assert out["first_end"] == eof_in
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k,world,eof_in,nbytes", [(12, 2, -1, 3_000_000), (12, 8, 3, 3_000_000),
+                                                  (14, 8, -1, 2_000_000), (16, 2, -1, 1_000_000)])
+def test_sharded_table_gloo_against_oracle(k, world, eof_in, nbytes):
+    """k > 11: the merged table sharded over the ranks by its top index bits
+    (rank r owns bins [r*4^k/G, (r+1)*4^k/G): the north star's "table shards
+    by top bits"), gathered in rank order on rank 0 == the oracle's table
+    (k = 14, 16: its sparse form); the counters, total and distinct bins
+    from the all-reduced limbs"""
+    out = _torchrun(world, 29750 + k + world + eof_in, os.path.join(REPO, "tests", "dist_worker.py"),
+                    ["--k", str(k), "--eof-in", str(eof_in), "--shard-table", "1", "--bytes", str(nbytes)])
+    assert out["table_equal"] and out["sharded"]
+    for key in ("windows", "valid_bases", "base_count", "depth1", "unknown_chars", "scanned_bytes",
+                "hit_eof_byte", "unterminated_header", "distinct"):
+        assert out[key][0] == out[key][1], (key, out[key])
+    assert not out["rollover"]
+    assert out["first_end"] == (eof_in if eof_in >= 0 else None)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k,shard,invalid", [(12, 1, 0), (6, 0, 1), (6, 1, 1), (11, 1, 0)])
+def test_rccl_single_rank_sharded_and_fallback(k, shard, invalid):
+    """The native RCCL exchange (world 1): the reduce-scatter of the table
+    with the slice statistics' all-reduce, and (invalid) a pack row forced
+    invalid after the one-collective all-reduce, so that the fallback runs
+    the stitched exchange over the merge buffer that collective already
+    changed"""
+    out = _torchrun(1, 29850 + 3 * k + shard + 7 * invalid, os.path.join(REPO, "tests", "dist_worker.py"),
+                    ["--k", str(k), "--backend", "nccl", "--input", "fasta", "--shard-table", str(shard),
+                     "--test-invalid", str(invalid)])
+    assert out["table_equal"] and out["transport"] == "rccl-native"
+    for key in ("windows", "valid_bases", "base_count", "depth1", "unknown_chars", "scanned_bytes",
+                "hit_eof_byte", "unterminated_header", "distinct"):
+        assert out[key][0] == out[key][1], (key, out[key])
+    assert out["path"] == "stitched"
+    assert out["sharded"] == bool(shard)

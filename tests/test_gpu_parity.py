@@ -782,16 +782,15 @@ def test_sparse_dense_entry_points_refuse():
 
 
 # ---- k_count's dynamic ranges (k <= 7): static ranges, then claims --------
-# FK_STATIC_PCT < 100 turns them on (the product default is 100: static
-# ranges only, measured as fast on plain streams) and FK_DYN_MIN_CHUNKS=1 for
+# static_pct < 100 turns them on (the product default is 100: static
+# ranges only, measured as fast on plain streams) and dyn_min_chunks=1 for
 # inputs of any size (else only segments of >= 8 chunks per wave slot), so
 # the claim path, k_tail's per-range chain items and the multi-launch
 # fallbacks over dynamic ranges all meet the oracle here.
 
 @pytest.fixture
 def dyn_env(monkeypatch):
-    monkeypatch.setenv("FK_DYN_MIN_CHUNKS", "1")
-    monkeypatch.setenv("FK_STATIC_PCT", "75")
+    monkeypatch.setenv("FINDKMER_TUNE", "dyn_min_chunks=1,static_pct=75")
     yield
 
 
@@ -826,7 +825,7 @@ def test_dynamic_ranges_acgt_and_streaming(dyn_env, k):
 @pytest.mark.parametrize("pct", ["1", "50", "99"])
 def test_dynamic_ranges_static_share(dyn_env, monkeypatch, k, pct):
     """from almost all dynamic to almost all static"""
-    monkeypatch.setenv("FK_STATIC_PCT", pct)
+    monkeypatch.setenv("FINDKMER_TUNE", f"dyn_min_chunks=1,static_pct={pct}")
     data = mixed_input(4000 + int(pct), 2_500_000)
     assert_same(data, k, want_nodes=False)
 
@@ -982,11 +981,11 @@ def test_mixed_tiles_ff_outside_comment(k):
 
 @pytest.mark.parametrize("k", [4, 6, 7, 11, 12])
 def test_mixed_tiles_match_general_path(k, monkeypatch):
-    # the same header-dense input with mixed tiles switched off (FK_NO_MIXED:
+    # the same header-dense input with mixed tiles switched off (no_mixed:
     # the byte walk of tile_general) counts identically
     data = _dense_records(4300 + k, 500_000)
     r1 = assert_same(data, k)
-    monkeypatch.setenv("FK_NO_MIXED", "1")
+    monkeypatch.setenv("FINDKMER_TUNE", "no_mixed=1")
     r2 = assert_same(data, k)
     assert (r1.windows, r1.valid_bases, r1.nodes) == (r2.windows, r2.valid_bases, r2.nodes)
 
@@ -997,8 +996,52 @@ def test_part_resume_budgets(k, budget, monkeypatch):
     # k_part stops a range after `budget` general tiles and k_part<RES> counts
     # the rest (mixed tiles into region 2 of the partition); ranges that stop
     # and ranges that do not in one feed
-    monkeypatch.setenv("FK_PART_GENERAL", budget)
+    monkeypatch.setenv("FINDKMER_TUNE", f"part_general={budget}")
     rng = random.Random(77 + k)
     data = _dense_records(4400 + k, 300_000) + random_text(rng, 900_000, b"ACGT", [1, 1, 1, 1]) + \
         _dense_records(4500 + k, 200_000)
     assert_same(data, k)
+
+
+@pytest.mark.parametrize("k", [5, 11, 13])
+def test_device_feed_segments(k, monkeypatch):
+    """a device feed cut into segments (the HBM budget of segment_budget when
+    other processes share the GPU; forced small here with seg_kb) counts
+    exactly as one segment: the scan state carries across the cuts"""
+    import torch
+    data = mixed_input(606 + k, 3_000_000).replace(b"\xff", b"Z")
+    dev = torch.frombuffer(bytearray(data), dtype=torch.uint8).cuda()
+    torch.cuda.synchronize()
+    t_o, r_o, ub_o = oracle.count_dense(data, k, unknown_cap=1 << 20)
+    monkeypatch.setenv("FINDKMER_TUNE", "seg_kb=272")
+    with fk.Engine(k, want_nodes=True, collect_unknown=True) as e:
+        e.feed_device(dev.data_ptr(), len(data))
+        rc, r = e.finish(allow=(fk.FK_OK, fk.FK_E_UNTERMINATED_HEADER))
+        t = e.table()
+        ub = e.unknown_bytes()
+    assert np.array_equal(t, t_o)
+    assert (r.windows, r.valid_bases, r.distinct, r.nodes) == (r_o.windows, r_o.valid_bases, r_o.distinct, r_o.nodes)
+    assert list(r.base_count) == list(r_o.base_count) and list(r.depth1) == list(r_o.depth1)
+    assert ub == ub_o
+
+
+def test_cli_concurrent_fanout_matches_goldens(manifest, tmp_path):
+    """k6thru11fullANDupstream.sh:16-24 on one node: ./Debug/findKmer and
+    ./findKmer for each k = 6..11 started together in one directory
+    (fk_device_select spreads them over the GPUs; here the box has one), the
+    outputs equal the reference's separate runs"""
+    import hashlib
+    name = "upstream1m.fas"
+    shutil.copy(os.path.join(REPO, "tests", "golden", "inputs", name), tmp_path / name)
+    procs = []
+    for k in range(6, 12):
+        for exe in ("Debug/findKmer", "findKmer"):
+            procs.append(subprocess.Popen([os.path.join(REPO, exe), "-q", "1", "-k", str(k), "-z", "3", "-p", name],
+                                          cwd=tmp_path, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE))
+    for p in procs:
+        _, err = p.communicate(timeout=300)
+        assert p.returncode == 0, err.decode()[-500:]
+    for k in range(6, 12):
+        for kind, rec in manifest[f"up_k{k}_z3"]["files"].items():
+            got = open(tmp_path / rec["name"], "rb").read()
+            assert hashlib.sha256(got).hexdigest() == rec["sha256"], (k, kind)
