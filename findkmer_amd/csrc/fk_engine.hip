@@ -1738,20 +1738,24 @@ k_redo(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint
  * k_bucket_count: one block per slice (and group of rows) counts its runs in
  *   an LDS slice of 2^sh bins and adds the slice into the table.
  */
-/* Waves per k_part block (template parameter W, 8 or 16; chosen per k by
-   part_waves()).  Larger blocks make k_part itself slower (more waves per
-   barrier) but its batches larger, so k_bucket_count reads longer runs:
-   16-wave blocks (one per CU, 136 KiB of LDS) take the k=11 FASTA step from
-   1.12 to 1.08 ms (k_part 616 -> 660 us) and k=12 from 1.85 to 1.73 ms, but
-   k=8 (80 slices: long runs already) from 0.98 to 1.02 ms; 4-wave blocks
-   made k=11 5 % slower and k=12 30 % slower. */
+/* Waves per k_part block (template parameter W, 8 or 16; part_waves_of()).
+   Larger blocks make k_part itself slower (more waves per barrier) but its
+   batches larger, so k_bucket_count reads longer runs: one block per CU for
+   the 512-slice tables (k = 11, 12: 16 waves, 132 KiB of LDS), two 8-wave
+   blocks per CU for k <= 10 (<= 128 slices, long runs already).  Round 2:
+   16-wave blocks took the k=11 FASTA step from 1.12 to 1.08 ms and k=12
+   from 1.85 to 1.73 ms against 8-wave ones; 4-wave blocks made k=11 5 %
+   slower and k=12 30 % slower. */
 #define PART_BLOCK_W(W) ((W) * 64u)
 /* tiles per wave per batch: 2 single-window tiles or 4 pair tiles fill the
    same LDS batch (a pair tile hands over half as many entries) */
 #define PART_TILES(PAIRS) ((PAIRS) ? 4u : 2u)
 #define PART_MAX_BATCH_W(W) (2u * (W) * FK_TILE_BYTES)   /* entries per batch */
 static_assert(PART_MAX_BATCH_W(16u) <= 65536u, "run index words hold 16-bit starts and counts - 1");
-#define PART_MAX_SLICES 1024u   /* k = 11 pairs: 2^24 / 2^15 pair slices + 2^22 / 2^15 single slices */
+/* slices of a batch: k = 11 pairs 2^24 / 2^15 (the single k-mers fold into
+   them, flagged), k = 12 2^24 / 2^15; k <= 10 at most 128 */
+#define PART_SM(W) ((W) >= 16u ? 512u : 128u)
+#define PART_SINGLE 0x8000u   /* a stored code with this bit: a single k-mer (pairs mode) */
 
 /* A run index word: (start << 16) | (count - 1) for a run of count >= 1
    codes (a batch holds up to 2^16 of them, all possibly in one slice), and
@@ -1768,9 +1772,10 @@ struct PartGeo {
     uint32_t *idx;         /* [slice][row]: run_word(start, count) */
     uint32_t rounds;       /* rows per block */
     uint32_t rows;         /* rows in all: grid * rounds */
-    uint32_t nslices;
+    uint32_t nslices;      /* a multiple of 8 */
     uint32_t sh;           /* slice index = code >> sh; stored code = code & (2^sh - 1) */
-    uint32_t npair;        /* pairs mode: slices [0, npair) hold (k+1)-mer pairs, the rest single k-mers */
+    uint32_t npair;        /* pairs mode: the slices hold (k+1)-mer pairs (npair = nslices) and single
+                              k-mers x as the pair code x << 2 with PART_SINGLE set */
     uint32_t *pairs;       /* pairs mode: 4^(k+1) pair bins (k_bucket_count -> k_pair_fold) */
     uint32_t *singles;     /* pairs mode: 4^k single k-mer bins */
     uint32_t nomix;        /* no_mixed: tiles the fast path cannot take go to tile_general */
@@ -1785,7 +1790,8 @@ struct PartGeo {
  * a window).  PAIRS (as half_windows<H_PAIRS> does in LDS): the (k+1)-mers
  * ending at the odd slots 1, 3, .., 15 of each half, each standing for the
  * two k-mers ending at slots (2j, 2j+1); without a real slot 0 the first one
- * is the single k-mer at slot 1, in slices npair and up. */
+ * is the single k-mer x at slot 1, filed under the pair code x << 2 (its
+ * slice) with PART_SINGLE set in the stored low bits. */
 template <bool PAIRS, bool MIX, typename F>
 __device__ __forceinline__ void part_entries(const Emit &em, uint32_t mk, uint32_t m1, uint32_t sh, uint32_t lowm,
                                              uint32_t npair, F &&f) {
@@ -1805,8 +1811,8 @@ __device__ __forceinline__ void part_entries(const Emit &em, uint32_t mk, uint32
                         f(v >> sh, v & lowm);
                     } else if (two) {
                         const uint32_t s = 2u * (uint32_t)j + (two == 1u ? 1u : 0u);
-                        const uint32_t v = (s < 15u ? __builtin_amdgcn_alignbit(C, S2, 2u * (15u - s)) : S2) & mk;
-                        f(npair + (v >> sh), v & lowm);
+                        const uint32_t v = ((s < 15u ? __builtin_amdgcn_alignbit(C, S2, 2u * (15u - s)) : S2) & mk) << 2;
+                        f(v >> sh, (v & lowm) | PART_SINGLE);
                     }
                 }
             } else {
@@ -1827,8 +1833,8 @@ __device__ __forceinline__ void part_entries(const Emit &em, uint32_t mk, uint32
         const bool skip0 = h ? em.h1 : em.h0;
         if (PAIRS) {
             const uint32_t v0 = __builtin_amdgcn_alignbit(C, S2, 28u);
-            const uint32_t c0 = skip0 ? (v0 & mk) : (v0 & m1);
-            f(skip0 ? npair + (c0 >> sh) : (c0 >> sh), c0 & lowm);
+            const uint32_t c0 = skip0 ? (v0 & mk) << 2 : (v0 & m1);
+            f(c0 >> sh, (c0 & lowm) | (skip0 ? PART_SINGLE : 0u));
 #pragma unroll
             for (int j = 1; j < 8; j++) {
                 const uint32_t v = (j < 7 ? __builtin_amdgcn_alignbit(C, S2, 28u - 4u * (uint32_t)j) : S2) & m1;
@@ -1846,7 +1852,17 @@ __device__ __forceinline__ void part_entries(const Emit &em, uint32_t mk, uint32
 
 /* The block-wide batch of one round: windows of the waves whose tile was
  * fast (have), counting-sorted by slice.  Every thread of the block calls
- * this the same number of times (it contains barriers). */
+ * this the same number of times (it contains barriers).
+ *
+ * Round 3 measured (tools/exp_part_probe.py: s_memtime per phase, k=11,
+ * 10 GB FASTA, cycles per wave and batch of 16 waves x 4 tiles): tiles 11.4 K,
+ * histogram atomics 2.7 K + barrier 5.7 K, wave 0's scan 5.2 K (the others
+ * wait 3.2 K), placement 14.3 K + barrier 3.0 K, write-out 2.4 K: the LDS
+ * atomics bind.  Spreading each slice's counters over 8 lane buckets (2-way
+ * instead of ~3.5-way bank conflicts) with a scan split over all waves did
+ * not make the atomic phases cheaper (the atomic instructions' issue, not
+ * the banks, sets their cost) and its extra barrier made the batch slower
+ * (47.0 K vs 45.7 K cycles), so the scan stays on wave 0. */
 template <bool PAIRS, bool MIX, uint32_t W>
 __device__ __forceinline__ bool part_batch(const Ctx &cx, const PartGeo &pg, const Emit *es, const bool *haves,
                                            bool more, uint32_t row, uint32_t *hist,
@@ -1920,7 +1936,7 @@ __global__ void __launch_bounds__(PART_BLOCK_W(W), 4) /* 4 waves per SIMD (<= 12
 k_part(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint32_t *table,
        uint32_t *shortcnt, unsigned long long *acc, DevRes *res, RangeRec *rr, uint64_t nchunks, uint64_t cpw,
        const XState *d_init, int has_init, PartGeo pg, ResumeRec *resume, const XState *exact) {
-    __shared__ uint32_t hist[PART_MAX_SLICES], cur[PART_MAX_SLICES], total;
+    __shared__ uint32_t hist[PART_SM(W)], cur[PART_SM(W)], total;
     __shared__ __attribute__((aligned(16))) uint16_t ent[PART_MAX_BATCH_W(W)];
     if (RES && *(volatile uint32_t *)pg.flag == 0) return;   /* uniform: no range stopped */
     /* open the feed's result block (the kernels after this one accumulate
@@ -2128,8 +2144,11 @@ __global__ void __launch_bounds__(1024)
 k_bucket_count(PartGeo pg, uint32_t groups, uint32_t *table) {
     extern __shared__ uint32_t slice[];
     const uint32_t nb = 1u << pg.sh;
+    /* pairs mode: the slice's 2^sh pair bins, then the 2^(sh-2) bins of the
+       single k-mers filed under it (PART_SINGLE codes) */
+    const uint32_t ns = pg.pairs ? nb >> 2 : 0u;
     const uint32_t b = blockIdx.x % pg.nslices, g = blockIdx.x / pg.nslices;
-    for (uint32_t i = threadIdx.x; i < nb; i += blockDim.x) slice[i] = 0;
+    for (uint32_t i = threadIdx.x; i < nb + ns; i += blockDim.x) slice[i] = 0;
     __syncthreads();
     const uint32_t *ix = pg.idx + (size_t)b * pg.stride;
     /* region 2 (k_part<RES>) holds rows only if some range went there */
@@ -2148,7 +2167,9 @@ k_bucket_count(PartGeo pg, uint32_t groups, uint32_t *table) {
 #pragma unroll
         for (int h = 0; h < 8; h++) {
             const uint64_t at = q * 8 + h;
-            if (at >= s0 && at < s1) atomicAdd(&slice[(w4[h >> 1] >> (16 * (h & 1))) & 0xFFFFu], 1u);
+            const uint32_t c = (w4[h >> 1] >> (16 * (h & 1))) & 0xFFFFu;
+            const uint32_t a = c & PART_SINGLE ? nb + ((c & ~PART_SINGLE) >> 2) : c;
+            if (at >= s0 && at < s1) atomicAdd(&slice[a], 1u);
         }
     };
     uint32_t en[BUCKET_ROWS];   /* the next iteration's index words, loaded with this one's codes */
@@ -2192,12 +2213,13 @@ k_bucket_count(PartGeo pg, uint32_t groups, uint32_t *table) {
     __syncthreads();
     if (pg.pairs) {
         /* pairs mode: the slice's bins, in kernel index order, into the pair
-           or single bins (k_pair_fold reduces them into the table) */
-        uint32_t *dst = b < pg.npair ? pg.pairs + ((size_t)b << pg.sh) : pg.singles + ((size_t)(b - pg.npair) << pg.sh);
-        for (uint32_t i = threadIdx.x; i < nb; i += blockDim.x) {
+           and single bins (k_pair_fold reduces them into the table) */
+        uint32_t *dp = pg.pairs + ((size_t)b << pg.sh), *ds = pg.singles + ((size_t)b << (pg.sh - 2));
+        for (uint32_t i = threadIdx.x; i < nb + ns; i += blockDim.x) {
             const uint32_t v = slice[i];
-            if (groups == 1) dst[i] = v;   /* this block owns the slice: every bin written */
-            else if (v) atomicAdd(&dst[i], v);
+            uint32_t *dst = i < nb ? dp + i : ds + (i - nb);
+            if (groups == 1) *dst = v;   /* this block owns the slice: every bin written */
+            else if (v) atomicAdd(dst, v);
         }
         return;
     }
@@ -3270,8 +3292,8 @@ extern "C" int fk_engine_create(int k, const fk_opts *opts, fk_engine **out) {
         hipFuncSetAttribute((const void *)k_redo<H_PAIRS>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh);
         hipFuncSetAttribute((const void *)k_resume<H_PAIRS>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh);
     }
-    if (e->part)   /* k_bucket_count: one 2^15-bin slice (128 KiB) in LDS */
-        hipFuncSetAttribute((const void *)k_bucket_count, hipFuncAttributeMaxDynamicSharedMemorySize, 4 << 15);
+    if (e->part)   /* k_bucket_count: one 2^15-bin slice + its 2^13 single bins (160 KiB) in LDS */
+        hipFuncSetAttribute((const void *)k_bucket_count, hipFuncAttributeMaxDynamicSharedMemorySize, 5 << 15);
     for (int i = 0; i < 3; i++)
         /* timing only (results travel through mapped memory): no system-scope
            fence, which costs a cache writeback + invalidate and a gap of
@@ -3339,10 +3361,18 @@ struct Geo {
     unsigned grid;        /* k_count's blocks */
     unsigned rgrid;       /* blocks of the one-wave-per-range kernels (k_resume, k_redo) */
 };
+/* k_part's waves per block (8 <= k <= 12): 16 for the 512-slice tables (one
+   block per CU), else 8 (two per CU); FINDKMER_TUNE part_waves forces one */
+static uint32_t part_waves_of(const fk_engine *e) {
+    return e->part_waves ? e->part_waves : (e->k >= 11 ? 16u : 8u);
+}
+
 static Geo geometry(const fk_engine *e, uint64_t len) {
     Geo g;
     g.nchunks = (len + FK_CHUNK_BYTES - 1) / FK_CHUNK_BYTES;
     uint64_t max_waves = (uint64_t)e->cus * blocks_per_cu(e) * FK_WAVES_PER_BLOCK;
+    /* k_part: one range per wave of its blocks, the blocks one round over the CUs */
+    if (e->part) max_waves = (uint64_t)e->cus * part_waves_of(e) * (part_waves_of(e) >= 16u ? 1u : 2u);
     /* k <= 7 (k_count counts in LDS): ranges_per_wave ranges per wave slot
        of the chip, i.e. that many rounds of blocks (experiment knob, default
        1).  Equal static ranges finish up to 35 % apart (tools/wave_times.py:
@@ -3538,7 +3568,7 @@ static int launch_part(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t l
     const int kb = pairs ? k + 1 : k;                      /* bits of a pair (or window) code: 2 kb */
     pg.sh = std::min(15, 2 * kb - 6);                      /* >= 64 slices, <= 2^15 bins (128 KiB) each */
     pg.npair = pairs ? 1u << (2 * kb - pg.sh) : 0u;
-    pg.nslices = pairs ? pg.npair + (1u << (2 * k - pg.sh)) : 1u << (2 * k - pg.sh);
+    pg.nslices = pairs ? pg.npair : 1u << (2 * k - pg.sh);   /* singles fold into the pair slices */
     pg.pairs = pg.singles = nullptr;
     pg.nomix = e->no_mixed ? 1u : 0u;
     if (pairs) {
@@ -3554,8 +3584,8 @@ static int launch_part(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t l
     }
     pg.rounds = (uint32_t)((g.cpw * FK_CHUNK_TILES + 2) / PART_TILES(pairs) + 2);   /* rows (batches) per block */
     /* block size: 16 waves (larger batches, longer runs for k_bucket_count)
-       for the many-slice tables, else 8 (FINDKMER_TUNE part_waves=8|16 forces one) */
-    const uint32_t W = e->part_waves ? e->part_waves : (k >= 11 ? 16u : 8u);
+       for the 512-slice tables, else 8 (FINDKMER_TUNE part_waves=8|16 forces one) */
+    const uint32_t W = part_waves_of(e);
     pg.batch = PART_MAX_BATCH_W(W);
     const unsigned pgrid = (unsigned)((g.nranges + W - 1) / W);   /* the same ranges as k_count's waves */
     pg.rows = pgrid * pg.rounds;
@@ -3603,8 +3633,9 @@ static int launch_part(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t l
     }
     const uint32_t groups = std::max<uint32_t>(1, (uint32_t)e->cus / pg.nslices);
     if (pairs && groups > 1) HIPCHK(hipMemsetAsync(e->d_pairs, 0, e->nbins * 5 * sizeof(uint32_t), e->stream));
-    hipLaunchKernelGGL(k_bucket_count, dim3(pg.nslices * groups), dim3(1024), (size_t)sizeof(uint32_t) << pg.sh,
-                       e->stream, pg, groups, e->d_table);
+    const size_t bc_lds = ((size_t)1 << pg.sh) * sizeof(uint32_t) * (pairs ? 5 : 4) / 4;   /* + single bins */
+    hipLaunchKernelGGL(k_bucket_count, dim3(pg.nslices * groups), dim3(1024), bc_lds, e->stream, pg, groups,
+                       e->d_table);
     HIPCHK(hipGetLastError());
     if (pairs) {
         const unsigned fg = (unsigned)std::min<uint64_t>((uint64_t)e->cus * 4, (e->nbins + 255) / 256);
