@@ -161,18 +161,22 @@ struct Counters {       /* per lane; flushed per range */
 enum HistMode {
     H_PAIRS = 0,    /* k <= 6: LDS bins of (k+1)-mers at every other base + LDS k-mer singles */
     H_LDS = 1,      /* k == 7: LDS k-mer bins */
-    H_GLOBAL = 2,   /* k >= 13, and cancellations: global u32 atomics */
-    H_NONE = 3,     /* 8 <= k <= 12, state pass: count nothing, only the scan state */
-    H_EMIT = 4,     /* 8 <= k <= 12, k_part: fast tiles hand their windows to the
+    H_GLOBAL = 2,   /* k >= 14, and cancellations: global u32 atomics */
+    H_NONE = 3,     /* 8 <= k <= 13, state pass: count nothing, only the scan state */
+    H_EMIT = 4,     /* 8 <= k <= 13, k_part: fast tiles hand their windows to the
                        partition, general tiles use global atomics */
     H_SPARSE = 5    /* 17 <= k <= 20: general tiles from exact states write every
                        window's index (and every short walk) at its byte's slot */
 };
 
-/* sparse slots (H_SPARSE, one u64 per input byte): a window's reference-order
-   index (< 2^40), a short walk (tag | depth << 40 | its code), or empty */
+/* sparse slots (H_SPARSE, k_sp_emit: one u64 per byte of the tile, in LDS):
+   a window's reference-order index (< 2^40), a short walk (tag | depth << 40
+   | its code), or empty.  Byte p of the tile (lane p / 32, byte p % 32) sits
+   at column-major slot (p % 32) * 64 + p / 32: the 64 lanes writing their
+   j-th bytes hit 64 consecutive slots (no bank conflicts). */
 #define SP_SHORT (1ull << 62)
 #define SP_EMPTY (~0ull)
+__device__ __forceinline__ uint32_t sp_slot(uint32_t pos) { return ((pos & 31u) << 6) | (pos >> 5); }
 
 /* a fast tile's windows for the partition (k_part): per half, the context
    word, the 16-slot word and whether slot 0 is not a window */
@@ -199,7 +203,7 @@ struct Ctx {            /* kernel-wide constants */
     uint32_t single_off;/* H_PAIRS: offset of the k-mer singles in LDS (4^(k+1)) */
     int k;
     uint32_t *flush;    /* where lds_flush adds the bins (nullptr: table) */
-    uint64_t *slots;    /* H_SPARSE: the current range's slots (range-relative byte offset) */
+    uint64_t *slots;    /* H_SPARSE: the tile's slots in LDS (k_sp_emit), or nullptr (counting only) */
 };
 
 /* LDS atomic add at a byte offset into the bins.  The kernels that count
@@ -406,8 +410,8 @@ __device__ __forceinline__ void tile_general(const Ctx &cx, const uint32_t w[8],
             if (s < 0) {                      /* run break: '>', N, other */
                 int seq = (int)R;
                 if (HM == H_SPARSE) {
-                    if (seq >= 1 && seq < k)
-                        cx.slots[tile_off + pos] =
+                    if (cx.slots && seq >= 1 && seq < k)
+                        cx.slots[sp_slot(pos)] =
                             SP_SHORT | ((uint64_t)seq << 40) | fk_sigma(lc & ((1ull << (2 * seq)) - 1));
                 } else if (HM != H_NONE && seq >= 1 && seq < k) {
                     short_run(cx, seq, lc, weight);
@@ -430,7 +434,7 @@ __device__ __forceinline__ void tile_general(const Ctx &cx, const uint32_t w[8],
             int seq = (int)R;
             if (seq >= k) {
                 uint64_t idx = lc & cx.maskk;
-                if (HM == H_SPARSE) cx.slots[tile_off + pos] = fk_sigma(idx);
+                if (HM == H_SPARSE) { if (cx.slots) cx.slots[sp_slot(pos)] = fk_sigma(idx); }
                 else hist_add<HM>(cx, idx, weight);
                 cnt.win += 1;
                 if (seq == k) {               /* first window: its first k-1 bases */
@@ -1672,7 +1676,7 @@ template <int HM>
 __global__ void __launch_bounds__(FK_BLOCK, 4)
 k_redo(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint32_t *table,
        uint32_t *shortcnt, unsigned long long *acc, DevRes *res, RangeRec *rr,
-       const XState *rtrue, const uint32_t *list, uint64_t nranges, int mode, uint64_t *slots, int mixed) {
+       const XState *rtrue, const uint32_t *list, uint64_t nranges, int mode, int mixed) {
     extern __shared__ uint32_t lds_bins[];
     const uint64_t n = mode != 0 ? nranges : (uint64_t)res->redo_n;
     if ((uint64_t)blockIdx.x * FK_WAVES_PER_BLOCK >= n) return;   /* uniform per block */
@@ -1687,7 +1691,6 @@ k_redo(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint
         RangeRec q = rr[r];
         const Span sp = range_span(q, len);
         const XState t = rtrue[r];
-        if (HM == H_SPARSE) cx.slots = slots + sp.rbase;
         DState ts{t.code, (uint32_t)t.R, t.hdr};
         /* passes over the range (one inlined count_range: its register
            footprint decides this kernel's occupancy):
@@ -1697,7 +1700,8 @@ k_redo(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint
                    no run break: a run longer than 2^31 bases, :977), where
                    the exact state counts nothing: one read instead of two;
            mode 1: -1 from the exact state;
-           mode 2: +1 from the exact state (H_SPARSE: the slots). */
+           mode 2: +1 from the exact state (H_SPARSE: counters and
+                   observations only; k_sp_emit emits the windows at finish). */
         const bool neg_zone = mode == 0 && !t.hdr && !q.tf.f0_const && (int32_t)(uint32_t)t.R < 0 &&
                               (uint64_t)(uint32_t)t.R + (sp.rend - sp.rbase) <= 0xFFFFFFFFull;
         const int npass = mode == 0 && !neg_zone ? 2 : 1;
@@ -1719,6 +1723,118 @@ k_redo(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint
         }
     }
     if (LDS_MODE(HM)) lds_flush<HM>(cx);
+}
+
+/*
+ * 17 <= k <= 20: the table is built at finish by key-range passes over the
+ * input the engine retained (1 byte per input byte, plus every range's exact
+ * entering state from the feed's k_scan), never by materialising a slot per
+ * byte.  k_sp_emit walks every range from its exact state, one 2 KiB tile at
+ * a time, with tile_general -- the same per-byte rules as every other count
+ * (findKmer.cpp:962-1069) -- writing each byte's window index (reference
+ * order, :719-724) or short walk (:1059-1062) into the wave's LDS slots, and
+ * then, per mode:
+ *   SP_HIST  every window's bucket (key >> shift) into an LDS histogram
+ *            (flushed with one atomic per bucket and block), every short
+ *            walk to a global list;
+ *   SP_KEYS  the windows with lo <= key < hi to a compact global list (one
+ *            atomic per tile and wave for the space, ballot-ordered writes);
+ *   SP_DENSE the windows with lo <= key < hi counted in a dense u64 table
+ *            (one bucket too large for a sorted pass: few distinct keys).
+ */
+struct SpEmit {
+    int mode;
+    uint32_t shift;                 /* bucket of a key: key >> shift */
+    uint64_t lo, hi;                /* SP_KEYS, SP_DENSE: the key range [lo, hi) */
+    unsigned long long *bhist;      /* SP_HIST: window count per bucket */
+    uint32_t nbuckets;
+    uint64_t *shorts;               /* SP_HIST: the short walks */
+    unsigned long long *nshort;
+    uint64_t short_cap;
+    uint64_t *out;                  /* SP_KEYS */
+    unsigned long long *nout;
+    uint64_t out_cap;
+    unsigned long long *dense;      /* SP_DENSE: count of key lo + i */
+};
+enum { SP_HIST = 1, SP_KEYS = 2, SP_DENSE = 3 };
+#define SP_WAVES 4u
+#define SP_BUCKET_BITS 12u
+
+__global__ void __launch_bounds__(SP_WAVES * 64u)
+k_sp_emit(const uint8_t *buf, uint64_t len, int k, uint64_t maskk, const XState *rst, uint64_t nranges,
+          uint64_t cpw, uint64_t nchunks, SpEmit em) {
+    extern __shared__ uint64_t sp_lds[];   /* SP_WAVES x 2048 slots, then (SP_HIST) the buckets */
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    uint64_t *slots = sp_lds + (size_t)wv * FK_TILE_BYTES;
+    uint32_t *bh = reinterpret_cast<uint32_t *>(sp_lds + (size_t)SP_WAVES * FK_TILE_BYTES);
+    if (em.mode == SP_HIST) {
+        for (uint32_t i = threadIdx.x; i < em.nbuckets; i += blockDim.x) bh[i] = 0;
+        __syncthreads();
+    }
+    Ctx cx{buf, len, 0, nullptr, nullptr, nullptr, nullptr, nullptr, maskk, 0, k, nullptr, slots};
+    const uint64_t nw = (uint64_t)gridDim.x * SP_WAVES;
+    for (uint64_t r = (uint64_t)blockIdx.x * SP_WAVES + wv; r < nranges; r += nw) {
+        const uint64_t c0 = r * cpw, c1 = min(c0 + cpw, nchunks);
+        const uint64_t rb = c0 * FK_CHUNK_BYTES, re = min(c1 * FK_CHUNK_BYTES, len);
+        const XState x = rst[r];
+        DState st{x.code, (uint32_t)x.R, x.hdr};
+        for (uint64_t tb = rb; tb < re; tb += FK_TILE_BYTES) {
+            /* a lane reads back only the slots of its own 32 bytes */
+#pragma unroll 8
+            for (uint32_t j = 0; j < FK_LANE_BYTES; j++) slots[j * 64u + lane] = SP_EMPTY;
+            uint32_t w[8];
+            const int nb = load_lane<FK_LANE_BYTES>(cx, (int64_t)(tb + (uint64_t)lane * FK_LANE_BYTES), w);
+            Facts f{0, 0, 0, 0, 0, 0};
+            Counters cnt{0, 0, 0, 0, 0, FK_NO_EOF, 0};
+            tile_general<true, H_SPARSE>(cx, w, nb, 0u, st, f, cnt, 1u);
+            if (em.mode == SP_KEYS) {
+                uint32_t mine = 0;
+#pragma unroll 8
+                for (uint32_t j = 0; j < FK_LANE_BYTES; j++) {
+                    const uint64_t v = slots[j * 64u + lane];
+                    mine += v >= em.lo && v < em.hi ? 1u : 0u;
+                }
+                const uint32_t tot = wsum32(mine);
+                if (tot) {
+                    unsigned long long base = 0;
+                    if (lane == 0) base = atomicAdd(em.nout, (unsigned long long)tot);
+                    base = rdlane64(base, 0);
+                    uint64_t run = 0;
+                    for (uint32_t j = 0; j < FK_LANE_BYTES; j++) {
+                        const uint64_t v = slots[j * 64u + lane];
+                        const bool m = v >= em.lo && v < em.hi;
+                        const uint64_t bal = __ballot(m);
+                        if (m) {
+                            const uint64_t at = base + run + (uint64_t)__popcll(bal & ((1ull << lane) - 1ull));
+                            if (at < em.out_cap) em.out[at] = v;
+                        }
+                        run += (uint64_t)__popcll(bal);
+                    }
+                }
+            } else if (em.mode == SP_DENSE) {
+#pragma unroll 8
+                for (uint32_t j = 0; j < FK_LANE_BYTES; j++) {
+                    const uint64_t v = slots[j * 64u + lane];
+                    if (v >= em.lo && v < em.hi) atomicAdd(&em.dense[v - em.lo], 1ull);
+                }
+            } else {
+                for (uint32_t j = 0; j < FK_LANE_BYTES; j++) {
+                    const uint64_t v = slots[j * 64u + lane];
+                    if (v < SP_SHORT) {
+                        atomicAdd(&bh[v >> em.shift], 1u);
+                    } else if (v != SP_EMPTY) {
+                        const unsigned long long i = atomicAdd(em.nshort, 1ull);
+                        if (i < em.short_cap) em.shorts[i] = v;
+                    }
+                }
+            }
+        }
+    }
+    if (em.mode == SP_HIST) {
+        __syncthreads();
+        for (uint32_t i = threadIdx.x; i < em.nbuckets; i += blockDim.x)
+            if (bh[i]) atomicAdd(&em.bhist[i], (unsigned long long)bh[i]);
+    }
 }
 
 /*
@@ -1753,8 +1869,8 @@ k_redo(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint
 #define PART_MAX_BATCH_W(W) (2u * (W) * FK_TILE_BYTES)   /* entries per batch */
 static_assert(PART_MAX_BATCH_W(16u) <= 65536u, "run index words hold 16-bit starts and counts - 1");
 /* slices of a batch: k = 11 pairs 2^24 / 2^15 (the single k-mers fold into
-   them, flagged), k = 12 2^24 / 2^15; k <= 10 at most 128 */
-#define PART_SM(W) ((W) >= 16u ? 512u : 128u)
+   them, flagged), k = 12 2^24 / 2^15, k = 13 2^26 / 2^15; k <= 10 at most 128 */
+#define PART_SM(W) ((W) >= 16u ? 2048u : 128u)   /* k = 13: 2^26 / 2^15 slices */
 #define PART_SINGLE 0x8000u   /* a stored code with this bit: a single k-mer (pairs mode) */
 
 /* A run index word: (start << 16) | (count - 1) for a run of count >= 1
@@ -1866,7 +1982,7 @@ __device__ __forceinline__ void part_entries(const Emit &em, uint32_t mk, uint32
 template <bool PAIRS, bool MIX, uint32_t W>
 __device__ __forceinline__ bool part_batch(const Ctx &cx, const PartGeo &pg, const Emit *es, const bool *haves,
                                            bool more, uint32_t row, uint32_t *hist,
-                                           uint32_t *cur, uint32_t *total, uint16_t *ent) {
+                                           uint32_t *cur, uint32_t *total, uint16_t *ent, uint32_t *scr) {
     constexpr int NT = PART_TILES(PAIRS);
     const uint32_t t = threadIdx.x, lane = t & 63;
     const uint32_t mk = (uint32_t)cx.maskk, sh = pg.sh, lowm = (1u << sh) - 1u;
@@ -1877,8 +1993,30 @@ __device__ __forceinline__ bool part_batch(const Ctx &cx, const PartGeo &pg, con
         if (haves[i]) part_entries<PAIRS, MIX>(es[i], mk, m1, sh, lowm, pg.npair, [&](uint32_t b, uint32_t) { atomicAdd(&hist[b], 1u); });
     /* (the barrier also tells whether any wave has tiles left) */
     const bool any_more = __syncthreads_or(more);
-    /* 2: exclusive scan of the slice counts (wave 0), index row */
-    if (t < 64) {
+    /* 2: exclusive scan of the slice counts, index row: wave 0 alone for up
+       to 512 slices; k = 13's 2048 slices split over all waves (each sums
+       its contiguous share, one more barrier, then scans it from the sum of
+       the shares before it) */
+    if (!PAIRS && W >= 16u && pg.nslices > 512u) {
+        const uint32_t per_w = pg.nslices / W, ppl = per_w / 64u;   /* multiples of 64 */
+        const uint32_t wv = t >> 6, b0 = wv * per_w + lane * ppl;
+        uint32_t mine = 0;
+        for (uint32_t j = 0; j < ppl; j++) mine += hist[b0 + j];
+        const uint32_t wt = wsum32(mine);
+        if (lane == 0) scr[wv] = wt;
+        __syncthreads();
+        const uint32_t off = wsum32(lane < wv ? scr[lane] : 0u);
+        const uint32_t inc = wscan_incl32(mine);
+        uint32_t run = off + inc - mine;
+        for (uint32_t j = 0; j < ppl; j++) {
+            const uint32_t b = b0 + j, c = hist[b];
+            cur[b] = run;
+            pg.idx[(size_t)b * pg.stride + row] = run_word(run, c);
+            hist[b] = 0;
+            run += c;
+        }
+        if (wv == W - 1u && lane == 63) *total = run;
+    } else if (t < 64) {
         const uint32_t per = (pg.nslices + 63) / 64;
         uint32_t sum = 0;
         for (uint32_t j = 0; j < per; j++) {
@@ -1936,7 +2074,7 @@ __global__ void __launch_bounds__(PART_BLOCK_W(W), 4) /* 4 waves per SIMD (<= 12
 k_part(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint32_t *table,
        uint32_t *shortcnt, unsigned long long *acc, DevRes *res, RangeRec *rr, uint64_t nchunks, uint64_t cpw,
        const XState *d_init, int has_init, PartGeo pg, ResumeRec *resume, const XState *exact) {
-    __shared__ uint32_t hist[PART_SM(W)], cur[PART_SM(W)], total;
+    __shared__ uint32_t hist[PART_SM(W)], cur[PART_SM(W)], total, scr[W];
     __shared__ __attribute__((aligned(16))) uint16_t ent[PART_MAX_BATCH_W(W)];
     if (RES && *(volatile uint32_t *)pg.flag == 0) return;   /* uniform: no range stopped */
     /* open the feed's result block (the kernels after this one accumulate
@@ -2064,7 +2202,7 @@ k_part(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint
             }                                                                        \
             if (ph_ == NT - 1) {                                                     \
                 const bool more_ = part_batch<PAIRS, RES, W>(cx, pg, stash, have_stash, !done, \
-                                                          row0 + round / NT, hist, cur, &total, ent); \
+                                                          row0 + round / NT, hist, cur, &total, ent, scr); \
                 if (!more_ || round / NT + 1 >= pg.rounds) { round++; break; }       \
             }                                                                        \
         }                                                                            \
@@ -2925,11 +3063,18 @@ __global__ void k_synth(uint8_t *out, uint64_t total, uint64_t seed, int fasta_l
    the work queued on it). */
 struct DevScratch {
     void *p = nullptr;
+    size_t bytes = 0;
     DevScratch() = default;
     DevScratch(const DevScratch &) = delete;
     DevScratch &operator=(const DevScratch &) = delete;
-    ~DevScratch() { if (p) hipFree(p); }
-    bool alloc(size_t n) { return hipMalloc(&p, n) == hipSuccess; }
+    ~DevScratch() { release(); }
+    bool alloc(size_t n) {
+        release();
+        if (hipMalloc(&p, n) != hipSuccess) { p = nullptr; return false; }
+        bytes = n;
+        return true;
+    }
+    void release() { if (p) hipFree(p); p = nullptr; bytes = 0; }
     template <class T> T *as() const { return (T *)p; }
 };
 
@@ -2945,12 +3090,18 @@ struct fk_engine {
     uint64_t nbins = 0, nshort = 0, maskk = 0;
     int cus = 256;
     uint32_t ts_blocks = 0;                   /* k_table_stats grid override (0 = default) */
-    bool part = false;                        /* 8 <= k <= 12: partitioned counting (k_part) */
-    bool sparse = false;                      /* 17 <= k <= 20: slots, sorted at finish (fk_sparse.hip) */
-    uint64_t *d_slots = nullptr;              /* sparse: one u64 per byte fed (+1: the final short walk) */
-    uint64_t slots_cap = 0, slots_len = 0;
+    bool part = false;                        /* 8 <= k <= 13: partitioned counting (k_part) */
+    bool sparse = false;                      /* 17 <= k <= 20: key-range passes at finish (k_sp_emit) */
+    uint8_t *d_keep = nullptr;                /* sparse: the input fed so far */
+    XState *d_kst = nullptr;                  /* sparse: every retained range's exact entering state */
+    uint64_t keep_len = 0, keep_cap = 0, kst_len = 0, kst_cap = 0;
+    struct SpSeg { uint64_t off, len, st, nranges, cpw, nchunks; };
+    std::vector<SpSeg> spsegs;                /* the retained segments */
+    std::vector<FksPart> spparts;              /* the finished table, one part per pass, ascending */
+    uint64_t sp_distinct = 0;
+    uint64_t sp_pass = 0;                     /* FINDKMER_TUNE sp_pass: window keys per pass (0: by free HBM) */
     FksState fks;
-    bool sp_done = false;                     /* fks holds the finished table */
+    bool sp_done = false;                     /* spparts holds the finished table */
     unsigned long long sp_nodes = 0, sp_roll = 0, sp_tstat[10] = {};
     uint16_t *d_codes = nullptr;              /* k_part: block code regions */
     uint32_t *d_pflag = nullptr;              /* k_part: a range went to k_part<RES> */
@@ -3129,6 +3280,12 @@ static size_t lds_bytes(const fk_engine *e) {
 }
 
 /* Zero table, counters and the stream state (asynchronous, stream-ordered). */
+static void sp_parts_free(fk_engine *e) {
+    for (auto &p : e->spparts) { hipFree(p.keys); hipFree(p.cnts); }
+    e->spparts.clear();
+    e->sp_distinct = 0;
+}
+
 static int zero_all(fk_engine *e) {
     e->zero_pending = true;
     e->dirty = false;
@@ -3142,7 +3299,9 @@ static int zero_all(fk_engine *e) {
     e->shard_pending = 0;
     e->dev_ms = e->main_ms = 0;
     e->timed_n = 0;
-    e->slots_len = 0;
+    e->keep_len = e->kst_len = 0;
+    e->spsegs.clear();
+    sp_parts_free(e);
     e->sp_done = false;
     e->unknown_bytes.clear();
     return FK_OK;
@@ -3159,7 +3318,9 @@ extern "C" void fk_engine_destroy(fk_engine *e) {
     hipFree(e->d_redo); hipFree(e->d_tf); hipFree(e->d_stage); hipFree(e->d_resume);
     hipFree(e->d_aggs); hipFree(e->d_flags);
     hipFree(e->d_bsum); hipFree(e->d_ctl); hipFree(e->d_opc);
-    hipFree(e->d_slots);
+    hipFree(e->d_keep);
+    hipFree(e->d_kst);
+    sp_parts_free(e);
     fks_free(&e->fks);
     if (e->h_stage) hipHostFree(e->h_stage);
     for (int i = 0; i < 3; i++) if (e->ev[i]) hipEventDestroy(e->ev[i]);
@@ -3229,7 +3390,9 @@ extern "C" int fk_engine_create(int k, const fk_opts *opts, fk_engine **out) {
        part_general=N (general tiles k_part takes per range before
        k_part<RES>), static_pct=P / dyn_min_chunks=N (k_count's dynamic
        ranges), part_waves=8|16 (k_part block size), events=0 (no HIP events),
-       seg_kb=N (device feeds cut into N-KiB segments) */
+       seg_kb=N (device feeds cut into N-KiB segments), sp_pass=N (17 <= k:
+       at most N window keys per sorted pass; smaller buckets merge, larger
+       ones take the dense path) */
     uint64_t kv = 0;
     if (tune_knob("no_mixed", &kv)) e->no_mixed = kv == 1;
     /* k_count takes a couple of general tiles per range (the stream start, an
@@ -3240,10 +3403,11 @@ extern "C" int fk_engine_create(int k, const fk_opts *opts, fk_engine **out) {
     if (tune_knob("events", &kv)) e->timing = kv != 0;
     if (tune_knob("static_pct", &kv)) e->static_pct = (uint32_t)std::min<uint64_t>(100u, std::max<uint64_t>(1u, kv));
     if (tune_knob("dyn_min_chunks", &kv)) e->dyn_min_chunks = kv;
+    if (tune_knob("sp_pass", &kv)) e->sp_pass = kv;
     if (e->opts.timing_every > 1) e->timing_every = (uint32_t)e->opts.timing_every;
     e->sparse = k > FK_K_MAX_DENSE;
     e->nbins = e->sparse ? 0 : 1ull << (2 * k);
-    e->part = k >= 8 && k <= 12;
+    e->part = k >= 8 && k <= 13;
     e->maskk = (1ull << (2 * k)) - 1;
     e->nshort = k > 1 && !e->sparse ? ((1ull << (2 * k)) - 4) / 3 : 0;
     if (e->opts.stream) {
@@ -3364,7 +3528,7 @@ struct Geo {
 /* k_part's waves per block (8 <= k <= 12): 16 for the 512-slice tables (one
    block per CU), else 8 (two per CU); FINDKMER_TUNE part_waves forces one */
 static uint32_t part_waves_of(const fk_engine *e) {
-    return e->part_waves ? e->part_waves : (e->k >= 11 ? 16u : 8u);
+    return e->k >= 13 ? 16u : e->part_waves ? e->part_waves : (e->k >= 11 ? 16u : 8u);
 }
 
 static Geo geometry(const fk_engine *e, uint64_t len) {
@@ -3484,13 +3648,12 @@ static int launch_resume(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t
     return FK_OK;
 }
 
-static int launch_redo(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t lo, const Geo &g, int mode,
-                       uint64_t *slots = nullptr) {
+static int launch_redo(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t lo, const Geo &g, int mode) {
     size_t sh = lds_bytes(e);
     FK_DISPATCH(hist_mode(e),
                 hipLaunchKernelGGL((k_redo<HM>), dim3(g.rgrid), dim3(FK_BLOCK), sh, e->stream, buf, len, lo, e->k,
                                    e->maskk, e->d_table, e->d_short, e->d_facc, e->d_res, e->d_rr,
-                                   e->d_rtrue, e->d_redo, g.nranges, mode, slots, e->no_mixed ? 0 : 1));
+                                   e->d_rtrue, e->d_redo, g.nranges, mode, e->no_mixed ? 0 : 1));
     HIPCHK(hipGetLastError());
     return FK_OK;
 }
@@ -3907,40 +4070,52 @@ static int finish_segment(fk_engine *e, const uint8_t *dbuf, uint64_t len, int64
     return collect_unknown(e, dbuf, len, lo, g);
 }
 
-/* sparse slots for `need` bytes (grown geometrically, contents kept) */
-static int ensure_slots(fk_engine *e, uint64_t need) {
-    if (need <= e->slots_cap && e->d_slots) return FK_OK;
-    uint64_t cap = std::max<uint64_t>(need, std::max<uint64_t>(2 * e->slots_cap, 1u << 20));
-    uint64_t *p = nullptr;
-    if (hipMalloc((void **)&p, cap * sizeof(uint64_t)) != hipSuccess) return FK_E_OOM;
-    if (e->slots_len)
-        HIPCHK(hipMemcpyAsync(p, e->d_slots, e->slots_len * sizeof(uint64_t), hipMemcpyDeviceToDevice, e->stream));
+/* grow a retained device buffer to `need` bytes (geometrically, contents kept) */
+static int sp_grow(fk_engine *e, void **buf, uint64_t *cap, uint64_t used, uint64_t need) {
+    if (need <= *cap && *buf) return FK_OK;
+    const uint64_t c = std::max<uint64_t>(need, std::max<uint64_t>(*cap + *cap / 2, 1u << 20));
+    void *p = nullptr;
+    if (hipMalloc(&p, c) != hipSuccess) return FK_E_OOM;
+    if (used) HIPCHK(hipMemcpyAsync(p, *buf, used, hipMemcpyDeviceToDevice, e->stream));
     HIPCHK(hipStreamSynchronize(e->stream));
-    hipFree(e->d_slots);
-    e->d_slots = p;
-    e->slots_cap = cap;
+    hipFree(*buf);
+    *buf = p;
+    *cap = c;
+    return FK_OK;
+}
+
+/* keep a counted segment's bytes and its ranges' exact entering states
+   (d_rtrue from the feed's k_scan) for finish's key-range passes */
+static int sp_retain(fk_engine *e, const uint8_t *dbuf, uint64_t len, const Geo &g) {
+    int rc = sp_grow(e, (void **)&e->d_keep, &e->keep_cap, e->keep_len, e->keep_len + len + FK_TILE_BYTES);
+    if (rc) return rc;
+    const uint64_t sb = g.nranges * sizeof(XState);
+    rc = sp_grow(e, (void **)&e->d_kst, &e->kst_cap, e->kst_len * sizeof(XState), (e->kst_len + g.nranges) * sizeof(XState));
+    if (rc) return rc;
+    HIPCHK(hipMemcpyAsync(e->d_keep + e->keep_len, dbuf, len, hipMemcpyDeviceToDevice, e->stream));
+    HIPCHK(hipMemcpyAsync(e->d_kst + e->kst_len, e->d_rtrue, sb, hipMemcpyDeviceToDevice, e->stream));
+    e->spsegs.push_back({e->keep_len, len, e->kst_len, g.nranges, g.cpw, g.nchunks});
+    /* segments start tile-aligned in d_keep (the emit kernel's loads) */
+    e->keep_len += (len + FK_TILE_BYTES - 1) / FK_TILE_BYTES * FK_TILE_BYTES;
+    e->kst_len += g.nranges;
     return FK_OK;
 }
 
 /*
  * A segment for 17 <= k <= 20: the state pass (k_count / k_resume in H_NONE
  * mode, k_scan) gives every range its exact entering state; k_redo mode 2
- * then writes the segment's slots (and its counters and exact observations)
- * from those states.  A 0xFF byte outside a header: cancel the counters,
- * clear the slots and count the prefix again.
+ * then takes the segment's counters and exact observations from those
+ * states, and the segment's bytes and states are retained for finish.  A
+ * 0xFF byte outside a header: cancel the counters and count the prefix again.
  */
 static int sparse_segment(fk_engine *e, const uint8_t *dbuf, uint64_t len, bool prefix = false) {
     const XState entering = e->state;
-    int rc = ensure_slots(e, e->slots_len + len + 1);   /* (+1: finish's final short walk) */
-    if (rc) return rc;
     Geo g;
-    rc = count_segment(e, dbuf, len, 0, 1, g);
+    int rc = count_segment(e, dbuf, len, 0, 1, g);
     if (rc) return rc;
-    uint64_t *sl = e->d_slots + e->slots_len;
-    HIPCHK(hipMemsetAsync(sl, 0xFF, len * sizeof(uint64_t), e->stream));
     rc = launch_scan(e, g, 0);
     if (rc) return rc;
-    rc = launch_redo(e, dbuf, len, 0, g, 2, sl);
+    rc = launch_redo(e, dbuf, len, 0, g, 2);
     if (rc) return rc;
     rc = launch_table_stats(e, false, tev(e, 2));   /* no dense table: publishes counters and state */
     if (rc) return rc;
@@ -3952,9 +4127,8 @@ static int sparse_segment(fk_engine *e, const uint8_t *dbuf, uint64_t len, bool 
         rc = exact_eof(e, g, eof);
         if (rc) return rc;
         if (eof != NO_EOF64) {
-            rc = launch_redo(e, dbuf, len, 0, g, 1, sl);
+            rc = launch_redo(e, dbuf, len, 0, g, 1);
             if (rc) return rc;
-            HIPCHK(hipMemsetAsync(sl, 0xFF, len * sizeof(uint64_t), e->stream));
             HIPCHK(write_dstate(e, entering));
             e->state = entering;
             e->ended = 1;
@@ -3969,7 +4143,8 @@ static int sparse_segment(fk_engine *e, const uint8_t *dbuf, uint64_t len, bool 
     }
     e->state = e->last.exit;
     if (!prefix) e->scanned += len;
-    e->slots_len += len;
+    rc = sp_retain(e, dbuf, len, g);
+    if (rc) return rc;
     return collect_unknown(e, dbuf, len, 0, g);
 }
 
@@ -4656,6 +4831,208 @@ extern "C" int fk_shard_rows_compose(const uint32_t *rows, int world, int rank, 
 
 /* ---- finish ---- */
 
+/* one k_sp_emit launch per retained segment */
+static int sp_emit_all(fk_engine *e, const SpEmit &em) {
+    const size_t lds = (size_t)SP_WAVES * FK_TILE_BYTES * sizeof(uint64_t) +
+                       (em.mode == SP_HIST ? (size_t)em.nbuckets * sizeof(uint32_t) : 0);
+    for (const auto &sg : e->spsegs) {
+        if (!sg.nranges) continue;
+        const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((sg.nranges + SP_WAVES - 1) / SP_WAVES,
+                                                                                 (uint64_t)e->cus * 8));
+        hipLaunchKernelGGL(k_sp_emit, dim3(grid), dim3(SP_WAVES * 64u), lds, e->stream, e->d_keep + sg.off, sg.len,
+                           e->k, e->maskk, e->d_kst + sg.st, sg.nranges, sg.cpw, sg.nchunks, em);
+        HIPCHK(hipGetLastError());
+    }
+    return FK_OK;
+}
+
+/*
+ * The sparse table (17 <= k <= 20) from the retained input, in key-range
+ * passes (k_sp_emit):
+ *   1. SP_HIST: window count per bucket (the top SP_BUCKET_BITS index bits)
+ *      and every short walk;
+ *   2. the passes: consecutive buckets merged while their windows fit one
+ *      sorted pass (capped by free HBM, or FINDKMER_TUNE sp_pass); a single
+ *      bucket above the cap is counted densely (2^(2k - SP_BUCKET_BITS) u64);
+ *   3. per pass: emit, sort + run-length encode (or select the nonzero dense
+ *      counts), statistics, prefix histogram, short-walk prefix marks, and
+ *      the runs kept as one part of the table.
+ * `seq`: the final run's length (its short walk if 1 <= seq < k).
+ */
+static int sparse_finish(fk_engine *e, int32_t seq) {
+    const int k = e->k;
+    sp_parts_free(e);
+    memset(e->sp_tstat, 0, sizeof e->sp_tstat);
+    e->sp_roll = e->sp_nodes = 0;
+    const uint32_t nbk = 1u << SP_BUCKET_BITS;
+    const uint32_t shift = 2u * (uint32_t)k - SP_BUCKET_BITS;
+    {   /* the HIST launch needs the larger LDS; set it once for every mode */
+        const size_t lds = (size_t)SP_WAVES * FK_TILE_BYTES * sizeof(uint64_t) + (size_t)nbk * sizeof(uint32_t);
+        HIPCHK(hipFuncSetAttribute((const void *)k_sp_emit, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    }
+    DevScratch acc, bh, ctr;
+    if (!acc.alloc(FKS_ACC_N * sizeof(unsigned long long)) || !bh.alloc((size_t)nbk * 8) || !ctr.alloc(16))
+        return FK_E_OOM;
+    unsigned long long *dacc = acc.as<unsigned long long>();
+    unsigned long long *nctr = ctr.as<unsigned long long>();
+    HIPCHK(hipMemsetAsync(dacc, 0, FKS_ACC_N * sizeof(unsigned long long), e->stream));
+
+    /* 1. bucket histogram and short walks (a second run if the list overflowed) */
+    const bool tail = !e->state.hdr && seq >= 1 && seq < k;
+    uint64_t scap = std::max<uint64_t>(1024, e->keep_len / 64);
+    DevScratch shorts;
+    uint64_t ns = 0;
+    for (int attempt = 0; attempt < 2; attempt++) {
+        if (!shorts.alloc((scap + 1) * 8)) return FK_E_OOM;
+        HIPCHK(hipMemsetAsync(bh.p, 0, (size_t)nbk * 8, e->stream));
+        HIPCHK(hipMemsetAsync(nctr, 0, 16, e->stream));
+        SpEmit em{};
+        em.mode = SP_HIST;
+        em.shift = shift;
+        em.bhist = bh.as<unsigned long long>();
+        em.nbuckets = nbk;
+        em.shorts = shorts.as<uint64_t>();
+        em.nshort = nctr;
+        em.short_cap = scap;
+        int rc = sp_emit_all(e, em);
+        if (rc) return rc;
+        unsigned long long got = 0;
+        HIPCHK(hipMemcpyAsync(&got, nctr, sizeof got, hipMemcpyDeviceToHost, e->stream));
+        HIPCHK(hipStreamSynchronize(e->stream));
+        ns = got;
+        if (ns <= scap) break;
+        if (attempt) return FK_E_HIP;
+        scap = ns;
+    }
+    if (tail) {   /* the input's last run, shorter than k (:1059-1062 at EOF) */
+        const uint64_t v = SP_SHORT | ((uint64_t)seq << 40) | fk_sigma(e->state.code & ((1ull << (2 * seq)) - 1));
+        HIPCHK(hipMemcpyAsync(shorts.as<uint64_t>() + ns, &v, sizeof v, hipMemcpyHostToDevice, e->stream));
+        HIPCHK(hipStreamSynchronize(e->stream));
+        ns++;
+    }
+    const bool nodes = e->opts.want_nodes != 0;
+    if (!nodes) ns = 0;
+    if (ns > 1) {   /* nodeCounter counts distinct prefixes: drop repeated walks */
+        uint64_t nu = 0;
+        if (fks_unique(&e->fks, shorts.as<uint64_t>(), ns, e->stream, &nu)) return FK_E_HIP;
+        ns = nu;
+    }
+    DevScratch found;
+    if (ns) {
+        if (!found.alloc(ns * 20)) return FK_E_OOM;
+        HIPCHK(hipMemsetAsync(found.p, 0, ns * 20, e->stream));
+    }
+    std::vector<unsigned long long> hb(nbk);
+    HIPCHK(hipMemcpyAsync(hb.data(), bh.p, (size_t)nbk * 8, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+
+    /* 2. passes: [b0, b1) buckets; dense when one bucket exceeds the cap */
+    uint64_t cap = e->sp_pass;
+    if (!cap) {
+        size_t fr = 0, tot = 0;
+        HIPCHK(hipMemGetInfo(&fr, &tot));
+        /* emit 8 + sort 8 + runs (kept) 8 + counts 8 + rocPRIM ~8 + kept counts 4 B per key, and
+           the parts of earlier passes */
+        const uint64_t margin = 1ull << 30;
+        cap = fr > margin ? (fr - margin) / 64 : 0;
+        cap = std::max<uint64_t>(1u << 20, std::min<uint64_t>(cap, 1ull << 32));
+    }
+    struct Pass { uint32_t b0, b1; uint64_t n; bool dense; };
+    std::vector<Pass> passes;
+    for (uint32_t b = 0; b < nbk;) {
+        if (!hb[b]) { b++; continue; }
+        if (hb[b] > cap) { passes.push_back({b, b + 1, hb[b], true}); b++; continue; }
+        uint32_t b1 = b;
+        uint64_t n = 0;
+        while (b1 < nbk && hb[b1] <= cap && n + hb[b1] <= cap) n += hb[b1++];
+        passes.push_back({b, b1, n, false});
+        b = b1;
+    }
+
+    /* 3. the passes */
+    DevScratch keys, dense;
+    uint64_t prev_last = 0;
+    bool have_prev = false;
+    std::vector<unsigned long long> edges(24, 0);   /* prefix histogram across pass boundaries */
+    for (const Pass &ps : passes) {
+        SpEmit em{};
+        em.shift = shift;
+        em.lo = (uint64_t)ps.b0 << shift;
+        em.hi = (uint64_t)ps.b1 << shift;
+        FksPart part{nullptr, nullptr, 0};
+        if (ps.dense) {
+            const uint64_t nd = 1ull << shift;
+            if (!dense.p && !dense.alloc(nd * 8)) return FK_E_OOM;
+            HIPCHK(hipMemsetAsync(dense.p, 0, nd * 8, e->stream));
+            em.mode = SP_DENSE;
+            em.dense = dense.as<unsigned long long>();
+            int rc = sp_emit_all(e, em);
+            if (rc) return rc;
+            if (fks_dense_runs(&e->fks, em.dense, nd, em.lo, k, e->stream, dacc, &part)) return FK_E_HIP;
+        } else {
+            if (keys.bytes < ps.n * 8) {
+                keys.release();
+                if (!keys.alloc(std::max<uint64_t>(ps.n, std::min<uint64_t>(cap, 2 * ps.n)) * 8)) return FK_E_OOM;
+            }
+            HIPCHK(hipMemsetAsync(nctr, 0, 8, e->stream));
+            em.mode = SP_KEYS;
+            em.out = keys.as<uint64_t>();
+            em.nout = nctr;
+            em.out_cap = ps.n;
+            int rc = sp_emit_all(e, em);
+            if (rc) return rc;
+            unsigned long long got = 0;
+            HIPCHK(hipMemcpyAsync(&got, nctr, sizeof got, hipMemcpyDeviceToHost, e->stream));
+            HIPCHK(hipStreamSynchronize(e->stream));
+            if (got != ps.n) return FK_E_HIP;   /* the histogram and the emit pass disagree */
+            if (fks_sort_runs(&e->fks, em.out, ps.n, k, e->stream, dacc, &part)) return FK_E_HIP;
+        }
+        if (part.keys || part.cnts) e->spparts.push_back(part);   /* owned (freed) from here on */
+        const uint64_t nw = part.n;
+        if (!nw) continue;
+        if (ns && fks_short_mark(&part, shorts.as<uint64_t>(), ns, k, found.as<uint8_t>(), e->stream))
+            return FK_E_HIP;
+        uint64_t fl[2];
+        HIPCHK(hipMemcpyAsync(&fl[0], part.keys, 8, hipMemcpyDeviceToHost, e->stream));
+        HIPCHK(hipMemcpyAsync(&fl[1], part.keys + (nw - 1), 8, hipMemcpyDeviceToHost, e->stream));
+        HIPCHK(hipStreamSynchronize(e->stream));
+        if (have_prev) {   /* the adjacent pair across the boundary: first differing base */
+            const uint64_t diff = fl[0] ^ prev_last;
+            const int lz = __builtin_clzll(diff) - (64 - 2 * k);
+            edges[lz / 2 + 1]++;
+        }
+        prev_last = fl[1];
+        have_prev = true;
+        e->sp_distinct += nw;
+    }
+    keys.release();
+    dense.release();
+
+    /* 4. totals: statistics, rollover, nodeCounter */
+    unsigned long long r[FKS_ACC_N];
+    HIPCHK(hipMemcpyAsync(r, dacc, sizeof r, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    for (int q = 0; q < 10; q++) e->sp_tstat[q] = r[q];
+    e->sp_roll = r[FKS_ACC_ROLL];
+    if (nodes) {
+        unsigned long long left = 0;
+        if (ns && fks_short_count(&e->fks, shorts.as<uint64_t>(), ns, found.as<uint8_t>(), e->stream, &left))
+            return FK_E_HIP;
+        if (e->sp_distinct || ns) {
+            unsigned long long nd = 0;
+            if (e->sp_distinct) {
+                unsigned long long run = 1;
+                for (int d = 1; d <= k; d++) {
+                    run += r[FKS_ACC_WPREFIX + d] + edges[d];
+                    nd += run;
+                }
+            }
+            e->sp_nodes = 1 + nd + left;
+        }
+    }
+    return FK_OK;
+}
+
 extern "C" int fk_engine_finish(fk_engine *e, fk_result *res) {
     if (!e || !res) return FK_E_INVALID;
     if (e->shard_pending) return FK_E_STATE;
@@ -4667,19 +5044,8 @@ extern "C" int fk_engine_finish(fk_engine *e, fk_result *res) {
     int32_t seq = (int32_t)(uint32_t)e->state.R;
     if (e->sparse) {
         if (!e->sp_done) {
-            /* sort the slots (+ the final short walk): table, statistics, nodes */
-            uint64_t n = e->slots_len;
-            if (!e->state.hdr && seq >= 1 && seq < k && e->opts.want_nodes) {
-                rc = ensure_slots(e, n + 1);
-                if (rc) return rc;
-                const uint64_t v = SP_SHORT | ((uint64_t)seq << 40) | fk_sigma(e->state.code & ((1ull << (2 * seq)) - 1));
-                HIPCHK(hipMemcpyAsync(e->d_slots + n, &v, sizeof v, hipMemcpyHostToDevice, e->stream));
-                HIPCHK(hipStreamSynchronize(e->stream));
-                n++;
-            }
-            if (fks_finalize(&e->fks, e->d_slots, n, k, e->opts.want_nodes, e->stream, e->sp_tstat, &e->sp_roll,
-                             &e->sp_nodes))
-                return FK_E_HIP;
+            rc = sparse_finish(e, seq);
+            if (rc) return rc;
             e->sp_done = true;
         }
     } else if (!e->state.hdr && seq >= 1 && seq < k && e->opts.want_nodes && !e->tail_added) {
@@ -4838,15 +5204,17 @@ extern "C" int fk_engine_table_from_device(fk_engine *e, const void *src) {
 extern "C" int fk_engine_sparse(fk_engine *e, uint64_t *keys, uint32_t *counts, uint64_t cap, uint64_t *n) {
     if (!e || !n) return FK_E_INVALID;
     if (!e->sparse || !e->sp_done) return FK_E_STATE;
-    *n = e->fks.nw;
+    *n = e->sp_distinct;
     if (!keys && !counts) return FK_OK;
-    if (cap < e->fks.nw) return FK_E_INVALID;
+    if (cap < e->sp_distinct) return FK_E_INVALID;
     int rc = set_dev(e);
     if (rc) return rc;
-    if (keys && e->fks.nw)
-        HIPCHK(hipMemcpyAsync(keys, e->fks.keys, e->fks.nw * sizeof(uint64_t), hipMemcpyDeviceToHost, e->stream));
-    if (counts && e->fks.nw)
-        HIPCHK(hipMemcpyAsync(counts, e->fks.lo, e->fks.nw * sizeof(uint32_t), hipMemcpyDeviceToHost, e->stream));
+    uint64_t at = 0;
+    for (const auto &p : e->spparts) {
+        if (keys) HIPCHK(hipMemcpyAsync(keys + at, p.keys, p.n * sizeof(uint64_t), hipMemcpyDeviceToHost, e->stream));
+        if (counts) HIPCHK(hipMemcpyAsync(counts + at, p.cnts, p.n * sizeof(uint32_t), hipMemcpyDeviceToHost, e->stream));
+        at += p.n;
+    }
     HIPCHK(hipStreamSynchronize(e->stream));
     return FK_OK;
 }

@@ -8,24 +8,44 @@
 
 /* Device buffers of one engine's sparse table (grown on demand). */
 struct FksState {
-    uint64_t *sorted = nullptr;   /* the slots, sorted */
-    uint64_t *keys = nullptr;     /* run values: window indices [0, nw), short walks [nw, nw+ns) */
+    uint64_t *sorted = nullptr;   /* a pass's keys, sorted */
+    uint64_t *keys = nullptr;     /* run values: the pass's distinct window indices */
     uint64_t *c64 = nullptr;      /* run lengths */
-    uint32_t *lo = nullptr;       /* window counts as the reference's u32 frequency */
-    uint32_t *hi = nullptr;
     void *tmp = nullptr;          /* rocPRIM temporary storage */
     unsigned long long *small = nullptr;
     uint64_t *cand = nullptr, *cand2 = nullptr;
-    size_t sorted_cap = 0, keys_cap = 0, c64_cap = 0, lo_cap = 0, hi_cap = 0, tmp_cap = 0, small_cap = 0,
+    size_t sorted_cap = 0, keys_cap = 0, c64_cap = 0, tmp_cap = 0, small_cap = 0,
            cand_cap = 0, cand2_cap = 0;
-    uint64_t nw = 0;              /* distinct k-mers */
-    uint64_t ns = 0;              /* distinct short walks */
 };
 
-/* Sort and run-length encode the n slots; table statistics as
- * k_table_stats's (distinct, u32 sum, last[4], first[4]); *rollover != 0 if
- * some k-mer occurs 2^32 times or more; nodeCounter if want_nodes.
- * Synchronises the stream.  0 or -1 (HIP error / out of memory). */
-int fks_finalize(FksState *st, uint64_t *slots, uint64_t n, int k, int want_nodes, hipStream_t s,
-                 unsigned long long tstat[10], unsigned long long *rollover, unsigned long long *nodes);
+/* One pass's part of the table: ascending distinct window indices and
+ * their u32 counts (device, owned by the caller: hipFree both). */
+struct FksPart {
+    uint64_t *keys;
+    uint32_t *cnts;
+    uint64_t n;
+};
+
+/* Device accumulators of a sparse finish (unsigned long long[FKS_ACC_N]):
+ * the table statistics as k_table_stats's (distinct, u32 sum, last[4],
+ * first[4]), the rollover flag (a count >= 2^32), and the prefix histogram
+ * of adjacent sorted keys (first differing base at depth d, [d]). */
+enum { FKS_ACC_ROLL = 10, FKS_ACC_WPREFIX = 11, FKS_ACC_N = 40 };
+
+/* One key-range pass: sort and run-length encode the n window keys (bits
+ * [0, 2k)) into *part; statistics, rollover and prefix histogram accumulate
+ * into dacc.  Synchronises the stream.  0 or -1 (HIP error / out of memory). */
+int fks_sort_runs(FksState *st, uint64_t *keys, uint64_t n, int k, hipStream_t s, unsigned long long *dacc,
+                  FksPart *part);
+/* The same for a dense count table of keys [lo, lo + n). */
+int fks_dense_runs(FksState *st, unsigned long long *dense, uint64_t n, uint64_t lo, int k, hipStream_t s,
+                   unsigned long long *dacc, FksPart *part);
+/* Sort v[0, n) (all 64 bits) and keep the distinct values in place. */
+int fks_unique(FksState *st, uint64_t *v, uint64_t n, hipStream_t s, uint64_t *n_out);
+/* Mark which short-walk prefixes a part's keys contain: found[i * 20 + d - 1]
+ * for depth d of short walk i. */
+int fks_short_mark(const FksPart *part, const uint64_t *shorts, uint64_t ns, int k, uint8_t *found, hipStream_t s);
+/* Distinct short-walk prefixes no window has (nodeCounter's short part). */
+int fks_short_count(FksState *st, const uint64_t *shorts, uint64_t ns, const uint8_t *found, hipStream_t s,
+                    unsigned long long *total);
 void fks_free(FksState *st);

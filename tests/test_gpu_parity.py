@@ -770,6 +770,29 @@ def test_sparse_long_headers_and_acgt(k):
     assert_same_sparse(bytes(random.Random(k).choices(b"ACGT", k=700_000)), k)
 
 
+@pytest.mark.parametrize("k", [17, 20])
+def test_sparse_key_range_passes(k, monkeypatch):
+    """the sparse table built in many key-range passes: FINDKMER_TUNE sp_pass=N
+    caps a sorted pass at N window keys (merged buckets), and a bucket with
+    more windows than that is counted in a dense table (a poly-A stretch puts
+    ~200k windows into bucket 0); boundaries between passes must not change
+    the table, the statistics or nodeCounter"""
+    monkeypatch.setenv("FINDKMER_TUNE", "sp_pass=5000")
+    rng = random.Random(k)
+    body = bytes(rng.choices(b"ACGT", k=150_000)) + b"A" * 200_000 + b"NN" + bytes(rng.choices(b"ACGTN", k=80_000))
+    lines = b"\n".join(body[i:i + 70] for i in range(0, len(body), 70))
+    assert_same_sparse(b">chr1\n" + lines + b"\n>chr2 x\nACGTAC\nGT\n", k)
+    assert_same_sparse(mixed_input(1300 + k, 300_000), k)
+
+
+def test_sparse_every_bucket_dense(monkeypatch):
+    """sp_pass=1: every nonempty bucket takes the dense path (k=17: 2^22 u64
+    per bucket), golden inputs"""
+    monkeypatch.setenv("FINDKMER_TUNE", "sp_pass=1")
+    for name in ("test.txt", "edge.txt", "shortruns.txt", "ffbyte.bin"):
+        assert_same_sparse(golden_input(name), 17)
+
+
 def test_sparse_dense_entry_points_refuse():
     """the dense-table calls answer FK_E_INVALID / FK_E_K_UNSUPPORTED for k > 16"""
     with fk.Engine(17) as e:
