@@ -217,7 +217,8 @@ def measure(ctx, k, n, L, seed, chrom, steps, warmup, verify=False):
     torch.cuda.synchronize()
 
     eng = fk.Engine(k, device=ctx.local, timing_every=args.timing_every)
-    merge_t = fkdist.merge_buffer(k, ctx.coll_dev) if sharded else None
+    # 17 <= k <= 20: sparse tables, merged by an all-to-all (no dense buffer)
+    merge_t = fkdist.merge_buffer(k, ctx.coll_dev) if sharded and k < fkdist.SPARSE_KMIN else None
     pinned = torch.empty(fkdist.COUNTER_SLOTS, dtype=torch.int32, pin_memory=True) \
         if (sharded and ctx.coll_dev == "cuda") else None
     phase_s = {}

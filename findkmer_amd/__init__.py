@@ -119,6 +119,9 @@ SIGNATURES = [
     ("fk_engine_merge_from", ctypes.c_int, [_P, _P]),
     ("fk_engine_unknown", ctypes.c_int, [_P, _U8P, ctypes.c_uint64, _U64P]),
     ("fk_engine_sparse", ctypes.c_int, [_P, _U64P, _U32P, ctypes.c_uint64, _U64P]),
+    ("fk_engine_sparse_device", ctypes.c_int, [_P, _P, _P, ctypes.c_uint64, _U64P]),
+    ("fk_engine_sparse_split", ctypes.c_int, [_P, ctypes.c_int, _U64P]),
+    ("fk_engine_sparse_adopt", ctypes.c_int, [_P, _P, _P, ctypes.c_uint64, _U64P]),
     ("fk_count", ctypes.c_int, [_P, ctypes.c_uint64, ctypes.c_int, ctypes.POINTER(FkOpts), _U32P, ctypes.POINTER(FkResult)]),
     ("fk_count_multi", ctypes.c_int, [_P, ctypes.c_uint64, ctypes.c_int, ctypes.c_int, ctypes.POINTER(FkOpts), _U32P, ctypes.POINTER(FkResult)]),
     ("fk_synth_device", ctypes.c_int, [_P, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int, _P, _U64P]),
@@ -320,6 +323,32 @@ class Engine:
         _check(lib().fk_engine_sparse(self.h, keys.ctypes.data_as(_U64P), cnts.ctypes.data_as(_U32P), n.value,
                                       ctypes.byref(n)), "sparse")
         return keys[: n.value], cnts[: n.value]
+
+    @property
+    def sparse_table(self):
+        """17 <= k <= 20: the table is sparse (sparse(), the sparse_* merge)"""
+        return self.k > 16
+
+    def sparse_split(self, world):
+        """after finish(): the table's run count per owner rank (owner of index
+        x: x // ceil(4^k / world))"""
+        out = (ctypes.c_uint64 * world)()
+        _check(lib().fk_engine_sparse_split(self.h, world, out), "sparse_split")
+        return [int(v) for v in out]
+
+    def sparse_device(self, keys_ptr, counts_ptr, cap):
+        """the sparse table into device buffers (uint64 keys, uint32 counts);
+        returns the run count"""
+        n = ctypes.c_uint64()
+        _check(lib().fk_engine_sparse_device(self.h, keys_ptr, counts_ptr, cap, ctypes.byref(n)), "sparse_device")
+        return n.value
+
+    def sparse_adopt(self, keys_ptr, counts_ptr, n):
+        """replace the sparse table by the runs received in the exchange
+        (device pointers); returns (distinct, sum of u32 counts)"""
+        st = (ctypes.c_uint64 * 2)()
+        _check(lib().fk_engine_sparse_adopt(self.h, keys_ptr, counts_ptr, n, st), "sparse_adopt")
+        return int(st[0]), int(st[1])
 
     def unknown_bytes(self):
         n = ctypes.c_uint64()

@@ -4406,6 +4406,20 @@ extern "C" int fk_engine_resolve(fk_engine *e, const fk_state *entering) {
         e->state = in;
         return FK_OK;
     }
+    if (e->sparse) {
+        /* 17 <= k <= 20: the shard's state pass only fixed its transfer
+           function; count it now from the exact entering state (and retain
+           it for finish's key-range passes) */
+        e->shard_pending = 0;
+        e->state = in;
+        HIPCHK(write_dstate(e, in));
+        if (e->shard_len == 0) {
+            HIPCHK(hipStreamSynchronize(e->stream));
+            return FK_OK;
+        }
+        e->chunks -= geometry(e, e->shard_len).nchunks;   /* counted again below */
+        return sparse_segment(e, e->shard_buf, e->shard_len);
+    }
     /* the shard's compact summary, taken while the shard is still pending
        (fk_engine_summary describes a pending shard only) */
     fk_summary s;
@@ -5198,10 +5212,8 @@ extern "C" int fk_engine_table_from_device(fk_engine *e, const void *src) {
     return FK_OK;
 }
 
-/* The sparse table (17 <= k <= 20) after fk_engine_finish: the distinct
-   k-mer indices (reference order, ascending = CSV row order) and their u32
-   frequencies.  keys/counts may be NULL to ask for *n only. */
-extern "C" int fk_engine_sparse(fk_engine *e, uint64_t *keys, uint32_t *counts, uint64_t cap, uint64_t *n) {
+static int sparse_copy(fk_engine *e, uint64_t *keys, uint32_t *counts, uint64_t cap, uint64_t *n,
+                       hipMemcpyKind kind) {
     if (!e || !n) return FK_E_INVALID;
     if (!e->sparse || !e->sp_done) return FK_E_STATE;
     *n = e->sp_distinct;
@@ -5211,11 +5223,96 @@ extern "C" int fk_engine_sparse(fk_engine *e, uint64_t *keys, uint32_t *counts, 
     if (rc) return rc;
     uint64_t at = 0;
     for (const auto &p : e->spparts) {
-        if (keys) HIPCHK(hipMemcpyAsync(keys + at, p.keys, p.n * sizeof(uint64_t), hipMemcpyDeviceToHost, e->stream));
-        if (counts) HIPCHK(hipMemcpyAsync(counts + at, p.cnts, p.n * sizeof(uint32_t), hipMemcpyDeviceToHost, e->stream));
+        if (keys) HIPCHK(hipMemcpyAsync(keys + at, p.keys, p.n * sizeof(uint64_t), kind, e->stream));
+        if (counts) HIPCHK(hipMemcpyAsync(counts + at, p.cnts, p.n * sizeof(uint32_t), kind, e->stream));
         at += p.n;
     }
     HIPCHK(hipStreamSynchronize(e->stream));
+    return FK_OK;
+}
+
+/* The sparse table (17 <= k <= 20) after fk_engine_finish: the distinct
+   k-mer indices (reference order, ascending = CSV row order) and their u32
+   frequencies.  keys/counts may be NULL to ask for *n only. */
+extern "C" int fk_engine_sparse(fk_engine *e, uint64_t *keys, uint32_t *counts, uint64_t cap, uint64_t *n) {
+    return sparse_copy(e, keys, counts, cap, n, hipMemcpyDeviceToHost);
+}
+
+/* The same into device buffers (the multi-GPU exchange's send buffers). */
+extern "C" int fk_engine_sparse_device(fk_engine *e, uint64_t *keys, uint32_t *counts, uint64_t cap, uint64_t *n) {
+    return sparse_copy(e, keys, counts, cap, n, hipMemcpyDeviceToDevice);
+}
+
+/* The finished sparse table's runs per owner rank: owner of index x is
+   x / S, S = ceil(4^k / world) (fk_merge_layout's slices). */
+extern "C" int fk_engine_sparse_split(fk_engine *e, int world, uint64_t *counts) {
+    if (!e || !counts || world < 1) return FK_E_INVALID;
+    if (!e->sparse || !e->sp_done) return FK_E_STATE;
+    int rc = set_dev(e);
+    if (rc) return rc;
+    const uint64_t nb = 1ull << (2 * e->k), S = (nb + (uint64_t)world - 1) / (uint64_t)world;
+    for (int r = 0; r < world; r++) counts[r] = 0;
+    for (const auto &p : e->spparts) {
+        if (!p.n) continue;
+        /* the part's keys are ascending: owners' runs are contiguous; the
+           boundaries by binary search over the device keys, one key per probe */
+        uint64_t first = 0, last = 0;
+        HIPCHK(hipMemcpyAsync(&first, p.keys, 8, hipMemcpyDeviceToHost, e->stream));
+        HIPCHK(hipMemcpyAsync(&last, p.keys + (p.n - 1), 8, hipMemcpyDeviceToHost, e->stream));
+        HIPCHK(hipStreamSynchronize(e->stream));
+        const int r0 = (int)(first / S), r1 = (int)(last / S);
+        uint64_t at = 0;
+        for (int r = r0; r <= r1; r++) {
+            uint64_t lo = at, hi = p.n;   /* first index with key >= (r + 1) * S */
+            if (r == r1) {
+                lo = p.n;
+            } else {
+                const uint64_t want = (uint64_t)(r + 1) * S;
+                while (lo < hi) {
+                    const uint64_t mid = (lo + hi) / 2;
+                    uint64_t v = 0;
+                    HIPCHK(hipMemcpy(&v, p.keys + mid, 8, hipMemcpyDeviceToHost));
+                    if (v < want) lo = mid + 1;
+                    else hi = mid;
+                }
+            }
+            counts[r] += lo - at;
+            at = lo;
+        }
+    }
+    return FK_OK;
+}
+
+/* Replace the finished sparse table by the runs this rank owns after the
+   exchange (keys/counts: device, any order, a key possibly from several
+   ranks): counts of a key summed, stats[0] = distinct k-mers, stats[1] = the
+   sum of their u32 counts (short of the windows when a sum wrapped: the
+   rollover check). */
+extern "C" int fk_engine_sparse_adopt(fk_engine *e, const uint64_t *keys, const uint32_t *counts, uint64_t n,
+                                      uint64_t *stats) {
+    if (!e || !stats || (n && (!keys || !counts))) return FK_E_INVALID;
+    if (!e->sparse || !e->sp_done) return FK_E_STATE;
+    int rc = set_dev(e);
+    if (rc) return rc;
+    DevScratch acc;
+    if (!acc.alloc(FKS_ACC_N * sizeof(unsigned long long))) return FK_E_OOM;
+    HIPCHK(hipMemsetAsync(acc.p, 0, FKS_ACC_N * sizeof(unsigned long long), e->stream));
+    FksPart part{nullptr, nullptr, 0};
+    if (fks_merge_runs(&e->fks, keys, counts, n, e->k, e->stream, acc.as<unsigned long long>(), &part)) {
+        hipFree(part.keys);
+        hipFree(part.cnts);
+        return FK_E_HIP;
+    }
+    unsigned long long r[FKS_ACC_N];
+    HIPCHK(hipMemcpyAsync(r, acc.p, sizeof r, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    sp_parts_free(e);
+    if (part.n) e->spparts.push_back(part);
+    e->sp_distinct = part.n;
+    memcpy(e->sp_tstat, r, sizeof e->sp_tstat);
+    e->sp_roll = r[FKS_ACC_ROLL];
+    stats[0] = r[0];
+    stats[1] = r[1];
     return FK_OK;
 }
 

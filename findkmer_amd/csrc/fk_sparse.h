@@ -40,6 +40,11 @@ int fks_sort_runs(FksState *st, uint64_t *keys, uint64_t n, int k, hipStream_t s
 /* The same for a dense count table of keys [lo, lo + n). */
 int fks_dense_runs(FksState *st, unsigned long long *dense, uint64_t n, uint64_t lo, int k, hipStream_t s,
                    unsigned long long *dacc, FksPart *part);
+/* Runs from several tables (any order, repeated keys): sorted, counts of a
+ * key summed (u64, then the u32 frequency), into *part, with statistics as
+ * fks_sort_runs.  The multi-GPU merge of the ranks' sparse tables. */
+int fks_merge_runs(FksState *st, const uint64_t *keys, const uint32_t *cnts, uint64_t n, int k, hipStream_t s,
+                   unsigned long long *dacc, FksPart *part);
 /* Sort v[0, n) (all 64 bits) and keep the distinct values in place. */
 int fks_unique(FksState *st, uint64_t *v, uint64_t n, hipStream_t s, uint64_t *n_out);
 /* Mark which short-walk prefixes a part's keys contain: found[i * 20 + d - 1]

@@ -241,6 +241,35 @@ int fks_dense_runs(FksState *st, unsigned long long *dense, uint64_t n, uint64_t
     return runs_stats(st, runs, k, s, dacc, part);
 }
 
+struct WidenU32 {
+    __device__ unsigned long long operator()(uint32_t v) const { return v; }
+};
+
+int fks_merge_runs(FksState *st, const uint64_t *keys, const uint32_t *cnts, uint64_t n, int k, hipStream_t s,
+                   unsigned long long *dacc, FksPart *part) {
+    *part = FksPart{nullptr, nullptr, 0};
+    if (n == 0) return 0;
+    if (ensure((void **)&st->sorted, &st->sorted_cap, n * 8) || ensure((void **)&st->keys, &st->keys_cap, n * 8) ||
+        ensure((void **)&st->c64, &st->c64_cap, n * 8) || ensure((void **)&st->cand2, &st->cand2_cap, n * 4) ||
+        ensure((void **)&st->small, &st->small_cap, 64 * sizeof(unsigned long long)))
+        return -1;
+    uint32_t *vs = reinterpret_cast<uint32_t *>(st->cand2);
+    auto wide = rocprim::make_transform_iterator(vs, WidenU32());
+    size_t tb = 0, tb2 = 0;
+    CK(rocprim::radix_sort_pairs(nullptr, tb, keys, st->sorted, cnts, vs, n, 0, 2 * k, s));
+    CK(rocprim::reduce_by_key(nullptr, tb2, st->sorted, wide, n, st->keys, st->c64, st->small,
+                              rocprim::plus<unsigned long long>(), rocprim::equal_to<uint64_t>(), s));
+    if (ensure(&st->tmp, &st->tmp_cap, tb > tb2 ? tb : tb2)) return -1;
+    tb = tb2 = st->tmp_cap;
+    CK(rocprim::radix_sort_pairs(st->tmp, tb, keys, st->sorted, cnts, vs, n, 0, 2 * k, s));
+    CK(rocprim::reduce_by_key(st->tmp, tb2, st->sorted, wide, n, st->keys, st->c64, st->small,
+                              rocprim::plus<unsigned long long>(), rocprim::equal_to<uint64_t>(), s));
+    unsigned long long runs = 0;
+    CK(hipMemcpyAsync(&runs, st->small, sizeof runs, hipMemcpyDeviceToHost, s));
+    CK(hipStreamSynchronize(s));
+    return runs_stats(st, runs, k, s, dacc, part);
+}
+
 int fks_unique(FksState *st, uint64_t *v, uint64_t n, hipStream_t s, uint64_t *n_out) {
     *n_out = n;
     if (n < 2) return 0;

@@ -34,6 +34,12 @@ only when a shard may end the stream:
    total and distinct bins (the rollover check needs the whole table's sum).
    ShardedResult.table_full() gathers the slices onto rank 0 when one
    process writes the CSV.
+   For 17 <= k <= 20 the tables are sparse (fk_engine_sparse: sorted
+   distinct indices + u32 counts) and the same ownership holds without a
+   dense buffer: each rank cuts its finished table at the owners' bounds
+   (fk_engine_sparse_split), one all-to-all sends every run to its owner,
+   and the owner sums repeated keys (fk_engine_sparse_adopt, on the GPU):
+   SparseShardedResult.
 
 The library's own RCCL communicator (backend nccl, native_comm) runs the
 whole exchange inside fk_engine_shard_exchange on the engine's stream: the
@@ -77,6 +83,7 @@ ROW_WORDS = FK_PACK_ROW_WORDS
 STAT_SLOTS = FK_PACK_STATS              # a sharded table's (total, distinct) as 4 limbs each
 FAST_KMAX = 7                          # shards counted in one pass (k_count + k_tail)
 SHARD_KMIN = 12                        # from here on the merged table is sharded over the ranks
+SPARSE_KMIN = 17                       # from here on the tables are sparse (fk_engine_sparse)
 
 
 def _to_i64(v):
@@ -289,6 +296,95 @@ class ShardedResult:
         return FK_OK
 
 
+class SparseShardedResult(ShardedResult):
+    """The merged result of a sharded pass for 17 <= k <= 20: this rank owns
+    the k-mer indices [lo, hi) of the merged sparse table (`keys`, `counts`,
+    numpy, ascending = CSV row order); the counters, total and distinct
+    k-mers are merged over all ranks (one all-reduce of limbs)."""
+
+    def __init__(self, buf, k, rank, first_end, local, world, group, engine):
+        super().__init__(buf, k, rank, first_end, local, path="stitched", transport="torch", world=world,
+                         sharded=True, group=group)
+        self.tw = 0                     # the buffer holds counters and slice statistics only
+        S = ((1 << (2 * k)) + world - 1) // world
+        self.lo, self.hi = min(rank * S, self.nb), min((rank + 1) * S, self.nb)
+        self.table = None
+        self.keys, self.counts = engine.sparse()
+
+    def _table_stats(self):
+        if self._tsum is None:
+            st = self.buf[COUNTER_SLOTS:COUNTER_SLOTS + STAT_SLOTS].tolist()
+            self._tsum, self._distinct = _limbs_value(st[:4]), _limbs_value(st[4:])
+        return self._tsum, self._distinct
+
+    def _decode(self):
+        if self._vals is None:
+            limbs = self.buf[:COUNTER_SLOTS].tolist()
+            self._vals = {name: _limbs_value(limbs[i * LIMBS:(i + 1) * LIMBS]) for i, name in enumerate(COUNTERS)}
+        return self._vals
+
+    def table_full(self, dst=0):
+        """(keys, counts) of the whole merged table on rank `dst` (a
+        collective: every rank calls it), None on the others."""
+        import numpy as np
+        dev = "cuda" if dist.get_backend(self.group) == "nccl" else "cpu"
+        n = torch.tensor([len(self.keys)], dtype=torch.int64, device=dev)
+        sizes = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in range(self.world)]
+        dist.all_gather(sizes, n, group=self.group)
+        sizes = [int(v.item()) for v in sizes]
+        m = max(1, max(sizes))
+        kp = torch.zeros(m, dtype=torch.int64)
+        cp = torch.zeros(m, dtype=torch.int32)
+        kp[:len(self.keys)] = torch.from_numpy(self.keys.view(np.int64))
+        cp[:len(self.counts)] = torch.from_numpy(self.counts.view(np.int32))
+        kp, cp = kp.to(dev), cp.to(dev)
+        gk = [torch.empty_like(kp) for _ in range(self.world)]
+        gc = [torch.empty_like(cp) for _ in range(self.world)]
+        dist.all_gather(gk, kp, group=self.group)
+        dist.all_gather(gc, cp, group=self.group)
+        if self.rank != dst:
+            return None
+        keys = np.concatenate([gk[r][:sizes[r]].cpu().numpy() for r in range(self.world)]).view(np.uint64)
+        cnts = np.concatenate([gc[r][:sizes[r]].cpu().numpy() for r in range(self.world)]).view(np.uint32)
+        return keys, cnts
+
+
+def _sparse_merge(engine, vals, counting, rank, world, group, first_end, r):
+    """17 <= k <= 20: every rank's runs to their owners (one all-to-all of
+    keys and one of counts, after one of the run counts), the owner's sum
+    (fk_engine_sparse_adopt), then one all-reduce of the counter and slice
+    statistic limbs."""
+    nccl = dist.get_backend(group) == "nccl"
+    coll = "cuda" if nccl else "cpu"
+    edev = getattr(engine, "device_str", "cuda")   # where the engine's buffers live
+    counts = engine.sparse_split(world) if counting else [0] * world
+    n = sum(counts)
+    keys = torch.empty(max(1, n), dtype=torch.int64, device=edev)
+    cnts = torch.empty(max(1, n), dtype=torch.int32, device=edev)
+    if n:
+        got = engine.sparse_device(keys.data_ptr(), cnts.data_ptr(), n)
+        assert got == n, (got, n)
+    send = torch.tensor(counts, dtype=torch.int64, device=coll)
+    recv = torch.empty(world, dtype=torch.int64, device=coll)
+    dist.all_to_all_single(recv, send, group=group)
+    rsizes = [int(v) for v in recv.tolist()]
+    m = sum(rsizes)
+    k_out = torch.empty(max(1, m), dtype=torch.int64, device=coll)
+    c_out = torch.empty(max(1, m), dtype=torch.int32, device=coll)
+    dist.all_to_all_single(k_out[:m], keys[:n].to(coll), rsizes, counts, group=group)
+    dist.all_to_all_single(c_out[:m], cnts[:n].to(coll), rsizes, counts, group=group)
+    k_in, c_in = k_out.to(edev), c_out.to(edev)
+    if edev != "cpu":
+        torch.cuda.synchronize()
+    distinct, total = engine.sparse_adopt(k_in.data_ptr(), c_in.data_ptr(), m)
+    buf = torch.zeros(COUNTER_SLOTS + STAT_SLOTS, dtype=torch.int32, device=coll)
+    _put_counters(buf, vals, None, 0)
+    buf[COUNTER_SLOTS:].copy_(torch.tensor([(v >> (16 * j)) & 0xFFFF for v in (total, distinct) for j in range(LIMBS)],
+                                           dtype=torch.int32))
+    dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=group)
+    return SparseShardedResult(buf.cpu(), engine.k, rank, first_end, r, world, group, engine)
+
+
 def _put_counters(buf, values, pinned, nb=None):
     """Write the u64 counters into the buffer's limb slots (host -> buffer),
     after the nb table words (default: the last COUNTER_SLOTS entries)."""
@@ -448,6 +544,9 @@ def count_sharded(engine, ptr, nbytes, halo, buf, group=None, times=None, pinned
     same feed_shard_device / summary / summary_full / resolve / finish /
     table_to_device / shard_pack methods).
 
+    17 <= k <= 20: `buf` is unused (may be None); the sparse tables are
+    merged by an all-to-all to their owners (SparseShardedResult).
+
     shard_table: the stitched path reduce-scatters the table (each rank
     keeps its slice of the merged table) instead of reducing it onto rank 0;
     None = for k >= SHARD_KMIN.  test_invalid (native path, tests): this
@@ -456,14 +555,16 @@ def count_sharded(engine, ptr, nbytes, halo, buf, group=None, times=None, pinned
     import time
     rank = dist.get_rank(group)
     world = dist.get_world_size(group)
-    dev = buf.device
+    dev = buf.device if buf is not None else None
     k = engine.k
     if shard_table is None:
         shard_table = k >= SHARD_KMIN
     t0 = time.perf_counter()
     engine.feed_shard_device(ptr, nbytes, halo)
     comm = None
-    if native and buf.is_cuda and hasattr(engine, "shard_exchange") and dist.get_backend(group) == "nccl":
+    sparse = bool(getattr(engine, "sparse_table", k >= SPARSE_KMIN))
+    if native and not sparse and buf is not None and buf.is_cuda and hasattr(engine, "shard_exchange") \
+            and dist.get_backend(group) == "nccl":
         comm = native_comm(group)
     if comm is not None:
         # the whole exchange inside the library, on the engine's stream: one
@@ -478,27 +579,39 @@ def count_sharded(engine, ptr, nbytes, halo, buf, group=None, times=None, pinned
             times["finish"] = times.get("finish", 0.0) + (time.perf_counter() - t1)
         return ShardedResult(buf, k, rank, first_end, r, path="fast" if one else "stitched",
                              transport="rccl-native", world=world, sharded=shard_table, group=group)
-    if fast and engine.k <= FAST_KMAX and hasattr(engine, "shard_pack"):
+    if fast and not sparse and engine.k <= FAST_KMAX and hasattr(engine, "shard_pack"):
         got = _fast_exchange(engine, buf, rank, world, group, times, t0)
         if got is not None:
             return got
     t1 = time.perf_counter()
-    got = stitch_entry_state(engine.summary(), group, dev)
+    sdev = dev if buf is not None else ("cuda" if dist.get_backend(group) == "nccl" else "cpu")
+    got = stitch_entry_state(engine.summary(), group, sdev)
     if got is None:
         # a compact summary did not apply somewhere: the full transfer
         # functions (every rank takes this branch together)
-        got = stitch_entry_state(engine.summary_full(), group, dev, full=True)
+        got = stitch_entry_state(engine.summary_full(), group, sdev, full=True)
     state, first_end, any_full = got
     engine.resolve(state)
     rc, r = engine.finish(allow=(FK_OK, FK_E_ROLLOVER, FK_E_UNTERMINATED_HEADER, FK_E_EMPTY))
     if any_full:
         # where the stream ends is exact only after the resolve: one more
         # small all-gather of the ranks' end flags
-        ends = _gather_rows([1 if (r.hit_eof_byte and not state.ended) else 0], group, dev)
+        ends = _gather_rows([1 if (r.hit_eof_byte and not state.ended) else 0], group, sdev)
         first_end = next((i for i, f in enumerate(ends) if f), None)
     t2 = time.perf_counter()
     counting = first_end is None or rank <= first_end
     last = first_end if first_end is not None else world - 1
+    if sparse:
+        vals = [0] * len(COUNTERS)
+        if counting:
+            vals = [r.windows, r.valid_bases, *r.base_count, *r.depth1, r.unknown_chars, r.scanned_bytes,
+                    1 if rank == first_end else 0, r.unterminated_header if rank == last else 0]
+        res = _sparse_merge(engine, vals, counting, rank, world, group, first_end, r)
+        if times is not None:
+            times["count"] = times.get("count", 0.0) + (t1 - t0)
+            times["stitch"] = times.get("stitch", 0.0) + (t2 - t1)
+            times["merge"] = times.get("merge", 0.0) + (time.perf_counter() - t2)
+        return res
     nb, tw, merged, _ = _regions(buf, k, world)
     if counting:
         if buf.is_cuda:

@@ -285,9 +285,25 @@ int  fk_engine_unknown(fk_engine *e, uint8_t *out, uint64_t cap, uint64_t *n);
  * fk_engine_finish, the distinct k-mer indices in ascending order (= the
  * CSV's row order) and their u32 frequencies; keys and counts may be NULL to
  * ask for *n.  The dense table calls (fk_engine_table...) return
- * FK_E_INVALID for these k.  Device memory: 8 bytes per input byte fed
- * (slots), plus ~24 per byte while fk_engine_finish sorts them. */
+ * FK_E_INVALID for these k.  Device memory: the input fed (1 byte per byte,
+ * kept until reset: fk_engine_finish builds the table from it in key-range
+ * passes sized to the free HBM) plus 12 bytes per distinct k-mer. */
 int  fk_engine_sparse(fk_engine *e, uint64_t *keys, uint32_t *counts, uint64_t cap, uint64_t *n);
+/* The same into device buffers. */
+int  fk_engine_sparse_device(fk_engine *e, uint64_t *keys, uint32_t *counts, uint64_t cap, uint64_t *n);
+
+/* Multi-GPU merge of sparse tables (replaces the reduce of dense ones): the
+ * ranks' runs go to their owners -- rank r owns indices [r*S, (r+1)*S),
+ * S = ceil(4^k / world), a contiguous run of CSV rows -- with one
+ * all-to-all.  fk_engine_sparse_split: the finished table's run count per
+ * owner (counts[world]; the runs are contiguous in owner order).
+ * fk_engine_sparse_adopt: replace the table by the runs received (device
+ * pointers, any order, repeated keys summed); stats[0] = distinct k-mers,
+ * stats[1] = the sum of their u32 counts (short of the windows when a sum
+ * reached 2^32: the reference's rollover exit, :642). */
+int  fk_engine_sparse_split(fk_engine *e, int world, uint64_t *counts);
+int  fk_engine_sparse_adopt(fk_engine *e, const uint64_t *keys, const uint32_t *counts, uint64_t n,
+                            uint64_t *stats /* [2] */);
 
 /* One-shot convenience: count a whole buffer on one device. */
 int  fk_count(const uint8_t *buf, uint64_t len, int k, const fk_opts *opts,

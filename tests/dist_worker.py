@@ -67,7 +67,8 @@ def main():
     dev[: hi - lo + halo].copy_(torch.frombuffer(bytearray(data[lo - halo:hi]), dtype=torch.uint8))
     torch.cuda.synchronize()
     eng = fk.Engine(args.k, device=0)
-    buf = fkdist.merge_buffer(args.k, "cuda" if args.backend == "nccl" else "cpu")
+    sparse = args.k >= fkdist.SPARSE_KMIN   # sparse tables: no merge buffer, an all-to-all to the owners
+    buf = None if sparse else fkdist.merge_buffer(args.k, "cuda" if args.backend == "nccl" else "cpu")
     # twice: the second pass reuses the engine, the buffer and the fast
     # path's scratch (stale rows from the first must not leak into it)
     shard = None if args.shard_table == "auto" else bool(int(args.shard_table))
@@ -77,7 +78,14 @@ def main():
                                    native=bool(args.native), shard_table=shard, test_invalid=bool(args.test_invalid))
     full = res.table_full()   # every rank (a gather when the table is sharded)
     out = {"rank": rank}
-    if rank == 0:
+    if sparse:
+        # every rank owns a contiguous key range of the merged table
+        assert len(res.keys) == 0 or (int(res.keys.min()) >= res.lo and int(res.keys.max()) < res.hi), \
+            "a key outside the owner's range"
+    if rank == 0 and sparse:
+        keys, cnts, r = oracle.count_sparse(data, args.k, cap=len(data) + 16)
+        equal = bool(np.array_equal(full[0], keys) and np.array_equal(full[1], cnts))
+    elif rank == 0:
         got = full.cpu().numpy().view(np.uint32)
         if args.k <= 13:
             want, r, _ = oracle.count_dense(data, args.k)
@@ -86,6 +94,7 @@ def main():
             keys, cnts, r = oracle.count_sparse(data, args.k, cap=len(data) + 16)
             nz = np.nonzero(got)[0]
             equal = bool(np.array_equal(nz.astype(np.uint64), keys) and np.array_equal(got[nz], cnts))
+    if rank == 0:
         out.update({
             "table_equal": equal,
             "sharded": res.sharded,

@@ -258,3 +258,49 @@ class ModelEngine:
 
     def table(self):
         return self.tab.copy()
+
+
+class SparseModelEngine(ModelEngine):
+    """ModelEngine with the sparse table interface of 17 <= k <= 20
+    (fk_engine_sparse / _split / _device / _adopt) on host buffers, so the
+    gloo tests drive dist.py's all-to-all merge (dist._sparse_merge) at a
+    small k."""
+
+    device_str = "cpu"
+    sparse_table = True
+
+    def __init__(self, k, shard, guess=None):
+        super().__init__(k, shard, guess)
+        self.runs = None
+
+    def finish(self, allow=None):
+        rc, res = super().finish(allow)
+        nz = np.nonzero(self.tab)[0]
+        self.runs = (nz.astype(np.uint64), self.tab[nz].astype(np.uint32))
+        return rc, res
+
+    def sparse(self):
+        return self.runs[0].copy(), self.runs[1].copy()
+
+    def sparse_split(self, world):
+        S = ((1 << (2 * self.k)) + world - 1) // world
+        owner = (self.runs[0] // np.uint64(S)).astype(np.int64)
+        return [int(v) for v in np.bincount(owner, minlength=world)[:world]]
+
+    def sparse_device(self, keys_ptr, counts_ptr, cap):
+        import ctypes
+        n = len(self.runs[0])
+        assert cap >= n
+        ctypes.memmove(keys_ptr, self.runs[0].ctypes.data, 8 * n)
+        ctypes.memmove(counts_ptr, self.runs[1].ctypes.data, 4 * n)
+        return n
+
+    def sparse_adopt(self, keys_ptr, counts_ptr, n):
+        import ctypes
+        keys = np.ctypeslib.as_array((ctypes.c_uint64 * max(1, n)).from_address(keys_ptr))[:n].copy()
+        cnts = np.ctypeslib.as_array((ctypes.c_uint32 * max(1, n)).from_address(counts_ptr))[:n].astype(np.uint64)
+        uk, inv = np.unique(keys, return_inverse=True)
+        sums = np.zeros(len(uk), dtype=np.uint64)
+        np.add.at(sums, inv, cnts)
+        self.runs = (uk, (sums & 0xFFFFFFFF).astype(np.uint32))
+        return len(uk), int(self.runs[1].astype(np.uint64).sum())

@@ -51,7 +51,7 @@ def _input(seed, n):
     return bytes(out[:n])
 
 
-def _worker(rank, world, port, data, bounds, mode, results, shard=False):
+def _worker(rank, world, port, data, bounds, mode, results, shard=False, sparse=False):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     import torch
@@ -79,11 +79,25 @@ def _worker(rank, world, port, data, bounds, mode, results, shard=False):
             guess = (1 - hdr, 0, 0)                # rank 1 guessed wrong: full summaries
         elif mode == "compact_miss":
             guess = (hdr, R, code)
-        eng = scan_model.ModelEngine(K, shard, guess)
-        buf = fkdist.merge_buffer(K, "cpu")
-        res = fkdist.count_sharded(eng, 0, len(shard), 0, buf, shard_table=bool(shard_table))
-        full = res.table_full()   # a collective when the table is sharded
-        if res.sharded:
+        if sparse:
+            # the sparse tables' all-to-all merge (17 <= k <= 20 on the GPU)
+            eng = scan_model.SparseModelEngine(K, shard, guess)
+            res = fkdist.count_sharded(eng, 0, len(shard), 0, None)
+            got = res.table_full()
+            S = ((1 << (2 * K)) + world - 1) // world
+            assert res.lo == min(rank * S, 1 << (2 * K)) and res.hi == min((rank + 1) * S, 1 << (2 * K))
+            assert all(res.lo <= int(x) < res.hi for x in res.keys), "a key outside the owner's range"
+            full = None
+            if rank == 0:
+                full = np.zeros(1 << (2 * K), dtype=np.uint32)
+                full[got[0].astype(np.int64)] = got[1]
+                full = __import__("torch").from_numpy(full.view(np.int32))
+        else:
+            eng = scan_model.ModelEngine(K, shard, guess)
+            buf = fkdist.merge_buffer(K, "cpu")
+            res = fkdist.count_sharded(eng, 0, len(shard), 0, buf, shard_table=bool(shard_table))
+            full = res.table_full()   # a collective when the table is sharded
+        if res.sharded and not sparse:
             # this rank's slice: the first bases' range [lo, hi) of the table
             want_lo = min(rank * (fkdist.table_words(K, world) // world), 1 << (2 * K))
             assert res.lo == want_lo and res.table.numel() == res.hi - res.lo
@@ -100,12 +114,12 @@ def _worker(rank, world, port, data, bounds, mode, results, shard=False):
         dist.destroy_process_group()
 
 
-def _run(world, data, bounds, mode, shard=False):
+def _run(world, data, bounds, mode, shard=False, sparse=False):
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     results = ctx.SimpleQueue()
-    mp.start_processes(_worker, args=(world, _free_port(), data, bounds, mode, results, shard), nprocs=world,
-                       join=True, start_method="spawn")
+    mp.start_processes(_worker, args=(world, _free_port(), data, bounds, mode, results, shard, sparse),
+                       nprocs=world, join=True, start_method="spawn")
     return None if mode == "state" else results.get()
 
 
@@ -119,9 +133,9 @@ def test_stitched_states_gloo(world):
     _run(world, data, _bounds(len(data), world), "state")
 
 
-def _check(data, world, mode, bounds=None, shard=False):
+def _check(data, world, mode, bounds=None, shard=False, sparse=False):
     bounds = bounds or _bounds(len(data), world)
-    table, got = _run(world, data, bounds, mode, shard)
+    table, got = _run(world, data, bounds, mode, shard, sparse)
     want, r, _ = oracle.count_dense(data, K)
     assert np.array_equal(np.frombuffer(table, dtype=np.uint32), want)
     assert got["windows"] == r.windows
@@ -216,3 +230,22 @@ def test_sharded_table_eof_in_middle_gloo():
     data[at - 2:at + 1] = b"\nA\xff"
     got = _check(bytes(data), 3, "full", b, shard=True)
     assert got["first_end"] == 1 and got["sharded"]
+
+
+@pytest.mark.parametrize("world,mode", [(2, "full"), (3, "compact_miss"), (8, "full")])
+def test_sparse_tables_all_to_all_gloo(world, mode):
+    """17 <= k <= 20's merge (dist._sparse_merge): every rank cuts its sparse
+    table at the owners' bounds, one all-to-all sends the runs to their
+    owners, each owner sums repeated keys; the owners' slices in rank order
+    are the oracle's table, the merged counters, total and distinct exact"""
+    got = _check(_input(world + 60, 24000), world, mode, sparse=True)
+    assert got["sharded"] and got["path"] == "stitched"
+
+
+def test_sparse_tables_eof_in_middle_gloo():
+    data = bytearray(_input(61, 24000))
+    b = _bounds(len(data), 3)
+    at = (b[1] + b[2]) // 2
+    data[at - 2:at + 1] = b"\nA\xff"
+    got = _check(bytes(data), 3, "full", b, sparse=True)
+    assert got["first_end"] == 1

@@ -151,3 +151,24 @@ def test_rccl_single_rank_sharded_and_fallback(k, shard, invalid):
         assert out[key][0] == out[key][1], (key, out[key])
     assert out["path"] == "stitched"
     assert out["sharded"] == bool(shard)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k,world,eof_in,backend", [(17, 2, -1, "gloo"), (17, 8, 3, "gloo"), (20, 3, -1, "gloo"),
+                                                    (18, 8, -1, "gloo"), (17, 1, -1, "nccl"), (20, 1, 0, "nccl")])
+def test_sparse_tables_all_to_all_against_oracle(k, world, eof_in, backend):
+    """17 <= k <= 20 over several ranks: each rank's sparse table (key-range
+    passes over its shard, counted from the stitched exact state) cut at the
+    owners' bounds, one all-to-all to the owners, the owner's sum on the GPU
+    (fk_engine_sparse_adopt); the owners' slices gathered in rank order ==
+    the oracle's sparse table, every merged counter exact.  nccl: world 1
+    over RCCL (the all-to-all with device buffers)"""
+    out = _torchrun(world, 29900 + k + 3 * world + eof_in + (50 if backend == "nccl" else 0),
+                    os.path.join(REPO, "tests", "dist_worker.py"),
+                    ["--k", str(k), "--eof-in", str(eof_in), "--bytes", "2000000", "--backend", backend])
+    assert out["table_equal"] and out["sharded"]
+    for key in ("windows", "valid_bases", "base_count", "depth1", "unknown_chars", "scanned_bytes",
+                "hit_eof_byte", "unterminated_header", "distinct"):
+        assert out[key][0] == out[key][1], (key, out[key])
+    assert not out["rollover"]
+    assert out["first_end"] == (eof_in if eof_in >= 0 else None)
