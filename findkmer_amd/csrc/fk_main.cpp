@@ -437,11 +437,12 @@ static int run_k(int argc) {
         /* the GPU of this process (fk_device_select: FINDKMER_DEVICE, else
            spread over the devices with room for the file and the engine's
            buffers: ~2 bytes of partition codes per input byte for
-           8 <= k <= 12, 8 bytes of slots for k >= 17) */
+           8 <= k <= 13; for k >= 17 the engine keeps a copy of the input
+           for its key-range passes, whose scratch fits what is left) */
         struct stat sb;
         const uint64_t fsize = stat(config.sequence_file, &sb) == 0 ? (uint64_t)sb.st_size : 0;
         const int kk = sweep_kmax > config.k ? sweep_kmax : config.k;
-        const uint64_t per = kk > FK_K_MAX_DENSE ? 10 : (kk >= 8 ? 4 : 2);
+        const uint64_t per = kk > FK_K_MAX_DENSE ? 3 : (kk >= 8 ? 4 : 2);
         int dsel = fk_device_select(fsize * per + (256ull << 20), &g_device);
         if (dsel == FK_E_INVALID) {
             fprintf(stderr, "findKmer: FINDKMER_DEVICE names no visible GPU\n");
@@ -482,9 +483,10 @@ static int run_k(int argc) {
     rc = on_device ? scan_device(eng, &res) : scan_file(eng, config.sequence_file_pointer, &res);
     phase(config.k, "scan", tp);
     if (rc == FK_E_OOM && on_device) {
-        /* the resident file copy and the engine's buffers (k >= 17: 8 bytes
-           of slots per input byte) do not fit together: drop the copy and
-           stream the file through the engine's pinned staging instead */
+        /* the resident file copy and the engine's buffers (k >= 17: its own
+           copy of the input plus a pass's scratch) do not fit together: drop
+           the file copy and stream the file through the engine's pinned
+           staging instead */
         fk_input_destroy(g_input);
         g_input = nullptr;
         rc = fk_engine_reset(eng);
