@@ -1871,6 +1871,10 @@ static_assert(PART_MAX_BATCH_W(16u) <= 65536u, "run index words hold 16-bit star
 /* slices of a batch: k = 11 pairs 2^24 / 2^15 (the single k-mers fold into
    them, flagged), k = 12 2^24 / 2^15, k = 13 2^26 / 2^15; k <= 10 at most 128 */
 #define PART_SM(W) ((W) >= 16u ? 2048u : 128u)   /* k = 13: 2^26 / 2^15 slices */
+/* Measured and not kept (round 3): pairs mode keeping 8 batches' run words
+   per slice in LDS and writing them as one 32-B piece (each scattered 4-B word
+   costs a ~40-B write-back, 1.6 GB per 10 GB step): k_part 5.54 -> 5.67 ms,
+   k=11 10 GB step 8.08 -> 8.21 ms (the flush and the extra LDS cost more). */
 #define PART_SINGLE 0x8000u   /* a stored code with this bit: a single k-mer (pairs mode) */
 
 /* A run index word: (start << 16) | (count - 1) for a run of count >= 1
@@ -2285,7 +2289,12 @@ k_bucket_count(PartGeo pg, uint32_t groups, uint32_t *table) {
     /* pairs mode: the slice's 2^sh pair bins, then the 2^(sh-2) bins of the
        single k-mers filed under it (PART_SINGLE codes) */
     const uint32_t ns = pg.pairs ? nb >> 2 : 0u;
-    const uint32_t b = blockIdx.x % pg.nslices, g = blockIdx.x / pg.nslices;
+    /* consecutive slices on one XCD (blocks b, b + 8, .. share an XCD): the
+       128-B line two neighbouring runs of a row share is fetched once into
+       that XCD's L2 (k=11: 1 GB step 1.085 -> 1.065 ms, 10 GB 8.10 -> 8.04) */
+    const uint32_t b = groups == 1 && (pg.nslices & 7u) == 0 ? (blockIdx.x & 7u) * (pg.nslices >> 3) + (blockIdx.x >> 3)
+                                                           : blockIdx.x % pg.nslices;
+    const uint32_t g = blockIdx.x / pg.nslices;
     for (uint32_t i = threadIdx.x; i < nb + ns; i += blockDim.x) slice[i] = 0;
     __syncthreads();
     const uint32_t *ix = pg.idx + (size_t)b * pg.stride;
@@ -3528,7 +3537,9 @@ struct Geo {
 /* k_part's waves per block (8 <= k <= 12): 16 for the 512-slice tables (one
    block per CU), else 8 (two per CU); FINDKMER_TUNE part_waves forces one */
 static uint32_t part_waves_of(const fk_engine *e) {
-    return e->k >= 13 ? 16u : e->part_waves ? e->part_waves : (e->k >= 11 ? 16u : 8u);
+    /* k >= 11: 512 or more slices, which only 16-wave blocks have LDS for
+       (PART_SM): the knob applies to k <= 10 */
+    return e->k >= 11 ? 16u : e->part_waves ? e->part_waves : 8u;
 }
 
 static Geo geometry(const fk_engine *e, uint64_t len) {
