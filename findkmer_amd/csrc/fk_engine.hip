@@ -1738,7 +1738,9 @@ k_redo(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint
  *            (flushed with one atomic per bucket and block), every short
  *            walk to a global list;
  *   SP_KEYS  the windows with lo <= key < hi to a compact global list (one
- *            atomic per tile and wave for the space, ballot-ordered writes);
+ *            atomic per tile and wave for the space, ballot-ordered writes),
+ *            and the short walks too when one pass takes every window (the
+ *            feed counted them; no SP_HIST launch then);
  *   SP_DENSE the windows with lo <= key < hi counted in a dense u64 table
  *            (one bucket too large for a sorted pass: few distinct keys).
  */
@@ -1793,6 +1795,10 @@ k_sp_emit(const uint8_t *buf, uint64_t len, int k, uint64_t maskk, const XState 
                 for (uint32_t j = 0; j < FK_LANE_BYTES; j++) {
                     const uint64_t v = slots[j * 64u + lane];
                     mine += v >= em.lo && v < em.hi ? 1u : 0u;
+                    if (em.shorts && v >= SP_SHORT && v != SP_EMPTY) {   /* (a single pass: no SP_HIST) */
+                        const unsigned long long i = atomicAdd(em.nshort, 1ull);
+                        if (i < em.short_cap) em.shorts[i] = v;
+                    }
                 }
                 const uint32_t tot = wsum32(mine);
                 if (tot) {
@@ -4902,56 +4908,7 @@ static int sparse_finish(fk_engine *e, int32_t seq) {
     unsigned long long *nctr = ctr.as<unsigned long long>();
     HIPCHK(hipMemsetAsync(dacc, 0, FKS_ACC_N * sizeof(unsigned long long), e->stream));
 
-    /* 1. bucket histogram and short walks (a second run if the list overflowed) */
-    const bool tail = !e->state.hdr && seq >= 1 && seq < k;
-    uint64_t scap = std::max<uint64_t>(1024, e->keep_len / 64);
-    DevScratch shorts;
-    uint64_t ns = 0;
-    for (int attempt = 0; attempt < 2; attempt++) {
-        if (!shorts.alloc((scap + 1) * 8)) return FK_E_OOM;
-        HIPCHK(hipMemsetAsync(bh.p, 0, (size_t)nbk * 8, e->stream));
-        HIPCHK(hipMemsetAsync(nctr, 0, 16, e->stream));
-        SpEmit em{};
-        em.mode = SP_HIST;
-        em.shift = shift;
-        em.bhist = bh.as<unsigned long long>();
-        em.nbuckets = nbk;
-        em.shorts = shorts.as<uint64_t>();
-        em.nshort = nctr;
-        em.short_cap = scap;
-        int rc = sp_emit_all(e, em);
-        if (rc) return rc;
-        unsigned long long got = 0;
-        HIPCHK(hipMemcpyAsync(&got, nctr, sizeof got, hipMemcpyDeviceToHost, e->stream));
-        HIPCHK(hipStreamSynchronize(e->stream));
-        ns = got;
-        if (ns <= scap) break;
-        if (attempt) return FK_E_HIP;
-        scap = ns;
-    }
-    if (tail) {   /* the input's last run, shorter than k (:1059-1062 at EOF) */
-        const uint64_t v = SP_SHORT | ((uint64_t)seq << 40) | fk_sigma(e->state.code & ((1ull << (2 * seq)) - 1));
-        HIPCHK(hipMemcpyAsync(shorts.as<uint64_t>() + ns, &v, sizeof v, hipMemcpyHostToDevice, e->stream));
-        HIPCHK(hipStreamSynchronize(e->stream));
-        ns++;
-    }
-    const bool nodes = e->opts.want_nodes != 0;
-    if (!nodes) ns = 0;
-    if (ns > 1) {   /* nodeCounter counts distinct prefixes: drop repeated walks */
-        uint64_t nu = 0;
-        if (fks_unique(&e->fks, shorts.as<uint64_t>(), ns, e->stream, &nu)) return FK_E_HIP;
-        ns = nu;
-    }
-    DevScratch found;
-    if (ns) {
-        if (!found.alloc(ns * 20)) return FK_E_OOM;
-        HIPCHK(hipMemsetAsync(found.p, 0, ns * 20, e->stream));
-    }
-    std::vector<unsigned long long> hb(nbk);
-    HIPCHK(hipMemcpyAsync(hb.data(), bh.p, (size_t)nbk * 8, hipMemcpyDeviceToHost, e->stream));
-    HIPCHK(hipStreamSynchronize(e->stream));
-
-    /* 2. passes: [b0, b1) buckets; dense when one bucket exceeds the cap */
+    /* the pass cap: window keys one sorted pass may hold */
     uint64_t cap = e->sp_pass;
     if (!cap) {
         size_t fr = 0, tot = 0;
@@ -4962,16 +4919,81 @@ static int sparse_finish(fk_engine *e, int32_t seq) {
         cap = fr > margin ? (fr - margin) / 64 : 0;
         cap = std::max<uint64_t>(1u << 20, std::min<uint64_t>(cap, 1ull << 32));
     }
+    /* all windows in one pass (the feed counted them): no histogram launch,
+       the keys pass collects the short walks */
+    const uint64_t wins = e->last.acc[ACC_WIN];
+    const bool single = wins <= cap;
+
+    const bool tail = !e->state.hdr && seq >= 1 && seq < k;
+    const bool nodes = e->opts.want_nodes != 0;
+    uint64_t scap = std::max<uint64_t>(1024, e->keep_len / 64);
+    DevScratch shorts, found;
+    uint64_t ns = 0;
+    /* the collected short walks (+ the input's last run, shorter than k:
+       :1059-1062 at EOF), distinct, with their found flags */
+    auto prep_shorts = [&]() -> int {
+        if (tail) {
+            const uint64_t v = SP_SHORT | ((uint64_t)seq << 40) | fk_sigma(e->state.code & ((1ull << (2 * seq)) - 1));
+            HIPCHK(hipMemcpyAsync(shorts.as<uint64_t>() + ns, &v, sizeof v, hipMemcpyHostToDevice, e->stream));
+            HIPCHK(hipStreamSynchronize(e->stream));
+            ns++;
+        }
+        if (!nodes) ns = 0;
+        if (ns > 1) {   /* nodeCounter counts distinct prefixes: drop repeated walks */
+            uint64_t nu = 0;
+            if (fks_unique(&e->fks, shorts.as<uint64_t>(), ns, e->stream, &nu)) return FK_E_HIP;
+            ns = nu;
+        }
+        if (ns) {
+            if (!found.alloc(ns * 20)) return FK_E_OOM;
+            HIPCHK(hipMemsetAsync(found.p, 0, ns * 20, e->stream));
+        }
+        return FK_OK;
+    };
+
     struct Pass { uint32_t b0, b1; uint64_t n; bool dense; };
     std::vector<Pass> passes;
-    for (uint32_t b = 0; b < nbk;) {
-        if (!hb[b]) { b++; continue; }
-        if (hb[b] > cap) { passes.push_back({b, b + 1, hb[b], true}); b++; continue; }
-        uint32_t b1 = b;
-        uint64_t n = 0;
-        while (b1 < nbk && hb[b1] <= cap && n + hb[b1] <= cap) n += hb[b1++];
-        passes.push_back({b, b1, n, false});
-        b = b1;
+    if (single) {
+        passes.push_back({0, nbk, wins, false});
+    } else {
+        /* 1. bucket histogram and short walks (a second run if the list overflowed) */
+        for (int attempt = 0; attempt < 2; attempt++) {
+            if (!shorts.alloc((scap + 1) * 8)) return FK_E_OOM;
+            HIPCHK(hipMemsetAsync(bh.p, 0, (size_t)nbk * 8, e->stream));
+            HIPCHK(hipMemsetAsync(nctr, 0, 16, e->stream));
+            SpEmit em{};
+            em.mode = SP_HIST;
+            em.shift = shift;
+            em.bhist = bh.as<unsigned long long>();
+            em.nbuckets = nbk;
+            em.shorts = shorts.as<uint64_t>();
+            em.nshort = nctr + 1;
+            em.short_cap = scap;
+            int rc = sp_emit_all(e, em);
+            if (rc) return rc;
+            unsigned long long got = 0;
+            HIPCHK(hipMemcpyAsync(&got, nctr + 1, sizeof got, hipMemcpyDeviceToHost, e->stream));
+            HIPCHK(hipStreamSynchronize(e->stream));
+            ns = got;
+            if (ns <= scap) break;
+            if (attempt) return FK_E_HIP;
+            scap = ns;
+        }
+        int rc = prep_shorts();
+        if (rc) return rc;
+        std::vector<unsigned long long> hb(nbk);
+        HIPCHK(hipMemcpyAsync(hb.data(), bh.p, (size_t)nbk * 8, hipMemcpyDeviceToHost, e->stream));
+        HIPCHK(hipStreamSynchronize(e->stream));
+        /* 2. passes: [b0, b1) buckets; dense when one bucket exceeds the cap */
+        for (uint32_t b = 0; b < nbk;) {
+            if (!hb[b]) { b++; continue; }
+            if (hb[b] > cap) { passes.push_back({b, b + 1, hb[b], true}); b++; continue; }
+            uint32_t b1 = b;
+            uint64_t n = 0;
+            while (b1 < nbk && hb[b1] <= cap && n + hb[b1] <= cap) n += hb[b1++];
+            passes.push_back({b, b1, n, false});
+            b = b1;
+        }
     }
 
     /* 3. the passes */
@@ -4999,17 +5021,31 @@ static int sparse_finish(fk_engine *e, int32_t seq) {
                 keys.release();
                 if (!keys.alloc(std::max<uint64_t>(ps.n, std::min<uint64_t>(cap, 2 * ps.n)) * 8)) return FK_E_OOM;
             }
-            HIPCHK(hipMemsetAsync(nctr, 0, 8, e->stream));
             em.mode = SP_KEYS;
             em.out = keys.as<uint64_t>();
             em.nout = nctr;
             em.out_cap = ps.n;
-            int rc = sp_emit_all(e, em);
-            if (rc) return rc;
-            unsigned long long got = 0;
-            HIPCHK(hipMemcpyAsync(&got, nctr, sizeof got, hipMemcpyDeviceToHost, e->stream));
-            HIPCHK(hipStreamSynchronize(e->stream));
-            if (got != ps.n) return FK_E_HIP;   /* the histogram and the emit pass disagree */
+            unsigned long long got[2] = {0, 0};
+            for (int attempt = 0; attempt < 2; attempt++) {
+                if (single && !shorts.alloc((scap + 1) * 8)) return FK_E_OOM;
+                HIPCHK(hipMemsetAsync(nctr, 0, 16, e->stream));
+                em.shorts = single ? shorts.as<uint64_t>() : nullptr;   /* the single pass collects them */
+                em.nshort = nctr + 1;
+                em.short_cap = scap;
+                int rc = sp_emit_all(e, em);
+                if (rc) return rc;
+                HIPCHK(hipMemcpyAsync(got, nctr, sizeof got, hipMemcpyDeviceToHost, e->stream));
+                HIPCHK(hipStreamSynchronize(e->stream));
+                if (!single || got[1] <= scap) break;
+                if (attempt) return FK_E_HIP;
+                scap = got[1];
+            }
+            if (got[0] != ps.n) return FK_E_HIP;   /* the feed's (or the histogram's) count and the emit pass disagree */
+            if (single) {
+                ns = got[1];
+                int rc = prep_shorts();
+                if (rc) return rc;
+            }
             if (fks_sort_runs(&e->fks, em.out, ps.n, k, e->stream, dacc, &part)) return FK_E_HIP;
         }
         if (part.keys || part.cnts) e->spparts.push_back(part);   /* owned (freed) from here on */

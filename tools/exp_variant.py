@@ -34,6 +34,10 @@ VARIANTS = {
          "    const uint32_t g = blockIdx.x / pg.nslices;\n"
          "    for (uint32_t i = threadIdx.x; i < nb + ns; i += blockDim.x) slice[i] = 0;"),
     ],
+    # k_bucket_count's first loads per quad: rows x 16-B pieces per lane
+    "u4r3": [("#define BUCKET_U 5", "#define BUCKET_U 4"), ("#define BUCKET_ROWS 2", "#define BUCKET_ROWS 3")],
+    "u6": [("#define BUCKET_U 5", "#define BUCKET_U 6")],
+    "u3r4": [("#define BUCKET_U 5", "#define BUCKET_U 3"), ("#define BUCKET_ROWS 2", "#define BUCKET_ROWS 4")],
 }
 
 
