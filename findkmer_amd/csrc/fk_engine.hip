@@ -1877,6 +1877,12 @@ static_assert(PART_MAX_BATCH_W(16u) <= 65536u, "run index words hold 16-bit star
 /* slices of a batch: k = 11 pairs 2^24 / 2^15 (the single k-mers fold into
    them, flagged), k = 12 2^24 / 2^15, k = 13 2^26 / 2^15; k <= 10 at most 128 */
 #define PART_SM(W) ((W) >= 16u ? 2048u : 128u)   /* k = 13: 2^26 / 2^15 slices */
+/* k = 14: 2^28 / 2^16 = 4096 slices of 16-bit codes (k_bucket_count counts a
+   slice as two halves of 2^15 bins, PartGeo::split).  Their run cursors are
+   packed two per word (16 KiB of counts + 8 KiB of cursors + the 128 KiB
+   batch fit the 160 KiB of LDS): a cursor only reaches 2^16 at the batch's
+   very end, where the carry lands on a slice with an empty run. */
+#define PART_BIG 4096u
 /* Measured and not kept (round 3): pairs mode keeping 8 batches' run words
    per slice in LDS and writing them as one 32-B piece (each scattered 4-B word
    costs a ~40-B write-back, 1.6 GB per 10 GB step): k_part 5.54 -> 5.67 ms,
@@ -1909,6 +1915,7 @@ struct PartGeo {
                               before k_part<RES> takes the rest */
     uint32_t stride;       /* index row stride: rows of both regions (k_part, then k_part<RES>) */
     uint32_t *flag;        /* [0] != 0: some range went to k_part<RES>, region 2 holds rows */
+    uint32_t split;        /* k = 14: a slice's 2^16 codes counted as two halves of 2^15 bins (0: one) */
 };
 
 /* Every entry a fast tile's Emit hands to the partition, as f(slice, low).
@@ -1989,7 +1996,7 @@ __device__ __forceinline__ void part_entries(const Emit &em, uint32_t mk, uint32
  * not make the atomic phases cheaper (the atomic instructions' issue, not
  * the banks, sets their cost) and its extra barrier made the batch slower
  * (47.0 K vs 45.7 K cycles), so the scan stays on wave 0. */
-template <bool PAIRS, bool MIX, uint32_t W>
+template <bool PAIRS, bool MIX, uint32_t W, uint32_t SM>
 __device__ __forceinline__ bool part_batch(const Ctx &cx, const PartGeo &pg, const Emit *es, const bool *haves,
                                            bool more, uint32_t row, uint32_t *hist,
                                            uint32_t *cur, uint32_t *total, uint16_t *ent, uint32_t *scr) {
@@ -2018,9 +2025,15 @@ __device__ __forceinline__ bool part_batch(const Ctx &cx, const PartGeo &pg, con
         const uint32_t off = wsum32(lane < wv ? scr[lane] : 0u);
         const uint32_t inc = wscan_incl32(mine);
         uint32_t run = off + inc - mine;
+        uint32_t lo16 = 0;
         for (uint32_t j = 0; j < ppl; j++) {
             const uint32_t b = b0 + j, c = hist[b];
-            cur[b] = run;
+            if (SM > 2048u) {   /* packed cursors (b0 and ppl are even) */
+                if ((b & 1u) == 0) lo16 = run & 0xFFFFu;
+                else cur[b >> 1] = lo16 | (run << 16);
+            } else {
+                cur[b] = run;
+            }
             pg.idx[(size_t)b * pg.stride + row] = run_word(run, c);
             hist[b] = 0;
             run += c;
@@ -2052,7 +2065,13 @@ __device__ __forceinline__ bool part_batch(const Ctx &cx, const PartGeo &pg, con
        Emit words (laundered, so the compiler cannot keep phase 1's codes
        live across the barriers: that costs more VGPRs than it saves VALU) */
     auto place = [&](uint32_t b, uint32_t low) {
-        const uint32_t p = atomicAdd(&cur[b], 1u);
+        uint32_t p;
+        if (SM > 2048u) {
+            const uint32_t h = (b & 1u) * 16u;
+            p = (atomicAdd(&cur[b >> 1], 1u << h) >> h) & 0xFFFFu;
+        } else {
+            p = atomicAdd(&cur[b], 1u);
+        }
         ent[p] = (uint16_t)low;
     };
 #pragma unroll
@@ -2079,12 +2098,12 @@ __device__ __forceinline__ bool part_batch(const Ctx &cx, const PartGeo &pg, con
  * the rest of it, each tile fast, mixed (the masked entries of tile_mixed)
  * or general.  Two kernels: tile_mixed's registers stay out of the main
  * pass.  k_part<RES> returns at once unless some range stopped. */
-template <bool PAIRS, bool RES, uint32_t W>
+template <bool PAIRS, bool RES, uint32_t W, uint32_t SM = PART_SM(W)>
 __global__ void __launch_bounds__(PART_BLOCK_W(W), 4) /* 4 waves per SIMD (<= 128 VGPRs): 16 waves per CU */
 k_part(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint32_t *table,
        uint32_t *shortcnt, unsigned long long *acc, DevRes *res, RangeRec *rr, uint64_t nchunks, uint64_t cpw,
        const XState *d_init, int has_init, PartGeo pg, ResumeRec *resume, const XState *exact) {
-    __shared__ uint32_t hist[PART_SM(W)], cur[PART_SM(W)], total, scr[W];
+    __shared__ uint32_t hist[SM], cur[SM > 2048u ? SM / 2u : SM], total, scr[W];
     __shared__ __attribute__((aligned(16))) uint16_t ent[PART_MAX_BATCH_W(W)];
     if (RES && *(volatile uint32_t *)pg.flag == 0) return;   /* uniform: no range stopped */
     /* open the feed's result block (the kernels after this one accumulate
@@ -2211,7 +2230,7 @@ k_part(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint
                 have_stash[i_] = have;                                               \
             }                                                                        \
             if (ph_ == NT - 1) {                                                     \
-                const bool more_ = part_batch<PAIRS, RES, W>(cx, pg, stash, have_stash, !done, \
+                const bool more_ = part_batch<PAIRS, RES, W, SM>(cx, pg, stash, have_stash, !done, \
                                                           row0 + round / NT, hist, cur, &total, ent, scr); \
                 if (!more_ || round / NT + 1 >= pg.rounds) { round++; break; }       \
             }                                                                        \
@@ -2291,16 +2310,21 @@ k_part(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint
 __global__ void __launch_bounds__(1024)
 k_bucket_count(PartGeo pg, uint32_t groups, uint32_t *table) {
     extern __shared__ uint32_t slice[];
-    const uint32_t nb = 1u << pg.sh;
+    const uint32_t binsh = pg.split ? pg.sh - 1u : pg.sh;
+    const uint32_t nb = 1u << binsh;
     /* pairs mode: the slice's 2^sh pair bins, then the 2^(sh-2) bins of the
        single k-mers filed under it (PART_SINGLE codes) */
     const uint32_t ns = pg.pairs ? nb >> 2 : 0u;
     /* consecutive slices on one XCD (blocks b, b + 8, .. share an XCD): the
        128-B line two neighbouring runs of a row share is fetched once into
        that XCD's L2 (k=11: 1 GB step 1.085 -> 1.065 ms, 10 GB 8.10 -> 8.04) */
-    const uint32_t b = groups == 1 && (pg.nslices & 7u) == 0 ? (blockIdx.x & 7u) * (pg.nslices >> 3) + (blockIdx.x >> 3)
-                                                           : blockIdx.x % pg.nslices;
-    const uint32_t g = blockIdx.x / pg.nslices;
+    /* k = 14 (split): the two halves of a slice on one XCD, 8 blocks apart
+       (the second reads the slice's codes from L2) */
+    const uint32_t half = pg.split ? (blockIdx.x >> 3) & 1u : 0u;
+    const uint32_t bx = pg.split ? (blockIdx.x & 7u) | ((blockIdx.x >> 4) << 3) : blockIdx.x;
+    const uint32_t b = groups == 1 && (pg.nslices & 7u) == 0 ? (bx & 7u) * (pg.nslices >> 3) + (bx >> 3)
+                                                           : bx % pg.nslices;
+    const uint32_t g = bx / pg.nslices;
     for (uint32_t i = threadIdx.x; i < nb + ns; i += blockDim.x) slice[i] = 0;
     __syncthreads();
     const uint32_t *ix = pg.idx + (size_t)b * pg.stride;
@@ -2321,6 +2345,10 @@ k_bucket_count(PartGeo pg, uint32_t groups, uint32_t *table) {
         for (int h = 0; h < 8; h++) {
             const uint64_t at = q * 8 + h;
             const uint32_t c = (w4[h >> 1] >> (16 * (h & 1))) & 0xFFFFu;
+            if (pg.split) {   /* k = 14: this block's half of the slice */
+                if (at >= s0 && at < s1 && (c >> binsh) == half) atomicAdd(&slice[c & (nb - 1u)], 1u);
+                continue;
+            }
             const uint32_t a = c & PART_SINGLE ? nb + ((c & ~PART_SINGLE) >> 2) : c;
             if (at >= s0 && at < s1) atomicAdd(&slice[a], 1u);
         }
@@ -2379,7 +2407,7 @@ k_bucket_count(PartGeo pg, uint32_t groups, uint32_t *table) {
     for (uint32_t i = threadIdx.x; i < nb; i += blockDim.x) {
         const uint32_t v = slice[i];
         if (!v) continue;
-        uint32_t *dst = &table[fk_sigma(((uint64_t)b << pg.sh) | i)];
+        uint32_t *dst = &table[fk_sigma(((uint64_t)b << pg.sh) | ((uint64_t)half << binsh) | i)];
         if (groups == 1) *dst += v;   /* this block owns the slice */
         else atomicAdd(dst, v);
     }
@@ -3422,7 +3450,7 @@ extern "C" int fk_engine_create(int k, const fk_opts *opts, fk_engine **out) {
     if (e->opts.timing_every > 1) e->timing_every = (uint32_t)e->opts.timing_every;
     e->sparse = k > FK_K_MAX_DENSE;
     e->nbins = e->sparse ? 0 : 1ull << (2 * k);
-    e->part = k >= 8 && k <= 13;
+    e->part = k >= 8 && k <= 14;
     e->maskk = (1ull << (2 * k)) - 1;
     e->nshort = k > 1 && !e->sparse ? ((1ull << (2 * k)) - 4) / 3 : 0;
     if (e->opts.stream) {
@@ -3746,7 +3774,10 @@ static int launch_part(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t l
        the single k-mers at the first slot of halves with a '\n' */
     const bool pairs = k <= e->part_pairs_kmax;
     const int kb = pairs ? k + 1 : k;                      /* bits of a pair (or window) code: 2 kb */
-    pg.sh = std::min(15, 2 * kb - 6);                      /* >= 64 slices, <= 2^15 bins (128 KiB) each */
+    /* >= 64 slices, <= 2^15 bins (128 KiB) each; k = 14: 2^16 codes per slice,
+       counted as two halves (PART_BIG) */
+    pg.sh = k == 14 ? 16 : std::min(15, 2 * kb - 6);
+    pg.split = k == 14 ? 1u : 0u;
     pg.npair = pairs ? 1u << (2 * kb - pg.sh) : 0u;
     pg.nslices = pairs ? pg.npair : 1u << (2 * k - pg.sh);   /* singles fold into the pair slices */
     pg.pairs = pg.singles = nullptr;
@@ -3795,15 +3826,17 @@ static int launch_part(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t l
     }
     pg.codes = e->d_codes;
     pg.idx = e->d_pidx;
-    auto kmain = W == 16u ? (pairs ? k_part<true, false, 16u> : k_part<false, false, 16u>)
-                          : (pairs ? k_part<true, false, 8u> : k_part<false, false, 8u>);
+    auto kmain = pg.split ? k_part<false, false, 16u, PART_BIG>
+                 : W == 16u ? (pairs ? k_part<true, false, 16u> : k_part<false, false, 16u>)
+                            : (pairs ? k_part<true, false, 8u> : k_part<false, false, 8u>);
     hipExtLaunchKernelGGL(kmain, dim3(pgrid), dim3(PART_BLOCK_W(W)), 0, e->stream, tev(e, 0), tev(e, 1), 0, buf, len,
                           lo, e->k, e->maskk, e->d_table, e->d_short, e->d_facc, e->d_res, e->d_rr, g.nchunks, g.cpw,
                           e->d_state, has_init, pg, e->d_resume, exact);
     HIPCHK(hipGetLastError());
     if (mixed) {
-        auto kres = W == 16u ? (pairs ? k_part<true, true, 16u> : k_part<false, true, 16u>)
-                             : (pairs ? k_part<true, true, 8u> : k_part<false, true, 8u>);
+        auto kres = pg.split ? k_part<false, true, 16u, PART_BIG>
+                    : W == 16u ? (pairs ? k_part<true, true, 16u> : k_part<false, true, 16u>)
+                               : (pairs ? k_part<true, true, 8u> : k_part<false, true, 8u>);
         hipLaunchKernelGGL(kres, dim3(pgrid), dim3(PART_BLOCK_W(W)), 0, e->stream, buf, len, lo, e->k, e->maskk,
                            e->d_table, e->d_short, e->d_facc, e->d_res, e->d_rr, g.nchunks, g.cpw, e->d_state,
                            has_init, pg, e->d_resume, exact);
@@ -3813,9 +3846,9 @@ static int launch_part(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t l
     }
     const uint32_t groups = std::max<uint32_t>(1, (uint32_t)e->cus / pg.nslices);
     if (pairs && groups > 1) HIPCHK(hipMemsetAsync(e->d_pairs, 0, e->nbins * 5 * sizeof(uint32_t), e->stream));
-    const size_t bc_lds = ((size_t)1 << pg.sh) * sizeof(uint32_t) * (pairs ? 5 : 4) / 4;   /* + single bins */
-    hipLaunchKernelGGL(k_bucket_count, dim3(pg.nslices * groups), dim3(1024), bc_lds, e->stream, pg, groups,
-                       e->d_table);
+    const size_t bc_lds = ((size_t)1 << (pg.sh - pg.split)) * sizeof(uint32_t) * (pairs ? 5 : 4) / 4;   /* + single bins */
+    hipLaunchKernelGGL(k_bucket_count, dim3(pg.nslices * groups << pg.split), dim3(1024), bc_lds, e->stream, pg,
+                       groups, e->d_table);
     HIPCHK(hipGetLastError());
     if (pairs) {
         const unsigned fg = (unsigned)std::min<uint64_t>((uint64_t)e->cus * 4, (e->nbins + 255) / 256);
@@ -4104,7 +4137,7 @@ static int sp_grow(fk_engine *e, void **buf, uint64_t *cap, uint64_t used, uint6
 /* keep a counted segment's bytes and its ranges' exact entering states
    (d_rtrue from the feed's k_scan) for finish's key-range passes */
 static int sp_retain(fk_engine *e, const uint8_t *dbuf, uint64_t len, const Geo &g) {
-    int rc = sp_grow(e, (void **)&e->d_keep, &e->keep_cap, e->keep_len, e->keep_len + len + FK_TILE_BYTES);
+    int rc = sp_grow(e, (void **)&e->d_keep, &e->keep_cap, e->keep_len, e->keep_len + len + 16);
     if (rc) return rc;
     const uint64_t sb = g.nranges * sizeof(XState);
     rc = sp_grow(e, (void **)&e->d_kst, &e->kst_cap, e->kst_len * sizeof(XState), (e->kst_len + g.nranges) * sizeof(XState));
@@ -4112,8 +4145,9 @@ static int sp_retain(fk_engine *e, const uint8_t *dbuf, uint64_t len, const Geo 
     HIPCHK(hipMemcpyAsync(e->d_keep + e->keep_len, dbuf, len, hipMemcpyDeviceToDevice, e->stream));
     HIPCHK(hipMemcpyAsync(e->d_kst + e->kst_len, e->d_rtrue, sb, hipMemcpyDeviceToDevice, e->stream));
     e->spsegs.push_back({e->keep_len, len, e->kst_len, g.nranges, g.cpw, g.nchunks});
-    /* segments start tile-aligned in d_keep (the emit kernel's loads) */
-    e->keep_len += (len + FK_TILE_BYTES - 1) / FK_TILE_BYTES * FK_TILE_BYTES;
+    /* segments start 16-B aligned in d_keep (load_lane's vector loads; it
+       never reads past a segment's end), so small feeds cost little */
+    e->keep_len += (len + 15) / 16 * 16;
     e->kst_len += g.nranges;
     return FK_OK;
 }

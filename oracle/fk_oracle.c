@@ -184,7 +184,7 @@ static uint64_t dense_nodes(const uint32_t *counts, int k, const short_list *s,
 
 int fko_count_dense(const uint8_t *buf, uint64_t len, int k, uint32_t *counts,
                     fko_result *res, uint8_t *unknown_out, uint64_t unknown_cap) {
-    if (k < 1 || k > 13) return -1;
+    if (k < 1 || k > 14) return -1;   /* (k = 14: a 1 GiB table; larger k: fko_count_sparse) */
     uint64_t n = 1ull << (2 * k);
     memset(counts, 0, n * sizeof(uint32_t));
     dense_ctx ctx = { counts };
@@ -326,7 +326,7 @@ static void *sum_run(void *arg) {
 
 int fko_count_dense_par(const uint8_t *buf, uint64_t len, int k, uint32_t *counts,
                         fko_result *res, uint8_t *unknown_out, uint64_t unknown_cap, int threads) {
-    if (k < 1 || k > 13) return -1;
+    if (k < 1 || k > 13) return -1;   /* (one table per thread) */
     if (threads < 1) threads = 1;
     if ((uint64_t)threads > len / 4096 + 1) threads = (int)(len / 4096 + 1);
     if (threads == 1) return fko_count_dense(buf, len, k, counts, res, unknown_out, unknown_cap);

@@ -608,6 +608,34 @@ def test_partition_skewed(k, kind):
     assert_same(data, k, want_nodes=False)
 
 
+@pytest.mark.parametrize("kind", ["mixed", "dense_records", "polyA", "fasta_polyA", "polyA_C", "acgt_feeds"])
+def test_partition_k14(kind):
+    """k = 14 through the partition: 4096 slices of 16-bit codes whose run
+    cursors are packed two per LDS word, each slice counted by two
+    k_bucket_count blocks (one per half of its 2^16 bins).  A poly-A batch
+    puts all 64 K entries into slice 0 (the packed cursor reaching 2^16 at
+    the batch's end), polyA_C two adjacent bins past 2^16 counts; headers
+    every few hundred bytes send ranges to k_part<RES>; 1 GiB of oracle
+    table, compared whole"""
+    n = 12 << 20
+    feeds = None
+    if kind == "mixed":
+        data = mixed_input(1414, n)
+    elif kind == "dense_records":
+        data = _dense_records(1415, n)
+    elif kind == "polyA":
+        data = b"A" * n
+    elif kind == "polyA_C":
+        data = ((b"A" * 30 + b"C") * (n // 31 + 1))[:n]
+    elif kind == "fasta_polyA":
+        line = b"A" * 60 + b"\n"
+        data = b">x\n" + line * (n // len(line))
+    else:
+        data = oracle.synth(n, 14, 80).tobytes()
+        feeds = [1_000_003, 17, 65_536, len(data) - 1_065_556]
+    assert_same(data, 14, want_nodes=kind != "polyA", feeds=feeds)
+
+
 def _long_header_input(seed, n):
     """ACGT runs with '>' lines longer than the 256-byte halo, so ranges
     start inside a header their halo cannot see the start of (the one-pass

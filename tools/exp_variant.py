@@ -38,6 +38,12 @@ VARIANTS = {
     "u4r3": [("#define BUCKET_U 5", "#define BUCKET_U 4"), ("#define BUCKET_ROWS 2", "#define BUCKET_ROWS 3")],
     "u6": [("#define BUCKET_U 5", "#define BUCKET_U 6")],
     "u3r4": [("#define BUCKET_U 5", "#define BUCKET_U 3"), ("#define BUCKET_ROWS 2", "#define BUCKET_ROWS 4")],
+    # k_bucket_count without the XCD-aware slice order
+    "noxcd": [
+        ("    const uint32_t b = groups == 1 && (pg.nslices & 7u) == 0 ? (bx & 7u) * (pg.nslices >> 3) + (bx >> 3)\n"
+         "                                                           : bx % pg.nslices;",
+         "    const uint32_t b = bx % pg.nslices;"),
+    ],
 }
 
 
