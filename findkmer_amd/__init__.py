@@ -118,6 +118,7 @@ SIGNATURES = [
     ("fk_engine_progress", ctypes.c_int, [_P, _U64P, _U64P]),
     ("fk_engine_merge_from", ctypes.c_int, [_P, _P]),
     ("fk_engine_unknown", ctypes.c_int, [_P, _U8P, ctypes.c_uint64, _U64P]),
+    ("fk_engine_unknown_since", ctypes.c_int, [_P, ctypes.c_uint64, _U8P, _U64P, ctypes.c_uint64, _U64P]),
     ("fk_engine_sparse", ctypes.c_int, [_P, _U64P, _U32P, ctypes.c_uint64, _U64P]),
     ("fk_engine_sparse_device", ctypes.c_int, [_P, _P, _P, ctypes.c_uint64, _U64P]),
     ("fk_engine_sparse_split", ctypes.c_int, [_P, ctypes.c_int, _U64P]),
@@ -207,7 +208,8 @@ class Engine:
         o = FkOpts()
         o.device = device
         o.want_nodes = 1 if want_nodes else 0
-        o.collect_unknown = 1 if collect_unknown else 0
+        # collect_unknown: True/1 = the bytes, 2 = also their stream offsets (unknown_positions)
+        o.collect_unknown = int(collect_unknown) if collect_unknown else 0
         o.stream = stream
         o.timing_every = int(timing_every)
         h = ctypes.c_void_p()
@@ -349,6 +351,16 @@ class Engine:
         st = (ctypes.c_uint64 * 2)()
         _check(lib().fk_engine_sparse_adopt(self.h, keys_ptr, counts_ptr, n, st), "sparse_adopt")
         return int(st[0]), int(st[1])
+
+    def unknown_positions(self):
+        """collect_unknown=2: the stream offset of every unknown byte, in order"""
+        import numpy as np
+        n = ctypes.c_uint64()
+        _check(lib().fk_engine_unknown_since(self.h, 0, None, None, 0, ctypes.byref(n)), "unknown_since")
+        pos = np.zeros(max(1, n.value), dtype=np.uint64)
+        _check(lib().fk_engine_unknown_since(self.h, 0, None, pos.ctypes.data_as(_U64P), n.value, ctypes.byref(n)),
+               "unknown_since")
+        return pos[: n.value]
 
     def unknown_bytes(self):
         n = ctypes.c_uint64()

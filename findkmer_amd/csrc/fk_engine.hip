@@ -2977,7 +2977,7 @@ __device__ __forceinline__ uint32_t lane_hdr_entry(const uint32_t w[4], int nb, 
  */
 __global__ void __launch_bounds__(FK_BLOCK)
 k_extract(const uint8_t *buf, uint64_t len, int64_t lo, const RangeRec *rr, const XState *rtrue,
-          const uint32_t *list, const uint64_t *offs, uint32_t nlist, uint8_t *out) {
+          const uint32_t *list, const uint64_t *offs, uint32_t nlist, uint8_t *out, uint64_t *opos) {
     const int lane = threadIdx.x & 63;
     Ctx cx{buf, len, lo, nullptr, nullptr, nullptr, nullptr, nullptr, 0, 0, 0};
     const uint64_t wave = blockIdx.x * FK_WAVES_PER_BLOCK + wave_in_block();
@@ -3018,7 +3018,10 @@ k_extract(const uint8_t *buf, uint64_t len, int64_t lo, const RangeRec *rr, cons
                     uint32_t ch = fk_byte(w, j);
                     if (h) { if (ch == '\n') h = 0; }
                     else if (ch == '>') h = 1;
-                    else if (ch != '\n' && ch != 'N' && ch != 0xFFu && fk_sym(ch) < 0) out[o++] = (uint8_t)ch;
+                    else if (ch != '\n' && ch != 'N' && ch != 0xFFu && fk_sym(ch) < 0) {
+                        if (opos) opos[o] = (uint64_t)(toff + lane * 16 + j);   /* (collect_unknown = 2) */
+                        out[o++] = (uint8_t)ch;
+                    }
                 }
             }
             base += rdlane(incl, 63);
@@ -3220,6 +3223,7 @@ struct fk_engine {
     uint32_t timing_every = 1;
     bool cur_timed = true;                    /* the current feed's launches record events */
     std::vector<uint8_t> unknown_bytes;
+    std::vector<uint64_t> unknown_pos;        /* collect_unknown = 2: their stream offsets */
     /* partitioned path near the reference's int32 seqSize zone: a segment
        whose guessed range states are mostly wrong is recounted from the exact
        states instead of cancelled range by range (resolve_and_fetch) */
@@ -3347,6 +3351,7 @@ static int zero_all(fk_engine *e) {
     sp_parts_free(e);
     e->sp_done = false;
     e->unknown_bytes.clear();
+    e->unknown_pos.clear();
     return FK_OK;
 }
 
@@ -3977,8 +3982,10 @@ static int collect_unknown(fk_engine *e, const uint8_t *dbuf, uint64_t len, int6
     for (uint64_t r = 0; r < g.nranges; r++)
         if (rr[(size_t)r].unknown) { list.push_back((uint32_t)r); offs.push_back(acc); acc += rr[(size_t)r].unknown; }
     if (!acc) return FK_OK;
-    DevScratch s_list, s_offs, s_out;
+    DevScratch s_list, s_offs, s_out, s_pos;
     if (!s_list.alloc(list.size() * 4) || !s_offs.alloc(offs.size() * 8) || !s_out.alloc(acc)) return FK_E_OOM;
+    const bool want_pos = e->opts.collect_unknown == 2;
+    if (want_pos && !s_pos.alloc(acc * 8)) return FK_E_OOM;
     uint32_t *d_list = s_list.as<uint32_t>();
     uint64_t *d_offs = s_offs.as<uint64_t>();
     uint8_t *d_out = s_out.as<uint8_t>();
@@ -3986,12 +3993,22 @@ static int collect_unknown(fk_engine *e, const uint8_t *dbuf, uint64_t len, int6
     HIPCHK(hipMemcpyAsync(d_offs, offs.data(), offs.size() * 8, hipMemcpyHostToDevice, e->stream));
     unsigned gx = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((list.size() + 7) / 8, (uint64_t)e->cus * 2));
     hipLaunchKernelGGL(k_extract, dim3(gx), dim3(FK_BLOCK), 0, e->stream, dbuf, len, lo, e->d_rr, e->d_rtrue, d_list,
-                       d_offs, (uint32_t)list.size(), d_out);
+                       d_offs, (uint32_t)list.size(), d_out, want_pos ? s_pos.as<uint64_t>() : nullptr);
     HIPCHK(hipGetLastError());
     size_t old = e->unknown_bytes.size();
     e->unknown_bytes.resize(old + acc);
     HIPCHK(hipMemcpyAsync(e->unknown_bytes.data() + old, d_out, acc, hipMemcpyDeviceToHost, e->stream));
+    if (want_pos) {
+        e->unknown_pos.resize(old + acc);
+        HIPCHK(hipMemcpyAsync(e->unknown_pos.data() + old, s_pos.p, acc * 8, hipMemcpyDeviceToHost, e->stream));
+    }
     HIPCHK(hipStreamSynchronize(e->stream));
+    if (want_pos) {
+        /* buffer offsets -> stream offsets: every caller has just added this
+           segment's `len` bytes to e->scanned */
+        const uint64_t seg0 = e->scanned - len;
+        for (size_t i = old; i < old + acc; i++) e->unknown_pos[i] += seg0;
+    }
     return FK_OK;
 }
 
@@ -5404,6 +5421,20 @@ extern "C" int fk_engine_unknown(fk_engine *e, uint8_t *out, uint64_t cap, uint6
     return FK_OK;
 }
 
+/* The unknown bytes from index `first` on (stream order) and, with
+   collect_unknown = 2, their stream offsets; *n receives the total so far. */
+extern "C" int fk_engine_unknown_since(fk_engine *e, uint64_t first, uint8_t *out, uint64_t *pos, uint64_t cap,
+                                       uint64_t *n) {
+    if (!e || !n) return FK_E_INVALID;
+    if (pos && e->opts.collect_unknown != 2) return FK_E_STATE;
+    *n = e->unknown_bytes.size();
+    if (first >= *n) return FK_OK;
+    const uint64_t m = std::min<uint64_t>(cap, *n - first);
+    if (out) memcpy(out, e->unknown_bytes.data() + first, m);
+    if (pos) memcpy(pos, e->unknown_pos.data() + first, m * sizeof(uint64_t));
+    return FK_OK;
+}
+
 __global__ void k_add_tables(uint32_t *dst, const uint32_t *src, uint64_t n) {
     for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
         dst[i] += src[i];
@@ -5441,6 +5472,7 @@ extern "C" int fk_engine_merge_from(fk_engine *dst, fk_engine *src) {
     HIPCHK(hipStreamSynchronize(dst->stream));
     dst->stats_valid = false;
     dst->unknown_bytes.insert(dst->unknown_bytes.end(), src->unknown_bytes.begin(), src->unknown_bytes.end());
+    dst->unknown_pos.insert(dst->unknown_pos.end(), src->unknown_pos.begin(), src->unknown_pos.end());   /* (shard-relative) */
     dst->chunks += src->chunks;
     dst->redo += src->redo;
     dst->dev_ms += src->dev_ms;

@@ -298,6 +298,29 @@ static void die_engine(int rc) {
     exit(EXIT_FAILURE);
 }
 
+/* "Unknown character" warnings (:582-584) of the unknown bytes not yet
+   printed, in stream order; by_pos: only those before stream offset `limit`
+   (the engine collects their offsets, collect_unknown = 2).  The reference
+   prints them during its scan, between the -q 0 progress lines (:997). */
+static uint64_t g_unk_done = 0;
+static void flush_unknown(fk_engine *e, uint64_t limit, bool by_pos) {
+    uint64_t n = 0;
+    if (fk_engine_unknown_since(e, g_unk_done, nullptr, nullptr, 0, &n)) return;
+    std::vector<uint8_t> u;
+    std::vector<uint64_t> p;
+    while (g_unk_done < n) {
+        const uint64_t m = std::min<uint64_t>(n - g_unk_done, 1u << 16);
+        u.resize((size_t)m);
+        p.resize(by_pos ? (size_t)m : 0);
+        if (fk_engine_unknown_since(e, g_unk_done, u.data(), by_pos ? p.data() : nullptr, m, &n)) return;
+        for (uint64_t i = 0; i < m; i++) {
+            if (by_pos && p[(size_t)i] >= limit) return;
+            fprintf(stderr, "Unknown character %c processed! File may be corrupted.\n", (char)u[(size_t)i]);
+            g_unk_done++;
+        }
+    }
+}
+
 /*
  * Drive the engine over the whole file.  With quiet == 0 the reference prints
  * "Read %llu bases\n>" + the header line at every '>' that starts a comment
@@ -352,6 +375,7 @@ static int scan_file(fk_engine *e, FILE *f, fk_result *res, bool echo = true) {
             uint64_t vb = 0;
             rc = fk_engine_progress(e, &vb, nullptr);
             if (rc) return rc;
+            flush_unknown(e, 0, false);   /* the warnings of the bytes before this '>' */
             fprintf(stdout, "Read %llu bases\n%c", (unsigned long long)vb, '>');   /* :997 */
             rc = fk_engine_feed(e, buf.data() + q, 1, 0);
             if (rc) return rc;
@@ -363,15 +387,23 @@ static int scan_file(fk_engine *e, FILE *f, fk_result *res, bool echo = true) {
 }
 
 /* -q 0 on a device-resident file: the progress lines of every comment line
-   (:996-1002) come from fk_input_headers, the header text from the file.
-   Returns FK_E_STATE when the file needs the streamed path. */
-static int print_progress(int k) {
+   (:996-1002) come from fk_input_headers (load_headers; FK_E_STATE when the
+   file needs the streamed path), the header text from the file; after the
+   scan, the unknown-character warnings go between them in stream order. */
+static int load_headers(int k, std::vector<uint64_t> &pos, std::vector<uint64_t> &bases) {
     uint64_t n = 0;
     int rc = fk_input_headers(g_input, k, nullptr, nullptr, 0, &n);
     if (rc) return rc;
-    std::vector<uint64_t> pos((size_t)n + 1), bases((size_t)n + 1);
+    pos.assign((size_t)n + 1, 0);
+    bases.assign((size_t)n + 1, 0);
     rc = fk_input_headers(g_input, k, pos.data(), bases.data(), n, &n);
-    if (rc) return rc;
+    pos.resize((size_t)n);
+    bases.resize((size_t)n);
+    return rc;
+}
+
+static int print_progress(fk_engine *eng, const std::vector<uint64_t> &pos, const std::vector<uint64_t> &bases) {
+    const uint64_t n = pos.size();
     /* the header text from a read-only mapping of the file */
     const int fd = fileno(config.sequence_file_pointer);
     struct stat sb;
@@ -385,6 +417,7 @@ static int print_progress(int k) {
         m = static_cast<const uint8_t *>(p);
     }
     for (uint64_t i = 0; i < n; i++) {
+        flush_unknown(eng, pos[(size_t)i], true);
         fprintf(stdout, "Read %llu bases\n%c", (unsigned long long)bases[(size_t)i], '>');   /* :997 */
         const size_t b = (size_t)pos[(size_t)i] + 1;
         const uint8_t *e = b < size ? static_cast<const uint8_t *>(memchr(m + b, '\n', size - b)) : nullptr;
@@ -416,7 +449,10 @@ static int run_k(int argc) {
     fprintf(stdout, "!!!Find The KMER!!!\n");
     fprintf(stdout, "Reading sequence from file\n");
     fprintf(stdout, "     2858658142 bases in the reference genome FYI.\nThat is 2,858,658,142 by the way.\n");
-    fflush(stdout);
+    /* (no flush here: the reference's stdout stays buffered through its scan,
+       and its "Unknown character" warnings (stderr) land between the
+       buffered blocks exactly where ours do -- the same bytes, flushed at
+       the same points) */
 
     /* empty-file check (:982-985) */
     int c0 = fgetc(config.sequence_file_pointer);
@@ -460,21 +496,22 @@ static int run_k(int argc) {
     }
     phase(config.k, "ingest", tp);
     bool on_device = g_input != nullptr;
-    bool echoed = false;   /* the -q 0 progress lines are already printed */
-    if (on_device && config.suppressOutputEnable == 0) {
-        /* -q 0: the per-record progress lines, from the device copy */
-        int prc = print_progress(config.k);
-        if (prc == FK_E_STATE) on_device = false;   /* 0xFF / int32 zone: the streamed path prints them */
+    /* -q 0: the per-record progress lines, from the device copy */
+    bool progress = on_device && config.suppressOutputEnable == 0;
+    std::vector<uint64_t> hpos, hbases;
+    if (progress) {
+        int prc = load_headers(config.k, hpos, hbases);
+        if (prc == FK_E_STATE) on_device = progress = false;   /* 0xFF / int32 zone: the streamed path prints them */
         else if (prc) die_engine(prc);
-        else echoed = true;
     }
+    g_unk_done = 0;
 
     fk_opts opts;
     memset(&opts, 0, sizeof opts);
     opts.device = g_device;
     if (on_device) fk_input_info(g_input, nullptr, nullptr, &opts.device, nullptr);
     opts.want_nodes = 1;
-    opts.collect_unknown = 1;
+    opts.collect_unknown = progress ? 2 : 1;   /* 2: with their offsets, to interleave */
     fk_engine *eng = nullptr;
     int rc = fk_engine_create(config.k, &opts, &eng);
     if (rc) die_engine(rc);
@@ -492,8 +529,16 @@ static int run_k(int argc) {
         rc = fk_engine_reset(eng);
         if (rc) die_engine(rc);
         rewind(config.sequence_file_pointer);
-        rc = scan_file(eng, config.sequence_file_pointer, &res, !echoed);
+        rc = scan_file(eng, config.sequence_file_pointer, &res);
+        progress = false;   /* the streamed path printed them */
     }
+    if (progress && (rc == FK_OK || rc == FK_E_ROLLOVER || rc == FK_E_UNTERMINATED_HEADER)) {
+        const int prc = print_progress(eng, hpos, hbases);
+        if (prc) die_engine(prc);
+    }
+    /* the "Unknown character" warnings not printed yet (:582-584): after the
+       last progress line, in stream order */
+    flush_unknown(eng, 0, false);
     if (rc == FK_E_ROLLOVER) {                                       /* :642-648 */
         const char *m = "\n\n!!! COUNTER ROLLOVER DETECTED! \nIncrease the number of bits used for the counter variable if you have the source code, else use a smaller sequence file.\n\n";
         fprintf(stderr, "%s", m);
@@ -505,15 +550,6 @@ static int run_k(int argc) {
         exit(EXIT_FAILURE);
     }
     if (rc != FK_OK && rc != FK_E_EMPTY) die_engine(rc);
-    /* "Unknown character" warnings (:582-584), in stream order */
-    if (res.unknown_chars) {
-        uint64_t n = 0;
-        fk_engine_unknown(eng, nullptr, 0, &n);
-        std::vector<uint8_t> u((size_t)n);
-        if (n) fk_engine_unknown(eng, u.data(), n, &n);
-        for (uint64_t i = 0; i < n; i++)
-            fprintf(stderr, "Unknown character %c processed! File may be corrupted.\n", (char)u[(size_t)i]);
-    }
 
     std::string stats_name = std::to_string(config.k) + "mer_Base_Stats_Of_" + config.sequence_file + ".txt";
     double prob[4];

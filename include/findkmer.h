@@ -107,7 +107,8 @@ typedef struct {
     void   *stream;           /* hipStream_t to use; NULL = an engine-owned
                                  blocking stream (orders after the device's
                                  legacy default stream) */
-    int32_t collect_unknown;  /* keep the unknown bytes for stderr replay */
+    int32_t collect_unknown;  /* keep the unknown bytes for stderr replay (2: and
+                                 their stream offsets, fk_engine_unknown_since) */
     int32_t timing_every;     /* time the count kernel with HIP events on every
                                  Nth launch (0 or 1: every launch) */
     int32_t reserved[6];
@@ -280,6 +281,13 @@ int  fk_engine_merge_from(fk_engine *dst, fk_engine *src);
 /* Unknown bytes in stream order (collect_unknown=1): *n receives the number
  * available; copies min(cap, n). */
 int  fk_engine_unknown(fk_engine *e, uint8_t *out, uint64_t cap, uint64_t *n);
+/* The unknown bytes from index `first` on, at most cap of them, and (opts
+ * collect_unknown = 2 only, else FK_E_STATE; pos may be NULL) their stream
+ * offsets -- what a caller needs to print the warnings between the -q 0
+ * progress lines in stream order, as the reference does (:582-584 during
+ * the scan at :997).  *n receives the total so far. */
+int  fk_engine_unknown_since(fk_engine *e, uint64_t first, uint8_t *out, uint64_t *pos, uint64_t cap,
+                             uint64_t *n);
 
 /* 17 <= k <= 20 (the reference's k limit, :438): the table is sparse.  After
  * fk_engine_finish, the distinct k-mer indices in ascending order (= the

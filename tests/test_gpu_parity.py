@@ -540,6 +540,89 @@ def test_cli_q0_progress_device_vs_stream(k, tmp_path):
         assert (a / f).read_bytes() == (b / f).read_bytes(), f
 
 
+def _unknown_positions(data):
+    """stream offsets of the bytes the reference warns about (:582-584): not
+    A/C/G/T/N/'\n', outside '>' lines, before the first 0xFF outside one (:988)"""
+    out, hdr = [], False
+    for i, c in enumerate(data):
+        if hdr:
+            hdr = c != 10
+            continue
+        if c == 0x3E:
+            hdr = True
+        elif c == 0xFF:
+            break
+        elif c not in b"ACGTN\n":
+            out.append(i)
+    return out
+
+
+def _unknown_records(seed, nrec):
+    """FASTA records with soft-masked and stray bytes (warnings in most records)"""
+    rng = random.Random(seed)
+    recs = []
+    for i in range(nrec):
+        body = bytes(rng.choices(b"ACGTNacgxy*", weights=[20, 20, 20, 20, 2, 1, 1, 1, 1, 1, 1],
+                                 k=rng.randint(0, 400)))
+        recs.append(b">rec%d %s\n" % (i, bytes(rng.choices(b"abc xyz", k=rng.randint(0, 30)))) +
+                    b"\n".join(body[j:j + 60] for j in range(0, len(body), 60)) + b"\n")
+    return b"ACGTqACGT\n" + b"".join(recs) + b"ACGzTT\n"
+
+
+@pytest.mark.parametrize("k", [4, 11, 17])
+def test_unknown_positions(k):
+    """collect_unknown=2: every unknown byte's stream offset, in order, over
+    several feeds (what the CLI interleaves with the -q 0 progress lines)"""
+    data = _unknown_records(5150 + k, 5000) + mixed_input(5150 + k, 300_000)
+    want = _unknown_positions(data)
+    arr = np.frombuffer(data, dtype=np.uint8)
+    with fk.Engine(k, collect_unknown=2) as e:
+        for a, b in ((0, 100_003), (100_003, 100_020), (100_020, 700_000), (700_000, len(arr))):
+            e.feed(np.ascontiguousarray(arr[a:b]))
+        e.finish(allow=(fk.FK_OK, fk.FK_E_EMPTY, fk.FK_E_UNTERMINATED_HEADER))
+        got = e.unknown_positions()
+        ub = e.unknown_bytes()
+    assert len(want) > 1000
+    assert got.tolist() == want
+    assert ub == bytes(data[i] for i in want)
+
+
+def _run_merged(cmd, cwd, env_extra=None):
+    """run cmd with stdout and stderr on one pipe (stdout fully buffered,
+    stderr not); returns (combined output, exit code)"""
+    env = dict(os.environ)
+    env.update(env_extra or {})
+    p = subprocess.run(cmd, cwd=cwd, stdin=subprocess.DEVNULL, stdout=subprocess.PIPE, stderr=subprocess.STDOUT,
+                       env=env, timeout=300)
+    return p.stdout, p.returncode
+
+
+@pytest.mark.parametrize("ingest", ["device", "stream"])
+def test_cli_q0_warnings_interleave_like_reference(ingest, tmp_path):
+    """-q 0 with unknown characters: the reference prints each "Unknown
+    character" warning (stderr, unbuffered, :582-584) during its scan, while
+    its progress lines (stdout, :997) sit in stdio's buffer until a block
+    fills.  With both streams on one pipe, the CLI's combined output must
+    equal the reference binary's (oracle/_ref, compiled from the reference
+    source) -- except that the reference's crash in free() at exit loses its
+    last unflushed stdout block, so its output is a prefix of ours"""
+    assert os.path.exists(oracle.REF_BIN), "oracle/_ref/findKmer_ref missing (make -C oracle)"
+    data = _unknown_records(9, 300)
+    a, b = tmp_path / "a", tmp_path / "b"
+    a.mkdir()
+    b.mkdir()
+    (a / "u.fa").write_bytes(data)
+    (b / "u.fa").write_bytes(data)
+    args = ["-q", "0", "-k", "4", "-p", "u.fa"]
+    env = {"FINDKMER_INGEST": "stream"} if ingest == "stream" else None
+    ours, rc = _run_merged([os.path.join(REPO, "findKmer")] + args, a, env)
+    ref, _ = _run_merged([oracle.REF_BIN] + args, b)
+    assert rc == 0, ours[-500:]
+    assert ref.count(b"Unknown character") > 100 and ref.count(b"Read ") > 100
+    assert ours.startswith(ref), next(i for i in range(len(ref)) if ours[i] != ref[i])
+    assert len(ours) - len(ref) <= 4096   # the reference's lost stdout block at most
+
+
 @pytest.mark.parametrize("k0,k1", [(5, 9), (15, 17)])
 def test_cli_sweep_matches_separate_runs(k0, k1, tmp_path):
     """--sweep k0..k1 over one device-resident read == separate runs
