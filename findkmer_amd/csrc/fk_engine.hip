@@ -2307,10 +2307,14 @@ k_part(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint
 #ifndef BUCKET_ROWS
 #define BUCKET_ROWS 2
 #endif
+/* SPLIT (k = 14, pg.split): a template parameter, so that the hot loop of
+   the other k carries no test of it (a runtime flag there cost ~0.9 ms of a
+   k=11 10 GB step) */
+template <bool SPLIT>
 __global__ void __launch_bounds__(1024)
 k_bucket_count(PartGeo pg, uint32_t groups, uint32_t *table) {
     extern __shared__ uint32_t slice[];
-    const uint32_t binsh = pg.split ? pg.sh - 1u : pg.sh;
+    const uint32_t binsh = SPLIT ? pg.sh - 1u : pg.sh;
     const uint32_t nb = 1u << binsh;
     /* pairs mode: the slice's 2^sh pair bins, then the 2^(sh-2) bins of the
        single k-mers filed under it (PART_SINGLE codes) */
@@ -2320,8 +2324,8 @@ k_bucket_count(PartGeo pg, uint32_t groups, uint32_t *table) {
        that XCD's L2 (k=11: 1 GB step 1.085 -> 1.065 ms, 10 GB 8.10 -> 8.04) */
     /* k = 14 (split): the two halves of a slice on one XCD, 8 blocks apart
        (the second reads the slice's codes from L2) */
-    const uint32_t half = pg.split ? (blockIdx.x >> 3) & 1u : 0u;
-    const uint32_t bx = pg.split ? (blockIdx.x & 7u) | ((blockIdx.x >> 4) << 3) : blockIdx.x;
+    const uint32_t half = SPLIT ? (blockIdx.x >> 3) & 1u : 0u;
+    const uint32_t bx = SPLIT ? (blockIdx.x & 7u) | ((blockIdx.x >> 4) << 3) : blockIdx.x;
     const uint32_t b = groups == 1 && (pg.nslices & 7u) == 0 ? (bx & 7u) * (pg.nslices >> 3) + (bx >> 3)
                                                            : bx % pg.nslices;
     const uint32_t g = bx / pg.nslices;
@@ -2345,12 +2349,12 @@ k_bucket_count(PartGeo pg, uint32_t groups, uint32_t *table) {
         for (int h = 0; h < 8; h++) {
             const uint64_t at = q * 8 + h;
             const uint32_t c = (w4[h >> 1] >> (16 * (h & 1))) & 0xFFFFu;
-            if (pg.split) {   /* k = 14: this block's half of the slice */
+            if (SPLIT) {   /* k = 14: this block's half of the slice */
                 if (at >= s0 && at < s1 && (c >> binsh) == half) atomicAdd(&slice[c & (nb - 1u)], 1u);
-                continue;
+            } else {
+                const uint32_t a = c & PART_SINGLE ? nb + ((c & ~PART_SINGLE) >> 2) : c;
+                if (at >= s0 && at < s1) atomicAdd(&slice[a], 1u);
             }
-            const uint32_t a = c & PART_SINGLE ? nb + ((c & ~PART_SINGLE) >> 2) : c;
-            if (at >= s0 && at < s1) atomicAdd(&slice[a], 1u);
         }
     };
     uint32_t en[BUCKET_ROWS];   /* the next iteration's index words, loaded with this one's codes */
@@ -3505,7 +3509,8 @@ extern "C" int fk_engine_create(int k, const fk_opts *opts, fk_engine **out) {
         hipFuncSetAttribute((const void *)k_resume<H_PAIRS>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh);
     }
     if (e->part)   /* k_bucket_count: one 2^15-bin slice + its 2^13 single bins (160 KiB) in LDS */
-        hipFuncSetAttribute((const void *)k_bucket_count, hipFuncAttributeMaxDynamicSharedMemorySize, 5 << 15);
+        for (const void *f : {(const void *)k_bucket_count<false>, (const void *)k_bucket_count<true>})
+            hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 5 << 15);
     for (int i = 0; i < 3; i++)
         /* timing only (results travel through mapped memory): no system-scope
            fence, which costs a cache writeback + invalidate and a gap of
@@ -3852,8 +3857,12 @@ static int launch_part(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t l
     const uint32_t groups = std::max<uint32_t>(1, (uint32_t)e->cus / pg.nslices);
     if (pairs && groups > 1) HIPCHK(hipMemsetAsync(e->d_pairs, 0, e->nbins * 5 * sizeof(uint32_t), e->stream));
     const size_t bc_lds = ((size_t)1 << (pg.sh - pg.split)) * sizeof(uint32_t) * (pairs ? 5 : 4) / 4;   /* + single bins */
-    hipLaunchKernelGGL(k_bucket_count, dim3(pg.nslices * groups << pg.split), dim3(1024), bc_lds, e->stream, pg,
-                       groups, e->d_table);
+    if (pg.split)
+        hipLaunchKernelGGL(k_bucket_count<true>, dim3(pg.nslices * groups << 1), dim3(1024), bc_lds, e->stream, pg,
+                           groups, e->d_table);
+    else
+        hipLaunchKernelGGL(k_bucket_count<false>, dim3(pg.nslices * groups), dim3(1024), bc_lds, e->stream, pg,
+                           groups, e->d_table);
     HIPCHK(hipGetLastError());
     if (pairs) {
         const unsigned fg = (unsigned)std::min<uint64_t>((uint64_t)e->cus * 4, (e->nbins + 255) / 256);
