@@ -4968,20 +4968,22 @@ static int sparse_finish(fk_engine *e, int32_t seq) {
     unsigned long long *nctr = ctr.as<unsigned long long>();
     HIPCHK(hipMemsetAsync(dacc, 0, FKS_ACC_N * sizeof(unsigned long long), e->stream));
 
-    /* the pass cap: window keys one sorted pass may hold */
+    /* the pass cap: window keys one sorted pass may hold.  A pass needs
+       ~56 B per key (emitted 8, sorted 8, runs 8, run lengths 8, rocPRIM's
+       scratch ~8, the part's keys 8 + counts 4, handed over), and the parts
+       of all passes together up to 12 B per window (distinct <= windows):
+       reserve those first */
+    const uint64_t wins = e->last.acc[ACC_WIN];
     uint64_t cap = e->sp_pass;
     if (!cap) {
         size_t fr = 0, tot = 0;
         HIPCHK(hipMemGetInfo(&fr, &tot));
-        /* emit 8 + sort 8 + runs (kept) 8 + counts 8 + rocPRIM ~8 + kept counts 4 B per key, and
-           the parts of earlier passes */
-        const uint64_t margin = 1ull << 30;
-        cap = fr > margin ? (fr - margin) / 64 : 0;
+        const uint64_t reserve = (1ull << 30) + 12 * wins;
+        cap = fr > reserve ? (fr - reserve) / 56 : 0;
         cap = std::max<uint64_t>(1u << 20, std::min<uint64_t>(cap, 1ull << 32));
     }
     /* all windows in one pass (the feed counted them): no histogram launch,
        the keys pass collects the short walks */
-    const uint64_t wins = e->last.acc[ACC_WIN];
     const bool single = wins <= cap;
 
     const bool tail = !e->state.hdr && seq >= 1 && seq < k;

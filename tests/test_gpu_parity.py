@@ -341,6 +341,35 @@ def test_baseline_genome_10g_vs_oracle(k, fasta, seed):
     assert ub_g == ub_o == b""
 
 
+@pytest.mark.parametrize("k", [17, 20])
+def test_sparse_genome_10g_properties(k):
+    """17 <= k <= 20 at the configs' size: the 10 G-base 80-column genome
+    (configs[2]'s input) through the key-range passes -- several of them,
+    since the finished table alone takes ~90 GB at k = 17 (sized to the free
+    HBM after reserving 12 B per window for the parts).  Size-independent
+    checks: windows and valid bases by formula, finish's rollover check (the
+    table's u32 total equals the windows), distinct k-mers within 0.1 % of
+    the occupancy expectation 4^k (1 - exp(-windows / 4^k)) for a uniform
+    genome"""
+    import math
+    import torch
+    import bench
+    n = 10_000_000_000
+    buf, size = bench.make_genome(n, 80, 2, bench.CHROM)
+    torch.cuda.synchronize()
+    with fk.Engine(k) as e:
+        e.feed_device(buf.data_ptr(), size)
+        rc, r = e.finish()
+    del buf
+    torch.cuda.empty_cache()
+    assert rc == fk.FK_OK
+    assert r.windows == bench.expected_windows(n, k, bench.CHROM)
+    assert r.valid_bases == bench.want_valid(n, k, bench.CHROM)
+    bins = float(1 << (2 * k))
+    want = bins * -math.expm1(-r.windows / bins)
+    assert abs(r.distinct - want) < 1e-3 * want, (r.distinct, want)
+
+
 @pytest.mark.parametrize("k", [6, 11])
 def test_full_size_properties(k):
     """BASELINE config sizes (1 GB stream, 1 GB of 80-col FASTA): exact
