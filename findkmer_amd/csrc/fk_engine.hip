@@ -3147,11 +3147,20 @@ struct fk_engine {
     uint64_t keep_len = 0, keep_cap = 0, kst_len = 0, kst_cap = 0;
     struct SpSeg { uint64_t off, len, st, nranges, cpw, nchunks; };
     std::vector<SpSeg> spsegs;                /* the retained segments */
-    std::vector<FksPart> spparts;              /* the finished table, one part per pass, ascending */
+    /* the finished table, contiguous (the passes append in key order): keys
+       ascending + u32 counts; kept across steps (grown, never shrunk), as are
+       a pass's emitted keys and the dense bucket table */
+    uint64_t *d_spk = nullptr;
+    uint32_t *d_spc = nullptr;
+    uint64_t spk_cap = 0, spc_cap = 0;
+    uint64_t *d_emit = nullptr;
+    uint64_t emit_cap = 0;
+    unsigned long long *d_spdense = nullptr;
+    uint64_t spdense_cap = 0;
     uint64_t sp_distinct = 0;
     uint64_t sp_pass = 0;                     /* FINDKMER_TUNE sp_pass: window keys per pass (0: by free HBM) */
     FksState fks;
-    bool sp_done = false;                     /* spparts holds the finished table */
+    bool sp_done = false;                     /* d_spk / d_spc hold the finished table */
     unsigned long long sp_nodes = 0, sp_roll = 0, sp_tstat[10] = {};
     uint16_t *d_codes = nullptr;              /* k_part: block code regions */
     uint32_t *d_pflag = nullptr;              /* k_part: a range went to k_part<RES> */
@@ -3331,10 +3340,16 @@ static size_t lds_bytes(const fk_engine *e) {
 }
 
 /* Zero table, counters and the stream state (asynchronous, stream-ordered). */
-static void sp_parts_free(fk_engine *e) {
-    for (auto &p : e->spparts) { hipFree(p.keys); hipFree(p.cnts); }
-    e->spparts.clear();
-    e->sp_distinct = 0;
+/* a sparse buffer of at least `n` elements of `sz` bytes (contents dropped) */
+static int sp_ensure(void **p, uint64_t *cap, uint64_t n, size_t sz) {
+    if (*p && *cap >= n) return FK_OK;
+    hipFree(*p);
+    *p = nullptr;
+    *cap = 0;
+    const uint64_t c = std::max<uint64_t>(n, 1024);
+    if (hipMalloc(p, c * sz) != hipSuccess) return FK_E_OOM;
+    *cap = c;
+    return FK_OK;
 }
 
 static int zero_all(fk_engine *e) {
@@ -3352,7 +3367,7 @@ static int zero_all(fk_engine *e) {
     e->timed_n = 0;
     e->keep_len = e->kst_len = 0;
     e->spsegs.clear();
-    sp_parts_free(e);
+    e->sp_distinct = 0;
     e->sp_done = false;
     e->unknown_bytes.clear();
     e->unknown_pos.clear();
@@ -3372,7 +3387,7 @@ extern "C" void fk_engine_destroy(fk_engine *e) {
     hipFree(e->d_bsum); hipFree(e->d_ctl); hipFree(e->d_opc);
     hipFree(e->d_keep);
     hipFree(e->d_kst);
-    sp_parts_free(e);
+    hipFree(e->d_spk); hipFree(e->d_spc); hipFree(e->d_emit); hipFree(e->d_spdense);
     fks_free(&e->fks);
     if (e->h_stage) hipHostFree(e->h_stage);
     for (int i = 0; i < 3; i++) if (e->ev[i]) hipEventDestroy(e->ev[i]);
@@ -4952,7 +4967,7 @@ static int sp_emit_all(fk_engine *e, const SpEmit &em) {
  */
 static int sparse_finish(fk_engine *e, int32_t seq) {
     const int k = e->k;
-    sp_parts_free(e);
+    e->sp_distinct = 0;
     memset(e->sp_tstat, 0, sizeof e->sp_tstat);
     e->sp_roll = e->sp_nodes = 0;
     const uint32_t nbk = 1u << SP_BUCKET_BITS;
@@ -4978,9 +4993,20 @@ static int sparse_finish(fk_engine *e, int32_t seq) {
     if (!cap) {
         size_t fr = 0, tot = 0;
         HIPCHK(hipMemGetInfo(&fr, &tot));
+        /* plus what the engine's sparse buffers already hold (reused, or
+           freed and reallocated larger) */
+        const uint64_t held = e->spk_cap * 8 + e->spc_cap * 4 + e->emit_cap * 8 + e->spdense_cap * 8 +
+                              e->fks.sorted_cap + e->fks.c64_cap + e->fks.tmp_cap;
+        const uint64_t avail = (uint64_t)fr + held;
         const uint64_t reserve = (1ull << 30) + 12 * wins;
-        cap = fr > reserve ? (fr - reserve) / 56 : 0;
+        cap = avail > reserve ? (avail - reserve) / 56 : 0;
         cap = std::max<uint64_t>(1u << 20, std::min<uint64_t>(cap, 1ull << 32));
+    }
+    /* the table's storage: room for every window (distinct <= windows) */
+    {
+        int rc = sp_ensure((void **)&e->d_spk, &e->spk_cap, wins + 1, 8);
+        if (!rc) rc = sp_ensure((void **)&e->d_spc, &e->spc_cap, wins + 1, 4);
+        if (rc) return rc;
     }
     /* all windows in one pass (the feed counted them): no histogram launch,
        the keys pass collects the short walks */
@@ -5059,7 +5085,6 @@ static int sparse_finish(fk_engine *e, int32_t seq) {
     }
 
     /* 3. the passes */
-    DevScratch keys, dense;
     uint64_t prev_last = 0;
     bool have_prev = false;
     std::vector<unsigned long long> edges(24, 0);   /* prefix histogram across pass boundaries */
@@ -5068,23 +5093,26 @@ static int sparse_finish(fk_engine *e, int32_t seq) {
         em.shift = shift;
         em.lo = (uint64_t)ps.b0 << shift;
         em.hi = (uint64_t)ps.b1 << shift;
-        FksPart part{nullptr, nullptr, 0};
+        uint64_t *out_k = e->d_spk + e->sp_distinct;   /* this pass's runs follow the earlier ones' */
+        uint32_t *out_c = e->d_spc + e->sp_distinct;
+        uint64_t nw = 0;
         if (ps.dense) {
             const uint64_t nd = 1ull << shift;
-            if (!dense.p && !dense.alloc(nd * 8)) return FK_E_OOM;
-            HIPCHK(hipMemsetAsync(dense.p, 0, nd * 8, e->stream));
-            em.mode = SP_DENSE;
-            em.dense = dense.as<unsigned long long>();
-            int rc = sp_emit_all(e, em);
+            int rc = sp_ensure((void **)&e->d_spdense, &e->spdense_cap, nd, 8);
             if (rc) return rc;
-            if (fks_dense_runs(&e->fks, em.dense, nd, em.lo, k, e->stream, dacc, &part)) return FK_E_HIP;
+            HIPCHK(hipMemsetAsync(e->d_spdense, 0, nd * 8, e->stream));
+            em.mode = SP_DENSE;
+            em.dense = e->d_spdense;
+            rc = sp_emit_all(e, em);
+            if (rc) return rc;
+            if (fks_dense_runs(&e->fks, em.dense, nd, em.lo, k, e->stream, dacc, out_k, out_c, &nw)) return FK_E_HIP;
         } else {
-            if (keys.bytes < ps.n * 8) {
-                keys.release();
-                if (!keys.alloc(std::max<uint64_t>(ps.n, std::min<uint64_t>(cap, 2 * ps.n)) * 8)) return FK_E_OOM;
+            if (ps.n) {
+                int rc = sp_ensure((void **)&e->d_emit, &e->emit_cap, std::max<uint64_t>(ps.n, std::min<uint64_t>(cap, wins)), 8);
+                if (rc) return rc;
             }
             em.mode = SP_KEYS;
-            em.out = keys.as<uint64_t>();
+            em.out = e->d_emit;
             em.nout = nctr;
             em.out_cap = ps.n;
             unsigned long long got[2] = {0, 0};
@@ -5108,16 +5136,15 @@ static int sparse_finish(fk_engine *e, int32_t seq) {
                 int rc = prep_shorts();
                 if (rc) return rc;
             }
-            if (fks_sort_runs(&e->fks, em.out, ps.n, k, e->stream, dacc, &part)) return FK_E_HIP;
+            if (fks_sort_runs(&e->fks, em.out, ps.n, k, e->stream, dacc, out_k, out_c, &nw)) return FK_E_HIP;
         }
-        if (part.keys || part.cnts) e->spparts.push_back(part);   /* owned (freed) from here on */
-        const uint64_t nw = part.n;
         if (!nw) continue;
-        if (ns && fks_short_mark(&part, shorts.as<uint64_t>(), ns, k, found.as<uint8_t>(), e->stream))
+        if (e->sp_distinct + nw > e->spk_cap) return FK_E_HIP;   /* cannot happen: distinct <= windows */
+        if (ns && fks_short_mark(out_k, nw, shorts.as<uint64_t>(), ns, k, found.as<uint8_t>(), e->stream))
             return FK_E_HIP;
         uint64_t fl[2];
-        HIPCHK(hipMemcpyAsync(&fl[0], part.keys, 8, hipMemcpyDeviceToHost, e->stream));
-        HIPCHK(hipMemcpyAsync(&fl[1], part.keys + (nw - 1), 8, hipMemcpyDeviceToHost, e->stream));
+        HIPCHK(hipMemcpyAsync(&fl[0], out_k, 8, hipMemcpyDeviceToHost, e->stream));
+        HIPCHK(hipMemcpyAsync(&fl[1], out_k + (nw - 1), 8, hipMemcpyDeviceToHost, e->stream));
         HIPCHK(hipStreamSynchronize(e->stream));
         if (have_prev) {   /* the adjacent pair across the boundary: first differing base */
             const uint64_t diff = fl[0] ^ prev_last;
@@ -5128,8 +5155,6 @@ static int sparse_finish(fk_engine *e, int32_t seq) {
         have_prev = true;
         e->sp_distinct += nw;
     }
-    keys.release();
-    dense.release();
 
     /* 4. totals: statistics, rollover, nodeCounter */
     unsigned long long r[FKS_ACC_N];
@@ -5330,11 +5355,9 @@ static int sparse_copy(fk_engine *e, uint64_t *keys, uint32_t *counts, uint64_t 
     if (cap < e->sp_distinct) return FK_E_INVALID;
     int rc = set_dev(e);
     if (rc) return rc;
-    uint64_t at = 0;
-    for (const auto &p : e->spparts) {
-        if (keys) HIPCHK(hipMemcpyAsync(keys + at, p.keys, p.n * sizeof(uint64_t), kind, e->stream));
-        if (counts) HIPCHK(hipMemcpyAsync(counts + at, p.cnts, p.n * sizeof(uint32_t), kind, e->stream));
-        at += p.n;
+    if (e->sp_distinct) {
+        if (keys) HIPCHK(hipMemcpyAsync(keys, e->d_spk, e->sp_distinct * sizeof(uint64_t), kind, e->stream));
+        if (counts) HIPCHK(hipMemcpyAsync(counts, e->d_spc, e->sp_distinct * sizeof(uint32_t), kind, e->stream));
     }
     HIPCHK(hipStreamSynchronize(e->stream));
     return FK_OK;
@@ -5361,33 +5384,34 @@ extern "C" int fk_engine_sparse_split(fk_engine *e, int world, uint64_t *counts)
     if (rc) return rc;
     const uint64_t nb = 1ull << (2 * e->k), S = (nb + (uint64_t)world - 1) / (uint64_t)world;
     for (int r = 0; r < world; r++) counts[r] = 0;
-    for (const auto &p : e->spparts) {
-        if (!p.n) continue;
-        /* the part's keys are ascending: owners' runs are contiguous; the
-           boundaries by binary search over the device keys, one key per probe */
-        uint64_t first = 0, last = 0;
-        HIPCHK(hipMemcpyAsync(&first, p.keys, 8, hipMemcpyDeviceToHost, e->stream));
-        HIPCHK(hipMemcpyAsync(&last, p.keys + (p.n - 1), 8, hipMemcpyDeviceToHost, e->stream));
-        HIPCHK(hipStreamSynchronize(e->stream));
-        const int r0 = (int)(first / S), r1 = (int)(last / S);
-        uint64_t at = 0;
-        for (int r = r0; r <= r1; r++) {
-            uint64_t lo = at, hi = p.n;   /* first index with key >= (r + 1) * S */
-            if (r == r1) {
-                lo = p.n;
-            } else {
-                const uint64_t want = (uint64_t)(r + 1) * S;
-                while (lo < hi) {
-                    const uint64_t mid = (lo + hi) / 2;
-                    uint64_t v = 0;
-                    HIPCHK(hipMemcpy(&v, p.keys + mid, 8, hipMemcpyDeviceToHost));
-                    if (v < want) lo = mid + 1;
-                    else hi = mid;
-                }
+    const uint64_t n = e->sp_distinct;
+    if (!n) return FK_OK;
+    /* the keys are ascending: owners' runs are contiguous; the boundaries by
+       binary search over the device keys, one key per probe */
+    const uint64_t *keys = e->d_spk;
+    uint64_t first = 0, last = 0;
+    HIPCHK(hipMemcpyAsync(&first, keys, 8, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipMemcpyAsync(&last, keys + (n - 1), 8, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    const int r0 = (int)(first / S), r1 = (int)(last / S);
+    uint64_t at = 0;
+    for (int r = r0; r <= r1; r++) {
+        uint64_t lo = at, hi = n;   /* first index with key >= (r + 1) * S */
+        if (r == r1) {
+            lo = n;
+        } else {
+            const uint64_t want = (uint64_t)(r + 1) * S;
+            while (lo < hi) {
+                const uint64_t mid = (lo + hi) / 2;
+                uint64_t v = 0;
+                HIPCHK(hipMemcpyAsync(&v, keys + mid, 8, hipMemcpyDeviceToHost, e->stream));
+                HIPCHK(hipStreamSynchronize(e->stream));
+                if (v < want) lo = mid + 1;
+                else hi = mid;
             }
-            counts[r] += lo - at;
-            at = lo;
         }
+        counts[r] = lo - at;
+        at = lo;
     }
     return FK_OK;
 }
@@ -5406,18 +5430,18 @@ extern "C" int fk_engine_sparse_adopt(fk_engine *e, const uint64_t *keys, const 
     DevScratch acc;
     if (!acc.alloc(FKS_ACC_N * sizeof(unsigned long long))) return FK_E_OOM;
     HIPCHK(hipMemsetAsync(acc.p, 0, FKS_ACC_N * sizeof(unsigned long long), e->stream));
-    FksPart part{nullptr, nullptr, 0};
-    if (fks_merge_runs(&e->fks, keys, counts, n, e->k, e->stream, acc.as<unsigned long long>(), &part)) {
-        hipFree(part.keys);
-        hipFree(part.cnts);
+    rc = sp_ensure((void **)&e->d_spk, &e->spk_cap, n + 1, 8);
+    if (!rc) rc = sp_ensure((void **)&e->d_spc, &e->spc_cap, n + 1, 4);
+    if (rc) return rc;
+    uint64_t nw = 0;
+    e->sp_distinct = 0;
+    if (fks_merge_runs(&e->fks, keys, counts, n, e->k, e->stream, acc.as<unsigned long long>(), e->d_spk, e->d_spc,
+                       &nw))
         return FK_E_HIP;
-    }
     unsigned long long r[FKS_ACC_N];
     HIPCHK(hipMemcpyAsync(r, acc.p, sizeof r, hipMemcpyDeviceToHost, e->stream));
     HIPCHK(hipStreamSynchronize(e->stream));
-    sp_parts_free(e);
-    if (part.n) e->spparts.push_back(part);
-    e->sp_distinct = part.n;
+    e->sp_distinct = nw;
     memcpy(e->sp_tstat, r, sizeof e->sp_tstat);
     e->sp_roll = r[FKS_ACC_ROLL];
     stats[0] = r[0];

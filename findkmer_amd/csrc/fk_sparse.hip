@@ -177,68 +177,59 @@ __global__ void k_sp_short_left(const uint64_t *shorts, uint64_t ns, const uint8
     }
 }
 
-/* runs (st->keys, st->c64)[0, nw) -> statistics, prefix histogram and the
-   pass's table part: the keys buffer itself (handed over) and u32 counts */
-static int runs_stats(FksState *st, uint64_t nw, int k, hipStream_t s, unsigned long long *dacc, FksPart *part) {
-    *part = FksPart{nullptr, nullptr, 0};
+/* runs (out_keys, st->c64)[0, nw) -> u32 counts into out_cnts, statistics,
+   prefix histogram */
+static int runs_stats(FksState *st, uint64_t nw, int k, hipStream_t s, unsigned long long *dacc,
+                      const uint64_t *out_keys, uint32_t *out_cnts) {
     if (!nw) return 0;
-    if (hipMalloc((void **)&part->cnts, nw * 4) != hipSuccess) return -1;
-    part->n = nw;
-    if (2 * nw * 8 >= st->keys_cap) {   /* mostly used: hand the buffer over */
-        part->keys = st->keys;
-        st->keys = nullptr;
-        st->keys_cap = 0;
-    } else {                            /* few runs (a dense bucket): an exact copy */
-        if (hipMalloc((void **)&part->keys, nw * 8) != hipSuccess) return -1;
-        CK(hipMemcpyAsync(part->keys, st->keys, nw * 8, hipMemcpyDeviceToDevice, s));
-    }
-    hipLaunchKernelGGL(k_sp_stats, dim3(grid_for(nw)), dim3(256), 0, s, part->keys, st->c64, part->cnts, nw, k, dacc,
+    hipLaunchKernelGGL(k_sp_stats, dim3(grid_for(nw)), dim3(256), 0, s, out_keys, st->c64, out_cnts, nw, k, dacc,
                        dacc + FKS_ACC_ROLL);
     if (nw > 1)
-        hipLaunchKernelGGL(k_sp_wprefix, dim3(grid_for(nw)), dim3(256), 0, s, part->keys, nw, k, dacc + FKS_ACC_WPREFIX);
+        hipLaunchKernelGGL(k_sp_wprefix, dim3(grid_for(nw)), dim3(256), 0, s, out_keys, nw, k, dacc + FKS_ACC_WPREFIX);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 int fks_sort_runs(FksState *st, uint64_t *keys, uint64_t n, int k, hipStream_t s, unsigned long long *dacc,
-                  FksPart *part) {
-    *part = FksPart{nullptr, nullptr, 0};
+                  uint64_t *out_keys, uint32_t *out_cnts, uint64_t *nw) {
+    *nw = 0;
     if (n == 0) return 0;
-    if (ensure((void **)&st->sorted, &st->sorted_cap, n * 8) || ensure((void **)&st->keys, &st->keys_cap, n * 8) ||
-        ensure((void **)&st->c64, &st->c64_cap, n * 8) ||
+    if (ensure((void **)&st->sorted, &st->sorted_cap, n * 8) || ensure((void **)&st->c64, &st->c64_cap, n * 8) ||
         ensure((void **)&st->small, &st->small_cap, 64 * sizeof(unsigned long long)))
         return -1;
     size_t tb = 0, tb2 = 0;
     CK(rocprim::radix_sort_keys(nullptr, tb, keys, st->sorted, n, 0, 2 * k, s));
-    CK(rocprim::run_length_encode(nullptr, tb2, st->sorted, n, st->keys, st->c64, st->small, s));
+    CK(rocprim::run_length_encode(nullptr, tb2, st->sorted, n, out_keys, st->c64, st->small, s));
     if (ensure(&st->tmp, &st->tmp_cap, tb > tb2 ? tb : tb2)) return -1;
     tb = st->tmp_cap;
     CK(rocprim::radix_sort_keys(st->tmp, tb, keys, st->sorted, n, 0, 2 * k, s));
     tb2 = st->tmp_cap;
-    CK(rocprim::run_length_encode(st->tmp, tb2, st->sorted, n, st->keys, st->c64, st->small, s));
+    CK(rocprim::run_length_encode(st->tmp, tb2, st->sorted, n, out_keys, st->c64, st->small, s));
     unsigned long long runs = 0;
     CK(hipMemcpyAsync(&runs, st->small, sizeof runs, hipMemcpyDeviceToHost, s));
     CK(hipStreamSynchronize(s));
-    return runs_stats(st, runs, k, s, dacc, part);
+    *nw = runs;
+    return runs_stats(st, runs, k, s, dacc, out_keys, out_cnts);
 }
 
 int fks_dense_runs(FksState *st, unsigned long long *dense, uint64_t n, uint64_t lo, int k, hipStream_t s,
-                   unsigned long long *dacc, FksPart *part) {
-    *part = FksPart{nullptr, nullptr, 0};
-    if (ensure((void **)&st->keys, &st->keys_cap, (n + 1) * 8) || ensure((void **)&st->c64, &st->c64_cap, (n + 1) * 8) ||
-        ensure((void **)&st->small, &st->small_cap, 64 * sizeof(unsigned long long)))
-        return -1;
+                   unsigned long long *dacc, uint64_t *out_keys, uint32_t *out_cnts, uint64_t *nw) {
+    *nw = 0;
+    if (ensure((void **)&st->small, &st->small_cap, 64 * sizeof(unsigned long long))) return -1;
     rocprim::counting_iterator<uint64_t> idx(lo);
     auto flags = rocprim::make_transform_iterator(dense, NonZero());
     size_t tb = 0;
-    CK(rocprim::select(nullptr, tb, idx, flags, st->keys, st->small, n, s));
+    CK(rocprim::select(nullptr, tb, idx, flags, out_keys, st->small, n, s));
     if (ensure(&st->tmp, &st->tmp_cap, tb)) return -1;
     tb = st->tmp_cap;
-    CK(rocprim::select(st->tmp, tb, idx, flags, st->keys, st->small, n, s));
+    CK(rocprim::select(st->tmp, tb, idx, flags, out_keys, st->small, n, s));
     unsigned long long runs = 0;
     CK(hipMemcpyAsync(&runs, st->small, sizeof runs, hipMemcpyDeviceToHost, s));
     CK(hipStreamSynchronize(s));
-    if (runs) hipLaunchKernelGGL(k_sp_gather, dim3(grid_for(runs)), dim3(256), 0, s, dense, st->keys, runs, lo, st->c64);
-    return runs_stats(st, runs, k, s, dacc, part);
+    *nw = runs;
+    if (!runs) return 0;
+    if (ensure((void **)&st->c64, &st->c64_cap, runs * 8)) return -1;
+    hipLaunchKernelGGL(k_sp_gather, dim3(grid_for(runs)), dim3(256), 0, s, dense, out_keys, runs, lo, st->c64);
+    return runs_stats(st, runs, k, s, dacc, out_keys, out_cnts);
 }
 
 struct WidenU32 {
@@ -246,28 +237,29 @@ struct WidenU32 {
 };
 
 int fks_merge_runs(FksState *st, const uint64_t *keys, const uint32_t *cnts, uint64_t n, int k, hipStream_t s,
-                   unsigned long long *dacc, FksPart *part) {
-    *part = FksPart{nullptr, nullptr, 0};
+                   unsigned long long *dacc, uint64_t *out_keys, uint32_t *out_cnts, uint64_t *nw) {
+    *nw = 0;
     if (n == 0) return 0;
-    if (ensure((void **)&st->sorted, &st->sorted_cap, n * 8) || ensure((void **)&st->keys, &st->keys_cap, n * 8) ||
-        ensure((void **)&st->c64, &st->c64_cap, n * 8) || ensure((void **)&st->cand2, &st->cand2_cap, n * 4) ||
+    if (ensure((void **)&st->sorted, &st->sorted_cap, n * 8) || ensure((void **)&st->c64, &st->c64_cap, n * 8) ||
+        ensure((void **)&st->cand2, &st->cand2_cap, n * 4) ||
         ensure((void **)&st->small, &st->small_cap, 64 * sizeof(unsigned long long)))
         return -1;
     uint32_t *vs = reinterpret_cast<uint32_t *>(st->cand2);
     auto wide = rocprim::make_transform_iterator(vs, WidenU32());
     size_t tb = 0, tb2 = 0;
     CK(rocprim::radix_sort_pairs(nullptr, tb, keys, st->sorted, cnts, vs, n, 0, 2 * k, s));
-    CK(rocprim::reduce_by_key(nullptr, tb2, st->sorted, wide, n, st->keys, st->c64, st->small,
+    CK(rocprim::reduce_by_key(nullptr, tb2, st->sorted, wide, n, out_keys, st->c64, st->small,
                               rocprim::plus<unsigned long long>(), rocprim::equal_to<uint64_t>(), s));
     if (ensure(&st->tmp, &st->tmp_cap, tb > tb2 ? tb : tb2)) return -1;
     tb = tb2 = st->tmp_cap;
     CK(rocprim::radix_sort_pairs(st->tmp, tb, keys, st->sorted, cnts, vs, n, 0, 2 * k, s));
-    CK(rocprim::reduce_by_key(st->tmp, tb2, st->sorted, wide, n, st->keys, st->c64, st->small,
+    CK(rocprim::reduce_by_key(st->tmp, tb2, st->sorted, wide, n, out_keys, st->c64, st->small,
                               rocprim::plus<unsigned long long>(), rocprim::equal_to<uint64_t>(), s));
     unsigned long long runs = 0;
     CK(hipMemcpyAsync(&runs, st->small, sizeof runs, hipMemcpyDeviceToHost, s));
     CK(hipStreamSynchronize(s));
-    return runs_stats(st, runs, k, s, dacc, part);
+    *nw = runs;
+    return runs_stats(st, runs, k, s, dacc, out_keys, out_cnts);
 }
 
 int fks_unique(FksState *st, uint64_t *v, uint64_t n, hipStream_t s, uint64_t *n_out) {
@@ -290,10 +282,10 @@ int fks_unique(FksState *st, uint64_t *v, uint64_t n, hipStream_t s, uint64_t *n
     return 0;
 }
 
-int fks_short_mark(const FksPart *part, const uint64_t *shorts, uint64_t ns, int k, uint8_t *found, hipStream_t s) {
-    if (!ns || !part->n) return 0;
-    hipLaunchKernelGGL(k_sp_short_mark, dim3(grid_for(ns)), dim3(256), 0, s, part->keys, part->n, shorts, ns, k,
-                       found);
+int fks_short_mark(const uint64_t *keys, uint64_t nw, const uint64_t *shorts, uint64_t ns, int k, uint8_t *found,
+                   hipStream_t s) {
+    if (!ns || !nw) return 0;
+    hipLaunchKernelGGL(k_sp_short_mark, dim3(grid_for(ns)), dim3(256), 0, s, keys, nw, shorts, ns, k, found);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -319,7 +311,7 @@ int fks_short_count(FksState *st, const uint64_t *shorts, uint64_t ns, const uin
 }
 
 void fks_free(FksState *st) {
-    hipFree(st->sorted); hipFree(st->keys); hipFree(st->c64);
+    hipFree(st->sorted); hipFree(st->c64);
     hipFree(st->tmp); hipFree(st->small); hipFree(st->cand); hipFree(st->cand2);
     *st = FksState{};
 }
