@@ -43,6 +43,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <type_traits>
 #include <vector>
 
 #include "findkmer.h"
@@ -1873,6 +1874,10 @@ k_sp_emit(const uint8_t *buf, uint64_t len, int k, uint64_t maskk, const XState 
    same LDS batch (a pair tile hands over half as many entries) */
 #define PART_TILES(PAIRS) ((PAIRS) ? 4u : 2u)
 #define PART_MAX_BATCH_W(W) (2u * (W) * FK_TILE_BYTES)   /* entries per batch */
+/* k = 15, 16 (C32): 32-bit codes under 2048 coarse slices, one tile per wave
+   per batch (W x 2048 entries, the same 128 KiB of LDS and row slot) */
+#define PART_TILES3(PAIRS, C32) ((C32) ? 1u : PART_TILES(PAIRS))
+#define PART_ROW_BYTES(W) (4u * (W) * FK_TILE_BYTES)   /* one batch's row slot in d_codes */
 static_assert(PART_MAX_BATCH_W(16u) <= 65536u, "run index words hold 16-bit starts and counts - 1");
 /* slices of a batch: k = 11 pairs 2^24 / 2^15 (the single k-mers fold into
    them, flagged), k = 12 2^24 / 2^15, k = 13 2^26 / 2^15; k <= 10 at most 128 */
@@ -1996,11 +2001,12 @@ __device__ __forceinline__ void part_entries(const Emit &em, uint32_t mk, uint32
  * not make the atomic phases cheaper (the atomic instructions' issue, not
  * the banks, sets their cost) and its extra barrier made the batch slower
  * (47.0 K vs 45.7 K cycles), so the scan stays on wave 0. */
-template <bool PAIRS, bool MIX, uint32_t W, uint32_t SM>
+template <bool PAIRS, bool MIX, uint32_t W, uint32_t SM, typename CT>
 __device__ __forceinline__ bool part_batch(const Ctx &cx, const PartGeo &pg, const Emit *es, const bool *haves,
                                            bool more, uint32_t row, uint32_t *hist,
-                                           uint32_t *cur, uint32_t *total, uint16_t *ent, uint32_t *scr) {
-    constexpr int NT = PART_TILES(PAIRS);
+                                           uint32_t *cur, uint32_t *total, CT *ent, uint32_t *scr) {
+    constexpr bool C32 = sizeof(CT) == 4;
+    constexpr int NT = PART_TILES3(PAIRS, C32);
     const uint32_t t = threadIdx.x, lane = t & 63;
     const uint32_t mk = (uint32_t)cx.maskk, sh = pg.sh, lowm = (1u << sh) - 1u;
     const uint32_t m1 = (mk << 2) | 3u;
@@ -2072,7 +2078,7 @@ __device__ __forceinline__ bool part_batch(const Ctx &cx, const PartGeo &pg, con
         } else {
             p = atomicAdd(&cur[b], 1u);
         }
-        ent[p] = (uint16_t)low;
+        ent[p] = (CT)low;
     };
 #pragma unroll
     for (int i = 0; i < NT; i++) {
@@ -2085,8 +2091,8 @@ __device__ __forceinline__ bool part_batch(const Ctx &cx, const PartGeo &pg, con
        PART_MAX_BATCH_W(W) entries: a run's position needs no per-row base),
        as 16-B pieces; the up to 7 codes past the batch's end are padding no
        run covers */
-    const uint32_t n8 = (*total + 7u) >> 3;
-    uint4 *dst = reinterpret_cast<uint4 *>(pg.codes + (size_t)row * PART_MAX_BATCH_W(W));
+    const uint32_t n8 = (*total * (uint32_t)sizeof(CT) + 15u) >> 4;
+    uint4 *dst = reinterpret_cast<uint4 *>(reinterpret_cast<uint8_t *>(pg.codes) + (size_t)row * PART_ROW_BYTES(W));
     const uint4 *src = reinterpret_cast<const uint4 *>(ent);
     for (uint32_t i = t; i < n8; i += PART_BLOCK_W(W)) dst[i] = src[i];
     return any_more;
@@ -2098,13 +2104,14 @@ __device__ __forceinline__ bool part_batch(const Ctx &cx, const PartGeo &pg, con
  * the rest of it, each tile fast, mixed (the masked entries of tile_mixed)
  * or general.  Two kernels: tile_mixed's registers stay out of the main
  * pass.  k_part<RES> returns at once unless some range stopped. */
-template <bool PAIRS, bool RES, uint32_t W, uint32_t SM = PART_SM(W)>
+template <bool PAIRS, bool RES, uint32_t W, uint32_t SM = PART_SM(W), bool C32 = false>
 __global__ void __launch_bounds__(PART_BLOCK_W(W), 4) /* 4 waves per SIMD (<= 128 VGPRs): 16 waves per CU */
 k_part(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint32_t *table,
        uint32_t *shortcnt, unsigned long long *acc, DevRes *res, RangeRec *rr, uint64_t nchunks, uint64_t cpw,
        const XState *d_init, int has_init, PartGeo pg, ResumeRec *resume, const XState *exact) {
     __shared__ uint32_t hist[SM], cur[SM > 2048u ? SM / 2u : SM], total, scr[W];
-    __shared__ __attribute__((aligned(16))) uint16_t ent[PART_MAX_BATCH_W(W)];
+    using CT = typename std::conditional<C32, uint32_t, uint16_t>::type;
+    __shared__ __attribute__((aligned(16))) CT ent[PART_ROW_BYTES(W) / sizeof(CT)];
     if (RES && *(volatile uint32_t *)pg.flag == 0) return;   /* uniform: no range stopped */
     /* open the feed's result block (the kernels after this one accumulate
        into it) */
@@ -2184,7 +2191,7 @@ k_part(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint
     uint32_t general_left = pg.nomix ? 0xFFFFFFFFu : pg.general;
     uint32_t round = 0;
     const uint32_t row0 = (RES ? pg.rows : 0u) + blockIdx.x * pg.rounds;
-    constexpr uint32_t NT = PART_TILES(PAIRS);
+    constexpr uint32_t NT = PART_TILES3(PAIRS, C32);
     Emit stash[NT];
     bool have_stash[NT];
 #pragma unroll
@@ -2230,7 +2237,7 @@ k_part(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint
                 have_stash[i_] = have;                                               \
             }                                                                        \
             if (ph_ == NT - 1) {                                                     \
-                const bool more_ = part_batch<PAIRS, RES, W, SM>(cx, pg, stash, have_stash, !done, \
+                const bool more_ = part_batch<PAIRS, RES, W, SM, CT>(cx, pg, stash, have_stash, !done, \
                                                           row0 + round / NT, hist, cur, &total, ent, scr); \
                 if (!more_ || round / NT + 1 >= pg.rounds) { round++; break; }       \
             }                                                                        \
@@ -2307,14 +2314,24 @@ k_part(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint
 #ifndef BUCKET_ROWS
 #define BUCKET_ROWS 2
 #endif
-/* SPLIT (k = 14, pg.split): a template parameter, so that the hot loop of
-   the other k carries no test of it (a runtime flag there cost ~0.9 ms of a
-   k=11 10 GB step) */
-template <bool SPLIT>
+/* MODE (a template parameter, so that the hot loop of the common k carries
+   no test of it: a runtime flag there cost ~0.9 ms of a k=11 10 GB step):
+   BK_PLAIN 16-bit codes, one block per slice (and row group);
+   BK_SPLIT k = 14: 16-bit codes, a slice counted as 2^(pg.split) parts of
+            2^15 bins, one block each;
+   BK_C32   k = 15, 16: 32-bit codes under 2048 coarse slices, each counted
+            as 2^(pg.split) parts of 2^15 bins.
+   A part block keeps only its codes; the parts of a slice run on one XCD
+   one after another, so all but the first read the slice's codes from L2. */
+enum { BK_PLAIN = 0, BK_SPLIT = 1, BK_C32 = 2 };
+template <int MODE>
 __global__ void __launch_bounds__(1024)
 k_bucket_count(PartGeo pg, uint32_t groups, uint32_t *table) {
     extern __shared__ uint32_t slice[];
-    const uint32_t binsh = SPLIT ? pg.sh - 1u : pg.sh;
+    constexpr bool PARTS = MODE != BK_PLAIN;
+    constexpr uint32_t CPP = MODE == BK_C32 ? 4u : 8u;     /* codes per 16-B piece */
+    constexpr uint32_t PSH = MODE == BK_C32 ? 2u : 3u;
+    const uint32_t binsh = PARTS ? 15u : pg.sh;
     const uint32_t nb = 1u << binsh;
     /* pairs mode: the slice's 2^sh pair bins, then the 2^(sh-2) bins of the
        single k-mers filed under it (PART_SINGLE codes) */
@@ -2322,13 +2339,17 @@ k_bucket_count(PartGeo pg, uint32_t groups, uint32_t *table) {
     /* consecutive slices on one XCD (blocks b, b + 8, .. share an XCD): the
        128-B line two neighbouring runs of a row share is fetched once into
        that XCD's L2 (k=11: 1 GB step 1.085 -> 1.065 ms, 10 GB 8.10 -> 8.04) */
-    /* k = 14 (split): the two halves of a slice on one XCD, 8 blocks apart
-       (the second reads the slice's codes from L2) */
-    const uint32_t half = SPLIT ? (blockIdx.x >> 3) & 1u : 0u;
-    const uint32_t bx = SPLIT ? (blockIdx.x & 7u) | ((blockIdx.x >> 4) << 3) : blockIdx.x;
-    const uint32_t b = groups == 1 && (pg.nslices & 7u) == 0 ? (bx & 7u) * (pg.nslices >> 3) + (bx >> 3)
-                                                           : bx % pg.nslices;
-    const uint32_t g = bx / pg.nslices;
+    uint32_t b, g, part = 0;
+    if (PARTS) {   /* (groups == 1, nslices a multiple of 8) */
+        const uint32_t j = blockIdx.x >> 3, np = 1u << pg.split;
+        part = j & (np - 1u);
+        b = (blockIdx.x & 7u) * (pg.nslices >> 3) + (j >> pg.split);
+        g = 0;
+    } else {
+        b = groups == 1 && (pg.nslices & 7u) == 0 ? (blockIdx.x & 7u) * (pg.nslices >> 3) + (blockIdx.x >> 3)
+                                                : blockIdx.x % pg.nslices;
+        g = blockIdx.x / pg.nslices;
+    }
     for (uint32_t i = threadIdx.x; i < nb + ns; i += blockDim.x) slice[i] = 0;
     __syncthreads();
     const uint32_t *ix = pg.idx + (size_t)b * pg.stride;
@@ -2341,16 +2362,19 @@ k_bucket_count(PartGeo pg, uint32_t groups, uint32_t *table) {
        rows' index words are all in flight together (a run is ~50-250 codes, so one
        dependent chain per run would leave the CU waiting on latency; rows
        sit at fixed offsets, so a run's position needs no further load) */
-    const uint32_t sub = threadIdx.x & 3u;
-    const uint32_t quads = blockDim.x / 4, step = groups * quads;
+    /* (k = 15's 32-bit runs are ~16 codes, one 64-B piece: a lane of its own
+       per run, reading consecutive pieces) */
+    constexpr uint32_t QL = MODE == BK_C32 ? 1u : 4u;
+    const uint32_t sub = threadIdx.x & (QL - 1u);
+    const uint32_t quads = blockDim.x / QL, step = groups * quads;
     auto add16 = [&](const uint4 &v, uint64_t q, uint64_t s0, uint64_t s1) {
         const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-        for (int h = 0; h < 8; h++) {
-            const uint64_t at = q * 8 + h;
-            const uint32_t c = (w4[h >> 1] >> (16 * (h & 1))) & 0xFFFFu;
-            if (SPLIT) {   /* k = 14: this block's half of the slice */
-                if (at >= s0 && at < s1 && (c >> binsh) == half) atomicAdd(&slice[c & (nb - 1u)], 1u);
+        for (int h = 0; h < (int)CPP; h++) {
+            const uint64_t at = q * CPP + h;
+            const uint32_t c = MODE == BK_C32 ? w4[h] : (w4[h >> 1] >> (16 * (h & 1))) & 0xFFFFu;
+            if (PARTS) {   /* this block's part of the slice */
+                if (at >= s0 && at < s1 && (c >> binsh) == part) atomicAdd(&slice[c & (nb - 1u)], 1u);
             } else {
                 const uint32_t a = c & PART_SINGLE ? nb + ((c & ~PART_SINGLE) >> 2) : c;
                 if (at >= s0 && at < s1) atomicAdd(&slice[a], 1u);
@@ -2358,7 +2382,7 @@ k_bucket_count(PartGeo pg, uint32_t groups, uint32_t *table) {
         }
     };
     uint32_t en[BUCKET_ROWS];   /* the next iteration's index words, loaded with this one's codes */
-    const uint32_t r00 = g * quads + threadIdx.x / 4;
+    const uint32_t r00 = g * quads + threadIdx.x / QL;
 #pragma unroll
     for (int j = 0; j < BUCKET_ROWS; j++) en[j] = r00 + j * step < nrows ? ix[r00 + j * step] : PART_NO_RUN;
     for (uint32_t r = r00; r < nrows; r += BUCKET_ROWS * step) {
@@ -2374,24 +2398,24 @@ k_bucket_count(PartGeo pg, uint32_t groups, uint32_t *table) {
         for (int j = 0; j < BUCKET_ROWS; j++) {
             s0[j] = (uint64_t)(r + j * step) * pg.batch + (e[j] == PART_NO_RUN ? 0u : e[j] >> 16);
             s1[j] = s0[j] + run_count(e[j]);
-            const uint64_t q0 = (s0[j] >> 3) + sub, q1 = (s1[j] + 7) >> 3;
+            const uint64_t q0 = (s0[j] >> PSH) + sub, q1 = (s1[j] + CPP - 1) >> PSH;
 #pragma unroll
-            for (int u = 0; u < BUCKET_U; u++) v[j][u] = q0 + 4 * u < q1 ? g4[q0 + 4 * u] : make_uint4(0, 0, 0, 0);
+            for (int u = 0; u < BUCKET_U; u++) v[j][u] = q0 + QL * u < q1 ? g4[q0 + QL * u] : make_uint4(0, 0, 0, 0);
         }
 #pragma unroll
         for (int j = 0; j < BUCKET_ROWS; j++) {
-            const uint64_t q0 = (s0[j] >> 3) + sub, q1 = (s1[j] + 7) >> 3;
+            const uint64_t q0 = (s0[j] >> PSH) + sub, q1 = (s1[j] + CPP - 1) >> PSH;
 #pragma unroll
             for (int u = 0; u < BUCKET_U; u++)
-                if (q0 + 4 * u < q1) add16(v[j][u], q0 + 4 * u, s0[j], s1[j]);
+                if (q0 + QL * u < q1) add16(v[j][u], q0 + QL * u, s0[j], s1[j]);
             /* the rest of a long run */
-            for (uint64_t q = q0 + 4 * BUCKET_U; q < q1; q += 16) {
+            for (uint64_t q = q0 + QL * BUCKET_U; q < q1; q += 4 * QL) {
                 uint4 w[4];
 #pragma unroll
-                for (int u = 0; u < 4; u++) w[u] = q + 4 * u < q1 ? g4[q + 4 * u] : make_uint4(0, 0, 0, 0);
+                for (int u = 0; u < 4; u++) w[u] = q + QL * u < q1 ? g4[q + QL * u] : make_uint4(0, 0, 0, 0);
 #pragma unroll
                 for (int u = 0; u < 4; u++)
-                    if (q + 4 * u < q1) add16(w[u], q + 4 * u, s0[j], s1[j]);
+                    if (q + QL * u < q1) add16(w[u], q + QL * u, s0[j], s1[j]);
             }
         }
     }
@@ -2411,7 +2435,7 @@ k_bucket_count(PartGeo pg, uint32_t groups, uint32_t *table) {
     for (uint32_t i = threadIdx.x; i < nb; i += blockDim.x) {
         const uint32_t v = slice[i];
         if (!v) continue;
-        uint32_t *dst = &table[fk_sigma(((uint64_t)b << pg.sh) | ((uint64_t)half << binsh) | i)];
+        uint32_t *dst = &table[fk_sigma(((uint64_t)b << pg.sh) | ((uint64_t)part << binsh) | i)];
         if (groups == 1) *dst += v;   /* this block owns the slice */
         else atomicAdd(dst, v);
     }
@@ -3474,7 +3498,11 @@ extern "C" int fk_engine_create(int k, const fk_opts *opts, fk_engine **out) {
     if (e->opts.timing_every > 1) e->timing_every = (uint32_t)e->opts.timing_every;
     e->sparse = k > FK_K_MAX_DENSE;
     e->nbins = e->sparse ? 0 : 1ull << (2 * k);
-    e->part = k >= 8 && k <= 14;
+    /* 8 <= k <= 15 partitioned; k = 16 stays on global atomics: its 2048
+       coarse slices would need 64 parts of 2^15 bins each, and 64 blocks
+       reading every run of a slice cost more than the atomics (83 vs 64 ms
+       per G-base; k = 15's 16 parts: 23 vs 55 ms) */
+    e->part = k >= 8 && k <= 15;
     e->maskk = (1ull << (2 * k)) - 1;
     e->nshort = k > 1 && !e->sparse ? ((1ull << (2 * k)) - 4) / 3 : 0;
     if (e->opts.stream) {
@@ -3524,7 +3552,8 @@ extern "C" int fk_engine_create(int k, const fk_opts *opts, fk_engine **out) {
         hipFuncSetAttribute((const void *)k_resume<H_PAIRS>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh);
     }
     if (e->part)   /* k_bucket_count: one 2^15-bin slice + its 2^13 single bins (160 KiB) in LDS */
-        for (const void *f : {(const void *)k_bucket_count<false>, (const void *)k_bucket_count<true>})
+        for (const void *f : {(const void *)k_bucket_count<BK_PLAIN>, (const void *)k_bucket_count<BK_SPLIT>,
+                              (const void *)k_bucket_count<BK_C32>})
             hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 5 << 15);
     for (int i = 0; i < 3; i++)
         /* timing only (results travel through mapped memory): no system-scope
@@ -3800,9 +3829,11 @@ static int launch_part(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t l
     const bool pairs = k <= e->part_pairs_kmax;
     const int kb = pairs ? k + 1 : k;                      /* bits of a pair (or window) code: 2 kb */
     /* >= 64 slices, <= 2^15 bins (128 KiB) each; k = 14: 2^16 codes per slice,
-       counted as two halves (PART_BIG) */
-    pg.sh = k == 14 ? 16 : std::min(15, 2 * kb - 6);
-    pg.split = k == 14 ? 1u : 0u;
+       counted as two halves (PART_BIG); k = 15, 16: 2048 coarse slices of
+       2^19 / 2^21 32-bit codes, counted in 2^15-bin parts */
+    const bool c32 = k >= 15;   /* (k = 15: e->part stops there) */
+    pg.sh = c32 ? 2 * k - 11 : k == 14 ? 16 : std::min(15, 2 * kb - 6);
+    pg.split = c32 ? (uint32_t)(pg.sh - 15) : k == 14 ? 1u : 0u;
     pg.npair = pairs ? 1u << (2 * kb - pg.sh) : 0u;
     pg.nslices = pairs ? pg.npair : 1u << (2 * k - pg.sh);   /* singles fold into the pair slices */
     pg.pairs = pg.singles = nullptr;
@@ -3818,11 +3849,11 @@ static int launch_part(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t l
         pg.pairs = e->d_pairs;
         pg.singles = e->d_pairs + e->nbins * 4;
     }
-    pg.rounds = (uint32_t)((g.cpw * FK_CHUNK_TILES + 2) / PART_TILES(pairs) + 2);   /* rows (batches) per block */
+    pg.rounds = (uint32_t)((g.cpw * FK_CHUNK_TILES + 2) / PART_TILES3(pairs, c32) + 2);   /* rows (batches) per block */
     /* block size: 16 waves (larger batches, longer runs for k_bucket_count)
        for the 512-slice tables, else 8 (FINDKMER_TUNE part_waves=8|16 forces one) */
     const uint32_t W = part_waves_of(e);
-    pg.batch = PART_MAX_BATCH_W(W);
+    pg.batch = c32 ? W * FK_TILE_BYTES : PART_MAX_BATCH_W(W);   /* entries per row slot */
     const unsigned pgrid = (unsigned)((g.nranges + W - 1) / W);   /* the same ranges as k_count's waves */
     pg.rows = pgrid * pg.rounds;
     /* mixed tiles: ranges past their general tiles go to k_part<RES>, whose
@@ -3836,7 +3867,8 @@ static int launch_part(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t l
     if (!e->d_pflag && hipMalloc((void **)&e->d_pflag, 64) != hipSuccess) return FK_E_OOM;
     pg.flag = e->d_pflag;
     HIPCHK(hipMemsetAsync(e->d_pflag, 0, sizeof(uint32_t), e->stream));
-    const uint64_t ncodes = (uint64_t)pg.stride * pg.batch, nidx = (uint64_t)pg.nslices * pg.stride;
+    const uint64_t ncodes = (uint64_t)pg.stride * PART_ROW_BYTES(W) / sizeof(uint16_t),
+                   nidx = (uint64_t)pg.nslices * pg.stride;
     if (ncodes > e->codes_cap) {
         hipFree(e->d_codes);
         e->d_codes = nullptr;
@@ -3851,7 +3883,8 @@ static int launch_part(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t l
     }
     pg.codes = e->d_codes;
     pg.idx = e->d_pidx;
-    auto kmain = pg.split ? k_part<false, false, 16u, PART_BIG>
+    auto kmain = c32 ? k_part<false, false, 16u, PART_SM(16u), true>
+                 : pg.split ? k_part<false, false, 16u, PART_BIG>
                  : W == 16u ? (pairs ? k_part<true, false, 16u> : k_part<false, false, 16u>)
                             : (pairs ? k_part<true, false, 8u> : k_part<false, false, 8u>);
     hipExtLaunchKernelGGL(kmain, dim3(pgrid), dim3(PART_BLOCK_W(W)), 0, e->stream, tev(e, 0), tev(e, 1), 0, buf, len,
@@ -3859,7 +3892,8 @@ static int launch_part(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t l
                           e->d_state, has_init, pg, e->d_resume, exact);
     HIPCHK(hipGetLastError());
     if (mixed) {
-        auto kres = pg.split ? k_part<false, true, 16u, PART_BIG>
+        auto kres = c32 ? k_part<false, true, 16u, PART_SM(16u), true>
+                    : pg.split ? k_part<false, true, 16u, PART_BIG>
                     : W == 16u ? (pairs ? k_part<true, true, 16u> : k_part<false, true, 16u>)
                                : (pairs ? k_part<true, true, 8u> : k_part<false, true, 8u>);
         hipLaunchKernelGGL(kres, dim3(pgrid), dim3(PART_BLOCK_W(W)), 0, e->stream, buf, len, lo, e->k, e->maskk,
@@ -3872,11 +3906,14 @@ static int launch_part(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t l
     const uint32_t groups = std::max<uint32_t>(1, (uint32_t)e->cus / pg.nslices);
     if (pairs && groups > 1) HIPCHK(hipMemsetAsync(e->d_pairs, 0, e->nbins * 5 * sizeof(uint32_t), e->stream));
     const size_t bc_lds = ((size_t)1 << (pg.sh - pg.split)) * sizeof(uint32_t) * (pairs ? 5 : 4) / 4;   /* + single bins */
-    if (pg.split)
-        hipLaunchKernelGGL(k_bucket_count<true>, dim3(pg.nslices * groups << 1), dim3(1024), bc_lds, e->stream, pg,
-                           groups, e->d_table);
+    if (c32)
+        hipLaunchKernelGGL(k_bucket_count<BK_C32>, dim3(pg.nslices << pg.split), dim3(1024), bc_lds, e->stream, pg,
+                           1u, e->d_table);
+    else if (pg.split)
+        hipLaunchKernelGGL(k_bucket_count<BK_SPLIT>, dim3(pg.nslices << pg.split), dim3(1024), bc_lds, e->stream, pg,
+                           1u, e->d_table);
     else
-        hipLaunchKernelGGL(k_bucket_count<false>, dim3(pg.nslices * groups), dim3(1024), bc_lds, e->stream, pg,
+        hipLaunchKernelGGL(k_bucket_count<BK_PLAIN>, dim3(pg.nslices * groups), dim3(1024), bc_lds, e->stream, pg,
                            groups, e->d_table);
     HIPCHK(hipGetLastError());
     if (pairs) {
@@ -4269,7 +4306,9 @@ static uint64_t segment_budget(fk_engine *e, uint64_t len) {
     if (tune_knob("seg_kb", &kv) && kv)   /* tests: segments of this many KiB */
         return std::max<uint64_t>(FK_CHUNK_BYTES, (kv << 10) / FK_CHUNK_BYTES * FK_CHUNK_BYTES);
     if (!e->part) return seg;
-    const uint64_t per = 2 * sizeof(uint16_t) + 1;     /* codes + run index, bytes per input byte */
+    /* codes (two row regions) + run index, bytes per input byte: 16-bit codes
+       of 2 tiles per row, or 32-bit codes of one tile (k >= 15) */
+    const uint64_t per = e->k >= 15 ? 2 * 2 * sizeof(uint32_t) + 1 : 2 * sizeof(uint16_t) + 1;
     if (std::min(len, seg) * per <= e->codes_cap * sizeof(uint16_t)) return seg;   /* already allocated */
     size_t fr = 0, tot = 0;
     if (hipMemGetInfo(&fr, &tot) != hipSuccess) return seg;

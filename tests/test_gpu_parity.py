@@ -748,6 +748,61 @@ def test_partition_k14(kind):
     assert_same(data, 14, want_nodes=kind != "polyA", feeds=feeds)
 
 
+def _assert_same_sparse_view(data, k, feeds=None, want_nodes=True):
+    """14 <= k <= 16 (dense table): the table's nonzero bins, read in 2^28-bin
+    ranges, and every scalar vs the sparse oracle"""
+    codes, cnts, r = oracle.count_sparse(data, k, cap=len(data) + 16)
+    arr = np.frombuffer(bytes(data), dtype=np.uint8)
+    with fk.Engine(k, want_nodes=want_nodes, collect_unknown=True) as e:
+        pos = 0
+        for n in (feeds or [len(arr)]):
+            e.feed(np.ascontiguousarray(arr[pos:pos + n]))
+            pos += n
+        assert pos == len(arr)
+        rc, rg = e.finish(allow=(fk.FK_OK, fk.FK_E_EMPTY, fk.FK_E_UNTERMINATED_HEADER))
+        step = 1 << 28
+        got_c, got_n = [], []
+        for first in range(0, 1 << (2 * k), step):
+            part = e.table_range(first, min(step, (1 << (2 * k)) - first))
+            nz = np.nonzero(part)[0]
+            got_c.append(nz.astype(np.uint64) + first)
+            got_n.append(part[nz])
+        ub = e.unknown_bytes()
+    assert np.array_equal(np.concatenate(got_c), codes)
+    assert np.array_equal(np.concatenate(got_n), cnts)
+    assert (rg.windows, rg.distinct, rg.valid_bases) == (r.windows, r.distinct, r.valid_bases)
+    assert list(rg.base_count) == list(r.base_count)
+    assert list(rg.depth1) == list(r.depth1)
+    assert (rg.unknown_chars, rg.scanned_bytes, rg.hit_eof_byte) == (r.unknown_chars, r.scanned_bytes, r.hit_eof_byte)
+    if want_nodes:
+        assert rg.nodes == r.nodes
+
+
+@pytest.mark.parametrize("k", [15, 16])
+@pytest.mark.parametrize("kind", ["mixed", "dense_records", "polyA", "fasta_polyA", "acgt_feeds"])
+def test_partition_k15_and_k16(k, kind):
+    """k = 15 through the partition: 2048 coarse slices of 32-bit codes, each
+    slice counted in 16 parts of 2^15 bins (16 blocks on one XCD, each
+    keeping its part's codes); poly-A puts every entry in coarse slice 0 and
+    part 0; header-dense records send ranges to k_part<RES>.  k = 16 (global
+    atomics) on the same inputs"""
+    n = 6 << 20
+    feeds = None
+    if kind == "mixed":
+        data = mixed_input(1515 + k, n)
+    elif kind == "dense_records":
+        data = _dense_records(1516 + k, n)
+    elif kind == "polyA":
+        data = b"A" * n
+    elif kind == "fasta_polyA":
+        line = b"A" * 60 + b"\n"
+        data = b">x\n" + line * (n // len(line))
+    else:
+        data = oracle.synth(n, k, 80).tobytes()
+        feeds = [1_000_003, 17, 65_536, len(data) - 1_065_556]
+    _assert_same_sparse_view(data, k, feeds, want_nodes=kind != "polyA")
+
+
 def _long_header_input(seed, n):
     """ACGT runs with '>' lines longer than the 256-byte halo, so ranges
     start inside a header their halo cannot see the start of (the one-pass
