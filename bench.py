@@ -276,7 +276,7 @@ def measure(ctx, k, n, L, seed, chrom, steps, warmup, verify=False):
     algo_bytes = nbytes + 4 * (1 << (2 * k))       # input read once + u32 table written once
     achieved = algo_bytes / (kern_ms * 1e-3) / 1e9 if kern_ms > 0 else 0.0   # 0: events off (FINDKMER_TUNE events=0)
     step_gbs = algo_bytes / (ms_step * 1e-3) / 1e9
-    main = "k_part" if 8 <= k <= 15 else "k_count"
+    main = "k_part" if 8 <= k <= 16 else "k_count"
     rec = {
         "value": world * n / (dt / steps),
         "ms_per_step": ms_step,

@@ -2317,20 +2317,20 @@ k_part(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint
 /* MODE (a template parameter, so that the hot loop of the common k carries
    no test of it: a runtime flag there cost ~0.9 ms of a k=11 10 GB step):
    BK_PLAIN 16-bit codes, one block per slice (and row group);
-   BK_SPLIT k = 14: 16-bit codes, a slice counted as 2^(pg.split) parts of
-            2^15 bins, one block each;
-   BK_C32   k = 15, 16: 32-bit codes under 2048 coarse slices, each counted
-            as 2^(pg.split) parts of 2^15 bins.
-   A part block keeps only its codes; the parts of a slice run on one XCD
-   one after another, so all but the first read the slice's codes from L2. */
-enum { BK_PLAIN = 0, BK_SPLIT = 1, BK_C32 = 2 };
+   BK_SPLIT k = 14: a slice counted as 2^(pg.split) parts of 2^15 bins, one
+            block each, keeping only its part's codes; the parts of a slice
+            run on one XCD one after another, so all but the first read the
+            slice's codes from L2.  (Counting k = 15's 32-bit coarse slices
+            the same way, 16 parts each, took 21.7 ms per G-base; the second
+            partition level, k_repart, takes 16.3.) */
+enum { BK_PLAIN = 0, BK_SPLIT = 1 };
 template <int MODE>
 __global__ void __launch_bounds__(1024)
 k_bucket_count(PartGeo pg, uint32_t groups, uint32_t *table) {
     extern __shared__ uint32_t slice[];
     constexpr bool PARTS = MODE != BK_PLAIN;
-    constexpr uint32_t CPP = MODE == BK_C32 ? 4u : 8u;     /* codes per 16-B piece */
-    constexpr uint32_t PSH = MODE == BK_C32 ? 2u : 3u;
+    constexpr uint32_t CPP = 8u;   /* 16-bit codes per 16-B piece */
+    constexpr uint32_t PSH = 3u;
     const uint32_t binsh = PARTS ? 15u : pg.sh;
     const uint32_t nb = 1u << binsh;
     /* pairs mode: the slice's 2^sh pair bins, then the 2^(sh-2) bins of the
@@ -2362,9 +2362,7 @@ k_bucket_count(PartGeo pg, uint32_t groups, uint32_t *table) {
        rows' index words are all in flight together (a run is ~50-250 codes, so one
        dependent chain per run would leave the CU waiting on latency; rows
        sit at fixed offsets, so a run's position needs no further load) */
-    /* (k = 15's 32-bit runs are ~16 codes, one 64-B piece: a lane of its own
-       per run, reading consecutive pieces) */
-    constexpr uint32_t QL = MODE == BK_C32 ? 1u : 4u;
+    constexpr uint32_t QL = 4u;   /* lanes per run */
     const uint32_t sub = threadIdx.x & (QL - 1u);
     const uint32_t quads = blockDim.x / QL, step = groups * quads;
     auto add16 = [&](const uint4 &v, uint64_t q, uint64_t s0, uint64_t s1) {
@@ -2372,7 +2370,7 @@ k_bucket_count(PartGeo pg, uint32_t groups, uint32_t *table) {
 #pragma unroll
         for (int h = 0; h < (int)CPP; h++) {
             const uint64_t at = q * CPP + h;
-            const uint32_t c = MODE == BK_C32 ? w4[h] : (w4[h >> 1] >> (16 * (h & 1))) & 0xFFFFu;
+            const uint32_t c = (w4[h >> 1] >> (16 * (h & 1))) & 0xFFFFu;
             if (PARTS) {   /* this block's part of the slice */
                 if (at >= s0 && at < s1 && (c >> binsh) == part) atomicAdd(&slice[c & (nb - 1u)], 1u);
             } else {
@@ -2438,6 +2436,105 @@ k_bucket_count(PartGeo pg, uint32_t groups, uint32_t *table) {
         uint32_t *dst = &table[fk_sigma(((uint64_t)b << pg.sh) | ((uint64_t)part << binsh) | i)];
         if (groups == 1) *dst += v;   /* this block owns the slice */
         else atomicAdd(dst, v);
+    }
+}
+
+/*
+ * k = 15, 16: the second partition level.  k_part leaves each of the 2048
+ * coarse slices as runs of 32-bit codes (low 2k - 11 index bits) in every
+ * batch row; a slice holds 2^(2k-26) parts of 2^15 bins (16 at k = 15, 64 at
+ * k = 16).  k_repart (one block per coarse slice) reads the slice's runs
+ * twice -- counting its entries per part, then writing each entry's low 15
+ * bits as a 16-bit code into its part's contiguous stream -- after taking the
+ * slice's region of the output with one global atomic.  k_count_parts (one
+ * block per part) then reads one contiguous stream into 2^15 LDS bins and
+ * adds them to the table: every code is read from HBM once per level.
+ */
+struct PartMeta {
+    unsigned long long off;   /* first code of the part's stream (a multiple of 8) */
+    uint32_t n, pad;
+};
+#define REPART_MAXP 64u
+
+__global__ void __launch_bounds__(1024)
+k_repart(PartGeo pg, uint16_t *out, unsigned long long *alloc, PartMeta *meta) {
+    __shared__ uint32_t cnt[16][REPART_MAXP], cur[REPART_MAXP];
+    __shared__ unsigned long long poff[REPART_MAXP];
+    const uint32_t b = blockIdx.x, t = threadIdx.x, wv = t >> 6;
+    const uint32_t np = 1u << pg.split;
+    for (uint32_t i = t; i < 16u * REPART_MAXP; i += blockDim.x) (&cnt[0][0])[i] = 0;
+    __syncthreads();
+    const uint32_t *ix = pg.idx + (size_t)b * pg.stride;
+    const uint32_t nrows = pg.flag && *pg.flag ? 2u * pg.rows : pg.rows;
+    const uint4 *g4 = reinterpret_cast<const uint4 *>(pg.codes);
+    /* a lane per run, its codes as 16-B pieces (4 codes each) */
+    auto each_code = [&](uint32_t r, auto &&f) {
+        const uint32_t e = ix[r];
+        if (e == PART_NO_RUN) return;
+        const uint64_t s0 = (uint64_t)r * pg.batch + (e >> 16), s1 = s0 + run_count(e);
+        for (uint64_t q = s0 >> 2; q < (s1 + 3) >> 2; q++) {
+            const uint4 v = g4[q];
+            const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int h = 0; h < 4; h++)
+                if (q * 4 + h >= s0 && q * 4 + h < s1) f(w4[h]);
+        }
+    };
+    /* pass A: entries per part (per-wave counters: fewer same-address atomics) */
+    for (uint32_t r = t; r < nrows; r += blockDim.x)
+        each_code(r, [&](uint32_t c) { atomicAdd(&cnt[wv][c >> 15], 1u); });
+    __syncthreads();
+    if (t < 64) {   /* part totals, their 8-aligned prefix, the slice's region */
+        uint32_t n = 0;
+        if (t < np)
+            for (uint32_t w = 0; w < 16; w++) n += cnt[w][t];
+        const uint32_t sz = (n + 7u) & ~7u;
+        const uint32_t inc = wscan_incl32(sz);
+        const uint32_t tot = rdlane(inc, 63);
+        unsigned long long b0 = 0;
+        if (t == 0) b0 = atomicAdd(alloc, (unsigned long long)tot);
+        b0 = rdlane64(b0, 0);
+        if (t < np) {
+            cur[t] = 0;
+            poff[t] = b0 + inc - sz;
+            meta[(size_t)b * np + t] = PartMeta{b0 + inc - sz, n, 0};
+        }
+    }
+    __syncthreads();
+    /* pass B: every entry's low 15 bits into its part's stream */
+    for (uint32_t r = t; r < nrows; r += blockDim.x)
+        each_code(r, [&](uint32_t c) {
+            const uint32_t p = c >> 15;
+            /* one cursor per part for the whole block: its waves' entries
+               land next to each other (per-wave cursors, 16 x more write
+               streams, made this kernel 2 x slower) */
+            const uint32_t at = atomicAdd(&cur[p], 1u);
+            out[poff[p] + at] = (uint16_t)(c & 0x7FFFu);
+        });
+}
+
+/* one block per part: its stream into 2^15 LDS bins, then into the table */
+__global__ void __launch_bounds__(1024)
+k_count_parts(PartGeo pg, const uint16_t *in, const PartMeta *meta, uint32_t *table) {
+    extern __shared__ uint32_t slice[];
+    const uint32_t np = 1u << pg.split;
+    const uint32_t b = blockIdx.x / np, part = blockIdx.x % np;
+    for (uint32_t i = threadIdx.x; i < (1u << 15); i += blockDim.x) slice[i] = 0;
+    __syncthreads();
+    const PartMeta m = meta[blockIdx.x];
+    const uint4 *g4 = reinterpret_cast<const uint4 *>(in + m.off);   /* 16-B aligned: off % 8 == 0 */
+    const uint32_t nq = (m.n + 7u) >> 3;
+    for (uint32_t q = threadIdx.x; q < nq; q += blockDim.x) {
+        const uint4 v = g4[q];
+        const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int h = 0; h < 8; h++)
+            if (q * 8u + (uint32_t)h < m.n) atomicAdd(&slice[(w4[h >> 1] >> (16 * (h & 1))) & 0x7FFFu], 1u);
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < (1u << 15); i += blockDim.x) {
+        const uint32_t v = slice[i];
+        if (v) table[fk_sigma(((uint64_t)b << pg.sh) | ((uint64_t)part << 15) | i)] += v;   /* the block owns it */
     }
 }
 
@@ -3191,6 +3288,9 @@ struct fk_engine {
     uint32_t *d_pidx = nullptr;               /* k_part: slice-major run index */
     uint64_t codes_cap = 0, pidx_cap = 0;
     uint32_t *d_pairs = nullptr;              /* k_part pairs mode: 4^(k+1) pair bins + 4^k single bins */
+    uint16_t *d_parts = nullptr;              /* k = 15, 16: the second level's part streams (k_repart) */
+    uint64_t parts_cap = 0;
+    void *d_pmeta = nullptr;                  /* k = 15, 16: PartMeta per part + the allocation counter */
     uint64_t pair_cap = 0;
     int part_pairs_kmax = 11;                 /* pairs mode for k <= this */
     uint32_t general_tiles = FK_COUNT_GENERAL_TILES;   /* per range in k_count */
@@ -3404,6 +3504,7 @@ extern "C" void fk_engine_destroy(fk_engine *e) {
     if (e->stream) hipStreamSynchronize(e->stream);
     hipFree(e->d_table); hipFree(e->d_short); hipFree(e->d_sub); hipFree(e->d_snap);
     hipFree(e->d_pairs);
+    hipFree(e->d_parts); hipFree(e->d_pmeta);
     hipFree(e->d_codes); hipFree(e->d_pidx); hipFree(e->d_pflag); hipFree(e->d_acc); hipFree(e->d_res); hipFree(e->d_tmp);
     hipFree(e->d_state); hipFree(e->d_rr); hipFree(e->d_rtrue);
     hipFree(e->d_redo); hipFree(e->d_tf); hipFree(e->d_stage); hipFree(e->d_resume);
@@ -3498,11 +3599,8 @@ extern "C" int fk_engine_create(int k, const fk_opts *opts, fk_engine **out) {
     if (e->opts.timing_every > 1) e->timing_every = (uint32_t)e->opts.timing_every;
     e->sparse = k > FK_K_MAX_DENSE;
     e->nbins = e->sparse ? 0 : 1ull << (2 * k);
-    /* 8 <= k <= 15 partitioned; k = 16 stays on global atomics: its 2048
-       coarse slices would need 64 parts of 2^15 bins each, and 64 blocks
-       reading every run of a slice cost more than the atomics (83 vs 64 ms
-       per G-base; k = 15's 16 parts: 23 vs 55 ms) */
-    e->part = k >= 8 && k <= 15;
+    /* 8 <= k <= 16 partitioned (k = 15, 16 with a second level, k_repart) */
+    e->part = k >= 8 && k <= 16;
     e->maskk = (1ull << (2 * k)) - 1;
     e->nshort = k > 1 && !e->sparse ? ((1ull << (2 * k)) - 4) / 3 : 0;
     if (e->opts.stream) {
@@ -3553,7 +3651,7 @@ extern "C" int fk_engine_create(int k, const fk_opts *opts, fk_engine **out) {
     }
     if (e->part)   /* k_bucket_count: one 2^15-bin slice + its 2^13 single bins (160 KiB) in LDS */
         for (const void *f : {(const void *)k_bucket_count<BK_PLAIN>, (const void *)k_bucket_count<BK_SPLIT>,
-                              (const void *)k_bucket_count<BK_C32>})
+                              (const void *)k_count_parts})
             hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 5 << 15);
     for (int i = 0; i < 3; i++)
         /* timing only (results travel through mapped memory): no system-scope
@@ -3831,7 +3929,7 @@ static int launch_part(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t l
     /* >= 64 slices, <= 2^15 bins (128 KiB) each; k = 14: 2^16 codes per slice,
        counted as two halves (PART_BIG); k = 15, 16: 2048 coarse slices of
        2^19 / 2^21 32-bit codes, counted in 2^15-bin parts */
-    const bool c32 = k >= 15;   /* (k = 15: e->part stops there) */
+    const bool c32 = k >= 15;
     pg.sh = c32 ? 2 * k - 11 : k == 14 ? 16 : std::min(15, 2 * kb - 6);
     pg.split = c32 ? (uint32_t)(pg.sh - 15) : k == 14 ? 1u : 0u;
     pg.npair = pairs ? 1u << (2 * kb - pg.sh) : 0u;
@@ -3906,10 +4004,29 @@ static int launch_part(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t l
     const uint32_t groups = std::max<uint32_t>(1, (uint32_t)e->cus / pg.nslices);
     if (pairs && groups > 1) HIPCHK(hipMemsetAsync(e->d_pairs, 0, e->nbins * 5 * sizeof(uint32_t), e->stream));
     const size_t bc_lds = ((size_t)1 << (pg.sh - pg.split)) * sizeof(uint32_t) * (pairs ? 5 : 4) / 4;   /* + single bins */
-    if (c32)
-        hipLaunchKernelGGL(k_bucket_count<BK_C32>, dim3(pg.nslices << pg.split), dim3(1024), bc_lds, e->stream, pg,
-                           1u, e->d_table);
-    else if (pg.split)
+    if (c32) {
+        /* the second partition level: each coarse slice's runs into one
+           contiguous 16-bit stream per part, then one block per part */
+        const uint64_t nparts = (uint64_t)pg.nslices << pg.split;
+        const uint64_t need = len + 8 * nparts + 16;   /* (entries <= bytes; 8-aligned parts) */
+        if (need > e->parts_cap) {
+            hipFree(e->d_parts);
+            e->d_parts = nullptr;
+            e->parts_cap = 0;
+            if (hipMalloc((void **)&e->d_parts, need * sizeof(uint16_t)) != hipSuccess) return FK_E_OOM;
+            e->parts_cap = need;
+        }
+        if (!e->d_pmeta &&
+            hipMalloc(&e->d_pmeta, (size_t)2048 * REPART_MAXP * sizeof(PartMeta) + 64) != hipSuccess)
+            return FK_E_OOM;
+        PartMeta *meta = static_cast<PartMeta *>(e->d_pmeta);
+        unsigned long long *alloc = reinterpret_cast<unsigned long long *>(meta + (size_t)2048 * REPART_MAXP);
+        HIPCHK(hipMemsetAsync(alloc, 0, sizeof(unsigned long long), e->stream));
+        hipLaunchKernelGGL(k_repart, dim3(pg.nslices), dim3(1024), 0, e->stream, pg, e->d_parts, alloc, meta);
+        HIPCHK(hipGetLastError());
+        hipLaunchKernelGGL(k_count_parts, dim3((unsigned)nparts), dim3(1024), (size_t)1 << 17, e->stream, pg,
+                           (const uint16_t *)e->d_parts, (const PartMeta *)meta, e->d_table);
+    } else if (pg.split)
         hipLaunchKernelGGL(k_bucket_count<BK_SPLIT>, dim3(pg.nslices << pg.split), dim3(1024), bc_lds, e->stream, pg,
                            1u, e->d_table);
     else
@@ -4308,7 +4425,7 @@ static uint64_t segment_budget(fk_engine *e, uint64_t len) {
     if (!e->part) return seg;
     /* codes (two row regions) + run index, bytes per input byte: 16-bit codes
        of 2 tiles per row, or 32-bit codes of one tile (k >= 15) */
-    const uint64_t per = e->k >= 15 ? 2 * 2 * sizeof(uint32_t) + 1 : 2 * sizeof(uint16_t) + 1;
+    const uint64_t per = e->k >= 15 ? 2 * 2 * sizeof(uint32_t) + 2 + 1 : 2 * sizeof(uint16_t) + 1;   /* (+ the part streams) */
     if (std::min(len, seg) * per <= e->codes_cap * sizeof(uint16_t)) return seg;   /* already allocated */
     size_t fr = 0, tot = 0;
     if (hipMemGetInfo(&fr, &tot) != hipSuccess) return seg;

@@ -781,11 +781,12 @@ def _assert_same_sparse_view(data, k, feeds=None, want_nodes=True):
 @pytest.mark.parametrize("k", [15, 16])
 @pytest.mark.parametrize("kind", ["mixed", "dense_records", "polyA", "fasta_polyA", "acgt_feeds"])
 def test_partition_k15_and_k16(k, kind):
-    """k = 15 through the partition: 2048 coarse slices of 32-bit codes, each
-    slice counted in 16 parts of 2^15 bins (16 blocks on one XCD, each
-    keeping its part's codes); poly-A puts every entry in coarse slice 0 and
-    part 0; header-dense records send ranges to k_part<RES>.  k = 16 (global
-    atomics) on the same inputs"""
+    """k = 15, 16 through the two-level partition: k_part's 2048 coarse
+    slices of 32-bit codes, k_repart splitting each into 16 / 64 contiguous
+    16-bit part streams, k_count_parts counting each part in 2^15 LDS bins;
+    poly-A puts every entry into coarse slice 0 and part 0 (one k_repart
+    block takes the whole input); header-dense records send ranges to
+    k_part<RES>"""
     n = 6 << 20
     feeds = None
     if kind == "mixed":

@@ -3,6 +3,10 @@ patches, as build/exp/libfk_<name>.so for an A/B run through FINDKMER_LIB
 (bench.py and findkmer_amd load it instead of the product library).
 
 usage: python3 tools/exp_variant.py NAME [NAME ...]    (run `make` first)
+
+Each variant's patches target the source as it was when that experiment ran
+(DESIGN.md records the outcomes); later edits can make an old one fail to
+apply, which the build reports.
 """
 import os
 import subprocess
@@ -43,6 +47,50 @@ VARIANTS = {
         ("    const uint32_t b = groups == 1 && (pg.nslices & 7u) == 0 ? (bx & 7u) * (pg.nslices >> 3) + (bx >> 3)\n"
          "                                                           : bx % pg.nslices;",
          "    const uint32_t b = bx % pg.nslices;"),
+    ],
+    # k_bucket_count: the run bounds of a 16-B piece as an 8-bit mask (32-bit
+    # arithmetic once per piece instead of two 64-bit compares per code)
+    "mask8": [
+        ("""        const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int h = 0; h < 8; h++) {
+            const uint64_t at = q * 8 + h;
+            const uint32_t c = (w4[h >> 1] >> (16 * (h & 1))) & 0xFFFFu;
+            if (SPLIT) {   /* k = 14: this block's half of the slice */
+                if (at >= s0 && at < s1 && (c >> binsh) == half) atomicAdd(&slice[c & (nb - 1u)], 1u);
+            } else {
+                const uint32_t a = c & PART_SINGLE ? nb + ((c & ~PART_SINGLE) >> 2) : c;
+                if (at >= s0 && at < s1) atomicAdd(&slice[a], 1u);
+            }
+        }""",
+         """        const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+        const uint64_t q8 = q * 8;
+        const uint32_t lo = s0 > q8 ? (uint32_t)min(s0 - q8, (uint64_t)8) : 0u;
+        const uint32_t hi = s1 > q8 ? (uint32_t)min(s1 - q8, (uint64_t)8) : 0u;
+        const uint32_t m = ((1u << hi) - 1u) & ~((1u << lo) - 1u);
+#pragma unroll
+        for (int h = 0; h < 8; h++) {
+            const uint32_t c = (w4[h >> 1] >> (16 * (h & 1))) & 0xFFFFu;
+            const bool in = (m >> h) & 1u;
+            if (SPLIT) {   /* k = 14: this block's half of the slice */
+                if (in && (c >> binsh) == half) atomicAdd(&slice[c & (nb - 1u)], 1u);
+            } else {
+                const uint32_t a = c & PART_SINGLE ? nb + ((c & ~PART_SINGLE) >> 2) : c;
+                if (in) atomicAdd(&slice[a], 1u);
+            }
+        }"""),
+    ],
+    # k_part: four tiles in flight per wave instead of three (the batch's
+    # barriers wait on the slowest wave's loads)
+    "pre4": [
+        ("    uint32_t A[8] = {}, B[8] = {}, C[8] = {};\n    asm volatile(\"\" ::: \"memory\");\n    FK_LOADP(A, t);",
+         "    uint32_t A[8] = {}, B[8] = {}, C[8] = {}, D[8] = {};\n    asm volatile(\"\" ::: \"memory\");\n    FK_LOADP(A, t);"),
+        ("    FK_LOADP(C, t + 2);\n    /* entering state: the known stream state for chunk 0, else a guess from\n       the halo (k_scan checks it",
+         "    FK_LOADP(C, t + 2);\n    asm volatile(\"\" ::: \"memory\");\n    FK_LOADP(D, t + 3);\n    /* entering state: the known stream state for chunk 0, else a guess from\n       the halo (k_scan checks it"),
+        ("        FK_LOADP(X, t + 2);                                                          \\\n        {   /* static stash slots",
+         "        FK_LOADP(X, t + 3);                                                          \\\n        {   /* static stash slots"),
+        ("        FK_ROUND(A);\n        FK_ROUND(B);\n        FK_ROUND(C);\n    }\n#undef FK_ROUND\n#undef FK_LOADP\n    /* rows the block",
+         "        FK_ROUND(A);\n        FK_ROUND(B);\n        FK_ROUND(C);\n        FK_ROUND(D);\n    }\n#undef FK_ROUND\n#undef FK_LOADP\n    /* rows the block"),
     ],
 }
 

@@ -38,7 +38,7 @@ out = os.path.join(repo, "profiles")
 os.makedirs(out, exist_ok=True)
 
 # k_part's template: <PAIRS, RES, W>; pairs mode for k <= 11, single windows for k = 12, 13
-main = args.kernel or ("k_part<true, false" if 8 <= k <= 11 else "k_part<false, false" if 12 <= k <= 15
+main = args.kernel or ("k_part<true, false" if 8 <= k <= 11 else "k_part<false, false" if 12 <= k <= 16
                        else "k_count<")
 main_short = main.split("<")[0]
 
