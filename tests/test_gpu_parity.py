@@ -271,9 +271,10 @@ def test_int32_seqsize_two_zones():
 
 
 @pytest.mark.parametrize("k,split,extra", [(11, 0, 1 << 22), (11, 0, 1 << 28), (11, 1 << 20, 1 << 28),
-                                           (12, 0, 1 << 28), (8, 1 << 20, 1 << 28)])
+                                           (12, 0, 1 << 28), (8, 1 << 20, 1 << 28), (14, 0, 1 << 28),
+                                           (15, 1 << 20, 1 << 28)])
 def test_int32_zone_partitioned(k, split, extra):
-    """8 <= k <= 12 on one run of random bases past 2^31-1 (the reference's
+    """8 <= k <= 15 on one run of random bases past 2^31-1 (the reference's
     int32 seqSize turns negative, findKmer.cpp:977): no windows in the zone,
     so the table is the table of the run's first 2^31-1 bases.  Most range
     guesses are wrong there, and the partitioned path recounts the segment
