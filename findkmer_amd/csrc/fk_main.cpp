@@ -478,8 +478,12 @@ static int run_k(int argc) {
         struct stat sb;
         const uint64_t fsize = stat(config.sequence_file, &sb) == 0 ? (uint64_t)sb.st_size : 0;
         const int kk = sweep_kmax > config.k ? sweep_kmax : config.k;
-        const uint64_t per = kk > FK_K_MAX_DENSE ? 3 : (kk >= 8 ? 4 : 2);
-        int dsel = fk_device_select(fsize * per + (256ull << 20), &g_device);
+        /* bytes per input byte: the file + partition codes (16-bit: 2 per
+           region; 32-bit for k = 15, 16: 8, + 2 of part streams), or for
+           k >= 17 the engine's copy of the input; plus the dense table */
+        const uint64_t per = kk > FK_K_MAX_DENSE ? 3 : kk >= 15 ? 11 : (kk >= 8 ? 4 : 2);
+        const uint64_t table = kk > FK_K_MAX_DENSE ? 0 : 4ull << (2 * kk);
+        int dsel = fk_device_select(fsize * per + table + (256ull << 20), &g_device);
         if (dsel == FK_E_INVALID) {
             fprintf(stderr, "findKmer: FINDKMER_DEVICE names no visible GPU\n");
             exit(EXIT_FAILURE);
