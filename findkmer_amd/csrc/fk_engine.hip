@@ -2098,18 +2098,68 @@ __device__ __forceinline__ bool part_batch(const Ctx &cx, const PartGeo &pg, con
     return any_more;
 }
 
+/*
+ * Pipelined batches (PIPE: the main pass of tables of at most 512 slices,
+ * whose scan wave 0 runs alone).  part_batch runs its phases one after
+ * another on every wave -- tiles (VALU), histogram atomics, barrier, scan,
+ * barrier, placement atomics (LDS), barrier, write-out -- so the CU's VALU
+ * idles while its LDS works and the other way round.  Here batch j's
+ * entries are placed while the waves count batch j+1's tiles: each round a
+ * wave counts one tile, adds its entries to the histogram of batch j+1 and
+ * places the entries of the tile it stashed in the same slot during batch j
+ * (every tile of a batch sits in its own stash slot, so one stash serves
+ * both batches).  At the end of a batch's tiles, one barrier (batch j's
+ * placement and batch j+1's histogram done), then wave 0 scans batch j+1's
+ * histogram (cursors, run index, total) while the other waves write batch j
+ * out, then a second barrier: two barriers per batch instead of three, and
+ * the tiles' VALU work overlaps the placement atomics across the waves.
+ */
+__device__ __forceinline__ void part_scan_w0(const PartGeo &pg, uint32_t row, uint32_t *hist, uint32_t *cur,
+                                             uint32_t *tot) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t per = (pg.nslices + 63) / 64;
+    uint32_t sum = 0;
+    for (uint32_t j = 0; j < per; j++) {
+        const uint32_t b = lane * per + j;
+        if (b < pg.nslices) sum += hist[b];
+    }
+    const uint32_t inc = wscan_incl32(sum);
+    uint32_t run = inc - sum;
+    for (uint32_t j = 0; j < per; j++) {
+        const uint32_t b = lane * per + j;
+        if (b < pg.nslices) {
+            const uint32_t c = hist[b];
+            cur[b] = run;
+            pg.idx[(size_t)b * pg.stride + row] = run_word(run, c);
+            hist[b] = 0;
+            run += c;
+        }
+    }
+    if (lane == 63) *tot = inc;
+}
+
+template <uint32_t W>
+__device__ __forceinline__ void part_writeout(const PartGeo &pg, uint32_t row, uint32_t total, const uint16_t *ent,
+                                              uint32_t t0, uint32_t nt) {
+    const uint32_t n8 = (total * (uint32_t)sizeof(uint16_t) + 15u) >> 4;
+    uint4 *dst = reinterpret_cast<uint4 *>(reinterpret_cast<uint8_t *>(pg.codes) + (size_t)row * PART_ROW_BYTES(W));
+    const uint4 *src = reinterpret_cast<const uint4 *>(ent);
+    for (uint32_t i = t0; i < n8; i += nt) dst[i] = src[i];
+}
+
 /* RES = false: the main pass.  With mixed tiles on, a range that needs more
  * than pg.general general tiles stops there (ResumeRec) and
  * RES = true -- the same blocks and ranges, their rows in region 2 -- counts
  * the rest of it, each tile fast, mixed (the masked entries of tile_mixed)
  * or general.  Two kernels: tile_mixed's registers stay out of the main
  * pass.  k_part<RES> returns at once unless some range stopped. */
-template <bool PAIRS, bool RES, uint32_t W, uint32_t SM = PART_SM(W), bool C32 = false>
+template <bool PAIRS, bool RES, uint32_t W, uint32_t SM = PART_SM(W), bool C32 = false, bool PIPE = false>
 __global__ void __launch_bounds__(PART_BLOCK_W(W), 4) /* 4 waves per SIMD (<= 128 VGPRs): 16 waves per CU */
 k_part(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint32_t *table,
        uint32_t *shortcnt, unsigned long long *acc, DevRes *res, RangeRec *rr, uint64_t nchunks, uint64_t cpw,
        const XState *d_init, int has_init, PartGeo pg, ResumeRec *resume, const XState *exact) {
-    __shared__ uint32_t hist[SM], cur[SM > 2048u ? SM / 2u : SM], total, scr[W];
+    static_assert(!PIPE || (!RES && !C32 && SM <= 2048u), "PIPE: the main pass, 16-bit codes, unpacked cursors");
+    __shared__ uint32_t hist[SM], cur[SM > 2048u ? SM / 2u : SM], total, scr[W], tot[2];
     using CT = typename std::conditional<C32, uint32_t, uint16_t>::type;
     __shared__ __attribute__((aligned(16))) CT ent[PART_ROW_BYTES(W) / sizeof(CT)];
     if (RES && *(volatile uint32_t *)pg.flag == 0) return;   /* uniform: no range stopped */
@@ -2199,6 +2249,9 @@ k_part(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint
         stash[i] = Emit{0, 0, 0, 0, false, false, false};
         have_stash[i] = false;
     }
+    /* PIPE: the codes of an entry and its placement (unpacked cursors) */
+    const uint32_t mk = (uint32_t)maskk, m1 = (mk << 2) | 3u, lowm = (1u << pg.sh) - 1u;
+    auto place = [&](uint32_t b, uint32_t low) { ent[atomicAdd(&cur[b], 1u)] = (CT)low; };
     __syncthreads();
 #define FK_ROUND(X)                                                                  \
     {                                                                                \
@@ -2230,7 +2283,39 @@ k_part(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint
         }                                                                            \
         consume(X);                                                                  \
         FK_LOADP(X, t + 2);                                                          \
-        {   /* static stash slots (no dynamic register indexing) */                 \
+        if (PIPE) {   /* batch j+1's histogram, batch j's placement (see part_scan_w0) */ \
+            const uint32_t ph_ = round % NT;                                         \
+            if (have) part_entries<PAIRS, false>(em, mk, m1, pg.sh, lowm, pg.npair,   \
+                                                 [&](uint32_t b_, uint32_t) { atomicAdd(&hist[b_], 1u); }); \
+            Emit old_ = stash[0];                                                    \
+            bool hold_ = have_stash[0];                                              \
+            _Pragma("unroll") for (uint32_t i_ = 1; i_ < NT; i_++) if (ph_ == i_) {  \
+                old_ = stash[i_];                                                    \
+                hold_ = have_stash[i_];                                              \
+            }                                                                        \
+            if (hold_) part_entries<PAIRS, false>(old_, mk, m1, pg.sh, lowm, pg.npair, place); \
+            _Pragma("unroll") for (uint32_t i_ = 0; i_ < NT; i_++) if (ph_ == i_) {  \
+                stash[i_] = em;                                                      \
+                have_stash[i_] = have;                                               \
+            }                                                                        \
+            if (ph_ == NT - 1) {                                                     \
+                const uint32_t j_ = round / NT;                                      \
+                const bool more_ = __syncthreads_or(!done);                          \
+                if (threadIdx.x < 64) part_scan_w0(pg, row0 + j_, hist, cur, &tot[j_ & 1u]); \
+                else if (j_ > 0) part_writeout<W>(pg, row0 + j_ - 1, tot[(j_ - 1) & 1u], (const uint16_t *)ent, \
+                                                  threadIdx.x - 64u, PART_BLOCK_W(W) - 64u); \
+                __syncthreads();                                                     \
+                if (!more_ || j_ + 1 >= pg.rounds) {                                 \
+                    /* the last batch: placed, then written out */                  \
+                    _Pragma("unroll") for (uint32_t i_ = 0; i_ < NT; i_++)           \
+                        if (have_stash[i_]) part_entries<PAIRS, false>(stash[i_], mk, m1, pg.sh, lowm, pg.npair, place); \
+                    __syncthreads();                                                 \
+                    part_writeout<W>(pg, row0 + j_, tot[j_ & 1u], (const uint16_t *)ent, threadIdx.x, PART_BLOCK_W(W)); \
+                    round++;                                                         \
+                    break;                                                           \
+                }                                                                    \
+            }                                                                        \
+        } else {   /* static stash slots (no dynamic register indexing) */          \
             const uint32_t ph_ = round % NT;                                         \
             _Pragma("unroll") for (uint32_t i_ = 0; i_ < NT; i_++) if (ph_ == i_) {  \
                 stash[i_] = em;                                                      \
@@ -3308,6 +3393,7 @@ struct fk_engine {
     bool no_mixed = false;                    /* FINDKMER_TUNE no_mixed=1: no mixed tiles (general byte walk) */
     uint32_t part_general = 1;                /* k_part: general tiles per range (FINDKMER_TUNE part_general) */
     uint32_t part_waves = 0;                  /* k_part: waves per block (FINDKMER_TUNE part_waves; 0 = by k) */
+    bool part_pipe = true;                    /* k_part: pipelined batches (FINDKMER_TUNE part_pipe=0: off) */
     uint32_t static_pct = 100;                /* k <= 7: % of a large segment in static ranges (FINDKMER_TUNE static_pct;
                                                  100 = no dynamic ranges: on a plain stream the waves that
                                                  finish early hand their bandwidth to the others, so
@@ -3581,7 +3667,8 @@ extern "C" int fk_engine_create(int k, const fk_opts *opts, fk_engine **out) {
        (tune_knob): no_mixed=1 (tile_general instead of mixed tiles),
        part_general=N (general tiles k_part takes per range before
        k_part<RES>), static_pct=P / dyn_min_chunks=N (k_count's dynamic
-       ranges), part_waves=8|16 (k_part block size), events=0 (no HIP events),
+       ranges), part_waves=8|16 (k_part block size), part_pipe=0 (k_part
+       without pipelined batches), events=0 (no HIP events),
        seg_kb=N (device feeds cut into N-KiB segments), sp_pass=N (17 <= k:
        at most N window keys per sorted pass; smaller buckets merge, larger
        ones take the dense path) */
@@ -3591,6 +3678,7 @@ extern "C" int fk_engine_create(int k, const fk_opts *opts, fk_engine **out) {
        isolated comment line) and leaves denser ones to k_resume's mixed tiles */
     if (!e->no_mixed) e->general_tiles = 2;
     if (tune_knob("part_waves", &kv)) e->part_waves = kv == 8u || kv == 16u ? (uint32_t)kv : 0u;
+    if (tune_knob("part_pipe", &kv)) e->part_pipe = kv != 0;
     if (tune_knob("part_general", &kv)) e->part_general = (uint32_t)kv;
     if (tune_knob("events", &kv)) e->timing = kv != 0;
     if (tune_knob("static_pct", &kv)) e->static_pct = (uint32_t)std::min<uint64_t>(100u, std::max<uint64_t>(1u, kv));
@@ -3981,10 +4069,14 @@ static int launch_part(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t l
     }
     pg.codes = e->d_codes;
     pg.idx = e->d_pidx;
+    /* the pipelined main pass where wave 0 scans the slices alone (<= 512) */
+    const bool pipe = e->part_pipe && !c32 && !pg.split && pg.nslices <= 512u;
     auto kmain = c32 ? k_part<false, false, 16u, PART_SM(16u), true>
                  : pg.split ? k_part<false, false, 16u, PART_BIG>
-                 : W == 16u ? (pairs ? k_part<true, false, 16u> : k_part<false, false, 16u>)
-                            : (pairs ? k_part<true, false, 8u> : k_part<false, false, 8u>);
+                 : W == 16u ? (pairs ? (pipe ? k_part<true, false, 16u, PART_SM(16u), false, true> : k_part<true, false, 16u>)
+                                     : (pipe ? k_part<false, false, 16u, PART_SM(16u), false, true> : k_part<false, false, 16u>))
+                            : (pairs ? (pipe ? k_part<true, false, 8u, PART_SM(8u), false, true> : k_part<true, false, 8u>)
+                                     : (pipe ? k_part<false, false, 8u, PART_SM(8u), false, true> : k_part<false, false, 8u>));
     hipExtLaunchKernelGGL(kmain, dim3(pgrid), dim3(PART_BLOCK_W(W)), 0, e->stream, tev(e, 0), tev(e, 1), 0, buf, len,
                           lo, e->k, e->maskk, e->d_table, e->d_short, e->d_facc, e->d_res, e->d_rr, g.nchunks, g.cpw,
                           e->d_state, has_init, pg, e->d_resume, exact);
