@@ -1921,6 +1921,10 @@ struct PartGeo {
     uint32_t stride;       /* index row stride: rows of both regions (k_part, then k_part<RES>) */
     uint32_t *flag;        /* [0] != 0: some range went to k_part<RES>, region 2 holds rows */
     uint32_t split;        /* k = 14: a slice's 2^16 codes counted as two halves of 2^15 bins (0: one) */
+    uint32_t stagger;      /* PIPE: waves with bit (stagger - 1) set place their stashed entries before
+                              their tile (0: every wave after it) */
+    uint32_t ss, rs;       /* run index word of (slice b, row r) at idx[b * ss + r * rs]: slice-major
+                              (ss = stride, rs = 1) or row-major (ss = 1, rs = nslices) */
 };
 
 /* Every entry a fast tile's Emit hands to the partition, as f(slice, low).
@@ -2040,7 +2044,7 @@ __device__ __forceinline__ bool part_batch(const Ctx &cx, const PartGeo &pg, con
             } else {
                 cur[b] = run;
             }
-            pg.idx[(size_t)b * pg.stride + row] = run_word(run, c);
+            pg.idx[(size_t)b * pg.ss + (size_t)row * pg.rs] = run_word(run, c);
             hist[b] = 0;
             run += c;
         }
@@ -2059,7 +2063,7 @@ __device__ __forceinline__ bool part_batch(const Ctx &cx, const PartGeo &pg, con
             if (b < pg.nslices) {
                 const uint32_t c = hist[b];
                 cur[b] = run;
-                pg.idx[(size_t)b * pg.stride + row] = run_word(run, c);
+                pg.idx[(size_t)b * pg.ss + (size_t)row * pg.rs] = run_word(run, c);
                 hist[b] = 0;
                 run += c;
             }
@@ -2114,6 +2118,49 @@ __device__ __forceinline__ bool part_batch(const Ctx &cx, const PartGeo &pg, con
  * out, then a second barrier: two barriers per batch instead of three, and
  * the tiles' VALU work overlaps the placement atomics across the waves.
  */
+/* A fast tile's entries (as part_entries without mixed tiles) placed at
+   their slices' cursors, eight at a time: the eight returning cursor
+   atomics are issued back to back and only then the eight code stores.
+   (One entry at a time -- atomic, wait, store -- the compiler cannot move
+   the next atomic above the previous store into the same LDS, so every
+   entry waited out a whole LDS round trip.) */
+template <bool PAIRS>
+__device__ __forceinline__ void part_place8(const Emit &em, uint32_t mk, uint32_t m1, uint32_t sh, uint32_t lowm,
+                                            uint32_t *cur, uint16_t *ent) {
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+        const uint32_t C = h ? em.BC : em.AC, S2 = h ? em.B2 : em.A2;
+        const bool skip0 = h ? em.h1 : em.h0;
+#pragma unroll
+        for (int g = 0; g < (PAIRS ? 1 : 2); g++) {
+            uint32_t b[8], low[8], p[8];
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+                uint32_t c;
+                if (PAIRS) {
+                    const uint32_t v = j < 7 ? __builtin_amdgcn_alignbit(C, S2, 28u - 4u * (uint32_t)j) : S2;
+                    c = j == 0 && skip0 ? (v & mk) << 2 : (v & m1);
+                } else {
+                    const int i = 8 * g + j;
+                    c = (i < 15 ? __builtin_amdgcn_alignbit(C, S2, 2u * (15u - (uint32_t)i)) : S2) & mk;
+                }
+                b[j] = c >> sh;
+                low[j] = (c & lowm) | (PAIRS && j == 0 && skip0 ? PART_SINGLE : 0u);
+            }
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+                if (!PAIRS && g == 0 && j == 0 && skip0) continue;   /* slot 0 is not a window */
+                p[j] = atomicAdd(&cur[b[j]], 1u);
+            }
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+                if (!PAIRS && g == 0 && j == 0 && skip0) continue;
+                ent[p[j]] = (uint16_t)low[j];
+            }
+        }
+    }
+}
+
 __device__ __forceinline__ void part_scan_w0(const PartGeo &pg, uint32_t row, uint32_t *hist, uint32_t *cur,
                                              uint32_t *tot) {
     const uint32_t lane = threadIdx.x & 63;
@@ -2130,7 +2177,7 @@ __device__ __forceinline__ void part_scan_w0(const PartGeo &pg, uint32_t row, ui
         if (b < pg.nslices) {
             const uint32_t c = hist[b];
             cur[b] = run;
-            pg.idx[(size_t)b * pg.stride + row] = run_word(run, c);
+            pg.idx[(size_t)b * pg.ss + (size_t)row * pg.rs] = run_word(run, c);
             hist[b] = 0;
             run += c;
         }
@@ -2253,9 +2300,25 @@ k_part(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint
     const uint32_t mk = (uint32_t)maskk, m1 = (mk << 2) | 3u, lowm = (1u << pg.sh) - 1u;
     auto place = [&](uint32_t b, uint32_t low) { ent[atomicAdd(&cur[b], 1u)] = (CT)low; };
     __syncthreads();
+    /* PIPE: the stashed entry of this round's slot (batch j) to its place; odd
+       waves place before their tile, even waves after it, so that the waves
+       of a SIMD tend to be in different phases (VALU / LDS) */
+    const bool early = PIPE && pg.stagger && ((wave_in_block() >> (pg.stagger - 1u)) & 1u);
+#define FK_PLACE_OLD()                                                               \
+    {                                                                                \
+        const uint32_t ph_ = round % NT;                                             \
+        Emit old_ = stash[0];                                                        \
+        bool hold_ = have_stash[0];                                                  \
+        _Pragma("unroll") for (uint32_t i_ = 1; i_ < NT; i_++) if (ph_ == i_) {      \
+            old_ = stash[i_];                                                        \
+            hold_ = have_stash[i_];                                                  \
+        }                                                                            \
+        if (hold_) part_place8<PAIRS>(old_, mk, m1, pg.sh, lowm, cur, (uint16_t *)ent); \
+    }
 #define FK_ROUND(X)                                                                  \
     {                                                                                \
         Emit em{0, 0, 0, 0, false, false, false};                                    \
+        if (PIPE && early) FK_PLACE_OLD();                                           \
         bool have = false, plain_ = false, kind_ = false;                            \
         if (!done) {                                                                 \
             if (t < sp.nfull && st.hdr == 0 && tile_fast<true, H_EMIT, true>(cx, X, st, f, cnt, 1u, &em, &kind_)) { \
@@ -2287,13 +2350,7 @@ k_part(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint
             const uint32_t ph_ = round % NT;                                         \
             if (have) part_entries<PAIRS, false>(em, mk, m1, pg.sh, lowm, pg.npair,   \
                                                  [&](uint32_t b_, uint32_t) { atomicAdd(&hist[b_], 1u); }); \
-            Emit old_ = stash[0];                                                    \
-            bool hold_ = have_stash[0];                                              \
-            _Pragma("unroll") for (uint32_t i_ = 1; i_ < NT; i_++) if (ph_ == i_) {  \
-                old_ = stash[i_];                                                    \
-                hold_ = have_stash[i_];                                              \
-            }                                                                        \
-            if (hold_) part_entries<PAIRS, false>(old_, mk, m1, pg.sh, lowm, pg.npair, place); \
+            if (!early) FK_PLACE_OLD();                                              \
             _Pragma("unroll") for (uint32_t i_ = 0; i_ < NT; i_++) if (ph_ == i_) {  \
                 stash[i_] = em;                                                      \
                 have_stash[i_] = have;                                               \
@@ -2308,7 +2365,7 @@ k_part(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint
                 if (!more_ || j_ + 1 >= pg.rounds) {                                 \
                     /* the last batch: placed, then written out */                  \
                     _Pragma("unroll") for (uint32_t i_ = 0; i_ < NT; i_++)           \
-                        if (have_stash[i_]) part_entries<PAIRS, false>(stash[i_], mk, m1, pg.sh, lowm, pg.npair, place); \
+                        if (have_stash[i_]) part_place8<PAIRS>(stash[i_], mk, m1, pg.sh, lowm, cur, (uint16_t *)ent); \
                     __syncthreads();                                                 \
                     part_writeout<W>(pg, row0 + j_, tot[j_ & 1u], (const uint16_t *)ent, threadIdx.x, PART_BLOCK_W(W)); \
                     round++;                                                         \
@@ -2335,11 +2392,12 @@ k_part(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint
         FK_ROUND(C);
     }
 #undef FK_ROUND
+#undef FK_PLACE_OLD
 #undef FK_LOADP
     /* rows the block did not reach are empty */
     for (uint32_t r = (round + NT - 1) / NT; r < pg.rounds; r++) {
         const uint32_t row = row0 + r;
-        for (uint32_t b = threadIdx.x; b < pg.nslices; b += PART_BLOCK_W(W)) pg.idx[(size_t)b * pg.stride + row] = PART_NO_RUN;
+        for (uint32_t b = threadIdx.x; b < pg.nslices; b += PART_BLOCK_W(W)) pg.idx[(size_t)b * pg.ss + (size_t)row * pg.rs] = PART_NO_RUN;
     }
     if (!has) {
         flush_counters(cx, cnt, 1u);
@@ -2437,7 +2495,7 @@ k_bucket_count(PartGeo pg, uint32_t groups, uint32_t *table) {
     }
     for (uint32_t i = threadIdx.x; i < nb + ns; i += blockDim.x) slice[i] = 0;
     __syncthreads();
-    const uint32_t *ix = pg.idx + (size_t)b * pg.stride;
+    const uint32_t *ix = pg.idx + (size_t)b * pg.ss;
     /* region 2 (k_part<RES>) holds rows only if some range went there */
     const uint32_t nrows = pg.flag && *pg.flag ? 2u * pg.rows : pg.rows;
     const uint4 *g4 = reinterpret_cast<const uint4 *>(pg.codes);
@@ -2467,14 +2525,14 @@ k_bucket_count(PartGeo pg, uint32_t groups, uint32_t *table) {
     uint32_t en[BUCKET_ROWS];   /* the next iteration's index words, loaded with this one's codes */
     const uint32_t r00 = g * quads + threadIdx.x / QL;
 #pragma unroll
-    for (int j = 0; j < BUCKET_ROWS; j++) en[j] = r00 + j * step < nrows ? ix[r00 + j * step] : PART_NO_RUN;
+    for (int j = 0; j < BUCKET_ROWS; j++) en[j] = r00 + j * step < nrows ? ix[(size_t)(r00 + j * step) * pg.rs] : PART_NO_RUN;
     for (uint32_t r = r00; r < nrows; r += BUCKET_ROWS * step) {
         uint32_t e[BUCKET_ROWS];
 #pragma unroll
         for (int j = 0; j < BUCKET_ROWS; j++) e[j] = en[j];
         const uint32_t rn = r + BUCKET_ROWS * step;
 #pragma unroll
-        for (int j = 0; j < BUCKET_ROWS; j++) en[j] = rn + j * step < nrows ? ix[rn + j * step] : PART_NO_RUN;
+        for (int j = 0; j < BUCKET_ROWS; j++) en[j] = rn + j * step < nrows ? ix[(size_t)(rn + j * step) * pg.rs] : PART_NO_RUN;
         uint64_t s0[BUCKET_ROWS], s1[BUCKET_ROWS];
         uint4 v[BUCKET_ROWS][BUCKET_U];
 #pragma unroll
@@ -2549,12 +2607,12 @@ k_repart(PartGeo pg, uint16_t *out, unsigned long long *alloc, PartMeta *meta) {
     const uint32_t np = 1u << pg.split;
     for (uint32_t i = t; i < 16u * REPART_MAXP; i += blockDim.x) (&cnt[0][0])[i] = 0;
     __syncthreads();
-    const uint32_t *ix = pg.idx + (size_t)b * pg.stride;
+    const uint32_t *ix = pg.idx + (size_t)b * pg.ss;
     const uint32_t nrows = pg.flag && *pg.flag ? 2u * pg.rows : pg.rows;
     const uint4 *g4 = reinterpret_cast<const uint4 *>(pg.codes);
     /* a lane per run, its codes as 16-B pieces (4 codes each) */
     auto each_code = [&](uint32_t r, auto &&f) {
-        const uint32_t e = ix[r];
+        const uint32_t e = ix[(size_t)r * pg.rs];
         if (e == PART_NO_RUN) return;
         const uint64_t s0 = (uint64_t)r * pg.batch + (e >> 16), s1 = s0 + run_count(e);
         for (uint64_t q = s0 >> 2; q < (s1 + 3) >> 2; q++) {
@@ -3394,6 +3452,9 @@ struct fk_engine {
     uint32_t part_general = 1;                /* k_part: general tiles per range (FINDKMER_TUNE part_general) */
     uint32_t part_waves = 0;                  /* k_part: waves per block (FINDKMER_TUNE part_waves; 0 = by k) */
     bool part_pipe = true;                    /* k_part: pipelined batches (FINDKMER_TUNE part_pipe=0: off) */
+    uint32_t part_stagger = 2;                /* k_part PIPE: waves with bit (part_stagger - 1) of their index set place
+                                                 first (FINDKMER_TUNE part_stagger=0: none) */
+    bool idx_rm = true;                       /* k_part: row-major run index (FINDKMER_TUNE idx_rm=0: slice-major) */
     uint32_t static_pct = 100;                /* k <= 7: % of a large segment in static ranges (FINDKMER_TUNE static_pct;
                                                  100 = no dynamic ranges: on a plain stream the waves that
                                                  finish early hand their bandwidth to the others, so
@@ -3679,6 +3740,8 @@ extern "C" int fk_engine_create(int k, const fk_opts *opts, fk_engine **out) {
     if (!e->no_mixed) e->general_tiles = 2;
     if (tune_knob("part_waves", &kv)) e->part_waves = kv == 8u || kv == 16u ? (uint32_t)kv : 0u;
     if (tune_knob("part_pipe", &kv)) e->part_pipe = kv != 0;
+    if (tune_knob("idx_rm", &kv)) e->idx_rm = kv != 0;
+    if (tune_knob("part_stagger", &kv)) e->part_stagger = (uint32_t)std::min<uint64_t>(kv, 4u);
     if (tune_knob("part_general", &kv)) e->part_general = (uint32_t)kv;
     if (tune_knob("events", &kv)) e->timing = kv != 0;
     if (tune_knob("static_pct", &kv)) e->static_pct = (uint32_t)std::min<uint64_t>(100u, std::max<uint64_t>(1u, kv));
@@ -4050,6 +4113,9 @@ static int launch_part(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t l
        when many ranges go there */
     pg.general = e->part_general;
     pg.stride = mixed ? 2 * pg.rows : pg.rows;
+    pg.stagger = e->part_stagger;
+    pg.ss = e->idx_rm ? 1u : pg.stride;
+    pg.rs = e->idx_rm ? pg.nslices : 1u;
     if (!e->d_pflag && hipMalloc((void **)&e->d_pflag, 64) != hipSuccess) return FK_E_OOM;
     pg.flag = e->d_pflag;
     HIPCHK(hipMemsetAsync(e->d_pflag, 0, sizeof(uint32_t), e->stream));

@@ -92,6 +92,31 @@ VARIANTS = {
         ("        FK_ROUND(A);\n        FK_ROUND(B);\n        FK_ROUND(C);\n    }\n#undef FK_ROUND\n#undef FK_LOADP\n    /* rows the block",
          "        FK_ROUND(A);\n        FK_ROUND(B);\n        FK_ROUND(C);\n        FK_ROUND(D);\n    }\n#undef FK_ROUND\n#undef FK_LOADP\n    /* rows the block"),
     ],
+    # ablations of the pipelined k_part (timing only: the counts are wrong):
+    # no placement of the stashed batch, no histogram atomics, no write-out
+    "noplace": [
+        ("            if (hold_) part_entries<PAIRS, false>(old_, mk, m1, pg.sh, lowm, pg.npair, place); \\\n",
+         "            if (hold_) keep(old_.AC ^ old_.A2 ^ old_.BC ^ old_.B2);                  \\\n"),
+    ],
+    "nohist": [
+        ("            if (have) part_entries<PAIRS, false>(em, mk, m1, pg.sh, lowm, pg.npair,   \\\n"
+         "                                                 [&](uint32_t b_, uint32_t) { atomicAdd(&hist[b_], 1u); }); \\\n",
+         "            if (have) keep(em.AC ^ em.A2 ^ em.BC ^ em.B2);                          \\\n"),
+    ],
+    "noout": [
+        ("    for (uint32_t i = t0; i < n8; i += nt) dst[i] = src[i];\n}",
+         "    if (total == 0xFFFFFFFFu) for (uint32_t i = t0; i < n8; i += nt) dst[i] = src[i];\n}"),
+    ],
+    # k_bucket_count without its LDS atomics (timing only): what the run
+    # reads alone cost
+    "bk_noadd": [
+        ("                if (at >= s0 && at < s1) atomicAdd(&slice[a], 1u);",
+         "                if (at >= s0 && at < s1) sink ^= a;"),
+        ("    constexpr uint32_t QL = 4u;   /* lanes per run */",
+         "    uint32_t sink = 0;\n    constexpr uint32_t QL = 4u;   /* lanes per run */"),
+        ("    __syncthreads();\n    if (pg.pairs) {\n        /* pairs mode: the slice's bins",
+         "    if (sink == 0x12345u) slice[0] = sink;\n    __syncthreads();\n    if (pg.pairs) {\n        /* pairs mode: the slice's bins"),
+    ],
 }
 
 
@@ -105,7 +130,7 @@ def build(name):
     dst = os.path.join(OUT, f"fk_engine_{name}.hip")
     open(dst, "w").write(src)
     inc = ["-I" + os.path.join(REPO, "include"), "-I" + os.path.join(REPO, "findkmer_amd", "csrc")]
-    flags = ["--offload-arch=gfx950", "-O3", "-fPIC", "-std=c++17", "-munsafe-fp-atomics"]
+    flags = ["--offload-arch=gfx950", "-O3", "-fPIC", "-std=c++17", "-munsafe-fp-atomics", "-Wno-unused-value"]
     obj = os.path.join(OUT, f"{name}.o")
     subprocess.run(["/opt/rocm/bin/hipcc", *flags, *inc, "-c", "-x", "hip", dst, "-o", obj], check=True)
     b = os.path.join(REPO, "build")
