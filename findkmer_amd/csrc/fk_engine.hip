@@ -2124,8 +2124,57 @@ __device__ __forceinline__ bool part_batch(const Ctx &cx, const PartGeo &pg, con
    (One entry at a time -- atomic, wait, store -- the compiler cannot move
    the next atomic above the previous store into the same LDS, so every
    entry waited out a whole LDS round trip.) */
+/* Entry j of group g of half h of a fast tile (as part_entries without
+   mixed tiles): its slice (one bit-field extract: the code's bits [sh, sh +
+   wsl), wsl = the slice bits) and its stored low bits (PAIRS: a single k-mer
+   x at slot 1 of a '\n' half is the pair code x << 2 with PART_SINGLE) */
 template <bool PAIRS>
-__device__ __forceinline__ void part_place8(const Emit &em, uint32_t mk, uint32_t m1, uint32_t sh, uint32_t lowm,
+__device__ __forceinline__ void part_entry(uint32_t C, uint32_t S2, bool skip0, int g, int j, uint32_t sh,
+                                           uint32_t wsl, uint32_t lowm, uint32_t &b, uint32_t *low) {
+    if (PAIRS) {
+        const uint32_t v = j < 7 ? __builtin_amdgcn_alignbit(C, S2, 28u - 4u * (uint32_t)j) : S2;
+        if (j == 0 && skip0) {   /* (v & mk) << 2: its slice is v's bits [sh - 2, sh - 2 + wsl) */
+            b = __builtin_amdgcn_ubfe(v, sh - 2u, wsl);
+            if (low) *low = ((v << 2) & lowm) | PART_SINGLE;
+        } else {
+            b = __builtin_amdgcn_ubfe(v, sh, wsl);
+            if (low) *low = v & lowm;
+        }
+    } else {
+        const int i = 8 * g + j;
+        const uint32_t v = i < 15 ? __builtin_amdgcn_alignbit(C, S2, 2u * (15u - (uint32_t)i)) : S2;
+        b = __builtin_amdgcn_ubfe(v, sh, wsl);
+        if (low) *low = v & lowm;
+    }
+}
+
+/* A fast tile's entries into the batch's slice histogram */
+template <bool PAIRS>
+__device__ __forceinline__ void part_hist8(const Emit &em, uint32_t sh, uint32_t wsl, uint32_t *hist) {
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+        const uint32_t C = h ? em.BC : em.AC, S2 = h ? em.B2 : em.A2;
+        const bool skip0 = h ? em.h1 : em.h0;
+#pragma unroll
+        for (int g = 0; g < (PAIRS ? 1 : 2); g++)
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+                if (!PAIRS && g == 0 && j == 0 && skip0) continue;   /* slot 0 is not a window */
+                uint32_t b;
+                part_entry<PAIRS>(C, S2, skip0, g, j, sh, wsl, 0u, b, nullptr);
+                atomicAdd(&hist[b], 1u);
+            }
+    }
+}
+
+/* A fast tile's entries placed at their slices' cursors (byte offsets into
+   the batch), eight at a time: the eight returning cursor atomics are issued
+   back to back and only then the eight code stores.  (One entry at a time --
+   atomic, wait, store -- the compiler cannot move the next atomic above the
+   previous store into the same LDS, so every entry waited out a whole LDS
+   round trip.) */
+template <bool PAIRS>
+__device__ __forceinline__ void part_place8(const Emit &em, uint32_t sh, uint32_t wsl, uint32_t lowm,
                                             uint32_t *cur, uint16_t *ent) {
 #pragma unroll
     for (int h = 0; h < 2; h++) {
@@ -2135,27 +2184,16 @@ __device__ __forceinline__ void part_place8(const Emit &em, uint32_t mk, uint32_
         for (int g = 0; g < (PAIRS ? 1 : 2); g++) {
             uint32_t b[8], low[8], p[8];
 #pragma unroll
-            for (int j = 0; j < 8; j++) {
-                uint32_t c;
-                if (PAIRS) {
-                    const uint32_t v = j < 7 ? __builtin_amdgcn_alignbit(C, S2, 28u - 4u * (uint32_t)j) : S2;
-                    c = j == 0 && skip0 ? (v & mk) << 2 : (v & m1);
-                } else {
-                    const int i = 8 * g + j;
-                    c = (i < 15 ? __builtin_amdgcn_alignbit(C, S2, 2u * (15u - (uint32_t)i)) : S2) & mk;
-                }
-                b[j] = c >> sh;
-                low[j] = (c & lowm) | (PAIRS && j == 0 && skip0 ? PART_SINGLE : 0u);
-            }
+            for (int j = 0; j < 8; j++) part_entry<PAIRS>(C, S2, skip0, g, j, sh, wsl, lowm, b[j], &low[j]);
 #pragma unroll
             for (int j = 0; j < 8; j++) {
                 if (!PAIRS && g == 0 && j == 0 && skip0) continue;   /* slot 0 is not a window */
-                p[j] = atomicAdd(&cur[b[j]], 1u);
+                p[j] = atomicAdd(&cur[b[j]], 2u);
             }
 #pragma unroll
             for (int j = 0; j < 8; j++) {
                 if (!PAIRS && g == 0 && j == 0 && skip0) continue;
-                ent[p[j]] = (uint16_t)low[j];
+                *reinterpret_cast<uint16_t *>(reinterpret_cast<uint8_t *>(ent) + p[j]) = (uint16_t)low[j];
             }
         }
     }
@@ -2176,7 +2214,7 @@ __device__ __forceinline__ void part_scan_w0(const PartGeo &pg, uint32_t row, ui
         const uint32_t b = lane * per + j;
         if (b < pg.nslices) {
             const uint32_t c = hist[b];
-            cur[b] = run;
+            cur[b] = 2u * run;   /* byte offsets (part_place8) */
             pg.idx[(size_t)b * pg.ss + (size_t)row * pg.rs] = run_word(run, c);
             hist[b] = 0;
             run += c;
@@ -2297,8 +2335,8 @@ k_part(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint
         have_stash[i] = false;
     }
     /* PIPE: the codes of an entry and its placement (unpacked cursors) */
-    const uint32_t mk = (uint32_t)maskk, m1 = (mk << 2) | 3u, lowm = (1u << pg.sh) - 1u;
-    auto place = [&](uint32_t b, uint32_t low) { ent[atomicAdd(&cur[b], 1u)] = (CT)low; };
+    const uint32_t lowm = (1u << pg.sh) - 1u;
+    const uint32_t wsl = 2u * (uint32_t)(PAIRS ? k + 1 : k) - pg.sh;   /* slice bits of a code */
     __syncthreads();
     /* PIPE: the stashed entry of this round's slot (batch j) to its place; odd
        waves place before their tile, even waves after it, so that the waves
@@ -2313,7 +2351,7 @@ k_part(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint
             old_ = stash[i_];                                                        \
             hold_ = have_stash[i_];                                                  \
         }                                                                            \
-        if (hold_) part_place8<PAIRS>(old_, mk, m1, pg.sh, lowm, cur, (uint16_t *)ent); \
+        if (hold_) part_place8<PAIRS>(old_, pg.sh, wsl, lowm, cur, (uint16_t *)ent); \
     }
 #define FK_ROUND(X)                                                                  \
     {                                                                                \
@@ -2348,8 +2386,7 @@ k_part(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint
         FK_LOADP(X, t + 2);                                                          \
         if (PIPE) {   /* batch j+1's histogram, batch j's placement (see part_scan_w0) */ \
             const uint32_t ph_ = round % NT;                                         \
-            if (have) part_entries<PAIRS, false>(em, mk, m1, pg.sh, lowm, pg.npair,   \
-                                                 [&](uint32_t b_, uint32_t) { atomicAdd(&hist[b_], 1u); }); \
+            if (have) part_hist8<PAIRS>(em, pg.sh, wsl, hist);                      \
             if (!early) FK_PLACE_OLD();                                              \
             _Pragma("unroll") for (uint32_t i_ = 0; i_ < NT; i_++) if (ph_ == i_) {  \
                 stash[i_] = em;                                                      \
@@ -2365,7 +2402,7 @@ k_part(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint
                 if (!more_ || j_ + 1 >= pg.rounds) {                                 \
                     /* the last batch: placed, then written out */                  \
                     _Pragma("unroll") for (uint32_t i_ = 0; i_ < NT; i_++)           \
-                        if (have_stash[i_]) part_place8<PAIRS>(stash[i_], mk, m1, pg.sh, lowm, cur, (uint16_t *)ent); \
+                        if (have_stash[i_]) part_place8<PAIRS>(stash[i_], pg.sh, wsl, lowm, cur, (uint16_t *)ent); \
                     __syncthreads();                                                 \
                     part_writeout<W>(pg, row0 + j_, tot[j_ & 1u], (const uint16_t *)ent, threadIdx.x, PART_BLOCK_W(W)); \
                     round++;                                                         \
