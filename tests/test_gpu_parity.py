@@ -1265,3 +1265,19 @@ def test_cli_concurrent_fanout_matches_goldens(manifest, tmp_path):
         for kind, rec in manifest[f"up_k{k}_z3"]["files"].items():
             got = open(tmp_path / rec["name"], "rb").read()
             assert hashlib.sha256(got).hexdigest() == rec["sha256"], (k, kind)
+
+
+@pytest.mark.parametrize("k", [9, 11, 12])
+@pytest.mark.parametrize("tune", ["part_pipe=0", "part_stagger=0", "part_stagger=3", "idx_rm=0",
+                                  "part_pipe=0,idx_rm=0", "part_waves=16", "part_waves=8"])
+def test_partition_orders_and_layouts(k, tune, monkeypatch):
+    # k_part's batch orders (pipelined or phase by phase, every stagger) and
+    # run-index layouts (row- or slice-major) count identically: FASTA lines,
+    # a '\n' in every 16-byte half now and then, a comment line, a poly-A
+    # stretch (one slice takes a whole batch) and a ragged end
+    monkeypatch.setenv("FINDKMER_TUNE", tune)
+    rng = random.Random(91 + k)
+    body = random_text(rng, 1_500_000, b"ACGT", [1, 1, 1, 1])
+    lines = b"\n".join(body[i:i + 61] for i in range(0, len(body), 61))
+    data = b">chr1\n" + lines + b"\n" + b"A" * 300_000 + b"\n>chr2 x\n" + lines[:400_003]
+    assert_same(data, k)
