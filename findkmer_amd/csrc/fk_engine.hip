@@ -2173,9 +2173,10 @@ __device__ __forceinline__ void part_hist8(const Emit &em, uint32_t sh, uint32_t
    atomic, wait, store -- the compiler cannot move the next atomic above the
    previous store into the same LDS, so every entry waited out a whole LDS
    round trip.) */
+typedef __attribute__((address_space(3))) uint16_t lds_u16;
 template <bool PAIRS>
 __device__ __forceinline__ void part_place8(const Emit &em, uint32_t sh, uint32_t wsl, uint32_t lowm,
-                                            uint32_t *cur, uint16_t *ent) {
+                                            uint32_t *cur) {
 #pragma unroll
     for (int h = 0; h < 2; h++) {
         const uint32_t C = h ? em.BC : em.AC, S2 = h ? em.B2 : em.A2;
@@ -2193,14 +2194,14 @@ __device__ __forceinline__ void part_place8(const Emit &em, uint32_t sh, uint32_
 #pragma unroll
             for (int j = 0; j < 8; j++) {
                 if (!PAIRS && g == 0 && j == 0 && skip0) continue;
-                *reinterpret_cast<uint16_t *>(reinterpret_cast<uint8_t *>(ent) + p[j]) = (uint16_t)low[j];
+                *(lds_u16 *)(uintptr_t)p[j] = (uint16_t)low[j];
             }
         }
     }
 }
 
 __device__ __forceinline__ void part_scan_w0(const PartGeo &pg, uint32_t row, uint32_t *hist, uint32_t *cur,
-                                             uint32_t *tot) {
+                                             uint32_t *tot, uint32_t ent_lds) {
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t per = (pg.nslices + 63) / 64;
     uint32_t sum = 0;
@@ -2214,7 +2215,7 @@ __device__ __forceinline__ void part_scan_w0(const PartGeo &pg, uint32_t row, ui
         const uint32_t b = lane * per + j;
         if (b < pg.nslices) {
             const uint32_t c = hist[b];
-            cur[b] = 2u * run;   /* byte offsets (part_place8) */
+            cur[b] = ent_lds + 2u * run;   /* LDS byte addresses (part_place8) */
             pg.idx[(size_t)b * pg.ss + (size_t)row * pg.rs] = run_word(run, c);
             hist[b] = 0;
             run += c;
@@ -2238,15 +2239,23 @@ __device__ __forceinline__ void part_writeout(const PartGeo &pg, uint32_t row, u
  * the rest of it, each tile fast, mixed (the masked entries of tile_mixed)
  * or general.  Two kernels: tile_mixed's registers stay out of the main
  * pass.  k_part<RES> returns at once unless some range stopped. */
-template <bool PAIRS, bool RES, uint32_t W, uint32_t SM = PART_SM(W), bool C32 = false, bool PIPE = false>
+template <bool PAIRS, bool RES, uint32_t W, uint32_t SM = PART_SM(W), bool C32 = false, bool PIPE = false,
+          uint32_t KC = 0>
 __global__ void __launch_bounds__(PART_BLOCK_W(W), 4) /* 4 waves per SIMD (<= 128 VGPRs): 16 waves per CU */
 k_part(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint32_t *table,
        uint32_t *shortcnt, unsigned long long *acc, DevRes *res, RangeRec *rr, uint64_t nchunks, uint64_t cpw,
        const XState *d_init, int has_init, PartGeo pg, ResumeRec *resume, const XState *exact) {
     static_assert(!PIPE || (!RES && !C32 && SM <= 2048u), "PIPE: the main pass, 16-bit codes, unpacked cursors");
-    __shared__ uint32_t hist[SM], cur[SM > 2048u ? SM / 2u : SM], total, scr[W], tot[2];
+    /* one LDS object: the histogram and the cursors first (below 64 KiB, so
+       their base folds into the LDS instructions' offset field), then the
+       batch */
     using CT = typename std::conditional<C32, uint32_t, uint16_t>::type;
-    __shared__ __attribute__((aligned(16))) CT ent[PART_ROW_BYTES(W) / sizeof(CT)];
+    constexpr uint32_t CURW = SM > 2048u ? SM / 2u : SM;
+    constexpr uint32_t ENT_OFF = (SM + CURW + 4u + W + 15u) & ~15u;   /* words, 64-B aligned */
+    __shared__ __attribute__((aligned(64))) uint32_t lds_part[ENT_OFF + PART_ROW_BYTES(W) / 4u];
+    uint32_t *const hist = lds_part, *const cur = lds_part + SM, &total = lds_part[SM + CURW],
+                    *const tot = lds_part + SM + CURW + 1u, *const scr = lds_part + SM + CURW + 4u;
+    CT *const ent = reinterpret_cast<CT *>(lds_part + ENT_OFF);
     if (RES && *(volatile uint32_t *)pg.flag == 0) return;   /* uniform: no range stopped */
     /* open the feed's result block (the kernels after this one accumulate
        into it) */
@@ -2335,8 +2344,14 @@ k_part(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint
         have_stash[i] = false;
     }
     /* PIPE: the codes of an entry and its placement (unpacked cursors) */
-    const uint32_t lowm = (1u << pg.sh) - 1u;
-    const uint32_t wsl = 2u * (uint32_t)(PAIRS ? k + 1 : k) - pg.sh;   /* slice bits of a code */
+    /* KC: k as a compile-time constant (the headline k = 11), so that the
+       slice and low-bit extracts fold into single bit-field ops */
+    constexpr uint32_t KBC = KC ? (PAIRS ? KC + 1u : KC) : 0u;
+    const uint32_t shv = KC ? (2u * KBC - 6u < 15u ? 2u * KBC - 6u : 15u) : pg.sh;
+    const uint32_t lowm = (1u << shv) - 1u;
+    /* the batch's LDS byte address (the PIPE cursors hold LDS addresses) */
+    const uint32_t ent_lds = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) CT *)ent;
+    const uint32_t wsl = 2u * (KC ? KBC : (uint32_t)(PAIRS ? k + 1 : k)) - shv;   /* slice bits of a code */
     __syncthreads();
     /* PIPE: the stashed entry of this round's slot (batch j) to its place; odd
        waves place before their tile, even waves after it, so that the waves
@@ -2351,7 +2366,7 @@ k_part(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint
             old_ = stash[i_];                                                        \
             hold_ = have_stash[i_];                                                  \
         }                                                                            \
-        if (hold_) part_place8<PAIRS>(old_, pg.sh, wsl, lowm, cur, (uint16_t *)ent); \
+        if (hold_) part_place8<PAIRS>(old_, shv, wsl, lowm, cur); \
     }
 #define FK_ROUND(X)                                                                  \
     {                                                                                \
@@ -2386,7 +2401,7 @@ k_part(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint
         FK_LOADP(X, t + 2);                                                          \
         if (PIPE) {   /* batch j+1's histogram, batch j's placement (see part_scan_w0) */ \
             const uint32_t ph_ = round % NT;                                         \
-            if (have) part_hist8<PAIRS>(em, pg.sh, wsl, hist);                      \
+            if (have) part_hist8<PAIRS>(em, shv, wsl, hist);                       \
             if (!early) FK_PLACE_OLD();                                              \
             _Pragma("unroll") for (uint32_t i_ = 0; i_ < NT; i_++) if (ph_ == i_) {  \
                 stash[i_] = em;                                                      \
@@ -2395,14 +2410,14 @@ k_part(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint
             if (ph_ == NT - 1) {                                                     \
                 const uint32_t j_ = round / NT;                                      \
                 const bool more_ = __syncthreads_or(!done);                          \
-                if (threadIdx.x < 64) part_scan_w0(pg, row0 + j_, hist, cur, &tot[j_ & 1u]); \
+                if (threadIdx.x < 64) part_scan_w0(pg, row0 + j_, hist, cur, &tot[j_ & 1u], ent_lds);\
                 else if (j_ > 0) part_writeout<W>(pg, row0 + j_ - 1, tot[(j_ - 1) & 1u], (const uint16_t *)ent, \
                                                   threadIdx.x - 64u, PART_BLOCK_W(W) - 64u); \
                 __syncthreads();                                                     \
                 if (!more_ || j_ + 1 >= pg.rounds) {                                 \
                     /* the last batch: placed, then written out */                  \
                     _Pragma("unroll") for (uint32_t i_ = 0; i_ < NT; i_++)           \
-                        if (have_stash[i_]) part_place8<PAIRS>(stash[i_], pg.sh, wsl, lowm, cur, (uint16_t *)ent); \
+                        if (have_stash[i_]) part_place8<PAIRS>(stash[i_], shv, wsl, lowm, cur); \
                     __syncthreads();                                                 \
                     part_writeout<W>(pg, row0 + j_, tot[j_ & 1u], (const uint16_t *)ent, threadIdx.x, PART_BLOCK_W(W)); \
                     round++;                                                         \
@@ -4176,7 +4191,9 @@ static int launch_part(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t l
     const bool pipe = e->part_pipe && !c32 && !pg.split && pg.nslices <= 512u;
     auto kmain = c32 ? k_part<false, false, 16u, PART_SM(16u), true>
                  : pg.split ? k_part<false, false, 16u, PART_BIG>
-                 : W == 16u ? (pairs ? (pipe ? k_part<true, false, 16u, PART_SM(16u), false, true> : k_part<true, false, 16u>)
+                 : W == 16u ? (pairs ? (pipe ? (k == 11 ? k_part<true, false, 16u, PART_SM(16u), false, true, 11u>
+                                                     : k_part<true, false, 16u, PART_SM(16u), false, true>)
+                                          : k_part<true, false, 16u>)
                                      : (pipe ? k_part<false, false, 16u, PART_SM(16u), false, true> : k_part<false, false, 16u>))
                             : (pairs ? (pipe ? k_part<true, false, 8u, PART_SM(8u), false, true> : k_part<true, false, 8u>)
                                      : (pipe ? k_part<false, false, 8u, PART_SM(8u), false, true> : k_part<false, false, 8u>));
