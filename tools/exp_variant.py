@@ -41,6 +41,10 @@ VARIANTS = {
     # k_bucket_count's first loads per quad: rows x 16-B pieces per lane
     "u4r3": [("#define BUCKET_U 5", "#define BUCKET_U 4"), ("#define BUCKET_ROWS 2", "#define BUCKET_ROWS 3")],
     "u6": [("#define BUCKET_U 5", "#define BUCKET_U 6")],
+    "u4": [("#define BUCKET_U 5", "#define BUCKET_U 4")],
+    "u3": [("#define BUCKET_U 5", "#define BUCKET_U 3")],
+    "r1": [("#define BUCKET_ROWS 2", "#define BUCKET_ROWS 1")],
+    "r1u8": [("#define BUCKET_U 5", "#define BUCKET_U 8"), ("#define BUCKET_ROWS 2", "#define BUCKET_ROWS 1")],
     "u3r4": [("#define BUCKET_U 5", "#define BUCKET_U 3"), ("#define BUCKET_ROWS 2", "#define BUCKET_ROWS 4")],
     # k_bucket_count without the XCD-aware slice order
     "noxcd": [
