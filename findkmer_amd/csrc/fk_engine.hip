@@ -2104,7 +2104,8 @@ __device__ __forceinline__ bool part_batch(const Ctx &cx, const PartGeo &pg, con
 
 /*
  * Pipelined batches (PIPE: the main pass of tables of at most 512 slices,
- * whose scan wave 0 runs alone).  part_batch runs its phases one after
+ * whose scan wave 0 runs alone, and of k = 13's 2048, whose scan all waves
+ * share: part_scan_sum).  part_batch runs its phases one after
  * another on every wave -- tiles (VALU), histogram atomics, barrier, scan,
  * barrier, placement atomics (LDS), barrier, write-out -- so the CU's VALU
  * idles while its LDS works and the other way round.  Here batch j's
@@ -2222,6 +2223,35 @@ __device__ __forceinline__ void part_scan_w0(const PartGeo &pg, uint32_t row, ui
         }
     }
     if (lane == 63) *tot = inc;
+}
+
+/* The same for 2048 slices (k = 13), over all W waves: each wave sums its
+   contiguous share (part 1, beside the write-out), one more barrier, then
+   scans its share from the sum of the shares before it (part 2) */
+__device__ __forceinline__ uint32_t part_scan_sum(const PartGeo &pg, const uint32_t *hist, uint32_t nw, uint32_t *scr) {
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint32_t per_w = pg.nslices / nw, ppl = per_w / 64u, b0 = wv * per_w + lane * ppl;
+    uint32_t mine = 0;
+    for (uint32_t j = 0; j < ppl; j++) mine += hist[b0 + j];
+    const uint32_t wt = wsum32(mine);
+    if (lane == 0) scr[wv] = wt;
+    return mine;
+}
+__device__ __forceinline__ void part_scan_place(const PartGeo &pg, uint32_t row, uint32_t *hist, uint32_t *cur,
+                                                uint32_t nw, const uint32_t *scr, uint32_t mine, uint32_t *tot,
+                                                uint32_t ent_lds) {
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint32_t per_w = pg.nslices / nw, ppl = per_w / 64u, b0 = wv * per_w + lane * ppl;
+    const uint32_t off = wsum32(lane < wv ? scr[lane] : 0u);
+    uint32_t run = off + wscan_incl32(mine) - mine;
+    for (uint32_t j = 0; j < ppl; j++) {
+        const uint32_t b = b0 + j, c = hist[b];
+        cur[b] = ent_lds + 2u * run;
+        pg.idx[(size_t)b * pg.ss + (size_t)row * pg.rs] = run_word(run, c);
+        hist[b] = 0;
+        run += c;
+    }
+    if (wv == nw - 1u && lane == 63) *tot = run;
 }
 
 template <uint32_t W>
@@ -2410,9 +2440,18 @@ k_part(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint
             if (ph_ == NT - 1) {                                                     \
                 const uint32_t j_ = round / NT;                                      \
                 const bool more_ = __syncthreads_or(!done);                          \
-                if (threadIdx.x < 64) part_scan_w0(pg, row0 + j_, hist, cur, &tot[j_ & 1u], ent_lds);\
-                else if (j_ > 0) part_writeout<W>(pg, row0 + j_ - 1, tot[(j_ - 1) & 1u], (const uint16_t *)ent, \
-                                                  threadIdx.x - 64u, PART_BLOCK_W(W) - 64u); \
+                if (pg.nslices > 512u) {   /* k = 13: the scan over all waves */    \
+                    const uint32_t mine_ = part_scan_sum(pg, hist, W, scr);          \
+                    if (j_ > 0) part_writeout<W>(pg, row0 + j_ - 1, tot[(j_ - 1) & 1u], (const uint16_t *)ent, \
+                                                 threadIdx.x, PART_BLOCK_W(W));       \
+                    __syncthreads();                                                 \
+                    part_scan_place(pg, row0 + j_, hist, cur, W, scr, mine_, &tot[j_ & 1u], ent_lds); \
+                } else if (threadIdx.x < 64) {                                       \
+                    part_scan_w0(pg, row0 + j_, hist, cur, &tot[j_ & 1u], ent_lds);  \
+                } else if (j_ > 0) {                                                 \
+                    part_writeout<W>(pg, row0 + j_ - 1, tot[(j_ - 1) & 1u], (const uint16_t *)ent, \
+                                     threadIdx.x - 64u, PART_BLOCK_W(W) - 64u);       \
+                }                                                                    \
                 __syncthreads();                                                     \
                 if (!more_ || j_ + 1 >= pg.rounds) {                                 \
                     /* the last batch: placed, then written out */                  \
@@ -4188,7 +4227,7 @@ static int launch_part(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t l
     pg.codes = e->d_codes;
     pg.idx = e->d_pidx;
     /* the pipelined main pass where wave 0 scans the slices alone (<= 512) */
-    const bool pipe = e->part_pipe && !c32 && !pg.split && pg.nslices <= 512u;
+    const bool pipe = e->part_pipe && !c32 && !pg.split && (pg.nslices <= 512u || (!pairs && W == 16u && pg.nslices == 2048u));
     auto kmain = c32 ? k_part<false, false, 16u, PART_SM(16u), true>
                  : pg.split ? k_part<false, false, 16u, PART_BIG>
                  : W == 16u ? (pairs ? (pipe ? (k == 11 ? k_part<true, false, 16u, PART_SM(16u), false, true, 11u>

@@ -1267,7 +1267,7 @@ def test_cli_concurrent_fanout_matches_goldens(manifest, tmp_path):
             assert hashlib.sha256(got).hexdigest() == rec["sha256"], (k, kind)
 
 
-@pytest.mark.parametrize("k", [9, 11, 12])
+@pytest.mark.parametrize("k", [9, 11, 12, 13])
 @pytest.mark.parametrize("tune", ["part_pipe=0", "part_stagger=0", "part_stagger=3", "idx_rm=0",
                                   "part_pipe=0,idx_rm=0", "part_waves=16", "part_waves=8"])
 def test_partition_orders_and_layouts(k, tune, monkeypatch):
