@@ -3526,7 +3526,9 @@ struct fk_engine {
     uint64_t parts_cap = 0;
     void *d_pmeta = nullptr;                  /* k = 15, 16: PartMeta per part + the allocation counter */
     uint64_t pair_cap = 0;
-    int part_pairs_kmax = 11;                 /* pairs mode for k <= this */
+    int part_pairs_kmax = 12;                 /* pairs mode for k <= this (FINDKMER_TUNE pairs_kmax; k = 12 pairs:
+                                                 2048 slices of 32-code runs, half the entries of
+                                                 512 single-window slices: 1 G-base step 1.63 -> 1.36 ms) */
     uint32_t general_tiles = FK_COUNT_GENERAL_TILES;   /* per range in k_count */
     /* device state */
     uint32_t *d_table = nullptr, *d_short = nullptr;
@@ -3831,6 +3833,7 @@ extern "C" int fk_engine_create(int k, const fk_opts *opts, fk_engine **out) {
     if (!e->no_mixed) e->general_tiles = 2;
     if (tune_knob("part_waves", &kv)) e->part_waves = kv == 8u || kv == 16u ? (uint32_t)kv : 0u;
     if (tune_knob("part_pipe", &kv)) e->part_pipe = kv != 0;
+    if (tune_knob("pairs_kmax", &kv)) e->part_pairs_kmax = (int)std::min<uint64_t>(kv, 12u);
     if (tune_knob("idx_rm", &kv)) e->idx_rm = kv != 0;
     if (tune_knob("part_stagger", &kv)) e->part_stagger = (uint32_t)std::min<uint64_t>(kv, 4u);
     if (tune_knob("part_general", &kv)) e->part_general = (uint32_t)kv;
@@ -4164,7 +4167,7 @@ static int launch_part(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t l
                        const XState *exact = nullptr) {
     PartGeo pg;
     const int k = e->k;
-    /* k <= 11: (k+1)-mer pairs at every other base (half the entries), plus
+    /* k <= 12: (k+1)-mer pairs at every other base (half the entries), plus
        the single k-mers at the first slot of halves with a '\n' */
     const bool pairs = k <= e->part_pairs_kmax;
     const int kb = pairs ? k + 1 : k;                      /* bits of a pair (or window) code: 2 kb */
@@ -4227,7 +4230,7 @@ static int launch_part(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t l
     pg.codes = e->d_codes;
     pg.idx = e->d_pidx;
     /* the pipelined main pass where wave 0 scans the slices alone (<= 512) */
-    const bool pipe = e->part_pipe && !c32 && !pg.split && (pg.nslices <= 512u || (!pairs && W == 16u && pg.nslices == 2048u));
+    const bool pipe = e->part_pipe && !c32 && !pg.split && (pg.nslices <= 512u || (W == 16u && pg.nslices == 2048u));
     auto kmain = c32 ? k_part<false, false, 16u, PART_SM(16u), true>
                  : pg.split ? k_part<false, false, 16u, PART_BIG>
                  : W == 16u ? (pairs ? (pipe ? (k == 11 ? k_part<true, false, 16u, PART_SM(16u), false, true, 11u>

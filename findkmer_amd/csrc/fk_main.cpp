@@ -480,9 +480,10 @@ static int run_k(int argc) {
         const int kk = sweep_kmax > config.k ? sweep_kmax : config.k;
         /* bytes per input byte: the file + partition codes (16-bit: 2 per
            region; 32-bit for k = 15, 16: 8, + 2 of part streams), or for
-           k >= 17 the engine's copy of the input; plus the dense table */
+           k >= 17 the engine's copy of the input; plus the dense table (and
+           for 8 <= k <= 12 the 4^(k+1) pair + 4^k single bins of pairs mode) */
         const uint64_t per = kk > FK_K_MAX_DENSE ? 3 : kk >= 15 ? 11 : (kk >= 8 ? 4 : 2);
-        const uint64_t table = kk > FK_K_MAX_DENSE ? 0 : 4ull << (2 * kk);
+        const uint64_t table = kk > FK_K_MAX_DENSE ? 0 : (4ull << (2 * kk)) * (kk >= 8 && kk <= 12 ? 6 : 1);   /* + pair bins */
         int dsel = fk_device_select(fsize * per + table + (256ull << 20), &g_device);
         if (dsel == FK_E_INVALID) {
             fprintf(stderr, "findKmer: FINDKMER_DEVICE names no visible GPU\n");

@@ -649,7 +649,15 @@ def test_cli_q0_warnings_interleave_like_reference(ingest, tmp_path):
     ref, _ = _run_merged([oracle.REF_BIN] + args, b)
     assert rc == 0, ours[-500:]
     assert ref.count(b"Unknown character") > 100 and ref.count(b"Read ") > 100
-    assert ours.startswith(ref), next(i for i in range(len(ref)) if ours[i] != ref[i])
+    # the reference's crash in free() at exit (:1370) may leave glibc's fatal
+    # message at the end of its stderr (when there is no terminal to write it
+    # to): it is no part of the program's output
+    for tag in (b"free(): ", b"double free", b"munmap_chunk(): ", b"malloc(): ", b"corrupted "):
+        cut = ref.rfind(tag)
+        if cut >= 0 and len(ref) - cut < 256:
+            ref = ref[:cut]
+    i = next((i for i in range(min(len(ref), len(ours))) if ours[i] != ref[i]), None)
+    assert ours.startswith(ref), (i, ref[max(0, (i or 0) - 80):(i or 0) + 80], ours[max(0, (i or 0) - 80):(i or 0) + 80])
     assert len(ours) - len(ref) <= 4096   # the reference's lost stdout block at most
 
 

@@ -8,8 +8,8 @@ under profiles/:
                                            for the workload of B input bytes
 
 The dominant kernel is matched by its exact template prefix: the main k_part
-pass `k_part<true, false` (8 <= k <= 11) / `k_part<false, false` (k = 12,
-13; not the k_part<.., true> resume launches) or `k_count<` (k <= 7 and
+pass `k_part<true, false` (8 <= k <= 12) / `k_part<false, false` (k = 13;
+not the k_part<.., true> resume launches) or `k_count<` (k <= 7 and
 14 <= k <= 16).
 
 HBM bytes per launch follow MI355X_MICROARCH.md (HBM section): FETCH_SIZE
@@ -37,8 +37,8 @@ repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 out = os.path.join(repo, "profiles")
 os.makedirs(out, exist_ok=True)
 
-# k_part's template: <PAIRS, RES, W>; pairs mode for k <= 11, single windows for k = 12, 13
-main = args.kernel or ("k_part<true, false" if 8 <= k <= 11 else "k_part<false, false" if 12 <= k <= 16
+# k_part's template: <PAIRS, RES, W>; pairs mode for k <= 12, single windows for k = 13..16
+main = args.kernel or ("k_part<true, false" if 8 <= k <= 12 else "k_part<false, false" if 13 <= k <= 16
                        else "k_count<")
 main_short = main.split("<")[0]
 
