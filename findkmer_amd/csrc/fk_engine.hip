@@ -2440,7 +2440,7 @@ k_part(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint
             if (ph_ == NT - 1) {                                                     \
                 const uint32_t j_ = round / NT;                                      \
                 const bool more_ = __syncthreads_or(!done);                          \
-                if (pg.nslices > 512u) {   /* k = 13: the scan over all waves */    \
+                if (KC == 0 && pg.nslices > 512u) {   /* 2048 slices: the scan over all waves */ \
                     const uint32_t mine_ = part_scan_sum(pg, hist, W, scr);          \
                     if (j_ > 0) part_writeout<W>(pg, row0 + j_ - 1, tot[(j_ - 1) & 1u], (const uint16_t *)ent, \
                                                  threadIdx.x, PART_BLOCK_W(W));       \
