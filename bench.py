@@ -268,6 +268,18 @@ def measure(ctx, k, n, L, seed, chrom, steps, warmup, verify=False):
         want = expected_windows(world * n, k, chrom if chrom_on else 0)
         assert total == want, (total, want)
 
+    # what RCCL itself reports for the communicator the exchange ran on, from
+    # every rank: the world the line claims is the world that ran
+    rccl = None
+    if merged is not None and merged.transport == "rccl-native":
+        comm = fkdist.native_comm(None)
+        mine = torch.tensor(list(comm.info()) + [ctx.local], dtype=torch.int64, device=ctx.coll_dev)
+        every = [torch.zeros_like(mine) for _ in range(world)]
+        dist.all_gather(every, mine)
+        rows = [[int(x) for x in t.tolist()] for t in every]
+        rccl = {"nranks": rows[0][0], "ranks": [r[1] for r in rows], "devices": [r[2] for r in rows],
+                "local_ranks": [r[3] for r in rows]}
+
     check = None
     if verify:
         check = verify_single(ctx, k, n, L, seed, chrom if chrom_on else 0, merged, last)
@@ -290,6 +302,7 @@ def measure(ctx, k, n, L, seed, chrom, steps, warmup, verify=False):
             "kernel": main, "kernel_ms": kern_ms, "timed_launches": timed,
             "algorithmic_bytes": algo_bytes,
             "step_achieved": step_gbs, "step_frac": step_gbs / HBM_PEAK_GBS,
+            "step_traffic": traffic_for(k, L, nbytes, main, "hbm_bytes_per_step"),
         },
     }
     if phase_s:
@@ -297,6 +310,8 @@ def measure(ctx, k, n, L, seed, chrom, steps, warmup, verify=False):
     if merged is not None:
         rec["exchange"] = merged.path
         rec["transport"] = merged.transport
+    if rccl is not None:
+        rec["rccl"] = rccl
     if check is not None:
         rec["verify"] = check
     eng.close()
@@ -305,26 +320,33 @@ def measure(ctx, k, n, L, seed, chrom, steps, warmup, verify=False):
     return rec
 
 
-def traffic_for(k, L, nbytes, main):
-    """HBM bytes per launch of the dominant kernel from the committed PMC
-    profile of this exact workload (profiles/traffic_k<K>_L<L>_n<bytes>.json,
-    written by tools/profile_summary.py), else None."""
+def traffic_for(k, L, nbytes, main, what="hbm_bytes_per_launch"):
+    """HBM bytes from the committed PMC profile of this exact workload
+    (profiles/traffic_k<K>_L<L>_n<bytes>.json, written by
+    tools/profile_summary.py), else None: per launch of the dominant kernel
+    (`hbm_bytes_per_launch`), or per step, every kernel of the step summed
+    (`hbm_bytes_per_step`)."""
     tf = os.path.join(REPO, "profiles", f"traffic_k{k}_L{L}_n{nbytes}.json")
     try:
         prof = json.load(open(tf))
     except Exception:
         return None
     if prof.get("input_bytes") == nbytes and prof.get("kernel") == main:
-        return prof.get("hbm_bytes_per_launch")
+        return prof.get(what)
     return None
 
 
 def verify_single(ctx, k, n, L, seed, chrom, merged, last):
     """configs[3] parity: rank 0 counts the whole world x n stream with one
-    engine and compares it with the sharded pass's merged table and counters."""
+    engine and compares it with the sharded pass's merged table and counters.
+    Every rank takes part in gathering the merged table first (a collective
+    when the table is sharded over the ranks: k >= 12, or sparse for k >= 17)."""
     import numpy as np
     import torch
     import findkmer_amd as fk
+    if merged is None:
+        raise SystemExit("--verify-single needs a sharded run (torchrun)")
+    full = merged.table_full()          # collective; None except on rank 0
     if ctx.rank != 0:
         return None
     buf, size = make_genome(ctx.world * n, L, seed, chrom)
@@ -332,13 +354,14 @@ def verify_single(ctx, k, n, L, seed, chrom, merged, last):
     with fk.Engine(k, device=ctx.local) as e:
         e.feed_device(buf.data_ptr(), size)
         rc, r = e.finish()
-        t = e.table()
+        if k > fk.FK_K_MAX_DENSE:
+            keys, cnts = e.sparse()
+            equal = bool(np.array_equal(full[0], keys) and np.array_equal(full[1], cnts))
+        else:
+            equal = bool(np.array_equal(full.cpu().numpy().view(np.uint32), e.table()))
     del buf
     torch.cuda.empty_cache()
-    if merged is None:
-        raise SystemExit("--verify-single needs a sharded run (torchrun)")
-    got = merged.table.cpu().numpy().view(np.uint32)
-    out = {"table_equal": bool(np.array_equal(got, t)), "status": rc}
+    out = {"table_equal": equal, "status": rc}
     for key in ("windows", "valid_bases", "unknown_chars", "scanned_bytes", "hit_eof_byte",
                 "unterminated_header", "distinct"):
         out[key] = [int(getattr(merged, key)), int(getattr(r, key))]
@@ -400,7 +423,7 @@ def main():
         },
         "roofline": head["roofline"],
     }
-    for key in ("phase_ms_per_step", "exchange", "transport", "verify"):
+    for key in ("phase_ms_per_step", "exchange", "transport", "rccl", "verify"):
         if key in head:
             out[key] = head[key]
     if ns is not None:
@@ -413,6 +436,13 @@ def main():
         out["cpu_baseline"] = cpu_baseline(args.k, args.seed, args.fasta_line, sample)
         out["cpu_baseline_multicore"] = cpu_baseline_multicore(args.k, args.seed, args.fasta_line,
                                                                min(1 << 30, args.bases))
+        # the sample's rate applied to the whole configured workload (the
+        # reference's loop is linear in the input: one fgetc and one trie walk
+        # per byte, findKmer.cpp:988-1062)
+        for key in ("cpu_baseline", "cpu_baseline_multicore"):
+            out[key]["extrapolated_s_full_config"] = round(args.bases / out[key]["value"], 1)
+            out[key]["extrapolation"] = (f"sample rate x {args.bases} bases (linear: the reference scans "
+                                         f"once per byte, findKmer.cpp:988)")
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist:

@@ -37,6 +37,7 @@ FK_XCHG_FAST = 1          # fk_engine_shard_exchange flags (info[0])
 FK_XCHG_SHARD_TABLE = 2
 FK_XCHG_TEST_INVALID = 4
 FK_COMM_ID_BYTES = 128
+FK_UPSTREAM_REC = 1019    # fk_synth_upstream_device's record: ">ENST%011u\n" + 1001 bases + "\n"
 
 
 class FkState(ctypes.Structure):
@@ -107,6 +108,8 @@ SIGNATURES = [
     ("fk_engine_shard_exchange", ctypes.c_int, [_P, _P, _P, ctypes.POINTER(ctypes.c_int32)]),
     ("fk_merge_layout", ctypes.c_int, [ctypes.c_int, ctypes.c_int, _U64P, _U64P]),
     ("fk_comm_available", ctypes.c_int, [ctypes.c_int]),
+    ("fk_comm_info", ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int),
+                                    ctypes.POINTER(ctypes.c_int)]),
     ("fk_shard_rows_compose", ctypes.c_int, [_P, ctypes.c_int, ctypes.c_int, ctypes.POINTER(FkState)]),
     ("fk_engine_finish", ctypes.c_int, [_P, ctypes.POINTER(FkResult)]),
     ("fk_engine_table", ctypes.c_int, [_P, _U32P]),
@@ -121,11 +124,15 @@ SIGNATURES = [
     ("fk_engine_unknown_since", ctypes.c_int, [_P, ctypes.c_uint64, _U8P, _U64P, ctypes.c_uint64, _U64P]),
     ("fk_engine_sparse", ctypes.c_int, [_P, _U64P, _U32P, ctypes.c_uint64, _U64P]),
     ("fk_engine_sparse_device", ctypes.c_int, [_P, _P, _P, ctypes.c_uint64, _U64P]),
+    ("fk_engine_sparse_range", ctypes.c_int, [_P, ctypes.c_uint64, ctypes.c_uint64, _U64P, _U32P, ctypes.c_uint64,
+                                              _U64P]),
     ("fk_engine_sparse_split", ctypes.c_int, [_P, ctypes.c_int, _U64P]),
     ("fk_engine_sparse_adopt", ctypes.c_int, [_P, _P, _P, ctypes.c_uint64, _U64P]),
     ("fk_count", ctypes.c_int, [_P, ctypes.c_uint64, ctypes.c_int, ctypes.POINTER(FkOpts), _U32P, ctypes.POINTER(FkResult)]),
     ("fk_count_multi", ctypes.c_int, [_P, ctypes.c_uint64, ctypes.c_int, ctypes.c_int, ctypes.POINTER(FkOpts), _U32P, ctypes.POINTER(FkResult)]),
     ("fk_synth_device", ctypes.c_int, [_P, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int, _P, _U64P]),
+    ("fk_synth_upstream_device", ctypes.c_int, [_P, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
+                                                ctypes.c_uint64, _P, _U64P]),
     ("fk_input_load", ctypes.c_int, [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.POINTER(_P)]),
     ("fk_input_info", ctypes.c_int, [_P, ctypes.POINTER(_P), _U64P, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_double)]),
     ("fk_input_destroy", None, [_P]),
@@ -326,6 +333,18 @@ class Engine:
                                       ctypes.byref(n)), "sparse")
         return keys[: n.value], cnts[: n.value]
 
+    def sparse_range(self, key_lo, key_hi):
+        """17 <= k <= 20, after finish(): the runs with keys in [key_lo,
+        key_hi) (uint64 keys ascending, uint32 counts)"""
+        import numpy as np
+        n = ctypes.c_uint64()
+        _check(lib().fk_engine_sparse_range(self.h, key_lo, key_hi, None, None, 0, ctypes.byref(n)), "sparse_range")
+        keys = np.zeros(max(1, n.value), dtype=np.uint64)
+        cnts = np.zeros(max(1, n.value), dtype=np.uint32)
+        _check(lib().fk_engine_sparse_range(self.h, key_lo, key_hi, keys.ctypes.data_as(_U64P),
+                                            cnts.ctypes.data_as(_U32P), n.value, ctypes.byref(n)), "sparse_range")
+        return keys[: n.value], cnts[: n.value]
+
     @property
     def sparse_table(self):
         """17 <= k <= 20: the table is sparse (sparse(), the sparse_* merge)"""
@@ -395,6 +414,13 @@ class Comm:
         self.h = h
         self.world, self.rank, self.device = world, rank, device
 
+    def info(self):
+        """(rank count, rank, device) as RCCL reports them (fk_comm_info;
+        -1 where this RCCL lacks the query)"""
+        n, r, d = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        _check(lib().fk_comm_info(self.h, ctypes.byref(n), ctypes.byref(r), ctypes.byref(d)), "comm_info")
+        return n.value, r.value, d.value
+
     def close(self):
         if getattr(self, "h", None):
             lib().fk_comm_destroy(self.h)
@@ -449,6 +475,16 @@ def count(data, k, ngpu=1, want_nodes=False):
 def synth_device(ptr, cap, n_bases, seed, fasta_line=0, stream=None):
     w = ctypes.c_uint64()
     _check(lib().fk_synth_device(ptr, cap, n_bases, seed, fasta_line, stream, ctypes.byref(w)), "synth")
+    return w.value
+
+
+def synth_upstream_device(ptr, cap, n_records, seed, first_rec=0, stream=None):
+    """fk_synth_upstream_device: records [first_rec, first_rec + n_records)
+    of the upstream-like FASTA (BASELINE.json configs[4]) into a device
+    buffer; returns the bytes written"""
+    w = ctypes.c_uint64()
+    _check(lib().fk_synth_upstream_device(ptr, cap, first_rec, n_records, seed, stream, ctypes.byref(w)),
+           "synth_upstream")
     return w.value
 
 

@@ -18,7 +18,3 @@ int fkc_reduce_i32(fk_comm *c, int32_t *buf, size_t n, int root, hipStream_t s);
 /* in-place reduce-scatter: the sum of buf[0, world * per_rank) over the
    ranks; rank r receives its block at buf + r * per_rank */
 int fkc_reduce_scatter_i32(fk_comm *c, int32_t *buf, size_t per_rank, hipStream_t s);
-/* all-to-all of byte ranges (grouped sends and receives): to rank p
-   send[send_off[p], +send_len[p]), from rank p into recv[recv_off[p], +recv_len[p]) */
-int fkc_alltoallv_u8(fk_comm *c, const uint8_t *send, const uint64_t *send_off, const uint64_t *send_len,
-                     uint8_t *recv, const uint64_t *recv_off, const uint64_t *recv_len, hipStream_t s);

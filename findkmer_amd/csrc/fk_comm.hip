@@ -31,11 +31,11 @@ struct Rccl {
     decltype(&ncclAllReduce) all_reduce = nullptr;
     decltype(&ncclReduce) reduce = nullptr;
     decltype(&ncclReduceScatter) reduce_scatter = nullptr;
-    decltype(&ncclAllGather) all_gather = nullptr;
-    decltype(&ncclSend) send = nullptr;
-    decltype(&ncclRecv) recv = nullptr;
-    decltype(&ncclGroupStart) group_start = nullptr;
-    decltype(&ncclGroupEnd) group_end = nullptr;
+    /* optional (fk_comm_info only; a missing one does not turn the
+       communicator off) */
+    decltype(&ncclCommCount) count = nullptr;
+    decltype(&ncclCommUserRank) user_rank = nullptr;
+    decltype(&ncclCommCuDevice) cu_device = nullptr;
     bool ok = false;
 };
 
@@ -54,13 +54,11 @@ const Rccl &rccl() {
         x.all_reduce = (decltype(x.all_reduce))dlsym(h, "ncclAllReduce");
         x.reduce = (decltype(x.reduce))dlsym(h, "ncclReduce");
         x.reduce_scatter = (decltype(x.reduce_scatter))dlsym(h, "ncclReduceScatter");
-        x.all_gather = (decltype(x.all_gather))dlsym(h, "ncclAllGather");
-        x.send = (decltype(x.send))dlsym(h, "ncclSend");
-        x.recv = (decltype(x.recv))dlsym(h, "ncclRecv");
-        x.group_start = (decltype(x.group_start))dlsym(h, "ncclGroupStart");
-        x.group_end = (decltype(x.group_end))dlsym(h, "ncclGroupEnd");
-        x.ok = x.get_id && x.init_rank && x.destroy && x.all_reduce && x.reduce && x.reduce_scatter &&
-               x.all_gather && x.send && x.recv && x.group_start && x.group_end;
+        x.count = (decltype(x.count))dlsym(h, "ncclCommCount");
+        x.user_rank = (decltype(x.user_rank))dlsym(h, "ncclCommUserRank");
+        x.cu_device = (decltype(x.cu_device))dlsym(h, "ncclCommCuDevice");
+        /* exactly the entry points the exchange calls */
+        x.ok = x.get_id && x.init_rank && x.destroy && x.all_reduce && x.reduce && x.reduce_scatter;
         return x;
     }();
     return r;
@@ -149,16 +147,17 @@ int fkc_reduce_scatter_i32(fk_comm *c, int32_t *buf, size_t per_rank, hipStream_
                : FK_E_RCCL;
 }
 
-int fkc_alltoallv_u8(fk_comm *c, const uint8_t *send, const uint64_t *send_off, const uint64_t *send_len,
-                     uint8_t *recv, const uint64_t *recv_off, const uint64_t *recv_len, hipStream_t s) {
+/* What RCCL itself reports for the communicator: its rank count, this
+   rank and the device it drives (-1 where this RCCL lacks the query). */
+extern "C" int fk_comm_info(fk_comm *c, int *nranks, int *rank, int *device) {
     if (!c || !c->nc || !rccl().ok) return FK_E_RCCL;
     const Rccl &r = rccl();
-    if (r.group_start() != ncclSuccess) return FK_E_RCCL;
-    bool ok = true;
-    for (int p = 0; p < c->world && ok; p++) {
-        if (send_len[p]) ok = r.send(send + send_off[p], send_len[p], ncclUint8, p, c->nc, s) == ncclSuccess;
-        if (ok && recv_len[p]) ok = r.recv(recv + recv_off[p], recv_len[p], ncclUint8, p, c->nc, s) == ncclSuccess;
-    }
-    const bool end_ok = r.group_end() == ncclSuccess;
-    return ok && end_ok ? FK_OK : FK_E_RCCL;
+    int n = -1, me = -1, dev = -1;
+    if (r.count && r.count(c->nc, &n) != ncclSuccess) return FK_E_RCCL;
+    if (r.user_rank && r.user_rank(c->nc, &me) != ncclSuccess) return FK_E_RCCL;
+    if (r.cu_device && r.cu_device(c->nc, &dev) != ncclSuccess) return FK_E_RCCL;
+    if (nranks) *nranks = n;
+    if (rank) *rank = me;
+    if (device) *device = dev;
+    return FK_OK;
 }

@@ -228,13 +228,10 @@ extern "C" int fk_device_select(uint64_t need, int *device) {
         std::vector<uint64_t> fr((size_t)ndev, 0);
         bool sysfs = true;
         for (int d = 0; d < ndev && sysfs; d++) sysfs = sysfs_free_vram(d, &fr[(size_t)d]);
-        if (!sysfs) {
-            for (int d = 0; d < ndev; d++) {
-                size_t f = 0, t = 0;
-                if (hipSetDevice(d) == hipSuccess && hipMemGetInfo(&f, &t) == hipSuccess) fr[(size_t)d] = f;
-            }
-        }
-        dev = fk_device_policy(ndev, fr.data(), need, (uint32_t)getpid());
+        /* without the sysfs counters, no probing: a hipMemGetInfo per device
+           would create a HIP context (and its HBM) on every GPU in every one
+           of the sweep's processes; spread them by pid alone */
+        dev = sysfs ? fk_device_policy(ndev, fr.data(), need, (uint32_t)getpid()) : (int)((uint32_t)getpid() % (uint32_t)ndev);
     }
     if (hipSetDevice(dev) != hipSuccess) return FK_E_HIP;
     *device = dev;

@@ -325,28 +325,37 @@ class SparseShardedResult(ShardedResult):
 
     def table_full(self, dst=0):
         """(keys, counts) of the whole merged table on rank `dst` (a
-        collective: every rank calls it), None on the others."""
+        collective: every rank calls it), None on the others.  Only `dst`
+        receives the other ranks' runs (point-to-point, exact sizes): no rank
+        but dst ever holds more than its own slice."""
         import numpy as np
         dev = "cuda" if dist.get_backend(self.group) == "nccl" else "cpu"
         n = torch.tensor([len(self.keys)], dtype=torch.int64, device=dev)
         sizes = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in range(self.world)]
         dist.all_gather(sizes, n, group=self.group)
         sizes = [int(v.item()) for v in sizes]
-        m = max(1, max(sizes))
-        kp = torch.zeros(m, dtype=torch.int64)
-        cp = torch.zeros(m, dtype=torch.int32)
-        kp[:len(self.keys)] = torch.from_numpy(self.keys.view(np.int64))
-        cp[:len(self.counts)] = torch.from_numpy(self.counts.view(np.int32))
-        kp, cp = kp.to(dev), cp.to(dev)
-        gk = [torch.empty_like(kp) for _ in range(self.world)]
-        gc = [torch.empty_like(cp) for _ in range(self.world)]
-        dist.all_gather(gk, kp, group=self.group)
-        dist.all_gather(gc, cp, group=self.group)
+        g = (lambda r: dist.get_global_rank(self.group, r)) if self.group is not None else (lambda r: r)
         if self.rank != dst:
+            if sizes[self.rank]:
+                kp = torch.from_numpy(self.keys.view(np.int64)).to(dev)
+                cp = torch.from_numpy(self.counts.view(np.int32)).to(dev)
+                dist.send(kp, g(dst), group=self.group)
+                dist.send(cp, g(dst), group=self.group)
             return None
-        keys = np.concatenate([gk[r][:sizes[r]].cpu().numpy() for r in range(self.world)]).view(np.uint64)
-        cnts = np.concatenate([gc[r][:sizes[r]].cpu().numpy() for r in range(self.world)]).view(np.uint32)
-        return keys, cnts
+        keys, cnts = [], []
+        for r in range(self.world):
+            if r == self.rank:
+                keys.append(self.keys)
+                cnts.append(self.counts)
+            elif sizes[r]:
+                kp = torch.empty(sizes[r], dtype=torch.int64, device=dev)
+                cp = torch.empty(sizes[r], dtype=torch.int32, device=dev)
+                dist.recv(kp, g(r), group=self.group)
+                dist.recv(cp, g(r), group=self.group)
+                keys.append(kp.cpu().numpy().view(np.uint64))
+                cnts.append(cp.cpu().numpy().view(np.uint32))
+        return (np.concatenate(keys) if keys else np.zeros(0, np.uint64),
+                np.concatenate(cnts) if cnts else np.zeros(0, np.uint32))
 
 
 def _sparse_merge(engine, vals, counting, rank, world, group, first_end, r):

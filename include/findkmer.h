@@ -33,7 +33,10 @@
 extern "C" {
 #endif
 
-#define FK_ABI_VERSION 1
+/* 2 (round 4): fk_engine_shard_exchange's merge buffer is the table padded
+   to a multiple of `world` plus FK_PACK_STATS words (fk_merge_layout), and
+   fk_state.ended is checked (it was padding in 1) */
+#define FK_ABI_VERSION 2
 #define FK_K_MIN 1
 #define FK_K_MAX_DENSE 16   /* 4^16 uint32 = 16 GiB table on one 288 GB GPU */
 #define FK_K_MAX_REF 20     /* the reference accepts k <= 20 (:438) */
@@ -203,6 +206,10 @@ typedef struct fk_comm fk_comm;
 int  fk_comm_id(uint8_t *id /* FK_COMM_ID_BYTES */);
 int  fk_comm_create(const uint8_t *id, int world, int rank, int device, fk_comm **out);
 void fk_comm_destroy(fk_comm *c);
+/* What RCCL reports for the communicator (ncclCommCount, ncclCommUserRank,
+ * ncclCommCuDevice; -1 for a query this RCCL lacks): lets a sharded run's
+ * output prove the world it ran in. */
+int  fk_comm_info(fk_comm *c, int *nranks, int *rank, int *device);
 /* The merge buffer of a sharded pass (int32 words, device memory for
  * fk_engine_shard_exchange):
  *   [0, TW)           the count table, TW = 4^k rounded up to a multiple of
@@ -297,6 +304,11 @@ int  fk_engine_unknown_since(fk_engine *e, uint64_t first, uint8_t *out, uint64_
  * kept until reset: fk_engine_finish builds the table from it in key-range
  * passes sized to the free HBM) plus 12 bytes per distinct k-mer. */
 int  fk_engine_sparse(fk_engine *e, uint64_t *keys, uint32_t *counts, uint64_t cap, uint64_t *n);
+/* The runs with keys in [key_lo, key_hi) (a contiguous piece of the table,
+ * found by binary search): *n = their number, min(cap, *n) copied to host
+ * memory -- a 10 GB input's table (~90 GB at k = 17) read piece by piece. */
+int  fk_engine_sparse_range(fk_engine *e, uint64_t key_lo, uint64_t key_hi, uint64_t *keys, uint32_t *counts,
+                            uint64_t cap, uint64_t *n);
 /* The same into device buffers. */
 int  fk_engine_sparse_device(fk_engine *e, uint64_t *keys, uint32_t *counts, uint64_t cap, uint64_t *n);
 
@@ -332,6 +344,20 @@ int  fk_synth_device(uint8_t *dev_out, uint64_t cap, uint64_t n_bases,
                      uint64_t seed, int fasta_line, void *stream,
                      uint64_t *written);
 
+/* Deterministic on-device upstream-regions-like FASTA (BASELINE.json
+ * configs[4]; what get_upstreams.pl writes, findKmer/get_upstreams.pl:82-91):
+ * records ">ENST%011u\n" + 1001 bases + "\n" (FK_UPSTREAM_REC bytes), record
+ * r numbered first_rec + r; its bases uniform ACGT from splitmix64 of (seed,
+ * record, word), and with probability 1/100 (from splitmix64 of (seed,
+ * record)) a run of 50 'N' at an offset in [0, 951) drawn from the same
+ * word.  Writes min(cap, n_records * FK_UPSTREAM_REC) bytes of records
+ * [first_rec, first_rec + n_records) into dev_out on `stream`; the bytes
+ * depend only on (seed, record number), so shards of one file are
+ * generated independently. */
+#define FK_UPSTREAM_REC 1019
+int  fk_synth_upstream_device(uint8_t *dev_out, uint64_t cap, uint64_t first_rec, uint64_t n_records,
+                              uint64_t seed, void *stream, uint64_t *written);
+
 /* ---- file ingest (replaces the reference's per-byte fgetc reads of
  * config.sequence_file_pointer, findKmer.cpp:988, with a device-resident
  * copy of the whole file) --------------------------------------------------
@@ -363,7 +389,8 @@ int  fk_input_headers(fk_input *in, int k, uint64_t *pos, uint64_t *bases, uint6
  * FK_E_INVALID for a bad value); otherwise, among the devices whose free HBM
  * is >= need bytes, the one at (pid mod their count), so processes started
  * together spread over the GPUs; if none has enough, the one with the most
- * free HBM.  fk_device_policy is that rule alone (free_bytes[ndev] given):
+ * free HBM.  Free HBM is read from sysfs (no HIP context on the other
+ * GPUs); where sysfs has no VRAM counters, the choice is pid mod ndev.  fk_device_policy is that rule alone (free_bytes[ndev] given):
  * returns the ordinal. */
 int  fk_device_select(uint64_t need, int *device);
 int  fk_device_policy(int ndev, const uint64_t *free_bytes, uint64_t need, uint32_t salt);

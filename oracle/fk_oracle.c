@@ -418,6 +418,124 @@ out:
     return rc;
 }
 
+/* ---------------- key ranges of a large-k table, split over threads ----
+ *
+ * The windows whose k-mer index falls in one of nr ascending, disjoint key
+ * ranges [key_lo[r], key_hi[r]) -- slices of the reference's trie leaves in
+ * DFS order (:719-724) -- counted in dense slice arrays, the stream cut into
+ * pieces as in fko_count_dense_par (each from its exact entering state), so
+ * that a 10 GB input's k >= 17 table can be checked slice by slice with
+ * bounded host memory, several slices per scan. */
+#define FKO_MAX_RANGES 8
+typedef struct { uint32_t *counts; int nr; uint64_t lo[FKO_MAX_RANGES], span[FKO_MAX_RANGES], base[FKO_MAX_RANGES]; } range_ctx;
+
+static inline void range_emit(void *ctx, uint64_t code) {
+    range_ctx *c = (range_ctx *)ctx;
+    for (int r = 0; r < c->nr; r++) {
+        const uint64_t d = code - c->lo[r];   /* wraps above 2^64 for code < lo */
+        if (d < c->span[r]) { c->counts[c->base[r] + d]++; return; }
+    }
+}
+
+typedef struct {
+    const uint8_t *buf;
+    uint64_t lo, hi;
+    int k;
+    range_ctx ctx;
+    fko_result res;
+    int rc;
+} rpiece_t;
+
+static void *rpiece_run(void *arg) {
+    rpiece_t *p = (rpiece_t *)arg;
+    scan_state st;
+    entry_state(p->buf, p->lo, p->k, &st);
+    fko_result res;
+    short_list shorts = { 0, 0, 0 };
+    p->rc = scan(p->buf + p->lo, p->hi - p->lo, p->k, range_emit, &p->ctx, &res, &shorts, NULL, 0,
+                 p->lo ? &st : NULL);
+    free(shorts.v);
+    p->res = res;
+    return NULL;
+}
+
+int fko_count_sparse_range(const uint8_t *buf, uint64_t len, int k, const uint64_t *key_lo, const uint64_t *key_hi,
+                           int nr, uint64_t *codes, uint32_t *counts, uint64_t cap, uint64_t *n_unique,
+                           fko_result *res, int threads) {
+    if (k < 1 || k > 20 || nr < 1 || nr > FKO_MAX_RANGES) return -1;
+    range_ctx proto;
+    memset(&proto, 0, sizeof proto);
+    proto.nr = nr;
+    uint64_t total = 0;
+    for (int r = 0; r < nr; r++) {
+        if (key_hi[r] <= key_lo[r] || (r && key_lo[r] < key_hi[r - 1])) return -1;
+        proto.lo[r] = key_lo[r];
+        proto.span[r] = key_hi[r] - key_lo[r];
+        proto.base[r] = total;
+        total += proto.span[r];
+    }
+    if (total > (1ull << 30)) return -1;
+    if (threads < 1) threads = 1;
+    if ((uint64_t)threads > len / 4096 + 1) threads = (int)(len / 4096 + 1);
+    rpiece_t *pc = (rpiece_t *)calloc((size_t)threads, sizeof(rpiece_t));
+    pthread_t *th = (pthread_t *)calloc((size_t)threads, sizeof(pthread_t));
+    int rc = -1;
+    if (!pc || !th) goto out;
+    for (int t = 0; t < threads; t++) {
+        pc[t].buf = buf;
+        pc[t].lo = len * (uint64_t)t / (uint64_t)threads;
+        pc[t].hi = len * (uint64_t)(t + 1) / (uint64_t)threads;
+        pc[t].k = k;
+        pc[t].ctx = proto;
+        pc[t].ctx.counts = (uint32_t *)calloc(total, sizeof(uint32_t));
+        if (!pc[t].ctx.counts) goto out;
+    }
+    for (int t = 0; t < threads; t++) pthread_create(&th[t], NULL, rpiece_run, &pc[t]);
+    for (int t = 0; t < threads; t++) pthread_join(th[t], NULL);
+    for (int t = 0; t < threads; t++) if (pc[t].rc) goto out;
+    int used = threads;
+    for (int t = 0; t < threads; t++)
+        if (pc[t].res.hit_eof_byte) { used = t + 1; break; }
+    for (int t = 1; t < used; t++)
+        for (uint64_t i = 0; i < total; i++) pc[0].ctx.counts[i] += pc[t].ctx.counts[i];   /* u32, wraps like :110 */
+    memset(res, 0, sizeof(*res));
+    for (int t = 0; t < used; t++) {
+        const fko_result *r = &pc[t].res;
+        for (int b = 0; b < 4; b++) {
+            res->base_count[b] += r->base_count[b];
+            res->depth1[b] += r->depth1[b];
+        }
+        res->valid_bases += r->valid_bases;
+        res->windows += r->windows;
+        res->unknown_chars += r->unknown_chars;
+        if (t == used - 1) {
+            res->scanned_bytes = pc[t].lo + r->scanned_bytes;
+            res->hit_eof_byte = r->hit_eof_byte;
+            res->unterminated_header = r->unterminated_header;
+        }
+    }
+    {
+        uint64_t u = 0;
+        for (int r = 0; r < nr; r++)
+            for (uint64_t i = 0; i < proto.span[r]; i++) {
+                const uint32_t c = pc[0].ctx.counts[proto.base[r] + i];
+                if (c) {
+                    if (u < cap) { codes[u] = proto.lo[r] + i; counts[u] = c; }
+                    u++;
+                }
+            }
+        *n_unique = u;
+        res->distinct = u;   /* within the ranges */
+        rc = u > cap ? -1 : 0;
+    }
+out:
+    if (pc)
+        for (int t = 0; t < threads; t++) free(pc[t].ctx.counts);
+    free(pc);
+    free(th);
+    return rc;
+}
+
 /* ---------------- sparse form ---------------- */
 
 typedef struct { uint64_t *v; uint64_t n, cap; int fail; } vec_ctx;

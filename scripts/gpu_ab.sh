@@ -1,17 +1,16 @@
-# A/B of experiment builds (tools/exp_variant.py) against the product library
-# on one bench workload, interleaved: VARIANTS="nt ntread", K, L, BASES
+# A/B of experiment builds (tools/exp_variant.py) against the product on one
+# box, interleaved: VARIANTS="a b" [ARGS="bench.py args"] [ROUNDS=n]
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-K=${K:-11}; L=${L:-80}; BASES=${BASES:-10000000000}
-one() {   # one <label> <lib or empty>
-  if [ -n "$2" ]; then export FINDKMER_LIB=$2; else unset FINDKMER_LIB; fi
-  timeout -k 10 240 python3 bench.py --k $K --fasta-line $L --bases $BASES --steps ${STEPS:-10} --warmup 2 \
-    --no-cpu-baseline --north-star-bases 0 > gpurun_out/ab.log 2>&1 || { tail -20 gpurun_out/ab.log; exit 1; }
-  python3 -c "import json; d=json.loads(open('gpurun_out/ab.log').read().strip().splitlines()[-1]); r=d['roofline']; print('$1', round(d['ms_per_step'],3), 'ms/step', r['kernel'], round(r['kernel_ms'],3), 'ms')"
-}
-for rep in 1 2; do
-  one product ""
-  for v in $VARIANTS; do one $v build/exp/libfk_$v.so; done
+ARGS=${ARGS:-"--steps 10 --warmup 3 --north-star-bases 0 --no-cpu-baseline"}
+for r in $(seq 1 ${ROUNDS:-2}); do
+  for v in product $VARIANTS; do
+    if [ $v = product ]; then lib=""; else lib=build/exp/libfk_$v.so; fi
+    FINDKMER_LIB=$lib timeout -k 10 240 python bench.py $ARGS > gpurun_out/ab_$v.json 2> gpurun_out/ab_$v.err || { echo "$v failed"; tail -20 gpurun_out/ab_$v.err; exit 1; }
+    python3 -c "
+import json,sys; d=json.load(open('gpurun_out/ab_$v.json')); r=d['roofline']
+print('%-12s step %.3f ms  %s %.3f ms' % ('$v', d['ms_per_step'], r['kernel'], r['kernel_ms']))"
+  done
 done

@@ -50,6 +50,11 @@ def olib():
         L.fko_count_sparse.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int,
                                        ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
                                        ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(FkoResult)]
+        L.fko_count_sparse_range.restype = ctypes.c_int
+        L.fko_count_sparse_range.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int, ctypes.c_void_p,
+                                             ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                                             ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64),
+                                             ctypes.POINTER(FkoResult), ctypes.c_int]
         L.fko_synth.restype = ctypes.c_uint64
         L.fko_synth.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
                                 ctypes.c_int]
@@ -97,6 +102,25 @@ def count_sparse(data, k, cap=1 << 22):
     r = FkoResult()
     rc = olib().fko_count_sparse(a.ctypes.data, n, k, codes.ctypes.data, cnts.ctypes.data, cap,
                                  ctypes.byref(nu), ctypes.byref(r))
+    assert rc == 0
+    return codes[: nu.value], cnts[: nu.value], r
+
+
+def count_sparse_range(data, k, ranges, threads=1):
+    """ranges: ascending disjoint (lo, hi) key ranges.  Returns (distinct
+    indices inside them ascending, their counts, result with the whole
+    stream's counters; result.distinct = the ranges')"""
+    a, n = _buf(data)
+    lo = np.array([r[0] for r in ranges], dtype=np.uint64)
+    hi = np.array([r[1] for r in ranges], dtype=np.uint64)
+    cap = max(1, int((hi - lo).sum()))
+    codes = np.zeros(cap, dtype=np.uint64)
+    cnts = np.zeros(cap, dtype=np.uint32)
+    nu = ctypes.c_uint64()
+    r = FkoResult()
+    rc = olib().fko_count_sparse_range(a.ctypes.data, n, k, lo.ctypes.data, hi.ctypes.data, len(ranges),
+                                       codes.ctypes.data, cnts.ctypes.data, cap, ctypes.byref(nu), ctypes.byref(r),
+                                       threads)
     assert rc == 0
     return codes[: nu.value], cnts[: nu.value], r
 

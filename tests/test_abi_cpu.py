@@ -45,7 +45,7 @@ def test_python_binding_covers_the_header():
 
 def test_abi_version_and_strerror():
     L = fk.lib()
-    assert L.fk_abi_version() == 1
+    assert L.fk_abi_version() == 2
     assert L.fk_strerror(fk.FK_E_EMPTY) == b"Sequence File Is Empty, Ending Program"
     assert L.fk_strerror(fk.FK_E_ROLLOVER) == b"COUNTER ROLLOVER DETECTED"
 

@@ -200,3 +200,32 @@ def test_oracle_pieces_equal_sequential(k):
             assert np.array_equal(t1, t2)
             assert bytes(r1) == bytes(r2)
             assert u1 == u2
+
+
+@pytest.mark.parametrize("k", [3, 9, 17, 20])
+def test_oracle_key_range_equals_sparse_slice(k):
+    """fko_count_sparse_range (one key range, pieces over threads) == the
+    matching slice of the sequential sparse oracle, for ranges at the start,
+    inside and at the end of the index space, with every counter of the
+    stream; the 10 GB k >= 17 GPU tests compare the engine with it"""
+    import random as _r
+    rng = _r.Random(k)
+    parts = []
+    for _ in range(300):
+        parts.append(bytes(rng.choices(b"ACGT", k=rng.randint(1, 3000))))
+        parts.append(rng.choice([b"\n", b"N", b">hdr x\n", b"\n\n", b"acgt"]))
+    data = b"".join(parts)
+    codes, cnts, r = oracle.count_sparse(data, k)
+    top = 1 << (2 * k)
+    span = min(top, 1 << 20)
+    for ranges in ([(0, span)], [(top // 3, top // 3 + span)], [(top - span, top)],
+                   [(0, span // 4), (top // 2, top // 2 + span // 4), (top - span // 4, top)]):
+        c2, n2, r2 = oracle.count_sparse_range(data, k, ranges, threads=5)
+        sel = np.zeros(len(codes), dtype=bool)
+        for lo, hi in ranges:
+            sel |= (codes >= lo) & (codes < hi)
+        assert np.array_equal(c2, codes[sel]) and np.array_equal(n2, cnts[sel])
+        assert r2.distinct == int(sel.sum())
+        assert (r2.windows, r2.valid_bases, list(r2.base_count), list(r2.depth1), r2.unknown_chars,
+                r2.scanned_bytes) == (r.windows, r.valid_bases, list(r.base_count), list(r.depth1),
+                                      r.unknown_chars, r.scanned_bytes)

@@ -172,3 +172,21 @@ def test_sparse_tables_all_to_all_against_oracle(k, world, eof_in, backend):
         assert out[key][0] == out[key][1], (key, out[key])
     assert not out["rollover"]
     assert out["first_end"] == (eof_in if eof_in >= 0 else None)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k,fasta", [(6, 0), (12, 80)])
+def test_rccl_single_rank_bench_line_reports_the_world(k, fasta):
+    """bench.py over RCCL (world 1, backend nccl, the library's communicator):
+    the line carries what RCCL itself reports -- its rank count, every
+    rank's rank and device (fk_comm_info: ncclCommCount / ncclCommUserRank /
+    ncclCommCuDevice) -- with the exchange path, transport and per-phase
+    host milliseconds, so that the driver's 8-GPU line proves its own world"""
+    out = _torchrun(1, 29960 + k, os.path.join(REPO, "bench.py"),
+                    ["--gpus", "1", "--steps", "2", "--warmup", "1", "--no-cpu-baseline", "--dist-backend", "nccl",
+                     "--north-star-bases", "0", "--k", str(k), "--fasta-line", str(fasta), "--bases", "64000000"])
+    assert out["n_gpus"] == 1 and out["transport"] == "rccl-native"
+    assert out["rccl"] == {"nranks": 1, "ranks": [0], "devices": [0], "local_ranks": [0]}
+    assert out["exchange"] == ("fast" if k <= 7 else "stitched")
+    assert set(out["phase_ms_per_step"]) >= {"exchange", "finish"}
+    assert all(v >= 0 for v in out["phase_ms_per_step"].values())

@@ -306,71 +306,6 @@ def test_int32_zone_partitioned(k, split, extra):
     assert list(r.depth1) == list(r2.depth1)
 
 
-@pytest.mark.parametrize("k,fasta,seed", [(11, 80, 2), (6, 0, 1)])
-def test_baseline_genome_10g_vs_oracle(k, fasta, seed):
-    """BASELINE.json configs[2] at its size -- k=11 over a 10 G-base
-    synthetic genome (80-column FASTA, 1.5-Gbase chromosomes, ≈1.0125e10
-    bytes), the bench's headline -- and the north-star genome (k=6, 10 G
-    pure-ACGT bases): the engine's table and every scalar against the CPU
-    oracle over all 10 GB (fko_count_dense_par: the same scan in pieces, each
-    from its exact entering state, on the box's host threads)"""
-    import torch
-    import bench
-    n = 10_000_000_000
-    buf, size = bench.make_genome(n, fasta, seed, bench.CHROM)
-    torch.cuda.synchronize()
-    with fk.Engine(k, want_nodes=True, collect_unknown=True) as e:
-        e.feed_device(buf.data_ptr(), size)
-        rc, r_g = e.finish()
-        t_g = e.table()
-        ub_g = e.unknown_bytes()
-    host = buf[:size].cpu().numpy()
-    del buf
-    torch.cuda.empty_cache()
-    assert rc == fk.FK_OK
-    assert r_g.windows == bench.expected_windows(n, k, bench.CHROM)
-    t_o, r_o, ub_o = oracle.count_dense(host, k, unknown_cap=16, threads=oracle.host_threads())
-    del host
-    bad = np.nonzero(t_o != t_g)[0]
-    assert len(bad) == 0, f"{len(bad)} bins differ, first {bad[:8]}"
-    assert list(r_g.base_count) == list(r_o.base_count)
-    assert (r_g.valid_bases, r_g.windows, r_g.distinct, r_g.nodes) == \
-        (r_o.valid_bases, r_o.windows, r_o.distinct, r_o.nodes)
-    assert list(r_g.depth1) == list(r_o.depth1)
-    assert (r_g.unknown_chars, r_g.scanned_bytes, r_g.hit_eof_byte, r_g.unterminated_header) == \
-        (r_o.unknown_chars, r_o.scanned_bytes, r_o.hit_eof_byte, r_o.unterminated_header)
-    assert ub_g == ub_o == b""
-
-
-@pytest.mark.parametrize("k", [17, 20])
-def test_sparse_genome_10g_properties(k):
-    """17 <= k <= 20 at the configs' size: the 10 G-base 80-column genome
-    (configs[2]'s input) through the key-range passes -- several of them,
-    since the finished table alone takes ~90 GB at k = 17 (sized to the free
-    HBM after reserving 12 B per window for the parts).  Size-independent
-    checks: windows and valid bases by formula, finish's rollover check (the
-    table's u32 total equals the windows), distinct k-mers within 0.1 % of
-    the occupancy expectation 4^k (1 - exp(-windows / 4^k)) for a uniform
-    genome"""
-    import math
-    import torch
-    import bench
-    n = 10_000_000_000
-    buf, size = bench.make_genome(n, 80, 2, bench.CHROM)
-    torch.cuda.synchronize()
-    with fk.Engine(k) as e:
-        e.feed_device(buf.data_ptr(), size)
-        rc, r = e.finish()
-    del buf
-    torch.cuda.empty_cache()
-    assert rc == fk.FK_OK
-    assert r.windows == bench.expected_windows(n, k, bench.CHROM)
-    assert r.valid_bases == bench.want_valid(n, k, bench.CHROM)
-    bins = float(1 << (2 * k))
-    want = bins * -math.expm1(-r.windows / bins)
-    assert abs(r.distinct - want) < 1e-3 * want, (r.distinct, want)
-
-
 @pytest.mark.parametrize("k", [6, 11])
 def test_full_size_properties(k):
     """BASELINE config sizes (1 GB stream, 1 GB of 80-col FASTA): exact
@@ -1275,14 +1210,12 @@ def test_cli_concurrent_fanout_matches_goldens(manifest, tmp_path):
             assert hashlib.sha256(got).hexdigest() == rec["sha256"], (k, kind)
 
 
-@pytest.mark.parametrize("k", [9, 11, 12, 13])
-@pytest.mark.parametrize("tune", ["part_pipe=0", "part_stagger=0", "part_stagger=3", "idx_rm=0",
-                                  "part_pipe=0,idx_rm=0", "part_waves=16", "part_waves=8"])
-def test_partition_orders_and_layouts(k, tune, monkeypatch):
-    # k_part's batch orders (pipelined or phase by phase, every stagger) and
-    # run-index layouts (row- or slice-major) count identically: FASTA lines,
-    # a '\n' in every 16-byte half now and then, a comment line, a poly-A
-    # stretch (one slice takes a whole batch) and a ragged end
+@pytest.mark.parametrize("k,tune", [(8, ""), (9, ""), (10, ""), (11, ""), (12, ""), (13, ""), (12, "pairs_kmax=11")])
+def test_partition_batches(k, tune, monkeypatch):
+    # k_part's pipelined batches (pairs for k <= 12, single windows for
+    # k = 13 and, with pairs_kmax=11, k = 12): FASTA lines, a '\n' in every
+    # 16-byte half now and then, a comment line, a poly-A stretch (one slice
+    # takes a whole batch) and a ragged end
     monkeypatch.setenv("FINDKMER_TUNE", tune)
     rng = random.Random(91 + k)
     body = random_text(rng, 1_500_000, b"ACGT", [1, 1, 1, 1])

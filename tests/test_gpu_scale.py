@@ -1,0 +1,195 @@
+"""GPU parity at BASELINE.json's full sizes (10 GB inputs) against the CPU
+oracle, bit-exact: the whole table (or, for 17 <= k <= 20, key ranges of it)
+and every scalar the reference's outputs depend on.
+
+The oracle runs the reference's scan (findKmer/src/findKmer.cpp:962-1069)
+over the same bytes, copied back from the device, on the box's host threads
+(fko_count_dense_par / fko_count_sparse_range: the stream in pieces, each
+from its exact entering state).  Each 10 GB input is made once per module and
+shared by the tests that read it.
+"""
+import numpy as np
+import pytest
+
+import findkmer_amd as fk
+import oracle
+
+pytestmark = pytest.mark.gpu
+
+N10G = 10_000_000_000
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if fk.device_count() < 1:
+        pytest.fail("no GPU visible: the gpu tests must run on the MI355X box")
+
+
+@pytest.fixture(scope="module")
+def genome10g():
+    """configs[2]'s input: 10 G bases of 80-column FASTA, 1.5-Gbase
+    chromosomes (bench.make_genome, seed 2) on the device, and its bytes on
+    the host"""
+    import torch
+    import bench
+    buf, size = bench.make_genome(N10G, 80, 2, bench.CHROM)
+    torch.cuda.synchronize()
+    host = buf[:size].cpu().numpy()
+    yield buf, size, host
+    del buf, host
+    torch.cuda.empty_cache()
+
+
+@pytest.fixture(scope="module")
+def upstream10g():
+    """configs[4]'s input: a 10 GB upstream-regions-like FASTA (">ENST%011u"
+    records of 1001 bases, 1 % of them with a 50-base N run;
+    fk_synth_upstream_device, seed 3) on the device, and its bytes on the
+    host"""
+    import torch
+    nrec = N10G // fk.FK_UPSTREAM_REC
+    size = nrec * fk.FK_UPSTREAM_REC
+    buf = torch.empty(size + 64, dtype=torch.uint8, device="cuda")
+    assert fk.synth_upstream_device(buf.data_ptr(), size, nrec, 3) == size
+    torch.cuda.synchronize()
+    host = buf[:size].cpu().numpy()
+    yield buf, size, host
+    del buf, host
+    torch.cuda.empty_cache()
+
+
+def _engine_dense(k, ptr, size):
+    with fk.Engine(k, want_nodes=True, collect_unknown=True) as e:
+        e.feed_device(ptr, size)
+        rc, r = e.finish()
+        t = e.table()
+        ub = e.unknown_bytes()
+    return rc, r, t, ub
+
+
+def _assert_dense_equal(k, host, rc, r_g, t_g, ub_g):
+    assert rc == fk.FK_OK
+    t_o, r_o, ub_o = oracle.count_dense(host, k, unknown_cap=1 << 16, threads=oracle.host_threads())
+    bad = np.nonzero(t_o != t_g)[0]
+    assert len(bad) == 0, f"k={k}: {len(bad)} bins differ, first {bad[:8]} oracle={t_o[bad[:8]]} gpu={t_g[bad[:8]]}"
+    assert list(r_g.base_count) == list(r_o.base_count)
+    assert (r_g.valid_bases, r_g.windows, r_g.distinct, r_g.nodes) == \
+        (r_o.valid_bases, r_o.windows, r_o.distinct, r_o.nodes)
+    assert list(r_g.depth1) == list(r_o.depth1)
+    assert (r_g.unknown_chars, r_g.scanned_bytes, r_g.hit_eof_byte, r_g.unterminated_header) == \
+        (r_o.unknown_chars, r_o.scanned_bytes, r_o.hit_eof_byte, r_o.unterminated_header)
+    assert ub_g == ub_o
+    return r_o
+
+
+@pytest.mark.parametrize("k", [11, 12, 13])
+def test_genome_10g_dense_vs_oracle(genome10g, k):
+    """BASELINE.json configs[2] at its size (k = 11: the bench's headline)
+    and the k > 11 paths north_star singles out on the same genome: k = 12
+    (pairs mode, 2048 slices) and k = 13 (single windows, 2048 slices, the
+    scan shared by all waves) -- whole tables against the oracle"""
+    import bench
+    buf, size, host = genome10g
+    rc, r_g, t_g, ub_g = _engine_dense(k, buf.data_ptr(), size)
+    assert r_g.windows == bench.expected_windows(N10G, k, bench.CHROM)
+    _assert_dense_equal(k, host, rc, r_g, t_g, ub_g)
+
+
+def _slices(k, width):
+    """key ranges around 1/4, 1/3, 1/2, 2/3, 3/4 of the index space (where a
+    key-range pass boundary falls for 2, 3 or 4 passes) and at both ends"""
+    top = 1 << (2 * k)
+    cs = [top // 4, top // 3, top // 2, 2 * top // 3, 3 * top // 4]
+    out = [(0, width // 2)] + [(c - width // 2, c + width // 2) for c in cs] + [(top - width // 2, top)]
+    return out
+
+
+@pytest.mark.parametrize("k", [17, 20])
+def test_sparse_genome_10g_key_ranges_vs_oracle(genome10g, k):
+    """17 <= k <= 20 at the configs' size: the 10 G-base genome through the
+    key-range passes (several of them: the finished k = 17 table alone is
+    ~90 GB); seven key ranges of the engine's table -- both ends of the index
+    space and the points where 2, 3 or 4 passes meet -- key by key against
+    the oracle's counts of the same ranges, plus every stream counter and
+    the total distinct k-mers against the occupancy expectation"""
+    import math
+    import bench
+    buf, size, host = genome10g
+    with fk.Engine(k) as e:
+        e.feed_device(buf.data_ptr(), size)
+        rc, r = e.finish()
+        assert rc == fk.FK_OK
+        width = 1 << 23
+        ranges = _slices(k, width)
+        got = [e.sparse_range(lo, hi) for lo, hi in ranges]
+    keys_g = np.concatenate([g[0] for g in got])
+    cnts_g = np.concatenate([g[1] for g in got])
+    keys_o, cnts_o, r_o = oracle.count_sparse_range(host, k, ranges, threads=oracle.host_threads())
+    assert len(keys_g) == len(keys_o) > 0
+    assert np.array_equal(keys_g, keys_o)
+    assert np.array_equal(cnts_g, cnts_o)
+    assert r.windows == r_o.windows == bench.expected_windows(N10G, k, bench.CHROM)
+    assert (r.valid_bases, list(r.base_count), list(r.depth1), r.scanned_bytes) == \
+        (r_o.valid_bases, list(r_o.base_count), list(r_o.depth1), r_o.scanned_bytes)
+    bins = float(1 << (2 * k))
+    want = bins * -math.expm1(-r.windows / bins)
+    assert abs(r.distinct - want) < 1e-3 * want, (r.distinct, want)
+
+
+@pytest.mark.parametrize("k", [14, 16])
+def test_genome_1g_table_range_vs_oracle(k):
+    """k = 14 (4096 slices, two halves per slice) and k = 16 (the second
+    partition level, k_repart + k_count_parts, 16 GiB table) over 1 G bases
+    of the 80-column genome: table ranges against the oracle's counts of the
+    same key ranges"""
+    import torch
+    import bench
+    n = 1_000_000_000
+    buf, size = bench.make_genome(n, 80, 2, 0)
+    torch.cuda.synchronize()
+    host = buf[:size].cpu().numpy()
+    width = 1 << 22
+    ranges = _slices(k, width)
+    with fk.Engine(k) as e:
+        e.feed_device(buf.data_ptr(), size)
+        rc, r = e.finish()
+        assert rc == fk.FK_OK
+        parts = [e.table_range(lo, hi - lo) for lo, hi in ranges]
+    del buf
+    torch.cuda.empty_cache()
+    keys_g = np.concatenate([np.nonzero(p)[0].astype(np.uint64) + lo for p, (lo, hi) in zip(parts, ranges)])
+    cnts_g = np.concatenate([p[p != 0] for p in parts])
+    keys_o, cnts_o, r_o = oracle.count_sparse_range(host, k, ranges, threads=oracle.host_threads())
+    assert len(keys_o) > 0
+    assert np.array_equal(keys_g, keys_o) and np.array_equal(cnts_g, cnts_o)
+    assert (r.windows, r.valid_bases, list(r.base_count), list(r.depth1)) == \
+        (r_o.windows, r_o.valid_bases, list(r_o.base_count), list(r_o.depth1))
+
+
+def test_north_star_genome_10g_vs_oracle():
+    """The north-star gate's workload: k = 6 over 10 G pure-ACGT bases
+    (1.5-Gbase chromosomes, seed 1), whole table against the oracle"""
+    import torch
+    import bench
+    buf, size = bench.make_genome(N10G, 0, 1, bench.CHROM)
+    torch.cuda.synchronize()
+    rc, r_g, t_g, ub_g = _engine_dense(6, buf.data_ptr(), size)
+    host = buf[:size].cpu().numpy()
+    del buf
+    torch.cuda.empty_cache()
+    assert r_g.windows == bench.expected_windows(N10G, 6, bench.CHROM)
+    _assert_dense_equal(6, host, rc, r_g, t_g, ub_g)
+
+
+@pytest.mark.parametrize("k", [6, 7, 8, 9, 10, 11])
+def test_upstream_10g_sweep_vs_oracle(upstream10g, k):
+    """BASELINE.json configs[4] at its size: the k = 6..11 sweep of
+    k6thru11fullANDupstream.sh:16-24 over one device-resident 10 GB
+    upstream-like FASTA (as ./findKmer --sweep counts it: one copy, one
+    engine per k) -- a '>' line every 1019 bytes, so the header-dense paths
+    (k_count's general tiles + k_resume's mixed tiles for k <= 7, k_part's
+    second region k_part<RES> for k >= 8) at full size"""
+    buf, size, host = upstream10g
+    rc, r_g, t_g, ub_g = _engine_dense(k, buf.data_ptr(), size)
+    r_o = _assert_dense_equal(k, host, rc, r_g, t_g, ub_g)
+    assert r_o.windows > 0.98 * (N10G // fk.FK_UPSTREAM_REC) * (1001 - k + 1) * 0.99

@@ -121,6 +121,33 @@ VARIANTS = {
         ("    __syncthreads();\n    if (pg.pairs) {\n        /* pairs mode: the slice's bins",
          "    if (sink == 0x12345u) slice[0] = sink;\n    __syncthreads();\n    if (pg.pairs) {\n        /* pairs mode: the slice's bins"),
     ],
+    # k = 11 through smaller k_part blocks (2 x 8 or 4 x 4 waves per CU, 512
+    # slices each): fewer waves per barrier, shorter runs for k_bucket_count
+    "k11w8": [
+        ("static uint32_t part_waves_of(const fk_engine *e) { return e->k >= 11 ? 16u : 8u; }",
+         "static uint32_t part_waves_of(const fk_engine *e) { return e->k == 11 ? 8u : e->k >= 11 ? 16u : 8u; }"),
+        ("    if (e->part) max_waves = (uint64_t)e->cus * part_waves_of(e) * (part_waves_of(e) >= 16u ? 1u : 2u);",
+         "    if (e->part) max_waves = (uint64_t)e->cus * 16u;"),
+        ("                            : (pairs ? k_part<true, false, 8u, PART_SM(8u), false, true>",
+         "                            : (pairs ? (k == 11 ? k_part<true, false, 8u, 512u, false, true, 11u> : k_part<true, false, 8u, PART_SM(8u), false, true>)"),
+        ("                               : (pairs ? k_part<true, true, 8u> : k_part<false, true, 8u>);",
+         "                               : (pairs ? (k == 11 ? k_part<true, true, 8u, 512u> : k_part<true, true, 8u>) : k_part<false, true, 8u>);"),
+    ],
+    "k11w4": [
+        ("static uint32_t part_waves_of(const fk_engine *e) { return e->k >= 11 ? 16u : 8u; }",
+         "static uint32_t part_waves_of(const fk_engine *e) { return e->k == 11 ? 4u : e->k >= 11 ? 16u : 8u; }"),
+        ("    if (e->part) max_waves = (uint64_t)e->cus * part_waves_of(e) * (part_waves_of(e) >= 16u ? 1u : 2u);",
+         "    if (e->part) max_waves = (uint64_t)e->cus * 16u;"),
+        ("    auto kmain = c32 ? k_part<false, false, 16u, PART_SM(16u), true>",
+         "    auto kmain = W == 4u ? k_part<true, false, 4u, 512u, false, true, 11u> : c32 ? k_part<false, false, 16u, PART_SM(16u), true>"),
+        ("        auto kres = c32 ? k_part<false, true, 16u, PART_SM(16u), true>",
+         "        auto kres = W == 4u ? k_part<true, true, 4u, 512u> : c32 ? k_part<false, true, 16u, PART_SM(16u), true>"),
+    ],
+    # chunked codes: the write-out without its global stores (timing only)
+    "ch_nostore": [
+        ("                    codes[p < n1 ? (uint64_t)d1 + p : (uint64_t)d2 + (p - n1)] = x;",
+         "                    if (x.x == 0x12345678u && x.y == 0x9abcdef0u) codes[p < n1 ? (uint64_t)d1 + p : (uint64_t)d2 + (p - n1)] = x;"),
+    ],
 }
 
 

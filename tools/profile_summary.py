@@ -56,6 +56,17 @@ def counter(pass_dir, name):
     return vals
 
 
+def counter_by_kernel(pass_dir, name):
+    """{kernel name (no arguments): total counter value over its launches}"""
+    tot = {}
+    for f in glob.glob(os.path.join(src, pass_dir, "**", "*counter_collection.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            if r["Counter_Name"] == name:
+                kn = r["Kernel_Name"].split("(")[0].replace("void ", "", 1)
+                tot[kn] = tot.get(kn, 0.0) + float(r["Counter_Value"])
+    return tot
+
+
 stats = glob.glob(os.path.join(src, "trace", "**", "*kernel_stats.csv"), recursive=True)
 summary = {"tag": tag, "k": k, "fasta_line": L, "input_bytes": args.input_bytes, "main_kernel": main,
            "kernels": {}}
@@ -73,8 +84,19 @@ if fetch and write:
     hbm = f_kib * 1024 * 2 + w_kib * 1024
     summary[main_short + "_pmc"] = {"launches": len(fetch), "fetch_size_kib": f_kib, "write_size_kib": w_kib,
                                     "hbm_bytes_per_launch": hbm}
+    # the whole step: every kernel's bytes (the generator's excepted) per
+    # launch of the main kernel (one per step)
+    fk_, wk_ = counter_by_kernel("pmc1", "FETCH_SIZE"), counter_by_kernel("pmc2", "WRITE_SIZE")
+    per_kernel = {}
+    for kn in sorted(set(fk_) | set(wk_)):
+        if kn.startswith("k_synth"):
+            continue
+        per_kernel[kn] = (fk_.get(kn, 0.0) * 2 + wk_.get(kn, 0.0)) * 1024 / len(fetch)
+    step = sum(per_kernel.values())
+    summary["step_pmc"] = {"hbm_bytes_per_step": step, "per_kernel_bytes_per_step": per_kernel}
     json.dump({"kernel": main_short, "kernel_template": main, "k": k, "fasta_line": L,
                "input_bytes": args.input_bytes, "hbm_bytes_per_launch": hbm,
+               "hbm_bytes_per_step": step, "per_kernel_bytes_per_step": per_kernel,
                "fetch_size_kib": f_kib, "write_size_kib": w_kib, "launches": len(fetch),
                "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes over bench.py "
                          f"(k={k}, fasta_line={L}, {args.input_bytes} input bytes); bytes = 2*FETCH_SIZE*1024 "
