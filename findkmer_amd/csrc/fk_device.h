@@ -223,8 +223,7 @@ struct DevRes {
     uint32_t redo_n;                /* ranges re-counted */
     uint32_t need;                  /* one-pass k_count: 0 = complete, else ONE_* bits
                                        (the host runs the rest of the path) */
-    uint32_t ovf;                   /* k_part (chunked codes): a block's chunk pool ran out
-                                       (cannot happen by its sizing; the feed fails if it does) */
+    uint32_t pad;
     ShardSum shard;                 /* one-pass shard feeds */
     uint32_t pad2;
     uint32_t seq;                   /* host copy: written last (feed sequence number) */

@@ -1905,7 +1905,8 @@ __device__ __forceinline__ uint32_t run_count(uint32_t e) { return e == PART_NO_
 
 struct PartGeo {
     uint16_t *codes;       /* per row (batch): `batch` entries at row * batch */
-    uint32_t batch;        /* PART_MAX_BATCH_W of k_part's block size */
+    uint32_t batch;        /* entries per row slot: PART_MAX_BATCH_W of k_part's block size (+ 8 per slice
+                              of pad pieces for PART_PAD) */
     uint32_t *idx;         /* [row][slice]: run_word(start, count) (row-major: one contiguous row of
                               words per batch; round 3: the slice-major layout's scattered 4-B writes
                               cost ~1.6 GB of write-backs per 10 GB step) */
@@ -1923,12 +1924,6 @@ struct PartGeo {
     uint32_t stride;       /* index row stride: rows of both regions (k_part, then k_part<RES>) */
     uint32_t *flag;        /* [0] != 0: some range went to k_part<RES>, region 2 holds rows */
     uint32_t split;        /* k = 14: a slice's 2^16 codes counted as two halves of 2^15 bins (0: one) */
-    /* chunked codes (k_part instances with at most 512 slices, PART_CH): each
-       block appends every slice's runs to 4 KiB chunks of its own pool, so
-       that k_bucket_chunks reads a slice's codes as whole chunks */
-    uint32_t cap;          /* chunks per block pool: block b owns chunks [b * cap, (b + 1) * cap) */
-    uint32_t *cmeta;       /* per chunk: (slice << 9) | 16-B pieces written (<= 256) */
-    uint32_t *pool_used;   /* per block: chunks taken from its pool (main pass, then k_part<RES>) */
 };
 
 /* Every entry a fast tile's Emit hands to the partition, as f(slice, low).
@@ -1997,152 +1992,20 @@ __device__ __forceinline__ void part_entries(const Emit &em, uint32_t mk, uint32
 }
 
 /*
- * Chunked codes (PART_CH: the k_part instances of at most 512 slices, i.e.
- * 8 <= k <= 11 in pairs mode).  A batch's runs sit in LDS padded to whole
- * 16-B pieces (8 codes); the write-out appends each slice's run to that
- * slice's current 4 KiB chunk (PART_CHUNK_PIECES pieces) in the block's pool,
- * taking new chunks from the pool (consecutive ids, so a run that crosses
- * into new chunks is one linear range of pieces), and the pad codes of a
- * run's last piece are written as PART_SENTINEL.  k_bucket_chunks then reads
- * a slice's codes as whole chunks -- contiguous 4 KiB reads instead of one
- * ~256-B run per 128 KiB batch row (tools/chunk_probe.hip, 10 GB of codes:
- * 6.1 TB/s against 5.4 TB/s for aligned 256-B runs; the row-layout kernel
- * reads its unaligned runs at ~4.2 TB/s).
+ * Padded runs (PART_PAD: the k_part instances of at most 512 slices, i.e.
+ * 8 <= k <= 11 in pairs mode).  A batch's runs start on 16-B pieces in LDS
+ * and in its row (the up to 7 codes after a run's last one are whatever the
+ * LDS held: k_bucket_count<BK_PAD> masks them by the run's count), so that
+ * k_bucket_count reads a run as whole aligned pieces with one mask for its
+ * last piece instead of a bounds check per code.  The row slot grows by 16 B
+ * per slice (<= 1 pad piece per run).  Measured and dropped (round 4):
+ * appending each slice's runs to its own 4 KiB chunks (tools/chunk_probe.hip:
+ * whole-chunk reads at 6.1 TB/s): k_bucket_count 2.46 -> 1.93 ms at k = 11
+ * over 10 G bases, but k_part 4.40 -> 6.75 ms -- the runs' scattered,
+ * line-unaligned stores cost 1.6 ms and the per-slice chunk bookkeeping 0.8.
  */
-#define PART_CH_MAX_SM 512u
-#define PART_CHUNK_PIECES 256u                 /* 16-B pieces per 4 KiB chunk */
-#define PART_SENTINEL 0xFFFFu                  /* a pad code: never a stored code (pairs: singles have
-                                                  their two low bits clear; else < 2^15) */
-#define PART_CH_NONE 0x7FFFFFu                 /* a slice's chunk state before its first run */
-#define PART_CH_INIT ((PART_CH_NONE << 9) | PART_CHUNK_PIECES)
-
-/* One wave (wave 0) scans a batch's slice counts in padded pieces and
-   places every run in the slices' chunks, taking the chunks the batch needs
-   from the block's pool (consecutive ids per slice; one wave scan): for each
-   slice, cur[] (placement cursor: LDS byte address, or with bytes = false an
-   entry index), desc[3 b .. 3 b + 2] = {first piece in LDS << 17 | count,
-   global piece index of the run's first piece, global piece index of the
-   first chunk after the current one}, and the slice's chunk state cst[]
-   (current chunk << 9 | pieces in it, < 256 after a run) and closed chunks'
-   metas.  The write-out (part_writeout_ch) then only copies. */
-__device__ __forceinline__ void part_scan_ch(const PartGeo &pg, uint32_t *hist, uint32_t *cur, uint32_t *desc,
-                                             uint32_t *cst, uint32_t *pnext, uint32_t ent_base, bool bytes,
-                                             uint32_t *ovf) {
-    const uint32_t lane = threadIdx.x & 63;
-    const uint32_t per = (pg.nslices + 63) / 64;
-    const uint64_t pool0 = (uint64_t)blockIdx.x * pg.cap;
-    /* pieces and new chunks of this lane's slices */
-    uint32_t sum = 0, nch = 0;
-    for (uint32_t j = 0; j < per; j++) {
-        const uint32_t b = lane * per + j;
-        if (b < pg.nslices) {
-            const uint32_t c = hist[b];
-            if (c) {
-                const uint32_t np = (c + 7u) >> 3, fill = cst[b] & 511u;
-                /* a full (or no) current chunk: a fresh one becomes current */
-                nch += (fill == PART_CHUNK_PIECES ? 1u : 0u) + (((fill & 255u) + np - 1u) >> 8);
-            }
-            sum += (c + 7u) >> 3;
-        }
-    }
-    uint32_t run = wscan_incl32(sum) - sum;
-    const uint32_t nch_incl = wscan_incl32(nch), pool = *pnext;
-    uint32_t next = pool + nch_incl - nch;
-    const uint32_t total = rdlane(nch_incl, 63);
-    if (pool + total > pg.cap) {   /* cannot happen (launch_part sizes the pools) */
-        if (lane == 0) atomicOr(ovf, 1u);
-        for (uint32_t j = 0; j < per; j++) {
-            const uint32_t b = lane * per + j;
-            if (b < pg.nslices) { desc[3 * b] = 0; hist[b] = 0; cur[b] = ent_base; }
-        }
-        return;
-    }
-    for (uint32_t j = 0; j < per; j++) {
-        const uint32_t b = lane * per + j;
-        if (b >= pg.nslices) continue;
-        const uint32_t c = hist[b];
-        hist[b] = 0;
-        cur[b] = ent_base + (bytes ? 16u : 8u) * run;
-        desc[3 * b] = (run << 17) | c;
-        if (c) {
-            const uint32_t np = (c + 7u) >> 3, cs = cst[b];
-            uint32_t ch = cs >> 9, fill = cs & 511u;
-            if (fill == PART_CHUNK_PIECES) {   /* close the full chunk, open a fresh one */
-                if (ch != PART_CH_NONE) pg.cmeta[pool0 + ch] = (b << 9) | PART_CHUNK_PIECES;
-                ch = next++;
-                fill = 0;
-            }
-            const uint32_t extra = (fill + np - 1u) >> 8;
-            desc[3 * b + 1] = (uint32_t)((pool0 + ch) * PART_CHUNK_PIECES) + fill;
-            desc[3 * b + 2] = (uint32_t)((pool0 + next) * PART_CHUNK_PIECES);
-            if (extra) {
-                pg.cmeta[pool0 + ch] = (b << 9) | PART_CHUNK_PIECES;
-                for (uint32_t i = 0; i + 1u < extra; i++) pg.cmeta[pool0 + next + i] = (b << 9) | PART_CHUNK_PIECES;
-                ch = next + extra - 1u;
-                next += extra;
-                fill = fill + np - PART_CHUNK_PIECES * extra;
-            } else {
-                fill += np;
-            }
-            cst[b] = (ch << 9) | fill;
-        }
-        run += (c + 7u) >> 3;
-    }
-    if (lane == 63) *pnext = next;
-}
-
-/* A batch's runs to their chunks (desc[] from part_scan_ch): 8 lanes per
-   slice, up to 4 pieces each at once (threads i0 .. of nt in all); the pad
-   codes of a run's last piece written as PART_SENTINEL */
-__device__ __forceinline__ void part_writeout_ch(const PartGeo &pg, const uint32_t *desc, const uint16_t *ent,
-                                                 uint32_t i0, uint32_t nt) {
-    const uint32_t l8 = i0 & 7u, ng = nt >> 3;
-    const uint4 *src = reinterpret_cast<const uint4 *>(ent);
-    uint4 *codes = reinterpret_cast<uint4 *>(pg.codes);
-    for (uint32_t b = i0 >> 3; b < pg.nslices; b += ng) {
-        const uint32_t d0 = desc[3 * b], c = d0 & 0x1FFFFu;
-        if (c == 0) continue;                      /* (uniform in the group) */
-        const uint32_t d1 = desc[3 * b + 1], d2 = desc[3 * b + 2];
-        const uint32_t sp = d0 >> 17, np = (c + 7u) >> 3, n1 = PART_CHUNK_PIECES - (d1 & 255u), m = c & 7u;
-        for (uint32_t p0 = 0; p0 < np; p0 += 32u) {
-            uint4 v[4];
-#pragma unroll
-            for (uint32_t u = 0; u < 4; u++) {
-                const uint32_t p = p0 + l8 + 8u * u;
-                if (p < np) v[u] = src[sp + p];
-            }
-#pragma unroll
-            for (uint32_t u = 0; u < 4; u++) {
-                const uint32_t p = p0 + l8 + 8u * u;
-                if (p < np) {
-                    uint4 x = v[u];
-                    if (p == np - 1u && m) {
-                        uint32_t w[4] = {x.x, x.y, x.z, x.w};
-#pragma unroll
-                        for (uint32_t h = 0; h < 4; h++) {
-                            if (2u * h >= m) w[h] |= 0xFFFFu;
-                            if (2u * h + 1u >= m) w[h] |= 0xFFFF0000u;
-                        }
-                        x = make_uint4(w[0], w[1], w[2], w[3]);
-                    }
-                    codes[p < n1 ? (uint64_t)d1 + p : (uint64_t)d2 + (p - n1)] = x;
-                }
-            }
-        }
-    }
-}
-
-/* end of a k_part pass (after a barrier): every slice's open chunk and the
-   pool's fill level */
-__device__ __forceinline__ void part_close_chunks(const PartGeo &pg, const uint32_t *cst, const uint32_t *pnext,
-                                                  uint32_t nthreads) {
-    const uint64_t pool0 = (uint64_t)blockIdx.x * pg.cap;
-    for (uint32_t b = threadIdx.x; b < pg.nslices; b += nthreads) {
-        const uint32_t cs = cst[b];
-        if ((cs >> 9) != PART_CH_NONE) pg.cmeta[pool0 + (cs >> 9)] = (b << 9) | (cs & 511u);
-    }
-    if (threadIdx.x == 0) pg.pool_used[blockIdx.x] = *pnext;
-}
+#define PART_PAD_MAX_SM 512u
+#define PART_ROW_PAD(SM) (16u * (SM))   /* bytes of pad pieces a row slot adds */
 
 /* The block-wide batch of one round: windows of the waves whose tile was
  * fast (have), counting-sorted by slice.  Every thread of the block calls
@@ -2160,10 +2023,9 @@ __device__ __forceinline__ void part_close_chunks(const PartGeo &pg, const uint3
 template <bool PAIRS, bool MIX, uint32_t W, uint32_t SM, typename CT>
 __device__ __forceinline__ bool part_batch(const Ctx &cx, const PartGeo &pg, const Emit *es, const bool *haves,
                                            bool more, uint32_t row, uint32_t *hist,
-                                           uint32_t *cur, uint32_t *total, CT *ent, uint32_t *scr,
-                                           uint32_t *desc, uint32_t *cst, uint32_t *pnext) {
+                                           uint32_t *cur, uint32_t *total, CT *ent, uint32_t *scr) {
     constexpr bool C32 = sizeof(CT) == 4;
-    constexpr bool CH = !C32 && SM <= PART_CH_MAX_SM;   /* chunked codes (see part_writeout_ch) */
+    constexpr bool PAD = !C32 && SM <= PART_PAD_MAX_SM;   /* runs padded to 16-B pieces (PART_PAD) */
     constexpr int NT = PART_TILES3(PAIRS, C32);
     const uint32_t t = threadIdx.x, lane = t & 63;
     const uint32_t mk = (uint32_t)cx.maskk, sh = pg.sh, lowm = (1u << sh) - 1u;
@@ -2203,10 +2065,27 @@ __device__ __forceinline__ bool part_batch(const Ctx &cx, const PartGeo &pg, con
             run += c;
         }
         if (wv == W - 1u && lane == 63) *total = run;
-    } else if (CH && t < 64) {
-        /* runs padded to whole 16-B pieces and placed in the slices' chunks;
-           cursors in entries */
-        part_scan_ch(pg, hist, cur, desc, cst, pnext, 0u, false, &cx.res->ovf);
+    } else if (PAD && t < 64) {
+        /* runs start on 16-B pieces; cursors and run index in entries / pieces */
+        const uint32_t per = (pg.nslices + 63) / 64;
+        uint32_t sum = 0;
+        for (uint32_t j = 0; j < per; j++) {
+            const uint32_t b = lane * per + j;
+            if (b < pg.nslices) sum += (hist[b] + 7u) >> 3;
+        }
+        const uint32_t inc = wscan_incl32(sum);
+        uint32_t run = inc - sum;
+        for (uint32_t j = 0; j < per; j++) {
+            const uint32_t b = lane * per + j;
+            if (b < pg.nslices) {
+                const uint32_t c = hist[b];
+                cur[b] = 8u * run;
+                pg.idx[(size_t)row * pg.nslices + b] = run_word(run, c);
+                hist[b] = 0;
+                run += (c + 7u) >> 3;
+            }
+        }
+        if (lane == 63) *total = 8u * inc;
     } else if (t < 64) {
         const uint32_t per = (pg.nslices + 63) / 64;
         uint32_t sum = 0;
@@ -2249,16 +2128,11 @@ __device__ __forceinline__ bool part_batch(const Ctx &cx, const PartGeo &pg, con
         if (haves[i]) part_entries<PAIRS, MIX>(f, mk, m1, sh, lowm, pg.npair, place);
     }
     __syncthreads();
-    /* 4: CH: the runs appended to the slices' chunks; else the sorted batch
-       into its row's fixed slot (a batch holds at most PART_MAX_BATCH_W(W)
-       entries: a run's position needs no per-row base), as 16-B pieces; the
-       up to 7 codes past the batch's end are padding no run covers */
-    if (CH) {
-        part_writeout_ch(pg, desc, reinterpret_cast<const uint16_t *>(ent), t, PART_BLOCK_W(W));
-        return any_more;
-    }
+    /* 4: the sorted batch into its row's fixed slot (pg.batch entries: a
+       run's position needs no per-row base), as 16-B pieces; the up to 7
+       codes past the batch's end are padding no run covers */
     const uint32_t n8 = (*total * (uint32_t)sizeof(CT) + 15u) >> 4;
-    uint4 *dst = reinterpret_cast<uint4 *>(reinterpret_cast<uint8_t *>(pg.codes) + (size_t)row * PART_ROW_BYTES(W));
+    uint4 *dst = reinterpret_cast<uint4 *>(reinterpret_cast<uint8_t *>(pg.codes) + (size_t)row * pg.batch * sizeof(CT));
     const uint4 *src = reinterpret_cast<const uint4 *>(ent);
     for (uint32_t i = t; i < n8; i += PART_BLOCK_W(W)) dst[i] = src[i];
     return any_more;
@@ -2363,6 +2237,9 @@ __device__ __forceinline__ void part_place8(const Emit &em, uint32_t sh, uint32_
     }
 }
 
+/* PAD: runs start on 16-B pieces (PART_PAD), the run index and the total in
+   pieces / entries (8 per piece) */
+template <bool PAD>
 __device__ __forceinline__ void part_scan_w0(const PartGeo &pg, uint32_t row, uint32_t *hist, uint32_t *cur,
                                              uint32_t *tot, uint32_t ent_lds) {
     const uint32_t lane = threadIdx.x & 63;
@@ -2370,7 +2247,7 @@ __device__ __forceinline__ void part_scan_w0(const PartGeo &pg, uint32_t row, ui
     uint32_t sum = 0;
     for (uint32_t j = 0; j < per; j++) {
         const uint32_t b = lane * per + j;
-        if (b < pg.nslices) sum += hist[b];
+        if (b < pg.nslices) sum += PAD ? (hist[b] + 7u) >> 3 : hist[b];
     }
     const uint32_t inc = wscan_incl32(sum);
     uint32_t run = inc - sum;
@@ -2378,13 +2255,13 @@ __device__ __forceinline__ void part_scan_w0(const PartGeo &pg, uint32_t row, ui
         const uint32_t b = lane * per + j;
         if (b < pg.nslices) {
             const uint32_t c = hist[b];
-            cur[b] = ent_lds + 2u * run;   /* LDS byte addresses (part_place8) */
+            cur[b] = ent_lds + (PAD ? 16u : 2u) * run;   /* LDS byte addresses (part_place8) */
             pg.idx[(size_t)row * pg.nslices + b] = run_word(run, c);
             hist[b] = 0;
-            run += c;
+            run += PAD ? (c + 7u) >> 3 : c;
         }
     }
-    if (lane == 63) *tot = inc;
+    if (lane == 63) *tot = PAD ? 8u * inc : inc;
 }
 
 /* The same for 2048 slices (k = 13), over all W waves: each wave sums its
@@ -2420,7 +2297,7 @@ template <uint32_t W>
 __device__ __forceinline__ void part_writeout(const PartGeo &pg, uint32_t row, uint32_t total, const uint16_t *ent,
                                               uint32_t t0, uint32_t nt) {
     const uint32_t n8 = (total * (uint32_t)sizeof(uint16_t) + 15u) >> 4;
-    uint4 *dst = reinterpret_cast<uint4 *>(reinterpret_cast<uint8_t *>(pg.codes) + (size_t)row * PART_ROW_BYTES(W));
+    uint4 *dst = reinterpret_cast<uint4 *>(reinterpret_cast<uint8_t *>(pg.codes) + (size_t)row * pg.batch * 2u);
     const uint4 *src = reinterpret_cast<const uint4 *>(ent);
     for (uint32_t i = t0; i < n8; i += nt) dst[i] = src[i];
 }
@@ -2442,19 +2319,14 @@ k_part(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint
        their base folds into the LDS instructions' offset field), then the
        batch */
     using CT = typename std::conditional<C32, uint32_t, uint16_t>::type;
-    /* chunked codes (PART_CH) for the tables of at most 512 slices */
-    constexpr bool CH = !C32 && SM <= PART_CH_MAX_SM;
+    /* runs padded to 16-B pieces (PART_PAD) for the tables of at most 512 slices */
+    constexpr bool PAD = !C32 && SM <= PART_PAD_MAX_SM;
     constexpr uint32_t CURW = SM > 2048u ? SM / 2u : SM;
-    /* CH: the write-out words of two batches (the one being written out
-       while the next one's are scanned), every slice's chunk state, the pool
-       counter; the batch padded to whole pieces per run (<= 16 B per slice) */
-    constexpr uint32_t DESCW = CH ? 6u * SM : 0u, CSTW = CH ? SM + 1u : 0u;
-    constexpr uint32_t ENT_OFF = (SM + CURW + 4u + W + DESCW + CSTW + 15u) & ~15u;   /* words, 64-B aligned */
-    constexpr uint32_t ENT_BYTES = PART_ROW_BYTES(W) + (CH ? 16u * SM : 0u);
+    constexpr uint32_t ENT_OFF = (SM + CURW + 4u + W + 15u) & ~15u;   /* words, 64-B aligned */
+    constexpr uint32_t ENT_BYTES = PART_ROW_BYTES(W) + (PAD ? PART_ROW_PAD(SM) : 0u);
     __shared__ __attribute__((aligned(64))) uint32_t lds_part[ENT_OFF + ENT_BYTES / 4u];
     uint32_t *const hist = lds_part, *const cur = lds_part + SM, &total = lds_part[SM + CURW],
                     *const tot = lds_part + SM + CURW + 1u, *const scr = lds_part + SM + CURW + 4u;
-    uint32_t *const desc = scr + W, *const cst = desc + DESCW, *const pnext = cst + SM;
     CT *const ent = reinterpret_cast<CT *>(lds_part + ENT_OFF);
     if (RES && *(volatile uint32_t *)pg.flag == 0) return;   /* uniform: no range stopped */
     /* open the feed's result block (the kernels after this one accumulate
@@ -2463,14 +2335,8 @@ k_part(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint
         if (threadIdx.x < 10) res->tstat[threadIdx.x] = 0;
         if (threadIdx.x == 10) res->eof_cand = ~0ull;
         if (threadIdx.x == 11) res->redo_n = 0;
-        if (threadIdx.x == 12) res->ovf = 0;
     }
     for (uint32_t i = threadIdx.x; i < pg.nslices; i += PART_BLOCK_W(W)) hist[i] = 0;
-    if (CH) {
-        for (uint32_t i = threadIdx.x; i < pg.nslices; i += PART_BLOCK_W(W)) cst[i] = PART_CH_INIT;
-        /* k_part<RES> takes chunks after the main pass's */
-        if (threadIdx.x == 0) *pnext = RES ? pg.pool_used[blockIdx.x] : 0u;
-    }
     Ctx cx{buf, len, lo, table, nullptr, shortcnt, acc, res, maskk, 0, k, nullptr};
     const int lane = threadIdx.x & 63;
     const uint64_t wave = blockIdx.x * W + wave_in_block();
@@ -2623,14 +2489,10 @@ k_part(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint
                     __syncthreads();                                                 \
                     part_scan_place(pg, row0 + j_, hist, cur, W, scr, mine_, &tot[j_ & 1u], ent_lds); \
                 } else if (threadIdx.x < 64) {                                       \
-                    if (CH) part_scan_ch(pg, hist, cur, desc + (j_ & 1u) * 3u * SM, cst, pnext, ent_lds, true, \
-                                         &res->ovf);                                  \
-                    else part_scan_w0(pg, row0 + j_, hist, cur, &tot[j_ & 1u], ent_lds); \
+                    part_scan_w0<PAD>(pg, row0 + j_, hist, cur, &tot[j_ & 1u], ent_lds); \
                 } else if (j_ > 0) {                                                 \
-                    if (CH) part_writeout_ch(pg, desc + ((j_ - 1) & 1u) * 3u * SM, (const uint16_t *)ent, \
-                                             threadIdx.x - 64u, PART_BLOCK_W(W) - 64u); \
-                    else part_writeout<W>(pg, row0 + j_ - 1, tot[(j_ - 1) & 1u], (const uint16_t *)ent, \
-                                          threadIdx.x - 64u, PART_BLOCK_W(W) - 64u);  \
+                    part_writeout<W>(pg, row0 + j_ - 1, tot[(j_ - 1) & 1u], (const uint16_t *)ent, \
+                                     threadIdx.x - 64u, PART_BLOCK_W(W) - 64u);       \
                 }                                                                    \
                 __syncthreads();                                                     \
                 if (!more_ || j_ + 1 >= pg.rounds) {                                 \
@@ -2638,9 +2500,7 @@ k_part(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint
                     _Pragma("unroll") for (uint32_t i_ = 0; i_ < NT; i_++)           \
                         if (have_stash[i_]) part_place8<PAIRS>(stash[i_], shv, wsl, lowm, cur); \
                     __syncthreads();                                                 \
-                    if (CH) part_writeout_ch(pg, desc + (j_ & 1u) * 3u * SM, (const uint16_t *)ent, \
-                                             threadIdx.x, PART_BLOCK_W(W));           \
-                    else part_writeout<W>(pg, row0 + j_, tot[j_ & 1u], (const uint16_t *)ent, threadIdx.x, PART_BLOCK_W(W)); \
+                    part_writeout<W>(pg, row0 + j_, tot[j_ & 1u], (const uint16_t *)ent, threadIdx.x, PART_BLOCK_W(W)); \
                     round++;                                                         \
                     break;                                                           \
                 }                                                                    \
@@ -2653,8 +2513,7 @@ k_part(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint
             }                                                                        \
             if (ph_ == NT - 1) {                                                     \
                 const bool more_ = part_batch<PAIRS, RES, W, SM, CT>(cx, pg, stash, have_stash, !done, \
-                                                          row0 + round / NT, hist, cur, &total, ent, scr, \
-                                                          desc, cst, pnext); \
+                                                          row0 + round / NT, hist, cur, &total, ent, scr); \
                 if (!more_ || round / NT + 1 >= pg.rounds) { round++; break; }       \
             }                                                                        \
         }                                                                            \
@@ -2668,16 +2527,10 @@ k_part(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint
 #undef FK_ROUND
 #undef FK_PLACE_OLD
 #undef FK_LOADP
-    if (CH) {
-        /* every slice's open chunk, the pool's fill level */
-        __syncthreads();
-        part_close_chunks(pg, cst, pnext, PART_BLOCK_W(W));
-    } else {
-        /* rows the block did not reach are empty */
-        for (uint32_t r = (round + NT - 1) / NT; r < pg.rounds; r++) {
-            const uint32_t row = row0 + r;
-            for (uint32_t b = threadIdx.x; b < pg.nslices; b += PART_BLOCK_W(W)) pg.idx[(size_t)row * pg.nslices + b] = PART_NO_RUN;
-        }
+    /* rows the block did not reach are empty */
+    for (uint32_t r = (round + NT - 1) / NT; r < pg.rounds; r++) {
+        const uint32_t row = row0 + r;
+        for (uint32_t b = threadIdx.x; b < pg.nslices; b += PART_BLOCK_W(W)) pg.idx[(size_t)row * pg.nslices + b] = PART_NO_RUN;
     }
     if (!has) {
         flush_counters(cx, cnt, 1u);
@@ -2746,12 +2599,15 @@ k_part(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint
             slice's codes from L2.  (Counting k = 15's 32-bit coarse slices
             the same way, 16 parts each, took 21.7 ms per G-base; the second
             partition level, k_repart, takes 16.3.) */
-enum { BK_PLAIN = 0, BK_SPLIT = 1 };
+/* BK_PAD: BK_PLAIN over padded runs (PART_PAD: a run starts on a 16-B
+            piece, its index word holds that piece; only its last piece
+            needs a mask) */
+enum { BK_PLAIN = 0, BK_SPLIT = 1, BK_PAD = 2 };
 template <int MODE>
 __global__ void __launch_bounds__(1024)
 k_bucket_count(PartGeo pg, uint32_t groups, uint32_t *table) {
     extern __shared__ uint32_t slice[];
-    constexpr bool PARTS = MODE != BK_PLAIN;
+    constexpr bool PARTS = MODE == BK_SPLIT, PADDED = MODE == BK_PAD;
     constexpr uint32_t CPP = 8u;   /* 16-bit codes per 16-B piece */
     constexpr uint32_t PSH = 3u;
     const uint32_t binsh = PARTS ? 15u : pg.sh;
@@ -2790,11 +2646,15 @@ k_bucket_count(PartGeo pg, uint32_t groups, uint32_t *table) {
     const uint32_t quads = blockDim.x / QL, step = groups * quads;
     auto add16 = [&](const uint4 &v, uint64_t q, uint64_t s0, uint64_t s1) {
         const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+        const uint32_t nv = PADDED ? (uint32_t)min<uint64_t>(CPP, s1 - q * CPP) : 0u;   /* codes of the run in q */
 #pragma unroll
         for (int h = 0; h < (int)CPP; h++) {
             const uint64_t at = q * CPP + h;
             const uint32_t c = (w4[h >> 1] >> (16 * (h & 1))) & 0xFFFFu;
-            if (PARTS) {   /* this block's part of the slice */
+            if (PADDED) {   /* the run starts on this lane's first piece: only its end bounds it */
+                const uint32_t a = c & PART_SINGLE ? nb + ((c & ~PART_SINGLE) >> 2) : c;
+                if ((uint32_t)h < nv) atomicAdd(&slice[a], 1u);
+            } else if (PARTS) {   /* this block's part of the slice */
                 if (at >= s0 && at < s1 && (c >> binsh) == part) atomicAdd(&slice[c & (nb - 1u)], 1u);
             } else {
                 const uint32_t a = c & PART_SINGLE ? nb + ((c & ~PART_SINGLE) >> 2) : c;
@@ -2817,7 +2677,7 @@ k_bucket_count(PartGeo pg, uint32_t groups, uint32_t *table) {
         uint4 v[BUCKET_ROWS][BUCKET_U];
 #pragma unroll
         for (int j = 0; j < BUCKET_ROWS; j++) {
-            s0[j] = (uint64_t)(r + j * step) * pg.batch + (e[j] == PART_NO_RUN ? 0u : e[j] >> 16);
+            s0[j] = (uint64_t)(r + j * step) * pg.batch + (e[j] == PART_NO_RUN ? 0u : (e[j] >> 16) * (PADDED ? CPP : 1u));
             s1[j] = s0[j] + run_count(e[j]);
             const uint64_t q0 = (s0[j] >> PSH) + sub, q1 = (s1[j] + CPP - 1) >> PSH;
 #pragma unroll
@@ -2858,128 +2718,6 @@ k_bucket_count(PartGeo pg, uint32_t groups, uint32_t *table) {
         if (!v) continue;
         uint32_t *dst = &table[fk_sigma(((uint64_t)b << pg.sh) | ((uint64_t)part << binsh) | i)];
         if (groups == 1) *dst += v;   /* this block owns the slice */
-        else atomicAdd(dst, v);
-    }
-}
-
-/*
- * Chunk index (PART_CH): every chunk k_part filled, grouped by slice --
- * k_cidx_count (per pool: chunks per slice), k_cidx_scan (one block: each
- * (pool, slice)'s first position in the list and each slice's offset),
- * k_cidx_place (per pool: (chunk, pieces) into the list).  ~3 M chunks per
- * 10 GB of k = 11 input.
- */
-__global__ void __launch_bounds__(256) k_cidx_count(PartGeo pg, uint32_t *chist) {
-    __shared__ uint32_t h[PART_CH_MAX_SM];
-    for (uint32_t i = threadIdx.x; i < pg.nslices; i += blockDim.x) h[i] = 0;
-    __syncthreads();
-    const uint32_t n = pg.pool_used[blockIdx.x];
-    const uint32_t *m = pg.cmeta + (uint64_t)blockIdx.x * pg.cap;
-    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) atomicAdd(&h[m[i] >> 9], 1u);
-    __syncthreads();
-    for (uint32_t i = threadIdx.x; i < pg.nslices; i += blockDim.x) chist[(size_t)blockIdx.x * pg.nslices + i] = h[i];
-}
-
-__global__ void __launch_bounds__(1024) k_cidx_scan(PartGeo pg, uint32_t npools, uint32_t *chist, uint32_t *coff) {
-    __shared__ uint32_t wsum[16];
-    const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6;
-    /* one thread per slice (nslices <= 1024): its total over the pools */
-    uint32_t tot = 0;
-    if (t < pg.nslices)
-        for (uint32_t b = 0; b < npools; b++) tot += chist[(size_t)b * pg.nslices + t];
-    const uint32_t inc = wscan_incl32(tot);
-    if (lane == 63) wsum[wv] = inc;
-    __syncthreads();
-    uint32_t off = 0;
-    for (uint32_t w = 0; w < wv; w++) off += wsum[w];
-    uint32_t run = off + inc - tot;
-    if (t < pg.nslices) {
-        coff[t] = run;
-        for (uint32_t b = 0; b < npools; b++) {
-            const uint32_t c = chist[(size_t)b * pg.nslices + t];
-            chist[(size_t)b * pg.nslices + t] = run;
-            run += c;
-        }
-        if (t == pg.nslices - 1u) coff[pg.nslices] = run;
-    }
-}
-
-__global__ void __launch_bounds__(256) k_cidx_place(PartGeo pg, const uint32_t *chist, uint2 *list) {
-    __shared__ uint32_t pos[PART_CH_MAX_SM];
-    for (uint32_t i = threadIdx.x; i < pg.nslices; i += blockDim.x) pos[i] = chist[(size_t)blockIdx.x * pg.nslices + i];
-    __syncthreads();
-    const uint32_t n = pg.pool_used[blockIdx.x];
-    const uint64_t pool0 = (uint64_t)blockIdx.x * pg.cap;
-    const uint32_t *m = pg.cmeta + pool0;
-    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
-        const uint32_t v = m[i];
-        list[atomicAdd(&pos[v >> 9], 1u)] = make_uint2((uint32_t)(pool0 + i), v & 511u);
-    }
-}
-
-/* k_bucket_count over chunked codes: one block per slice (and group of
- * chunks when groups > 1), consecutive slices on one XCD; each wave takes
- * whole chunks (four 1-KiB wave loads each, two chunks in flight), skipping
- * the pad codes.  Pairs mode as k_bucket_count. */
-__global__ void __launch_bounds__(1024)
-k_bucket_chunks(PartGeo pg, uint32_t groups, uint32_t *table, const uint2 *list, const uint32_t *coff) {
-    extern __shared__ uint32_t slice[];
-    const uint32_t binsh = pg.sh, nb = 1u << binsh;
-    const uint32_t ns = pg.pairs ? nb >> 2 : 0u;
-    const uint32_t b = groups == 1 && (pg.nslices & 7u) == 0 ? (blockIdx.x & 7u) * (pg.nslices >> 3) + (blockIdx.x >> 3)
-                                                            : blockIdx.x % pg.nslices;
-    const uint32_t g = blockIdx.x / pg.nslices;
-    for (uint32_t i = threadIdx.x; i < nb + ns; i += blockDim.x) slice[i] = 0;
-    __syncthreads();
-    const uint32_t lane = threadIdx.x & 63u, nw = blockDim.x >> 6;
-    const uint32_t step = groups * nw;
-    const uint32_t c0 = coff[b], c1 = coff[b + 1];
-    const uint4 *g4 = reinterpret_cast<const uint4 *>(pg.codes);
-    auto add8 = [&](const uint4 &v) {
-        const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-        for (int h = 0; h < 8; h++) {
-            const uint32_t c = (w4[h >> 1] >> (16 * (h & 1))) & 0xFFFFu;
-            if (c != PART_SENTINEL) atomicAdd(&slice[c & PART_SINGLE ? nb + ((c & ~PART_SINGLE) >> 2) : c], 1u);
-        }
-    };
-    constexpr uint4 SENT4 = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
-    uint32_t i = c0 + g * nw + (threadIdx.x >> 6);
-    uint2 e0 = i < c1 ? list[i] : make_uint2(0, 0), e1 = i + step < c1 ? list[i + step] : make_uint2(0, 0);
-    for (; i < c1; i += 2 * step) {
-        const uint2 a = e0, c = e1;
-        /* the next iteration's list entries fly with this one's chunks */
-        e0 = i + 2 * step < c1 ? list[i + 2 * step] : make_uint2(0, 0);
-        e1 = i + 3 * step < c1 ? list[i + 3 * step] : make_uint2(0, 0);
-        uint4 v[2][4];
-#pragma unroll
-        for (int u = 0; u < 4; u++) {
-            const uint32_t p = lane + 64u * u;
-            v[0][u] = p < a.y ? g4[(uint64_t)a.x * PART_CHUNK_PIECES + p] : SENT4;
-            v[1][u] = p < c.y ? g4[(uint64_t)c.x * PART_CHUNK_PIECES + p] : SENT4;
-        }
-#pragma unroll
-        for (int u = 0; u < 4; u++) {
-            add8(v[0][u]);
-            add8(v[1][u]);
-        }
-    }
-    __syncthreads();
-    if (pg.pairs) {
-        uint32_t *dp = pg.pairs + ((size_t)b << pg.sh), *ds = pg.singles + ((size_t)b << (pg.sh - 2));
-        for (uint32_t j = threadIdx.x; j < nb + ns; j += blockDim.x) {
-            const uint32_t v = slice[j];
-            uint32_t *dst = j < nb ? dp + j : ds + (j - nb);
-            if (groups == 1) *dst = v;   /* this block owns the slice: every bin written */
-            else if (v) atomicAdd(dst, v);
-        }
-        return;
-    }
-    for (uint32_t j = threadIdx.x; j < nb; j += blockDim.x) {
-        const uint32_t v = slice[j];
-        if (!v) continue;
-        uint32_t *dst = &table[fk_sigma(((uint64_t)b << pg.sh) | j)];
-        if (groups == 1) *dst += v;
         else atomicAdd(dst, v);
     }
 }
@@ -3873,8 +3611,6 @@ struct fk_engine {
     uint32_t *d_pflag = nullptr;              /* k_part: a range went to k_part<RES> */
     uint32_t *d_pidx = nullptr;               /* k_part: slice-major run index */
     uint64_t codes_cap = 0, pidx_cap = 0;
-    uint32_t *d_cidx = nullptr;               /* k_part chunked codes: chunk metas, pool levels, chunk index */
-    uint64_t cidx_cap = 0;
     uint32_t *d_pairs = nullptr;              /* k_part pairs mode: 4^(k+1) pair bins + 4^k single bins */
     uint16_t *d_parts = nullptr;              /* k = 15, 16: the second level's part streams (k_repart) */
     uint64_t parts_cap = 0;
@@ -4094,7 +3830,7 @@ extern "C" void fk_engine_destroy(fk_engine *e) {
     hipFree(e->d_table); hipFree(e->d_short); hipFree(e->d_sub); hipFree(e->d_snap);
     hipFree(e->d_pairs);
     hipFree(e->d_parts); hipFree(e->d_pmeta);
-    hipFree(e->d_codes); hipFree(e->d_pidx); hipFree(e->d_cidx); hipFree(e->d_pflag); hipFree(e->d_acc); hipFree(e->d_res); hipFree(e->d_tmp);
+    hipFree(e->d_codes); hipFree(e->d_pidx); hipFree(e->d_pflag); hipFree(e->d_acc); hipFree(e->d_res); hipFree(e->d_tmp);
     hipFree(e->d_state); hipFree(e->d_rr); hipFree(e->d_rtrue);
     hipFree(e->d_redo); hipFree(e->d_tf); hipFree(e->d_stage); hipFree(e->d_resume);
     hipFree(e->d_aggs); hipFree(e->d_flags);
@@ -4244,7 +3980,7 @@ extern "C" int fk_engine_create(int k, const fk_opts *opts, fk_engine **out) {
     }
     if (e->part)   /* k_bucket_count: one 2^15-bin slice + its 2^13 single bins (160 KiB) in LDS */
         for (const void *f : {(const void *)k_bucket_count<BK_PLAIN>, (const void *)k_bucket_count<BK_SPLIT>,
-                              (const void *)k_count_parts, (const void *)k_bucket_chunks})
+                              (const void *)k_count_parts, (const void *)k_bucket_count<BK_PAD>})
             hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 5 << 15);
     for (int i = 0; i < 3; i++)
         /* timing only (results travel through mapped memory): no system-scope
@@ -4503,9 +4239,6 @@ static int wait_results(fk_engine *e) {
         __builtin_ia32_pause();
     }
     memcpy(&e->last, e->h_res, sizeof(DevRes));
-    /* a k_part chunk pool ran out (its sizing makes this impossible): the
-       counts would be incomplete, so the feed fails */
-    if (e->part && e->last.ovf) return FK_E_OOM;
     return FK_OK;
 }
 
@@ -4558,39 +4291,13 @@ static int launch_part(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t l
     if (!e->d_pflag && hipMalloc((void **)&e->d_pflag, 64) != hipSuccess) return FK_E_OOM;
     pg.flag = e->d_pflag;
     HIPCHK(hipMemsetAsync(e->d_pflag, 0, sizeof(uint32_t), e->stream));
-    /* chunked codes (PART_CH: the instances of at most 512 slices, i.e. the
-       8-wave blocks of k <= 10 and k = 11's pairs) or batch rows */
-    const bool ch = !c32 && !pg.split && (W == 8u || (k == 11 && pairs));
-    pg.cap = 0;
-    pg.cmeta = pg.pool_used = nullptr;
-    uint64_t ncodes = (uint64_t)pg.stride * PART_ROW_BYTES(W) / sizeof(uint16_t),
-             nidx = ch ? 0 : (uint64_t)pg.nslices * pg.stride;
-    if (ch) {
-        /* a block's pool: its range's entries (<= 1 per 2 bytes in pairs
-           mode, else 1 per byte) as 16-B pieces, plus <= 1 pad piece per
-           slice and batch in each of the two passes (main, k_part<RES>), as
-           4 KiB chunks, plus each slice's last open chunk of each pass */
-        const uint64_t bytes = g.cpw * W * FK_CHUNK_BYTES;
-        const uint64_t pieces = (pairs ? bytes / 2 : bytes) / 8 + 2ull * pg.rounds * pg.nslices;
-        const uint64_t cap = (pieces + PART_CHUNK_PIECES - 1) / PART_CHUNK_PIECES + 2ull * pg.nslices + 2;
-        /* chunk ids below PART_CH_NONE, global piece indices in 32 bits (a
-           16 GiB segment at k = 11: ~1.3e9 pieces) */
-        if (cap >= PART_CH_NONE || cap * pgrid * PART_CHUNK_PIECES >= (1ull << 32)) return FK_E_INVALID;
-        pg.cap = (uint32_t)cap;
-        ncodes = cap * pgrid * PART_CHUNK_PIECES * 8;
-        const uint64_t nch = cap * pgrid;
-        /* chunk metas + pool levels + (pool, slice) counts + slice offsets, then the list */
-        const uint64_t words = nch + pgrid + (uint64_t)pgrid * pg.nslices + pg.nslices + 1 + 2 * nch;
-        if (words > e->cidx_cap) {
-            hipFree(e->d_cidx);
-            e->d_cidx = nullptr;
-            e->cidx_cap = 0;
-            if (hipMalloc((void **)&e->d_cidx, words * sizeof(uint32_t)) != hipSuccess) return FK_E_OOM;
-            e->cidx_cap = words;
-        }
-        pg.cmeta = e->d_cidx;
-        pg.pool_used = pg.cmeta + nch;
-    }
+    /* runs padded to 16-B pieces (PART_PAD: the instances of at most 512
+       slices, i.e. the 8-wave blocks of k <= 10 and k = 11's pairs): the row
+       slot grows by one pad piece per slice */
+    const bool padded = !c32 && !pg.split && (W == 8u || (k == 11 && pairs));
+    if (padded) pg.batch += PART_ROW_PAD(W == 8u ? PART_SM(8u) : PART_PAD_MAX_SM) / 2u;
+    const uint64_t ncodes = (uint64_t)pg.stride * pg.batch * (c32 ? 2u : 1u),
+                   nidx = (uint64_t)pg.nslices * pg.stride;
     if (ncodes > e->codes_cap) {
         hipFree(e->d_codes);
         e->d_codes = nullptr;
@@ -4611,7 +4318,7 @@ static int launch_part(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t l
        (C32); the headline k = 11 with k a compile-time constant */
     auto kmain = c32 ? k_part<false, false, 16u, PART_SM(16u), true>
                  : pg.split ? k_part<false, false, 16u, PART_BIG>
-                 : W == 16u ? (pairs ? (k == 11 ? k_part<true, false, 16u, PART_CH_MAX_SM, false, true, 11u>
+                 : W == 16u ? (pairs ? (k == 11 ? k_part<true, false, 16u, PART_PAD_MAX_SM, false, true, 11u>
                                                 : k_part<true, false, 16u, PART_SM(16u), false, true>)
                                      : k_part<false, false, 16u, PART_SM(16u), false, true>)
                             : (pairs ? k_part<true, false, 8u, PART_SM(8u), false, true>
@@ -4623,7 +4330,7 @@ static int launch_part(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t l
     if (mixed) {
         auto kres = c32 ? k_part<false, true, 16u, PART_SM(16u), true>
                     : pg.split ? k_part<false, true, 16u, PART_BIG>
-                    : W == 16u ? (pairs ? (k == 11 ? k_part<true, true, 16u, PART_CH_MAX_SM> : k_part<true, true, 16u>)
+                    : W == 16u ? (pairs ? (k == 11 ? k_part<true, true, 16u, PART_PAD_MAX_SM> : k_part<true, true, 16u>)
                                         : k_part<false, true, 16u>)
                                : (pairs ? k_part<true, true, 8u> : k_part<false, true, 8u>);
         hipLaunchKernelGGL(kres, dim3(pgrid), dim3(PART_BLOCK_W(W)), 0, e->stream, buf, len, lo, e->k, e->maskk,
@@ -4658,18 +4365,9 @@ static int launch_part(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t l
         HIPCHK(hipGetLastError());
         hipLaunchKernelGGL(k_count_parts, dim3((unsigned)nparts), dim3(1024), (size_t)1 << 17, e->stream, pg,
                            (const uint16_t *)e->d_parts, (const PartMeta *)meta, e->d_table);
-    } else if (ch) {
-        /* the chunk index (chunks grouped by slice), then the slices */
-        uint32_t *chist = pg.pool_used + pgrid, *coff = chist + (size_t)pgrid * pg.nslices;
-        uint2 *list = reinterpret_cast<uint2 *>(coff + pg.nslices + 1);
-        hipLaunchKernelGGL(k_cidx_count, dim3(pgrid), dim3(256), 0, e->stream, pg, chist);
-        HIPCHK(hipGetLastError());
-        hipLaunchKernelGGL(k_cidx_scan, dim3(1), dim3(1024), 0, e->stream, pg, (uint32_t)pgrid, chist, coff);
-        HIPCHK(hipGetLastError());
-        hipLaunchKernelGGL(k_cidx_place, dim3(pgrid), dim3(256), 0, e->stream, pg, (const uint32_t *)chist, list);
-        HIPCHK(hipGetLastError());
-        hipLaunchKernelGGL(k_bucket_chunks, dim3(pg.nslices * groups), dim3(1024), bc_lds, e->stream, pg, groups,
-                           e->d_table, (const uint2 *)list, (const uint32_t *)coff);
+    } else if (padded) {
+        hipLaunchKernelGGL(k_bucket_count<BK_PAD>, dim3(pg.nslices * groups), dim3(1024), bc_lds, e->stream, pg,
+                           groups, e->d_table);
     } else if (pg.split)
         hipLaunchKernelGGL(k_bucket_count<BK_SPLIT>, dim3(pg.nslices << pg.split), dim3(1024), bc_lds, e->stream, pg,
                            1u, e->d_table);
