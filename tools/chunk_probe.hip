@@ -119,6 +119,59 @@ __global__ void __launch_bounds__(1024) r_chunks(const uint4 *codes, const uint3
     for (uint32_t i = threadIdx.x; i < 40960; i += blockDim.x) out[(uint64_t)blockIdx.x * 40960 + i] = bins[i];
 }
 
+
+/* rows layout, as k_bucket_count<BK_PAD> reads it: run (row, slice) at the
+   16-B piece idx >> 16 of its row, idx & 0xFFFF + 1 codes (variable), rows of
+   ROWB + 16 * NSLICE bytes; QL lanes per run, RR rows per quad at once, U
+   pieces per lane, index words one iteration ahead */
+template <int QL, int RR, int U>
+__global__ void __launch_bounds__(1024) r_rows_idx(const uint4 *codes, const uint32_t *idx, uint64_t nrows,
+                                                    uint32_t rowp, uint32_t *out) {
+    extern __shared__ uint32_t bins[];
+    const uint32_t s = (blockIdx.x & 7u) * (NSLICE / 8) + (blockIdx.x >> 3);
+    for (uint32_t i = threadIdx.x; i < 40960; i += blockDim.x) bins[i] = 0;
+    __syncthreads();
+    const uint32_t sub = threadIdx.x & (QL - 1), runs = blockDim.x / QL;
+    uint32_t en[RR];
+    const uint64_t r00 = threadIdx.x / QL;
+#pragma unroll
+    for (int j = 0; j < RR; j++) en[j] = r00 + j * runs < nrows ? idx[(r00 + j * runs) * NSLICE + s] : 0xFFFFFFFFu;
+    for (uint64_t r = r00; r < nrows; r += RR * runs) {
+        uint32_t e[RR];
+#pragma unroll
+        for (int j = 0; j < RR; j++) e[j] = en[j];
+        const uint64_t rn = r + RR * runs;
+#pragma unroll
+        for (int j = 0; j < RR; j++) en[j] = rn + j * runs < nrows ? idx[(rn + j * runs) * NSLICE + s] : 0xFFFFFFFFu;
+        uint4 v[RR][U];
+        uint32_t np[RR], last[RR];
+#pragma unroll
+        for (int j = 0; j < RR; j++) {
+            const uint32_t c = e[j] == 0xFFFFFFFFu ? 0u : (e[j] & 0xFFFFu) + 1u;
+            np[j] = (c + 7u) >> 3;
+            last[j] = c & 7u;
+            const uint4 *p = codes + (r + j * runs) * rowp + (e[j] >> 16) + sub;
+#pragma unroll
+            for (int u = 0; u < U; u++) v[j][u] = sub + QL * u < np[j] ? p[QL * u] : make_uint4(0, 0, 0, 0);
+        }
+#pragma unroll
+        for (int j = 0; j < RR; j++)
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                const uint32_t q = sub + QL * u;
+                if (q < np[j]) {
+                    const uint32_t nv = q + 1 == np[j] && last[j] ? last[j] : 8u;
+                    const uint32_t w[4] = {v[j][u].x, v[j][u].y, v[j][u].z, v[j][u].w};
+#pragma unroll
+                    for (int h = 0; h < 8; h++)
+                        if ((uint32_t)h < nv) atomicAdd(&bins[(w[h >> 1] >> (16 * (h & 1))) & 0x7FFFu], 1u);
+                }
+            }
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < 40960; i += blockDim.x) out[(uint64_t)blockIdx.x * 40960 + i] = bins[i];
+}
+
 int main(int argc, char **argv) {
     const uint64_t GB = argc > 1 ? strtoull(argv[1], 0, 10) : 10;   /* codes bytes, GB */
     const uint32_t blocks = 256;
@@ -175,6 +228,36 @@ int main(int argc, char **argv) {
     timeit("r_chunks", [&] {
         hipLaunchKernelGGL(r_chunks, dim3(NSLICE), dim3(1024), 163840, 0, codes, list, blocks * cpb, out);
     });
+    /* realistic rows: ROWB + 16 * NSLICE bytes per row; run lengths around 128 codes (a 64K-entry batch
+       over 512 slices, multinomial), padded to 16-B pieces */
+    {
+        const uint32_t rowp = (ROWB + 16 * NSLICE) / 16;       /* pieces per row */
+        const uint64_t nr = bytes / ((uint64_t)rowp * 16);
+        std::vector<uint32_t> ix(nr * NSLICE);
+        std::mt19937_64 g(7);
+        std::vector<uint32_t> cnt(NSLICE);
+        for (uint64_t r = 0; r < nr; r++) {
+            for (uint32_t b = 0; b < NSLICE; b++) cnt[b] = RUN - 11 + (uint32_t)(g() % 23);   /* ~ binomial spread */
+            uint32_t at = 0;
+            for (uint32_t b = 0; b < NSLICE; b++) {
+                ix[r * NSLICE + b] = cnt[b] ? (at << 16) | (cnt[b] - 1) : 0xFFFFFFFFu;
+                at += (cnt[b] + 7) / 8;
+            }
+        }
+        uint32_t *didx;
+        CHK(hipMalloc(&didx, ix.size() * 4));
+        CHK(hipMemcpy(didx, ix.data(), ix.size() * 4, hipMemcpyHostToDevice));
+        CHK(hipFuncSetAttribute((const void *)r_rows_idx<4, 2, 5>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840));
+        CHK(hipFuncSetAttribute((const void *)r_rows_idx<8, 2, 3>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840));
+        CHK(hipFuncSetAttribute((const void *)r_rows_idx<4, 3, 5>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840));
+        CHK(hipFuncSetAttribute((const void *)r_rows_idx<16, 2, 2>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840));
+        CHK(hipFuncSetAttribute((const void *)r_rows_idx<4, 4, 5>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840));
+        timeit("idx q4r2u5", [&] { hipLaunchKernelGGL((r_rows_idx<4, 2, 5>), dim3(NSLICE), dim3(1024), 163840, 0, codes, didx, nr, rowp, out); });
+        timeit("idx q8r2u3", [&] { hipLaunchKernelGGL((r_rows_idx<8, 2, 3>), dim3(NSLICE), dim3(1024), 163840, 0, codes, didx, nr, rowp, out); });
+        timeit("idx q4r3u5", [&] { hipLaunchKernelGGL((r_rows_idx<4, 3, 5>), dim3(NSLICE), dim3(1024), 163840, 0, codes, didx, nr, rowp, out); });
+        timeit("idx q16r2u2", [&] { hipLaunchKernelGGL((r_rows_idx<16, 2, 2>), dim3(NSLICE), dim3(1024), 163840, 0, codes, didx, nr, rowp, out); });
+        timeit("idx q4r4u5", [&] { hipLaunchKernelGGL((r_rows_idx<4, 4, 5>), dim3(NSLICE), dim3(1024), 163840, 0, codes, didx, nr, rowp, out); });
+    }
     CHK(hipDeviceSynchronize());
     return 0;
 }
