@@ -222,7 +222,13 @@ __device__ __forceinline__ void lds_add(const Ctx &, uint32_t byte_off, uint32_t
 template <int HM>
 __device__ __forceinline__ void hist_add(const Ctx &cx, uint64_t idx, uint32_t w) {
     if (HM == H_NONE) return;
-    if (HM == H_GLOBAL || HM == H_EMIT) {
+    if (HM == H_EMIT && cx.flush) {
+        /* k_part over a fresh k = 15, 16 table (not zeroed: k_count_parts
+           writes every bin): the window to the list k_list_add adds after
+           it (cx.flush: [0] count, [1] capacity, then the indices) */
+        const uint32_t i = atomicAdd(cx.flush, 1u);
+        if (i < cx.flush[1]) cx.flush[2 + i] = (uint32_t)fk_sigma(idx);
+    } else if (HM == H_GLOBAL || HM == H_EMIT) {
         atomicAdd(&cx.table[fk_sigma(idx)], w);
     } else if (HM == H_LDS) {
         lds_add(cx, (uint32_t)idx * 4u, w);
@@ -236,7 +242,7 @@ __device__ __forceinline__ void short_run(const Ctx &cx, int seq, uint64_t code,
        for nodeCounter (:1059-1062).  Offset of depth d: (4^d - 4) / 3. */
     uint64_t off = ((1ull << (2 * seq)) - 4) / 3;
     uint64_t m = (1ull << (2 * seq)) - 1;
-    atomicAdd(&cx.shortcnt[off + fk_sigma(code & m)], w);
+    if (cx.shortcnt) atomicAdd(&cx.shortcnt[off + fk_sigma(code & m)], w);   /* (none without nodeCounter) */
 }
 
 /* Load lane bytes [off, off+nbytes) (nbytes = 16 or 32, relative to cx.buf;
@@ -1763,6 +1769,68 @@ enum { SP_HIST = 1, SP_KEYS = 2, SP_DENSE = 3 };
 #define SP_WAVES 4u
 #define SP_BUCKET_BITS 12u
 
+/* The windows of a fast tile (contiguous layout, tile_fast's Emit) as
+ * reference-order keys, handed to the pass's mode.  Half h of a lane holds D
+ * = 16 digits (15 with a '\n', right-aligned in its word R); the 32 digits
+ * before the half are the previous half's {C, S2} (half 1: this lane's half
+ * 0; half 0: the previous lane's half 1, lane 0: the tile's entering code),
+ * so the window ending at digit j of the half is
+ *   ((prev << 2(j+1)) | (R >> 2(D-1-j))) & (4^k - 1)
+ * -- up to 20 bases from two words, which the 16-base {C, S2} of the dense
+ * path cannot give. */
+__device__ __forceinline__ void sp_fast_emit(const SpEmit &em, const Emit &fe, uint64_t c0, uint64_t maskk,
+                                             uint32_t *bh, uint32_t lane) {
+    const uint64_t pv0 = ((uint64_t)from_prev_lane(fe.BC, (uint32_t)(c0 >> 32)) << 32) |
+                         from_prev_lane(fe.B2, (uint32_t)c0);
+    const uint64_t pv1 = ((uint64_t)fe.AC << 32) | fe.A2;
+    const uint32_t R0 = fe.h0 ? fe.A2 & 0x3FFFFFFFu : fe.A2, R1 = fe.h1 ? fe.B2 & 0x3FFFFFFFu : fe.B2;
+    const uint32_t D0 = fe.h0 ? 15u : 16u, D1 = fe.h1 ? 15u : 16u;
+    /* window jj (half jj / 16, digit jj % 16), or SP_EMPTY past the half's digits */
+    auto key = [&](uint32_t jj) -> uint64_t {
+        const bool h = jj >= 16u;
+        const uint32_t j = jj & 15u, D = h ? D1 : D0, R = h ? R1 : R0;
+        const uint64_t pv = h ? pv1 : pv0;
+        if (j >= D) return SP_EMPTY;
+        return fk_sigma(((pv << (2u * (j + 1u))) | (uint64_t)(R >> (2u * (D - 1u - j)))) & maskk);
+    };
+    if (em.mode == SP_KEYS) {
+        uint32_t mine = 0;
+#pragma unroll 8
+        for (uint32_t jj = 0; jj < 32u; jj++) {
+            const uint64_t v = key(jj);
+            mine += v >= em.lo && v < em.hi ? 1u : 0u;
+        }
+        const uint32_t tot = wsum32(mine);
+        if (!tot) return;
+        unsigned long long base = 0;
+        if (lane == 0) base = atomicAdd(em.nout, (unsigned long long)tot);
+        base = rdlane64(base, 0);
+        uint64_t run = 0;
+        for (uint32_t jj = 0; jj < 32u; jj++) {
+            const uint64_t v = key(jj);
+            const bool m = v >= em.lo && v < em.hi;
+            const uint64_t bal = __ballot(m);
+            if (m) {
+                const uint64_t at = base + run + (uint64_t)__popcll(bal & ((1ull << lane) - 1ull));
+                if (at < em.out_cap) em.out[at] = v;
+            }
+            run += (uint64_t)__popcll(bal);
+        }
+    } else if (em.mode == SP_DENSE) {
+#pragma unroll 8
+        for (uint32_t jj = 0; jj < 32u; jj++) {
+            const uint64_t v = key(jj);
+            if (v >= em.lo && v < em.hi) atomicAdd(&em.dense[v - em.lo], 1ull);
+        }
+    } else {
+#pragma unroll 8
+        for (uint32_t jj = 0; jj < 32u; jj++) {
+            const uint64_t v = key(jj);
+            if (v != SP_EMPTY) atomicAdd(&bh[v >> em.shift], 1u);
+        }
+    }
+}
+
 __global__ void __launch_bounds__(SP_WAVES * 64u)
 k_sp_emit(const uint8_t *buf, uint64_t len, int k, uint64_t maskk, const XState *rst, uint64_t nranges,
           uint64_t cpw, uint64_t nchunks, SpEmit em) {
@@ -1781,14 +1849,44 @@ k_sp_emit(const uint8_t *buf, uint64_t len, int k, uint64_t maskk, const XState 
         const uint64_t rb = c0 * FK_CHUNK_BYTES, re = min(c1 * FK_CHUNK_BYTES, len);
         const XState x = rst[r];
         DState st{x.code, (uint32_t)x.R, x.hdr};
+        /* the next full tile's words load while this one is counted (one
+           dependent load per tile left the walk latency-bound) */
+        uint32_t wn[8];
+        auto load_full = [&](uint64_t at) {
+            const u32x4 *p = reinterpret_cast<const u32x4 *>(buf + at + (uint64_t)lane * FK_LANE_BYTES);
+            const u32x4 a = __builtin_nontemporal_load(p), c = __builtin_nontemporal_load(p + 1);
+            wn[0] = a.x; wn[1] = a.y; wn[2] = a.z; wn[3] = a.w;
+            wn[4] = c.x; wn[5] = c.y; wn[6] = c.z; wn[7] = c.w;
+        };
+        if (rb + FK_TILE_BYTES <= re) load_full(rb);
         for (uint64_t tb = rb; tb < re; tb += FK_TILE_BYTES) {
+            uint32_t w[8];
+            int nb = (int)FK_LANE_BYTES;
+            if (tb + FK_TILE_BYTES <= re) {
+#pragma unroll
+                for (int d = 0; d < 8; d++) w[d] = wn[d];
+            } else {
+                nb = load_lane<FK_LANE_BYTES>(cx, (int64_t)(tb + (uint64_t)lane * FK_LANE_BYTES), w);
+            }
+            if (tb + 2 * FK_TILE_BYTES <= re) load_full(tb + FK_TILE_BYTES);
+            Facts f{0, 0, 0, 0, 0, 0};
+            Counters cnt{0, 0, 0, 0, 0, FK_NO_EOF, 0};
+            /* a fast tile (bases and at most one '\n' per half, deep in a run,
+               outside a header: no short walks, every base ends a window)
+               computes its 40-bit windows in registers: no byte walk, no
+               slots */
+            {
+                const uint64_t c0 = st.code;
+                Emit fe{0, 0, 0, 0, false, false, false};
+                if (tb + FK_TILE_BYTES <= re && st.hdr == 0 &&
+                    tile_fast<true, H_EMIT, false>(cx, w, st, f, cnt, 1u, &fe)) {
+                    if (fe.deep) sp_fast_emit(em, fe, c0, maskk, bh, lane);
+                    continue;
+                }
+            }
             /* a lane reads back only the slots of its own 32 bytes */
 #pragma unroll 8
             for (uint32_t j = 0; j < FK_LANE_BYTES; j++) slots[j * 64u + lane] = SP_EMPTY;
-            uint32_t w[8];
-            const int nb = load_lane<FK_LANE_BYTES>(cx, (int64_t)(tb + (uint64_t)lane * FK_LANE_BYTES), w);
-            Facts f{0, 0, 0, 0, 0, 0};
-            Counters cnt{0, 0, 0, 0, 0, FK_NO_EOF, 0};
             tile_general<true, H_SPARSE>(cx, w, nb, 0u, st, f, cnt, 1u);
             if (em.mode == SP_KEYS) {
                 uint32_t mine = 0;
@@ -1924,7 +2022,11 @@ struct PartGeo {
     uint32_t stride;       /* index row stride: rows of both regions (k_part, then k_part<RES>) */
     uint32_t *flag;        /* [0] != 0: some range went to k_part<RES>, region 2 holds rows */
     uint32_t split;        /* k = 14: a slice's 2^16 codes counted as two halves of 2^15 bins (0: one) */
+    uint32_t *glist;       /* k = 15, 16 over a fresh table: the general tiles' windows (hist_add), or nullptr */
+    unsigned long long *fz;/* ... and the table statistics k_count_parts takes of it: FZ_SLOTS x 10 partials */
+    uint32_t kk;           /* k */
 };
+#define FZ_SLOTS 1024u   /* (spread: 128 same-address atomics each at k = 16, not 2048) */
 
 /* Every entry a fast tile's Emit hands to the partition, as f(slice, low).
  * Single windows: the 16 windows ending in each half (15 when slot 0 is not
@@ -2337,7 +2439,7 @@ k_part(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint
         if (threadIdx.x == 11) res->redo_n = 0;
     }
     for (uint32_t i = threadIdx.x; i < pg.nslices; i += PART_BLOCK_W(W)) hist[i] = 0;
-    Ctx cx{buf, len, lo, table, nullptr, shortcnt, acc, res, maskk, 0, k, nullptr};
+    Ctx cx{buf, len, lo, table, nullptr, shortcnt, acc, res, maskk, 0, k, pg.glist};
     const int lane = threadIdx.x & 63;
     const uint64_t wave = blockIdx.x * W + wave_in_block();
     const uint64_t c0 = wave * cpw, c1 = min(c0 + cpw, nchunks);
@@ -2636,7 +2738,11 @@ k_bucket_count(PartGeo pg, uint32_t groups, uint32_t *table) {
     const uint32_t nrows = pg.flag && *pg.flag ? 2u * pg.rows : pg.rows;
     const uint4 *g4 = reinterpret_cast<const uint4 *>(pg.codes);
     /* four lanes share a run and read it as contiguous 64-byte pieces (one
-       request per quad instead of one per lane).  A quad takes BUCKET_ROWS
+       request per quad instead of one per lane).  (k = 14, round 4: a lane
+       per run with 4 rows and 3 pieces each in flight fetched 19.4 GB per
+       G-base instead of 5.3 -- 33 MB of lines in flight per XCD evict the
+       lines the slice's other half and its neighbours would read from L2 --
+       and took 3.46 ms instead of 2.86.)  A quad takes BUCKET_ROWS
        rows at once: their first 64 * BUCKET_U bytes of codes and the next
        rows' index words are all in flight together (a run is ~50-250 codes, so one
        dependent chain per run would leave the CU waiting on latency; rows
@@ -2713,12 +2819,29 @@ k_bucket_count(PartGeo pg, uint32_t groups, uint32_t *table) {
         }
         return;
     }
-    for (uint32_t i = threadIdx.x; i < nb; i += blockDim.x) {
-        const uint32_t v = slice[i];
-        if (!v) continue;
-        uint32_t *dst = &table[fk_sigma(((uint64_t)b << pg.sh) | ((uint64_t)part << binsh) | i)];
-        if (groups == 1) *dst += v;   /* this block owns the slice */
-        else atomicAdd(dst, v);
+    const uint64_t base = ((uint64_t)b << pg.sh) | ((uint64_t)part << binsh);
+    if (groups != 1) {
+        for (uint32_t i = threadIdx.x; i < nb; i += blockDim.x) {
+            const uint32_t v = slice[i];
+            if (v) atomicAdd(&table[fk_sigma(base | i)], v);
+        }
+        return;
+    }
+    /* this block owns the slice: eight loads in flight per lane before the
+       adds and stores (one load-add-store chain at a time is latency-bound) */
+    constexpr uint32_t U = 8u;
+    for (uint32_t i0 = threadIdx.x; i0 < nb; i0 += U * blockDim.x) {
+        uint32_t v[U], o[U];
+#pragma unroll
+        for (uint32_t j = 0; j < U; j++) {
+            const uint32_t i = i0 + j * blockDim.x;
+            v[j] = i < nb ? slice[i] : 0u;
+        }
+#pragma unroll
+        for (uint32_t j = 0; j < U; j++) o[j] = v[j] ? table[fk_sigma(base | (i0 + j * blockDim.x))] : 0u;
+#pragma unroll
+        for (uint32_t j = 0; j < U; j++)
+            if (v[j]) table[fk_sigma(base | (i0 + j * blockDim.x))] = o[j] + v[j];
     }
 }
 
@@ -2726,74 +2849,166 @@ k_bucket_count(PartGeo pg, uint32_t groups, uint32_t *table) {
  * k = 15, 16: the second partition level.  k_part leaves each of the 2048
  * coarse slices as runs of 32-bit codes (low 2k - 11 index bits) in every
  * batch row; a slice holds 2^(2k-26) parts of 2^15 bins (16 at k = 15, 64 at
- * k = 16).  k_repart (one block per coarse slice) reads the slice's runs
- * twice -- counting its entries per part, then writing each entry's low 15
- * bits as a 16-bit code into its part's contiguous stream -- after taking the
- * slice's region of the output with one global atomic.  k_count_parts (one
- * block per part) then reads one contiguous stream into 2^15 LDS bins and
- * adds them to the table: every code is read from HBM once per level.
+ * k = 16).  k_repart (one block per REPART_G consecutive coarse slices)
+ * reads the slices' runs -- counting their entries per part, then writing
+ * each entry's low 15 bits as a 16-bit code into its part's contiguous
+ * stream -- after taking the group's region of the output with one global
+ * atomic.  k_count_parts (one block per part) then reads one contiguous
+ * stream into 2^15 LDS bins and adds them to the table.
+ *
+ * Round 4 (k = 15 / 16, 1 G bases): one block per coarse slice, a lane per
+ * row, and the entries stored one at a time at a per-part cursor moved 68-70
+ * GB of HBM per step for ~14 GB of codes (10.3 / 11.8 ms): each lane's 64-B
+ * run straddled lines no neighbour shared, and every 2-B store wrote back a
+ * partial line.  Now the lanes of a row take the group's adjacent runs (one
+ * contiguous span per row) and each round's entries are counting-sorted by
+ * part in LDS and written out as contiguous segments.
  */
 struct PartMeta {
     unsigned long long off;   /* first code of the part's stream (a multiple of 8) */
     uint32_t n, pad;
 };
-#define REPART_MAXP 64u
+#define REPART_MAXP 64u       /* parts per coarse slice (k = 16) */
+#define REPART_G 8u           /* coarse slices per k_repart block */
+#define REPART_GP (REPART_G * REPART_MAXP)
+#define REPART_CAP 32768u     /* entries per pass-B round: a batch (16 waves x 2048), the longest run */
+static_assert(16u * FK_TILE_BYTES <= REPART_CAP, "a C32 row's run fits one k_repart round");
 
 __global__ void __launch_bounds__(1024)
 k_repart(PartGeo pg, uint16_t *out, unsigned long long *alloc, PartMeta *meta) {
-    __shared__ uint32_t cnt[16][REPART_MAXP], cur[REPART_MAXP];
-    __shared__ unsigned long long poff[REPART_MAXP];
-    const uint32_t b = blockIdx.x, t = threadIdx.x, wv = t >> 6;
-    const uint32_t np = 1u << pg.split;
-    for (uint32_t i = t; i < 16u * REPART_MAXP; i += blockDim.x) (&cnt[0][0])[i] = 0;
+    /* per (slice in the group, part): entries, round count / offset /
+       cursor, written so far, stream start */
+    __shared__ uint32_t cnt[REPART_GP], hc[REPART_GP], ho[REPART_GP], cur[REPART_GP], wr[REPART_GP];
+    __shared__ unsigned long long poff[REPART_GP];
+    __shared__ uint32_t scn[17];
+    __shared__ __attribute__((aligned(16))) uint16_t rbuf[REPART_CAP];
+    const uint32_t t = threadIdx.x, wv = t >> 6, lane = t & 63;
+    const uint32_t np = 1u << pg.split, gp = REPART_G * np;   /* parts of the block */
+    const uint32_t b0 = blockIdx.x * REPART_G;                /* its first coarse slice */
+    for (uint32_t i = t; i < gp; i += blockDim.x) cnt[i] = 0;
     __syncthreads();
-    const uint32_t *ix = pg.idx + b;
     const uint32_t nrows = pg.flag && *pg.flag ? 2u * pg.rows : pg.rows;
+    const uint32_t nitems = nrows * REPART_G;   /* (row, slice) pairs, row-major: a row's runs side by side */
     const uint4 *g4 = reinterpret_cast<const uint4 *>(pg.codes);
-    /* a lane per run, its codes as 16-B pieces (4 codes each) */
-    auto each_code = [&](uint32_t r, auto &&f) {
-        const uint32_t e = ix[(size_t)r * pg.nslices];
+    /* item i: row i / G, slice b0 + i % G; its codes as 16-B pieces (4 each)
+       -- the G lanes of a row read one contiguous span */
+    auto each_code = [&](uint32_t i, auto &&f) {
+        const uint32_t r = i / REPART_G, sl = i % REPART_G;
+        const uint32_t e = pg.idx[(size_t)r * pg.nslices + b0 + sl];
         if (e == PART_NO_RUN) return;
         const uint64_t s0 = (uint64_t)r * pg.batch + (e >> 16), s1 = s0 + run_count(e);
-        for (uint64_t q = s0 >> 2; q < (s1 + 3) >> 2; q++) {
-            const uint4 v = g4[q];
+        const uint64_t q0 = s0 >> 2, q1 = (s1 + 3) >> 2;
+        auto piece = [&](const uint4 &v, uint64_t q) {
             const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
             for (int h = 0; h < 4; h++)
-                if (q * 4 + h >= s0 && q * 4 + h < s1) f(w4[h]);
-        }
+                if (q * 4 + h >= s0 && q * 4 + h < s1) f(sl * np + (w4[h] >> 15), w4[h]);
+        };
+        /* the pieces of a run of up to 17 codes in flight together (one
+           load at a time left the kernel latency-bound) */
+        uint4 v[5];
+#pragma unroll
+        for (uint32_t u = 0; u < 5u; u++) v[u] = q0 + u < q1 ? g4[q0 + u] : make_uint4(0, 0, 0, 0);
+#pragma unroll
+        for (uint32_t u = 0; u < 5u; u++)
+            if (q0 + u < q1) piece(v[u], q0 + u);
+        for (uint64_t q = q0 + 5u; q < q1; q++) piece(g4[q], q);
     };
-    /* pass A: entries per part (per-wave counters: fewer same-address atomics) */
-    for (uint32_t r = t; r < nrows; r += blockDim.x)
-        each_code(r, [&](uint32_t c) { atomicAdd(&cnt[wv][c >> 15], 1u); });
+    /* pass A: entries per part */
+    for (uint32_t i = t; i < nitems; i += blockDim.x)
+        each_code(i, [&](uint32_t p, uint32_t) { atomicAdd(&cnt[p], 1u); });
     __syncthreads();
-    if (t < 64) {   /* part totals, their 8-aligned prefix, the slice's region */
-        uint32_t n = 0;
-        if (t < np)
-            for (uint32_t w = 0; w < 16; w++) n += cnt[w][t];
-        const uint32_t sz = (n + 7u) & ~7u;
-        const uint32_t inc = wscan_incl32(sz);
-        const uint32_t tot = rdlane(inc, 63);
-        unsigned long long b0 = 0;
-        if (t == 0) b0 = atomicAdd(alloc, (unsigned long long)tot);
-        b0 = rdlane64(b0, 0);
-        if (t < np) {
-            cur[t] = 0;
-            poff[t] = b0 + inc - sz;
-            meta[(size_t)b * np + t] = PartMeta{b0 + inc - sz, n, 0};
+    if (t < 64) {   /* the parts' 8-aligned stream starts in the group's region */
+        uint32_t carry = 0;
+        for (uint32_t p0 = 0; p0 < gp; p0 += 64u) {
+            const uint32_t p = p0 + lane;
+            const uint32_t sz = p < gp ? (cnt[p] + 7u) & ~7u : 0u;
+            const uint32_t inc = wscan_incl32(sz);
+            if (p < gp) ho[p] = carry + inc - sz;   /* (ho: scratch here) */
+            carry += rdlane(inc, 63);
+        }
+        unsigned long long g0 = 0;
+        if (lane == 0) g0 = atomicAdd(alloc, (unsigned long long)carry);
+        g0 = rdlane64(g0, 0);
+        for (uint32_t p = lane; p < gp; p += 64u) {
+            poff[p] = g0 + ho[p];
+            wr[p] = 0;
+            meta[(size_t)b0 * np + p] = PartMeta{g0 + ho[p], cnt[p], 0};   /* slice-major: (b0 + p / np) * np + p % np */
         }
     }
+    /* pass B: rounds of whole runs (a lane per item) holding up to
+       REPART_CAP entries: counted by part, placed in LDS by part, and each
+       part's segment written after the part's earlier rounds */
+    uint32_t base = 0;
     __syncthreads();
-    /* pass B: every entry's low 15 bits into its part's stream */
-    for (uint32_t r = t; r < nrows; r += blockDim.x)
-        each_code(r, [&](uint32_t c) {
-            const uint32_t p = c >> 15;
-            /* one cursor per part for the whole block: its waves' entries
-               land next to each other (per-wave cursors, 16 x more write
-               streams, made this kernel 2 x slower) */
+    auto item_count = [&](uint32_t i) -> uint32_t {
+        return i < nitems ? run_count(pg.idx[(size_t)(i / REPART_G) * pg.nslices + b0 + i % REPART_G]) : 0u;
+    };
+    for (;;) {
+        const uint32_t i = base + t;
+        const uint32_t c = item_count(i);
+        const uint32_t wi = wscan_incl32(c);
+        if (lane == 63) scn[wv] = wi;
+        for (uint32_t p = t; p < gp; p += blockDim.x) hc[p] = 0;
+        __syncthreads();
+        uint32_t before = 0;
+        for (uint32_t w = 0; w < wv; w++) before += scn[w];
+        /* the leading items whose runs fit (item `base`'s always does) */
+        const bool take = i < nitems && before + wi <= REPART_CAP;
+        const uint32_t ntake = (uint32_t)__syncthreads_count(take);
+        /* the item's first pieces stay in registers from the count to the
+           placement (one read of the codes per round, not two) */
+        const uint32_t sl = i % REPART_G;
+        const uint32_t ie = take ? pg.idx[(size_t)(i / REPART_G) * pg.nslices + b0 + sl] : PART_NO_RUN;
+        /* (an empty run -- PART_NO_RUN, count 0 -- reads nothing) */
+        const uint64_t s0 = (uint64_t)(i / REPART_G) * pg.batch + (ie == PART_NO_RUN ? 0u : ie >> 16);
+        const uint64_t s1 = s0 + (ie == PART_NO_RUN ? 0u : c);
+        const uint64_t q0 = s0 >> 2, q1 = (s1 + 3) >> 2;
+        uint4 pv[5];
+#pragma unroll
+        for (uint32_t u = 0; u < 5u; u++) pv[u] = q0 + u < q1 ? g4[q0 + u] : make_uint4(0, 0, 0, 0);
+        auto codes = [&](auto &&f) {
+            auto piece = [&](const uint4 &v, uint64_t q) {
+                const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+                for (int h = 0; h < 4; h++)
+                    if (q * 4 + h >= s0 && q * 4 + h < s1) f(sl * np + (w4[h] >> 15), w4[h]);
+            };
+#pragma unroll
+            for (uint32_t u = 0; u < 5u; u++)
+                if (q0 + u < q1) piece(pv[u], q0 + u);
+            for (uint64_t q = q0 + 5u; q < q1; q++) piece(g4[q], q);
+        };
+        codes([&](uint32_t p, uint32_t) { atomicAdd(&hc[p], 1u); });
+        __syncthreads();
+        if (t < 64) {
+            uint32_t carry = 0;
+            for (uint32_t p0 = 0; p0 < gp; p0 += 64u) {
+                const uint32_t p = p0 + lane;
+                const uint32_t n = p < gp ? hc[p] : 0u;
+                const uint32_t inc = wscan_incl32(n);
+                if (p < gp) { ho[p] = carry + inc - n; cur[p] = carry + inc - n; }
+                carry += rdlane(inc, 63);
+            }
+        }
+        __syncthreads();
+        codes([&](uint32_t p, uint32_t v) {
             const uint32_t at = atomicAdd(&cur[p], 1u);
-            out[poff[p] + at] = (uint16_t)(c & 0x7FFFu);
+            rbuf[at] = (uint16_t)(v & 0x7FFFu);
         });
+        __syncthreads();
+        /* a wave per part: consecutive entries to consecutive 2-B slots */
+        for (uint32_t p = wv; p < gp; p += 16u) {
+            const uint32_t n = hc[p], o = ho[p];
+            uint16_t *dst = out + poff[p] + wr[p];
+            for (uint32_t j = lane; j < n; j += 64u) dst[j] = rbuf[o + j];
+        }
+        __syncthreads();
+        for (uint32_t p = t; p < gp; p += blockDim.x) wr[p] += hc[p];
+        base += ntake;
+        if (base >= nitems || ntake == 0) break;
+        __syncthreads();
+    }
 }
 
 /* one block per part: its stream into 2^15 LDS bins, then into the table */
@@ -2815,9 +3030,94 @@ k_count_parts(PartGeo pg, const uint16_t *in, const PartMeta *meta, uint32_t *ta
             if (q * 8u + (uint32_t)h < m.n) atomicAdd(&slice[(w4[h >> 1] >> (16 * (h & 1))) & 0x7FFFu], 1u);
     }
     __syncthreads();
-    for (uint32_t i = threadIdx.x; i < (1u << 15); i += blockDim.x) {
-        const uint32_t v = slice[i];
-        if (v) table[fk_sigma(((uint64_t)b << pg.sh) | ((uint64_t)part << 15) | i)] += v;   /* the block owns it */
+    /* the part's bins into the table (the block owns them), eight loads in
+       flight per lane before the adds and stores: one load-add-store chain
+       at a time left this loop latency-bound (k = 16: 13.3 ms per G-base) */
+    const uint64_t base = ((uint64_t)b << pg.sh) | ((uint64_t)part << 15);
+    if (pg.glist) {
+        /* a fresh table (the segment's k_zero left it out): every bin of
+           the part written, no read (k = 16: 17 GB of zeroing and 17 GB of
+           reads less per step); the general tiles' windows follow
+           (k_list_add) */
+        /* with the statistics k_table_stats would read the table for
+           (distinct, sum, last- and first-base marginals): they stand unless
+           the general tiles' list or k_redo adds to the table afterwards */
+        const int fs = 2 * pg.kk - 2;
+        /* a lane's bins i = lane + 1024 j all end in the same base (sigma
+           maps digits one by one, and i & 3 = lane & 3): its sum is its
+           last-base marginal */
+        uint32_t dist = 0;
+        unsigned long long sum = 0;
+        for (uint32_t i = threadIdx.x; i < (1u << 15); i += 1024u) {
+            const uint32_t v = slice[i];
+            table[fk_sigma(base | i)] = v;
+            dist += v != 0;
+            sum += v;
+        }
+        const uint32_t ld = (uint32_t)(fk_sigma((uint64_t)(threadIdx.x & 3u)) & 3u);
+        unsigned long long v10[6] = {dist, sum, ld == 0 ? sum : 0ull, ld == 1 ? sum : 0ull,
+                                     ld == 2 ? sum : 0ull, ld == 3 ? sum : 0ull};
+#pragma unroll
+        for (int q = 0; q < 6; q++) v10[q] = wsum64(v10[q]);
+        /* the wave sums in the bins' LDS, once every lane has read its bins
+           (no static LDS: the kernel's dynamic maximum is the whole 160 KiB) */
+        __syncthreads();
+        unsigned long long *wp = reinterpret_cast<unsigned long long *>(slice);
+        const uint32_t wv = threadIdx.x >> 6;
+        if ((threadIdx.x & 63) == 0)
+#pragma unroll
+            for (int q = 0; q < 6; q++) wp[wv * 6u + q] = v10[q];
+        __syncthreads();
+        if (threadIdx.x < 10) {
+            unsigned long long t = 0;
+            const uint32_t q = threadIdx.x;
+            if (q < 6) {
+                for (uint32_t w = 0; w < 16; w++) t += wp[w * 6u + q];
+            } else {   /* the first base of every bin of the part: one digit */
+                for (uint32_t w = 0; w < 16; w++) t += wp[w * 6u + 1u];
+                if ((uint32_t)((fk_sigma(base) >> fs) & 3u) != q - 6u) t = 0;
+            }
+            if (t) atomicAdd(&pg.fz[(blockIdx.x % FZ_SLOTS) * 10u + q], t);
+        }
+        return;
+    }
+    constexpr uint32_t U = 8u;
+    for (uint32_t i0 = threadIdx.x; i0 < (1u << 15); i0 += U * 1024u) {
+        uint32_t v[U], o[U];
+#pragma unroll
+        for (uint32_t j = 0; j < U; j++) v[j] = slice[i0 + j * 1024u];
+#pragma unroll
+        for (uint32_t j = 0; j < U; j++) o[j] = v[j] ? table[fk_sigma(base | (i0 + j * 1024u))] : 0u;
+#pragma unroll
+        for (uint32_t j = 0; j < U; j++)
+            if (v[j]) table[fk_sigma(base | (i0 + j * 1024u))] = o[j] + v[j];
+    }
+}
+
+/* the general tiles' windows of a fresh two-level table (hist_add's list) */
+__global__ void k_list_init(uint32_t *list, uint32_t cap, unsigned long long *fz) {
+    if (threadIdx.x == 0) { list[0] = 0; list[1] = cap; }
+    for (uint32_t i = threadIdx.x; i < FZ_SLOTS * 10u; i += blockDim.x) fz[i] = 0;
+}
+__global__ void __launch_bounds__(256)
+k_list_add(const uint32_t *list, uint32_t *table, int k, unsigned long long *fz) {
+    const uint32_t n = min(list[0], list[1]);
+    const int fs = 2 * k - 2;
+    /* with what each window changes in the statistics k_count_parts took
+       (the old value of its bin tells whether it was distinct before) */
+    unsigned long long v10[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const uint32_t x = list[2 + i];
+        const uint32_t old = atomicAdd(&table[x], 1u);
+        v10[0] += old == 0;
+        v10[1] += 1;
+        v10[2 + (x & 3u)] += 1;
+        v10[6 + ((x >> fs) & 3u)] += 1;
+    }
+#pragma unroll
+    for (int q = 0; q < 10; q++) {
+        const unsigned long long t = wsum64(v10[q]);
+        if ((threadIdx.x & 63) == 0 && t) atomicAdd(&fz[((blockIdx.x * 4u + (threadIdx.x >> 6)) % FZ_SLOTS) * 10u + q], t);
     }
 }
 
@@ -3246,7 +3546,8 @@ __device__ void stats_publish(DevRes *res, DevRes *host_res, const unsigned long
 __global__ void __launch_bounds__(256)
 k_table_stats(uint32_t *table, uint64_t n, int k, DevRes *res,
               unsigned long long *acc, unsigned long long *facc, int fresh, DevRes *host_res, uint32_t *done,
-              uint32_t seq, uint32_t *subs, int nsub, unsigned long long *part, int split) {
+              uint32_t seq, uint32_t *subs, int nsub, unsigned long long *part, int split,
+              const unsigned long long *fz, const uint32_t *glist) {
     if (blockIdx.x == 0) {
         /* the feed's counters (facc, zero between feeds) join the engine's */
         if (threadIdx.x < ACC_N) {
@@ -3261,7 +3562,20 @@ k_table_stats(uint32_t *table, uint64_t n, int k, DevRes *res,
         if (threadIdx.x == 0) res->need = 0;
     }
     unsigned long long dist = 0, sum = 0, last[4] = {0, 0, 0, 0}, first[4] = {0, 0, 0, 0};
-    const uint64_t n4 = n / 4;
+    uint64_t n4 = n / 4;
+    /* a fresh k = 15, 16 table whose statistics k_count_parts and
+       k_list_add took: they stand unless k_redo changed it since */
+    if (fz && res->redo_n == 0) {
+        n4 = 0;
+        if (threadIdx.x == 0) {
+            for (uint32_t sl = blockIdx.x; sl < FZ_SLOTS; sl += gridDim.x) {
+                const unsigned long long *z = fz + sl * 10u;
+                dist += z[0]; sum += z[1];
+                last[0] += z[2]; last[1] += z[3]; last[2] += z[4]; last[3] += z[5];
+                first[0] += z[6]; first[1] += z[7]; first[2] += z[8]; first[3] += z[9];
+            }
+        }
+    }
     uint4 *t4 = reinterpret_cast<uint4 *>(table);
     const int fs = 2 * (k - 1);
     for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n4; i += (uint64_t)gridDim.x * blockDim.x) {
@@ -3693,6 +4007,12 @@ struct fk_engine {
     bool dstate_pending = false;
     bool dirty = false;                       /* table / short walks changed since the last reset */
     bool seg_clean = true;                    /* ... not before the current segment */
+    bool tab_fresh = false;                   /* k = 15, 16: this segment's k_zero left the table out
+                                                 (k_count_parts writes every bin, k_list_add the rest) */
+    uint32_t *d_glist = nullptr;              /* ... the general tiles' windows: [0] count, [1] cap, indices */
+    uint64_t glist_cap = 0;
+    unsigned long long *d_fz = nullptr;       /* ... and its statistics from k_count_parts (FZ_SLOTS x 10) */
+    bool fz_ready = false;                    /* the next launch_table_stats may take them */
     bool seg_snap = false;                    /* d_snap holds them as before the current segment */
     uint32_t *d_snap = nullptr;
     uint64_t snap_cap = 0;
@@ -3726,12 +4046,13 @@ static hipError_t write_dstate(fk_engine *e, const XState &x) {
     return hipMemcpyAsync(e->d_state, &x, sizeof x, hipMemcpyHostToDevice, e->stream);
 }
 
-static int flush_zero(fk_engine *e) {
+static int flush_zero(fk_engine *e, bool keep_table = false) {
     if (!e->zero_pending) return FK_OK;
     e->zero_pending = false;
-    const uint64_t work = std::max<uint64_t>(e->nbins / 4, std::max<uint64_t>(e->nshort, (1 + FK_ACC_COPIES) * ACC_N));
+    const uint64_t nb = keep_table ? 0 : e->nbins;   /* (a fresh two-level count writes every bin itself) */
+    const uint64_t work = std::max<uint64_t>(nb / 4, std::max<uint64_t>(e->nshort, (1 + FK_ACC_COPIES) * ACC_N));
     const unsigned grid = (unsigned)std::min<uint64_t>((uint64_t)e->cus * 8, (work + 255) / 256);
-    hipLaunchKernelGGL(k_zero, dim3(grid), dim3(256), 0, e->stream, e->d_table, e->nbins, e->d_short, e->nshort,
+    hipLaunchKernelGGL(k_zero, dim3(grid), dim3(256), 0, e->stream, e->d_table, nb, e->d_short, e->nshort,
                        e->d_acc, e->d_state, e->d_sub, e->d_sub ? FK_SUBTABLES : 0);
     HIPCHK(hipGetLastError());
     return FK_OK;
@@ -3829,7 +4150,7 @@ extern "C" void fk_engine_destroy(fk_engine *e) {
     if (e->stream) hipStreamSynchronize(e->stream);
     hipFree(e->d_table); hipFree(e->d_short); hipFree(e->d_sub); hipFree(e->d_snap);
     hipFree(e->d_pairs);
-    hipFree(e->d_parts); hipFree(e->d_pmeta);
+    hipFree(e->d_parts); hipFree(e->d_pmeta); hipFree(e->d_glist); hipFree(e->d_fz);
     hipFree(e->d_codes); hipFree(e->d_pidx); hipFree(e->d_pflag); hipFree(e->d_acc); hipFree(e->d_res); hipFree(e->d_tmp);
     hipFree(e->d_state); hipFree(e->d_rr); hipFree(e->d_rtrue);
     hipFree(e->d_redo); hipFree(e->d_tf); hipFree(e->d_stage); hipFree(e->d_resume);
@@ -3927,7 +4248,10 @@ extern "C" int fk_engine_create(int k, const fk_opts *opts, fk_engine **out) {
     /* 8 <= k <= 16 partitioned (k = 15, 16 with a second level, k_repart) */
     e->part = k >= 8 && k <= 16;
     e->maskk = (1ull << (2 * k)) - 1;
-    e->nshort = k > 1 && !e->sparse ? ((1ull << (2 * k)) - 4) / 3 : 0;
+    /* the short walks' counts serve nodeCounter alone (depth-1 touches are
+       counters): an engine without it keeps none (k = 16: 5.7 GB less to
+       zero per step) */
+    e->nshort = k > 1 && !e->sparse && e->opts.want_nodes ? ((1ull << (2 * k)) - 4) / 3 : 0;
     if (e->opts.stream) {
         e->stream = (hipStream_t)e->opts.stream;
     } else {
@@ -3981,7 +4305,10 @@ extern "C" int fk_engine_create(int k, const fk_opts *opts, fk_engine **out) {
     if (e->part)   /* k_bucket_count: one 2^15-bin slice + its 2^13 single bins (160 KiB) in LDS */
         for (const void *f : {(const void *)k_bucket_count<BK_PLAIN>, (const void *)k_bucket_count<BK_SPLIT>,
                               (const void *)k_count_parts, (const void *)k_bucket_count<BK_PAD>})
-            hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 5 << 15);
+            if (hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 5 << 15) != hipSuccess) {
+                fk_engine_destroy(e);
+                return FK_E_HIP;
+            }
     for (int i = 0; i < 3; i++)
         /* timing only (results travel through mapped memory): no system-scope
            fence, which costs a cache writeback + invalidate and a gap of
@@ -4209,9 +4536,12 @@ static int launch_table_stats(fk_engine *e, bool zero_first, hipEvent_t stop = n
     if (e->ts_blocks) gd = std::min<unsigned>(e->ts_blocks, (unsigned)e->cus * 4);
     const int split = gd > 16;   /* large tables: partials, then k_table_final */
     if (++e->res_seq == 0) e->res_seq = 1;
+    const bool fz = e->fz_ready;   /* only for the statistics right after a fresh two-level count */
+    e->fz_ready = false;
     hipExtLaunchKernelGGL(k_table_stats, dim3(gd), dim3(256), 0, e->stream, nullptr, split ? nullptr : stop, 0,
                           e->d_table, e->nbins, e->k, e->d_res, e->d_acc, e->d_facc, fresh ? 1 : 0, e->h_res_dev,
-                          e->d_done, e->res_seq, e->d_sub, (subs && e->d_sub) ? FK_SUBTABLES : 0, e->d_tpart, split);
+                          e->d_done, e->res_seq, e->d_sub, (subs && e->d_sub) ? FK_SUBTABLES : 0, e->d_tpart, split,
+                          fz ? (const unsigned long long *)e->d_fz : nullptr, fz ? (const uint32_t *)e->d_glist : nullptr);
     HIPCHK(hipGetLastError());
     if (split) {
         hipExtLaunchKernelGGL(k_table_final, dim3(1), dim3(256), 0, e->stream, nullptr, stop, 0, e->d_res,
@@ -4262,6 +4592,33 @@ static int launch_part(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t l
     pg.nslices = pairs ? pg.npair : 1u << (2 * k - pg.sh);   /* singles fold into the pair slices */
     pg.pairs = pg.singles = nullptr;
     pg.nomix = e->no_mixed ? 1u : 0u;
+    pg.glist = nullptr;
+    pg.fz = nullptr;
+    pg.kk = (uint32_t)k;
+    e->fz_ready = false;
+    if (c32 && e->tab_fresh && !exact) {
+        /* the general tiles' windows go to a list (hist_add): at most 4
+           general tiles per range (one comment line or run break and the
+           bases-only tiles around it in k_part, the ragged last tile in
+           k_part<RES>; tile_mixed takes every other tile outside the int32
+           zone, which tab_fresh excludes) */
+        const uint64_t cap = (uint64_t)g.nranges * 4u * FK_TILE_BYTES + 4096u;
+        if (cap + 2 > e->glist_cap) {
+            hipFree(e->d_glist);
+            e->d_glist = nullptr;
+            e->glist_cap = 0;
+            if (hipMalloc((void **)&e->d_glist, (cap + 2) * sizeof(uint32_t)) != hipSuccess) return FK_E_OOM;
+            e->glist_cap = cap + 2;
+        }
+        if (!e->d_fz && hipMalloc((void **)&e->d_fz, FZ_SLOTS * 10 * sizeof(unsigned long long)) != hipSuccess)
+            return FK_E_OOM;
+        hipLaunchKernelGGL(k_list_init, dim3(1), dim3(256), 0, e->stream, e->d_glist, (uint32_t)cap, e->d_fz);
+        HIPCHK(hipGetLastError());
+        pg.glist = e->d_glist;
+        pg.fz = e->d_fz;
+        e->fz_ready = true;
+    }
+    e->tab_fresh = false;
     if (pairs) {
         const uint64_t need = e->nbins * 5;                 /* 4^(k+1) pair bins + 4^k single bins */
         if (need > e->pair_cap) {
@@ -4361,10 +4718,15 @@ static int launch_part(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t l
         PartMeta *meta = static_cast<PartMeta *>(e->d_pmeta);
         unsigned long long *alloc = reinterpret_cast<unsigned long long *>(meta + (size_t)2048 * REPART_MAXP);
         HIPCHK(hipMemsetAsync(alloc, 0, sizeof(unsigned long long), e->stream));
-        hipLaunchKernelGGL(k_repart, dim3(pg.nslices), dim3(1024), 0, e->stream, pg, e->d_parts, alloc, meta);
+        hipLaunchKernelGGL(k_repart, dim3(pg.nslices / REPART_G), dim3(1024), 0, e->stream, pg, e->d_parts, alloc, meta);
         HIPCHK(hipGetLastError());
         hipLaunchKernelGGL(k_count_parts, dim3((unsigned)nparts), dim3(1024), (size_t)1 << 17, e->stream, pg,
                            (const uint16_t *)e->d_parts, (const PartMeta *)meta, e->d_table);
+        if (pg.glist) {
+            HIPCHK(hipGetLastError());
+            hipLaunchKernelGGL(k_list_add, dim3((unsigned)e->cus * 4), dim3(256), 0, e->stream, pg.glist, e->d_table,
+                               k, pg.fz);
+        }
     } else if (padded) {
         hipLaunchKernelGGL(k_bucket_count<BK_PAD>, dim3(pg.nslices * groups), dim3(1024), bc_lds, e->stream, pg,
                            groups, e->d_table);
@@ -4574,10 +4936,15 @@ static int count_segment(fk_engine *e, const uint8_t *dbuf, uint64_t len, int64_
        adds to from every block) */
     bool op = e->onepass && !e->part && LDS_MODE(hist_mode(e)) && (has_init || shard);
     const bool fresh = op && e->zero_pending && !e->opts.want_nodes;
+    /* k = 15, 16 right after a reset: k_count_parts writes every bin of the
+       table, so the reset leaves the table out (16 GiB at k = 16); not where
+       the int32 seqSize zone can be reached (its recount needs the zeroed
+       table, and k_part<RES> counts such tiles with the general walk) */
+    e->tab_fresh = e->part && e->k >= 15 && e->zero_pending && !int32_zone_possible(e, len);
     if (fresh) {
         e->zero_pending = false;
     } else {
-        rc = flush_zero(e);      /* a pending reset, just before the first launch */
+        rc = flush_zero(e, e->tab_fresh);      /* a pending reset, just before the first launch */
         if (rc) return rc;
     }
     e->op_pending = op;
