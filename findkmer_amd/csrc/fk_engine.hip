@@ -1761,13 +1761,54 @@ struct SpEmit {
     unsigned long long *nshort;
     uint64_t short_cap;
     uint64_t *out;                  /* SP_KEYS */
-    unsigned long long *nout;
+    unsigned long long *nout;       /* ... slots claimed (whole SP_CHUNKs) */
     uint64_t out_cap;
+    unsigned long long *nreal;      /* ... windows written (the rest of the claimed slots: SP_PAD) */
     unsigned long long *dense;      /* SP_DENSE: count of key lo + i */
 };
 enum { SP_HIST = 1, SP_KEYS = 2, SP_DENSE = 3 };
 #define SP_WAVES 4u
 #define SP_BUCKET_BITS 12u
+/* SP_KEYS output: each wave claims SP_CHUNK slots at a time from the pass's
+   counter and fills them in order; the unfilled end of its last chunk holds
+   SP_PAD (4^k: above every key, so the sort puts the pads last and the
+   run-length encode leaves them as one final run).  Round 4: one claim per
+   tile and wave -- 5 M same-address atomics per 10 GB pass -- made each keys
+   pass take 60 ms against 10 ms for the histogram pass of the same walk. */
+#define SP_CHUNK 8192u
+struct SpOut {
+    uint64_t base;    /* the wave's current chunk (wave-uniform) */
+    uint32_t fill;    /* slots of it used (SP_CHUNK: none claimed yet) */
+    uint64_t real;    /* windows written by the wave */
+};
+/* the wave's tot entries of this tile: slots for positions 0..tot-1 (a new
+   chunk claimed when the current one runs out; tot <= one tile < SP_CHUNK) */
+__device__ __forceinline__ uint64_t sp_claim(const SpEmit &em, SpOut &o, uint32_t tot, uint64_t &nb, uint32_t &rem) {
+    rem = SP_CHUNK - o.fill;
+    nb = 0;
+    if (tot > rem) {
+        unsigned long long b = 0;
+        if ((threadIdx.x & 63) == 0) b = atomicAdd(em.nout, (unsigned long long)SP_CHUNK);
+        nb = rdlane64(b, 0);
+    }
+    return o.base + o.fill;
+}
+__device__ __forceinline__ uint64_t sp_slot_at(const SpOut &o, uint64_t cur, uint64_t nb, uint32_t rem, uint64_t p) {
+    return p < rem ? cur + p : nb + (p - rem);
+}
+__device__ __forceinline__ void sp_advance(SpOut &o, uint32_t tot, uint64_t nb, uint32_t rem) {
+    if (tot > rem) { o.base = nb; o.fill = tot - rem; }
+    else o.fill += tot;
+    o.real += tot;
+}
+/* the end of the wave's walk: pad its chunk, count its windows */
+__device__ __forceinline__ void sp_close(const SpEmit &em, const SpOut &o, uint64_t pad) {
+    const uint32_t lane = threadIdx.x & 63;
+    if (o.fill < SP_CHUNK)
+        for (uint32_t i = o.fill + lane; i < SP_CHUNK; i += 64u)
+            if (o.base + i < em.out_cap) em.out[o.base + i] = pad;
+    if (lane == 0 && o.real) atomicAdd(em.nreal, (unsigned long long)o.real);
+}
 
 /* The windows of a fast tile (contiguous layout, tile_fast's Emit) as
  * reference-order keys, handed to the pass's mode.  Half h of a lane holds D
@@ -1779,7 +1820,7 @@ enum { SP_HIST = 1, SP_KEYS = 2, SP_DENSE = 3 };
  * -- up to 20 bases from two words, which the 16-base {C, S2} of the dense
  * path cannot give. */
 __device__ __forceinline__ void sp_fast_emit(const SpEmit &em, const Emit &fe, uint64_t c0, uint64_t maskk,
-                                             uint32_t *bh, uint32_t lane) {
+                                             uint32_t *bh, uint32_t lane, SpOut &so) {
     const uint64_t pv0 = ((uint64_t)from_prev_lane(fe.BC, (uint32_t)(c0 >> 32)) << 32) |
                          from_prev_lane(fe.B2, (uint32_t)c0);
     const uint64_t pv1 = ((uint64_t)fe.AC << 32) | fe.A2;
@@ -1802,20 +1843,21 @@ __device__ __forceinline__ void sp_fast_emit(const SpEmit &em, const Emit &fe, u
         }
         const uint32_t tot = wsum32(mine);
         if (!tot) return;
-        unsigned long long base = 0;
-        if (lane == 0) base = atomicAdd(em.nout, (unsigned long long)tot);
-        base = rdlane64(base, 0);
+        uint64_t nb;
+        uint32_t rem;
+        const uint64_t cur = sp_claim(em, so, tot, nb, rem);
         uint64_t run = 0;
         for (uint32_t jj = 0; jj < 32u; jj++) {
             const uint64_t v = key(jj);
             const bool m = v >= em.lo && v < em.hi;
             const uint64_t bal = __ballot(m);
             if (m) {
-                const uint64_t at = base + run + (uint64_t)__popcll(bal & ((1ull << lane) - 1ull));
+                const uint64_t at = sp_slot_at(so, cur, nb, rem, run + (uint64_t)__popcll(bal & ((1ull << lane) - 1ull)));
                 if (at < em.out_cap) em.out[at] = v;
             }
             run += (uint64_t)__popcll(bal);
         }
+        sp_advance(so, tot, nb, rem);
     } else if (em.mode == SP_DENSE) {
 #pragma unroll 8
         for (uint32_t jj = 0; jj < 32u; jj++) {
@@ -1844,13 +1886,13 @@ k_sp_emit(const uint8_t *buf, uint64_t len, int k, uint64_t maskk, const XState 
     }
     Ctx cx{buf, len, 0, nullptr, nullptr, nullptr, nullptr, nullptr, maskk, 0, k, nullptr, slots};
     const uint64_t nw = (uint64_t)gridDim.x * SP_WAVES;
+    SpOut so{0, SP_CHUNK, 0};   /* SP_KEYS: the wave's output chunk */
     for (uint64_t r = (uint64_t)blockIdx.x * SP_WAVES + wv; r < nranges; r += nw) {
         const uint64_t c0 = r * cpw, c1 = min(c0 + cpw, nchunks);
         const uint64_t rb = c0 * FK_CHUNK_BYTES, re = min(c1 * FK_CHUNK_BYTES, len);
         const XState x = rst[r];
         DState st{x.code, (uint32_t)x.R, x.hdr};
-        /* the next full tile's words load while this one is counted (one
-           dependent load per tile left the walk latency-bound) */
+        /* the next full tile's words load while this one is counted */
         uint32_t wn[8];
         auto load_full = [&](uint64_t at) {
             const u32x4 *p = reinterpret_cast<const u32x4 *>(buf + at + (uint64_t)lane * FK_LANE_BYTES);
@@ -1880,7 +1922,7 @@ k_sp_emit(const uint8_t *buf, uint64_t len, int k, uint64_t maskk, const XState 
                 Emit fe{0, 0, 0, 0, false, false, false};
                 if (tb + FK_TILE_BYTES <= re && st.hdr == 0 &&
                     tile_fast<true, H_EMIT, false>(cx, w, st, f, cnt, 1u, &fe)) {
-                    if (fe.deep) sp_fast_emit(em, fe, c0, maskk, bh, lane);
+                    if (fe.deep) sp_fast_emit(em, fe, c0, maskk, bh, lane, so);
                     continue;
                 }
             }
@@ -1901,20 +1943,21 @@ k_sp_emit(const uint8_t *buf, uint64_t len, int k, uint64_t maskk, const XState 
                 }
                 const uint32_t tot = wsum32(mine);
                 if (tot) {
-                    unsigned long long base = 0;
-                    if (lane == 0) base = atomicAdd(em.nout, (unsigned long long)tot);
-                    base = rdlane64(base, 0);
+                    uint64_t nb;
+                    uint32_t rem;
+                    const uint64_t cur = sp_claim(em, so, tot, nb, rem);
                     uint64_t run = 0;
                     for (uint32_t j = 0; j < FK_LANE_BYTES; j++) {
                         const uint64_t v = slots[j * 64u + lane];
                         const bool m = v >= em.lo && v < em.hi;
                         const uint64_t bal = __ballot(m);
                         if (m) {
-                            const uint64_t at = base + run + (uint64_t)__popcll(bal & ((1ull << lane) - 1ull));
+                            const uint64_t at = sp_slot_at(so, cur, nb, rem, run + (uint64_t)__popcll(bal & ((1ull << lane) - 1ull)));
                             if (at < em.out_cap) em.out[at] = v;
                         }
                         run += (uint64_t)__popcll(bal);
                     }
+                    sp_advance(so, tot, nb, rem);
                 }
             } else if (em.mode == SP_DENSE) {
 #pragma unroll 8
@@ -1935,6 +1978,7 @@ k_sp_emit(const uint8_t *buf, uint64_t len, int k, uint64_t maskk, const XState 
             }
         }
     }
+    if (em.mode == SP_KEYS) sp_close(em, so, 1ull << (2 * k));
     if (em.mode == SP_HIST) {
         __syncthreads();
         for (uint32_t i = threadIdx.x; i < em.nbuckets; i += blockDim.x)
@@ -2944,40 +2988,63 @@ k_repart(PartGeo pg, uint16_t *out, unsigned long long *alloc, PartMeta *meta) {
     auto item_count = [&](uint32_t i) -> uint32_t {
         return i < nitems ? run_count(pg.idx[(size_t)(i / REPART_G) * pg.nslices + b0 + i % REPART_G]) : 0u;
     };
+    /* RI adjacent items per lane and round (rounds of up to REPART_CAP
+       entries: half the rounds -- each a chain of index and code loads and
+       five barriers -- of one item per lane) */
+    constexpr uint32_t RI = 2u;
     for (;;) {
-        const uint32_t i = base + t;
-        const uint32_t c = item_count(i);
-        const uint32_t wi = wscan_incl32(c);
+        const uint32_t i0 = base + RI * t;
+        uint32_t c[RI], csum = 0;
+#pragma unroll
+        for (uint32_t r = 0; r < RI; r++) { c[r] = item_count(i0 + r); csum += c[r]; }
+        const uint32_t wi = wscan_incl32(csum);
         if (lane == 63) scn[wv] = wi;
         for (uint32_t p = t; p < gp; p += blockDim.x) hc[p] = 0;
         __syncthreads();
-        uint32_t before = 0;
+        uint32_t before = wi - csum;
         for (uint32_t w = 0; w < wv; w++) before += scn[w];
-        /* the leading items whose runs fit (item `base`'s always does) */
-        const bool take = i < nitems && before + wi <= REPART_CAP;
-        const uint32_t ntake = (uint32_t)__syncthreads_count(take);
-        /* the item's first pieces stay in registers from the count to the
+        /* the leading items whose runs fit (item `base`'s always does: a
+           run holds at most one batch) */
+        bool take[RI];
+        uint32_t nt = 0;
+#pragma unroll
+        for (uint32_t r = 0; r < RI; r++) {
+            before += c[r];
+            take[r] = i0 + r < nitems && before <= REPART_CAP;
+            nt += take[r] ? 1u : 0u;
+        }
+        const uint32_t ntake = (uint32_t)__syncthreads_count(nt >= 1u) + (uint32_t)__syncthreads_count(nt >= 2u);
+        /* the items' first pieces stay in registers from the count to the
            placement (one read of the codes per round, not two) */
-        const uint32_t sl = i % REPART_G;
-        const uint32_t ie = take ? pg.idx[(size_t)(i / REPART_G) * pg.nslices + b0 + sl] : PART_NO_RUN;
-        /* (an empty run -- PART_NO_RUN, count 0 -- reads nothing) */
-        const uint64_t s0 = (uint64_t)(i / REPART_G) * pg.batch + (ie == PART_NO_RUN ? 0u : ie >> 16);
-        const uint64_t s1 = s0 + (ie == PART_NO_RUN ? 0u : c);
-        const uint64_t q0 = s0 >> 2, q1 = (s1 + 3) >> 2;
-        uint4 pv[5];
+        uint64_t s0[RI], s1[RI];
+        uint4 pv[RI][5];
 #pragma unroll
-        for (uint32_t u = 0; u < 5u; u++) pv[u] = q0 + u < q1 ? g4[q0 + u] : make_uint4(0, 0, 0, 0);
+        for (uint32_t r = 0; r < RI; r++) {
+            const uint32_t i = i0 + r;
+            const uint32_t ie = take[r] ? pg.idx[(size_t)(i / REPART_G) * pg.nslices + b0 + i % REPART_G] : PART_NO_RUN;
+            /* (an empty run -- PART_NO_RUN, count 0 -- reads nothing) */
+            s0[r] = (uint64_t)(i / REPART_G) * pg.batch + (ie == PART_NO_RUN ? 0u : ie >> 16);
+            s1[r] = s0[r] + (ie == PART_NO_RUN ? 0u : c[r]);
+            const uint64_t q0 = s0[r] >> 2, q1 = (s1[r] + 3) >> 2;
+#pragma unroll
+            for (uint32_t u = 0; u < 5u; u++) pv[r][u] = q0 + u < q1 ? g4[q0 + u] : make_uint4(0, 0, 0, 0);
+        }
         auto codes = [&](auto &&f) {
-            auto piece = [&](const uint4 &v, uint64_t q) {
-                const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-                for (int h = 0; h < 4; h++)
-                    if (q * 4 + h >= s0 && q * 4 + h < s1) f(sl * np + (w4[h] >> 15), w4[h]);
-            };
+            for (uint32_t r = 0; r < RI; r++) {
+                const uint32_t sl = (i0 + r) % REPART_G;
+                const uint64_t a0 = s0[r], a1 = s1[r], q0 = a0 >> 2, q1 = (a1 + 3) >> 2;
+                auto piece = [&](const uint4 &v, uint64_t q) {
+                    const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-            for (uint32_t u = 0; u < 5u; u++)
-                if (q0 + u < q1) piece(pv[u], q0 + u);
-            for (uint64_t q = q0 + 5u; q < q1; q++) piece(g4[q], q);
+                    for (int h = 0; h < 4; h++)
+                        if (q * 4 + h >= a0 && q * 4 + h < a1) f(sl * np + (w4[h] >> 15), w4[h]);
+                };
+#pragma unroll
+                for (uint32_t u = 0; u < 5u; u++)
+                    if (q0 + u < q1) piece(pv[r][u], q0 + u);
+                for (uint64_t q = q0 + 5u; q < q1; q++) piece(g4[q], q);
+            }
         };
         codes([&](uint32_t p, uint32_t) { atomicAdd(&hc[p], 1u); });
         __syncthreads();
@@ -5842,8 +5909,15 @@ static int sparse_finish(fk_engine *e, int32_t seq) {
         HIPCHK(hipFuncSetAttribute((const void *)k_sp_emit, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     }
     DevScratch acc, bh, ctr;
-    if (!acc.alloc(FKS_ACC_N * sizeof(unsigned long long)) || !bh.alloc((size_t)nbk * 8) || !ctr.alloc(16))
+    if (!acc.alloc(FKS_ACC_N * sizeof(unsigned long long)) || !bh.alloc((size_t)nbk * 8) || !ctr.alloc(24))
         return FK_E_OOM;
+    /* a keys pass claims its output in SP_CHUNKs per wave: at most one
+       chunk's worth of pads per wave of every emit launch */
+    uint64_t pad_max = 0;
+    for (const auto &sg : e->spsegs)
+        if (sg.nranges)
+            pad_max += std::max<uint64_t>(1, std::min<uint64_t>((sg.nranges + SP_WAVES - 1) / SP_WAVES, (uint64_t)e->cus * 8)) *
+                       SP_WAVES * SP_CHUNK;
     unsigned long long *dacc = acc.as<unsigned long long>();
     unsigned long long *nctr = ctr.as<unsigned long long>();
     HIPCHK(hipMemsetAsync(dacc, 0, FKS_ACC_N * sizeof(unsigned long long), e->stream));
@@ -5973,17 +6047,19 @@ static int sparse_finish(fk_engine *e, int32_t seq) {
             if (fks_dense_runs(&e->fks, em.dense, nd, em.lo, k, e->stream, dacc, out_k, out_c, &nw)) return FK_E_HIP;
         } else {
             if (ps.n) {
-                int rc = sp_ensure((void **)&e->d_emit, &e->emit_cap, std::max<uint64_t>(ps.n, std::min<uint64_t>(cap, wins)), 8);
+                int rc = sp_ensure((void **)&e->d_emit, &e->emit_cap,
+                                   std::max<uint64_t>(ps.n, std::min<uint64_t>(cap, wins)) + pad_max, 8);
                 if (rc) return rc;
             }
             em.mode = SP_KEYS;
             em.out = e->d_emit;
             em.nout = nctr;
-            em.out_cap = ps.n;
-            unsigned long long got[2] = {0, 0};
+            em.nreal = nctr + 2;
+            em.out_cap = ps.n + pad_max;
+            unsigned long long got[3] = {0, 0, 0};
             for (int attempt = 0; attempt < 2; attempt++) {
                 if (single && !shorts.alloc((scap + 1) * 8)) return FK_E_OOM;
-                HIPCHK(hipMemsetAsync(nctr, 0, 16, e->stream));
+                HIPCHK(hipMemsetAsync(nctr, 0, 24, e->stream));
                 em.shorts = single ? shorts.as<uint64_t>() : nullptr;   /* the single pass collects them */
                 em.nshort = nctr + 1;
                 em.short_cap = scap;
@@ -5995,13 +6071,16 @@ static int sparse_finish(fk_engine *e, int32_t seq) {
                 if (attempt) return FK_E_HIP;
                 scap = got[1];
             }
-            if (got[0] != ps.n) return FK_E_HIP;   /* the feed's (or the histogram's) count and the emit pass disagree */
+            /* the feed's (or the histogram's) count and the emit pass agree,
+               and the claimed slots (windows + pads) fit */
+            if (got[2] != ps.n || got[0] > em.out_cap) return FK_E_HIP;
             if (single) {
                 ns = got[1];
                 int rc = prep_shorts();
                 if (rc) return rc;
             }
-            if (fks_sort_runs(&e->fks, em.out, ps.n, k, e->stream, dacc, out_k, out_c, &nw)) return FK_E_HIP;
+            if (fks_sort_runs(&e->fks, em.out, got[0], k, e->stream, dacc, out_k, out_c, &nw, got[0] > got[2]))
+                return FK_E_HIP;
         }
         if (!nw) continue;
         if (e->sp_distinct + nw > e->spk_cap) return FK_E_HIP;   /* cannot happen: distinct <= windows */

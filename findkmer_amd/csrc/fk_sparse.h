@@ -26,10 +26,12 @@ enum { FKS_ACC_ROLL = 10, FKS_ACC_WPREFIX = 11, FKS_ACC_N = 40 };
 /* One key-range pass: sort and run-length encode the n window keys (bits
  * [0, 2k)) into out_keys (ascending distinct indices) and out_cnts (their u32
  * counts), *nw of them -- the caller's table storage, room for n; statistics,
- * rollover and prefix histogram accumulate into dacc.  Synchronises the
- * stream.  0 or -1 (HIP error / out of memory). */
+ * rollover and prefix histogram accumulate into dacc.  `pad`: some keys are
+ * the pad value 4^k (bit 2k, above every window key), sorted last and
+ * dropped as the final run (its key lands in out_keys[*nw]: room for one
+ * more).  Synchronises the stream.  0 or -1 (HIP error / out of memory). */
 int fks_sort_runs(FksState *st, uint64_t *keys, uint64_t n, int k, hipStream_t s, unsigned long long *dacc,
-                  uint64_t *out_keys, uint32_t *out_cnts, uint64_t *nw);
+                  uint64_t *out_keys, uint32_t *out_cnts, uint64_t *nw, bool pad = false);
 /* The same for a dense count table of keys [lo, lo + n) (room for its
  * nonzero entries). */
 int fks_dense_runs(FksState *st, unsigned long long *dense, uint64_t n, uint64_t lo, int k, hipStream_t s,

@@ -594,6 +594,19 @@ def test_cli_q0_warnings_interleave_like_reference(ingest, tmp_path):
     i = next((i for i in range(min(len(ref), len(ours))) if ours[i] != ref[i]), None)
     assert ours.startswith(ref), (i, ref[max(0, (i or 0) - 80):(i or 0) + 80], ours[max(0, (i or 0) - 80):(i or 0) + 80])
     assert len(ours) - len(ref) <= 4096   # the reference's lost stdout block at most
+    # what the reference lost is the end of our stdout alone (every warning
+    # precedes it): run ours again with the streams apart and check the tail
+    # byte for byte, so the final progress and "histogram creation" lines
+    # are verified in merged mode too
+    tail = ours[len(ref):]
+    if tail:
+        c = tmp_path / "c"
+        c.mkdir()
+        (c / "u.fa").write_bytes(data)
+        p = _run_cli(args, c, env)
+        assert p.returncode == 0
+        assert p.stdout.endswith(tail), (tail[-200:], p.stdout[-200:])
+        assert b"Unknown character" not in tail
 
 
 @pytest.mark.parametrize("k0,k1", [(5, 9), (15, 17)])
