@@ -2985,66 +2985,61 @@ k_repart(PartGeo pg, uint16_t *out, unsigned long long *alloc, PartMeta *meta) {
        part's segment written after the part's earlier rounds */
     uint32_t base = 0;
     __syncthreads();
-    auto item_count = [&](uint32_t i) -> uint32_t {
-        return i < nitems ? run_count(pg.idx[(size_t)(i / REPART_G) * pg.nslices + b0 + i % REPART_G]) : 0u;
+    /* one item per lane and round, software-pipelined: the next round's
+       items are known once this round's are taken, so their index words
+       load during this round's count and their first pieces during its
+       placement and write-out (each round was a chain of an index load, a
+       code load and five barriers: k_repart latency-bound) */
+    auto idx_word = [&](uint32_t i) -> uint32_t {
+        return i < nitems ? pg.idx[(size_t)(i / REPART_G) * pg.nslices + b0 + i % REPART_G] : PART_NO_RUN;
     };
-    /* RI adjacent items per lane and round (rounds of up to REPART_CAP
-       entries: half the rounds -- each a chain of index and code loads and
-       five barriers -- of one item per lane) */
-    constexpr uint32_t RI = 2u;
-    for (;;) {
-        const uint32_t i0 = base + RI * t;
-        uint32_t c[RI], csum = 0;
+    auto span = [&](uint32_t i, uint32_t e, uint64_t &s0, uint64_t &s1) {
+        /* (an empty run -- PART_NO_RUN, count 0 -- reads nothing) */
+        s0 = (uint64_t)(i / REPART_G) * pg.batch + (e == PART_NO_RUN ? 0u : e >> 16);
+        s1 = s0 + run_count(e);
+    };
+    auto load5 = [&](uint64_t s0, uint64_t s1, uint4 *v) {
+        const uint64_t q0 = s0 >> 2, q1 = (s1 + 3) >> 2;
 #pragma unroll
-        for (uint32_t r = 0; r < RI; r++) { c[r] = item_count(i0 + r); csum += c[r]; }
-        const uint32_t wi = wscan_incl32(csum);
+        for (uint32_t u = 0; u < 5u; u++) v[u] = q0 + u < q1 ? g4[q0 + u] : make_uint4(0, 0, 0, 0);
+    };
+    uint32_t ie = idx_word(base + t);
+    uint4 pv[5];
+    {
+        uint64_t a0, a1;
+        span(base + t, ie, a0, a1);
+        load5(a0, a1, pv);
+    }
+    for (;;) {
+        const uint32_t i = base + t;
+        const uint32_t c = run_count(ie);
+        const uint32_t wi = wscan_incl32(c);
         if (lane == 63) scn[wv] = wi;
         for (uint32_t p = t; p < gp; p += blockDim.x) hc[p] = 0;
         __syncthreads();
-        uint32_t before = wi - csum;
+        uint32_t before = 0;
         for (uint32_t w = 0; w < wv; w++) before += scn[w];
         /* the leading items whose runs fit (item `base`'s always does: a
            run holds at most one batch) */
-        bool take[RI];
-        uint32_t nt = 0;
-#pragma unroll
-        for (uint32_t r = 0; r < RI; r++) {
-            before += c[r];
-            take[r] = i0 + r < nitems && before <= REPART_CAP;
-            nt += take[r] ? 1u : 0u;
-        }
-        const uint32_t ntake = (uint32_t)__syncthreads_count(nt >= 1u) + (uint32_t)__syncthreads_count(nt >= 2u);
-        /* the items' first pieces stay in registers from the count to the
-           placement (one read of the codes per round, not two) */
-        uint64_t s0[RI], s1[RI];
-        uint4 pv[RI][5];
-#pragma unroll
-        for (uint32_t r = 0; r < RI; r++) {
-            const uint32_t i = i0 + r;
-            const uint32_t ie = take[r] ? pg.idx[(size_t)(i / REPART_G) * pg.nslices + b0 + i % REPART_G] : PART_NO_RUN;
-            /* (an empty run -- PART_NO_RUN, count 0 -- reads nothing) */
-            s0[r] = (uint64_t)(i / REPART_G) * pg.batch + (ie == PART_NO_RUN ? 0u : ie >> 16);
-            s1[r] = s0[r] + (ie == PART_NO_RUN ? 0u : c[r]);
-            const uint64_t q0 = s0[r] >> 2, q1 = (s1[r] + 3) >> 2;
-#pragma unroll
-            for (uint32_t u = 0; u < 5u; u++) pv[r][u] = q0 + u < q1 ? g4[q0 + u] : make_uint4(0, 0, 0, 0);
-        }
+        const bool take = i < nitems && before + wi <= REPART_CAP;
+        const uint32_t ntake = (uint32_t)__syncthreads_count(take);
+        const uint32_t nbase = base + ntake;
+        const uint32_t ien = idx_word(nbase + t);   /* the next round's item */
+        uint64_t s0, s1;
+        span(i, take ? ie : PART_NO_RUN, s0, s1);
+        const uint32_t sl = i % REPART_G;
+        const uint64_t q0 = s0 >> 2, q1 = (s1 + 3) >> 2;
         auto codes = [&](auto &&f) {
+            auto piece = [&](const uint4 &v, uint64_t q) {
+                const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-            for (uint32_t r = 0; r < RI; r++) {
-                const uint32_t sl = (i0 + r) % REPART_G;
-                const uint64_t a0 = s0[r], a1 = s1[r], q0 = a0 >> 2, q1 = (a1 + 3) >> 2;
-                auto piece = [&](const uint4 &v, uint64_t q) {
-                    const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+                for (int h = 0; h < 4; h++)
+                    if (q * 4 + h >= s0 && q * 4 + h < s1) f(sl * np + (w4[h] >> 15), w4[h]);
+            };
 #pragma unroll
-                    for (int h = 0; h < 4; h++)
-                        if (q * 4 + h >= a0 && q * 4 + h < a1) f(sl * np + (w4[h] >> 15), w4[h]);
-                };
-#pragma unroll
-                for (uint32_t u = 0; u < 5u; u++)
-                    if (q0 + u < q1) piece(pv[r][u], q0 + u);
-                for (uint64_t q = q0 + 5u; q < q1; q++) piece(g4[q], q);
-            }
+            for (uint32_t u = 0; u < 5u; u++)
+                if (q0 + u < q1) piece(pv[u], q0 + u);
+            for (uint64_t q = q0 + 5u; q < q1; q++) piece(g4[q], q);
         };
         codes([&](uint32_t p, uint32_t) { atomicAdd(&hc[p], 1u); });
         __syncthreads();
@@ -3063,6 +3058,13 @@ k_repart(PartGeo pg, uint16_t *out, unsigned long long *alloc, PartMeta *meta) {
             const uint32_t at = atomicAdd(&cur[p], 1u);
             rbuf[at] = (uint16_t)(v & 0x7FFFu);
         });
+        /* the next round's first pieces (this round's are consumed) */
+        {
+            uint64_t a0, a1;
+            span(nbase + t, ien, a0, a1);
+            load5(a0, a1, pv);
+        }
+        ie = ien;
         __syncthreads();
         /* a wave per part: consecutive entries to consecutive 2-B slots */
         for (uint32_t p = wv; p < gp; p += 16u) {
@@ -3072,7 +3074,7 @@ k_repart(PartGeo pg, uint16_t *out, unsigned long long *alloc, PartMeta *meta) {
         }
         __syncthreads();
         for (uint32_t p = t; p < gp; p += blockDim.x) wr[p] += hc[p];
-        base += ntake;
+        base = nbase;
         if (base >= nitems || ntake == 0) break;
         __syncthreads();
     }
