@@ -1761,6 +1761,7 @@ struct SpEmit {
     unsigned long long *nshort;
     uint64_t short_cap;
     uint64_t *out;                  /* SP_KEYS */
+    uint32_t *out32;                /* ... a pass spanning <= 2^32 keys: key - lo as 32 bits instead (or nullptr) */
     unsigned long long *nout;       /* ... slots claimed (whole SP_CHUNKs) */
     uint64_t out_cap;
     unsigned long long *nreal;      /* ... windows written (the rest of the claimed slots: SP_PAD) */
@@ -1801,12 +1802,22 @@ __device__ __forceinline__ void sp_advance(SpOut &o, uint32_t tot, uint64_t nb, 
     else o.fill += tot;
     o.real += tot;
 }
-/* the end of the wave's walk: pad its chunk, count its windows */
+/* one window key to its slot (a 32-bit pass: relative to lo) */
+__device__ __forceinline__ void sp_put(const SpEmit &em, uint64_t at, uint64_t v) {
+    if (at >= em.out_cap) return;
+    if (em.out32) em.out32[at] = (uint32_t)(v - em.lo);
+    else em.out[at] = v;
+}
+/* the end of the wave's walk: pad its chunk (4^k, or 0xFFFFFFFF in a
+   32-bit pass), count its windows */
 __device__ __forceinline__ void sp_close(const SpEmit &em, const SpOut &o, uint64_t pad) {
     const uint32_t lane = threadIdx.x & 63;
     if (o.fill < SP_CHUNK)
-        for (uint32_t i = o.fill + lane; i < SP_CHUNK; i += 64u)
-            if (o.base + i < em.out_cap) em.out[o.base + i] = pad;
+        for (uint32_t i = o.fill + lane; i < SP_CHUNK; i += 64u) {
+            if (o.base + i >= em.out_cap) continue;
+            if (em.out32) em.out32[o.base + i] = 0xFFFFFFFFu;
+            else em.out[o.base + i] = pad;
+        }
     if (lane == 0 && o.real) atomicAdd(em.nreal, (unsigned long long)o.real);
 }
 
@@ -1852,8 +1863,7 @@ __device__ __forceinline__ void sp_fast_emit(const SpEmit &em, const Emit &fe, u
             const bool m = v >= em.lo && v < em.hi;
             const uint64_t bal = __ballot(m);
             if (m) {
-                const uint64_t at = sp_slot_at(so, cur, nb, rem, run + (uint64_t)__popcll(bal & ((1ull << lane) - 1ull)));
-                if (at < em.out_cap) em.out[at] = v;
+                sp_put(em, sp_slot_at(so, cur, nb, rem, run + (uint64_t)__popcll(bal & ((1ull << lane) - 1ull))), v);
             }
             run += (uint64_t)__popcll(bal);
         }
@@ -1952,8 +1962,7 @@ k_sp_emit(const uint8_t *buf, uint64_t len, int k, uint64_t maskk, const XState 
                         const bool m = v >= em.lo && v < em.hi;
                         const uint64_t bal = __ballot(m);
                         if (m) {
-                            const uint64_t at = sp_slot_at(so, cur, nb, rem, run + (uint64_t)__popcll(bal & ((1ull << lane) - 1ull)));
-                            if (at < em.out_cap) em.out[at] = v;
+                            sp_put(em, sp_slot_at(so, cur, nb, rem, run + (uint64_t)__popcll(bal & ((1ull << lane) - 1ull))), v);
                         }
                         run += (uint64_t)__popcll(bal);
                     }
@@ -6019,7 +6028,12 @@ static int sparse_finish(fk_engine *e, int32_t seq) {
             if (hb[b] > cap) { passes.push_back({b, b + 1, hb[b], true}); b++; continue; }
             uint32_t b1 = b;
             uint64_t n = 0;
-            while (b1 < nbk && hb[b1] <= cap && n + hb[b1] <= cap) n += hb[b1++];
+            /* k = 17 (2^34 keys): passes of at most 2^32 keys sort 32-bit
+               keys (half the bytes); 4 such spans cover the key space, as
+               many passes as a 10 G-base input needs anyway */
+            while (b1 < nbk && hb[b1] <= cap && n + hb[b1] <= cap &&
+                   (k != 17 || ((uint64_t)(b1 + 1 - b) << shift) <= (1ull << 32)))
+                n += hb[b1++];
             passes.push_back({b, b1, n, false});
             b = b1;
         }
@@ -6055,6 +6069,8 @@ static int sparse_finish(fk_engine *e, int32_t seq) {
             }
             em.mode = SP_KEYS;
             em.out = e->d_emit;
+            const bool rel32 = em.hi - em.lo <= (1ull << 32);
+            em.out32 = rel32 ? reinterpret_cast<uint32_t *>(e->d_emit) : nullptr;
             em.nout = nctr;
             em.nreal = nctr + 2;
             em.out_cap = ps.n + pad_max;
@@ -6081,7 +6097,9 @@ static int sparse_finish(fk_engine *e, int32_t seq) {
                 int rc = prep_shorts();
                 if (rc) return rc;
             }
-            if (fks_sort_runs(&e->fks, em.out, got[0], k, e->stream, dacc, out_k, out_c, &nw, got[0] > got[2]))
+            if (rel32 ? fks_sort_runs32(&e->fks, em.out32, got[0], em.lo, got[0] - got[2], k, e->stream, dacc, out_k,
+                                        out_c, &nw)
+                      : fks_sort_runs(&e->fks, em.out, got[0], k, e->stream, dacc, out_k, out_c, &nw, got[0] > got[2]))
                 return FK_E_HIP;
         }
         if (!nw) continue;
