@@ -3095,7 +3095,8 @@ k_count_parts(PartGeo pg, const uint16_t *in, const PartMeta *meta, uint32_t *ta
     extern __shared__ uint32_t slice[];
     const uint32_t np = 1u << pg.split;
     const uint32_t b = blockIdx.x / np, part = blockIdx.x % np;
-    for (uint32_t i = threadIdx.x; i < (1u << 15); i += blockDim.x) slice[i] = 0;
+    for (uint32_t i = threadIdx.x; i < (1u << 13); i += blockDim.x)
+        reinterpret_cast<uint4 *>(slice)[i] = make_uint4(0, 0, 0, 0);
     __syncthreads();
     const PartMeta m = meta[blockIdx.x];
     const uint4 *g4 = reinterpret_cast<const uint4 *>(in + m.off);   /* 16-B aligned: off % 8 == 0 */
@@ -3124,17 +3125,22 @@ k_count_parts(PartGeo pg, const uint16_t *in, const PartMeta *meta, uint32_t *ta
         /* a lane's bins i = lane + 1024 j all end in the same base (sigma
            maps digits one by one, and i & 3 = lane & 3): its sum is its
            last-base marginal */
+        /* four bins per lane: kernel bins 4m + d land at reference index
+           sigma(base | 4m) + sigma(d), i.e. the last digits 0 1 3 2 (sigma
+           maps digit by digit): one 16-B store */
         uint32_t dist = 0;
-        unsigned long long sum = 0;
-        for (uint32_t i = threadIdx.x; i < (1u << 15); i += 1024u) {
-            const uint32_t v = slice[i];
-            table[fk_sigma(base | i)] = v;
-            dist += v != 0;
-            sum += v;
+        unsigned long long last[4] = {0, 0, 0, 0};
+        const uint4 *s4 = reinterpret_cast<const uint4 *>(slice);
+        uint4 *t4 = reinterpret_cast<uint4 *>(table);
+        for (uint32_t m = threadIdx.x; m < (1u << 13); m += 1024u) {
+            const uint4 q = s4[m];
+            const uint4 o = make_uint4(q.x, q.y, q.w, q.z);
+            t4[fk_sigma(base | ((uint64_t)m << 2)) >> 2] = o;
+            dist += (o.x != 0) + (o.y != 0) + (o.z != 0) + (o.w != 0);
+            last[0] += o.x; last[1] += o.y; last[2] += o.z; last[3] += o.w;
         }
-        const uint32_t ld = (uint32_t)(fk_sigma((uint64_t)(threadIdx.x & 3u)) & 3u);
-        unsigned long long v10[6] = {dist, sum, ld == 0 ? sum : 0ull, ld == 1 ? sum : 0ull,
-                                     ld == 2 ? sum : 0ull, ld == 3 ? sum : 0ull};
+        const unsigned long long sum = last[0] + last[1] + last[2] + last[3];
+        unsigned long long v10[6] = {dist, sum, last[0], last[1], last[2], last[3]};
 #pragma unroll
         for (int q = 0; q < 6; q++) v10[q] = wsum64(v10[q]);
         /* the wave sums in the bins' LDS, once every lane has read its bins
