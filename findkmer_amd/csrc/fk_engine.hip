@@ -595,6 +595,8 @@ __device__ __forceinline__ bool tile_finish(const Ctx &cx, const uint32_t x[8], 
             em->AC = AC; em->A2 = A2; em->BC = BC; em->B2 = B2;
             em->h0 = h0; em->h1 = h1; em->deep = deep;
             if (deep) cnt.win_u += nsym;
+        } else if (HM == H_SPARSE) {   /* the sparse feed's counters (k_redo mode 2): windows, no slots */
+            if (deep) cnt.win_u += nsym;
         } else if (HM == H_NONE) {
         } else if (deep) {
             half_windows<HM>(cx, AC, A2, h0, weight);
@@ -1008,7 +1010,10 @@ template <int HM>
 __device__ __forceinline__ void do_tile(const Ctx &cx, const uint32_t w[8], int64_t toff, uint32_t tile_off,
                                         bool full, DState &st, Facts &f, Counters &cnt, uint32_t weight,
                                         bool mixed) {
-    if (HM != H_SPARSE && full && st.hdr == 0 && tile_fast<true, HM, true>(cx, w, st, f, cnt, weight)) return;
+    /* (H_SPARSE: only when counting, without slots -- the sparse feed's
+       counters; k_sp_emit takes fast tiles itself) */
+    if ((HM != H_SPARSE || !cx.slots) && full && st.hdr == 0 && tile_fast<true, HM, true>(cx, w, st, f, cnt, weight))
+        return;
     bool plain;
     if (HM != H_SPARSE && full && mixed && tile_mixed<HM>(cx, w, tile_off, st, f, cnt, weight, plain)) return;
     const int lane = threadIdx.x & 63;
