@@ -1769,7 +1769,7 @@ struct SpEmit {
     uint32_t *out32;                /* ... a pass spanning <= 2^32 keys: key - lo as 32 bits instead (or nullptr) */
     unsigned long long *nout;       /* ... slots claimed (whole SP_CHUNKs) */
     uint64_t out_cap;
-    unsigned long long *nreal;      /* ... windows written (the rest of the claimed slots: SP_PAD) */
+    unsigned long long *nreal;      /* ... windows written (the rest of the claimed slots: pads) */
     unsigned long long *dense;      /* SP_DENSE: count of key lo + i */
 };
 enum { SP_HIST = 1, SP_KEYS = 2, SP_DENSE = 3 };
@@ -1777,8 +1777,8 @@ enum { SP_HIST = 1, SP_KEYS = 2, SP_DENSE = 3 };
 #define SP_BUCKET_BITS 12u
 /* SP_KEYS output: each wave claims SP_CHUNK slots at a time from the pass's
    counter and fills them in order; the unfilled end of its last chunk holds
-   SP_PAD (4^k: above every key, so the sort puts the pads last and the
-   run-length encode leaves them as one final run).  Round 4: one claim per
+   pads (4^k - 1, the largest key -- 0xFFFFFFFF in a 32-bit pass -- so the
+   sort puts them last, and their number is taken off the last run).  Round 4: one claim per
    tile and wave -- 5 M same-address atomics per 10 GB pass -- made each keys
    pass take 60 ms against 10 ms for the histogram pass of the same walk. */
 #define SP_CHUNK 8192u
@@ -1813,7 +1813,7 @@ __device__ __forceinline__ void sp_put(const SpEmit &em, uint64_t at, uint64_t v
     if (em.out32) em.out32[at] = (uint32_t)(v - em.lo);
     else em.out[at] = v;
 }
-/* the end of the wave's walk: pad its chunk (4^k, or 0xFFFFFFFF in a
+/* the end of the wave's walk: pad its chunk (4^k - 1, or 0xFFFFFFFF in a
    32-bit pass), count its windows */
 __device__ __forceinline__ void sp_close(const SpEmit &em, const SpOut &o, uint64_t pad) {
     const uint32_t lane = threadIdx.x & 63;
@@ -1992,7 +1992,7 @@ k_sp_emit(const uint8_t *buf, uint64_t len, int k, uint64_t maskk, const XState 
             }
         }
     }
-    if (em.mode == SP_KEYS) sp_close(em, so, 1ull << (2 * k));
+    if (em.mode == SP_KEYS) sp_close(em, so, (1ull << (2 * k)) - 1);
     if (em.mode == SP_HIST) {
         __syncthreads();
         for (uint32_t i = threadIdx.x; i < em.nbuckets; i += blockDim.x)
@@ -6114,7 +6114,7 @@ static int sparse_finish(fk_engine *e, int32_t seq) {
             }
             if (rel32 ? fks_sort_runs32(&e->fks, em.out32, got[0], em.lo, got[0] - got[2], k, e->stream, dacc, out_k,
                                         out_c, &nw)
-                      : fks_sort_runs(&e->fks, em.out, got[0], k, e->stream, dacc, out_k, out_c, &nw, got[0] > got[2]))
+                      : fks_sort_runs(&e->fks, em.out, got[0], k, e->stream, dacc, out_k, out_c, &nw, got[0] - got[2]))
                 return FK_E_HIP;
         }
         if (!nw) continue;

@@ -27,12 +27,13 @@ enum { FKS_ACC_ROLL = 10, FKS_ACC_WPREFIX = 11, FKS_ACC_N = 40 };
 /* One key-range pass: sort and run-length encode the n window keys (bits
  * [0, 2k)) into out_keys (ascending distinct indices) and out_cnts (their u32
  * counts), *nw of them -- the caller's table storage, room for n; statistics,
- * rollover and prefix histogram accumulate into dacc.  `pad`: some keys are
- * the pad value 4^k (bit 2k, above every window key), sorted last and
- * dropped as the final run (its key lands in out_keys[*nw]: room for one
- * more).  Synchronises the stream.  0 or -1 (HIP error / out of memory). */
+ * rollover and prefix histogram accumulate into dacc.  `npads` of the keys
+ * are the pad 4^k - 1 (the largest key: sorted last, with the real key
+ * 4^k - 1 if any), taken off the last run's count (the run is dropped when
+ * nothing else is in it).  Synchronises the stream.  0 or -1 (HIP error /
+ * out of memory). */
 int fks_sort_runs(FksState *st, uint64_t *keys, uint64_t n, int k, hipStream_t s, unsigned long long *dacc,
-                  uint64_t *out_keys, uint32_t *out_cnts, uint64_t *nw, bool pad = false);
+                  uint64_t *out_keys, uint32_t *out_cnts, uint64_t *nw, uint64_t npads = 0);
 /* The same for a pass whose keys span at most 2^32 (lo <= key < lo + 2^32),
  * emitted as 32-bit keys - lo: half the bytes sorted.  `npads` of the keys
  * are the pad 0xFFFFFFFF, sorted last together with any real key lo +

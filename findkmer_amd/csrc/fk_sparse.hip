@@ -190,13 +190,13 @@ static int runs_stats(FksState *st, uint64_t nw, int k, hipStream_t s, unsigned 
 }
 
 int fks_sort_runs(FksState *st, uint64_t *keys, uint64_t n, int k, hipStream_t s, unsigned long long *dacc,
-                  uint64_t *out_keys, uint32_t *out_cnts, uint64_t *nw, bool pad) {
+                  uint64_t *out_keys, uint32_t *out_cnts, uint64_t *nw, uint64_t npads) {
     *nw = 0;
     if (n == 0) return 0;
     if (ensure((void **)&st->sorted, &st->sorted_cap, n * 8) || ensure((void **)&st->c64, &st->c64_cap, n * 8) ||
         ensure((void **)&st->small, &st->small_cap, 64 * sizeof(unsigned long long)))
         return -1;
-    const int bits = 2 * k + (pad ? 1 : 0);   /* the pads' bit 2k */
+    const int bits = 2 * k;
     size_t tb = 0, tb2 = 0;
     CK(rocprim::radix_sort_keys(nullptr, tb, keys, st->sorted, n, 0, bits, s));
     CK(rocprim::run_length_encode(nullptr, tb2, st->sorted, n, out_keys, st->c64, st->small, s));
@@ -208,7 +208,20 @@ int fks_sort_runs(FksState *st, uint64_t *keys, uint64_t n, int k, hipStream_t s
     unsigned long long runs = 0;
     CK(hipMemcpyAsync(&runs, st->small, sizeof runs, hipMemcpyDeviceToHost, s));
     CK(hipStreamSynchronize(s));
-    if (pad && runs) runs--;   /* the pads' run, last */
+    if (npads && runs) {
+        /* the pads (4^k - 1, the largest key) are the last run, with the
+           real key 4^k - 1 if the pass has it: take them off its count */
+        uint64_t last = 0;
+        CK(hipMemcpyAsync(&last, st->c64 + (runs - 1), sizeof last, hipMemcpyDeviceToHost, s));
+        CK(hipStreamSynchronize(s));
+        if (last <= npads) {
+            runs--;
+        } else {
+            last -= npads;
+            CK(hipMemcpyAsync(st->c64 + (runs - 1), &last, sizeof last, hipMemcpyHostToDevice, s));
+            CK(hipStreamSynchronize(s));
+        }
+    }
     *nw = runs;
     return runs_stats(st, runs, k, s, dacc, out_keys, out_cnts);
 }
