@@ -2,7 +2,7 @@
 """bench.py — k-mer scan throughput on MI355X (BASELINE.json metric).
 
 Headline workload (BASELINE.json configs[2], the largest single-GPU config):
-k=11 over a 10 G-base synthetic genome per GPU — 80-column FASTA (one
+k=11 over a 10 G-base synthetic genome — 80-column FASTA (one
 ">synthetic" header, ≈1.0125e10 bytes), an 'N' run break every 1.5 Gbases
 (chromosomes), generated in HBM before the timed region.  One step = one pass
 of the hot path over the batch: reset, the engine's feed (k_part +
@@ -13,11 +13,14 @@ The same line carries the north-star gate as a sub-record ("north_star"):
 k=6 over a 10 G-base pure-ACGT genome (1.5-Gbase chromosomes), with its own
 value, ms_per_step and roofline (k_count).
 
-With --gpus N (one process per GPU, torch.distributed over RCCL) each rank
-owns the next 10 G-base shard of one N x 10 G-base stream (weak scaling): the
-shard entry state is stitched and the count tables merged onto rank 0 inside
-the library (findkmer_amd/dist.py, fk_engine_shard_exchange) -- the path's
-real exchange steps.
+With --gpus N (one process per GPU, torch.distributed over RCCL; without a
+launcher `python bench.py --gpus N` starts torch.distributed.run itself as a
+child process) the headline is BASELINE.json configs[3]: the same 10 G-base
+genome cut into N shards (strong scaling).  Each shard's entry state is
+stitched and the count tables merged inside the library
+(findkmer_amd/dist.py, fk_engine_shard_exchange) -- the path's real exchange
+steps.  A "weak_scaling" sub-record gives every rank a whole 10 G-base shard
+of an N x 10 G-base stream.
 
 Prints ONE JSON line on rank 0 (contract in the task statement): value =
 bases/s over all ranks, "roofline" for the dominant kernel (HIP events on the
@@ -27,6 +30,7 @@ binary on a bounded sample, rank 0 at N=1 only) and "cpu_baseline_multicore"
 """
 import argparse
 import json
+import math
 import os
 import subprocess
 import sys
@@ -48,7 +52,10 @@ def parse(argv=None):
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--k", type=int, default=11)
-    ap.add_argument("--bases", type=int, default=10_000_000_000, help="bases per GPU")
+    ap.add_argument("--bases", type=int, default=10_000_000_000,
+                    help="bases of the headline stream, split over the --gpus ranks (strong scaling)")
+    ap.add_argument("--weak-bases", type=int, default=10_000_000_000,
+                    help="N > 1 sub-record: this many bases per GPU (weak scaling; 0 = skip)")
     ap.add_argument("--fasta-line", type=int, default=80, help="80 = FASTA (configs[2]); 0 = pure ACGT stream")
     ap.add_argument("--seed", type=int, default=2)
     ap.add_argument("--chrom", type=int, default=CHROM,
@@ -292,8 +299,9 @@ def measure(ctx, k, n, L, seed, chrom, steps, warmup, verify=False):
     rec = {
         "value": world * n / (dt / steps),
         "ms_per_step": ms_step,
-        "workload": (f"k={k} over a {n / 1e9:g} G-base synthetic "
-                     + ("ACGT stream" if L == 0 else f"FASTA genome ({L}-col lines)") + " per GPU"
+        "workload": (f"k={k} over a {world * n / 1e9:g} G-base synthetic "
+                     + ("ACGT stream" if L == 0 else f"FASTA genome ({L}-col lines)")
+                     + (f" cut into {world} shards of {n / 1e9:g} G bases, one per GPU" if world > 1 else "")
                      + (f", {args.chrom / 1e9:g} G-base chromosomes" if chrom_on else ", one run")),
         "k": k, "bases_per_gpu": n, "input_bytes_per_gpu": nbytes,
         "roofline": {
@@ -370,8 +378,53 @@ def verify_single(ctx, k, n, L, seed, chrom, merged, last):
     return out
 
 
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launcher_cmd(gpus, argv, port):
+    """`python bench.py --gpus N` without a launcher: the torchrun command
+    that runs this same script with the same arguments, one rank per GPU."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(gpus),
+            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + list(argv)
+
+
+def world_check(gpus, env):
+    """None when this process may run the bench as is; "spawn" when it must
+    launch --gpus ranks itself (no WORLD_SIZE, N > 1); else the error text of
+    a launcher world that is not the one --gpus asks for."""
+    if "WORLD_SIZE" not in env:
+        return "spawn" if gpus > 1 else None
+    world = int(env["WORLD_SIZE"])
+    if world != gpus:
+        return f"bench.py: WORLD_SIZE={world} but --gpus {gpus}: the line would claim a world that did not run"
+    return None
+
+
+def shard_bases(total, world, L):
+    """Bases per rank when the `total`-base stream is cut into `world` equal
+    shards (configs[3]: one 10 G-base genome split N ways).  A shard is a
+    whole number of generator words (32 bases) and FASTA lines."""
+    if world == 1:
+        return total
+    unit = 32 if L <= 0 else 32 * L // math.gcd(32, L)
+    return total // world // unit * unit
+
+
 def main():
     args = parse()
+    chk = world_check(args.gpus, os.environ)
+    if chk == "spawn":
+        # before torch or any GPU call: this process only waits for the ranks
+        # (a child process, never an exec, from a process that touched no GPU)
+        p = subprocess.run(launcher_cmd(args.gpus, sys.argv[1:], free_port()))
+        sys.exit(p.returncode)
+    if chk is not None:
+        print(chk, file=sys.stderr)
+        sys.exit(2)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -392,8 +445,21 @@ def main():
     coll_dev = "cuda" if args.dist_backend == "nccl" else "cpu"
     ctx = Ctx(args, world, rank, local, dist, coll_dev)
 
-    head = measure(ctx, args.k, args.bases, args.fasta_line, args.seed, args.chrom, args.steps, args.warmup,
+    # the headline: one `args.bases`-base stream, cut into `world` shards
+    # (strong scaling; at N > 1 this is configs[3]: the 10 G-base genome of
+    # configs[2] split N ways, counted by N ranks, merged)
+    n = shard_bases(args.bases, world, args.fasta_line)
+    head = measure(ctx, args.k, n, args.fasta_line, args.seed, args.chrom, args.steps, args.warmup,
                    verify=args.verify_single)
+    if head.get("transport") == "rccl-native":
+        # the world this line claims is the world RCCL itself reports
+        assert head["rccl"]["nranks"] == world, (head["rccl"], world)
+    weak = None
+    if world > 1 and args.weak_bases > 0:
+        # sub-record: every rank a whole `weak_bases` shard of an N x as long
+        # stream (per-GPU work fixed as N grows)
+        weak = measure(ctx, args.k, shard_bases(args.weak_bases, 1, args.fasta_line), args.fasta_line, args.seed,
+                       args.chrom, args.steps, args.warmup)
     ns = None
     if args.north_star_bases > 0:
         ns = measure(ctx, 6, args.north_star_bases, 0, 1, CHROM, args.steps, args.warmup)
@@ -401,8 +467,8 @@ def main():
 
     cfg_tag = {(11, 80, 10_000_000_000): " (BASELINE.json configs[2])",
                (6, 0, 1_000_000_000): " (BASELINE.json configs[1])"}.get((args.k, args.fasta_line, args.bases), "")
-    if world > 1 and (args.k, args.fasta_line) == (11, 80):
-        cfg_tag = f" (BASELINE.json configs[3] layout, weak scaling: {args.bases / 1e9:g} G bases per GPU)"
+    if world > 1 and (args.k, args.fasta_line, args.bases) == (11, 80, 10_000_000_000):
+        cfg_tag = f" (BASELINE.json configs[3]: the configs[2] genome split over {world} GPUs)"
     out = {
         "metric": METRIC,
         "value": head["value"],
@@ -412,13 +478,15 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": head["ms_per_step"],
         "higher_is_better": True,
-        "scaling": "weak",
+        # the stream is the same `--bases` bases whatever N is
+        "scaling": "strong",
         "vs_baseline": None,
         "dtype": "u8",
         "data": "synthetic (splitmix64 uniform ACGT genome, generated in HBM)",
         "config": {
             "workload": head["workload"] + cfg_tag,
-            "k": args.k, "bases_per_gpu": args.bases, "input_bytes_per_gpu": head["input_bytes_per_gpu"],
+            "k": args.k, "total_bases": n * world, "bases_per_gpu": n,
+            "input_bytes_per_gpu": head["input_bytes_per_gpu"],
             "parallelism": f"shard{world}",
         },
         "roofline": head["roofline"],
@@ -426,6 +494,11 @@ def main():
     for key in ("phase_ms_per_step", "exchange", "transport", "rccl", "verify"):
         if key in head:
             out[key] = head[key]
+    if weak is not None:
+        out["weak_scaling"] = {key: weak[key] for key in ("workload", "value", "ms_per_step", "bases_per_gpu",
+                                                           "roofline", "exchange", "transport", "rccl",
+                                                           "phase_ms_per_step") if key in weak}
+        out["weak_scaling"]["scaling"] = "weak"
     if ns is not None:
         out["north_star"] = {key: ns[key] for key in ("workload", "gate", "value", "ms_per_step", "roofline",
                                                        "exchange", "transport") if key in ns}

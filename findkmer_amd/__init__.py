@@ -29,6 +29,7 @@ FK_E_UNTERMINATED_HEADER = -7
 FK_E_ROLLOVER = -8
 FK_E_STATE = -9
 FK_E_SUMMARY = -12
+FK_E_INTERNAL = -13
 FK_K_MAX_DENSE = 16
 FK_PACK_COUNTERS = 14     # include/findkmer.h: fk_engine_shard_pack's counters
 FK_PACK_ROW_WORDS = 32    # ... and its rows (uint32 words)

@@ -215,6 +215,15 @@ struct ShardSum {
 };
 
 /* Per-feed results, fetched with one device-to-host copy. */
+/* DevRes::fault: what a device-side bound check of the k = 15, 16 path saw.
+   LIST: more general-tile windows than the fresh table's list holds (they
+   were not written; the segment is counted again without the list).  PARTS /
+   META: k_repart's output region or a part's stream past the parts buffer
+   (nothing was written past it; the feed fails with FK_E_INTERNAL). */
+#define FK_FAULT_LIST 1u
+#define FK_FAULT_PARTS 2u
+#define FK_FAULT_META 4u
+
 struct DevRes {
     unsigned long long tstat[10];   /* k_table_stats: distinct, sum, last[4], first[4] */
     unsigned long long acc[16];     /* k_table_stats: snapshot of the accumulators */
@@ -223,7 +232,7 @@ struct DevRes {
     uint32_t redo_n;                /* ranges re-counted */
     uint32_t need;                  /* one-pass k_count: 0 = complete, else ONE_* bits
                                        (the host runs the rest of the path) */
-    uint32_t pad;
+    uint32_t fault;                 /* k_table_stats: FK_FAULT_* bits of the counted segment */
     ShardSum shard;                 /* one-pass shard feeds */
     uint32_t pad2;
     uint32_t seq;                   /* host copy: written last (feed sequence number) */

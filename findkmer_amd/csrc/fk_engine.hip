@@ -2937,7 +2937,8 @@ struct PartMeta {
 static_assert(16u * FK_TILE_BYTES <= REPART_CAP, "a C32 row's run fits one k_repart round");
 
 __global__ void __launch_bounds__(1024)
-k_repart(PartGeo pg, uint16_t *out, unsigned long long *alloc, PartMeta *meta) {
+k_repart(PartGeo pg, uint16_t *out, unsigned long long *alloc, PartMeta *meta, uint64_t cap,
+         unsigned long long *err) {
     /* per (slice in the group, part): entries, round count / offset /
        cursor, written so far, stream start */
     __shared__ uint32_t cnt[REPART_GP], hc[REPART_GP], ho[REPART_GP], cur[REPART_GP], wr[REPART_GP];
@@ -2992,10 +2993,16 @@ k_repart(PartGeo pg, uint16_t *out, unsigned long long *alloc, PartMeta *meta) {
         unsigned long long g0 = 0;
         if (lane == 0) g0 = atomicAdd(alloc, (unsigned long long)carry);
         g0 = rdlane64(g0, 0);
+        /* bound check: the group's region inside the `cap` codes of `out`
+           (the host sizes it for every entry a segment can hold); past it,
+           nothing is written, the parts read as empty and the feed fails */
+        const bool over = g0 + carry > cap;
+        if (over && lane == 0) atomicOr(err, (unsigned long long)FK_FAULT_PARTS);
         for (uint32_t p = lane; p < gp; p += 64u) {
-            poff[p] = g0 + ho[p];
+            poff[p] = over ? ~0ull : g0 + ho[p];
             wr[p] = 0;
-            meta[(size_t)b0 * np + p] = PartMeta{g0 + ho[p], cnt[p], 0};   /* slice-major: (b0 + p / np) * np + p % np */
+            /* slice-major: (b0 + p / np) * np + p % np */
+            meta[(size_t)b0 * np + p] = over ? PartMeta{0, 0, 0} : PartMeta{g0 + ho[p], cnt[p], 0};
         }
     }
     /* pass B: rounds of whole runs (a lane per item) holding up to
@@ -3086,7 +3093,7 @@ k_repart(PartGeo pg, uint16_t *out, unsigned long long *alloc, PartMeta *meta) {
         __syncthreads();
         /* a wave per part: consecutive entries to consecutive 2-B slots */
         for (uint32_t p = wv; p < gp; p += 16u) {
-            const uint32_t n = hc[p], o = ho[p];
+            const uint32_t n = poff[p] == ~0ull ? 0u : hc[p], o = ho[p];
             uint16_t *dst = out + poff[p] + wr[p];
             for (uint32_t j = lane; j < n; j += 64u) dst[j] = rbuf[o + j];
         }
@@ -3100,14 +3107,20 @@ k_repart(PartGeo pg, uint16_t *out, unsigned long long *alloc, PartMeta *meta) {
 
 /* one block per part: its stream into 2^15 LDS bins, then into the table */
 __global__ void __launch_bounds__(1024)
-k_count_parts(PartGeo pg, const uint16_t *in, const PartMeta *meta, uint32_t *table) {
+k_count_parts(PartGeo pg, const uint16_t *in, const PartMeta *meta, uint32_t *table, uint64_t cap,
+              unsigned long long *err) {
     extern __shared__ uint32_t slice[];
     const uint32_t np = 1u << pg.split;
     const uint32_t b = blockIdx.x / np, part = blockIdx.x % np;
     for (uint32_t i = threadIdx.x; i < (1u << 13); i += blockDim.x)
         reinterpret_cast<uint4 *>(slice)[i] = make_uint4(0, 0, 0, 0);
     __syncthreads();
-    const PartMeta m = meta[blockIdx.x];
+    PartMeta m = meta[blockIdx.x];
+    if (m.off + m.n > cap) {   /* bound check: a stream past the parts buffer is not read */
+        if (threadIdx.x == 0) atomicOr(err, (unsigned long long)FK_FAULT_META);
+        m.n = 0;
+        m.off = 0;
+    }
     const uint4 *g4 = reinterpret_cast<const uint4 *>(in + m.off);   /* 16-B aligned: off % 8 == 0 */
     const uint32_t nq = (m.n + 7u) >> 3;
     for (uint32_t q = threadIdx.x; q < nq; q += blockDim.x) {
@@ -3640,8 +3653,15 @@ __global__ void __launch_bounds__(256)
 k_table_stats(uint32_t *table, uint64_t n, int k, DevRes *res,
               unsigned long long *acc, unsigned long long *facc, int fresh, DevRes *host_res, uint32_t *done,
               uint32_t seq, uint32_t *subs, int nsub, unsigned long long *part, int split,
-              const unsigned long long *fz, const uint32_t *glist) {
+              const unsigned long long *fz, const uint32_t *glist, const unsigned long long *perr) {
     if (blockIdx.x == 0) {
+        if (threadIdx.x == 0) {
+            /* the segment's bound checks (k = 15, 16): the general tiles'
+               list past its capacity, k_repart / k_count_parts past theirs */
+            uint32_t f = perr ? (uint32_t)*perr : 0u;
+            if (glist && glist[0] > glist[1]) f |= FK_FAULT_LIST;
+            res->fault = f;
+        }
         /* the feed's counters (facc, zero between feeds) join the engine's */
         if (threadIdx.x < ACC_N) {
             unsigned long long v = fresh ? 0ull : acc[threadIdx.x];
@@ -4106,6 +4126,10 @@ struct fk_engine {
     uint64_t glist_cap = 0;
     unsigned long long *d_fz = nullptr;       /* ... and its statistics from k_count_parts (FZ_SLOTS x 10) */
     bool fz_ready = false;                    /* the next launch_table_stats may take them */
+    unsigned long long *d_perr = nullptr;     /* k = 15, 16: k_repart / k_count_parts bound-check bits */
+    bool perr_live = false;                   /* ... set by the last launch_part, for the next statistics */
+    uint64_t glist_force = 0;                 /* FINDKMER_TUNE glist_cap=N: the list's capacity (tests) */
+    uint64_t list_recounts = 0;               /* segments counted again after the list overflowed */
     bool seg_snap = false;                    /* d_snap holds them as before the current segment */
     uint32_t *d_snap = nullptr;
     uint64_t snap_cap = 0;
@@ -4178,6 +4202,7 @@ extern "C" const char *fk_strerror(int s) {
     case FK_E_IO: return "I/O error";
     case FK_E_RCCL: return "collective failed";
     case FK_E_SUMMARY: return "shard summary does not apply to this state (exchange the full summaries)";
+    case FK_E_INTERNAL: return "device-side bound check failed (counts not valid)";
     default: return "unknown error";
     }
 }
@@ -4234,6 +4259,10 @@ static int zero_all(fk_engine *e) {
     e->sp_done = false;
     e->unknown_bytes.clear();
     e->unknown_pos.clear();
+    /* statistics a fresh two-level count left for the next launch_table_stats
+       belong to the count this reset discards */
+    e->fz_ready = false;
+    e->perr_live = false;
     return FK_OK;
 }
 
@@ -4331,6 +4360,7 @@ extern "C" int fk_engine_create(int k, const fk_opts *opts, fk_engine **out) {
     if (!e->no_mixed) e->general_tiles = 2;
     if (tune_knob("pairs_kmax", &kv)) e->part_pairs_kmax = (int)std::min<uint64_t>(kv, 12u);
     if (tune_knob("part_general", &kv)) e->part_general = (uint32_t)kv;
+    if (tune_knob("glist_cap", &kv)) e->glist_force = kv;
     if (tune_knob("events", &kv)) e->timing = kv != 0;
     if (tune_knob("static_pct", &kv)) e->static_pct = (uint32_t)std::min<uint64_t>(100u, std::max<uint64_t>(1u, kv));
     if (tune_knob("dyn_min_chunks", &kv)) e->dyn_min_chunks = kv;
@@ -4631,10 +4661,13 @@ static int launch_table_stats(fk_engine *e, bool zero_first, hipEvent_t stop = n
     if (++e->res_seq == 0) e->res_seq = 1;
     const bool fz = e->fz_ready;   /* only for the statistics right after a fresh two-level count */
     e->fz_ready = false;
+    unsigned long long *perr = e->perr_live ? e->d_perr : nullptr;
+    e->perr_live = false;
     hipExtLaunchKernelGGL(k_table_stats, dim3(gd), dim3(256), 0, e->stream, nullptr, split ? nullptr : stop, 0,
                           e->d_table, e->nbins, e->k, e->d_res, e->d_acc, e->d_facc, fresh ? 1 : 0, e->h_res_dev,
                           e->d_done, e->res_seq, e->d_sub, (subs && e->d_sub) ? FK_SUBTABLES : 0, e->d_tpart, split,
-                          fz ? (const unsigned long long *)e->d_fz : nullptr, fz ? (const uint32_t *)e->d_glist : nullptr);
+                          fz ? (const unsigned long long *)e->d_fz : nullptr, fz ? (const uint32_t *)e->d_glist : nullptr,
+                          (const unsigned long long *)perr);
     HIPCHK(hipGetLastError());
     if (split) {
         hipExtLaunchKernelGGL(k_table_final, dim3(1), dim3(256), 0, e->stream, nullptr, stop, 0, e->d_res,
@@ -4690,12 +4723,16 @@ static int launch_part(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t l
     pg.kk = (uint32_t)k;
     e->fz_ready = false;
     if (c32 && e->tab_fresh && !exact) {
-        /* the general tiles' windows go to a list (hist_add): at most 4
-           general tiles per range (one comment line or run break and the
-           bases-only tiles around it in k_part, the ragged last tile in
-           k_part<RES>; tile_mixed takes every other tile outside the int32
-           zone, which tab_fresh excludes) */
-        const uint64_t cap = (uint64_t)g.nranges * 4u * FK_TILE_BYTES + 4096u;
+        /* the general tiles' windows go to a list (hist_add): at most
+           part_general + 3 general tiles per range (the comment lines or run
+           breaks k_part takes and the bases-only tiles around them, the
+           ragged last tile in k_part<RES>; tile_mixed takes every other tile
+           outside the int32 zone, which tab_fresh excludes, and with
+           no_mixed there is no fresh table).  Should a segment hold more,
+           hist_add drops what does not fit and k_table_stats flags it
+           (FK_FAULT_LIST): resolve_and_fetch counts the segment again */
+        uint64_t cap = (uint64_t)g.nranges * (e->part_general + 3u) * FK_TILE_BYTES + 4096u;
+        if (e->glist_force) cap = e->glist_force;
         if (cap + 2 > e->glist_cap) {
             hipFree(e->d_glist);
             e->d_glist = nullptr;
@@ -4809,12 +4846,17 @@ static int launch_part(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t l
             hipMalloc(&e->d_pmeta, (size_t)2048 * REPART_MAXP * sizeof(PartMeta) + 64) != hipSuccess)
             return FK_E_OOM;
         PartMeta *meta = static_cast<PartMeta *>(e->d_pmeta);
+        /* [0]: the output claim, [1]: bound-check bits (DevRes::fault) */
         unsigned long long *alloc = reinterpret_cast<unsigned long long *>(meta + (size_t)2048 * REPART_MAXP);
-        HIPCHK(hipMemsetAsync(alloc, 0, sizeof(unsigned long long), e->stream));
-        hipLaunchKernelGGL(k_repart, dim3(pg.nslices / REPART_G), dim3(1024), 0, e->stream, pg, e->d_parts, alloc, meta);
+        e->d_perr = alloc + 1;
+        e->perr_live = true;
+        HIPCHK(hipMemsetAsync(alloc, 0, 2 * sizeof(unsigned long long), e->stream));
+        hipLaunchKernelGGL(k_repart, dim3(pg.nslices / REPART_G), dim3(1024), 0, e->stream, pg, e->d_parts, alloc, meta,
+                           (uint64_t)e->parts_cap, e->d_perr);
         HIPCHK(hipGetLastError());
         hipLaunchKernelGGL(k_count_parts, dim3((unsigned)nparts), dim3(1024), (size_t)1 << 17, e->stream, pg,
-                           (const uint16_t *)e->d_parts, (const PartMeta *)meta, e->d_table);
+                           (const uint16_t *)e->d_parts, (const PartMeta *)meta, e->d_table, (uint64_t)e->parts_cap,
+                           e->d_perr);
         if (pg.glist) {
             HIPCHK(hipGetLastError());
             hipLaunchKernelGGL(k_list_add, dim3((unsigned)e->cus * 4), dim3(256), 0, e->stream, pg.glist, e->d_table,
@@ -4845,6 +4887,30 @@ static int launch_part(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t l
 static bool int32_zone_possible(const fk_engine *e, uint64_t len) {
     const uint64_t r0 = e->state.hdr ? 0 : (uint64_t)(uint32_t)e->state.R;
     return r0 + len + FK_CHUNK_BYTES > 0x7FFFFFFFull;
+}
+
+/* What the segment's device-side bound checks saw (DevRes::fault, k = 15,
+   16).  A general-tile list that overflowed left windows out of a fresh
+   table: the segment is the first since the reset (tab_fresh), so it is
+   counted again over a zeroed table from the exact range states k_scan just
+   computed, its general tiles' windows added by global atomics (launch_part
+   with `exact` keeps no list).  Any other bit fails the feed. */
+static int check_fault(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t lo, const Geo &g) {
+    const uint32_t f = e->last.fault;
+    if (!f) return FK_OK;
+    if (f != FK_FAULT_LIST || !e->seg_clean) return FK_E_INTERNAL;
+    HIPCHK(hipMemsetAsync(e->d_table, 0, e->nbins * sizeof(uint32_t), e->stream));
+    if (e->nshort) HIPCHK(hipMemsetAsync(e->d_short, 0, e->nshort * sizeof(uint32_t), e->stream));
+    /* (k_table_stats cleared the feed counters when it folded them) */
+    int rc = launch_part(e, buf, len, lo, g, 1, e->d_rtrue);
+    if (rc) return rc;
+    rc = launch_table_stats(e, false, tev(e, 2), true, true);   /* fresh: the counters start over */
+    if (rc) return rc;
+    rc = wait_results(e);
+    if (rc) return rc;
+    e->list_recounts++;
+    e->redo += g.nranges;   /* (fk_result.redo_chunks: every range of the segment again) */
+    return e->last.fault ? FK_E_INTERNAL : FK_OK;
 }
 
 static int resolve_and_fetch(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t lo, const Geo &g) {
@@ -4911,6 +4977,7 @@ static int resolve_and_fetch(fk_engine *e, const uint8_t *buf, uint64_t len, int
             if (rc) return rc;
             rc = wait_results(e);
             if (rc) return rc;
+            if (e->last.fault) return FK_E_INTERNAL;   /* (no list: exact states) */
             e->stats_valid = true;
             e->redo += n;
             return FK_OK;
@@ -4922,8 +4989,10 @@ static int resolve_and_fetch(fk_engine *e, const uint8_t *buf, uint64_t len, int
     if (rc) return rc;
     rc = wait_results(e);
     if (rc) return rc;
-    e->stats_valid = true;
     e->redo += e->last.redo_n;
+    rc = check_fault(e, buf, len, lo, g);
+    if (rc) return rc;
+    e->stats_valid = true;
     return FK_OK;
 }
 
@@ -5033,7 +5102,7 @@ static int count_segment(fk_engine *e, const uint8_t *dbuf, uint64_t len, int64_
        table, so the reset leaves the table out (16 GiB at k = 16); not where
        the int32 seqSize zone can be reached (its recount needs the zeroed
        table, and k_part<RES> counts such tiles with the general walk) */
-    e->tab_fresh = e->part && e->k >= 15 && e->zero_pending && !int32_zone_possible(e, len);
+    e->tab_fresh = e->part && e->k >= 15 && e->zero_pending && !e->no_mixed && !int32_zone_possible(e, len);
     if (fresh) {
         e->zero_pending = false;
     } else {
@@ -6498,6 +6567,9 @@ __global__ void k_add_acc(unsigned long long *dst, const unsigned long long *src
 extern "C" int fk_engine_merge_from(fk_engine *dst, fk_engine *src) {
     if (!dst || !src || dst->k != src->k) return FK_E_INVALID;
     if (dst->sparse || src->sparse) return FK_E_INVALID;
+    /* both keep short-walk counts (nodeCounter) or neither: a merge would
+       otherwise peer-copy from a null d_short */
+    if (dst->nshort != src->nshort) return FK_E_INVALID;
     int rc = set_dev(src);
     if (rc) return rc;
     HIPCHK(hipStreamSynchronize(src->stream));

@@ -60,9 +60,13 @@ enum {
     FK_E_STATE = -9,            /* API called out of order */
     FK_E_IO = -10,              /* host file I/O failed */
     FK_E_RCCL = -11,            /* a collective failed */
-    FK_E_SUMMARY = -12          /* a compact shard summary does not apply to
+    FK_E_SUMMARY = -12,         /* a compact shard summary does not apply to
                                    this entering state: exchange the full ones
                                    (fk_engine_summary_full) */
+    FK_E_INTERNAL = -13         /* a device-side bound check failed: a kernel's
+                                   output would have passed the end of its
+                                   buffer.  Nothing was written past it; the
+                                   feed's counts are not valid (reset) */
 };
 
 /* Scan state carried between byte ranges (exact; used for streaming feeds and

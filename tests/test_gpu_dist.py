@@ -32,7 +32,8 @@ def test_two_rank_shards_gloo(k, fasta, chrom):
     out = _torchrun(2, 29600 + k + chrom % 97, os.path.join(REPO, "bench.py"),
                     ["--gpus", "2", "--steps", "2", "--warmup", "1", "--no-cpu-baseline", "--dist-backend", "gloo",
                      "--north-star-bases", "0",
-                     "--k", str(k), "--fasta-line", str(fasta), "--bases", "12800000", "--chrom", str(chrom)])
+                     "--k", str(k), "--fasta-line", str(fasta), "--bases", "25600000", "--chrom", str(chrom),
+                     "--weak-bases", "0"])
     assert out["n_gpus"] == 2 and out["value"] > 0
     # pure ACGT shards with a halo that fixes the state: one all-reduce
     assert out["exchange"] == ("fast" if k <= 7 else "stitched")
@@ -48,9 +49,31 @@ def test_eight_rank_shards_gloo(k, fasta):
     out = _torchrun(8, 29650 + k, os.path.join(REPO, "bench.py"),
                     ["--gpus", "8", "--steps", "2", "--warmup", "1", "--no-cpu-baseline", "--dist-backend", "gloo",
                      "--north-star-bases", "0",
-                     "--k", str(k), "--fasta-line", str(fasta), "--bases", "12800000", "--chrom", "40000000"])
+                     "--k", str(k), "--fasta-line", str(fasta), "--bases", "102400000", "--chrom", "40000000",
+                     "--weak-bases", "0"])
     assert out["n_gpus"] == 8 and out["value"] > 0
     assert out["exchange"] in (("fast", "stitched") if k <= 7 else ("stitched",))
+
+
+@pytest.mark.gpu
+def test_bench_gpus_flag_launches_the_ranks():
+    """`python bench.py --gpus 2` with no launcher (the driver's form): the
+    bench starts torch.distributed.run itself as a child process, two ranks
+    count the two halves of one stream (strong scaling), and the merged-count
+    guard holds; the weak sub-record gives each rank a whole shard"""
+    cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--dist-backend", "gloo",
+           "--steps", "2", "--warmup", "1", "--no-cpu-baseline", "--north-star-bases", "0",
+           "--k", "11", "--fasta-line", "80", "--bases", "25600000", "--weak-bases", "12800000",
+           "--chrom", "20000000"]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    p = subprocess.run(cmd, cwd=REPO, capture_output=True, text=True, timeout=600, env=env)
+    assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-4000:]
+    out = json.loads([l for l in p.stdout.splitlines() if l.startswith("{")][-1])
+    assert out["n_gpus"] == 2 and out["scaling"] == "strong" and out["value"] > 0
+    assert out["config"]["total_bases"] == 25_600_000 and out["config"]["bases_per_gpu"] == 12_800_000
+    assert out["exchange"] == "stitched"
+    w = out["weak_scaling"]
+    assert w["scaling"] == "weak" and w["bases_per_gpu"] == 12_800_000 and w["value"] > 0
 
 
 @pytest.mark.gpu
@@ -62,9 +85,11 @@ def test_configs3_eight_ranks_full_size():
     the merged table and every counter must equal it"""
     out = _torchrun(8, 29690, os.path.join(REPO, "bench.py"),
                     ["--gpus", "8", "--steps", "1", "--warmup", "0", "--no-cpu-baseline", "--dist-backend", "gloo",
-                     "--north-star-bases", "0", "--k", "11", "--fasta-line", "80", "--bases", "1250000000",
-                     "--verify-single"])
+                     "--north-star-bases", "0", "--k", "11", "--fasta-line", "80", "--bases", "10000000000",
+                     "--weak-bases", "0", "--verify-single"])
     assert out["n_gpus"] == 8 and out["exchange"] == "stitched"
+    assert out["scaling"] == "strong" and out["config"]["total_bases"] == 10_000_000_000
+    assert out["config"]["bases_per_gpu"] == 1_250_000_000
     v = out["verify"]
     assert v["table_equal"] and v["status"] == 0
     for key in ("windows", "valid_bases", "base_count", "depth1", "unknown_chars", "scanned_bytes",
@@ -117,13 +142,16 @@ def test_rccl_single_rank_merge(k, fast, eof_in, native):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("k,world,eof_in,nbytes", [(12, 2, -1, 3_000_000), (12, 8, 3, 3_000_000),
-                                                  (14, 8, -1, 2_000_000), (16, 2, -1, 1_000_000)])
+                                                  (14, 8, -1, 2_000_000), (16, 2, -1, 1_000_000),
+                                                  (16, 2, 0, 1_000_000), (15, 3, 1, 1_500_000)])
 def test_sharded_table_gloo_against_oracle(k, world, eof_in, nbytes):
     """k > 11: the merged table sharded over the ranks by its top index bits
     (rank r owns bins [r*4^k/G, (r+1)*4^k/G): the north star's "table shards
     by top bits"), gathered in rank order on rank 0 == the oracle's table
     (k = 14, 16: its sparse form); the counters, total and distinct bins
-    from the all-reduced limbs"""
+    from the all-reduced limbs.  eof_in >= 0 at k = 15, 16: the shards after
+    the 0xFF byte were counted into fresh tables and are then discarded (the
+    statistics that count left must not reach finish)"""
     out = _torchrun(world, 29750 + k + world + eof_in, os.path.join(REPO, "tests", "dist_worker.py"),
                     ["--k", str(k), "--eof-in", str(eof_in), "--shard-table", "1", "--bytes", str(nbytes)])
     assert out["table_equal"] and out["sharded"]

@@ -733,6 +733,29 @@ def _assert_same_sparse_view(data, k, feeds=None, want_nodes=True):
     assert (rg.unknown_chars, rg.scanned_bytes, rg.hit_eof_byte) == (r.unknown_chars, r.scanned_bytes, r.hit_eof_byte)
     if want_nodes:
         assert rg.nodes == r.nodes
+    return rg
+
+
+@pytest.mark.parametrize("k,tune", [(15, "glist_cap=1"), (16, "glist_cap=4096"), (15, "no_mixed=1"),
+                                    (16, "part_general=5")])
+def test_fresh_table_window_list_never_truncates(k, tune, monkeypatch):
+    """k = 15, 16 right after a reset: k_count_parts writes every bin (no
+    zeroing) and the general tiles' windows go to a list added afterwards.
+    A list forced tiny (glist_cap) overflows on header-dense input: the
+    overflow is flagged on the device (FK_FAULT_LIST) and the segment counted
+    again from its exact range states, never truncated.
+    no_mixed (no fresh table) and a larger part_general budget (the list's
+    capacity follows it) count exactly too"""
+    data = _dense_records(1717 + k, 3 << 20)
+    base = None
+    if tune.startswith("glist_cap"):
+        with fk.Engine(k) as e:   # the same feed with the list's own capacity
+            e.feed(np.frombuffer(data, dtype=np.uint8).copy())
+            base = e.finish(allow=(fk.FK_OK, fk.FK_E_UNTERMINATED_HEADER))[1].redo_chunks
+    monkeypatch.setenv("FINDKMER_TUNE", tune)
+    rg = _assert_same_sparse_view(data, k)
+    if base is not None:
+        assert rg.redo_chunks > base   # the whole segment was counted again
 
 
 @pytest.mark.parametrize("k", [15, 16])
