@@ -3,7 +3,8 @@
 #   python3 tools/profile_summary.py $OUT <tag> --k K --fasta-line L --input-bytes B
 # K, L, BASES, SEED select the workload (default: the bench's headline,
 # configs[2]: k=11 over 10 G bases of 80-column FASTA).  SQ=1 adds two SQ
-# counter passes (LDS / VALU / wait cycles).
+# counter passes (LDS / VALU / wait cycles); TRACE_ONLY=1 skips the PMC passes.
+# FINDKMER_LIB=build/exp/libfk_<name>.so profiles an experiment build.
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
@@ -18,6 +19,7 @@ run() {   # run <dir> <rocprofv3 options...>
 }
 run trace --kernel-trace --stats
 tail -1 $OUT/trace.log
+[ "${TRACE_ONLY:-0}" = 1 ] && { echo profile-done; exit 0; }
 run pmc1 --pmc FETCH_SIZE
 run pmc2 --pmc WRITE_SIZE
 if [ "${SQ:-0}" = 1 ]; then
