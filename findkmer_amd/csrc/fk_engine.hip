@@ -123,6 +123,18 @@ __device__ __forceinline__ uint32_t wscan_incl32(uint32_t v) {
     t = dpp_mov32<0x143>(v); if (lane >= 32) v += t;
     return v;
 }
+/* inclusive wave scan (max), the same DPP sequence */
+__device__ __forceinline__ uint32_t wscan_max32(uint32_t v) {
+    const uint32_t lane = threadIdx.x & 63, rl = lane & 15;
+    uint32_t t;
+    t = dpp_mov32<0x111>(v); if (rl >= 1) v = max(v, t);
+    t = dpp_mov32<0x112>(v); if (rl >= 2) v = max(v, t);
+    t = dpp_mov32<0x114>(v); if (rl >= 4) v = max(v, t);
+    t = dpp_mov32<0x118>(v); if (rl >= 8) v = max(v, t);
+    t = dpp_mov32<0x142>(v); if ((lane & 31) >= 16) v = max(v, t);
+    t = dpp_mov32<0x143>(v); if (lane >= 32) v = max(v, t);
+    return v;
+}
 struct OpAdd32 { __device__ uint32_t operator()(uint32_t a, uint32_t b) const { return a + b; } };
 struct OpMin32 { __device__ uint32_t operator()(uint32_t a, uint32_t b) const { return a < b ? a : b; } };
 __device__ __forceinline__ uint32_t wsum32(uint32_t v) { return wred32(v, OpAdd32{}); }
@@ -2070,8 +2082,14 @@ struct PartGeo {
     uint32_t rows;         /* rows in all: grid * rounds */
     uint32_t nslices;      /* a multiple of 8 */
     uint32_t sh;           /* slice index = code >> sh; stored code = code & (2^sh - 1) */
-    uint32_t npair;        /* pairs mode: the slices hold (k+1)-mer pairs (npair = nslices) and single
-                              k-mers x as the pair code x << 2 with PART_SINGLE set */
+    uint32_t npair;        /* pairs mode: slices [0, npair) hold (k+1)-mer pairs */
+    /* pairs mode, a single k-mer x (a '\n' half's slot 1): slice sbase + ((x << slsh) >> sh), stored
+       ((x << slsh) & lowm) | sflag.  2^15-bin slices: x filed under the pair code x << 2 with
+       PART_SINGLE set (sbase 0, slsh 2); 2^16-bin slices (W16, k_bucket16): the singles' own slices
+       [npair, npair + 4^k / 2^16) (sbase npair, slsh 0, sflag 0) */
+    uint32_t sbase, slsh, sflag;
+    uint32_t w16;          /* 2^16-bin slices counted in packed 16-bit LDS bins (k_bucket16): k = 11..14 */
+    uint32_t nbk;          /* W16: slices k_bucket16 counts ([0, nbk): the index row may be wider) */
     uint32_t *pairs;       /* pairs mode: 4^(k+1) pair bins (k_bucket_count -> k_pair_fold) */
     uint32_t *singles;     /* pairs mode: 4^k single k-mer bins */
     uint32_t nomix;        /* no_mixed: tiles the fast path cannot take go to tile_general */
@@ -2079,7 +2097,7 @@ struct PartGeo {
                               before k_part<RES> takes the rest */
     uint32_t stride;       /* index row stride: rows of both regions (k_part, then k_part<RES>) */
     uint32_t *flag;        /* [0] != 0: some range went to k_part<RES>, region 2 holds rows */
-    uint32_t split;        /* k = 14: a slice's 2^16 codes counted as two halves of 2^15 bins (0: one) */
+    uint32_t split;        /* k = 15, 16: a coarse slice holds 2^split parts of 2^15 bins */
     uint32_t *glist;       /* k = 15, 16 over a fresh table: the general tiles' windows (hist_add), or nullptr */
     unsigned long long *fz;/* ... and the table statistics k_count_parts takes of it: FZ_SLOTS x 10 partials */
     uint32_t kk;           /* k */
@@ -2093,9 +2111,13 @@ struct PartGeo {
  * two k-mers ending at slots (2j, 2j+1); without a real slot 0 the first one
  * is the single k-mer x at slot 1, filed under the pair code x << 2 (its
  * slice) with PART_SINGLE set in the stored low bits. */
+/* where a pairs-mode single k-mer goes (PartGeo::sbase, slsh, sflag) */
+struct SingleEnc {
+    uint32_t sbase, slsh, sflag;
+};
 template <bool PAIRS, bool MIX, typename F>
 __device__ __forceinline__ void part_entries(const Emit &em, uint32_t mk, uint32_t m1, uint32_t sh, uint32_t lowm,
-                                             uint32_t npair, F &&f) {
+                                             const SingleEnc &se, F &&f) {
     if (MIX && em.masked) {
         /* a mixed tile: only the slots in the mask end windows; a pair where
            both of its slots do, else the single k-mer of the one that does */
@@ -2112,8 +2134,8 @@ __device__ __forceinline__ void part_entries(const Emit &em, uint32_t mk, uint32
                         f(v >> sh, v & lowm);
                     } else if (two) {
                         const uint32_t s = 2u * (uint32_t)j + (two == 1u ? 1u : 0u);
-                        const uint32_t v = ((s < 15u ? __builtin_amdgcn_alignbit(C, S2, 2u * (15u - s)) : S2) & mk) << 2;
-                        f(v >> sh, (v & lowm) | PART_SINGLE);
+                        const uint32_t v = ((s < 15u ? __builtin_amdgcn_alignbit(C, S2, 2u * (15u - s)) : S2) & mk) << se.slsh;
+                        f(se.sbase + (v >> sh), (v & lowm) | se.sflag);
                     }
                 }
             } else {
@@ -2134,8 +2156,8 @@ __device__ __forceinline__ void part_entries(const Emit &em, uint32_t mk, uint32
         const bool skip0 = h ? em.h1 : em.h0;
         if (PAIRS) {
             const uint32_t v0 = __builtin_amdgcn_alignbit(C, S2, 28u);
-            const uint32_t c0 = skip0 ? (v0 & mk) << 2 : (v0 & m1);
-            f(c0 >> sh, (c0 & lowm) | (skip0 ? PART_SINGLE : 0u));
+            const uint32_t c0 = skip0 ? (v0 & mk) << se.slsh : (v0 & m1);
+            f((skip0 ? se.sbase : 0u) + (c0 >> sh), (c0 & lowm) | (skip0 ? se.sflag : 0u));
 #pragma unroll
             for (int j = 1; j < 8; j++) {
                 const uint32_t v = (j < 7 ? __builtin_amdgcn_alignbit(C, S2, 28u - 4u * (uint32_t)j) : S2) & m1;
@@ -2190,10 +2212,11 @@ __device__ __forceinline__ bool part_batch(const Ctx &cx, const PartGeo &pg, con
     const uint32_t t = threadIdx.x, lane = t & 63;
     const uint32_t mk = (uint32_t)cx.maskk, sh = pg.sh, lowm = (1u << sh) - 1u;
     const uint32_t m1 = (mk << 2) | 3u;
+    const SingleEnc se{pg.sbase, pg.slsh, pg.sflag};
     /* 1: slice histogram */
 #pragma unroll
     for (int i = 0; i < NT; i++)
-        if (haves[i]) part_entries<PAIRS, MIX>(es[i], mk, m1, sh, lowm, pg.npair, [&](uint32_t b, uint32_t) { atomicAdd(&hist[b], 1u); });
+        if (haves[i]) part_entries<PAIRS, MIX>(es[i], mk, m1, sh, lowm, se, [&](uint32_t b, uint32_t) { atomicAdd(&hist[b], 1u); });
     /* (the barrier also tells whether any wave has tiles left) */
     const bool any_more = __syncthreads_or(more);
     /* 2: exclusive scan of the slice counts, index row: wave 0 alone for up
@@ -2285,7 +2308,7 @@ __device__ __forceinline__ bool part_batch(const Ctx &cx, const PartGeo &pg, con
     for (int i = 0; i < NT; i++) {
         Emit f = es[i];
         asm volatile("" : "+v"(f.AC), "+v"(f.A2), "+v"(f.BC), "+v"(f.B2));
-        if (haves[i]) part_entries<PAIRS, MIX>(f, mk, m1, sh, lowm, pg.npair, place);
+        if (haves[i]) part_entries<PAIRS, MIX>(f, mk, m1, sh, lowm, se, place);
     }
     __syncthreads();
     /* 4: the sorted batch into its row's fixed slot (pg.batch entries: a
@@ -2327,12 +2350,13 @@ __device__ __forceinline__ bool part_batch(const Ctx &cx, const PartGeo &pg, con
    x at slot 1 of a '\n' half is the pair code x << 2 with PART_SINGLE) */
 template <bool PAIRS>
 __device__ __forceinline__ void part_entry(uint32_t C, uint32_t S2, bool skip0, int g, int j, uint32_t sh,
-                                           uint32_t wsl, uint32_t lowm, uint32_t &b, uint32_t *low) {
+                                           uint32_t wsl, uint32_t lowm, const SingleEnc &se, uint32_t &b,
+                                           uint32_t *low) {
     if (PAIRS) {
         const uint32_t v = j < 7 ? __builtin_amdgcn_alignbit(C, S2, 28u - 4u * (uint32_t)j) : S2;
-        if (j == 0 && skip0) {   /* (v & mk) << 2: its slice is v's bits [sh - 2, sh - 2 + wsl) */
-            b = __builtin_amdgcn_ubfe(v, sh - 2u, wsl);
-            if (low) *low = ((v << 2) & lowm) | PART_SINGLE;
+        if (j == 0 && skip0) {   /* x = v & mk, as (x << slsh): its slice is v's bits [sh - slsh, 2k) */
+            b = se.sbase + __builtin_amdgcn_ubfe(v, sh - se.slsh, wsl - 2u + se.slsh);
+            if (low) *low = ((v << se.slsh) & lowm) | se.sflag;
         } else {
             b = __builtin_amdgcn_ubfe(v, sh, wsl);
             if (low) *low = v & lowm;
@@ -2347,7 +2371,8 @@ __device__ __forceinline__ void part_entry(uint32_t C, uint32_t S2, bool skip0, 
 
 /* A fast tile's entries into the batch's slice histogram */
 template <bool PAIRS>
-__device__ __forceinline__ void part_hist8(const Emit &em, uint32_t sh, uint32_t wsl, uint32_t *hist) {
+__device__ __forceinline__ void part_hist8(const Emit &em, uint32_t sh, uint32_t wsl, const SingleEnc &se,
+                                           uint32_t *hist) {
 #pragma unroll
     for (int h = 0; h < 2; h++) {
         const uint32_t C = h ? em.BC : em.AC, S2 = h ? em.B2 : em.A2;
@@ -2358,7 +2383,7 @@ __device__ __forceinline__ void part_hist8(const Emit &em, uint32_t sh, uint32_t
             for (int j = 0; j < 8; j++) {
                 if (!PAIRS && g == 0 && j == 0 && skip0) continue;   /* slot 0 is not a window */
                 uint32_t b;
-                part_entry<PAIRS>(C, S2, skip0, g, j, sh, wsl, 0u, b, nullptr);
+                part_entry<PAIRS>(C, S2, skip0, g, j, sh, wsl, 0u, se, b, nullptr);
                 atomicAdd(&hist[b], 1u);
             }
     }
@@ -2373,7 +2398,7 @@ __device__ __forceinline__ void part_hist8(const Emit &em, uint32_t sh, uint32_t
 typedef __attribute__((address_space(3))) uint16_t lds_u16;
 template <bool PAIRS>
 __device__ __forceinline__ void part_place8(const Emit &em, uint32_t sh, uint32_t wsl, uint32_t lowm,
-                                            uint32_t *cur) {
+                                            const SingleEnc &se, uint32_t *cur) {
 #pragma unroll
     for (int h = 0; h < 2; h++) {
         const uint32_t C = h ? em.BC : em.AC, S2 = h ? em.B2 : em.A2;
@@ -2382,7 +2407,7 @@ __device__ __forceinline__ void part_place8(const Emit &em, uint32_t sh, uint32_
         for (int g = 0; g < (PAIRS ? 1 : 2); g++) {
             uint32_t b[8], low[8], p[8];
 #pragma unroll
-            for (int j = 0; j < 8; j++) part_entry<PAIRS>(C, S2, skip0, g, j, sh, wsl, lowm, b[j], &low[j]);
+            for (int j = 0; j < 8; j++) part_entry<PAIRS>(C, S2, skip0, g, j, sh, wsl, lowm, se, b[j], &low[j]);
 #pragma unroll
             for (int j = 0; j < 8; j++) {
                 if (!PAIRS && g == 0 && j == 0 && skip0) continue;   /* slot 0 is not a window */
@@ -2579,8 +2604,10 @@ k_part(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint
     /* KC: k as a compile-time constant (the headline k = 11), so that the
        slice and low-bit extracts fold into single bit-field ops */
     constexpr uint32_t KBC = KC ? (PAIRS ? KC + 1u : KC) : 0u;
+    /* (KC: 2^15-bin slices, singles filed under their pair code, PART_SINGLE) */
     const uint32_t shv = KC ? (2u * KBC - 6u < 15u ? 2u * KBC - 6u : 15u) : pg.sh;
     const uint32_t lowm = (1u << shv) - 1u;
+    const SingleEnc se = KC ? SingleEnc{0u, 2u, PART_SINGLE} : SingleEnc{pg.sbase, pg.slsh, pg.sflag};
     /* the batch's LDS byte address (the PIPE cursors hold LDS addresses) */
     const uint32_t ent_lds = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) CT *)ent;
     const uint32_t wsl = 2u * (KC ? KBC : (uint32_t)(PAIRS ? k + 1 : k)) - shv;   /* slice bits of a code */
@@ -2598,7 +2625,7 @@ k_part(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint
             old_ = stash[i_];                                                        \
             hold_ = have_stash[i_];                                                  \
         }                                                                            \
-        if (hold_) part_place8<PAIRS>(old_, shv, wsl, lowm, cur); \
+        if (hold_) part_place8<PAIRS>(old_, shv, wsl, lowm, se, cur); \
     }
 /* (a macro, not a lambda: the same body as an always-inline lambda called
    three times gave the compiler a different register allocation -- 107
@@ -2637,7 +2664,7 @@ k_part(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint
         FK_LOADP(X, t + 2);                                                          \
         if (PIPE) {   /* batch j+1's histogram, batch j's placement (see part_scan_w0) */ \
             const uint32_t ph_ = round % NT;                                         \
-            if (have) part_hist8<PAIRS>(em, shv, wsl, hist);                       \
+            if (have) part_hist8<PAIRS>(em, shv, wsl, se, hist);                   \
             if (!early) FK_PLACE_OLD();                                              \
             _Pragma("unroll") for (uint32_t i_ = 0; i_ < NT; i_++) if (ph_ == i_) {  \
                 stash[i_] = em;                                                      \
@@ -2662,7 +2689,7 @@ k_part(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint
                 if (!more_ || j_ + 1 >= pg.rounds) {                                 \
                     /* the last batch: placed, then written out */                  \
                     _Pragma("unroll") for (uint32_t i_ = 0; i_ < NT; i_++)           \
-                        if (have_stash[i_]) part_place8<PAIRS>(stash[i_], shv, wsl, lowm, cur); \
+                        if (have_stash[i_]) part_place8<PAIRS>(stash[i_], shv, wsl, lowm, se, cur); \
                     __syncthreads();                                                 \
                     part_writeout<W>(pg, row0 + j_, tot[j_ & 1u], (const uint16_t *)ent, threadIdx.x, PART_BLOCK_W(W)); \
                     round++;                                                         \
@@ -2756,43 +2783,30 @@ k_part(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint
 #endif
 /* MODE (a template parameter, so that the hot loop of the common k carries
    no test of it: a runtime flag there cost ~0.9 ms of a k=11 10 GB step):
-   BK_PLAIN 16-bit codes, one block per slice (and row group);
-   BK_SPLIT k = 14: a slice counted as 2^(pg.split) parts of 2^15 bins, one
-            block each, keeping only its part's codes; the parts of a slice
-            run on one XCD one after another, so all but the first read the
-            slice's codes from L2.  (Counting k = 15's 32-bit coarse slices
-            the same way, 16 parts each, took 21.7 ms per G-base; the second
-            partition level, k_repart, takes 16.3.) */
+   BK_PLAIN 16-bit codes, one block per slice (and row group).  (Round 4's
+            BK_SPLIT, k = 14 counted as two blocks per 2^16-bin slice that
+            each read all of its codes, is k_bucket16's now.) */
 /* BK_PAD: BK_PLAIN over padded runs (PART_PAD: a run starts on a 16-B
             piece, its index word holds that piece; only its last piece
             needs a mask) */
-enum { BK_PLAIN = 0, BK_SPLIT = 1, BK_PAD = 2 };
+enum { BK_PLAIN = 0, BK_PAD = 2 };
 template <int MODE>
 __global__ void __launch_bounds__(1024)
 k_bucket_count(PartGeo pg, uint32_t groups, uint32_t *table) {
     extern __shared__ uint32_t slice[];
-    constexpr bool PARTS = MODE == BK_SPLIT, PADDED = MODE == BK_PAD;
+    constexpr bool PADDED = MODE == BK_PAD;
     constexpr uint32_t CPP = 8u;   /* 16-bit codes per 16-B piece */
     constexpr uint32_t PSH = 3u;
-    const uint32_t binsh = PARTS ? 15u : pg.sh;
-    const uint32_t nb = 1u << binsh;
+    const uint32_t nb = 1u << pg.sh;
     /* pairs mode: the slice's 2^sh pair bins, then the 2^(sh-2) bins of the
        single k-mers filed under it (PART_SINGLE codes) */
     const uint32_t ns = pg.pairs ? nb >> 2 : 0u;
     /* consecutive slices on one XCD (blocks b, b + 8, .. share an XCD): the
        128-B line two neighbouring runs of a row share is fetched once into
        that XCD's L2 (k=11: 1 GB step 1.085 -> 1.065 ms, 10 GB 8.10 -> 8.04) */
-    uint32_t b, g, part = 0;
-    if (PARTS) {   /* (groups == 1, nslices a multiple of 8) */
-        const uint32_t j = blockIdx.x >> 3, np = 1u << pg.split;
-        part = j & (np - 1u);
-        b = (blockIdx.x & 7u) * (pg.nslices >> 3) + (j >> pg.split);
-        g = 0;
-    } else {
-        b = groups == 1 && (pg.nslices & 7u) == 0 ? (blockIdx.x & 7u) * (pg.nslices >> 3) + (blockIdx.x >> 3)
-                                                : blockIdx.x % pg.nslices;
-        g = blockIdx.x / pg.nslices;
-    }
+    const uint32_t b = groups == 1 && (pg.nslices & 7u) == 0 ? (blockIdx.x & 7u) * (pg.nslices >> 3) + (blockIdx.x >> 3)
+                                                             : blockIdx.x % pg.nslices;
+    const uint32_t g = blockIdx.x / pg.nslices;
     for (uint32_t i = threadIdx.x; i < nb + ns; i += blockDim.x) slice[i] = 0;
     __syncthreads();
     const uint32_t *ix = pg.idx + b;
@@ -2822,8 +2836,6 @@ k_bucket_count(PartGeo pg, uint32_t groups, uint32_t *table) {
             if (PADDED) {   /* the run starts on this lane's first piece: only its end bounds it */
                 const uint32_t a = c & PART_SINGLE ? nb + ((c & ~PART_SINGLE) >> 2) : c;
                 if ((uint32_t)h < nv) atomicAdd(&slice[a], 1u);
-            } else if (PARTS) {   /* this block's part of the slice */
-                if (at >= s0 && at < s1 && (c >> binsh) == part) atomicAdd(&slice[c & (nb - 1u)], 1u);
             } else {
                 const uint32_t a = c & PART_SINGLE ? nb + ((c & ~PART_SINGLE) >> 2) : c;
                 if (at >= s0 && at < s1) atomicAdd(&slice[a], 1u);
@@ -2881,7 +2893,7 @@ k_bucket_count(PartGeo pg, uint32_t groups, uint32_t *table) {
         }
         return;
     }
-    const uint64_t base = ((uint64_t)b << pg.sh) | ((uint64_t)part << binsh);
+    const uint64_t base = (uint64_t)b << pg.sh;
     if (groups != 1) {
         for (uint32_t i = threadIdx.x; i < nb; i += blockDim.x) {
             const uint32_t v = slice[i];
@@ -2904,6 +2916,197 @@ k_bucket_count(PartGeo pg, uint32_t groups, uint32_t *table) {
 #pragma unroll
         for (uint32_t j = 0; j < U; j++)
             if (v[j]) table[fk_sigma(base | (i0 + j * blockDim.x))] = o[j] + v[j];
+    }
+}
+
+/*
+ * W16 (k = 11..14): slices of 2^16 bins counted in 16-bit LDS bins, two per
+ * word (128 KiB for the whole slice).  Against 2^15-bin slices in 32-bit bins
+ * that halves the slices, so every run a block reads is twice as long (k =
+ * 11: ~240 codes, 480 B) and the reads of a run's partial first and last
+ * lines are half as many; k = 14 counts a slice in one block instead of two
+ * blocks that each read all of its codes.  A code c adds 1 << 16 (c & 1) to
+ * word c >> 1 (non-returning, as the 32-bit bins).  A 16-bit bin that wraps
+ * carries into its neighbour (low half) or out of the word (high half): both
+ * make the sum of the halves fall short of the codes counted, and nothing
+ * else does, so the block checks that sum against its exact count and, only
+ * if it fell short (a bin past 65535 codes in one slice: poly-A stretches),
+ * counts the slice again as two halves of 2^15 32-bit bins.  (Round 2 tried
+ * 16-bit bins with returning atomics to catch wraps as they happen: 20 %
+ * slower; the sum check costs one add per word.)
+ *
+ * Blocks: pairs mode puts the single k-mers (a '\n' half's slot 1) in their
+ * own slices [npair, nbk), lightly loaded: they come first, so the pair
+ * slices -- consecutive ones on one XCD, as k_bucket_count -- start at most
+ * one light block late.
+ */
+/* Every code of slice b's runs (index column ix) as f(code): QL lanes per
+   run reading 16-B pieces (QL x 16 B contiguous per request), ROWS rows per
+   lane group in flight with U pieces each, the next rows' index words loaded
+   with this iteration's codes (k_bucket_count's shape) */
+template <uint32_t QL, uint32_t ROWS, uint32_t U, bool PADDED, typename F>
+__device__ __forceinline__ void walk_runs(const PartGeo &pg, const uint32_t *ix, uint32_t nrows, F &&f) {
+    constexpr uint32_t CPP = 8u, PSH = 3u;
+    const uint4 *g4 = reinterpret_cast<const uint4 *>(pg.codes);
+    const uint32_t sub = threadIdx.x & (QL - 1u), groups = blockDim.x / QL;
+    auto add16 = [&](const uint4 &v, uint64_t q, uint64_t s0, uint64_t s1) {
+        const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+        const uint32_t nv = PADDED ? (uint32_t)min<uint64_t>(CPP, s1 - q * CPP) : 0u;
+#pragma unroll
+        for (int h = 0; h < (int)CPP; h++) {
+            const uint64_t at = q * CPP + h;
+            const uint32_t c = (w4[h >> 1] >> (16 * (h & 1))) & 0xFFFFu;
+            if (PADDED ? (uint32_t)h < nv : (at >= s0 && at < s1)) f(c);
+        }
+    };
+    uint32_t en[ROWS];
+    const uint32_t r00 = threadIdx.x / QL;
+#pragma unroll
+    for (uint32_t j = 0; j < ROWS; j++)
+        en[j] = r00 + j * groups < nrows ? ix[(size_t)(r00 + j * groups) * pg.nslices] : PART_NO_RUN;
+    for (uint32_t r = r00; r < nrows; r += ROWS * groups) {
+        uint32_t e[ROWS];
+#pragma unroll
+        for (uint32_t j = 0; j < ROWS; j++) e[j] = en[j];
+        const uint32_t rn = r + ROWS * groups;
+#pragma unroll
+        for (uint32_t j = 0; j < ROWS; j++)
+            en[j] = rn + j * groups < nrows ? ix[(size_t)(rn + j * groups) * pg.nslices] : PART_NO_RUN;
+        uint64_t s0[ROWS], s1[ROWS];
+        uint4 v[ROWS][U];
+#pragma unroll
+        for (uint32_t j = 0; j < ROWS; j++) {
+            s0[j] = (uint64_t)(r + j * groups) * pg.batch + (e[j] == PART_NO_RUN ? 0u : (e[j] >> 16) * (PADDED ? CPP : 1u));
+            s1[j] = s0[j] + run_count(e[j]);
+            const uint64_t q0 = (s0[j] >> PSH) + sub, q1 = (s1[j] + CPP - 1) >> PSH;
+#pragma unroll
+            for (uint32_t u = 0; u < U; u++) v[j][u] = q0 + QL * u < q1 ? g4[q0 + QL * u] : make_uint4(0, 0, 0, 0);
+        }
+#pragma unroll
+        for (uint32_t j = 0; j < ROWS; j++) {
+            const uint64_t q0 = (s0[j] >> PSH) + sub, q1 = (s1[j] + CPP - 1) >> PSH;
+#pragma unroll
+            for (uint32_t u = 0; u < U; u++)
+                if (q0 + QL * u < q1) add16(v[j][u], q0 + QL * u, s0[j], s1[j]);
+            for (uint64_t q = q0 + QL * U; q < q1; q += 4 * QL) {
+                uint4 w[4];
+#pragma unroll
+                for (uint32_t u = 0; u < 4; u++) w[u] = q + QL * u < q1 ? g4[q + QL * u] : make_uint4(0, 0, 0, 0);
+#pragma unroll
+                for (uint32_t u = 0; u < 4; u++)
+                    if (q + QL * u < q1) add16(w[u], q + QL * u, s0[j], s1[j]);
+            }
+        }
+    }
+}
+
+/* the heavy (pair or plain) slices' walk shape: 4 lanes per run, 2 rows x 5
+   pieces in flight (k_bucket_count's); the singles' slices hold a few codes
+   per run, so a lane per run and 4 rows in flight (their walk is a chain of
+   index and code loads: with the heavy shape the 64 single-slice blocks of
+   k = 11 took ~0.3 ms, which the pair slices' last blocks waited out) */
+/* W16 for k = 12, 13, 14 (1 G-base FASTA steps, round 5: k = 12 1.33 ->
+   1.22 ms, k = 13 2.12 -> 1.84 ms, k = 14 4.4 -> 3.35 ms).  Not k = 11:
+   its runs are long already (~120 codes), and with half the slices k_part's
+   histogram and cursor atomics collide more often within a wave (k_part
+   4.40 -> 4.51 ms per 10 G bases) while k_bucket16's 256 heavy blocks run
+   as one round (k_bucket 2.31 -> 2.6-3.0 ms over the shapes tried): step
+   6.79 -> 7.2-7.7 ms.  k = 14 has no other path (2^16-bin slices). */
+#define W16_KS_DEFAULT ((1u << 12) | (1u << 13) | (1u << 14))
+#ifndef B16_QL
+#define B16_QL 4
+#endif
+#ifndef B16_ROWS
+#define B16_ROWS 2
+#endif
+#ifndef B16_U
+#define B16_U 5
+#endif
+#ifndef B16L_QL
+#define B16L_QL 1
+#endif
+#ifndef B16L_ROWS
+#define B16L_ROWS 4
+#endif
+#ifndef B16L_U
+#define B16L_U 1
+#endif
+template <bool PADDED>
+__global__ void __launch_bounds__(1024)
+k_bucket16(PartGeo pg, uint32_t *table) {
+    extern __shared__ uint32_t bins[];
+    constexpr uint32_t NW = 1u << 15;   /* words: 2^16 16-bit bins, or 2^15 32-bit ones */
+    const uint32_t nsing = pg.pairs ? pg.nbk - pg.npair : 0u;
+    uint32_t b;
+    if (blockIdx.x < nsing) {
+        b = pg.npair + blockIdx.x;
+    } else {
+        const uint32_t j = blockIdx.x - nsing, nh = pg.nbk - nsing;   /* (nh a multiple of 8) */
+        b = (j & 7u) * (nh >> 3) + (j >> 3);
+    }
+    const bool light = b >= pg.npair && nsing;
+    const uint32_t *ix = pg.idx + b;
+    const uint32_t nrows = pg.flag && *pg.flag ? 2u * pg.rows : pg.rows;
+    auto walk = [&](auto &&f) {
+        if (light) walk_runs<B16L_QL, B16L_ROWS, B16L_U, PADDED>(pg, ix, nrows, f);
+        else walk_runs<B16_QL, B16_ROWS, B16_U, PADDED>(pg, ix, nrows, f);
+    };
+    /* where bin i of the slice goes: pairs mode -> the pair or single bins
+       (k_pair_fold reduces them, this block owns them: stored), else the
+       table (added, reference index order) */
+    uint32_t *dst = nullptr;
+    if (pg.pairs) dst = b < pg.npair ? pg.pairs + ((size_t)b << 16) : pg.singles + ((size_t)(b - pg.npair) << 16);
+    const uint64_t base = (uint64_t)b << 16;
+    auto out2 = [&](uint32_t i2, uint32_t lo, uint32_t hi) {   /* bins 2 i2, 2 i2 + 1 */
+        if (!(lo | hi) && !pg.pairs) return;
+        if (pg.pairs) {
+            reinterpret_cast<uint2 *>(dst)[i2] = make_uint2(lo, hi);
+        } else {
+            /* sigma maps the last digit 0 1 2 3 -> 0 1 3 2: the pair stays
+               adjacent, swapped when the last digit of 2 i2 is 2 */
+            uint2 *t2 = reinterpret_cast<uint2 *>(table + (fk_sigma(base | (2u * i2)) & ~1ull));
+            uint2 o = *t2;
+            if (i2 & 1u) { o.x += hi; o.y += lo; } else { o.x += lo; o.y += hi; }
+            *t2 = o;
+        }
+    };
+    for (uint32_t i = threadIdx.x; i < NW / 4u; i += blockDim.x) reinterpret_cast<uint4 *>(bins)[i] = make_uint4(0, 0, 0, 0);
+    __syncthreads();
+    uint32_t n = 0;
+    walk([&](uint32_t c) {
+        atomicAdd(&bins[c >> 1], 1u << ((c & 1u) << 4));
+        n++;
+    });
+    __syncthreads();
+    /* the wrap check: sum of the halves == codes counted */
+    unsigned long long hs = 0;
+    for (uint32_t i = threadIdx.x; i < NW; i += blockDim.x) hs += (bins[i] & 0xFFFFu) + (bins[i] >> 16);
+    __shared__ unsigned long long red[2][16];
+    {
+        const unsigned long long a = wsum64(hs), c = wsum64((unsigned long long)n);
+        if ((threadIdx.x & 63) == 0) { red[0][threadIdx.x >> 6] = a; red[1][threadIdx.x >> 6] = c; }
+    }
+    __syncthreads();
+    unsigned long long sa = 0, sc = 0;
+#pragma unroll
+    for (int w = 0; w < 16; w++) { sa += red[0][w]; sc += red[1][w]; }
+    if (sa == sc) {
+        for (uint32_t i = threadIdx.x; i < NW; i += blockDim.x) out2(i, bins[i] & 0xFFFFu, bins[i] >> 16);
+        return;
+    }
+    /* a 16-bit bin wrapped: the slice again, as two halves of 2^15 32-bit bins */
+    for (uint32_t h = 0; h < 2u; h++) {
+        __syncthreads();
+        for (uint32_t i = threadIdx.x; i < NW / 4u; i += blockDim.x) reinterpret_cast<uint4 *>(bins)[i] = make_uint4(0, 0, 0, 0);
+        __syncthreads();
+        walk([&](uint32_t c) {
+            if ((c >> 15) == h) atomicAdd(&bins[c & 0x7FFFu], 1u);
+        });
+        __syncthreads();
+        for (uint32_t i = threadIdx.x; i < NW / 2u; i += blockDim.x) {
+            const uint32_t i2 = (h << 14) + i;   /* bins (h << 15) + 2 i, + 1 */
+            out2(i2, bins[2u * i], bins[2u * i + 1u]);
+        }
     }
 }
 
@@ -2936,15 +3139,20 @@ struct PartMeta {
 #define REPART_CAP 32768u     /* entries per pass-B round: a batch (16 waves x 2048), the longest run */
 static_assert(16u * FK_TILE_BYTES <= REPART_CAP, "a C32 row's run fits one k_repart round");
 
+/* OT = uint16_t: a code's part is its bits [15, 15 + split), stored as its
+   low 15 bits (k = 15, 16; k = 17 passes, psh = 15).  OT = uint32_t (wide
+   sparse passes): part bits [psh, psh + 6), stored as the low psh bits. */
+template <typename OT>
 __global__ void __launch_bounds__(1024)
-k_repart(PartGeo pg, uint16_t *out, unsigned long long *alloc, PartMeta *meta, uint64_t cap,
-         unsigned long long *err) {
+k_repart(PartGeo pg, OT *out, unsigned long long *alloc, PartMeta *meta, uint64_t cap,
+         unsigned long long *err, uint32_t psh) {
     /* per (slice in the group, part): entries, round count / offset /
        cursor, written so far, stream start */
     __shared__ uint32_t cnt[REPART_GP], hc[REPART_GP], ho[REPART_GP], cur[REPART_GP], wr[REPART_GP];
     __shared__ unsigned long long poff[REPART_GP];
     __shared__ uint32_t scn[17];
-    __shared__ __attribute__((aligned(16))) uint16_t rbuf[REPART_CAP];
+    __shared__ __attribute__((aligned(16))) OT rbuf[REPART_CAP];
+    const uint32_t pmask = (1u << psh) - 1u;
     const uint32_t t = threadIdx.x, wv = t >> 6, lane = t & 63;
     const uint32_t np = 1u << pg.split, gp = REPART_G * np;   /* parts of the block */
     const uint32_t b0 = blockIdx.x * REPART_G;                /* its first coarse slice */
@@ -2965,7 +3173,7 @@ k_repart(PartGeo pg, uint16_t *out, unsigned long long *alloc, PartMeta *meta, u
             const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
             for (int h = 0; h < 4; h++)
-                if (q * 4 + h >= s0 && q * 4 + h < s1) f(sl * np + (w4[h] >> 15), w4[h]);
+                if (q * 4 + h >= s0 && q * 4 + h < s1) f(sl * np + (w4[h] >> psh), w4[h]);
         };
         /* the pieces of a run of up to 17 codes in flight together (one
            load at a time left the kernel latency-bound) */
@@ -3059,7 +3267,7 @@ k_repart(PartGeo pg, uint16_t *out, unsigned long long *alloc, PartMeta *meta, u
                 const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
                 for (int h = 0; h < 4; h++)
-                    if (q * 4 + h >= s0 && q * 4 + h < s1) f(sl * np + (w4[h] >> 15), w4[h]);
+                    if (q * 4 + h >= s0 && q * 4 + h < s1) f(sl * np + (w4[h] >> psh), w4[h]);
             };
 #pragma unroll
             for (uint32_t u = 0; u < 5u; u++)
@@ -3081,7 +3289,7 @@ k_repart(PartGeo pg, uint16_t *out, unsigned long long *alloc, PartMeta *meta, u
         __syncthreads();
         codes([&](uint32_t p, uint32_t v) {
             const uint32_t at = atomicAdd(&cur[p], 1u);
-            rbuf[at] = (uint16_t)(v & 0x7FFFu);
+            rbuf[at] = (OT)(v & pmask);
         });
         /* the next round's first pieces (this round's are consumed) */
         {
@@ -3094,7 +3302,7 @@ k_repart(PartGeo pg, uint16_t *out, unsigned long long *alloc, PartMeta *meta, u
         /* a wave per part: consecutive entries to consecutive 2-B slots */
         for (uint32_t p = wv; p < gp; p += 16u) {
             const uint32_t n = poff[p] == ~0ull ? 0u : hc[p], o = ho[p];
-            uint16_t *dst = out + poff[p] + wr[p];
+            OT *dst = out + poff[p] + wr[p];
             for (uint32_t j = lane; j < n; j += 64u) dst[j] = rbuf[o + j];
         }
         __syncthreads();
@@ -4043,6 +4251,7 @@ struct fk_engine {
     uint64_t parts_cap = 0;
     void *d_pmeta = nullptr;                  /* k = 15, 16: PartMeta per part + the allocation counter */
     uint64_t pair_cap = 0;
+    uint32_t w16_ks = W16_KS_DEFAULT;         /* k (bits) counted through k_bucket16 (FINDKMER_TUNE w16=mask) */
     int part_pairs_kmax = 12;                 /* pairs mode for k <= this (FINDKMER_TUNE pairs_kmax; k = 12 pairs:
                                                  2048 slices of 32-code runs, half the entries of
                                                  512 single-window slices: 1 G-base step 1.63 -> 1.36 ms) */
@@ -4361,6 +4570,7 @@ extern "C" int fk_engine_create(int k, const fk_opts *opts, fk_engine **out) {
     if (tune_knob("pairs_kmax", &kv)) e->part_pairs_kmax = (int)std::min<uint64_t>(kv, 12u);
     if (tune_knob("part_general", &kv)) e->part_general = (uint32_t)kv;
     if (tune_knob("glist_cap", &kv)) e->glist_force = kv;
+    if (tune_knob("w16", &kv)) e->w16_ks = ((uint32_t)kv & 0x3000u) | (1u << 14);   /* k = 12, 13 (14 always) */
     if (tune_knob("events", &kv)) e->timing = kv != 0;
     if (tune_knob("static_pct", &kv)) e->static_pct = (uint32_t)std::min<uint64_t>(100u, std::max<uint64_t>(1u, kv));
     if (tune_knob("dyn_min_chunks", &kv)) e->dyn_min_chunks = kv;
@@ -4426,9 +4636,13 @@ extern "C" int fk_engine_create(int k, const fk_opts *opts, fk_engine **out) {
         hipFuncSetAttribute((const void *)k_resume<H_PAIRS>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh);
     }
     if (e->part)   /* k_bucket_count: one 2^15-bin slice + its 2^13 single bins (160 KiB) in LDS */
-        for (const void *f : {(const void *)k_bucket_count<BK_PLAIN>, (const void *)k_bucket_count<BK_SPLIT>,
-                              (const void *)k_count_parts, (const void *)k_bucket_count<BK_PAD>})
-            if (hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 5 << 15) != hipSuccess) {
+        for (const void *f : {(const void *)k_bucket_count<BK_PLAIN>, (const void *)k_count_parts,
+                              (const void *)k_bucket_count<BK_PAD>, (const void *)k_bucket16<true>,
+                              (const void *)k_bucket16<false>})
+            /* (k_bucket16: 128 KiB of bins beside its static reduction words) */
+            if (hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (f == (const void *)k_bucket16<true> || f == (const void *)k_bucket16<false>)
+                                        ? 1 << 17 : 5 << 15) != hipSuccess) {
                 fk_engine_destroy(e);
                 return FK_E_HIP;
             }
@@ -4712,10 +4926,30 @@ static int launch_part(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t l
        counted as two halves (PART_BIG); k = 15, 16: 2048 coarse slices of
        2^19 / 2^21 32-bit codes, counted in 2^15-bin parts */
     const bool c32 = k >= 15;
-    pg.sh = c32 ? 2 * k - 11 : k == 14 ? 16 : std::min(15, 2 * kb - 6);
-    pg.split = c32 ? (uint32_t)(pg.sh - 15) : k == 14 ? 1u : 0u;
+    /* 2^16-bin slices counted in 16-bit LDS bins (k_bucket16) for the k in
+       e->w16_ks (12 <= k <= 14) */
+    const bool w16 = !c32 && k >= 12 && ((e->w16_ks >> k) & 1u);
+    pg.w16 = w16 ? 1u : 0u;
+    pg.sh = c32 ? 2 * k - 11 : w16 ? 16 : std::min(15, 2 * kb - 6);
+    pg.split = c32 ? (uint32_t)(pg.sh - 15) : 0u;
     pg.npair = pairs ? 1u << (2 * kb - pg.sh) : 0u;
-    pg.nslices = pairs ? pg.npair : 1u << (2 * k - pg.sh);   /* singles fold into the pair slices */
+    if (pairs && w16) {
+        /* the single k-mers in their own 2^16-bin slices after the pair slices */
+        pg.sbase = pg.npair;
+        pg.slsh = 0;
+        pg.sflag = 0;
+        pg.nbk = pg.npair + (1u << (2 * k - 16));
+        /* (k = 12: 1280 slices in an index row of 2048, the width k_part's
+           all-wave scan divides among its 16 waves) */
+        pg.nslices = pg.nbk <= 512u ? pg.nbk : (pg.nbk + 1023u) & ~1023u;
+    } else {
+        /* singles filed under the pair code x << 2 (PART_SINGLE) */
+        pg.sbase = 0;
+        pg.slsh = 2;
+        pg.sflag = PART_SINGLE;
+        pg.nslices = pairs ? pg.npair : 1u << (2 * k - pg.sh);
+        pg.nbk = pg.nslices;
+    }
     pg.pairs = pg.singles = nullptr;
     pg.nomix = e->no_mixed ? 1u : 0u;
     pg.glist = nullptr;
@@ -4781,7 +5015,7 @@ static int launch_part(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t l
     /* runs padded to 16-B pieces (PART_PAD: the instances of at most 512
        slices, i.e. the 8-wave blocks of k <= 10 and k = 11's pairs): the row
        slot grows by one pad piece per slice */
-    const bool padded = !c32 && !pg.split && (W == 8u || (k == 11 && pairs));
+    const bool padded = !c32 && k != 14 && (W == 8u || (k == 11 && pairs));
     if (padded) pg.batch += PART_ROW_PAD(W == 8u ? PART_SM(8u) : PART_PAD_MAX_SM) / 2u;
     const uint64_t ncodes = (uint64_t)pg.stride * pg.batch * (c32 ? 2u : 1u),
                    nidx = (uint64_t)pg.nslices * pg.stride;
@@ -4804,7 +5038,7 @@ static int launch_part(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t l
        over all waves), phase by phase for k = 14 (PART_BIG) and k = 15, 16
        (C32); the headline k = 11 with k a compile-time constant */
     auto kmain = c32 ? k_part<false, false, 16u, PART_SM(16u), true>
-                 : pg.split ? k_part<false, false, 16u, PART_BIG>
+                 : k == 14 ? k_part<false, false, 16u, PART_BIG>
                  : W == 16u ? (pairs ? (k == 11 ? k_part<true, false, 16u, PART_PAD_MAX_SM, false, true, 11u>
                                                 : k_part<true, false, 16u, PART_SM(16u), false, true>)
                                      : k_part<false, false, 16u, PART_SM(16u), false, true>)
@@ -4816,7 +5050,7 @@ static int launch_part(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t l
     HIPCHK(hipGetLastError());
     if (mixed) {
         auto kres = c32 ? k_part<false, true, 16u, PART_SM(16u), true>
-                    : pg.split ? k_part<false, true, 16u, PART_BIG>
+                    : k == 14 ? k_part<false, true, 16u, PART_BIG>
                     : W == 16u ? (pairs ? (k == 11 ? k_part<true, true, 16u, PART_PAD_MAX_SM> : k_part<true, true, 16u>)
                                         : k_part<false, true, 16u>)
                                : (pairs ? k_part<true, true, 8u> : k_part<false, true, 8u>);
@@ -4827,7 +5061,7 @@ static int launch_part(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t l
     } else {
         pg.flag = nullptr;
     }
-    const uint32_t groups = std::max<uint32_t>(1, (uint32_t)e->cus / pg.nslices);
+    const uint32_t groups = w16 ? 1u : std::max<uint32_t>(1, (uint32_t)e->cus / pg.nslices);
     if (pairs && groups > 1) HIPCHK(hipMemsetAsync(e->d_pairs, 0, e->nbins * 5 * sizeof(uint32_t), e->stream));
     const size_t bc_lds = ((size_t)1 << (pg.sh - pg.split)) * sizeof(uint32_t) * (pairs ? 5 : 4) / 4;   /* + single bins */
     if (c32) {
@@ -4851,8 +5085,8 @@ static int launch_part(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t l
         e->d_perr = alloc + 1;
         e->perr_live = true;
         HIPCHK(hipMemsetAsync(alloc, 0, 2 * sizeof(unsigned long long), e->stream));
-        hipLaunchKernelGGL(k_repart, dim3(pg.nslices / REPART_G), dim3(1024), 0, e->stream, pg, e->d_parts, alloc, meta,
-                           (uint64_t)e->parts_cap, e->d_perr);
+        hipLaunchKernelGGL(k_repart<uint16_t>, dim3(pg.nslices / REPART_G), dim3(1024), 0, e->stream, pg, e->d_parts,
+                           alloc, meta, (uint64_t)e->parts_cap, e->d_perr, 15u);
         HIPCHK(hipGetLastError());
         hipLaunchKernelGGL(k_count_parts, dim3((unsigned)nparts), dim3(1024), (size_t)1 << 17, e->stream, pg,
                            (const uint16_t *)e->d_parts, (const PartMeta *)meta, e->d_table, (uint64_t)e->parts_cap,
@@ -4862,13 +5096,15 @@ static int launch_part(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t l
             hipLaunchKernelGGL(k_list_add, dim3((unsigned)e->cus * 4), dim3(256), 0, e->stream, pg.glist, e->d_table,
                                k, pg.fz);
         }
+    } else if (w16) {
+        if (padded)
+            hipLaunchKernelGGL(k_bucket16<true>, dim3(pg.nbk), dim3(1024), (size_t)1 << 17, e->stream, pg, e->d_table);
+        else
+            hipLaunchKernelGGL(k_bucket16<false>, dim3(pg.nbk), dim3(1024), (size_t)1 << 17, e->stream, pg, e->d_table);
     } else if (padded) {
         hipLaunchKernelGGL(k_bucket_count<BK_PAD>, dim3(pg.nslices * groups), dim3(1024), bc_lds, e->stream, pg,
                            groups, e->d_table);
-    } else if (pg.split)
-        hipLaunchKernelGGL(k_bucket_count<BK_SPLIT>, dim3(pg.nslices << pg.split), dim3(1024), bc_lds, e->stream, pg,
-                           1u, e->d_table);
-    else
+    } else
         hipLaunchKernelGGL(k_bucket_count<BK_PLAIN>, dim3(pg.nslices * groups), dim3(1024), bc_lds, e->stream, pg,
                            groups, e->d_table);
     HIPCHK(hipGetLastError());
@@ -5980,6 +6216,662 @@ static int sp_emit_all(fk_engine *e, const SpEmit &em) {
 }
 
 /*
+ * A k = 17 key-range pass (keys lo + r, r < 2^32, emitted as 32-bit r) into
+ * its runs without a sort (round 5; rocPRIM's radix sort and run-length
+ * encode took 228 ms of a 10 G-base step's 390).  The pass is a 2^32-bin
+ * count table, so it is counted the way k = 16's dense table is, and only
+ * its nonzero bins are written:
+ *   k_kpart       the key list in batches of 32 K keys, counting-sorted in LDS
+ *                 by r's top 11 bits into 2048 coarse slices (k_part<C32>'s
+ *                 row layout: each batch one row of runs of 21-bit codes and a
+ *                 row of run words);
+ *   k_repart      (as for k = 15, 16) each coarse slice into 64 contiguous
+ *                 part streams of 15-bit codes;
+ *   k_kp_count    one block per part (2^15 bins, in key order): the part's
+ *                 stream into LDS bins, the pads taken off the last bin, the
+ *                 nonzero bins' offset from the parts before it (a chained
+ *                 scan: each block publishes its distinct count, then looks
+ *                 back for the earlier parts' total), then the bins written
+ *                 as (key, u32 count) in ascending order with the statistics,
+ *                 the rollover check and the adjacent keys' prefix histogram;
+ *   k_kp_fold     the blocks' partial statistics into the pass accumulators,
+ *                 the prefix histogram of each part's first key against the
+ *                 last key of the nonempty part before it, and the pass's
+ *                 distinct count.
+ */
+#define KP_BATCH 32768u      /* keys per k_kpart batch (16 waves x 2048) */
+#define KP_SLOTS 64u         /* partial-statistics slots (block % KP_SLOTS) */
+#define KP_SLOT_W 36u        /* per slot: 10 statistics, rollover, 24 prefix-histogram entries, spare */
+#define KP_EMPTY (~0ull)
+
+/* KT = uint32_t: 32-bit relative keys r (slice r >> 21, code r & (2^21 - 1));
+   KT = uint64_t: keys lo + r with r < 2^(cs + 11) (slice r >> cs, code r &
+   (2^cs - 1), cs <= 29); keys >= hi (pads past the pass's range) are left out */
+template <typename KT>
+__global__ void __launch_bounds__(1024)
+k_kpart(const KT *keys, uint64_t n, PartGeo pg, uint64_t lo, uint64_t hi, uint32_t cs) {
+    constexpr bool WIDE = sizeof(KT) == 8;
+    __shared__ uint32_t hist[2048], cur[2048];
+    extern __shared__ uint32_t ent[];   /* KP_BATCH codes */
+    const uint32_t t = threadIdx.x;
+    const uint32_t sh = WIDE ? cs : 21u;
+    const KT cmask = (KT)(((uint64_t)1 << sh) - 1);
+    for (uint32_t i = t; i < 2048u; i += 1024u) hist[i] = 0;
+    const uint64_t per = (uint64_t)pg.rounds * KP_BATCH;
+    const uint64_t k0 = blockIdx.x * per, k1 = min(k0 + per, n);
+    uint32_t *codes = reinterpret_cast<uint32_t *>(pg.codes);
+    for (uint32_t r = 0; r < pg.rounds; r++) {
+        const uint32_t row = blockIdx.x * pg.rounds + r;
+        const uint64_t b0 = k0 + (uint64_t)r * KP_BATCH;
+        const uint32_t nv = b0 < k1 ? (uint32_t)min<uint64_t>(KP_BATCH, k1 - b0) : 0u;
+        __syncthreads();
+        if (nv == 0) {   /* rows past the block's keys are empty */
+            for (uint32_t b = t; b < 2048u; b += 1024u) pg.idx[(size_t)row * 2048u + b] = PART_NO_RUN;
+            continue;
+        }
+        /* relative keys (WIDE: ~0 for a key left out; a 32-bit ~0 is a real
+           key or a pad, which the caller takes off the last bin) */
+        KT v[32];
+#pragma unroll
+        for (uint32_t j = 0; j < 32u; j++) {
+            v[j] = (KT)~(KT)0;
+            if (j * 1024u + t < nv) {
+                const KT x = keys[b0 + j * 1024u + t];
+                if (!WIDE) v[j] = x;
+                else if ((uint64_t)x < hi) v[j] = (KT)((uint64_t)x - lo);
+            }
+        }
+#define KP_IN(j) ((j) * 1024u + t < nv && (!WIDE || v[j] != (KT)~(KT)0))
+#pragma unroll
+        for (uint32_t j = 0; j < 32u; j++)
+            if (KP_IN(j)) atomicAdd(&hist[(uint32_t)(v[j] >> sh)], 1u);
+        __syncthreads();
+        if (t < 64) {   /* cursors and the row's run words: 32 slices per lane */
+            uint32_t sum = 0;
+            for (uint32_t j = 0; j < 32u; j++) sum += hist[t * 32u + j];
+            uint32_t run = wscan_incl32(sum) - sum;
+            for (uint32_t j = 0; j < 32u; j++) {
+                const uint32_t b = t * 32u + j, c = hist[b];
+                cur[b] = run;
+                pg.idx[(size_t)row * 2048u + b] = run_word(run, c);
+                hist[b] = 0;
+                run += c;
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (uint32_t j = 0; j < 32u; j++)
+            if (KP_IN(j)) ent[atomicAdd(&cur[(uint32_t)(v[j] >> sh)], 1u)] = (uint32_t)(v[j] & cmask);
+#undef KP_IN
+        __syncthreads();
+        /* the row: its runs end at cur[2047] (every entry placed) */
+        const uint32_t tot = cur[2047];
+        uint4 *dst = reinterpret_cast<uint4 *>(codes + (size_t)row * pg.batch);
+        const uint4 *src = reinterpret_cast<const uint4 *>(ent);
+        for (uint32_t i = t; i < (tot + 3u) / 4u; i += 1024u) dst[i] = src[i];
+    }
+}
+
+/* the bins of a part: thread t takes bins [32 t, 32 t + 32) */
+__global__ void __launch_bounds__(1024)
+k_kp_count(const uint16_t *in, const PartMeta *meta, uint64_t cap_in, uint64_t lo, uint64_t npads, uint32_t nparts,
+           int k, unsigned long long *flags, uint64_t *out_k, uint32_t *out_c, unsigned long long *slots,
+           uint64_t *fl, unsigned long long *err) {
+    extern __shared__ uint32_t bins[];   /* 2^15 */
+    __shared__ unsigned long long wred[16][10];
+    __shared__ uint32_t hpre[24];
+    __shared__ uint32_t wnz[16], wmx[16];
+    __shared__ unsigned long long bprefix;
+    const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6, blk = blockIdx.x;
+    for (uint32_t i = t; i < (1u << 13); i += 1024u) reinterpret_cast<uint4 *>(bins)[i] = make_uint4(0, 0, 0, 0);
+    if (t < 24) hpre[t] = 0;
+    __syncthreads();
+    PartMeta m = meta[blk];
+    if (m.off + m.n > cap_in) {   /* bound check (k_count_parts's) */
+        if (t == 0) atomicOr(err, (unsigned long long)FK_FAULT_META);
+        m.n = 0;
+        m.off = 0;
+    }
+    const uint4 *g4 = reinterpret_cast<const uint4 *>(in + m.off);
+    const uint32_t nq = (m.n + 7u) >> 3;
+    for (uint32_t q = t; q < nq; q += 1024u) {
+        const uint4 v = g4[q];
+        const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int h = 0; h < 8; h++)
+            if (q * 8u + (uint32_t)h < m.n) atomicAdd(&bins[(w4[h >> 1] >> (16 * (h & 1))) & 0x7FFFu], 1u);
+    }
+    __syncthreads();
+    /* the pads (relative key 0xFFFFFFFF: the last bin of the last part) */
+    if (t == 0 && npads && blk == nparts - 1u) bins[0x7FFFu] -= (uint32_t)npads;
+    __syncthreads();
+    uint32_t c[32];
+#pragma unroll
+    for (uint32_t j = 0; j < 8u; j++) {
+        const uint4 q = reinterpret_cast<const uint4 *>(bins)[t * 8u + j];
+        c[4 * j] = q.x; c[4 * j + 1] = q.y; c[4 * j + 2] = q.z; c[4 * j + 3] = q.w;
+    }
+    const int fs = 2 * (k - 1);
+    const uint64_t kb = lo + ((uint64_t)blk << 15) + t * 32u;   /* key of my first bin */
+    uint32_t nz = 0;
+    unsigned long long st[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (uint32_t j = 0; j < 32u; j++) {
+        const uint32_t x = c[j];
+        const uint64_t key = kb + j;
+        nz += x != 0;
+        st[1] += x;
+        st[2 + (uint32_t)(key & 3)] += x;
+        st[6 + (uint32_t)((key >> fs) & 3)] += x;
+    }
+    st[0] = nz;
+    /* block scan of the nonzero counts */
+    const uint32_t inc = wscan_incl32(nz);
+    if (lane == 63) wnz[wv] = inc;
+    __syncthreads();
+    uint32_t before = 0, total = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < 16u; w++) {
+        const uint32_t x = wnz[w];
+        before += w < wv ? x : 0u;
+        total += x;
+    }
+    const uint32_t off = before + inc - nz;
+    /* chained scan over the parts: publish this part's total, look back */
+    if (t == 0) {
+        const unsigned long long A = 1ull << 62, P = 2ull << 62, M = (1ull << 62) - 1;
+        unsigned long long pre = 0;
+        if (blk == 0) {
+            __hip_atomic_store(&flags[0], P | total, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            __hip_atomic_store(&flags[blk], A | total, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            uint32_t j = blk - 1u;
+            /* every earlier part was dispatched before this one and publishes
+               unconditionally; the spin bound only guards against a broken
+               invariant (the pass then fails with FK_E_INTERNAL) */
+            for (uint64_t spin = 0;;) {
+                const unsigned long long f = __hip_atomic_load(&flags[j], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+                if ((f >> 62) == 0) {
+                    if (++spin > (1ull << 26)) { atomicOr(err, (unsigned long long)FK_FAULT_PARTS); break; }
+                    __builtin_amdgcn_s_sleep(1);
+                    continue;
+                }
+                pre += f & M;
+                if ((f >> 62) == 2 || j == 0) break;
+                j--;
+            }
+            __hip_atomic_store(&flags[blk], P | (pre + total), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        bprefix = pre;
+        if (!total) fl[2 * (size_t)blk] = KP_EMPTY;
+    }
+    /* the nearest earlier thread holding a nonzero bin (an exclusive max
+       scan of t + 1), for the adjacent pair across threads */
+    const uint32_t im = wscan_max32(nz ? t + 1u : 0u);
+    if (lane == 63) wmx[wv] = im;
+    __syncthreads();   /* (also: every thread has its bins in registers) */
+    uint32_t pm = (uint32_t)__shfl_up((int)im, 1, 64);
+    if (lane == 0) pm = 0;
+    for (uint32_t w = 0; w < wv; w++) pm = max(pm, wmx[w]);
+    const uint64_t base = bprefix + off;
+    uint32_t o = 0;
+    uint64_t first = 0, prev = 0;
+    bool have = false;
+#pragma unroll
+    for (uint32_t j = 0; j < 32u; j++) {
+        if (c[j]) {
+            const uint64_t key = kb + j;
+            out_k[base + o] = key;
+            out_c[base + o] = c[j];
+            if (have) {   /* first differing base of adjacent keys (k_sp_wprefix) */
+                const int lz = __clzll((long long)(key ^ prev)) - (64 - 2 * k);
+                atomicAdd(&hpre[lz / 2 + 1], 1u);
+            } else {
+                first = key;
+            }
+            prev = key;
+            have = true;
+            o++;
+        }
+    }
+    /* every thread's last key in the (now free) bins' LDS */
+    uint64_t *lastk = reinterpret_cast<uint64_t *>(bins);
+    lastk[t] = prev;
+    __syncthreads();
+    if (nz && pm) {
+        const uint64_t pk = lastk[pm - 1u];
+        const int lz = __clzll((long long)(first ^ pk)) - (64 - 2 * k);
+        atomicAdd(&hpre[lz / 2 + 1], 1u);
+    }
+    if (nz && !pm) fl[2 * (size_t)blk] = first;
+    if (nz && off + nz == total) fl[2 * (size_t)blk + 1] = prev;
+    /* the rollover check: a bin past 2^32 codes wrapped, so its sum falls
+       short of the codes (less the pads) */
+    unsigned long long v10[10];
+#pragma unroll
+    for (int q = 0; q < 10; q++) v10[q] = wsum64(st[q]);
+    if (lane == 0)
+#pragma unroll
+        for (int q = 0; q < 10; q++) wred[wv][q] = v10[q];
+    __syncthreads();
+    if (t < 10) {
+        unsigned long long a = 0;
+        for (uint32_t w = 0; w < 16u; w++) a += wred[w][t];
+        if (a) atomicAdd(&slots[(blk % KP_SLOTS) * KP_SLOT_W + t], a);
+        if (t == 1) {
+            const uint64_t want = (uint64_t)m.n - (blk == nparts - 1u ? npads : 0u);
+            if (a != want) atomicOr(&slots[(blk % KP_SLOTS) * KP_SLOT_W + 10], 1ull);
+        }
+    }
+    if (t < 24 && hpre[t]) atomicAdd(&slots[(blk % KP_SLOTS) * KP_SLOT_W + 11 + t], (unsigned long long)hpre[t]);
+}
+
+/*
+ * Wide passes (18 <= k <= 20, a key range of more than 2^32 keys): the same
+ * two partition levels (64-bit keys in, the parts' codes 32-bit), then each
+ * part -- up to KS_CAP keys of at most 23 bits, ~20 K at k = 20 over 10 G
+ * bases -- sorted in LDS instead of counted: bucketed by its top 8 bits
+ * (LDS histogram, scan, scatter), each bucket sorted by one wave in
+ * registers (a bitonic network over 64 N keys, N = 1..16 per lane), then run-
+ * length encoded.  A part or bucket above those sizes (a k-mer repeated
+ * tens of thousands of times in one part) flags the pass, which then takes
+ * the library sort (fks_sort_runs) instead.
+ */
+#define KS_CAP 24576u
+#define KS_ITEMS (KS_CAP / 1024u)
+#define FK_FAULT_SORTCAP 8u
+
+/* bitonic sort of the 64 N values x[i] (element i * 64 + lane), ascending */
+template <int N>
+__device__ __forceinline__ void wave_bitonic(uint32_t (&x)[N]) {
+    const uint32_t lane = threadIdx.x & 63;
+#pragma unroll
+    for (uint32_t s2 = 2; s2 <= 64u * N; s2 <<= 1) {
+#pragma unroll
+        for (uint32_t d = s2 >> 1; d > 0; d >>= 1) {
+            if (d >= 64) {
+                const uint32_t dr = d / 64;
+#pragma unroll
+                for (int i = 0; i < N; i++) {
+                    if ((uint32_t)i & dr) continue;
+                    const int j = i | (int)dr;
+                    const uint32_t e = (uint32_t)i * 64u + lane;
+                    const bool up = (e & s2) == 0;
+                    const uint32_t a = x[i], b = x[j];
+                    x[i] = up ? min(a, b) : max(a, b);
+                    x[j] = up ? max(a, b) : min(a, b);
+                }
+            } else {
+#pragma unroll
+                for (int i = 0; i < N; i++) {
+                    const uint32_t e = (uint32_t)i * 64u + lane;
+                    const uint32_t o = (uint32_t)__shfl_xor((int)x[i], (int)d, 64);
+                    const bool up = (e & s2) == 0, low = (lane & d) == 0;
+                    x[i] = (low == up) ? min(x[i], o) : max(x[i], o);
+                }
+            }
+        }
+    }
+}
+
+template <int N>
+__device__ __forceinline__ void wave_sort_bucket(uint32_t *k, uint32_t n) {
+    const uint32_t lane = threadIdx.x & 63;
+    uint32_t x[N];
+#pragma unroll
+    for (int i = 0; i < N; i++) {
+        const uint32_t e = (uint32_t)i * 64u + lane;
+        x[i] = e < n ? k[e] : ~0u;
+    }
+    wave_bitonic<N>(x);
+#pragma unroll
+    for (int i = 0; i < N; i++) {
+        const uint32_t e = (uint32_t)i * 64u + lane;
+        if (e < n) k[e] = x[i];
+    }
+}
+
+__global__ void __launch_bounds__(1024)
+k_kp_sort(const uint32_t *in, const PartMeta *meta, uint64_t cap_in, uint64_t lo, uint32_t psh, uint64_t npads,
+          uint32_t pad_part, uint32_t nparts, int k, unsigned long long *flags, uint64_t *out_k, uint32_t *out_c,
+          unsigned long long *slots, uint64_t *fl, unsigned long long *err) {
+    extern __shared__ uint32_t keys[];   /* KS_CAP */
+    __shared__ uint32_t bh[256], bo[257];
+    __shared__ unsigned long long wred[16][10];
+    __shared__ uint32_t hpre[24];
+    __shared__ uint32_t wnz[16];
+    __shared__ unsigned long long bprefix;
+    __shared__ uint32_t bad;
+    const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6, blk = blockIdx.x;
+    if (t < 256) bh[t] = 0;
+    if (t < 24) hpre[t] = 0;
+    if (t == 0) bad = 0;
+    __syncthreads();
+    PartMeta m = meta[blk];
+    if (m.off + m.n > cap_in) {
+        if (t == 0) atomicOr(err, (unsigned long long)FK_FAULT_META);
+        m.n = 0;
+        m.off = 0;
+    }
+    if (m.n > KS_CAP) {   /* too many keys for one block's LDS: the library sort */
+        if (t == 0) atomicOr(err, (unsigned long long)FK_FAULT_SORTCAP);
+        m.n = 0;
+    }
+    const uint32_t n = m.n, bsh = psh - 8u;
+    /* 1. bucket by the top 8 bits of the part's code */
+    uint32_t v[KS_ITEMS];
+#pragma unroll
+    for (uint32_t j = 0; j < KS_ITEMS; j++) {
+        v[j] = j * 1024u + t < n ? in[m.off + j * 1024u + t] : 0u;
+        if (j * 1024u + t < n) atomicAdd(&bh[v[j] >> bsh], 1u);
+    }
+    __syncthreads();
+    if (t < 64) {
+        uint32_t c4[4], sum = 0;
+#pragma unroll
+        for (int q = 0; q < 4; q++) { c4[q] = bh[t * 4 + q]; sum += c4[q]; }
+        uint32_t run = wscan_incl32(sum) - sum;
+#pragma unroll
+        for (int q = 0; q < 4; q++) { bo[t * 4 + q] = run; bh[t * 4 + q] = run; run += c4[q]; }
+        if (t == 63) bo[256] = run;
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t j = 0; j < KS_ITEMS; j++)
+        if (j * 1024u + t < n) keys[atomicAdd(&bh[v[j] >> bsh], 1u)] = v[j];
+    __syncthreads();
+    /* 2. each bucket sorted by one wave */
+    for (uint32_t b = wv; b < 256u; b += 16u) {
+        const uint32_t b0 = bo[b], nb = bo[b + 1] - b0;
+        if (nb <= 1) continue;
+        if (nb <= 64) wave_sort_bucket<1>(keys + b0, nb);
+        else if (nb <= 128) wave_sort_bucket<2>(keys + b0, nb);
+        else if (nb <= 256) wave_sort_bucket<4>(keys + b0, nb);
+        else if (nb <= 512) wave_sort_bucket<8>(keys + b0, nb);
+        else if (nb <= 1024) wave_sort_bucket<16>(keys + b0, nb);
+        else if (lane == 0) bad = 1;
+    }
+    __syncthreads();
+    if (bad) {
+        if (t == 0) atomicOr(err, (unsigned long long)FK_FAULT_SORTCAP);
+    }
+    const uint32_t nn = bad ? 0u : n;
+    /* 3. runs: thread t takes positions [t * KS_ITEMS, +KS_ITEMS); a run
+       starts where the key changes */
+    const uint32_t p0 = t * KS_ITEMS;
+    uint32_t nz = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < KS_ITEMS; j++) {
+        const uint32_t i = p0 + j;
+        if (i < nn && (i == 0 || keys[i] != keys[i - 1])) nz++;
+    }
+    const uint32_t inc = wscan_incl32(nz);
+    if (lane == 63) wnz[wv] = inc;
+    __syncthreads();
+    uint32_t before = 0, total = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < 16u; w++) {
+        const uint32_t x = wnz[w];
+        before += w < wv ? x : 0u;
+        total += x;
+    }
+    /* the pads (the key 4^k - 1 when the pass holds it) come off its run:
+       the last run of the pad part; a run left empty is dropped */
+    const bool padp = npads && blk == pad_part && total;
+    if (padp) {
+        /* the last run's count, from its start */
+        uint32_t ls = nn - 1;
+        while (ls > 0 && keys[ls - 1] == keys[nn - 1]) ls--;
+        if ((uint64_t)(nn - ls) <= npads) total--;   /* (the dropped run is the last one) */
+    }
+    const uint32_t off = before + inc - nz;
+    if (t == 0) {
+        const unsigned long long A = 1ull << 62, P = 2ull << 62, M = (1ull << 62) - 1;
+        unsigned long long pre = 0;
+        if (blk == 0) {
+            __hip_atomic_store(&flags[0], P | total, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            __hip_atomic_store(&flags[blk], A | total, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            uint32_t j = blk - 1u;
+            for (uint64_t spin = 0;;) {
+                const unsigned long long f = __hip_atomic_load(&flags[j], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+                if ((f >> 62) == 0) {
+                    if (++spin > (1ull << 26)) { atomicOr(err, (unsigned long long)FK_FAULT_PARTS); break; }
+                    __builtin_amdgcn_s_sleep(1);
+                    continue;
+                }
+                pre += f & M;
+                if ((f >> 62) == 2 || j == 0) break;
+                j--;
+            }
+            __hip_atomic_store(&flags[blk], P | (pre + total), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        bprefix = pre;
+        if (!total) fl[2 * (size_t)blk] = KP_EMPTY;
+    }
+    __syncthreads();
+    const int fs = 2 * (k - 1);
+    const uint64_t kb = lo + ((uint64_t)blk << psh);
+    unsigned long long st[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    uint32_t o = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < KS_ITEMS; j++) {
+        const uint32_t i = p0 + j;
+        if (i < nn && (i == 0 || keys[i] != keys[i - 1])) {
+            uint32_t e2 = i + 1;
+            while (e2 < nn && keys[e2] == keys[i]) e2++;
+            uint64_t cnt = e2 - i;
+            const uint64_t key = kb + keys[i];
+            if (padp && e2 == nn) {
+                if (cnt <= npads) continue;   /* (counted off `total` above) */
+                cnt -= npads;
+            }
+            const uint32_t c = (uint32_t)cnt;
+            out_k[bprefix + off + o] = key;
+            out_c[bprefix + off + o] = c;
+            st[0] += 1;
+            st[1] += c;
+            st[2 + (uint32_t)(key & 3)] += c;
+            st[6 + (uint32_t)((key >> fs) & 3)] += c;
+            if (i > 0) {   /* against the run before it, in this part */
+                const int lz = __clzll((long long)(key ^ (kb + keys[i - 1]))) - (64 - 2 * k);
+                atomicAdd(&hpre[lz / 2 + 1], 1u);
+            }
+            if (bprefix + off + o == bprefix) fl[2 * (size_t)blk] = key;
+            if (off + o + 1 == total) fl[2 * (size_t)blk + 1] = key;
+            o++;
+        }
+    }
+    unsigned long long v10[10];
+#pragma unroll
+    for (int q = 0; q < 10; q++) v10[q] = wsum64(st[q]);
+    if (lane == 0)
+#pragma unroll
+        for (int q = 0; q < 10; q++) wred[wv][q] = v10[q];
+    __syncthreads();
+    if (t < 10) {
+        unsigned long long a = 0;
+        for (uint32_t w = 0; w < 16u; w++) a += wred[w][t];
+        if (a) atomicAdd(&slots[(blk % KP_SLOTS) * KP_SLOT_W + t], a);
+    }
+    if (t < 24 && hpre[t]) atomicAdd(&slots[(blk % KP_SLOTS) * KP_SLOT_W + 11 + t], (unsigned long long)hpre[t]);
+}
+
+/* the partials into the pass accumulators (FKS_ACC layout), the prefix
+   histogram of each nonempty part's first key against the last key of the
+   nonempty part before it, and the pass's distinct count (res[0]) */
+__global__ void __launch_bounds__(256)
+k_kp_fold(const unsigned long long *slots, const uint64_t *fl, uint32_t nparts, int k,
+          const unsigned long long *flags, unsigned long long *dacc, unsigned long long *res) {
+    __shared__ uint32_t h[24];
+    if (threadIdx.x < 24) h[threadIdx.x] = 0;
+    __syncthreads();
+    if (blockIdx.x == 0) {
+        if (threadIdx.x < 10) {
+            unsigned long long a = 0;
+            for (uint32_t sl = 0; sl < KP_SLOTS; sl++) a += slots[sl * KP_SLOT_W + threadIdx.x];
+            if (a) atomicAdd(&dacc[threadIdx.x], a);
+        } else if (threadIdx.x == 10) {
+            unsigned long long a = 0;
+            for (uint32_t sl = 0; sl < KP_SLOTS; sl++) a |= slots[sl * KP_SLOT_W + 10];
+            if (a) atomicAdd(&dacc[FKS_ACC_ROLL], 1ull);   /* (k_sp_stats adds wrapped counts' high words) */
+        } else if (threadIdx.x >= 32 && threadIdx.x < 56) {
+            unsigned long long a = 0;
+            for (uint32_t sl = 0; sl < KP_SLOTS; sl++) a += slots[sl * KP_SLOT_W + 11 + (threadIdx.x - 32)];
+            if (a) atomicAdd(&dacc[FKS_ACC_WPREFIX + (threadIdx.x - 32)], a);
+        } else if (threadIdx.x == 64) {
+            res[0] = flags[nparts - 1] & ((1ull << 62) - 1);
+        }
+    }
+    for (uint32_t p = blockIdx.x * blockDim.x + threadIdx.x; p < nparts; p += gridDim.x * blockDim.x) {
+        const uint64_t first = fl[2 * (size_t)p];
+        if (first == KP_EMPTY || p == 0) continue;
+        uint32_t q = p - 1;
+        while (q > 0 && fl[2 * (size_t)q] == KP_EMPTY) q--;
+        if (fl[2 * (size_t)q] == KP_EMPTY) continue;
+        const uint64_t pk = fl[2 * (size_t)q + 1];
+        const int lz = __clzll((long long)(first ^ pk)) - (64 - 2 * k);
+        atomicAdd(&h[lz / 2 + 1], 1u);
+    }
+    __syncthreads();
+    if (threadIdx.x < 24 && h[threadIdx.x]) atomicAdd(&dacc[FKS_ACC_WPREFIX + threadIdx.x], (unsigned long long)h[threadIdx.x]);
+}
+
+/* The pass (keys lo + r for the n 32-bit r, npads of them the pad
+   0xFFFFFFFF) into its runs at out_k / out_c: *nw of them */
+static int sp_count_runs32(fk_engine *e, const uint32_t *keys, uint64_t n, uint64_t lo, uint64_t npads,
+                           unsigned long long *dacc, uint64_t *out_k, uint32_t *out_c, uint64_t *nw) {
+    *nw = 0;
+    if (n == 0) return FK_OK;
+    const int k = e->k;
+    PartGeo pg{};
+    pg.nslices = 2048u;
+    pg.split = 6u;   /* 2^21-bin coarse slices, 64 parts of 2^15 */
+    pg.batch = KP_BATCH;
+    const uint32_t grid = (uint32_t)std::max(1, e->cus);
+    pg.rounds = (uint32_t)((n + (uint64_t)grid * KP_BATCH - 1) / ((uint64_t)grid * KP_BATCH));
+    pg.rows = grid * pg.rounds;
+    pg.flag = nullptr;
+    const uint64_t ncodes = (uint64_t)pg.rows * KP_BATCH;   /* u32 codes */
+    const uint32_t nparts = 2048u << 6;
+    int rc = sp_ensure((void **)&e->d_codes, &e->codes_cap, 2 * ncodes, sizeof(uint16_t));
+    if (!rc) rc = sp_ensure((void **)&e->d_pidx, &e->pidx_cap, (uint64_t)pg.rows * 2048u, sizeof(uint32_t));
+    if (!rc) rc = sp_ensure((void **)&e->d_parts, &e->parts_cap, n + 8ull * nparts + 16, sizeof(uint16_t));
+    if (rc) return rc;
+    if (!e->d_pmeta && hipMalloc(&e->d_pmeta, (size_t)2048 * REPART_MAXP * sizeof(PartMeta) + 64) != hipSuccess)
+        return FK_E_OOM;
+    DevScratch flags, slots, fl, res;
+    if (!flags.alloc((size_t)nparts * 8) || !slots.alloc((size_t)KP_SLOTS * KP_SLOT_W * 8) ||
+        !fl.alloc((size_t)nparts * 16) || !res.alloc(16))
+        return FK_E_OOM;
+    pg.codes = e->d_codes;
+    pg.idx = e->d_pidx;
+    PartMeta *meta = static_cast<PartMeta *>(e->d_pmeta);
+    unsigned long long *alloc = reinterpret_cast<unsigned long long *>(meta + (size_t)2048 * REPART_MAXP);
+    HIPCHK(hipMemsetAsync(alloc, 0, 2 * sizeof(unsigned long long), e->stream));
+    HIPCHK(hipMemsetAsync(flags.p, 0, (size_t)nparts * 8, e->stream));
+    HIPCHK(hipMemsetAsync(slots.p, 0, (size_t)KP_SLOTS * KP_SLOT_W * 8, e->stream));
+    hipLaunchKernelGGL(k_kpart<uint32_t>, dim3(grid), dim3(1024), (size_t)KP_BATCH * 4, e->stream, keys, n, pg, 0ull,
+                       0ull, 21u);
+    HIPCHK(hipGetLastError());
+    hipLaunchKernelGGL(k_repart<uint16_t>, dim3(2048u / REPART_G), dim3(1024), 0, e->stream, pg, e->d_parts, alloc,
+                       meta, (uint64_t)e->parts_cap, alloc + 1, 15u);
+    HIPCHK(hipGetLastError());
+    hipLaunchKernelGGL(k_kp_count, dim3(nparts), dim3(1024), (size_t)1 << 17, e->stream, (const uint16_t *)e->d_parts,
+                       (const PartMeta *)meta, (uint64_t)e->parts_cap, lo, npads, nparts, k, flags.as<unsigned long long>(),
+                       out_k, out_c, slots.as<unsigned long long>(), fl.as<uint64_t>(), alloc + 1);
+    HIPCHK(hipGetLastError());
+    hipLaunchKernelGGL(k_kp_fold, dim3(64), dim3(256), 0, e->stream, (const unsigned long long *)slots.p,
+                       (const uint64_t *)fl.p, nparts, k, (const unsigned long long *)flags.p, dacc,
+                       res.as<unsigned long long>());
+    HIPCHK(hipGetLastError());
+    unsigned long long r[2] = {0, 0};
+    HIPCHK(hipMemcpyAsync(&r[0], res.p, 8, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipMemcpyAsync(&r[1], alloc + 1, 8, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    if (r[1]) return FK_E_INTERNAL;
+    *nw = r[0];
+    return FK_OK;
+}
+
+/* A wide pass (keys[0, n) in [lo, hi), hi - lo > 2^32, npads of them the
+   pad 4^k - 1) into its runs at out_k / out_c (*nw).  `fallback` is set
+   when a part or bucket is too large for k_kp_sort: nothing was folded into
+   dacc and the caller sorts the pass with the library instead. */
+static int sp_sort_runs64(fk_engine *e, const uint64_t *keys, uint64_t n, uint64_t lo, uint64_t hi, uint64_t npads,
+                          unsigned long long *dacc, uint64_t *out_k, uint32_t *out_c, uint64_t *nw, bool *fallback) {
+    *nw = 0;
+    *fallback = false;
+    if (n == 0) return FK_OK;
+    const int k = e->k;
+    uint32_t sbits = 33;
+    while (sbits < 64 && ((hi - lo - 1) >> sbits)) sbits++;
+    const uint32_t cs = sbits - 11, psh = cs - 6;   /* 2048 coarse slices, 64 parts each */
+    PartGeo pg{};
+    pg.nslices = 2048u;
+    pg.split = 6u;
+    pg.batch = KP_BATCH;
+    const uint32_t grid = (uint32_t)std::max(1, e->cus);
+    pg.rounds = (uint32_t)((n + (uint64_t)grid * KP_BATCH - 1) / ((uint64_t)grid * KP_BATCH));
+    pg.rows = grid * pg.rounds;
+    pg.flag = nullptr;
+    const uint64_t ncodes = (uint64_t)pg.rows * KP_BATCH;
+    const uint32_t nparts = 2048u << 6;
+    int rc = sp_ensure((void **)&e->d_codes, &e->codes_cap, 2 * ncodes, sizeof(uint16_t));
+    if (!rc) rc = sp_ensure((void **)&e->d_pidx, &e->pidx_cap, (uint64_t)pg.rows * 2048u, sizeof(uint32_t));
+    /* (the part streams as 32-bit codes: twice the u16 capacity) */
+    if (!rc) rc = sp_ensure((void **)&e->d_parts, &e->parts_cap, 2 * (n + 8ull * nparts + 16), sizeof(uint16_t));
+    if (rc) return rc;
+    if (!e->d_pmeta && hipMalloc(&e->d_pmeta, (size_t)2048 * REPART_MAXP * sizeof(PartMeta) + 64) != hipSuccess)
+        return FK_E_OOM;
+    DevScratch flags, slots, fl, res;
+    if (!flags.alloc((size_t)nparts * 8) || !slots.alloc((size_t)KP_SLOTS * KP_SLOT_W * 8) ||
+        !fl.alloc((size_t)nparts * 16) || !res.alloc(16))
+        return FK_E_OOM;
+    pg.codes = e->d_codes;
+    pg.idx = e->d_pidx;
+    PartMeta *meta = static_cast<PartMeta *>(e->d_pmeta);
+    unsigned long long *alloc = reinterpret_cast<unsigned long long *>(meta + (size_t)2048 * REPART_MAXP);
+    uint32_t *parts32 = reinterpret_cast<uint32_t *>(e->d_parts);
+    const uint64_t cap32 = e->parts_cap / 2;
+    HIPCHK(hipMemsetAsync(alloc, 0, 2 * sizeof(unsigned long long), e->stream));
+    HIPCHK(hipMemsetAsync(flags.p, 0, (size_t)nparts * 8, e->stream));
+    HIPCHK(hipMemsetAsync(slots.p, 0, (size_t)KP_SLOTS * KP_SLOT_W * 8, e->stream));
+    hipLaunchKernelGGL(k_kpart<uint64_t>, dim3(grid), dim3(1024), (size_t)KP_BATCH * 4, e->stream, keys, n, pg, lo, hi,
+                       cs);
+    HIPCHK(hipGetLastError());
+    hipLaunchKernelGGL(k_repart<uint32_t>, dim3(2048u / REPART_G), dim3(1024), 0, e->stream, pg, parts32, alloc, meta,
+                       cap32, alloc + 1, psh);
+    HIPCHK(hipGetLastError());
+    /* the pads are in the pass only when it holds the key 4^k - 1 */
+    const uint64_t top = (1ull << (2 * k)) - 1;
+    const bool pads_in = npads && top >= lo && top < hi;
+    const uint32_t pad_part = pads_in ? (uint32_t)((top - lo) >> psh) : 0u;
+    hipLaunchKernelGGL(k_kp_sort, dim3(nparts), dim3(1024), (size_t)KS_CAP * 4, e->stream, (const uint32_t *)parts32,
+                       (const PartMeta *)meta, cap32, lo, psh, pads_in ? npads : 0ull, pad_part, nparts, k,
+                       flags.as<unsigned long long>(), out_k, out_c, slots.as<unsigned long long>(), fl.as<uint64_t>(),
+                       alloc + 1);
+    HIPCHK(hipGetLastError());
+    unsigned long long ferr = 0;
+    HIPCHK(hipMemcpyAsync(&ferr, alloc + 1, 8, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    if (ferr & FK_FAULT_SORTCAP) {
+        *fallback = true;
+        return FK_OK;
+    }
+    if (ferr) return FK_E_INTERNAL;
+    hipLaunchKernelGGL(k_kp_fold, dim3(64), dim3(256), 0, e->stream, (const unsigned long long *)slots.p,
+                       (const uint64_t *)fl.p, nparts, k, (const unsigned long long *)flags.p, dacc,
+                       res.as<unsigned long long>());
+    HIPCHK(hipGetLastError());
+    unsigned long long r0 = 0;
+    HIPCHK(hipMemcpyAsync(&r0, res.p, 8, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    *nw = r0;
+    return FK_OK;
+}
+
+/*
  * The sparse table (17 <= k <= 20) from the retained input, in key-range
  * passes (k_sp_emit):
  *   1. SP_HIST: window count per bucket (the top SP_BUCKET_BITS index bits)
@@ -6002,6 +6894,10 @@ static int sparse_finish(fk_engine *e, int32_t seq) {
     {   /* the HIST launch needs the larger LDS; set it once for every mode */
         const size_t lds = (size_t)SP_WAVES * FK_TILE_BYTES * sizeof(uint64_t) + (size_t)nbk * sizeof(uint32_t);
         HIPCHK(hipFuncSetAttribute((const void *)k_sp_emit, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        for (const void *f : {(const void *)k_kpart<uint32_t>, (const void *)k_kpart<uint64_t>})
+            HIPCHK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(KP_BATCH * 4)));
+        HIPCHK(hipFuncSetAttribute((const void *)k_kp_sort, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(KS_CAP * 4)));
+        HIPCHK(hipFuncSetAttribute((const void *)k_kp_count, hipFuncAttributeMaxDynamicSharedMemorySize, 1 << 17));
     }
     DevScratch acc, bh, ctr;
     if (!acc.alloc(FKS_ACC_N * sizeof(unsigned long long)) || !bh.alloc((size_t)nbk * 8) || !ctr.alloc(24))
@@ -6043,8 +6939,9 @@ static int sparse_finish(fk_engine *e, int32_t seq) {
         if (rc) return rc;
     }
     /* all windows in one pass (the feed counted them): no histogram launch,
-       the keys pass collects the short walks */
-    const bool single = wins <= cap;
+       the keys pass collects the short walks.  Not k = 17: its passes span
+       2^32 keys, which sp_count_runs32 counts instead of sorting */
+    const bool single = wins <= cap && k != 17;
 
     const bool tail = !e->state.hdr && seq >= 1 && seq < k;
     const bool nodes = e->opts.want_nodes != 0;
@@ -6181,9 +7078,16 @@ static int sparse_finish(fk_engine *e, int32_t seq) {
                 int rc = prep_shorts();
                 if (rc) return rc;
             }
-            if (rel32 ? fks_sort_runs32(&e->fks, em.out32, got[0], em.lo, got[0] - got[2], k, e->stream, dacc, out_k,
-                                        out_c, &nw)
-                      : fks_sort_runs(&e->fks, em.out, got[0], k, e->stream, dacc, out_k, out_c, &nw, got[0] - got[2]))
+            bool lib = false;
+            if (rel32) {   /* counted, not sorted (sp_count_runs32) */
+                int rc = sp_count_runs32(e, em.out32, got[0], em.lo, got[0] - got[2], dacc, out_k, out_c, &nw);
+                if (rc) return rc;
+            } else {       /* partitioned and sorted in LDS (sp_sort_runs64) */
+                int rc = sp_sort_runs64(e, em.out, got[0], em.lo, em.hi, got[0] - got[2], dacc, out_k, out_c, &nw, &lib);
+                if (rc) return rc;
+            }
+            /* a part or bucket past k_kp_sort's sizes: the library sort */
+            if (lib && fks_sort_runs(&e->fks, em.out, got[0], k, e->stream, dacc, out_k, out_c, &nw, got[0] - got[2]))
                 return FK_E_HIP;
         }
         if (!nw) continue;

@@ -13,9 +13,8 @@ struct FksState {
     void *tmp = nullptr;          /* rocPRIM temporary storage */
     unsigned long long *small = nullptr;
     uint64_t *cand = nullptr, *cand2 = nullptr;
-    uint32_t *k32 = nullptr;      /* a 32-bit pass's distinct keys (relative) */
     size_t sorted_cap = 0, c64_cap = 0, tmp_cap = 0, small_cap = 0,
-           cand_cap = 0, cand2_cap = 0, k32_cap = 0;
+           cand_cap = 0, cand2_cap = 0;
 };
 
 /* Device accumulators of a sparse finish (unsigned long long[FKS_ACC_N]):
@@ -34,14 +33,7 @@ enum { FKS_ACC_ROLL = 10, FKS_ACC_WPREFIX = 11, FKS_ACC_N = 40 };
  * out of memory). */
 int fks_sort_runs(FksState *st, uint64_t *keys, uint64_t n, int k, hipStream_t s, unsigned long long *dacc,
                   uint64_t *out_keys, uint32_t *out_cnts, uint64_t *nw, uint64_t npads = 0);
-/* The same for a pass whose keys span at most 2^32 (lo <= key < lo + 2^32),
- * emitted as 32-bit keys - lo: half the bytes sorted.  `npads` of the keys
- * are the pad 0xFFFFFFFF, sorted last together with any real key lo +
- * 0xFFFFFFFF; they are taken off that last run's count (the run is dropped
- * when nothing else is in it).  out_keys get the absolute keys. */
-int fks_sort_runs32(FksState *st, uint32_t *keys, uint64_t n, uint64_t lo, uint64_t npads, int k, hipStream_t s,
-                    unsigned long long *dacc, uint64_t *out_keys, uint32_t *out_cnts, uint64_t *nw);
-/* The same for a dense count table of keys [lo, lo + n) (room for its
+/* fks_sort_runs for a dense count table of keys [lo, lo + n) (room for its
  * nonzero entries). */
 int fks_dense_runs(FksState *st, unsigned long long *dense, uint64_t n, uint64_t lo, int k, hipStream_t s,
                    unsigned long long *dacc, uint64_t *out_keys, uint32_t *out_cnts, uint64_t *nw);

@@ -6,13 +6,18 @@
  * The engine keeps the input it was fed and, at finish, builds the table in
  * key-range passes (fk_engine.hip, k_sp_emit): a histogram of the window
  * keys' top bits plans the passes; each pass emits the window indices of its
- * key range (reference order, < 2^40) compactly, and fks_sort_runs radix-sorts
- * and run-length encodes them (rocPRIM): the pass's distinct indices in
- * ascending order -- the trie's DFS order, which is the CSV row order
- * (histo_recursive :699-942) -- with their counts.  A single bucket too large
- * for a sorted pass (a few k-mers repeated billions of times) is counted in
- * a dense table instead (fks_dense_runs).  Device memory is bounded by the
- * input plus one pass, never one slot per input byte.
+ * key range (reference order, < 2^40) compactly, and turns them into the
+ * pass's distinct indices in ascending order -- the trie's DFS order, which
+ * is the CSV row order (histo_recursive :699-942) -- with their counts.
+ * Round 5: the engine does that itself for every pass (fk_engine.hip:
+ * sp_count_runs32 counts a pass of at most 2^32 keys in LDS bins,
+ * sp_sort_runs64 sorts a wider one in LDS); this file keeps the library
+ * (rocPRIM) versions for what those do not take: fks_sort_runs for a pass
+ * whose keys crowd one part past what a block's LDS sorts, fks_dense_runs
+ * for a single bucket too large for any pass (a few k-mers repeated billions
+ * of times), fks_merge_runs for the multi-GPU merge, fks_unique /
+ * fks_short_count for the short walks' nodeCounter.  Device memory is
+ * bounded by the input plus one pass, never one slot per input byte.
  *
  * From each pass's runs, on the GPU:
  *   - the table statistics k_table_stats computes for the dense table
@@ -226,95 +231,6 @@ int fks_sort_runs(FksState *st, uint64_t *keys, uint64_t n, int k, hipStream_t s
     return runs_stats(st, runs, k, s, dacc, out_keys, out_cnts);
 }
 
-/* a 32-bit pass's runs in one read: the absolute keys into the table store,
-   the u32 counts, the statistics and rollover flag (as k_sp_stats) and the
-   prefix histogram (as k_sp_wprefix, adjacent keys from the 32-bit copy) */
-__global__ void __launch_bounds__(256)
-k_sp_stats32(const uint32_t *k32, uint64_t lo, const uint64_t *c64, uint32_t *cnt, uint64_t *out, uint64_t nw, int k,
-             unsigned long long *out10, unsigned long long *big, unsigned long long *hist) {
-    __shared__ unsigned int h[24];
-    if (threadIdx.x < 24) h[threadIdx.x] = 0;
-    __syncthreads();
-    unsigned long long v[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-    unsigned long long wrap = 0;
-    const int fs = 2 * (k - 1);
-    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < nw; i += (uint64_t)gridDim.x * blockDim.x) {
-        const uint32_t r = k32[i];
-        const uint64_t key = lo + r;
-        out[i] = key;
-        const uint64_t c6 = c64[i];
-        const uint32_t c = (uint32_t)c6;   /* the reference's u32 frequency (:110) */
-        cnt[i] = c;
-        wrap |= c6 >> 32;                  /* a count >= 2^32: the rollover exit (:642) */
-        v[0] += 1;
-        v[1] += c;
-        v[2 + (uint32_t)(key & 3)] += c;
-        v[6 + (uint32_t)((key >> fs) & 3)] += c;
-        if (i) {   /* leading zero digits of the 2k-bit difference */
-            const uint64_t diff = key ^ (lo + k32[i - 1]);
-            const int lz = __clzll((long long)diff) - (64 - 2 * k);
-            atomicAdd(&h[lz / 2 + 1], 1u);
-        }
-    }
-    __shared__ unsigned long long sh[4][11];
-    const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-#pragma unroll
-    for (int q = 0; q < 10; q++) v[q] = wsum(v[q]);
-    wrap = wsum(wrap);
-    if (lane == 0) {
-#pragma unroll
-        for (int q = 0; q < 10; q++) sh[w][q] = v[q];
-        sh[w][10] = wrap;
-    }
-    __syncthreads();
-    if (threadIdx.x < 11) {
-        unsigned long long t = 0;
-        for (uint32_t j = 0; j < blockDim.x / 64; j++) t += sh[j][threadIdx.x];
-        if (t) atomicAdd(threadIdx.x < 10 ? &out10[threadIdx.x] : big, t);
-    }
-    if (threadIdx.x < 24 && h[threadIdx.x]) atomicAdd(&hist[threadIdx.x], (unsigned long long)h[threadIdx.x]);
-}
-
-int fks_sort_runs32(FksState *st, uint32_t *keys, uint64_t n, uint64_t lo, uint64_t npads, int k, hipStream_t s,
-                    unsigned long long *dacc, uint64_t *out_keys, uint32_t *out_cnts, uint64_t *nw) {
-    *nw = 0;
-    if (n == 0) return 0;
-    if (ensure((void **)&st->sorted, &st->sorted_cap, n * 4) || ensure((void **)&st->c64, &st->c64_cap, n * 8) ||
-        ensure((void **)&st->k32, &st->k32_cap, n * 4) ||
-        ensure((void **)&st->small, &st->small_cap, 64 * sizeof(unsigned long long)))
-        return -1;
-    uint32_t *sorted = reinterpret_cast<uint32_t *>(st->sorted);
-    size_t tb = 0, tb2 = 0;
-    CK(rocprim::radix_sort_keys(nullptr, tb, keys, sorted, n, 0, 32, s));
-    CK(rocprim::run_length_encode(nullptr, tb2, sorted, n, st->k32, st->c64, st->small, s));
-    if (ensure(&st->tmp, &st->tmp_cap, tb > tb2 ? tb : tb2)) return -1;
-    tb = st->tmp_cap;
-    CK(rocprim::radix_sort_keys(st->tmp, tb, keys, sorted, n, 0, 32, s));
-    tb2 = st->tmp_cap;
-    CK(rocprim::run_length_encode(st->tmp, tb2, sorted, n, st->k32, st->c64, st->small, s));
-    unsigned long long runs = 0;
-    CK(hipMemcpyAsync(&runs, st->small, sizeof runs, hipMemcpyDeviceToHost, s));
-    CK(hipStreamSynchronize(s));
-    if (npads && runs) {
-        /* the last run holds the pads (and maybe the real key lo + 0xFFFFFFFF) */
-        uint64_t last = 0;
-        CK(hipMemcpyAsync(&last, st->c64 + (runs - 1), sizeof last, hipMemcpyDeviceToHost, s));
-        CK(hipStreamSynchronize(s));
-        if (last <= npads) {
-            runs--;
-        } else {
-            last -= npads;
-            CK(hipMemcpyAsync(st->c64 + (runs - 1), &last, sizeof last, hipMemcpyHostToDevice, s));
-            CK(hipStreamSynchronize(s));
-        }
-    }
-    *nw = runs;
-    if (!runs) return 0;
-    hipLaunchKernelGGL(k_sp_stats32, dim3(grid_for(runs)), dim3(256), 0, s, st->k32, lo, st->c64, out_cnts, out_keys,
-                       runs, k, dacc, dacc + FKS_ACC_ROLL, dacc + FKS_ACC_WPREFIX);
-    return hipGetLastError() == hipSuccess ? 0 : -1;
-}
-
 int fks_dense_runs(FksState *st, unsigned long long *dense, uint64_t n, uint64_t lo, int k, hipStream_t s,
                    unsigned long long *dacc, uint64_t *out_keys, uint32_t *out_cnts, uint64_t *nw) {
     *nw = 0;
@@ -416,6 +332,6 @@ int fks_short_count(FksState *st, const uint64_t *shorts, uint64_t ns, const uin
 
 void fks_free(FksState *st) {
     hipFree(st->sorted); hipFree(st->c64);
-    hipFree(st->tmp); hipFree(st->small); hipFree(st->cand); hipFree(st->cand2); hipFree(st->k32);
+    hipFree(st->tmp); hipFree(st->small); hipFree(st->cand); hipFree(st->cand2);
     *st = FksState{};
 }

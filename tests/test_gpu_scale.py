@@ -136,10 +136,11 @@ def test_sparse_genome_10g_key_ranges_vs_oracle(genome10g, k):
     assert abs(r.distinct - want) < 1e-3 * want, (r.distinct, want)
 
 
-@pytest.mark.parametrize("k", [14, 16])
+@pytest.mark.parametrize("k", [14, 15, 16])
 def test_genome_1g_table_range_vs_oracle(k):
-    """k = 14 (4096 slices, two halves per slice) and k = 16 (the second
-    partition level, k_repart + k_count_parts, 16 GiB table) over 1 G bases
+    """k = 14 (4096 slices of 2^16 bins, k_bucket16), k = 15 and k = 16 (the
+    second partition level, k_repart + k_count_parts: 16 parts per coarse
+    slice at k = 15, 64 at k = 16; a 4 / 16 GiB table) over 1 G bases
     of the 80-column genome: table ranges against the oracle's counts of the
     same key ranges"""
     import torch
