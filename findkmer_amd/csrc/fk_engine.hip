@@ -3135,17 +3135,19 @@ struct PartMeta {
 };
 #define REPART_MAXP 64u       /* parts per coarse slice (k = 16) */
 #define REPART_G 8u           /* coarse slices per k_repart block */
-#define REPART_GP (REPART_G * REPART_MAXP)
+#define REPART_GP (REPART_G * REPART_MAXP)   /* parts per block: G x parts per slice <= this */
+#define REPART_METAP 128u     /* meta entries per coarse slice (wide sparse passes: 128 parts, G = 4) */
 #define REPART_CAP 32768u     /* entries per pass-B round: a batch (16 waves x 2048), the longest run */
 static_assert(16u * FK_TILE_BYTES <= REPART_CAP, "a C32 row's run fits one k_repart round");
 
 /* OT = uint16_t: a code's part is its bits [15, 15 + split), stored as its
    low 15 bits (k = 15, 16; k = 17 passes, psh = 15).  OT = uint32_t (wide
    sparse passes): part bits [psh, psh + 6), stored as the low psh bits. */
-template <typename OT>
+template <typename OT, uint32_t G = REPART_G>
 __global__ void __launch_bounds__(1024)
 k_repart(PartGeo pg, OT *out, unsigned long long *alloc, PartMeta *meta, uint64_t cap,
          unsigned long long *err, uint32_t psh) {
+    /* (G coarse slices of 2^split parts: G << split <= REPART_GP, checked by the host) */
     /* per (slice in the group, part): entries, round count / offset /
        cursor, written so far, stream start */
     __shared__ uint32_t cnt[REPART_GP], hc[REPART_GP], ho[REPART_GP], cur[REPART_GP], wr[REPART_GP];
@@ -3154,17 +3156,17 @@ k_repart(PartGeo pg, OT *out, unsigned long long *alloc, PartMeta *meta, uint64_
     __shared__ __attribute__((aligned(16))) OT rbuf[REPART_CAP];
     const uint32_t pmask = (1u << psh) - 1u;
     const uint32_t t = threadIdx.x, wv = t >> 6, lane = t & 63;
-    const uint32_t np = 1u << pg.split, gp = REPART_G * np;   /* parts of the block */
-    const uint32_t b0 = blockIdx.x * REPART_G;                /* its first coarse slice */
+    const uint32_t np = 1u << pg.split, gp = G * np;   /* parts of the block */
+    const uint32_t b0 = blockIdx.x * G;                /* its first coarse slice */
     for (uint32_t i = t; i < gp; i += blockDim.x) cnt[i] = 0;
     __syncthreads();
     const uint32_t nrows = pg.flag && *pg.flag ? 2u * pg.rows : pg.rows;
-    const uint32_t nitems = nrows * REPART_G;   /* (row, slice) pairs, row-major: a row's runs side by side */
+    const uint32_t nitems = nrows * G;   /* (row, slice) pairs, row-major: a row's runs side by side */
     const uint4 *g4 = reinterpret_cast<const uint4 *>(pg.codes);
     /* item i: row i / G, slice b0 + i % G; its codes as 16-B pieces (4 each)
        -- the G lanes of a row read one contiguous span */
     auto each_code = [&](uint32_t i, auto &&f) {
-        const uint32_t r = i / REPART_G, sl = i % REPART_G;
+        const uint32_t r = i / G, sl = i % G;
         const uint32_t e = pg.idx[(size_t)r * pg.nslices + b0 + sl];
         if (e == PART_NO_RUN) return;
         const uint64_t s0 = (uint64_t)r * pg.batch + (e >> 16), s1 = s0 + run_count(e);
@@ -3224,11 +3226,11 @@ k_repart(PartGeo pg, OT *out, unsigned long long *alloc, PartMeta *meta, uint64_
        placement and write-out (each round was a chain of an index load, a
        code load and five barriers: k_repart latency-bound) */
     auto idx_word = [&](uint32_t i) -> uint32_t {
-        return i < nitems ? pg.idx[(size_t)(i / REPART_G) * pg.nslices + b0 + i % REPART_G] : PART_NO_RUN;
+        return i < nitems ? pg.idx[(size_t)(i / G) * pg.nslices + b0 + i % G] : PART_NO_RUN;
     };
     auto span = [&](uint32_t i, uint32_t e, uint64_t &s0, uint64_t &s1) {
         /* (an empty run -- PART_NO_RUN, count 0 -- reads nothing) */
-        s0 = (uint64_t)(i / REPART_G) * pg.batch + (e == PART_NO_RUN ? 0u : e >> 16);
+        s0 = (uint64_t)(i / G) * pg.batch + (e == PART_NO_RUN ? 0u : e >> 16);
         s1 = s0 + run_count(e);
     };
     auto load5 = [&](uint64_t s0, uint64_t s1, uint4 *v) {
@@ -3260,7 +3262,7 @@ k_repart(PartGeo pg, OT *out, unsigned long long *alloc, PartMeta *meta, uint64_
         const uint32_t ien = idx_word(nbase + t);   /* the next round's item */
         uint64_t s0, s1;
         span(i, take ? ie : PART_NO_RUN, s0, s1);
-        const uint32_t sl = i % REPART_G;
+        const uint32_t sl = i % G;
         const uint64_t q0 = s0 >> 2, q1 = (s1 + 3) >> 2;
         auto codes = [&](auto &&f) {
             auto piece = [&](const uint4 &v, uint64_t q) {
@@ -5077,11 +5079,11 @@ static int launch_part(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t l
             e->parts_cap = need;
         }
         if (!e->d_pmeta &&
-            hipMalloc(&e->d_pmeta, (size_t)2048 * REPART_MAXP * sizeof(PartMeta) + 64) != hipSuccess)
+            hipMalloc(&e->d_pmeta, (size_t)2048 * REPART_METAP * sizeof(PartMeta) + 64) != hipSuccess)
             return FK_E_OOM;
         PartMeta *meta = static_cast<PartMeta *>(e->d_pmeta);
         /* [0]: the output claim, [1]: bound-check bits (DevRes::fault) */
-        unsigned long long *alloc = reinterpret_cast<unsigned long long *>(meta + (size_t)2048 * REPART_MAXP);
+        unsigned long long *alloc = reinterpret_cast<unsigned long long *>(meta + (size_t)2048 * REPART_METAP);
         e->d_perr = alloc + 1;
         e->perr_live = true;
         HIPCHK(hipMemsetAsync(alloc, 0, 2 * sizeof(unsigned long long), e->stream));
@@ -6247,19 +6249,28 @@ static int sp_emit_all(fk_engine *e, const SpEmit &em) {
 /* KT = uint32_t: 32-bit relative keys r (slice r >> 21, code r & (2^21 - 1));
    KT = uint64_t: keys lo + r with r < 2^(cs + 11) (slice r >> cs, code r &
    (2^cs - 1), cs <= 29); keys >= hi (pads past the pass's range) are left out */
+/* The top key `tkey` (the pads' value: relative 0xFFFFFFFF, or 4^k - 1 when
+   the pass holds it; ~0 for none) is left out of the partition and only
+   counted into *tcount: the chunk pads of every emitting wave (tens of
+   millions per pass) would otherwise crowd one part, whose k_repart block
+   and LDS bin then serialise the whole pass. */
 template <typename KT>
 __global__ void __launch_bounds__(1024)
-k_kpart(const KT *keys, uint64_t n, PartGeo pg, uint64_t lo, uint64_t hi, uint32_t cs) {
+k_kpart(const KT *keys, uint64_t n, PartGeo pg, uint64_t lo, uint64_t hi, uint32_t cs, uint64_t tkey,
+        unsigned long long *tcount) {
     constexpr bool WIDE = sizeof(KT) == 8;
     __shared__ uint32_t hist[2048], cur[2048];
+    __shared__ uint32_t ntop;
     extern __shared__ uint32_t ent[];   /* KP_BATCH codes */
     const uint32_t t = threadIdx.x;
     const uint32_t sh = WIDE ? cs : 21u;
     const KT cmask = (KT)(((uint64_t)1 << sh) - 1);
     for (uint32_t i = t; i < 2048u; i += 1024u) hist[i] = 0;
+    if (t == 0) ntop = 0;
     const uint64_t per = (uint64_t)pg.rounds * KP_BATCH;
     const uint64_t k0 = blockIdx.x * per, k1 = min(k0 + per, n);
     uint32_t *codes = reinterpret_cast<uint32_t *>(pg.codes);
+    uint32_t mytop = 0;
     for (uint32_t r = 0; r < pg.rounds; r++) {
         const uint32_t row = blockIdx.x * pg.rounds + r;
         const uint64_t b0 = k0 + (uint64_t)r * KP_BATCH;
@@ -6269,22 +6280,35 @@ k_kpart(const KT *keys, uint64_t n, PartGeo pg, uint64_t lo, uint64_t hi, uint32
             for (uint32_t b = t; b < 2048u; b += 1024u) pg.idx[(size_t)row * 2048u + b] = PART_NO_RUN;
             continue;
         }
-        /* relative keys (WIDE: ~0 for a key left out; a 32-bit ~0 is a real
-           key or a pad, which the caller takes off the last bin) */
-        KT v[32];
+        /* each key's slice (two 16-bit slices per word, 0xFFFF: left out --
+           past hi, or the top key) and code: 48 registers where 32 64-bit
+           keys took 64 and spilled */
+        uint32_t cd[32], sp[16];
+#pragma unroll
+        for (uint32_t j = 0; j < 16u; j++) sp[j] = 0xFFFFFFFFu;
 #pragma unroll
         for (uint32_t j = 0; j < 32u; j++) {
-            v[j] = (KT)~(KT)0;
+            cd[j] = 0;
             if (j * 1024u + t < nv) {
                 const KT x = keys[b0 + j * 1024u + t];
-                if (!WIDE) v[j] = x;
-                else if ((uint64_t)x < hi) v[j] = (KT)((uint64_t)x - lo);
+                uint32_t sl = 0xFFFFu;
+                if ((uint64_t)x == tkey) {
+                    mytop++;
+                } else if (!WIDE) {
+                    sl = (uint32_t)x >> 21;
+                    cd[j] = (uint32_t)x & 0x1FFFFFu;
+                } else if ((uint64_t)x < hi) {
+                    const uint64_t r = (uint64_t)x - lo;
+                    sl = (uint32_t)(r >> sh);
+                    cd[j] = (uint32_t)(r & (uint64_t)cmask);
+                }
+                sp[j >> 1] = (j & 1) ? (sp[j >> 1] & 0xFFFFu) | (sl << 16) : (sp[j >> 1] & 0xFFFF0000u) | sl;
             }
         }
-#define KP_IN(j) ((j) * 1024u + t < nv && (!WIDE || v[j] != (KT)~(KT)0))
+#define KP_SL(j) ((sp[(j) >> 1] >> (((j) & 1) * 16)) & 0xFFFFu)
 #pragma unroll
         for (uint32_t j = 0; j < 32u; j++)
-            if (KP_IN(j)) atomicAdd(&hist[(uint32_t)(v[j] >> sh)], 1u);
+            if (KP_SL(j) != 0xFFFFu) atomicAdd(&hist[KP_SL(j)], 1u);
         __syncthreads();
         if (t < 64) {   /* cursors and the row's run words: 32 slices per lane */
             uint32_t sum = 0;
@@ -6301,8 +6325,8 @@ k_kpart(const KT *keys, uint64_t n, PartGeo pg, uint64_t lo, uint64_t hi, uint32
         __syncthreads();
 #pragma unroll
         for (uint32_t j = 0; j < 32u; j++)
-            if (KP_IN(j)) ent[atomicAdd(&cur[(uint32_t)(v[j] >> sh)], 1u)] = (uint32_t)(v[j] & cmask);
-#undef KP_IN
+            if (KP_SL(j) != 0xFFFFu) ent[atomicAdd(&cur[KP_SL(j)], 1u)] = cd[j];
+#undef KP_SL
         __syncthreads();
         /* the row: its runs end at cur[2047] (every entry placed) */
         const uint32_t tot = cur[2047];
@@ -6310,13 +6334,66 @@ k_kpart(const KT *keys, uint64_t n, PartGeo pg, uint64_t lo, uint64_t hi, uint32
         const uint4 *src = reinterpret_cast<const uint4 *>(ent);
         for (uint32_t i = t; i < (tot + 3u) / 4u; i += 1024u) dst[i] = src[i];
     }
+    if (mytop) atomicAdd(&ntop, mytop);
+    __syncthreads();
+    if (t == 0 && ntop) atomicAdd(tcount, (unsigned long long)ntop);
+}
+
+/* A chained scan over the blocks in dispatch order (wave 0 of every block
+   calls it): this block's `total` published (status A: aggregate), the
+   earlier blocks' sum found by looking back 64 flags at a time -- up to the
+   nearest one with status P (inclusive prefix) -- and this block's own
+   inclusive prefix published.  Returns the exclusive prefix.  Every earlier
+   block was dispatched before this one and publishes unconditionally; the
+   spin bound only guards a broken invariant (FK_FAULT_PARTS: the pass fails
+   with FK_E_INTERNAL instead of hanging the GPU). */
+__device__ unsigned long long chain_prefix(unsigned long long *flags, uint32_t blk, uint32_t total,
+                                           unsigned long long *err) {
+    const uint32_t lane = threadIdx.x & 63;
+    const unsigned long long A = 1ull << 62, P = 2ull << 62, M = (1ull << 62) - 1;
+    if (blk == 0) {
+        if (lane == 0) __hip_atomic_store(&flags[0], P | total, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        return 0;
+    }
+    if (lane == 0) __hip_atomic_store(&flags[blk], A | total, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    unsigned long long pre = 0;
+    int64_t j = (int64_t)blk - 1;
+    uint64_t spin = 0;
+    for (;;) {
+        const int64_t idx = j - (int64_t)lane;
+        unsigned long long f = idx >= 0 ? __hip_atomic_load(&flags[idx], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) : P;
+        /* wait only for the flags up to the nearest inclusive prefix (the
+           blocks farther back may still be counting) */
+        for (;;) {
+            const unsigned long long pm0 = __ballot((f >> 62) == 2);
+            const unsigned long long need = pm0 ? (pm0 & (~pm0 + 1)) * 2 - 1 : ~0ull;   /* lanes 0 .. first P */
+            if (!(__ballot((f >> 62) == 0) & need)) break;
+            if (++spin > (1ull << 24)) {
+                if (lane == 0) atomicOr(err, (unsigned long long)FK_FAULT_PARTS);
+                return pre;
+            }
+            __builtin_amdgcn_s_sleep(1);
+            if ((f >> 62) == 0) f = __hip_atomic_load(&flags[idx], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        const unsigned long long pm = __ballot((f >> 62) == 2);
+        const unsigned long long val = f & M;
+        if (pm) {
+            const uint32_t first = (uint32_t)__builtin_ctzll(pm);   /* the nearest prefix */
+            pre += wsum64(lane <= first ? val : 0ull);
+            break;
+        }
+        pre += wsum64(val);
+        j -= 64;
+    }
+    if (lane == 0) __hip_atomic_store(&flags[blk], P | (pre + total), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    return pre;
 }
 
 /* the bins of a part: thread t takes bins [32 t, 32 t + 32) */
 __global__ void __launch_bounds__(1024)
-k_kp_count(const uint16_t *in, const PartMeta *meta, uint64_t cap_in, uint64_t lo, uint64_t npads, uint32_t nparts,
-           int k, unsigned long long *flags, uint64_t *out_k, uint32_t *out_c, unsigned long long *slots,
-           uint64_t *fl, unsigned long long *err) {
+k_kp_count(const uint16_t *in, const PartMeta *meta, uint64_t cap_in, uint64_t lo, uint64_t npads,
+           const unsigned long long *tcount, uint32_t nparts, int k, unsigned long long *flags, uint64_t *out_k,
+           uint32_t *out_c, unsigned long long *slots, uint64_t *fl, unsigned long long *err) {
     extern __shared__ uint32_t bins[];   /* 2^15 */
     __shared__ unsigned long long wred[16][10];
     __shared__ uint32_t hpre[24];
@@ -6334,6 +6411,7 @@ k_kp_count(const uint16_t *in, const PartMeta *meta, uint64_t cap_in, uint64_t l
     }
     const uint4 *g4 = reinterpret_cast<const uint4 *>(in + m.off);
     const uint32_t nq = (m.n + 7u) >> 3;
+#ifndef KPX_NOCNT
     for (uint32_t q = t; q < nq; q += 1024u) {
         const uint4 v = g4[q];
         const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
@@ -6341,9 +6419,12 @@ k_kp_count(const uint16_t *in, const PartMeta *meta, uint64_t cap_in, uint64_t l
         for (int h = 0; h < 8; h++)
             if (q * 8u + (uint32_t)h < m.n) atomicAdd(&bins[(w4[h >> 1] >> (16 * (h & 1))) & 0x7FFFu], 1u);
     }
+#endif
     __syncthreads();
-    /* the pads (relative key 0xFFFFFFFF: the last bin of the last part) */
-    if (t == 0 && npads && blk == nparts - 1u) bins[0x7FFFu] -= (uint32_t)npads;
+    /* the top key (relative 0xFFFFFFFF, the last bin of the last part) was
+       only counted (k_kpart): its real windows, the pads taken off */
+    const unsigned long long extra = blk == nparts - 1u ? *tcount - npads : 0ull;
+    if (t == 0 && extra) bins[0x7FFFu] += (uint32_t)extra;
     __syncthreads();
     uint32_t c[32];
 #pragma unroll
@@ -6352,19 +6433,21 @@ k_kp_count(const uint16_t *in, const PartMeta *meta, uint64_t cap_in, uint64_t l
         c[4 * j] = q.x; c[4 * j + 1] = q.y; c[4 * j + 2] = q.z; c[4 * j + 3] = q.w;
     }
     const int fs = 2 * (k - 1);
-    const uint64_t kb = lo + ((uint64_t)blk << 15) + t * 32u;   /* key of my first bin */
+    const uint64_t kb = lo + ((uint64_t)blk << 15) + t * 32u;   /* key of my first bin (a multiple of 4) */
+    /* statistics with constant register indices (a runtime index into a
+       register array put it in scratch memory): bin j's last base is j & 3,
+       and the first base is the same for all 32 bins */
     uint32_t nz = 0;
-    unsigned long long st[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long l4[4] = {0, 0, 0, 0};
 #pragma unroll
     for (uint32_t j = 0; j < 32u; j++) {
-        const uint32_t x = c[j];
-        const uint64_t key = kb + j;
-        nz += x != 0;
-        st[1] += x;
-        st[2 + (uint32_t)(key & 3)] += x;
-        st[6 + (uint32_t)((key >> fs) & 3)] += x;
+        nz += c[j] != 0;
+        l4[j & 3] += c[j];
     }
-    st[0] = nz;
+    const unsigned long long sum = l4[0] + l4[1] + l4[2] + l4[3];
+    const uint32_t fd = (uint32_t)((kb >> fs) & 3);
+    unsigned long long st[10] = {nz, sum, l4[0], l4[1], l4[2], l4[3], fd == 0 ? sum : 0ull, fd == 1 ? sum : 0ull,
+                                 fd == 2 ? sum : 0ull, fd == 3 ? sum : 0ull};
     /* block scan of the nonzero counts */
     const uint32_t inc = wscan_incl32(nz);
     if (lane == 63) wnz[wv] = inc;
@@ -6377,33 +6460,17 @@ k_kp_count(const uint16_t *in, const PartMeta *meta, uint64_t cap_in, uint64_t l
         total += x;
     }
     const uint32_t off = before + inc - nz;
-    /* chained scan over the parts: publish this part's total, look back */
-    if (t == 0) {
-        const unsigned long long A = 1ull << 62, P = 2ull << 62, M = (1ull << 62) - 1;
-        unsigned long long pre = 0;
-        if (blk == 0) {
-            __hip_atomic_store(&flags[0], P | total, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-        } else {
-            __hip_atomic_store(&flags[blk], A | total, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-            uint32_t j = blk - 1u;
-            /* every earlier part was dispatched before this one and publishes
-               unconditionally; the spin bound only guards against a broken
-               invariant (the pass then fails with FK_E_INTERNAL) */
-            for (uint64_t spin = 0;;) {
-                const unsigned long long f = __hip_atomic_load(&flags[j], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-                if ((f >> 62) == 0) {
-                    if (++spin > (1ull << 26)) { atomicOr(err, (unsigned long long)FK_FAULT_PARTS); break; }
-                    __builtin_amdgcn_s_sleep(1);
-                    continue;
-                }
-                pre += f & M;
-                if ((f >> 62) == 2 || j == 0) break;
-                j--;
-            }
-            __hip_atomic_store(&flags[blk], P | (pre + total), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    /* the parts' chained scan */
+    if (wv == 0) {
+#ifdef KPX_NOLB
+        const unsigned long long pre = 0;
+#else
+        const unsigned long long pre = chain_prefix(flags, blk, total, err);
+#endif
+        if (lane == 0) {
+            bprefix = pre;
+            if (!total) fl[2 * (size_t)blk] = KP_EMPTY;
         }
-        bprefix = pre;
-        if (!total) fl[2 * (size_t)blk] = KP_EMPTY;
     }
     /* the nearest earlier thread holding a nonzero bin (an exclusive max
        scan of t + 1), for the adjacent pair across threads */
@@ -6413,25 +6480,33 @@ k_kp_count(const uint16_t *in, const PartMeta *meta, uint64_t cap_in, uint64_t l
     uint32_t pm = (uint32_t)__shfl_up((int)im, 1, 64);
     if (lane == 0) pm = 0;
     for (uint32_t w = 0; w < wv; w++) pm = max(pm, wmx[w]);
-    const uint64_t base = bprefix + off;
-    uint32_t o = 0;
     uint64_t first = 0, prev = 0;
     bool have = false;
+    /* adjacent keys inside my 32 bins differ in one of the last three bases
+       (depths k, k - 1, k - 2): counted in registers */
+    uint32_t h0 = 0, h1 = 0, h2 = 0;
 #pragma unroll
     for (uint32_t j = 0; j < 32u; j++) {
         if (c[j]) {
             const uint64_t key = kb + j;
-            out_k[base + o] = key;
-            out_c[base + o] = c[j];
             if (have) {   /* first differing base of adjacent keys (k_sp_wprefix) */
-                const int lz = __clzll((long long)(key ^ prev)) - (64 - 2 * k);
-                atomicAdd(&hpre[lz / 2 + 1], 1u);
+                const uint32_t d = (uint32_t)(key ^ prev);   /* < 32 */
+                h0 += d < 4u;
+                h1 += d >= 4u && d < 16u;
+                h2 += d >= 16u;
             } else {
                 first = key;
             }
             prev = key;
             have = true;
-            o++;
+        }
+    }
+    {
+        const uint32_t a0 = wsum32(h0), a1 = wsum32(h1), a2 = wsum32(h2);
+        if (lane == 0) {
+            if (a0) atomicAdd(&hpre[k], a0);
+            if (a1) atomicAdd(&hpre[k - 1], a1);
+            if (a2) atomicAdd(&hpre[k - 2], a2);
         }
     }
     /* every thread's last key in the (now free) bins' LDS */
@@ -6445,6 +6520,37 @@ k_kp_count(const uint16_t *in, const PartMeta *meta, uint64_t cap_in, uint64_t l
     }
     if (nz && !pm) fl[2 * (size_t)blk] = first;
     if (nz && off + nz == total) fl[2 * (size_t)blk + 1] = prev;
+    /* the nonzero bins out, in rounds of KC_STAGE entries staged in the
+       bins' LDS (bin index u16, count u32) and written as contiguous words:
+       one thread writing its own bins strided the stores 64 lines per
+       instruction, and the output (12 B per distinct k-mer, ~90 GB per
+       10 G-base step) cost more than the count */
+    constexpr uint32_t KC_STAGE = 16384u;
+    uint16_t *sidx = reinterpret_cast<uint16_t *>(bins);
+    uint32_t *scnt = bins + KC_STAGE / 2u;
+    const uint64_t kpart = lo + ((uint64_t)blk << 15);
+    for (uint32_t r0 = 0; r0 < total; r0 += KC_STAGE) {
+        __syncthreads();   /* (the staging area is free: lastk read, or the last round written out) */
+        uint32_t o = off;
+#pragma unroll
+        for (uint32_t j = 0; j < 32u; j++) {
+            if (c[j]) {
+                if (o >= r0 && o < r0 + KC_STAGE) {
+                    sidx[o - r0] = (uint16_t)(t * 32u + j);
+                    scnt[o - r0] = c[j];
+                }
+                o++;
+            }
+        }
+        __syncthreads();
+        const uint32_t nr = min(KC_STAGE, total - r0);
+#ifndef KPX_NOOUT
+        for (uint32_t i = t; i < nr; i += 1024u) {
+            out_k[bprefix + r0 + i] = kpart + sidx[i];
+            out_c[bprefix + r0 + i] = scnt[i];
+        }
+#endif
+    }
     /* the rollover check: a bin past 2^32 codes wrapped, so its sum falls
        short of the codes (less the pads) */
     unsigned long long v10[10];
@@ -6458,10 +6564,7 @@ k_kp_count(const uint16_t *in, const PartMeta *meta, uint64_t cap_in, uint64_t l
         unsigned long long a = 0;
         for (uint32_t w = 0; w < 16u; w++) a += wred[w][t];
         if (a) atomicAdd(&slots[(blk % KP_SLOTS) * KP_SLOT_W + t], a);
-        if (t == 1) {
-            const uint64_t want = (uint64_t)m.n - (blk == nparts - 1u ? npads : 0u);
-            if (a != want) atomicOr(&slots[(blk % KP_SLOTS) * KP_SLOT_W + 10], 1ull);
-        }
+        if (t == 1 && a != (uint64_t)m.n + extra) atomicOr(&slots[(blk % KP_SLOTS) * KP_SLOT_W + 10], 1ull);
     }
     if (t < 24 && hpre[t]) atomicAdd(&slots[(blk % KP_SLOTS) * KP_SLOT_W + 11 + t], (unsigned long long)hpre[t]);
 }
@@ -6533,9 +6636,10 @@ __device__ __forceinline__ void wave_sort_bucket(uint32_t *k, uint32_t n) {
 
 __global__ void __launch_bounds__(1024)
 k_kp_sort(const uint32_t *in, const PartMeta *meta, uint64_t cap_in, uint64_t lo, uint32_t psh, uint64_t npads,
-          uint32_t pad_part, uint32_t nparts, int k, unsigned long long *flags, uint64_t *out_k, uint32_t *out_c,
-          unsigned long long *slots, uint64_t *fl, unsigned long long *err) {
-    extern __shared__ uint32_t keys[];   /* KS_CAP */
+          const unsigned long long *tcount, uint32_t top_part, uint32_t nparts, int k, unsigned long long *flags,
+          uint64_t *out_k, uint32_t *out_c, unsigned long long *slots, uint64_t *fl, unsigned long long *err) {
+    extern __shared__ uint32_t keys[];   /* KS_CAP keys, then KS_CAP + 1 u16 run starts */
+    uint16_t *const rs = reinterpret_cast<uint16_t *>(keys + KS_CAP);
     __shared__ uint32_t bh[256], bo[257];
     __shared__ unsigned long long wred[16][10];
     __shared__ uint32_t hpre[24];
@@ -6583,6 +6687,9 @@ k_kp_sort(const uint32_t *in, const PartMeta *meta, uint64_t cap_in, uint64_t lo
     /* 2. each bucket sorted by one wave */
     for (uint32_t b = wv; b < 256u; b += 16u) {
         const uint32_t b0 = bo[b], nb = bo[b + 1] - b0;
+#ifdef KPX_NOSORT
+        continue;
+#endif
         if (nb <= 1) continue;
         if (nb <= 64) wave_sort_bucket<1>(keys + b0, nb);
         else if (nb <= 128) wave_sort_bucket<2>(keys + b0, nb);
@@ -6608,80 +6715,88 @@ k_kp_sort(const uint32_t *in, const PartMeta *meta, uint64_t cap_in, uint64_t lo
     const uint32_t inc = wscan_incl32(nz);
     if (lane == 63) wnz[wv] = inc;
     __syncthreads();
-    uint32_t before = 0, total = 0;
+    uint32_t before = 0, runs = 0;
 #pragma unroll
     for (uint32_t w = 0; w < 16u; w++) {
         const uint32_t x = wnz[w];
         before += w < wv ? x : 0u;
-        total += x;
+        runs += x;
     }
-    /* the pads (the key 4^k - 1 when the pass holds it) come off its run:
-       the last run of the pad part; a run left empty is dropped */
-    const bool padp = npads && blk == pad_part && total;
-    if (padp) {
-        /* the last run's count, from its start */
-        uint32_t ls = nn - 1;
-        while (ls > 0 && keys[ls - 1] == keys[nn - 1]) ls--;
-        if ((uint64_t)(nn - ls) <= npads) total--;   /* (the dropped run is the last one) */
-    }
+    /* the top key 4^k - 1 (when the pass holds it: the last key of the top
+       part) was only counted (k_kpart): its real windows, the pads taken
+       off, are one more run after this part's others */
+    const unsigned long long extra = blk == top_part ? *tcount - npads : 0ull;
+    const uint32_t total = runs + (extra ? 1u : 0u);
     const uint32_t off = before + inc - nz;
-    if (t == 0) {
-        const unsigned long long A = 1ull << 62, P = 2ull << 62, M = (1ull << 62) - 1;
-        unsigned long long pre = 0;
-        if (blk == 0) {
-            __hip_atomic_store(&flags[0], P | total, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-        } else {
-            __hip_atomic_store(&flags[blk], A | total, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-            uint32_t j = blk - 1u;
-            for (uint64_t spin = 0;;) {
-                const unsigned long long f = __hip_atomic_load(&flags[j], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-                if ((f >> 62) == 0) {
-                    if (++spin > (1ull << 26)) { atomicOr(err, (unsigned long long)FK_FAULT_PARTS); break; }
-                    __builtin_amdgcn_s_sleep(1);
-                    continue;
-                }
-                pre += f & M;
-                if ((f >> 62) == 2 || j == 0) break;
-                j--;
-            }
-            __hip_atomic_store(&flags[blk], P | (pre + total), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    /* every run's start in LDS (rs[runs] = the end), so that run r is
+       written by thread r % 1024: contiguous stores */
+    {
+        uint32_t o = off;
+#pragma unroll
+        for (uint32_t j = 0; j < KS_ITEMS; j++) {
+            const uint32_t i = p0 + j;
+            if (i < nn && (i == 0 || keys[i] != keys[i - 1])) rs[o++] = (uint16_t)i;
         }
-        bprefix = pre;
-        if (!total) fl[2 * (size_t)blk] = KP_EMPTY;
+        if (t == 0) rs[runs] = (uint16_t)nn;
+    }
+    if (wv == 0) {
+#ifdef KPX_NOLB
+        const unsigned long long pre = 0;
+#else
+        const unsigned long long pre = chain_prefix(flags, blk, total, err);
+#endif
+        if (lane == 0) {
+            bprefix = pre;
+            if (!total) fl[2 * (size_t)blk] = KP_EMPTY;
+        }
     }
     __syncthreads();
     const int fs = 2 * (k - 1);
     const uint64_t kb = lo + ((uint64_t)blk << psh);
-    unsigned long long st[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-    uint32_t o = 0;
-#pragma unroll
-    for (uint32_t j = 0; j < KS_ITEMS; j++) {
-        const uint32_t i = p0 + j;
-        if (i < nn && (i == 0 || keys[i] != keys[i - 1])) {
-            uint32_t e2 = i + 1;
-            while (e2 < nn && keys[e2] == keys[i]) e2++;
-            uint64_t cnt = e2 - i;
-            const uint64_t key = kb + keys[i];
-            if (padp && e2 == nn) {
-                if (cnt <= npads) continue;   /* (counted off `total` above) */
-                cnt -= npads;
-            }
-            const uint32_t c = (uint32_t)cnt;
-            out_k[bprefix + off + o] = key;
-            out_c[bprefix + off + o] = c;
-            st[0] += 1;
-            st[1] += c;
-            st[2 + (uint32_t)(key & 3)] += c;
-            st[6 + (uint32_t)((key >> fs) & 3)] += c;
-            if (i > 0) {   /* against the run before it, in this part */
-                const int lz = __clzll((long long)(key ^ (kb + keys[i - 1]))) - (64 - 2 * k);
-                atomicAdd(&hpre[lz / 2 + 1], 1u);
-            }
-            if (bprefix + off + o == bprefix) fl[2 * (size_t)blk] = key;
-            if (off + o + 1 == total) fl[2 * (size_t)blk + 1] = key;
-            o++;
+    /* (named accumulators: a runtime index into a register array lives in
+       scratch memory; the first base is the part's, psh < 2k - 2) */
+    unsigned long long l0 = 0, l1 = 0, l2 = 0, l3 = 0, nd = 0;
+    for (uint32_t r = t; r < runs; r += 1024u) {
+        const uint32_t i = rs[r];
+        const uint64_t key = kb + keys[i];
+        const uint32_t c = (uint32_t)rs[r + 1] - i;
+#ifndef KPX_NOOUT
+        out_k[bprefix + r] = key;
+        out_c[bprefix + r] = c;
+#endif
+        const uint32_t ld = (uint32_t)(key & 3);
+        nd += 1;
+        l0 += ld == 0 ? c : 0u;
+        l1 += ld == 1 ? c : 0u;
+        l2 += ld == 2 ? c : 0u;
+        l3 += ld == 3 ? c : 0u;
+        if (r > 0) {   /* against the run before it, in this part */
+            const int lz = __clzll((long long)(key ^ (kb + keys[i - 1]))) - (64 - 2 * k);
+            atomicAdd(&hpre[lz / 2 + 1], 1u);
         }
+        if (r == 0) fl[2 * (size_t)blk] = key;
+        if (r + 1 == total) fl[2 * (size_t)blk + 1] = key;
     }
+    if (t == 0 && extra) {   /* the top key's run, last in the part */
+        const uint64_t key = (1ull << (2 * k)) - 1;
+        const uint32_t c = (uint32_t)extra;
+        out_k[bprefix + runs] = key;
+        out_c[bprefix + runs] = c;
+        nd += 1;
+        l3 += c;   /* (the key 4^k - 1 ends in base T = 3) */
+        if (runs) {
+            const int lz = __clzll((long long)(key ^ (kb + keys[nn - 1]))) - (64 - 2 * k);
+            atomicAdd(&hpre[lz / 2 + 1], 1u);
+        } else {
+            fl[2 * (size_t)blk] = key;
+        }
+        fl[2 * (size_t)blk + 1] = key;
+        if (extra >> 32) atomicOr(&slots[(blk % KP_SLOTS) * KP_SLOT_W + 10], 1ull);   /* a u32 count wrapped */
+    }
+    const unsigned long long sum = l0 + l1 + l2 + l3;
+    const uint32_t fd = (uint32_t)((kb >> fs) & 3);
+    const unsigned long long st[10] = {nd, sum, l0, l1, l2, l3, fd == 0 ? sum : 0ull, fd == 1 ? sum : 0ull,
+                                       fd == 2 ? sum : 0ull, fd == 3 ? sum : 0ull};
     unsigned long long v10[10];
 #pragma unroll
     for (int q = 0; q < 10; q++) v10[q] = wsum64(st[q]);
@@ -6758,7 +6873,7 @@ static int sp_count_runs32(fk_engine *e, const uint32_t *keys, uint64_t n, uint6
     if (!rc) rc = sp_ensure((void **)&e->d_pidx, &e->pidx_cap, (uint64_t)pg.rows * 2048u, sizeof(uint32_t));
     if (!rc) rc = sp_ensure((void **)&e->d_parts, &e->parts_cap, n + 8ull * nparts + 16, sizeof(uint16_t));
     if (rc) return rc;
-    if (!e->d_pmeta && hipMalloc(&e->d_pmeta, (size_t)2048 * REPART_MAXP * sizeof(PartMeta) + 64) != hipSuccess)
+    if (!e->d_pmeta && hipMalloc(&e->d_pmeta, (size_t)2048 * REPART_METAP * sizeof(PartMeta) + 64) != hipSuccess)
         return FK_E_OOM;
     DevScratch flags, slots, fl, res;
     if (!flags.alloc((size_t)nparts * 8) || !slots.alloc((size_t)KP_SLOTS * KP_SLOT_W * 8) ||
@@ -6767,19 +6882,22 @@ static int sp_count_runs32(fk_engine *e, const uint32_t *keys, uint64_t n, uint6
     pg.codes = e->d_codes;
     pg.idx = e->d_pidx;
     PartMeta *meta = static_cast<PartMeta *>(e->d_pmeta);
-    unsigned long long *alloc = reinterpret_cast<unsigned long long *>(meta + (size_t)2048 * REPART_MAXP);
+    unsigned long long *alloc = reinterpret_cast<unsigned long long *>(meta + (size_t)2048 * REPART_METAP);
     HIPCHK(hipMemsetAsync(alloc, 0, 2 * sizeof(unsigned long long), e->stream));
     HIPCHK(hipMemsetAsync(flags.p, 0, (size_t)nparts * 8, e->stream));
     HIPCHK(hipMemsetAsync(slots.p, 0, (size_t)KP_SLOTS * KP_SLOT_W * 8, e->stream));
+    HIPCHK(hipMemsetAsync(res.p, 0, 16, e->stream));
+    unsigned long long *tcount = res.as<unsigned long long>() + 1;
     hipLaunchKernelGGL(k_kpart<uint32_t>, dim3(grid), dim3(1024), (size_t)KP_BATCH * 4, e->stream, keys, n, pg, 0ull,
-                       0ull, 21u);
+                       0ull, 21u, 0xFFFFFFFFull, tcount);
     HIPCHK(hipGetLastError());
     hipLaunchKernelGGL(k_repart<uint16_t>, dim3(2048u / REPART_G), dim3(1024), 0, e->stream, pg, e->d_parts, alloc,
                        meta, (uint64_t)e->parts_cap, alloc + 1, 15u);
     HIPCHK(hipGetLastError());
     hipLaunchKernelGGL(k_kp_count, dim3(nparts), dim3(1024), (size_t)1 << 17, e->stream, (const uint16_t *)e->d_parts,
-                       (const PartMeta *)meta, (uint64_t)e->parts_cap, lo, npads, nparts, k, flags.as<unsigned long long>(),
-                       out_k, out_c, slots.as<unsigned long long>(), fl.as<uint64_t>(), alloc + 1);
+                       (const PartMeta *)meta, (uint64_t)e->parts_cap, lo, npads, (const unsigned long long *)tcount, nparts,
+                       k, flags.as<unsigned long long>(), out_k, out_c, slots.as<unsigned long long>(), fl.as<uint64_t>(),
+                       alloc + 1);
     HIPCHK(hipGetLastError());
     hipLaunchKernelGGL(k_kp_fold, dim3(64), dim3(256), 0, e->stream, (const unsigned long long *)slots.p,
                        (const uint64_t *)fl.p, nparts, k, (const unsigned long long *)flags.p, dacc,
@@ -6806,23 +6924,27 @@ static int sp_sort_runs64(fk_engine *e, const uint64_t *keys, uint64_t n, uint64
     const int k = e->k;
     uint32_t sbits = 33;
     while (sbits < 64 && ((hi - lo - 1) >> sbits)) sbits++;
-    const uint32_t cs = sbits - 11, psh = cs - 6;   /* 2048 coarse slices, 64 parts each */
+    /* 2048 coarse slices of 128 parts (k_repart: 4 slices per block): at k
+       = 20 a pass of up to 2^32 keys leaves ~16 K per part, within k_kp_sort's
+       KS_CAP (64 parts per slice left ~33 K, and every pass took the library
+       sort) */
+    const uint32_t cs = sbits - 11, psh = cs - 7;
     PartGeo pg{};
     pg.nslices = 2048u;
-    pg.split = 6u;
+    pg.split = 7u;
     pg.batch = KP_BATCH;
     const uint32_t grid = (uint32_t)std::max(1, e->cus);
     pg.rounds = (uint32_t)((n + (uint64_t)grid * KP_BATCH - 1) / ((uint64_t)grid * KP_BATCH));
     pg.rows = grid * pg.rounds;
     pg.flag = nullptr;
     const uint64_t ncodes = (uint64_t)pg.rows * KP_BATCH;
-    const uint32_t nparts = 2048u << 6;
+    const uint32_t nparts = 2048u << 7;
     int rc = sp_ensure((void **)&e->d_codes, &e->codes_cap, 2 * ncodes, sizeof(uint16_t));
     if (!rc) rc = sp_ensure((void **)&e->d_pidx, &e->pidx_cap, (uint64_t)pg.rows * 2048u, sizeof(uint32_t));
     /* (the part streams as 32-bit codes: twice the u16 capacity) */
     if (!rc) rc = sp_ensure((void **)&e->d_parts, &e->parts_cap, 2 * (n + 8ull * nparts + 16), sizeof(uint16_t));
     if (rc) return rc;
-    if (!e->d_pmeta && hipMalloc(&e->d_pmeta, (size_t)2048 * REPART_MAXP * sizeof(PartMeta) + 64) != hipSuccess)
+    if (!e->d_pmeta && hipMalloc(&e->d_pmeta, (size_t)2048 * REPART_METAP * sizeof(PartMeta) + 64) != hipSuccess)
         return FK_E_OOM;
     DevScratch flags, slots, fl, res;
     if (!flags.alloc((size_t)nparts * 8) || !slots.alloc((size_t)KP_SLOTS * KP_SLOT_W * 8) ||
@@ -6831,26 +6953,29 @@ static int sp_sort_runs64(fk_engine *e, const uint64_t *keys, uint64_t n, uint64
     pg.codes = e->d_codes;
     pg.idx = e->d_pidx;
     PartMeta *meta = static_cast<PartMeta *>(e->d_pmeta);
-    unsigned long long *alloc = reinterpret_cast<unsigned long long *>(meta + (size_t)2048 * REPART_MAXP);
+    unsigned long long *alloc = reinterpret_cast<unsigned long long *>(meta + (size_t)2048 * REPART_METAP);
     uint32_t *parts32 = reinterpret_cast<uint32_t *>(e->d_parts);
     const uint64_t cap32 = e->parts_cap / 2;
     HIPCHK(hipMemsetAsync(alloc, 0, 2 * sizeof(unsigned long long), e->stream));
     HIPCHK(hipMemsetAsync(flags.p, 0, (size_t)nparts * 8, e->stream));
     HIPCHK(hipMemsetAsync(slots.p, 0, (size_t)KP_SLOTS * KP_SLOT_W * 8, e->stream));
+    HIPCHK(hipMemsetAsync(res.p, 0, 16, e->stream));
+    unsigned long long *tcount = res.as<unsigned long long>() + 1;
+    /* the top key 4^k - 1 (the pads' value; past hi they are left out as
+       out of range) counted apart when the pass holds it */
+    const uint64_t top = (1ull << (2 * k)) - 1;
+    const bool top_in = top >= lo && top < hi;
     hipLaunchKernelGGL(k_kpart<uint64_t>, dim3(grid), dim3(1024), (size_t)KP_BATCH * 4, e->stream, keys, n, pg, lo, hi,
-                       cs);
+                       cs, top_in ? top : ~0ull, tcount);
     HIPCHK(hipGetLastError());
-    hipLaunchKernelGGL(k_repart<uint32_t>, dim3(2048u / REPART_G), dim3(1024), 0, e->stream, pg, parts32, alloc, meta,
+    hipLaunchKernelGGL((k_repart<uint32_t, 4u>), dim3(2048u / 4u), dim3(1024), 0, e->stream, pg, parts32, alloc, meta,
                        cap32, alloc + 1, psh);
     HIPCHK(hipGetLastError());
-    /* the pads are in the pass only when it holds the key 4^k - 1 */
-    const uint64_t top = (1ull << (2 * k)) - 1;
-    const bool pads_in = npads && top >= lo && top < hi;
-    const uint32_t pad_part = pads_in ? (uint32_t)((top - lo) >> psh) : 0u;
-    hipLaunchKernelGGL(k_kp_sort, dim3(nparts), dim3(1024), (size_t)KS_CAP * 4, e->stream, (const uint32_t *)parts32,
-                       (const PartMeta *)meta, cap32, lo, psh, pads_in ? npads : 0ull, pad_part, nparts, k,
-                       flags.as<unsigned long long>(), out_k, out_c, slots.as<unsigned long long>(), fl.as<uint64_t>(),
-                       alloc + 1);
+    const uint32_t top_part = top_in ? (uint32_t)((top - lo) >> psh) : ~0u;
+    hipLaunchKernelGGL(k_kp_sort, dim3(nparts), dim3(1024), (size_t)KS_CAP * 6 + 16, e->stream, (const uint32_t *)parts32,
+                       (const PartMeta *)meta, cap32, lo, psh, top_in ? npads : 0ull, (const unsigned long long *)tcount,
+                       top_part, nparts, k, flags.as<unsigned long long>(), out_k, out_c, slots.as<unsigned long long>(),
+                       fl.as<uint64_t>(), alloc + 1);
     HIPCHK(hipGetLastError());
     unsigned long long ferr = 0;
     HIPCHK(hipMemcpyAsync(&ferr, alloc + 1, 8, hipMemcpyDeviceToHost, e->stream));
@@ -6896,7 +7021,7 @@ static int sparse_finish(fk_engine *e, int32_t seq) {
         HIPCHK(hipFuncSetAttribute((const void *)k_sp_emit, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
         for (const void *f : {(const void *)k_kpart<uint32_t>, (const void *)k_kpart<uint64_t>})
             HIPCHK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(KP_BATCH * 4)));
-        HIPCHK(hipFuncSetAttribute((const void *)k_kp_sort, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(KS_CAP * 4)));
+        HIPCHK(hipFuncSetAttribute((const void *)k_kp_sort, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(KS_CAP * 6 + 16)));
         HIPCHK(hipFuncSetAttribute((const void *)k_kp_count, hipFuncAttributeMaxDynamicSharedMemorySize, 1 << 17));
     }
     DevScratch acc, bh, ctr;
