@@ -6368,7 +6368,7 @@ __device__ unsigned long long chain_prefix(unsigned long long *flags, uint32_t b
             const unsigned long long pm0 = __ballot((f >> 62) == 2);
             const unsigned long long need = pm0 ? (pm0 & (~pm0 + 1)) * 2 - 1 : ~0ull;   /* lanes 0 .. first P */
             if (!(__ballot((f >> 62) == 0) & need)) break;
-            if (++spin > (1ull << 24)) {
+            if (++spin > (1ull << 22)) {
                 if (lane == 0) atomicOr(err, (unsigned long long)FK_FAULT_PARTS);
                 return pre;
             }
@@ -6399,10 +6399,17 @@ k_kp_count(const uint16_t *in, const PartMeta *meta, uint64_t cap_in, uint64_t l
     __shared__ uint32_t hpre[24];
     __shared__ uint32_t wnz[16], wmx[16];
     __shared__ unsigned long long bprefix;
-    const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6, blk = blockIdx.x;
+    __shared__ uint32_t vblk;
+    const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    /* the part: a ticket in the order blocks start (flags[nparts]), not
+       blockIdx -- the chained scan may only wait on blocks that are already
+       running, and across the 8 XCDs (and other processes' kernels)
+       blockIdx order is not start order */
+    if (t == 0) vblk = (uint32_t)atomicAdd(&flags[nparts], 1ull);
     for (uint32_t i = t; i < (1u << 13); i += 1024u) reinterpret_cast<uint4 *>(bins)[i] = make_uint4(0, 0, 0, 0);
     if (t < 24) hpre[t] = 0;
     __syncthreads();
+    const uint32_t blk = vblk;
     PartMeta m = meta[blk];
     if (m.off + m.n > cap_in) {   /* bound check (k_count_parts's) */
         if (t == 0) atomicOr(err, (unsigned long long)FK_FAULT_META);
@@ -6645,12 +6652,16 @@ k_kp_sort(const uint32_t *in, const PartMeta *meta, uint64_t cap_in, uint64_t lo
     __shared__ uint32_t hpre[24];
     __shared__ uint32_t wnz[16];
     __shared__ unsigned long long bprefix;
-    __shared__ uint32_t bad;
-    const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6, blk = blockIdx.x;
+    __shared__ uint32_t bad, vblk;
+    const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6;
     if (t < 256) bh[t] = 0;
     if (t < 24) hpre[t] = 0;
-    if (t == 0) bad = 0;
+    if (t == 0) {
+        bad = 0;
+        vblk = (uint32_t)atomicAdd(&flags[nparts], 1ull);   /* (k_kp_count: start order) */
+    }
     __syncthreads();
+    const uint32_t blk = vblk;
     PartMeta m = meta[blk];
     if (m.off + m.n > cap_in) {
         if (t == 0) atomicOr(err, (unsigned long long)FK_FAULT_META);
@@ -6876,7 +6887,7 @@ static int sp_count_runs32(fk_engine *e, const uint32_t *keys, uint64_t n, uint6
     if (!e->d_pmeta && hipMalloc(&e->d_pmeta, (size_t)2048 * REPART_METAP * sizeof(PartMeta) + 64) != hipSuccess)
         return FK_E_OOM;
     DevScratch flags, slots, fl, res;
-    if (!flags.alloc((size_t)nparts * 8) || !slots.alloc((size_t)KP_SLOTS * KP_SLOT_W * 8) ||
+    if (!flags.alloc((size_t)(nparts + 1) * 8) || !slots.alloc((size_t)KP_SLOTS * KP_SLOT_W * 8) ||
         !fl.alloc((size_t)nparts * 16) || !res.alloc(16))
         return FK_E_OOM;
     pg.codes = e->d_codes;
@@ -6884,7 +6895,7 @@ static int sp_count_runs32(fk_engine *e, const uint32_t *keys, uint64_t n, uint6
     PartMeta *meta = static_cast<PartMeta *>(e->d_pmeta);
     unsigned long long *alloc = reinterpret_cast<unsigned long long *>(meta + (size_t)2048 * REPART_METAP);
     HIPCHK(hipMemsetAsync(alloc, 0, 2 * sizeof(unsigned long long), e->stream));
-    HIPCHK(hipMemsetAsync(flags.p, 0, (size_t)nparts * 8, e->stream));
+    HIPCHK(hipMemsetAsync(flags.p, 0, (size_t)(nparts + 1) * 8, e->stream));   /* (+ the block tickets) */
     HIPCHK(hipMemsetAsync(slots.p, 0, (size_t)KP_SLOTS * KP_SLOT_W * 8, e->stream));
     HIPCHK(hipMemsetAsync(res.p, 0, 16, e->stream));
     unsigned long long *tcount = res.as<unsigned long long>() + 1;
@@ -6947,7 +6958,7 @@ static int sp_sort_runs64(fk_engine *e, const uint64_t *keys, uint64_t n, uint64
     if (!e->d_pmeta && hipMalloc(&e->d_pmeta, (size_t)2048 * REPART_METAP * sizeof(PartMeta) + 64) != hipSuccess)
         return FK_E_OOM;
     DevScratch flags, slots, fl, res;
-    if (!flags.alloc((size_t)nparts * 8) || !slots.alloc((size_t)KP_SLOTS * KP_SLOT_W * 8) ||
+    if (!flags.alloc((size_t)(nparts + 1) * 8) || !slots.alloc((size_t)KP_SLOTS * KP_SLOT_W * 8) ||
         !fl.alloc((size_t)nparts * 16) || !res.alloc(16))
         return FK_E_OOM;
     pg.codes = e->d_codes;
@@ -6957,7 +6968,7 @@ static int sp_sort_runs64(fk_engine *e, const uint64_t *keys, uint64_t n, uint64
     uint32_t *parts32 = reinterpret_cast<uint32_t *>(e->d_parts);
     const uint64_t cap32 = e->parts_cap / 2;
     HIPCHK(hipMemsetAsync(alloc, 0, 2 * sizeof(unsigned long long), e->stream));
-    HIPCHK(hipMemsetAsync(flags.p, 0, (size_t)nparts * 8, e->stream));
+    HIPCHK(hipMemsetAsync(flags.p, 0, (size_t)(nparts + 1) * 8, e->stream));   /* (+ the block tickets) */
     HIPCHK(hipMemsetAsync(slots.p, 0, (size_t)KP_SLOTS * KP_SLOT_W * 8, e->stream));
     HIPCHK(hipMemsetAsync(res.p, 0, 16, e->stream));
     unsigned long long *tcount = res.as<unsigned long long>() + 1;

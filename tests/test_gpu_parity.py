@@ -165,10 +165,10 @@ def mixed_input(seed, n):
     return b"".join(parts)
 
 
-@pytest.mark.parametrize("seed", range(6))
+@pytest.mark.parametrize("seed", range(3))
 @pytest.mark.parametrize("k", [2, 5, 6, 7, 9, 11, 13])
 def test_mixed_random(seed, k):
-    data = mixed_input(1000 + seed, 1_500_000 + 300_000 * seed)
+    data = mixed_input(1000 + 2 * seed, 1_500_000 + 600_000 * seed)
     assert_same(data, k)
 
 
