@@ -18,3 +18,6 @@ int fkc_reduce_i32(fk_comm *c, int32_t *buf, size_t n, int root, hipStream_t s);
 /* in-place reduce-scatter: the sum of buf[0, world * per_rank) over the
    ranks; rank r receives its block at buf + r * per_rank */
 int fkc_reduce_scatter_i32(fk_comm *c, int32_t *buf, size_t per_rank, hipStream_t s);
+/* out of place: the sum of send[0, world * per_rank) over the ranks; rank
+   r receives its block at buf + r * per_rank (buf's other blocks untouched) */
+int fkc_reduce_scatter_from_i32(fk_comm *c, const int32_t *send, int32_t *buf, size_t per_rank, hipStream_t s);

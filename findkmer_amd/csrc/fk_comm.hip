@@ -147,6 +147,14 @@ int fkc_reduce_scatter_i32(fk_comm *c, int32_t *buf, size_t per_rank, hipStream_
                : FK_E_RCCL;
 }
 
+int fkc_reduce_scatter_from_i32(fk_comm *c, const int32_t *send, int32_t *buf, size_t per_rank, hipStream_t s) {
+    if (!c || !c->nc || !rccl().ok) return FK_E_RCCL;
+    return rccl().reduce_scatter(send, buf + (size_t)c->rank * per_rank, per_rank, ncclInt32, ncclSum, c->nc, s) ==
+                   ncclSuccess
+               ? FK_OK
+               : FK_E_RCCL;
+}
+
 /* What RCCL itself reports for the communicator: its rank count, this
    rank and the device it drives (-1 where this RCCL lacks the query). */
 extern "C" int fk_comm_info(fk_comm *c, int *nranks, int *rank, int *device) {

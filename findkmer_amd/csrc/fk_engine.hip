@@ -6077,11 +6077,22 @@ static int stitched_exchange(fk_engine *e, fk_comm *comm, int32_t *merge, int32_
         v[10] = res.unknown_chars; v[11] = res.scanned_bytes;
         v[12] = rank == first_end ? 1u : 0u;
         v[13] = rank == last ? (uint64_t)res.unterminated_header : 0u;
+    }
+    /* the reduce-scatter reads the engine's own table when its blocks divide
+       it exactly (a power-of-two world): no copy of the whole table into
+       the merge buffer first (k = 16: 16 GiB, ~5 ms per step); a rank whose
+       shard the stream never reached sends zeros (its table, zeroed: the
+       engine's count is discarded anyway) */
+    const bool direct = scatter && tw == e->nbins;
+    if (direct) {
+        if (!counting) HIPCHK(hipMemsetAsync(e->d_table, 0, e->nbins * sizeof(uint32_t), e->stream));
+    } else if (counting) {
         HIPCHK(hipMemcpyAsync(merge, e->d_table, e->nbins * sizeof(uint32_t), hipMemcpyDeviceToDevice, e->stream));
     } else {
         HIPCHK(hipMemsetAsync(merge, 0, e->nbins * sizeof(uint32_t), e->stream));
     }
-    if (tw > e->nbins) HIPCHK(hipMemsetAsync(merge + e->nbins, 0, (tw - e->nbins) * sizeof(uint32_t), e->stream));
+    if (!direct && tw > e->nbins)
+        HIPCHK(hipMemsetAsync(merge + e->nbins, 0, (tw - e->nbins) * sizeof(uint32_t), e->stream));
     uint32_t *limbs = e->h_rows + 32 + e->rows_cap;   /* pinned staging */
     for (int i = 0; i < FK_PACK_COUNTERS; i++)
         for (int j = 0; j < 4; j++) limbs[4 * i + j] = (uint32_t)((v[i] >> (16 * j)) & 0xFFFFu);
@@ -6093,7 +6104,8 @@ static int stitched_exchange(fk_engine *e, fk_comm *comm, int32_t *merge, int32_
            keeps bins [r * S, (r + 1) * S) of the sum, S = tw / world; the
            counters and every slice's (sum, distinct) are all-reduced */
         const uint64_t S = tw / (uint64_t)world;
-        rc = fkc_reduce_scatter_i32(comm, merge, S, e->stream);
+        rc = direct ? fkc_reduce_scatter_from_i32(comm, reinterpret_cast<const int32_t *>(e->d_table), merge, S, e->stream)
+                    : fkc_reduce_scatter_i32(comm, merge, S, e->stream);
         if (rc) return rc;
         const uint64_t lo = (uint64_t)rank * S, n = lo < e->nbins ? std::min(S, e->nbins - lo) : 0;
         HIPCHK(hipMemsetAsync(e->d_tmp, 0, 2 * sizeof(unsigned long long), e->stream));
