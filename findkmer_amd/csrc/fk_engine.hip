@@ -1768,20 +1768,27 @@ k_redo(const uint8_t *buf, uint64_t len, int64_t lo, int k, uint64_t maskk, uint
  *   SP_DENSE the windows with lo <= key < hi counted in a dense u64 table
  *            (one bucket too large for a sorted pass: few distinct keys).
  */
+/* SP_KEYS: one key range [lo, hi) of a walk and its list */
+#define SP_MAXP 4u                  /* key ranges (passes) one SP_KEYS walk emits (round 5) */
+struct SpPass {
+    uint64_t lo, hi;
+    uint64_t *out;                  /* the keys, or */
+    uint32_t *out32;                /* ... (a range of <= 2^32 keys) key - lo as 32 bits */
+    uint64_t cap;                   /* slots of the list */
+    unsigned long long *ctr;        /* [0] slots claimed (whole SP_CHUNKs), [1] windows written (the rest: pads) */
+};
 struct SpEmit {
     int mode;
     uint32_t shift;                 /* bucket of a key: key >> shift */
-    uint64_t lo, hi;                /* SP_KEYS, SP_DENSE: the key range [lo, hi) */
+    uint64_t lo, hi;                /* SP_DENSE: the key range [lo, hi) */
     unsigned long long *bhist;      /* SP_HIST: window count per bucket */
     uint32_t nbuckets;
     uint64_t *shorts;               /* SP_HIST: the short walks */
     unsigned long long *nshort;
     uint64_t short_cap;
-    uint64_t *out;                  /* SP_KEYS */
-    uint32_t *out32;                /* ... a pass spanning <= 2^32 keys: key - lo as 32 bits instead (or nullptr) */
-    unsigned long long *nout;       /* ... slots claimed (whole SP_CHUNKs) */
-    uint64_t out_cap;
-    unsigned long long *nreal;      /* ... windows written (the rest of the claimed slots: pads) */
+    uint32_t np;                    /* SP_KEYS: the walk's key ranges, ascending (unused: lo = ~0) */
+    uint64_t gend;                  /* ... the last range's hi */
+    SpPass ps[SP_MAXP];
     unsigned long long *dense;      /* SP_DENSE: count of key lo + i */
 };
 enum { SP_HIST = 1, SP_KEYS = 2, SP_DENSE = 3 };
@@ -1799,43 +1806,71 @@ struct SpOut {
     uint32_t fill;    /* slots of it used (SP_CHUNK: none claimed yet) */
     uint64_t real;    /* windows written by the wave */
 };
-/* the wave's tot entries of this tile: slots for positions 0..tot-1 (a new
-   chunk claimed when the current one runs out; tot <= one tile < SP_CHUNK) */
-__device__ __forceinline__ uint64_t sp_claim(const SpEmit &em, SpOut &o, uint32_t tot, uint64_t &nb, uint32_t &rem) {
-    rem = SP_CHUNK - o.fill;
-    nb = 0;
-    if (tot > rem) {
-        unsigned long long b = 0;
-        if ((threadIdx.x & 63) == 0) b = atomicAdd(em.nout, (unsigned long long)SP_CHUNK);
-        nb = rdlane64(b, 0);
-    }
-    return o.base + o.fill;
+/* One window per lane (v, or SP_EMPTY / a short walk: none) into its key
+   range's list, every lane of the wave calling together.  The ranges are
+   told apart by a wave multisplit (3 ballots: range bits 0 and 1, and
+   "in a range"), each range's entries placed at its chunk's fill point in
+   lane order; a range claims a new SP_CHUNK (one atomic) when this step's
+   entries run past its chunk.  One walk thus emits every range's keys:
+   round 4 walked the input once per range, computing every window's key
+   twice each time. */
+static_assert(SP_MAXP == 4u, "sp_range compares three range starts");
+/* the range of key v (SP_MAXP: none).  The host groups consecutive passes
+   only: between two ranges lie empty buckets, which hold no key */
+__device__ __forceinline__ uint32_t sp_range(const SpEmit &em, uint64_t v) {
+    if (v < em.ps[0].lo || v >= em.gend) return SP_MAXP;
+    return (uint32_t)(v >= em.ps[1].lo) + (uint32_t)(v >= em.ps[2].lo) + (uint32_t)(v >= em.ps[3].lo);
 }
-__device__ __forceinline__ uint64_t sp_slot_at(const SpOut &o, uint64_t cur, uint64_t nb, uint32_t rem, uint64_t p) {
-    return p < rem ? cur + p : nb + (p - rem);
-}
-__device__ __forceinline__ void sp_advance(SpOut &o, uint32_t tot, uint64_t nb, uint32_t rem) {
-    if (tot > rem) { o.base = nb; o.fill = tot - rem; }
-    else o.fill += tot;
-    o.real += tot;
-}
-/* one window key to its slot (a 32-bit pass: relative to lo) */
-__device__ __forceinline__ void sp_put(const SpEmit &em, uint64_t at, uint64_t v) {
-    if (at >= em.out_cap) return;
-    if (em.out32) em.out32[at] = (uint32_t)(v - em.lo);
-    else em.out[at] = v;
-}
-/* the end of the wave's walk: pad its chunk (4^k - 1, or 0xFFFFFFFF in a
-   32-bit pass), count its windows */
-__device__ __forceinline__ void sp_close(const SpEmit &em, const SpOut &o, uint64_t pad) {
-    const uint32_t lane = threadIdx.x & 63;
-    if (o.fill < SP_CHUNK)
-        for (uint32_t i = o.fill + lane; i < SP_CHUNK; i += 64u) {
-            if (o.base + i >= em.out_cap) continue;
-            if (em.out32) em.out32[o.base + i] = 0xFFFFFFFFu;
-            else em.out[o.base + i] = pad;
+__device__ __forceinline__ void sp_place(const SpEmit &em, SpOut (&so)[SP_MAXP], uint64_t v, uint32_t lane) {
+    const uint32_t q = sp_range(em, v);
+    const unsigned long long bv = __ballot(q < SP_MAXP);
+    if (!bv) return;
+    const unsigned long long b0 = __ballot((q & 1u) != 0u), b1 = __ballot((q & 2u) != 0u);
+    const unsigned long long lt = (1ull << lane) - 1ull;
+#pragma unroll
+    for (uint32_t i = 0; i < SP_MAXP; i++) {
+        if (i >= em.np) break;
+        const unsigned long long mi = bv & ((i & 1u) ? b0 : ~b0) & ((i & 2u) ? b1 : ~b1);
+        if (!mi) continue;
+        const uint32_t cnt = (uint32_t)__popcll(mi);
+        const uint32_t rem = SP_CHUNK - so[i].fill;
+        uint64_t nb = 0;
+        if (cnt > rem) {
+            unsigned long long c = 0;
+            if (lane == 0) c = atomicAdd(em.ps[i].ctr, (unsigned long long)SP_CHUNK);
+            nb = rdlane64(c, 0);
         }
-    if (lane == 0 && o.real) atomicAdd(em.nreal, (unsigned long long)o.real);
+        if (q == i) {
+            const uint64_t p = (uint64_t)__popcll(mi & lt);
+            const uint64_t at = p < rem ? so[i].base + so[i].fill + p : nb + (p - rem);
+#ifndef SPX_NOSTORE
+            if (at < em.ps[i].cap) {
+                if (em.ps[i].out32) em.ps[i].out32[at] = (uint32_t)(v - em.ps[i].lo);
+                else em.ps[i].out[at] = v;
+            }
+#endif
+        }
+        if (cnt > rem) { so[i].base = nb; so[i].fill = cnt - rem; }
+        else so[i].fill += cnt;
+        so[i].real += cnt;
+    }
+}
+/* the end of the wave's walk: pad each range's chunk (4^k - 1, or
+   0xFFFFFFFF in a 32-bit list), count its windows */
+__device__ __forceinline__ void sp_close(const SpEmit &em, const SpOut (&so)[SP_MAXP], uint64_t pad) {
+    const uint32_t lane = threadIdx.x & 63;
+#pragma unroll
+    for (uint32_t q = 0; q < SP_MAXP; q++) {
+        if (q >= em.np) break;
+        const SpPass &ps = em.ps[q];
+        if (so[q].fill < SP_CHUNK)
+            for (uint32_t i = so[q].fill + lane; i < SP_CHUNK; i += 64u) {
+                if (so[q].base + i >= ps.cap) continue;
+                if (ps.out32) ps.out32[so[q].base + i] = 0xFFFFFFFFu;
+                else ps.out[so[q].base + i] = pad;
+            }
+        if (lane == 0 && so[q].real) atomicAdd(ps.ctr + 1, (unsigned long long)so[q].real);
+    }
 }
 
 /* The windows of a fast tile (contiguous layout, tile_fast's Emit) as
@@ -1848,7 +1883,7 @@ __device__ __forceinline__ void sp_close(const SpEmit &em, const SpOut &o, uint6
  * -- up to 20 bases from two words, which the 16-base {C, S2} of the dense
  * path cannot give. */
 __device__ __forceinline__ void sp_fast_emit(const SpEmit &em, const Emit &fe, uint64_t c0, uint64_t maskk,
-                                             uint32_t *bh, uint32_t lane, SpOut &so) {
+                                             uint32_t *bh, uint32_t lane, SpOut (&so)[SP_MAXP], uint64_t *stg) {
     const uint64_t pv0 = ((uint64_t)from_prev_lane(fe.BC, (uint32_t)(c0 >> 32)) << 32) |
                          from_prev_lane(fe.B2, (uint32_t)c0);
     const uint64_t pv1 = ((uint64_t)fe.AC << 32) | fe.A2;
@@ -1863,28 +1898,65 @@ __device__ __forceinline__ void sp_fast_emit(const SpEmit &em, const Emit &fe, u
         return fk_sigma(((pv << (2u * (j + 1u))) | (uint64_t)(R >> (2u * (D - 1u - j)))) & maskk);
     };
     if (em.mode == SP_KEYS) {
-        uint32_t mine = 0;
-#pragma unroll 8
+        /* the tile's <= 2048 windows staged in the wave's slots, grouped by
+           range (a wave scan of each lane's per-range counts, packed two
+           16-bit fields a word), then copied out range by range, 64
+           consecutive entries a store */
+        uint64_t kv[32];
+        uint32_t c01 = 0, c23 = 0;
+#pragma unroll
         for (uint32_t jj = 0; jj < 32u; jj++) {
-            const uint64_t v = key(jj);
-            mine += v >= em.lo && v < em.hi ? 1u : 0u;
+            kv[jj] = key(jj);
+            const uint32_t q = sp_range(em, kv[jj]), inc = 1u << (16u * (q & 1u));
+            c01 += q < 2u ? inc : 0u;
+            c23 += (q - 2u) < 2u ? inc : 0u;
         }
-        const uint32_t tot = wsum32(mine);
-        if (!tot) return;
-        uint64_t nb;
-        uint32_t rem;
-        const uint64_t cur = sp_claim(em, so, tot, nb, rem);
-        uint64_t run = 0;
+        const uint32_t i01 = wscan_incl32(c01), i23 = wscan_incl32(c23);
+        const uint32_t t01 = rdlane(i01, 63), t23 = rdlane(i23, 63);
+        const uint32_t T[4] = {t01 & 0xFFFFu, t01 >> 16, t23 & 0xFFFFu, t23 >> 16};
+        const uint32_t S[4] = {0u, T[0], T[0] + T[1], T[0] + T[1] + T[2]};
+        const uint32_t e01 = i01 - c01, e23 = i23 - c23;
+        uint32_t p0 = e01 & 0xFFFFu, p1 = S[1] + (e01 >> 16), p2 = S[2] + (e23 & 0xFFFFu), p3 = S[3] + (e23 >> 16);
+#pragma unroll
         for (uint32_t jj = 0; jj < 32u; jj++) {
-            const uint64_t v = key(jj);
-            const bool m = v >= em.lo && v < em.hi;
-            const uint64_t bal = __ballot(m);
-            if (m) {
-                sp_put(em, sp_slot_at(so, cur, nb, rem, run + (uint64_t)__popcll(bal & ((1ull << lane) - 1ull))), v);
+            const uint32_t q = sp_range(em, kv[jj]);
+            if (q < SP_MAXP) {
+                const uint32_t at = q == 0u ? p0 : q == 1u ? p1 : q == 2u ? p2 : p3;
+                stg[at] = kv[jj];
+                p0 += q == 0u; p1 += q == 1u; p2 += q == 2u; p3 += q == 3u;
             }
-            run += (uint64_t)__popcll(bal);
         }
-        sp_advance(so, tot, nb, rem);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+        for (uint32_t q = 0; q < SP_MAXP; q++) {
+            if (q >= em.np) break;
+            const uint32_t t = T[q];
+            if (!t) continue;
+            const SpPass &ps = em.ps[q];
+            const uint32_t rem = SP_CHUNK - so[q].fill;
+            uint64_t nb = 0;
+            if (t > rem) {   /* (t <= 2048 < SP_CHUNK: one new chunk at most) */
+                unsigned long long c = 0;
+                if (lane == 0) c = atomicAdd(ps.ctr, (unsigned long long)SP_CHUNK);
+                nb = rdlane64(c, 0);
+            }
+            for (uint32_t j = lane; j < t; j += 64u) {
+                const uint64_t v = stg[S[q] + j];
+                const uint64_t at = j < rem ? so[q].base + so[q].fill + j : nb + (j - rem);
+#ifndef SPX_NOSTORE
+                if (at < ps.cap) {
+                    if (ps.out32) ps.out32[at] = (uint32_t)(v - ps.lo);
+                    else ps.out[at] = v;
+                }
+#endif
+            }
+            if (t > rem) { so[q].base = nb; so[q].fill = t - rem; }
+            else so[q].fill += t;
+            so[q].real += t;
+        }
+        __builtin_amdgcn_wave_barrier();
     } else if (em.mode == SP_DENSE) {
 #pragma unroll 8
         for (uint32_t jj = 0; jj < 32u; jj++) {
@@ -1913,7 +1985,9 @@ k_sp_emit(const uint8_t *buf, uint64_t len, int k, uint64_t maskk, const XState 
     }
     Ctx cx{buf, len, 0, nullptr, nullptr, nullptr, nullptr, nullptr, maskk, 0, k, nullptr, slots};
     const uint64_t nw = (uint64_t)gridDim.x * SP_WAVES;
-    SpOut so{0, SP_CHUNK, 0};   /* SP_KEYS: the wave's output chunk */
+    SpOut so[SP_MAXP];          /* SP_KEYS: the wave's output chunk in each range's list */
+#pragma unroll
+    for (uint32_t q = 0; q < SP_MAXP; q++) so[q] = SpOut{0, SP_CHUNK, 0};
     for (uint64_t r = (uint64_t)blockIdx.x * SP_WAVES + wv; r < nranges; r += nw) {
         const uint64_t c0 = r * cpw, c1 = min(c0 + cpw, nchunks);
         const uint64_t rb = c0 * FK_CHUNK_BYTES, re = min(c1 * FK_CHUNK_BYTES, len);
@@ -1949,7 +2023,7 @@ k_sp_emit(const uint8_t *buf, uint64_t len, int k, uint64_t maskk, const XState 
                 Emit fe{0, 0, 0, 0, false, false, false};
                 if (tb + FK_TILE_BYTES <= re && st.hdr == 0 &&
                     tile_fast<true, H_EMIT, false>(cx, w, st, f, cnt, 1u, &fe)) {
-                    if (fe.deep) sp_fast_emit(em, fe, c0, maskk, bh, lane, so);
+                    if (fe.deep) sp_fast_emit(em, fe, c0, maskk, bh, lane, so, slots);
                     continue;
                 }
             }
@@ -1958,33 +2032,17 @@ k_sp_emit(const uint8_t *buf, uint64_t len, int k, uint64_t maskk, const XState 
             for (uint32_t j = 0; j < FK_LANE_BYTES; j++) slots[j * 64u + lane] = SP_EMPTY;
             tile_general<true, H_SPARSE>(cx, w, nb, 0u, st, f, cnt, 1u);
             if (em.mode == SP_KEYS) {
-                uint32_t mine = 0;
+                if (em.shorts) {   /* (a single pass: no SP_HIST) */
 #pragma unroll 8
-                for (uint32_t j = 0; j < FK_LANE_BYTES; j++) {
-                    const uint64_t v = slots[j * 64u + lane];
-                    mine += v >= em.lo && v < em.hi ? 1u : 0u;
-                    if (em.shorts && v >= SP_SHORT && v != SP_EMPTY) {   /* (a single pass: no SP_HIST) */
-                        const unsigned long long i = atomicAdd(em.nshort, 1ull);
-                        if (i < em.short_cap) em.shorts[i] = v;
-                    }
-                }
-                const uint32_t tot = wsum32(mine);
-                if (tot) {
-                    uint64_t nb;
-                    uint32_t rem;
-                    const uint64_t cur = sp_claim(em, so, tot, nb, rem);
-                    uint64_t run = 0;
                     for (uint32_t j = 0; j < FK_LANE_BYTES; j++) {
                         const uint64_t v = slots[j * 64u + lane];
-                        const bool m = v >= em.lo && v < em.hi;
-                        const uint64_t bal = __ballot(m);
-                        if (m) {
-                            sp_put(em, sp_slot_at(so, cur, nb, rem, run + (uint64_t)__popcll(bal & ((1ull << lane) - 1ull))), v);
+                        if (v >= SP_SHORT && v != SP_EMPTY) {
+                            const unsigned long long i = atomicAdd(em.nshort, 1ull);
+                            if (i < em.short_cap) em.shorts[i] = v;
                         }
-                        run += (uint64_t)__popcll(bal);
                     }
-                    sp_advance(so, tot, nb, rem);
                 }
+                for (uint32_t j = 0; j < FK_LANE_BYTES; j++) sp_place(em, so, slots[j * 64u + lane], lane);
             } else if (em.mode == SP_DENSE) {
 #pragma unroll 8
                 for (uint32_t j = 0; j < FK_LANE_BYTES; j++) {
@@ -3000,8 +3058,8 @@ __device__ __forceinline__ void walk_runs(const PartGeo &pg, const uint32_t *ix,
     }
 }
 
-/* the heavy (pair or plain) slices' walk shape: 4 lanes per run, 2 rows x 5
-   pieces in flight (k_bucket_count's); the singles' slices hold a few codes
+/* the heavy (pair or plain) slices' walk shape: 4 lanes per run, 2 rows x 3
+   pieces in flight (QL 1, 2, 8 and U 4, 5 measured slower); the singles' slices hold a few codes
    per run, so a lane per run and 4 rows in flight (their walk is a chain of
    index and code loads: with the heavy shape the 64 single-slice blocks of
    k = 11 took ~0.3 ms, which the pair slices' last blocks waited out) */
@@ -3020,7 +3078,7 @@ __device__ __forceinline__ void walk_runs(const PartGeo &pg, const uint32_t *ix,
 #define B16_ROWS 2
 #endif
 #ifndef B16_U
-#define B16_U 5
+#define B16_U 3   /* (5: k = 12 1.250, 13 1.837, 14 3.348 ms per G-base; 3: 1.228, 1.820, 3.294) */
 #endif
 #ifndef B16L_QL
 #define B16L_QL 1
@@ -7047,8 +7105,9 @@ static int sparse_finish(fk_engine *e, int32_t seq) {
         HIPCHK(hipFuncSetAttribute((const void *)k_kp_sort, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(KS_CAP * 6 + 16)));
         HIPCHK(hipFuncSetAttribute((const void *)k_kp_count, hipFuncAttributeMaxDynamicSharedMemorySize, 1 << 17));
     }
-    DevScratch acc, bh, ctr;
-    if (!acc.alloc(FKS_ACC_N * sizeof(unsigned long long)) || !bh.alloc((size_t)nbk * 8) || !ctr.alloc(24))
+    DevScratch acc, bh, ctr, pctr;
+    if (!acc.alloc(FKS_ACC_N * sizeof(unsigned long long)) || !bh.alloc((size_t)nbk * 8) || !ctr.alloc(24) ||
+        !pctr.alloc(2 * SP_MAXP * sizeof(unsigned long long)))
         return FK_E_OOM;
     /* a keys pass claims its output in SP_CHUNKs per wave: at most one
        chunk's worth of pads per wave of every emit launch */
@@ -7068,18 +7127,23 @@ static int sparse_finish(fk_engine *e, int32_t seq) {
        reserve those first */
     const uint64_t wins = e->last.acc[ACC_WIN];
     uint64_t cap = e->sp_pass;
-    if (!cap) {
+    uint64_t room = 0;   /* bytes for the passes' key lists and their processing */
+    {
         size_t fr = 0, tot = 0;
         HIPCHK(hipMemGetInfo(&fr, &tot));
         /* plus what the engine's sparse buffers already hold (reused, or
            freed and reallocated larger) */
         const uint64_t held = e->spk_cap * 8 + e->spc_cap * 4 + e->emit_cap * 8 + e->spdense_cap * 8 +
-                              e->fks.sorted_cap + e->fks.c64_cap + e->fks.tmp_cap;
+                              e->fks.sorted_cap + e->fks.c64_cap + e->fks.tmp_cap + e->codes_cap * 2 +
+                              e->parts_cap * 2 + e->pidx_cap * 4;
         const uint64_t avail = (uint64_t)fr + held;
         const uint64_t reserve = (1ull << 30) + 12 * wins;
-        cap = avail > reserve ? (avail - reserve) / 56 : 0;
-        cap = std::max<uint64_t>(1u << 20, std::min<uint64_t>(cap, 1ull << 32));
+        room = avail > reserve ? avail - reserve : 0;
     }
+    /* a pass takes ~8 B per key for its list and ~9 for its processing
+       (k_kpart's row codes 4 + run words, k_repart's part streams 2-4, the
+       library sort's ~40 if a pass falls back to it: kept inside the cap) */
+    if (!cap) cap = std::max<uint64_t>(1u << 20, std::min<uint64_t>(room / 56, 1ull << 32));
     /* the table's storage: room for every window (distinct <= windows) */
     {
         int rc = sp_ensure((void **)&e->d_spk, &e->spk_cap, wins + 1, 8);
@@ -7168,77 +7232,18 @@ static int sparse_finish(fk_engine *e, int32_t seq) {
         }
     }
 
-    /* 3. the passes */
+    /* 3. the passes.  Consecutive sorted or counted passes share one walk
+       (up to SP_MAXP key ranges, their lists side by side in d_emit) as
+       far as their lists fit beside one pass's processing */
     uint64_t prev_last = 0;
     bool have_prev = false;
     std::vector<unsigned long long> edges(24, 0);   /* prefix histogram across pass boundaries */
-    for (const Pass &ps : passes) {
-        SpEmit em{};
-        em.shift = shift;
-        em.lo = (uint64_t)ps.b0 << shift;
-        em.hi = (uint64_t)ps.b1 << shift;
-        uint64_t *out_k = e->d_spk + e->sp_distinct;   /* this pass's runs follow the earlier ones' */
-        uint32_t *out_c = e->d_spc + e->sp_distinct;
-        uint64_t nw = 0;
-        if (ps.dense) {
-            const uint64_t nd = 1ull << shift;
-            int rc = sp_ensure((void **)&e->d_spdense, &e->spdense_cap, nd, 8);
-            if (rc) return rc;
-            HIPCHK(hipMemsetAsync(e->d_spdense, 0, nd * 8, e->stream));
-            em.mode = SP_DENSE;
-            em.dense = e->d_spdense;
-            rc = sp_emit_all(e, em);
-            if (rc) return rc;
-            if (fks_dense_runs(&e->fks, em.dense, nd, em.lo, k, e->stream, dacc, out_k, out_c, &nw)) return FK_E_HIP;
-        } else {
-            if (ps.n) {
-                int rc = sp_ensure((void **)&e->d_emit, &e->emit_cap,
-                                   std::max<uint64_t>(ps.n, std::min<uint64_t>(cap, wins)) + pad_max, 8);
-                if (rc) return rc;
-            }
-            em.mode = SP_KEYS;
-            em.out = e->d_emit;
-            const bool rel32 = em.hi - em.lo <= (1ull << 32);
-            em.out32 = rel32 ? reinterpret_cast<uint32_t *>(e->d_emit) : nullptr;
-            em.nout = nctr;
-            em.nreal = nctr + 2;
-            em.out_cap = ps.n + pad_max;
-            unsigned long long got[3] = {0, 0, 0};
-            for (int attempt = 0; attempt < 2; attempt++) {
-                if (single && !shorts.alloc((scap + 1) * 8)) return FK_E_OOM;
-                HIPCHK(hipMemsetAsync(nctr, 0, 24, e->stream));
-                em.shorts = single ? shorts.as<uint64_t>() : nullptr;   /* the single pass collects them */
-                em.nshort = nctr + 1;
-                em.short_cap = scap;
-                int rc = sp_emit_all(e, em);
-                if (rc) return rc;
-                HIPCHK(hipMemcpyAsync(got, nctr, sizeof got, hipMemcpyDeviceToHost, e->stream));
-                HIPCHK(hipStreamSynchronize(e->stream));
-                if (!single || got[1] <= scap) break;
-                if (attempt) return FK_E_HIP;
-                scap = got[1];
-            }
-            /* the feed's (or the histogram's) count and the emit pass agree,
-               and the claimed slots (windows + pads) fit */
-            if (got[2] != ps.n || got[0] > em.out_cap) return FK_E_HIP;
-            if (single) {
-                ns = got[1];
-                int rc = prep_shorts();
-                if (rc) return rc;
-            }
-            bool lib = false;
-            if (rel32) {   /* counted, not sorted (sp_count_runs32) */
-                int rc = sp_count_runs32(e, em.out32, got[0], em.lo, got[0] - got[2], dacc, out_k, out_c, &nw);
-                if (rc) return rc;
-            } else {       /* partitioned and sorted in LDS (sp_sort_runs64) */
-                int rc = sp_sort_runs64(e, em.out, got[0], em.lo, em.hi, got[0] - got[2], dacc, out_k, out_c, &nw, &lib);
-                if (rc) return rc;
-            }
-            /* a part or bucket past k_kp_sort's sizes: the library sort */
-            if (lib && fks_sort_runs(&e->fks, em.out, got[0], k, e->stream, dacc, out_k, out_c, &nw, got[0] - got[2]))
-                return FK_E_HIP;
-        }
-        if (!nw) continue;
+    const uint64_t list_room = room > 9 * cap ? room - 9 * cap : 0;
+    bool solo = false;   /* a pass fell back to the library sort: one pass per walk from there on */
+    /* after a pass: its runs joined to the table (short-walk marks, the
+       prefix pair across the pass boundary) */
+    auto join = [&](uint64_t *out_k, uint64_t nw) -> int {
+        if (!nw) return FK_OK;
         if (e->sp_distinct + nw > e->spk_cap) return FK_E_HIP;   /* cannot happen: distinct <= windows */
         if (ns && fks_short_mark(out_k, nw, shorts.as<uint64_t>(), ns, k, found.as<uint8_t>(), e->stream))
             return FK_E_HIP;
@@ -7254,6 +7259,127 @@ static int sparse_finish(fk_engine *e, int32_t seq) {
         prev_last = fl[1];
         have_prev = true;
         e->sp_distinct += nw;
+        return FK_OK;
+    };
+    for (size_t pi = 0; pi < passes.size();) {
+        const Pass &p0 = passes[pi];
+        uint64_t *out_k = e->d_spk + e->sp_distinct;   /* this pass's runs follow the earlier ones' */
+        uint32_t *out_c = e->d_spc + e->sp_distinct;
+        if (p0.dense) {
+            SpEmit em{};
+            em.shift = shift;
+            em.lo = (uint64_t)p0.b0 << shift;
+            em.hi = (uint64_t)p0.b1 << shift;
+            uint64_t nw = 0;
+            const uint64_t nd = 1ull << shift;
+            int rc = sp_ensure((void **)&e->d_spdense, &e->spdense_cap, nd, 8);
+            if (rc) return rc;
+            HIPCHK(hipMemsetAsync(e->d_spdense, 0, nd * 8, e->stream));
+            em.mode = SP_DENSE;
+            em.dense = e->d_spdense;
+            rc = sp_emit_all(e, em);
+            if (rc) return rc;
+            if (fks_dense_runs(&e->fks, em.dense, nd, em.lo, k, e->stream, dacc, out_k, out_c, &nw)) return FK_E_HIP;
+            rc = join(out_k, nw);
+            if (rc) return rc;
+            pi++;
+            continue;
+        }
+        /* the group: its lists' offsets (16-B aligned) in d_emit */
+        size_t pj = pi;
+        uint64_t bytes = 0, offs[SP_MAXP];
+        while (pj < passes.size() && !passes[pj].dense && pj - pi < (solo ? 1u : SP_MAXP)) {
+            const uint64_t span = (uint64_t)(passes[pj].b1 - passes[pj].b0) << shift;
+            const uint64_t need = (((passes[pj].n + pad_max) * (span <= (1ull << 32) ? 4u : 8u)) + 15) & ~15ull;
+            if (pj > pi && bytes + need > list_room) break;
+            offs[pj - pi] = bytes;
+            bytes += need;
+            pj++;
+        }
+        {
+            int rc = sp_ensure((void **)&e->d_emit, &e->emit_cap, bytes / 8 + 2, 8);
+            if (rc) return rc;
+        }
+        SpEmit em{};
+        em.shift = shift;
+        em.mode = SP_KEYS;
+        em.np = (uint32_t)(pj - pi);
+        for (uint32_t q = 0; q < SP_MAXP; q++) em.ps[q].lo = ~0ull;
+        em.gend = (uint64_t)passes[pj - 1].b1 << shift;
+        unsigned long long *pc = pctr.as<unsigned long long>();
+        for (uint32_t q = 0; q < em.np; q++) {
+            const Pass &ps = passes[pi + q];
+            SpPass &sp = em.ps[q];
+            sp.lo = (uint64_t)ps.b0 << shift;
+            sp.hi = (uint64_t)ps.b1 << shift;
+            uint8_t *base = reinterpret_cast<uint8_t *>(e->d_emit) + offs[q];
+            const bool rel32 = sp.hi - sp.lo <= (1ull << 32);
+            sp.out = rel32 ? nullptr : reinterpret_cast<uint64_t *>(base);
+            sp.out32 = rel32 ? reinterpret_cast<uint32_t *>(base) : nullptr;
+            sp.cap = ps.n + pad_max;
+            sp.ctr = pc + 2 * q;
+        }
+        unsigned long long got[2 * SP_MAXP] = {};
+        for (int attempt = 0; attempt < 2; attempt++) {
+            if (single && !shorts.alloc((scap + 1) * 8)) return FK_E_OOM;
+            HIPCHK(hipMemsetAsync(nctr, 0, 24, e->stream));
+            HIPCHK(hipMemsetAsync(pc, 0, 2 * SP_MAXP * sizeof(unsigned long long), e->stream));
+            em.shorts = single ? shorts.as<uint64_t>() : nullptr;   /* the single pass collects them */
+            em.nshort = nctr + 1;
+            em.short_cap = scap;
+            int rc = sp_emit_all(e, em);
+            if (rc) return rc;
+            unsigned long long nsh = 0;
+            HIPCHK(hipMemcpyAsync(got, pc, 2 * SP_MAXP * sizeof(unsigned long long), hipMemcpyDeviceToHost, e->stream));
+            HIPCHK(hipMemcpyAsync(&nsh, nctr + 1, sizeof nsh, hipMemcpyDeviceToHost, e->stream));
+            HIPCHK(hipStreamSynchronize(e->stream));
+            if (!single || nsh <= scap) {
+                if (single) ns = nsh;
+                break;
+            }
+            if (attempt) return FK_E_HIP;
+            scap = nsh;
+        }
+        if (single) {
+            int rc = prep_shorts();
+            if (rc) return rc;
+        }
+#ifdef SPX_NOSTORE
+        pi = pj;
+        continue;
+#endif
+        for (uint32_t q = 0; q < em.np; q++) {
+            const Pass &ps = passes[pi + q];
+            const SpPass &sp = em.ps[q];
+            const uint64_t claimed = got[2 * q], real = got[2 * q + 1];
+            /* the feed's (or the histogram's) count and the walk agree, and
+               the claimed slots (windows + pads) fit */
+            if (real != ps.n || claimed > sp.cap) return FK_E_HIP;
+            uint64_t *ok = e->d_spk + e->sp_distinct;
+            uint32_t *oc = e->d_spc + e->sp_distinct;
+            uint64_t nw = 0;
+            bool lib = false;
+            if (sp.out32) {   /* counted, not sorted (sp_count_runs32) */
+                int rc = sp_count_runs32(e, sp.out32, claimed, sp.lo, claimed - real, dacc, ok, oc, &nw);
+                if (rc) return rc;
+            } else {          /* partitioned and sorted in LDS (sp_sort_runs64) */
+                int rc = sp_sort_runs64(e, sp.out, claimed, sp.lo, sp.hi, claimed - real, dacc, ok, oc, &nw, &lib);
+                if (rc) return rc;
+            }
+            /* a part or bucket past k_kp_sort's sizes: the library sort,
+               which needs the room the group's other lists hold: walk this
+               pass again alone */
+            if (lib && em.np > 1) {
+                solo = true;
+                pj = pi + q;
+                break;
+            }
+            if (lib && fks_sort_runs(&e->fks, sp.out, claimed, k, e->stream, dacc, ok, oc, &nw, claimed - real))
+                return FK_E_HIP;
+            int rc = join(ok, nw);
+            if (rc) return rc;
+        }
+        pi = pj;
     }
 
     /* 4. totals: statistics, rollover, nodeCounter */

@@ -961,6 +961,17 @@ def test_sparse_key_range_passes(k, monkeypatch):
     assert_same_sparse(mixed_input(1300 + k, 300_000), k)
 
 
+def test_sparse_shared_walk_falls_back_alone(monkeypatch):
+    """k=20, sp_pass=300000: ~4 wide passes share one emit walk; the first
+    holds a poly-A stretch (100k windows of key 0, one part past k_kp_sort's
+    LDS), takes the library sort and the walk is redone one pass at a time"""
+    monkeypatch.setenv("FINDKMER_TUNE", "sp_pass=300000")
+    rng = random.Random(20)
+    body = b"A" * 100_000 + bytes(rng.choices(b"ACGT", k=1_000_000))
+    lines = b"\n".join(body[i:i + 60] for i in range(0, len(body), 60))
+    assert_same_sparse(b">p\n" + lines + b"\n", 20)
+
+
 def test_sparse_every_bucket_dense(monkeypatch):
     """sp_pass=1: every nonempty bucket takes the dense path (k=17: 2^22 u64
     per bucket), golden inputs"""
