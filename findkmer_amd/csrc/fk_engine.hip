@@ -3204,7 +3204,7 @@ static_assert(16u * FK_TILE_BYTES <= REPART_CAP, "a C32 row's run fits one k_rep
 template <typename OT, uint32_t G = REPART_G>
 __global__ void __launch_bounds__(1024)
 k_repart(PartGeo pg, OT *out, unsigned long long *alloc, PartMeta *meta, uint64_t cap,
-         unsigned long long *err, uint32_t psh) {
+         unsigned long long *err, uint32_t psh, unsigned long long *pmax) {
     /* (G coarse slices of 2^split parts: G << split <= REPART_GP, checked by the host) */
     /* per (slice in the group, part): entries, round count / offset /
        cursor, written so far, stream start */
@@ -3271,6 +3271,12 @@ k_repart(PartGeo pg, OT *out, unsigned long long *alloc, PartMeta *meta, uint64_
             wr[p] = 0;
             /* slice-major: (b0 + p / np) * np + p % np */
             meta[(size_t)b0 * np + p] = over ? PartMeta{0, 0, 0} : PartMeta{g0 + ho[p], cnt[p], 0};
+        }
+        if (pmax) {   /* the largest part (k_kp_sort's LDS size) */
+            uint32_t mx = 0;
+            for (uint32_t p = lane; p < gp; p += 64u) mx = max(mx, cnt[p]);
+            mx = wscan_max32(mx);
+            if (lane == 63) atomicMax(pmax, (unsigned long long)mx);
         }
     }
     /* pass B: rounds of whole runs (a lane per item) holding up to
@@ -5146,7 +5152,7 @@ static int launch_part(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t l
         e->perr_live = true;
         HIPCHK(hipMemsetAsync(alloc, 0, 2 * sizeof(unsigned long long), e->stream));
         hipLaunchKernelGGL(k_repart<uint16_t>, dim3(pg.nslices / REPART_G), dim3(1024), 0, e->stream, pg, e->d_parts,
-                           alloc, meta, (uint64_t)e->parts_cap, e->d_perr, 15u);
+                           alloc, meta, (uint64_t)e->parts_cap, e->d_perr, 15u, nullptr);
         HIPCHK(hipGetLastError());
         hipLaunchKernelGGL(k_count_parts, dim3((unsigned)nparts), dim3(1024), (size_t)1 << 17, e->stream, pg,
                            (const uint16_t *)e->d_parts, (const PartMeta *)meta, e->d_table, (uint64_t)e->parts_cap,
@@ -6649,7 +6655,7 @@ k_kp_count(const uint16_t *in, const PartMeta *meta, uint64_t cap_in, uint64_t l
 /*
  * Wide passes (18 <= k <= 20, a key range of more than 2^32 keys): the same
  * two partition levels (64-bit keys in, the parts' codes 32-bit), then each
- * part -- up to KS_CAP keys of at most 23 bits, ~20 K at k = 20 over 10 G
+ * part -- up to KS_CAP keys of at most 23 bits, ~10 K at k = 20 over 10 G
  * bases -- sorted in LDS instead of counted: bucketed by its top 8 bits
  * (LDS histogram, scan, scatter), each bucket sorted by one wave in
  * registers (a bitonic network over 64 N keys, N = 1..16 per lane), then run-
@@ -6657,8 +6663,8 @@ k_kp_count(const uint16_t *in, const PartMeta *meta, uint64_t cap_in, uint64_t l
  * tens of thousands of times in one part) flags the pass, which then takes
  * the library sort (fks_sort_runs) instead.
  */
-#define KS_CAP 24576u
-#define KS_ITEMS (KS_CAP / 1024u)
+#define KS_CAP 24576u        /* k_kp_sort<KS_CAP>: one block per CU */
+#define KS_CAP_S 12288u      /* k_kp_sort<KS_CAP_S>: two (every part of the pass fits) */
 #define FK_FAULT_SORTCAP 8u
 
 /* bitonic sort of the 64 N values x[i] (element i * 64 + lane), ascending */
@@ -6694,6 +6700,25 @@ __device__ __forceinline__ void wave_bitonic(uint32_t (&x)[N]) {
     }
 }
 
+/* Batcher's odd-even merge sort of N (a power of two) registers, ascending
+   (63 compare-exchanges at N = 16, every index a constant) */
+template <int N>
+__device__ __forceinline__ void reg_sort(uint32_t (&x)[N]) {
+#pragma unroll
+    for (int p = 1; p < N; p <<= 1)
+#pragma unroll
+        for (int k = p; k >= 1; k >>= 1)
+#pragma unroll
+            for (int j = k % p; j + k < N; j += 2 * k)
+#pragma unroll
+                for (int i = 0; i < k; i++)
+                    if (i + j + k < N && (i + j) / (2 * p) == (i + j + k) / (2 * p)) {
+                        const uint32_t a = x[i + j], b = x[i + j + k];
+                        x[i + j] = min(a, b);
+                        x[i + j + k] = max(a, b);
+                    }
+}
+
 template <int N>
 __device__ __forceinline__ void wave_sort_bucket(uint32_t *k, uint32_t n) {
     const uint32_t lane = threadIdx.x & 63;
@@ -6711,20 +6736,25 @@ __device__ __forceinline__ void wave_sort_bucket(uint32_t *k, uint32_t n) {
     }
 }
 
+template <uint32_t CAP>
 __global__ void __launch_bounds__(1024)
 k_kp_sort(const uint32_t *in, const PartMeta *meta, uint64_t cap_in, uint64_t lo, uint32_t psh, uint64_t npads,
           const unsigned long long *tcount, uint32_t top_part, uint32_t nparts, int k, unsigned long long *flags,
           uint64_t *out_k, uint32_t *out_c, unsigned long long *slots, uint64_t *fl, unsigned long long *err) {
-    extern __shared__ uint32_t keys[];   /* KS_CAP keys, then KS_CAP + 1 u16 run starts */
-    uint16_t *const rs = reinterpret_cast<uint16_t *>(keys + KS_CAP);
-    __shared__ uint32_t bh[256], bo[257];
+    constexpr uint32_t KSI = CAP / 1024u;
+    extern __shared__ uint32_t keys[];   /* CAP keys, then CAP + 1 u16 run starts */
+    uint16_t *const rs = reinterpret_cast<uint16_t *>(keys + CAP);
+    /* the bucket cursors live where the run starts go later (two blocks of
+       the small instance per CU: 80 KB of LDS each at most) */
+    uint32_t *const bh = reinterpret_cast<uint32_t *>(rs);
+    __shared__ uint32_t bo[1025];
     __shared__ unsigned long long wred[16][10];
     __shared__ uint32_t hpre[24];
     __shared__ uint32_t wnz[16];
     __shared__ unsigned long long bprefix;
     __shared__ uint32_t bad, vblk;
     const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6;
-    if (t < 256) bh[t] = 0;
+    bh[t] = 0;
     if (t < 24) hpre[t] = 0;
     if (t == 0) {
         bad = 0;
@@ -6738,40 +6768,56 @@ k_kp_sort(const uint32_t *in, const PartMeta *meta, uint64_t cap_in, uint64_t lo
         m.n = 0;
         m.off = 0;
     }
-    if (m.n > KS_CAP) {   /* too many keys for one block's LDS: the library sort */
+    if (m.n > CAP) {   /* too many keys for one block's LDS: the library sort */
         if (t == 0) atomicOr(err, (unsigned long long)FK_FAULT_SORTCAP);
         m.n = 0;
     }
-    const uint32_t n = m.n, bsh = psh - 8u;
-    /* 1. bucket by the top 8 bits of the part's code */
-    uint32_t v[KS_ITEMS];
+    const uint32_t n = m.n, bsh = psh - 10u;
+    /* 1. bucket by the top 10 bits of the part's code (~10 keys a bucket) */
+    uint32_t v[KSI];
 #pragma unroll
-    for (uint32_t j = 0; j < KS_ITEMS; j++) {
+    for (uint32_t j = 0; j < KSI; j++) {
         v[j] = j * 1024u + t < n ? in[m.off + j * 1024u + t] : 0u;
         if (j * 1024u + t < n) atomicAdd(&bh[v[j] >> bsh], 1u);
     }
     __syncthreads();
-    if (t < 64) {
-        uint32_t c4[4], sum = 0;
+    {   /* bucket t's start: a block scan */
+        const uint32_t c = bh[t], inc = wscan_incl32(c);
+        if (lane == 63) wnz[wv] = inc;
+        __syncthreads();
+        uint32_t before = 0;
 #pragma unroll
-        for (int q = 0; q < 4; q++) { c4[q] = bh[t * 4 + q]; sum += c4[q]; }
-        uint32_t run = wscan_incl32(sum) - sum;
-#pragma unroll
-        for (int q = 0; q < 4; q++) { bo[t * 4 + q] = run; bh[t * 4 + q] = run; run += c4[q]; }
-        if (t == 63) bo[256] = run;
+        for (uint32_t w = 0; w < 16u; w++) before += w < wv ? wnz[w] : 0u;
+        bo[t] = bh[t] = before + inc - c;
+        if (t == 1023) bo[1024] = before + inc;
     }
     __syncthreads();
 #pragma unroll
-    for (uint32_t j = 0; j < KS_ITEMS; j++)
+    for (uint32_t j = 0; j < KSI; j++)
         if (j * 1024u + t < n) keys[atomicAdd(&bh[v[j] >> bsh], 1u)] = v[j];
     __syncthreads();
-    /* 2. each bucket sorted by one wave */
-    for (uint32_t b = wv; b < 256u; b += 16u) {
+    /* 2. bucket t of up to 16 keys sorted by thread t in registers; the
+       larger ones (~2 % at 10 a bucket on average) each by one wave */
+#ifndef KPX_NOSORT
+    {
+        const uint32_t b0 = bo[t], nb = bo[t + 1] - b0;
+        if (nb > 1u && nb <= 16u) {
+            uint32_t x[16];
+#pragma unroll
+            for (uint32_t i = 0; i < 16u; i++) x[i] = i < nb ? keys[b0 + i] : ~0u;
+            reg_sort<16>(x);
+#pragma unroll
+            for (uint32_t i = 0; i < 16u; i++)
+                if (i < nb) keys[b0 + i] = x[i];
+        }
+    }
+#endif
+    for (unsigned long long big = __ballot(bo[wv * 64u + lane + 1] - bo[wv * 64u + lane] > 16u); big; big &= big - 1) {
+        const uint32_t b = wv * 64u + (uint32_t)__builtin_ctzll(big);
         const uint32_t b0 = bo[b], nb = bo[b + 1] - b0;
 #ifdef KPX_NOSORT
         continue;
 #endif
-        if (nb <= 1) continue;
         if (nb <= 64) wave_sort_bucket<1>(keys + b0, nb);
         else if (nb <= 128) wave_sort_bucket<2>(keys + b0, nb);
         else if (nb <= 256) wave_sort_bucket<4>(keys + b0, nb);
@@ -6784,12 +6830,12 @@ k_kp_sort(const uint32_t *in, const PartMeta *meta, uint64_t cap_in, uint64_t lo
         if (t == 0) atomicOr(err, (unsigned long long)FK_FAULT_SORTCAP);
     }
     const uint32_t nn = bad ? 0u : n;
-    /* 3. runs: thread t takes positions [t * KS_ITEMS, +KS_ITEMS); a run
+    /* 3. runs: thread t takes positions [t * KSI, +KSI); a run
        starts where the key changes */
-    const uint32_t p0 = t * KS_ITEMS;
+    const uint32_t p0 = t * KSI;
     uint32_t nz = 0;
 #pragma unroll
-    for (uint32_t j = 0; j < KS_ITEMS; j++) {
+    for (uint32_t j = 0; j < KSI; j++) {
         const uint32_t i = p0 + j;
         if (i < nn && (i == 0 || keys[i] != keys[i - 1])) nz++;
     }
@@ -6814,7 +6860,7 @@ k_kp_sort(const uint32_t *in, const PartMeta *meta, uint64_t cap_in, uint64_t lo
     {
         uint32_t o = off;
 #pragma unroll
-        for (uint32_t j = 0; j < KS_ITEMS; j++) {
+        for (uint32_t j = 0; j < KSI; j++) {
             const uint32_t i = p0 + j;
             if (i < nn && (i == 0 || keys[i] != keys[i - 1])) rs[o++] = (uint16_t)i;
         }
@@ -6973,7 +7019,7 @@ static int sp_count_runs32(fk_engine *e, const uint32_t *keys, uint64_t n, uint6
                        0ull, 21u, 0xFFFFFFFFull, tcount);
     HIPCHK(hipGetLastError());
     hipLaunchKernelGGL(k_repart<uint16_t>, dim3(2048u / REPART_G), dim3(1024), 0, e->stream, pg, e->d_parts, alloc,
-                       meta, (uint64_t)e->parts_cap, alloc + 1, 15u);
+                       meta, (uint64_t)e->parts_cap, alloc + 1, 15u, nullptr);
     HIPCHK(hipGetLastError());
     hipLaunchKernelGGL(k_kp_count, dim3(nparts), dim3(1024), (size_t)1 << 17, e->stream, (const uint16_t *)e->d_parts,
                        (const PartMeta *)meta, (uint64_t)e->parts_cap, lo, npads, (const unsigned long long *)tcount, nparts,
@@ -7037,7 +7083,7 @@ static int sp_sort_runs64(fk_engine *e, const uint64_t *keys, uint64_t n, uint64
     unsigned long long *alloc = reinterpret_cast<unsigned long long *>(meta + (size_t)2048 * REPART_METAP);
     uint32_t *parts32 = reinterpret_cast<uint32_t *>(e->d_parts);
     const uint64_t cap32 = e->parts_cap / 2;
-    HIPCHK(hipMemsetAsync(alloc, 0, 2 * sizeof(unsigned long long), e->stream));
+    HIPCHK(hipMemsetAsync(alloc, 0, 3 * sizeof(unsigned long long), e->stream));
     HIPCHK(hipMemsetAsync(flags.p, 0, (size_t)(nparts + 1) * 8, e->stream));   /* (+ the block tickets) */
     HIPCHK(hipMemsetAsync(slots.p, 0, (size_t)KP_SLOTS * KP_SLOT_W * 8, e->stream));
     HIPCHK(hipMemsetAsync(res.p, 0, 16, e->stream));
@@ -7050,13 +7096,27 @@ static int sp_sort_runs64(fk_engine *e, const uint64_t *keys, uint64_t n, uint64
                        cs, top_in ? top : ~0ull, tcount);
     HIPCHK(hipGetLastError());
     hipLaunchKernelGGL((k_repart<uint32_t, 4u>), dim3(2048u / 4u), dim3(1024), 0, e->stream, pg, parts32, alloc, meta,
-                       cap32, alloc + 1, psh);
+                       cap32, alloc + 1, psh, alloc + 2);
     HIPCHK(hipGetLastError());
+    unsigned long long pmax = 0;
+    HIPCHK(hipMemcpyAsync(&pmax, alloc + 2, 8, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    if (pmax > KS_CAP) {   /* a part past one block's LDS: the library sort */
+        *fallback = true;
+        return FK_OK;
+    }
+    const bool small = pmax <= KS_CAP_S;
     const uint32_t top_part = top_in ? (uint32_t)((top - lo) >> psh) : ~0u;
-    hipLaunchKernelGGL(k_kp_sort, dim3(nparts), dim3(1024), (size_t)KS_CAP * 6 + 16, e->stream, (const uint32_t *)parts32,
-                       (const PartMeta *)meta, cap32, lo, psh, top_in ? npads : 0ull, (const unsigned long long *)tcount,
-                       top_part, nparts, k, flags.as<unsigned long long>(), out_k, out_c, slots.as<unsigned long long>(),
-                       fl.as<uint64_t>(), alloc + 1);
+    if (small)
+        hipLaunchKernelGGL(k_kp_sort<KS_CAP_S>, dim3(nparts), dim3(1024), (size_t)KS_CAP_S * 6 + 16, e->stream,
+                           (const uint32_t *)parts32, (const PartMeta *)meta, cap32, lo, psh, top_in ? npads : 0ull,
+                           (const unsigned long long *)tcount, top_part, nparts, k, flags.as<unsigned long long>(), out_k,
+                           out_c, slots.as<unsigned long long>(), fl.as<uint64_t>(), alloc + 1);
+    else
+        hipLaunchKernelGGL(k_kp_sort<KS_CAP>, dim3(nparts), dim3(1024), (size_t)KS_CAP * 6 + 16, e->stream,
+                           (const uint32_t *)parts32, (const PartMeta *)meta, cap32, lo, psh, top_in ? npads : 0ull,
+                           (const unsigned long long *)tcount, top_part, nparts, k, flags.as<unsigned long long>(), out_k,
+                           out_c, slots.as<unsigned long long>(), fl.as<uint64_t>(), alloc + 1);
     HIPCHK(hipGetLastError());
     unsigned long long ferr = 0;
     HIPCHK(hipMemcpyAsync(&ferr, alloc + 1, 8, hipMemcpyDeviceToHost, e->stream));
@@ -7102,7 +7162,10 @@ static int sparse_finish(fk_engine *e, int32_t seq) {
         HIPCHK(hipFuncSetAttribute((const void *)k_sp_emit, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
         for (const void *f : {(const void *)k_kpart<uint32_t>, (const void *)k_kpart<uint64_t>})
             HIPCHK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(KP_BATCH * 4)));
-        HIPCHK(hipFuncSetAttribute((const void *)k_kp_sort, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(KS_CAP * 6 + 16)));
+        HIPCHK(hipFuncSetAttribute((const void *)k_kp_sort<KS_CAP>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   (int)(KS_CAP * 6 + 16)));
+        HIPCHK(hipFuncSetAttribute((const void *)k_kp_sort<KS_CAP_S>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   (int)(KS_CAP_S * 6 + 16)));
         HIPCHK(hipFuncSetAttribute((const void *)k_kp_count, hipFuncAttributeMaxDynamicSharedMemorySize, 1 << 17));
     }
     DevScratch acc, bh, ctr, pctr;
@@ -7215,17 +7278,28 @@ static int sparse_finish(fk_engine *e, int32_t seq) {
         std::vector<unsigned long long> hb(nbk);
         HIPCHK(hipMemcpyAsync(hb.data(), bh.p, (size_t)nbk * 8, hipMemcpyDeviceToHost, e->stream));
         HIPCHK(hipStreamSynchronize(e->stream));
-        /* 2. passes: [b0, b1) buckets; dense when one bucket exceeds the cap */
+        /* 2. passes: [b0, b1) buckets; dense when one bucket exceeds the
+           cap.  A pass stays inside one aligned block of 2^P keys: k = 17
+           (2^34 keys), P = 32, counts 32-bit keys (half the bytes; 4 such
+           blocks, as many passes as a 10 G-base input needs anyway); k >= 18
+           takes the largest P whose blocks hold at most `cap` windows on
+           average, so that a sorted pass spans a power of two and
+           sp_sort_runs64's 2^18 parts split it evenly (a pass of 0.28 x 2^40
+           keys at k = 20 left half of them empty, and the rest twice as
+           large as one block's LDS sorts at full occupancy) */
+        uint32_t P = 2u * (uint32_t)k;
+        if (k == 17) {
+            P = 32;
+        } else if (k > 17) {
+            P = shift;
+            while (P < 2u * (uint32_t)k && (wins >> (2u * (uint32_t)k - P - 1u)) <= cap) P++;
+        }
         for (uint32_t b = 0; b < nbk;) {
             if (!hb[b]) { b++; continue; }
             if (hb[b] > cap) { passes.push_back({b, b + 1, hb[b], true}); b++; continue; }
             uint32_t b1 = b;
             uint64_t n = 0;
-            /* k = 17 (2^34 keys): passes of at most 2^32 keys sort 32-bit
-               keys (half the bytes); 4 such spans cover the key space, as
-               many passes as a 10 G-base input needs anyway */
-            while (b1 < nbk && hb[b1] <= cap && n + hb[b1] <= cap &&
-                   (k != 17 || ((uint64_t)(b1 + 1 - b) << shift) <= (1ull << 32)))
+            while (b1 < nbk && hb[b1] <= cap && n + hb[b1] <= cap && (b1 >> (P - shift)) == (b >> (P - shift)))
                 n += hb[b1++];
             passes.push_back({b, b1, n, false});
             b = b1;
