@@ -758,8 +758,8 @@ def test_fresh_table_window_list_never_truncates(k, tune, monkeypatch):
         assert rg.redo_chunks > base   # the whole segment was counted again
 
 
-@pytest.mark.parametrize("k", [15, 16])
-@pytest.mark.parametrize("kind", ["mixed", "dense_records", "polyA", "fasta_polyA", "acgt_feeds"])
+@pytest.mark.parametrize("k,kind", [(15, "mixed"), (15, "dense_records"), (15, "polyA"), (15, "fasta_polyA"),
+                                    (15, "acgt_feeds"), (16, "mixed"), (16, "fasta_polyA"), (16, "acgt_feeds")])
 def test_partition_k15_and_k16(k, kind):
     """k = 15, 16 through the two-level partition: k_part's 2048 coarse
     slices of 32-bit codes, k_repart splitting each into 16 / 64 contiguous
@@ -976,7 +976,7 @@ def test_sparse_every_bucket_dense(monkeypatch):
     """sp_pass=1: every nonempty bucket takes the dense path (k=17: 2^22 u64
     per bucket), golden inputs"""
     monkeypatch.setenv("FINDKMER_TUNE", "sp_pass=1")
-    for name in ("test.txt", "edge.txt", "shortruns.txt", "ffbyte.bin"):
+    for name in ("edge.txt", "ffbyte.bin"):
         assert_same_sparse(golden_input(name), 17)
 
 
