@@ -268,7 +268,8 @@ def measure(ctx, k, n, L, seed, chrom, steps, warmup, verify=False):
     if not os.environ.get("FINDKMER_LIB") and rank == 0:
         total = merged.windows if merged is not None else last.windows
         if merged is not None:
-            assert merged.status() == fk.FK_OK, "merged table: rollover or unterminated header"
+            assert merged.status() == fk.FK_OK, ("merged table: rollover or unterminated header",
+                                                 merged._table_stats(), merged.windows, merged.unterminated_header)
         valid = merged.valid_bases if merged is not None else last.valid_bases
         if chrom_on and chrom < (1 << 31):
             assert valid == want_valid(world * n, k, chrom), (valid, want_valid(world * n, k, chrom))

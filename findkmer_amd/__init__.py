@@ -36,6 +36,7 @@ FK_PACK_ROW_WORDS = 32    # ... and its rows (uint32 words)
 FK_PACK_STATS = 8         # a sharded table's (total, distinct) as limbs
 FK_XCHG_FAST = 1          # fk_engine_shard_exchange flags (info[0])
 FK_XCHG_SHARD_TABLE = 2
+FK_ROUTE_KMIN = 15        # routed sharded tables from this k (include/findkmer.h)
 FK_XCHG_TEST_INVALID = 4
 FK_COMM_ID_BYTES = 128
 FK_UPSTREAM_REC = 1019    # fk_synth_upstream_device's record: ">ENST%011u\n" + 1001 bases + "\n"
@@ -108,6 +109,9 @@ SIGNATURES = [
     ("fk_comm_destroy", None, [_P]),
     ("fk_engine_shard_exchange", ctypes.c_int, [_P, _P, _P, ctypes.POINTER(ctypes.c_int32)]),
     ("fk_merge_layout", ctypes.c_int, [ctypes.c_int, ctypes.c_int, _U64P, _U64P]),
+    ("fk_engine_route_pack", ctypes.c_int, [_P, ctypes.c_int, ctypes.c_int, _U64P]),
+    ("fk_engine_route_copy", ctypes.c_int, [_P, _P]),
+    ("fk_engine_route_absorb", ctypes.c_int, [_P, ctypes.c_int, ctypes.c_int, _P, _U64P, _P]),
     ("fk_comm_available", ctypes.c_int, [ctypes.c_int]),
     ("fk_comm_info", ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int),
                                     ctypes.POINTER(ctypes.c_int)]),
@@ -281,6 +285,24 @@ class Engine:
         info = (ctypes.c_int32 * 2)(flags, -1)
         _check(lib().fk_engine_shard_exchange(self.h, comm.h, merge_ptr, info), "shard_exchange")
         return bool(info[0]), (info[1] if info[1] >= 0 else None)
+
+    def route_pack(self, world, counting=True):
+        """fk_engine_route_pack: the finished table's blobs for owners
+        0..world-1 (routed sharded table, k >= FK_ROUTE_KMIN); returns their
+        sizes in int32 words (fk_engine_route_copy fetches them)."""
+        words = (ctypes.c_uint64 * world)()
+        _check(lib().fk_engine_route_pack(self.h, world, 1 if counting else 0, words), "route_pack")
+        return [int(w) for w in words]
+
+    def route_copy(self, ptr):
+        _check(lib().fk_engine_route_copy(self.h, ptr), "route_copy")
+
+    def route_absorb(self, world, rank, recv_ptr, words, slice_ptr):
+        """fk_engine_route_absorb: the blobs received from every source
+        (words[s] int32 each, side by side at recv_ptr) into this rank's
+        slice of the merged table (device int32 at slice_ptr)."""
+        w = (ctypes.c_uint64 * world)(*words)
+        _check(lib().fk_engine_route_absorb(self.h, world, rank, recv_ptr, w, slice_ptr), "route_absorb")
 
     def stream(self):
         """The engine's hipStream_t (as an int)."""

@@ -21,3 +21,8 @@ int fkc_reduce_scatter_i32(fk_comm *c, int32_t *buf, size_t per_rank, hipStream_
 /* out of place: the sum of send[0, world * per_rank) over the ranks; rank
    r receives its block at buf + r * per_rank (buf's other blocks untouched) */
 int fkc_reduce_scatter_from_i32(fk_comm *c, const int32_t *send, int32_t *buf, size_t per_rank, hipStream_t s);
+/* all-to-all with per-peer word counts and offsets (ncclSend/ncclRecv in one
+   group); fkc_has_alltoallv: this RCCL exports them */
+bool fkc_has_alltoallv(const fk_comm *c);
+int fkc_alltoallv_i32(fk_comm *c, const int32_t *send, const uint64_t *scount, const uint64_t *sdispl,
+                      int32_t *recv, const uint64_t *rcount, const uint64_t *rdispl, hipStream_t s);

@@ -16,6 +16,8 @@
 #include <dlfcn.h>
 #include <string.h>
 
+#include <algorithm>
+
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -36,6 +38,12 @@ struct Rccl {
     decltype(&ncclCommCount) count = nullptr;
     decltype(&ncclCommUserRank) user_rank = nullptr;
     decltype(&ncclCommCuDevice) cu_device = nullptr;
+    /* optional (the routed table exchange, fkc_alltoallv_i32; without them
+       the sharded table is reduce-scattered) */
+    decltype(&ncclSend) send = nullptr;
+    decltype(&ncclRecv) recv = nullptr;
+    decltype(&ncclGroupStart) group_start = nullptr;
+    decltype(&ncclGroupEnd) group_end = nullptr;
     bool ok = false;
 };
 
@@ -57,6 +65,10 @@ const Rccl &rccl() {
         x.count = (decltype(x.count))dlsym(h, "ncclCommCount");
         x.user_rank = (decltype(x.user_rank))dlsym(h, "ncclCommUserRank");
         x.cu_device = (decltype(x.cu_device))dlsym(h, "ncclCommCuDevice");
+        x.send = (decltype(x.send))dlsym(h, "ncclSend");
+        x.recv = (decltype(x.recv))dlsym(h, "ncclRecv");
+        x.group_start = (decltype(x.group_start))dlsym(h, "ncclGroupStart");
+        x.group_end = (decltype(x.group_end))dlsym(h, "ncclGroupEnd");
         /* exactly the entry points the exchange calls */
         x.ok = x.get_id && x.init_rank && x.destroy && x.all_reduce && x.reduce && x.reduce_scatter;
         return x;
@@ -153,6 +165,43 @@ int fkc_reduce_scatter_from_i32(fk_comm *c, const int32_t *send, int32_t *buf, s
                    ncclSuccess
                ? FK_OK
                : FK_E_RCCL;
+}
+
+bool fkc_has_alltoallv(const fk_comm *c) {
+    const Rccl &r = rccl();
+    return c && c->nc && r.ok && r.send && r.recv && r.group_start && r.group_end;
+}
+
+/* every rank sends scount[p] words at send + sdispl[p] to rank p and
+   receives rcount[p] words from rank p at recv + rdispl[p] (point-to-point
+   pairs in one group: over xGMI each pair takes its own link) */
+int fkc_alltoallv_i32(fk_comm *c, const int32_t *send, const uint64_t *scount, const uint64_t *sdispl,
+                      int32_t *recv, const uint64_t *rcount, const uint64_t *rdispl, hipStream_t s) {
+    if (!fkc_has_alltoallv(c)) return FK_E_RCCL;
+    const Rccl &r = rccl();
+    /* this rank's own blob: a device copy (a 1.5 GB ncclSend to self
+       delivered about half of it at k = 16) */
+    const int me = c->rank;
+    if (scount[me] != rcount[me]) return FK_E_INVALID;
+    if (scount[me] && hipMemcpyAsync(recv + rdispl[me], send + sdispl[me], scount[me] * sizeof(int32_t),
+                                     hipMemcpyDeviceToDevice, s) != hipSuccess)
+        return FK_E_HIP;
+    if (c->world == 1) return FK_OK;
+    /* the others in pieces of at most 2^28 words, matched in order */
+    const uint64_t CH = 1ull << 28;
+    if (r.group_start() != ncclSuccess) return FK_E_RCCL;
+    int rc = FK_OK;
+    for (int p = 0; p < c->world && rc == FK_OK; p++) {
+        if (p == me) continue;
+        for (uint64_t o = 0; o < scount[p] && rc == FK_OK; o += CH)
+            if (r.send(send + sdispl[p] + o, std::min(CH, scount[p] - o), ncclInt32, p, c->nc, s) != ncclSuccess)
+                rc = FK_E_RCCL;
+        for (uint64_t o = 0; o < rcount[p] && rc == FK_OK; o += CH)
+            if (r.recv(recv + rdispl[p] + o, std::min(CH, rcount[p] - o), ncclInt32, p, c->nc, s) != ncclSuccess)
+                rc = FK_E_RCCL;
+    }
+    if (r.group_end() != ncclSuccess) rc = FK_E_RCCL;
+    return rc;
 }
 
 /* What RCCL itself reports for the communicator: its rank count, this

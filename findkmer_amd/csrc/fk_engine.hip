@@ -4316,6 +4316,13 @@ struct fk_engine {
     uint16_t *d_parts = nullptr;              /* k = 15, 16: the second level's part streams (k_repart) */
     uint64_t parts_cap = 0;
     void *d_pmeta = nullptr;                  /* k = 15, 16: PartMeta per part + the allocation counter */
+    int32_t *d_rsend = nullptr, *d_rrecv = nullptr;   /* routed sharded tables: blobs out / in (fk_engine_route_*) */
+    uint64_t rsend_cap = 0, rrecv_cap = 0, rsend_words = 0;
+    void *d_raux = nullptr;                   /* ... their per-destination geometry and slot offsets */
+    uint64_t raux_cap = 0;
+    int route_mode = 1;                       /* FINDKMER_TUNE route: 0 = reduce-scatter the table, 1 = route it
+                                                 when world > 1 (at world 1 the reduce-scatter is a local copy,
+                                                 ~11 ms less per k = 16 step), 2 = route at any world (tests) */
     uint64_t pair_cap = 0;
     uint32_t w16_ks = W16_KS_DEFAULT;         /* k (bits) counted through k_bucket16 (FINDKMER_TUNE w16=mask) */
     int part_pairs_kmax = 12;                 /* pairs mode for k <= this (FINDKMER_TUNE pairs_kmax; k = 12 pairs:
@@ -4548,6 +4555,7 @@ extern "C" void fk_engine_destroy(fk_engine *e) {
     hipFree(e->d_table); hipFree(e->d_short); hipFree(e->d_sub); hipFree(e->d_snap);
     hipFree(e->d_pairs);
     hipFree(e->d_parts); hipFree(e->d_pmeta); hipFree(e->d_glist); hipFree(e->d_fz);
+    hipFree(e->d_rsend); hipFree(e->d_rrecv); hipFree(e->d_raux);
     hipFree(e->d_codes); hipFree(e->d_pidx); hipFree(e->d_pflag); hipFree(e->d_acc); hipFree(e->d_res); hipFree(e->d_tmp);
     hipFree(e->d_state); hipFree(e->d_rr); hipFree(e->d_rtrue);
     hipFree(e->d_redo); hipFree(e->d_tf); hipFree(e->d_stage); hipFree(e->d_resume);
@@ -4634,6 +4642,7 @@ extern "C" int fk_engine_create(int k, const fk_opts *opts, fk_engine **out) {
        isolated comment line) and leaves denser ones to k_resume's mixed tiles */
     if (!e->no_mixed) e->general_tiles = 2;
     if (tune_knob("pairs_kmax", &kv)) e->part_pairs_kmax = (int)std::min<uint64_t>(kv, 12u);
+    if (tune_knob("route", &kv)) e->route_mode = (int)std::min<uint64_t>(kv, 2u);
     if (tune_knob("part_general", &kv)) e->part_general = (uint32_t)kv;
     if (tune_knob("glist_cap", &kv)) e->glist_force = kv;
     if (tune_knob("w16", &kv)) e->w16_ks = ((uint32_t)kv & 0x3000u) | (1u << 14);   /* k = 12, 13 (14 always) */
@@ -6090,6 +6099,413 @@ __global__ void k_slice_limbs(const unsigned long long *in2, int32_t *limbs8) {
     if (i < 8) limbs8[i] = (int32_t)((in2[i >> 2] >> (16 * (i & 3))) & 0xFFFFu);
 }
 
+/*
+ * Routed sharded tables (k >= 15, FK_XCHG_SHARD_TABLE over RCCL or a gloo
+ * rehearsal): instead of reduce-scattering the whole 4^k table (k = 16:
+ * 16 GiB a rank, ~15 GiB of it over xGMI), each rank sends every owner only
+ * the nonzero bins of the owner's range, as one blob of 4-B entries per
+ * destination, and each owner counts the blobs it receives into its slice.
+ * A shard of 1.25 G windows leaves ~1.1 G nonzero bins at k = 16: ~4.4 GB
+ * sent instead of 15 GiB, and nothing sent for bins no rank saw.
+ *
+ * Parts: 2^15-bin blocks of the table (reference index order).  Owner d holds
+ * bins [d S, min((d + 1) S, 4^k)), S = TW / world (fk_merge_layout), so a part
+ * belongs to one owner or, at a range boundary, to two.  A (destination,
+ * part) pair is a slot, slots destination-major.  Blob for destination d:
+ *   [0, 4)           E_d (entries) and O_d (overflow pairs), u64 as 2 words
+ *   [4, 4 + P_d)     entries per slot of d (P_d slots: its parts)
+ *   [.., + E_d)      entries, slot by slot: (bin offset in the part << 17) | count
+ *   [.., + 2 O_d)    overflow pairs (bin - d S, count): counts >= 2^17 - 1
+ */
+#define RT_SH 15u
+#define RT_ESC 0x1FFFFu
+#define RT_HDR 4u
+
+/* per-destination arrays in one device buffer (u64 each, world W):
+   p0 [0,W) first part, sb [W, 2W+1) first slot, np [2W+1, 3W+1) parts,
+   bb [3W+1, 4W+1) blob start (words), ne [4W+1, 5W+1) entries,
+   no [5W+1, 6W+1) overflow pairs, oc [6W+1, 7W+1) overflow cursor; then
+   off[nslots + 1] (exclusive entry offset of each slot), then cnt[nslots] u32 */
+struct RouteGeo {
+    uint64_t nbins, S;
+    uint32_t world, nparts;
+    unsigned long long *aux;
+    __device__ __forceinline__ unsigned long long *p0() const { return aux; }
+    __device__ __forceinline__ unsigned long long *sb() const { return aux + world; }
+    __device__ __forceinline__ unsigned long long *np() const { return aux + 2 * world + 1; }
+    __device__ __forceinline__ unsigned long long *bb() const { return aux + 3 * world + 1; }
+    __device__ __forceinline__ unsigned long long *ne() const { return aux + 4 * world + 1; }
+    __device__ __forceinline__ unsigned long long *no() const { return aux + 5 * world + 1; }
+    __device__ __forceinline__ unsigned long long *oc() const { return aux + 6 * world + 1; }
+    __device__ __forceinline__ unsigned long long *off() const { return aux + 7 * world + 1; }
+};
+
+/* a part's owner(s): d0 and, when the part crosses d0's end b, d0 + 1 */
+__device__ __forceinline__ void rt_owners(const RouteGeo &g, uint64_t x0, uint32_t &d0, uint64_t &b, bool &two) {
+    d0 = (uint32_t)min<uint64_t>(x0 / g.S, (uint64_t)g.world - 1);
+    b = (uint64_t)(d0 + 1) * g.S;
+    two = d0 + 1 < g.world && b < x0 + (1ull << RT_SH);
+}
+
+/* one block per part: its entries and overflow bins per owner */
+__global__ void __launch_bounds__(256)
+k_route_count(const uint32_t *table, RouteGeo g, int counting, uint32_t *cnt) {
+    __shared__ uint32_t ws[4][4];
+    const uint32_t p = blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    const uint64_t x0 = (uint64_t)p << RT_SH;
+    uint32_t d0;
+    uint64_t b;
+    bool two;
+    rt_owners(g, x0, d0, b, two);
+    uint32_t c[4] = {0, 0, 0, 0};   /* entries lo / hi, overflow lo / hi */
+    if (counting) {
+        const uint4 *t4 = reinterpret_cast<const uint4 *>(table + x0);
+        for (uint32_t q = t; q < (1u << RT_SH) / 4u; q += 256u) {
+            const uint4 v4 = t4[q];
+            const uint32_t w[4] = {v4.x, v4.y, v4.z, v4.w};
+#pragma unroll
+            for (int h = 0; h < 4; h++) {
+                const bool hi = x0 + q * 4u + (uint32_t)h >= b;
+                const uint32_t v = w[h];
+                c[hi ? 1 : 0] += v != 0u && v < RT_ESC;
+                c[hi ? 3 : 2] += v >= RT_ESC;
+            }
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; i++) c[i] = wsum32(c[i]);
+    if (lane == 0)
+#pragma unroll
+        for (int i = 0; i < 4; i++) ws[wv][i] = c[i];
+    __syncthreads();
+    if (t == 0) {
+        uint32_t s[4] = {0, 0, 0, 0};
+        for (int w = 0; w < 4; w++)
+            for (int i = 0; i < 4; i++) s[i] += ws[w][i];
+        cnt[g.sb()[d0] + p - g.p0()[d0]] = s[0];
+        if (s[2]) atomicAdd(&g.no()[d0], (unsigned long long)s[2]);
+        if (two) {
+            cnt[g.sb()[d0 + 1] + p - g.p0()[d0 + 1]] = s[1];
+            if (s[3]) atomicAdd(&g.no()[d0 + 1], (unsigned long long)s[3]);
+        }
+    }
+}
+
+/* exclusive prefix of cnt[0, n) into off[0, n], off[n] = the total (one
+   block: a few hundred K slots at most) */
+__global__ void __launch_bounds__(1024)
+k_route_scan(const uint32_t *cnt, uint64_t n, unsigned long long *off) {
+    __shared__ unsigned long long part[1024];
+    const uint32_t t = threadIdx.x;
+    const uint64_t per = (n + 1023) / 1024, b0 = min<uint64_t>(n, per * t), b1 = min<uint64_t>(n, b0 + per);
+    unsigned long long s = 0;
+    for (uint64_t i = b0; i < b1; i++) s += cnt[i];
+    part[t] = s;
+    __syncthreads();
+    if (t == 0) {
+        unsigned long long run = 0;
+        for (uint32_t i = 0; i < 1024u; i++) {
+            const unsigned long long v = part[i];
+            part[i] = run;
+            run += v;
+        }
+        off[n] = run;
+    }
+    __syncthreads();
+    unsigned long long run = part[t];
+    for (uint64_t i = b0; i < b1; i++) {
+        off[i] = run;
+        run += cnt[i];
+    }
+}
+
+/* one block per part: its entries in bin order into each owner's blob (a
+   wave per quarter of the part, its start from the waves before it),
+   overflow bins appended to the owner's pairs, the slot counts, and (block
+   0) every blob's header */
+__global__ void __launch_bounds__(256)
+k_route_write(const uint32_t *table, RouteGeo g, int counting, const uint32_t *cnt, uint32_t *send) {
+    __shared__ uint32_t wc[4][2];
+    const uint32_t p = blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    if (p == 0 && t < g.world) {
+        const unsigned long long e = g.ne()[t], o = g.no()[t];
+        uint32_t *h = send + g.bb()[t];
+        h[0] = (uint32_t)e; h[1] = (uint32_t)(e >> 32); h[2] = (uint32_t)o; h[3] = (uint32_t)(o >> 32);
+    }
+    const uint64_t x0 = (uint64_t)p << RT_SH;
+    uint32_t d0;
+    uint64_t b;
+    bool two;
+    rt_owners(g, x0, d0, b, two);
+    const uint32_t d1 = two ? d0 + 1 : d0;
+    const uint64_t s0 = g.sb()[d0] + p - g.p0()[d0], s1 = g.sb()[d1] + p - g.p0()[d1];
+    if (t == 0) {
+        send[g.bb()[d0] + RT_HDR + (s0 - g.sb()[d0])] = cnt[s0];
+        if (two) send[g.bb()[d1] + RT_HDR + (s1 - g.sb()[d1])] = cnt[s1];
+    }
+    if (!counting) return;
+    constexpr uint32_t QW = (1u << RT_SH) / 4u;   /* bins per wave */
+    const uint32_t *tw = table + x0 + (uint64_t)wv * QW;
+    uint32_t c0 = 0, c1 = 0;
+    for (uint32_t i = lane; i < QW; i += 64u) {
+        const uint32_t v = tw[i];
+        const bool hi = x0 + wv * QW + i >= b, nz = v != 0u && v < RT_ESC;
+        c0 += nz && !hi;
+        c1 += nz && hi;
+    }
+    c0 = wsum32(c0);
+    c1 = wsum32(c1);
+    if (lane == 0) { wc[wv][0] = c0; wc[wv][1] = c1; }
+    __syncthreads();
+    uint64_t pos0 = g.off()[s0] - g.off()[g.sb()[d0]], pos1 = g.off()[s1] - g.off()[g.sb()[d1]];
+    for (uint32_t w = 0; w < wv; w++) { pos0 += wc[w][0]; pos1 += wc[w][1]; }
+    uint32_t *e0 = send + g.bb()[d0] + RT_HDR + g.np()[d0], *e1 = send + g.bb()[d1] + RT_HDR + g.np()[d1];
+    const unsigned long long lt = (1ull << lane) - 1ull;
+    for (uint32_t i0 = 0; i0 < QW; i0 += 64u) {
+        const uint32_t i = i0 + lane;
+        const uint32_t v = tw[i];
+        const uint64_t x = x0 + wv * QW + i;
+        const bool hi = x >= b, nz = v != 0u && v < RT_ESC;
+        const unsigned long long m0 = __ballot(nz && !hi), m1 = __ballot(nz && hi);
+        const uint32_t ent = ((wv * QW + i) << 17) | v;
+        if (nz) {
+            if (hi) e1[pos1 + __popcll(m1 & lt)] = ent;
+            else e0[pos0 + __popcll(m0 & lt)] = ent;
+        }
+        if (v >= RT_ESC) {
+            const uint32_t d = hi ? d1 : d0;
+            const unsigned long long at = atomicAdd(&g.oc()[d], 1ull);
+            uint32_t *op = send + g.bb()[d] + RT_HDR + g.np()[d] + g.ne()[d] + 2 * at;
+            op[0] = (uint32_t)(x - (uint64_t)d * g.S);
+            op[1] = v;
+        }
+        pos0 += __popcll(m0);
+        pos1 += __popcll(m1);
+    }
+}
+
+/* the owner: one block per part of its range, every source's entries for
+   the part into 2^15 LDS bins, then the part's owned bins into the slice
+   (written, not added: the slice holds nothing before) */
+__global__ void __launch_bounds__(1024)
+k_route_absorb(const uint32_t *recv, const unsigned long long *rd, const unsigned long long *roff, uint32_t world,
+               uint32_t np, uint64_t p0, uint64_t lo, uint64_t hi, uint32_t *out) {
+    extern __shared__ uint32_t bins[];
+    const uint32_t j = blockIdx.x, t = threadIdx.x;
+    for (uint32_t i = t; i < (1u << RT_SH) / 4u; i += 1024u) reinterpret_cast<uint4 *>(bins)[i] = make_uint4(0, 0, 0, 0);
+    __syncthreads();
+    for (uint32_t s = 0; s < world; s++) {
+        const uint32_t *blob = recv + rd[s];
+        const uint32_t n = blob[RT_HDR + j];
+        const uint32_t *ent = blob + RT_HDR + np + roff[(uint64_t)s * (np + 1) + j];
+        for (uint32_t i = t; i < n; i += 1024u) {
+            const uint32_t e = ent[i];
+            atomicAdd(&bins[e >> 17], e & RT_ESC);
+        }
+    }
+    __syncthreads();
+    const uint64_t x0 = (p0 + j) << RT_SH;
+    for (uint32_t i = t; i < (1u << RT_SH); i += 1024u) {
+        const uint64_t x = x0 + i;
+        if (x >= lo && x < hi) out[x - lo] = bins[i];
+    }
+}
+
+/* every source's overflow pairs added into the slice */
+__global__ void __launch_bounds__(256)
+k_route_overflow(const uint32_t *recv, const unsigned long long *rd, uint32_t np, uint32_t *out) {
+    const uint32_t *blob = recv + rd[blockIdx.x];
+    const uint64_t ne = blob[0] | ((uint64_t)blob[1] << 32), no = blob[2] | ((uint64_t)blob[3] << 32);
+    const uint32_t *op = blob + RT_HDR + np + ne;
+    for (uint64_t i = threadIdx.x; i < no; i += 256u) atomicAdd(&out[op[2 * i]], op[2 * i + 1]);
+}
+
+/* the owners' geometry for (nbins, world) on the host */
+struct RouteHost {
+    uint64_t S = 0, nslots = 0;
+    uint32_t nparts = 0;
+    std::vector<unsigned long long> p0, sb, np;
+};
+static RouteHost route_geometry(uint64_t nbins, int world) {
+    RouteHost h;
+    h.S = merge_table_words(nbins, world) / (uint64_t)world;
+    h.nparts = (uint32_t)(nbins >> RT_SH);
+    h.p0.assign(world, 0);
+    h.sb.assign(world + 1, 0);
+    h.np.assign(world, 0);
+    for (int d = 0; d < world; d++) {
+        const uint64_t a = (uint64_t)d * h.S, z = std::min<uint64_t>((uint64_t)(d + 1) * h.S, nbins);
+        if (a < z) {
+            h.p0[d] = a >> RT_SH;
+            h.np[d] = ((z - 1) >> RT_SH) - h.p0[d] + 1;
+        } else {
+            h.p0[d] = h.nparts;
+        }
+        h.sb[d + 1] = h.sb[d] + h.np[d];
+    }
+    h.nslots = h.sb[world];
+    return h;
+}
+
+/* fk_engine_route_pack: the finished table's blobs, one per destination,
+   side by side in e->d_rsend (words[d] each) */
+static int route_pack(fk_engine *e, int world, bool counting, uint64_t *words) {
+    if (e->sparse || e->k < 8 || world < 1) return FK_E_INVALID;
+    const RouteHost h = route_geometry(e->nbins, world);
+    if (h.S < (1ull << RT_SH)) return FK_E_INVALID;   /* (a part spans at most two owners) */
+    const uint64_t W = (uint64_t)world;
+    const uint64_t naux = 7 * W + 1 + h.nslots + 1, aux_bytes = naux * 8 + h.nslots * 4 + 16;
+    int rc = sp_ensure(&e->d_raux, &e->raux_cap, aux_bytes, 1);
+    if (rc) return rc;
+    unsigned long long *aux = static_cast<unsigned long long *>(e->d_raux);
+    uint32_t *cnt = reinterpret_cast<uint32_t *>(aux + naux);
+    std::vector<unsigned long long> ha(7 * W + 1, 0);
+    for (int d = 0; d < world; d++) { ha[d] = h.p0[d]; ha[2 * W + 1 + d] = h.np[d]; }
+    for (int d = 0; d <= world; d++) ha[W + d] = h.sb[d];
+    HIPCHK(hipMemcpyAsync(aux, ha.data(), ha.size() * 8, hipMemcpyHostToDevice, e->stream));
+    RouteGeo g{e->nbins, h.S, (uint32_t)world, h.nparts, aux};
+    hipLaunchKernelGGL(k_route_count, dim3(h.nparts), dim3(256), 0, e->stream, (const uint32_t *)e->d_table, g,
+                       counting ? 1 : 0, cnt);
+    HIPCHK(hipGetLastError());
+    hipLaunchKernelGGL(k_route_scan, dim3(1), dim3(1024), 0, e->stream, (const uint32_t *)cnt, h.nslots,
+                       aux + 7 * W + 1);
+    HIPCHK(hipGetLastError());
+    std::vector<unsigned long long> off(h.nslots + 1), no(W);
+    HIPCHK(hipMemcpyAsync(off.data(), aux + 7 * W + 1, (h.nslots + 1) * 8, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipMemcpyAsync(no.data(), aux + 5 * W + 1, W * 8, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    uint64_t total = 0;
+    for (int d = 0; d < world; d++) {
+        const uint64_t ne = off[h.sb[d + 1]] - off[h.sb[d]];
+        words[d] = RT_HDR + h.np[d] + ne + 2 * no[d];
+        ha[3 * W + 1 + d] = total;   /* bb */
+        ha[4 * W + 1 + d] = ne;      /* ne */
+        total += words[d];
+    }
+    rc = sp_ensure((void **)&e->d_rsend, &e->rsend_cap, total, sizeof(uint32_t));
+    if (rc) return rc;
+    e->rsend_words = total;
+    HIPCHK(hipMemcpyAsync(aux + 3 * W + 1, ha.data() + 3 * W + 1, 2 * W * 8, hipMemcpyHostToDevice, e->stream));
+    HIPCHK(hipMemsetAsync(aux + 6 * W + 1, 0, W * 8, e->stream));
+    hipLaunchKernelGGL(k_route_write, dim3(h.nparts), dim3(256), 0, e->stream, (const uint32_t *)e->d_table, g,
+                       counting ? 1 : 0, (const uint32_t *)cnt, reinterpret_cast<uint32_t *>(e->d_rsend));
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(e->stream));
+    return FK_OK;
+}
+
+/* fk_engine_route_absorb: the blobs received from every source (words[s]
+   each, side by side at recv) into this rank's slice of the merged table */
+static int route_absorb(fk_engine *e, int world, int rank, const int32_t *recv, const uint64_t *words, int32_t *slice) {
+    if (e->sparse || e->k < 8 || world < 1 || rank < 0 || rank >= world) return FK_E_INVALID;
+    const RouteHost h = route_geometry(e->nbins, world);
+    if (h.S < (1ull << RT_SH)) return FK_E_INVALID;
+    const uint64_t np = h.np[rank];
+    if (!np) return FK_OK;   /* (owns no bin) */
+    const uint64_t W = (uint64_t)world;
+    std::vector<unsigned long long> rd(W);
+    uint64_t at = 0;
+    for (int s = 0; s < world; s++) {
+        rd[s] = at;
+        if (words[s] < RT_HDR + np) return FK_E_INVALID;
+        at += words[s];
+    }
+    /* every blob's header against its size */
+    std::vector<uint32_t> hdr(4 * W);
+    for (int s = 0; s < world; s++)
+        HIPCHK(hipMemcpyAsync(&hdr[4 * s], recv + rd[s], 16, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    for (int s = 0; s < world; s++) {
+        const uint64_t ne = hdr[4 * s] | ((uint64_t)hdr[4 * s + 1] << 32),
+                       no = hdr[4 * s + 2] | ((uint64_t)hdr[4 * s + 3] << 32);
+        if (RT_HDR + np + ne + 2 * no != words[s]) return FK_E_INVALID;
+    }
+    const uint64_t aux_bytes = (W + W * (np + 1)) * 8 + 16;
+    int rc = sp_ensure(&e->d_raux, &e->raux_cap, aux_bytes, 1);
+    if (rc) return rc;
+    unsigned long long *drd = static_cast<unsigned long long *>(e->d_raux), *roff = drd + W;
+    HIPCHK(hipMemcpyAsync(drd, rd.data(), W * 8, hipMemcpyHostToDevice, e->stream));
+    const uint32_t *r32 = reinterpret_cast<const uint32_t *>(recv);
+    for (int s = 0; s < world; s++) {
+        hipLaunchKernelGGL(k_route_scan, dim3(1), dim3(1024), 0, e->stream, r32 + rd[s] + RT_HDR, np,
+                           roff + (uint64_t)s * (np + 1));
+        HIPCHK(hipGetLastError());
+    }
+    const uint64_t lo = (uint64_t)rank * h.S, hi = std::min<uint64_t>(lo + h.S, e->nbins);
+    HIPCHK(hipFuncSetAttribute((const void *)k_route_absorb, hipFuncAttributeMaxDynamicSharedMemorySize, 1 << 17));
+    uint32_t *out = reinterpret_cast<uint32_t *>(slice);
+    hipLaunchKernelGGL(k_route_absorb, dim3((uint32_t)np), dim3(1024), (size_t)1 << 17, e->stream, r32,
+                       (const unsigned long long *)drd, (const unsigned long long *)roff, (uint32_t)world, (uint32_t)np,
+                       (uint64_t)h.p0[rank], lo, hi, out);
+    HIPCHK(hipGetLastError());
+    hipLaunchKernelGGL(k_route_overflow, dim3((uint32_t)world), dim3(256), 0, e->stream, r32,
+                       (const unsigned long long *)drd, (uint32_t)np, out);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(e->stream));
+    return FK_OK;
+}
+
+extern "C" int fk_engine_route_pack(fk_engine *e, int world, int counting, uint64_t *words) {
+    if (!e || !words) return FK_E_INVALID;
+    int rc = set_dev(e);
+    if (rc) return rc;
+    return route_pack(e, world, counting != 0, words);
+}
+
+extern "C" int fk_engine_route_copy(fk_engine *e, void *dst) {
+    if (!e || !dst || !e->d_rsend) return FK_E_INVALID;
+    int rc = set_dev(e);
+    if (rc) return rc;
+    HIPCHK(hipMemcpyAsync(dst, e->d_rsend, e->rsend_words * sizeof(uint32_t), hipMemcpyDeviceToDevice, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    return FK_OK;
+}
+
+extern "C" int fk_engine_route_absorb(fk_engine *e, int world, int rank, const int32_t *recv, const uint64_t *words,
+                                      int32_t *slice) {
+    if (!e || !recv || !words || !slice) return FK_E_INVALID;
+    int rc = set_dev(e);
+    if (rc) return rc;
+    return route_absorb(e, world, rank, recv, words, slice);
+}
+
+/* the routed exchange over RCCL: blobs packed, their sizes all-reduced as a
+   world x world matrix of 16-bit limbs, one grouped send/recv, the received
+   blobs into this rank's slice */
+static int route_exchange(fk_engine *e, fk_comm *comm, bool counting, int32_t *slice) {
+    const int world = fkc_world(comm), rank = fkc_rank(comm);
+    const uint64_t W = (uint64_t)world;
+    std::vector<uint64_t> sw(W), rw(W), sd(W), rdsp(W);
+    int rc = route_pack(e, world, counting, sw.data());
+    if (rc) return rc;
+    DevScratch m;
+    const uint64_t nm = W * W * 3;
+    if (!m.alloc(nm * 4)) return FK_E_OOM;
+    std::vector<int32_t> hm(nm, 0);
+    for (uint64_t d = 0; d < W; d++)
+        for (int j = 0; j < 3; j++) hm[((uint64_t)rank * W + d) * 3 + j] = (int32_t)((sw[d] >> (16 * j)) & 0xFFFFu);
+    HIPCHK(hipMemcpyAsync(m.p, hm.data(), nm * 4, hipMemcpyHostToDevice, e->stream));
+    rc = fkc_allreduce_i32(comm, m.as<int32_t>(), nm, e->stream);
+    if (rc) return rc;
+    HIPCHK(hipMemcpyAsync(hm.data(), m.p, nm * 4, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    uint64_t sat = 0, rat = 0;
+    for (uint64_t s = 0; s < W; s++) {
+        uint64_t v = 0;
+        for (int j = 0; j < 3; j++) v |= (uint64_t)(uint32_t)hm[(s * W + (uint64_t)rank) * 3 + j] << (16 * j);
+        rw[s] = v;
+        rdsp[s] = rat;
+        rat += v;
+        sd[s] = sat;
+        sat += sw[s];
+    }
+    rc = sp_ensure((void **)&e->d_rrecv, &e->rrecv_cap, rat, sizeof(int32_t));
+    if (rc) return rc;
+    rc = fkc_alltoallv_i32(comm, e->d_rsend, sw.data(), sd.data(), e->d_rrecv, rw.data(), rdsp.data(), e->stream);
+    if (rc) return rc;
+    return route_absorb(e, world, rank, e->d_rrecv, rw.data(), slice);
+}
+
 static int stitched_exchange(fk_engine *e, fk_comm *comm, int32_t *merge, int32_t *first_end_out, bool scatter) {
     const int world = fkc_world(comm), rank = fkc_rank(comm);
     const uint64_t tw = merge_table_words(e->nbins, world);
@@ -6147,15 +6563,19 @@ static int stitched_exchange(fk_engine *e, fk_comm *comm, int32_t *merge, int32_
        the merge buffer first (k = 16: 16 GiB, ~5 ms per step); a rank whose
        shard the stream never reached sends zeros (its table, zeroed: the
        engine's count is discarded anyway) */
+    const bool route = scatter && e->k >= FK_ROUTE_KMIN && fkc_has_alltoallv(comm) &&
+                       (e->route_mode == 2 || (e->route_mode == 1 && world > 1));
     const bool direct = scatter && tw == e->nbins;
-    if (direct) {
+    if (route) {
+        /* (the table stays where it is: route_pack reads it) */
+    } else if (direct) {
         if (!counting) HIPCHK(hipMemsetAsync(e->d_table, 0, e->nbins * sizeof(uint32_t), e->stream));
     } else if (counting) {
         HIPCHK(hipMemcpyAsync(merge, e->d_table, e->nbins * sizeof(uint32_t), hipMemcpyDeviceToDevice, e->stream));
     } else {
         HIPCHK(hipMemsetAsync(merge, 0, e->nbins * sizeof(uint32_t), e->stream));
     }
-    if (!direct && tw > e->nbins)
+    if (!route && !direct && tw > e->nbins)
         HIPCHK(hipMemsetAsync(merge + e->nbins, 0, (tw - e->nbins) * sizeof(uint32_t), e->stream));
     uint32_t *limbs = e->h_rows + 32 + e->rows_cap;   /* pinned staging */
     for (int i = 0; i < FK_PACK_COUNTERS; i++)
@@ -6168,8 +6588,13 @@ static int stitched_exchange(fk_engine *e, fk_comm *comm, int32_t *merge, int32_
            keeps bins [r * S, (r + 1) * S) of the sum, S = tw / world; the
            counters and every slice's (sum, distinct) are all-reduced */
         const uint64_t S = tw / (uint64_t)world;
-        rc = direct ? fkc_reduce_scatter_from_i32(comm, reinterpret_cast<const int32_t *>(e->d_table), merge, S, e->stream)
-                    : fkc_reduce_scatter_i32(comm, merge, S, e->stream);
+        if (route) {
+            rc = route_exchange(e, comm, counting, merge + (uint64_t)rank * S);
+        } else {
+            rc = direct ? fkc_reduce_scatter_from_i32(comm, reinterpret_cast<const int32_t *>(e->d_table), merge, S,
+                                                      e->stream)
+                        : fkc_reduce_scatter_i32(comm, merge, S, e->stream);
+        }
         if (rc) return rc;
         const uint64_t lo = (uint64_t)rank * S, n = lo < e->nbins ? std::min(S, e->nbins - lo) : 0;
         HIPCHK(hipMemsetAsync(e->d_tmp, 0, 2 * sizeof(unsigned long long), e->stream));

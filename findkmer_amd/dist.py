@@ -64,7 +64,7 @@ and over gloo on the CPU (tests/test_dist_cpu.py, with a model engine).
 import torch
 import torch.distributed as dist
 
-from . import FK_E_EMPTY, FK_E_ROLLOVER, FK_E_SUMMARY, FK_E_UNTERMINATED_HEADER, FK_OK
+from . import FK_E_EMPTY, FK_E_ROLLOVER, FK_E_SUMMARY, FK_E_UNTERMINATED_HEADER, FK_OK, FK_ROUTE_KMIN
 from . import FK_PACK_COUNTERS, FK_PACK_ROW_WORDS, FK_PACK_STATS
 from . import Comm, FindKmerError, FkState, FkSummary, comm_id, lib, shard_rows_compose, summary_apply, summary_is_full
 
@@ -622,8 +622,14 @@ def count_sharded(engine, ptr, nbytes, halo, buf, group=None, times=None, pinned
             times["merge"] = times.get("merge", 0.0) + (time.perf_counter() - t2)
         return res
     nb, tw, merged, _ = _regions(buf, k, world)
+    # k >= FK_ROUTE_KMIN over gloo: each owner gets only the nonzero bins of
+    # its slice (fk_engine_route_*), not the whole table
+    route = shard_table and k >= FK_ROUTE_KMIN and hasattr(engine, "route_pack") and \
+        dist.get_backend(group) != "nccl" and torch.cuda.is_available()
     if counting:
-        if buf.is_cuda:
+        if route:
+            pass
+        elif buf.is_cuda:
             engine.table_to_device(buf.data_ptr())
         else:
             buf[:nb].copy_(torch.from_numpy(engine.table().view("int32")))
@@ -631,13 +637,15 @@ def count_sharded(engine, ptr, nbytes, halo, buf, group=None, times=None, pinned
                 1 if rank == first_end else 0,
                 r.unterminated_header if rank == last else 0]
     else:
-        buf[:nb].zero_()
+        if not route:
+            buf[:nb].zero_()
         vals = [0] * len(COUNTERS)
-    buf[nb:tw].zero_()
+    if not route:
+        buf[nb:tw].zero_()
     buf[tw + COUNTER_SLOTS:tw + COUNTER_SLOTS + STAT_SLOTS].zero_()
     _put_counters(buf, vals, pinned, tw)
     if shard_table:
-        _scatter_tables(buf, k, rank, world, group)
+        _scatter_tables(buf, k, rank, world, group, engine=engine if route else None, counting=counting)
     else:
         sum_tables(merged, group)
     if times is not None:
@@ -649,7 +657,33 @@ def count_sharded(engine, ptr, nbytes, halo, buf, group=None, times=None, pinned
     return ShardedResult(buf, k, rank, first_end, r, world=world, sharded=shard_table, group=group)
 
 
-def _scatter_tables(buf, k, rank, world, group):
+def _route_tables(engine, buf, k, rank, world, group, counting):
+    """The routed sharded merge over torch.distributed (gloo): every rank's
+    blobs (fk_engine_route_pack: the nonzero bins of each owner's slice) go
+    to their owners by all_to_all_single, and the owner counts what it got
+    into its slice (fk_engine_route_absorb), then copies the slice to `buf`."""
+    nb, tw = 1 << (2 * k), table_words(k, world)
+    S = tw // world
+    dev = torch.device("cuda", torch.cuda.current_device())
+    words = engine.route_pack(world, counting)
+    send = torch.empty(max(1, sum(words)), dtype=torch.int32, device=dev)
+    engine.route_copy(send.data_ptr())
+    coll = buf.device
+    rsz = torch.empty(world, dtype=torch.int64, device=coll)
+    dist.all_to_all_single(rsz, torch.tensor(words, dtype=torch.int64, device=coll), group=group)
+    rwords = [int(v) for v in rsz.tolist()]
+    recv = torch.empty(sum(rwords), dtype=torch.int32, device=coll)
+    dist.all_to_all_single(recv, send[:sum(words)].to(coll), rwords, words, group=group)
+    lo = rank * S
+    n = max(0, min(S, nb - lo))
+    mine = torch.zeros(max(1, n), dtype=torch.int32, device=dev)
+    recv_d = recv.to(dev)
+    engine.route_absorb(world, rank, recv_d.data_ptr(), rwords, mine.data_ptr())
+    if n:
+        buf[lo:lo + n].copy_(mine[:n])
+
+
+def _scatter_tables(buf, k, rank, world, group, engine=None, counting=True):
     """The sharded merge through torch.distributed: rank r gets bins
     [r*S, (r+1)*S) of the summed table (a reduce-scatter over RCCL; gloo has
     none, so an all-reduce whose other slices are then ignored), then the
@@ -657,7 +691,9 @@ def _scatter_tables(buf, k, rank, world, group):
     nb, tw = 1 << (2 * k), table_words(k, world)
     S = tw // world
     table = buf[:tw]
-    if dist.get_backend(group) == "nccl":
+    if engine is not None:
+        _route_tables(engine, buf, k, rank, world, group, counting)
+    elif dist.get_backend(group) == "nccl":
         mine = torch.empty(S, dtype=buf.dtype, device=buf.device)
         dist.reduce_scatter_tensor(mine, table, op=dist.ReduceOp.SUM, group=group)
         buf[rank * S:(rank + 1) * S].copy_(mine)

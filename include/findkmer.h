@@ -264,6 +264,26 @@ int  fk_comm_available(int device);
  * (the reference is single-threaded, findKmer.cpp:962). */
 int  fk_engine_shard_exchange(fk_engine *e, fk_comm *comm, int32_t *merge, int32_t *info /* [2], may be NULL */);
 
+/* Routed sharded tables (round 5): for k >= FK_ROUTE_KMIN the stitched
+ * exchange with FK_XCHG_SHARD_TABLE sends each owner only the nonzero bins of
+ * its range instead of reduce-scattering the whole table, when world > 1
+ * (FINDKMER_TUNE route=0: never, route=2: at world 1 too; an RCCL without
+ * ncclSend/ncclRecv reduce-scatters).
+ * The same steps for a caller-driven transport (the gloo rehearsal):
+ *  - fk_engine_route_pack: after fk_engine_finish, the finished table's blobs
+ *    for owners 0..world-1 (words[d] int32 each, side by side; counting == 0:
+ *    empty blobs, for a rank the stream never reached);
+ *  - fk_engine_route_copy: that buffer into a caller-owned device buffer;
+ *  - fk_engine_route_absorb: the blobs `rank` received (words[s] from source
+ *    s, side by side at recv, device memory) counted into its slice of the
+ *    merged table (device, bins [rank*TW/world, ...) of fk_merge_layout).
+ * Replaces no reference call (the reference is single-threaded). */
+#define FK_ROUTE_KMIN 15
+int  fk_engine_route_pack(fk_engine *e, int world, int counting, uint64_t *words /* [world] */);
+int  fk_engine_route_copy(fk_engine *e, void *dst);
+int  fk_engine_route_absorb(fk_engine *e, int world, int rank, const int32_t *recv, const uint64_t *words /* [world] */,
+                            int32_t *slice);
+
 /* Finish the stream (end-of-input rules) and fill *res.  Returns FK_OK or one
  * of FK_E_EMPTY / FK_E_UNTERMINATED_HEADER / FK_E_ROLLOVER (res is filled in
  * every case). */

@@ -160,13 +160,18 @@ def test_sharded_table_gloo_against_oracle(k, world, eof_in, nbytes):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("k,shard,invalid", [(12, 1, 0), (6, 0, 1), (11, 1, 0)])
-def test_rccl_single_rank_sharded_and_fallback(k, shard, invalid):
+@pytest.mark.parametrize("k,shard,invalid", [(12, 1, 0), (6, 0, 1), (11, 1, 0), (15, 1, 0)])
+def test_rccl_single_rank_sharded_and_fallback(k, shard, invalid, monkeypatch):
     """The native RCCL exchange (world 1): the reduce-scatter of the table
     with the slice statistics' all-reduce, and (invalid) a pack row forced
     invalid after the one-collective all-reduce, so that the fallback runs
     the stitched exchange over the merge buffer that collective already
-    changed"""
+    changed.  k = 15: the routed table (fk_engine_route_*: the
+    nonzero bins packed per owner, one grouped ncclSend/ncclRecv, counted
+    into the slice) instead of the reduce-scatter (FINDKMER_TUNE route=2: at
+    world 1 too)"""
+    if k >= 15:
+        monkeypatch.setenv("FINDKMER_TUNE", "route=2")
     out = _torchrun(1, 29850 + 3 * k + shard + 7 * invalid, os.path.join(REPO, "tests", "dist_worker.py"),
                     ["--k", str(k), "--backend", "nccl", "--input", "fasta", "--shard-table", str(shard),
                      "--test-invalid", str(invalid)])
@@ -215,3 +220,60 @@ def test_rccl_single_rank_bench_line_reports_the_world(k, fasta):
     assert out["exchange"] == ("fast" if k <= 7 else "stitched")
     assert set(out["phase_ms_per_step"]) >= {"exchange", "finish"}
     assert all(v >= 0 for v in out["phase_ms_per_step"].values())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k,world", [(15, 3), (16, 2)])
+def test_routed_table_blobs_against_the_summed_tables(k, world):
+    """fk_engine_route_pack / _absorb in one process: `world` engines over
+    different inputs pack their finished tables for `world` owners, each
+    owner's blobs from every source are absorbed into its slice, and the
+    slices side by side == the sum of the engines' tables.  world 3 puts
+    owner boundaries inside 2^15-bin parts; a 300 K-base poly-A stretch
+    gives one bin a count past the 2^17 - 1 an entry holds (the overflow
+    pairs); the last source packs as a rank the stream never reached
+    (counting = 0: empty blobs) and must not count."""
+    import numpy as np
+    import torch
+
+    import findkmer_amd as fk
+    from test_gpu_parity import mixed_input
+    dev = torch.device("cuda", 0)
+    nb = 1 << (2 * k)
+    tw = (nb + world - 1) // world * world
+    S = tw // world
+    inputs = [b"A" * 300_000 + mixed_input(7 + k, 400_000), mixed_input(8 + k, 900_000)]
+    inputs += [mixed_input(9 + k + s, 300_000) for s in range(world - len(inputs))]
+    engines, blobs, words, want = [], [], [], torch.zeros(nb, dtype=torch.int32, device=dev)
+    try:
+        for s, data in enumerate(inputs[:world]):
+            e = fk.Engine(k)
+            engines.append(e)
+            e.feed(np.frombuffer(data, dtype=np.uint8).copy())
+            e.finish(allow=(fk.FK_OK, fk.FK_E_UNTERMINATED_HEADER))
+            counting = s < world - 1 or world == 2
+            w = e.route_pack(world, counting)
+            b = torch.empty(max(1, sum(w)), dtype=torch.int32, device=dev)
+            e.route_copy(b.data_ptr())
+            blobs.append(b)
+            words.append(w)
+            if counting:
+                t = torch.empty(nb, dtype=torch.int32, device=dev)
+                e.table_to_device(t.data_ptr())
+                want += t
+                del t
+        assert words[0][0] > 4 + (S >> 15)   # entries were packed
+        got = torch.empty(tw, dtype=torch.int32, device=dev)
+        for r in range(world):
+            parts, rw = [], []
+            for s in range(world):
+                off = sum(words[s][:r])
+                parts.append(blobs[s][off:off + words[s][r]])
+                rw.append(words[s][r])
+            recv = torch.cat(parts)
+            engines[r].route_absorb(world, r, recv.data_ptr(), rw, got[r * S:].data_ptr())
+        assert torch.equal(got[:nb], want)
+        assert int(want.max()) >= (1 << 17)   # an overflow pair was needed
+    finally:
+        for e in engines:
+            e.close()
