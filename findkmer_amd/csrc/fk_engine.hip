@@ -6079,12 +6079,21 @@ static uint64_t merge_table_words(uint64_t nbins, int world) {
 
 /* the u64 sum and the nonzero bins of one table slice (sharded table) */
 __global__ void __launch_bounds__(256) k_slice_sum(const uint32_t *t, uint64_t n, unsigned long long *out2) {
+    /* 16-B loads between a scalar head (to the first aligned word: a slice
+       starts at rank * S) and tail; one 4-B load per lane left the k = 16
+       slice at 2.2 TB/s */
     unsigned long long sum = 0, nz = 0;
-    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
-        const uint32_t v = t[i];
-        sum += v;
-        nz += v != 0;
+    const uint64_t tid = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x, nth = (uint64_t)gridDim.x * blockDim.x;
+    const uint64_t head = std::min<uint64_t>(n, ((16u - ((uintptr_t)t & 15u)) & 15u) / 4u);
+    const uint64_t n4 = (n - head) / 4;
+    if (tid < head) { const uint32_t v = t[tid]; sum += v; nz += v != 0; }
+    const u32x4 *t4 = reinterpret_cast<const u32x4 *>(t + head);
+    for (uint64_t q = tid; q < n4; q += nth) {
+        const u32x4 v = __builtin_nontemporal_load(t4 + q);
+        sum += (unsigned long long)v.x + v.y + v.z + v.w;
+        nz += (v.x != 0) + (v.y != 0) + (v.z != 0) + (v.w != 0);
     }
+    for (uint64_t i = head + n4 * 4 + tid; i < n; i += nth) { const uint32_t v = t[i]; sum += v; nz += v != 0; }
     sum = wsum64(sum);
     nz = wsum64(nz);
     if ((threadIdx.x & 63) == 0) {
@@ -6120,6 +6129,7 @@ __global__ void k_slice_limbs(const unsigned long long *in2, int32_t *limbs8) {
 #define RT_SH 15u
 #define RT_ESC 0x1FFFFu
 #define RT_HDR 4u
+#define RT_STAT_SLOTS 512u
 
 /* per-destination arrays in one device buffer (u64 each, world W):
    p0 [0,W) first part, sb [W, 2W+1) first slot, np [2W+1, 3W+1) parts,
@@ -6147,9 +6157,10 @@ __device__ __forceinline__ void rt_owners(const RouteGeo &g, uint64_t x0, uint32
     two = d0 + 1 < g.world && b < x0 + (1ull << RT_SH);
 }
 
-/* one block per part: its entries and overflow bins per owner */
+/* one block per part: its entries and overflow bins per owner, and per wave
+   (a quarter of the part each: k_route_write's start positions, wc) */
 __global__ void __launch_bounds__(256)
-k_route_count(const uint32_t *table, RouteGeo g, int counting, uint32_t *cnt) {
+k_route_count(const uint32_t *table, RouteGeo g, int counting, uint32_t *cnt, uint32_t *wc) {
     __shared__ uint32_t ws[4][4];
     const uint32_t p = blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
     const uint64_t x0 = (uint64_t)p << RT_SH;
@@ -6159,13 +6170,13 @@ k_route_count(const uint32_t *table, RouteGeo g, int counting, uint32_t *cnt) {
     rt_owners(g, x0, d0, b, two);
     uint32_t c[4] = {0, 0, 0, 0};   /* entries lo / hi, overflow lo / hi */
     if (counting) {
-        const uint4 *t4 = reinterpret_cast<const uint4 *>(table + x0);
-        for (uint32_t q = t; q < (1u << RT_SH) / 4u; q += 256u) {
-            const uint4 v4 = t4[q];
+        const u32x4 *t4 = reinterpret_cast<const u32x4 *>(table + x0) + (size_t)wv * ((1u << RT_SH) / 16u);
+        for (uint32_t q = lane; q < (1u << RT_SH) / 16u; q += 64u) {
+            const u32x4 v4 = __builtin_nontemporal_load(t4 + q);
             const uint32_t w[4] = {v4.x, v4.y, v4.z, v4.w};
 #pragma unroll
             for (int h = 0; h < 4; h++) {
-                const bool hi = x0 + q * 4u + (uint32_t)h >= b;
+                const bool hi = x0 + wv * ((1u << RT_SH) / 4u) + q * 4u + (uint32_t)h >= b;
                 const uint32_t v = w[h];
                 c[hi ? 1 : 0] += v != 0u && v < RT_ESC;
                 c[hi ? 3 : 2] += v >= RT_ESC;
@@ -6174,9 +6185,12 @@ k_route_count(const uint32_t *table, RouteGeo g, int counting, uint32_t *cnt) {
     }
 #pragma unroll
     for (int i = 0; i < 4; i++) c[i] = wsum32(c[i]);
-    if (lane == 0)
+    if (lane == 0) {
 #pragma unroll
         for (int i = 0; i < 4; i++) ws[wv][i] = c[i];
+        wc[(size_t)p * 8u + wv * 2u] = c[0];
+        wc[(size_t)p * 8u + wv * 2u + 1u] = c[1];
+    }
     __syncthreads();
     if (t == 0) {
         uint32_t s[4] = {0, 0, 0, 0};
@@ -6224,8 +6238,8 @@ k_route_scan(const uint32_t *cnt, uint64_t n, unsigned long long *off) {
    overflow bins appended to the owner's pairs, the slot counts, and (block
    0) every blob's header */
 __global__ void __launch_bounds__(256)
-k_route_write(const uint32_t *table, RouteGeo g, int counting, const uint32_t *cnt, uint32_t *send) {
-    __shared__ uint32_t wc[4][2];
+k_route_write(const uint32_t *table, RouteGeo g, int counting, const uint32_t *cnt, const uint32_t *wc,
+              uint32_t *send) {
     const uint32_t p = blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
     if (p == 0 && t < g.world) {
         const unsigned long long e = g.ne()[t], o = g.no()[t];
@@ -6246,19 +6260,8 @@ k_route_write(const uint32_t *table, RouteGeo g, int counting, const uint32_t *c
     if (!counting) return;
     constexpr uint32_t QW = (1u << RT_SH) / 4u;   /* bins per wave */
     const uint32_t *tw = table + x0 + (uint64_t)wv * QW;
-    uint32_t c0 = 0, c1 = 0;
-    for (uint32_t i = lane; i < QW; i += 64u) {
-        const uint32_t v = tw[i];
-        const bool hi = x0 + wv * QW + i >= b, nz = v != 0u && v < RT_ESC;
-        c0 += nz && !hi;
-        c1 += nz && hi;
-    }
-    c0 = wsum32(c0);
-    c1 = wsum32(c1);
-    if (lane == 0) { wc[wv][0] = c0; wc[wv][1] = c1; }
-    __syncthreads();
     uint64_t pos0 = g.off()[s0] - g.off()[g.sb()[d0]], pos1 = g.off()[s1] - g.off()[g.sb()[d1]];
-    for (uint32_t w = 0; w < wv; w++) { pos0 += wc[w][0]; pos1 += wc[w][1]; }
+    for (uint32_t w = 0; w < wv; w++) { pos0 += wc[(size_t)p * 8u + w * 2u]; pos1 += wc[(size_t)p * 8u + w * 2u + 1u]; }
     uint32_t *e0 = send + g.bb()[d0] + RT_HDR + g.np()[d0], *e1 = send + g.bb()[d1] + RT_HDR + g.np()[d1];
     const unsigned long long lt = (1ull << lane) - 1ull;
     for (uint32_t i0 = 0; i0 < QW; i0 += 64u) {
@@ -6289,7 +6292,7 @@ k_route_write(const uint32_t *table, RouteGeo g, int counting, const uint32_t *c
    (written, not added: the slice holds nothing before) */
 __global__ void __launch_bounds__(1024)
 k_route_absorb(const uint32_t *recv, const unsigned long long *rd, const unsigned long long *roff, uint32_t world,
-               uint32_t np, uint64_t p0, uint64_t lo, uint64_t hi, uint32_t *out) {
+               uint32_t np, uint64_t p0, uint64_t lo, uint64_t hi, uint32_t *out, unsigned long long *stats) {
     extern __shared__ uint32_t bins[];
     const uint32_t j = blockIdx.x, t = threadIdx.x;
     for (uint32_t i = t; i < (1u << RT_SH) / 4u; i += 1024u) reinterpret_cast<uint4 *>(bins)[i] = make_uint4(0, 0, 0, 0);
@@ -6305,19 +6308,59 @@ k_route_absorb(const uint32_t *recv, const unsigned long long *rd, const unsigne
     }
     __syncthreads();
     const uint64_t x0 = (p0 + j) << RT_SH;
+    unsigned long long sum = 0, nz = 0;
     for (uint32_t i = t; i < (1u << RT_SH); i += 1024u) {
         const uint64_t x = x0 + i;
-        if (x >= lo && x < hi) out[x - lo] = bins[i];
+        if (x >= lo && x < hi) {
+            const uint32_t v = bins[i];
+            out[x - lo] = v;
+            sum += v;
+            nz += v != 0;
+        }
+    }
+    /* the slice's total and nonzero bins (k_slice_sum's), before the
+       overflow pairs add theirs (k_route_overflow): a block's sums into one
+       of RT_STAT_SLOTS slot pairs (per-wave atomics on one address took
+       50 ms at k = 16), k_route_stats folds them */
+    if (stats) {
+        __shared__ unsigned long long bs[16][2];
+        sum = wsum64(sum);
+        nz = wsum64(nz);
+        if ((t & 63) == 0) { bs[t >> 6][0] = sum; bs[t >> 6][1] = nz; }
+        __syncthreads();
+        if (t < 2) {
+            unsigned long long a = 0;
+            for (int w = 0; w < 16; w++) a += bs[w][t];
+            if (a) atomicAdd(&stats[(j % RT_STAT_SLOTS) * 2 + t], a);
+        }
+    }
+}
+
+__global__ void __launch_bounds__(256) k_route_stats(const unsigned long long *slots, unsigned long long *out2) {
+    unsigned long long a = 0, b = 0;
+    for (uint32_t i = threadIdx.x; i < RT_STAT_SLOTS; i += 256u) { a += slots[2 * i]; b += slots[2 * i + 1]; }
+    a = wsum64(a);
+    b = wsum64(b);
+    if ((threadIdx.x & 63) == 0) {
+        if (a) atomicAdd(&out2[0], a);
+        if (b) atomicAdd(&out2[1], b);
     }
 }
 
 /* every source's overflow pairs added into the slice */
 __global__ void __launch_bounds__(256)
-k_route_overflow(const uint32_t *recv, const unsigned long long *rd, uint32_t np, uint32_t *out) {
+k_route_overflow(const uint32_t *recv, const unsigned long long *rd, uint32_t np, uint32_t *out,
+                 unsigned long long *stats) {
     const uint32_t *blob = recv + rd[blockIdx.x];
     const uint64_t ne = blob[0] | ((uint64_t)blob[1] << 32), no = blob[2] | ((uint64_t)blob[3] << 32);
     const uint32_t *op = blob + RT_HDR + np + ne;
-    for (uint64_t i = threadIdx.x; i < no; i += 256u) atomicAdd(&out[op[2 * i]], op[2 * i + 1]);
+    for (uint64_t i = threadIdx.x; i < no; i += 256u) {
+        const uint32_t old = atomicAdd(&out[op[2 * i]], op[2 * i + 1]);
+        if (stats) {
+            atomicAdd(&stats[0], (unsigned long long)op[2 * i + 1]);
+            if (old == 0) atomicAdd(&stats[1], 1ull);
+        }
+    }
 }
 
 /* the owners' geometry for (nbins, world) on the host */
@@ -6354,18 +6397,18 @@ static int route_pack(fk_engine *e, int world, bool counting, uint64_t *words) {
     const RouteHost h = route_geometry(e->nbins, world);
     if (h.S < (1ull << RT_SH)) return FK_E_INVALID;   /* (a part spans at most two owners) */
     const uint64_t W = (uint64_t)world;
-    const uint64_t naux = 7 * W + 1 + h.nslots + 1, aux_bytes = naux * 8 + h.nslots * 4 + 16;
+    const uint64_t naux = 7 * W + 1 + h.nslots + 1, aux_bytes = naux * 8 + h.nslots * 4 + (uint64_t)h.nparts * 32 + 16;
     int rc = sp_ensure(&e->d_raux, &e->raux_cap, aux_bytes, 1);
     if (rc) return rc;
     unsigned long long *aux = static_cast<unsigned long long *>(e->d_raux);
-    uint32_t *cnt = reinterpret_cast<uint32_t *>(aux + naux);
+    uint32_t *cnt = reinterpret_cast<uint32_t *>(aux + naux), *wcnt = cnt + h.nslots;
     std::vector<unsigned long long> ha(7 * W + 1, 0);
     for (int d = 0; d < world; d++) { ha[d] = h.p0[d]; ha[2 * W + 1 + d] = h.np[d]; }
     for (int d = 0; d <= world; d++) ha[W + d] = h.sb[d];
     HIPCHK(hipMemcpyAsync(aux, ha.data(), ha.size() * 8, hipMemcpyHostToDevice, e->stream));
     RouteGeo g{e->nbins, h.S, (uint32_t)world, h.nparts, aux};
     hipLaunchKernelGGL(k_route_count, dim3(h.nparts), dim3(256), 0, e->stream, (const uint32_t *)e->d_table, g,
-                       counting ? 1 : 0, cnt);
+                       counting ? 1 : 0, cnt, wcnt);
     HIPCHK(hipGetLastError());
     hipLaunchKernelGGL(k_route_scan, dim3(1), dim3(1024), 0, e->stream, (const uint32_t *)cnt, h.nslots,
                        aux + 7 * W + 1);
@@ -6388,7 +6431,8 @@ static int route_pack(fk_engine *e, int world, bool counting, uint64_t *words) {
     HIPCHK(hipMemcpyAsync(aux + 3 * W + 1, ha.data() + 3 * W + 1, 2 * W * 8, hipMemcpyHostToDevice, e->stream));
     HIPCHK(hipMemsetAsync(aux + 6 * W + 1, 0, W * 8, e->stream));
     hipLaunchKernelGGL(k_route_write, dim3(h.nparts), dim3(256), 0, e->stream, (const uint32_t *)e->d_table, g,
-                       counting ? 1 : 0, (const uint32_t *)cnt, reinterpret_cast<uint32_t *>(e->d_rsend));
+                       counting ? 1 : 0, (const uint32_t *)cnt, (const uint32_t *)wcnt,
+                       reinterpret_cast<uint32_t *>(e->d_rsend));
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(e->stream));
     return FK_OK;
@@ -6396,7 +6440,8 @@ static int route_pack(fk_engine *e, int world, bool counting, uint64_t *words) {
 
 /* fk_engine_route_absorb: the blobs received from every source (words[s]
    each, side by side at recv) into this rank's slice of the merged table */
-static int route_absorb(fk_engine *e, int world, int rank, const int32_t *recv, const uint64_t *words, int32_t *slice) {
+static int route_absorb(fk_engine *e, int world, int rank, const int32_t *recv, const uint64_t *words, int32_t *slice,
+                        unsigned long long *stats) {
     if (e->sparse || e->k < 8 || world < 1 || rank < 0 || rank >= world) return FK_E_INVALID;
     const RouteHost h = route_geometry(e->nbins, world);
     if (h.S < (1ull << RT_SH)) return FK_E_INVALID;
@@ -6420,10 +6465,12 @@ static int route_absorb(fk_engine *e, int world, int rank, const int32_t *recv, 
                        no = hdr[4 * s + 2] | ((uint64_t)hdr[4 * s + 3] << 32);
         if (RT_HDR + np + ne + 2 * no != words[s]) return FK_E_INVALID;
     }
-    const uint64_t aux_bytes = (W + W * (np + 1)) * 8 + 16;
+    const uint64_t aux_bytes = (W + W * (np + 1) + 2 * RT_STAT_SLOTS) * 8 + 16;
     int rc = sp_ensure(&e->d_raux, &e->raux_cap, aux_bytes, 1);
     if (rc) return rc;
-    unsigned long long *drd = static_cast<unsigned long long *>(e->d_raux), *roff = drd + W;
+    unsigned long long *drd = static_cast<unsigned long long *>(e->d_raux), *roff = drd + W,
+                       *sslots = roff + W * (np + 1);
+    if (stats) HIPCHK(hipMemsetAsync(sslots, 0, 2 * RT_STAT_SLOTS * 8, e->stream));
     HIPCHK(hipMemcpyAsync(drd, rd.data(), W * 8, hipMemcpyHostToDevice, e->stream));
     const uint32_t *r32 = reinterpret_cast<const uint32_t *>(recv);
     for (int s = 0; s < world; s++) {
@@ -6436,11 +6483,15 @@ static int route_absorb(fk_engine *e, int world, int rank, const int32_t *recv, 
     uint32_t *out = reinterpret_cast<uint32_t *>(slice);
     hipLaunchKernelGGL(k_route_absorb, dim3((uint32_t)np), dim3(1024), (size_t)1 << 17, e->stream, r32,
                        (const unsigned long long *)drd, (const unsigned long long *)roff, (uint32_t)world, (uint32_t)np,
-                       (uint64_t)h.p0[rank], lo, hi, out);
+                       (uint64_t)h.p0[rank], lo, hi, out, stats ? sslots : nullptr);
     HIPCHK(hipGetLastError());
     hipLaunchKernelGGL(k_route_overflow, dim3((uint32_t)world), dim3(256), 0, e->stream, r32,
-                       (const unsigned long long *)drd, (uint32_t)np, out);
+                       (const unsigned long long *)drd, (uint32_t)np, out, stats);
     HIPCHK(hipGetLastError());
+    if (stats) {
+        hipLaunchKernelGGL(k_route_stats, dim3(1), dim3(256), 0, e->stream, (const unsigned long long *)sslots, stats);
+        HIPCHK(hipGetLastError());
+    }
     HIPCHK(hipStreamSynchronize(e->stream));
     return FK_OK;
 }
@@ -6466,13 +6517,13 @@ extern "C" int fk_engine_route_absorb(fk_engine *e, int world, int rank, const i
     if (!e || !recv || !words || !slice) return FK_E_INVALID;
     int rc = set_dev(e);
     if (rc) return rc;
-    return route_absorb(e, world, rank, recv, words, slice);
+    return route_absorb(e, world, rank, recv, words, slice, nullptr);
 }
 
 /* the routed exchange over RCCL: blobs packed, their sizes all-reduced as a
    world x world matrix of 16-bit limbs, one grouped send/recv, the received
    blobs into this rank's slice */
-static int route_exchange(fk_engine *e, fk_comm *comm, bool counting, int32_t *slice) {
+static int route_exchange(fk_engine *e, fk_comm *comm, bool counting, int32_t *slice, unsigned long long *stats) {
     const int world = fkc_world(comm), rank = fkc_rank(comm);
     const uint64_t W = (uint64_t)world;
     std::vector<uint64_t> sw(W), rw(W), sd(W), rdsp(W);
@@ -6503,7 +6554,7 @@ static int route_exchange(fk_engine *e, fk_comm *comm, bool counting, int32_t *s
     if (rc) return rc;
     rc = fkc_alltoallv_i32(comm, e->d_rsend, sw.data(), sd.data(), e->d_rrecv, rw.data(), rdsp.data(), e->stream);
     if (rc) return rc;
-    return route_absorb(e, world, rank, e->d_rrecv, rw.data(), slice);
+    return route_absorb(e, world, rank, e->d_rrecv, rw.data(), slice, stats);
 }
 
 static int stitched_exchange(fk_engine *e, fk_comm *comm, int32_t *merge, int32_t *first_end_out, bool scatter) {
@@ -6588,8 +6639,9 @@ static int stitched_exchange(fk_engine *e, fk_comm *comm, int32_t *merge, int32_
            keeps bins [r * S, (r + 1) * S) of the sum, S = tw / world; the
            counters and every slice's (sum, distinct) are all-reduced */
         const uint64_t S = tw / (uint64_t)world;
-        if (route) {
-            rc = route_exchange(e, comm, counting, merge + (uint64_t)rank * S);
+        HIPCHK(hipMemsetAsync(e->d_tmp, 0, 2 * sizeof(unsigned long long), e->stream));
+        if (route) {   /* (the slice's total and nonzero bins as it is absorbed) */
+            rc = route_exchange(e, comm, counting, merge + (uint64_t)rank * S, e->d_tmp);
         } else {
             rc = direct ? fkc_reduce_scatter_from_i32(comm, reinterpret_cast<const int32_t *>(e->d_table), merge, S,
                                                       e->stream)
@@ -6597,9 +6649,8 @@ static int stitched_exchange(fk_engine *e, fk_comm *comm, int32_t *merge, int32_
         }
         if (rc) return rc;
         const uint64_t lo = (uint64_t)rank * S, n = lo < e->nbins ? std::min(S, e->nbins - lo) : 0;
-        HIPCHK(hipMemsetAsync(e->d_tmp, 0, 2 * sizeof(unsigned long long), e->stream));
-        if (n) {
-            const unsigned gr = (unsigned)std::min<uint64_t>((uint64_t)e->cus * 4, (n + 255) / 256);
+        if (n && !route) {
+            const unsigned gr = (unsigned)std::min<uint64_t>((uint64_t)e->cus * 8, (n + 1023) / 1024);
             hipLaunchKernelGGL(k_slice_sum, dim3(gr), dim3(256), 0, e->stream,
                                reinterpret_cast<const uint32_t *>(merge) + lo, n, e->d_tmp);
         }
