@@ -3115,17 +3115,49 @@ k_bucket16(PartGeo pg, uint32_t *table) {
     uint32_t *dst = nullptr;
     if (pg.pairs) dst = b < pg.npair ? pg.pairs + ((size_t)b << 16) : pg.singles + ((size_t)(b - pg.npair) << 16);
     const uint64_t base = (uint64_t)b << 16;
+    /* fresh (round 5: the segment's k_zero left the table out, the general
+       tiles' windows wait in pg.glist): every bin of the slice written, no
+       read, and the table statistics taken here (pg.fz, as k_count_parts) */
+    const bool fresh = pg.glist != nullptr && !pg.pairs;
+    unsigned long long sd = 0, l0 = 0, l1 = 0, l2 = 0, l3 = 0;
     auto out2 = [&](uint32_t i2, uint32_t lo, uint32_t hi) {   /* bins 2 i2, 2 i2 + 1 */
-        if (!(lo | hi) && !pg.pairs) return;
+        if (!(lo | hi) && !pg.pairs && !fresh) return;
         if (pg.pairs) {
             reinterpret_cast<uint2 *>(dst)[i2] = make_uint2(lo, hi);
         } else {
             /* sigma maps the last digit 0 1 2 3 -> 0 1 3 2: the pair stays
                adjacent, swapped when the last digit of 2 i2 is 2 */
             uint2 *t2 = reinterpret_cast<uint2 *>(table + (fk_sigma(base | (2u * i2)) & ~1ull));
+            if (fresh) {
+                *t2 = (i2 & 1u) ? make_uint2(hi, lo) : make_uint2(lo, hi);
+                sd += (lo != 0u) + (hi != 0u);
+                if (i2 & 1u) { l3 += lo; l2 += hi; } else { l0 += lo; l1 += hi; }
+                return;
+            }
             uint2 o = *t2;
             if (i2 & 1u) { o.x += hi; o.y += lo; } else { o.x += lo; o.y += hi; }
             *t2 = o;
+        }
+    };
+    /* the block's statistics into one of the FZ_SLOTS partials: distinct,
+       sum, last-base marginals, and the sum under the slice's first base
+       (the slice's bins share their top 16 index bits) */
+    __shared__ unsigned long long fzw[16][6];
+    auto fz_flush = [&]() {
+        if (!fresh) return;
+        unsigned long long v6[6] = {sd, l0 + l1 + l2 + l3, l0, l1, l2, l3};
+#pragma unroll
+        for (int q = 0; q < 6; q++) v6[q] = wsum64(v6[q]);
+        if ((threadIdx.x & 63) == 0)
+#pragma unroll
+            for (int q = 0; q < 6; q++) fzw[threadIdx.x >> 6][q] = v6[q];
+        __syncthreads();
+        if (threadIdx.x < 10) {
+            const uint32_t q = threadIdx.x;
+            unsigned long long t = 0;
+            for (uint32_t w = 0; w < 16; w++) t += fzw[w][q < 6 ? q : 1u];
+            if (q >= 6 && (uint32_t)((fk_sigma(base) >> (2 * pg.kk - 2)) & 3u) != q - 6u) t = 0;
+            if (t) atomicAdd(&pg.fz[(blockIdx.x % FZ_SLOTS) * 10u + q], t);
         }
     };
     for (uint32_t i = threadIdx.x; i < NW / 4u; i += blockDim.x) reinterpret_cast<uint4 *>(bins)[i] = make_uint4(0, 0, 0, 0);
@@ -3150,6 +3182,7 @@ k_bucket16(PartGeo pg, uint32_t *table) {
     for (int w = 0; w < 16; w++) { sa += red[0][w]; sc += red[1][w]; }
     if (sa == sc) {
         for (uint32_t i = threadIdx.x; i < NW; i += blockDim.x) out2(i, bins[i] & 0xFFFFu, bins[i] >> 16);
+        fz_flush();
         return;
     }
     /* a 16-bit bin wrapped: the slice again, as two halves of 2^15 32-bit bins */
@@ -3166,6 +3199,7 @@ k_bucket16(PartGeo pg, uint32_t *table) {
             out2(i2, bins[2u * i], bins[2u * i + 1u]);
         }
     }
+    fz_flush();
 }
 
 /*
@@ -3505,13 +3539,14 @@ k_list_add(const uint32_t *list, uint32_t *table, int k, unsigned long long *fz)
  * 4x + b and the suffix of the pairs b*4^k + x (a pair stands for both of
  * its k-mers), plus the single windows counted at x */
 __global__ void __launch_bounds__(256)
-k_pair_fold(const uint32_t *pairs, const uint32_t *singles, uint64_t nbins, uint32_t *table) {
+k_pair_fold(const uint32_t *pairs, const uint32_t *singles, uint64_t nbins, uint32_t *table, int fresh) {
     for (uint64_t x = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; x < nbins; x += (uint64_t)gridDim.x * blockDim.x) {
         const uint4 pre = reinterpret_cast<const uint4 *>(pairs)[x];
         uint32_t v = pre.x + pre.y + pre.z + pre.w + singles[x];
 #pragma unroll
         for (int b = 0; b < 4; b++) v += pairs[(uint64_t)b * nbins + x];
-        if (v) table[fk_sigma(x)] += v;
+        if (fresh) table[fk_sigma(x)] = v;   /* (a fresh table: k_zero left it out) */
+        else if (v) table[fk_sigma(x)] += v;
     }
 }
 
@@ -4408,6 +4443,7 @@ struct fk_engine {
     uint64_t glist_cap = 0;
     unsigned long long *d_fz = nullptr;       /* ... and its statistics from k_count_parts (FZ_SLOTS x 10) */
     bool fz_ready = false;                    /* the next launch_table_stats may take them */
+    bool glist_live = false;                  /* ... and must check the general tiles' list for overflow */
     unsigned long long *d_perr = nullptr;     /* k = 15, 16: k_repart / k_count_parts bound-check bits */
     bool perr_live = false;                   /* ... set by the last launch_part, for the next statistics */
     uint64_t glist_force = 0;                 /* FINDKMER_TUNE glist_cap=N: the list's capacity (tests) */
@@ -4544,6 +4580,7 @@ static int zero_all(fk_engine *e) {
     /* statistics a fresh two-level count left for the next launch_table_stats
        belong to the count this reset discards */
     e->fz_ready = false;
+    e->glist_live = false;
     e->perr_live = false;
     return FK_OK;
 }
@@ -4950,12 +4987,14 @@ static int launch_table_stats(fk_engine *e, bool zero_first, hipEvent_t stop = n
     if (++e->res_seq == 0) e->res_seq = 1;
     const bool fz = e->fz_ready;   /* only for the statistics right after a fresh two-level count */
     e->fz_ready = false;
+    const bool gl = fz || e->glist_live;
+    e->glist_live = false;
     unsigned long long *perr = e->perr_live ? e->d_perr : nullptr;
     e->perr_live = false;
     hipExtLaunchKernelGGL(k_table_stats, dim3(gd), dim3(256), 0, e->stream, nullptr, split ? nullptr : stop, 0,
                           e->d_table, e->nbins, e->k, e->d_res, e->d_acc, e->d_facc, fresh ? 1 : 0, e->h_res_dev,
                           e->d_done, e->res_seq, e->d_sub, (subs && e->d_sub) ? FK_SUBTABLES : 0, e->d_tpart, split,
-                          fz ? (const unsigned long long *)e->d_fz : nullptr, fz ? (const uint32_t *)e->d_glist : nullptr,
+                          fz ? (const unsigned long long *)e->d_fz : nullptr, gl ? (const uint32_t *)e->d_glist : nullptr,
                           (const unsigned long long *)perr);
     HIPCHK(hipGetLastError());
     if (split) {
@@ -5031,7 +5070,8 @@ static int launch_part(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t l
     pg.fz = nullptr;
     pg.kk = (uint32_t)k;
     e->fz_ready = false;
-    if (c32 && e->tab_fresh && !exact) {
+    e->glist_live = false;
+    if ((c32 || w16) && e->tab_fresh && !exact) {
         /* the general tiles' windows go to a list (hist_add): at most
            part_general + 3 general tiles per range (the comment lines or run
            breaks k_part takes and the bases-only tiles around them, the
@@ -5055,7 +5095,10 @@ static int launch_part(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t l
         HIPCHK(hipGetLastError());
         pg.glist = e->d_glist;
         pg.fz = e->d_fz;
-        e->fz_ready = true;
+        /* the statistics: k_count_parts / k_bucket16 take them (pairs mode:
+           k_table_stats reads the folded table) */
+        e->fz_ready = !pairs;
+        e->glist_live = true;
     }
     e->tab_fresh = false;
     if (pairs) {
@@ -5176,6 +5219,11 @@ static int launch_part(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t l
             hipLaunchKernelGGL(k_bucket16<true>, dim3(pg.nbk), dim3(1024), (size_t)1 << 17, e->stream, pg, e->d_table);
         else
             hipLaunchKernelGGL(k_bucket16<false>, dim3(pg.nbk), dim3(1024), (size_t)1 << 17, e->stream, pg, e->d_table);
+        if (pg.glist && !pairs) {   /* (pairs mode: after k_pair_fold below) */
+            HIPCHK(hipGetLastError());
+            hipLaunchKernelGGL(k_list_add, dim3((unsigned)e->cus * 4), dim3(256), 0, e->stream, pg.glist, e->d_table,
+                               k, pg.fz);
+        }
     } else if (padded) {
         hipLaunchKernelGGL(k_bucket_count<BK_PAD>, dim3(pg.nslices * groups), dim3(1024), bc_lds, e->stream, pg,
                            groups, e->d_table);
@@ -5186,8 +5234,13 @@ static int launch_part(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t l
     if (pairs) {
         const unsigned fg = (unsigned)std::min<uint64_t>((uint64_t)e->cus * 4, (e->nbins + 255) / 256);
         hipLaunchKernelGGL(k_pair_fold, dim3(fg), dim3(256), 0, e->stream, e->d_pairs, e->d_pairs + e->nbins * 4,
-                           e->nbins, e->d_table);
+                           e->nbins, e->d_table, pg.glist ? 1 : 0);
         HIPCHK(hipGetLastError());
+        if (pg.glist) {
+            hipLaunchKernelGGL(k_list_add, dim3((unsigned)e->cus * 4), dim3(256), 0, e->stream, pg.glist, e->d_table,
+                               k, pg.fz);
+            HIPCHK(hipGetLastError());
+        }
     }
     return FK_OK;
 }
@@ -5413,7 +5466,9 @@ static int count_segment(fk_engine *e, const uint8_t *dbuf, uint64_t len, int64_
        table, so the reset leaves the table out (16 GiB at k = 16); not where
        the int32 seqSize zone can be reached (its recount needs the zeroed
        table, and k_part<RES> counts such tiles with the general walk) */
-    e->tab_fresh = e->part && e->k >= 15 && e->zero_pending && !e->no_mixed && !int32_zone_possible(e, len);
+    /* (k = 12..14 through k_bucket16 too, round 5) */
+    e->tab_fresh = e->part && (e->k >= 15 || (e->k >= 12 && ((e->w16_ks >> e->k) & 1u))) && e->zero_pending &&
+                   !e->no_mixed && !int32_zone_possible(e, len);
     if (fresh) {
         e->zero_pending = false;
     } else {

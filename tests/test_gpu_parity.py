@@ -737,10 +737,12 @@ def _assert_same_sparse_view(data, k, feeds=None, want_nodes=True):
 
 
 @pytest.mark.parametrize("k,tune", [(15, "glist_cap=1"), (16, "glist_cap=4096"), (15, "no_mixed=1"),
-                                    (16, "part_general=5")])
+                                    (16, "part_general=5"), (12, "glist_cap=1"), (13, "glist_cap=1"),
+                                    (14, "part_general=5")])
 def test_fresh_table_window_list_never_truncates(k, tune, monkeypatch):
-    """k = 15, 16 right after a reset: k_count_parts writes every bin (no
-    zeroing) and the general tiles' windows go to a list added afterwards.
+    """k = 12..16 right after a reset: k_count_parts / k_bucket16 (k_pair_fold
+    at k = 12) write every bin (no zeroing) and the general tiles' windows go
+    to a list added afterwards.
     A list forced tiny (glist_cap) overflows on header-dense input: the
     overflow is flagged on the device (FK_FAULT_LIST) and the segment counted
     again from its exact range states, never truncated.
