@@ -6953,22 +6953,25 @@ k_kpart(const KT *keys, uint64_t n, PartGeo pg, uint64_t lo, uint64_t hi, uint32
    inclusive prefix published.  Returns the exclusive prefix.  Every earlier
    block was dispatched before this one and publishes unconditionally; the
    spin bound only guards a broken invariant (FK_FAULT_PARTS: the pass fails
-   with FK_E_INTERNAL instead of hanging the GPU). */
+   with FK_E_INTERNAL instead of hanging the GPU).  The flags are relaxed
+   agent-scope atomics: a flag word carries all a reader needs (status and
+   value in one 64-bit access), and a release store would write back this
+   XCD's whole L2 -- the parts' output just written -- once per part. */
 __device__ unsigned long long chain_prefix(unsigned long long *flags, uint32_t blk, uint32_t total,
                                            unsigned long long *err) {
     const uint32_t lane = threadIdx.x & 63;
     const unsigned long long A = 1ull << 62, P = 2ull << 62, M = (1ull << 62) - 1;
     if (blk == 0) {
-        if (lane == 0) __hip_atomic_store(&flags[0], P | total, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        if (lane == 0) __hip_atomic_store(&flags[0], P | total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         return 0;
     }
-    if (lane == 0) __hip_atomic_store(&flags[blk], A | total, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    if (lane == 0) __hip_atomic_store(&flags[blk], A | total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     unsigned long long pre = 0;
     int64_t j = (int64_t)blk - 1;
     uint64_t spin = 0;
     for (;;) {
         const int64_t idx = j - (int64_t)lane;
-        unsigned long long f = idx >= 0 ? __hip_atomic_load(&flags[idx], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) : P;
+        unsigned long long f = idx >= 0 ? __hip_atomic_load(&flags[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : P;
         /* wait only for the flags up to the nearest inclusive prefix (the
            blocks farther back may still be counting) */
         for (;;) {
@@ -6980,7 +6983,7 @@ __device__ unsigned long long chain_prefix(unsigned long long *flags, uint32_t b
                 return pre;
             }
             __builtin_amdgcn_s_sleep(1);
-            if ((f >> 62) == 0) f = __hip_atomic_load(&flags[idx], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+            if ((f >> 62) == 0) f = __hip_atomic_load(&flags[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         const unsigned long long pm = __ballot((f >> 62) == 2);
         const unsigned long long val = f & M;
@@ -6992,7 +6995,7 @@ __device__ unsigned long long chain_prefix(unsigned long long *flags, uint32_t b
         pre += wsum64(val);
         j -= 64;
     }
-    if (lane == 0) __hip_atomic_store(&flags[blk], P | (pre + total), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    if (lane == 0) __hip_atomic_store(&flags[blk], P | (pre + total), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return pre;
 }
 
