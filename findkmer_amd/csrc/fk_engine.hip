@@ -6999,12 +6999,18 @@ __device__ unsigned long long chain_prefix(unsigned long long *flags, uint32_t b
     return pre;
 }
 
-/* the bins of a part: thread t takes bins [32 t, 32 t + 32) */
+/* the bins of a part: thread t takes bins [32 t, 32 t + 32).  The 2^15
+   bins are 16-bit halves of 2^14 LDS words (64 KiB instead of 128: half the
+   zeroing and reading, 16.9 -> 13.1 ms per k = 17 pass; a second block per
+   CU would need <= 64 VGPRs, and forced there the spills made it 21 ms).  A half that wraps (a k-mer 65536 times in
+   one part) makes the halves' sum fall short of the codes: the part is then
+   counted again as two halves of 2^14 32-bit bins. */
+#define KC_WORDS (1u << 14)
 __global__ void __launch_bounds__(1024)
 k_kp_count(const uint16_t *in, const PartMeta *meta, uint64_t cap_in, uint64_t lo, uint64_t npads,
            const unsigned long long *tcount, uint32_t nparts, int k, unsigned long long *flags, uint64_t *out_k,
            uint32_t *out_c, unsigned long long *slots, uint64_t *fl, unsigned long long *err) {
-    extern __shared__ uint32_t bins[];   /* 2^15 */
+    extern __shared__ uint32_t bins[];   /* KC_WORDS */
     __shared__ unsigned long long wred[16][10];
     __shared__ uint32_t hpre[24];
     __shared__ uint32_t wnz[16], wmx[16];
@@ -7016,7 +7022,7 @@ k_kp_count(const uint16_t *in, const PartMeta *meta, uint64_t cap_in, uint64_t l
        running, and across the 8 XCDs (and other processes' kernels)
        blockIdx order is not start order */
     if (t == 0) vblk = (uint32_t)atomicAdd(&flags[nparts], 1ull);
-    for (uint32_t i = t; i < (1u << 13); i += 1024u) reinterpret_cast<uint4 *>(bins)[i] = make_uint4(0, 0, 0, 0);
+    for (uint32_t i = t; i < KC_WORDS / 4u; i += 1024u) reinterpret_cast<uint4 *>(bins)[i] = make_uint4(0, 0, 0, 0);
     if (t < 24) hpre[t] = 0;
     __syncthreads();
     const uint32_t blk = vblk;
@@ -7028,27 +7034,71 @@ k_kp_count(const uint16_t *in, const PartMeta *meta, uint64_t cap_in, uint64_t l
     }
     const uint4 *g4 = reinterpret_cast<const uint4 *>(in + m.off);
     const uint32_t nq = (m.n + 7u) >> 3;
+    /* each code to its bin, bin b at half b & 1 of word b >> 1 (hsel: the
+       32-bit pass of half h, bins [h 2^14, (h + 1) 2^14) only) */
+    auto count = [&](int hsel) {
 #ifndef KPX_NOCNT
-    for (uint32_t q = t; q < nq; q += 1024u) {
-        const uint4 v = g4[q];
-        const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+        for (uint32_t q = t; q < nq; q += 1024u) {
+            const uint4 v = g4[q];
+            const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-        for (int h = 0; h < 8; h++)
-            if (q * 8u + (uint32_t)h < m.n) atomicAdd(&bins[(w4[h >> 1] >> (16 * (h & 1))) & 0x7FFFu], 1u);
-    }
+            for (int h = 0; h < 8; h++) {
+                if (q * 8u + (uint32_t)h >= m.n) continue;
+                const uint32_t b = (w4[h >> 1] >> (16 * (h & 1))) & 0x7FFFu;
+                if (hsel < 0) atomicAdd(&bins[b >> 1], 1u << ((b & 1u) << 4));
+                else if ((b >> 14) == (uint32_t)hsel) atomicAdd(&bins[b & (KC_WORDS - 1u)], 1u);
+            }
+        }
 #endif
+    };
+    count(-1);
     __syncthreads();
+    /* thread t's 32 bins: words [16 t, 16 t + 16) */
+    uint32_t c[32];
+    unsigned long long hs = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < 4u; j++) {
+        const uint4 q = reinterpret_cast<const uint4 *>(bins)[t * 4u + j];
+        const uint32_t w4[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+        for (int h = 0; h < 4; h++) {
+            c[8 * j + 2 * h] = w4[h] & 0xFFFFu;
+            c[8 * j + 2 * h + 1] = w4[h] >> 16;
+            hs += (w4[h] & 0xFFFFu) + (w4[h] >> 16);
+        }
+    }
+    {   /* the wrap check (block-wide: the halves' sum against the codes) */
+        const unsigned long long a = wsum64(hs);
+        if (lane == 0) wred[wv][0] = a;
+        __syncthreads();
+        unsigned long long sa = 0;
+#pragma unroll
+        for (uint32_t w = 0; w < 16u; w++) sa += wred[w][0];
+#ifndef KPX_NOCNT
+        if (sa != (unsigned long long)m.n) {
+            for (int h = 0; h < 2; h++) {
+                __syncthreads();
+                for (uint32_t i = t; i < KC_WORDS / 4u; i += 1024u)
+                    reinterpret_cast<uint4 *>(bins)[i] = make_uint4(0, 0, 0, 0);
+                __syncthreads();
+                count(h);
+                __syncthreads();
+                if ((t >> 9) == (uint32_t)h) {   /* (thread t's bins lie in half t / 512) */
+#pragma unroll
+                    for (uint32_t j = 0; j < 8u; j++) {
+                        const uint4 q = reinterpret_cast<const uint4 *>(bins)[(t & 511u) * 8u + j];
+                        c[4 * j] = q.x; c[4 * j + 1] = q.y; c[4 * j + 2] = q.z; c[4 * j + 3] = q.w;
+                    }
+                }
+            }
+        }
+#endif
+        __syncthreads();   /* (wred is reused below) */
+    }
     /* the top key (relative 0xFFFFFFFF, the last bin of the last part) was
        only counted (k_kpart): its real windows, the pads taken off */
     const unsigned long long extra = blk == nparts - 1u ? *tcount - npads : 0ull;
-    if (t == 0 && extra) bins[0x7FFFu] += (uint32_t)extra;
-    __syncthreads();
-    uint32_t c[32];
-#pragma unroll
-    for (uint32_t j = 0; j < 8u; j++) {
-        const uint4 q = reinterpret_cast<const uint4 *>(bins)[t * 8u + j];
-        c[4 * j] = q.x; c[4 * j + 1] = q.y; c[4 * j + 2] = q.z; c[4 * j + 3] = q.w;
-    }
+    if (t == 1023u && extra) c[31] += (uint32_t)extra;
     const int fs = 2 * (k - 1);
     const uint64_t kb = lo + ((uint64_t)blk << 15) + t * 32u;   /* key of my first bin (a multiple of 4) */
     /* statistics with constant register indices (a runtime index into a
@@ -7142,7 +7192,7 @@ k_kp_count(const uint16_t *in, const PartMeta *meta, uint64_t cap_in, uint64_t l
        one thread writing its own bins strided the stores 64 lines per
        instruction, and the output (12 B per distinct k-mer, ~90 GB per
        10 G-base step) cost more than the count */
-    constexpr uint32_t KC_STAGE = 16384u;
+    constexpr uint32_t KC_STAGE = 8192u;   /* (u16 + u32 each: 48 KiB of the 64) */
     uint16_t *sidx = reinterpret_cast<uint16_t *>(bins);
     uint32_t *scnt = bins + KC_STAGE / 2u;
     const uint64_t kpart = lo + ((uint64_t)blk << 15);
@@ -7555,7 +7605,7 @@ static int sp_count_runs32(fk_engine *e, const uint32_t *keys, uint64_t n, uint6
     hipLaunchKernelGGL(k_repart<uint16_t>, dim3(2048u / REPART_G), dim3(1024), 0, e->stream, pg, e->d_parts, alloc,
                        meta, (uint64_t)e->parts_cap, alloc + 1, 15u, nullptr);
     HIPCHK(hipGetLastError());
-    hipLaunchKernelGGL(k_kp_count, dim3(nparts), dim3(1024), (size_t)1 << 17, e->stream, (const uint16_t *)e->d_parts,
+    hipLaunchKernelGGL(k_kp_count, dim3(nparts), dim3(1024), (size_t)KC_WORDS * 4, e->stream, (const uint16_t *)e->d_parts,
                        (const PartMeta *)meta, (uint64_t)e->parts_cap, lo, npads, (const unsigned long long *)tcount, nparts,
                        k, flags.as<unsigned long long>(), out_k, out_c, slots.as<unsigned long long>(), fl.as<uint64_t>(),
                        alloc + 1);
@@ -7700,7 +7750,8 @@ static int sparse_finish(fk_engine *e, int32_t seq) {
                                    (int)(KS_CAP * 6 + 16)));
         HIPCHK(hipFuncSetAttribute((const void *)k_kp_sort<KS_CAP_S>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                    (int)(KS_CAP_S * 6 + 16)));
-        HIPCHK(hipFuncSetAttribute((const void *)k_kp_count, hipFuncAttributeMaxDynamicSharedMemorySize, 1 << 17));
+        HIPCHK(hipFuncSetAttribute((const void *)k_kp_count, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   (int)(KC_WORDS * 4)));
     }
     DevScratch acc, bh, ctr, pctr;
     if (!acc.alloc(FKS_ACC_N * sizeof(unsigned long long)) || !bh.alloc((size_t)nbk * 8) || !ctr.alloc(24) ||

@@ -963,6 +963,18 @@ def test_sparse_key_range_passes(k, monkeypatch):
     assert_same_sparse(mixed_input(1300 + k, 300_000), k)
 
 
+@pytest.mark.parametrize("k", [17])
+def test_sparse_count_bins_wrap_and_top_key(k):
+    """k_kp_count's 16-bit bins: a 70 K-base poly-A stretch puts ~70 K windows
+    into one bin of part 0 (the halves' sum falls short: the part is counted
+    again in 32-bit halves), and a 70 K-base poly-T stretch ~70 K windows of
+    the top key 4^k - 1, which k_kpart counts apart and the last part adds"""
+    rng = random.Random(k)
+    body = b"A" * 70_000 + bytes(rng.choices(b"ACGT", k=300_000)) + b"T" * 70_000
+    lines = b"\n".join(body[i:i + 60] for i in range(0, len(body), 60))
+    assert_same_sparse(b">w\n" + lines + b"\n", k)
+
+
 def test_sparse_shared_walk_falls_back_alone(monkeypatch):
     """k=20, sp_pass=300000: ~4 wide passes share one emit walk; the first
     holds a poly-A stretch (100k windows of key 0, one part past k_kp_sort's
