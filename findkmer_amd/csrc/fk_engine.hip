@@ -3226,8 +3226,19 @@ struct PartMeta {
     uint32_t n, pad;
 };
 #define REPART_MAXP 64u       /* parts per coarse slice (k = 16) */
-#define REPART_G 8u           /* coarse slices per k_repart block */
-#define REPART_GP (REPART_G * REPART_MAXP)   /* parts per block: G x parts per slice <= this */
+/* coarse slices per k_repart block, and (16-bit parts) two blocks per CU:
+   <= 64 VGPRs (a few spill) beside 72 KiB of LDS each.  k = 16 1 G-base
+   step 11.5 -> 10.5 ms, k = 17 10 G-base 204 -> 195 ms against G = 8 with
+   one block per CU (G = 4 alone: 10.8 / 198) */
+#ifndef REPART_G
+#define REPART_G 4u
+#endif
+#ifndef REPART_MINW
+#define REPART_MINW 8
+#endif
+/* parts per block: G x parts per slice (16-bit parts: up to REPART_MAXP a
+   slice; the wide sparse passes' 32-bit parts: REPART_METAP) */
+#define REPART_GP(OT, G) ((G) * (sizeof(OT) == 2 ? REPART_MAXP : REPART_METAP))
 #define REPART_METAP 128u     /* meta entries per coarse slice (wide sparse passes: 128 parts, G = 4) */
 #define REPART_CAP 32768u     /* entries per pass-B round: a batch (16 waves x 2048), the longest run */
 static_assert(16u * FK_TILE_BYTES <= REPART_CAP, "a C32 row's run fits one k_repart round");
@@ -3236,14 +3247,20 @@ static_assert(16u * FK_TILE_BYTES <= REPART_CAP, "a C32 row's run fits one k_rep
    low 15 bits (k = 15, 16; k = 17 passes, psh = 15).  OT = uint32_t (wide
    sparse passes): part bits [psh, psh + 6), stored as the low psh bits. */
 template <typename OT, uint32_t G = REPART_G>
-__global__ void __launch_bounds__(1024)
+__global__ void __launch_bounds__(1024, sizeof(OT) == 2 ? REPART_MINW : 1)
 k_repart(PartGeo pg, OT *out, unsigned long long *alloc, PartMeta *meta, uint64_t cap,
          unsigned long long *err, uint32_t psh, unsigned long long *pmax) {
-    /* (G coarse slices of 2^split parts: G << split <= REPART_GP, checked by the host) */
+    /* (G coarse slices of 2^split parts: G << split <= GP, else nothing is
+       done and the pass fails -- the arrays below are sized by GP) */
+    constexpr uint32_t GP = REPART_GP(OT, G);
     /* per (slice in the group, part): entries, round count / offset /
        cursor, written so far, stream start */
-    __shared__ uint32_t cnt[REPART_GP], hc[REPART_GP], ho[REPART_GP], cur[REPART_GP], wr[REPART_GP];
-    __shared__ unsigned long long poff[REPART_GP];
+    __shared__ uint32_t cnt[GP], hc[GP], ho[GP], cur[GP], wr[GP];
+    __shared__ unsigned long long poff[GP];
+    if ((G << pg.split) > GP) {
+        if (threadIdx.x == 0) atomicOr(err, (unsigned long long)FK_FAULT_PARTS);
+        return;
+    }
     __shared__ uint32_t scn[17];
     __shared__ __attribute__((aligned(16))) OT rbuf[REPART_CAP];
     const uint32_t pmask = (1u << psh) - 1u;
