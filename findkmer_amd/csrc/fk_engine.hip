@@ -3247,7 +3247,7 @@ static_assert(16u * FK_TILE_BYTES <= REPART_CAP, "a C32 row's run fits one k_rep
    low 15 bits (k = 15, 16; k = 17 passes, psh = 15).  OT = uint32_t (wide
    sparse passes): part bits [psh, psh + 6), stored as the low psh bits. */
 template <typename OT, uint32_t G = REPART_G>
-__global__ void __launch_bounds__(1024, sizeof(OT) == 2 ? REPART_MINW : 1)
+__global__ void __launch_bounds__(1024, sizeof(OT) == 2 && G == REPART_G ? REPART_MINW : 1)
 k_repart(PartGeo pg, OT *out, unsigned long long *alloc, PartMeta *meta, uint64_t cap,
          unsigned long long *err, uint32_t psh, unsigned long long *pmax) {
     /* (G coarse slices of 2^split parts: G << split <= GP, else nothing is
@@ -5220,8 +5220,14 @@ static int launch_part(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t l
         e->d_perr = alloc + 1;
         e->perr_live = true;
         HIPCHK(hipMemsetAsync(alloc, 0, 2 * sizeof(unsigned long long), e->stream));
-        hipLaunchKernelGGL(k_repart<uint16_t>, dim3(pg.nslices / REPART_G), dim3(1024), 0, e->stream, pg, e->d_parts,
-                           alloc, meta, (uint64_t)e->parts_cap, e->d_perr, 15u, nullptr);
+        /* k = 15 (16 parts a slice): 8 slices per block, one block per CU
+           (4.27 ms per G-base against 4.68 with two blocks of 4) */
+        if (pg.split <= 4)
+            hipLaunchKernelGGL((k_repart<uint16_t, 8u>), dim3(pg.nslices / 8u), dim3(1024), 0, e->stream, pg,
+                               e->d_parts, alloc, meta, (uint64_t)e->parts_cap, e->d_perr, 15u, nullptr);
+        else
+            hipLaunchKernelGGL(k_repart<uint16_t>, dim3(pg.nslices / REPART_G), dim3(1024), 0, e->stream, pg,
+                               e->d_parts, alloc, meta, (uint64_t)e->parts_cap, e->d_perr, 15u, nullptr);
         HIPCHK(hipGetLastError());
         hipLaunchKernelGGL(k_count_parts, dim3((unsigned)nparts), dim3(1024), (size_t)1 << 17, e->stream, pg,
                            (const uint16_t *)e->d_parts, (const PartMeta *)meta, e->d_table, (uint64_t)e->parts_cap,
