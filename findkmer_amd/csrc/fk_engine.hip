@@ -6889,7 +6889,7 @@ __global__ void __launch_bounds__(1024)
 k_kpart(const KT *keys, uint64_t n, PartGeo pg, uint64_t lo, uint64_t hi, uint32_t cs, uint64_t tkey,
         unsigned long long *tcount) {
     constexpr bool WIDE = sizeof(KT) == 8;
-    __shared__ uint32_t hist[2048], cur[2048];
+    __shared__ uint32_t hist[2048], cur[2048], wtot[16];
     __shared__ uint32_t ntop;
     extern __shared__ uint32_t ent[];   /* KP_BATCH codes */
     const uint32_t t = threadIdx.x;
@@ -6940,17 +6940,20 @@ k_kpart(const KT *keys, uint64_t n, PartGeo pg, uint64_t lo, uint64_t hi, uint32
         for (uint32_t j = 0; j < 32u; j++)
             if (KP_SL(j) != 0xFFFFu) atomicAdd(&hist[KP_SL(j)], 1u);
         __syncthreads();
-        if (t < 64) {   /* cursors and the row's run words: 32 slices per lane */
-            uint32_t sum = 0;
-            for (uint32_t j = 0; j < 32u; j++) sum += hist[t * 32u + j];
-            uint32_t run = wscan_incl32(sum) - sum;
-            for (uint32_t j = 0; j < 32u; j++) {
-                const uint32_t b = t * 32u + j, c = hist[b];
-                cur[b] = run;
-                pg.idx[(size_t)row * 2048u + b] = run_word(run, c);
-                hist[b] = 0;
-                run += c;
-            }
+        {   /* cursors and the row's run words: two slices per thread, a block
+               scan (one wave walking 32 slices a lane kept 15 waiting) */
+            const uint32_t b = 2u * t, c0 = hist[b], c1 = hist[b + 1u], sum = c0 + c1;
+            const uint32_t inc = wscan_incl32(sum);
+            if ((t & 63u) == 63u) wtot[t >> 6] = inc;
+            __syncthreads();
+            uint32_t run = inc - sum;
+#pragma unroll
+            for (uint32_t w = 0; w < 16u; w++) run += w < (t >> 6) ? wtot[w] : 0u;
+            cur[b] = run;
+            cur[b + 1u] = run + c0;
+            reinterpret_cast<uint2 *>(pg.idx + (size_t)row * 2048u)[t] = make_uint2(run_word(run, c0), run_word(run + c0, c1));
+            hist[b] = 0;
+            hist[b + 1u] = 0;
         }
         __syncthreads();
 #pragma unroll
