@@ -737,7 +737,7 @@ def _assert_same_sparse_view(data, k, feeds=None, want_nodes=True):
 
 
 @pytest.mark.parametrize("k,tune", [(15, "glist_cap=1"), (16, "glist_cap=4096"), (15, "no_mixed=1"),
-                                    (16, "part_general=5"), (12, "glist_cap=1"), (13, "glist_cap=1"),
+                                    (15, "part_general=5"), (12, "glist_cap=1"), (13, "glist_cap=1"),
                                     (14, "part_general=5")])
 def test_fresh_table_window_list_never_truncates(k, tune, monkeypatch):
     """k = 12..16 right after a reset: k_count_parts / k_bucket16 (k_pair_fold
@@ -761,7 +761,7 @@ def test_fresh_table_window_list_never_truncates(k, tune, monkeypatch):
 
 
 @pytest.mark.parametrize("k,kind", [(15, "mixed"), (15, "dense_records"), (15, "polyA"), (15, "fasta_polyA"),
-                                    (15, "acgt_feeds"), (16, "mixed"), (16, "fasta_polyA"), (16, "acgt_feeds")])
+                                    (15, "acgt_feeds"), (16, "fasta_polyA"), (16, "acgt_feeds")])
 def test_partition_k15_and_k16(k, kind):
     """k = 15, 16 through the two-level partition: k_part's 2048 coarse
     slices of 32-bit codes, k_repart splitting each into 16 / 64 contiguous
