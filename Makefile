@@ -19,7 +19,15 @@ WFLAGS   := -O2 -fPIC -std=c++17 -ffp-contract=off -fno-fast-math -I$(ROOT)inclu
 
 all: $(LIB) $(ROOT)findKmer $(ROOT)Debug/findKmer oracle
 
-$(BUILD)/fk_engine.o: $(CSRC)/fk_engine.hip $(CSRC)/fk_device.h $(CSRC)/fk_sparse.h $(CSRC)/fk_comm.h $(ROOT)include/findkmer.h
+# the engine's translation units (one per path: state pass and k <= 7, the
+# partition for 8 <= k <= 16, the sparse passes, the multi-GPU exchange, and
+# the engine core / C-ABI) share fk_engine_internal.h
+ENGINE_H := $(CSRC)/fk_engine_internal.h $(CSRC)/fk_part_kern.h $(CSRC)/fk_tiles.h $(CSRC)/fk_part.h $(CSRC)/fk_device.h \
+            $(CSRC)/fk_sparse.h $(CSRC)/fk_comm.h $(ROOT)include/findkmer.h
+ENGINE_TUS := fk_engine fk_scan fk_part fk_part_pipe fk_part_res fk_sparse_pass fk_exchange
+ENGINE_OBJS := $(patsubst %,$(BUILD)/%.o,$(ENGINE_TUS))
+
+$(ENGINE_OBJS): $(BUILD)/%.o: $(CSRC)/%.hip $(ENGINE_H)
 	@mkdir -p $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -c -x hip $< -o $@
 
@@ -39,7 +47,7 @@ $(BUILD)/fk_ingest.o: $(CSRC)/fk_ingest.hip $(ROOT)include/findkmer.h
 	@mkdir -p $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -c -x hip $< -o $@
 
-$(LIB): $(BUILD)/fk_engine.o $(BUILD)/fk_sparse.o $(BUILD)/fk_ingest.o $(BUILD)/fk_comm.o $(BUILD)/fk_writer.o
+$(LIB): $(ENGINE_OBJS) $(BUILD)/fk_sparse.o $(BUILD)/fk_ingest.o $(BUILD)/fk_comm.o $(BUILD)/fk_writer.o
 	@mkdir -p $(LIBDIR)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -lpthread -ldl
 

@@ -1,0 +1,1702 @@
+/*
+ * fk_sparse_pass.hip -- 17 <= k <= 20 (findKmer.cpp:429-445, :663-690): the
+ * sparse table built at finish by key-range passes over the retained input
+ * (k_sp_emit, then per pass k_kpart + k_repart + k_kp_count / k_kp_sort), and
+ * the sparse-table C-ABI (fk_engine_sparse*).
+ */
+#include "fk_engine_internal.h"
+
+/*
+ * 17 <= k <= 20: the table is built at finish by key-range passes over the
+ * input the engine retained (1 byte per input byte, plus every range's exact
+ * entering state from the feed's k_scan), never by materialising a slot per
+ * byte.  k_sp_emit walks every range from its exact state, one 2 KiB tile at
+ * a time, with tile_general -- the same per-byte rules as every other count
+ * (findKmer.cpp:962-1069) -- writing each byte's window index (reference
+ * order, :719-724) or short walk (:1059-1062) into the wave's LDS slots, and
+ * then, per mode:
+ *   SP_HIST  every window's bucket (key >> shift) into an LDS histogram
+ *            (flushed with one atomic per bucket and block), every short
+ *            walk to a global list;
+ *   SP_KEYS  the windows with lo <= key < hi to a compact global list (one
+ *            atomic per tile and wave for the space, ballot-ordered writes),
+ *            and the short walks too when one pass takes every window (the
+ *            feed counted them; no SP_HIST launch then);
+ *   SP_DENSE the windows with lo <= key < hi counted in a dense u64 table
+ *            (one bucket too large for a sorted pass: few distinct keys).
+ */
+/* SP_KEYS: one key range [lo, hi) of a walk and its list */
+#define SP_MAXP 4u                  /* key ranges (passes) one SP_KEYS walk emits (round 5) */
+struct SpPass {
+    uint64_t lo, hi;
+    uint64_t *out;                  /* the keys, or */
+    uint32_t *out32;                /* ... (a range of <= 2^32 keys) key - lo as 32 bits */
+    uint64_t cap;                   /* slots of the list */
+    unsigned long long *ctr;        /* [0] slots claimed (whole SP_CHUNKs), [1] windows written (the rest: pads) */
+};
+struct SpEmit {
+    int mode;
+    uint32_t shift;                 /* bucket of a key: key >> shift */
+    uint64_t lo, hi;                /* SP_DENSE: the key range [lo, hi) */
+    unsigned long long *bhist;      /* SP_HIST: window count per bucket */
+    uint32_t nbuckets;
+    uint64_t *shorts;               /* SP_HIST: the short walks */
+    unsigned long long *nshort;
+    uint64_t short_cap;
+    uint32_t np;                    /* SP_KEYS: the walk's key ranges, ascending (unused: lo = ~0) */
+    uint64_t gend;                  /* ... the last range's hi */
+    SpPass ps[SP_MAXP];
+    unsigned long long *dense;      /* SP_DENSE: count of key lo + i */
+};
+enum { SP_HIST = 1, SP_KEYS = 2, SP_DENSE = 3 };
+#define SP_WAVES 4u
+#define SP_BUCKET_BITS 12u
+/* SP_KEYS output: each wave claims SP_CHUNK slots at a time from the pass's
+   counter and fills them in order; the unfilled end of its last chunk holds
+   pads (4^k - 1, the largest key -- 0xFFFFFFFF in a 32-bit pass -- so the
+   sort puts them last, and their number is taken off the last run).  Round 4: one claim per
+   tile and wave -- 5 M same-address atomics per 10 GB pass -- made each keys
+   pass take 60 ms against 10 ms for the histogram pass of the same walk. */
+#define SP_CHUNK 8192u
+struct SpOut {
+    uint64_t base;    /* the wave's current chunk (wave-uniform) */
+    uint32_t fill;    /* slots of it used (SP_CHUNK: none claimed yet) */
+    uint64_t real;    /* windows written by the wave */
+};
+/* One window per lane (v, or SP_EMPTY / a short walk: none) into its key
+   range's list, every lane of the wave calling together.  The ranges are
+   told apart by a wave multisplit (3 ballots: range bits 0 and 1, and
+   "in a range"), each range's entries placed at its chunk's fill point in
+   lane order; a range claims a new SP_CHUNK (one atomic) when this step's
+   entries run past its chunk.  One walk thus emits every range's keys:
+   round 4 walked the input once per range, computing every window's key
+   twice each time. */
+static_assert(SP_MAXP == 4u, "sp_range compares three range starts");
+/* the range of key v (SP_MAXP: none).  The host groups consecutive passes
+   only: between two ranges lie empty buckets, which hold no key */
+__device__ __forceinline__ uint32_t sp_range(const SpEmit &em, uint64_t v) {
+    if (v < em.ps[0].lo || v >= em.gend) return SP_MAXP;
+    return (uint32_t)(v >= em.ps[1].lo) + (uint32_t)(v >= em.ps[2].lo) + (uint32_t)(v >= em.ps[3].lo);
+}
+__device__ __forceinline__ void sp_place(const SpEmit &em, SpOut (&so)[SP_MAXP], uint64_t v, uint32_t lane) {
+    const uint32_t q = sp_range(em, v);
+    const unsigned long long bv = __ballot(q < SP_MAXP);
+    if (!bv) return;
+    const unsigned long long b0 = __ballot((q & 1u) != 0u), b1 = __ballot((q & 2u) != 0u);
+    const unsigned long long lt = (1ull << lane) - 1ull;
+#pragma unroll
+    for (uint32_t i = 0; i < SP_MAXP; i++) {
+        if (i >= em.np) break;
+        const unsigned long long mi = bv & ((i & 1u) ? b0 : ~b0) & ((i & 2u) ? b1 : ~b1);
+        if (!mi) continue;
+        const uint32_t cnt = (uint32_t)__popcll(mi);
+        const uint32_t rem = SP_CHUNK - so[i].fill;
+        uint64_t nb = 0;
+        if (cnt > rem) {
+            unsigned long long c = 0;
+            if (lane == 0) c = atomicAdd(em.ps[i].ctr, (unsigned long long)SP_CHUNK);
+            nb = rdlane64(c, 0);
+        }
+        if (q == i) {
+            const uint64_t p = (uint64_t)__popcll(mi & lt);
+            const uint64_t at = p < rem ? so[i].base + so[i].fill + p : nb + (p - rem);
+            if (at < em.ps[i].cap) {
+                if (em.ps[i].out32) em.ps[i].out32[at] = (uint32_t)(v - em.ps[i].lo);
+                else em.ps[i].out[at] = v;
+            }
+        }
+        if (cnt > rem) { so[i].base = nb; so[i].fill = cnt - rem; }
+        else so[i].fill += cnt;
+        so[i].real += cnt;
+    }
+}
+/* the end of the wave's walk: pad each range's chunk (4^k - 1, or
+   0xFFFFFFFF in a 32-bit list), count its windows */
+__device__ __forceinline__ void sp_close(const SpEmit &em, const SpOut (&so)[SP_MAXP], uint64_t pad) {
+    const uint32_t lane = threadIdx.x & 63;
+#pragma unroll
+    for (uint32_t q = 0; q < SP_MAXP; q++) {
+        if (q >= em.np) break;
+        const SpPass &ps = em.ps[q];
+        if (so[q].fill < SP_CHUNK)
+            for (uint32_t i = so[q].fill + lane; i < SP_CHUNK; i += 64u) {
+                if (so[q].base + i >= ps.cap) continue;
+                if (ps.out32) ps.out32[so[q].base + i] = 0xFFFFFFFFu;
+                else ps.out[so[q].base + i] = pad;
+            }
+        if (lane == 0 && so[q].real) atomicAdd(ps.ctr + 1, (unsigned long long)so[q].real);
+    }
+}
+
+/* The windows of a fast tile (contiguous layout, tile_fast's Emit) as
+ * reference-order keys, handed to the pass's mode.  Half h of a lane holds D
+ * = 16 digits (15 with a '\n', right-aligned in its word R); the 32 digits
+ * before the half are the previous half's {C, S2} (half 1: this lane's half
+ * 0; half 0: the previous lane's half 1, lane 0: the tile's entering code),
+ * so the window ending at digit j of the half is
+ *   ((prev << 2(j+1)) | (R >> 2(D-1-j))) & (4^k - 1)
+ * -- up to 20 bases from two words, which the 16-base {C, S2} of the dense
+ * path cannot give. */
+__device__ __forceinline__ void sp_fast_emit(const SpEmit &em, const Emit &fe, uint64_t c0, uint64_t maskk,
+                                             uint32_t *bh, uint32_t lane, SpOut (&so)[SP_MAXP], uint64_t *stg) {
+    const uint64_t pv0 = ((uint64_t)from_prev_lane(fe.BC, (uint32_t)(c0 >> 32)) << 32) |
+                         from_prev_lane(fe.B2, (uint32_t)c0);
+    const uint64_t pv1 = ((uint64_t)fe.AC << 32) | fe.A2;
+    const uint32_t R0 = fe.h0 ? fe.A2 & 0x3FFFFFFFu : fe.A2, R1 = fe.h1 ? fe.B2 & 0x3FFFFFFFu : fe.B2;
+    const uint32_t D0 = fe.h0 ? 15u : 16u, D1 = fe.h1 ? 15u : 16u;
+    /* window jj (half jj / 16, digit jj % 16), or SP_EMPTY past the half's digits */
+    auto key = [&](uint32_t jj) -> uint64_t {
+        const bool h = jj >= 16u;
+        const uint32_t j = jj & 15u, D = h ? D1 : D0, R = h ? R1 : R0;
+        const uint64_t pv = h ? pv1 : pv0;
+        if (j >= D) return SP_EMPTY;
+        return fk_sigma(((pv << (2u * (j + 1u))) | (uint64_t)(R >> (2u * (D - 1u - j)))) & maskk);
+    };
+    if (em.mode == SP_KEYS) {
+        /* the tile's <= 2048 windows staged in the wave's slots, grouped by
+           range (a wave scan of each lane's per-range counts, packed two
+           16-bit fields a word), then copied out range by range, 64
+           consecutive entries a store */
+        uint64_t kv[32];
+        uint32_t c01 = 0, c23 = 0;
+#pragma unroll
+        for (uint32_t jj = 0; jj < 32u; jj++) {
+            kv[jj] = key(jj);
+            const uint32_t q = sp_range(em, kv[jj]), inc = 1u << (16u * (q & 1u));
+            c01 += q < 2u ? inc : 0u;
+            c23 += (q - 2u) < 2u ? inc : 0u;
+        }
+        const uint32_t i01 = wscan_incl32(c01), i23 = wscan_incl32(c23);
+        const uint32_t t01 = rdlane(i01, 63), t23 = rdlane(i23, 63);
+        const uint32_t T[4] = {t01 & 0xFFFFu, t01 >> 16, t23 & 0xFFFFu, t23 >> 16};
+        const uint32_t S[4] = {0u, T[0], T[0] + T[1], T[0] + T[1] + T[2]};
+        const uint32_t e01 = i01 - c01, e23 = i23 - c23;
+        uint32_t p0 = e01 & 0xFFFFu, p1 = S[1] + (e01 >> 16), p2 = S[2] + (e23 & 0xFFFFu), p3 = S[3] + (e23 >> 16);
+#pragma unroll
+        for (uint32_t jj = 0; jj < 32u; jj++) {
+            const uint32_t q = sp_range(em, kv[jj]);
+            if (q < SP_MAXP) {
+                const uint32_t at = q == 0u ? p0 : q == 1u ? p1 : q == 2u ? p2 : p3;
+                stg[at] = kv[jj];
+                p0 += q == 0u; p1 += q == 1u; p2 += q == 2u; p3 += q == 3u;
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+        for (uint32_t q = 0; q < SP_MAXP; q++) {
+            if (q >= em.np) break;
+            const uint32_t t = T[q];
+            if (!t) continue;
+            const SpPass &ps = em.ps[q];
+            const uint32_t rem = SP_CHUNK - so[q].fill;
+            uint64_t nb = 0;
+            if (t > rem) {   /* (t <= 2048 < SP_CHUNK: one new chunk at most) */
+                unsigned long long c = 0;
+                if (lane == 0) c = atomicAdd(ps.ctr, (unsigned long long)SP_CHUNK);
+                nb = rdlane64(c, 0);
+            }
+            for (uint32_t j = lane; j < t; j += 64u) {
+                const uint64_t v = stg[S[q] + j];
+                const uint64_t at = j < rem ? so[q].base + so[q].fill + j : nb + (j - rem);
+                if (at < ps.cap) {
+                    if (ps.out32) ps.out32[at] = (uint32_t)(v - ps.lo);
+                    else ps.out[at] = v;
+                }
+            }
+            if (t > rem) { so[q].base = nb; so[q].fill = t - rem; }
+            else so[q].fill += t;
+            so[q].real += t;
+        }
+        __builtin_amdgcn_wave_barrier();
+    } else if (em.mode == SP_DENSE) {
+#pragma unroll 8
+        for (uint32_t jj = 0; jj < 32u; jj++) {
+            const uint64_t v = key(jj);
+            if (v >= em.lo && v < em.hi) atomicAdd(&em.dense[v - em.lo], 1ull);
+        }
+    } else {
+#pragma unroll 8
+        for (uint32_t jj = 0; jj < 32u; jj++) {
+            const uint64_t v = key(jj);
+            if (v != SP_EMPTY) atomicAdd(&bh[v >> em.shift], 1u);
+        }
+    }
+}
+
+__global__ void __launch_bounds__(SP_WAVES * 64u)
+k_sp_emit(const uint8_t *buf, uint64_t len, int k, uint64_t maskk, const XState *rst, uint64_t nranges,
+          uint64_t cpw, uint64_t nchunks, SpEmit em) {
+    extern __shared__ uint64_t sp_lds[];   /* SP_WAVES x 2048 slots, then (SP_HIST) the buckets */
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    uint64_t *slots = sp_lds + (size_t)wv * FK_TILE_BYTES;
+    uint32_t *bh = reinterpret_cast<uint32_t *>(sp_lds + (size_t)SP_WAVES * FK_TILE_BYTES);
+    if (em.mode == SP_HIST) {
+        for (uint32_t i = threadIdx.x; i < em.nbuckets; i += blockDim.x) bh[i] = 0;
+        __syncthreads();
+    }
+    Ctx cx{buf, len, 0, nullptr, nullptr, nullptr, nullptr, nullptr, maskk, 0, k, nullptr, slots};
+    const uint64_t nw = (uint64_t)gridDim.x * SP_WAVES;
+    SpOut so[SP_MAXP];          /* SP_KEYS: the wave's output chunk in each range's list */
+#pragma unroll
+    for (uint32_t q = 0; q < SP_MAXP; q++) so[q] = SpOut{0, SP_CHUNK, 0};
+    for (uint64_t r = (uint64_t)blockIdx.x * SP_WAVES + wv; r < nranges; r += nw) {
+        const uint64_t c0 = r * cpw, c1 = min(c0 + cpw, nchunks);
+        const uint64_t rb = c0 * FK_CHUNK_BYTES, re = min(c1 * FK_CHUNK_BYTES, len);
+        const XState x = rst[r];
+        DState st{x.code, (uint32_t)x.R, x.hdr};
+        /* the next full tile's words load while this one is counted */
+        uint32_t wn[8];
+        auto load_full = [&](uint64_t at) {
+            const u32x4 *p = reinterpret_cast<const u32x4 *>(buf + at + (uint64_t)lane * FK_LANE_BYTES);
+            const u32x4 a = __builtin_nontemporal_load(p), c = __builtin_nontemporal_load(p + 1);
+            wn[0] = a.x; wn[1] = a.y; wn[2] = a.z; wn[3] = a.w;
+            wn[4] = c.x; wn[5] = c.y; wn[6] = c.z; wn[7] = c.w;
+        };
+        if (rb + FK_TILE_BYTES <= re) load_full(rb);
+        for (uint64_t tb = rb; tb < re; tb += FK_TILE_BYTES) {
+            uint32_t w[8];
+            int nb = (int)FK_LANE_BYTES;
+            if (tb + FK_TILE_BYTES <= re) {
+#pragma unroll
+                for (int d = 0; d < 8; d++) w[d] = wn[d];
+            } else {
+                nb = load_lane<FK_LANE_BYTES>(cx, (int64_t)(tb + (uint64_t)lane * FK_LANE_BYTES), w);
+            }
+            if (tb + 2 * FK_TILE_BYTES <= re) load_full(tb + FK_TILE_BYTES);
+            Facts f{0, 0, 0, 0, 0, 0};
+            Counters cnt{0, 0, 0, 0, 0, FK_NO_EOF, 0};
+            /* a fast tile (bases and at most one '\n' per half, deep in a run,
+               outside a header: no short walks, every base ends a window)
+               computes its 40-bit windows in registers: no byte walk, no
+               slots */
+            {
+                const uint64_t c0 = st.code;
+                Emit fe{0, 0, 0, 0, false, false, false};
+                if (tb + FK_TILE_BYTES <= re && st.hdr == 0 &&
+                    tile_fast<true, H_EMIT, false>(cx, w, st, f, cnt, 1u, &fe)) {
+                    if (fe.deep) sp_fast_emit(em, fe, c0, maskk, bh, lane, so, slots);
+                    continue;
+                }
+            }
+            /* a lane reads back only the slots of its own 32 bytes */
+#pragma unroll 8
+            for (uint32_t j = 0; j < FK_LANE_BYTES; j++) slots[j * 64u + lane] = SP_EMPTY;
+            tile_general<true, H_SPARSE>(cx, w, nb, 0u, st, f, cnt, 1u);
+            if (em.mode == SP_KEYS) {
+                if (em.shorts) {   /* (a single pass: no SP_HIST) */
+#pragma unroll 8
+                    for (uint32_t j = 0; j < FK_LANE_BYTES; j++) {
+                        const uint64_t v = slots[j * 64u + lane];
+                        if (v >= SP_SHORT && v != SP_EMPTY) {
+                            const unsigned long long i = atomicAdd(em.nshort, 1ull);
+                            if (i < em.short_cap) em.shorts[i] = v;
+                        }
+                    }
+                }
+                for (uint32_t j = 0; j < FK_LANE_BYTES; j++) sp_place(em, so, slots[j * 64u + lane], lane);
+            } else if (em.mode == SP_DENSE) {
+#pragma unroll 8
+                for (uint32_t j = 0; j < FK_LANE_BYTES; j++) {
+                    const uint64_t v = slots[j * 64u + lane];
+                    if (v >= em.lo && v < em.hi) atomicAdd(&em.dense[v - em.lo], 1ull);
+                }
+            } else {
+                for (uint32_t j = 0; j < FK_LANE_BYTES; j++) {
+                    const uint64_t v = slots[j * 64u + lane];
+                    if (v < SP_SHORT) {
+                        atomicAdd(&bh[v >> em.shift], 1u);
+                    } else if (v != SP_EMPTY) {
+                        const unsigned long long i = atomicAdd(em.nshort, 1ull);
+                        if (i < em.short_cap) em.shorts[i] = v;
+                    }
+                }
+            }
+        }
+    }
+    if (em.mode == SP_KEYS) sp_close(em, so, (1ull << (2 * k)) - 1);
+    if (em.mode == SP_HIST) {
+        __syncthreads();
+        for (uint32_t i = threadIdx.x; i < em.nbuckets; i += blockDim.x)
+            if (bh[i]) atomicAdd(&em.bhist[i], (unsigned long long)bh[i]);
+    }
+}
+
+/* ---- finish ---- */
+
+/* one k_sp_emit launch per retained segment */
+int sp_emit_all(fk_engine *e, const SpEmit &em) {
+    const size_t lds = (size_t)SP_WAVES * FK_TILE_BYTES * sizeof(uint64_t) +
+                       (em.mode == SP_HIST ? (size_t)em.nbuckets * sizeof(uint32_t) : 0);
+    for (const auto &sg : e->spsegs) {
+        if (!sg.nranges) continue;
+        const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((sg.nranges + SP_WAVES - 1) / SP_WAVES,
+                                                                                 (uint64_t)e->cus * 8));
+        hipLaunchKernelGGL(k_sp_emit, dim3(grid), dim3(SP_WAVES * 64u), lds, e->stream, e->d_keep + sg.off, sg.len,
+                           e->k, e->maskk, e->d_kst + sg.st, sg.nranges, sg.cpw, sg.nchunks, em);
+        HIPCHK(hipGetLastError());
+    }
+    return FK_OK;
+}
+
+/*
+ * A k = 17 key-range pass (keys lo + r, r < 2^32, emitted as 32-bit r) into
+ * its runs without a sort (round 5; rocPRIM's radix sort and run-length
+ * encode took 228 ms of a 10 G-base step's 390).  The pass is a 2^32-bin
+ * count table, so it is counted the way k = 16's dense table is, and only
+ * its nonzero bins are written:
+ *   k_kpart       the key list in batches of 32 K keys, counting-sorted in LDS
+ *                 by r's top 11 bits into 2048 coarse slices (k_part<C32>'s
+ *                 row layout: each batch one row of runs of 21-bit codes and a
+ *                 row of run words);
+ *   k_repart      (as for k = 15, 16) each coarse slice into 64 contiguous
+ *                 part streams of 15-bit codes;
+ *   k_kp_count    one block per part (2^15 bins, in key order): the part's
+ *                 stream into LDS bins, the pads taken off the last bin, the
+ *                 nonzero bins' offset from the parts before it (a chained
+ *                 scan: each block publishes its distinct count, then looks
+ *                 back for the earlier parts' total), then the bins written
+ *                 as (key, u32 count) in ascending order with the statistics,
+ *                 the rollover check and the adjacent keys' prefix histogram;
+ *   k_kp_fold     the blocks' partial statistics into the pass accumulators,
+ *                 the prefix histogram of each part's first key against the
+ *                 last key of the nonempty part before it, and the pass's
+ *                 distinct count.
+ */
+#define KP_BATCH 32768u      /* keys per k_kpart batch (16 waves x 2048) */
+#define KP_SLOTS 64u         /* partial-statistics slots (block % KP_SLOTS) */
+#define KP_SLOT_W 36u        /* per slot: 10 statistics, rollover, 24 prefix-histogram entries, spare */
+#define KP_EMPTY (~0ull)
+
+/* KT = uint32_t: 32-bit relative keys r (slice r >> 21, code r & (2^21 - 1));
+   KT = uint64_t: keys lo + r with r < 2^(cs + 11) (slice r >> cs, code r &
+   (2^cs - 1), cs <= 29); keys >= hi (pads past the pass's range) are left out */
+/* The top key `tkey` (the pads' value: relative 0xFFFFFFFF, or 4^k - 1 when
+   the pass holds it; ~0 for none) is left out of the partition and only
+   counted into *tcount: the chunk pads of every emitting wave (tens of
+   millions per pass) would otherwise crowd one part, whose k_repart block
+   and LDS bin then serialise the whole pass. */
+template <typename KT>
+__global__ void __launch_bounds__(1024)
+k_kpart(const KT *keys, uint64_t n, PartGeo pg, uint64_t lo, uint64_t hi, uint32_t cs, uint64_t tkey,
+        unsigned long long *tcount) {
+    constexpr bool WIDE = sizeof(KT) == 8;
+    __shared__ uint32_t hist[2048], cur[2048], wtot[16];
+    __shared__ uint32_t ntop;
+    extern __shared__ uint32_t ent[];   /* KP_BATCH codes */
+    const uint32_t t = threadIdx.x;
+    const uint32_t sh = WIDE ? cs : 21u;
+    const KT cmask = (KT)(((uint64_t)1 << sh) - 1);
+    for (uint32_t i = t; i < 2048u; i += 1024u) hist[i] = 0;
+    if (t == 0) ntop = 0;
+    const uint64_t per = (uint64_t)pg.rounds * KP_BATCH;
+    const uint64_t k0 = blockIdx.x * per, k1 = min(k0 + per, n);
+    uint32_t *codes = reinterpret_cast<uint32_t *>(pg.codes);
+    uint32_t mytop = 0;
+    for (uint32_t r = 0; r < pg.rounds; r++) {
+        const uint32_t row = blockIdx.x * pg.rounds + r;
+        const uint64_t b0 = k0 + (uint64_t)r * KP_BATCH;
+        const uint32_t nv = b0 < k1 ? (uint32_t)min<uint64_t>(KP_BATCH, k1 - b0) : 0u;
+        __syncthreads();
+        if (nv == 0) {   /* rows past the block's keys are empty */
+            for (uint32_t b = t; b < 2048u; b += 1024u) pg.idx[(size_t)row * 2048u + b] = PART_NO_RUN;
+            continue;
+        }
+        /* each key's slice (two 16-bit slices per word, 0xFFFF: left out --
+           past hi, or the top key) and code: 48 registers where 32 64-bit
+           keys took 64 and spilled */
+        uint32_t cd[32], sp[16];
+#pragma unroll
+        for (uint32_t j = 0; j < 16u; j++) sp[j] = 0xFFFFFFFFu;
+#pragma unroll
+        for (uint32_t j = 0; j < 32u; j++) {
+            cd[j] = 0;
+            if (j * 1024u + t < nv) {
+                const KT x = keys[b0 + j * 1024u + t];
+                uint32_t sl = 0xFFFFu;
+                if ((uint64_t)x == tkey) {
+                    mytop++;
+                } else if (!WIDE) {
+                    sl = (uint32_t)x >> 21;
+                    cd[j] = (uint32_t)x & 0x1FFFFFu;
+                } else if ((uint64_t)x < hi) {
+                    const uint64_t r = (uint64_t)x - lo;
+                    sl = (uint32_t)(r >> sh);
+                    cd[j] = (uint32_t)(r & (uint64_t)cmask);
+                }
+                sp[j >> 1] = (j & 1) ? (sp[j >> 1] & 0xFFFFu) | (sl << 16) : (sp[j >> 1] & 0xFFFF0000u) | sl;
+            }
+        }
+#define KP_SL(j) ((sp[(j) >> 1] >> (((j) & 1) * 16)) & 0xFFFFu)
+#pragma unroll
+        for (uint32_t j = 0; j < 32u; j++)
+            if (KP_SL(j) != 0xFFFFu) atomicAdd(&hist[KP_SL(j)], 1u);
+        __syncthreads();
+        {   /* cursors and the row's run words: two slices per thread, a block
+               scan (one wave walking 32 slices a lane kept 15 waiting) */
+            const uint32_t b = 2u * t, c0 = hist[b], c1 = hist[b + 1u], sum = c0 + c1;
+            const uint32_t inc = wscan_incl32(sum);
+            if ((t & 63u) == 63u) wtot[t >> 6] = inc;
+            __syncthreads();
+            uint32_t run = inc - sum;
+#pragma unroll
+            for (uint32_t w = 0; w < 16u; w++) run += w < (t >> 6) ? wtot[w] : 0u;
+            cur[b] = run;
+            cur[b + 1u] = run + c0;
+            reinterpret_cast<uint2 *>(pg.idx + (size_t)row * 2048u)[t] = make_uint2(run_word(run, c0), run_word(run + c0, c1));
+            hist[b] = 0;
+            hist[b + 1u] = 0;
+        }
+        __syncthreads();
+#pragma unroll
+        for (uint32_t j = 0; j < 32u; j++)
+            if (KP_SL(j) != 0xFFFFu) ent[atomicAdd(&cur[KP_SL(j)], 1u)] = cd[j];
+#undef KP_SL
+        __syncthreads();
+        /* the row: its runs end at cur[2047] (every entry placed) */
+        const uint32_t tot = cur[2047];
+        uint4 *dst = reinterpret_cast<uint4 *>(codes + (size_t)row * pg.batch);
+        const uint4 *src = reinterpret_cast<const uint4 *>(ent);
+        for (uint32_t i = t; i < (tot + 3u) / 4u; i += 1024u) dst[i] = src[i];
+    }
+    if (mytop) atomicAdd(&ntop, mytop);
+    __syncthreads();
+    if (t == 0 && ntop) atomicAdd(tcount, (unsigned long long)ntop);
+}
+
+/* A chained scan over the blocks in dispatch order (wave 0 of every block
+   calls it): this block's `total` published (status A: aggregate), the
+   earlier blocks' sum found by looking back 64 flags at a time -- up to the
+   nearest one with status P (inclusive prefix) -- and this block's own
+   inclusive prefix published.  Returns the exclusive prefix.  Every earlier
+   block was dispatched before this one and publishes unconditionally; the
+   spin bound only guards a broken invariant (FK_FAULT_PARTS: the pass fails
+   with FK_E_INTERNAL instead of hanging the GPU).  The flags are relaxed
+   agent-scope atomics: a flag word carries all a reader needs (status and
+   value in one 64-bit access), and a release store would write back this
+   XCD's whole L2 -- the parts' output just written -- once per part. */
+__device__ unsigned long long chain_prefix(unsigned long long *flags, uint32_t blk, uint32_t total,
+                                           unsigned long long *err) {
+    const uint32_t lane = threadIdx.x & 63;
+    const unsigned long long A = 1ull << 62, P = 2ull << 62, M = (1ull << 62) - 1;
+    if (blk == 0) {
+        if (lane == 0) __hip_atomic_store(&flags[0], P | total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return 0;
+    }
+    if (lane == 0) __hip_atomic_store(&flags[blk], A | total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    unsigned long long pre = 0;
+    int64_t j = (int64_t)blk - 1;
+    uint64_t spin = 0;
+    for (;;) {
+        const int64_t idx = j - (int64_t)lane;
+        unsigned long long f = idx >= 0 ? __hip_atomic_load(&flags[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : P;
+        /* wait only for the flags up to the nearest inclusive prefix (the
+           blocks farther back may still be counting) */
+        for (;;) {
+            const unsigned long long pm0 = __ballot((f >> 62) == 2);
+            const unsigned long long need = pm0 ? (pm0 & (~pm0 + 1)) * 2 - 1 : ~0ull;   /* lanes 0 .. first P */
+            if (!(__ballot((f >> 62) == 0) & need)) break;
+            if (++spin > (1ull << 22)) {
+                if (lane == 0) atomicOr(err, (unsigned long long)FK_FAULT_PARTS);
+                return pre;
+            }
+            __builtin_amdgcn_s_sleep(1);
+            if ((f >> 62) == 0) f = __hip_atomic_load(&flags[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        const unsigned long long pm = __ballot((f >> 62) == 2);
+        const unsigned long long val = f & M;
+        if (pm) {
+            const uint32_t first = (uint32_t)__builtin_ctzll(pm);   /* the nearest prefix */
+            pre += wsum64(lane <= first ? val : 0ull);
+            break;
+        }
+        pre += wsum64(val);
+        j -= 64;
+    }
+    if (lane == 0) __hip_atomic_store(&flags[blk], P | (pre + total), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return pre;
+}
+
+/* the bins of a part: thread t takes bins [32 t, 32 t + 32).  The 2^15
+   bins are 16-bit halves of 2^14 LDS words (64 KiB instead of 128: half the
+   zeroing and reading, 16.9 -> 13.1 ms per k = 17 pass; a second block per
+   CU would need <= 64 VGPRs, and forced there the spills made it 21 ms).  A half that wraps (a k-mer 65536 times in
+   one part) makes the halves' sum fall short of the codes: the part is then
+   counted again as two halves of 2^14 32-bit bins. */
+#define KC_WORDS (1u << 14)
+__global__ void __launch_bounds__(1024)
+k_kp_count(const uint16_t *in, const PartMeta *meta, uint64_t cap_in, uint64_t lo, uint64_t npads,
+           const unsigned long long *tcount, uint32_t nparts, int k, unsigned long long *flags, uint64_t *out_k,
+           uint32_t *out_c, unsigned long long *slots, uint64_t *fl, unsigned long long *err) {
+    extern __shared__ uint32_t bins[];   /* KC_WORDS */
+    __shared__ unsigned long long wred[16][10];
+    __shared__ uint32_t hpre[24];
+    __shared__ uint32_t wnz[16], wmx[16];
+    __shared__ unsigned long long bprefix;
+    __shared__ uint32_t vblk;
+    const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    /* the part: a ticket in the order blocks start (flags[nparts]), not
+       blockIdx -- the chained scan may only wait on blocks that are already
+       running, and across the 8 XCDs (and other processes' kernels)
+       blockIdx order is not start order */
+    if (t == 0) vblk = (uint32_t)atomicAdd(&flags[nparts], 1ull);
+    for (uint32_t i = t; i < KC_WORDS / 4u; i += 1024u) reinterpret_cast<uint4 *>(bins)[i] = make_uint4(0, 0, 0, 0);
+    if (t < 24) hpre[t] = 0;
+    __syncthreads();
+    const uint32_t blk = vblk;
+    PartMeta m = meta[blk];
+    if (m.off + m.n > cap_in) {   /* bound check (k_count_parts's) */
+        if (t == 0) atomicOr(err, (unsigned long long)FK_FAULT_META);
+        m.n = 0;
+        m.off = 0;
+    }
+    const uint4 *g4 = reinterpret_cast<const uint4 *>(in + m.off);
+    const uint32_t nq = (m.n + 7u) >> 3;
+    /* each code to its bin, bin b at half b & 1 of word b >> 1 (hsel: the
+       32-bit pass of half h, bins [h 2^14, (h + 1) 2^14) only) */
+    auto count = [&](int hsel) {
+        for (uint32_t q = t; q < nq; q += 1024u) {
+            const uint4 v = g4[q];
+            const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int h = 0; h < 8; h++) {
+                if (q * 8u + (uint32_t)h >= m.n) continue;
+                const uint32_t b = (w4[h >> 1] >> (16 * (h & 1))) & 0x7FFFu;
+                if (hsel < 0) atomicAdd(&bins[b >> 1], 1u << ((b & 1u) << 4));
+                else if ((b >> 14) == (uint32_t)hsel) atomicAdd(&bins[b & (KC_WORDS - 1u)], 1u);
+            }
+        }
+    };
+    count(-1);
+    __syncthreads();
+    /* thread t's 32 bins: words [16 t, 16 t + 16) */
+    uint32_t c[32];
+    unsigned long long hs = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < 4u; j++) {
+        const uint4 q = reinterpret_cast<const uint4 *>(bins)[t * 4u + j];
+        const uint32_t w4[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+        for (int h = 0; h < 4; h++) {
+            c[8 * j + 2 * h] = w4[h] & 0xFFFFu;
+            c[8 * j + 2 * h + 1] = w4[h] >> 16;
+            hs += (w4[h] & 0xFFFFu) + (w4[h] >> 16);
+        }
+    }
+    {   /* the wrap check (block-wide: the halves' sum against the codes) */
+        const unsigned long long a = wsum64(hs);
+        if (lane == 0) wred[wv][0] = a;
+        __syncthreads();
+        unsigned long long sa = 0;
+#pragma unroll
+        for (uint32_t w = 0; w < 16u; w++) sa += wred[w][0];
+        if (sa != (unsigned long long)m.n) {
+            for (int h = 0; h < 2; h++) {
+                __syncthreads();
+                for (uint32_t i = t; i < KC_WORDS / 4u; i += 1024u)
+                    reinterpret_cast<uint4 *>(bins)[i] = make_uint4(0, 0, 0, 0);
+                __syncthreads();
+                count(h);
+                __syncthreads();
+                if ((t >> 9) == (uint32_t)h) {   /* (thread t's bins lie in half t / 512) */
+#pragma unroll
+                    for (uint32_t j = 0; j < 8u; j++) {
+                        const uint4 q = reinterpret_cast<const uint4 *>(bins)[(t & 511u) * 8u + j];
+                        c[4 * j] = q.x; c[4 * j + 1] = q.y; c[4 * j + 2] = q.z; c[4 * j + 3] = q.w;
+                    }
+                }
+            }
+        }
+        __syncthreads();   /* (wred is reused below) */
+    }
+    /* the top key (relative 0xFFFFFFFF, the last bin of the last part) was
+       only counted (k_kpart): its real windows, the pads taken off */
+    const unsigned long long extra = blk == nparts - 1u ? *tcount - npads : 0ull;
+    if (t == 1023u && extra) c[31] += (uint32_t)extra;
+    const int fs = 2 * (k - 1);
+    const uint64_t kb = lo + ((uint64_t)blk << 15) + t * 32u;   /* key of my first bin (a multiple of 4) */
+    /* statistics with constant register indices (a runtime index into a
+       register array put it in scratch memory): bin j's last base is j & 3,
+       and the first base is the same for all 32 bins */
+    uint32_t nz = 0;
+    unsigned long long l4[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (uint32_t j = 0; j < 32u; j++) {
+        nz += c[j] != 0;
+        l4[j & 3] += c[j];
+    }
+    const unsigned long long sum = l4[0] + l4[1] + l4[2] + l4[3];
+    const uint32_t fd = (uint32_t)((kb >> fs) & 3);
+    unsigned long long st[10] = {nz, sum, l4[0], l4[1], l4[2], l4[3], fd == 0 ? sum : 0ull, fd == 1 ? sum : 0ull,
+                                 fd == 2 ? sum : 0ull, fd == 3 ? sum : 0ull};
+    /* block scan of the nonzero counts */
+    const uint32_t inc = wscan_incl32(nz);
+    if (lane == 63) wnz[wv] = inc;
+    __syncthreads();
+    uint32_t before = 0, total = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < 16u; w++) {
+        const uint32_t x = wnz[w];
+        before += w < wv ? x : 0u;
+        total += x;
+    }
+    const uint32_t off = before + inc - nz;
+    /* the parts' chained scan */
+    if (wv == 0) {
+        const unsigned long long pre = chain_prefix(flags, blk, total, err);
+        if (lane == 0) {
+            bprefix = pre;
+            if (!total) fl[2 * (size_t)blk] = KP_EMPTY;
+        }
+    }
+    /* the nearest earlier thread holding a nonzero bin (an exclusive max
+       scan of t + 1), for the adjacent pair across threads */
+    const uint32_t im = wscan_max32(nz ? t + 1u : 0u);
+    if (lane == 63) wmx[wv] = im;
+    __syncthreads();   /* (also: every thread has its bins in registers) */
+    uint32_t pm = (uint32_t)__shfl_up((int)im, 1, 64);
+    if (lane == 0) pm = 0;
+    for (uint32_t w = 0; w < wv; w++) pm = max(pm, wmx[w]);
+    uint64_t first = 0, prev = 0;
+    bool have = false;
+    /* adjacent keys inside my 32 bins differ in one of the last three bases
+       (depths k, k - 1, k - 2): counted in registers */
+    uint32_t h0 = 0, h1 = 0, h2 = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < 32u; j++) {
+        if (c[j]) {
+            const uint64_t key = kb + j;
+            if (have) {   /* first differing base of adjacent keys (k_sp_wprefix) */
+                const uint32_t d = (uint32_t)(key ^ prev);   /* < 32 */
+                h0 += d < 4u;
+                h1 += d >= 4u && d < 16u;
+                h2 += d >= 16u;
+            } else {
+                first = key;
+            }
+            prev = key;
+            have = true;
+        }
+    }
+    {
+        const uint32_t a0 = wsum32(h0), a1 = wsum32(h1), a2 = wsum32(h2);
+        if (lane == 0) {
+            if (a0) atomicAdd(&hpre[k], a0);
+            if (a1) atomicAdd(&hpre[k - 1], a1);
+            if (a2) atomicAdd(&hpre[k - 2], a2);
+        }
+    }
+    /* every thread's last key in the (now free) bins' LDS */
+    uint64_t *lastk = reinterpret_cast<uint64_t *>(bins);
+    lastk[t] = prev;
+    __syncthreads();
+    if (nz && pm) {
+        const uint64_t pk = lastk[pm - 1u];
+        const int lz = __clzll((long long)(first ^ pk)) - (64 - 2 * k);
+        atomicAdd(&hpre[lz / 2 + 1], 1u);
+    }
+    if (nz && !pm) fl[2 * (size_t)blk] = first;
+    if (nz && off + nz == total) fl[2 * (size_t)blk + 1] = prev;
+    /* the nonzero bins out, in rounds of KC_STAGE entries staged in the
+       bins' LDS (bin index u16, count u32) and written as contiguous words:
+       one thread writing its own bins strided the stores 64 lines per
+       instruction, and the output (12 B per distinct k-mer, ~90 GB per
+       10 G-base step) cost more than the count */
+    constexpr uint32_t KC_STAGE = 8192u;   /* (u16 + u32 each: 48 KiB of the 64) */
+    uint16_t *sidx = reinterpret_cast<uint16_t *>(bins);
+    uint32_t *scnt = bins + KC_STAGE / 2u;
+    const uint64_t kpart = lo + ((uint64_t)blk << 15);
+    for (uint32_t r0 = 0; r0 < total; r0 += KC_STAGE) {
+        __syncthreads();   /* (the staging area is free: lastk read, or the last round written out) */
+        uint32_t o = off;
+#pragma unroll
+        for (uint32_t j = 0; j < 32u; j++) {
+            if (c[j]) {
+                if (o >= r0 && o < r0 + KC_STAGE) {
+                    sidx[o - r0] = (uint16_t)(t * 32u + j);
+                    scnt[o - r0] = c[j];
+                }
+                o++;
+            }
+        }
+        __syncthreads();
+        const uint32_t nr = min(KC_STAGE, total - r0);
+        for (uint32_t i = t; i < nr; i += 1024u) {
+            __builtin_nontemporal_store((uint64_t)(kpart + sidx[i]), out_k + bprefix + r0 + i);
+            __builtin_nontemporal_store(scnt[i], out_c + bprefix + r0 + i);
+        }
+    }
+    /* the rollover check: a bin past 2^32 codes wrapped, so its sum falls
+       short of the codes (less the pads) */
+    unsigned long long v10[10];
+#pragma unroll
+    for (int q = 0; q < 10; q++) v10[q] = wsum64(st[q]);
+    if (lane == 0)
+#pragma unroll
+        for (int q = 0; q < 10; q++) wred[wv][q] = v10[q];
+    __syncthreads();
+    if (t < 10) {
+        unsigned long long a = 0;
+        for (uint32_t w = 0; w < 16u; w++) a += wred[w][t];
+        if (a) atomicAdd(&slots[(blk % KP_SLOTS) * KP_SLOT_W + t], a);
+        if (t == 1 && a != (uint64_t)m.n + extra) atomicOr(&slots[(blk % KP_SLOTS) * KP_SLOT_W + 10], 1ull);
+    }
+    if (t < 24 && hpre[t]) atomicAdd(&slots[(blk % KP_SLOTS) * KP_SLOT_W + 11 + t], (unsigned long long)hpre[t]);
+}
+
+/*
+ * Wide passes (18 <= k <= 20, a key range of more than 2^32 keys): the same
+ * two partition levels (64-bit keys in, the parts' codes 32-bit), then each
+ * part -- up to KS_CAP keys of at most 23 bits, ~10 K at k = 20 over 10 G
+ * bases -- sorted in LDS instead of counted: bucketed by its top 8 bits
+ * (LDS histogram, scan, scatter), each bucket sorted by one wave in
+ * registers (a bitonic network over 64 N keys, N = 1..16 per lane), then run-
+ * length encoded.  A part or bucket above those sizes (a k-mer repeated
+ * tens of thousands of times in one part) flags the pass, which then takes
+ * the library sort (fks_sort_runs) instead.
+ */
+#define KS_CAP 24576u        /* k_kp_sort<KS_CAP>: one block per CU */
+#define KS_CAP_S 12288u      /* k_kp_sort<KS_CAP_S>: two (every part of the pass fits) */
+#define FK_FAULT_SORTCAP 8u
+
+/* bitonic sort of the 64 N values x[i] (element i * 64 + lane), ascending */
+template <int N>
+__device__ __forceinline__ void wave_bitonic(uint32_t (&x)[N]) {
+    const uint32_t lane = threadIdx.x & 63;
+#pragma unroll
+    for (uint32_t s2 = 2; s2 <= 64u * N; s2 <<= 1) {
+#pragma unroll
+        for (uint32_t d = s2 >> 1; d > 0; d >>= 1) {
+            if (d >= 64) {
+                const uint32_t dr = d / 64;
+#pragma unroll
+                for (int i = 0; i < N; i++) {
+                    if ((uint32_t)i & dr) continue;
+                    const int j = i | (int)dr;
+                    const uint32_t e = (uint32_t)i * 64u + lane;
+                    const bool up = (e & s2) == 0;
+                    const uint32_t a = x[i], b = x[j];
+                    x[i] = up ? min(a, b) : max(a, b);
+                    x[j] = up ? max(a, b) : min(a, b);
+                }
+            } else {
+#pragma unroll
+                for (int i = 0; i < N; i++) {
+                    const uint32_t e = (uint32_t)i * 64u + lane;
+                    const uint32_t o = (uint32_t)__shfl_xor((int)x[i], (int)d, 64);
+                    const bool up = (e & s2) == 0, low = (lane & d) == 0;
+                    x[i] = (low == up) ? min(x[i], o) : max(x[i], o);
+                }
+            }
+        }
+    }
+}
+
+/* Batcher's odd-even merge sort of N (a power of two) registers, ascending
+   (63 compare-exchanges at N = 16, every index a constant) */
+template <int N>
+__device__ __forceinline__ void reg_sort(uint32_t (&x)[N]) {
+#pragma unroll
+    for (int p = 1; p < N; p <<= 1)
+#pragma unroll
+        for (int k = p; k >= 1; k >>= 1)
+#pragma unroll
+            for (int j = k % p; j + k < N; j += 2 * k)
+#pragma unroll
+                for (int i = 0; i < k; i++)
+                    if (i + j + k < N && (i + j) / (2 * p) == (i + j + k) / (2 * p)) {
+                        const uint32_t a = x[i + j], b = x[i + j + k];
+                        x[i + j] = min(a, b);
+                        x[i + j + k] = max(a, b);
+                    }
+}
+
+template <int N>
+__device__ __forceinline__ void wave_sort_bucket(uint32_t *k, uint32_t n) {
+    const uint32_t lane = threadIdx.x & 63;
+    uint32_t x[N];
+#pragma unroll
+    for (int i = 0; i < N; i++) {
+        const uint32_t e = (uint32_t)i * 64u + lane;
+        x[i] = e < n ? k[e] : ~0u;
+    }
+    wave_bitonic<N>(x);
+#pragma unroll
+    for (int i = 0; i < N; i++) {
+        const uint32_t e = (uint32_t)i * 64u + lane;
+        if (e < n) k[e] = x[i];
+    }
+}
+
+template <uint32_t CAP>
+__global__ void __launch_bounds__(1024)
+k_kp_sort(const uint32_t *in, const PartMeta *meta, uint64_t cap_in, uint64_t lo, uint32_t psh, uint64_t npads,
+          const unsigned long long *tcount, uint32_t top_part, uint32_t nparts, int k, unsigned long long *flags,
+          uint64_t *out_k, uint32_t *out_c, unsigned long long *slots, uint64_t *fl, unsigned long long *err) {
+    constexpr uint32_t KSI = CAP / 1024u;
+    extern __shared__ uint32_t keys[];   /* CAP keys, then CAP + 1 u16 run starts */
+    uint16_t *const rs = reinterpret_cast<uint16_t *>(keys + CAP);
+    /* the bucket cursors live where the run starts go later (two blocks of
+       the small instance per CU: 80 KB of LDS each at most) */
+    uint32_t *const bh = reinterpret_cast<uint32_t *>(rs);
+    __shared__ uint32_t bo[1025];
+    __shared__ unsigned long long wred[16][10];
+    __shared__ uint32_t hpre[24];
+    __shared__ uint32_t wnz[16];
+    __shared__ unsigned long long bprefix;
+    __shared__ uint32_t bad, vblk;
+    const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    bh[t] = 0;
+    if (t < 24) hpre[t] = 0;
+    if (t == 0) {
+        bad = 0;
+        vblk = (uint32_t)atomicAdd(&flags[nparts], 1ull);   /* (k_kp_count: start order) */
+    }
+    __syncthreads();
+    const uint32_t blk = vblk;
+    PartMeta m = meta[blk];
+    if (m.off + m.n > cap_in) {
+        if (t == 0) atomicOr(err, (unsigned long long)FK_FAULT_META);
+        m.n = 0;
+        m.off = 0;
+    }
+    if (m.n > CAP) {   /* too many keys for one block's LDS: the library sort */
+        if (t == 0) atomicOr(err, (unsigned long long)FK_FAULT_SORTCAP);
+        m.n = 0;
+    }
+    const uint32_t n = m.n, bsh = psh - 10u;
+    /* 1. bucket by the top 10 bits of the part's code (~10 keys a bucket) */
+    uint32_t v[KSI];
+#pragma unroll
+    for (uint32_t j = 0; j < KSI; j++) {
+        v[j] = j * 1024u + t < n ? in[m.off + j * 1024u + t] : 0u;
+        if (j * 1024u + t < n) atomicAdd(&bh[v[j] >> bsh], 1u);
+    }
+    __syncthreads();
+    {   /* bucket t's start: a block scan */
+        const uint32_t c = bh[t], inc = wscan_incl32(c);
+        if (lane == 63) wnz[wv] = inc;
+        __syncthreads();
+        uint32_t before = 0;
+#pragma unroll
+        for (uint32_t w = 0; w < 16u; w++) before += w < wv ? wnz[w] : 0u;
+        bo[t] = bh[t] = before + inc - c;
+        if (t == 1023) bo[1024] = before + inc;
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t j = 0; j < KSI; j++)
+        if (j * 1024u + t < n) keys[atomicAdd(&bh[v[j] >> bsh], 1u)] = v[j];
+    __syncthreads();
+    /* 2. bucket t of up to 16 keys sorted by thread t in registers; the
+       larger ones (~2 % at 10 a bucket on average) each by one wave */
+    {
+        const uint32_t b0 = bo[t], nb = bo[t + 1] - b0;
+        if (nb > 1u && nb <= 16u) {
+            uint32_t x[16];
+#pragma unroll
+            for (uint32_t i = 0; i < 16u; i++) x[i] = i < nb ? keys[b0 + i] : ~0u;
+            reg_sort<16>(x);
+#pragma unroll
+            for (uint32_t i = 0; i < 16u; i++)
+                if (i < nb) keys[b0 + i] = x[i];
+        }
+    }
+    for (unsigned long long big = __ballot(bo[wv * 64u + lane + 1] - bo[wv * 64u + lane] > 16u); big; big &= big - 1) {
+        const uint32_t b = wv * 64u + (uint32_t)__builtin_ctzll(big);
+        const uint32_t b0 = bo[b], nb = bo[b + 1] - b0;
+        if (nb <= 64) wave_sort_bucket<1>(keys + b0, nb);
+        else if (nb <= 128) wave_sort_bucket<2>(keys + b0, nb);
+        else if (nb <= 256) wave_sort_bucket<4>(keys + b0, nb);
+        else if (nb <= 512) wave_sort_bucket<8>(keys + b0, nb);
+        else if (nb <= 1024) wave_sort_bucket<16>(keys + b0, nb);
+        else if (lane == 0) bad = 1;
+    }
+    __syncthreads();
+    if (bad) {
+        if (t == 0) atomicOr(err, (unsigned long long)FK_FAULT_SORTCAP);
+    }
+    const uint32_t nn = bad ? 0u : n;
+    /* 3. runs: thread t takes positions [t * KSI, +KSI); a run
+       starts where the key changes */
+    const uint32_t p0 = t * KSI;
+    uint32_t nz = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < KSI; j++) {
+        const uint32_t i = p0 + j;
+        if (i < nn && (i == 0 || keys[i] != keys[i - 1])) nz++;
+    }
+    const uint32_t inc = wscan_incl32(nz);
+    if (lane == 63) wnz[wv] = inc;
+    __syncthreads();
+    uint32_t before = 0, runs = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < 16u; w++) {
+        const uint32_t x = wnz[w];
+        before += w < wv ? x : 0u;
+        runs += x;
+    }
+    /* the top key 4^k - 1 (when the pass holds it: the last key of the top
+       part) was only counted (k_kpart): its real windows, the pads taken
+       off, are one more run after this part's others */
+    const unsigned long long extra = blk == top_part ? *tcount - npads : 0ull;
+    const uint32_t total = runs + (extra ? 1u : 0u);
+    const uint32_t off = before + inc - nz;
+    /* every run's start in LDS (rs[runs] = the end), so that run r is
+       written by thread r % 1024: contiguous stores */
+    {
+        uint32_t o = off;
+#pragma unroll
+        for (uint32_t j = 0; j < KSI; j++) {
+            const uint32_t i = p0 + j;
+            if (i < nn && (i == 0 || keys[i] != keys[i - 1])) rs[o++] = (uint16_t)i;
+        }
+        if (t == 0) rs[runs] = (uint16_t)nn;
+    }
+    if (wv == 0) {
+        const unsigned long long pre = chain_prefix(flags, blk, total, err);
+        if (lane == 0) {
+            bprefix = pre;
+            if (!total) fl[2 * (size_t)blk] = KP_EMPTY;
+        }
+    }
+    __syncthreads();
+    const int fs = 2 * (k - 1);
+    const uint64_t kb = lo + ((uint64_t)blk << psh);
+    /* (named accumulators: a runtime index into a register array lives in
+       scratch memory; the first base is the part's, psh < 2k - 2) */
+    unsigned long long l0 = 0, l1 = 0, l2 = 0, l3 = 0, nd = 0;
+    for (uint32_t r = t; r < runs; r += 1024u) {
+        const uint32_t i = rs[r];
+        const uint64_t key = kb + keys[i];
+        const uint32_t c = (uint32_t)rs[r + 1] - i;
+        __builtin_nontemporal_store(key, out_k + bprefix + r);
+        __builtin_nontemporal_store(c, out_c + bprefix + r);
+        const uint32_t ld = (uint32_t)(key & 3);
+        nd += 1;
+        l0 += ld == 0 ? c : 0u;
+        l1 += ld == 1 ? c : 0u;
+        l2 += ld == 2 ? c : 0u;
+        l3 += ld == 3 ? c : 0u;
+        if (r > 0) {   /* against the run before it, in this part */
+            const int lz = __clzll((long long)(key ^ (kb + keys[i - 1]))) - (64 - 2 * k);
+            atomicAdd(&hpre[lz / 2 + 1], 1u);
+        }
+        if (r == 0) fl[2 * (size_t)blk] = key;
+        if (r + 1 == total) fl[2 * (size_t)blk + 1] = key;
+    }
+    if (t == 0 && extra) {   /* the top key's run, last in the part */
+        const uint64_t key = (1ull << (2 * k)) - 1;
+        const uint32_t c = (uint32_t)extra;
+        out_k[bprefix + runs] = key;
+        out_c[bprefix + runs] = c;
+        nd += 1;
+        l3 += c;   /* (the key 4^k - 1 ends in base T = 3) */
+        if (runs) {
+            const int lz = __clzll((long long)(key ^ (kb + keys[nn - 1]))) - (64 - 2 * k);
+            atomicAdd(&hpre[lz / 2 + 1], 1u);
+        } else {
+            fl[2 * (size_t)blk] = key;
+        }
+        fl[2 * (size_t)blk + 1] = key;
+        if (extra >> 32) atomicOr(&slots[(blk % KP_SLOTS) * KP_SLOT_W + 10], 1ull);   /* a u32 count wrapped */
+    }
+    const unsigned long long sum = l0 + l1 + l2 + l3;
+    const uint32_t fd = (uint32_t)((kb >> fs) & 3);
+    const unsigned long long st[10] = {nd, sum, l0, l1, l2, l3, fd == 0 ? sum : 0ull, fd == 1 ? sum : 0ull,
+                                       fd == 2 ? sum : 0ull, fd == 3 ? sum : 0ull};
+    unsigned long long v10[10];
+#pragma unroll
+    for (int q = 0; q < 10; q++) v10[q] = wsum64(st[q]);
+    if (lane == 0)
+#pragma unroll
+        for (int q = 0; q < 10; q++) wred[wv][q] = v10[q];
+    __syncthreads();
+    if (t < 10) {
+        unsigned long long a = 0;
+        for (uint32_t w = 0; w < 16u; w++) a += wred[w][t];
+        if (a) atomicAdd(&slots[(blk % KP_SLOTS) * KP_SLOT_W + t], a);
+    }
+    if (t < 24 && hpre[t]) atomicAdd(&slots[(blk % KP_SLOTS) * KP_SLOT_W + 11 + t], (unsigned long long)hpre[t]);
+}
+
+/* the partials into the pass accumulators (FKS_ACC layout), the prefix
+   histogram of each nonempty part's first key against the last key of the
+   nonempty part before it, and the pass's distinct count (res[0]) */
+__global__ void __launch_bounds__(256)
+k_kp_fold(const unsigned long long *slots, const uint64_t *fl, uint32_t nparts, int k,
+          const unsigned long long *flags, unsigned long long *dacc, unsigned long long *res) {
+    __shared__ uint32_t h[24];
+    if (threadIdx.x < 24) h[threadIdx.x] = 0;
+    __syncthreads();
+    if (blockIdx.x == 0) {
+        if (threadIdx.x < 10) {
+            unsigned long long a = 0;
+            for (uint32_t sl = 0; sl < KP_SLOTS; sl++) a += slots[sl * KP_SLOT_W + threadIdx.x];
+            if (a) atomicAdd(&dacc[threadIdx.x], a);
+        } else if (threadIdx.x == 10) {
+            unsigned long long a = 0;
+            for (uint32_t sl = 0; sl < KP_SLOTS; sl++) a |= slots[sl * KP_SLOT_W + 10];
+            if (a) atomicAdd(&dacc[FKS_ACC_ROLL], 1ull);   /* (k_sp_stats adds wrapped counts' high words) */
+        } else if (threadIdx.x >= 32 && threadIdx.x < 56) {
+            unsigned long long a = 0;
+            for (uint32_t sl = 0; sl < KP_SLOTS; sl++) a += slots[sl * KP_SLOT_W + 11 + (threadIdx.x - 32)];
+            if (a) atomicAdd(&dacc[FKS_ACC_WPREFIX + (threadIdx.x - 32)], a);
+        } else if (threadIdx.x == 64) {
+            res[0] = flags[nparts - 1] & ((1ull << 62) - 1);
+        }
+    }
+    for (uint32_t p = blockIdx.x * blockDim.x + threadIdx.x; p < nparts; p += gridDim.x * blockDim.x) {
+        const uint64_t first = fl[2 * (size_t)p];
+        if (first == KP_EMPTY || p == 0) continue;
+        uint32_t q = p - 1;
+        while (q > 0 && fl[2 * (size_t)q] == KP_EMPTY) q--;
+        if (fl[2 * (size_t)q] == KP_EMPTY) continue;
+        const uint64_t pk = fl[2 * (size_t)q + 1];
+        const int lz = __clzll((long long)(first ^ pk)) - (64 - 2 * k);
+        atomicAdd(&h[lz / 2 + 1], 1u);
+    }
+    __syncthreads();
+    if (threadIdx.x < 24 && h[threadIdx.x]) atomicAdd(&dacc[FKS_ACC_WPREFIX + threadIdx.x], (unsigned long long)h[threadIdx.x]);
+}
+
+/* The pass (keys lo + r for the n 32-bit r, npads of them the pad
+   0xFFFFFFFF) into its runs at out_k / out_c: *nw of them */
+int sp_count_runs32(fk_engine *e, const uint32_t *keys, uint64_t n, uint64_t lo, uint64_t npads,
+                           unsigned long long *dacc, uint64_t *out_k, uint32_t *out_c, uint64_t *nw) {
+    *nw = 0;
+    if (n == 0) return FK_OK;
+    const int k = e->k;
+    PartGeo pg{};
+    pg.nslices = 2048u;
+    pg.split = 6u;   /* 2^21-bin coarse slices, 64 parts of 2^15 */
+    pg.batch = KP_BATCH;
+    const uint32_t grid = (uint32_t)std::max(1, e->cus);
+    pg.rounds = (uint32_t)((n + (uint64_t)grid * KP_BATCH - 1) / ((uint64_t)grid * KP_BATCH));
+    pg.rows = grid * pg.rounds;
+    pg.flag = nullptr;
+    const uint64_t ncodes = (uint64_t)pg.rows * KP_BATCH;   /* u32 codes */
+    const uint32_t nparts = 2048u << 6;
+    int rc = sp_ensure((void **)&e->d_codes, &e->codes_cap, 2 * ncodes, sizeof(uint16_t));
+    if (!rc) rc = sp_ensure((void **)&e->d_pidx, &e->pidx_cap, (uint64_t)pg.rows * 2048u, sizeof(uint32_t));
+    if (!rc) rc = sp_ensure((void **)&e->d_parts, &e->parts_cap, n + 8ull * nparts + 16, sizeof(uint16_t));
+    if (rc) return rc;
+    if (!e->d_pmeta && hipMalloc(&e->d_pmeta, (size_t)2048 * REPART_METAP * sizeof(PartMeta) + 64) != hipSuccess)
+        return FK_E_OOM;
+    DevScratch flags, slots, fl, res;
+    if (!flags.alloc((size_t)(nparts + 1) * 8) || !slots.alloc((size_t)KP_SLOTS * KP_SLOT_W * 8) ||
+        !fl.alloc((size_t)nparts * 16) || !res.alloc(16))
+        return FK_E_OOM;
+    pg.codes = e->d_codes;
+    pg.idx = e->d_pidx;
+    PartMeta *meta = static_cast<PartMeta *>(e->d_pmeta);
+    unsigned long long *alloc = reinterpret_cast<unsigned long long *>(meta + (size_t)2048 * REPART_METAP);
+    HIPCHK(hipMemsetAsync(alloc, 0, 2 * sizeof(unsigned long long), e->stream));
+    HIPCHK(hipMemsetAsync(flags.p, 0, (size_t)(nparts + 1) * 8, e->stream));   /* (+ the block tickets) */
+    HIPCHK(hipMemsetAsync(slots.p, 0, (size_t)KP_SLOTS * KP_SLOT_W * 8, e->stream));
+    HIPCHK(hipMemsetAsync(res.p, 0, 16, e->stream));
+    unsigned long long *tcount = res.as<unsigned long long>() + 1;
+    hipLaunchKernelGGL(k_kpart<uint32_t>, dim3(grid), dim3(1024), (size_t)KP_BATCH * 4, e->stream, keys, n, pg, 0ull,
+                       0ull, 21u, 0xFFFFFFFFull, tcount);
+    HIPCHK(hipGetLastError());
+    hipLaunchKernelGGL(k_repart<uint16_t>, dim3(2048u / REPART_G), dim3(1024), 0, e->stream, pg, e->d_parts, alloc,
+                       meta, (uint64_t)e->parts_cap, alloc + 1, 15u, nullptr);
+    HIPCHK(hipGetLastError());
+    hipLaunchKernelGGL(k_kp_count, dim3(nparts), dim3(1024), (size_t)KC_WORDS * 4, e->stream, (const uint16_t *)e->d_parts,
+                       (const PartMeta *)meta, (uint64_t)e->parts_cap, lo, npads, (const unsigned long long *)tcount, nparts,
+                       k, flags.as<unsigned long long>(), out_k, out_c, slots.as<unsigned long long>(), fl.as<uint64_t>(),
+                       alloc + 1);
+    HIPCHK(hipGetLastError());
+    hipLaunchKernelGGL(k_kp_fold, dim3(64), dim3(256), 0, e->stream, (const unsigned long long *)slots.p,
+                       (const uint64_t *)fl.p, nparts, k, (const unsigned long long *)flags.p, dacc,
+                       res.as<unsigned long long>());
+    HIPCHK(hipGetLastError());
+    unsigned long long r[2] = {0, 0};
+    HIPCHK(hipMemcpyAsync(&r[0], res.p, 8, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipMemcpyAsync(&r[1], alloc + 1, 8, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    if (r[1]) return FK_E_INTERNAL;
+    *nw = r[0];
+    return FK_OK;
+}
+
+/* A wide pass (keys[0, n) in [lo, hi), hi - lo > 2^32, npads of them the
+   pad 4^k - 1) into its runs at out_k / out_c (*nw).  `fallback` is set
+   when a part or bucket is too large for k_kp_sort: nothing was folded into
+   dacc and the caller sorts the pass with the library instead. */
+int sp_sort_runs64(fk_engine *e, const uint64_t *keys, uint64_t n, uint64_t lo, uint64_t hi, uint64_t npads,
+                          unsigned long long *dacc, uint64_t *out_k, uint32_t *out_c, uint64_t *nw, bool *fallback) {
+    *nw = 0;
+    *fallback = false;
+    if (n == 0) return FK_OK;
+    const int k = e->k;
+    uint32_t sbits = 33;
+    while (sbits < 64 && ((hi - lo - 1) >> sbits)) sbits++;
+    /* 2048 coarse slices of 128 parts (k_repart: 4 slices per block): at k
+       = 20 a pass of up to 2^32 keys leaves ~16 K per part, within k_kp_sort's
+       KS_CAP (64 parts per slice left ~33 K, and every pass took the library
+       sort) */
+    const uint32_t cs = sbits - 11, psh = cs - 7;
+    PartGeo pg{};
+    pg.nslices = 2048u;
+    pg.split = 7u;
+    pg.batch = KP_BATCH;
+    const uint32_t grid = (uint32_t)std::max(1, e->cus);
+    pg.rounds = (uint32_t)((n + (uint64_t)grid * KP_BATCH - 1) / ((uint64_t)grid * KP_BATCH));
+    pg.rows = grid * pg.rounds;
+    pg.flag = nullptr;
+    const uint64_t ncodes = (uint64_t)pg.rows * KP_BATCH;
+    const uint32_t nparts = 2048u << 7;
+    int rc = sp_ensure((void **)&e->d_codes, &e->codes_cap, 2 * ncodes, sizeof(uint16_t));
+    if (!rc) rc = sp_ensure((void **)&e->d_pidx, &e->pidx_cap, (uint64_t)pg.rows * 2048u, sizeof(uint32_t));
+    /* (the part streams as 32-bit codes: twice the u16 capacity) */
+    if (!rc) rc = sp_ensure((void **)&e->d_parts, &e->parts_cap, 2 * (n + 8ull * nparts + 16), sizeof(uint16_t));
+    if (rc) return rc;
+    if (!e->d_pmeta && hipMalloc(&e->d_pmeta, (size_t)2048 * REPART_METAP * sizeof(PartMeta) + 64) != hipSuccess)
+        return FK_E_OOM;
+    DevScratch flags, slots, fl, res;
+    if (!flags.alloc((size_t)(nparts + 1) * 8) || !slots.alloc((size_t)KP_SLOTS * KP_SLOT_W * 8) ||
+        !fl.alloc((size_t)nparts * 16) || !res.alloc(16))
+        return FK_E_OOM;
+    pg.codes = e->d_codes;
+    pg.idx = e->d_pidx;
+    PartMeta *meta = static_cast<PartMeta *>(e->d_pmeta);
+    unsigned long long *alloc = reinterpret_cast<unsigned long long *>(meta + (size_t)2048 * REPART_METAP);
+    uint32_t *parts32 = reinterpret_cast<uint32_t *>(e->d_parts);
+    const uint64_t cap32 = e->parts_cap / 2;
+    HIPCHK(hipMemsetAsync(alloc, 0, 3 * sizeof(unsigned long long), e->stream));
+    HIPCHK(hipMemsetAsync(flags.p, 0, (size_t)(nparts + 1) * 8, e->stream));   /* (+ the block tickets) */
+    HIPCHK(hipMemsetAsync(slots.p, 0, (size_t)KP_SLOTS * KP_SLOT_W * 8, e->stream));
+    HIPCHK(hipMemsetAsync(res.p, 0, 16, e->stream));
+    unsigned long long *tcount = res.as<unsigned long long>() + 1;
+    /* the top key 4^k - 1 (the pads' value; past hi they are left out as
+       out of range) counted apart when the pass holds it */
+    const uint64_t top = (1ull << (2 * k)) - 1;
+    const bool top_in = top >= lo && top < hi;
+    hipLaunchKernelGGL(k_kpart<uint64_t>, dim3(grid), dim3(1024), (size_t)KP_BATCH * 4, e->stream, keys, n, pg, lo, hi,
+                       cs, top_in ? top : ~0ull, tcount);
+    HIPCHK(hipGetLastError());
+    hipLaunchKernelGGL((k_repart<uint32_t, 4u>), dim3(2048u / 4u), dim3(1024), 0, e->stream, pg, parts32, alloc, meta,
+                       cap32, alloc + 1, psh, alloc + 2);
+    HIPCHK(hipGetLastError());
+    unsigned long long pmax = 0;
+    HIPCHK(hipMemcpyAsync(&pmax, alloc + 2, 8, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    if (pmax > KS_CAP) {   /* a part past one block's LDS: the library sort */
+        *fallback = true;
+        return FK_OK;
+    }
+    const bool small = pmax <= KS_CAP_S;
+    const uint32_t top_part = top_in ? (uint32_t)((top - lo) >> psh) : ~0u;
+    if (small)
+        hipLaunchKernelGGL(k_kp_sort<KS_CAP_S>, dim3(nparts), dim3(1024), (size_t)KS_CAP_S * 6 + 16, e->stream,
+                           (const uint32_t *)parts32, (const PartMeta *)meta, cap32, lo, psh, top_in ? npads : 0ull,
+                           (const unsigned long long *)tcount, top_part, nparts, k, flags.as<unsigned long long>(), out_k,
+                           out_c, slots.as<unsigned long long>(), fl.as<uint64_t>(), alloc + 1);
+    else
+        hipLaunchKernelGGL(k_kp_sort<KS_CAP>, dim3(nparts), dim3(1024), (size_t)KS_CAP * 6 + 16, e->stream,
+                           (const uint32_t *)parts32, (const PartMeta *)meta, cap32, lo, psh, top_in ? npads : 0ull,
+                           (const unsigned long long *)tcount, top_part, nparts, k, flags.as<unsigned long long>(), out_k,
+                           out_c, slots.as<unsigned long long>(), fl.as<uint64_t>(), alloc + 1);
+    HIPCHK(hipGetLastError());
+    unsigned long long ferr = 0;
+    HIPCHK(hipMemcpyAsync(&ferr, alloc + 1, 8, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    if (ferr & FK_FAULT_SORTCAP) {
+        *fallback = true;
+        return FK_OK;
+    }
+    if (ferr) return FK_E_INTERNAL;
+    hipLaunchKernelGGL(k_kp_fold, dim3(64), dim3(256), 0, e->stream, (const unsigned long long *)slots.p,
+                       (const uint64_t *)fl.p, nparts, k, (const unsigned long long *)flags.p, dacc,
+                       res.as<unsigned long long>());
+    HIPCHK(hipGetLastError());
+    unsigned long long r0 = 0;
+    HIPCHK(hipMemcpyAsync(&r0, res.p, 8, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    *nw = r0;
+    return FK_OK;
+}
+
+/*
+ * The sparse table (17 <= k <= 20) from the retained input, in key-range
+ * passes (k_sp_emit):
+ *   1. SP_HIST: window count per bucket (the top SP_BUCKET_BITS index bits)
+ *      and every short walk;
+ *   2. the passes: consecutive buckets merged while their windows fit one
+ *      sorted pass (capped by free HBM, or FINDKMER_TUNE sp_pass); a single
+ *      bucket above the cap is counted densely (2^(2k - SP_BUCKET_BITS) u64);
+ *   3. per pass: emit, sort + run-length encode (or select the nonzero dense
+ *      counts), statistics, prefix histogram, short-walk prefix marks, and
+ *      the runs kept as one part of the table.
+ * `seq`: the final run's length (its short walk if 1 <= seq < k).
+ */
+int sparse_finish(fk_engine *e, int32_t seq) {
+    const int k = e->k;
+    e->sp_distinct = 0;
+    memset(e->sp_tstat, 0, sizeof e->sp_tstat);
+    e->sp_roll = e->sp_nodes = 0;
+    const uint32_t nbk = 1u << SP_BUCKET_BITS;
+    const uint32_t shift = 2u * (uint32_t)k - SP_BUCKET_BITS;
+    {   /* the HIST launch needs the larger LDS; set it once for every mode */
+        const size_t lds = (size_t)SP_WAVES * FK_TILE_BYTES * sizeof(uint64_t) + (size_t)nbk * sizeof(uint32_t);
+        HIPCHK(hipFuncSetAttribute((const void *)k_sp_emit, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        for (const void *f : {(const void *)k_kpart<uint32_t>, (const void *)k_kpart<uint64_t>})
+            HIPCHK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(KP_BATCH * 4)));
+        HIPCHK(hipFuncSetAttribute((const void *)k_kp_sort<KS_CAP>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   (int)(KS_CAP * 6 + 16)));
+        HIPCHK(hipFuncSetAttribute((const void *)k_kp_sort<KS_CAP_S>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   (int)(KS_CAP_S * 6 + 16)));
+        HIPCHK(hipFuncSetAttribute((const void *)k_kp_count, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   (int)(KC_WORDS * 4)));
+    }
+    DevScratch acc, bh, ctr, pctr;
+    if (!acc.alloc(FKS_ACC_N * sizeof(unsigned long long)) || !bh.alloc((size_t)nbk * 8) || !ctr.alloc(24) ||
+        !pctr.alloc(2 * SP_MAXP * sizeof(unsigned long long)))
+        return FK_E_OOM;
+    /* a keys pass claims its output in SP_CHUNKs per wave: at most one
+       chunk's worth of pads per wave of every emit launch */
+    uint64_t pad_max = 0;
+    for (const auto &sg : e->spsegs)
+        if (sg.nranges)
+            pad_max += std::max<uint64_t>(1, std::min<uint64_t>((sg.nranges + SP_WAVES - 1) / SP_WAVES, (uint64_t)e->cus * 8)) *
+                       SP_WAVES * SP_CHUNK;
+    unsigned long long *dacc = acc.as<unsigned long long>();
+    unsigned long long *nctr = ctr.as<unsigned long long>();
+    HIPCHK(hipMemsetAsync(dacc, 0, FKS_ACC_N * sizeof(unsigned long long), e->stream));
+
+    /* the pass cap: window keys one sorted pass may hold.  A pass needs
+       ~56 B per key (emitted 8, sorted 8, runs 8, run lengths 8, rocPRIM's
+       scratch ~8, the part's keys 8 + counts 4, handed over), and the parts
+       of all passes together up to 12 B per window (distinct <= windows):
+       reserve those first */
+    const uint64_t wins = e->last.acc[ACC_WIN];
+    uint64_t cap = e->sp_pass;
+    uint64_t room = 0;   /* bytes for the passes' key lists and their processing */
+    {
+        size_t fr = 0, tot = 0;
+        HIPCHK(hipMemGetInfo(&fr, &tot));
+        /* plus what the engine's sparse buffers already hold (reused, or
+           freed and reallocated larger) */
+        const uint64_t held = e->spk_cap * 8 + e->spc_cap * 4 + e->emit_cap * 8 + e->spdense_cap * 8 +
+                              e->fks.sorted_cap + e->fks.c64_cap + e->fks.tmp_cap + e->codes_cap * 2 +
+                              e->parts_cap * 2 + e->pidx_cap * 4;
+        const uint64_t avail = (uint64_t)fr + held;
+        const uint64_t reserve = (1ull << 30) + 12 * wins;
+        room = avail > reserve ? avail - reserve : 0;
+    }
+    /* a pass takes ~8 B per key for its list and ~9 for its processing
+       (k_kpart's row codes 4 + run words, k_repart's part streams 2-4, the
+       library sort's ~40 if a pass falls back to it: kept inside the cap) */
+    if (!cap) cap = std::max<uint64_t>(1u << 20, std::min<uint64_t>(room / 56, 1ull << 32));
+    /* the table's storage: room for every window (distinct <= windows) */
+    {
+        int rc = sp_ensure((void **)&e->d_spk, &e->spk_cap, wins + 1, 8);
+        if (!rc) rc = sp_ensure((void **)&e->d_spc, &e->spc_cap, wins + 1, 4);
+        if (rc) return rc;
+    }
+    /* all windows in one pass (the feed counted them): no histogram launch,
+       the keys pass collects the short walks.  Not k = 17: its passes span
+       2^32 keys, which sp_count_runs32 counts instead of sorting */
+    const bool single = wins <= cap && k != 17;
+
+    const bool tail = !e->state.hdr && seq >= 1 && seq < k;
+    const bool nodes = e->opts.want_nodes != 0;
+    uint64_t scap = std::max<uint64_t>(1024, e->keep_len / 64);
+    DevScratch shorts, found;
+    uint64_t ns = 0;
+    /* the collected short walks (+ the input's last run, shorter than k:
+       :1059-1062 at EOF), distinct, with their found flags */
+    auto prep_shorts = [&]() -> int {
+        if (tail) {
+            const uint64_t v = SP_SHORT | ((uint64_t)seq << 40) | fk_sigma(e->state.code & ((1ull << (2 * seq)) - 1));
+            HIPCHK(hipMemcpyAsync(shorts.as<uint64_t>() + ns, &v, sizeof v, hipMemcpyHostToDevice, e->stream));
+            HIPCHK(hipStreamSynchronize(e->stream));
+            ns++;
+        }
+        if (!nodes) ns = 0;
+        if (ns > 1) {   /* nodeCounter counts distinct prefixes: drop repeated walks */
+            uint64_t nu = 0;
+            if (fks_unique(&e->fks, shorts.as<uint64_t>(), ns, e->stream, &nu)) return FK_E_HIP;
+            ns = nu;
+        }
+        if (ns) {
+            if (!found.alloc(ns * 20)) return FK_E_OOM;
+            HIPCHK(hipMemsetAsync(found.p, 0, ns * 20, e->stream));
+        }
+        return FK_OK;
+    };
+
+    struct Pass { uint32_t b0, b1; uint64_t n; bool dense; };
+    std::vector<Pass> passes;
+    if (single) {
+        passes.push_back({0, nbk, wins, false});
+    } else {
+        /* 1. bucket histogram and short walks (a second run if the list overflowed) */
+        for (int attempt = 0; attempt < 2; attempt++) {
+            if (!shorts.alloc((scap + 1) * 8)) return FK_E_OOM;
+            HIPCHK(hipMemsetAsync(bh.p, 0, (size_t)nbk * 8, e->stream));
+            HIPCHK(hipMemsetAsync(nctr, 0, 16, e->stream));
+            SpEmit em{};
+            em.mode = SP_HIST;
+            em.shift = shift;
+            em.bhist = bh.as<unsigned long long>();
+            em.nbuckets = nbk;
+            em.shorts = shorts.as<uint64_t>();
+            em.nshort = nctr + 1;
+            em.short_cap = scap;
+            int rc = sp_emit_all(e, em);
+            if (rc) return rc;
+            unsigned long long got = 0;
+            HIPCHK(hipMemcpyAsync(&got, nctr + 1, sizeof got, hipMemcpyDeviceToHost, e->stream));
+            HIPCHK(hipStreamSynchronize(e->stream));
+            ns = got;
+            if (ns <= scap) break;
+            if (attempt) return FK_E_HIP;
+            scap = ns;
+        }
+        int rc = prep_shorts();
+        if (rc) return rc;
+        std::vector<unsigned long long> hb(nbk);
+        HIPCHK(hipMemcpyAsync(hb.data(), bh.p, (size_t)nbk * 8, hipMemcpyDeviceToHost, e->stream));
+        HIPCHK(hipStreamSynchronize(e->stream));
+        /* 2. passes: [b0, b1) buckets; dense when one bucket exceeds the
+           cap.  A pass stays inside one aligned block of 2^P keys: k = 17
+           (2^34 keys), P = 32, counts 32-bit keys (half the bytes; 4 such
+           blocks, as many passes as a 10 G-base input needs anyway); k >= 18
+           takes the largest P whose blocks hold at most `cap` windows on
+           average, so that a sorted pass spans a power of two and
+           sp_sort_runs64's 2^18 parts split it evenly (a pass of 0.28 x 2^40
+           keys at k = 20 left half of them empty, and the rest twice as
+           large as one block's LDS sorts at full occupancy) */
+        uint32_t P = 2u * (uint32_t)k;
+        if (k == 17) {
+            P = 32;
+        } else if (k > 17) {
+            P = shift;
+            while (P < 2u * (uint32_t)k && (wins >> (2u * (uint32_t)k - P - 1u)) <= cap) P++;
+        }
+        for (uint32_t b = 0; b < nbk;) {
+            if (!hb[b]) { b++; continue; }
+            if (hb[b] > cap) { passes.push_back({b, b + 1, hb[b], true}); b++; continue; }
+            uint32_t b1 = b;
+            uint64_t n = 0;
+            while (b1 < nbk && hb[b1] <= cap && n + hb[b1] <= cap && (b1 >> (P - shift)) == (b >> (P - shift)))
+                n += hb[b1++];
+            passes.push_back({b, b1, n, false});
+            b = b1;
+        }
+    }
+
+    /* 3. the passes.  Consecutive sorted or counted passes share one walk
+       (up to SP_MAXP key ranges, their lists side by side in d_emit) as
+       far as their lists fit beside one pass's processing */
+    uint64_t prev_last = 0;
+    bool have_prev = false;
+    std::vector<unsigned long long> edges(24, 0);   /* prefix histogram across pass boundaries */
+    const uint64_t list_room = room > 9 * cap ? room - 9 * cap : 0;
+    bool solo = false;   /* a pass fell back to the library sort: one pass per walk from there on */
+    /* after a pass: its runs joined to the table (short-walk marks, the
+       prefix pair across the pass boundary) */
+    auto join = [&](uint64_t *out_k, uint64_t nw) -> int {
+        if (!nw) return FK_OK;
+        if (e->sp_distinct + nw > e->spk_cap) return FK_E_HIP;   /* cannot happen: distinct <= windows */
+        if (ns && fks_short_mark(out_k, nw, shorts.as<uint64_t>(), ns, k, found.as<uint8_t>(), e->stream))
+            return FK_E_HIP;
+        uint64_t fl[2];
+        HIPCHK(hipMemcpyAsync(&fl[0], out_k, 8, hipMemcpyDeviceToHost, e->stream));
+        HIPCHK(hipMemcpyAsync(&fl[1], out_k + (nw - 1), 8, hipMemcpyDeviceToHost, e->stream));
+        HIPCHK(hipStreamSynchronize(e->stream));
+        if (have_prev) {   /* the adjacent pair across the boundary: first differing base */
+            const uint64_t diff = fl[0] ^ prev_last;
+            const int lz = __builtin_clzll(diff) - (64 - 2 * k);
+            edges[lz / 2 + 1]++;
+        }
+        prev_last = fl[1];
+        have_prev = true;
+        e->sp_distinct += nw;
+        return FK_OK;
+    };
+    for (size_t pi = 0; pi < passes.size();) {
+        const Pass &p0 = passes[pi];
+        uint64_t *out_k = e->d_spk + e->sp_distinct;   /* this pass's runs follow the earlier ones' */
+        uint32_t *out_c = e->d_spc + e->sp_distinct;
+        if (p0.dense) {
+            SpEmit em{};
+            em.shift = shift;
+            em.lo = (uint64_t)p0.b0 << shift;
+            em.hi = (uint64_t)p0.b1 << shift;
+            uint64_t nw = 0;
+            const uint64_t nd = 1ull << shift;
+            int rc = sp_ensure((void **)&e->d_spdense, &e->spdense_cap, nd, 8);
+            if (rc) return rc;
+            HIPCHK(hipMemsetAsync(e->d_spdense, 0, nd * 8, e->stream));
+            em.mode = SP_DENSE;
+            em.dense = e->d_spdense;
+            rc = sp_emit_all(e, em);
+            if (rc) return rc;
+            if (fks_dense_runs(&e->fks, em.dense, nd, em.lo, k, e->stream, dacc, out_k, out_c, &nw)) return FK_E_HIP;
+            rc = join(out_k, nw);
+            if (rc) return rc;
+            pi++;
+            continue;
+        }
+        /* the group: its lists' offsets (16-B aligned) in d_emit */
+        size_t pj = pi;
+        uint64_t bytes = 0, offs[SP_MAXP];
+        while (pj < passes.size() && !passes[pj].dense && pj - pi < (solo ? 1u : SP_MAXP)) {
+            const uint64_t span = (uint64_t)(passes[pj].b1 - passes[pj].b0) << shift;
+            const uint64_t need = (((passes[pj].n + pad_max) * (span <= (1ull << 32) ? 4u : 8u)) + 15) & ~15ull;
+            if (pj > pi && bytes + need > list_room) break;
+            offs[pj - pi] = bytes;
+            bytes += need;
+            pj++;
+        }
+        {
+            int rc = sp_ensure((void **)&e->d_emit, &e->emit_cap, bytes / 8 + 2, 8);
+            if (rc) return rc;
+        }
+        SpEmit em{};
+        em.shift = shift;
+        em.mode = SP_KEYS;
+        em.np = (uint32_t)(pj - pi);
+        for (uint32_t q = 0; q < SP_MAXP; q++) em.ps[q].lo = ~0ull;
+        em.gend = (uint64_t)passes[pj - 1].b1 << shift;
+        unsigned long long *pc = pctr.as<unsigned long long>();
+        for (uint32_t q = 0; q < em.np; q++) {
+            const Pass &ps = passes[pi + q];
+            SpPass &sp = em.ps[q];
+            sp.lo = (uint64_t)ps.b0 << shift;
+            sp.hi = (uint64_t)ps.b1 << shift;
+            uint8_t *base = reinterpret_cast<uint8_t *>(e->d_emit) + offs[q];
+            const bool rel32 = sp.hi - sp.lo <= (1ull << 32);
+            sp.out = rel32 ? nullptr : reinterpret_cast<uint64_t *>(base);
+            sp.out32 = rel32 ? reinterpret_cast<uint32_t *>(base) : nullptr;
+            sp.cap = ps.n + pad_max;
+            sp.ctr = pc + 2 * q;
+        }
+        unsigned long long got[2 * SP_MAXP] = {};
+        for (int attempt = 0; attempt < 2; attempt++) {
+            if (single && !shorts.alloc((scap + 1) * 8)) return FK_E_OOM;
+            HIPCHK(hipMemsetAsync(nctr, 0, 24, e->stream));
+            HIPCHK(hipMemsetAsync(pc, 0, 2 * SP_MAXP * sizeof(unsigned long long), e->stream));
+            em.shorts = single ? shorts.as<uint64_t>() : nullptr;   /* the single pass collects them */
+            em.nshort = nctr + 1;
+            em.short_cap = scap;
+            int rc = sp_emit_all(e, em);
+            if (rc) return rc;
+            unsigned long long nsh = 0;
+            HIPCHK(hipMemcpyAsync(got, pc, 2 * SP_MAXP * sizeof(unsigned long long), hipMemcpyDeviceToHost, e->stream));
+            HIPCHK(hipMemcpyAsync(&nsh, nctr + 1, sizeof nsh, hipMemcpyDeviceToHost, e->stream));
+            HIPCHK(hipStreamSynchronize(e->stream));
+            if (!single || nsh <= scap) {
+                if (single) ns = nsh;
+                break;
+            }
+            if (attempt) return FK_E_HIP;
+            scap = nsh;
+        }
+        if (single) {
+            int rc = prep_shorts();
+            if (rc) return rc;
+        }
+        for (uint32_t q = 0; q < em.np; q++) {
+            const Pass &ps = passes[pi + q];
+            const SpPass &sp = em.ps[q];
+            const uint64_t claimed = got[2 * q], real = got[2 * q + 1];
+            /* the feed's (or the histogram's) count and the walk agree, and
+               the claimed slots (windows + pads) fit */
+            if (real != ps.n || claimed > sp.cap) return FK_E_HIP;
+            uint64_t *ok = e->d_spk + e->sp_distinct;
+            uint32_t *oc = e->d_spc + e->sp_distinct;
+            uint64_t nw = 0;
+            bool lib = false;
+            if (sp.out32) {   /* counted, not sorted (sp_count_runs32) */
+                int rc = sp_count_runs32(e, sp.out32, claimed, sp.lo, claimed - real, dacc, ok, oc, &nw);
+                if (rc) return rc;
+            } else {          /* partitioned and sorted in LDS (sp_sort_runs64) */
+                int rc = sp_sort_runs64(e, sp.out, claimed, sp.lo, sp.hi, claimed - real, dacc, ok, oc, &nw, &lib);
+                if (rc) return rc;
+            }
+            /* a part or bucket past k_kp_sort's sizes: the library sort,
+               which needs the room the group's other lists hold: walk this
+               pass again alone */
+            if (lib && em.np > 1) {
+                solo = true;
+                pj = pi + q;
+                break;
+            }
+            if (lib && fks_sort_runs(&e->fks, sp.out, claimed, k, e->stream, dacc, ok, oc, &nw, claimed - real))
+                return FK_E_HIP;
+            int rc = join(ok, nw);
+            if (rc) return rc;
+        }
+        pi = pj;
+    }
+
+    /* 4. totals: statistics, rollover, nodeCounter */
+    unsigned long long r[FKS_ACC_N];
+    HIPCHK(hipMemcpyAsync(r, dacc, sizeof r, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    for (int q = 0; q < 10; q++) e->sp_tstat[q] = r[q];
+    e->sp_roll = r[FKS_ACC_ROLL];
+    if (nodes) {
+        unsigned long long left = 0;
+        if (ns && fks_short_count(&e->fks, shorts.as<uint64_t>(), ns, found.as<uint8_t>(), e->stream, &left))
+            return FK_E_HIP;
+        if (e->sp_distinct || ns) {
+            unsigned long long nd = 0;
+            if (e->sp_distinct) {
+                unsigned long long run = 1;
+                for (int d = 1; d <= k; d++) {
+                    run += r[FKS_ACC_WPREFIX + d] + edges[d];
+                    nd += run;
+                }
+            }
+            e->sp_nodes = 1 + nd + left;
+        }
+    }
+    return FK_OK;
+}
+
+
+int sparse_copy(fk_engine *e, uint64_t *keys, uint32_t *counts, uint64_t cap, uint64_t *n,
+                       hipMemcpyKind kind) {
+    if (!e || !n) return FK_E_INVALID;
+    if (!e->sparse || !e->sp_done) return FK_E_STATE;
+    *n = e->sp_distinct;
+    if (!keys && !counts) return FK_OK;
+    if (cap < e->sp_distinct) return FK_E_INVALID;
+    int rc = set_dev(e);
+    if (rc) return rc;
+    if (e->sp_distinct) {
+        if (keys) HIPCHK(hipMemcpyAsync(keys, e->d_spk, e->sp_distinct * sizeof(uint64_t), kind, e->stream));
+        if (counts) HIPCHK(hipMemcpyAsync(counts, e->d_spc, e->sp_distinct * sizeof(uint32_t), kind, e->stream));
+    }
+    HIPCHK(hipStreamSynchronize(e->stream));
+    return FK_OK;
+}
+
+/* The sparse table (17 <= k <= 20) after fk_engine_finish: the distinct
+   k-mer indices (reference order, ascending = CSV row order) and their u32
+   frequencies.  keys/counts may be NULL to ask for *n only. */
+extern "C" int fk_engine_sparse(fk_engine *e, uint64_t *keys, uint32_t *counts, uint64_t cap, uint64_t *n) {
+    return sparse_copy(e, keys, counts, cap, n, hipMemcpyDeviceToHost);
+}
+
+/* The same into device buffers (the multi-GPU exchange's send buffers). */
+extern "C" int fk_engine_sparse_device(fk_engine *e, uint64_t *keys, uint32_t *counts, uint64_t cap, uint64_t *n) {
+    return sparse_copy(e, keys, counts, cap, n, hipMemcpyDeviceToDevice);
+}
+
+/* first index of the ascending device keys[0, n) with key >= want (binary
+   search, one key per probe) */
+int sparse_lower_bound(fk_engine *e, uint64_t want, uint64_t *at) {
+    uint64_t lo = 0, hi = e->sp_distinct;
+    while (lo < hi) {
+        const uint64_t mid = (lo + hi) / 2;
+        uint64_t v = 0;
+        HIPCHK(hipMemcpyAsync(&v, e->d_spk + mid, 8, hipMemcpyDeviceToHost, e->stream));
+        HIPCHK(hipStreamSynchronize(e->stream));
+        if (v < want) lo = mid + 1;
+        else hi = mid;
+    }
+    *at = lo;
+    return FK_OK;
+}
+
+/* The runs of the finished sparse table whose keys fall in [key_lo, key_hi)
+   (a contiguous piece of it: CSV rows key_lo.. in order), to host memory:
+   *n receives their number, min(cap, n) are copied (keys/counts may be
+   NULL to ask for *n). */
+extern "C" int fk_engine_sparse_range(fk_engine *e, uint64_t key_lo, uint64_t key_hi, uint64_t *keys,
+                                      uint32_t *counts, uint64_t cap, uint64_t *n) {
+    if (!e || !n || key_hi < key_lo) return FK_E_INVALID;
+    if (!e->sparse || !e->sp_done) return FK_E_STATE;
+    int rc = set_dev(e);
+    if (rc) return rc;
+    uint64_t a = 0, b = 0;
+    if ((rc = sparse_lower_bound(e, key_lo, &a)) || (rc = sparse_lower_bound(e, key_hi, &b))) return rc;
+    *n = b - a;
+    const uint64_t m = std::min(cap, b - a);
+    if (m && keys) HIPCHK(hipMemcpyAsync(keys, e->d_spk + a, m * sizeof(uint64_t), hipMemcpyDeviceToHost, e->stream));
+    if (m && counts)
+        HIPCHK(hipMemcpyAsync(counts, e->d_spc + a, m * sizeof(uint32_t), hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    return FK_OK;
+}
+
+/* The finished sparse table's runs per owner rank: owner of index x is
+   x / S, S = ceil(4^k / world) (fk_merge_layout's slices). */
+extern "C" int fk_engine_sparse_split(fk_engine *e, int world, uint64_t *counts) {
+    if (!e || !counts || world < 1) return FK_E_INVALID;
+    if (!e->sparse || !e->sp_done) return FK_E_STATE;
+    int rc = set_dev(e);
+    if (rc) return rc;
+    const uint64_t nb = 1ull << (2 * e->k), S = (nb + (uint64_t)world - 1) / (uint64_t)world;
+    for (int r = 0; r < world; r++) counts[r] = 0;
+    const uint64_t n = e->sp_distinct;
+    if (!n) return FK_OK;
+    /* the keys are ascending: owners' runs are contiguous; the boundaries by
+       binary search over the device keys, one key per probe */
+    const uint64_t *keys = e->d_spk;
+    uint64_t first = 0, last = 0;
+    HIPCHK(hipMemcpyAsync(&first, keys, 8, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipMemcpyAsync(&last, keys + (n - 1), 8, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    const int r0 = (int)(first / S), r1 = (int)(last / S);
+    uint64_t at = 0;
+    for (int r = r0; r <= r1; r++) {
+        uint64_t lo = at, hi = n;   /* first index with key >= (r + 1) * S */
+        if (r == r1) {
+            lo = n;
+        } else {
+            const uint64_t want = (uint64_t)(r + 1) * S;
+            while (lo < hi) {
+                const uint64_t mid = (lo + hi) / 2;
+                uint64_t v = 0;
+                HIPCHK(hipMemcpyAsync(&v, keys + mid, 8, hipMemcpyDeviceToHost, e->stream));
+                HIPCHK(hipStreamSynchronize(e->stream));
+                if (v < want) lo = mid + 1;
+                else hi = mid;
+            }
+        }
+        counts[r] = lo - at;
+        at = lo;
+    }
+    return FK_OK;
+}
+
+/* Replace the finished sparse table by the runs this rank owns after the
+   exchange (keys/counts: device, any order, a key possibly from several
+   ranks): counts of a key summed, stats[0] = distinct k-mers, stats[1] = the
+   sum of their u32 counts (short of the windows when a sum wrapped: the
+   rollover check). */
+extern "C" int fk_engine_sparse_adopt(fk_engine *e, const uint64_t *keys, const uint32_t *counts, uint64_t n,
+                                      uint64_t *stats) {
+    if (!e || !stats || (n && (!keys || !counts))) return FK_E_INVALID;
+    if (!e->sparse || !e->sp_done) return FK_E_STATE;
+    int rc = set_dev(e);
+    if (rc) return rc;
+    DevScratch acc;
+    if (!acc.alloc(FKS_ACC_N * sizeof(unsigned long long))) return FK_E_OOM;
+    HIPCHK(hipMemsetAsync(acc.p, 0, FKS_ACC_N * sizeof(unsigned long long), e->stream));
+    rc = sp_ensure((void **)&e->d_spk, &e->spk_cap, n + 1, 8);
+    if (!rc) rc = sp_ensure((void **)&e->d_spc, &e->spc_cap, n + 1, 4);
+    if (rc) return rc;
+    uint64_t nw = 0;
+    e->sp_distinct = 0;
+    if (fks_merge_runs(&e->fks, keys, counts, n, e->k, e->stream, acc.as<unsigned long long>(), e->d_spk, e->d_spc,
+                       &nw))
+        return FK_E_HIP;
+    unsigned long long r[FKS_ACC_N];
+    HIPCHK(hipMemcpyAsync(r, acc.p, sizeof r, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    e->sp_distinct = nw;
+    memcpy(e->sp_tstat, r, sizeof e->sp_tstat);
+    e->sp_roll = r[FKS_ACC_ROLL];
+    stats[0] = r[0];
+    stats[1] = r[1];
+    return FK_OK;
+}

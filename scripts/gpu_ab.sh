@@ -1,4 +1,4 @@
-# A/B of experiment builds (tools/exp_variant.py, exp_macro.py, exp_rev.py)
+# A/B of experiment builds (tools/exp_variant.py, exp_rev.py)
 # against the product on one box, interleaved: VARIANTS="a b" [ROUNDS=n]
 # [WORK="k:line:bases ..."] (default: the bench's headline, configs[2])
 set -o pipefail

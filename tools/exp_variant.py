@@ -1,6 +1,9 @@
 """Experiment builds (never the product): the engine with named source
 patches, as build/exp/libfk_<name>.so for an A/B run through FINDKMER_LIB
-(bench.py and findkmer_amd load it instead of the product library).
+(bench.py and findkmer_amd load it instead of the product library).  Each
+patch applies to whichever source file of findkmer_amd/csrc holds its text.
+The ablations of the sparse passes (round 5: no key stores, no counting, no
+look-back, no output, no sort) live here, not as #ifdefs in the product.
 
 usage: python3 tools/exp_variant.py NAME [NAME ...]    (run `make` first)
 
@@ -13,7 +16,7 @@ import subprocess
 import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-SRC = os.path.join(REPO, "findkmer_amd", "csrc", "fk_engine.hip")
+CSRC = os.path.join(REPO, "findkmer_amd", "csrc")
 OUT = os.path.join(REPO, "build", "exp")
 
 VARIANTS = {
@@ -148,28 +151,72 @@ VARIANTS = {
         ("                    codes[p < n1 ? (uint64_t)d1 + p : (uint64_t)d2 + (p - n1)] = x;",
          "                    if (x.x == 0x12345678u && x.y == 0x9abcdef0u) codes[p < n1 ? (uint64_t)d1 + p : (uint64_t)d2 + (p - n1)] = x;"),
     ],
+    # sparse passes (round 5 ablations, timing only): k_sp_emit without its
+    # key stores; k_kp_count without counting; the chained scan's look-back
+    # skipped; no run output; k_kp_sort without sorting
+    "spx_nostore": [
+        ("            if (at < em.ps[i].cap) {", "            if (at < em.ps[i].cap && v == ~0ull - 1) {"),
+        ("                if (at < ps.cap) {", "                if (at < ps.cap && v == ~0ull - 1) {"),
+    ],
+    "kpx_nocnt": [
+        ("                if (hsel < 0) atomicAdd(&bins[b >> 1], 1u << ((b & 1u) << 4));",
+         "                if (hsel < -1) atomicAdd(&bins[b >> 1], 1u << ((b & 1u) << 4));"),
+        ("        if (sa != (unsigned long long)m.n) {", "        if (sa == ~0ull) {"),
+    ],
+    "kpx_nolb": [
+        ("        const unsigned long long pre = chain_prefix(flags, blk, total, err);\n        if (lane == 0) {\n            bprefix = pre;\n            if (!total) fl[2 * (size_t)blk] = KP_EMPTY;\n        }\n    }\n    /* the nearest",
+         "        const unsigned long long pre = 0;\n        if (lane == 0) {\n            bprefix = pre;\n            if (!total) fl[2 * (size_t)blk] = KP_EMPTY;\n        }\n    }\n    /* the nearest"),
+    ],
+    "kpx_noout": [
+        ("        for (uint32_t i = t; i < nr; i += 1024u) {\n            __builtin_nontemporal_store(",
+         "        for (uint32_t i = t; i < nr && total == ~0u; i += 1024u) {\n            __builtin_nontemporal_store("),
+    ],
+    "kpx_nosort": [
+        ("        if (nb > 1u && nb <= 16u) {", "        if (nb > 1u && nb <= 16u && nb == 99u) {"),
+        ("        if (nb <= 64) wave_sort_bucket<1>(keys + b0, nb);", "        if (nb != 99u) continue;\n        if (nb <= 64) wave_sort_bucket<1>(keys + b0, nb);"),
+    ],
 }
 
 
-def build(name):
-    src = open(SRC).read()
-    for part in name.split("+"):
-        for old, new in VARIANTS[part]:
-            assert src.count(old) == 1, (part, old[:80])
-            src = src.replace(old, new)
-    os.makedirs(OUT, exist_ok=True)
-    dst = os.path.join(OUT, f"fk_engine_{name}.hip")
-    open(dst, "w").write(src)
-    inc = ["-I" + os.path.join(REPO, "include"), "-I" + os.path.join(REPO, "findkmer_amd", "csrc")]
+ENGINE_TUS = ("fk_engine", "fk_scan", "fk_part", "fk_part_pipe", "fk_part_res", "fk_sparse_pass", "fk_exchange")
+
+
+def build_tree(name, files):
+    """compile the engine's translation units from `files` ({file name:
+    text}, every file of findkmer_amd/csrc) into build/exp/libfk_<name>.so,
+    linked with the working tree's other objects (sparse, ingest, comm,
+    writer: run `make` first)"""
+    d = os.path.join(OUT, name)
+    os.makedirs(d, exist_ok=True)
+    for fn, text in files.items():
+        open(os.path.join(d, fn), "w").write(text)
+    inc = ["-I" + os.path.join(REPO, "include"), "-I" + d]
     flags = ["--offload-arch=gfx950", "-O3", "-fPIC", "-std=c++17", "-munsafe-fp-atomics", "-Wno-unused-value"]
-    obj = os.path.join(OUT, f"{name}.o")
-    subprocess.run(["/opt/rocm/bin/hipcc", *flags, *inc, "-c", "-x", "hip", dst, "-o", obj], check=True)
+    procs = [subprocess.Popen(["/opt/rocm/bin/hipcc", *flags, *inc, "-c", "-x", "hip", os.path.join(d, t + ".hip"),
+                               "-o", os.path.join(d, t + ".o")]) for t in ENGINE_TUS]
+    assert all(p.wait() == 0 for p in procs), "compile failed"
     b = os.path.join(REPO, "build")
     lib = os.path.join(OUT, f"libfk_{name}.so")
-    subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-shared", "-fPIC", "-o", lib, obj] +
+    subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-shared", "-fPIC", "-o", lib] +
+                   [os.path.join(d, t + ".o") for t in ENGINE_TUS] +
                    [os.path.join(b, f) for f in ("fk_sparse.o", "fk_ingest.o", "fk_comm.o", "fk_writer.o")] +
                    ["-lpthread", "-ldl"], check=True)
     print("built", lib)
+
+
+def sources():
+    return {fn: open(os.path.join(CSRC, fn)).read() for fn in os.listdir(CSRC)
+            if fn.endswith((".hip", ".h"))}
+
+
+def build(name):
+    files = sources()
+    for part in name.split("+"):
+        for old, new in VARIANTS[part]:
+            hits = [fn for fn, text in files.items() if old in text]
+            assert len(hits) == 1 and files[hits[0]].count(old) == 1, (part, old[:80], hits)
+            files[hits[0]] = files[hits[0]].replace(old, new)
+    build_tree(name, files)
 
 
 if __name__ == "__main__":
