@@ -174,8 +174,9 @@ def cpu_baseline(k, seed, fasta_line, n_sample):
 
 def cpu_baseline_multicore(k, seed, fasta_line, n_sample):
     """BASELINE.md's "fast CPU": the oracle's dense-table scan split over the
-    host threads this process may use (fko_count_dense_par, 16 on the GPU
-    box), on a bounded prefix of the same stream, input in host memory."""
+    host threads this process may use (fko_count_dense_par; oracle.host_threads:
+    its CPU affinity capped by the cgroup quota), on a bounded prefix of the
+    same stream, input in host memory."""
     sys.path.insert(0, os.path.join(REPO, "tests"))
     import oracle
     data = oracle.synth(n_sample, seed, fasta_line)
@@ -190,7 +191,8 @@ def cpu_baseline_multicore(k, seed, fasta_line, n_sample):
     except Exception:
         pass
     return {"value": n_sample / dt, "unit": "bases/s", "cores": th, "kind": "port",
-            "sample": f"fko_count_dense_par (dense u32 table, {th} threads) on the first {n_sample} bases "
+            "sample": f"fko_count_dense_par (dense u32 table, {th} threads = this process's CPU affinity "
+                      f"capped by its cgroup CPU quota) on the first {n_sample} bases "
                       f"of the same stream, k={k}; host CPU {cpu}, os.cpu_count()={os.cpu_count()}",
             "seconds": round(dt, 3)}
 

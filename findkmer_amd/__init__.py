@@ -28,6 +28,8 @@ FK_E_EMPTY = -6
 FK_E_UNTERMINATED_HEADER = -7
 FK_E_ROLLOVER = -8
 FK_E_STATE = -9
+FK_E_IO = -10
+FK_E_RCCL = -11
 FK_E_SUMMARY = -12
 FK_E_INTERNAL = -13
 FK_K_MAX_DENSE = 16
@@ -133,6 +135,7 @@ SIGNATURES = [
                                               _U64P]),
     ("fk_engine_sparse_split", ctypes.c_int, [_P, ctypes.c_int, _U64P]),
     ("fk_engine_sparse_adopt", ctypes.c_int, [_P, _P, _P, ctypes.c_uint64, _U64P]),
+    ("fk_engine_sparse_exchange", ctypes.c_int, [_P, _P, ctypes.c_int, _P, _U64P]),
     ("fk_count", ctypes.c_int, [_P, ctypes.c_uint64, ctypes.c_int, ctypes.POINTER(FkOpts), _U32P, ctypes.POINTER(FkResult)]),
     ("fk_count_multi", ctypes.c_int, [_P, ctypes.c_uint64, ctypes.c_int, ctypes.c_int, ctypes.POINTER(FkOpts), _U32P, ctypes.POINTER(FkResult)]),
     ("fk_synth_device", ctypes.c_int, [_P, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int, _P, _U64P]),
@@ -386,6 +389,16 @@ class Engine:
         n = ctypes.c_uint64()
         _check(lib().fk_engine_sparse_device(self.h, keys_ptr, counts_ptr, cap, ctypes.byref(n)), "sparse_device")
         return n.value
+
+    def sparse_exchange(self, comm, counting, limbs_ptr):
+        """fk_engine_sparse_exchange: the sparse tables merged to their
+        owners over `comm` (a Comm), the counter limbs at limbs_ptr (device
+        int32) completed with this slice's (total, distinct) and all-reduced.
+        Returns (distinct, total) of this rank's slice."""
+        st = (ctypes.c_uint64 * 2)()
+        _check(lib().fk_engine_sparse_exchange(self.h, comm.h, 1 if counting else 0, limbs_ptr, st),
+               "sparse_exchange")
+        return int(st[0]), int(st[1])
 
     def sparse_adopt(self, keys_ptr, counts_ptr, n):
         """replace the sparse table by the runs received in the exchange

@@ -357,7 +357,7 @@ extern "C" void fk_engine_destroy(fk_engine *e) {
     hipFree(e->d_table); hipFree(e->d_short); hipFree(e->d_sub); hipFree(e->d_snap);
     hipFree(e->d_pairs);
     hipFree(e->d_parts); hipFree(e->d_pmeta); hipFree(e->d_glist); hipFree(e->d_fz);
-    hipFree(e->d_rsend); hipFree(e->d_rrecv); hipFree(e->d_raux);
+    hipFree(e->d_rsend); hipFree(e->d_rrecv); hipFree(e->d_raux); hipFree(e->d_rsz);
     hipFree(e->d_codes); hipFree(e->d_pidx); hipFree(e->d_pflag); hipFree(e->d_acc); hipFree(e->d_res); hipFree(e->d_tmp);
     hipFree(e->d_state); hipFree(e->d_rr); hipFree(e->d_rtrue);
     hipFree(e->d_redo); hipFree(e->d_tf); hipFree(e->d_stage); hipFree(e->d_resume);

@@ -86,9 +86,12 @@ struct fk_engine {
     uint64_t rsend_cap = 0, rrecv_cap = 0, rsend_words = 0;
     void *d_raux = nullptr;                   /* ... their per-destination geometry and slot offsets */
     uint64_t raux_cap = 0;
-    int route_mode = 1;                       /* FINDKMER_TUNE route: 0 = reduce-scatter the table, 1 = route it
-                                                 when world > 1 (at world 1 the reduce-scatter is a local copy,
-                                                 ~11 ms less per k = 16 step), 2 = route at any world (tests) */
+    int32_t *d_rsz = nullptr;                 /* ... the world x world blob-size matrix (16-bit limbs) */
+    uint64_t rsz_cap = 0;
+    int route_mode = 0;                       /* FINDKMER_TUNE route: 0 = reduce-scatter the table (default: the
+                                                 routed send/recv has not run at world > 1 on hardware, ADVICE
+                                                 r5), 1 = route it when world > 1 (at world 1 the reduce-scatter
+                                                 is a local copy), 2 = route at any world (tests) */
     uint64_t pair_cap = 0;
     uint32_t w16_ks = W16_KS_DEFAULT;         /* k (bits) counted through k_bucket16 (FINDKMER_TUNE w16=mask) */
     int part_pairs_kmax = 12;                 /* pairs mode for k <= this (FINDKMER_TUNE pairs_kmax; k = 12 pairs:

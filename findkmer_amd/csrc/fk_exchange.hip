@@ -217,11 +217,20 @@ __global__ void k_slice_limbs(const unsigned long long *in2, int32_t *limbs8) {
  *   [4, 4 + P_d)     entries per slot of d (P_d slots: its parts)
  *   [.., + E_d)      entries, slot by slot: (bin offset in the part << 17) | count
  *   [.., + 2 O_d)    overflow pairs (bin - d S, count): counts >= 2^17 - 1
+ *   [.., + 2)        trailer: RT_MAGIC, the sum of the words before it
  */
 #define RT_SH 15u
 #define RT_ESC 0x1FFFFu
 #define RT_HDR 4u
 #define RT_STAT_SLOTS 512u
+/* every blob ends in a trailer {RT_MAGIC, sum of the blob's other words mod
+   2^32}: the owner checks it before trusting what it counted (a
+   transfer that delivers only part of a blob would otherwise go unnoticed,
+   and a receive buffer reused across steps would even hide it behind the
+   previous step's identical blob).  The trailer words of the receive
+   buffer are cleared before the transfer. */
+#define RT_TRL 2u
+#define RT_MAGIC 0x52544231u   /* "RTB1" */
 
 /* per-destination arrays in one device buffer (u64 each, world W):
    p0 [0,W) first part, sb [W, 2W+1) first slot, np [2W+1, 3W+1) parts,
@@ -240,6 +249,7 @@ struct RouteGeo {
     __device__ __forceinline__ unsigned long long *no() const { return aux + 5 * world + 1; }
     __device__ __forceinline__ unsigned long long *oc() const { return aux + 6 * world + 1; }
     __device__ __forceinline__ unsigned long long *off() const { return aux + 7 * world + 1; }
+    uint32_t *ck;          /* per destination: the blob's word sum so far (k_route_write) */
 };
 
 /* a part's owner(s): d0 and, when the part crosses d0's end b, d0 + 1 */
@@ -337,6 +347,7 @@ k_route_write(const uint32_t *table, RouteGeo g, int counting, const uint32_t *c
         const unsigned long long e = g.ne()[t], o = g.no()[t];
         uint32_t *h = send + g.bb()[t];
         h[0] = (uint32_t)e; h[1] = (uint32_t)(e >> 32); h[2] = (uint32_t)o; h[3] = (uint32_t)(o >> 32);
+        atomicAdd(&g.ck[t], h[0] + h[1] + h[2] + h[3]);
     }
     const uint64_t x0 = (uint64_t)p << RT_SH;
     uint32_t d0;
@@ -347,7 +358,11 @@ k_route_write(const uint32_t *table, RouteGeo g, int counting, const uint32_t *c
     const uint64_t s0 = g.sb()[d0] + p - g.p0()[d0], s1 = g.sb()[d1] + p - g.p0()[d1];
     if (t == 0) {
         send[g.bb()[d0] + RT_HDR + (s0 - g.sb()[d0])] = cnt[s0];
-        if (two) send[g.bb()[d1] + RT_HDR + (s1 - g.sb()[d1])] = cnt[s1];
+        atomicAdd(&g.ck[d0], cnt[s0]);
+        if (two) {
+            send[g.bb()[d1] + RT_HDR + (s1 - g.sb()[d1])] = cnt[s1];
+            atomicAdd(&g.ck[d1], cnt[s1]);
+        }
     }
     if (!counting) return;
     constexpr uint32_t QW = (1u << RT_SH) / 4u;   /* bins per wave */
@@ -356,6 +371,7 @@ k_route_write(const uint32_t *table, RouteGeo g, int counting, const uint32_t *c
     for (uint32_t w = 0; w < wv; w++) { pos0 += wc[(size_t)p * 8u + w * 2u]; pos1 += wc[(size_t)p * 8u + w * 2u + 1u]; }
     uint32_t *e0 = send + g.bb()[d0] + RT_HDR + g.np()[d0], *e1 = send + g.bb()[d1] + RT_HDR + g.np()[d1];
     const unsigned long long lt = (1ull << lane) - 1ull;
+    uint32_t ck0 = 0, ck1 = 0;   /* this lane's words into each blob */
     for (uint32_t i0 = 0; i0 < QW; i0 += 64u) {
         const uint32_t i = i0 + lane;
         const uint32_t v = tw[i];
@@ -374,8 +390,26 @@ k_route_write(const uint32_t *table, RouteGeo g, int counting, const uint32_t *c
             op[0] = (uint32_t)(x - (uint64_t)d * g.S);
             op[1] = v;
         }
+        const uint32_t w = (nz ? ent : 0u) + (v >= RT_ESC ? (uint32_t)(x - (uint64_t)(hi ? d1 : d0) * g.S) + v : 0u);
+        if (hi) ck1 += w;
+        else ck0 += w;
         pos0 += __popcll(m0);
         pos1 += __popcll(m1);
+    }
+    ck0 = wsum32(ck0);
+    ck1 = wsum32(ck1);
+    if (lane == 0) {
+        if (ck0) atomicAdd(&g.ck[d0], ck0);
+        if (ck1) atomicAdd(&g.ck[d1], ck1);
+    }
+}
+
+/* each blob's trailer, once k_route_write has summed its words */
+__global__ void __launch_bounds__(64) k_route_seal(RouteGeo g, uint32_t *send) {
+    for (uint32_t d = threadIdx.x; d < g.world; d += 64u) {
+        uint32_t *tr = send + g.bb()[d] + RT_HDR + g.np()[d] + g.ne()[d] + 2 * g.no()[d];
+        tr[0] = RT_MAGIC;
+        tr[1] = g.ck[d];
     }
 }
 
@@ -384,7 +418,8 @@ k_route_write(const uint32_t *table, RouteGeo g, int counting, const uint32_t *c
    (written, not added: the slice holds nothing before) */
 __global__ void __launch_bounds__(1024)
 k_route_absorb(const uint32_t *recv, const unsigned long long *rd, const unsigned long long *roff, uint32_t world,
-               uint32_t np, uint64_t p0, uint64_t lo, uint64_t hi, uint32_t *out, unsigned long long *stats) {
+               uint32_t np, uint64_t p0, uint64_t lo, uint64_t hi, uint32_t *out, unsigned long long *stats,
+               uint32_t *vck) {
     extern __shared__ uint32_t bins[];
     const uint32_t j = blockIdx.x, t = threadIdx.x;
     for (uint32_t i = t; i < (1u << RT_SH) / 4u; i += 1024u) reinterpret_cast<uint4 *>(bins)[i] = make_uint4(0, 0, 0, 0);
@@ -393,10 +428,14 @@ k_route_absorb(const uint32_t *recv, const unsigned long long *rd, const unsigne
         const uint32_t *blob = recv + rd[s];
         const uint32_t n = blob[RT_HDR + j];
         const uint32_t *ent = blob + RT_HDR + np + roff[(uint64_t)s * (np + 1) + j];
+        uint32_t ck = t == 0 ? n : 0u;   /* (the slot's count word, read here) */
         for (uint32_t i = t; i < n; i += 1024u) {
             const uint32_t e = ent[i];
+            ck += e;
             atomicAdd(&bins[e >> 17], e & RT_ESC);
         }
+        ck = wsum32(ck);
+        if ((t & 63) == 0 && ck) atomicAdd(&vck[s], ck);
     }
     __syncthreads();
     const uint64_t x0 = (p0 + j) << RT_SH;
@@ -428,6 +467,19 @@ k_route_absorb(const uint32_t *recv, const unsigned long long *rd, const unsigne
     }
 }
 
+/* every source's trailer against the sum of the words the owner read
+   (k_route_absorb, k_route_overflow): bad[0] = 1 on any mismatch */
+__global__ void __launch_bounds__(64)
+k_route_verify(const uint32_t *recv, const unsigned long long *rd, uint32_t np, const uint32_t *vck, uint32_t world,
+               uint32_t *bad) {
+    for (uint32_t s = threadIdx.x; s < world; s += 64u) {
+        const uint32_t *blob = recv + rd[s];
+        const uint64_t ne = blob[0] | ((uint64_t)blob[1] << 32), no = blob[2] | ((uint64_t)blob[3] << 32);
+        const uint32_t *tr = blob + RT_HDR + np + ne + 2 * no;
+        if (tr[0] != RT_MAGIC || tr[1] != vck[s]) atomicOr(bad, 1u);
+    }
+}
+
 __global__ void __launch_bounds__(256) k_route_stats(const unsigned long long *slots, unsigned long long *out2) {
     unsigned long long a = 0, b = 0;
     for (uint32_t i = threadIdx.x; i < RT_STAT_SLOTS; i += 256u) { a += slots[2 * i]; b += slots[2 * i + 1]; }
@@ -442,10 +494,14 @@ __global__ void __launch_bounds__(256) k_route_stats(const unsigned long long *s
 /* every source's overflow pairs added into the slice */
 __global__ void __launch_bounds__(256)
 k_route_overflow(const uint32_t *recv, const unsigned long long *rd, uint32_t np, uint32_t *out,
-                 unsigned long long *stats) {
+                 unsigned long long *stats, uint32_t *vck) {
     const uint32_t *blob = recv + rd[blockIdx.x];
     const uint64_t ne = blob[0] | ((uint64_t)blob[1] << 32), no = blob[2] | ((uint64_t)blob[3] << 32);
     const uint32_t *op = blob + RT_HDR + np + ne;
+    uint32_t ck = threadIdx.x == 0 ? blob[0] + blob[1] + blob[2] + blob[3] : 0u;   /* (the header) */
+    for (uint64_t i = threadIdx.x; i < no; i += 256u) ck += op[2 * i] + op[2 * i + 1];
+    ck = wsum32(ck);
+    if ((threadIdx.x & 63) == 0 && ck) atomicAdd(&vck[blockIdx.x], ck);
     for (uint64_t i = threadIdx.x; i < no; i += 256u) {
         const uint32_t old = atomicAdd(&out[op[2 * i]], op[2 * i + 1]);
         if (stats) {
@@ -489,16 +545,18 @@ int route_pack(fk_engine *e, int world, bool counting, uint64_t *words) {
     const RouteHost h = route_geometry(e->nbins, world);
     if (h.S < (1ull << RT_SH)) return FK_E_INVALID;   /* (a part spans at most two owners) */
     const uint64_t W = (uint64_t)world;
-    const uint64_t naux = 7 * W + 1 + h.nslots + 1, aux_bytes = naux * 8 + h.nslots * 4 + (uint64_t)h.nparts * 32 + 16;
+    const uint64_t naux = 7 * W + 1 + h.nslots + 1,
+                   aux_bytes = naux * 8 + h.nslots * 4 + (uint64_t)h.nparts * 32 + W * 4 + 16;
     int rc = sp_ensure(&e->d_raux, &e->raux_cap, aux_bytes, 1);
     if (rc) return rc;
     unsigned long long *aux = static_cast<unsigned long long *>(e->d_raux);
-    uint32_t *cnt = reinterpret_cast<uint32_t *>(aux + naux), *wcnt = cnt + h.nslots;
+    uint32_t *cnt = reinterpret_cast<uint32_t *>(aux + naux), *wcnt = cnt + h.nslots,
+             *ck = wcnt + (uint64_t)h.nparts * 8;
     std::vector<unsigned long long> ha(7 * W + 1, 0);
     for (int d = 0; d < world; d++) { ha[d] = h.p0[d]; ha[2 * W + 1 + d] = h.np[d]; }
     for (int d = 0; d <= world; d++) ha[W + d] = h.sb[d];
     HIPCHK(hipMemcpyAsync(aux, ha.data(), ha.size() * 8, hipMemcpyHostToDevice, e->stream));
-    RouteGeo g{e->nbins, h.S, (uint32_t)world, h.nparts, aux};
+    RouteGeo g{e->nbins, h.S, (uint32_t)world, h.nparts, aux, ck};
     hipLaunchKernelGGL(k_route_count, dim3(h.nparts), dim3(256), 0, e->stream, (const uint32_t *)e->d_table, g,
                        counting ? 1 : 0, cnt, wcnt);
     HIPCHK(hipGetLastError());
@@ -512,7 +570,7 @@ int route_pack(fk_engine *e, int world, bool counting, uint64_t *words) {
     uint64_t total = 0;
     for (int d = 0; d < world; d++) {
         const uint64_t ne = off[h.sb[d + 1]] - off[h.sb[d]];
-        words[d] = RT_HDR + h.np[d] + ne + 2 * no[d];
+        words[d] = RT_HDR + h.np[d] + ne + 2 * no[d] + RT_TRL;
         ha[3 * W + 1 + d] = total;   /* bb */
         ha[4 * W + 1 + d] = ne;      /* ne */
         total += words[d];
@@ -522,9 +580,12 @@ int route_pack(fk_engine *e, int world, bool counting, uint64_t *words) {
     e->rsend_words = total;
     HIPCHK(hipMemcpyAsync(aux + 3 * W + 1, ha.data() + 3 * W + 1, 2 * W * 8, hipMemcpyHostToDevice, e->stream));
     HIPCHK(hipMemsetAsync(aux + 6 * W + 1, 0, W * 8, e->stream));
+    HIPCHK(hipMemsetAsync(ck, 0, W * 4, e->stream));
     hipLaunchKernelGGL(k_route_write, dim3(h.nparts), dim3(256), 0, e->stream, (const uint32_t *)e->d_table, g,
                        counting ? 1 : 0, (const uint32_t *)cnt, (const uint32_t *)wcnt,
                        reinterpret_cast<uint32_t *>(e->d_rsend));
+    HIPCHK(hipGetLastError());
+    hipLaunchKernelGGL(k_route_seal, dim3(1), dim3(64), 0, e->stream, g, reinterpret_cast<uint32_t *>(e->d_rsend));
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(e->stream));
     return FK_OK;
@@ -544,7 +605,7 @@ int route_absorb(fk_engine *e, int world, int rank, const int32_t *recv, const u
     uint64_t at = 0;
     for (int s = 0; s < world; s++) {
         rd[s] = at;
-        if (words[s] < RT_HDR + np) return FK_E_INVALID;
+        if (words[s] < RT_HDR + np + RT_TRL) return FK_E_INVALID;
         at += words[s];
     }
     /* every blob's header against its size */
@@ -555,13 +616,15 @@ int route_absorb(fk_engine *e, int world, int rank, const int32_t *recv, const u
     for (int s = 0; s < world; s++) {
         const uint64_t ne = hdr[4 * s] | ((uint64_t)hdr[4 * s + 1] << 32),
                        no = hdr[4 * s + 2] | ((uint64_t)hdr[4 * s + 3] << 32);
-        if (RT_HDR + np + ne + 2 * no != words[s]) return FK_E_INVALID;
+        if (RT_HDR + np + ne + 2 * no + RT_TRL != words[s]) return FK_E_RCCL;   /* (a header that does not fit) */
     }
-    const uint64_t aux_bytes = (W + W * (np + 1) + 2 * RT_STAT_SLOTS) * 8 + 16;
+    const uint64_t aux_bytes = (W + W * (np + 1) + 2 * RT_STAT_SLOTS) * 8 + W * 4 + 16;
     int rc = sp_ensure(&e->d_raux, &e->raux_cap, aux_bytes, 1);
     if (rc) return rc;
     unsigned long long *drd = static_cast<unsigned long long *>(e->d_raux), *roff = drd + W,
                        *sslots = roff + W * (np + 1);
+    uint32_t *vck = reinterpret_cast<uint32_t *>(sslots + 2 * RT_STAT_SLOTS), *bad = vck + W;
+    HIPCHK(hipMemsetAsync(vck, 0, W * 4 + 4, e->stream));
     if (stats) HIPCHK(hipMemsetAsync(sslots, 0, 2 * RT_STAT_SLOTS * 8, e->stream));
     HIPCHK(hipMemcpyAsync(drd, rd.data(), W * 8, hipMemcpyHostToDevice, e->stream));
     const uint32_t *r32 = reinterpret_cast<const uint32_t *>(recv);
@@ -575,17 +638,22 @@ int route_absorb(fk_engine *e, int world, int rank, const int32_t *recv, const u
     uint32_t *out = reinterpret_cast<uint32_t *>(slice);
     hipLaunchKernelGGL(k_route_absorb, dim3((uint32_t)np), dim3(1024), (size_t)1 << 17, e->stream, r32,
                        (const unsigned long long *)drd, (const unsigned long long *)roff, (uint32_t)world, (uint32_t)np,
-                       (uint64_t)h.p0[rank], lo, hi, out, stats ? sslots : nullptr);
+                       (uint64_t)h.p0[rank], lo, hi, out, stats ? sslots : nullptr, vck);
     HIPCHK(hipGetLastError());
     hipLaunchKernelGGL(k_route_overflow, dim3((uint32_t)world), dim3(256), 0, e->stream, r32,
-                       (const unsigned long long *)drd, (uint32_t)np, out, stats);
+                       (const unsigned long long *)drd, (uint32_t)np, out, stats, vck);
+    HIPCHK(hipGetLastError());
+    hipLaunchKernelGGL(k_route_verify, dim3(1), dim3(64), 0, e->stream, r32, (const unsigned long long *)drd,
+                       (uint32_t)np, (const uint32_t *)vck, (uint32_t)world, bad);
     HIPCHK(hipGetLastError());
     if (stats) {
         hipLaunchKernelGGL(k_route_stats, dim3(1), dim3(256), 0, e->stream, (const unsigned long long *)sslots, stats);
         HIPCHK(hipGetLastError());
     }
+    uint32_t hbad = 0;
+    HIPCHK(hipMemcpyAsync(&hbad, bad, 4, hipMemcpyDeviceToHost, e->stream));
     HIPCHK(hipStreamSynchronize(e->stream));
-    return FK_OK;
+    return hbad ? FK_E_RCCL : FK_OK;   /* a blob arrived short or corrupt */
 }
 
 extern "C" int fk_engine_route_pack(fk_engine *e, int world, int counting, uint64_t *words) {
@@ -621,16 +689,18 @@ int route_exchange(fk_engine *e, fk_comm *comm, bool counting, int32_t *slice, u
     std::vector<uint64_t> sw(W), rw(W), sd(W), rdsp(W);
     int rc = route_pack(e, world, counting, sw.data());
     if (rc) return rc;
-    DevScratch m;
+    /* the size matrix in the engine's own buffer (a scratch allocation's
+       hipFree synchronised the device inside the step) */
     const uint64_t nm = W * W * 3;
-    if (!m.alloc(nm * 4)) return FK_E_OOM;
+    rc = sp_ensure((void **)&e->d_rsz, &e->rsz_cap, nm, sizeof(int32_t));
+    if (rc) return rc;
     std::vector<int32_t> hm(nm, 0);
     for (uint64_t d = 0; d < W; d++)
         for (int j = 0; j < 3; j++) hm[((uint64_t)rank * W + d) * 3 + j] = (int32_t)((sw[d] >> (16 * j)) & 0xFFFFu);
-    HIPCHK(hipMemcpyAsync(m.p, hm.data(), nm * 4, hipMemcpyHostToDevice, e->stream));
-    rc = fkc_allreduce_i32(comm, m.as<int32_t>(), nm, e->stream);
+    HIPCHK(hipMemcpyAsync(e->d_rsz, hm.data(), nm * 4, hipMemcpyHostToDevice, e->stream));
+    rc = fkc_allreduce_i32(comm, e->d_rsz, nm, e->stream);
     if (rc) return rc;
-    HIPCHK(hipMemcpyAsync(hm.data(), m.p, nm * 4, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipMemcpyAsync(hm.data(), e->d_rsz, nm * 4, hipMemcpyDeviceToHost, e->stream));
     HIPCHK(hipStreamSynchronize(e->stream));
     uint64_t sat = 0, rat = 0;
     for (uint64_t s = 0; s < W; s++) {
@@ -644,6 +714,10 @@ int route_exchange(fk_engine *e, fk_comm *comm, bool counting, int32_t *slice, u
     }
     rc = sp_ensure((void **)&e->d_rrecv, &e->rrecv_cap, rat, sizeof(int32_t));
     if (rc) return rc;
+    /* the trailers cleared: each must arrive with its blob */
+    for (uint64_t s = 0; s < W; s++)
+        if (rw[s] >= RT_TRL)
+            HIPCHK(hipMemsetAsync(e->d_rrecv + rdsp[s] + rw[s] - RT_TRL, 0, RT_TRL * sizeof(int32_t), e->stream));
     rc = fkc_alltoallv_i32(comm, e->d_rsend, sw.data(), sd.data(), e->d_rrecv, rw.data(), rdsp.data(), e->stream);
     if (rc) return rc;
     return route_absorb(e, world, rank, e->d_rrecv, rw.data(), slice, stats);
@@ -841,5 +915,82 @@ extern "C" int fk_shard_rows_compose(const uint32_t *rows, int world, int rank, 
     entering->code = fk_sigma(mine.code);
     entering->hdr = mine.hdr;
     entering->ended = 0;
+    return FK_OK;
+}
+
+/* 17 <= k <= 20 over the library's communicator (round 6; the all-to-all
+ * had gone through torch.distributed, a stream gap per collective): this
+ * rank's finished sparse table cut at the owners' bounds (each owner's runs
+ * are contiguous: the keys ascend), the world x world run counts all-reduced
+ * as 16-bit limbs, the keys (two words each) and the counts sent to their
+ * owners by grouped ncclSend / ncclRecv (a rank's own runs by a device copy),
+ * the received sorted runs merged (fk_engine_sparse_adopt: merge path,
+ * equal keys summed), then the caller's counter limbs -- `limbs`, device,
+ * FK_PACK_COUNTERS x 4 16-bit limbs already in place -- completed with the
+ * slice's (total, distinct) and all-reduced, all on the engine's stream.
+ * counting = 0: a rank the stream never reached (sends nothing). */
+extern "C" int fk_engine_sparse_exchange(fk_engine *e, fk_comm *comm, int counting, int32_t *limbs,
+                                         uint64_t *stats) {
+    if (!e || !comm || !limbs || !stats) return FK_E_INVALID;
+    if (!e->sparse || !e->sp_done) return FK_E_STATE;
+    if (fkc_device(comm) != e->dev) return FK_E_INVALID;
+    if (!fkc_has_alltoallv(comm)) return FK_E_RCCL;
+    const int world = fkc_world(comm), rank = fkc_rank(comm);
+    const uint64_t W = (uint64_t)world;
+    int rc = set_dev(e);
+    if (rc) return rc;
+    std::vector<uint64_t> cnt(W, 0), rw(W), sd(W), rdsp(W), w2(W), sd2(W), rw2(W), rdsp2(W);
+    if (counting) {
+        rc = fk_engine_sparse_split(e, world, cnt.data());
+        if (rc) return rc;
+    }
+    const uint64_t nm = W * W * 4;
+    rc = sp_ensure((void **)&e->d_rsz, &e->rsz_cap, nm, sizeof(int32_t));
+    if (rc) return rc;
+    std::vector<int32_t> hm(nm, 0);
+    for (uint64_t d = 0; d < W; d++)
+        for (int j = 0; j < 4; j++) hm[((uint64_t)rank * W + d) * 4 + j] = (int32_t)((cnt[d] >> (16 * j)) & 0xFFFFu);
+    HIPCHK(hipMemcpyAsync(e->d_rsz, hm.data(), nm * 4, hipMemcpyHostToDevice, e->stream));
+    rc = fkc_allreduce_i32(comm, e->d_rsz, nm, e->stream);
+    if (rc) return rc;
+    HIPCHK(hipMemcpyAsync(hm.data(), e->d_rsz, nm * 4, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    uint64_t m = 0, at = 0;
+    for (uint64_t s = 0; s < W; s++) {
+        uint64_t v = 0;
+        for (int j = 0; j < 4; j++) v |= (uint64_t)(uint32_t)hm[(s * W + (uint64_t)rank) * 4 + j] << (16 * j);
+        rw[s] = v;
+        rdsp[s] = m;
+        m += v;
+        sd[s] = at;
+        at += cnt[s];
+        w2[s] = 2 * cnt[s]; sd2[s] = 2 * sd[s]; rw2[s] = 2 * rw[s]; rdsp2[s] = 2 * rdsp[s];
+    }
+    rc = sp_ensure((void **)&e->d_rrecv, &e->rrecv_cap, 3 * m + 2, sizeof(int32_t));
+    if (rc) return rc;
+    int32_t *rk = e->d_rrecv, *rcnt = e->d_rrecv + 2 * m;
+    rc = fkc_alltoallv_i32(comm, reinterpret_cast<const int32_t *>(e->d_spk), w2.data(), sd2.data(), rk, rw2.data(),
+                           rdsp2.data(), e->stream);
+    if (!rc) rc = fkc_alltoallv_i32(comm, reinterpret_cast<const int32_t *>(e->d_spc), cnt.data(), sd.data(), rcnt,
+                                    rw.data(), rdsp.data(), e->stream);
+    if (rc) return rc;
+    /* (the table the sends read is replaced next: let them finish first) */
+    HIPCHK(hipStreamSynchronize(e->stream));
+    uint64_t st[2] = {0, 0};
+    rc = fk_engine_sparse_adopt(e, reinterpret_cast<const uint64_t *>(rk), reinterpret_cast<const uint32_t *>(rcnt), m,
+                                st);
+    if (rc) return rc;
+    /* the slice's (total, distinct) as limbs after the counters' */
+    int32_t sl[FK_PACK_STATS];
+    for (int j = 0; j < 4; j++) {
+        sl[j] = (int32_t)((st[1] >> (16 * j)) & 0xFFFFu);
+        sl[4 + j] = (int32_t)((st[0] >> (16 * j)) & 0xFFFFu);
+    }
+    HIPCHK(hipMemcpyAsync(limbs + 4 * FK_PACK_COUNTERS, sl, sizeof sl, hipMemcpyHostToDevice, e->stream));
+    rc = fkc_allreduce_i32(comm, limbs, 4 * FK_PACK_COUNTERS + FK_PACK_STATS, e->stream);
+    if (rc) return rc;
+    HIPCHK(hipStreamSynchronize(e->stream));
+    stats[0] = st[0];
+    stats[1] = st[1];
     return FK_OK;
 }

@@ -469,13 +469,20 @@ k_kpart(const KT *keys, uint64_t n, PartGeo pg, uint64_t lo, uint64_t hi, uint32
    calls it): this block's `total` published (status A: aggregate), the
    earlier blocks' sum found by looking back 64 flags at a time -- up to the
    nearest one with status P (inclusive prefix) -- and this block's own
-   inclusive prefix published.  Returns the exclusive prefix.  Every earlier
-   block was dispatched before this one and publishes unconditionally; the
-   spin bound only guards a broken invariant (FK_FAULT_PARTS: the pass fails
-   with FK_E_INTERNAL instead of hanging the GPU).  The flags are relaxed
+   inclusive prefix published.  Returns the exclusive prefix.  Parts are
+   taken by start-order tickets, so every earlier part is already running
+   and publishes unconditionally: a wait only lasts as long as a slow
+   predecessor (a part holding one k-mer's billions of windows, counted
+   twice over for its 16-bit wrap, takes seconds).  The bound is wall-clock
+   (s_memrealtime, 100 MHz), CHAIN_WAIT_S seconds since this block started
+   waiting -- far past any valid part -- and only guards a broken invariant
+   (FK_FAULT_PARTS: the pass fails with FK_E_INTERNAL instead of hanging the
+   GPU).  (Round 5 bounded it by 2^22 spin iterations, which a slow but
+   valid predecessor could exceed.)  The flags are relaxed
    agent-scope atomics: a flag word carries all a reader needs (status and
    value in one 64-bit access), and a release store would write back this
    XCD's whole L2 -- the parts' output just written -- once per part. */
+#define CHAIN_WAIT_S 60ull
 __device__ unsigned long long chain_prefix(unsigned long long *flags, uint32_t blk, uint32_t total,
                                            unsigned long long *err) {
     const uint32_t lane = threadIdx.x & 63;
@@ -487,7 +494,7 @@ __device__ unsigned long long chain_prefix(unsigned long long *flags, uint32_t b
     if (lane == 0) __hip_atomic_store(&flags[blk], A | total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     unsigned long long pre = 0;
     int64_t j = (int64_t)blk - 1;
-    uint64_t spin = 0;
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     for (;;) {
         const int64_t idx = j - (int64_t)lane;
         unsigned long long f = idx >= 0 ? __hip_atomic_load(&flags[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : P;
@@ -497,7 +504,7 @@ __device__ unsigned long long chain_prefix(unsigned long long *flags, uint32_t b
             const unsigned long long pm0 = __ballot((f >> 62) == 2);
             const unsigned long long need = pm0 ? (pm0 & (~pm0 + 1)) * 2 - 1 : ~0ull;   /* lanes 0 .. first P */
             if (!(__ballot((f >> 62) == 0) & need)) break;
-            if (++spin > (1ull << 22)) {
+            if (__builtin_amdgcn_s_memrealtime() - t0 > CHAIN_WAIT_S * 100000000ull) {
                 if (lane == 0) atomicOr(err, (unsigned long long)FK_FAULT_PARTS);
                 return pre;
             }

@@ -61,6 +61,7 @@ work.  Otherwise every rank sees the same failure and runs steps 1-2 above.
 The same functions run over RCCL (backend "nccl", device tensors, bench.py)
 and over gloo on the CPU (tests/test_dist_cpu.py, with a model engine).
 """
+import os
 import torch
 import torch.distributed as dist
 
@@ -615,7 +616,19 @@ def count_sharded(engine, ptr, nbytes, halo, buf, group=None, times=None, pinned
         if counting:
             vals = [r.windows, r.valid_bases, *r.base_count, *r.depth1, r.unknown_chars, r.scanned_bytes,
                     1 if rank == first_end else 0, r.unterminated_header if rank == last else 0]
-        res = _sparse_merge(engine, vals, counting, rank, world, group, first_end, r)
+        scomm = None
+        if native and hasattr(engine, "sparse_exchange") and dist.get_backend(group) == "nccl":
+            scomm = native_comm(group)
+        if scomm is not None:
+            # over RCCL: the all-to-all of runs, their merge and the counter
+            # all-reduce inside the library, on the engine's stream
+            limbs = torch.zeros(COUNTER_SLOTS + STAT_SLOTS, dtype=torch.int32, device="cuda")
+            _put_counters(limbs, vals, None, 0)
+            engine.sparse_exchange(scomm, counting, limbs.data_ptr())
+            res = SparseShardedResult(limbs.cpu(), engine.k, rank, first_end, r, world, group, engine)
+            res.transport = "rccl-native"
+        else:
+            res = _sparse_merge(engine, vals, counting, rank, world, group, first_end, r)
         if times is not None:
             times["count"] = times.get("count", 0.0) + (t1 - t0)
             times["stitch"] = times.get("stitch", 0.0) + (t2 - t1)
@@ -625,7 +638,7 @@ def count_sharded(engine, ptr, nbytes, halo, buf, group=None, times=None, pinned
     # k >= FK_ROUTE_KMIN over gloo: each owner gets only the nonzero bins of
     # its slice (fk_engine_route_*), not the whole table
     route = shard_table and k >= FK_ROUTE_KMIN and hasattr(engine, "route_pack") and \
-        dist.get_backend(group) != "nccl" and torch.cuda.is_available()
+        dist.get_backend(group) != "nccl" and torch.cuda.is_available() and route_mode() >= 1
     if counting:
         if route:
             pass
@@ -657,6 +670,18 @@ def count_sharded(engine, ptr, nbytes, halo, buf, group=None, times=None, pinned
     return ShardedResult(buf, k, rank, first_end, r, world=world, sharded=shard_table, group=group)
 
 
+def route_mode():
+    """FINDKMER_TUNE route (the library's knob, fk_engine_create): 0 (the
+    default) = the sharded table is reduce-scattered, 1 / 2 = routed (the
+    nonzero bins of each owner's slice) -- so the gloo rehearsal takes the
+    path the library's RCCL exchange takes."""
+    for item in os.environ.get("FINDKMER_TUNE", "").split(","):
+        name, _, val = item.partition("=")
+        if name == "route" and val.isdigit():
+            return min(int(val), 2)
+    return 0
+
+
 def _route_tables(engine, buf, k, rank, world, group, counting):
     """The routed sharded merge over torch.distributed (gloo): every rank's
     blobs (fk_engine_route_pack: the nonzero bins of each owner's slice) go
@@ -673,6 +698,10 @@ def _route_tables(engine, buf, k, rank, world, group, counting):
     dist.all_to_all_single(rsz, torch.tensor(words, dtype=torch.int64, device=coll), group=group)
     rwords = [int(v) for v in rsz.tolist()]
     recv = torch.empty(sum(rwords), dtype=torch.int32, device=coll)
+    at = 0
+    for w in rwords:   # each blob's trailer must arrive with it (fk_engine_route_absorb checks it)
+        at += w
+        recv[max(0, at - 2):at] = 0
     dist.all_to_all_single(recv, send[:sum(words)].to(coll), rwords, words, group=group)
     lo = rank * S
     n = max(0, min(S, nb - lo))

@@ -265,10 +265,14 @@ int  fk_comm_available(int device);
 int  fk_engine_shard_exchange(fk_engine *e, fk_comm *comm, int32_t *merge, int32_t *info /* [2], may be NULL */);
 
 /* Routed sharded tables (round 5): for k >= FK_ROUTE_KMIN the stitched
- * exchange with FK_XCHG_SHARD_TABLE sends each owner only the nonzero bins of
- * its range instead of reduce-scattering the whole table, when world > 1
- * (FINDKMER_TUNE route=0: never, route=2: at world 1 too; an RCCL without
- * ncclSend/ncclRecv reduce-scatters).
+ * exchange with FK_XCHG_SHARD_TABLE can send each owner only the nonzero bins
+ * of its range instead of reduce-scattering the whole table: FINDKMER_TUNE
+ * route=1 at world > 1, route=2 at world 1 too.  The default (route=0) is the
+ * reduce-scatter until the grouped ncclSend/ncclRecv has run at world > 1 on
+ * hardware (round 6); an RCCL without ncclSend/ncclRecv always reduce-scatters.
+ * Every blob ends in a trailer (a magic word and the sum of its other words,
+ * mod 2^32) that the owner checks: a blob that arrived short or corrupt makes
+ * the exchange (and fk_engine_route_absorb) fail with FK_E_RCCL.
  * The same steps for a caller-driven transport (the gloo rehearsal):
  *  - fk_engine_route_pack: after fk_engine_finish, the finished table's blobs
  *    for owners 0..world-1 (words[d] int32 each, side by side; counting == 0:
@@ -348,6 +352,18 @@ int  fk_engine_sparse_device(fk_engine *e, uint64_t *keys, uint32_t *counts, uin
 int  fk_engine_sparse_split(fk_engine *e, int world, uint64_t *counts);
 int  fk_engine_sparse_adopt(fk_engine *e, const uint64_t *keys, const uint32_t *counts, uint64_t n,
                             uint64_t *stats /* [2] */);
+/* The same merge over the library's communicator (round 6): this rank's
+ * finished table cut at the owners' bounds, sent to its owners (grouped
+ * ncclSend / ncclRecv, sizes as a world x world matrix of 16-bit limbs in
+ * one all-reduce), the received runs adopted, then `limbs` (device, the
+ * FK_PACK_COUNTERS counters as 4 16-bit limbs each, filled by the caller)
+ * completed with this slice's (total, distinct) limbs (FK_PACK_STATS) and
+ * all-reduced -- every collective on the engine's stream.  stats[0] =
+ * distinct k-mers of this rank's slice, stats[1] = the sum of their u32
+ * counts.  counting = 0: this rank sends nothing (a rank after the shard
+ * that ended the stream).  Collective: every rank of comm calls it.
+ * Replaces no reference call (the reference is single-threaded). */
+int  fk_engine_sparse_exchange(fk_engine *e, fk_comm *comm, int counting, int32_t *limbs, uint64_t *stats /* [2] */);
 
 /* One-shot convenience: count a whole buffer on one device. */
 int  fk_count(const uint8_t *buf, uint64_t len, int k, const fk_opts *opts,

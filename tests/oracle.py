@@ -71,9 +71,30 @@ def _buf(data):
 
 
 def host_threads():
-    """Threads for the oracle on this host: the GPU box gives a process 16
-    CPUs although os.cpu_count() shows the whole machine's."""
-    return max(1, min(16, os.cpu_count() or 1))
+    """Threads for the oracle on this host, measured: the CPUs this process
+    may run on (sched_getaffinity), capped by the cgroup's CPU quota
+    (cpu.max, cgroup v2; cpu.cfs_quota_us / cfs_period_us, v1) where one is
+    set -- os.cpu_count() shows the whole machine's CPUs on the GPU box."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        n = os.cpu_count() or 1
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = int(q) / int(per)
+    except (OSError, ValueError):
+        try:
+            q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+            per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+            if q > 0:
+                quota = q / per
+        except (OSError, ValueError):
+            pass
+    if quota is not None:
+        n = min(n, max(1, int(quota)))
+    return max(1, n)
 
 
 def count_dense(data, k, unknown_cap=0, threads=1):

@@ -139,16 +139,23 @@ def test_rccl_single_rank_merge(k, fast, eof_in, native):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("k,world,eof_in,nbytes", [(12, 2, -1, 3_000_000), (12, 8, 3, 3_000_000),
-                                                  (15, 3, 1, 1_500_000)])
-def test_sharded_table_gloo_against_oracle(k, world, eof_in, nbytes):
+@pytest.mark.parametrize("k,world,eof_in,nbytes,route", [(12, 2, -1, 3_000_000, 0), (12, 8, 3, 3_000_000, 0),
+                                                        (14, 8, -1, 3_000_000, 0), (15, 3, 1, 1_500_000, 1),
+                                                        (16, 2, -1, 1_500_000, 1)])
+def test_sharded_table_gloo_against_oracle(k, world, eof_in, nbytes, route, monkeypatch):
     """k > 11: the merged table sharded over the ranks by its top index bits
     (rank r owns bins [r*4^k/G, (r+1)*4^k/G): the north star's "table shards
     by top bits"), gathered in rank order on rank 0 == the oracle's table
     (k = 14, 16: its sparse form); the counters, total and distinct bins
-    from the all-reduced limbs.  eof_in >= 0 at k = 15: the shards after the
-    0xFF byte were counted into fresh tables and are then discarded (the
-    statistics that count left must not reach finish)"""
+    from the all-reduced limbs.  k = 14 over 8 ranks: k_bucket16's fresh
+    tables reduced.  route = 1 (k = 15, 16; FINDKMER_TUNE route=1): the
+    routed exchange end to end (fk_engine_route_pack, all_to_all_single,
+    fk_engine_route_absorb with its trailer check) instead of the table
+    reduction.  eof_in >= 0 at k = 15: the shards after the 0xFF byte were
+    counted into fresh tables and are then discarded (the statistics that
+    count left must not reach finish)"""
+    if route:
+        monkeypatch.setenv("FINDKMER_TUNE", f"route={route}")
     out = _torchrun(world, 29750 + k + world + eof_in, os.path.join(REPO, "tests", "dist_worker.py"),
                     ["--k", str(k), "--eof-in", str(eof_in), "--shard-table", "1", "--bytes", str(nbytes)])
     assert out["table_equal"] and out["sharded"]
@@ -192,11 +199,14 @@ def test_sparse_tables_all_to_all_against_oracle(k, world, eof_in, backend):
     owners' bounds, one all-to-all to the owners, the owner's sum on the GPU
     (fk_engine_sparse_adopt); the owners' slices gathered in rank order ==
     the oracle's sparse table, every merged counter exact.  nccl: world 1
-    over RCCL (the all-to-all with device buffers)"""
+    over RCCL through the library's communicator (fk_engine_sparse_exchange:
+    the run counts, keys and counts by grouped send/recv, the merge, the
+    counter all-reduce, on the engine's stream)"""
     out = _torchrun(world, 29900 + k + 3 * world + eof_in + (50 if backend == "nccl" else 0),
                     os.path.join(REPO, "tests", "dist_worker.py"),
                     ["--k", str(k), "--eof-in", str(eof_in), "--bytes", "2000000", "--backend", backend])
     assert out["table_equal"] and out["sharded"]
+    assert out["transport"] == ("rccl-native" if backend == "nccl" else "torch")
     for key in ("windows", "valid_bases", "base_count", "depth1", "unknown_chars", "scanned_bytes",
                 "hit_eof_byte", "unterminated_header", "distinct"):
         assert out[key][0] == out[key][1], (key, out[key])
@@ -274,6 +284,22 @@ def test_routed_table_blobs_against_the_summed_tables(k, world):
             engines[r].route_absorb(world, r, recv.data_ptr(), rw, got[r * S:].data_ptr())
         assert torch.equal(got[:nb], want)
         assert int(want.max()) >= (1 << 17)   # an overflow pair was needed
+        # a blob that arrives short (its trailer cleared, as the exchange
+        # clears the receive buffer's) or with one word changed is refused
+        for damage in ("short", "word"):
+            parts, rw = [], []
+            for s in range(world):
+                off = sum(words[s][:0])
+                parts.append(blobs[s][off:off + words[s][0]].clone())
+                rw.append(words[s][0])
+            if damage == "short":
+                parts[0][-2:] = 0
+            else:
+                parts[0][4 + (S >> 15) // 2] += 1
+            recv = torch.cat(parts)
+            with pytest.raises(fk.FindKmerError) as ei:
+                engines[0].route_absorb(world, 0, recv.data_ptr(), rw, got.data_ptr())
+            assert ei.value.code == fk.FK_E_RCCL, damage
     finally:
         for e in engines:
             e.close()

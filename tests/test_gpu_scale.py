@@ -194,3 +194,44 @@ def test_upstream_10g_sweep_vs_oracle(upstream10g, k):
     rc, r_g, t_g, ub_g = _engine_dense(k, buf.data_ptr(), size)
     r_o = _assert_dense_equal(k, host, rc, r_g, t_g, ub_g)
     assert r_o.windows > 0.98 * (N10G // fk.FK_UPSTREAM_REC) * (1001 - k + 1) * 0.99
+
+
+@pytest.mark.parametrize("k", [17, 20])
+def test_sparse_low_complexity_2g_vs_oracle(k):
+    """17 <= k <= 20 on skewed input: a 2 G-base
+    low-complexity stream -- 1 G bases of poly-A, then 1 G bases of an
+    (ACGTT)n repeat -- puts ~half of all windows on one key and the rest on
+    five, so one sparse part holds a billion windows of one k-mer (k = 17:
+    k_kp_count's 16-bit bins wrap and the part is counted again in 32-bit
+    halves, while the chained scan's later parts wait on it; k = 20: the part
+    is past k_kp_sort's LDS and the pass takes the library sort).  The
+    distinct keys come from the oracle over a short stream with the same
+    junction; their counts over the whole stream from the oracle's threaded
+    scan (fko_count_sparse_range) -- the engine's whole table must equal them
+    key for key, with every counter."""
+    import torch
+    half = 1_000_000_000
+    dev = torch.device("cuda", 0)
+    buf = torch.empty(2 * half + 64, dtype=torch.uint8, device=dev)
+    buf[:half] = ord("A")
+    buf[half:2 * half] = torch.tensor(list(b"ACGTT"), dtype=torch.uint8, device=dev).repeat(half // 5)
+    torch.cuda.synchronize()
+    size = 2 * half
+    with fk.Engine(k) as e:
+        e.feed_device(buf.data_ptr(), size)
+        rc, r = e.finish()
+        assert rc == fk.FK_OK
+        keys_g, cnts_g = e.sparse()
+    host = buf[:size].cpu().numpy()
+    del buf
+    torch.cuda.empty_cache()
+    small = b"A" * 1000 + b"ACGTT" * 200
+    keys_s, _, r_s = oracle.count_sparse(small, k)
+    ranges = [(int(x), int(x) + 1) for x in sorted(keys_s)]
+    keys_o, cnts_o, r_o = oracle.count_sparse_range(host, k, ranges, threads=oracle.host_threads())
+    assert len(keys_o) == len(keys_s) == r.distinct
+    assert np.array_equal(np.asarray(keys_g, dtype=np.uint64), keys_o)
+    assert np.array_equal(np.asarray(cnts_g, dtype=np.uint32), cnts_o)
+    assert int(cnts_o.max()) > half - k   # the poly-A k-mer
+    assert (r.windows, r.valid_bases, list(r.base_count), list(r.depth1), r.scanned_bytes) == \
+        (r_o.windows, r_o.valid_bases, list(r_o.base_count), list(r_o.depth1), r_o.scanned_bytes)

@@ -175,6 +175,22 @@ VARIANTS = {
         ("        if (nb > 1u && nb <= 16u) {", "        if (nb > 1u && nb <= 16u && nb == 99u) {"),
         ("        if (nb <= 64) wave_sort_bucket<1>(keys + b0, nb);", "        if (nb != 99u) continue;\n        if (nb <= 64) wave_sort_bucket<1>(keys + b0, nb);"),
     ],
+    # k_repart (round 6, timing only): pass A twice (its cost = the delta),
+    # no pass-B write-out, no pass B at all
+    "rp_a2": [
+        ("    /* pass A: entries per part */\n    for (uint32_t i = t; i < nitems; i += blockDim.x)\n",
+         "    /* pass A: entries per part */\n    for (uint32_t i = t; i < nitems; i += blockDim.x)\n"
+         "        each_code(i, [&](uint32_t p, uint32_t) { atomicAdd(&hc[p], 1u); });\n    __syncthreads();\n"
+         "    for (uint32_t i = t; i < nitems; i += blockDim.x)\n"),
+    ],
+    "rp_noout": [
+        ("            for (uint32_t j = lane; j < n; j += 64u) dst[j] = rbuf[o + j];",
+         "            for (uint32_t j = lane; j < n && n == 0xFFFFFFFFu; j += 64u) dst[j] = rbuf[o + j];"),
+    ],
+    "rp_nob": [
+        ("    /* pass B: rounds of whole runs (a lane per item) holding up to",
+         "    if (nitems != 0xFFFFFFFFu) return;\n    /* pass B: rounds of whole runs (a lane per item) holding up to"),
+    ],
 }
 
 
