@@ -145,12 +145,29 @@ struct PartMeta {
    slice; the wide sparse passes' 32-bit parts: REPART_METAP) */
 #define REPART_GP(OT, G) ((G) * (sizeof(OT) == 2 ? REPART_MAXP : REPART_METAP))
 #define REPART_METAP 128u     /* meta entries per coarse slice (wide sparse passes: 128 parts, G = 4) */
-#define REPART_CAP 32768u     /* entries per pass-B round: a batch (16 waves x 2048), the longest run */
-static_assert(16u * FK_TILE_BYTES <= REPART_CAP, "a C32 row's run fits one k_repart round");
+/*
+ * Round 6: span-streamed.  The block's rows are taken RP_CHUNK at a time:
+ * a lane per row reads the row's G run words (its span: the G slices' runs
+ * lie side by side in slice order) into LDS -- the span's first code, the
+ * cumulative run lengths, a block scan of the span's 16-B pieces -- and the
+ * chunk's pieces are then streamed in rounds of 1024 x PPT pieces, PPT
+ * consecutive pieces per thread (a piece's row by binary search over the
+ * scan, its slice by the cumulative lengths).  Work per round is a fixed
+ * number of codes whatever the runs' lengths: round 5's lane per run took a
+ * round per pair of 16 K-code runs on skewed input (a 1 G-base poly-A
+ * stretch: minutes in one block).  Codes of one thread that fall into the
+ * same part consecutively are counted and placed with one atomic.
+ * Pass A counts each part's entries (its stream is sized exactly, one global
+ * atomic claims the group's region); pass B counts a round by part, places
+ * it in LDS by part and writes each part's segment after its earlier rounds'.
+ */
+#define RP_CHUNK 1024u                  /* rows per chunk: a lane each */
+#define RP_NOPART 0xFFFFu
 
 /* OT = uint16_t: a code's part is its bits [15, 15 + split), stored as its
    low 15 bits (k = 15, 16; k = 17 passes, psh = 15).  OT = uint32_t (wide
-   sparse passes): part bits [psh, psh + 6), stored as the low psh bits. */
+   sparse passes): part bits [psh, psh + 7), stored as the low psh bits.
+   The rows' runs hold at most 65535 codes (C32 / k_kpart rows: 32 K). */
 template <typename OT, uint32_t G = REPART_G>
 __global__ void __launch_bounds__(1024, sizeof(OT) == 2 && G == REPART_G ? REPART_MINW : 1)
 k_repart(PartGeo pg, OT *out, unsigned long long *alloc, PartMeta *meta, uint64_t cap,
@@ -158,53 +175,144 @@ k_repart(PartGeo pg, OT *out, unsigned long long *alloc, PartMeta *meta, uint64_
     /* (G coarse slices of 2^split parts: G << split <= GP, else nothing is
        done and the pass fails -- the arrays below are sized by GP) */
     constexpr uint32_t GP = REPART_GP(OT, G);
+    /* 16-B pieces per thread and round: 4 (16 K codes, 64 a part at k =
+       16) for 16-bit parts; 8 (32 K codes, 64 a part) for the wide passes'
+       512 parts of 32-bit codes, one block per CU (with 4, or 2 and two
+       blocks per CU, their 128 / 64-B segments took the k = 20 step from
+       274 to 287 / 308 ms) */
+    constexpr uint32_t PPT = sizeof(OT) == 2 ? 4u : 8u, ROUND = 1024u * PPT;
     /* per (slice in the group, part): entries, round count / offset /
        cursor, written so far, stream start */
     __shared__ uint32_t cnt[GP], hc[GP], ho[GP], cur[GP], wr[GP];
     __shared__ unsigned long long poff[GP];
+    /* the chunk's rows: pieces before each, the span's first code in the
+       row, its cumulative run lengths after slices 0 .. G-1 */
+    __shared__ uint32_t pre[RP_CHUNK + 1], rs0[RP_CHUNK];
+    __shared__ uint16_t rcum[RP_CHUNK][G];
+    __shared__ uint32_t wsc[16];
+    __shared__ __attribute__((aligned(16))) OT rbuf[ROUND * 4u];
     if ((G << pg.split) > GP) {
         if (threadIdx.x == 0) atomicOr(err, (unsigned long long)FK_FAULT_PARTS);
         return;
     }
-    __shared__ uint32_t scn[17];
-    __shared__ __attribute__((aligned(16))) OT rbuf[REPART_CAP];
     const uint32_t pmask = (1u << psh) - 1u;
     const uint32_t t = threadIdx.x, wv = t >> 6, lane = t & 63;
     const uint32_t np = 1u << pg.split, gp = G * np;   /* parts of the block */
     const uint32_t b0 = blockIdx.x * G;                /* its first coarse slice */
-    for (uint32_t i = t; i < gp; i += blockDim.x) cnt[i] = 0;
-    __syncthreads();
+    for (uint32_t i = t; i < gp; i += blockDim.x) { cnt[i] = 0; hc[i] = 0; }
     const uint32_t nrows = pg.flag && *pg.flag ? 2u * pg.rows : pg.rows;
-    const uint32_t nitems = nrows * G;   /* (row, slice) pairs, row-major: a row's runs side by side */
-    const uint4 *g4 = reinterpret_cast<const uint4 *>(pg.codes);
-    /* item i: row i / G, slice b0 + i % G; its codes as 16-B pieces (4 each)
-       -- the G lanes of a row read one contiguous span */
-    auto each_code = [&](uint32_t i, auto &&f) {
-        const uint32_t r = i / G, sl = i % G;
-        const uint32_t e = pg.idx[(size_t)r * pg.nslices + b0 + sl];
-        if (e == PART_NO_RUN) return;
-        const uint64_t s0 = (uint64_t)r * pg.batch + (e >> 16), s1 = s0 + run_count(e);
-        const uint64_t q0 = s0 >> 2, q1 = (s1 + 3) >> 2;
-        auto piece = [&](const uint4 &v, uint64_t q) {
-            const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+    const uint4 *g4 = reinterpret_cast<const uint4 *>(pg.codes);   /* u32 codes, 4 a piece */
+    /* one chunk's rows into LDS; returns its pieces (block-uniform) */
+    auto load_chunk = [&](uint32_t c0) -> uint32_t {
+        const uint32_t r = c0 + t;
+        uint32_t npc = 0, s0 = 0, cum = 0;
+        if (r < nrows) {
+            bool have = false;
 #pragma unroll
-            for (int h = 0; h < 4; h++)
-                if (q * 4 + h >= s0 && q * 4 + h < s1) f(sl * np + (w4[h] >> psh), w4[h]);
-        };
-        /* the pieces of a run of up to 17 codes in flight together (one
-           load at a time left the kernel latency-bound) */
-        uint4 v[5];
+            for (uint32_t j = 0; j < G; j++) {
+                const uint32_t e = pg.idx[(size_t)r * pg.nslices + b0 + j];
+                const uint32_t c = run_count(e);
+                if (c && !have) { s0 = e >> 16; have = true; }
+                cum += c;
+                rcum[t][j] = (uint16_t)cum;
+            }
+            if (cum) {
+                const uint64_t a = (uint64_t)r * pg.batch + s0;
+                npc = (uint32_t)(((a + cum + 3u) >> 2) - (a >> 2));
+            }
+        }
+        rs0[t] = s0;
+        const uint32_t inc = wscan_incl32(npc);
+        if (lane == 63) wsc[wv] = inc;
+        __syncthreads();
+        uint32_t before = 0, all = 0;
 #pragma unroll
-        for (uint32_t u = 0; u < 5u; u++) v[u] = q0 + u < q1 ? g4[q0 + u] : make_uint4(0, 0, 0, 0);
-#pragma unroll
-        for (uint32_t u = 0; u < 5u; u++)
-            if (q0 + u < q1) piece(v[u], q0 + u);
-        for (uint64_t q = q0 + 5u; q < q1; q++) piece(g4[q], q);
+        for (uint32_t w = 0; w < 16u; w++) {
+            const uint32_t x = wsc[w];
+            before += w < wv ? x : 0u;
+            all += x;
+        }
+        pre[t] = before + inc - npc;
+        if (t == 0) pre[RP_CHUNK] = all;
+        __syncthreads();
+        return all;
     };
-    /* pass A: entries per part */
-    for (uint32_t i = t; i < nitems; i += blockDim.x)
-        each_code(i, [&](uint32_t p, uint32_t) { atomicAdd(&cnt[p], 1u); });
-    __syncthreads();
+    /* this thread's pieces [q, q + PPT) of the chunk (q < tot): codes and
+       their parts (RP_NOPART: outside the span).  (Round 6: pieces q0 +
+       1024 u + t instead -- a wave's loads 1 KiB contiguous -- took k = 16's
+       k_repart from 5.1 to 5.8 ms: four row searches a thread, and the
+       spans' 256 B are what a load can use either way) */
+    auto load_pieces = [&](uint32_t c0, uint32_t q, uint32_t tot, uint32_t (&code)[4 * PPT],
+                           uint32_t (&part)[4 * PPT]) {
+        /* the row holding piece q: the last row whose pieces start at or before it */
+        uint32_t lo = 0, hi = RP_CHUNK;
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (pre[mid] <= q) lo = mid;
+            else hi = mid;
+        }
+        uint32_t rr = lo;
+        uint4 v[PPT];
+        uint64_t a[PPT];
+        uint32_t rw[PPT];
+#pragma unroll
+        for (uint32_t u = 0; u < PPT; u++) {
+            const uint32_t qq = q + u;
+            if (qq < tot) {
+                while (pre[rr + 1] <= qq) rr++;
+                a[u] = (uint64_t)(c0 + rr) * pg.batch + rs0[rr];   /* the span's first code */
+                v[u] = g4[(a[u] >> 2) + (qq - pre[rr])];
+            } else {
+                a[u] = 0;
+                v[u] = make_uint4(0, 0, 0, 0);
+            }
+            rw[u] = rr;
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < PPT; u++) {
+            const uint32_t qq = q + u;
+            const uint32_t w4[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+            const uint32_t rr2 = rw[u];
+            const uint32_t span = rcum[rr2][G - 1];
+            const uint64_t pb = ((a[u] >> 2) + (qq - pre[rr2])) * 4u;   /* the piece's first code */
+#pragma unroll
+            for (uint32_t h = 0; h < 4u; h++) {
+                const int64_t off = (int64_t)(pb + h) - (int64_t)a[u];
+                uint32_t pt = RP_NOPART;
+                if (qq < tot && off >= 0 && off < (int64_t)span) {
+                    uint32_t j = 0;
+#pragma unroll
+                    for (uint32_t g = 0; g + 1 < G; g++) j += (uint32_t)off >= rcum[rr2][g];
+                    pt = j * np + (w4[h] >> psh);
+                }
+                code[4 * u + h] = w4[h];
+                part[4 * u + h] = pt;
+            }
+        }
+    };
+    /* pass A: entries per part (runs of one part in a thread's codes: one atomic) */
+    for (uint32_t c0 = 0; c0 < nrows; c0 += RP_CHUNK) {
+        const uint32_t tot = load_chunk(c0);
+        for (uint32_t q0 = 0; q0 < tot; q0 += ROUND) {
+            const uint32_t q = q0 + t * PPT;
+            if (q < tot) {
+                uint32_t code[4 * PPT], part[4 * PPT];
+                load_pieces(c0, q, tot, code, part);
+                uint32_t rp = RP_NOPART, rn = 0;
+#pragma unroll
+                for (uint32_t i = 0; i < 4 * PPT; i++) {
+                    if (part[i] != rp) {
+                        if (rn) atomicAdd(&cnt[rp], rn);
+                        rp = part[i];
+                        rn = 0;
+                    }
+                    rn += part[i] != RP_NOPART;
+                }
+                if (rn) atomicAdd(&cnt[rp], rn);
+            }
+        }
+        __syncthreads();   /* (the chunk's LDS rows are rewritten next) */
+    }
     if (t < 64) {   /* the parts' 8-aligned stream starts in the group's region */
         uint32_t carry = 0;
         for (uint32_t p0 = 0; p0 < gp; p0 += 64u) {
@@ -235,103 +343,80 @@ k_repart(PartGeo pg, OT *out, unsigned long long *alloc, PartMeta *meta, uint64_
             if (lane == 63) atomicMax(pmax, (unsigned long long)mx);
         }
     }
-    /* pass B: rounds of whole runs (a lane per item) holding up to
-       REPART_CAP entries: counted by part, placed in LDS by part, and each
-       part's segment written after the part's earlier rounds */
-    uint32_t base = 0;
     __syncthreads();
-    /* one item per lane and round, software-pipelined: the next round's
-       items are known once this round's are taken, so their index words
-       load during this round's count and their first pieces during its
-       placement and write-out (each round was a chain of an index load, a
-       code load and five barriers: k_repart latency-bound) */
-    auto idx_word = [&](uint32_t i) -> uint32_t {
-        return i < nitems ? pg.idx[(size_t)(i / G) * pg.nslices + b0 + i % G] : PART_NO_RUN;
-    };
-    auto span = [&](uint32_t i, uint32_t e, uint64_t &s0, uint64_t &s1) {
-        /* (an empty run -- PART_NO_RUN, count 0 -- reads nothing) */
-        s0 = (uint64_t)(i / G) * pg.batch + (e == PART_NO_RUN ? 0u : e >> 16);
-        s1 = s0 + run_count(e);
-    };
-    auto load5 = [&](uint64_t s0, uint64_t s1, uint4 *v) {
-        const uint64_t q0 = s0 >> 2, q1 = (s1 + 3) >> 2;
+    /* pass B: each round counted by part, placed in LDS by part, and each
+       part's segment written after its earlier rounds' */
+    for (uint32_t c0 = 0; c0 < nrows; c0 += RP_CHUNK) {
+        const uint32_t tot = load_chunk(c0);
+        for (uint32_t q0 = 0; q0 < tot; q0 += ROUND) {
+            const uint32_t q = q0 + t * PPT;
+            uint32_t code[4 * PPT], part[4 * PPT];
+            if (q < tot) {
+                load_pieces(c0, q, tot, code, part);
+            } else {
 #pragma unroll
-        for (uint32_t u = 0; u < 5u; u++) v[u] = q0 + u < q1 ? g4[q0 + u] : make_uint4(0, 0, 0, 0);
-    };
-    uint32_t ie = idx_word(base + t);
-    uint4 pv[5];
-    {
-        uint64_t a0, a1;
-        span(base + t, ie, a0, a1);
-        load5(a0, a1, pv);
-    }
-    for (;;) {
-        const uint32_t i = base + t;
-        const uint32_t c = run_count(ie);
-        const uint32_t wi = wscan_incl32(c);
-        if (lane == 63) scn[wv] = wi;
-        for (uint32_t p = t; p < gp; p += blockDim.x) hc[p] = 0;
-        __syncthreads();
-        uint32_t before = 0;
-        for (uint32_t w = 0; w < wv; w++) before += scn[w];
-        /* the leading items whose runs fit (item `base`'s always does: a
-           run holds at most one batch) */
-        const bool take = i < nitems && before + wi <= REPART_CAP;
-        const uint32_t ntake = (uint32_t)__syncthreads_count(take);
-        const uint32_t nbase = base + ntake;
-        const uint32_t ien = idx_word(nbase + t);   /* the next round's item */
-        uint64_t s0, s1;
-        span(i, take ? ie : PART_NO_RUN, s0, s1);
-        const uint32_t sl = i % G;
-        const uint64_t q0 = s0 >> 2, q1 = (s1 + 3) >> 2;
-        auto codes = [&](auto &&f) {
-            auto piece = [&](const uint4 &v, uint64_t q) {
-                const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-                for (int h = 0; h < 4; h++)
-                    if (q * 4 + h >= s0 && q * 4 + h < s1) f(sl * np + (w4[h] >> psh), w4[h]);
-            };
-#pragma unroll
-            for (uint32_t u = 0; u < 5u; u++)
-                if (q0 + u < q1) piece(pv[u], q0 + u);
-            for (uint64_t q = q0 + 5u; q < q1; q++) piece(g4[q], q);
-        };
-        codes([&](uint32_t p, uint32_t) { atomicAdd(&hc[p], 1u); });
-        __syncthreads();
-        if (t < 64) {
-            uint32_t carry = 0;
-            for (uint32_t p0 = 0; p0 < gp; p0 += 64u) {
-                const uint32_t p = p0 + lane;
-                const uint32_t n = p < gp ? hc[p] : 0u;
-                const uint32_t inc = wscan_incl32(n);
-                if (p < gp) { ho[p] = carry + inc - n; cur[p] = carry + inc - n; }
-                carry += rdlane(inc, 63);
+                for (uint32_t i = 0; i < 4 * PPT; i++) { code[i] = 0; part[i] = RP_NOPART; }
             }
+            /* count (a run of one part: one atomic) */
+            {
+                uint32_t rp = RP_NOPART, rn = 0;
+#pragma unroll
+                for (uint32_t i = 0; i < 4 * PPT; i++) {
+                    if (part[i] != rp) {
+                        if (rn) atomicAdd(&hc[rp], rn);
+                        rp = part[i];
+                        rn = 0;
+                    }
+                    rn += part[i] != RP_NOPART;
+                }
+                if (rn) atomicAdd(&hc[rp], rn);
+            }
+            __syncthreads();
+            if (t < 64) {
+                uint32_t carry = 0;
+                for (uint32_t p0 = 0; p0 < gp; p0 += 64u) {
+                    const uint32_t p = p0 + lane;
+                    const uint32_t n = p < gp ? hc[p] : 0u;
+                    const uint32_t inc = wscan_incl32(n);
+                    if (p < gp) { ho[p] = carry + inc - n; cur[p] = carry + inc - n; }
+                    carry += rdlane(inc, 63);
+                }
+            }
+            __syncthreads();
+            /* place: a run of one part takes its slots with one atomic (its
+               length from a backward pass over the thread's codes) */
+            {
+                uint32_t len[4 * PPT];
+                uint32_t follow = 0;
+#pragma unroll
+                for (int i = 4 * PPT - 1; i >= 0; i--) {
+                    const bool same = i + 1 < (int)(4 * PPT) && part[i] == part[i + 1];
+                    follow = same ? follow + 1u : 1u;
+                    len[i] = follow;
+                }
+                uint32_t at = 0;
+#pragma unroll
+                for (uint32_t i = 0; i < 4 * PPT; i++) {
+                    if (part[i] == RP_NOPART) continue;
+                    if (i == 0 || part[i] != part[i - 1]) at = atomicAdd(&cur[part[i]], len[i]);
+                    rbuf[at++] = (OT)(code[i] & pmask);
+                }
+            }
+            __syncthreads();
+            /* a wave per part: consecutive entries to consecutive slots; the
+               part's round count cleared and its written count advanced by
+               that wave alone.  (Round 6: whole aligned 16-B pieces with the
+               unaligned rest carried to the next round measured slower.) */
+            for (uint32_t p = wv; p < gp; p += 16u) {
+                const uint32_t n = hc[p], o = ho[p];
+                if (poff[p] != ~0ull) {
+                    OT *dst = out + poff[p] + wr[p];
+                    for (uint32_t j = lane; j < n; j += 64u) dst[j] = rbuf[o + j];
+                }
+                if (lane == 0) { wr[p] += n; hc[p] = 0; }
+            }
+            __syncthreads();
         }
-        __syncthreads();
-        codes([&](uint32_t p, uint32_t v) {
-            const uint32_t at = atomicAdd(&cur[p], 1u);
-            rbuf[at] = (OT)(v & pmask);
-        });
-        /* the next round's first pieces (this round's are consumed) */
-        {
-            uint64_t a0, a1;
-            span(nbase + t, ien, a0, a1);
-            load5(a0, a1, pv);
-        }
-        ie = ien;
-        __syncthreads();
-        /* a wave per part: consecutive entries to consecutive 2-B slots */
-        for (uint32_t p = wv; p < gp; p += 16u) {
-            const uint32_t n = poff[p] == ~0ull ? 0u : hc[p], o = ho[p];
-            OT *dst = out + poff[p] + wr[p];
-            for (uint32_t j = lane; j < n; j += 64u) dst[j] = rbuf[o + j];
-        }
-        __syncthreads();
-        for (uint32_t p = t; p < gp; p += blockDim.x) wr[p] += hc[p];
-        base = nbase;
-        if (base >= nitems || ntake == 0) break;
-        __syncthreads();
     }
 }
 

@@ -695,9 +695,11 @@ int launch_part(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t lo, cons
         e->d_perr = alloc + 1;
         e->perr_live = true;
         HIPCHK(hipMemsetAsync(alloc, 0, 2 * sizeof(unsigned long long), e->stream));
-        /* k = 15 (16 parts a slice): 8 slices per block, one block per CU
-           (4.27 ms per G-base against 4.68 with two blocks of 4) */
-        if (pg.split <= 4)
+        /* k = 15 (16 parts a slice) as k = 16: 4 coarse slices a block, two
+           blocks per CU.  (Round 5's lane-per-run k_repart took 8 slices a
+           block there: 4.27 ms per G-base against 4.68 with two blocks of 4;
+           the span-streamed one 5.42 with 8, 4.50 with 4.) */
+        if (pg.split <= 3)
             hipLaunchKernelGGL((k_repart<uint16_t, 8u>), dim3(pg.nslices / 8u), dim3(1024), 0, e->stream, pg,
                                e->d_parts, alloc, meta, (uint64_t)e->parts_cap, e->d_perr, 15u, nullptr);
         else

@@ -228,7 +228,11 @@ def test_sparse_low_complexity_2g_vs_oracle(k):
     small = b"A" * 1000 + b"ACGTT" * 200
     keys_s, _, r_s = oracle.count_sparse(small, k)
     ranges = [(int(x), int(x) + 1) for x in sorted(keys_s)]
-    keys_o, cnts_o, r_o = oracle.count_sparse_range(host, k, ranges, threads=oracle.host_threads())
+    got = [oracle.count_sparse_range(host, k, ranges[i:i + 8], threads=oracle.host_threads())
+           for i in range(0, len(ranges), 8)]   # (the oracle takes 8 ranges a scan)
+    keys_o = np.concatenate([g[0] for g in got])
+    cnts_o = np.concatenate([g[1] for g in got])
+    r_o = got[0][2]
     assert len(keys_o) == len(keys_s) == r.distinct
     assert np.array_equal(np.asarray(keys_g, dtype=np.uint64), keys_o)
     assert np.array_equal(np.asarray(cnts_g, dtype=np.uint32), cnts_o)

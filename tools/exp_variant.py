@@ -175,21 +175,28 @@ VARIANTS = {
         ("        if (nb > 1u && nb <= 16u) {", "        if (nb > 1u && nb <= 16u && nb == 99u) {"),
         ("        if (nb <= 64) wave_sort_bucket<1>(keys + b0, nb);", "        if (nb != 99u) continue;\n        if (nb <= 64) wave_sort_bucket<1>(keys + b0, nb);"),
     ],
-    # k_repart (round 6, timing only): pass A twice (its cost = the delta),
-    # no pass-B write-out, no pass B at all
-    "rp_a2": [
-        ("    /* pass A: entries per part */\n    for (uint32_t i = t; i < nitems; i += blockDim.x)\n",
-         "    /* pass A: entries per part */\n    for (uint32_t i = t; i < nitems; i += blockDim.x)\n"
-         "        each_code(i, [&](uint32_t p, uint32_t) { atomicAdd(&hc[p], 1u); });\n    __syncthreads();\n"
-         "    for (uint32_t i = t; i < nitems; i += blockDim.x)\n"),
+    # k_repart (round 6, span-streamed; timing only): no pass B; pass B
+    # without its write-out
+    "rp_nob": [
+        ("    /* pass B: each round counted by part,",
+         "    if (nrows != 0xFFFFFFFFu) return;\n    /* pass B: each round counted by part,"),
     ],
     "rp_noout": [
-        ("            for (uint32_t j = lane; j < n; j += 64u) dst[j] = rbuf[o + j];",
-         "            for (uint32_t j = lane; j < n && n == 0xFFFFFFFFu; j += 64u) dst[j] = rbuf[o + j];"),
+        ("                    for (uint32_t j = lane; j < n; j += 64u) dst[j] = rbuf[o + j];",
+         "                    for (uint32_t j = lane; j < n && n == 0xFFFFFFFFu; j += 64u) dst[j] = rbuf[o + j];"),
     ],
-    "rp_nob": [
-        ("    /* pass B: rounds of whole runs (a lane per item) holding up to",
-         "    if (nitems != 0xFFFFFFFFu) return;\n    /* pass B: rounds of whole runs (a lane per item) holding up to"),
+    "rpa_noatom": [
+        ("                        if (rn) atomicAdd(&cnt[rp], rn);", "                        if (rn == 0xFFFFFFu) atomicAdd(&cnt[rp], rn);"),
+        ("                if (rn) atomicAdd(&cnt[rp], rn);\n            }\n        }",
+         "                if (rn == 0xFFFFFFu) atomicAdd(&cnt[rp], rn);\n            }\n        }"),
+    ],
+    "rp_noplace": [
+        ("                    if (i == 0 || part[i] != part[i - 1]) at = atomicAdd(&cur[part[i]], len[i]);",
+         "                    if (i == 0) at = t * 16u + len[i] * 0u;"),
+    ],
+    # k = 15 through k_repart<uint16_t, 4> (two blocks per CU) instead of 8 slices a block
+    "k15g4": [
+        ("        if (pg.split <= 4)\n", "        if (pg.split <= 3)\n"),
     ],
 }
 
