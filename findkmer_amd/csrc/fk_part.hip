@@ -383,9 +383,6 @@ k_count_parts(PartGeo pg, const uint16_t *in, const PartMeta *meta, uint32_t *ta
     extern __shared__ uint32_t slice[];
     const uint32_t np = 1u << pg.split;
     const uint32_t b = blockIdx.x / np, part = blockIdx.x % np;
-    for (uint32_t i = threadIdx.x; i < (1u << 13); i += blockDim.x)
-        reinterpret_cast<uint4 *>(slice)[i] = make_uint4(0, 0, 0, 0);
-    __syncthreads();
     PartMeta m = meta[blockIdx.x];
     if (m.off + m.n > cap) {   /* bound check: a stream past the parts buffer is not read */
         if (threadIdx.x == 0) atomicOr(err, (unsigned long long)FK_FAULT_META);
@@ -394,12 +391,32 @@ k_count_parts(PartGeo pg, const uint16_t *in, const PartMeta *meta, uint32_t *ta
     }
     const uint4 *g4 = reinterpret_cast<const uint4 *>(in + m.off);   /* 16-B aligned: off % 8 == 0 */
     const uint32_t nq = (m.n + 7u) >> 3;
-    for (uint32_t q = threadIdx.x; q < nq; q += blockDim.x) {
-        const uint4 v = g4[q];
+    auto add8 = [&](const uint4 &v, uint32_t q) {
         const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
         for (int h = 0; h < 8; h++)
             if (q * 8u + (uint32_t)h < m.n) atomicAdd(&slice[(w4[h >> 1] >> (16 * (h & 1))) & 0x7FFFu], 1u);
+    };
+    /* the part's first CP_U pieces per thread (16 K codes: ~2 k = 16 parts)
+       in flight while the bins are zeroed (round 6: the stream had been
+       read one latency-bound piece at a time after the zeroing) */
+    constexpr uint32_t CP_U = 2u;
+    const uint32_t t = threadIdx.x;
+    uint4 pv[CP_U];
+#pragma unroll
+    for (uint32_t u = 0; u < CP_U; u++) pv[u] = t + u * 1024u < nq ? g4[t + u * 1024u] : make_uint4(0, 0, 0, 0);
+    for (uint32_t i = t; i < (1u << 13); i += blockDim.x)
+        reinterpret_cast<uint4 *>(slice)[i] = make_uint4(0, 0, 0, 0);
+    __syncthreads();
+#pragma unroll
+    for (uint32_t u = 0; u < CP_U; u++)
+        if (t + u * 1024u < nq) add8(pv[u], t + u * 1024u);
+    for (uint32_t q0 = t + CP_U * 1024u; q0 < nq; q0 += CP_U * 1024u) {
+#pragma unroll
+        for (uint32_t u = 0; u < CP_U; u++) pv[u] = q0 + u * 1024u < nq ? g4[q0 + u * 1024u] : make_uint4(0, 0, 0, 0);
+#pragma unroll
+        for (uint32_t u = 0; u < CP_U; u++)
+            if (q0 + u * 1024u < nq) add8(pv[u], q0 + u * 1024u);
     }
     __syncthreads();
     /* the part's bins into the table (the block owns them), eight loads in

@@ -548,7 +548,6 @@ k_kp_count(const uint16_t *in, const PartMeta *meta, uint64_t cap_in, uint64_t l
        running, and across the 8 XCDs (and other processes' kernels)
        blockIdx order is not start order */
     if (t == 0) vblk = (uint32_t)atomicAdd(&flags[nparts], 1ull);
-    for (uint32_t i = t; i < KC_WORDS / 4u; i += 1024u) reinterpret_cast<uint4 *>(bins)[i] = make_uint4(0, 0, 0, 0);
     if (t < 24) hpre[t] = 0;
     __syncthreads();
     const uint32_t blk = vblk;
@@ -562,20 +561,39 @@ k_kp_count(const uint16_t *in, const PartMeta *meta, uint64_t cap_in, uint64_t l
     const uint32_t nq = (m.n + 7u) >> 3;
     /* each code to its bin, bin b at half b & 1 of word b >> 1 (hsel: the
        32-bit pass of half h, bins [h 2^14, (h + 1) 2^14) only) */
-    auto count = [&](int hsel) {
-        for (uint32_t q = t; q < nq; q += 1024u) {
-            const uint4 v = g4[q];
-            const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+    auto count8 = [&](const uint4 &v, uint32_t q, int hsel) {
+        const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-            for (int h = 0; h < 8; h++) {
-                if (q * 8u + (uint32_t)h >= m.n) continue;
-                const uint32_t b = (w4[h >> 1] >> (16 * (h & 1))) & 0x7FFFu;
-                if (hsel < 0) atomicAdd(&bins[b >> 1], 1u << ((b & 1u) << 4));
-                else if ((b >> 14) == (uint32_t)hsel) atomicAdd(&bins[b & (KC_WORDS - 1u)], 1u);
-            }
+        for (int h = 0; h < 8; h++) {
+            if (q * 8u + (uint32_t)h >= m.n) continue;
+            const uint32_t b = (w4[h >> 1] >> (16 * (h & 1))) & 0x7FFFu;
+            if (hsel < 0) atomicAdd(&bins[b >> 1], 1u << ((b & 1u) << 4));
+            else if ((b >> 14) == (uint32_t)hsel) atomicAdd(&bins[b & (KC_WORDS - 1u)], 1u);
         }
     };
-    count(-1);
+    auto count = [&](int hsel) {
+        for (uint32_t q = t; q < nq; q += 1024u) count8(g4[q], q, hsel);
+    };
+    /* the part's first KP_U pieces per thread (32 K codes: most parts whole)
+       loaded before the bins are zeroed, so that the stream is in flight
+       while they are: one load at a time left the count latency-bound (7 of
+       the pass's 13 ms at k = 17, ablation kpx_nocnt) */
+    constexpr uint32_t KP_U = 4u;
+    uint4 pv[KP_U];
+#pragma unroll
+    for (uint32_t u = 0; u < KP_U; u++) pv[u] = t + u * 1024u < nq ? g4[t + u * 1024u] : make_uint4(0, 0, 0, 0);
+    for (uint32_t i = t; i < KC_WORDS / 4u; i += 1024u) reinterpret_cast<uint4 *>(bins)[i] = make_uint4(0, 0, 0, 0);
+    __syncthreads();
+#pragma unroll
+    for (uint32_t u = 0; u < KP_U; u++)
+        if (t + u * 1024u < nq) count8(pv[u], t + u * 1024u, -1);
+    for (uint32_t q0 = t + KP_U * 1024u; q0 < nq; q0 += KP_U * 1024u) {
+#pragma unroll
+        for (uint32_t u = 0; u < KP_U; u++) pv[u] = q0 + u * 1024u < nq ? g4[q0 + u * 1024u] : make_uint4(0, 0, 0, 0);
+#pragma unroll
+        for (uint32_t u = 0; u < KP_U; u++)
+            if (q0 + u * 1024u < nq) count8(pv[u], q0 + u * 1024u, -1);
+    }
     __syncthreads();
     /* thread t's 32 bins: words [16 t, 16 t + 16) */
     uint32_t c[32];

@@ -159,8 +159,8 @@ VARIANTS = {
         ("                if (at < ps.cap) {", "                if (at < ps.cap && v == ~0ull - 1) {"),
     ],
     "kpx_nocnt": [
-        ("                if (hsel < 0) atomicAdd(&bins[b >> 1], 1u << ((b & 1u) << 4));",
-         "                if (hsel < -1) atomicAdd(&bins[b >> 1], 1u << ((b & 1u) << 4));"),
+        ("            if (hsel < 0) atomicAdd(&bins[b >> 1], 1u << ((b & 1u) << 4));",
+         "            if (hsel < -1) atomicAdd(&bins[b >> 1], 1u << ((b & 1u) << 4));"),
         ("        if (sa != (unsigned long long)m.n) {", "        if (sa == ~0ull) {"),
     ],
     "kpx_nolb": [
