@@ -609,10 +609,10 @@ def test_cli_q0_warnings_interleave_like_reference(ingest, tmp_path):
         assert b"Unknown character" not in tail
 
 
-@pytest.mark.parametrize("k0,k1", [(5, 9), (15, 17)])
+@pytest.mark.parametrize("k0,k1", [(5, 9), (16, 17)])
 def test_cli_sweep_matches_separate_runs(k0, k1, tmp_path):
     """--sweep k0..k1 over one device-resident read == separate runs
-    (stdout concatenated, the same CSV and stats files per k); 15..17
+    (stdout concatenated, the same CSV and stats files per k); 16..17
     crosses from the dense table to the sparse one"""
     name = "mix.fa"
     data = _long_header_input(11, 3 << 20)
