@@ -532,14 +532,22 @@ __device__ unsigned long long chain_prefix(unsigned long long *flags, uint32_t b
    one part) makes the halves' sum fall short of the codes: the part is then
    counted again as two halves of 2^14 32-bit bins. */
 #define KC_WORDS (1u << 14)
-__global__ void __launch_bounds__(1024)
+/* NT threads a block: 1024 (32 bins a thread, one block per CU).  (Round 6:
+   512 threads with 64 bins a thread, two blocks per CU so that one block's
+   barriers and chained-scan wait would overlap the other's count, needed
+   168 VGPRs; held to 128 they spilled 164 B a lane and the k = 17 step went
+   193 -> 213 ms) */
+#define KC_NT 1024u
+template <uint32_t NT>
+__global__ void __launch_bounds__(NT, NT == 512u ? 4 : 1)
 k_kp_count(const uint16_t *in, const PartMeta *meta, uint64_t cap_in, uint64_t lo, uint64_t npads,
            const unsigned long long *tcount, uint32_t nparts, int k, unsigned long long *flags, uint64_t *out_k,
            uint32_t *out_c, unsigned long long *slots, uint64_t *fl, unsigned long long *err) {
+    constexpr uint32_t NW = NT / 64u, BT = 32768u / NT;   /* waves; bins a thread */
     extern __shared__ uint32_t bins[];   /* KC_WORDS */
-    __shared__ unsigned long long wred[16][10];
+    __shared__ unsigned long long wred[NW][10];
     __shared__ uint32_t hpre[24];
-    __shared__ uint32_t wnz[16], wmx[16];
+    __shared__ uint32_t wnz[NW], wmx[NW];
     __shared__ unsigned long long bprefix;
     __shared__ uint32_t vblk;
     const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6;
@@ -572,7 +580,7 @@ k_kp_count(const uint16_t *in, const PartMeta *meta, uint64_t cap_in, uint64_t l
         }
     };
     auto count = [&](int hsel) {
-        for (uint32_t q = t; q < nq; q += 1024u) count8(g4[q], q, hsel);
+        for (uint32_t q = t; q < nq; q += NT) count8(g4[q], q, hsel);
     };
     /* the part's first KP_U pieces per thread (32 K codes: most parts whole)
        loaded before the bins are zeroed, so that the stream is in flight
@@ -581,26 +589,26 @@ k_kp_count(const uint16_t *in, const PartMeta *meta, uint64_t cap_in, uint64_t l
     constexpr uint32_t KP_U = 4u;
     uint4 pv[KP_U];
 #pragma unroll
-    for (uint32_t u = 0; u < KP_U; u++) pv[u] = t + u * 1024u < nq ? g4[t + u * 1024u] : make_uint4(0, 0, 0, 0);
-    for (uint32_t i = t; i < KC_WORDS / 4u; i += 1024u) reinterpret_cast<uint4 *>(bins)[i] = make_uint4(0, 0, 0, 0);
+    for (uint32_t u = 0; u < KP_U; u++) pv[u] = t + u * NT < nq ? g4[t + u * NT] : make_uint4(0, 0, 0, 0);
+    for (uint32_t i = t; i < KC_WORDS / 4u; i += NT) reinterpret_cast<uint4 *>(bins)[i] = make_uint4(0, 0, 0, 0);
     __syncthreads();
 #pragma unroll
     for (uint32_t u = 0; u < KP_U; u++)
-        if (t + u * 1024u < nq) count8(pv[u], t + u * 1024u, -1);
-    for (uint32_t q0 = t + KP_U * 1024u; q0 < nq; q0 += KP_U * 1024u) {
+        if (t + u * NT < nq) count8(pv[u], t + u * NT, -1);
+    for (uint32_t q0 = t + KP_U * NT; q0 < nq; q0 += KP_U * NT) {
 #pragma unroll
-        for (uint32_t u = 0; u < KP_U; u++) pv[u] = q0 + u * 1024u < nq ? g4[q0 + u * 1024u] : make_uint4(0, 0, 0, 0);
+        for (uint32_t u = 0; u < KP_U; u++) pv[u] = q0 + u * NT < nq ? g4[q0 + u * NT] : make_uint4(0, 0, 0, 0);
 #pragma unroll
         for (uint32_t u = 0; u < KP_U; u++)
-            if (q0 + u * 1024u < nq) count8(pv[u], q0 + u * 1024u, -1);
+            if (q0 + u * NT < nq) count8(pv[u], q0 + u * NT, -1);
     }
     __syncthreads();
-    /* thread t's 32 bins: words [16 t, 16 t + 16) */
-    uint32_t c[32];
+    /* thread t's BT bins: words [BT / 2 t, BT / 2 (t + 1)) */
+    uint32_t c[BT];
     unsigned long long hs = 0;
 #pragma unroll
-    for (uint32_t j = 0; j < 4u; j++) {
-        const uint4 q = reinterpret_cast<const uint4 *>(bins)[t * 4u + j];
+    for (uint32_t j = 0; j < BT / 8u; j++) {
+        const uint4 q = reinterpret_cast<const uint4 *>(bins)[t * (BT / 8u) + j];
         const uint32_t w4[4] = {q.x, q.y, q.z, q.w};
 #pragma unroll
         for (int h = 0; h < 4; h++) {
@@ -615,19 +623,19 @@ k_kp_count(const uint16_t *in, const PartMeta *meta, uint64_t cap_in, uint64_t l
         __syncthreads();
         unsigned long long sa = 0;
 #pragma unroll
-        for (uint32_t w = 0; w < 16u; w++) sa += wred[w][0];
+        for (uint32_t w = 0; w < NW; w++) sa += wred[w][0];
         if (sa != (unsigned long long)m.n) {
             for (int h = 0; h < 2; h++) {
                 __syncthreads();
-                for (uint32_t i = t; i < KC_WORDS / 4u; i += 1024u)
+                for (uint32_t i = t; i < KC_WORDS / 4u; i += NT)
                     reinterpret_cast<uint4 *>(bins)[i] = make_uint4(0, 0, 0, 0);
                 __syncthreads();
                 count(h);
                 __syncthreads();
-                if ((t >> 9) == (uint32_t)h) {   /* (thread t's bins lie in half t / 512) */
+                if (((BT * t) >> 14) == (uint32_t)h) {   /* (thread t's bins lie in half BT t / 2^14) */
 #pragma unroll
-                    for (uint32_t j = 0; j < 8u; j++) {
-                        const uint4 q = reinterpret_cast<const uint4 *>(bins)[(t & 511u) * 8u + j];
+                    for (uint32_t j = 0; j < BT / 4u; j++) {
+                        const uint4 q = reinterpret_cast<const uint4 *>(bins)[((BT * t) & (KC_WORDS - 1u)) / 4u + j];
                         c[4 * j] = q.x; c[4 * j + 1] = q.y; c[4 * j + 2] = q.z; c[4 * j + 3] = q.w;
                     }
                 }
@@ -638,16 +646,16 @@ k_kp_count(const uint16_t *in, const PartMeta *meta, uint64_t cap_in, uint64_t l
     /* the top key (relative 0xFFFFFFFF, the last bin of the last part) was
        only counted (k_kpart): its real windows, the pads taken off */
     const unsigned long long extra = blk == nparts - 1u ? *tcount - npads : 0ull;
-    if (t == 1023u && extra) c[31] += (uint32_t)extra;
+    if (t == NT - 1u && extra) c[BT - 1] += (uint32_t)extra;
     const int fs = 2 * (k - 1);
-    const uint64_t kb = lo + ((uint64_t)blk << 15) + t * 32u;   /* key of my first bin (a multiple of 4) */
+    const uint64_t kb = lo + ((uint64_t)blk << 15) + t * BT;   /* key of my first bin (a multiple of 4) */
     /* statistics with constant register indices (a runtime index into a
        register array put it in scratch memory): bin j's last base is j & 3,
-       and the first base is the same for all 32 bins */
+       and the first base is the same for all BT bins */
     uint32_t nz = 0;
     unsigned long long l4[4] = {0, 0, 0, 0};
 #pragma unroll
-    for (uint32_t j = 0; j < 32u; j++) {
+    for (uint32_t j = 0; j < BT; j++) {
         nz += c[j] != 0;
         l4[j & 3] += c[j];
     }
@@ -661,7 +669,7 @@ k_kp_count(const uint16_t *in, const PartMeta *meta, uint64_t cap_in, uint64_t l
     __syncthreads();
     uint32_t before = 0, total = 0;
 #pragma unroll
-    for (uint32_t w = 0; w < 16u; w++) {
+    for (uint32_t w = 0; w < NW; w++) {
         const uint32_t x = wnz[w];
         before += w < wv ? x : 0u;
         total += x;
@@ -685,15 +693,15 @@ k_kp_count(const uint16_t *in, const PartMeta *meta, uint64_t cap_in, uint64_t l
     for (uint32_t w = 0; w < wv; w++) pm = max(pm, wmx[w]);
     uint64_t first = 0, prev = 0;
     bool have = false;
-    /* adjacent keys inside my 32 bins differ in one of the last three bases
-       (depths k, k - 1, k - 2): counted in registers */
+    /* adjacent keys inside my BT <= 64 bins differ in one of the last three
+       bases (depths k, k - 1, k - 2): counted in registers */
     uint32_t h0 = 0, h1 = 0, h2 = 0;
 #pragma unroll
-    for (uint32_t j = 0; j < 32u; j++) {
+    for (uint32_t j = 0; j < BT; j++) {
         if (c[j]) {
             const uint64_t key = kb + j;
             if (have) {   /* first differing base of adjacent keys (k_sp_wprefix) */
-                const uint32_t d = (uint32_t)(key ^ prev);   /* < 32 */
+                const uint32_t d = (uint32_t)(key ^ prev);   /* < BT */
                 h0 += d < 4u;
                 h1 += d >= 4u && d < 16u;
                 h2 += d >= 16u;
@@ -736,10 +744,10 @@ k_kp_count(const uint16_t *in, const PartMeta *meta, uint64_t cap_in, uint64_t l
         __syncthreads();   /* (the staging area is free: lastk read, or the last round written out) */
         uint32_t o = off;
 #pragma unroll
-        for (uint32_t j = 0; j < 32u; j++) {
+        for (uint32_t j = 0; j < BT; j++) {
             if (c[j]) {
                 if (o >= r0 && o < r0 + KC_STAGE) {
-                    sidx[o - r0] = (uint16_t)(t * 32u + j);
+                    sidx[o - r0] = (uint16_t)(t * BT + j);
                     scnt[o - r0] = c[j];
                 }
                 o++;
@@ -747,7 +755,7 @@ k_kp_count(const uint16_t *in, const PartMeta *meta, uint64_t cap_in, uint64_t l
         }
         __syncthreads();
         const uint32_t nr = min(KC_STAGE, total - r0);
-        for (uint32_t i = t; i < nr; i += 1024u) {
+        for (uint32_t i = t; i < nr; i += NT) {
             __builtin_nontemporal_store((uint64_t)(kpart + sidx[i]), out_k + bprefix + r0 + i);
             __builtin_nontemporal_store(scnt[i], out_c + bprefix + r0 + i);
         }
@@ -763,7 +771,7 @@ k_kp_count(const uint16_t *in, const PartMeta *meta, uint64_t cap_in, uint64_t l
     __syncthreads();
     if (t < 10) {
         unsigned long long a = 0;
-        for (uint32_t w = 0; w < 16u; w++) a += wred[w][t];
+        for (uint32_t w = 0; w < NW; w++) a += wred[w][t];
         if (a) atomicAdd(&slots[(blk % KP_SLOTS) * KP_SLOT_W + t], a);
         if (t == 1 && a != (uint64_t)m.n + extra) atomicOr(&slots[(blk % KP_SLOTS) * KP_SLOT_W + 10], 1ull);
     }
@@ -1128,7 +1136,7 @@ int sp_count_runs32(fk_engine *e, const uint32_t *keys, uint64_t n, uint64_t lo,
     hipLaunchKernelGGL(k_repart<uint16_t>, dim3(2048u / REPART_G), dim3(1024), 0, e->stream, pg, e->d_parts, alloc,
                        meta, (uint64_t)e->parts_cap, alloc + 1, 15u, nullptr);
     HIPCHK(hipGetLastError());
-    hipLaunchKernelGGL(k_kp_count, dim3(nparts), dim3(1024), (size_t)KC_WORDS * 4, e->stream, (const uint16_t *)e->d_parts,
+    hipLaunchKernelGGL(k_kp_count<KC_NT>, dim3(nparts), dim3(KC_NT), (size_t)KC_WORDS * 4, e->stream, (const uint16_t *)e->d_parts,
                        (const PartMeta *)meta, (uint64_t)e->parts_cap, lo, npads, (const unsigned long long *)tcount, nparts,
                        k, flags.as<unsigned long long>(), out_k, out_c, slots.as<unsigned long long>(), fl.as<uint64_t>(),
                        alloc + 1);
@@ -1273,7 +1281,7 @@ int sparse_finish(fk_engine *e, int32_t seq) {
                                    (int)(KS_CAP * 6 + 16)));
         HIPCHK(hipFuncSetAttribute((const void *)k_kp_sort<KS_CAP_S>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                    (int)(KS_CAP_S * 6 + 16)));
-        HIPCHK(hipFuncSetAttribute((const void *)k_kp_count, hipFuncAttributeMaxDynamicSharedMemorySize,
+        HIPCHK(hipFuncSetAttribute((const void *)k_kp_count<KC_NT>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                    (int)(KC_WORDS * 4)));
     }
     DevScratch acc, bh, ctr, pctr;
