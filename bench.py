@@ -225,7 +225,9 @@ def measure(ctx, k, n, L, seed, chrom, steps, warmup, verify=False):
     nbytes = size - halo
     torch.cuda.synchronize()
 
-    eng = fk.Engine(k, device=ctx.local, timing_every=args.timing_every)
+    # (17 <= k <= 20: finish re-reads the step's input from `buf`, which stays
+    # unchanged, instead of a copy the engine keeps: fk_opts.borrow_input)
+    eng = fk.Engine(k, device=ctx.local, timing_every=args.timing_every, borrow_input=True)
     # 17 <= k <= 20: sparse tables, merged by an all-to-all (no dense buffer)
     merge_t = fkdist.merge_buffer(k, ctx.coll_dev) if sharded and k < fkdist.SPARSE_KMIN else None
     pinned = torch.empty(fkdist.COUNTER_SLOTS, dtype=torch.int32, pin_memory=True) \

@@ -78,7 +78,8 @@ class FkResult(ctypes.Structure):
 class FkOpts(ctypes.Structure):
     _fields_ = [("device", ctypes.c_int32), ("want_nodes", ctypes.c_int32),
                 ("stream", ctypes.c_void_p), ("collect_unknown", ctypes.c_int32),
-                ("timing_every", ctypes.c_int32), ("reserved", ctypes.c_int32 * 6)]
+                ("timing_every", ctypes.c_int32), ("borrow_input", ctypes.c_int32),
+                ("reserved", ctypes.c_int32 * 5)]
 
 
 class FkSummary(ctypes.Structure):
@@ -217,7 +218,8 @@ def _ptr(obj):
 class Engine:
     """One k-mer engine on one GPU (mirrors the findKmer() scan, :962-1069)."""
 
-    def __init__(self, k, device=-1, want_nodes=False, collect_unknown=False, stream=None, timing_every=1):
+    def __init__(self, k, device=-1, want_nodes=False, collect_unknown=False, stream=None, timing_every=1,
+                 borrow_input=False):
         L = lib()
         self.k = k
         o = FkOpts()
@@ -227,6 +229,9 @@ class Engine:
         o.collect_unknown = int(collect_unknown) if collect_unknown else 0
         o.stream = stream
         o.timing_every = int(timing_every)
+        # 17 <= k <= 20: finish re-reads the caller's device feeds (kept unchanged
+        # until finish) instead of a copy (fk_opts.borrow_input)
+        o.borrow_input = 1 if borrow_input else 0
         h = ctypes.c_void_p()
         _check(L.fk_engine_create(k, ctypes.byref(o), ctypes.byref(h)), "fk_engine_create")
         self.h = h

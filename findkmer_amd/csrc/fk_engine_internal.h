@@ -57,7 +57,9 @@ struct fk_engine {
     uint8_t *d_keep = nullptr;                /* sparse: the input fed so far */
     XState *d_kst = nullptr;                  /* sparse: every retained range's exact entering state */
     uint64_t keep_len = 0, keep_cap = 0, kst_len = 0, kst_cap = 0;
-    struct SpSeg { uint64_t off, len, st, nranges, cpw, nchunks; };
+    /* src: the caller's bytes (opts.borrow_input), else at d_keep + off */
+    struct SpSeg { uint64_t off, len, st, nranges, cpw, nchunks; const uint8_t *src; };
+    bool seg_borrow = false;                  /* the segment being fed lies in the caller's device buffer */
     std::vector<SpSeg> spsegs;                /* the retained segments */
     /* the finished table, contiguous (the passes append in key order): keys
        ascending + u32 counts; kept across steps (grown, never shrunk), as are
@@ -190,6 +192,34 @@ struct fk_engine {
     uint32_t *h_rows = nullptr, *h_rows_dev = nullptr;
     uint32_t *d_rows = nullptr;               /* the stitched exchange's rows (device) */
     uint32_t rows_cap = 0, rows_seq = 0;
+    /* scratch buffers kept across calls (PoolScratch): the sparse finish
+       and its passes took ~20 hipMalloc / hipFree pairs a step, and a
+       hipFree waits for the device */
+    static const int NPOOL = 12;
+    void *pool_p[NPOOL] = {};
+    size_t pool_cap[NPOOL] = {};
+};
+
+/* A scratch device buffer from the engine's pool slot `i` (grown on demand,
+   freed with the engine): DevScratch's interface without a hipFree per use.
+   Two buffers live at the same time must use different slots. */
+struct PoolScratch {
+    fk_engine *e;
+    int i;
+    void *p = nullptr;
+    PoolScratch(fk_engine *eng, int slot) : e(eng), i(slot) {}
+    bool alloc(size_t n) {
+        if (n > e->pool_cap[i] || !e->pool_p[i]) {
+            hipFree(e->pool_p[i]);
+            e->pool_p[i] = nullptr;
+            e->pool_cap[i] = 0;
+            if (hipMalloc(&e->pool_p[i], n) != hipSuccess) return false;
+            e->pool_cap[i] = n;
+        }
+        p = e->pool_p[i];
+        return true;
+    }
+    template <class T> T *as() const { return (T *)p; }
 };
 
 static inline int hist_mode(const fk_engine *e) {

@@ -517,6 +517,9 @@ static int run_k(int argc) {
     if (on_device) fk_input_info(g_input, nullptr, nullptr, &opts.device, nullptr);
     opts.want_nodes = 1;
     opts.collect_unknown = progress ? 2 : 1;   /* 2: with their offsets, to interleave */
+    /* k >= 17: finish re-reads the resident file, which outlives the engine,
+       instead of keeping a copy of it */
+    opts.borrow_input = on_device ? 1 : 0;
     fk_engine *eng = nullptr;
     int rc = fk_engine_create(config.k, &opts, &eng);
     if (rc) die_engine(rc);

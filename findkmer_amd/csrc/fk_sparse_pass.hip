@@ -333,7 +333,7 @@ int sp_emit_all(fk_engine *e, const SpEmit &em) {
         if (!sg.nranges) continue;
         const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((sg.nranges + SP_WAVES - 1) / SP_WAVES,
                                                                                  (uint64_t)e->cus * 8));
-        hipLaunchKernelGGL(k_sp_emit, dim3(grid), dim3(SP_WAVES * 64u), lds, e->stream, e->d_keep + sg.off, sg.len,
+        hipLaunchKernelGGL(k_sp_emit, dim3(grid), dim3(SP_WAVES * 64u), lds, e->stream, sg.src ? sg.src : e->d_keep + sg.off, sg.len,
                            e->k, e->maskk, e->d_kst + sg.st, sg.nranges, sg.cpw, sg.nchunks, em);
         HIPCHK(hipGetLastError());
     }
@@ -1117,7 +1117,7 @@ int sp_count_runs32(fk_engine *e, const uint32_t *keys, uint64_t n, uint64_t lo,
     if (rc) return rc;
     if (!e->d_pmeta && hipMalloc(&e->d_pmeta, (size_t)2048 * REPART_METAP * sizeof(PartMeta) + 64) != hipSuccess)
         return FK_E_OOM;
-    DevScratch flags, slots, fl, res;
+    PoolScratch flags(e, 0), slots(e, 1), fl(e, 2), res(e, 3);
     if (!flags.alloc((size_t)(nparts + 1) * 8) || !slots.alloc((size_t)KP_SLOTS * KP_SLOT_W * 8) ||
         !fl.alloc((size_t)nparts * 16) || !res.alloc(16))
         return FK_E_OOM;
@@ -1188,7 +1188,7 @@ int sp_sort_runs64(fk_engine *e, const uint64_t *keys, uint64_t n, uint64_t lo, 
     if (rc) return rc;
     if (!e->d_pmeta && hipMalloc(&e->d_pmeta, (size_t)2048 * REPART_METAP * sizeof(PartMeta) + 64) != hipSuccess)
         return FK_E_OOM;
-    DevScratch flags, slots, fl, res;
+    PoolScratch flags(e, 0), slots(e, 1), fl(e, 2), res(e, 3);
     if (!flags.alloc((size_t)(nparts + 1) * 8) || !slots.alloc((size_t)KP_SLOTS * KP_SLOT_W * 8) ||
         !fl.alloc((size_t)nparts * 16) || !res.alloc(16))
         return FK_E_OOM;
@@ -1284,7 +1284,7 @@ int sparse_finish(fk_engine *e, int32_t seq) {
         HIPCHK(hipFuncSetAttribute((const void *)k_kp_count<KC_NT>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                    (int)(KC_WORDS * 4)));
     }
-    DevScratch acc, bh, ctr, pctr;
+    PoolScratch acc(e, 4), bh(e, 5), ctr(e, 6), pctr(e, 7);
     if (!acc.alloc(FKS_ACC_N * sizeof(unsigned long long)) || !bh.alloc((size_t)nbk * 8) || !ctr.alloc(24) ||
         !pctr.alloc(2 * SP_MAXP * sizeof(unsigned long long)))
         return FK_E_OOM;
@@ -1337,7 +1337,7 @@ int sparse_finish(fk_engine *e, int32_t seq) {
     const bool tail = !e->state.hdr && seq >= 1 && seq < k;
     const bool nodes = e->opts.want_nodes != 0;
     uint64_t scap = std::max<uint64_t>(1024, e->keep_len / 64);
-    DevScratch shorts, found;
+    PoolScratch shorts(e, 8), found(e, 9);
     uint64_t ns = 0;
     /* the collected short walks (+ the input's last run, shorter than k:
        :1059-1062 at EOF), distinct, with their found flags */

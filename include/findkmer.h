@@ -118,7 +118,13 @@ typedef struct {
                                  their stream offsets, fk_engine_unknown_since) */
     int32_t timing_every;     /* time the count kernel with HIP events on every
                                  Nth launch (0 or 1: every launch) */
-    int32_t reserved[6];
+    int32_t borrow_input;     /* 17 <= k <= 20: device feeds (16-B aligned, at
+                                 least FK_LANE_BYTES) and shards are read again
+                                 at finish from the caller's buffer instead of
+                                 a copy the engine keeps: the caller leaves
+                                 those bytes unchanged until fk_engine_finish
+                                 (or reset / destroy) returns.  0: copy (round 6) */
+    int32_t reserved[5];
 } fk_opts;
 
 typedef struct fk_engine fk_engine;

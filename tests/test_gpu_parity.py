@@ -894,16 +894,26 @@ def test_shards_summaries_take_both_paths(k):
     assert shard_count.compact_failed == failed0 + 1, "the shard inside a long comment must refuse its compact summary"
 
 
-def assert_same_sparse(data, k, feeds=None):
-    """17 <= k <= 20: the engine's sparse table and scalars vs the oracle's"""
+def assert_same_sparse(data, k, feeds=None, borrow=False):
+    """17 <= k <= 20: the engine's sparse table and scalars vs the oracle's.
+    borrow: the feeds are slices of one device buffer and the engine re-reads
+    them at finish instead of keeping a copy (fk_opts.borrow_input)"""
     keys_o, cnt_o, r_o = oracle.count_sparse(data, k, cap=max(16, len(data) + 16))
-    with fk.Engine(k, want_nodes=True, collect_unknown=True) as e:
+    dev = None
+    if borrow:
+        import torch
+        dev = torch.zeros(len(data) + 64, dtype=torch.uint8, device="cuda")
+        dev[:len(data)].copy_(torch.frombuffer(bytearray(data), dtype=torch.uint8))
+        torch.cuda.synchronize()
+    with fk.Engine(k, want_nodes=True, collect_unknown=True, borrow_input=borrow) as e:
         arr = np.frombuffer(bytes(data), dtype=np.uint8)
         if feeds is None:
             feeds = [len(arr)]
         pos = 0
         for n in feeds:
-            if n:
+            if n and dev is not None:
+                e.feed_device(dev.data_ptr() + pos, n)
+            elif n:
                 e.feed(np.ascontiguousarray(arr[pos:pos + n]))
             pos += n
         assert pos == len(arr)
@@ -940,6 +950,16 @@ def test_sparse_mixed_and_streaming(k):
         feeds.append(n)
         left -= n
     assert_same_sparse(data, k, feeds=feeds)
+
+
+@pytest.mark.parametrize("k", [17, 20])
+def test_sparse_borrowed_device_feeds(k):
+    """fk_opts.borrow_input: device feeds (16-B aligned pieces of one buffer,
+    one piece too short for the device path and one misaligned, which the
+    engine stages and copies) re-read at finish from the caller's buffer"""
+    data = mixed_input(1300 + k, 600_000)
+    feeds = [4096, 160_000, 16, 7, 200_009, len(data) - 4096 - 160_000 - 16 - 7 - 200_009]
+    assert_same_sparse(data, k, feeds=feeds, borrow=True)
 
 
 @pytest.mark.parametrize("k", [17, 20])
