@@ -195,7 +195,7 @@ struct fk_engine {
     /* scratch buffers kept across calls (PoolScratch): the sparse finish
        and its passes took ~20 hipMalloc / hipFree pairs a step, and a
        hipFree waits for the device */
-    static const int NPOOL = 12;
+    static const int NPOOL = 14;
     void *pool_p[NPOOL] = {};
     size_t pool_cap[NPOOL] = {};
 };

@@ -465,6 +465,363 @@ k_kpart(const KT *keys, uint64_t n, PartGeo pg, uint64_t lo, uint64_t hi, uint32
     if (t == 0 && ntop) atomicAdd(tcount, (unsigned long long)ntop);
 }
 
+/*
+ * k = 17, round 6: a pass's partition fused into the walk (k_sp_wpart).  The
+ * key-list route above walks the input once to emit every window's 32-bit
+ * key into its pass's list (36 ms per 10 G-base step: 40 GB written), then
+ * k_kpart reads each list back to partition it (4 x 9 ms), after a
+ * histogram walk (10.6 ms) that sizes the passes.  Here pass q (the windows
+ * whose first base is q: keys [q 2^32, (q + 1) 2^32)) walks the input
+ * itself -- four walks, no key list, no histogram walk -- and writes k_kpart's
+ * rows directly: each round every wave of a 16-wave block counts one tile;
+ * after WP_NT rounds the block counting-sorts the in-pass windows of its
+ * stashed fast tiles by coarse slice (the top 11 bits of the 32-bit key) in
+ * LDS and writes the sorted batch as one row of 21-bit codes with its 2048
+ * run words (the row claimed from a global counter).  A stashed fast tile is
+ * five words a lane; its 17-mers are recomputed from them in each phase:
+ * the 16-mer ending at slot i is one alignbit of the half's {context, word}
+ * pair (as in k_part), and its first base the context's digit above it --
+ * the context taken from the previous half's full 16-digit word, since a
+ * '\n' half's context word (Emit::AC / BC) lost its top digit.  A batch with
+ * more in-pass windows than a row holds (skewed input: at most WP_NT x 16 x
+ * 2048) is written as several rows, each placing the entries whose sorted
+ * position falls in its window.  A tile the fast path cannot take only
+ * advances the wave's state (tile_general without counting: a few registers,
+ * where the counting general path would crowd the fast tiles' loop out of
+ * its 128 VGPRs); walk 0 records it with its entering state, and after walk
+ * 0 k_sp_gtiles counts every recorded tile as k_sp_emit would (slots in
+ * LDS), listing its windows by first base as 32-bit keys -- partitioned into
+ * further rows of their pass by k_kpart -- and its short walks.  A row or
+ * list past its capacity fails the walk, and the finish takes the key-list
+ * route instead.
+ */
+#define SP_RETRY 1000      /* (host) the fused walks gave up: the key-list passes instead */
+#define WP_NT 3u            /* tiles per wave per batch: ~24 K of a row's 32 K on random input */
+#define WP_FAULT 1ull
+/* a tile the fast path did not take: where (its segment, offset) and its
+   entering state */
+struct SpDefer {
+    uint64_t tb, code;
+    uint32_t R, hdr, seg, pad;
+};
+struct SpWalk {
+    uint32_t qdig;                 /* the pass's first base in the internal encoding */
+    uint32_t *codes;               /* rows of KP_BATCH codes (k_kpart's layout) */
+    uint32_t *idx;                 /* [row][2048] run words */
+    unsigned long long *ctr;       /* [0] rows claimed, [1] tiles deferred, [3] windows placed in rows,
+                                      [4] faults */
+    uint64_t rows_cap;
+    SpDefer *defer;                /* walk 0: the other tiles (else nullptr) */
+    uint64_t defer_cap;
+    uint32_t seg;                  /* the launch's segment */
+    uint32_t dbg;                  /* FINDKMER_TUNE sp_walk_dbg: 1 = every tile deferred (tests) */
+};
+struct WpTile {
+    uint32_t c0, s0, c1, s1;       /* per half: 16-digit context, 16-digit word */
+    uint32_t fl;                   /* bit 0: has windows, bits 1, 2: half 0 / 1 had a '\n' (slot 0 no window) */
+};
+/* a stashed fast tile's in-pass windows: HIST into the slices' counts, else
+   placed at their slices' cursors */
+template <bool HIST>
+__device__ __forceinline__ void wp_tile(const WpTile &x, uint32_t qdig, uint32_t *hist, uint32_t *cur, uint32_t *ent) {
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+        const uint32_t C = h ? x.c1 : x.c0, S = h ? x.s1 : x.s0;
+        const bool skip0 = (x.fl >> (1 + h)) & 1u;
+#pragma unroll
+        for (int g = 0; g < 2; g++) {
+            uint32_t b[8], cd[8], p[8];
+            bool in[8];
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+                const int i = 8 * g + j;
+                const uint32_t sh = 30u - 2u * (uint32_t)i;
+                const uint32_t v = i < 15 ? __builtin_amdgcn_alignbit(C, S, sh) : S;
+                const uint32_t r = v ^ ((v >> 1) & 0x55555555u);   /* fk_sigma of the low 16 digits */
+                in[j] = __builtin_amdgcn_ubfe(C, sh, 2u) == qdig && (i > 0 || !skip0);
+                b[j] = r >> 21;
+                cd[j] = r & 0x1FFFFFu;
+            }
+            if (HIST) {
+#pragma unroll
+                for (int j = 0; j < 8; j++)
+                    if (in[j]) atomicAdd(&hist[b[j]], 1u);
+            } else {
+                /* the eight returning cursor atomics back to back, then the stores */
+#pragma unroll
+                for (int j = 0; j < 8; j++)
+                    if (in[j]) p[j] = atomicAdd(&cur[b[j]], 1u);
+#pragma unroll
+                for (int j = 0; j < 8; j++)
+                    if (in[j] && p[j] < KP_BATCH) ent[p[j]] = cd[j];
+            }
+        }
+    }
+}
+
+__global__ void __launch_bounds__(1024, 1)
+k_sp_wpart(const uint8_t *buf, uint64_t len, int k, uint64_t maskk, const XState *rst, uint64_t nranges, uint64_t cpw,
+           uint64_t nchunks, SpWalk wk) {
+    __shared__ uint32_t hist[2048], cur[2048], vst[2048], wtot[16];
+    __shared__ uint32_t s_total;
+    __shared__ unsigned long long s_row;
+    extern __shared__ uint32_t ent[];   /* KP_BATCH codes */
+    const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    for (uint32_t i = t; i < 2048u; i += 1024u) hist[i] = 0;
+    __syncthreads();
+    const uint64_t gw = (uint64_t)blockIdx.x * 16u + wv, nw = (uint64_t)gridDim.x * 16u;
+    Ctx cx{buf, len, 0, nullptr, nullptr, nullptr, nullptr, nullptr, maskk, 0, k, nullptr, nullptr};
+    /* the wave's tile cursor: range r, tile tb of [.., re), state st */
+    uint64_t r = gw, tb = 0, re = 0;
+    DState st{0, 0, 0};
+    uint32_t wn[8] = {};
+    auto load_full = [&](uint64_t at) {
+        const u32x4 *p = reinterpret_cast<const u32x4 *>(buf + at + (uint64_t)lane * FK_LANE_BYTES);
+        const u32x4 a = __builtin_nontemporal_load(p), c = __builtin_nontemporal_load(p + 1);
+        wn[0] = a.x; wn[1] = a.y; wn[2] = a.z; wn[3] = a.w;
+        wn[4] = c.x; wn[5] = c.y; wn[6] = c.z; wn[7] = c.w;
+    };
+    auto open = [&]() {   /* range r from its exact entering state */
+        const uint64_t c0 = r * cpw, c1 = min(c0 + cpw, nchunks);
+        tb = c0 * FK_CHUNK_BYTES;
+        re = min(c1 * FK_CHUNK_BYTES, len);
+        const XState x = rst[r];
+        st = DState{x.code, (uint32_t)x.R, x.hdr};
+        if (tb + FK_TILE_BYTES <= re) load_full(tb);
+    };
+    bool done = r >= nranges;
+    if (!done) open();
+    /* one tile of the wave's ranges: a fast tile stashed, any other only
+       advancing the state (walk 0: recorded for k_sp_gtiles) */
+    auto step = [&]() -> WpTile {
+        WpTile x{0, 0, 0, 0, 0};
+        if (done) return x;
+        uint32_t w[8];
+        int nb = (int)FK_LANE_BYTES;
+        const bool full = tb + FK_TILE_BYTES <= re;
+        if (full) {
+#pragma unroll
+            for (int d = 0; d < 8; d++) w[d] = wn[d];
+        } else {
+            nb = load_lane<FK_LANE_BYTES>(cx, (int64_t)(tb + (uint64_t)lane * FK_LANE_BYTES), w);
+        }
+        if (tb + 2 * FK_TILE_BYTES <= re) load_full(tb + FK_TILE_BYTES);
+        Facts f{0, 0, 0, 0, 0, 0};
+        Counters cnt{0, 0, 0, 0, 0, FK_NO_EOF, 0};
+        const uint64_t c0 = st.code;
+        Emit fe{0, 0, 0, 0, false, false, false};
+        if (full && st.hdr == 0 && !(wk.dbg & 1u) && tile_fast<true, H_EMIT, false>(cx, w, st, f, cnt, 1u, &fe)) {
+            if (fe.deep) {
+                const uint32_t xp = from_prev_lane(fe.B2, (uint32_t)c0);   /* the 16 digits before half 0 */
+                x.c0 = fe.h0 ? xp >> 2 : xp;
+                x.s0 = fe.A2;
+                x.c1 = fe.h1 ? fe.A2 >> 2 : fe.A2;
+                x.s1 = fe.B2;
+                x.fl = 1u | (fe.h0 ? 2u : 0u) | (fe.h1 ? 4u : 0u);
+            }
+        } else {
+            if (wk.defer && lane == 0) {
+                const unsigned long long i = atomicAdd(&wk.ctr[1], 1ull);
+                if (i < wk.defer_cap) wk.defer[i] = SpDefer{tb, st.code, st.R, st.hdr, wk.seg, 0u};
+            }
+            tile_general<false, H_NONE>(cx, w, nb, 0u, st, f, cnt, 1u);
+        }
+        tb += FK_TILE_BYTES;
+        if (tb >= re) {
+            r += nw;
+            done = r >= nranges;
+            if (!done) open();
+        }
+        return x;
+    };
+    WpTile xs[WP_NT];
+    /* the stashed tiles' in-pass windows into the slices' counts (sel: one
+       stash slot, or ~0 all).  One stashed tile at a time: unrolled over the
+       stash, the compiler interleaved all 96 windows and spilled */
+    auto wp_hist = [&](uint32_t sel) {
+#pragma unroll 1
+        for (uint32_t i = 0; i < WP_NT; i++) {
+            WpTile x = xs[0];
+#pragma unroll
+            for (uint32_t ii = 1; ii < WP_NT; ii++)
+                if (i == ii) x = xs[ii];
+            if ((x.fl & 1u) && (sel == ~0u || sel == i)) wp_tile<true>(x, wk.qdig, hist, cur, ent);
+        }
+    };
+    /* sorted starts (two slices a thread, a block scan), the counts cleared
+       for the next histogram; returns the total */
+    auto wp_scan = [&]() -> uint32_t {
+        const uint32_t b = 2u * t, n0 = hist[b], n1 = hist[b + 1u], sum = n0 + n1;
+        const uint32_t inc = wscan_incl32(sum);
+        if (lane == 63) wtot[wv] = inc;
+        __syncthreads();
+        uint32_t run = inc - sum;
+#pragma unroll
+        for (uint32_t w = 0; w < 16u; w++) run += w < wv ? wtot[w] : 0u;
+        vst[b] = run;
+        vst[b + 1u] = run + n0;
+        cur[b] = run;
+        cur[b + 1u] = run + n0;
+        hist[b] = 0;
+        hist[b + 1u] = 0;
+        if (t == 1023u) s_total = run + sum;
+        __syncthreads();
+        return s_total;
+    };
+    /* the sorted windows (T <= KP_BATCH) as one row: claimed, run words,
+       placed, written out */
+    auto wp_row = [&](uint32_t sel, uint32_t T) {
+        if (T == 0) return;
+        if (t == 0) {
+            const unsigned long long rw = atomicAdd(&wk.ctr[0], 1ull);
+            s_row = rw;
+            if (rw >= wk.rows_cap) atomicOr(&wk.ctr[4], WP_FAULT);
+            atomicAdd(&wk.ctr[3], (unsigned long long)T);
+        }
+        __syncthreads();
+        const unsigned long long row = s_row;
+        const bool ok = row < wk.rows_cap;
+        if (ok) {
+            const uint32_t b = 2u * t, e2 = b + 2u < 2048u ? vst[b + 2u] : T;
+            reinterpret_cast<uint2 *>(wk.idx + (size_t)row * 2048u)[t] =
+                make_uint2(run_word(vst[b], vst[b + 1u] - vst[b]), run_word(vst[b + 1u], e2 - vst[b + 1u]));
+        }
+#pragma unroll 1
+        for (uint32_t i = 0; i < WP_NT; i++) {
+            WpTile x = xs[0];
+#pragma unroll
+            for (uint32_t ii = 1; ii < WP_NT; ii++)
+                if (i == ii) x = xs[ii];
+            if ((x.fl & 1u) && (sel == ~0u || sel == i)) wp_tile<false>(x, wk.qdig, hist, cur, ent);
+        }
+        __syncthreads();
+        if (ok) {
+            uint4 *dst = reinterpret_cast<uint4 *>(wk.codes + (size_t)row * KP_BATCH);
+            const uint4 *src = reinterpret_cast<const uint4 *>(ent);
+            for (uint32_t i = t; i < (T + 3u) / 4u; i += 1024u) dst[i] = src[i];
+        }
+        __syncthreads();
+    };
+    for (;;) {
+#pragma unroll 1
+        for (uint32_t u = 0; u < WP_NT; u++) {
+            const WpTile x = step();
+#pragma unroll
+            for (uint32_t i = 0; i < WP_NT; i++)
+                if (u == i) xs[i] = x;
+        }
+        wp_hist(~0u);
+        /* (the barrier also tells whether any wave has tiles left) */
+        const bool more = __syncthreads_or(!done);
+        const uint32_t T = wp_scan();
+        if (T <= KP_BATCH) {
+            wp_row(~0u, T);
+        } else {
+            /* more windows of the pass than a row holds: one row per stash
+               slot (16 x 2048 windows at most), each counted again on its
+               own.  (Splitting the batch's sorted order at KP_BATCH instead
+               let the atomics' order decide which of a straddling slice's
+               entries fell before the split -- differently in each row's
+               placement: an entry twice, another lost.) */
+#pragma unroll 1
+            for (uint32_t i = 0; i < WP_NT; i++) {
+                wp_hist(i);
+                __syncthreads();
+                wp_row(i, wp_scan());
+            }
+        }
+        if (!more) break;
+    }
+}
+
+/* the recorded tiles (walk 0), one wave at a time each from its entering
+   state with k_sp_emit's general path: FILL = false counts each first
+   base's windows (cnt[0..3]) and lists the short walks; FILL = true lists
+   the windows, first base q at glist + goff[q], as key - q 2^32 */
+struct SpSegDev {
+    const uint8_t *src;
+    uint64_t len;
+};
+template <bool FILL>
+__global__ void __launch_bounds__(SP_WAVES * 64u)
+k_sp_gtiles(const SpDefer *df, uint64_t n, const SpSegDev *segs, int k, uint64_t maskk, uint32_t *glist,
+            const uint64_t *goff, unsigned long long *cnt, uint64_t *shorts, uint64_t short_cap) {
+    extern __shared__ uint64_t gt_lds[];   /* SP_WAVES x 2048 slots */
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    uint64_t *slots = gt_lds + (size_t)wv * FK_TILE_BYTES;
+    const uint64_t nw = (uint64_t)gridDim.x * SP_WAVES;
+    for (uint64_t i = (uint64_t)blockIdx.x * SP_WAVES + wv; i < n; i += nw) {
+        const SpDefer d = df[i];
+        const SpSegDev sg = segs[d.seg];
+        Ctx cx{sg.src, sg.len, 0, nullptr, nullptr, nullptr, nullptr, nullptr, maskk, 0, k, nullptr, slots};
+        uint32_t w[8];
+        const int nb = load_lane<FK_LANE_BYTES>(cx, (int64_t)(d.tb + (uint64_t)lane * FK_LANE_BYTES), w);
+        DState st{d.code, d.R, d.hdr};
+        Facts f{0, 0, 0, 0, 0, 0};
+        Counters c{0, 0, 0, 0, 0, FK_NO_EOF, 0};
+#pragma unroll 8
+        for (uint32_t j = 0; j < FK_LANE_BYTES; j++) slots[j * 64u + lane] = SP_EMPTY;
+        tile_general<true, H_SPARSE>(cx, w, nb, 0u, st, f, c, 1u);
+        /* per first base: this lane's windows (16-bit fields), then a wave scan */
+        uint32_t c01 = 0, c23 = 0, nsh = 0;
+        for (uint32_t j = 0; j < FK_LANE_BYTES; j++) {
+            const uint64_t v = slots[j * 64u + lane];
+            if (v < SP_SHORT) {
+                const uint32_t q = (uint32_t)(v >> 32), inc = 1u << (16u * (q & 1u));
+                c01 += q < 2u ? inc : 0u;
+                c23 += q >= 2u ? inc : 0u;
+            } else if (v != SP_EMPTY) {
+                nsh++;
+            }
+        }
+        if (!FILL) {
+            const uint32_t a01 = wsum32(c01), a23 = wsum32(c23), ash = shorts ? wscan_incl32(nsh) : 0u;
+            const uint32_t tsh = rdlane(ash, 63);
+            unsigned long long sb = 0;
+            if (lane == 0) {
+                if (a01 & 0xFFFFu) atomicAdd(&cnt[0], (unsigned long long)(a01 & 0xFFFFu));
+                if (a01 >> 16) atomicAdd(&cnt[1], (unsigned long long)(a01 >> 16));
+                if (a23 & 0xFFFFu) atomicAdd(&cnt[2], (unsigned long long)(a23 & 0xFFFFu));
+                if (a23 >> 16) atomicAdd(&cnt[3], (unsigned long long)(a23 >> 16));
+                if (tsh) sb = atomicAdd(&cnt[4], (unsigned long long)tsh);
+            }
+            sb = rdlane64(sb, 0) + (ash - nsh);
+            if (shorts && nsh)
+                for (uint32_t j = 0; j < FK_LANE_BYTES; j++) {
+                    const uint64_t v = slots[j * 64u + lane];
+                    if (v >= SP_SHORT && v != SP_EMPTY) {
+                        if (sb < short_cap) shorts[sb] = v;
+                        sb++;
+                    }
+                }
+        } else {
+            const uint32_t i01 = wscan_incl32(c01), i23 = wscan_incl32(c23);
+            const uint32_t t01 = rdlane(i01, 63), t23 = rdlane(i23, 63);
+            unsigned long long b4[4] = {0, 0, 0, 0};
+            if (lane == 0) {
+                if (t01 & 0xFFFFu) b4[0] = atomicAdd(&cnt[0], (unsigned long long)(t01 & 0xFFFFu));
+                if (t01 >> 16) b4[1] = atomicAdd(&cnt[1], (unsigned long long)(t01 >> 16));
+                if (t23 & 0xFFFFu) b4[2] = atomicAdd(&cnt[2], (unsigned long long)(t23 & 0xFFFFu));
+                if (t23 >> 16) b4[3] = atomicAdd(&cnt[3], (unsigned long long)(t23 >> 16));
+            }
+            const uint32_t e01 = i01 - c01, e23 = i23 - c23;
+            uint64_t at[4] = {rdlane64(b4[0], 0) + (e01 & 0xFFFFu), rdlane64(b4[1], 0) + (e01 >> 16),
+                              rdlane64(b4[2], 0) + (e23 & 0xFFFFu), rdlane64(b4[3], 0) + (e23 >> 16)};
+            if (c01 | c23)
+                for (uint32_t j = 0; j < FK_LANE_BYTES; j++) {
+                    const uint64_t v = slots[j * 64u + lane];
+                    if (v < SP_SHORT) {
+                        const uint32_t q = (uint32_t)(v >> 32);
+                        const uint64_t a = q == 0u ? at[0] : q == 1u ? at[1] : q == 2u ? at[2] : at[3];
+                        glist[goff[q] + a] = (uint32_t)v;
+                        at[0] += q == 0u; at[1] += q == 1u; at[2] += q == 2u; at[3] += q == 3u;
+                    }
+                }
+        }
+        __builtin_amdgcn_wave_barrier();   /* (the slots are rewritten by the next tile) */
+    }
+}
+
 /* A chained scan over the blocks in dispatch order (wave 0 of every block
    calls it): this block's `total` published (status A: aggregate), the
    earlier blocks' sum found by looking back 64 flags at a time -- up to the
@@ -1094,64 +1451,98 @@ k_kp_fold(const unsigned long long *slots, const uint64_t *fl, uint32_t nparts, 
     if (threadIdx.x < 24 && h[threadIdx.x]) atomicAdd(&dacc[FKS_ACC_WPREFIX + threadIdx.x], (unsigned long long)h[threadIdx.x]);
 }
 
-/* The pass (keys lo + r for the n 32-bit r, npads of them the pad
-   0xFFFFFFFF) into its runs at out_k / out_c: *nw of them */
-int sp_count_runs32(fk_engine *e, const uint32_t *keys, uint64_t n, uint64_t lo, uint64_t npads,
-                           unsigned long long *dacc, uint64_t *out_k, uint32_t *out_c, uint64_t *nw) {
-    *nw = 0;
-    if (n == 0) return FK_OK;
+/* The rows pg.rows of 21-bit codes under 2048 coarse slices of a 2^32-key
+   pass [lo, lo + 2^32) -- k_kpart's over a key list, or the fused walk's
+   (k_sp_wpart) -- into the pass's runs at out_k / out_c (*nw of them):
+   k_repart, k_kp_count, k_kp_fold.  n: the codes the rows hold; res: 16 B
+   of zeroed device scratch, res[1] the top key counted apart by k_kpart
+   (npads of them pads) */
+static int sp_count_rows32(fk_engine *e, const PartGeo &pg, uint64_t n, uint64_t lo, uint64_t npads,
+                           unsigned long long *res, unsigned long long *dacc, uint64_t *out_k, uint32_t *out_c,
+                           uint64_t *nw) {
     const int k = e->k;
+    const uint32_t nparts = 2048u << 6;
+    int rc = sp_ensure((void **)&e->d_parts, &e->parts_cap, n + 8ull * nparts + 16, sizeof(uint16_t));
+    if (rc) return rc;
+    if (!e->d_pmeta && hipMalloc(&e->d_pmeta, (size_t)2048 * REPART_METAP * sizeof(PartMeta) + 64) != hipSuccess)
+        return FK_E_OOM;
+    PoolScratch flags(e, 0), slots(e, 1), fl(e, 2);
+    if (!flags.alloc((size_t)(nparts + 1) * 8) || !slots.alloc((size_t)KP_SLOTS * KP_SLOT_W * 8) ||
+        !fl.alloc((size_t)nparts * 16))
+        return FK_E_OOM;
+    PartMeta *meta = static_cast<PartMeta *>(e->d_pmeta);
+    unsigned long long *alloc = reinterpret_cast<unsigned long long *>(meta + (size_t)2048 * REPART_METAP);
+    HIPCHK(hipMemsetAsync(alloc, 0, 2 * sizeof(unsigned long long), e->stream));
+    HIPCHK(hipMemsetAsync(flags.p, 0, (size_t)(nparts + 1) * 8, e->stream));   /* (+ the block tickets) */
+    HIPCHK(hipMemsetAsync(slots.p, 0, (size_t)KP_SLOTS * KP_SLOT_W * 8, e->stream));
+    hipLaunchKernelGGL(k_repart<uint16_t>, dim3(2048u / REPART_G), dim3(1024), 0, e->stream, pg, e->d_parts, alloc,
+                       meta, (uint64_t)e->parts_cap, alloc + 1, 15u, nullptr);
+    HIPCHK(hipGetLastError());
+    hipLaunchKernelGGL(k_kp_count<KC_NT>, dim3(nparts), dim3(KC_NT), (size_t)KC_WORDS * 4, e->stream, (const uint16_t *)e->d_parts,
+                       (const PartMeta *)meta, (uint64_t)e->parts_cap, lo, npads, (const unsigned long long *)(res + 1), nparts,
+                       k, flags.as<unsigned long long>(), out_k, out_c, slots.as<unsigned long long>(), fl.as<uint64_t>(),
+                       alloc + 1);
+    HIPCHK(hipGetLastError());
+    hipLaunchKernelGGL(k_kp_fold, dim3(64), dim3(256), 0, e->stream, (const unsigned long long *)slots.p,
+                       (const uint64_t *)fl.p, nparts, k, (const unsigned long long *)flags.p, dacc, res);
+    HIPCHK(hipGetLastError());
+    unsigned long long r[2] = {0, 0};
+    HIPCHK(hipMemcpyAsync(&r[0], res, 8, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipMemcpyAsync(&r[1], alloc + 1, 8, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    if (r[1]) return FK_E_INTERNAL;
+    *nw = r[0];
+    return FK_OK;
+}
+
+/* The 2048-slice row geometry of a 32-bit pass; `rows0` rows already
+   written (the fused walk's) before k_kpart's over n keys */
+static PartGeo sp_geo32(fk_engine *e, uint64_t rows0, uint64_t n) {
     PartGeo pg{};
     pg.nslices = 2048u;
     pg.split = 6u;   /* 2^21-bin coarse slices, 64 parts of 2^15 */
     pg.batch = KP_BATCH;
     const uint32_t grid = (uint32_t)std::max(1, e->cus);
     pg.rounds = (uint32_t)((n + (uint64_t)grid * KP_BATCH - 1) / ((uint64_t)grid * KP_BATCH));
-    pg.rows = grid * pg.rounds;
+    pg.rows = (uint32_t)rows0 + grid * pg.rounds;
     pg.flag = nullptr;
-    const uint64_t ncodes = (uint64_t)pg.rows * KP_BATCH;   /* u32 codes */
-    const uint32_t nparts = 2048u << 6;
-    int rc = sp_ensure((void **)&e->d_codes, &e->codes_cap, 2 * ncodes, sizeof(uint16_t));
-    if (!rc) rc = sp_ensure((void **)&e->d_pidx, &e->pidx_cap, (uint64_t)pg.rows * 2048u, sizeof(uint32_t));
-    if (!rc) rc = sp_ensure((void **)&e->d_parts, &e->parts_cap, n + 8ull * nparts + 16, sizeof(uint16_t));
-    if (rc) return rc;
-    if (!e->d_pmeta && hipMalloc(&e->d_pmeta, (size_t)2048 * REPART_METAP * sizeof(PartMeta) + 64) != hipSuccess)
-        return FK_E_OOM;
-    PoolScratch flags(e, 0), slots(e, 1), fl(e, 2), res(e, 3);
-    if (!flags.alloc((size_t)(nparts + 1) * 8) || !slots.alloc((size_t)KP_SLOTS * KP_SLOT_W * 8) ||
-        !fl.alloc((size_t)nparts * 16) || !res.alloc(16))
-        return FK_E_OOM;
-    pg.codes = e->d_codes;
-    pg.idx = e->d_pidx;
-    PartMeta *meta = static_cast<PartMeta *>(e->d_pmeta);
-    unsigned long long *alloc = reinterpret_cast<unsigned long long *>(meta + (size_t)2048 * REPART_METAP);
-    HIPCHK(hipMemsetAsync(alloc, 0, 2 * sizeof(unsigned long long), e->stream));
-    HIPCHK(hipMemsetAsync(flags.p, 0, (size_t)(nparts + 1) * 8, e->stream));   /* (+ the block tickets) */
-    HIPCHK(hipMemsetAsync(slots.p, 0, (size_t)KP_SLOTS * KP_SLOT_W * 8, e->stream));
-    HIPCHK(hipMemsetAsync(res.p, 0, 16, e->stream));
-    unsigned long long *tcount = res.as<unsigned long long>() + 1;
-    hipLaunchKernelGGL(k_kpart<uint32_t>, dim3(grid), dim3(1024), (size_t)KP_BATCH * 4, e->stream, keys, n, pg, 0ull,
+    return pg;
+}
+
+/* k_kpart over the n 32-bit keys into rows [rows0, pg.rows) of pg */
+static int sp_kpart32(fk_engine *e, const PartGeo &pg, uint64_t rows0, const uint32_t *keys, uint64_t n,
+                      unsigned long long *tcount) {
+    if (!n) return FK_OK;
+    PartGeo g = pg;
+    g.codes = reinterpret_cast<uint16_t *>(reinterpret_cast<uint32_t *>(pg.codes) + rows0 * KP_BATCH);
+    g.idx = pg.idx + rows0 * 2048u;
+    const uint32_t grid = (uint32_t)std::max(1, e->cus);
+    hipLaunchKernelGGL(k_kpart<uint32_t>, dim3(grid), dim3(1024), (size_t)KP_BATCH * 4, e->stream, keys, n, g, 0ull,
                        0ull, 21u, 0xFFFFFFFFull, tcount);
     HIPCHK(hipGetLastError());
-    hipLaunchKernelGGL(k_repart<uint16_t>, dim3(2048u / REPART_G), dim3(1024), 0, e->stream, pg, e->d_parts, alloc,
-                       meta, (uint64_t)e->parts_cap, alloc + 1, 15u, nullptr);
-    HIPCHK(hipGetLastError());
-    hipLaunchKernelGGL(k_kp_count<KC_NT>, dim3(nparts), dim3(KC_NT), (size_t)KC_WORDS * 4, e->stream, (const uint16_t *)e->d_parts,
-                       (const PartMeta *)meta, (uint64_t)e->parts_cap, lo, npads, (const unsigned long long *)tcount, nparts,
-                       k, flags.as<unsigned long long>(), out_k, out_c, slots.as<unsigned long long>(), fl.as<uint64_t>(),
-                       alloc + 1);
-    HIPCHK(hipGetLastError());
-    hipLaunchKernelGGL(k_kp_fold, dim3(64), dim3(256), 0, e->stream, (const unsigned long long *)slots.p,
-                       (const uint64_t *)fl.p, nparts, k, (const unsigned long long *)flags.p, dacc,
-                       res.as<unsigned long long>());
-    HIPCHK(hipGetLastError());
-    unsigned long long r[2] = {0, 0};
-    HIPCHK(hipMemcpyAsync(&r[0], res.p, 8, hipMemcpyDeviceToHost, e->stream));
-    HIPCHK(hipMemcpyAsync(&r[1], alloc + 1, 8, hipMemcpyDeviceToHost, e->stream));
-    HIPCHK(hipStreamSynchronize(e->stream));
-    if (r[1]) return FK_E_INTERNAL;
-    *nw = r[0];
     return FK_OK;
+}
+
+/* The pass (keys lo + r for the n 32-bit r, npads of them the pad
+   0xFFFFFFFF) into its runs at out_k / out_c: *nw of them */
+int sp_count_runs32(fk_engine *e, const uint32_t *keys, uint64_t n, uint64_t lo, uint64_t npads,
+                           unsigned long long *dacc, uint64_t *out_k, uint32_t *out_c, uint64_t *nw) {
+    *nw = 0;
+    if (n == 0) return FK_OK;
+    PartGeo pg = sp_geo32(e, 0, n);
+    const uint64_t ncodes = (uint64_t)pg.rows * KP_BATCH;   /* u32 codes */
+    int rc = sp_ensure((void **)&e->d_codes, &e->codes_cap, 2 * ncodes, sizeof(uint16_t));
+    if (!rc) rc = sp_ensure((void **)&e->d_pidx, &e->pidx_cap, (uint64_t)pg.rows * 2048u, sizeof(uint32_t));
+    if (rc) return rc;
+    pg.codes = e->d_codes;
+    pg.idx = e->d_pidx;
+    PoolScratch res(e, 3);
+    if (!res.alloc(16)) return FK_E_OOM;
+    HIPCHK(hipMemsetAsync(res.p, 0, 16, e->stream));
+    unsigned long long *r = res.as<unsigned long long>();
+    rc = sp_kpart32(e, pg, 0, keys, n, r + 1);
+    if (!rc) rc = sp_count_rows32(e, pg, n, lo, npads, r, dacc, out_k, out_c, nw);
+    return rc;
 }
 
 /* A wide pass (keys[0, n) in [lo, hi), hi - lo > 2^32, npads of them the
@@ -1363,6 +1754,11 @@ int sparse_finish(fk_engine *e, int32_t seq) {
 
     struct Pass { uint32_t b0, b1; uint64_t n; bool dense; };
     std::vector<Pass> passes;
+    /* k = 17: the fused walks (k_sp_wpart) unless FINDKMER_TUNE sp_walk=0,
+       or sp_pass (a test knob of the key-list passes) is set */
+    uint64_t kv = 1;
+    const bool fused = k == 17 && wins > 0 && !e->sp_pass && (!tune_knob("sp_walk", &kv) || kv != 0);
+    auto plan = [&]() -> int {
     if (single) {
         passes.push_back({0, nbk, wins, false});
     } else {
@@ -1421,6 +1817,12 @@ int sparse_finish(fk_engine *e, int32_t seq) {
             b = b1;
         }
     }
+    return FK_OK;
+    };
+    if (!fused) {
+        int rc = plan();
+        if (rc) return rc;
+    }
 
     /* 3. the passes.  Consecutive sorted or counted passes share one walk
        (up to SP_MAXP key ranges, their lists side by side in d_emit) as
@@ -1451,6 +1853,141 @@ int sparse_finish(fk_engine *e, int32_t seq) {
         e->sp_distinct += nw;
         return FK_OK;
     };
+    /* k = 17: the four first-base passes, each a walk that partitions its
+       windows (k_sp_wpart) + the general tiles' list (k_kpart), then
+       k_repart / k_kp_count; SP_RETRY: a row or list overflowed, or it does
+       not fit -- the key-list passes instead */
+    auto walk17 = [&]() -> int {
+        const uint32_t grid = (uint32_t)std::max(1, e->cus);
+        uint64_t nbatch = 0, ntiles = 0;   /* batches of all blocks: one row each (+ a row per KP_BATCH windows) */
+        std::vector<SpSegDev> hsegs;
+        for (const auto &sg : e->spsegs) {
+            hsegs.push_back({sg.src ? sg.src : e->d_keep + sg.off, sg.len});
+            if (!sg.nranges) continue;
+            const uint64_t rpw = (sg.nranges + (uint64_t)grid * 16 - 1) / ((uint64_t)grid * 16);
+            const uint64_t tpr = (sg.cpw * FK_CHUNK_BYTES + FK_TILE_BYTES - 1) / FK_TILE_BYTES;
+            nbatch += (uint64_t)grid * ((rpw * tpr + WP_NT - 1) / WP_NT + 1);
+            ntiles += (sg.len + FK_TILE_BYTES - 1) / FK_TILE_BYTES + sg.nranges;
+        }
+        /* rows for a pass of up to half the windows, general-tile windows
+           of up to an eighth, a quarter of the tiles recorded
+           (FINDKMER_TUNE sp_walk_rows / sp_walk_glist: tests) */
+        uint64_t rows_walk = nbatch + wins / 2 / KP_BATCH + 1, gcap = wins / 8 + (1u << 20), kv2 = 0;
+        if (tune_knob("sp_walk_rows", &kv2)) rows_walk = kv2;
+        if (tune_knob("sp_walk_glist", &kv2)) gcap = std::max<uint64_t>(1, kv2);
+        const uint64_t dcap = ntiles / 4 + 1024;
+        const uint64_t grows = (uint64_t)grid * ((gcap + (uint64_t)grid * KP_BATCH - 1) / ((uint64_t)grid * KP_BATCH));
+        const uint64_t rows_all = rows_walk + grows;
+        const uint64_t need = rows_all * (KP_BATCH * 4ull + 2048ull * 4) + gcap * 4 + dcap * sizeof(SpDefer) +
+                              2 * wins + 16ull * (2048u << 6);
+        if (need > room || rows_all > 0xFFFFFFFFull) return SP_RETRY;
+        int rc = sp_ensure((void **)&e->d_codes, &e->codes_cap, 2 * rows_all * KP_BATCH, sizeof(uint16_t));
+        if (!rc) rc = sp_ensure((void **)&e->d_pidx, &e->pidx_cap, rows_all * 2048u, sizeof(uint32_t));
+        if (rc) return rc;
+        PoolScratch wc(e, 10), gl(e, 11), dfr(e, 12), sgd(e, 13), res(e, 3);
+        if (!wc.alloc(128) || !dfr.alloc(dcap * sizeof(SpDefer)) || !sgd.alloc(hsegs.size() * sizeof(SpSegDev) + 16) ||
+            !res.alloc(16))
+            return FK_E_OOM;
+        if (nodes && !shorts.alloc((scap + 1) * 8)) return FK_E_OOM;
+        unsigned long long *wctr = wc.as<unsigned long long>(), *r = res.as<unsigned long long>();
+        unsigned long long *gctr = wctr + 8;   /* k_sp_gtiles: [0..3] windows per first base, [4] short walks */
+        uint64_t *goff_d = reinterpret_cast<uint64_t *>(wctr + 12);
+        HIPCHK(hipMemcpyAsync(sgd.p, hsegs.data(), hsegs.size() * sizeof(SpSegDev), hipMemcpyHostToDevice, e->stream));
+        HIPCHK(hipFuncSetAttribute((const void *)k_sp_wpart, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   (int)(KP_BATCH * 4)));
+        const uint32_t dbg = tune_knob("sp_walk_dbg", &kv2) ? (uint32_t)kv2 : 0u;
+        uint64_t gn[4] = {0, 0, 0, 0}, goff[4] = {0, 0, 0, 0};
+        for (uint32_t q = 0; q < 4; q++) {
+            HIPCHK(hipMemsetAsync(wctr, 0, 64, e->stream));
+            HIPCHK(hipMemsetAsync(r, 0, 16, e->stream));
+            SpWalk wk{};
+            wk.qdig = q ^ (q >> 1);   /* (fk_sigma of one digit) */
+            wk.codes = reinterpret_cast<uint32_t *>(e->d_codes);
+            wk.idx = e->d_pidx;
+            wk.ctr = wctr;
+            wk.rows_cap = rows_walk;
+            wk.defer = q == 0 ? dfr.as<SpDefer>() : nullptr;
+            wk.defer_cap = dcap;
+            wk.dbg = dbg;
+            for (size_t si = 0; si < e->spsegs.size(); si++) {
+                const auto &sg = e->spsegs[si];
+                if (!sg.nranges) continue;
+                wk.seg = (uint32_t)si;
+                hipLaunchKernelGGL(k_sp_wpart, dim3(grid), dim3(1024), (size_t)KP_BATCH * 4, e->stream, hsegs[si].src,
+                                   sg.len, e->k, e->maskk, e->d_kst + sg.st, sg.nranges, sg.cpw, sg.nchunks, wk);
+                HIPCHK(hipGetLastError());
+            }
+            unsigned long long c[5];   /* rows, tiles deferred, -, windows in rows, faults */
+            HIPCHK(hipMemcpyAsync(c, wctr, sizeof c, hipMemcpyDeviceToHost, e->stream));
+            HIPCHK(hipStreamSynchronize(e->stream));
+            if (c[4] || c[0] > rows_walk) return SP_RETRY;
+            if (q == 0) {   /* the deferred tiles: windows per first base and short walks, then listed */
+                if (c[1] > dcap) return SP_RETRY;
+                unsigned long long g[5] = {0, 0, 0, 0, 0};
+                if (c[1]) {
+                    const unsigned gg = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((c[1] + SP_WAVES - 1) / SP_WAVES,
+                                                                                         (uint64_t)e->cus * 8));
+                    const size_t lds = (size_t)SP_WAVES * FK_TILE_BYTES * sizeof(uint64_t);
+                    HIPCHK(hipFuncSetAttribute((const void *)k_sp_gtiles<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+                    HIPCHK(hipFuncSetAttribute((const void *)k_sp_gtiles<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+                    HIPCHK(hipMemsetAsync(gctr, 0, 40, e->stream));
+                    hipLaunchKernelGGL(k_sp_gtiles<false>, dim3(gg), dim3(SP_WAVES * 64u), lds, e->stream,
+                                       (const SpDefer *)dfr.p, (uint64_t)c[1], (const SpSegDev *)sgd.p, e->k, e->maskk,
+                                       (uint32_t *)nullptr, (const uint64_t *)nullptr, gctr,
+                                       nodes ? shorts.as<uint64_t>() : nullptr, scap);
+                    HIPCHK(hipGetLastError());
+                    HIPCHK(hipMemcpyAsync(g, gctr, sizeof g, hipMemcpyDeviceToHost, e->stream));
+                    HIPCHK(hipStreamSynchronize(e->stream));
+                    uint64_t tot = 0;
+                    for (int j = 0; j < 4; j++) {
+                        gn[j] = g[j];
+                        goff[j] = tot;
+                        tot += g[j];
+                        if (g[j] > gcap) return SP_RETRY;
+                    }
+                    if (nodes && g[4] > scap) return SP_RETRY;
+                    if (tot) {
+                        if (!gl.alloc(tot * 4)) return FK_E_OOM;
+                        HIPCHK(hipMemcpyAsync(goff_d, goff, sizeof goff, hipMemcpyHostToDevice, e->stream));
+                        HIPCHK(hipMemsetAsync(gctr, 0, 32, e->stream));
+                        hipLaunchKernelGGL(k_sp_gtiles<true>, dim3(gg), dim3(SP_WAVES * 64u), lds, e->stream,
+                                           (const SpDefer *)dfr.p, (uint64_t)c[1], (const SpSegDev *)sgd.p, e->k, e->maskk,
+                                           gl.as<uint32_t>(), (const uint64_t *)goff_d, gctr, (uint64_t *)nullptr, scap);
+                        HIPCHK(hipGetLastError());
+                    }
+                }
+                ns = nodes ? g[4] : 0;
+                rc = prep_shorts();
+                if (rc) return rc;
+            }
+            if (c[3] + gn[q] == 0) continue;
+            PartGeo pg = sp_geo32(e, c[0], gn[q]);
+            pg.codes = e->d_codes;
+            pg.idx = e->d_pidx;
+            if (pg.rows > rows_all) return FK_E_INTERNAL;   /* (cannot happen: grows rows hold gcap keys) */
+            uint64_t nw = 0;
+            uint64_t *ok = e->d_spk + e->sp_distinct;
+            uint32_t *oc = e->d_spc + e->sp_distinct;
+            rc = sp_kpart32(e, pg, c[0], gl.as<uint32_t>() + goff[q], gn[q], r + 1);
+            if (!rc) rc = sp_count_rows32(e, pg, c[3] + gn[q], (uint64_t)q << 32, 0, r, dacc, ok, oc, &nw);
+            if (!rc) rc = join(ok, nw);
+            if (rc) return rc;
+        }
+        return FK_OK;
+    };
+    if (fused) {
+        int rc = walk17();
+        if (rc == SP_RETRY) {   /* from the start, by the key-list passes */
+            e->sp_distinct = 0;
+            HIPCHK(hipMemsetAsync(dacc, 0, FKS_ACC_N * sizeof(unsigned long long), e->stream));
+            prev_last = 0;
+            have_prev = false;
+            std::fill(edges.begin(), edges.end(), 0ull);
+            ns = 0;
+            rc = plan();
+        }
+        if (rc) return rc;
+    }
     for (size_t pi = 0; pi < passes.size();) {
         const Pass &p0 = passes[pi];
         uint64_t *out_k = e->d_spk + e->sp_distinct;   /* this pass's runs follow the earlier ones' */

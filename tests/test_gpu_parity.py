@@ -995,6 +995,24 @@ def test_sparse_count_bins_wrap_and_top_key(k):
     assert_same_sparse(b">w\n" + lines + b"\n", k)
 
 
+@pytest.mark.parametrize("tune", ["sp_walk=0", "sp_walk_rows=1", "sp_walk_glist=1"])
+def test_sparse_k17_walk_fallbacks(tune, monkeypatch):
+    """k = 17's fused walks (k_sp_wpart) against the key-list passes:
+    sp_walk=0 takes the key lists; a row or general-tile list capacity of 1
+    overflows in the first walk and the finish restarts by the key lists"""
+    monkeypatch.setenv("FINDKMER_TUNE", tune)
+    assert_same_sparse(mixed_input(1717, 300_000), 17)
+
+
+def test_sparse_k17_walk_rows_split():
+    """a batch of the fused walk with more windows of its pass than a row
+    holds (poly-A: every window is key 0, 16 x 3 x 2048 of them a batch) is
+    written as several rows; poly-T puts them all into the last pass"""
+    body = b"A" * 400_000 + b"C" * 5 + b"T" * 300_000
+    lines = b"\n".join(body[i:i + 61] for i in range(0, len(body), 61))
+    assert_same_sparse(b">s\n" + lines + b"\n", 17)
+
+
 def test_sparse_shared_walk_falls_back_alone(monkeypatch):
     """k=20, sp_pass=300000: ~4 wide passes share one emit walk; the first
     holds a poly-A stretch (100k windows of key 0, one part past k_kp_sort's
