@@ -496,7 +496,13 @@ k_kpart(const KT *keys, uint64_t n, PartGeo pg, uint64_t lo, uint64_t hi, uint32
  * route instead.
  */
 #define SP_RETRY 1000      /* (host) the fused walks gave up: the key-list passes instead */
-#define WP_NT 3u            /* tiles per wave per batch: ~24 K of a row's 32 K on random input */
+/* tiles per wave per batch, and the row: 16 x 4 x 2048 windows, a quarter
+   of them (~32.8 K) in the pass on random input, in rows of 36 K codes
+   (145 KiB of the 160 KiB of LDS).  Round 6: 3 tiles in 32 K rows filled
+   them three quarters, and k_repart, reading runs of ~12 codes, took 14.4
+   ms a pass against 12.7 for full rows */
+#define WP_NT 4u
+#define WP_BATCH 36352u
 #define WP_FAULT 1ull
 /* a tile the fast path did not take: where (its segment, offset) and its
    entering state */
@@ -506,7 +512,7 @@ struct SpDefer {
 };
 struct SpWalk {
     uint32_t qdig;                 /* the pass's first base in the internal encoding */
-    uint32_t *codes;               /* rows of KP_BATCH codes (k_kpart's layout) */
+    uint32_t *codes;               /* rows of WP_BATCH codes (k_kpart's layout) */
     uint32_t *idx;                 /* [row][2048] run words */
     unsigned long long *ctr;       /* [0] rows claimed, [1] tiles deferred, [3] windows placed in rows,
                                       [4] faults */
@@ -553,7 +559,7 @@ __device__ __forceinline__ void wp_tile(const WpTile &x, uint32_t qdig, uint32_t
                     if (in[j]) p[j] = atomicAdd(&cur[b[j]], 1u);
 #pragma unroll
                 for (int j = 0; j < 8; j++)
-                    if (in[j] && p[j] < KP_BATCH) ent[p[j]] = cd[j];
+                    if (in[j] && p[j] < WP_BATCH) ent[p[j]] = cd[j];
             }
         }
     }
@@ -562,10 +568,10 @@ __device__ __forceinline__ void wp_tile(const WpTile &x, uint32_t qdig, uint32_t
 __global__ void __launch_bounds__(1024, 1)
 k_sp_wpart(const uint8_t *buf, uint64_t len, int k, uint64_t maskk, const XState *rst, uint64_t nranges, uint64_t cpw,
            uint64_t nchunks, SpWalk wk) {
-    __shared__ uint32_t hist[2048], cur[2048], vst[2048], wtot[16];
+    __shared__ uint32_t hist[2048], cur[2048], wtot[16];
     __shared__ uint32_t s_total;
     __shared__ unsigned long long s_row;
-    extern __shared__ uint32_t ent[];   /* KP_BATCH codes */
+    extern __shared__ uint32_t ent[];   /* WP_BATCH codes */
     const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6;
     for (uint32_t i = t; i < 2048u; i += 1024u) hist[i] = 0;
     __syncthreads();
@@ -648,8 +654,17 @@ k_sp_wpart(const uint8_t *buf, uint64_t len, int k, uint64_t maskk, const XState
             if ((x.fl & 1u) && (sel == ~0u || sel == i)) wp_tile<true>(x, wk.qdig, hist, cur, ent);
         }
     };
-    /* sorted starts (two slices a thread, a block scan), the counts cleared
-       for the next histogram; returns the total */
+    /* a new row, claimed by thread 0 (seen by all after the next barrier) */
+    auto wp_claim = [&]() {
+        if (t == 0) {
+            const unsigned long long rw = atomicAdd(&wk.ctr[0], 1ull);
+            s_row = rw;
+            if (rw >= wk.rows_cap) atomicOr(&wk.ctr[4], WP_FAULT);
+        }
+    };
+    /* sorted starts (two slices a thread, a block scan) as cursors and as
+       the row's run words, the counts cleared for the next histogram;
+       returns the total (past WP_BATCH the run words are rewritten) */
     auto wp_scan = [&]() -> uint32_t {
         const uint32_t b = 2u * t, n0 = hist[b], n1 = hist[b + 1u], sum = n0 + n1;
         const uint32_t inc = wscan_incl32(sum);
@@ -658,34 +673,20 @@ k_sp_wpart(const uint8_t *buf, uint64_t len, int k, uint64_t maskk, const XState
         uint32_t run = inc - sum;
 #pragma unroll
         for (uint32_t w = 0; w < 16u; w++) run += w < wv ? wtot[w] : 0u;
-        vst[b] = run;
-        vst[b + 1u] = run + n0;
         cur[b] = run;
         cur[b + 1u] = run + n0;
         hist[b] = 0;
         hist[b + 1u] = 0;
+        const unsigned long long row = s_row;
+        if (row < wk.rows_cap && run + sum <= 65536u)
+            reinterpret_cast<uint2 *>(wk.idx + (size_t)row * 2048u)[t] = make_uint2(run_word(run, n0), run_word(run + n0, n1));
         if (t == 1023u) s_total = run + sum;
         __syncthreads();
         return s_total;
     };
-    /* the sorted windows (T <= KP_BATCH) as one row: claimed, run words,
-       placed, written out */
+    /* the stashed windows (sel: one slot, or ~0 all; T <= WP_BATCH of them)
+       placed and written out as the claimed row */
     auto wp_row = [&](uint32_t sel, uint32_t T) {
-        if (T == 0) return;
-        if (t == 0) {
-            const unsigned long long rw = atomicAdd(&wk.ctr[0], 1ull);
-            s_row = rw;
-            if (rw >= wk.rows_cap) atomicOr(&wk.ctr[4], WP_FAULT);
-            atomicAdd(&wk.ctr[3], (unsigned long long)T);
-        }
-        __syncthreads();
-        const unsigned long long row = s_row;
-        const bool ok = row < wk.rows_cap;
-        if (ok) {
-            const uint32_t b = 2u * t, e2 = b + 2u < 2048u ? vst[b + 2u] : T;
-            reinterpret_cast<uint2 *>(wk.idx + (size_t)row * 2048u)[t] =
-                make_uint2(run_word(vst[b], vst[b + 1u] - vst[b]), run_word(vst[b + 1u], e2 - vst[b + 1u]));
-        }
 #pragma unroll 1
         for (uint32_t i = 0; i < WP_NT; i++) {
             WpTile x = xs[0];
@@ -695,8 +696,10 @@ k_sp_wpart(const uint8_t *buf, uint64_t len, int k, uint64_t maskk, const XState
             if ((x.fl & 1u) && (sel == ~0u || sel == i)) wp_tile<false>(x, wk.qdig, hist, cur, ent);
         }
         __syncthreads();
-        if (ok) {
-            uint4 *dst = reinterpret_cast<uint4 *>(wk.codes + (size_t)row * KP_BATCH);
+        const unsigned long long row = s_row;
+        if (row < wk.rows_cap) {
+            if (t == 0) atomicAdd(&wk.ctr[3], (unsigned long long)T);
+            uint4 *dst = reinterpret_cast<uint4 *>(wk.codes + (size_t)row * WP_BATCH);
             const uint4 *src = reinterpret_cast<const uint4 *>(ent);
             for (uint32_t i = t; i < (T + 3u) / 4u; i += 1024u) dst[i] = src[i];
         }
@@ -710,21 +713,24 @@ k_sp_wpart(const uint8_t *buf, uint64_t len, int k, uint64_t maskk, const XState
             for (uint32_t i = 0; i < WP_NT; i++)
                 if (u == i) xs[i] = x;
         }
+        wp_claim();   /* (a batch without windows leaves an empty row) */
         wp_hist(~0u);
         /* (the barrier also tells whether any wave has tiles left) */
         const bool more = __syncthreads_or(!done);
         const uint32_t T = wp_scan();
-        if (T <= KP_BATCH) {
-            wp_row(~0u, T);
+        if (T <= WP_BATCH) {
+            if (T) wp_row(~0u, T);
         } else {
-            /* more windows of the pass than a row holds: one row per stash
-               slot (16 x 2048 windows at most), each counted again on its
-               own.  (Splitting the batch's sorted order at KP_BATCH instead
-               let the atomics' order decide which of a straddling slice's
-               entries fell before the split -- differently in each row's
-               placement: an entry twice, another lost.) */
+            /* more windows of the pass than a row holds (skewed input): one
+               row per stash slot (16 x 2048 windows at most), each counted
+               again on its own.  (Splitting the batch's sorted order at the
+               row size instead let the atomics' order decide which of a
+               straddling slice's entries fell before the split --
+               differently in each row's placement: an entry twice, another
+               lost.) */
 #pragma unroll 1
             for (uint32_t i = 0; i < WP_NT; i++) {
+                if (i) wp_claim();
                 wp_hist(i);
                 __syncthreads();
                 wp_row(i, wp_scan());
@@ -1495,13 +1501,14 @@ static int sp_count_rows32(fk_engine *e, const PartGeo &pg, uint64_t n, uint64_t
     return FK_OK;
 }
 
-/* The 2048-slice row geometry of a 32-bit pass; `rows0` rows already
-   written (the fused walk's) before k_kpart's over n keys */
-static PartGeo sp_geo32(fk_engine *e, uint64_t rows0, uint64_t n) {
+/* The 2048-slice row geometry of a 32-bit pass (rows of `batch` codes);
+   `rows0` rows already written (the fused walk's) before k_kpart's over n
+   keys */
+static PartGeo sp_geo32(fk_engine *e, uint64_t rows0, uint64_t n, uint32_t batch = KP_BATCH) {
     PartGeo pg{};
     pg.nslices = 2048u;
     pg.split = 6u;   /* 2^21-bin coarse slices, 64 parts of 2^15 */
-    pg.batch = KP_BATCH;
+    pg.batch = batch;
     const uint32_t grid = (uint32_t)std::max(1, e->cus);
     pg.rounds = (uint32_t)((n + (uint64_t)grid * KP_BATCH - 1) / ((uint64_t)grid * KP_BATCH));
     pg.rows = (uint32_t)rows0 + grid * pg.rounds;
@@ -1514,7 +1521,7 @@ static int sp_kpart32(fk_engine *e, const PartGeo &pg, uint64_t rows0, const uin
                       unsigned long long *tcount) {
     if (!n) return FK_OK;
     PartGeo g = pg;
-    g.codes = reinterpret_cast<uint16_t *>(reinterpret_cast<uint32_t *>(pg.codes) + rows0 * KP_BATCH);
+    g.codes = reinterpret_cast<uint16_t *>(reinterpret_cast<uint32_t *>(pg.codes) + rows0 * pg.batch);
     g.idx = pg.idx + rows0 * 2048u;
     const uint32_t grid = (uint32_t)std::max(1, e->cus);
     hipLaunchKernelGGL(k_kpart<uint32_t>, dim3(grid), dim3(1024), (size_t)KP_BATCH * 4, e->stream, keys, n, g, 0ull,
@@ -1859,7 +1866,7 @@ int sparse_finish(fk_engine *e, int32_t seq) {
        not fit -- the key-list passes instead */
     auto walk17 = [&]() -> int {
         const uint32_t grid = (uint32_t)std::max(1, e->cus);
-        uint64_t nbatch = 0, ntiles = 0;   /* batches of all blocks: one row each (+ a row per KP_BATCH windows) */
+        uint64_t nbatch = 0, ntiles = 0;   /* batches of all blocks: a row each (+ one per WP_BATCH windows) */
         std::vector<SpSegDev> hsegs;
         for (const auto &sg : e->spsegs) {
             hsegs.push_back({sg.src ? sg.src : e->d_keep + sg.off, sg.len});
@@ -1872,16 +1879,16 @@ int sparse_finish(fk_engine *e, int32_t seq) {
         /* rows for a pass of up to half the windows, general-tile windows
            of up to an eighth, a quarter of the tiles recorded
            (FINDKMER_TUNE sp_walk_rows / sp_walk_glist: tests) */
-        uint64_t rows_walk = nbatch + wins / 2 / KP_BATCH + 1, gcap = wins / 8 + (1u << 20), kv2 = 0;
+        uint64_t rows_walk = nbatch + wins / 2 / WP_BATCH + 1, gcap = wins / 8 + (1u << 20), kv2 = 0;
         if (tune_knob("sp_walk_rows", &kv2)) rows_walk = kv2;
         if (tune_knob("sp_walk_glist", &kv2)) gcap = std::max<uint64_t>(1, kv2);
         const uint64_t dcap = ntiles / 4 + 1024;
         const uint64_t grows = (uint64_t)grid * ((gcap + (uint64_t)grid * KP_BATCH - 1) / ((uint64_t)grid * KP_BATCH));
         const uint64_t rows_all = rows_walk + grows;
-        const uint64_t need = rows_all * (KP_BATCH * 4ull + 2048ull * 4) + gcap * 4 + dcap * sizeof(SpDefer) +
+        const uint64_t need = rows_all * (WP_BATCH * 4ull + 2048ull * 4) + gcap * 4 + dcap * sizeof(SpDefer) +
                               2 * wins + 16ull * (2048u << 6);
         if (need > room || rows_all > 0xFFFFFFFFull) return SP_RETRY;
-        int rc = sp_ensure((void **)&e->d_codes, &e->codes_cap, 2 * rows_all * KP_BATCH, sizeof(uint16_t));
+        int rc = sp_ensure((void **)&e->d_codes, &e->codes_cap, 2 * rows_all * WP_BATCH, sizeof(uint16_t));
         if (!rc) rc = sp_ensure((void **)&e->d_pidx, &e->pidx_cap, rows_all * 2048u, sizeof(uint32_t));
         if (rc) return rc;
         PoolScratch wc(e, 10), gl(e, 11), dfr(e, 12), sgd(e, 13), res(e, 3);
@@ -1894,7 +1901,7 @@ int sparse_finish(fk_engine *e, int32_t seq) {
         uint64_t *goff_d = reinterpret_cast<uint64_t *>(wctr + 12);
         HIPCHK(hipMemcpyAsync(sgd.p, hsegs.data(), hsegs.size() * sizeof(SpSegDev), hipMemcpyHostToDevice, e->stream));
         HIPCHK(hipFuncSetAttribute((const void *)k_sp_wpart, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                   (int)(KP_BATCH * 4)));
+                                   (int)(WP_BATCH * 4)));
         const uint32_t dbg = tune_knob("sp_walk_dbg", &kv2) ? (uint32_t)kv2 : 0u;
         uint64_t gn[4] = {0, 0, 0, 0}, goff[4] = {0, 0, 0, 0};
         for (uint32_t q = 0; q < 4; q++) {
@@ -1913,7 +1920,7 @@ int sparse_finish(fk_engine *e, int32_t seq) {
                 const auto &sg = e->spsegs[si];
                 if (!sg.nranges) continue;
                 wk.seg = (uint32_t)si;
-                hipLaunchKernelGGL(k_sp_wpart, dim3(grid), dim3(1024), (size_t)KP_BATCH * 4, e->stream, hsegs[si].src,
+                hipLaunchKernelGGL(k_sp_wpart, dim3(grid), dim3(1024), (size_t)WP_BATCH * 4, e->stream, hsegs[si].src,
                                    sg.len, e->k, e->maskk, e->d_kst + sg.st, sg.nranges, sg.cpw, sg.nchunks, wk);
                 HIPCHK(hipGetLastError());
             }
@@ -1961,7 +1968,7 @@ int sparse_finish(fk_engine *e, int32_t seq) {
                 if (rc) return rc;
             }
             if (c[3] + gn[q] == 0) continue;
-            PartGeo pg = sp_geo32(e, c[0], gn[q]);
+            PartGeo pg = sp_geo32(e, c[0], gn[q], WP_BATCH);
             pg.codes = e->d_codes;
             pg.idx = e->d_pidx;
             if (pg.rows > rows_all) return FK_E_INTERNAL;   /* (cannot happen: grows rows hold gcap keys) */

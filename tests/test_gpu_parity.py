@@ -1006,7 +1006,7 @@ def test_sparse_k17_walk_fallbacks(tune, monkeypatch):
 
 def test_sparse_k17_walk_rows_split():
     """a batch of the fused walk with more windows of its pass than a row
-    holds (poly-A: every window is key 0, 16 x 3 x 2048 of them a batch) is
+    holds (poly-A: every window is key 0, 16 x 4 x 2048 of them a batch) is
     written as several rows; poly-T puts them all into the last pass"""
     body = b"A" * 400_000 + b"C" * 5 + b"T" * 300_000
     lines = b"\n".join(body[i:i + 61] for i in range(0, len(body), 61))
