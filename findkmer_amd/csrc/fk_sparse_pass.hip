@@ -1,7 +1,8 @@
 /*
  * fk_sparse_pass.hip -- 17 <= k <= 20 (findKmer.cpp:429-445, :663-690): the
  * sparse table built at finish by key-range passes over the retained input
- * (k_sp_emit, then per pass k_kpart + k_repart + k_kp_count / k_kp_sort), and
+ * (k_sp_emit or k_sp_wpart, then per pass k_kpart + k_repart + k_kp_cnt2 /
+ * k_kp_sort), and
  * the sparse-table C-ABI (fk_engine_sparse*).
  */
 #include "fk_engine_internal.h"
@@ -352,7 +353,7 @@ int sp_emit_all(fk_engine *e, const SpEmit &em) {
  *                 row of run words);
  *   k_repart      (as for k = 15, 16) each coarse slice into 64 contiguous
  *                 part streams of 15-bit codes;
- *   k_kp_count    one block per part (2^15 bins, in key order): the part's
+ *   k_kp_cnt2     one block per part (2^15 bins, in key order): the part's
  *                 stream into LDS bins, the pads taken off the last bin, the
  *                 nonzero bins' offset from the parts before it (a chained
  *                 scan: each block publishes its distinct count, then looks
@@ -888,50 +889,59 @@ __device__ unsigned long long chain_prefix(unsigned long long *flags, uint32_t b
     return pre;
 }
 
-/* the bins of a part: thread t takes bins [32 t, 32 t + 32).  The 2^15
-   bins are 16-bit halves of 2^14 LDS words (64 KiB instead of 128: half the
-   zeroing and reading, 16.9 -> 13.1 ms per k = 17 pass; a second block per
-   CU would need <= 64 VGPRs, and forced there the spills made it 21 ms).  A half that wraps (a k-mer 65536 times in
-   one part) makes the halves' sum fall short of the codes: the part is then
-   counted again as two halves of 2^14 32-bit bins. */
+/* The part's 2^15 bins are 16-bit halves of 2^14 LDS words (64 KiB instead
+   of 128: half the zeroing and reading, 16.9 -> 13.1 ms per k = 17 pass in
+   round 5).  A half that wraps (a k-mer 65536 times in one part) makes the
+   halves' sum fall short of the codes: the part is then counted again as two
+   halves of 2^14 32-bit bins. */
 #define KC_WORDS (1u << 14)
-/* NT threads a block: 1024 (32 bins a thread, one block per CU).  (Round 6:
-   512 threads with 64 bins a thread, two blocks per CU so that one block's
-   barriers and chained-scan wait would overlap the other's count, needed
-   168 VGPRs; held to 128 they spilled 164 B a lane and the k = 17 step went
-   193 -> 213 ms) */
-#define KC_NT 1024u
-template <uint32_t NT>
-__global__ void __launch_bounds__(NT, NT == 512u ? 4 : 1)
-k_kp_count(const uint16_t *in, const PartMeta *meta, uint64_t cap_in, uint64_t lo, uint64_t npads,
-           const unsigned long long *tcount, uint32_t nparts, int k, unsigned long long *flags, uint64_t *out_k,
-           uint32_t *out_c, unsigned long long *slots, uint64_t *fl, unsigned long long *err) {
-    constexpr uint32_t NW = NT / 64u, BT = 32768u / NT;   /* waves; bins a thread */
+/*
+ * k_kp_cnt2: one block per part, two blocks per CU (round 6), so that one
+ * block's latency-bound phases -- the part's first loads, the barriers, the
+ * chained scan's wait, the output -- overlap the other's.  Round 5's
+ * k_kp_count held a thread's 32 bins in registers from the count to the
+ * output (114 VGPRs, one block per CU: 12.7 ms per k = 17 pass against
+ * 10.4 here); here the bins stay in LDS and are read twice, one 64-bin step of a wave's
+ * 2048 at a time (consecutive 16-bit bins a lane each: no bank conflicts):
+ * pass 1 takes the statistics, the wave's distinct count and its last
+ * nonzero bin; after the chained scan, pass 2 writes each step's nonzero
+ * bins compacted by a ballot (the wave's output one contiguous run) with
+ * the first differing base of each adjacent pair (the nearest nonzero bin
+ * below, in the step, the wave's earlier steps or the earlier waves).  A
+ * lane's bins all end in base lane & 3.  A wrapped 16-bit bin: the part
+ * counted again as two halves of 2^14 32-bit bins, each pass once per half
+ * (32 virtual waves of 1024 bins).
+ */
+#define KC2_VW 32u
+__global__ void __launch_bounds__(1024, 8)   /* 8 waves per SIMD: two blocks per CU */
+k_kp_cnt2(const uint16_t *in, const PartMeta *meta, uint64_t cap_in, uint64_t lo, uint64_t npads,
+          const unsigned long long *tcount, uint32_t nparts, int k, unsigned long long *flags, uint64_t *out_k,
+          uint32_t *out_c, unsigned long long *slots, uint64_t *fl, unsigned long long *err) {
     extern __shared__ uint32_t bins[];   /* KC_WORDS */
-    __shared__ unsigned long long wred[NW][10];
-    __shared__ uint32_t hpre[24];
-    __shared__ uint32_t wnz[NW], wmx[NW];
+    __shared__ uint32_t wnz[KC2_VW], wlast[KC2_VW], hpre[8], s_hs;
+    __shared__ unsigned long long wred[16][7];
     __shared__ unsigned long long bprefix;
     __shared__ uint32_t vblk;
     const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6;
-    /* the part: a ticket in the order blocks start (flags[nparts]), not
-       blockIdx -- the chained scan may only wait on blocks that are already
-       running, and across the 8 XCDs (and other processes' kernels)
-       blockIdx order is not start order */
-    if (t == 0) vblk = (uint32_t)atomicAdd(&flags[nparts], 1ull);
-    if (t < 24) hpre[t] = 0;
+    if (t == 0) {
+        /* the part: a ticket in the order blocks start, not blockIdx -- the
+           chained scan may only wait on blocks that are already running,
+           and across the 8 XCDs (and other processes' kernels) blockIdx
+           order is not start order */
+        vblk = (uint32_t)atomicAdd(&flags[nparts], 1ull);
+        s_hs = 0;
+    }
+    if (t < 8) hpre[t] = 0;
     __syncthreads();
     const uint32_t blk = vblk;
     PartMeta m = meta[blk];
-    if (m.off + m.n > cap_in) {   /* bound check (k_count_parts's) */
+    if (m.off + m.n > cap_in) {
         if (t == 0) atomicOr(err, (unsigned long long)FK_FAULT_META);
         m.n = 0;
         m.off = 0;
     }
     const uint4 *g4 = reinterpret_cast<const uint4 *>(in + m.off);
     const uint32_t nq = (m.n + 7u) >> 3;
-    /* each code to its bin, bin b at half b & 1 of word b >> 1 (hsel: the
-       32-bit pass of half h, bins [h 2^14, (h + 1) 2^14) only) */
     auto count8 = [&](const uint4 &v, uint32_t q, int hsel) {
         const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
@@ -942,103 +952,79 @@ k_kp_count(const uint16_t *in, const PartMeta *meta, uint64_t cap_in, uint64_t l
             else if ((b >> 14) == (uint32_t)hsel) atomicAdd(&bins[b & (KC_WORDS - 1u)], 1u);
         }
     };
-    auto count = [&](int hsel) {
-        for (uint32_t q = t; q < nq; q += NT) count8(g4[q], q, hsel);
+    auto zero = [&]() {
+        for (uint32_t i = t; i < KC_WORDS / 4u; i += 1024u) reinterpret_cast<uint4 *>(bins)[i] = make_uint4(0, 0, 0, 0);
     };
-    /* the part's first KP_U pieces per thread (32 K codes: most parts whole)
-       loaded before the bins are zeroed, so that the stream is in flight
-       while they are: one load at a time left the count latency-bound (7 of
-       the pass's 13 ms at k = 17, ablation kpx_nocnt) */
-    constexpr uint32_t KP_U = 4u;
-    uint4 pv[KP_U];
+    constexpr uint32_t KP_U = 2u;   /* (4: 10 VGPRs spilled at the 64 of two blocks per CU) */
+    {
+        uint4 pv[KP_U];
 #pragma unroll
-    for (uint32_t u = 0; u < KP_U; u++) pv[u] = t + u * NT < nq ? g4[t + u * NT] : make_uint4(0, 0, 0, 0);
-    for (uint32_t i = t; i < KC_WORDS / 4u; i += NT) reinterpret_cast<uint4 *>(bins)[i] = make_uint4(0, 0, 0, 0);
-    __syncthreads();
-#pragma unroll
-    for (uint32_t u = 0; u < KP_U; u++)
-        if (t + u * NT < nq) count8(pv[u], t + u * NT, -1);
-    for (uint32_t q0 = t + KP_U * NT; q0 < nq; q0 += KP_U * NT) {
-#pragma unroll
-        for (uint32_t u = 0; u < KP_U; u++) pv[u] = q0 + u * NT < nq ? g4[q0 + u * NT] : make_uint4(0, 0, 0, 0);
+        for (uint32_t u = 0; u < KP_U; u++) pv[u] = t + u * 1024u < nq ? g4[t + u * 1024u] : make_uint4(0, 0, 0, 0);
+        zero();
+        __syncthreads();
 #pragma unroll
         for (uint32_t u = 0; u < KP_U; u++)
-            if (q0 + u * NT < nq) count8(pv[u], q0 + u * NT, -1);
+            if (t + u * 1024u < nq) count8(pv[u], t + u * 1024u, -1);
+        for (uint32_t q0 = t + KP_U * 1024u; q0 < nq; q0 += KP_U * 1024u) {
+#pragma unroll
+            for (uint32_t u = 0; u < KP_U; u++) pv[u] = q0 + u * 1024u < nq ? g4[q0 + u * 1024u] : make_uint4(0, 0, 0, 0);
+#pragma unroll
+            for (uint32_t u = 0; u < KP_U; u++)
+                if (q0 + u * 1024u < nq) count8(pv[u], q0 + u * 1024u, -1);
+        }
     }
     __syncthreads();
-    /* thread t's BT bins: words [BT / 2 t, BT / 2 (t + 1)) */
-    uint32_t c[BT];
-    unsigned long long hs = 0;
-#pragma unroll
-    for (uint32_t j = 0; j < BT / 8u; j++) {
-        const uint4 q = reinterpret_cast<const uint4 *>(bins)[t * (BT / 8u) + j];
-        const uint32_t w4[4] = {q.x, q.y, q.z, q.w};
-#pragma unroll
-        for (int h = 0; h < 4; h++) {
-            c[8 * j + 2 * h] = w4[h] & 0xFFFFu;
-            c[8 * j + 2 * h + 1] = w4[h] >> 16;
-            hs += (w4[h] & 0xFFFFu) + (w4[h] >> 16);
-        }
-    }
-    {   /* the wrap check (block-wide: the halves' sum against the codes) */
-        const unsigned long long a = wsum64(hs);
-        if (lane == 0) wred[wv][0] = a;
-        __syncthreads();
-        unsigned long long sa = 0;
-#pragma unroll
-        for (uint32_t w = 0; w < NW; w++) sa += wred[w][0];
-        if (sa != (unsigned long long)m.n) {
-            for (int h = 0; h < 2; h++) {
-                __syncthreads();
-                for (uint32_t i = t; i < KC_WORDS / 4u; i += NT)
-                    reinterpret_cast<uint4 *>(bins)[i] = make_uint4(0, 0, 0, 0);
-                __syncthreads();
-                count(h);
-                __syncthreads();
-                if (((BT * t) >> 14) == (uint32_t)h) {   /* (thread t's bins lie in half BT t / 2^14) */
-#pragma unroll
-                    for (uint32_t j = 0; j < BT / 4u; j++) {
-                        const uint4 q = reinterpret_cast<const uint4 *>(bins)[((BT * t) & (KC_WORDS - 1u)) / 4u + j];
-                        c[4 * j] = q.x; c[4 * j + 1] = q.y; c[4 * j + 2] = q.z; c[4 * j + 3] = q.w;
-                    }
-                }
-            }
-        }
-        __syncthreads();   /* (wred is reused below) */
-    }
     /* the top key (relative 0xFFFFFFFF, the last bin of the last part) was
        only counted (k_kpart): its real windows, the pads taken off */
-    const unsigned long long extra = blk == nparts - 1u ? *tcount - npads : 0ull;
-    if (t == NT - 1u && extra) c[BT - 1] += (uint32_t)extra;
-    const int fs = 2 * (k - 1);
-    const uint64_t kb = lo + ((uint64_t)blk << 15) + t * BT;   /* key of my first bin (a multiple of 4) */
-    /* statistics with constant register indices (a runtime index into a
-       register array put it in scratch memory): bin j's last base is j & 3,
-       and the first base is the same for all BT bins */
-    uint32_t nz = 0;
-    unsigned long long l4[4] = {0, 0, 0, 0};
-#pragma unroll
-    for (uint32_t j = 0; j < BT; j++) {
-        nz += c[j] != 0;
-        l4[j & 3] += c[j];
+    const uint32_t extra = blk == nparts - 1u ? (uint32_t)(*tcount - npads) : 0u;
+    const uint64_t kpart = lo + ((uint64_t)blk << 15);
+    const uint32_t fd = (uint32_t)((kpart >> (2 * (k - 1))) & 3);
+    const uint16_t *b16 = reinterpret_cast<const uint16_t *>(bins);
+    /* bin i's count: 16-bit bins, or (wrap path, half h) 32-bit bins of [h 2^14, (h + 1) 2^14) */
+    auto rd = [&](uint32_t i, int wrap) -> uint32_t {
+        const uint32_t c = wrap ? bins[i & (KC_WORDS - 1u)] : (uint32_t)b16[i];
+        return c + (i == 32767u ? extra : 0u);
+    };
+    uint32_t nz = 0, hs = 0;
+    unsigned long long lsum = 0;
+    /* pass 1 over virtual wave vw's bins [i0, i0 + 64 nsteps) */
+    auto pass1 = [&](uint32_t vw, uint32_t i0, uint32_t nsteps, int wrap) {
+        uint32_t cnt = 0, last = ~0u;
+        for (uint32_t s = 0; s < nsteps; s++) {
+            const uint32_t i = i0 + 64u * s + lane;
+            const uint32_t c = rd(i, wrap);
+            hs += c - (i == 32767u ? extra : 0u);
+            nz += c != 0u;
+            lsum += c;
+            const unsigned long long bl = __ballot(c != 0u);
+            cnt += (uint32_t)__popcll(bl);
+            if (bl) last = i0 + 64u * s + 63u - (uint32_t)__clzll((long long)bl);
+        }
+        if (lane == 0) { wnz[vw] = cnt; wlast[vw] = last; }
+    };
+    pass1(wv, wv * 2048u, 32u, 0);
+    {
+        const uint32_t a = wsum32(hs);
+        if (lane == 0) atomicAdd(&s_hs, a);
     }
-    const unsigned long long sum = l4[0] + l4[1] + l4[2] + l4[3];
-    const uint32_t fd = (uint32_t)((kb >> fs) & 3);
-    unsigned long long st[10] = {nz, sum, l4[0], l4[1], l4[2], l4[3], fd == 0 ? sum : 0ull, fd == 1 ? sum : 0ull,
-                                 fd == 2 ? sum : 0ull, fd == 3 ? sum : 0ull};
-    /* block scan of the nonzero counts */
-    const uint32_t inc = wscan_incl32(nz);
-    if (lane == 63) wnz[wv] = inc;
     __syncthreads();
-    uint32_t before = 0, total = 0;
-#pragma unroll
-    for (uint32_t w = 0; w < NW; w++) {
-        const uint32_t x = wnz[w];
-        before += w < wv ? x : 0u;
-        total += x;
+    const bool wrap = s_hs != m.n;   /* a 16-bit bin wrapped: the halves' sum falls short of the codes */
+    if (wrap) {
+        nz = 0;
+        lsum = 0;
+        for (int h = 0; h < 2; h++) {
+            __syncthreads();
+            zero();
+            __syncthreads();
+            for (uint32_t q = t; q < nq; q += 1024u) count8(g4[q], q, h);
+            __syncthreads();
+            pass1(16u * h + wv, (uint32_t)h * 16384u + wv * 1024u, 16u, 1);
+        }
     }
-    const uint32_t off = before + inc - nz;
-    /* the parts' chained scan */
+    const uint32_t nvw = wrap ? 32u : 16u;
+    __syncthreads();
+    uint32_t total = 0;
+    for (uint32_t v = 0; v < nvw; v++) total += wnz[v];
     if (wv == 0) {
         const unsigned long long pre = chain_prefix(flags, blk, total, err);
         if (lane == 0) {
@@ -1046,99 +1032,86 @@ k_kp_count(const uint16_t *in, const PartMeta *meta, uint64_t cap_in, uint64_t l
             if (!total) fl[2 * (size_t)blk] = KP_EMPTY;
         }
     }
-    /* the nearest earlier thread holding a nonzero bin (an exclusive max
-       scan of t + 1), for the adjacent pair across threads */
-    const uint32_t im = wscan_max32(nz ? t + 1u : 0u);
-    if (lane == 63) wmx[wv] = im;
-    __syncthreads();   /* (also: every thread has its bins in registers) */
-    uint32_t pm = (uint32_t)__shfl_up((int)im, 1, 64);
-    if (lane == 0) pm = 0;
-    for (uint32_t w = 0; w < wv; w++) pm = max(pm, wmx[w]);
-    uint64_t first = 0, prev = 0;
-    bool have = false;
-    /* adjacent keys inside my BT <= 64 bins differ in one of the last three
-       bases (depths k, k - 1, k - 2): counted in registers */
-    uint32_t h0 = 0, h1 = 0, h2 = 0;
-#pragma unroll
-    for (uint32_t j = 0; j < BT; j++) {
-        if (c[j]) {
-            const uint64_t key = kb + j;
-            if (have) {   /* first differing base of adjacent keys (k_sp_wprefix) */
-                const uint32_t d = (uint32_t)(key ^ prev);   /* < BT */
-                h0 += d < 4u;
-                h1 += d >= 4u && d < 16u;
-                h2 += d >= 16u;
-            } else {
-                first = key;
-            }
-            prev = key;
-            have = true;
-        }
-    }
-    {
-        const uint32_t a0 = wsum32(h0), a1 = wsum32(h1), a2 = wsum32(h2);
-        if (lane == 0) {
-            if (a0) atomicAdd(&hpre[k], a0);
-            if (a1) atomicAdd(&hpre[k - 1], a1);
-            if (a2) atomicAdd(&hpre[k - 2], a2);
-        }
-    }
-    /* every thread's last key in the (now free) bins' LDS */
-    uint64_t *lastk = reinterpret_cast<uint64_t *>(bins);
-    lastk[t] = prev;
     __syncthreads();
-    if (nz && pm) {
-        const uint64_t pk = lastk[pm - 1u];
-        const int lz = __clzll((long long)(first ^ pk)) - (64 - 2 * k);
-        atomicAdd(&hpre[lz / 2 + 1], 1u);
-    }
-    if (nz && !pm) fl[2 * (size_t)blk] = first;
-    if (nz && off + nz == total) fl[2 * (size_t)blk + 1] = prev;
-    /* the nonzero bins out, in rounds of KC_STAGE entries staged in the
-       bins' LDS (bin index u16, count u32) and written as contiguous words:
-       one thread writing its own bins strided the stores 64 lines per
-       instruction, and the output (12 B per distinct k-mer, ~90 GB per
-       10 G-base step) cost more than the count */
-    constexpr uint32_t KC_STAGE = 8192u;   /* (u16 + u32 each: 48 KiB of the 64) */
-    uint16_t *sidx = reinterpret_cast<uint16_t *>(bins);
-    uint32_t *scnt = bins + KC_STAGE / 2u;
-    const uint64_t kpart = lo + ((uint64_t)blk << 15);
-    for (uint32_t r0 = 0; r0 < total; r0 += KC_STAGE) {
-        __syncthreads();   /* (the staging area is free: lastk read, or the last round written out) */
-        uint32_t o = off;
+    /* pass 2: the nonzero bins out, and the adjacent pairs' first differing base */
+    uint32_t hc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    auto pass2 = [&](uint32_t vw, uint32_t i0, uint32_t nsteps, int wrap) {
+        uint64_t o = bprefix;
+        uint32_t prev = ~0u;   /* the nearest nonzero bin below (none: the part's first) */
+        for (uint32_t v = 0; v < vw; v++) {
+            o += wnz[v];
+            if (wlast[v] != ~0u) prev = wlast[v];
+        }
+        for (uint32_t s = 0; s < nsteps; s++) {
+            const uint32_t i = i0 + 64u * s + lane;
+            const uint32_t c = rd(i, wrap);
+            const unsigned long long bl = __ballot(c != 0u);
+            if (c) {
+                const unsigned long long below = bl & ((1ull << lane) - 1ull);
+                const uint32_t at = (uint32_t)__popcll(below);
+                __builtin_nontemporal_store((uint64_t)(kpart + i), out_k + o + at);
+                __builtin_nontemporal_store(c, out_c + o + at);
+                const uint32_t p = below ? i - lane + 63u - (uint32_t)__clzll((long long)below) : prev;
+                if (p != ~0u) {
+                    const uint32_t j = 7u - (hibit(i ^ p) >> 1);   /* depth k - 7 + j */
 #pragma unroll
-        for (uint32_t j = 0; j < BT; j++) {
-            if (c[j]) {
-                if (o >= r0 && o < r0 + KC_STAGE) {
-                    sidx[o - r0] = (uint16_t)(t * BT + j);
-                    scnt[o - r0] = c[j];
+                    for (uint32_t q = 0; q < 8u; q++) hc[q] += j == q;
+                } else {
+                    fl[2 * (size_t)blk] = kpart + i;   /* the part's first key */
                 }
-                o++;
             }
+            o += (uint64_t)__popcll(bl);
+            if (bl) prev = i0 + 64u * s + 63u - (uint32_t)__clzll((long long)bl);
         }
-        __syncthreads();
-        const uint32_t nr = min(KC_STAGE, total - r0);
-        for (uint32_t i = t; i < nr; i += NT) {
-            __builtin_nontemporal_store((uint64_t)(kpart + sidx[i]), out_k + bprefix + r0 + i);
-            __builtin_nontemporal_store(scnt[i], out_c + bprefix + r0 + i);
+    };
+    if (!wrap) {
+        pass2(wv, wv * 2048u, 32u, 0);
+    } else {
+        for (int h = 0; h < 2; h++) {
+            __syncthreads();
+            zero();
+            __syncthreads();
+            for (uint32_t q = t; q < nq; q += 1024u) count8(g4[q], q, h);
+            __syncthreads();
+            pass2(16u * h + wv, (uint32_t)h * 16384u + wv * 1024u, 16u, 1);
         }
     }
-    /* the rollover check: a bin past 2^32 codes wrapped, so its sum falls
-       short of the codes (less the pads) */
-    unsigned long long v10[10];
+    /* the part's last key */
+    if (t == 0 && total) {
+        uint32_t last = 0;
+        for (uint32_t v = 0; v < nvw; v++)
+            if (wlast[v] != ~0u) last = wlast[v];
+        fl[2 * (size_t)blk + 1] = kpart + last;
+    }
 #pragma unroll
-    for (int q = 0; q < 10; q++) v10[q] = wsum64(st[q]);
-    if (lane == 0)
+    for (uint32_t q = 0; q < 8u; q++) {
+        const uint32_t a = wsum32(hc[q]);
+        if (lane == 0 && a) atomicAdd(&hpre[q], a);
+    }
+    /* statistics: distinct, sum, last-base marginals (lane & 3), first base fd */
+    {
+        unsigned long long v6[6];
+        v6[0] = wsum32(nz);
 #pragma unroll
-        for (int q = 0; q < 10; q++) wred[wv][q] = v10[q];
+        for (uint32_t d = 0; d < 4u; d++) {
+            const unsigned long long x = (lane & 3u) == d ? lsum : 0ull;
+            v6[2 + d] = wsum64(x);
+        }
+        v6[1] = v6[2] + v6[3] + v6[4] + v6[5];
+        if (lane == 0)
+#pragma unroll
+            for (int q = 0; q < 6; q++) wred[wv][q] = v6[q];
+    }
     __syncthreads();
     if (t < 10) {
         unsigned long long a = 0;
-        for (uint32_t w = 0; w < NW; w++) a += wred[w][t];
+        const uint32_t q = t < 6u ? t : 1u;   /* 6..9: the sum under first base fd */
+        for (uint32_t w = 0; w < 16u; w++) a += wred[w][q];
+        if (t >= 6u && t - 6u != fd) a = 0;
         if (a) atomicAdd(&slots[(blk % KP_SLOTS) * KP_SLOT_W + t], a);
         if (t == 1 && a != (uint64_t)m.n + extra) atomicOr(&slots[(blk % KP_SLOTS) * KP_SLOT_W + 10], 1ull);
     }
-    if (t < 24 && hpre[t]) atomicAdd(&slots[(blk % KP_SLOTS) * KP_SLOT_W + 11 + t], (unsigned long long)hpre[t]);
+    if (t < 8 && hpre[t]) atomicAdd(&slots[(blk % KP_SLOTS) * KP_SLOT_W + 11 + (k - 7 + (int)t)], (unsigned long long)hpre[t]);
 }
 
 /*
@@ -1247,7 +1220,7 @@ k_kp_sort(const uint32_t *in, const PartMeta *meta, uint64_t cap_in, uint64_t lo
     if (t < 24) hpre[t] = 0;
     if (t == 0) {
         bad = 0;
-        vblk = (uint32_t)atomicAdd(&flags[nparts], 1ull);   /* (k_kp_count: start order) */
+        vblk = (uint32_t)atomicAdd(&flags[nparts], 1ull);   /* (k_kp_cnt2: start order) */
     }
     __syncthreads();
     const uint32_t blk = vblk;
@@ -1460,7 +1433,7 @@ k_kp_fold(const unsigned long long *slots, const uint64_t *fl, uint32_t nparts, 
 /* The rows pg.rows of 21-bit codes under 2048 coarse slices of a 2^32-key
    pass [lo, lo + 2^32) -- k_kpart's over a key list, or the fused walk's
    (k_sp_wpart) -- into the pass's runs at out_k / out_c (*nw of them):
-   k_repart, k_kp_count, k_kp_fold.  n: the codes the rows hold; res: 16 B
+   k_repart, k_kp_cnt2, k_kp_fold.  n: the codes the rows hold; res: 16 B
    of zeroed device scratch, res[1] the top key counted apart by k_kpart
    (npads of them pads) */
 static int sp_count_rows32(fk_engine *e, const PartGeo &pg, uint64_t n, uint64_t lo, uint64_t npads,
@@ -1484,7 +1457,7 @@ static int sp_count_rows32(fk_engine *e, const PartGeo &pg, uint64_t n, uint64_t
     hipLaunchKernelGGL(k_repart<uint16_t>, dim3(2048u / REPART_G), dim3(1024), 0, e->stream, pg, e->d_parts, alloc,
                        meta, (uint64_t)e->parts_cap, alloc + 1, 15u, nullptr);
     HIPCHK(hipGetLastError());
-    hipLaunchKernelGGL(k_kp_count<KC_NT>, dim3(nparts), dim3(KC_NT), (size_t)KC_WORDS * 4, e->stream, (const uint16_t *)e->d_parts,
+    hipLaunchKernelGGL(k_kp_cnt2, dim3(nparts), dim3(1024), (size_t)KC_WORDS * 4, e->stream, (const uint16_t *)e->d_parts,
                        (const PartMeta *)meta, (uint64_t)e->parts_cap, lo, npads, (const unsigned long long *)(res + 1), nparts,
                        k, flags.as<unsigned long long>(), out_k, out_c, slots.as<unsigned long long>(), fl.as<uint64_t>(),
                        alloc + 1);
@@ -1679,7 +1652,7 @@ int sparse_finish(fk_engine *e, int32_t seq) {
                                    (int)(KS_CAP * 6 + 16)));
         HIPCHK(hipFuncSetAttribute((const void *)k_kp_sort<KS_CAP_S>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                    (int)(KS_CAP_S * 6 + 16)));
-        HIPCHK(hipFuncSetAttribute((const void *)k_kp_count<KC_NT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+        HIPCHK(hipFuncSetAttribute((const void *)k_kp_cnt2, hipFuncAttributeMaxDynamicSharedMemorySize,
                                    (int)(KC_WORDS * 4)));
     }
     PoolScratch acc(e, 4), bh(e, 5), ctr(e, 6), pctr(e, 7);
@@ -1862,7 +1835,7 @@ int sparse_finish(fk_engine *e, int32_t seq) {
     };
     /* k = 17: the four first-base passes, each a walk that partitions its
        windows (k_sp_wpart) + the general tiles' list (k_kpart), then
-       k_repart / k_kp_count; SP_RETRY: a row or list overflowed, or it does
+       k_repart / k_kp_cnt2; SP_RETRY: a row or list overflowed, or it does
        not fit -- the key-list passes instead */
     auto walk17 = [&]() -> int {
         const uint32_t grid = (uint32_t)std::max(1, e->cus);

@@ -7,7 +7,7 @@ mkdir -p gpurun_out
 timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -v --timeout 120 --timeout-method thread -k "sparse" \
   > gpurun_out/c8_tests.log 2>&1 || { tail -40 gpurun_out/c8_tests.log; exit 1; }
 tail -3 gpurun_out/c8_tests.log
-for tune in "" "sp_walk=0" ""; do
+for tune in "" "kp_count=1" ""; do
   FINDKMER_TUNE=$tune timeout -k 10 240 python bench.py --k 17 --fasta-line 80 --bases 10000000000 --steps 4 --warmup 2 \
     --north-star-bases 0 --no-cpu-baseline > gpurun_out/c8_b.json 2> gpurun_out/c8_b.err || { tail -20 gpurun_out/c8_b.err; exit 1; }
   python3 -c "import json; d=json.loads(open('gpurun_out/c8_b.json').read().strip().splitlines()[-1]); print('tune=$tune', round(d['ms_per_step'],2), 'ms')"
