@@ -376,119 +376,139 @@ k_bucket16(PartGeo pg, uint32_t *table) {
 }
 
 
-/* one block per part: its stream into 2^15 LDS bins, then into the table */
-__global__ void __launch_bounds__(1024)
+/* k_count_parts: one block per part, its stream into 2^15 LDS bins, then
+   into the table.  The bins are 16-bit halves of 2^14 LDS words (64 KiB, two
+   blocks per CU: one block's count overlaps the other's table writes; round
+   5's 128 KiB of 32-bit bins left one block per CU alternating between them:
+   k = 16 1 G-base step 10.1 -> 9.5 ms, k = 15 equal).  A wrapped bin (the
+   halves' sum short of the part's codes) counts the part again as two
+   halves of 2^14 32-bit bins.  The part's first pieces load while the bins
+   are zeroed (round 6: the stream had been read one latency-bound piece at a
+   time after the zeroing).  On a fresh table (the segment's k_zero left it
+   out) every bin is written, no read (k = 16: 17 GB of zeroing and 17 GB of
+   reads less per step), with streaming stores (the 16 GiB table is not read
+   back soon: 10.74 -> 10.42 ms), and the statistics k_table_stats would
+   read the table for (distinct, sum, last- and first-base marginals) taken
+   here: they stand unless the general tiles' list or k_redo adds to the
+   table afterwards. */
+__global__ void __launch_bounds__(1024, 8)
 k_count_parts(PartGeo pg, const uint16_t *in, const PartMeta *meta, uint32_t *table, uint64_t cap,
-              unsigned long long *err) {
-    extern __shared__ uint32_t slice[];
+               unsigned long long *err) {
+    extern __shared__ uint32_t bins[];   /* 2^14 words */
+    __shared__ uint32_t s_hs;
+    __shared__ unsigned long long wred[16][6];
+    const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6;
     const uint32_t np = 1u << pg.split;
     const uint32_t b = blockIdx.x / np, part = blockIdx.x % np;
     PartMeta m = meta[blockIdx.x];
-    if (m.off + m.n > cap) {   /* bound check: a stream past the parts buffer is not read */
-        if (threadIdx.x == 0) atomicOr(err, (unsigned long long)FK_FAULT_META);
+    if (m.off + m.n > cap) {
+        if (t == 0) atomicOr(err, (unsigned long long)FK_FAULT_META);
         m.n = 0;
         m.off = 0;
     }
-    const uint4 *g4 = reinterpret_cast<const uint4 *>(in + m.off);   /* 16-B aligned: off % 8 == 0 */
+    if (t == 0) s_hs = 0;
+    const uint4 *g4 = reinterpret_cast<const uint4 *>(in + m.off);
     const uint32_t nq = (m.n + 7u) >> 3;
-    auto add8 = [&](const uint4 &v, uint32_t q) {
+    /* hsel < 0: bin c at half c & 1 of word c >> 1; else only bins [hsel 2^14, ..) as 32-bit words */
+    auto add8 = [&](const uint4 &v, uint32_t q, int hsel) {
         const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-        for (int h = 0; h < 8; h++)
-            if (q * 8u + (uint32_t)h < m.n) atomicAdd(&slice[(w4[h >> 1] >> (16 * (h & 1))) & 0x7FFFu], 1u);
+        for (int h = 0; h < 8; h++) {
+            if (q * 8u + (uint32_t)h >= m.n) continue;
+            const uint32_t c = (w4[h >> 1] >> (16 * (h & 1))) & 0x7FFFu;
+            if (hsel < 0) atomicAdd(&bins[c >> 1], 1u << ((c & 1u) << 4));
+            else if ((c >> 14) == (uint32_t)hsel) atomicAdd(&bins[c & 0x3FFFu], 1u);
+        }
     };
-    /* the part's first CP_U pieces per thread (16 K codes: ~2 k = 16 parts)
-       in flight while the bins are zeroed (round 6: the stream had been
-       read one latency-bound piece at a time after the zeroing) */
-    constexpr uint32_t CP_U = 2u;
-    const uint32_t t = threadIdx.x;
-    uint4 pv[CP_U];
+    auto zero = [&]() {
+        for (uint32_t i = t; i < (1u << 12); i += 1024u) reinterpret_cast<uint4 *>(bins)[i] = make_uint4(0, 0, 0, 0);
+    };
+    {
+        constexpr uint32_t CP_U = 2u;
+        uint4 pv[CP_U];
 #pragma unroll
-    for (uint32_t u = 0; u < CP_U; u++) pv[u] = t + u * 1024u < nq ? g4[t + u * 1024u] : make_uint4(0, 0, 0, 0);
-    for (uint32_t i = t; i < (1u << 13); i += blockDim.x)
-        reinterpret_cast<uint4 *>(slice)[i] = make_uint4(0, 0, 0, 0);
-    __syncthreads();
-#pragma unroll
-    for (uint32_t u = 0; u < CP_U; u++)
-        if (t + u * 1024u < nq) add8(pv[u], t + u * 1024u);
-    for (uint32_t q0 = t + CP_U * 1024u; q0 < nq; q0 += CP_U * 1024u) {
-#pragma unroll
-        for (uint32_t u = 0; u < CP_U; u++) pv[u] = q0 + u * 1024u < nq ? g4[q0 + u * 1024u] : make_uint4(0, 0, 0, 0);
+        for (uint32_t u = 0; u < CP_U; u++) pv[u] = t + u * 1024u < nq ? g4[t + u * 1024u] : make_uint4(0, 0, 0, 0);
+        zero();
+        __syncthreads();
 #pragma unroll
         for (uint32_t u = 0; u < CP_U; u++)
-            if (q0 + u * 1024u < nq) add8(pv[u], q0 + u * 1024u);
+            if (t + u * 1024u < nq) add8(pv[u], t + u * 1024u, -1);
+        for (uint32_t q0 = t + CP_U * 1024u; q0 < nq; q0 += CP_U * 1024u) {
+#pragma unroll
+            for (uint32_t u = 0; u < CP_U; u++) pv[u] = q0 + u * 1024u < nq ? g4[q0 + u * 1024u] : make_uint4(0, 0, 0, 0);
+#pragma unroll
+            for (uint32_t u = 0; u < CP_U; u++)
+                if (q0 + u * 1024u < nq) add8(pv[u], q0 + u * 1024u, -1);
+        }
     }
     __syncthreads();
-    /* the part's bins into the table (the block owns them), eight loads in
-       flight per lane before the adds and stores: one load-add-store chain
-       at a time left this loop latency-bound (k = 16: 13.3 ms per G-base) */
-    const uint64_t base = ((uint64_t)b << pg.sh) | ((uint64_t)part << 15);
-    if (pg.glist) {
-        /* a fresh table (the segment's k_zero left it out): every bin of
-           the part written, no read (k = 16: 17 GB of zeroing and 17 GB of
-           reads less per step); the general tiles' windows follow
-           (k_list_add) */
-        /* with the statistics k_table_stats would read the table for
-           (distinct, sum, last- and first-base marginals): they stand unless
-           the general tiles' list or k_redo adds to the table afterwards */
-        const int fs = 2 * pg.kk - 2;
-        /* a lane's bins i = lane + 1024 j all end in the same base (sigma
-           maps digits one by one, and i & 3 = lane & 3): its sum is its
-           last-base marginal */
-        /* four bins per lane: kernel bins 4m + d land at reference index
-           sigma(base | 4m) + sigma(d), i.e. the last digits 0 1 3 2 (sigma
-           maps digit by digit): one 16-B store */
-        uint32_t dist = 0;
-        unsigned long long last[4] = {0, 0, 0, 0};
-        const uint4 *s4 = reinterpret_cast<const uint4 *>(slice);
-        uint4 *t4 = reinterpret_cast<uint4 *>(table);
-        for (uint32_t m = threadIdx.x; m < (1u << 13); m += 1024u) {
-            const uint4 q = s4[m];
-            const uint4 o = make_uint4(q.x, q.y, q.w, q.z);
-            {   /* streaming stores: the 16 GiB table is not read back soon
-                   (k = 16 1 G-base step 10.74 -> 10.42 ms) */
-                const u32x4 ov = {o.x, o.y, o.z, o.w};
-                __builtin_nontemporal_store(ov, reinterpret_cast<u32x4 *>(t4) + (fk_sigma(base | ((uint64_t)m << 2)) >> 2));
-            }
-            dist += (o.x != 0) + (o.y != 0) + (o.z != 0) + (o.w != 0);
-            last[0] += o.x; last[1] += o.y; last[2] += o.z; last[3] += o.w;
-        }
-        const unsigned long long sum = last[0] + last[1] + last[2] + last[3];
-        unsigned long long v10[6] = {dist, sum, last[0], last[1], last[2], last[3]};
-#pragma unroll
-        for (int q = 0; q < 6; q++) v10[q] = wsum64(v10[q]);
-        /* the wave sums in the bins' LDS, once every lane has read its bins
-           (no static LDS: the kernel's dynamic maximum is the whole 160 KiB) */
-        __syncthreads();
-        unsigned long long *wp = reinterpret_cast<unsigned long long *>(slice);
-        const uint32_t wv = threadIdx.x >> 6;
-        if ((threadIdx.x & 63) == 0)
-#pragma unroll
-            for (int q = 0; q < 6; q++) wp[wv * 6u + q] = v10[q];
-        __syncthreads();
-        if (threadIdx.x < 10) {
-            unsigned long long t = 0;
-            const uint32_t q = threadIdx.x;
-            if (q < 6) {
-                for (uint32_t w = 0; w < 16; w++) t += wp[w * 6u + q];
-            } else {   /* the first base of every bin of the part: one digit */
-                for (uint32_t w = 0; w < 16; w++) t += wp[w * 6u + 1u];
-                if ((uint32_t)((fk_sigma(base) >> fs) & 3u) != q - 6u) t = 0;
-            }
-            if (t) atomicAdd(&pg.fz[(blockIdx.x % FZ_SLOTS) * 10u + q], t);
-        }
-        return;
+    {   /* the wrap check */
+        uint32_t hs = 0;
+        for (uint32_t i = t; i < (1u << 14); i += 1024u) hs += (bins[i] & 0xFFFFu) + (bins[i] >> 16);
+        const uint32_t a = wsum32(hs);
+        if (lane == 0) atomicAdd(&s_hs, a);
     }
-    constexpr uint32_t U = 8u;
-    for (uint32_t i0 = threadIdx.x; i0 < (1u << 15); i0 += U * 1024u) {
-        uint32_t v[U], o[U];
+    __syncthreads();
+    const bool wrap = s_hs != m.n;
+    const uint64_t base = ((uint64_t)b << pg.sh) | ((uint64_t)part << 15);
+    const bool fresh = pg.glist != nullptr;
+    uint32_t dist = 0;
+    unsigned long long last[4] = {0, 0, 0, 0};
+    /* bins 4 m4 .. 4 m4 + 3 of the part: kernel bins 4m + d land at reference
+       index sigma(base | 4m) + sigma(d), i.e. the last digits 0 1 3 2: one
+       16-B store on a fresh table (streaming: the table is not read back
+       soon), else each nonzero bin added */
+    auto out4 = [&](uint32_t m4, uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3) {
+        const uint64_t r = fk_sigma(base | ((uint64_t)m4 << 2));
+        if (fresh) {
+            const u32x4 ov = {c0, c1, c3, c2};
+            __builtin_nontemporal_store(ov, reinterpret_cast<u32x4 *>(table) + (r >> 2));
+            dist += (c0 != 0) + (c1 != 0) + (c2 != 0) + (c3 != 0);
+            last[0] += c0; last[1] += c1; last[2] += c3; last[3] += c2;
+        } else {
+            const uint32_t cc[4] = {c0, c1, c3, c2};
 #pragma unroll
-        for (uint32_t j = 0; j < U; j++) v[j] = slice[i0 + j * 1024u];
+            for (int d = 0; d < 4; d++)
+                if (cc[d]) table[r + (uint64_t)d] += cc[d];
+        }
+    };
+    if (!wrap) {
+        for (uint32_t m4 = t; m4 < (1u << 13); m4 += 1024u) {
+            const uint2 w = reinterpret_cast<const uint2 *>(bins)[m4];
+            out4(m4, w.x & 0xFFFFu, w.x >> 16, w.y & 0xFFFFu, w.y >> 16);
+        }
+    } else {
+        for (int h = 0; h < 2; h++) {
+            __syncthreads();
+            zero();
+            __syncthreads();
+            for (uint32_t q = t; q < nq; q += 1024u) add8(g4[q], q, h);
+            __syncthreads();
+            for (uint32_t i = t; i < (1u << 12); i += 1024u) {
+                const uint4 w = reinterpret_cast<const uint4 *>(bins)[i];
+                out4(((uint32_t)h << 12) + i, w.x, w.y, w.z, w.w);
+            }
+        }
+    }
+    if (!fresh) return;
+    const int fs = 2 * pg.kk - 2;
+    const unsigned long long sum = last[0] + last[1] + last[2] + last[3];
+    unsigned long long v6[6] = {dist, sum, last[0], last[1], last[2], last[3]};
 #pragma unroll
-        for (uint32_t j = 0; j < U; j++) o[j] = v[j] ? table[fk_sigma(base | (i0 + j * 1024u))] : 0u;
+    for (int q = 0; q < 6; q++) v6[q] = wsum64(v6[q]);
+    if (lane == 0)
 #pragma unroll
-        for (uint32_t j = 0; j < U; j++)
-            if (v[j]) table[fk_sigma(base | (i0 + j * 1024u))] = o[j] + v[j];
+        for (int q = 0; q < 6; q++) wred[wv][q] = v6[q];
+    __syncthreads();
+    if (t < 10) {
+        unsigned long long a = 0;
+        if (t < 6) {
+            for (uint32_t w = 0; w < 16; w++) a += wred[w][t];
+        } else {   /* the first base of every bin of the part: one digit */
+            for (uint32_t w = 0; w < 16; w++) a += wred[w][1];
+            if ((uint32_t)((fk_sigma(base) >> fs) & 3u) != t - 6u) a = 0;
+        }
+        if (a) atomicAdd(&pg.fz[(blockIdx.x % FZ_SLOTS) * 10u + t], a);
     }
 }
 
@@ -723,9 +743,9 @@ int launch_part(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t lo, cons
             hipLaunchKernelGGL(k_repart<uint16_t>, dim3(pg.nslices / REPART_G), dim3(1024), 0, e->stream, pg,
                                e->d_parts, alloc, meta, (uint64_t)e->parts_cap, e->d_perr, 15u, nullptr);
         HIPCHK(hipGetLastError());
-        hipLaunchKernelGGL(k_count_parts, dim3((unsigned)nparts), dim3(1024), (size_t)1 << 17, e->stream, pg,
-                           (const uint16_t *)e->d_parts, (const PartMeta *)meta, e->d_table, (uint64_t)e->parts_cap,
-                           e->d_perr);
+        hipLaunchKernelGGL(k_count_parts, dim3((unsigned)nparts), dim3(1024), (size_t)1 << 16, e->stream, pg,
+                               (const uint16_t *)e->d_parts, (const PartMeta *)meta, e->d_table, (uint64_t)e->parts_cap,
+                               e->d_perr);
         if (pg.glist) {
             HIPCHK(hipGetLastError());
             hipLaunchKernelGGL(k_list_add, dim3((unsigned)e->cus * 4), dim3(256), 0, e->stream, pg.glist, e->d_table,
@@ -765,12 +785,14 @@ int launch_part(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t lo, cons
 /* k_bucket_count: one 2^15-bin slice + its 2^13 single bins (160 KiB) in
    LDS; k_bucket16: 128 KiB of bins beside its static reduction words */
 int part_kernels_init() {
-    for (const void *f : {(const void *)k_bucket_count<BK_PLAIN>, (const void *)k_count_parts,
+    for (const void *f : {(const void *)k_bucket_count<BK_PLAIN>,
                           (const void *)k_bucket_count<BK_PAD>, (const void *)k_bucket16<true>,
                           (const void *)k_bucket16<false>})
         if (hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (f == (const void *)k_bucket16<true> || f == (const void *)k_bucket16<false>)
                                     ? 1 << 17 : 5 << 15) != hipSuccess)
             return FK_E_HIP;
+    if (hipFuncSetAttribute((const void *)k_count_parts, hipFuncAttributeMaxDynamicSharedMemorySize, 1 << 16) != hipSuccess)
+        return FK_E_HIP;
     return FK_OK;
 }
