@@ -512,7 +512,8 @@ struct SpDefer {
     uint32_t R, hdr, seg, pad;
 };
 struct SpWalk {
-    uint32_t qdig;                 /* the pass's first base in the internal encoding */
+    uint32_t qdig;                 /* k = 17: the pass's first base in the internal encoding */
+    uint32_t q, ktop, cs;          /* k >= 18: the first base (reference order), its bit 2k - 2, code bits */
     uint32_t *codes;               /* rows of WP_BATCH codes (k_kpart's layout) */
     uint32_t *idx;                 /* [row][2048] run words */
     unsigned long long *ctr;       /* [0] rows claimed, [1] tiles deferred, [3] windows placed in rows,
@@ -524,8 +525,15 @@ struct SpWalk {
     uint32_t dbg;                  /* FINDKMER_TUNE sp_walk_dbg: 1 = every tile deferred (tests) */
 };
 struct WpTile {
-    uint32_t c0, s0, c1, s1;       /* per half: 16-digit context, 16-digit word */
+    uint32_t c0, s0, c1, s1;       /* k = 17, per half: 16-digit context, 16-digit word */
     uint32_t fl;                   /* bit 0: has windows, bits 1, 2: half 0 / 1 had a '\n' (slot 0 no window) */
+};
+/* 18 <= k <= 20 (windows up to 20 digits): as k_sp_emit's sp_fast_emit, the
+   32 digits before half 0 (the previous lane's {BC, B2}) and the Emit words
+   AC, A2, B2 (half 1's 32 digits before it are {AC, A2}) */
+struct WpTileW {
+    uint32_t p0h, p0l, ac, a2, b2;
+    uint32_t fl;
 };
 /* a stashed fast tile's in-pass windows: HIST into the slices' counts, else
    placed at their slices' cursors */
@@ -566,6 +574,52 @@ __device__ __forceinline__ void wp_tile(const WpTile &x, uint32_t qdig, uint32_t
     }
 }
 
+/* the wide passes' windows: keys of 2k bits, the pass's first base q the
+   top digit (bit ktop = 2k - 2 up), slice the top 11 bits of the relative
+   key, code its low cs bits */
+template <bool HIST>
+__device__ __forceinline__ void wp_tile_w(const WpTileW &x, uint32_t q, uint32_t ktop, uint64_t maskk, uint32_t cs,
+                                          uint32_t *hist, uint32_t *cur, uint32_t *ent) {
+    const uint64_t relm = (1ull << ktop) - 1ull;
+    const uint32_t cm = (1u << cs) - 1u;
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+        const uint64_t pv = h ? (((uint64_t)x.ac << 32) | x.a2) : (((uint64_t)x.p0h << 32) | x.p0l);
+        const bool hf = (x.fl >> (1 + h)) & 1u;
+        const uint32_t R = (h ? x.b2 : x.a2) & (hf ? 0x3FFFFFFFu : 0xFFFFFFFFu);
+        const uint32_t D = hf ? 15u : 16u;   /* the half's digits (right-aligned in R) */
+#pragma unroll
+        for (int g = 0; g < 2; g++) {
+            uint32_t b[8], cd[8], p[8];
+            bool in[8];
+#pragma unroll
+            for (int jj = 0; jj < 8; jj++) {
+                const uint32_t j = 8u * (uint32_t)g + (uint32_t)jj;
+                const bool valid = j < D;
+                const uint32_t sh = valid ? 2u * (D - 1u - j) : 0u;
+                const uint64_t key = fk_sigma(((pv << (2u * j + 2u)) | (uint64_t)(R >> sh)) & maskk);
+                in[jj] = valid && (uint32_t)(key >> ktop) == q;
+                const uint64_t rel = key & relm;
+                b[jj] = (uint32_t)(rel >> cs);
+                cd[jj] = (uint32_t)rel & cm;
+            }
+            if (HIST) {
+#pragma unroll
+                for (int jj = 0; jj < 8; jj++)
+                    if (in[jj]) atomicAdd(&hist[b[jj]], 1u);
+            } else {
+#pragma unroll
+                for (int jj = 0; jj < 8; jj++)
+                    if (in[jj]) p[jj] = atomicAdd(&cur[b[jj]], 1u);
+#pragma unroll
+                for (int jj = 0; jj < 8; jj++)
+                    if (in[jj] && p[jj] < WP_BATCH) ent[p[jj]] = cd[jj];
+            }
+        }
+    }
+}
+
+template <bool WIDE>
 __global__ void __launch_bounds__(1024, 1)
 k_sp_wpart(const uint8_t *buf, uint64_t len, int k, uint64_t maskk, const XState *rst, uint64_t nranges, uint64_t cpw,
            uint64_t nchunks, SpWalk wk) {
@@ -600,8 +654,9 @@ k_sp_wpart(const uint8_t *buf, uint64_t len, int k, uint64_t maskk, const XState
     if (!done) open();
     /* one tile of the wave's ranges: a fast tile stashed, any other only
        advancing the state (walk 0: recorded for k_sp_gtiles) */
-    auto step = [&]() -> WpTile {
-        WpTile x{0, 0, 0, 0, 0};
+    using Tile = typename std::conditional<WIDE, WpTileW, WpTile>::type;
+    auto step = [&]() -> Tile {
+        Tile x{};
         if (done) return x;
         uint32_t w[8];
         int nb = (int)FK_LANE_BYTES;
@@ -619,11 +674,19 @@ k_sp_wpart(const uint8_t *buf, uint64_t len, int k, uint64_t maskk, const XState
         Emit fe{0, 0, 0, 0, false, false, false};
         if (full && st.hdr == 0 && !(wk.dbg & 1u) && tile_fast<true, H_EMIT, false>(cx, w, st, f, cnt, 1u, &fe)) {
             if (fe.deep) {
-                const uint32_t xp = from_prev_lane(fe.B2, (uint32_t)c0);   /* the 16 digits before half 0 */
-                x.c0 = fe.h0 ? xp >> 2 : xp;
-                x.s0 = fe.A2;
-                x.c1 = fe.h1 ? fe.A2 >> 2 : fe.A2;
-                x.s1 = fe.B2;
+                if constexpr (WIDE) {
+                    x.p0h = from_prev_lane(fe.BC, (uint32_t)(c0 >> 32));
+                    x.p0l = from_prev_lane(fe.B2, (uint32_t)c0);
+                    x.ac = fe.AC;
+                    x.a2 = fe.A2;
+                    x.b2 = fe.B2;
+                } else {
+                    const uint32_t xp = from_prev_lane(fe.B2, (uint32_t)c0);   /* the 16 digits before half 0 */
+                    x.c0 = fe.h0 ? xp >> 2 : xp;
+                    x.s0 = fe.A2;
+                    x.c1 = fe.h1 ? fe.A2 >> 2 : fe.A2;
+                    x.s1 = fe.B2;
+                }
                 x.fl = 1u | (fe.h0 ? 2u : 0u) | (fe.h1 ? 4u : 0u);
             }
         } else {
@@ -641,18 +704,27 @@ k_sp_wpart(const uint8_t *buf, uint64_t len, int k, uint64_t maskk, const XState
         }
         return x;
     };
-    WpTile xs[WP_NT];
+    Tile xs[WP_NT];
+    auto apply = [&](const Tile &x, bool hst) {
+        if constexpr (WIDE) {
+            if (hst) wp_tile_w<true>(x, wk.q, wk.ktop, maskk, wk.cs, hist, cur, ent);
+            else wp_tile_w<false>(x, wk.q, wk.ktop, maskk, wk.cs, hist, cur, ent);
+        } else {
+            if (hst) wp_tile<true>(x, wk.qdig, hist, cur, ent);
+            else wp_tile<false>(x, wk.qdig, hist, cur, ent);
+        }
+    };
     /* the stashed tiles' in-pass windows into the slices' counts (sel: one
        stash slot, or ~0 all).  One stashed tile at a time: unrolled over the
        stash, the compiler interleaved all 96 windows and spilled */
     auto wp_hist = [&](uint32_t sel) {
 #pragma unroll 1
         for (uint32_t i = 0; i < WP_NT; i++) {
-            WpTile x = xs[0];
+            Tile x = xs[0];
 #pragma unroll
             for (uint32_t ii = 1; ii < WP_NT; ii++)
                 if (i == ii) x = xs[ii];
-            if ((x.fl & 1u) && (sel == ~0u || sel == i)) wp_tile<true>(x, wk.qdig, hist, cur, ent);
+            if ((x.fl & 1u) && (sel == ~0u || sel == i)) apply(x, true);
         }
     };
     /* a new row, claimed by thread 0 (seen by all after the next barrier) */
@@ -690,11 +762,11 @@ k_sp_wpart(const uint8_t *buf, uint64_t len, int k, uint64_t maskk, const XState
     auto wp_row = [&](uint32_t sel, uint32_t T) {
 #pragma unroll 1
         for (uint32_t i = 0; i < WP_NT; i++) {
-            WpTile x = xs[0];
+            Tile x = xs[0];
 #pragma unroll
             for (uint32_t ii = 1; ii < WP_NT; ii++)
                 if (i == ii) x = xs[ii];
-            if ((x.fl & 1u) && (sel == ~0u || sel == i)) wp_tile<false>(x, wk.qdig, hist, cur, ent);
+            if ((x.fl & 1u) && (sel == ~0u || sel == i)) apply(x, false);
         }
         __syncthreads();
         const unsigned long long row = s_row;
@@ -709,7 +781,7 @@ k_sp_wpart(const uint8_t *buf, uint64_t len, int k, uint64_t maskk, const XState
     for (;;) {
 #pragma unroll 1
         for (uint32_t u = 0; u < WP_NT; u++) {
-            const WpTile x = step();
+            const Tile x = step();
 #pragma unroll
             for (uint32_t i = 0; i < WP_NT; i++)
                 if (u == i) xs[i] = x;
@@ -744,15 +816,18 @@ k_sp_wpart(const uint8_t *buf, uint64_t len, int k, uint64_t maskk, const XState
 /* the recorded tiles (walk 0), one wave at a time each from its entering
    state with k_sp_emit's general path: FILL = false counts each first
    base's windows (cnt[0..3]) and lists the short walks; FILL = true lists
-   the windows, first base q at glist + goff[q], as key - q 2^32 */
+   the windows, first base q at glist + goff[q], as key - q 4^(k - 1) (KT:
+   32 bits at k = 17) */
 struct SpSegDev {
     const uint8_t *src;
     uint64_t len;
 };
-template <bool FILL>
+template <bool FILL, typename KT>
 __global__ void __launch_bounds__(SP_WAVES * 64u)
-k_sp_gtiles(const SpDefer *df, uint64_t n, const SpSegDev *segs, int k, uint64_t maskk, uint32_t *glist,
+k_sp_gtiles(const SpDefer *df, uint64_t n, const SpSegDev *segs, int k, uint64_t maskk, KT *glist,
             const uint64_t *goff, unsigned long long *cnt, uint64_t *shorts, uint64_t short_cap) {
+    const uint32_t ktop = 2u * (uint32_t)k - 2u;   /* a key's first base: its bits from 2k - 2 */
+    const uint64_t relm = (1ull << ktop) - 1ull;
     extern __shared__ uint64_t gt_lds[];   /* SP_WAVES x 2048 slots */
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     uint64_t *slots = gt_lds + (size_t)wv * FK_TILE_BYTES;
@@ -774,7 +849,7 @@ k_sp_gtiles(const SpDefer *df, uint64_t n, const SpSegDev *segs, int k, uint64_t
         for (uint32_t j = 0; j < FK_LANE_BYTES; j++) {
             const uint64_t v = slots[j * 64u + lane];
             if (v < SP_SHORT) {
-                const uint32_t q = (uint32_t)(v >> 32), inc = 1u << (16u * (q & 1u));
+                const uint32_t q = (uint32_t)(v >> ktop), inc = 1u << (16u * (q & 1u));
                 c01 += q < 2u ? inc : 0u;
                 c23 += q >= 2u ? inc : 0u;
             } else if (v != SP_EMPTY) {
@@ -818,9 +893,9 @@ k_sp_gtiles(const SpDefer *df, uint64_t n, const SpSegDev *segs, int k, uint64_t
                 for (uint32_t j = 0; j < FK_LANE_BYTES; j++) {
                     const uint64_t v = slots[j * 64u + lane];
                     if (v < SP_SHORT) {
-                        const uint32_t q = (uint32_t)(v >> 32);
+                        const uint32_t q = (uint32_t)(v >> ktop);
                         const uint64_t a = q == 0u ? at[0] : q == 1u ? at[1] : q == 2u ? at[2] : at[3];
-                        glist[goff[q] + a] = (uint32_t)v;
+                        glist[goff[q] + a] = (KT)(v & relm);
                         at[0] += q == 0u; at[1] += q == 1u; at[2] += q == 2u; at[3] += q == 3u;
                     }
                 }
@@ -1525,6 +1600,90 @@ int sp_count_runs32(fk_engine *e, const uint32_t *keys, uint64_t n, uint64_t lo,
     return rc;
 }
 
+/* The rows pg.rows of cs-bit codes under 2048 coarse slices of a wide pass
+   (keys lo + r, r < 2^(cs + 11)) -- k_kpart's over a key list, or the fused
+   walk's -- into its runs at out_k / out_c (*nw): k_repart (128 parts a
+   slice), k_kp_sort, k_kp_fold.  res: 16 B of zeroed device scratch, res[1]
+   the top key counted apart (top_part: its part, ~0 none; npads of them
+   pads).  `fallback`: a part or bucket too large for k_kp_sort -- nothing was
+   folded into dacc. */
+static int sp_sort_rows64(fk_engine *e, const PartGeo &pg, uint64_t n, uint64_t lo, uint32_t psh, uint64_t npads,
+                          uint32_t top_part, unsigned long long *res, unsigned long long *dacc, uint64_t *out_k,
+                          uint32_t *out_c, uint64_t *nw, bool *fallback) {
+    const int k = e->k;
+    const uint32_t nparts = 2048u << 7;
+    /* (the part streams as 32-bit codes: twice the u16 capacity) */
+    int rc = sp_ensure((void **)&e->d_parts, &e->parts_cap, 2 * (n + 8ull * nparts + 16), sizeof(uint16_t));
+    if (rc) return rc;
+    if (!e->d_pmeta && hipMalloc(&e->d_pmeta, (size_t)2048 * REPART_METAP * sizeof(PartMeta) + 64) != hipSuccess)
+        return FK_E_OOM;
+    PoolScratch flags(e, 0), slots(e, 1), fl(e, 2);
+    if (!flags.alloc((size_t)(nparts + 1) * 8) || !slots.alloc((size_t)KP_SLOTS * KP_SLOT_W * 8) ||
+        !fl.alloc((size_t)nparts * 16))
+        return FK_E_OOM;
+    PartMeta *meta = static_cast<PartMeta *>(e->d_pmeta);
+    unsigned long long *alloc = reinterpret_cast<unsigned long long *>(meta + (size_t)2048 * REPART_METAP);
+    uint32_t *parts32 = reinterpret_cast<uint32_t *>(e->d_parts);
+    const uint64_t cap32 = e->parts_cap / 2;
+    HIPCHK(hipMemsetAsync(alloc, 0, 3 * sizeof(unsigned long long), e->stream));
+    HIPCHK(hipMemsetAsync(flags.p, 0, (size_t)(nparts + 1) * 8, e->stream));   /* (+ the block tickets) */
+    HIPCHK(hipMemsetAsync(slots.p, 0, (size_t)KP_SLOTS * KP_SLOT_W * 8, e->stream));
+    const unsigned long long *tcount = res + 1;
+    hipLaunchKernelGGL((k_repart<uint32_t, 4u>), dim3(2048u / 4u), dim3(1024), 0, e->stream, pg, parts32, alloc, meta,
+                       cap32, alloc + 1, psh, alloc + 2);
+    HIPCHK(hipGetLastError());
+    unsigned long long pmax = 0;
+    HIPCHK(hipMemcpyAsync(&pmax, alloc + 2, 8, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    if (pmax > KS_CAP) {   /* a part past one block's LDS: the library sort */
+        *fallback = true;
+        return FK_OK;
+    }
+    const bool small = pmax <= KS_CAP_S;
+    if (small)
+        hipLaunchKernelGGL(k_kp_sort<KS_CAP_S>, dim3(nparts), dim3(1024), (size_t)KS_CAP_S * 6 + 16, e->stream,
+                           (const uint32_t *)parts32, (const PartMeta *)meta, cap32, lo, psh, npads, tcount, top_part,
+                           nparts, k, flags.as<unsigned long long>(), out_k, out_c, slots.as<unsigned long long>(),
+                           fl.as<uint64_t>(), alloc + 1);
+    else
+        hipLaunchKernelGGL(k_kp_sort<KS_CAP>, dim3(nparts), dim3(1024), (size_t)KS_CAP * 6 + 16, e->stream,
+                           (const uint32_t *)parts32, (const PartMeta *)meta, cap32, lo, psh, npads, tcount, top_part,
+                           nparts, k, flags.as<unsigned long long>(), out_k, out_c, slots.as<unsigned long long>(),
+                           fl.as<uint64_t>(), alloc + 1);
+    HIPCHK(hipGetLastError());
+    unsigned long long ferr = 0;
+    HIPCHK(hipMemcpyAsync(&ferr, alloc + 1, 8, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    if (ferr & FK_FAULT_SORTCAP) {
+        *fallback = true;
+        return FK_OK;
+    }
+    if (ferr) return FK_E_INTERNAL;
+    hipLaunchKernelGGL(k_kp_fold, dim3(64), dim3(256), 0, e->stream, (const unsigned long long *)slots.p,
+                       (const uint64_t *)fl.p, nparts, k, (const unsigned long long *)flags.p, dacc, res);
+    HIPCHK(hipGetLastError());
+    unsigned long long r0 = 0;
+    HIPCHK(hipMemcpyAsync(&r0, res, 8, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    *nw = r0;
+    return FK_OK;
+}
+
+/* k_kpart over n 64-bit keys in [lo, hi) into rows [rows0, ..) of pg (cs-bit
+   codes), the top key tkey counted apart into *tcount */
+static int sp_kpart64(fk_engine *e, const PartGeo &pg, uint64_t rows0, const uint64_t *keys, uint64_t n, uint64_t lo,
+                      uint64_t hi, uint32_t cs, uint64_t tkey, unsigned long long *tcount) {
+    if (!n) return FK_OK;
+    PartGeo g = pg;
+    g.codes = reinterpret_cast<uint16_t *>(reinterpret_cast<uint32_t *>(pg.codes) + rows0 * pg.batch);
+    g.idx = pg.idx + rows0 * 2048u;
+    const uint32_t grid = (uint32_t)std::max(1, e->cus);
+    hipLaunchKernelGGL(k_kpart<uint64_t>, dim3(grid), dim3(1024), (size_t)KP_BATCH * 4, e->stream, keys, n, g, lo, hi,
+                       cs, tkey, tcount);
+    HIPCHK(hipGetLastError());
+    return FK_OK;
+}
+
 /* A wide pass (keys[0, n) in [lo, hi), hi - lo > 2^32, npads of them the
    pad 4^k - 1) into its runs at out_k / out_c (*nw).  `fallback` is set
    when a part or bucket is too large for k_kp_sort: nothing was folded into
@@ -1542,85 +1701,26 @@ int sp_sort_runs64(fk_engine *e, const uint64_t *keys, uint64_t n, uint64_t lo, 
        KS_CAP (64 parts per slice left ~33 K, and every pass took the library
        sort) */
     const uint32_t cs = sbits - 11, psh = cs - 7;
-    PartGeo pg{};
-    pg.nslices = 2048u;
+    PartGeo pg = sp_geo32(e, 0, n);
     pg.split = 7u;
-    pg.batch = KP_BATCH;
-    const uint32_t grid = (uint32_t)std::max(1, e->cus);
-    pg.rounds = (uint32_t)((n + (uint64_t)grid * KP_BATCH - 1) / ((uint64_t)grid * KP_BATCH));
-    pg.rows = grid * pg.rounds;
-    pg.flag = nullptr;
     const uint64_t ncodes = (uint64_t)pg.rows * KP_BATCH;
-    const uint32_t nparts = 2048u << 7;
     int rc = sp_ensure((void **)&e->d_codes, &e->codes_cap, 2 * ncodes, sizeof(uint16_t));
     if (!rc) rc = sp_ensure((void **)&e->d_pidx, &e->pidx_cap, (uint64_t)pg.rows * 2048u, sizeof(uint32_t));
-    /* (the part streams as 32-bit codes: twice the u16 capacity) */
-    if (!rc) rc = sp_ensure((void **)&e->d_parts, &e->parts_cap, 2 * (n + 8ull * nparts + 16), sizeof(uint16_t));
     if (rc) return rc;
-    if (!e->d_pmeta && hipMalloc(&e->d_pmeta, (size_t)2048 * REPART_METAP * sizeof(PartMeta) + 64) != hipSuccess)
-        return FK_E_OOM;
-    PoolScratch flags(e, 0), slots(e, 1), fl(e, 2), res(e, 3);
-    if (!flags.alloc((size_t)(nparts + 1) * 8) || !slots.alloc((size_t)KP_SLOTS * KP_SLOT_W * 8) ||
-        !fl.alloc((size_t)nparts * 16) || !res.alloc(16))
-        return FK_E_OOM;
     pg.codes = e->d_codes;
     pg.idx = e->d_pidx;
-    PartMeta *meta = static_cast<PartMeta *>(e->d_pmeta);
-    unsigned long long *alloc = reinterpret_cast<unsigned long long *>(meta + (size_t)2048 * REPART_METAP);
-    uint32_t *parts32 = reinterpret_cast<uint32_t *>(e->d_parts);
-    const uint64_t cap32 = e->parts_cap / 2;
-    HIPCHK(hipMemsetAsync(alloc, 0, 3 * sizeof(unsigned long long), e->stream));
-    HIPCHK(hipMemsetAsync(flags.p, 0, (size_t)(nparts + 1) * 8, e->stream));   /* (+ the block tickets) */
-    HIPCHK(hipMemsetAsync(slots.p, 0, (size_t)KP_SLOTS * KP_SLOT_W * 8, e->stream));
+    PoolScratch res(e, 3);
+    if (!res.alloc(16)) return FK_E_OOM;
     HIPCHK(hipMemsetAsync(res.p, 0, 16, e->stream));
-    unsigned long long *tcount = res.as<unsigned long long>() + 1;
+    unsigned long long *r = res.as<unsigned long long>();
     /* the top key 4^k - 1 (the pads' value; past hi they are left out as
        out of range) counted apart when the pass holds it */
     const uint64_t top = (1ull << (2 * k)) - 1;
     const bool top_in = top >= lo && top < hi;
-    hipLaunchKernelGGL(k_kpart<uint64_t>, dim3(grid), dim3(1024), (size_t)KP_BATCH * 4, e->stream, keys, n, pg, lo, hi,
-                       cs, top_in ? top : ~0ull, tcount);
-    HIPCHK(hipGetLastError());
-    hipLaunchKernelGGL((k_repart<uint32_t, 4u>), dim3(2048u / 4u), dim3(1024), 0, e->stream, pg, parts32, alloc, meta,
-                       cap32, alloc + 1, psh, alloc + 2);
-    HIPCHK(hipGetLastError());
-    unsigned long long pmax = 0;
-    HIPCHK(hipMemcpyAsync(&pmax, alloc + 2, 8, hipMemcpyDeviceToHost, e->stream));
-    HIPCHK(hipStreamSynchronize(e->stream));
-    if (pmax > KS_CAP) {   /* a part past one block's LDS: the library sort */
-        *fallback = true;
-        return FK_OK;
-    }
-    const bool small = pmax <= KS_CAP_S;
-    const uint32_t top_part = top_in ? (uint32_t)((top - lo) >> psh) : ~0u;
-    if (small)
-        hipLaunchKernelGGL(k_kp_sort<KS_CAP_S>, dim3(nparts), dim3(1024), (size_t)KS_CAP_S * 6 + 16, e->stream,
-                           (const uint32_t *)parts32, (const PartMeta *)meta, cap32, lo, psh, top_in ? npads : 0ull,
-                           (const unsigned long long *)tcount, top_part, nparts, k, flags.as<unsigned long long>(), out_k,
-                           out_c, slots.as<unsigned long long>(), fl.as<uint64_t>(), alloc + 1);
-    else
-        hipLaunchKernelGGL(k_kp_sort<KS_CAP>, dim3(nparts), dim3(1024), (size_t)KS_CAP * 6 + 16, e->stream,
-                           (const uint32_t *)parts32, (const PartMeta *)meta, cap32, lo, psh, top_in ? npads : 0ull,
-                           (const unsigned long long *)tcount, top_part, nparts, k, flags.as<unsigned long long>(), out_k,
-                           out_c, slots.as<unsigned long long>(), fl.as<uint64_t>(), alloc + 1);
-    HIPCHK(hipGetLastError());
-    unsigned long long ferr = 0;
-    HIPCHK(hipMemcpyAsync(&ferr, alloc + 1, 8, hipMemcpyDeviceToHost, e->stream));
-    HIPCHK(hipStreamSynchronize(e->stream));
-    if (ferr & FK_FAULT_SORTCAP) {
-        *fallback = true;
-        return FK_OK;
-    }
-    if (ferr) return FK_E_INTERNAL;
-    hipLaunchKernelGGL(k_kp_fold, dim3(64), dim3(256), 0, e->stream, (const unsigned long long *)slots.p,
-                       (const uint64_t *)fl.p, nparts, k, (const unsigned long long *)flags.p, dacc,
-                       res.as<unsigned long long>());
-    HIPCHK(hipGetLastError());
-    unsigned long long r0 = 0;
-    HIPCHK(hipMemcpyAsync(&r0, res.p, 8, hipMemcpyDeviceToHost, e->stream));
-    HIPCHK(hipStreamSynchronize(e->stream));
-    *nw = r0;
-    return FK_OK;
+    rc = sp_kpart64(e, pg, 0, keys, n, lo, hi, cs, top_in ? top : ~0ull, r + 1);
+    if (rc) return rc;
+    return sp_sort_rows64(e, pg, n, lo, psh, top_in ? npads : 0ull, top_in ? (uint32_t)((top - lo) >> psh) : ~0u, r,
+                          dacc, out_k, out_c, nw, fallback);
 }
 
 /*
@@ -1734,10 +1834,13 @@ int sparse_finish(fk_engine *e, int32_t seq) {
 
     struct Pass { uint32_t b0, b1; uint64_t n; bool dense; };
     std::vector<Pass> passes;
-    /* k = 17: the fused walks (k_sp_wpart) unless FINDKMER_TUNE sp_walk=0,
-       or sp_pass (a test knob of the key-list passes) is set */
+    /* the fused walks (k_sp_wpart) unless FINDKMER_TUNE sp_walk=0, or sp_pass
+       (a test knob of the key-list passes) is set; k >= 18 while the four
+       first-base passes leave k_kp_sort's parts (2048 x 128 a pass) within
+       its two-blocks-per-CU size on uniform input */
     uint64_t kv = 1;
-    const bool fused = k == 17 && wins > 0 && !e->sp_pass && (!tune_knob("sp_walk", &kv) || kv != 0);
+    const bool fused = wins > 0 && !e->sp_pass && (!tune_knob("sp_walk", &kv) || kv != 0) &&
+                       (k == 17 || wins / 4 <= (2048ull << 7) * (KS_CAP_S - 1024));
     auto plan = [&]() -> int {
     if (single) {
         passes.push_back({0, nbk, wins, false});
@@ -1833,11 +1936,15 @@ int sparse_finish(fk_engine *e, int32_t seq) {
         e->sp_distinct += nw;
         return FK_OK;
     };
-    /* k = 17: the four first-base passes, each a walk that partitions its
-       windows (k_sp_wpart) + the general tiles' list (k_kpart), then
-       k_repart / k_kp_cnt2; SP_RETRY: a row or list overflowed, or it does
-       not fit -- the key-list passes instead */
-    auto walk17 = [&]() -> int {
+    /* the four first-base passes, each a walk that partitions its windows
+       (k_sp_wpart) + the general tiles' list (k_kpart), then k_repart and
+       k_kp_cnt2 (k = 17) or k_kp_sort (k >= 18); SP_RETRY: a row or list
+       overflowed, a part past k_kp_sort's LDS, or it does not fit -- the
+       key-list passes instead */
+    auto walkq = [&]() -> int {
+        const bool wide = k >= 18;
+        const uint32_t ktop = 2u * (uint32_t)k - 2u, cs = ktop - 11u, psh = wide ? cs - 7u : 15u;
+        const size_t gsz = wide ? 8 : 4;   /* a listed window: its key less the pass's base */
         const uint32_t grid = (uint32_t)std::max(1, e->cus);
         uint64_t nbatch = 0, ntiles = 0;   /* batches of all blocks: a row each (+ one per WP_BATCH windows) */
         std::vector<SpSegDev> hsegs;
@@ -1858,8 +1965,8 @@ int sparse_finish(fk_engine *e, int32_t seq) {
         const uint64_t dcap = ntiles / 4 + 1024;
         const uint64_t grows = (uint64_t)grid * ((gcap + (uint64_t)grid * KP_BATCH - 1) / ((uint64_t)grid * KP_BATCH));
         const uint64_t rows_all = rows_walk + grows;
-        const uint64_t need = rows_all * (WP_BATCH * 4ull + 2048ull * 4) + gcap * 4 + dcap * sizeof(SpDefer) +
-                              2 * wins + 16ull * (2048u << 6);
+        const uint64_t need = rows_all * (WP_BATCH * 4ull + 2048ull * 4) + 4 * gcap * gsz + dcap * sizeof(SpDefer) +
+                              (wide ? 4 : 2) * wins + 32ull * (2048u << 7);
         if (need > room || rows_all > 0xFFFFFFFFull) return SP_RETRY;
         int rc = sp_ensure((void **)&e->d_codes, &e->codes_cap, 2 * rows_all * WP_BATCH, sizeof(uint16_t));
         if (!rc) rc = sp_ensure((void **)&e->d_pidx, &e->pidx_cap, rows_all * 2048u, sizeof(uint32_t));
@@ -1873,8 +1980,8 @@ int sparse_finish(fk_engine *e, int32_t seq) {
         unsigned long long *gctr = wctr + 8;   /* k_sp_gtiles: [0..3] windows per first base, [4] short walks */
         uint64_t *goff_d = reinterpret_cast<uint64_t *>(wctr + 12);
         HIPCHK(hipMemcpyAsync(sgd.p, hsegs.data(), hsegs.size() * sizeof(SpSegDev), hipMemcpyHostToDevice, e->stream));
-        HIPCHK(hipFuncSetAttribute((const void *)k_sp_wpart, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                   (int)(WP_BATCH * 4)));
+        const void *wfn = wide ? (const void *)k_sp_wpart<true> : (const void *)k_sp_wpart<false>;
+        HIPCHK(hipFuncSetAttribute(wfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(WP_BATCH * 4)));
         const uint32_t dbg = tune_knob("sp_walk_dbg", &kv2) ? (uint32_t)kv2 : 0u;
         uint64_t gn[4] = {0, 0, 0, 0}, goff[4] = {0, 0, 0, 0};
         for (uint32_t q = 0; q < 4; q++) {
@@ -1882,6 +1989,9 @@ int sparse_finish(fk_engine *e, int32_t seq) {
             HIPCHK(hipMemsetAsync(r, 0, 16, e->stream));
             SpWalk wk{};
             wk.qdig = q ^ (q >> 1);   /* (fk_sigma of one digit) */
+            wk.q = q;
+            wk.ktop = ktop;
+            wk.cs = cs;
             wk.codes = reinterpret_cast<uint32_t *>(e->d_codes);
             wk.idx = e->d_pidx;
             wk.ctr = wctr;
@@ -1893,8 +2003,14 @@ int sparse_finish(fk_engine *e, int32_t seq) {
                 const auto &sg = e->spsegs[si];
                 if (!sg.nranges) continue;
                 wk.seg = (uint32_t)si;
-                hipLaunchKernelGGL(k_sp_wpart, dim3(grid), dim3(1024), (size_t)WP_BATCH * 4, e->stream, hsegs[si].src,
-                                   sg.len, e->k, e->maskk, e->d_kst + sg.st, sg.nranges, sg.cpw, sg.nchunks, wk);
+                if (wide)
+                    hipLaunchKernelGGL(k_sp_wpart<true>, dim3(grid), dim3(1024), (size_t)WP_BATCH * 4, e->stream,
+                                       hsegs[si].src, sg.len, e->k, e->maskk, e->d_kst + sg.st, sg.nranges, sg.cpw,
+                                       sg.nchunks, wk);
+                else
+                    hipLaunchKernelGGL(k_sp_wpart<false>, dim3(grid), dim3(1024), (size_t)WP_BATCH * 4, e->stream,
+                                       hsegs[si].src, sg.len, e->k, e->maskk, e->d_kst + sg.st, sg.nranges, sg.cpw,
+                                       sg.nchunks, wk);
                 HIPCHK(hipGetLastError());
             }
             unsigned long long c[5];   /* rows, tiles deferred, -, windows in rows, faults */
@@ -1908,10 +2024,11 @@ int sparse_finish(fk_engine *e, int32_t seq) {
                     const unsigned gg = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((c[1] + SP_WAVES - 1) / SP_WAVES,
                                                                                          (uint64_t)e->cus * 8));
                     const size_t lds = (size_t)SP_WAVES * FK_TILE_BYTES * sizeof(uint64_t);
-                    HIPCHK(hipFuncSetAttribute((const void *)k_sp_gtiles<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-                    HIPCHK(hipFuncSetAttribute((const void *)k_sp_gtiles<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+                    for (const void *f : {(const void *)k_sp_gtiles<false, uint32_t>, (const void *)k_sp_gtiles<true, uint32_t>,
+                                          (const void *)k_sp_gtiles<true, uint64_t>})
+                        HIPCHK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
                     HIPCHK(hipMemsetAsync(gctr, 0, 40, e->stream));
-                    hipLaunchKernelGGL(k_sp_gtiles<false>, dim3(gg), dim3(SP_WAVES * 64u), lds, e->stream,
+                    hipLaunchKernelGGL((k_sp_gtiles<false, uint32_t>), dim3(gg), dim3(SP_WAVES * 64u), lds, e->stream,
                                        (const SpDefer *)dfr.p, (uint64_t)c[1], (const SpSegDev *)sgd.p, e->k, e->maskk,
                                        (uint32_t *)nullptr, (const uint64_t *)nullptr, gctr,
                                        nodes ? shorts.as<uint64_t>() : nullptr, scap);
@@ -1927,12 +2044,19 @@ int sparse_finish(fk_engine *e, int32_t seq) {
                     }
                     if (nodes && g[4] > scap) return SP_RETRY;
                     if (tot) {
-                        if (!gl.alloc(tot * 4)) return FK_E_OOM;
+                        if (!gl.alloc(tot * gsz)) return FK_E_OOM;
                         HIPCHK(hipMemcpyAsync(goff_d, goff, sizeof goff, hipMemcpyHostToDevice, e->stream));
                         HIPCHK(hipMemsetAsync(gctr, 0, 32, e->stream));
-                        hipLaunchKernelGGL(k_sp_gtiles<true>, dim3(gg), dim3(SP_WAVES * 64u), lds, e->stream,
-                                           (const SpDefer *)dfr.p, (uint64_t)c[1], (const SpSegDev *)sgd.p, e->k, e->maskk,
-                                           gl.as<uint32_t>(), (const uint64_t *)goff_d, gctr, (uint64_t *)nullptr, scap);
+                        if (wide)
+                            hipLaunchKernelGGL((k_sp_gtiles<true, uint64_t>), dim3(gg), dim3(SP_WAVES * 64u), lds, e->stream,
+                                               (const SpDefer *)dfr.p, (uint64_t)c[1], (const SpSegDev *)sgd.p, e->k,
+                                               e->maskk, gl.as<uint64_t>(), (const uint64_t *)goff_d, gctr,
+                                               (uint64_t *)nullptr, scap);
+                        else
+                            hipLaunchKernelGGL((k_sp_gtiles<true, uint32_t>), dim3(gg), dim3(SP_WAVES * 64u), lds, e->stream,
+                                               (const SpDefer *)dfr.p, (uint64_t)c[1], (const SpSegDev *)sgd.p, e->k,
+                                               e->maskk, gl.as<uint32_t>(), (const uint64_t *)goff_d, gctr,
+                                               (uint64_t *)nullptr, scap);
                         HIPCHK(hipGetLastError());
                     }
                 }
@@ -1948,15 +2072,23 @@ int sparse_finish(fk_engine *e, int32_t seq) {
             uint64_t nw = 0;
             uint64_t *ok = e->d_spk + e->sp_distinct;
             uint32_t *oc = e->d_spc + e->sp_distinct;
-            rc = sp_kpart32(e, pg, c[0], gl.as<uint32_t>() + goff[q], gn[q], r + 1);
-            if (!rc) rc = sp_count_rows32(e, pg, c[3] + gn[q], (uint64_t)q << 32, 0, r, dacc, ok, oc, &nw);
+            if (wide) {
+                pg.split = 7u;
+                bool fb = false;
+                rc = sp_kpart64(e, pg, c[0], gl.as<uint64_t>() + goff[q], gn[q], 0, 1ull << ktop, cs, ~0ull, r + 1);
+                if (!rc) rc = sp_sort_rows64(e, pg, c[3] + gn[q], (uint64_t)q << ktop, psh, 0, ~0u, r, dacc, ok, oc, &nw, &fb);
+                if (!rc && fb) return SP_RETRY;   /* (the library sort needs the pass's key list) */
+            } else {
+                rc = sp_kpart32(e, pg, c[0], gl.as<uint32_t>() + goff[q], gn[q], r + 1);
+                if (!rc) rc = sp_count_rows32(e, pg, c[3] + gn[q], (uint64_t)q << 32, 0, r, dacc, ok, oc, &nw);
+            }
             if (!rc) rc = join(ok, nw);
             if (rc) return rc;
         }
         return FK_OK;
     };
     if (fused) {
-        int rc = walk17();
+        int rc = walkq();
         if (rc == SP_RETRY) {   /* from the start, by the key-list passes */
             e->sp_distinct = 0;
             HIPCHK(hipMemsetAsync(dacc, 0, FKS_ACC_N * sizeof(unsigned long long), e->stream));

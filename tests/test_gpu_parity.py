@@ -995,13 +995,15 @@ def test_sparse_count_bins_wrap_and_top_key(k):
     assert_same_sparse(b">w\n" + lines + b"\n", k)
 
 
-@pytest.mark.parametrize("tune", ["sp_walk=0", "sp_walk_rows=1", "sp_walk_glist=1"])
-def test_sparse_k17_walk_fallbacks(tune, monkeypatch):
-    """k = 17's fused walks (k_sp_wpart) against the key-list passes:
-    sp_walk=0 takes the key lists; a row or general-tile list capacity of 1
-    overflows in the first walk and the finish restarts by the key lists"""
+@pytest.mark.parametrize("tune", ["sp_walk=0", "sp_walk_rows=1", "sp_walk_glist=1", "sp_walk_dbg=1"])
+@pytest.mark.parametrize("k", [17, 20])
+def test_sparse_walk_fallbacks(k, tune, monkeypatch):
+    """the fused walks (k_sp_wpart) against the key-list passes: sp_walk=0
+    takes the key lists; a row or general-tile list capacity of 1 overflows
+    in the first walk and the finish restarts by the key lists; sp_walk_dbg=1
+    sends every tile through k_sp_gtiles' list"""
     monkeypatch.setenv("FINDKMER_TUNE", tune)
-    assert_same_sparse(mixed_input(1717, 300_000), 17)
+    assert_same_sparse(mixed_input(1717 + k, 300_000), k)
 
 
 def test_sparse_k17_walk_rows_split():
