@@ -194,6 +194,11 @@ VARIANTS = {
         ("                    if (i == 0 || part[i] != part[i - 1]) at = atomicAdd(&cur[part[i]], len[i]);",
          "                    if (i == 0) at = t * 16u + len[i] * 0u;"),
     ],
+    # k = 17's passes through k_repart<uint16_t, 8> (8 coarse slices a block: 512-B row spans, 64-B part segments)
+    "rp17g8": [
+        ("    hipLaunchKernelGGL(k_repart<uint16_t>, dim3(2048u / REPART_G), dim3(1024), 0, e->stream, pg, e->d_parts, alloc,\n                       meta, (uint64_t)e->parts_cap, alloc + 1, 15u, nullptr);",
+         "    hipLaunchKernelGGL((k_repart<uint16_t, 8u>), dim3(2048u / 8u), dim3(1024), 0, e->stream, pg, e->d_parts, alloc,\n                       meta, (uint64_t)e->parts_cap, alloc + 1, 15u, nullptr);"),
+    ],
     # k = 15 through k_repart<uint16_t, 4> (two blocks per CU) instead of 8 slices a block
     "k15g4": [
         ("        if (pg.split <= 4)\n", "        if (pg.split <= 3)\n"),
