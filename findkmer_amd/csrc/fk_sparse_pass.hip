@@ -512,8 +512,8 @@ struct SpDefer {
     uint32_t R, hdr, seg, pad;
 };
 struct SpWalk {
-    uint32_t qdig;                 /* k = 17: the pass's first base in the internal encoding */
-    uint32_t q, ktop, cs;          /* k >= 18: the first base (reference order), its bit 2k - 2, code bits */
+    uint32_t q;                    /* the pass's first base (reference order) */
+    uint32_t ktop, cs;             /* k >= 18: the first base's bit 2k - 2, code bits */
     uint32_t *codes;               /* rows of WP_BATCH codes (k_kpart's layout) */
     uint32_t *idx;                 /* [row][2048] run words */
     unsigned long long *ctr;       /* [0] rows claimed, [1] tiles deferred, [3] windows placed in rows,
@@ -524,13 +524,19 @@ struct SpWalk {
     uint32_t seg;                  /* the launch's segment */
     uint32_t dbg;                  /* FINDKMER_TUNE sp_walk_dbg: 1 = every tile deferred (tests) */
 };
+/* sigma32: fk_sigma of 16 digits (the internal A0 C1 T2 G3 to the
+   reference's A0 C1 G2 T3, digit by digit: so a window of mapped words is
+   the mapped window, and the stashed words are mapped once per tile) */
+__device__ __forceinline__ uint32_t sigma32(uint32_t x) { return x ^ ((x >> 1) & 0x55555555u); }
 struct WpTile {
-    uint32_t c0, s0, c1, s1;       /* k = 17, per half: 16-digit context, 16-digit word */
+    uint32_t c0, s0, c1, s1;       /* k = 17, per half: 16-digit context, 16-digit word (reference order) */
     uint32_t fl;                   /* bit 0: has windows, bits 1, 2: half 0 / 1 had a '\n' (slot 0 no window) */
 };
 /* 18 <= k <= 20 (windows up to 20 digits): as k_sp_emit's sp_fast_emit, the
    32 digits before half 0 (the previous lane's {BC, B2}) and the Emit words
-   AC, A2, B2 (half 1's 32 digits before it are {AC, A2}) */
+   AC, A2, B2 (half 1's 32 digits before it are {AC, A2}), all mapped to the
+   reference's digit order (fk_sigma maps digit by digit, so a window of the
+   mapped words is the mapped window) */
 struct WpTileW {
     uint32_t p0h, p0l, ac, a2, b2;
     uint32_t fl;
@@ -538,7 +544,7 @@ struct WpTileW {
 /* a stashed fast tile's in-pass windows: HIST into the slices' counts, else
    placed at their slices' cursors */
 template <bool HIST>
-__device__ __forceinline__ void wp_tile(const WpTile &x, uint32_t qdig, uint32_t *hist, uint32_t *cur, uint32_t *ent) {
+__device__ __forceinline__ void wp_tile(const WpTile &x, uint32_t q, uint32_t *hist, uint32_t *cur, uint32_t *ent) {
 #pragma unroll
     for (int h = 0; h < 2; h++) {
         const uint32_t C = h ? x.c1 : x.c0, S = h ? x.s1 : x.s0;
@@ -551,9 +557,9 @@ __device__ __forceinline__ void wp_tile(const WpTile &x, uint32_t qdig, uint32_t
             for (int j = 0; j < 8; j++) {
                 const int i = 8 * g + j;
                 const uint32_t sh = 30u - 2u * (uint32_t)i;
-                const uint32_t v = i < 15 ? __builtin_amdgcn_alignbit(C, S, sh) : S;
-                const uint32_t r = v ^ ((v >> 1) & 0x55555555u);   /* fk_sigma of the low 16 digits */
-                in[j] = __builtin_amdgcn_ubfe(C, sh, 2u) == qdig && (i > 0 || !skip0);
+                /* (the words are in reference digit order already: see WpTile) */
+                const uint32_t r = i < 15 ? __builtin_amdgcn_alignbit(C, S, sh) : S;
+                in[j] = __builtin_amdgcn_ubfe(C, sh, 2u) == q && (i > 0 || !skip0);
                 b[j] = r >> 21;
                 cd[j] = r & 0x1FFFFFu;
             }
@@ -580,28 +586,29 @@ __device__ __forceinline__ void wp_tile(const WpTile &x, uint32_t qdig, uint32_t
 template <bool HIST>
 __device__ __forceinline__ void wp_tile_w(const WpTileW &x, uint32_t q, uint32_t ktop, uint64_t maskk, uint32_t cs,
                                           uint32_t *hist, uint32_t *cur, uint32_t *ent) {
-    const uint64_t relm = (1ull << ktop) - 1ull;
-    const uint32_t cm = (1u << cs) - 1u;
+    (void)maskk;
+    const uint32_t cm = (1u << cs) - 1u, tsh = ktop - 32u;   /* the first base: bits [ktop, ktop + 2) of the key */
 #pragma unroll
     for (int h = 0; h < 2; h++) {
-        const uint64_t pv = h ? (((uint64_t)x.ac << 32) | x.a2) : (((uint64_t)x.p0h << 32) | x.p0l);
+        /* the 96-bit stream {pvh, pvl, ra}: the 32 digits before the half,
+           then its 16 (or, after a '\n', 15 left-aligned) digits; the window
+           ending at the half's digit j is its bits [30 - 2j, 30 - 2j + 2k) */
+        const uint32_t pvh = h ? x.ac : x.p0h, pvl = h ? x.a2 : x.p0l;
         const bool hf = (x.fl >> (1 + h)) & 1u;
-        const uint32_t R = (h ? x.b2 : x.a2) & (hf ? 0x3FFFFFFFu : 0xFFFFFFFFu);
-        const uint32_t D = hf ? 15u : 16u;   /* the half's digits (right-aligned in R) */
+        const uint32_t r = h ? x.b2 : x.a2;
+        const uint32_t ra = hf ? r << 2 : r;
 #pragma unroll
         for (int g = 0; g < 2; g++) {
             uint32_t b[8], cd[8], p[8];
             bool in[8];
 #pragma unroll
             for (int jj = 0; jj < 8; jj++) {
-                const uint32_t j = 8u * (uint32_t)g + (uint32_t)jj;
-                const bool valid = j < D;
-                const uint32_t sh = valid ? 2u * (D - 1u - j) : 0u;
-                const uint64_t key = fk_sigma(((pv << (2u * j + 2u)) | (uint64_t)(R >> sh)) & maskk);
-                in[jj] = valid && (uint32_t)(key >> ktop) == q;
-                const uint64_t rel = key & relm;
-                b[jj] = (uint32_t)(rel >> cs);
-                cd[jj] = (uint32_t)rel & cm;
+                const uint32_t j = 8u * (uint32_t)g + (uint32_t)jj, sh = 30u - 2u * j;
+                const uint32_t lo = j < 15u ? __builtin_amdgcn_alignbit(pvl, ra, sh) : ra;
+                const uint32_t hi = j < 15u ? __builtin_amdgcn_alignbit(pvh, pvl, sh) : pvl;
+                in[jj] = (j < 15u || !hf) && __builtin_amdgcn_ubfe(hi, tsh, 2u) == q;
+                b[jj] = __builtin_amdgcn_alignbit(hi, lo, cs) & 0x7FFu;
+                cd[jj] = lo & cm;
             }
             if (HIST) {
 #pragma unroll
@@ -675,17 +682,19 @@ k_sp_wpart(const uint8_t *buf, uint64_t len, int k, uint64_t maskk, const XState
         if (full && st.hdr == 0 && !(wk.dbg & 1u) && tile_fast<true, H_EMIT, false>(cx, w, st, f, cnt, 1u, &fe)) {
             if (fe.deep) {
                 if constexpr (WIDE) {
-                    x.p0h = from_prev_lane(fe.BC, (uint32_t)(c0 >> 32));
-                    x.p0l = from_prev_lane(fe.B2, (uint32_t)c0);
-                    x.ac = fe.AC;
-                    x.a2 = fe.A2;
-                    x.b2 = fe.B2;
+                    x.p0h = sigma32(from_prev_lane(fe.BC, (uint32_t)(c0 >> 32)));
+                    x.p0l = sigma32(from_prev_lane(fe.B2, (uint32_t)c0));
+                    x.ac = sigma32(fe.AC);
+                    /* (a '\n' half's word: its top digit is the digit before it, masked off) */
+                    x.a2 = sigma32(fe.A2);
+                    x.b2 = sigma32(fe.h1 ? fe.B2 & 0x3FFFFFFFu : fe.B2);
                 } else {
-                    const uint32_t xp = from_prev_lane(fe.B2, (uint32_t)c0);   /* the 16 digits before half 0 */
+                    const uint32_t xp = sigma32(from_prev_lane(fe.B2, (uint32_t)c0));   /* the 16 digits before half 0 */
+                    const uint32_t a2 = sigma32(fe.A2);
                     x.c0 = fe.h0 ? xp >> 2 : xp;
-                    x.s0 = fe.A2;
-                    x.c1 = fe.h1 ? fe.A2 >> 2 : fe.A2;
-                    x.s1 = fe.B2;
+                    x.s0 = a2;
+                    x.c1 = fe.h1 ? a2 >> 2 : a2;
+                    x.s1 = sigma32(fe.B2);
                 }
                 x.fl = 1u | (fe.h0 ? 2u : 0u) | (fe.h1 ? 4u : 0u);
             }
@@ -710,8 +719,8 @@ k_sp_wpart(const uint8_t *buf, uint64_t len, int k, uint64_t maskk, const XState
             if (hst) wp_tile_w<true>(x, wk.q, wk.ktop, maskk, wk.cs, hist, cur, ent);
             else wp_tile_w<false>(x, wk.q, wk.ktop, maskk, wk.cs, hist, cur, ent);
         } else {
-            if (hst) wp_tile<true>(x, wk.qdig, hist, cur, ent);
-            else wp_tile<false>(x, wk.qdig, hist, cur, ent);
+            if (hst) wp_tile<true>(x, wk.q, hist, cur, ent);
+            else wp_tile<false>(x, wk.q, hist, cur, ent);
         }
     };
     /* the stashed tiles' in-pass windows into the slices' counts (sel: one
@@ -1988,7 +1997,6 @@ int sparse_finish(fk_engine *e, int32_t seq) {
             HIPCHK(hipMemsetAsync(wctr, 0, 64, e->stream));
             HIPCHK(hipMemsetAsync(r, 0, 16, e->stream));
             SpWalk wk{};
-            wk.qdig = q ^ (q >> 1);   /* (fk_sigma of one digit) */
             wk.q = q;
             wk.ktop = ktop;
             wk.cs = cs;

@@ -7,7 +7,7 @@ mkdir -p gpurun_out
 timeout -k 10 500 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_scale.py -m gpu -x -v --timeout 120 --timeout-method thread -k "sparse" \
   > gpurun_out/c10_tests.log 2>&1 || { tail -40 gpurun_out/c10_tests.log; exit 1; }
 tail -3 gpurun_out/c10_tests.log
-for kt in "20:" "20:sp_walk=0" "18:" "17:"; do
+for kt in "17:" "20:"; do
   IFS=: read k tune <<< "$kt"
   FINDKMER_TUNE=$tune timeout -k 10 240 python bench.py --k $k --fasta-line 80 --bases 10000000000 --steps 4 --warmup 2 \
     --north-star-bases 0 --no-cpu-baseline > gpurun_out/c10_b.json 2> gpurun_out/c10_b.err || { tail -20 gpurun_out/c10_b.err; exit 1; }
