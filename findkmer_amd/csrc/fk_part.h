@@ -208,9 +208,18 @@ k_repart(PartGeo pg, OT *out, unsigned long long *alloc, PartMeta *meta, uint64_
         uint32_t npc = 0, s0 = 0, cum = 0;
         if (r < nrows) {
             bool have = false;
+            /* the row's G run words as 16-B pieces (b0 and the row stride
+               are multiples of 4 words) */
+            static_assert(G % 4u == 0u, "G run words as 16-B pieces");
+            uint32_t ew[G];
+#pragma unroll
+            for (uint32_t j = 0; j < G; j += 4u) {
+                const uint4 q = *reinterpret_cast<const uint4 *>(pg.idx + (size_t)r * pg.nslices + b0 + j);
+                ew[j] = q.x; ew[j + 1] = q.y; ew[j + 2] = q.z; ew[j + 3] = q.w;
+            }
 #pragma unroll
             for (uint32_t j = 0; j < G; j++) {
-                const uint32_t e = pg.idx[(size_t)r * pg.nslices + b0 + j];
+                const uint32_t e = ew[j];
                 const uint32_t c = run_count(e);
                 if (c && !have) { s0 = e >> 16; have = true; }
                 cum += c;

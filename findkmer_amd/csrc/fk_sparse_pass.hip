@@ -1372,14 +1372,24 @@ k_kp_sort(const uint32_t *in, const PartMeta *meta, uint64_t cap_in, uint64_t lo
     }
     const uint32_t nn = bad ? 0u : n;
     /* 3. runs: thread t takes positions [t * KSI, +KSI); a run
-       starts where the key changes */
+       starts where the key changes (the thread's keys read once, as 16-B
+       pieces: its 48 or 96 bytes start 16-B aligned) */
     const uint32_t p0 = t * KSI;
-    uint32_t nz = 0;
+    uint32_t kk[KSI];
+    static_assert(KSI % 4u == 0u, "KSI keys as 16-B pieces");
+#pragma unroll
+    for (uint32_t j = 0; j < KSI; j += 4u) {
+        const uint4 q = reinterpret_cast<const uint4 *>(keys + p0)[j / 4u];
+        kk[j] = q.x; kk[j + 1] = q.y; kk[j + 2] = q.z; kk[j + 3] = q.w;
+    }
+    const uint32_t kprev = p0 ? keys[p0 - 1] : 0u;
+    uint32_t starts = 0;   /* bit j: a run starts at p0 + j */
 #pragma unroll
     for (uint32_t j = 0; j < KSI; j++) {
         const uint32_t i = p0 + j;
-        if (i < nn && (i == 0 || keys[i] != keys[i - 1])) nz++;
+        if (i < nn && (i == 0 || kk[j] != (j ? kk[j - 1] : kprev))) starts |= 1u << j;
     }
+    const uint32_t nz = (uint32_t)__popc(starts);
     const uint32_t inc = wscan_incl32(nz);
     if (lane == 63) wnz[wv] = inc;
     __syncthreads();
@@ -1401,10 +1411,8 @@ k_kp_sort(const uint32_t *in, const PartMeta *meta, uint64_t cap_in, uint64_t lo
     {
         uint32_t o = off;
 #pragma unroll
-        for (uint32_t j = 0; j < KSI; j++) {
-            const uint32_t i = p0 + j;
-            if (i < nn && (i == 0 || keys[i] != keys[i - 1])) rs[o++] = (uint16_t)i;
-        }
+        for (uint32_t j = 0; j < KSI; j++)
+            if ((starts >> j) & 1u) rs[o++] = (uint16_t)(p0 + j);
         if (t == 0) rs[runs] = (uint16_t)nn;
     }
     if (wv == 0) {
