@@ -194,6 +194,8 @@ VARIANTS = {
         ("                    if (i == 0 || part[i] != part[i - 1]) at = atomicAdd(&cur[part[i]], len[i]);",
          "                    if (i == 0) at = t * 16u + len[i] * 0u;"),
     ],
+    # the source as it is (an A/B baseline built before a product edit)
+    "base": [],
     # k = 17's passes through k_repart<uint16_t, 8> (8 coarse slices a block: 512-B row spans, 64-B part segments)
     "rp17g8": [
         ("    hipLaunchKernelGGL(k_repart<uint16_t>, dim3(2048u / REPART_G), dim3(1024), 0, e->stream, pg, e->d_parts, alloc,\n                       meta, (uint64_t)e->parts_cap, alloc + 1, 15u, nullptr);",
