@@ -422,7 +422,13 @@ extern "C" int fk_engine_create(int k, const fk_opts *opts, fk_engine **out) {
        ranges), events=0 (no HIP events),
        seg_kb=N (device feeds cut into N-KiB segments), sp_pass=N (17 <= k:
        at most N window keys per sorted pass; smaller buckets merge, larger
-       ones take the dense path) */
+       ones take the dense path; the key-list route), route=0/1/2 (k = 15,
+       16 sharded tables reduce-scattered / routed at world > 1 / routed at
+       world 1 too).  Read at finish (sparse_finish): sp_walk=0 (the
+       key-list passes instead of the fused first-base walks),
+       sp_walk_rows=N / sp_walk_glist=N (the walks' row and general-tile
+       list capacities: tests of the restart), sp_walk_dbg=1 (every tile
+       through k_sp_gtiles) */
     uint64_t kv = 0;
     if (tune_knob("no_mixed", &kv)) e->no_mixed = kv == 1;
     /* k_count takes a couple of general tiles per range (the stream start, an
