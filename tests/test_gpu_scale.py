@@ -136,6 +136,36 @@ def test_sparse_genome_10g_key_ranges_vs_oracle(genome10g, k):
     assert abs(r.distinct - want) < 1e-3 * want, (r.distinct, want)
 
 
+@pytest.mark.parametrize("k", [17, 20])
+def test_sparse_segmented_feeds_equal_one_feed(genome10g, k):
+    """the fused first-base walks over many segments (every feed is one; a
+    walk launch per segment, their rows and listed tiles shared) against one
+    feed of the same 3 G bases: uneven device feeds, misaligned ones staged
+    (retained copies) and aligned ones borrowed -- the same statistics and
+    the same runs in seven key ranges"""
+    buf, size, host = genome10g
+    n = 3_000_000_000 + 12_345
+    cuts = [0, 1 << 20, (1 << 20) + 17, 700_000_001, 700_000_001 + 4096, 1_900_000_000, n]
+    ranges = _slices(k, 1 << 22)
+    res = []
+    for split, borrow in ((False, False), (True, True)):
+        with fk.Engine(k, want_nodes=True, borrow_input=borrow) as e:
+            if split:
+                for a, b in zip(cuts[:-1], cuts[1:]):
+                    e.feed_device(buf.data_ptr() + a, b - a)
+            else:
+                e.feed_device(buf.data_ptr(), n)
+            rc, r = e.finish(allow=(fk.FK_OK, fk.FK_E_UNTERMINATED_HEADER))
+            got = [e.sparse_range(lo, hi) for lo, hi in ranges]
+        res.append((r, got))
+    (r1, g1), (r2, g2) = res
+    assert (r1.windows, r1.distinct, r1.nodes, r1.valid_bases, list(r1.base_count), list(r1.depth1)) == \
+        (r2.windows, r2.distinct, r2.nodes, r2.valid_bases, list(r2.base_count), list(r2.depth1))
+    for (k1, c1), (k2, c2) in zip(g1, g2):
+        assert np.array_equal(k1, k2) and np.array_equal(c1, c2)
+    assert sum(len(x[0]) for x in g1) > 0
+
+
 @pytest.mark.parametrize("k", [14, 15, 16])
 def test_genome_1g_table_range_vs_oracle(k):
     """k = 14 (4096 slices of 2^16 bins, k_bucket16), k = 15 and k = 16 (the
