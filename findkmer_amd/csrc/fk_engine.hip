@@ -356,7 +356,7 @@ extern "C" void fk_engine_destroy(fk_engine *e) {
     if (e->stream) hipStreamSynchronize(e->stream);
     hipFree(e->d_table); hipFree(e->d_short); hipFree(e->d_sub); hipFree(e->d_snap);
     hipFree(e->d_pairs);
-    hipFree(e->d_parts); hipFree(e->d_pmeta); hipFree(e->d_glist); hipFree(e->d_fz);
+    hipFree(e->d_parts); hipFree(e->d_pmeta); hipFree(e->d_rdesc); hipFree(e->d_rbm); hipFree(e->d_glist); hipFree(e->d_fz);
     hipFree(e->d_rsend); hipFree(e->d_rrecv); hipFree(e->d_raux); hipFree(e->d_rsz);
     for (int i = 0; i < fk_engine::NPOOL; i++) hipFree(e->pool_p[i]);
     hipFree(e->d_codes); hipFree(e->d_pidx); hipFree(e->d_pflag); hipFree(e->d_acc); hipFree(e->d_res); hipFree(e->d_tmp);

@@ -84,6 +84,9 @@ struct fk_engine {
     uint16_t *d_parts = nullptr;              /* k = 15, 16: the second level's part streams (k_repart) */
     uint64_t parts_cap = 0;
     void *d_pmeta = nullptr;                  /* k = 15, 16: PartMeta per part + the allocation counter */
+    /* k_repart<SEG>'s segment table and per-block (base, rounds) + its claim counter */
+    unsigned long long *d_rdesc = nullptr, *d_rbm = nullptr;
+    uint64_t rdesc_cap = 0, rbm_cap = 0;
     int32_t *d_rsend = nullptr, *d_rrecv = nullptr;   /* routed sharded tables: blobs out / in (fk_engine_route_*) */
     uint64_t rsend_cap = 0, rrecv_cap = 0, rsend_words = 0;
     void *d_raux = nullptr;                   /* ... their per-destination geometry and slot offsets */
@@ -383,6 +386,9 @@ int flush_zero(fk_engine *e, bool keep_table = false);
 int set_dev(fk_engine *e, bool flush = true);
 int zero_all(fk_engine *e);
 bool tune_knob(const char *name, uint64_t *v);
+/* k_repart<SEG> over pg's rows (ncodes codes at most): its segment table,
+   block metadata and the parts buffer sized, the claim counters zeroed */
+int repart_seg_alloc(fk_engine *e, const PartGeo &pg, uint64_t ncodes, uint32_t gp, RepartSeg *sg);
 int grow_arrays(fk_engine *e, uint64_t nranges);
 bool int32_zone_possible(const fk_engine *e, uint64_t len);
 int check_fault(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t lo, const Geo &g);

@@ -164,14 +164,77 @@ struct PartMeta {
 #define RP_CHUNK 1024u                  /* rows per chunk: a lane each */
 #define RP_NOPART 0xFFFFu
 
+/*
+ * SEG (round 6, 16-bit parts): one pass over the codes instead of two.  A
+ * round's codes, counting-sorted by part in LDS, are written as one
+ * contiguous run at an offset claimed for the round (pass A sized every
+ * part's stream exactly and pass B wrote each part's segment after its
+ * earlier rounds', 30 % and 17 % of k = 16's k_repart); each part's
+ * segment of the round -- (its codes' first position, count) -- goes to a
+ * segment table, part-major per block, so that the consumer gathers a part
+ * from its segments.  The block's rounds (counted from the run words alone
+ * before the pass) size its table: desc[dbase + part * R + round], and
+ * bmeta[2 blk] = dbase, [2 blk + 1] = R.  Table entries are staged in LDS
+ * for RP_SEGS rounds and written as 64-B pieces per part.
+ */
+#define RP_SEGS 8u
+struct RepartSeg {
+    unsigned long long *desc;       /* (code position << 16) | count per (part, round) */
+    uint64_t dcap;                  /* entries of desc */
+    unsigned long long *dalloc;     /* entries claimed */
+    unsigned long long *bmeta;      /* per block: dbase, rounds */
+};
+
 /* OT = uint16_t: a code's part is its bits [15, 15 + split), stored as its
    low 15 bits (k = 15, 16; k = 17 passes, psh = 15).  OT = uint32_t (wide
    sparse passes): part bits [psh, psh + 7), stored as the low psh bits.
    The rows' runs hold at most 65535 codes (C32 / k_kpart rows: 32 K). */
-template <typename OT, uint32_t G = REPART_G>
+/* the codes of part i of a SEG k_repart block (its table row at desc +
+   dbase + i R) as f(code); the number of codes is returned to every lane
+   of the block through *mn (block-uniform after a barrier the caller
+   places).  A wave takes every nw-th segment: its lanes load up to 64
+   segments' entries at once, then U segments' codes are in flight per
+   lane (a segment is one round's codes of the part: ~64 at k = 16, 17,
+   ~256 at k = 15). */
+template <uint32_t U = 4u, typename F>
+__device__ __forceinline__ uint32_t seg_codes(const uint16_t *in, const unsigned long long *desc,
+                                              unsigned long long dbase, uint32_t R, uint32_t i, F &&f) {
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    const unsigned long long *d = desc + dbase + (unsigned long long)i * R;
+    uint32_t mine = 0;   /* codes of the segments this lane's entries name */
+    for (uint32_t r0 = wv; r0 < R; r0 += 64u * nw) {
+        const uint32_t rl = r0 + lane * nw;
+        const unsigned long long e = rl < R ? d[rl] : 0ull;
+        mine += (uint32_t)(e & 0xFFFFu);
+        const uint32_t ns = min(64u, (R - r0 + nw - 1u) / nw);
+        for (uint32_t s = 0; s < ns; s += U) {
+            uint64_t a[U];
+            uint32_t n[U], mx = 0;
+#pragma unroll
+            for (uint32_t u = 0; u < U; u++) {
+                const unsigned long long eu = s + u < ns ? rdlane64(e, (int)(s + u)) : 0ull;
+                a[u] = eu >> 16;
+                n[u] = (uint32_t)(eu & 0xFFFFu);
+                mx = max(mx, n[u]);
+            }
+            for (uint32_t j = lane; j < mx; j += 64u) {
+                uint32_t c[U];
+#pragma unroll
+                for (uint32_t u = 0; u < U; u++) c[u] = j < n[u] ? (uint32_t)in[a[u] + j] : 0u;
+#pragma unroll
+                for (uint32_t u = 0; u < U; u++)
+                    if (j < n[u]) f(c[u]);
+            }
+        }
+    }
+    return mine;
+}
+
+template <typename OT, uint32_t G = REPART_G, bool SEG = false>
 __global__ void __launch_bounds__(1024, sizeof(OT) == 2 && G == REPART_G ? REPART_MINW : 1)
 k_repart(PartGeo pg, OT *out, unsigned long long *alloc, PartMeta *meta, uint64_t cap,
-         unsigned long long *err, uint32_t psh, unsigned long long *pmax) {
+         unsigned long long *err, uint32_t psh, unsigned long long *pmax, RepartSeg sg = RepartSeg{}) {
+    static_assert(!SEG || sizeof(OT) == 2, "SEG: 16-bit parts");
     /* (G coarse slices of 2^split parts: G << split <= GP, else nothing is
        done and the pass fails -- the arrays below are sized by GP) */
     constexpr uint32_t GP = REPART_GP(OT, G);
@@ -191,6 +254,9 @@ k_repart(PartGeo pg, OT *out, unsigned long long *alloc, PartMeta *meta, uint64_
     __shared__ uint16_t rcum[RP_CHUNK][G];
     __shared__ uint32_t wsc[16];
     __shared__ __attribute__((aligned(16))) OT rbuf[ROUND * 4u];
+    __shared__ unsigned long long stage[SEG ? RP_SEGS : 1u][SEG ? GP : 1u];
+    __shared__ unsigned long long s_base, s_dbase;
+    __shared__ uint32_t s_n;
     if ((G << pg.split) > GP) {
         if (threadIdx.x == 0) atomicOr(err, (unsigned long long)FK_FAULT_PARTS);
         return;
@@ -299,8 +365,21 @@ k_repart(PartGeo pg, OT *out, unsigned long long *alloc, PartMeta *meta, uint64_
             }
         }
     };
+    uint32_t R = 0;   /* SEG: the block's rounds */
+    if constexpr (SEG) {
+        for (uint32_t c0 = 0; c0 < nrows; c0 += RP_CHUNK) R += (load_chunk(c0) + ROUND - 1u) / ROUND;
+        if (t == 0) {
+            const unsigned long long d = atomicAdd(sg.dalloc, (unsigned long long)gp * R);
+            const bool over = d + (unsigned long long)gp * R > sg.dcap;
+            if (over) atomicOr(err, (unsigned long long)FK_FAULT_PARTS);
+            s_dbase = over ? ~0ull : d;
+            sg.bmeta[2 * (size_t)blockIdx.x] = over ? 0ull : d;
+            sg.bmeta[2 * (size_t)blockIdx.x + 1] = over ? 0ull : R;
+        }
+        __syncthreads();
+    }
     /* pass A: entries per part (runs of one part in a thread's codes: one atomic) */
-    for (uint32_t c0 = 0; c0 < nrows; c0 += RP_CHUNK) {
+    for (uint32_t c0 = 0; c0 < (SEG ? 0u : nrows); c0 += RP_CHUNK) {
         const uint32_t tot = load_chunk(c0);
         for (uint32_t q0 = 0; q0 < tot; q0 += ROUND) {
             const uint32_t q = q0 + t * PPT;
@@ -322,7 +401,7 @@ k_repart(PartGeo pg, OT *out, unsigned long long *alloc, PartMeta *meta, uint64_
         }
         __syncthreads();   /* (the chunk's LDS rows are rewritten next) */
     }
-    if (t < 64) {   /* the parts' 8-aligned stream starts in the group's region */
+    if (!SEG && t < 64) {   /* the parts' 8-aligned stream starts in the group's region */
         uint32_t carry = 0;
         for (uint32_t p0 = 0; p0 < gp; p0 += 64u) {
             const uint32_t p = p0 + lane;
@@ -354,7 +433,9 @@ k_repart(PartGeo pg, OT *out, unsigned long long *alloc, PartMeta *meta, uint64_
     }
     __syncthreads();
     /* pass B: each round counted by part, placed in LDS by part, and each
-       part's segment written after its earlier rounds' */
+       part's segment written after its earlier rounds' (SEG: the round
+       written as one run, its segments to the table) */
+    uint32_t rr = 0;   /* SEG: the round's index in the block */
     for (uint32_t c0 = 0; c0 < nrows; c0 += RP_CHUNK) {
         const uint32_t tot = load_chunk(c0);
         for (uint32_t q0 = 0; q0 < tot; q0 += ROUND) {
@@ -390,6 +471,19 @@ k_repart(PartGeo pg, OT *out, unsigned long long *alloc, PartMeta *meta, uint64_
                     if (p < gp) { ho[p] = carry + inc - n; cur[p] = carry + inc - n; }
                     carry += rdlane(inc, 63);
                 }
+                if constexpr (SEG) {
+                    /* the round's run: claimed (8-aligned), its parts' segments staged */
+                    unsigned long long g0 = 0;
+                    if (lane == 0) g0 = atomicAdd(alloc, (unsigned long long)((carry + 7u) & ~7u));
+                    g0 = rdlane64(g0, 0);
+                    const bool over = g0 + carry > cap;
+                    if (over && lane == 0) atomicOr(err, (unsigned long long)FK_FAULT_PARTS);
+                    if (lane == 0) { s_base = over ? ~0ull : g0; s_n = carry; }
+                    for (uint32_t p = lane; p < gp; p += 64u) {
+                        stage[rr % RP_SEGS][p] = over ? 0ull : ((g0 + ho[p]) << 16) | hc[p];
+                        hc[p] = 0;
+                    }
+                }
             }
             __syncthreads();
             /* place: a run of one part takes its slots with one atomic (its
@@ -412,6 +506,29 @@ k_repart(PartGeo pg, OT *out, unsigned long long *alloc, PartMeta *meta, uint64_
                 }
             }
             __syncthreads();
+            if constexpr (SEG) {
+                /* the round as one run (16-B pieces: the claim and rbuf are
+                   8-code aligned); every RP_SEGS rounds, and after the last,
+                   the staged segments to the table, 64 B a part */
+                const unsigned long long base = s_base;
+                if (base != ~0ull) {
+                    const uint32_t n8 = (s_n + 7u) >> 3;
+                    uint4 *dst = reinterpret_cast<uint4 *>(out + base);
+                    const uint4 *src = reinterpret_cast<const uint4 *>(rbuf);
+                    for (uint32_t i = t; i < n8; i += blockDim.x) dst[i] = src[i];
+                }
+                const uint32_t s = rr % RP_SEGS;
+                if ((s == RP_SEGS - 1u || rr + 1u == R) && s_dbase != ~0ull) {
+                    const uint32_t r0 = rr - s;
+                    for (uint32_t i = t; i < gp * (s + 1u); i += blockDim.x) {
+                        const uint32_t p = i / (s + 1u), j = i % (s + 1u);
+                        sg.desc[s_dbase + (unsigned long long)p * R + r0 + j] = stage[j][p];
+                    }
+                }
+                rr++;
+                __syncthreads();
+                continue;
+            }
             /* a wave per part: consecutive entries to consecutive slots; the
                part's round count cleared and its written count advanced by
                that wave alone.  (Round 6: whole aligned 16-B pieces with the

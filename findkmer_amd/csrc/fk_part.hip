@@ -392,56 +392,36 @@ k_bucket16(PartGeo pg, uint32_t *table) {
    here: they stand unless the general tiles' list or k_redo adds to the
    table afterwards. */
 __global__ void __launch_bounds__(1024, 8)
-k_count_parts(PartGeo pg, const uint16_t *in, const PartMeta *meta, uint32_t *table, uint64_t cap,
-               unsigned long long *err) {
+k_count_parts(PartGeo pg, const uint16_t *in, RepartSeg sg, uint32_t *table) {
     extern __shared__ uint32_t bins[];   /* 2^14 words */
-    __shared__ uint32_t s_hs;
+    __shared__ uint32_t s_hs, s_n;
     __shared__ unsigned long long wred[16][6];
     const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6;
-    const uint32_t np = 1u << pg.split;
+    const uint32_t np = 1u << pg.split, gp = REPART_G * np;
     const uint32_t b = blockIdx.x / np, part = blockIdx.x % np;
-    PartMeta m = meta[blockIdx.x];
-    if (m.off + m.n > cap) {
-        if (t == 0) atomicOr(err, (unsigned long long)FK_FAULT_META);
-        m.n = 0;
-        m.off = 0;
-    }
-    if (t == 0) s_hs = 0;
-    const uint4 *g4 = reinterpret_cast<const uint4 *>(in + m.off);
-    const uint32_t nq = (m.n + 7u) >> 3;
+    /* the part's segments: row blockIdx % gp of k_repart block blockIdx / gp's table */
+    const uint32_t g = blockIdx.x / gp, pi = blockIdx.x % gp;
+    const unsigned long long dbase = sg.bmeta[2 * (size_t)g];
+    const uint32_t R = (uint32_t)sg.bmeta[2 * (size_t)g + 1];
+    if (t == 0) { s_hs = 0; s_n = 0; }
     /* hsel < 0: bin c at half c & 1 of word c >> 1; else only bins [hsel 2^14, ..) as 32-bit words */
-    auto add8 = [&](const uint4 &v, uint32_t q, int hsel) {
-        const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-        for (int h = 0; h < 8; h++) {
-            if (q * 8u + (uint32_t)h >= m.n) continue;
-            const uint32_t c = (w4[h >> 1] >> (16 * (h & 1))) & 0x7FFFu;
-            if (hsel < 0) atomicAdd(&bins[c >> 1], 1u << ((c & 1u) << 4));
-            else if ((c >> 14) == (uint32_t)hsel) atomicAdd(&bins[c & 0x3FFFu], 1u);
-        }
+    auto add1 = [&](uint32_t c, int hsel) {
+        c &= 0x7FFFu;
+        if (hsel < 0) atomicAdd(&bins[c >> 1], 1u << ((c & 1u) << 4));
+        else if ((c >> 14) == (uint32_t)hsel) atomicAdd(&bins[c & 0x3FFFu], 1u);
     };
     auto zero = [&]() {
         for (uint32_t i = t; i < (1u << 12); i += 1024u) reinterpret_cast<uint4 *>(bins)[i] = make_uint4(0, 0, 0, 0);
     };
+    zero();
+    __syncthreads();
     {
-        constexpr uint32_t CP_U = 2u;
-        uint4 pv[CP_U];
-#pragma unroll
-        for (uint32_t u = 0; u < CP_U; u++) pv[u] = t + u * 1024u < nq ? g4[t + u * 1024u] : make_uint4(0, 0, 0, 0);
-        zero();
-        __syncthreads();
-#pragma unroll
-        for (uint32_t u = 0; u < CP_U; u++)
-            if (t + u * 1024u < nq) add8(pv[u], t + u * 1024u, -1);
-        for (uint32_t q0 = t + CP_U * 1024u; q0 < nq; q0 += CP_U * 1024u) {
-#pragma unroll
-            for (uint32_t u = 0; u < CP_U; u++) pv[u] = q0 + u * 1024u < nq ? g4[q0 + u * 1024u] : make_uint4(0, 0, 0, 0);
-#pragma unroll
-            for (uint32_t u = 0; u < CP_U; u++)
-                if (q0 + u * 1024u < nq) add8(pv[u], q0 + u * 1024u, -1);
-        }
+        const uint32_t mine = seg_codes(in, sg.desc, dbase, R, pi, [&](uint32_t c) { add1(c, -1); });
+        const uint32_t a = wsum32(mine);
+        if (lane == 0 && a) atomicAdd(&s_n, a);
     }
     __syncthreads();
+    const struct { uint32_t n; } m{s_n};
     {   /* the wrap check */
         uint32_t hs = 0;
         for (uint32_t i = t; i < (1u << 14); i += 1024u) hs += (bins[i] & 0xFFFFu) + (bins[i] >> 16);
@@ -482,7 +462,7 @@ k_count_parts(PartGeo pg, const uint16_t *in, const PartMeta *meta, uint32_t *ta
             __syncthreads();
             zero();
             __syncthreads();
-            for (uint32_t q = t; q < nq; q += 1024u) add8(g4[q], q, h);
+            seg_codes(in, sg.desc, dbase, R, pi, [&](uint32_t c) { add1(c, h); });
             __syncthreads();
             for (uint32_t i = t; i < (1u << 12); i += 1024u) {
                 const uint4 w = reinterpret_cast<const uint4 *>(bins)[i];
@@ -715,13 +695,10 @@ int launch_part(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t lo, cons
         /* the second partition level: each coarse slice's runs into one
            contiguous 16-bit stream per part, then one block per part */
         const uint64_t nparts = (uint64_t)pg.nslices << pg.split;
-        const uint64_t need = len + 8 * nparts + 16;   /* (entries <= bytes; 8-aligned parts) */
-        if (need > e->parts_cap) {
-            hipFree(e->d_parts);
-            e->d_parts = nullptr;
-            e->parts_cap = 0;
-            if (hipMalloc((void **)&e->d_parts, need * sizeof(uint16_t)) != hipSuccess) return FK_E_OOM;
-            e->parts_cap = need;
+        RepartSeg sgs{};
+        {   /* (entries <= bytes) */
+            int rc = repart_seg_alloc(e, pg, len, REPART_G << pg.split, &sgs);
+            if (rc) return rc;
         }
         if (!e->d_pmeta &&
             hipMalloc(&e->d_pmeta, (size_t)2048 * REPART_METAP * sizeof(PartMeta) + 64) != hipSuccess)
@@ -736,16 +713,11 @@ int launch_part(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t lo, cons
            blocks per CU.  (Round 5's lane-per-run k_repart took 8 slices a
            block there: 4.27 ms per G-base against 4.68 with two blocks of 4;
            the span-streamed one 5.42 with 8, 4.50 with 4.) */
-        if (pg.split <= 3)
-            hipLaunchKernelGGL((k_repart<uint16_t, 8u>), dim3(pg.nslices / 8u), dim3(1024), 0, e->stream, pg,
-                               e->d_parts, alloc, meta, (uint64_t)e->parts_cap, e->d_perr, 15u, nullptr);
-        else
-            hipLaunchKernelGGL(k_repart<uint16_t>, dim3(pg.nslices / REPART_G), dim3(1024), 0, e->stream, pg,
-                               e->d_parts, alloc, meta, (uint64_t)e->parts_cap, e->d_perr, 15u, nullptr);
+        hipLaunchKernelGGL((k_repart<uint16_t, REPART_G, true>), dim3(pg.nslices / REPART_G), dim3(1024), 0, e->stream,
+                           pg, e->d_parts, alloc, meta, (uint64_t)e->parts_cap, e->d_perr, 15u, nullptr, sgs);
         HIPCHK(hipGetLastError());
         hipLaunchKernelGGL(k_count_parts, dim3((unsigned)nparts), dim3(1024), (size_t)1 << 16, e->stream, pg,
-                               (const uint16_t *)e->d_parts, (const PartMeta *)meta, e->d_table, (uint64_t)e->parts_cap,
-                               e->d_perr);
+                           (const uint16_t *)e->d_parts, sgs, e->d_table);
         if (pg.glist) {
             HIPCHK(hipGetLastError());
             hipLaunchKernelGGL(k_list_add, dim3((unsigned)e->cus * 4), dim3(256), 0, e->stream, pg.glist, e->d_table,
@@ -779,6 +751,24 @@ int launch_part(fk_engine *e, const uint8_t *buf, uint64_t len, int64_t lo, cons
             HIPCHK(hipGetLastError());
         }
     }
+    return FK_OK;
+}
+
+int repart_seg_alloc(fk_engine *e, const PartGeo &pg, uint64_t ncodes, uint32_t gp, RepartSeg *sg) {
+    /* rounds: a block's chunk of up to RP_CHUNK rows takes ceil(pieces /
+       4096) rounds, a row's span adding at most two partial pieces */
+    const uint64_t nrows = pg.flag ? (uint64_t)pg.stride : (uint64_t)pg.rows;   /* (both regions at most) */
+    const uint64_t nblocks = pg.nslices / REPART_G, nchunks = (nrows + RP_CHUNK - 1) / RP_CHUNK;
+    const uint64_t rounds = (ncodes / 4 + 2 * nrows * nblocks) / (1024u * 4u) + nblocks * nchunks + 1;
+    int rc = sp_ensure((void **)&e->d_parts, &e->parts_cap, ncodes + 8 * rounds + 16, sizeof(uint16_t));
+    if (!rc) rc = sp_ensure((void **)&e->d_rdesc, &e->rdesc_cap, (uint64_t)gp * rounds, sizeof(unsigned long long));
+    if (!rc) rc = sp_ensure((void **)&e->d_rbm, &e->rbm_cap, 2 * nblocks + 2, sizeof(unsigned long long));
+    if (rc) return rc;
+    HIPCHK(hipMemsetAsync(e->d_rbm + 2 * nblocks, 0, 2 * sizeof(unsigned long long), e->stream));
+    sg->desc = e->d_rdesc;
+    sg->dcap = e->rdesc_cap;
+    sg->dalloc = e->d_rbm + 2 * nblocks;
+    sg->bmeta = e->d_rbm;
     return FK_OK;
 }
 

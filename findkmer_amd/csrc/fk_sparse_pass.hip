@@ -998,11 +998,11 @@ __device__ unsigned long long chain_prefix(unsigned long long *flags, uint32_t b
  */
 #define KC2_VW 32u
 __global__ void __launch_bounds__(1024, 8)   /* 8 waves per SIMD: two blocks per CU */
-k_kp_cnt2(const uint16_t *in, const PartMeta *meta, uint64_t cap_in, uint64_t lo, uint64_t npads,
+k_kp_cnt2(const uint16_t *in, RepartSeg sg, uint32_t gp, uint64_t lo, uint64_t npads,
           const unsigned long long *tcount, uint32_t nparts, int k, unsigned long long *flags, uint64_t *out_k,
           uint32_t *out_c, unsigned long long *slots, uint64_t *fl, unsigned long long *err) {
     extern __shared__ uint32_t bins[];   /* KC_WORDS */
-    __shared__ uint32_t wnz[KC2_VW], wlast[KC2_VW], hpre[8], s_hs;
+    __shared__ uint32_t wnz[KC2_VW], wlast[KC2_VW], hpre[8], s_hs, s_n;
     __shared__ unsigned long long wred[16][7];
     __shared__ unsigned long long bprefix;
     __shared__ uint32_t vblk;
@@ -1014,52 +1014,36 @@ k_kp_cnt2(const uint16_t *in, const PartMeta *meta, uint64_t cap_in, uint64_t lo
            order is not start order */
         vblk = (uint32_t)atomicAdd(&flags[nparts], 1ull);
         s_hs = 0;
+        s_n = 0;
     }
     if (t < 8) hpre[t] = 0;
     __syncthreads();
     const uint32_t blk = vblk;
-    PartMeta m = meta[blk];
-    if (m.off + m.n > cap_in) {
-        if (t == 0) atomicOr(err, (unsigned long long)FK_FAULT_META);
-        m.n = 0;
-        m.off = 0;
-    }
-    const uint4 *g4 = reinterpret_cast<const uint4 *>(in + m.off);
-    const uint32_t nq = (m.n + 7u) >> 3;
-    auto count8 = [&](const uint4 &v, uint32_t q, int hsel) {
-        const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-        for (int h = 0; h < 8; h++) {
-            if (q * 8u + (uint32_t)h >= m.n) continue;
-            const uint32_t b = (w4[h >> 1] >> (16 * (h & 1))) & 0x7FFFu;
-            if (hsel < 0) atomicAdd(&bins[b >> 1], 1u << ((b & 1u) << 4));
-            else if ((b >> 14) == (uint32_t)hsel) atomicAdd(&bins[b & (KC_WORDS - 1u)], 1u);
-        }
+    /* the part's segments: row blk % gp of k_repart block blk / gp's table */
+    const uint32_t sgb = blk / gp, spi = blk % gp;
+    const unsigned long long dbase = sg.bmeta[2 * (size_t)sgb];
+    const uint32_t R = (uint32_t)sg.bmeta[2 * (size_t)sgb + 1];
+    /* bin b at half b & 1 of word b >> 1 (hsel: the 32-bit pass of half h,
+       bins [h 2^14, (h + 1) 2^14) only) */
+    auto count1 = [&](uint32_t b, int hsel) {
+        b &= 0x7FFFu;
+        if (hsel < 0) atomicAdd(&bins[b >> 1], 1u << ((b & 1u) << 4));
+        else if ((b >> 14) == (uint32_t)hsel) atomicAdd(&bins[b & (KC_WORDS - 1u)], 1u);
     };
     auto zero = [&]() {
         for (uint32_t i = t; i < KC_WORDS / 4u; i += 1024u) reinterpret_cast<uint4 *>(bins)[i] = make_uint4(0, 0, 0, 0);
     };
-    constexpr uint32_t KP_U = 2u;   /* (4: 10 VGPRs spilled at the 64 of two blocks per CU) */
+    zero();
+    __syncthreads();
     {
-        uint4 pv[KP_U];
-#pragma unroll
-        for (uint32_t u = 0; u < KP_U; u++) pv[u] = t + u * 1024u < nq ? g4[t + u * 1024u] : make_uint4(0, 0, 0, 0);
-        zero();
-        __syncthreads();
-#pragma unroll
-        for (uint32_t u = 0; u < KP_U; u++)
-            if (t + u * 1024u < nq) count8(pv[u], t + u * 1024u, -1);
-        for (uint32_t q0 = t + KP_U * 1024u; q0 < nq; q0 += KP_U * 1024u) {
-#pragma unroll
-            for (uint32_t u = 0; u < KP_U; u++) pv[u] = q0 + u * 1024u < nq ? g4[q0 + u * 1024u] : make_uint4(0, 0, 0, 0);
-#pragma unroll
-            for (uint32_t u = 0; u < KP_U; u++)
-                if (q0 + u * 1024u < nq) count8(pv[u], q0 + u * 1024u, -1);
-        }
+        const uint32_t mine = seg_codes<2>(in, sg.desc, dbase, R, spi, [&](uint32_t c) { count1(c, -1); });
+        const uint32_t a = wsum32(mine);
+        if (lane == 0 && a) atomicAdd(&s_n, a);
     }
     __syncthreads();
     /* the top key (relative 0xFFFFFFFF, the last bin of the last part) was
        only counted (k_kpart): its real windows, the pads taken off */
+    const struct { uint32_t n; } m{s_n};
     const uint32_t extra = blk == nparts - 1u ? (uint32_t)(*tcount - npads) : 0u;
     const uint64_t kpart = lo + ((uint64_t)blk << 15);
     const uint32_t fd = (uint32_t)((kpart >> (2 * (k - 1))) & 3);
@@ -1100,7 +1084,7 @@ k_kp_cnt2(const uint16_t *in, const PartMeta *meta, uint64_t cap_in, uint64_t lo
             __syncthreads();
             zero();
             __syncthreads();
-            for (uint32_t q = t; q < nq; q += 1024u) count8(g4[q], q, h);
+            seg_codes<2>(in, sg.desc, dbase, R, spi, [&](uint32_t c) { count1(c, h); });
             __syncthreads();
             pass1(16u * h + wv, (uint32_t)h * 16384u + wv * 1024u, 16u, 1);
         }
@@ -1155,7 +1139,7 @@ k_kp_cnt2(const uint16_t *in, const PartMeta *meta, uint64_t cap_in, uint64_t lo
             __syncthreads();
             zero();
             __syncthreads();
-            for (uint32_t q = t; q < nq; q += 1024u) count8(g4[q], q, h);
+            seg_codes<2>(in, sg.desc, dbase, R, spi, [&](uint32_t c) { count1(c, h); });
             __syncthreads();
             pass2(16u * h + wv, (uint32_t)h * 16384u + wv * 1024u, 16u, 1);
         }
@@ -1532,8 +1516,9 @@ static int sp_count_rows32(fk_engine *e, const PartGeo &pg, uint64_t n, uint64_t
                            unsigned long long *res, unsigned long long *dacc, uint64_t *out_k, uint32_t *out_c,
                            uint64_t *nw) {
     const int k = e->k;
-    const uint32_t nparts = 2048u << 6;
-    int rc = sp_ensure((void **)&e->d_parts, &e->parts_cap, n + 8ull * nparts + 16, sizeof(uint16_t));
+    const uint32_t nparts = 2048u << 6, gp = REPART_G << 6;
+    RepartSeg sgs{};
+    int rc = repart_seg_alloc(e, pg, n, gp, &sgs);
     if (rc) return rc;
     if (!e->d_pmeta && hipMalloc(&e->d_pmeta, (size_t)2048 * REPART_METAP * sizeof(PartMeta) + 64) != hipSuccess)
         return FK_E_OOM;
@@ -1546,11 +1531,11 @@ static int sp_count_rows32(fk_engine *e, const PartGeo &pg, uint64_t n, uint64_t
     HIPCHK(hipMemsetAsync(alloc, 0, 2 * sizeof(unsigned long long), e->stream));
     HIPCHK(hipMemsetAsync(flags.p, 0, (size_t)(nparts + 1) * 8, e->stream));   /* (+ the block tickets) */
     HIPCHK(hipMemsetAsync(slots.p, 0, (size_t)KP_SLOTS * KP_SLOT_W * 8, e->stream));
-    hipLaunchKernelGGL(k_repart<uint16_t>, dim3(2048u / REPART_G), dim3(1024), 0, e->stream, pg, e->d_parts, alloc,
-                       meta, (uint64_t)e->parts_cap, alloc + 1, 15u, nullptr);
+    hipLaunchKernelGGL((k_repart<uint16_t, REPART_G, true>), dim3(2048u / REPART_G), dim3(1024), 0, e->stream, pg,
+                       e->d_parts, alloc, meta, (uint64_t)e->parts_cap, alloc + 1, 15u, nullptr, sgs);
     HIPCHK(hipGetLastError());
     hipLaunchKernelGGL(k_kp_cnt2, dim3(nparts), dim3(1024), (size_t)KC_WORDS * 4, e->stream, (const uint16_t *)e->d_parts,
-                       (const PartMeta *)meta, (uint64_t)e->parts_cap, lo, npads, (const unsigned long long *)(res + 1), nparts,
+                       sgs, gp, lo, npads, (const unsigned long long *)(res + 1), nparts,
                        k, flags.as<unsigned long long>(), out_k, out_c, slots.as<unsigned long long>(), fl.as<uint64_t>(),
                        alloc + 1);
     HIPCHK(hipGetLastError());
