@@ -190,40 +190,44 @@ struct RepartSeg {
    sparse passes): part bits [psh, psh + 7), stored as the low psh bits.
    The rows' runs hold at most 65535 codes (C32 / k_kpart rows: 32 K). */
 /* the codes of part i of a SEG k_repart block (its table row at desc +
-   dbase + i R) as f(code); the number of codes is returned to every lane
-   of the block through *mn (block-uniform after a barrier the caller
-   places).  A wave takes every nw-th segment: its lanes load up to 64
-   segments' entries at once, then U segments' codes are in flight per
-   lane (a segment is one round's codes of the part: ~64 at k = 16, 17,
-   ~256 at k = 15). */
-template <uint32_t U = 4u, typename F>
+   dbase + i R) as f(code); returns the codes of the segments this lane's
+   entries named (their block sum is the part's size).  A wave takes 8
+   segments at a time, 8 lanes each: a lane loads the segment's 16-B pieces
+   sub, sub + 8, .. (a 64-code segment is ~9 pieces), two in flight, and
+   hands on the codes inside the segment.  (Round 6: a lane per code, 2-B
+   loads, took k = 16's k_count_parts from 3.5 to 4.8 ms.) */
+template <typename F>
 __device__ __forceinline__ uint32_t seg_codes(const uint16_t *in, const unsigned long long *desc,
                                               unsigned long long dbase, uint32_t R, uint32_t i, F &&f) {
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    const uint32_t sl = lane >> 3, sub = lane & 7u;
     const unsigned long long *d = desc + dbase + (unsigned long long)i * R;
-    uint32_t mine = 0;   /* codes of the segments this lane's entries name */
-    for (uint32_t r0 = wv; r0 < R; r0 += 64u * nw) {
-        const uint32_t rl = r0 + lane * nw;
-        const unsigned long long e = rl < R ? d[rl] : 0ull;
-        mine += (uint32_t)(e & 0xFFFFu);
-        const uint32_t ns = min(64u, (R - r0 + nw - 1u) / nw);
-        for (uint32_t s = 0; s < ns; s += U) {
-            uint64_t a[U];
-            uint32_t n[U], mx = 0;
+    const uint4 *g4 = reinterpret_cast<const uint4 *>(in);
+    uint32_t mine = 0;
+    for (uint32_t r0 = wv * 8u; r0 < R; r0 += nw * 8u) {
+        const uint32_t r = r0 + sl;
+        const unsigned long long e = r < R ? d[r] : 0ull;
+        const uint64_t a = e >> 16;
+        const uint32_t n = (uint32_t)(e & 0xFFFFu);
+        if (sub == 0) mine += n;
+        const uint64_t q0 = a >> 3;
+        const uint32_t npc = n ? (uint32_t)(((a + n + 7u) >> 3) - q0) : 0u;
+        const uint32_t mxp = rdlane(wscan_max32(npc), 63);
+        for (uint32_t x = sub; x < mxp; x += 16u) {
+            uint4 v[2];
 #pragma unroll
-            for (uint32_t u = 0; u < U; u++) {
-                const unsigned long long eu = s + u < ns ? rdlane64(e, (int)(s + u)) : 0ull;
-                a[u] = eu >> 16;
-                n[u] = (uint32_t)(eu & 0xFFFFu);
-                mx = max(mx, n[u]);
-            }
-            for (uint32_t j = lane; j < mx; j += 64u) {
-                uint32_t c[U];
+            for (uint32_t u = 0; u < 2u; u++)
+                v[u] = x + 8u * u < npc ? g4[q0 + x + 8u * u] : make_uint4(0, 0, 0, 0);
 #pragma unroll
-                for (uint32_t u = 0; u < U; u++) c[u] = j < n[u] ? (uint32_t)in[a[u] + j] : 0u;
+            for (uint32_t u = 0; u < 2u; u++) {
+                if (x + 8u * u >= npc) continue;
+                const uint64_t pb = (q0 + x + 8u * u) * 8u;   /* the piece's first code */
+                const uint32_t w4[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
 #pragma unroll
-                for (uint32_t u = 0; u < U; u++)
-                    if (j < n[u]) f(c[u]);
+                for (uint32_t h = 0; h < 8u; h++) {
+                    const uint64_t pos = pb + h;
+                    if (pos >= a && pos < a + n) f((w4[h >> 1] >> (16u * (h & 1u))) & 0xFFFFu);
+                }
             }
         }
     }

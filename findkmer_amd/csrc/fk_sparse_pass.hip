@@ -1036,7 +1036,7 @@ k_kp_cnt2(const uint16_t *in, RepartSeg sg, uint32_t gp, uint64_t lo, uint64_t n
     zero();
     __syncthreads();
     {
-        const uint32_t mine = seg_codes<2>(in, sg.desc, dbase, R, spi, [&](uint32_t c) { count1(c, -1); });
+        const uint32_t mine = seg_codes(in, sg.desc, dbase, R, spi, [&](uint32_t c) { count1(c, -1); });
         const uint32_t a = wsum32(mine);
         if (lane == 0 && a) atomicAdd(&s_n, a);
     }
@@ -1084,7 +1084,7 @@ k_kp_cnt2(const uint16_t *in, RepartSeg sg, uint32_t gp, uint64_t lo, uint64_t n
             __syncthreads();
             zero();
             __syncthreads();
-            seg_codes<2>(in, sg.desc, dbase, R, spi, [&](uint32_t c) { count1(c, h); });
+            seg_codes(in, sg.desc, dbase, R, spi, [&](uint32_t c) { count1(c, h); });
             __syncthreads();
             pass1(16u * h + wv, (uint32_t)h * 16384u + wv * 1024u, 16u, 1);
         }
@@ -1139,7 +1139,7 @@ k_kp_cnt2(const uint16_t *in, RepartSeg sg, uint32_t gp, uint64_t lo, uint64_t n
             __syncthreads();
             zero();
             __syncthreads();
-            seg_codes<2>(in, sg.desc, dbase, R, spi, [&](uint32_t c) { count1(c, h); });
+            seg_codes(in, sg.desc, dbase, R, spi, [&](uint32_t c) { count1(c, h); });
             __syncthreads();
             pass2(16u * h + wv, (uint32_t)h * 16384u + wv * 1024u, 16u, 1);
         }
