@@ -195,29 +195,45 @@ struct RepartSeg {
    segments at a time, 8 lanes each: a lane loads the segment's 16-B pieces
    sub, sub + 8, .. (a 64-code segment is ~9 pieces), two in flight, and
    hands on the codes inside the segment.  (Round 6: a lane per code, 2-B
-   loads, took k = 16's k_count_parts from 3.5 to 4.8 ms.) */
-template <typename F>
+   loads, took k = 16's k_count_parts from 3.5 to 4.8 ms.)  `pre` runs once
+   per thread after the first batch's loads are issued (the consumers zero
+   their bins there, as they did while a contiguous stream's first pieces
+   loaded). */
+template <typename F, typename P>
 __device__ __forceinline__ uint32_t seg_codes(const uint16_t *in, const unsigned long long *desc,
-                                              unsigned long long dbase, uint32_t R, uint32_t i, F &&f) {
+                                              unsigned long long dbase, uint32_t R, uint32_t i, F &&f, P &&pre) {
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
     const uint32_t sl = lane >> 3, sub = lane & 7u;
     const unsigned long long *d = desc + dbase + (unsigned long long)i * R;
     const uint4 *g4 = reinterpret_cast<const uint4 *>(in);
     uint32_t mine = 0;
-    for (uint32_t r0 = wv * 8u; r0 < R; r0 += nw * 8u) {
+    uint64_t a = 0, q0 = 0;
+    uint32_t n = 0, npc = 0;
+    auto entry = [&](uint32_t r0) {
         const uint32_t r = r0 + sl;
         const unsigned long long e = r < R ? d[r] : 0ull;
-        const uint64_t a = e >> 16;
-        const uint32_t n = (uint32_t)(e & 0xFFFFu);
+        a = e >> 16;
+        n = (uint32_t)(e & 0xFFFFu);
+        q0 = a >> 3;
+        npc = n ? (uint32_t)(((a + n + 7u) >> 3) - q0) : 0u;
+    };
+    uint4 v[2];
+    auto load = [&](uint32_t x) {
+#pragma unroll
+        for (uint32_t u = 0; u < 2u; u++) v[u] = x + 8u * u < npc ? g4[q0 + x + 8u * u] : make_uint4(0, 0, 0, 0);
+    };
+    /* the first batch's entries and pieces in flight before `pre` (the
+       caller's zeroing of its bins and barrier: every thread calls it once) */
+    uint32_t r0 = wv * 8u;
+    entry(r0);
+    load(sub);
+    pre();
+    for (bool first = true; r0 < R; r0 += nw * 8u, first = false) {
+        if (!first) entry(r0);
         if (sub == 0) mine += n;
-        const uint64_t q0 = a >> 3;
-        const uint32_t npc = n ? (uint32_t)(((a + n + 7u) >> 3) - q0) : 0u;
         const uint32_t mxp = rdlane(wscan_max32(npc), 63);
         for (uint32_t x = sub; x < mxp; x += 16u) {
-            uint4 v[2];
-#pragma unroll
-            for (uint32_t u = 0; u < 2u; u++)
-                v[u] = x + 8u * u < npc ? g4[q0 + x + 8u * u] : make_uint4(0, 0, 0, 0);
+            if (!first || x != sub) load(x);
 #pragma unroll
             for (uint32_t u = 0; u < 2u; u++) {
                 if (x + 8u * u >= npc) continue;
@@ -232,6 +248,11 @@ __device__ __forceinline__ uint32_t seg_codes(const uint16_t *in, const unsigned
         }
     }
     return mine;
+}
+template <typename F>
+__device__ __forceinline__ uint32_t seg_codes(const uint16_t *in, const unsigned long long *desc,
+                                              unsigned long long dbase, uint32_t R, uint32_t i, F &&f) {
+    return seg_codes(in, desc, dbase, R, i, f, []() {});
 }
 
 template <typename OT, uint32_t G = REPART_G, bool SEG = false>

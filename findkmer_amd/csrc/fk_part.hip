@@ -413,10 +413,11 @@ k_count_parts(PartGeo pg, const uint16_t *in, RepartSeg sg, uint32_t *table) {
     auto zero = [&]() {
         for (uint32_t i = t; i < (1u << 12); i += 1024u) reinterpret_cast<uint4 *>(bins)[i] = make_uint4(0, 0, 0, 0);
     };
-    zero();
-    __syncthreads();
     {
-        const uint32_t mine = seg_codes(in, sg.desc, dbase, R, pi, [&](uint32_t c) { add1(c, -1); });
+        const uint32_t mine = seg_codes(in, sg.desc, dbase, R, pi, [&](uint32_t c) { add1(c, -1); }, [&]() {
+            zero();
+            __syncthreads();
+        });
         const uint32_t a = wsum32(mine);
         if (lane == 0 && a) atomicAdd(&s_n, a);
     }

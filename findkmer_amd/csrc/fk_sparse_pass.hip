@@ -1033,10 +1033,11 @@ k_kp_cnt2(const uint16_t *in, RepartSeg sg, uint32_t gp, uint64_t lo, uint64_t n
     auto zero = [&]() {
         for (uint32_t i = t; i < KC_WORDS / 4u; i += 1024u) reinterpret_cast<uint4 *>(bins)[i] = make_uint4(0, 0, 0, 0);
     };
-    zero();
-    __syncthreads();
     {
-        const uint32_t mine = seg_codes(in, sg.desc, dbase, R, spi, [&](uint32_t c) { count1(c, -1); });
+        const uint32_t mine = seg_codes(in, sg.desc, dbase, R, spi, [&](uint32_t c) { count1(c, -1); }, [&]() {
+            zero();
+            __syncthreads();
+        });
         const uint32_t a = wsum32(mine);
         if (lane == 0 && a) atomicAdd(&s_n, a);
     }
